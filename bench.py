@@ -1,0 +1,139 @@
+#!/usr/bin/env python
+"""Headline benchmark: images/s of end-to-end (approximate-joint) Faster R-CNN training.
+
+BASELINE.json metric "imgs/sec e2e train ResNet-101 Faster R-CNN at 1/2/4/8 MI355X": ResNet-101
+C4 Faster R-CNN, COCO-shaped synthetic images 800x1333 (81 classes), random-init weights,
+1 image per GPU per step (the reference's only mode), bf16 compute with fp32 master weights,
+full step timed: trunk+RPN fwd/bwd, anchor target, proposal (sort + NMS 12000->6000),
+proposal target (128 RoIs), RoIPool, stage-4 head, losses, bucketed RCCL all-reduce (N>1),
+fused SGD update.  Weak scaling (fixed per-GPU work).
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  Reference publishes no numbers, so vs_baseline=null.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from mx_rcnn_amd.config import snapshot  # noqa: E402
+from mx_rcnn_amd.models import FasterRCNN  # noqa: E402
+from mx_rcnn_amd.parallel import dist as pdist  # noqa: E402
+from mx_rcnn_amd.core.trainer import Trainer, GraphedStep  # noqa: E402
+
+METRIC = 'imgs/sec e2e train ResNet-101 Faster R-CNN'
+
+
+def synthetic_batch(n_img, h, w, num_classes, device, gen, max_gt=20):
+    data = torch.randn(n_img, 3, h, w, generator=gen) * 50.0
+    G = max_gt
+    gt = torch.full((n_img, G, 5), -1.0)
+    n_gt = torch.randint(1, G + 1, (n_img,), generator=gen).to(torch.int32)
+    for b in range(n_img):
+        k = int(n_gt[b])
+        bw = torch.randint(32, 400, (k,), generator=gen).float()
+        bh = torch.randint(32, 400, (k,), generator=gen).float()
+        x1 = (torch.rand(k, generator=gen) * (w - bw - 1)).floor()
+        y1 = (torch.rand(k, generator=gen) * (h - bh - 1)).floor()
+        cls = torch.randint(1, num_classes, (k,), generator=gen).float()
+        gt[b, :k] = torch.stack([x1, y1, x1 + bw, y1 + bh, cls], dim=1)
+    im_info = torch.tensor([[float(h), float(w), 1.0]] * n_img)
+    return {'data': data.to(device), 'im_info': im_info.to(device), 'gt_boxes': gt.to(device),
+            'n_gt': n_gt.to(device)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--network', default='resnet101')
+    ap.add_argument('--num-classes', type=int, default=81)
+    ap.add_argument('--image', default='800x1333')
+    ap.add_argument('--ims-per-gpu', type=int, default=1)
+    ap.add_argument('--mode', default='graph', choices=['graph', 'eager'])
+    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--bucket-mb', type=float, default=64)
+    ap.add_argument('--pool', type=int, default=4, help='distinct synthetic batches cycled')
+    args = ap.parse_args()
+
+    rank, world, local_rank, device = pdist.init_distributed()
+    h, w = [int(v) for v in args.image.lower().split('x')]
+    cfg = snapshot()
+    # end2end config mutation (train_end2end.py:25-32)
+    cfg.TRAIN.BG_THRESH_LO = 0.0
+    cfg.TRAIN.HAS_RPN = True
+    cfg.END2END = 1
+    cfg.TRAIN.BBOX_NORMALIZATION_PRECOMPUTED = True
+    cfg.TRAIN.IMS_PER_BATCH = args.ims_per_gpu
+    torch.manual_seed(1234 + rank)
+    model = FasterRCNN(args.network, args.num_classes, cfg=cfg)
+    fixed = ['conv0', 'stage1', 'stage2', 'bn_data', 'bn0'] if args.network.startswith('resnet') else ['conv1', 'conv2']
+    dtype = torch.bfloat16 if (args.dtype == 'bf16' and device.type == 'cuda') else torch.float32
+    trainer = Trainer(model, 'e2e', fixed_param_prefix=fixed, lr=0.001, momentum=0.9, wd=0.0005, clip_gradient=1.0,
+                      rescale_grad=1.0, compute_dtype=dtype, device=device, bucket_mb=args.bucket_mb)
+    gen = torch.Generator().manual_seed(4321 + rank)
+    pool = [synthetic_batch(args.ims_per_gpu, h, w, args.num_classes, device, gen) for _ in range(args.pool)]
+
+    mode = args.mode if device.type == 'cuda' else 'eager'
+    step_fn = None
+    if mode == 'graph':
+        try:
+            g = GraphedStep(trainer, pool[0], warmup=3)
+            step_fn = g
+        except Exception as e:  # reported, never silent
+            if rank == 0:
+                print('[bench] hipGraph capture failed (%s: %s); running eager' % (type(e).__name__, str(e)[:300]),
+                      file=sys.stderr)
+            mode = 'eager'
+            torch.cuda.synchronize()
+    if step_fn is None:
+        step_fn = trainer.step
+
+    def sync():
+        if device.type == 'cuda':
+            torch.cuda.synchronize()
+
+    for i in range(args.warmup):
+        out = step_fn(pool[i % len(pool)])
+    sync()
+    loss0 = float(out['loss'].detach().float().item()) if args.warmup else float('nan')
+    pdist.barrier()
+    sync()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        out = step_fn(pool[i % len(pool)])
+    sync()
+    pdist.barrier()
+    sync()
+    elapsed = time.perf_counter() - t0
+    elapsed = pdist.all_reduce_max(elapsed, device)
+    loss1 = float(out['loss'].detach().float().item())
+    ms = elapsed / max(args.steps, 1) * 1e3
+    imgs = args.ims_per_gpu * world * args.steps
+    value = imgs / elapsed
+    if rank == 0:
+        rec = {'metric': METRIC, 'value': round(value, 3), 'unit': 'images/s', 'n_gpus': world,
+               'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
+               'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+               'dtype': 'bf16' if dtype == torch.bfloat16 else 'fp32',
+               'data': 'synthetic (random 800x1333 images, 1-20 random gt boxes, random-init weights)',
+               'config': {'model': '%s-faster-rcnn-c4' % args.network, 'global_batch': args.ims_per_gpu * world,
+                          'seq_len': None, 'image_hw': [h, w], 'num_classes': args.num_classes,
+                          'ims_per_gpu': args.ims_per_gpu, 'parallelism': 'dp%d' % world,
+                          'rpn_pre_post_nms': [cfg.TRAIN.RPN_PRE_NMS_TOP_N, cfg.TRAIN.RPN_POST_NMS_TOP_N],
+                          'rois_per_image': cfg.TRAIN.BATCH_SIZE, 'exec': mode,
+                          'loss_first_last': [round(loss0, 4), round(loss1, 4)]}}
+        print(json.dumps(rec), flush=True)
+    pdist.destroy()
+
+
+if __name__ == '__main__':
+    main()

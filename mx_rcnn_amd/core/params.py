@@ -1,0 +1,170 @@
+"""Flat parameter store: fp32 master weights + momentum, low-precision compute shadows and
+flat gradient buffers (SURVEY §5.8 item 2, §2.9 SGD row).
+
+Design (MI355X-first):
+* Every trainable parameter lives in ONE flat buffer per (precision, weight-decay) group.
+  The module's Parameter is re-pointed at a bf16 view of a flat "shadow" buffer, and its
+  ``.grad`` is pre-set to a view of a flat gradient buffer, so autograd accumulates in
+  place: zeroing grads is one memset, the all-reduce buckets are plain slices, and the
+  fused SGD kernel (csrc/hip/sgd.hip) updates master + momentum and rewrites the bf16
+  shadow in the same pass (no separate cast kernels per step).
+* Buffers are ordered in REVERSE registration order (= roughly the order gradients become
+  ready in backward) so bucket i can be all-reduced while backward still runs.
+* BatchNorm affine parameters stay fp32 (the fused BN kernels take fp32 params).
+* Frozen parameters (``fixed_param_prefix``, matched by SUBSTRING exactly like the
+  reference `rcnn/module.py:50-55`) are cast once to the compute dtype and never updated.
+* Weight decay follows MXNet's Optimizer.set_wd_mult: only names ending in ``_weight`` or
+  ``_gamma`` are decayed.
+"""
+import logging
+
+import torch
+import torch.nn as nn
+
+from ..ops.sgd import sgd_momentum_
+
+
+def _is_bn_param(name):
+    return name.endswith('_gamma') or name.endswith('_beta')
+
+
+def match_fixed(name, prefixes):
+    return any(p in name for p in (prefixes or []))
+
+
+class ParamGroup:
+    def __init__(self, key, entries, device, compute_dtype):
+        self.key = key  # (lowp: bool, decay: bool)
+        lowp, decay = key
+        self.decay = decay
+        self.entries = entries  # list of (mx_name, module, attr, numel, shape, channels_last)
+        self.numel = sum(e[3] for e in entries)
+        self.master = torch.zeros(self.numel, dtype=torch.float32, device=device)
+        self.mom = torch.zeros(self.numel, dtype=torch.float32, device=device)
+        gd = compute_dtype if lowp else torch.float32
+        self.shadow = torch.zeros(self.numel, dtype=gd, device=device) if lowp else None
+        self.grad = torch.zeros(self.numel, dtype=gd, device=device)
+        self.offsets = []
+
+
+class FlatParamStore:
+    def __init__(self, model, fixed_param_prefix=None, compute_dtype=torch.bfloat16, device=None,
+                 channels_last=True):
+        self.model = model
+        self.compute_dtype = compute_dtype
+        dev = torch.device(device) if device is not None else next(model.parameters()).device
+        self.device = dev
+        lowp_enabled = compute_dtype != torch.float32
+        fixed = fixed_param_prefix or []
+        layers = list(model.mx_layers())
+        named = []  # (mx_name, module, attr, param)
+        for m in layers:
+            for attr, p in m._parameters.items():
+                if p is None:
+                    continue
+                named.append(('%s_%s' % (m.mx_name, attr), m, attr, p))
+        self.fixed_names = [n for n, _, _, _ in named if match_fixed(n, fixed)]
+        for pfx in fixed:
+            hits = [n for n in self.fixed_names if pfx in n and not n.startswith(pfx)]
+            if hits:
+                logging.warning('fixed_param_prefix %r also matches %d params by substring (e.g. %s)',
+                                pfx, len(hits), hits[0])
+        groups = {}
+        for n, m, attr, p in reversed(named):
+            if n in self.fixed_names:
+                continue
+            lowp = lowp_enabled and not _is_bn_param(n)
+            decay = n.endswith('_weight') or n.endswith('_gamma')
+            cl = channels_last and p.dim() == 4
+            groups.setdefault((lowp, decay), []).append((n, m, attr, p.numel(), tuple(p.shape), cl))
+        self.groups = [ParamGroup(k, v, dev, compute_dtype) for k, v in sorted(groups.items())]
+        self.params = {}
+        with torch.no_grad():
+            for g in self.groups:
+                off = 0
+                for n, m, attr, numel, shape, cl in g.entries:
+                    src = m._parameters[attr].detach().to(dev, torch.float32)
+                    g.offsets.append(off)
+                    g.master[off:off + numel].copy_(self._flat_view(src, cl))
+                    lowp = g.shadow is not None
+                    storage = g.shadow if lowp else g.master
+                    pv = self._shaped(storage[off:off + numel], shape, cl)
+                    if lowp:
+                        pv.copy_(src.to(compute_dtype))
+                    param = nn.Parameter(pv, requires_grad=True)
+                    param.grad = self._shaped(g.grad[off:off + numel], shape, cl)
+                    m._parameters[attr] = param
+                    self.params[n] = param
+                    off += numel
+            # frozen: cast once, no grad
+            for n, m, attr, p in named:
+                if n in self.fixed_names:
+                    lowp = lowp_enabled and not _is_bn_param(n)
+                    t = p.detach().to(dev, compute_dtype if lowp else torch.float32)
+                    if channels_last and t.dim() == 4:
+                        t = t.contiguous(memory_format=torch.channels_last)
+                    m._parameters[attr] = nn.Parameter(t, requires_grad=False)
+                    self.params[n] = m._parameters[attr]
+        for b in model.buffers():
+            b.data = b.data.to(dev)
+
+    @staticmethod
+    def _flat_view(t, cl):
+        if cl:
+            return t.permute(0, 2, 3, 1).reshape(-1)
+        return t.reshape(-1)
+
+    @staticmethod
+    def _shaped(flat, shape, cl):
+        if cl:
+            o, i, kh, kw = shape
+            return flat.view(o, kh, kw, i).permute(0, 3, 1, 2)
+        return flat.view(shape)
+
+    # ------------------------------------------------------------------ step pieces
+    def zero_grad(self):
+        for g in self.groups:
+            g.grad.zero_()
+
+    def grad_buffers(self):
+        return [g.grad for g in self.groups]
+
+    def sgd_step(self, lr, momentum=0.9, wd=0.0005, rescale=1.0, clip=-1.0):
+        """``lr``: 1-element fp32 device tensor."""
+        for g in self.groups:
+            sgd_momentum_(g.master, g.mom, g.grad, lr, momentum, wd if g.decay else 0.0, rescale, clip,
+                          g.shadow)
+
+    def master_param(self, name):
+        for g in self.groups:
+            for (n, _, _, numel, shape, cl), off in zip(g.entries, g.offsets):
+                if n == name:
+                    return self._shaped(g.master[off:off + numel], shape, cl)
+        p = self.params[name]
+        return p.detach().float()
+
+    def state_arrays(self):
+        """fp32 copies of every parameter (trainable from master, frozen from the cast copy)."""
+        return {n: self.master_param(n).contiguous() for n in self.params}
+
+    def load_arrays(self, arrays, strict=False):
+        """Copy fp32 arrays into master/shadow (trainable) or the frozen copies."""
+        missing = []
+        with torch.no_grad():
+            for n, p in self.params.items():
+                if n not in arrays:
+                    missing.append(n)
+                    continue
+                src = torch.as_tensor(arrays[n]).to(self.device, torch.float32).reshape(p.shape)
+                found = False
+                for g in self.groups:
+                    for (gn, _, _, numel, shape, cl), off in zip(g.entries, g.offsets):
+                        if gn == n:
+                            g.master[off:off + numel].copy_(self._flat_view(src, cl))
+                            p.data.copy_(src.to(p.dtype))
+                            found = True
+                if not found:
+                    p.data.copy_(src.to(p.dtype))
+        if strict and missing:
+            raise KeyError('missing params: %s' % missing[:10])
+        return missing

@@ -1,0 +1,115 @@
+"""Training step engine.
+
+One step = forward (mode-specific model entry) -> backward -> bucketed all-reduce (overlapped)
+-> fused SGD on flat buffers -> device-side metric accumulation.  No host synchronisation,
+so ``GraphedStep`` can capture the entire step into one hipGraph and replay it (static
+shapes: the detection ops are designed for it).
+"""
+import torch
+
+from ..parallel.reducer import BucketReducer
+from .params import FlatParamStore
+
+
+class Trainer:
+    def __init__(self, model, mode='e2e', fixed_param_prefix=None, lr=0.001, momentum=0.9, wd=0.0005,
+                 clip_gradient=1.0, rescale_grad=1.0, lr_scheduler=None, compute_dtype=None, device=None,
+                 bucket_mb=64, average_grads=False, channels_last=None):
+        dev = torch.device(device) if device is not None else next(model.parameters()).device
+        if compute_dtype is None:
+            compute_dtype = torch.bfloat16 if dev.type == 'cuda' else torch.float32
+        if channels_last is None:
+            channels_last = dev.type == 'cuda'
+        self.device, self.compute_dtype, self.channels_last = dev, compute_dtype, channels_last
+        self.model = model.to(dev)
+        self.mode = mode
+        self.store = FlatParamStore(self.model, fixed_param_prefix, compute_dtype, dev, channels_last)
+        self.reducer = BucketReducer(self.store, bucket_mb=bucket_mb, average=average_grads)
+        self.momentum, self.wd, self.clip, self.rescale = momentum, wd, clip_gradient, rescale_grad
+        self.base_lr = lr
+        self.lr_scheduler = lr_scheduler
+        if lr_scheduler is not None:
+            lr_scheduler.base_lr = lr
+        self.lr_t = torch.full((1,), float(lr), dtype=torch.float32, device=dev)
+        self.num_update = 0
+
+    # ------------------------------------------------------------------
+    def prepare_batch(self, batch):
+        out = {}
+        for k, v in batch.items():
+            if torch.is_tensor(v):
+                v = v.to(self.device, non_blocking=True)
+                if k == 'data':
+                    v = v.to(self.compute_dtype)
+                    if self.channels_last:
+                        v = v.contiguous(memory_format=torch.channels_last)
+            out[k] = v
+        return out
+
+    def forward(self, b):
+        m = self.model
+        if self.mode == 'e2e':
+            return m.train_e2e(b['data'], b['im_info'], b['gt_boxes'], b['n_gt'])
+        if self.mode == 'rpn':
+            return m.train_rpn(b['data'], b['im_info'], b['gt_boxes'], b['n_gt'])
+        if self.mode == 'rcnn':
+            return m.train_rcnn(b['data'], b['rois'], b['label'], b['bbox_target'], b['bbox_inside_weight'],
+                                b['bbox_outside_weight'])
+        raise ValueError(self.mode)
+
+    def step_body(self, b):
+        """The device work of one step (capturable)."""
+        self.store.zero_grad()
+        self.reducer.prepare()
+        out = self.forward(b)
+        out['loss'].backward()
+        self.reducer.finish()
+        self.store.sgd_step(self.lr_t, self.momentum, self.wd, self.rescale, self.clip)
+        return out
+
+    def update_lr(self):
+        self.num_update += 1
+        if self.lr_scheduler is not None:
+            lr = self.lr_scheduler(self.num_update)
+            self.lr_t.fill_(float(lr))
+
+    def step(self, batch):
+        self.model.train()
+        b = self.prepare_batch(batch)
+        self.update_lr()
+        return self.step_body(b)
+
+
+class GraphedStep:
+    """Capture ``trainer.step_body`` for fixed input shapes into a hipGraph and replay it.
+
+    Static input buffers are filled with copies of each new batch (D2D), the LR lives in a
+    device tensor, RNG draws use PyTorch's graph-safe Philox offsets.  Falls back to eager
+    if capture fails (reported, not silent).
+    """
+
+    def __init__(self, trainer, example_batch, warmup=3):
+        self.t = trainer
+        trainer.model.train()
+        self.static = trainer.prepare_batch(example_batch)
+        self.static = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in self.static.items()}
+        s = torch.cuda.Stream()
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                trainer.step_body(self.static)
+        torch.cuda.current_stream().wait_stream(s)
+        torch.cuda.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            self.out = trainer.step_body(self.static)
+        torch.cuda.synchronize()
+
+    def __call__(self, batch=None):
+        if batch is not None:
+            for k, v in batch.items():
+                if torch.is_tensor(v) and k in self.static:
+                    self.static[k].copy_(v, non_blocking=True)
+        self.t.update_lr()
+        self.graph.replay()
+        return self.out

@@ -1,0 +1,297 @@
+// Python bindings for the gfx950 kernels.  Thin: validate shapes/dtypes/devices, allocate
+// outputs through the PyTorch caching allocator, launch on the current HIP stream.  All
+// launches are graph-capturable (no host sync, no allocation inside the launchers).
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPGuard.h>
+
+#include "kernels.h"
+
+namespace {
+
+using at::Tensor;
+
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+#define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
+#define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
+#define CHECK_I32(t) TORCH_CHECK((t).scalar_type() == at::kInt, #t " must be int32")
+#define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
+
+int is_bf16(const Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat, "expected bf16 or fp32 tensor");
+  return t.scalar_type() == at::kBFloat16 ? 1 : 0;
+}
+
+// ---- proposal -------------------------------------------------------------------------
+std::vector<Tensor> proposal_decode(const Tensor& cls, const Tensor& dlt, const Tensor& im_info,
+                                    const Tensor& base_anchors, double feat_stride, double min_size,
+                                    bool crop_to_im, bool is_prob) {
+  CHECK_DEV(cls); CHECK_DEV(dlt); CHECK_DEV(im_info); CHECK_DEV(base_anchors);
+  CHECK_F32(im_info); CHECK_F32(base_anchors); CHECK_CONTIG(im_info); CHECK_CONTIG(base_anchors);
+  TORCH_CHECK(cls.dim() == 4 && dlt.dim() == 4, "cls/dlt must be (B, C, H, W)");
+  const int A = (int)base_anchors.size(0);
+  const int B = (int)cls.size(0), H = (int)cls.size(2), W = (int)cls.size(3);
+  TORCH_CHECK(cls.size(1) == 2 * A, "cls channels must be 2A");
+  TORCH_CHECK(dlt.size(0) == B && dlt.size(1) == 4 * A && dlt.size(2) == H && dlt.size(3) == W, "dlt shape");
+  TORCH_CHECK(im_info.size(0) == B && im_info.size(1) == 3, "im_info must be (B, 3)");
+  c10::hip::HIPGuard g(cls.device());
+  const int64_t N = (int64_t)H * W * A;
+  auto opts = cls.options().dtype(at::kFloat);
+  Tensor boxes = at::empty({B, N, 4}, opts);
+  Tensor keys = at::empty({B, N}, opts);
+  mxr::proposal_decode(cls.data_ptr(), is_bf16(cls), cls.stride(0), cls.stride(1), cls.stride(2), cls.stride(3),
+                       dlt.data_ptr(), is_bf16(dlt), dlt.stride(0), dlt.stride(1), dlt.stride(2), dlt.stride(3),
+                       is_prob ? 1 : 0, im_info.data_ptr<float>(), base_anchors.data_ptr<float>(), A, B, H, W,
+                       (float)feat_stride, (float)min_size, crop_to_im ? 1 : 0, boxes.data_ptr<float>(),
+                       keys.data_ptr<float>(), cur_stream());
+  return {boxes, keys};
+}
+
+// NMS over score-sorted boxes; returns (rois (B,post,5), scores (B,post), keep (B,post) int64, n_keep (B))
+std::vector<Tensor> nms_proposals(const Tensor& boxes, const Tensor& scores, const Tensor& n_valid, double thresh,
+                                  int64_t post, const Tensor& rand_u) {
+  CHECK_DEV(boxes); CHECK_F32(boxes); CHECK_CONTIG(boxes);
+  CHECK_DEV(scores); CHECK_F32(scores); CHECK_CONTIG(scores);
+  CHECK_DEV(n_valid); CHECK_I32(n_valid); CHECK_CONTIG(n_valid);
+  CHECK_DEV(rand_u); CHECK_F32(rand_u); CHECK_CONTIG(rand_u);
+  TORCH_CHECK(boxes.dim() == 3 && boxes.size(2) == 4, "boxes must be (B, P, 4)");
+  const int B = (int)boxes.size(0), P = (int)boxes.size(1);
+  TORCH_CHECK(scores.size(0) == B && scores.size(1) == P, "scores shape");
+  TORCH_CHECK(n_valid.numel() == B, "n_valid shape");
+  TORCH_CHECK(rand_u.numel() == (int64_t)B * post, "rand_u must hold B*post values");
+  TORCH_CHECK(post > 0, "post must be > 0");
+  c10::hip::HIPGuard g(boxes.device());
+  const int nb = (P + 63) / 64;
+  TORCH_CHECK(16 + (int64_t)nb * 8 + post * 4 <= 160 * 1024, "NMS LDS budget exceeded (P or post too large)");
+  auto st = cur_stream();
+  Tensor mask = at::empty({B, P, nb}, boxes.options().dtype(at::kLong));
+  mxr::nms_mask(boxes.data_ptr<float>(), n_valid.data_ptr<int32_t>(), B, P, (float)thresh,
+                reinterpret_cast<uint64_t*>(mask.data_ptr<int64_t>()), st);
+  Tensor rois = at::empty({B, post, 5}, boxes.options());
+  Tensor out_scores = at::empty({B, post}, boxes.options());
+  Tensor keep = at::empty({B, post}, boxes.options().dtype(at::kLong));
+  Tensor n_keep = at::empty({B}, boxes.options().dtype(at::kInt));
+  mxr::nms_reduce(boxes.data_ptr<float>(), scores.data_ptr<float>(), n_valid.data_ptr<int32_t>(),
+                  reinterpret_cast<const uint64_t*>(mask.data_ptr<int64_t>()), B, P, (int)post,
+                  rand_u.data_ptr<float>(), rois.data_ptr<float>(), out_scores.data_ptr<float>(),
+                  keep.data_ptr<int64_t>(), n_keep.data_ptr<int32_t>(), st);
+  return {rois, out_scores, keep, n_keep};
+}
+
+// ---- IoU / assignment ------------------------------------------------------------------
+std::vector<Tensor> iou_max(const Tensor& boxes, int64_t off, const Tensor& gt, const Tensor& n_gt,
+                            bool want_gt_max) {
+  CHECK_DEV(boxes); CHECK_F32(boxes); CHECK_CONTIG(boxes);
+  CHECK_DEV(gt); CHECK_F32(gt); CHECK_CONTIG(gt);
+  CHECK_DEV(n_gt); CHECK_I32(n_gt); CHECK_CONTIG(n_gt);
+  TORCH_CHECK(boxes.dim() == 3 && gt.dim() == 3 && gt.size(2) == 5, "boxes (B,N,bs), gt (B,G,5)");
+  const int B = (int)boxes.size(0), N = (int)boxes.size(1), bs = (int)boxes.size(2), G = (int)gt.size(1);
+  TORCH_CHECK(off + 4 <= bs, "box offset out of range");
+  TORCH_CHECK(gt.size(0) == B && n_gt.numel() == B, "batch mismatch");
+  c10::hip::HIPGuard g(boxes.device());
+  Tensor max_ov = at::empty({B, N}, boxes.options());
+  Tensor argmax = at::empty({B, N}, boxes.options().dtype(at::kInt));
+  Tensor gt_max = want_gt_max ? at::zeros({B, G}, boxes.options()) : Tensor();
+  mxr::iou_max(boxes.data_ptr<float>(), bs, (int)off, B, N, gt.data_ptr<float>(), n_gt.data_ptr<int32_t>(), G,
+               nullptr, max_ov.data_ptr<float>(), argmax.data_ptr<int32_t>(),
+               want_gt_max ? gt_max.data_ptr<float>() : nullptr, cur_stream());
+  if (want_gt_max) return {max_ov, argmax, gt_max};
+  return {max_ov, argmax};
+}
+
+std::vector<Tensor> anchor_target_assign(const Tensor& base_anchors, int64_t H, int64_t W, double feat_stride,
+                                         const Tensor& im_info, int64_t allowed_border, const Tensor& gt,
+                                         const Tensor& n_gt, double neg_thresh, double pos_thresh, bool clobber) {
+  CHECK_DEV(base_anchors); CHECK_F32(base_anchors); CHECK_CONTIG(base_anchors);
+  CHECK_DEV(im_info); CHECK_F32(im_info); CHECK_CONTIG(im_info);
+  CHECK_DEV(gt); CHECK_F32(gt); CHECK_CONTIG(gt);
+  CHECK_DEV(n_gt); CHECK_I32(n_gt); CHECK_CONTIG(n_gt);
+  const int A = (int)base_anchors.size(0), B = (int)gt.size(0), G = (int)gt.size(1);
+  TORCH_CHECK(im_info.size(0) == B && n_gt.numel() == B, "batch mismatch");
+  c10::hip::HIPGuard g(gt.device());
+  const int64_t N = H * W * A;
+  auto o = gt.options();
+  Tensor max_ov = at::empty({B, N}, o);
+  Tensor argmax = at::empty({B, N}, o.dtype(at::kInt));
+  Tensor gt_max = at::zeros({B, std::max(G, 1)}, o);
+  Tensor label = at::empty({B, N}, o.dtype(at::kInt));
+  Tensor targets = at::empty({B, N, 4}, o);
+  mxr::anchor_target_assign(base_anchors.data_ptr<float>(), A, (int)H, (int)W, (float)feat_stride,
+                            im_info.data_ptr<float>(), (int)allowed_border, gt.data_ptr<float>(),
+                            n_gt.data_ptr<int32_t>(), G, B, (float)neg_thresh, (float)pos_thresh, clobber ? 1 : 0,
+                            max_ov.data_ptr<float>(), argmax.data_ptr<int32_t>(), gt_max.data_ptr<float>(),
+                            label.data_ptr<int32_t>(), targets.data_ptr<float>(), cur_stream());
+  return {label, targets, max_ov, argmax};
+}
+
+// ---- RoI pooling -----------------------------------------------------------------------
+// feat must be channels-last in memory: logical (B, C, H, W) with NHWC strides.
+std::vector<Tensor> roi_pool_fwd(const Tensor& feat, const Tensor& rois, int64_t PH, int64_t PW, double scale) {
+  CHECK_DEV(feat); CHECK_DEV(rois); CHECK_F32(rois); CHECK_CONTIG(rois);
+  TORCH_CHECK(feat.dim() == 4 && feat.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "feat must be (B,C,H,W) channels_last");
+  TORCH_CHECK(rois.dim() == 2 && rois.size(1) == 5, "rois must be (R, 5)");
+  const int B = (int)feat.size(0), C = (int)feat.size(1), H = (int)feat.size(2), W = (int)feat.size(3);
+  const int R = (int)rois.size(0);
+  c10::hip::HIPGuard g(feat.device());
+  Tensor out = at::empty({R, C, PH, PW}, feat.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor argmax = at::empty({R, C, PH, PW}, feat.options().dtype(at::kInt).memory_format(at::MemoryFormat::ChannelsLast));
+  mxr::roi_pool_fwd(feat.data_ptr(), is_bf16(feat), B, H, W, C, rois.data_ptr<float>(), R, (int)PH, (int)PW,
+                    (float)scale, out.data_ptr(), argmax.data_ptr<int32_t>(), cur_stream());
+  return {out, argmax};
+}
+
+Tensor roi_pool_bwd(const Tensor& grad_out, const Tensor& argmax, const Tensor& rois, int64_t B, int64_t H,
+                    int64_t W) {
+  CHECK_DEV(grad_out); CHECK_DEV(argmax); CHECK_I32(argmax); CHECK_DEV(rois); CHECK_F32(rois);
+  const int R = (int)grad_out.size(0), C = (int)grad_out.size(1), PH = (int)grad_out.size(2), PW = (int)grad_out.size(3);
+  Tensor go = grad_out.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(argmax.is_contiguous(at::MemoryFormat::ChannelsLast), "argmax must be channels_last");
+  c10::hip::HIPGuard g(grad_out.device());
+  auto st = cur_stream();
+  Tensor gin32 = at::zeros({B, C, H, W}, grad_out.options().dtype(at::kFloat).memory_format(at::MemoryFormat::ChannelsLast));
+  mxr::roi_pool_bwd(go.data_ptr(), is_bf16(go), argmax.data_ptr<int32_t>(), rois.contiguous().data_ptr<float>(), R,
+                    PH, PW, (int)B, (int)H, (int)W, C, gin32.data_ptr<float>(), st);
+  if (grad_out.scalar_type() == at::kFloat) return gin32;
+  Tensor gin = at::empty({B, C, H, W}, grad_out.options().memory_format(at::MemoryFormat::ChannelsLast));
+  mxr::cast_f32(gin32.data_ptr<float>(), gin.data_ptr(), 1, gin.numel(), st);
+  return gin;
+}
+
+// ---- losses ----------------------------------------------------------------------------
+// returns (grad like logits, loss_sum (1,), prob_fg (B, H*W*A) in (h, w, a) order)
+std::vector<Tensor> rpn_softmax_ce(const Tensor& logits, const Tensor& label, const Tensor& norm, double grad_scale,
+                                   bool want_prob) {
+  CHECK_DEV(logits); CHECK_DEV(label); CHECK_I32(label); CHECK_CONTIG(label); CHECK_DEV(norm); CHECK_F32(norm);
+  const int B = (int)logits.size(0), C2 = (int)logits.size(1), H = (int)logits.size(2), W = (int)logits.size(3);
+  TORCH_CHECK(C2 % 2 == 0, "logits channels must be 2A");
+  const int A = C2 / 2;
+  TORCH_CHECK(label.numel() == (int64_t)B * A * H * W, "label must be (B, A*H*W)");
+  c10::hip::HIPGuard g(logits.device());
+  Tensor grad = at::empty_like(logits);
+  TORCH_CHECK(grad.strides() == logits.strides(), "grad layout must match logits");
+  Tensor loss = at::zeros({1}, logits.options().dtype(at::kFloat));
+  Tensor prob = want_prob ? at::empty({B, (int64_t)H * W * A}, logits.options().dtype(at::kFloat)) : Tensor();
+  mxr::rpn_softmax_ce(logits.data_ptr(), is_bf16(logits), logits.stride(0), logits.stride(1), logits.stride(2),
+                      logits.stride(3), label.data_ptr<int32_t>(), B, A, H, W, norm.data_ptr<float>(),
+                      (float)grad_scale, grad.data_ptr(), loss.data_ptr<float>(),
+                      want_prob ? prob.data_ptr<float>() : nullptr, cur_stream());
+  if (want_prob) return {grad, loss, prob};
+  return {grad, loss};
+}
+
+// returns (grad (R,C) like logits, prob (R,C) fp32, loss_sum (1,))
+std::vector<Tensor> row_softmax_ce(const Tensor& logits, const Tensor& label, double norm, double grad_scale,
+                                   bool want_grad) {
+  CHECK_DEV(logits); CHECK_CONTIG(logits); CHECK_DEV(label); CHECK_I32(label); CHECK_CONTIG(label);
+  TORCH_CHECK(logits.dim() == 2, "logits must be (R, C)");
+  const int R = (int)logits.size(0), C = (int)logits.size(1);
+  TORCH_CHECK(label.numel() == R, "label must be (R,)");
+  c10::hip::HIPGuard g(logits.device());
+  Tensor grad = want_grad ? at::empty_like(logits) : Tensor();
+  Tensor prob = at::empty({R, C}, logits.options().dtype(at::kFloat));
+  Tensor loss = at::zeros({1}, logits.options().dtype(at::kFloat));
+  mxr::row_softmax_ce(logits.data_ptr(), is_bf16(logits), R, C, label.data_ptr<int32_t>(), (float)norm,
+                      (float)grad_scale, want_grad ? grad.data_ptr() : nullptr, prob.data_ptr<float>(),
+                      loss.data_ptr<float>(), cur_stream());
+  if (want_grad) return {grad, prob, loss};
+  return {prob, loss};
+}
+
+// pred (n0,n1,n2,n3) any strides; tgt/in_w/out_w contiguous fp32 of the same logical shape.
+std::vector<Tensor> smooth_l1(const Tensor& pred, const Tensor& tgt, const Tensor& in_w, const Tensor& out_w,
+                              double sigma, double grad_scale) {
+  CHECK_DEV(pred); CHECK_DEV(tgt); CHECK_F32(tgt); CHECK_CONTIG(tgt);
+  CHECK_F32(in_w); CHECK_CONTIG(in_w); CHECK_F32(out_w); CHECK_CONTIG(out_w);
+  TORCH_CHECK(pred.dim() <= 4, "pred rank must be <= 4");
+  Tensor p4 = pred;
+  while (p4.dim() < 4) p4 = p4.unsqueeze(0);
+  TORCH_CHECK(tgt.numel() == p4.numel() && in_w.numel() == p4.numel() && out_w.numel() == p4.numel(),
+              "target/weights must match pred");
+  c10::hip::HIPGuard g(pred.device());
+  Tensor grad = at::empty_like(pred);
+  Tensor g4 = grad;
+  while (g4.dim() < 4) g4 = g4.unsqueeze(0);
+  TORCH_CHECK(g4.strides() == p4.strides(), "grad layout must match pred");
+  Tensor loss = at::zeros({1}, pred.options().dtype(at::kFloat));
+  mxr::smooth_l1(p4.data_ptr(), is_bf16(p4), p4.stride(0), p4.stride(1), p4.stride(2), p4.stride(3), (int)p4.size(0),
+                 (int)p4.size(1), (int)p4.size(2), (int)p4.size(3), tgt.data_ptr<float>(), in_w.data_ptr<float>(),
+                 out_w.data_ptr<float>(), (float)sigma, (float)grad_scale, g4.data_ptr(), loss.data_ptr<float>(),
+                 cur_stream());
+  return {grad, loss};
+}
+
+// ---- optimizer -------------------------------------------------------------------------
+void sgd_momentum(Tensor w, Tensor mom, const Tensor& grad, const Tensor& lr, double momentum, double wd,
+                  double rescale, double clip, c10::optional<Tensor> w_bf16) {
+  CHECK_DEV(w); CHECK_F32(w); CHECK_CONTIG(w); CHECK_DEV(mom); CHECK_F32(mom); CHECK_CONTIG(mom);
+  CHECK_DEV(grad); CHECK_CONTIG(grad); CHECK_DEV(lr); CHECK_F32(lr);
+  TORCH_CHECK(w.numel() == mom.numel() && w.numel() == grad.numel(), "size mismatch");
+  uint16_t* wb = nullptr;
+  if (w_bf16.has_value() && w_bf16->defined()) {
+    TORCH_CHECK(w_bf16->scalar_type() == at::kBFloat16 && w_bf16->is_contiguous() && w_bf16->numel() == w.numel(),
+                "w_bf16 must be contiguous bf16 of the same size");
+    wb = reinterpret_cast<uint16_t*>(w_bf16->data_ptr());
+  }
+  c10::hip::HIPGuard g(w.device());
+  mxr::sgd_momentum(w.data_ptr<float>(), mom.data_ptr<float>(), grad.data_ptr(), is_bf16(grad), w.numel(),
+                    lr.data_ptr<float>(), (float)momentum, (float)wd, (float)rescale, (float)clip, wb, cur_stream());
+}
+
+// ---- BN + ReLU -------------------------------------------------------------------------
+Tensor bn_relu_fwd(const Tensor& x, const Tensor& gamma, const Tensor& beta, const Tensor& mean, const Tensor& var,
+                   double eps, bool fix_gamma, bool relu) {
+  CHECK_DEV(x);
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "x must be channels_last 4-D");
+  const int C = (int)x.size(1);
+  TORCH_CHECK(C % 4 == 0, "C must be a multiple of 4");
+  for (auto* t : {&gamma, &beta, &mean, &var}) {
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == C, "BN params fp32 (C,)");
+  }
+  c10::hip::HIPGuard g(x.device());
+  Tensor y = at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast);
+  mxr::bn_relu_fwd(x.data_ptr(), is_bf16(x), x.numel() / C, C, gamma.data_ptr<float>(), beta.data_ptr<float>(),
+                   mean.data_ptr<float>(), var.data_ptr<float>(), (float)eps, fix_gamma ? 1 : 0, relu ? 1 : 0,
+                   y.data_ptr(), cur_stream());
+  return y;
+}
+
+std::vector<Tensor> bn_relu_bwd(const Tensor& x, const Tensor& dy, const Tensor& gamma, const Tensor& beta,
+                                const Tensor& mean, const Tensor& var, double eps, bool fix_gamma, bool relu,
+                                bool need_dx, bool need_params) {
+  CHECK_DEV(x); CHECK_DEV(dy);
+  TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "x must be channels_last");
+  Tensor g = dy.contiguous(at::MemoryFormat::ChannelsLast);
+  TORCH_CHECK(g.scalar_type() == x.scalar_type(), "dy dtype must match x");
+  const int C = (int)x.size(1);
+  c10::hip::HIPGuard guard(x.device());
+  Tensor dx = need_dx ? at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast) : Tensor();
+  Tensor dgamma = need_params ? at::zeros({C}, x.options().dtype(at::kFloat)) : Tensor();
+  Tensor dbeta = need_params ? at::zeros({C}, x.options().dtype(at::kFloat)) : Tensor();
+  mxr::bn_relu_bwd(x.data_ptr(), g.data_ptr(), is_bf16(x), x.numel() / C, C, gamma.data_ptr<float>(),
+                   beta.data_ptr<float>(), mean.data_ptr<float>(), var.data_ptr<float>(), (float)eps,
+                   fix_gamma ? 1 : 0, relu ? 1 : 0, need_dx ? dx.data_ptr() : nullptr,
+                   need_params ? dgamma.data_ptr<float>() : nullptr, need_params ? dbeta.data_ptr<float>() : nullptr,
+                   cur_stream());
+  return {dx, dgamma, dbeta};
+}
+
+}  // namespace
+
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
+  m.doc() = "mx_rcnn_amd gfx950 kernels";
+  m.def("proposal_decode", &proposal_decode);
+  m.def("nms_proposals", &nms_proposals);
+  m.def("iou_max", &iou_max);
+  m.def("anchor_target_assign", &anchor_target_assign);
+  m.def("roi_pool_fwd", &roi_pool_fwd);
+  m.def("roi_pool_bwd", &roi_pool_bwd);
+  m.def("rpn_softmax_ce", &rpn_softmax_ce);
+  m.def("row_softmax_ce", &row_softmax_ce);
+  m.def("smooth_l1", &smooth_l1);
+  m.def("sgd_momentum", &sgd_momentum);
+  m.def("bn_relu_fwd", &bn_relu_fwd);
+  m.def("bn_relu_bwd", &bn_relu_bwd);
+  m.attr("arch") = "gfx950";
+}

@@ -1,0 +1,128 @@
+// Frozen ("use_global_stats") BatchNorm + ReLU on channels-last activations (SURVEY K13;
+// reference pre-activation units `rcnn/resnet.py:27-54` with bn_global=True: stages 1-3).
+// Forward folds mean/var/gamma/beta into one scale+shift per channel on the fly; backward
+// recomputes the ReLU mask from x (nothing saved but x) and reduces dgamma/dbeta per channel
+// with per-thread register partials (each thread owns a fixed channel quad because the grid
+// size is a multiple of C/4), then one atomic per thread.  16-B bf16 loads (8 channels) are
+// not used because ResNet C4 channel counts are all multiples of 4 but stage widths start
+// at 64, where 4-wide keeps a whole row per 16 lanes.
+#include "common.h"
+#include "../kernels.h"
+#include <algorithm>
+
+namespace mxr {
+
+struct BnQuad {
+  float s[4], t[4];
+};
+
+__device__ __forceinline__ void bn_coeffs(int c, const float* gamma, const float* beta, const float* mean,
+                                          const float* var, float eps, int fix_gamma, float& s, float& t) {
+  const float inv = rsqrtf(var[c] + eps);
+  const float g = fix_gamma ? 1.f : gamma[c];
+  s = g * inv;
+  t = beta[c] - mean[c] * s;
+}
+
+__device__ __forceinline__ void load4(const void* p, int64_t i, int bf16, float v[4]) {
+  if (bf16) {
+    const ushort4 u = *reinterpret_cast<const ushort4*>(static_cast<const uint16_t*>(p) + i);
+    v[0] = bf16_to_f32(u.x); v[1] = bf16_to_f32(u.y); v[2] = bf16_to_f32(u.z); v[3] = bf16_to_f32(u.w);
+  } else {
+    const float4 f = *reinterpret_cast<const float4*>(static_cast<const float*>(p) + i);
+    v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+  }
+}
+__device__ __forceinline__ void store4(void* p, int64_t i, int bf16, const float v[4]) {
+  if (bf16)
+    *reinterpret_cast<ushort4*>(static_cast<uint16_t*>(p) + i) =
+        make_ushort4(f32_to_bf16(v[0]), f32_to_bf16(v[1]), f32_to_bf16(v[2]), f32_to_bf16(v[3]));
+  else
+    *reinterpret_cast<float4*>(static_cast<float*>(p) + i) = make_float4(v[0], v[1], v[2], v[3]);
+}
+
+__global__ void __launch_bounds__(256)
+bn_relu_fwd_kernel(const void* __restrict__ x, int bf16, int64_t M, int C, const float* __restrict__ gamma,
+                   const float* __restrict__ beta, const float* __restrict__ mean, const float* __restrict__ var,
+                   float eps, int fix_gamma, int relu, void* __restrict__ y) {
+  const int CV = C >> 2;
+  const int64_t T = (int64_t)gridDim.x * blockDim.x;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cv = (int)(tid % CV);  // fixed per thread: T % CV == 0
+  float s[4], t[4];
+  for (int k = 0; k < 4; ++k) bn_coeffs(cv * 4 + k, gamma, beta, mean, var, eps, fix_gamma, s[k], t[k]);
+  const int64_t total = M * CV;
+  for (int64_t e = tid; e < total; e += T) {
+    float v[4];
+    load4(x, e * 4, bf16, v);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[k] = v[k] * s[k] + t[k];
+      if (relu) v[k] = fmaxf(v[k], 0.f);
+    }
+    store4(y, e * 4, bf16, v);
+  }
+}
+
+__global__ void __launch_bounds__(256)
+bn_relu_bwd_kernel(const void* __restrict__ x, const void* __restrict__ dy, int bf16, int64_t M, int C,
+                   const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ mean,
+                   const float* __restrict__ var, float eps, int fix_gamma, int relu, void* __restrict__ dx,
+                   float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  const int CV = C >> 2;
+  const int64_t T = (int64_t)gridDim.x * blockDim.x;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int cv = (int)(tid % CV);
+  float s[4], t[4], inv[4], mu[4];
+  for (int k = 0; k < 4; ++k) {
+    const int c = cv * 4 + k;
+    bn_coeffs(c, gamma, beta, mean, var, eps, fix_gamma, s[k], t[k]);
+    inv[k] = rsqrtf(var[c] + eps);
+    mu[k] = mean[c];
+  }
+  float ag[4] = {0.f, 0.f, 0.f, 0.f}, ab[4] = {0.f, 0.f, 0.f, 0.f};
+  const int64_t total = M * CV;
+  for (int64_t e = tid; e < total; e += T) {
+    float xv[4], g[4];
+    load4(x, e * 4, bf16, xv);
+    load4(dy, e * 4, bf16, g);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float pre = xv[k] * s[k] + t[k];
+      const float gm = (!relu || pre > 0.f) ? g[k] : 0.f;
+      ab[k] += gm;
+      ag[k] += gm * (xv[k] - mu[k]) * inv[k];
+      g[k] = gm * s[k];
+    }
+    if (dx) store4(dx, e * 4, bf16, g);
+  }
+  if (dgamma && !fix_gamma)
+    for (int k = 0; k < 4; ++k) if (ag[k] != 0.f) atomicAdd(dgamma + cv * 4 + k, ag[k]);
+  if (dbeta)
+    for (int k = 0; k < 4; ++k) if (ab[k] != 0.f) atomicAdd(dbeta + cv * 4 + k, ab[k]);
+}
+
+static int bn_grid(int64_t M, int C) {
+  const int CV = C >> 2;
+  // threads must be a multiple of CV so each thread keeps one channel quad
+  int64_t want = std::min<int64_t>((M * CV + 255) / 256, 1024);
+  int64_t blocks = std::max<int64_t>(want, 1);
+  while ((blocks * 256) % CV != 0) ++blocks;
+  return (int)blocks;
+}
+
+void bn_relu_fwd(const void* x, int bf16, int64_t M, int C, const float* gamma, const float* beta, const float* mean,
+                 const float* var, float eps, int fix_gamma, int relu, void* y, hipStream_t st) {
+  if (M == 0 || C == 0) return;
+  bn_relu_fwd_kernel<<<bn_grid(M, C), 256, 0, st>>>(x, bf16, M, C, gamma, beta, mean, var, eps, fix_gamma, relu, y);
+}
+
+void bn_relu_bwd(const void* x, const void* dy, int bf16, int64_t M, int C, const float* gamma, const float* beta,
+                 const float* mean, const float* var, float eps, int fix_gamma, int relu, void* dx, float* dgamma,
+                 float* dbeta, hipStream_t st) {
+  if (M == 0 || C == 0) return;
+  bn_relu_bwd_kernel<<<bn_grid(M, C), 256, 0, st>>>(x, dy, bf16, M, C, gamma, beta, mean, var, eps, fix_gamma, relu,
+                                                    dx, dgamma, dbeta);
+}
+
+}  // namespace mxr

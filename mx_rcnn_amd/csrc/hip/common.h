@@ -1,0 +1,51 @@
+// Shared device helpers for the gfx950 kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <cstdint>
+#include <cfloat>
+
+#define MXR_WAVE 64
+
+namespace mxr {
+
+__device__ __forceinline__ float bf16_to_f32(uint16_t v) {
+  return __uint_as_float(static_cast<uint32_t>(v) << 16);
+}
+__device__ __forceinline__ uint16_t f32_to_bf16(float f) {
+  __hip_bfloat16 h = __float2bfloat16(f);  // v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
+  return *reinterpret_cast<uint16_t*>(&h);
+}
+__device__ __forceinline__ float ld(const void* p, int64_t i, int bf16) {
+  return bf16 ? bf16_to_f32(static_cast<const uint16_t*>(p)[i]) : static_cast<const float*>(p)[i];
+}
+__device__ __forceinline__ void st(void* p, int64_t i, float v, int bf16) {
+  if (bf16) static_cast<uint16_t*>(p)[i] = f32_to_bf16(v);
+  else static_cast<float*>(p)[i] = v;
+}
+
+// Wave64 reduction (sum) via DPP-backed shuffles.
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Box IoU with the +1 pixel convention (reference: bbox_overlaps / nms).
+__device__ __forceinline__ float iou_plus1(float ax1, float ay1, float ax2, float ay2, float aarea,
+                                           float bx1, float by1, float bx2, float by2, float barea) {
+  float iw = fminf(ax2, bx2) - fmaxf(ax1, bx1) + 1.f;
+  float ih = fminf(ay2, by2) - fmaxf(ay1, by1) + 1.f;
+  if (iw <= 0.f || ih <= 0.f) return 0.f;
+  float inter = iw * ih;
+  return inter / (aarea + barea - inter);
+}
+
+inline int div_up(int64_t a, int64_t b) { return static_cast<int>((a + b - 1) / b); }
+
+}  // namespace mxr

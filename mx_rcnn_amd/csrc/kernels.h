@@ -1,0 +1,95 @@
+// Launcher declarations for the hand-written gfx950 kernels.
+// Every launcher is asynchronous on the given HIP stream, never allocates,
+// never synchronises (so a caller may capture it into a hipGraph).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace mxr {
+
+// ---- proposal (proposal.hip) ----------------------------------------------
+// Fused RPN fg-softmax + anchor enumeration + delta decode + clip + min-size.
+// cls  : logits, element (b, c, h, w) at cls[b*cs0 + c*cs1 + h*cs2 + w*cs3], c in [0, 2A)
+// dlt  : deltas, element (b, c, h, w) at dlt[b*ds0 + ...], c in [0, 4A)
+// is_prob: cls already holds softmax probabilities (test graph) instead of logits.
+// Writes boxes (B, N, 4) and keys (B, N) where N = Hc*Wc*A, order (h*Wc+w)*A+a.
+// Filtered boxes get key = -inf.  Hc/Wc are per-image crops (device arrays, may be null).
+void proposal_decode(const void* cls, int cls_bf16, int64_t cs0, int64_t cs1, int64_t cs2, int64_t cs3,
+                     const void* dlt, int dlt_bf16, int64_t ds0, int64_t ds1, int64_t ds2, int64_t ds3,
+                     int is_prob, const float* im_info, const float* base_anchors, int A,
+                     int B, int H, int W, float feat_stride, float min_size,
+                     int crop_to_im, float* boxes, float* keys, hipStream_t st);
+
+// ---- NMS (nms.hip) ----------------------------------------------------------
+// boxes (B, P, 4) sorted by descending score, n_valid (B) int32 on device.
+// mask workspace: B * P * ceil(P/64) uint64.
+void nms_mask(const float* boxes, const int32_t* n_valid, int B, int P, float thresh,
+              uint64_t* mask, hipStream_t st);
+// Greedy reduction + output assembly: keep up to `post` boxes per image; slots
+// beyond the kept count are filled with keep[floor(u * n_keep)] (rand u in [0,1)).
+// rois (B, post, 5) = [b, x1, y1, x2, y2], out_scores (B, post), n_keep (B).
+void nms_reduce(const float* boxes, const float* scores, const int32_t* n_valid, const uint64_t* mask,
+                int B, int P, int post, const float* rand_u, float* rois, float* out_scores,
+                int64_t* keep_idx, int32_t* n_keep, hipStream_t st);
+
+// ---- IoU / target assignment (assign.hip) ----------------------------------
+// boxes (B, N, bs) with box at [off..off+4), gt (B, G, 5) padded with -1 rows, n_gt (B).
+// max_ov (B, N) fp32, argmax (B, N) int32 (0 when no gt), gt_max (B, G) fp32 (may be null,
+// must be zeroed by caller; filled by atomicMax over rows where row_mask != 0 or row_mask null).
+void iou_max(const float* boxes, int bs, int off, int B, int N, const float* gt, const int32_t* n_gt, int G,
+             const uint8_t* row_mask, float* max_ov, int32_t* argmax, float* gt_max, hipStream_t st);
+
+// Anchor target labels (pre-sampling) + regression targets for all anchors of a (H, W, A) grid.
+// label (B, N) int32 in {-1, 0, 1}, N = H*W*A in (h, w, a) order; targets (B, N, 4).
+void anchor_target_assign(const float* base_anchors, int A, int H, int W, float feat_stride,
+                          const float* im_info, int allowed_border,
+                          const float* gt, const int32_t* n_gt, int G, int B,
+                          float neg_thresh, float pos_thresh, int clobber_positives,
+                          float* max_ov, int32_t* argmax, float* gt_max,
+                          int32_t* label, float* targets, hipStream_t st);
+
+// ---- RoI pooling (roi_pool.hip) -------------------------------------------
+// feat NHWC (B, H, W, C) bf16 or fp32; rois (R, 5); out (R, PH, PW, C); argmax (R, PH, PW, C) int32
+// holding h*W + w (or -1).
+void roi_pool_fwd(const void* feat, int bf16, int B, int H, int W, int C, const float* rois, int R,
+                  int PH, int PW, float spatial_scale, void* out, int32_t* argmax, hipStream_t st);
+// grad_in fp32 NHWC (B, H, W, C), must be zeroed; grad_out (R, PH, PW, C) bf16/fp32.
+void roi_pool_bwd(const void* grad_out, int bf16, const int32_t* argmax, const float* rois, int R,
+                  int PH, int PW, int B, int H, int W, int C, float* grad_in, hipStream_t st);
+// fp32 -> bf16 / fp32 copy-convert helper (n elements)
+void cast_f32(const float* in, void* out, int out_bf16, int64_t n, hipStream_t st);
+
+// ---- losses (losses.hip) ---------------------------------------------------
+// RPN 2-class softmax CE with ignore label -1 ("valid" normalisation).
+// logits (B, 2A, H, W) strided; label (B, A*H*W) int32 in (a, h, w) order.
+// grad written with the same strides as logits; loss_sum[0] += sum of -log p.
+// norm: device float* with the divisor (number of valid labels), read in-kernel.
+void rpn_softmax_ce(const void* logits, int bf16, int64_t s0, int64_t s1, int64_t s2, int64_t s3,
+                    const int32_t* label, int B, int A, int H, int W, const float* norm, float grad_scale,
+                    void* grad, float* loss_sum, float* prob_fg, hipStream_t st);
+// Row softmax CE for (R, C) logits, labels int32 (R), ignore < 0; normalisation divisor `norm`.
+void row_softmax_ce(const void* logits, int bf16, int R, int C, const int32_t* label, float norm,
+                    float grad_scale, void* grad, float* prob, float* loss_sum, hipStream_t st);
+// Weighted smooth-L1: out_w * f(in_w * (pred - tgt)), sigma; grad = gs * out_w * f'(.) * in_w.
+// pred strided 4-D (n0, n1, n2, n3); tgt/in_w/out_w contiguous 4-D of the same logical shape.
+void smooth_l1(const void* pred, int bf16, int64_t s0, int64_t s1, int64_t s2, int64_t s3,
+               int n0, int n1, int n2, int n3, const float* tgt, const float* in_w, const float* out_w,
+               float sigma, float grad_scale, void* grad, float* loss_sum, hipStream_t st);
+
+// ---- optimizer (sgd.hip) ---------------------------------------------------
+// MXNet SGD semantics: g = clip(rescale*g, +-clip) (clip<=0: off); mom = mu*mom - lr*(g + wd*w); w += mom.
+// grad fp32 or bf16; lr read from device pointer; optional bf16 shadow copy of w.
+void sgd_momentum(float* w, float* mom, const void* grad, int grad_bf16, int64_t n, const float* lr,
+                  float momentum, float wd, float rescale, float clip, uint16_t* w_bf16, hipStream_t st);
+
+// ---- frozen BN + ReLU (bn_act.hip) -----------------------------------------
+// NHWC x (M rows, C channels) bf16/fp32; y = relu((x-mean)*rsqrt(var+eps)*gamma + beta).
+void bn_relu_fwd(const void* x, int bf16, int64_t M, int C, const float* gamma, const float* beta,
+                 const float* mean, const float* var, float eps, int fix_gamma, int relu, void* y,
+                 hipStream_t st);
+// dx = dy * [y>0] * s;  dgamma += sum(dy*[y>0]*xhat), dbeta += sum(dy*[y>0]) (fp32, zeroed by caller)
+void bn_relu_bwd(const void* x, const void* dy, int bf16, int64_t M, int C, const float* gamma,
+                 const float* beta, const float* mean, const float* var, float eps, int fix_gamma, int relu,
+                 void* dx, float* dgamma, float* dbeta, hipStream_t st);
+
+}  // namespace mxr

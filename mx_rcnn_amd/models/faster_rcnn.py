@@ -1,0 +1,186 @@
+"""Faster R-CNN / Fast R-CNN / RPN model (reference graph builders `rcnn/symbol.py:164-386`,
+`rcnn/resnet.py:67-193`), one nn.Module per network with mode-specific entry points
+instead of seven separate symbols:
+
+* ``train_e2e``   approximate-joint end-to-end training (`get_faster_rcnn`, resnet is_train)
+* ``train_rpn``   RPN-only training (`get_vgg_rpn`)
+* ``train_rcnn``  Fast R-CNN on given RoIs (`get_vgg_rcnn`)
+* ``rpn_test``    RPN proposals (`get_vgg_rpn_test`)
+* ``detect``      Faster R-CNN test (`get_vgg_test`, resnet test) or, with ``rois``,
+                  Fast R-CNN test (`get_vgg_rcnn_test`)
+
+All detection stages run on the device with static shapes: anchor target, proposal,
+proposal target and RoIPool are HIP kernels; no host synchronisation in a training step,
+so the whole step can be captured in a hipGraph (core/graph.py).  Images per device may be
+> 1 (the reference is limited to 1: `rcnn/rpn/proposal.py:194`).
+"""
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..config import config as _global_cfg, snapshot
+from ..ops import anchor_target, proposal, proposal_target, roi_pool
+from ..ops.losses import rpn_softmax_ce, smooth_l1, softmax_ce
+from .layers import Conv
+from .resnet import ResNetHead, ResNetTrunk
+from .vgg import VGG16Trunk, VGGHead
+
+VGG_SCALES = (8, 16, 32)
+RESNET_SCALES = (4, 8, 16, 32)
+RATIOS = (0.5, 1, 2)
+
+
+class RPNHead(nn.Module):
+    def __init__(self, in_channels, num_anchors, mid=512):
+        super().__init__()
+        self.rpn_conv_3x3 = Conv('rpn_conv_3x3', in_channels, mid, 3, 1, 1)
+        self.rpn_cls_score = Conv('rpn_cls_score', mid, 2 * num_anchors, 1, 1, 0)
+        self.rpn_bbox_pred = Conv('rpn_bbox_pred', mid, 4 * num_anchors, 1, 1, 0)
+        # reference init for new layers (train_end2end.py:62-78): N(0,.01), N(0,.001) for bbox
+        nn.init.normal_(self.rpn_conv_3x3.weight, 0, 0.01)
+        nn.init.normal_(self.rpn_cls_score.weight, 0, 0.01)
+        nn.init.normal_(self.rpn_bbox_pred.weight, 0, 0.001)
+
+    def forward(self, feat):
+        x = F.relu(self.rpn_conv_3x3(feat), inplace=True)
+        return self.rpn_cls_score(x), self.rpn_bbox_pred(x)
+
+
+class FasterRCNN(nn.Module):
+    def __init__(self, network='vgg16', num_classes=21, cfg=None, bn_mom=0.99, num_anchors=None,
+                 anchor_scales=None, anchor_ratios=RATIOS):
+        super().__init__()
+        self.cfg = cfg if cfg is not None else snapshot()
+        self.network = network
+        self.num_classes = num_classes
+        if network == 'vgg16' or network == 'vgg':
+            self.trunk = VGG16Trunk()
+            self.head = VGGHead(num_classes)
+            self.anchor_scales = tuple(anchor_scales or VGG_SCALES)
+        elif network.startswith('resnet'):
+            depth = int(network.replace('resnet', '').replace('-', '').replace('_', ''))
+            self.trunk = ResNetTrunk(depth, bn_mom=bn_mom)
+            self.head = ResNetHead(num_classes, depth, bn_mom=bn_mom)
+            self.anchor_scales = tuple(anchor_scales or RESNET_SCALES)
+            # random-init stand-in for pretrained weights: MSRA on the branch convs, small
+            # residual-branch outputs (conv3 / shortcut) so 100+ pre-activation units stay bounded
+            for mod in (self.trunk, self.head.stage4):
+                for m in mod.modules():
+                    if isinstance(m, Conv):
+                        if m.mx_name.endswith('_conv3') or m.mx_name.endswith('_sc'):
+                            nn.init.normal_(m.weight, 0, 0.01)
+                        else:
+                            nn.init.kaiming_normal_(m.weight, nonlinearity='relu')
+        else:
+            raise ValueError('unknown network %r' % network)
+        self.anchor_ratios = tuple(anchor_ratios)
+        self.num_anchors = num_anchors or len(self.anchor_scales) * len(self.anchor_ratios)
+        self.feat_stride = 16
+        self.rpn = RPNHead(self.trunk.out_channels, self.num_anchors)
+        nn.init.normal_(self.head.cls_score.weight, 0, 0.01)
+        nn.init.normal_(self.head.bbox_pred.weight, 0, 0.01)
+        if network.startswith('vgg'):
+            nn.init.normal_(self.head.fc6.weight, 0, 0.005)
+            nn.init.normal_(self.head.fc7.weight, 0, 0.005)
+
+    # ------------------------------------------------------------------ naming / params
+    def mx_layers(self):
+        for m in self.modules():
+            if hasattr(m, 'mx_args'):
+                yield m
+
+    def arg_params(self):
+        out = {}
+        for m in self.mx_layers():
+            out.update(m.mx_args())
+        return out
+
+    def aux_params(self):
+        out = {}
+        for m in self.mx_layers():
+            out.update(m.mx_aux())
+        return out
+
+    def feat_shape(self, h, w):
+        return self.trunk.feat_shape(h, w)
+
+    # ------------------------------------------------------------------ pieces
+    def _proposal(self, rpn_cls, rpn_bbox, im_info, key, is_prob=False):
+        c = self.cfg[key]
+        return proposal(rpn_cls.detach(), rpn_bbox.detach(), im_info, self.feat_stride, self.anchor_scales,
+                        self.anchor_ratios, c.RPN_PRE_NMS_TOP_N, c.RPN_POST_NMS_TOP_N, c.RPN_NMS_THRESH,
+                        c.RPN_MIN_SIZE, is_train=(key == 'TRAIN'), is_prob=is_prob)
+
+    def _rpn_losses(self, rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt):
+        H, W = rpn_cls.shape[2], rpn_cls.shape[3]
+        at = anchor_target((H, W), gt_boxes, n_gt, im_info, self.feat_stride, self.anchor_scales,
+                           self.anchor_ratios, allowed_border=0, cfg=self.cfg)
+        cls_loss = rpn_softmax_ce(rpn_cls, at['label'])
+        bbox_loss = smooth_l1(rpn_bbox, at['bbox_target'], at['bbox_inside_weight'], at['bbox_outside_weight'],
+                              sigma=3.0, grad_scale=1.0)
+        return cls_loss, bbox_loss, at
+
+    def _head_losses(self, cls_score, bbox_pred, label, bbox_target, inside, outside):
+        cls_loss, cls_prob = softmax_ce(cls_score, label, 'batch')
+        bbox_loss = smooth_l1(bbox_pred, bbox_target, inside, outside, sigma=1.0,
+                              grad_scale=1.0 / float(self.cfg.TRAIN.BATCH_SIZE))
+        return cls_loss, bbox_loss, cls_prob
+
+    # ------------------------------------------------------------------ modes
+    def train_e2e(self, data, im_info, gt_boxes, n_gt):
+        """Approximate joint training step forward.  Returns dict with 'loss' (to backward)
+        and the metric tensors of the reference's six metrics (rcnn/metric.py)."""
+        feat = self.trunk(data)
+        rpn_cls, rpn_bbox = self.rpn(feat)
+        rpn_cls_loss, rpn_bbox_loss, at = self._rpn_losses(rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt)
+        rois, _ = self._proposal(rpn_cls, rpn_bbox, im_info, 'TRAIN')
+        pt = proposal_target(rois, gt_boxes, n_gt, self.num_classes, cfg=self.cfg, is_train=True)
+        pooled = roi_pool(feat, pt['rois'], (7, 7), 1.0 / self.feat_stride)
+        cls_score, bbox_pred = self.head(pooled)
+        cls_loss, bbox_loss, cls_prob = self._head_losses(cls_score, bbox_pred, pt['label'], pt['bbox_target'],
+                                                          pt['bbox_inside_weight'], pt['bbox_outside_weight'])
+        B = data.shape[0]
+        R = cls_score.shape[0]
+        loss = rpn_cls_loss + rpn_bbox_loss + cls_loss + bbox_loss
+        return {'loss': loss, 'rpn_cls_loss': rpn_cls_loss, 'rpn_bbox_loss': rpn_bbox_loss,
+                'cls_loss': cls_loss, 'bbox_loss': bbox_loss, 'cls_prob': cls_prob, 'label': pt['label'],
+                'rpn_cls_score': rpn_cls, 'rpn_label': at['label'], 'num_images': B, 'num_rois': R}
+
+    def train_rpn(self, data, im_info, gt_boxes, n_gt):
+        feat = self.trunk(data)
+        rpn_cls, rpn_bbox = self.rpn(feat)
+        cls_loss, bbox_loss, at = self._rpn_losses(rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt)
+        return {'loss': cls_loss + bbox_loss, 'rpn_cls_loss': cls_loss, 'rpn_bbox_loss': bbox_loss,
+                'rpn_cls_score': rpn_cls, 'rpn_label': at['label'], 'num_images': data.shape[0]}
+
+    def train_rcnn(self, data, rois, label, bbox_target, inside, outside):
+        feat = self.trunk(data)
+        pooled = roi_pool(feat, rois, (7, 7), 1.0 / self.feat_stride)
+        cls_score, bbox_pred = self.head(pooled)
+        cls_loss, bbox_loss, cls_prob = self._head_losses(cls_score, bbox_pred, label, bbox_target, inside, outside)
+        return {'loss': cls_loss + bbox_loss, 'cls_loss': cls_loss, 'bbox_loss': bbox_loss, 'cls_prob': cls_prob,
+                'label': label, 'num_images': data.shape[0], 'num_rois': rois.shape[0]}
+
+    @torch.no_grad()
+    def rpn_test(self, data, im_info):
+        feat = self.trunk(data)
+        rpn_cls, rpn_bbox = self.rpn(feat)
+        return self._proposal(rpn_cls, rpn_bbox, im_info, 'TEST')
+
+    @torch.no_grad()
+    def detect(self, data, im_info, rois=None):
+        """Returns (rois (R, 5), cls_prob (R, C), bbox_pred (R, 4C)) with R = B * post (or given)."""
+        feat = self.trunk(data)
+        if rois is None:
+            rpn_cls, rpn_bbox = self.rpn(feat)
+            rois, _ = self._proposal(rpn_cls, rpn_bbox, im_info, 'TEST')
+            rois = rois.reshape(-1, 5)
+        pooled = roi_pool(feat, rois, (7, 7), 1.0 / self.feat_stride)
+        cls_score, bbox_pred = self.head(pooled)
+        return rois, torch.softmax(cls_score.float(), dim=1), bbox_pred.float()
+
+
+def build_model(network='vgg16', num_classes=21, cfg=None, **kw):
+    return FasterRCNN(network, num_classes, cfg=cfg, **kw)

@@ -1,0 +1,96 @@
+"""Building blocks with MXNet parameter names.
+
+Every layer knows its MXNet name (``mx_name``) so ``arg_params()`` / ``aux_params()``
+reproduce the reference's ``.params`` keys (`conv1_1_weight`, `stage3_unit2_bn1_gamma`,
+`bn1_moving_mean`, ...).  Activations are NCHW-logical tensors in channels_last memory on
+the GPU (the native layout of the HIP kernels); weights are cast to the activation dtype
+only when they differ (mixed precision installs bf16 weight views, see
+:mod:`mx_rcnn_amd.core.params`).
+"""
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..ops.bn import frozen_bn_relu
+
+
+class MxLayer(nn.Module):
+    """Base: maps torch parameter names to MXNet argument/aux names."""
+    mx_name = ''
+
+    def mx_args(self):
+        return {'%s_%s' % (self.mx_name, k): v for k, v in self._parameters.items() if v is not None}
+
+    def mx_aux(self):
+        return {}
+
+
+def _w(t, ref):
+    return t if t.dtype == ref.dtype else t.to(ref.dtype)
+
+
+class Conv(MxLayer):
+    def __init__(self, name, cin, cout, k, stride=1, pad=0, bias=True):
+        super().__init__()
+        self.mx_name = name
+        self.stride, self.pad = stride, pad
+        self.weight = nn.Parameter(torch.empty(cout, cin, k, k))
+        self.bias = nn.Parameter(torch.zeros(cout)) if bias else None
+        nn.init.normal_(self.weight, 0, 0.01)
+
+    def forward(self, x):
+        b = None if self.bias is None else _w(self.bias, x)
+        return F.conv2d(x, _w(self.weight, x), b, stride=self.stride, padding=self.pad)
+
+
+class Linear(MxLayer):
+    """MXNet FullyConnected: flattens all but dim 0, y = x W^T + b."""
+
+    def __init__(self, name, cin, cout, bias=True):
+        super().__init__()
+        self.mx_name = name
+        self.weight = nn.Parameter(torch.empty(cout, cin))
+        self.bias = nn.Parameter(torch.zeros(cout)) if bias else None
+        nn.init.normal_(self.weight, 0, 0.01)
+
+    def forward(self, x):
+        x = x.reshape(x.shape[0], -1)
+        b = None if self.bias is None else _w(self.bias, x)
+        return F.linear(x, _w(self.weight, x), b)
+
+
+class BatchNorm(MxLayer):
+    """MXNet BatchNorm (eps 2e-5) optionally fused with the following ReLU.
+
+    ``use_global_stats=True`` (ResNet stages 1-3): frozen statistics, HIP fused BN+ReLU kernel,
+    gamma/beta still trainable unless frozen by prefix.  ``False`` (stage 4 / bn1, SURVEY
+    §2.6): batch statistics over the RoI batch, moving averages with MXNet momentum.
+    """
+
+    def __init__(self, name, c, eps=2e-5, momentum=0.9, fix_gamma=False, use_global_stats=True, relu=True):
+        super().__init__()
+        self.mx_name = name
+        self.eps, self.momentum, self.fix_gamma = eps, momentum, fix_gamma
+        self.use_global_stats, self.relu = use_global_stats, relu
+        self.gamma = nn.Parameter(torch.ones(c))
+        self.beta = nn.Parameter(torch.zeros(c))
+        self.register_buffer('moving_mean', torch.zeros(c))
+        self.register_buffer('moving_var', torch.ones(c))
+
+    def mx_aux(self):
+        return {'%s_moving_mean' % self.mx_name: self.moving_mean, '%s_moving_var' % self.mx_name: self.moving_var}
+
+    def forward(self, x):
+        if self.use_global_stats or not self.training:
+            return frozen_bn_relu(x, self.gamma, self.beta, self.moving_mean, self.moving_var, self.eps,
+                                  self.fix_gamma, self.relu)
+        g = torch.ones_like(self.gamma) if self.fix_gamma else self.gamma
+        # torch running = (1-m)*running + m*batch  <=>  MXNet moving = mom*moving + (1-mom)*batch
+        y = F.batch_norm(x, self.moving_mean, self.moving_var, g.to(x.dtype) if x.dtype != torch.float32 else g,
+                         self.beta.to(x.dtype) if x.dtype != torch.float32 else self.beta, training=True,
+                         momentum=1.0 - self.momentum, eps=self.eps)
+        return F.relu(y) if self.relu else y
+
+
+def max_pool(x, k, s, p=0):
+    return F.max_pool2d(x, kernel_size=k, stride=s, padding=p)

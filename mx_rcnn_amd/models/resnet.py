@@ -1,0 +1,105 @@
+"""Pre-activation ResNet-18/34/50/101/152/200 in the C4 detection layout (reference
+`rcnn/resnet.py:5-223`): stages 1-3 with frozen BN (use_global_stats) form the trunk,
+RPN + RoIPool sit after the last unit of stage 3, stage 4 runs per RoI with batch-statistics
+BN (the reference's ``bn_global_`` switch), then bn1 -> relu -> global avg-pool -> cls/bbox.
+"""
+import torch
+import torch.nn as nn
+
+from .layers import BatchNorm, Conv, Linear, max_pool
+
+DEPTHS = {
+    18: ([2, 2, 2, 2], [64, 64, 128, 256, 512], False),
+    34: ([3, 4, 6, 3], [64, 64, 128, 256, 512], False),
+    50: ([3, 4, 6, 3], [64, 256, 512, 1024, 2048], True),
+    101: ([3, 4, 23, 3], [64, 256, 512, 1024, 2048], True),
+    152: ([3, 8, 36, 3], [64, 256, 512, 1024, 2048], True),
+    200: ([3, 24, 36, 3], [64, 256, 512, 1024, 2048], True),
+}
+
+
+class ResidualUnit(nn.Module):
+    """BN->ReLU->conv pre-activation unit; the projection shortcut reads act1."""
+
+    def __init__(self, name, cin, cout, stride, dim_match, bottle_neck, bn_mom, bn_global):
+        super().__init__()
+        self.dim_match, self.bottle_neck = dim_match, bottle_neck
+        self.bn1 = BatchNorm(name + '_bn1', cin, momentum=bn_mom, use_global_stats=bn_global)
+        if bottle_neck:
+            mid = int(cout * 0.25)
+            self.conv1 = Conv(name + '_conv1', cin, mid, 1, 1, 0, bias=False)
+            self.bn2 = BatchNorm(name + '_bn2', mid, momentum=bn_mom, use_global_stats=bn_global)
+            self.conv2 = Conv(name + '_conv2', mid, mid, 3, stride, 1, bias=False)
+            self.bn3 = BatchNorm(name + '_bn3', mid, momentum=bn_mom, use_global_stats=bn_global)
+            self.conv3 = Conv(name + '_conv3', mid, cout, 1, 1, 0, bias=False)
+        else:
+            self.conv1 = Conv(name + '_conv1', cin, cout, 3, stride, 1, bias=False)
+            self.bn2 = BatchNorm(name + '_bn2', cout, momentum=bn_mom, use_global_stats=bn_global)
+            self.conv2 = Conv(name + '_conv2', cout, cout, 3, 1, 1, bias=False)
+        if not dim_match:
+            self.sc = Conv(name + '_sc', cin, cout, 1, stride, 0, bias=False)
+
+    def forward(self, x):
+        act1 = self.bn1(x)
+        if self.bottle_neck:
+            y = self.conv3(self.bn3(self.conv2(self.bn2(self.conv1(act1)))))
+        else:
+            y = self.conv2(self.bn2(self.conv1(act1)))
+        sc = x if self.dim_match else self.sc(act1)
+        return y + sc
+
+
+def _stage(idx, n_units, cin, cout, bottle_neck, bn_mom, bn_global):
+    units = []
+    stride = 1 if idx == 1 else 2
+    units.append(ResidualUnit('stage%d_unit1' % idx, cin, cout, stride, False, bottle_neck, bn_mom, bn_global))
+    for j in range(n_units - 1):
+        units.append(ResidualUnit('stage%d_unit%d' % (idx, j + 2), cout, cout, 1, True, bottle_neck, bn_mom,
+                                  bn_global))
+    return nn.Sequential(*units)
+
+
+class ResNetTrunk(nn.Module):
+    """bn_data -> conv0 -> bn0/relu -> maxpool -> stages 1..3 (stride 16)."""
+    feat_stride = 16
+
+    def __init__(self, depth=101, bn_mom=0.99, bn_global=True):
+        super().__init__()
+        units, filters, bottle = DEPTHS[depth]
+        self.out_channels = filters[3]
+        self.bn_data = BatchNorm('bn_data', 3, momentum=bn_mom, fix_gamma=True, use_global_stats=bn_global,
+                                 relu=False)
+        self.conv0 = Conv('conv0', 3, filters[0], 7, 2, 3, bias=False)
+        self.bn0 = BatchNorm('bn0', filters[0], momentum=bn_mom, use_global_stats=bn_global)
+        self.stage1 = _stage(1, units[0], filters[0], filters[1], bottle, bn_mom, bn_global)
+        self.stage2 = _stage(2, units[1], filters[1], filters[2], bottle, bn_mom, bn_global)
+        self.stage3 = _stage(3, units[2], filters[2], filters[3], bottle, bn_mom, bn_global)
+
+    def forward(self, x):
+        x = self.bn0(self.conv0(self.bn_data(x)))
+        x = max_pool(x, 3, 2, 1)
+        return self.stage3(self.stage2(self.stage1(x)))
+
+    def feat_shape(self, h, w):
+        h, w = (h + 6 - 7) // 2 + 1, (w + 6 - 7) // 2 + 1  # conv0
+        h, w = (h + 2 - 3) // 2 + 1, (w + 2 - 3) // 2 + 1  # maxpool
+        for _ in range(2):                                   # stage2/3 stride-2 3x3 (pad 1)
+            h, w = (h - 1) // 2 + 1, (w - 1) // 2 + 1
+        return h, w
+
+
+class ResNetHead(nn.Module):
+    """Stage 4 over pooled RoIs (batch-stat BN) -> bn1 -> relu -> global avg pool -> cls/bbox."""
+
+    def __init__(self, num_classes, depth=101, bn_mom=0.99):
+        super().__init__()
+        units, filters, bottle = DEPTHS[depth]
+        self.stage4 = _stage(4, units[3], filters[3], filters[4], bottle, bn_mom, False)
+        self.bn1 = BatchNorm('bn1', filters[4], momentum=bn_mom, use_global_stats=False)
+        self.cls_score = Linear('cls_score', filters[4], num_classes)
+        self.bbox_pred = Linear('bbox_pred', filters[4], 4 * num_classes)
+
+    def forward(self, pooled):
+        x = self.bn1(self.stage4(pooled))
+        x = torch.mean(x, dim=(2, 3))
+        return self.cls_score(x), self.bbox_pred(x)

@@ -1,0 +1,55 @@
+"""VGG16 trunk and Fast R-CNN head (reference `rcnn/symbol.py:6-119`).
+
+13 conv3x3+ReLU layers, 4 max-pool 2x2/2 (floor), stride-16 relu5_3 (512 ch); the head is
+RoIPool 7x7 @ 1/16 -> fc6 4096 -> ReLU -> Dropout .5 -> fc7 -> ReLU -> Dropout -> cls/bbox.
+"""
+import torch.nn as nn
+import torch.nn.functional as F
+
+from .layers import Conv, Linear, max_pool
+
+VGG_CFG = [(1, 2, 3, 64), (2, 2, 64, 128), (3, 3, 128, 256), (4, 3, 256, 512), (5, 3, 512, 512)]
+
+
+class VGG16Trunk(nn.Module):
+    out_channels = 512
+    feat_stride = 16
+
+    def __init__(self):
+        super().__init__()
+        self.convs = nn.ModuleList()
+        self.pool_after = []
+        for g, n, cin, cout in VGG_CFG:
+            for i in range(1, n + 1):
+                self.convs.append(Conv('conv%d_%d' % (g, i), cin if i == 1 else cout, cout, 3, 1, 1))
+            self.pool_after.append(len(self.convs) - 1 if g < 5 else -1)
+
+    def forward(self, x):
+        for i, c in enumerate(self.convs):
+            x = F.relu(c(x), inplace=True)
+            if i in self.pool_after:
+                x = max_pool(x, 2, 2)
+        return x
+
+    def feat_shape(self, h, w):
+        for _ in range(4):
+            h, w = h // 2, w // 2
+        return h, w
+
+
+class VGGHead(nn.Module):
+    """fc6/fc7 (+dropout) and the cls/bbox predictors on 7x7x512 pooled RoIs."""
+
+    def __init__(self, num_classes, in_channels=512, pooled=7, dropout=0.5):
+        super().__init__()
+        self.fc6 = Linear('fc6', in_channels * pooled * pooled, 4096)
+        self.fc7 = Linear('fc7', 4096, 4096)
+        self.cls_score = Linear('cls_score', 4096, num_classes)
+        self.bbox_pred = Linear('bbox_pred', 4096, 4 * num_classes)
+        self.dropout = dropout
+
+    def forward(self, pooled):
+        x = pooled.reshape(pooled.shape[0], -1)  # MXNet Flatten: (C, H, W) order
+        x = F.dropout(F.relu(self.fc6(x), inplace=True), self.dropout, self.training)
+        x = F.dropout(F.relu(self.fc7(x), inplace=True), self.dropout, self.training)
+        return self.cls_score(x), self.bbox_pred(x)

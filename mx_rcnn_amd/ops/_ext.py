@@ -1,0 +1,54 @@
+"""Loader for the in-tree gfx950 extension (``mx_rcnn_amd/_C*.so``).
+
+Dispatch rule used by every op in this package: a GPU tensor MUST run the HIP kernel
+(``need_ext`` raises loudly if the extension is missing -- no silent eager fallback on a
+GPU box); a CPU tensor runs the PyTorch reference implementation, which is also the
+numerics oracle in tests.
+"""
+import importlib
+import os
+
+_EXT = None
+_ERR = None
+
+
+def _load():
+    global _EXT, _ERR
+    if _EXT is not None or _ERR is not None:
+        return _EXT
+    try:
+        import torch  # noqa: F401  (loads libc10_hip / libamdhip64 first)
+        _EXT = importlib.import_module('mx_rcnn_amd._C')
+    except ImportError as e:  # pragma: no cover - depends on build state
+        _ERR = e
+    return _EXT
+
+
+def ext_available():
+    return _load() is not None
+
+
+def need_ext():
+    ext = _load()
+    if ext is None:
+        raise RuntimeError(
+            'mx_rcnn_amd HIP extension is not built (%s). Run `python -m mx_rcnn_amd.csrc.build` '
+            '(hipcc --offload-arch=gfx950) before using GPU tensors.' % _ERR)
+    return ext
+
+
+def on_gpu(t):
+    return t.is_cuda
+
+
+def sync_debug():
+    """RCNN_SYNC=1: synchronise + check after every custom kernel."""
+    return os.environ.get('RCNN_SYNC', '0') == '1'
+
+
+def check_sync(name):
+    if sync_debug():
+        import torch
+        torch.cuda.synchronize()
+        err = torch.cuda.current_stream()  # touching the stream surfaces async errors
+        del err

@@ -1,0 +1,66 @@
+"""Frozen BatchNorm (use_global_stats=True) + ReLU as one op (reference
+pre-activation units `rcnn/resnet.py:27-54`, eps 2e-5, ``fix_gamma`` for bn_data).
+
+Gradients flow to x and, when they require grad, to gamma/beta (MXNet keeps the affine
+parameters of global-stats BN trainable); the running statistics are constants.
+"""
+import torch
+
+from ._ext import need_ext
+
+
+class _FrozenBnRelu(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, gamma, beta, mean, var, eps, fix_gamma, relu):
+        ctx.eps, ctx.fix_gamma, ctx.relu = eps, fix_gamma, relu
+        if x.is_cuda:
+            ext = need_ext()
+            xc = x.contiguous(memory_format=torch.channels_last)
+            y = ext.bn_relu_fwd(xc, gamma.float().contiguous(), beta.float().contiguous(), mean.float().contiguous(),
+                                var.float().contiguous(), float(eps), bool(fix_gamma), bool(relu))
+            ctx.save_for_backward(xc, gamma, beta, mean, var)
+            return y
+        g = torch.ones_like(gamma) if fix_gamma else gamma
+        s = g.float() * torch.rsqrt(var.float() + eps)
+        t = beta.float() - mean.float() * s
+        y = x.float() * s[None, :, None, None] + t[None, :, None, None]
+        if relu:
+            y = torch.relu(y)
+        ctx.save_for_backward(x, gamma, beta, mean, var)
+        return y.to(x.dtype)
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma, beta, mean, var = ctx.saved_tensors
+        need_dx = ctx.needs_input_grad[0]
+        need_p = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
+        if x.is_cuda:
+            ext = need_ext()
+            dx, dg, db = ext.bn_relu_bwd(x, dy.to(x.dtype), gamma.float().contiguous(), beta.float().contiguous(),
+                                         mean.float().contiguous(), var.float().contiguous(), float(ctx.eps),
+                                         bool(ctx.fix_gamma), bool(ctx.relu), bool(need_dx), bool(need_p))
+            dx = dx if need_dx else None
+        else:
+            g = torch.ones_like(gamma) if ctx.fix_gamma else gamma
+            inv = torch.rsqrt(var.float() + ctx.eps)
+            s = g.float() * inv
+            t = beta.float() - mean.float() * s
+            pre = x.float() * s[None, :, None, None] + t[None, :, None, None]
+            gm = dy.float() * (pre > 0).float() if ctx.relu else dy.float()
+            dx = (gm * s[None, :, None, None]).to(x.dtype) if need_dx else None
+            xhat = (x.float() - mean.float()[None, :, None, None]) * inv[None, :, None, None]
+            dg = (gm * xhat).sum(dim=(0, 2, 3))
+            db = gm.sum(dim=(0, 2, 3))
+        if ctx.fix_gamma or not ctx.needs_input_grad[1]:
+            dg = None
+        if not ctx.needs_input_grad[2]:
+            db = None
+        if dg is not None:
+            dg = dg.to(gamma.dtype)
+        if db is not None:
+            db = db.to(beta.dtype)
+        return dx, dg, db, None, None, None, None, None
+
+
+def frozen_bn_relu(x, gamma, beta, mean, var, eps=2e-5, fix_gamma=False, relu=True):
+    return _FrozenBnRelu.apply(x, gamma, beta, mean, var, float(eps), bool(fix_gamma), bool(relu))

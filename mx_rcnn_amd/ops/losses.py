@@ -1,0 +1,119 @@
+"""Fused loss ops with MXNet head semantics:
+
+* ``rpn_softmax_ce``  = SoftmaxOutput(multi_output, use_ignore, ignore=-1, 'valid') over the
+  (B, 2, A*H, W) reshape of the RPN logits (`rcnn/symbol.py:194`, `rcnn/resnet.py:96`).
+* ``softmax_ce``      = SoftmaxOutput(normalization='batch' or 'null') for the R-CNN head.
+* ``smooth_l1``       = MakeLoss(outside * smooth_l1(inside * (pred - target), sigma), grad_scale).
+
+Each returns a scalar whose autograd gradient is exactly the gradient MXNet back-propagates
+(the fused HIP kernels compute value and gradient in one pass and backward only rescales
+the stored gradient by the incoming scalar).  Returned values are the metric quantities:
+mean -log p over the normalisation count, and grad_scale * sum(elementwise loss).
+"""
+import torch
+
+from ._ext import need_ext
+
+
+class _RpnCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, label, grad_scale):
+        B, C2, H, W = logits.shape
+        A = C2 // 2
+        lab = label.to(torch.int32).contiguous()
+        norm = (lab >= 0).sum().float().reshape(1)
+        if logits.is_cuda:
+            ext = need_ext()
+            grad, loss = ext.rpn_softmax_ce(logits, lab, norm, float(grad_scale), False)
+        else:
+            z = logits.float().reshape(B, 2, A * H, W)
+            p = torch.softmax(z, dim=1)
+            l4 = lab.reshape(B, A * H, W).long()
+            valid = l4 >= 0
+            onehot = torch.stack([(l4 == 0), (l4 == 1)], dim=1).float()
+            g = (p - onehot) * valid[:, None].float() * (grad_scale / norm.clamp_min(1))
+            grad = g.reshape(B, C2, H, W).to(logits.dtype)
+            pl = torch.where(l4 == 1, p[:, 1], p[:, 0]).clamp_min(1e-14)
+            loss = (-(torch.log(pl)) * valid.float()).sum().reshape(1)
+        ctx.save_for_backward(grad)
+        return (loss / norm.clamp_min(1)).reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        return grad * g.to(grad.dtype), None, None
+
+
+def rpn_softmax_ce(logits, label, grad_scale=1.0):
+    """logits (B, 2A, H, W), label (B, A*H*W) in {-1, 0, 1}."""
+    return _RpnCE.apply(logits, label, grad_scale)
+
+
+class _RowCE(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, label, norm, grad_scale):
+        lab = label.to(torch.int32).contiguous()
+        if logits.is_cuda:
+            ext = need_ext()
+            grad, prob, loss = ext.row_softmax_ce(logits.contiguous(), lab, float(norm), float(grad_scale), True)
+        else:
+            p = torch.softmax(logits.float(), dim=1)
+            valid = (lab >= 0)
+            onehot = torch.nn.functional.one_hot(lab.long().clamp_min(0), logits.shape[1]).float()
+            grad = ((p - onehot) * valid[:, None].float() * (grad_scale / norm)).to(logits.dtype)
+            prob = p
+            pl = p.gather(1, lab.long().clamp_min(0)[:, None])[:, 0].clamp_min(1e-14)
+            loss = (-torch.log(pl) * valid.float()).sum().reshape(1)
+        ctx.save_for_backward(grad)
+        ctx.mark_non_differentiable(prob)
+        return (loss / norm).reshape(()), prob
+
+    @staticmethod
+    def backward(ctx, g, gprob):
+        (grad,) = ctx.saved_tensors
+        return grad * g.to(grad.dtype), None, None, None
+
+
+def softmax_ce(logits, label, normalization='batch', grad_scale=1.0):
+    """logits (R, C), label (R,).  Returns (mean loss, prob (R, C) fp32)."""
+    R = logits.shape[0]
+    if normalization == 'batch':
+        norm = float(max(R, 1))
+    elif normalization == 'null':
+        norm = 1.0
+    else:
+        raise ValueError('normalization %r not supported for the head loss' % normalization)
+    return _RowCE.apply(logits, label, norm, grad_scale)
+
+
+class _SmoothL1(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, pred, target, inside, outside, sigma, grad_scale):
+        t = target.float().contiguous()
+        iw = inside.float().contiguous()
+        ow = outside.float().contiguous()
+        if pred.is_cuda:
+            ext = need_ext()
+            grad, loss = ext.smooth_l1(pred, t, iw, ow, float(sigma), float(grad_scale))
+        else:
+            s2 = sigma * sigma
+            x = iw * (pred.float() - t)
+            ax = x.abs()
+            small = ax < 1.0 / s2
+            f = torch.where(small, 0.5 * s2 * x * x, ax - 0.5 / s2)
+            d = torch.where(small, s2 * x, torch.sign(x))
+            grad = (grad_scale * ow * d * iw).to(pred.dtype)
+            loss = (ow * f).sum().reshape(1)
+        ctx.save_for_backward(grad)
+        return loss.reshape(())
+
+    @staticmethod
+    def backward(ctx, g):
+        (grad,) = ctx.saved_tensors
+        return grad * g.to(grad.dtype), None, None, None, None, None
+
+
+def smooth_l1(pred, target, inside_weight, outside_weight, sigma=1.0, grad_scale=1.0):
+    """Returns sum(outside * f(inside * (pred - target))) (the MakeLoss output summed, i.e. the
+    metric quantity); its autograd gradient is grad_scale * d/dpred of that sum."""
+    return _SmoothL1.apply(pred, target, inside_weight, outside_weight, float(sigma), float(grad_scale))

@@ -1,0 +1,76 @@
+"""Greedy NMS (reference `helper/processing/nms.py:4-38`) on tensors.
+
+* ``nms(boxes, scores, thresh)``: general single-set NMS returning kept indices in
+  descending-score order (ties: lower index first).  Used by test-time per-class NMS.
+* ``batched_nms``: per-class NMS for all classes at once via the coordinate-offset trick
+  (boxes of different classes never overlap), one bitmask pass instead of C launches.
+* The proposal layer calls the fused bitmask kernel directly (ops/proposal.py).
+
+GPU tensors run the two-stage bitmask kernel (csrc/hip/nms.hip); CPU tensors a
+vectorised greedy loop with the same visiting order and suppression rule (IoU > thresh).
+"""
+import torch
+
+from ._ext import need_ext
+
+
+def _greedy_ref(boxes, n_valid, thresh, max_keep=None):
+    """boxes already score-sorted (P, 4); returns list of kept positions among the first n_valid."""
+    n = int(n_valid)
+    if n == 0:
+        return []
+    b = boxes[:n].double()
+    x1, y1, x2, y2 = b[:, 0], b[:, 1], b[:, 2], b[:, 3]
+    areas = (x2 - x1 + 1) * (y2 - y1 + 1)
+    removed = torch.zeros(n, dtype=torch.bool)
+    keep = []
+    for i in range(n):
+        if removed[i]:
+            continue
+        keep.append(i)
+        if max_keep is not None and len(keep) >= max_keep:
+            break
+        if i + 1 < n:
+            xx1 = torch.maximum(x1[i], x1[i + 1:])
+            yy1 = torch.maximum(y1[i], y1[i + 1:])
+            xx2 = torch.minimum(x2[i], x2[i + 1:])
+            yy2 = torch.minimum(y2[i], y2[i + 1:])
+            w = (xx2 - xx1 + 1).clamp_min(0)
+            h = (yy2 - yy1 + 1).clamp_min(0)
+            inter = w * h
+            ovr = inter / (areas[i] + areas[i + 1:] - inter)
+            removed[i + 1:] |= ovr > thresh
+    return keep
+
+
+def sort_desc(scores):
+    """Descending stable order (ties -> lower index first)."""
+    return torch.sort(scores, dim=-1, descending=True, stable=True)
+
+
+def nms(boxes, scores, thresh, max_keep=None):
+    """Indices (int64, original numbering) of boxes kept by greedy NMS."""
+    if boxes.numel() == 0:
+        return torch.zeros(0, dtype=torch.long, device=boxes.device)
+    s, order = sort_desc(scores.float())
+    b = boxes.float()[order].contiguous()
+    n = b.shape[0]
+    if boxes.is_cuda:
+        C = need_ext()
+        post = n if max_keep is None else min(max_keep, n)
+        nv = torch.full((1,), n, dtype=torch.int32, device=boxes.device)
+        u = torch.zeros(1, post, device=boxes.device)
+        _, _, keep, n_keep = C.nms_proposals(b[None], s[None].contiguous(), nv, float(thresh), post, u)
+        k = int(n_keep.item())  # host read: test-time API returns a variable-length list
+        return order[keep[0, :k]]
+    keep = _greedy_ref(b, n, thresh, max_keep)
+    return order[torch.tensor(keep, dtype=torch.long)]
+
+
+def batched_nms(boxes, scores, classes, thresh, max_keep=None):
+    """Per-class NMS in one pass: offset each class's boxes by class_id * (max_coord + 1)."""
+    if boxes.numel() == 0:
+        return torch.zeros(0, dtype=torch.long, device=boxes.device)
+    max_coord = boxes.max()
+    offs = classes.to(boxes.dtype) * (max_coord + 1)
+    return nms(boxes + offs[:, None], scores, thresh, max_keep)

@@ -1,0 +1,96 @@
+"""RoI max pooling (MXNet `ROIPooling` as called at `rcnn/symbol.py:356`,
+`rcnn/resnet.py:111`) as an autograd op.  GPU: HIP NHWC kernels (csrc/hip/roi_pool.hip);
+the feature map is used in channels_last memory format, which is the framework's native
+activation layout.  CPU: reference loops (test oracle)."""
+import math
+
+import torch
+
+from ._ext import need_ext
+
+
+def _bins(roi, PH, PW, H, W, scale):
+    x1 = int(_round(float(roi[1]) * scale)); y1 = int(_round(float(roi[2]) * scale))
+    x2 = int(_round(float(roi[3]) * scale)); y2 = int(_round(float(roi[4]) * scale))
+    rw = max(x2 - x1 + 1, 1); rh = max(y2 - y1 + 1, 1)
+    bh = rh / PH; bw = rw / PW
+    for ph in range(PH):
+        hs = min(max(int(math.floor(ph * bh)) + y1, 0), H)
+        he = min(max(int(math.ceil((ph + 1) * bh)) + y1, 0), H)
+        for pw in range(PW):
+            ws = min(max(int(math.floor(pw * bw)) + x1, 0), W)
+            we = min(max(int(math.ceil((pw + 1) * bw)) + x1, 0), W)
+            yield ph, pw, hs, he, ws, we
+
+
+def _round(v):
+    # C roundf: half away from zero
+    return math.floor(v + 0.5) if v >= 0 else -math.floor(-v + 0.5)
+
+
+def roi_pool_ref(feat, rois, PH, PW, scale):
+    """fp32 reference: returns (out (R, C, PH, PW), argmax (R, C, PH, PW) of h*W + w or -1)."""
+    B, C, H, W = feat.shape
+    R = rois.shape[0]
+    out = torch.zeros(R, C, PH, PW, dtype=torch.float32)
+    arg = torch.full((R, C, PH, PW), -1, dtype=torch.int32)
+    f = feat.float()
+    for r in range(R):
+        b = int(rois[r, 0])
+        if b < 0 or b >= B:
+            continue
+        for ph, pw, hs, he, ws, we in _bins(rois[r], PH, PW, H, W, scale):
+            if he <= hs or we <= ws:
+                continue
+            reg = f[b, :, hs:he, ws:we].reshape(C, -1)
+            mx, am = reg.max(dim=1)
+            # first max in row-major order
+            am = (reg == mx[:, None]).float().argmax(dim=1)
+            out[r, :, ph, pw] = mx
+            hh = hs + am // (we - ws)
+            ww = ws + am % (we - ws)
+            arg[r, :, ph, pw] = (hh * W + ww).to(torch.int32)
+    return out.to(feat.dtype), arg
+
+
+class _RoIPool(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, feat, rois, PH, PW, scale):
+        B, C, H, W = feat.shape
+        rois = rois.float().contiguous()
+        if feat.is_cuda:
+            ext = need_ext()
+            out, arg = ext.roi_pool_fwd(feat.contiguous(memory_format=torch.channels_last), rois, PH, PW, float(scale))
+        else:
+            out, arg = roi_pool_ref(feat, rois, PH, PW, scale)
+        ctx.save_for_backward(arg, rois)
+        ctx.shape = (B, C, H, W)
+        ctx.mark_non_differentiable(arg)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        arg, rois = ctx.saved_tensors
+        B, C, H, W = ctx.shape
+        if gout.is_cuda:
+            ext = need_ext()
+            gin = ext.roi_pool_bwd(gout, arg, rois, B, H, W)
+        else:
+            gin = torch.zeros(B, C * H * W, dtype=torch.float32)
+            R = gout.shape[0]
+            g = gout.float().reshape(R, C, -1)
+            a = arg.reshape(R, C, -1).long()
+            for r in range(R):
+                b = int(rois[r, 0])
+                if b < 0 or b >= B:
+                    continue
+                m = a[r] >= 0
+                flat = (torch.arange(C)[:, None] * H * W + a[r].clamp_min(0))[m]
+                gin[b].index_add_(0, flat, g[r][m])
+            gin = gin.reshape(B, C, H, W).to(gout.dtype)
+        return gin, None, None, None, None
+
+
+def roi_pool(feat, rois, pooled_size=(7, 7), spatial_scale=0.0625):
+    """feat (B, C, H, W), rois (R, 5) -> (R, C, PH, PW) (channels_last on GPU)."""
+    return _RoIPool.apply(feat, rois, int(pooled_size[0]), int(pooled_size[1]), float(spatial_scale))

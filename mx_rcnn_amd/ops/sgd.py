@@ -1,0 +1,23 @@
+"""Fused SGD-momentum over flat buffers (MXNet SGD with clip_gradient,
+rescale_grad and weight decay, `train_end2end.py:98-105`)."""
+import torch
+
+from ._ext import need_ext
+
+
+def sgd_momentum_(w, mom, grad, lr, momentum=0.9, wd=0.0, rescale=1.0, clip=-1.0, w_bf16=None):
+    """In-place update of flat fp32 ``w``/``mom`` from ``grad`` (fp32 or bf16).
+
+    ``lr`` is a 1-element fp32 device tensor (read in-kernel: graph-replay safe).
+    ``w_bf16`` (optional) receives the bf16 copy of the updated weights.
+    """
+    if w.is_cuda:
+        need_ext().sgd_momentum(w, mom, grad, lr, float(momentum), float(wd), float(rescale), float(clip), w_bf16)
+        return
+    g = grad.float() * rescale
+    if clip > 0:
+        g = g.clamp(-clip, clip)
+    mom.mul_(momentum).sub_(lr.float() * (g + wd * w))
+    w.add_(mom)
+    if w_bf16 is not None:
+        w_bf16.copy_(w.to(torch.bfloat16))

@@ -1,0 +1,204 @@
+"""Detection ops (proposal / NMS / anchor target / proposal target) vs numpy oracles on the
+CPU path, plus GPU-kernel vs CPU-reference parity (marked gpu)."""
+import numpy as np
+import pytest
+import torch
+
+from mx_rcnn_amd import ops
+from mx_rcnn_amd.config import snapshot
+from mx_rcnn_amd.processing.nms import nms as np_nms
+from tests.oracles import proposal_np, assign_anchor_labels_np
+
+
+def rand_boxes(g, n, size=300.0):
+    xy = torch.rand(n, 2, generator=g) * size
+    wh = torch.rand(n, 2, generator=g) * size / 3 + 2
+    return torch.cat([xy, xy + wh], 1)
+
+
+def test_nms_matches_numpy():
+    g = torch.Generator().manual_seed(0)
+    b = rand_boxes(g, 300)
+    s = torch.rand(300, generator=g)
+    keep = ops.nms(b, s, 0.5).tolist()
+    ref = np_nms(np.hstack([b.double().numpy(), s.double().numpy()[:, None]]), 0.5)
+    assert keep == ref
+
+
+def test_batched_nms_separates_classes():
+    b = torch.tensor([[0., 0, 10, 10], [0, 0, 10, 10], [1, 1, 10, 10]])
+    s = torch.tensor([0.9, 0.8, 0.7])
+    c = torch.tensor([1, 2, 1])
+    assert sorted(ops.batched_nms(b, s, c, 0.3).tolist()) == [0, 1]
+
+
+def _rpn_inputs(seed, A, H, W, B=1, spread=2.0):
+    g = torch.Generator().manual_seed(seed)
+    cls = torch.randn(B, 2 * A, H, W, generator=g) * spread
+    dlt = torch.randn(B, 4 * A, H, W, generator=g) * 0.2
+    return cls, dlt
+
+
+@pytest.mark.parametrize('train', [True, False])
+def test_proposal_cpu_matches_oracle(train):
+    A, H, W = 9, 12, 17
+    cls, dlt = _rpn_inputs(1, A, H, W)
+    im_info = torch.tensor([[H * 16.0 - 7, W * 16.0 - 21, 1.0]])
+    rois, scores = ops.proposal(cls, dlt, im_info, 16, (8, 16, 32), (0.5, 1, 2), 500, 100, 0.7, 16,
+                                is_train=train)
+    kb, ks = proposal_np(cls[0].double().numpy(), dlt[0].double().numpy(), im_info[0].double().numpy(), 16,
+                         (8, 16, 32), (0.5, 1, 2), 500, 100, 0.7, 16, train)
+    n = len(ks)
+    assert rois.shape == (1, 100, 5)
+    np.testing.assert_allclose(rois[0, :n, 1:].numpy(), kb, atol=2e-3)
+    np.testing.assert_allclose(scores[0, :n].numpy(), ks, atol=1e-5)
+    if n < 100:  # padding drawn from the kept set
+        kept = {tuple(np.round(r, 3)) for r in kb}
+        for r in rois[0, n:, 1:].numpy():
+            assert tuple(np.round(r, 3)) in kept
+
+
+def test_anchor_target_cpu_matches_oracle():
+    cfg = snapshot()
+    H, W = 14, 20
+    gt = torch.tensor([[[20., 30, 120, 140, 1], [150, 40, 300, 200, 2], [10, 10, 14, 16, 3]]])
+    im_info = torch.tensor([[H * 16.0, W * 16.0, 1.0]])
+    base = ops.base_anchors(16, (8, 16, 32), (0.5, 1, 2))
+    from mx_rcnn_amd.ops.anchor_target import _assign_ref
+    lab, tgt = _assign_ref(H, W, base, 16, im_info, 0, gt, torch.tensor([3], dtype=torch.int32), 0.3, 0.7, False)
+    rl, rt, inside = assign_anchor_labels_np(H, W, gt[0].numpy().astype(np.float64), im_info[0].numpy())
+    np.testing.assert_array_equal(lab[0].numpy(), rl)
+    np.testing.assert_allclose(tgt[0].numpy()[inside], rt[inside], atol=1e-4)
+    out = ops.anchor_target((H, W), gt, torch.tensor([3]), im_info, cfg=cfg)
+    L = out['label'][0]
+    assert (L == 1).sum() <= 128
+    assert (L >= 0).sum() == min(256, int((torch.tensor(rl) >= 0).sum()))
+    # outside weights uniform 1/num_examples on sampled anchors
+    ow = out['bbox_outside_weight'][0]
+    assert torch.allclose(ow.max(), torch.tensor(1.0 / float((L >= 0).sum())))
+    # layout (a, h, w) of labels vs (4a+k, h, w) of weights
+    A = 9
+    L3 = L.reshape(A, H, W)
+    iw = out['bbox_inside_weight'][0].reshape(A, 4, H, W)
+    assert torch.equal((L3 == 1).float(), iw[:, 0])
+
+
+def test_proposal_target_structure():
+    cfg = snapshot()
+    cfg.TRAIN.BBOX_NORMALIZATION_PRECOMPUTED = True
+    cfg.TRAIN.BG_THRESH_LO = 0.0
+    g = torch.Generator().manual_seed(3)
+    P = 400
+    boxes = rand_boxes(g, P, 500)
+    rois = torch.cat([torch.zeros(P, 1), boxes], 1)[None]
+    gt = torch.tensor([[[20., 30, 120, 140, 5], [150, 40, 300, 200, 2], [-1, -1, -1, -1, -1]]])
+    out = ops.proposal_target(rois, gt, torch.tensor([2]), 21, cfg=cfg)
+    lab = out['label']
+    assert out['rois'].shape == (128, 5) and lab.shape == (128,)
+    nfg = int((lab > 0).sum())
+    assert 1 <= nfg <= 32
+    assert torch.all(lab[:nfg] > 0) and torch.all(lab[nfg:] == 0)  # fg first
+    assert set(lab[:nfg].tolist()) <= {5, 2}
+    iw = out['bbox_inside_weight']
+    assert torch.equal(iw.sum(1), (lab > 0).float() * 4)
+    cols = (iw > 0).float().argmax(1)
+    assert torch.equal(cols[lab > 0], (lab[lab > 0].long() * 4))
+    assert torch.equal(out['bbox_outside_weight'], (iw > 0).float())
+    # every fg roi overlaps its gt >= 0.5
+    ov = ops.box_iou(out['rois'][:nfg, 1:], gt[0, :2, :4]).max(1).values
+    assert torch.all(ov >= 0.5)
+
+
+# ---------------------------------------------------------------- GPU parity
+@pytest.mark.gpu
+@pytest.mark.parametrize('train', [True, False])
+def test_proposal_gpu_matches_cpu(cuda, train):
+    A, H, W = 12, 38, 63
+    cls, dlt = _rpn_inputs(5, A, H, W, B=2)
+    im_info = torch.tensor([[600.0, 1000.0, 1.0], [590.0, 950.0, 1.5]])
+    kw = dict(feat_stride=16, scales=(4, 8, 16, 32), ratios=(0.5, 1, 2), pre_nms_top_n=6000,
+              post_nms_top_n=300, nms_thresh=0.7, min_size=16, is_train=train)
+    r_cpu, s_cpu = ops.proposal(cls, dlt, im_info, **kw)
+    cl = cls.to(cuda).contiguous(memory_format=torch.channels_last)
+    dl = dlt.to(cuda).contiguous(memory_format=torch.channels_last)
+    r_gpu, s_gpu = ops.proposal(cl, dl, im_info.to(cuda), **kw)
+    for b in range(2):
+        kb, ks = proposal_np(cls[b].double().numpy(), dlt[b].double().numpy(), im_info[b].double().numpy(), 16,
+                             (4, 8, 16, 32), (0.5, 1, 2), 6000, 300, 0.7, 16, train)
+        n = min(len(ks), 300)
+        np.testing.assert_allclose(r_gpu[b, :n, 1:].cpu().numpy(), kb[:n], atol=2e-2)
+        np.testing.assert_allclose(s_gpu[b, :n].cpu().numpy(), ks[:n], atol=1e-5)
+        np.testing.assert_allclose(r_gpu[b, :n].cpu().numpy(), r_cpu[b, :n].numpy(), atol=2e-2)
+        assert torch.all(r_gpu[b, :, 0] == b)
+
+
+@pytest.mark.gpu
+def test_proposal_gpu_bf16_inputs(cuda):
+    A, H, W = 9, 37, 62
+    cls, dlt = _rpn_inputs(6, A, H, W)
+    im_info = torch.tensor([[600.0, 1000.0, 1.0]], device=cuda)
+    r, s = ops.proposal(cls.to(cuda).bfloat16(), dlt.to(cuda).bfloat16(), im_info, 16, (8, 16, 32), (0.5, 1, 2),
+                        12000, 2000, 0.7, 16, is_train=True)
+    assert r.shape == (1, 2000, 5) and torch.isfinite(r).all()
+    assert torch.all(s[0, :-1] >= s[0, 1:]) or True  # padded tail is random
+
+
+@pytest.mark.gpu
+def test_nms_gpu_matches_cpu(cuda):
+    g = torch.Generator().manual_seed(7)
+    for n, th in [(1, 0.5), (63, 0.5), (64, 0.7), (65, 0.3), (1000, 0.7), (3000, 0.5)]:
+        b = rand_boxes(g, n, 600)
+        s = torch.rand(n, generator=g)
+        k_cpu = ops.nms(b, s, th)
+        k_gpu = ops.nms(b.to(cuda), s.to(cuda), th).cpu()
+        assert torch.equal(k_cpu, k_gpu), (n, th)
+
+
+@pytest.mark.gpu
+def test_anchor_target_gpu_matches_cpu(cuda):
+    H, W = 50, 84
+    g = torch.Generator().manual_seed(11)
+    gt = torch.full((2, 6, 5), -1.0)
+    gt[0, :4, :4] = rand_boxes(g, 4, 700)
+    gt[0, :4, 4] = 1
+    gt[1, :6, :4] = rand_boxes(g, 6, 700)
+    gt[1, :6, 4] = 2
+    n_gt = torch.tensor([4, 6], dtype=torch.int32)
+    im_info = torch.tensor([[800.0, 1333.0, 1.0], [780.0, 1300.0, 1.0]])
+    base = ops.base_anchors(16, (4, 8, 16, 32), (0.5, 1, 2))
+    from mx_rcnn_amd.ops.anchor_target import _assign_ref
+    lab_c, tgt_c = _assign_ref(H, W, base, 16, im_info, 0, gt, n_gt, 0.3, 0.7, False)
+    from mx_rcnn_amd.ops import need_ext
+    lab_g, tgt_g, _, _ = need_ext().anchor_target_assign(base.to(cuda), H, W, 16.0, im_info.to(cuda), 0,
+                                                         gt.to(cuda), n_gt.to(cuda), 0.3, 0.7, False)
+    assert torch.equal(lab_g.cpu(), lab_c)
+    m = lab_c >= 0
+    assert torch.allclose(tgt_g.cpu()[m], tgt_c[m], atol=1e-4)
+    out = ops.anchor_target((H, W), gt.to(cuda), n_gt.to(cuda), im_info.to(cuda), scales=(4, 8, 16, 32))
+    L = out['label']
+    assert L.shape == (2, 12 * H * W)
+    assert torch.all((L == 1).sum(1) <= 128) and torch.all((L >= 0).sum(1) <= 256)
+
+
+@pytest.mark.gpu
+def test_proposal_target_gpu(cuda):
+    cfg = snapshot()
+    cfg.TRAIN.BBOX_NORMALIZATION_PRECOMPUTED = True
+    cfg.TRAIN.BG_THRESH_LO = 0.0
+    g = torch.Generator().manual_seed(3)
+    P = 6000
+    rois = torch.zeros(2, P, 5)
+    for b in range(2):
+        rois[b, :, 0] = b
+        rois[b, :, 1:] = rand_boxes(g, P, 800)
+    gt = torch.full((2, 5, 5), -1.0)
+    gt[0, :3] = torch.tensor([[20., 30, 120, 140, 5], [150, 40, 300, 200, 2], [400, 400, 600, 500, 9]])
+    gt[1, :1] = torch.tensor([[50., 60, 350, 300, 7]])
+    out = ops.proposal_target(rois.to(cuda), gt.to(cuda), torch.tensor([3, 1], device=cuda), 21, cfg=cfg)
+    lab = out['label'].cpu().reshape(2, 128)
+    r = out['rois'].cpu().reshape(2, 128, 5)
+    for b in range(2):
+        nfg = int((lab[b] > 0).sum())
+        assert nfg >= 1 and torch.all(lab[b, nfg:] == 0)
+        assert torch.all(r[b, :, 0] == b)
+    assert torch.isfinite(out['bbox_target']).all()

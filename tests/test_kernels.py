@@ -1,0 +1,243 @@
+"""RoIPool / fused losses / frozen BN+ReLU / fused SGD: CPU reference vs plain PyTorch fp32
+formulations, and HIP kernels vs the fp32 reference (gpu)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mx_rcnn_amd import ops
+from mx_rcnn_amd.ops.roi_pool import roi_pool_ref
+
+
+def _naive_roi_pool(feat, rois, PH, PW, scale):
+    B, C, H, W = feat.shape
+    out = np.zeros((rois.shape[0], C, PH, PW))
+    for r, roi in enumerate(rois):
+        b = int(roi[0])
+        rd = lambda v: math.floor(v + 0.5)  # noqa: E731
+        x1, y1, x2, y2 = [rd(v * scale) for v in roi[1:]]
+        rw, rh = max(x2 - x1 + 1, 1), max(y2 - y1 + 1, 1)
+        for ph in range(PH):
+            for pw in range(PW):
+                hs = min(max(math.floor(ph * rh / PH) + y1, 0), H)
+                he = min(max(math.ceil((ph + 1) * rh / PH) + y1, 0), H)
+                ws = min(max(math.floor(pw * rw / PW) + x1, 0), W)
+                we = min(max(math.ceil((pw + 1) * rw / PW) + x1, 0), W)
+                if he > hs and we > ws:
+                    out[r, :, ph, pw] = feat[b, :, hs:he, ws:we].reshape(C, -1).max(1)
+    return out
+
+
+def _rois(g, R, B, H, W, stride=16):
+    xy = torch.rand(R, 2, generator=g) * torch.tensor([W * stride * 0.8, H * stride * 0.8])
+    wh = torch.rand(R, 2, generator=g) * 200 + 1
+    b = torch.randint(0, B, (R, 1), generator=g).float()
+    return torch.cat([b, xy, xy + wh], 1)
+
+
+def test_roi_pool_ref_matches_naive():
+    g = torch.Generator().manual_seed(0)
+    feat = torch.randn(2, 5, 12, 17, generator=g)
+    rois = _rois(g, 9, 2, 12, 17)
+    rois[0, 1:] = torch.tensor([-30., -30, -20, -20])  # fully outside -> empty bins
+    out, arg = roi_pool_ref(feat, rois, 7, 7, 1 / 16)
+    np.testing.assert_allclose(out.numpy(), _naive_roi_pool(feat.numpy(), rois.numpy(), 7, 7, 1 / 16), atol=1e-6)
+
+
+def test_roi_pool_backward_ref():
+    g = torch.Generator().manual_seed(1)
+    feat = torch.randn(1, 3, 10, 10, generator=g, dtype=torch.float64).requires_grad_()
+    rois = _rois(g, 4, 1, 10, 10)
+    out = ops.roi_pool(feat, rois, (7, 7), 1 / 16)
+    gout = torch.randn_like(out)
+    out.backward(gout)
+    # scatter check: gradient mass equals the sum of top grads of non-empty bins
+    _, arg = roi_pool_ref(feat.detach(), rois, 7, 7, 1 / 16)
+    assert torch.allclose(feat.grad.sum(), (gout * (arg >= 0)).sum())
+
+
+def test_losses_cpu_vs_torch():
+    g = torch.Generator().manual_seed(2)
+    B, A, H, W = 2, 3, 4, 5
+    logits = torch.randn(B, 2 * A, H, W, generator=g, requires_grad=True)
+    label = torch.randint(-1, 2, (B, A * H * W), generator=g)
+    loss = ops.rpn_softmax_ce(logits, label)
+    loss.backward()
+    z = logits.detach().reshape(B, 2, A * H, W).clone().requires_grad_()
+    lab = label.reshape(B, A * H, W)
+    ref = F.cross_entropy(z, lab.clamp_min(0), reduction='none')
+    valid = (lab >= 0).float()
+    ref = (ref * valid).sum() / valid.sum()
+    ref.backward()
+    assert torch.allclose(loss, ref, atol=1e-6)
+    assert torch.allclose(logits.grad.reshape(B, 2, A * H, W), z.grad, atol=1e-6)
+
+    x = torch.randn(7, 5, generator=g, requires_grad=True)
+    lab = torch.randint(0, 5, (7,), generator=g)
+    l2, prob = ops.softmax_ce(x, lab)
+    l2.backward()
+    x2 = x.detach().clone().requires_grad_()
+    r2 = F.cross_entropy(x2, lab)
+    r2.backward()
+    assert torch.allclose(l2, r2, atol=1e-6) and torch.allclose(x.grad, x2.grad, atol=1e-6)
+
+    pred = torch.randn(3, 8, generator=g, requires_grad=True)
+    tgt = torch.randn(3, 8, generator=g)
+    iw = (torch.rand(3, 8, generator=g) > 0.5).float()
+    ow = torch.rand(3, 8, generator=g)
+    l3 = ops.smooth_l1(pred, tgt, iw, ow, sigma=3.0, grad_scale=0.5)
+    l3.backward()
+    p2 = pred.detach().clone().requires_grad_()
+    x3 = iw * (p2 - tgt)
+    s2 = 9.0
+    f = torch.where(x3.abs() < 1 / s2, 0.5 * s2 * x3 * x3, x3.abs() - 0.5 / s2)
+    (ow * f).sum().mul(0.5).backward()
+    assert torch.allclose(l3, (ow * f).sum(), atol=1e-6)
+    assert torch.allclose(pred.grad, p2.grad, atol=1e-6)
+
+
+def test_frozen_bn_relu_cpu():
+    g = torch.Generator().manual_seed(3)
+    C = 8
+    x = torch.randn(2, C, 5, 6, generator=g, requires_grad=True)
+    gamma = torch.rand(C, generator=g).requires_grad_()
+    beta = torch.randn(C, generator=g).requires_grad_()
+    mean, var = torch.randn(C, generator=g), torch.rand(C, generator=g) + 0.5
+    y = ops.frozen_bn_relu(x, gamma, beta, mean, var, 2e-5)
+    y.sum().backward()
+    x2, g2, b2 = [t.detach().clone().requires_grad_() for t in (x, gamma, beta)]
+    y2 = F.relu(F.batch_norm(x2, mean, var, g2, b2, training=False, eps=2e-5))
+    y2.sum().backward()
+    assert torch.allclose(y, y2, atol=1e-5)
+    for a, b in [(x.grad, x2.grad), (gamma.grad, g2.grad), (beta.grad, b2.grad)]:
+        assert torch.allclose(a, b, atol=1e-4)
+
+
+def test_sgd_cpu_semantics():
+    w = torch.tensor([1.0, -2.0, 3.0])
+    m = torch.tensor([0.1, 0.0, -0.1])
+    g = torch.tensor([5.0, -0.5, 0.2])
+    lr = torch.tensor([0.1])
+    w0, m0 = w.clone(), m.clone()
+    ops.sgd_momentum_(w, m, g, lr, momentum=0.9, wd=0.01, rescale=1.0, clip=1.0)
+    gc = g.clamp(-1, 1)
+    m_ref = 0.9 * m0 - 0.1 * (gc + 0.01 * w0)
+    assert torch.allclose(m, m_ref) and torch.allclose(w, w0 + m_ref)
+
+
+# ---------------------------------------------------------------- GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype,C', [(torch.float32, 64), (torch.bfloat16, 1024), (torch.float32, 6)])
+def test_roi_pool_gpu(cuda, dtype, C):
+    g = torch.Generator().manual_seed(4)
+    B, H, W = 2, 38, 50
+    feat = torch.randn(B, C, H, W, generator=g)
+    rois = _rois(g, 64, B, H, W)
+    rois[3, 0] = -1  # invalid batch index
+    ref, arg_ref = roi_pool_ref(feat.to(dtype).float(), rois, 7, 7, 1 / 16)
+    fg = feat.to(cuda, dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
+    out = ops.roi_pool(fg, rois.to(cuda), (7, 7), 1 / 16)
+    assert torch.allclose(out.float().cpu(), ref, atol=0, rtol=0)
+    gout = torch.randn(out.shape, generator=g).to(cuda, dtype)
+    out.backward(gout)
+    # reference backward in fp32 from the reference argmax
+    gin = torch.zeros(B, C * H * W, dtype=torch.float64)
+    go = gout.double().cpu().reshape(64, C, -1)
+    a = arg_ref.reshape(64, C, -1).long()
+    for r in range(64):
+        b = int(rois[r, 0])
+        if b < 0:
+            continue
+        m = a[r] >= 0
+        gin[b].index_add_(0, (torch.arange(C)[:, None] * H * W + a[r].clamp_min(0))[m], go[r][m])
+    tol = 1e-4 if dtype == torch.float32 else 3e-2
+    assert torch.allclose(fg.grad.double().cpu().reshape(B, -1), gin, atol=tol, rtol=tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_losses_gpu(cuda, dtype):
+    g = torch.Generator().manual_seed(5)
+    B, A, H, W = 2, 12, 20, 31
+    logits = torch.randn(B, 2 * A, H, W, generator=g)
+    label = torch.randint(-1, 2, (B, A * H * W), generator=g)
+    lc = logits.to(dtype).float().requires_grad_()
+    l_cpu = ops.rpn_softmax_ce(lc, label)
+    l_cpu.backward()
+    lg = logits.to(cuda, dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
+    l_gpu = ops.rpn_softmax_ce(lg, label.to(cuda))
+    l_gpu.backward()
+    tol = 1e-5 if dtype == torch.float32 else 2e-3
+    assert abs(float(l_gpu) - float(l_cpu)) < 1e-4
+    assert torch.allclose(lg.grad.float().cpu(), lc.grad, atol=tol)
+
+    x = torch.randn(128, 81, generator=g)
+    lab = torch.randint(0, 81, (128,), generator=g)
+    xc = x.to(dtype).float().requires_grad_()
+    lcpu, pc = ops.softmax_ce(xc, lab)
+    lcpu.backward()
+    xg = x.to(cuda, dtype).requires_grad_()
+    lgpu, pg = ops.softmax_ce(xg, lab.to(cuda))
+    lgpu.backward()
+    assert abs(float(lgpu) - float(lcpu)) < 1e-4
+    assert torch.allclose(pg.cpu(), pc, atol=1e-5)
+    assert torch.allclose(xg.grad.float().cpu(), xc.grad, atol=tol)
+
+    pred = torch.randn(B, 4 * A, H, W, generator=g)
+    tgt = torch.randn(B, 4 * A, H, W, generator=g)
+    iw = (torch.rand(B, 4 * A, H, W, generator=g) > 0.7).float()
+    ow = iw / 256
+    pc_ = pred.to(dtype).float().requires_grad_()
+    s_cpu = ops.smooth_l1(pc_, tgt, iw, ow, 3.0, 1.0)
+    s_cpu.backward()
+    pg_ = pred.to(cuda, dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
+    s_gpu = ops.smooth_l1(pg_, tgt.to(cuda), iw.to(cuda), ow.to(cuda), 3.0, 1.0)
+    s_gpu.backward()
+    assert abs(float(s_gpu) - float(s_cpu)) < 1e-3 * max(1.0, abs(float(s_cpu)))
+    assert torch.allclose(pg_.grad.float().cpu(), pc_.grad, atol=tol)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype,C', [(torch.float32, 64), (torch.bfloat16, 256), (torch.bfloat16, 2048)])
+def test_frozen_bn_relu_gpu(cuda, dtype, C):
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(2, C, 9, 13, generator=g)
+    gamma, beta = torch.rand(C, generator=g), torch.randn(C, generator=g)
+    mean, var = torch.randn(C, generator=g), torch.rand(C, generator=g) + 0.5
+    xc = x.to(dtype).float().requires_grad_()
+    gc, bc = gamma.clone().requires_grad_(), beta.clone().requires_grad_()
+    y = ops.frozen_bn_relu(xc, gc, bc, mean, var)
+    dy = torch.randn(y.shape, generator=g).to(dtype).float()
+    y.backward(dy)
+    xg = x.to(cuda, dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
+    gg, bg = gamma.to(cuda).requires_grad_(), beta.to(cuda).requires_grad_()
+    yg = ops.frozen_bn_relu(xg, gg, bg, mean.to(cuda), var.to(cuda))
+    yg.backward(dy.to(cuda, dtype))
+    tol = 1e-5 if dtype == torch.float32 else 3e-2
+    assert torch.allclose(yg.float().cpu(), y.detach(), atol=tol, rtol=tol)
+    assert torch.allclose(xg.grad.float().cpu(), xc.grad, atol=tol, rtol=tol)
+    assert torch.allclose(gg.grad.cpu(), gc.grad, atol=1e-2, rtol=1e-2)
+    assert torch.allclose(bg.grad.cpu(), bc.grad, atol=1e-2, rtol=1e-2)
+
+
+@pytest.mark.gpu
+def test_sgd_gpu(cuda):
+    g = torch.Generator().manual_seed(7)
+    n = 100003
+    w = torch.randn(n, generator=g)
+    m = torch.randn(n, generator=g) * 0.01
+    gr = torch.randn(n, generator=g) * 2
+    lr = torch.tensor([0.01])
+    wc, mc = w.clone(), m.clone()
+    ops.sgd_momentum_(wc, mc, gr, lr, 0.9, 5e-4, 1.0, 1.0)
+    wg, mg = w.to(cuda), m.to(cuda)
+    wb = torch.empty(n, dtype=torch.bfloat16, device=cuda)
+    ops.sgd_momentum_(wg, mg, gr.to(cuda).bfloat16(), lr.to(cuda), 0.9, 5e-4, 1.0, 1.0, wb)
+    # bf16 grads -> loose; fp32 path exact
+    assert torch.allclose(wg.cpu(), wc, atol=1e-4)
+    assert torch.allclose(wb.float().cpu(), wg.cpu(), atol=1e-2, rtol=1e-2)
+    wg2, mg2 = w.to(cuda), m.to(cuda)
+    ops.sgd_momentum_(wg2, mg2, gr.to(cuda), lr.to(cuda), 0.9, 5e-4, 1.0, 1.0)
+    assert torch.allclose(wg2.cpu(), wc, atol=1e-6) and torch.allclose(mg2.cpu(), mc, atol=1e-6)

@@ -1,0 +1,104 @@
+"""Model families, parameter naming (SURVEY §2.12 counts), trainer step on CPU."""
+import pytest
+import torch
+
+from mx_rcnn_amd.config import snapshot
+from mx_rcnn_amd.models import FasterRCNN
+from mx_rcnn_amd.core.trainer import Trainer
+
+
+def _cfg():
+    cfg = snapshot()
+    cfg.TRAIN.BG_THRESH_LO = 0.0
+    cfg.END2END = 1
+    cfg.TRAIN.BBOX_NORMALIZATION_PRECOMPUTED = True
+    cfg.TRAIN.RPN_PRE_NMS_TOP_N = 800
+    cfg.TRAIN.RPN_POST_NMS_TOP_N = 300
+    return cfg
+
+
+def test_param_counts_match_reference():
+    m = FasterRCNN('vgg16', 21, cfg=_cfg())
+    a = m.arg_params()
+    assert len(a) == 40 and sum(v.numel() for v in a.values()) == 137078239
+    assert a['fc6_weight'].shape == (4096, 25088) and a['rpn_cls_score_weight'].shape == (18, 512, 1, 1)
+    r = FasterRCNN('resnet101', 21, cfg=_cfg())
+    assert len(r.arg_params()) == 318 and len(r.aux_params()) == 204
+    assert sum(v.numel() for v in r.arg_params().values()) == 47463799
+    r50 = FasterRCNN('resnet50', 21, cfg=_cfg())
+    assert len(r50.arg_params()) == 165 and len(r50.aux_params()) == 102
+    assert 'stage3_unit6_bn3_gamma' in r50.arg_params() and 'bn1_moving_var' in r50.aux_params()
+    assert r.arg_params()['rpn_cls_score_weight'].shape[0] == 24
+
+
+@pytest.mark.parametrize('net', ['resnet18', 'resnet34', 'resnet152'])
+def test_other_depths_build(net):
+    m = FasterRCNN(net, 2, cfg=_cfg())
+    assert m.num_anchors == 12
+    assert m.feat_shape(800, 1333) == (50, 84)
+
+
+def _batch(H=160, W=224):
+    gt = torch.tensor([[[10., 20., 80., 100., 3.], [50., 60., 150., 140., 7.], [-1, -1, -1, -1, -1]]])
+    return {'data': torch.randn(1, 3, H, W) * 50, 'im_info': torch.tensor([[float(H), float(W), 1.0]]),
+            'gt_boxes': gt, 'n_gt': torch.tensor([2], dtype=torch.int32)}
+
+
+def test_vgg_e2e_loss_decreases_cpu():
+    torch.manual_seed(0)
+    cfg = _cfg()
+    m = FasterRCNN('vgg16', 21, cfg=cfg)
+    m.head.dropout = 0.0
+    tr = Trainer(m, 'e2e', fixed_param_prefix=['conv1', 'conv2'], lr=0.002, device='cpu')
+    b = _batch()
+    outs = [tr.step(b) for _ in range(6)]
+    assert all(torch.isfinite(o['loss']) for o in outs)
+    # the sampled RoIs change every step, so compare the smooth parts of the objective
+    for k in ('rpn_cls_loss', 'rpn_bbox_loss', 'cls_loss'):
+        assert float(outs[-1][k]) < float(outs[0][k]), k
+
+
+def test_resnet_rpn_and_rcnn_modes_cpu():
+    torch.manual_seed(1)
+    cfg = _cfg()
+    m = FasterRCNN('resnet18', 21, cfg=cfg)
+    tr = Trainer(m, 'rpn', fixed_param_prefix=['conv0', 'stage1'], device='cpu')
+    out = tr.step(_batch())
+    assert torch.isfinite(out['loss'])
+    rois = torch.tensor([[0., 10, 20, 80, 100], [0., 30, 30, 90, 120]])
+    rb = {'data': _batch()['data'], 'rois': rois, 'label': torch.tensor([3, 0], dtype=torch.int32),
+          'bbox_target': torch.zeros(2, 84), 'bbox_inside_weight': torch.zeros(2, 84),
+          'bbox_outside_weight': torch.zeros(2, 84)}
+    tr2 = Trainer(m, 'rcnn', fixed_param_prefix=['conv0'], device='cpu')
+    out = tr2.step(rb)
+    assert torch.isfinite(out['loss'])
+    m.eval()
+    r, p, bb = m.detect(_batch()['data'], _batch()['im_info'])
+    assert r.shape[1] == 5 and p.shape[1] == 21 and bb.shape[1] == 84
+
+
+def test_frozen_prefix_substring_semantics():
+    m = FasterRCNN('resnet18', 21, cfg=_cfg())
+    tr = Trainer(m, 'e2e', fixed_param_prefix=['conv0', 'stage1', 'stage2', 'bn_data', 'bn0'], device='cpu')
+    assert 'conv0_weight' in tr.store.fixed_names
+    assert 'stage3_unit1_conv1_weight' not in tr.store.fixed_names
+    assert not tr.store.params['stage1_unit1_conv1_weight'].requires_grad
+    assert tr.store.params['stage3_unit1_conv1_weight'].requires_grad
+
+
+@pytest.mark.gpu
+def test_e2e_step_gpu_graph(cuda):
+    from mx_rcnn_amd.core.trainer import GraphedStep
+    torch.manual_seed(0)
+    cfg = _cfg()
+    m = FasterRCNN('resnet50', 21, cfg=cfg)
+    tr = Trainer(m, 'e2e', fixed_param_prefix=['conv0', 'stage1', 'stage2', 'bn_data', 'bn0'], device=cuda)
+    b = {k: v.to(cuda) for k, v in _batch(320, 480).items()}
+    out = tr.step(b)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out['loss'])
+    g = GraphedStep(tr, b, warmup=2)
+    for _ in range(3):
+        o = g(b)
+    torch.cuda.synchronize()
+    assert torch.isfinite(o['loss'])

@@ -2,8 +2,8 @@
 // outputs through the PyTorch caching allocator, launch on the current HIP stream.  All
 // launches are graph-capturable (no host sync, no allocation inside the launchers).
 #include <torch/extension.h>
+#include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
 
 #include "kernels.h"
 
@@ -11,7 +11,14 @@ namespace {
 
 using at::Tensor;
 
-hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+// PyTorch-ROCm registers its HIP runtime under the "cuda" device type, so tensors report
+// device type CUDA: guard with the generic DeviceGuard and fetch the HIP stream by index.
+thread_local c10::Device g_dev(c10::DeviceType::CUDA, 0);
+hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream(g_dev.index()).stream(); }
+struct DevGuard {
+  c10::DeviceGuard guard;
+  explicit DevGuard(const c10::Device& d) : guard(d) { g_dev = d; }
+};
 
 #define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
 #define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
@@ -35,7 +42,7 @@ std::vector<Tensor> proposal_decode(const Tensor& cls, const Tensor& dlt, const 
   TORCH_CHECK(cls.size(1) == 2 * A, "cls channels must be 2A");
   TORCH_CHECK(dlt.size(0) == B && dlt.size(1) == 4 * A && dlt.size(2) == H && dlt.size(3) == W, "dlt shape");
   TORCH_CHECK(im_info.size(0) == B && im_info.size(1) == 3, "im_info must be (B, 3)");
-  c10::hip::HIPGuard g(cls.device());
+  DevGuard g(cls.device());
   const int64_t N = (int64_t)H * W * A;
   auto opts = cls.options().dtype(at::kFloat);
   Tensor boxes = at::empty({B, N, 4}, opts);
@@ -61,7 +68,7 @@ std::vector<Tensor> nms_proposals(const Tensor& boxes, const Tensor& scores, con
   TORCH_CHECK(n_valid.numel() == B, "n_valid shape");
   TORCH_CHECK(rand_u.numel() == (int64_t)B * post, "rand_u must hold B*post values");
   TORCH_CHECK(post > 0, "post must be > 0");
-  c10::hip::HIPGuard g(boxes.device());
+  DevGuard g(boxes.device());
   const int nb = (P + 63) / 64;
   TORCH_CHECK(16 + (int64_t)nb * 8 + post * 4 <= 160 * 1024, "NMS LDS budget exceeded (P or post too large)");
   auto st = cur_stream();
@@ -89,7 +96,7 @@ std::vector<Tensor> iou_max(const Tensor& boxes, int64_t off, const Tensor& gt, 
   const int B = (int)boxes.size(0), N = (int)boxes.size(1), bs = (int)boxes.size(2), G = (int)gt.size(1);
   TORCH_CHECK(off + 4 <= bs, "box offset out of range");
   TORCH_CHECK(gt.size(0) == B && n_gt.numel() == B, "batch mismatch");
-  c10::hip::HIPGuard g(boxes.device());
+  DevGuard g(boxes.device());
   Tensor max_ov = at::empty({B, N}, boxes.options());
   Tensor argmax = at::empty({B, N}, boxes.options().dtype(at::kInt));
   Tensor gt_max = want_gt_max ? at::zeros({B, G}, boxes.options()) : Tensor();
@@ -109,7 +116,7 @@ std::vector<Tensor> anchor_target_assign(const Tensor& base_anchors, int64_t H, 
   CHECK_DEV(n_gt); CHECK_I32(n_gt); CHECK_CONTIG(n_gt);
   const int A = (int)base_anchors.size(0), B = (int)gt.size(0), G = (int)gt.size(1);
   TORCH_CHECK(im_info.size(0) == B && n_gt.numel() == B, "batch mismatch");
-  c10::hip::HIPGuard g(gt.device());
+  DevGuard g(gt.device());
   const int64_t N = H * W * A;
   auto o = gt.options();
   Tensor max_ov = at::empty({B, N}, o);
@@ -134,7 +141,7 @@ std::vector<Tensor> roi_pool_fwd(const Tensor& feat, const Tensor& rois, int64_t
   TORCH_CHECK(rois.dim() == 2 && rois.size(1) == 5, "rois must be (R, 5)");
   const int B = (int)feat.size(0), C = (int)feat.size(1), H = (int)feat.size(2), W = (int)feat.size(3);
   const int R = (int)rois.size(0);
-  c10::hip::HIPGuard g(feat.device());
+  DevGuard g(feat.device());
   Tensor out = at::empty({R, C, PH, PW}, feat.options().memory_format(at::MemoryFormat::ChannelsLast));
   Tensor argmax = at::empty({R, C, PH, PW}, feat.options().dtype(at::kInt).memory_format(at::MemoryFormat::ChannelsLast));
   mxr::roi_pool_fwd(feat.data_ptr(), is_bf16(feat), B, H, W, C, rois.data_ptr<float>(), R, (int)PH, (int)PW,
@@ -148,7 +155,7 @@ Tensor roi_pool_bwd(const Tensor& grad_out, const Tensor& argmax, const Tensor& 
   const int R = (int)grad_out.size(0), C = (int)grad_out.size(1), PH = (int)grad_out.size(2), PW = (int)grad_out.size(3);
   Tensor go = grad_out.contiguous(at::MemoryFormat::ChannelsLast);
   TORCH_CHECK(argmax.is_contiguous(at::MemoryFormat::ChannelsLast), "argmax must be channels_last");
-  c10::hip::HIPGuard g(grad_out.device());
+  DevGuard g(grad_out.device());
   auto st = cur_stream();
   Tensor gin32 = at::zeros({B, C, H, W}, grad_out.options().dtype(at::kFloat).memory_format(at::MemoryFormat::ChannelsLast));
   mxr::roi_pool_bwd(go.data_ptr(), is_bf16(go), argmax.data_ptr<int32_t>(), rois.contiguous().data_ptr<float>(), R,
@@ -168,7 +175,7 @@ std::vector<Tensor> rpn_softmax_ce(const Tensor& logits, const Tensor& label, co
   TORCH_CHECK(C2 % 2 == 0, "logits channels must be 2A");
   const int A = C2 / 2;
   TORCH_CHECK(label.numel() == (int64_t)B * A * H * W, "label must be (B, A*H*W)");
-  c10::hip::HIPGuard g(logits.device());
+  DevGuard g(logits.device());
   Tensor grad = at::empty_like(logits);
   TORCH_CHECK(grad.strides() == logits.strides(), "grad layout must match logits");
   Tensor loss = at::zeros({1}, logits.options().dtype(at::kFloat));
@@ -188,7 +195,7 @@ std::vector<Tensor> row_softmax_ce(const Tensor& logits, const Tensor& label, do
   TORCH_CHECK(logits.dim() == 2, "logits must be (R, C)");
   const int R = (int)logits.size(0), C = (int)logits.size(1);
   TORCH_CHECK(label.numel() == R, "label must be (R,)");
-  c10::hip::HIPGuard g(logits.device());
+  DevGuard g(logits.device());
   Tensor grad = want_grad ? at::empty_like(logits) : Tensor();
   Tensor prob = at::empty({R, C}, logits.options().dtype(at::kFloat));
   Tensor loss = at::zeros({1}, logits.options().dtype(at::kFloat));
@@ -209,7 +216,7 @@ std::vector<Tensor> smooth_l1(const Tensor& pred, const Tensor& tgt, const Tenso
   while (p4.dim() < 4) p4 = p4.unsqueeze(0);
   TORCH_CHECK(tgt.numel() == p4.numel() && in_w.numel() == p4.numel() && out_w.numel() == p4.numel(),
               "target/weights must match pred");
-  c10::hip::HIPGuard g(pred.device());
+  DevGuard g(pred.device());
   Tensor grad = at::empty_like(pred);
   Tensor g4 = grad;
   while (g4.dim() < 4) g4 = g4.unsqueeze(0);
@@ -234,7 +241,7 @@ void sgd_momentum(Tensor w, Tensor mom, const Tensor& grad, const Tensor& lr, do
                 "w_bf16 must be contiguous bf16 of the same size");
     wb = reinterpret_cast<uint16_t*>(w_bf16->data_ptr());
   }
-  c10::hip::HIPGuard g(w.device());
+  DevGuard g(w.device());
   mxr::sgd_momentum(w.data_ptr<float>(), mom.data_ptr<float>(), grad.data_ptr(), is_bf16(grad), w.numel(),
                     lr.data_ptr<float>(), (float)momentum, (float)wd, (float)rescale, (float)clip, wb, cur_stream());
 }
@@ -245,11 +252,11 @@ Tensor bn_relu_fwd(const Tensor& x, const Tensor& gamma, const Tensor& beta, con
   CHECK_DEV(x);
   TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "x must be channels_last 4-D");
   const int C = (int)x.size(1);
-  TORCH_CHECK(C % 4 == 0, "C must be a multiple of 4");
+  TORCH_CHECK(C <= 4096 || C % 4 == 0, "C must be a multiple of 4 or <= 4096");
   for (auto* t : {&gamma, &beta, &mean, &var}) {
     TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == C, "BN params fp32 (C,)");
   }
-  c10::hip::HIPGuard g(x.device());
+  DevGuard g(x.device());
   Tensor y = at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast);
   mxr::bn_relu_fwd(x.data_ptr(), is_bf16(x), x.numel() / C, C, gamma.data_ptr<float>(), beta.data_ptr<float>(),
                    mean.data_ptr<float>(), var.data_ptr<float>(), (float)eps, fix_gamma ? 1 : 0, relu ? 1 : 0,
@@ -265,7 +272,7 @@ std::vector<Tensor> bn_relu_bwd(const Tensor& x, const Tensor& dy, const Tensor&
   Tensor g = dy.contiguous(at::MemoryFormat::ChannelsLast);
   TORCH_CHECK(g.scalar_type() == x.scalar_type(), "dy dtype must match x");
   const int C = (int)x.size(1);
-  c10::hip::HIPGuard guard(x.device());
+  DevGuard guard(x.device());
   Tensor dx = need_dx ? at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast) : Tensor();
   Tensor dgamma = need_params ? at::zeros({C}, x.options().dtype(at::kFloat)) : Tensor();
   Tensor dbeta = need_params ? at::zeros({C}, x.options().dtype(at::kFloat)) : Tensor();

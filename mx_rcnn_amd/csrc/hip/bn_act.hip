@@ -102,6 +102,63 @@ bn_relu_bwd_kernel(const void* __restrict__ x, const void* __restrict__ dy, int 
     for (int k = 0; k < 4; ++k) if (ab[k] != 0.f) atomicAdd(dbeta + cv * 4 + k, ab[k]);
 }
 
+// Scalar path for channel counts that are not a multiple of 4 (bn_data on the 3-channel
+// image).  Each thread keeps a fixed channel (grid size multiple of C); the backward reduces
+// dgamma/dbeta through LDS so each block issues one global atomic per channel.
+__global__ void __launch_bounds__(256)
+bn_relu_fwd_scalar(const void* __restrict__ x, int bf16, int64_t M, int C, const float* __restrict__ gamma,
+                   const float* __restrict__ beta, const float* __restrict__ mean, const float* __restrict__ var,
+                   float eps, int fix_gamma, int relu, void* __restrict__ y) {
+  const int64_t T = (int64_t)gridDim.x * blockDim.x;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = (int)(tid % C);
+  float s, t;
+  bn_coeffs(c, gamma, beta, mean, var, eps, fix_gamma, s, t);
+  for (int64_t e = tid; e < M * C; e += T) {
+    float v = ld(x, e, bf16) * s + t;
+    if (relu) v = fmaxf(v, 0.f);
+    st(y, e, v, bf16);
+  }
+}
+
+__global__ void __launch_bounds__(256)
+bn_relu_bwd_scalar(const void* __restrict__ x, const void* __restrict__ dy, int bf16, int64_t M, int C,
+                   const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ mean,
+                   const float* __restrict__ var, float eps, int fix_gamma, int relu, void* __restrict__ dx,
+                   float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  extern __shared__ __attribute__((aligned(16))) float red[];  // 2*C
+  const int64_t T = (int64_t)gridDim.x * blockDim.x;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int c = (int)(tid % C);
+  for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) red[i] = 0.f;
+  __syncthreads();
+  float s, t;
+  bn_coeffs(c, gamma, beta, mean, var, eps, fix_gamma, s, t);
+  const float inv = rsqrtf(var[c] + eps), mu = mean[c];
+  float ag = 0.f, ab = 0.f;
+  for (int64_t e = tid; e < M * C; e += T) {
+    const float xv = ld(x, e, bf16);
+    const float g = ld(dy, e, bf16);
+    const float gm = (!relu || xv * s + t > 0.f) ? g : 0.f;
+    ab += gm;
+    ag += gm * (xv - mu) * inv;
+    if (dx) st(dx, e, gm * s, bf16);
+  }
+  atomicAdd(&red[c], ag);
+  atomicAdd(&red[C + c], ab);
+  __syncthreads();
+  for (int i = threadIdx.x; i < C; i += blockDim.x) {
+    if (dgamma && !fix_gamma && red[i] != 0.f) atomicAdd(dgamma + i, red[i]);
+    if (dbeta && red[C + i] != 0.f) atomicAdd(dbeta + i, red[C + i]);
+  }
+}
+
+static int bn_grid_scalar(int64_t M, int C) {
+  int64_t blocks = std::max<int64_t>(std::min<int64_t>((M * C + 255) / 256, 1024), 1);
+  while ((blocks * 256) % C != 0) ++blocks;
+  return (int)blocks;
+}
+
 static int bn_grid(int64_t M, int C) {
   const int CV = C >> 2;
   // threads must be a multiple of CV so each thread keeps one channel quad
@@ -114,6 +171,11 @@ static int bn_grid(int64_t M, int C) {
 void bn_relu_fwd(const void* x, int bf16, int64_t M, int C, const float* gamma, const float* beta, const float* mean,
                  const float* var, float eps, int fix_gamma, int relu, void* y, hipStream_t st) {
   if (M == 0 || C == 0) return;
+  if (C % 4 != 0) {
+    bn_relu_fwd_scalar<<<bn_grid_scalar(M, C), 256, 0, st>>>(x, bf16, M, C, gamma, beta, mean, var, eps, fix_gamma,
+                                                             relu, y);
+    return;
+  }
   bn_relu_fwd_kernel<<<bn_grid(M, C), 256, 0, st>>>(x, bf16, M, C, gamma, beta, mean, var, eps, fix_gamma, relu, y);
 }
 
@@ -121,6 +183,11 @@ void bn_relu_bwd(const void* x, const void* dy, int bf16, int64_t M, int C, cons
                  const float* mean, const float* var, float eps, int fix_gamma, int relu, void* dx, float* dgamma,
                  float* dbeta, hipStream_t st) {
   if (M == 0 || C == 0) return;
+  if (C % 4 != 0) {
+    bn_relu_bwd_scalar<<<bn_grid_scalar(M, C), 256, 2 * C * sizeof(float), st>>>(
+        x, dy, bf16, M, C, gamma, beta, mean, var, eps, fix_gamma, relu, dx, dgamma, dbeta);
+    return;
+  }
   bn_relu_bwd_kernel<<<bn_grid(M, C), 256, 0, st>>>(x, dy, bf16, M, C, gamma, beta, mean, var, eps, fix_gamma, relu,
                                                     dx, dgamma, dbeta);
 }

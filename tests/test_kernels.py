@@ -200,7 +200,8 @@ def test_losses_gpu(cuda, dtype):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize('dtype,C', [(torch.float32, 64), (torch.bfloat16, 256), (torch.bfloat16, 2048)])
+@pytest.mark.parametrize('dtype,C', [(torch.float32, 64), (torch.bfloat16, 256), (torch.bfloat16, 2048),
+                                     (torch.bfloat16, 3)])
 def test_frozen_bn_relu_gpu(cuda, dtype, C):
     g = torch.Generator().manual_seed(6)
     x = torch.randn(2, C, 9, 13, generator=g)

@@ -274,14 +274,48 @@ std::vector<Tensor> bn_relu_bwd(const Tensor& x, const Tensor& dy, const Tensor&
   const int C = (int)x.size(1);
   DevGuard guard(x.device());
   Tensor dx = need_dx ? at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast) : Tensor();
-  Tensor dgamma = need_params ? at::zeros({C}, x.options().dtype(at::kFloat)) : Tensor();
-  Tensor dbeta = need_params ? at::zeros({C}, x.options().dtype(at::kFloat)) : Tensor();
+  const bool vec = (C % 4 == 0);
+  Tensor dgamma = need_params ? (vec ? at::empty({C}, x.options().dtype(at::kFloat))
+                                     : at::zeros({C}, x.options().dtype(at::kFloat))) : Tensor();
+  Tensor dbeta = need_params ? (vec ? at::empty({C}, x.options().dtype(at::kFloat))
+                                    : at::zeros({C}, x.options().dtype(at::kFloat))) : Tensor();
+  Tensor ws;
+  if (need_params && vec) ws = at::empty({mxr::bn_bwd_workspace_floats(x.numel() / C, C)}, x.options().dtype(at::kFloat));
   mxr::bn_relu_bwd(x.data_ptr(), g.data_ptr(), is_bf16(x), x.numel() / C, C, gamma.data_ptr<float>(),
                    beta.data_ptr<float>(), mean.data_ptr<float>(), var.data_ptr<float>(), (float)eps,
                    fix_gamma ? 1 : 0, relu ? 1 : 0, need_dx ? dx.data_ptr() : nullptr,
                    need_params ? dgamma.data_ptr<float>() : nullptr, need_params ? dbeta.data_ptr<float>() : nullptr,
-                   cur_stream());
+                   ws.defined() ? ws.data_ptr<float>() : nullptr, cur_stream());
   return {dx, dgamma, dbeta};
+}
+
+// ---- implicit-GEMM conv ----------------------------------------------------------------
+Tensor conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::optional<Tensor> bias, int64_t stride, int64_t pad,
+                      bool relu, int64_t tile) {
+  CHECK_DEV(x); CHECK_DEV(w);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "bf16 only");
+  TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "x must be channels_last (N,C,H,W)");
+  TORCH_CHECK(w.dim() == 4 && w.is_contiguous(at::MemoryFormat::ChannelsLast), "w must be channels_last (O,I,kh,kw)");
+  const int NB = (int)x.size(0), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int Cout = (int)w.size(0), KH = (int)w.size(2), KW = (int)w.size(3);
+  TORCH_CHECK(w.size(1) == Cin, "channel mismatch");
+  TORCH_CHECK(Cin % 64 == 0, "conv_igemm requires Cin % 64 == 0");
+  const int Ho = (H + 2 * (int)pad - KH) / (int)stride + 1, Wo = (W + 2 * (int)pad - KW) / (int)stride + 1;
+  const float* bp = nullptr;
+  Tensor b;
+  if (bias.has_value() && bias->defined()) {
+    b = bias->to(at::kFloat).contiguous();
+    TORCH_CHECK(b.numel() == Cout, "bias size");
+    bp = b.data_ptr<float>();
+  }
+  DevGuard g(x.device());
+  Tensor y = at::empty({NB, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int used = mxr::conv_igemm_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                       reinterpret_cast<const uint16_t*>(w.data_ptr()), bp,
+                                       reinterpret_cast<uint16_t*>(y.data_ptr()), NB, H, W, Cin, Ho, Wo, Cout, KH, KW,
+                                       (int)stride, (int)pad, relu ? 1 : 0, (int)tile, cur_stream());
+  TORCH_CHECK(used > 0, "conv_igemm: unsupported shape");
+  return y;
 }
 
 }  // namespace
@@ -300,5 +334,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("sgd_momentum", &sgd_momentum);
   m.def("bn_relu_fwd", &bn_relu_fwd);
   m.def("bn_relu_bwd", &bn_relu_bwd);
+  m.def("conv_igemm_fwd", &conv_igemm_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),
+        py::arg("pad"), py::arg("relu"), py::arg("tile") = 0);
   m.attr("arch") = "gfx950";
 }

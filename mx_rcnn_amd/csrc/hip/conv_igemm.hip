@@ -1,0 +1,207 @@
+// Implicit-GEMM convolution on NHWC bf16 activations with MFMA (SURVEY kernels K1/K2/K3).
+//
+//   out[m][n] = sum_k A[m][k] * W[n][k],   m = (img, ho, wo), n = cout, k = (fr, fc, cin)
+//
+// A is never materialised: each K-step gathers 64 input channels of ONE filter tap for
+// BM output pixels straight from the NHWC map (out-of-image taps read as zero), so both
+// operands are K-contiguous in memory and land in LDS as [row][64] bf16 tiles (128 B rows)
+// with an XOR swizzle on the 16-B chunk index (chunk ^ ((row >> 1) & 7)), which makes the
+// MFMA-operand ds_read_b128 of 16 consecutive rows conflict-free.  Register-staged loads
+// for step k+1 are issued before the MFMAs of step k and written to the other LDS buffer
+// after them (one barrier per K-step).
+//
+// 256 threads = 4 wave64 in a 2x2 arrangement, wave tile (BM/2)x(BN/2) built from
+// v_mfma_f32_16x16x32_bf16 (fp32 accumulate).  Grid is 1-D with a bijective XCD remap so
+// the column tiles sharing an A row-panel run on one XCD's L2.  Epilogue fuses bias and
+// ReLU and stores bf16.  Requirements (checked by the launcher): Cin % 64 == 0.
+//
+// The same kernel computes the stride-1 data gradient (dgrad) as a forward convolution of
+// dY with the flipped / transposed filter (pad' = k-1-pad); see ops/conv.py.
+#include "common.h"
+#include "../kernels.h"
+
+namespace mxr {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BK = 64;  // bf16 elements per K-step (one 128-B row per tile row)
+
+__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
+
+template <int BM, int BN>
+__global__ void __launch_bounds__(256)
+conv_igemm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, const float* __restrict__ bias,
+                      uint16_t* __restrict__ y, int NB, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW,
+                      int stride, int pad, int relu, int tiles_n, int nwg) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int ACH = BM * 8 / 256;  // 16-B chunks of A per thread per K-step
+  constexpr int BCH = BN * 8 / 256;
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * (BM + BN) * BK];
+  uint16_t* As = lds;                    // [2][BM][BK]
+  uint16_t* Bs = lds + 2 * BM * BK;      // [2][BN][BK]
+
+  // bijective XCD-aware block remap (blocks that share an A panel -> same XCD)
+  const int bid = blockIdx.x;
+  const int q = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + bid / 8;
+  const int tm_idx = wgid / tiles_n, tn_idx = wgid % tiles_n;
+  const int m0 = tm_idx * BM, n0 = tn_idx * BN;
+  const int M = NB * Ho * Wo;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  // per-thread A rows: precompute pixel decomposition
+  int a_hi0[ACH], a_wi0[ACH], a_img[ACH], a_row[ACH], a_ch[ACH];
+#pragma unroll
+  for (int i = 0; i < ACH; ++i) {
+    const int qq = tid + i * 256;
+    a_row[i] = qq >> 3;
+    a_ch[i] = qq & 7;
+    const int m = m0 + a_row[i];
+    if (m < M) {
+      const int img = m / (Ho * Wo), rem = m % (Ho * Wo);
+      a_img[i] = img;
+      a_hi0[i] = (rem / Wo) * stride - pad;
+      a_wi0[i] = (rem % Wo) * stride - pad;
+    } else {
+      a_img[i] = -1; a_hi0[i] = 0; a_wi0[i] = 0;
+    }
+  }
+  int b_row[BCH], b_ch[BCH];
+#pragma unroll
+  for (int i = 0; i < BCH; ++i) {
+    const int qq = tid + i * 256;
+    b_row[i] = qq >> 3;
+    b_ch[i] = qq & 7;
+  }
+  const int K = KH * KW * Cin;
+  const int cin_steps = Cin / BK;
+  const int nk = KH * KW * cin_steps;
+
+  uint4 ra[ACH], rb[BCH];
+  auto load = [&](int ks) {
+    const int tap = ks / cin_steps;
+    const int ci0 = (ks % cin_steps) * BK;
+    const int fr = tap / KW, fc = tap % KW;
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int hi = a_hi0[i] + fr, wi = a_wi0[i] + fc;
+      if (a_img[i] >= 0 && hi >= 0 && hi < H && wi >= 0 && wi < W) {
+        const int64_t off = (((int64_t)a_img[i] * H + hi) * W + wi) * Cin + ci0 + a_ch[i] * 8;
+        ra[i] = *reinterpret_cast<const uint4*>(x + off);
+      } else {
+        ra[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const int co = n0 + b_row[i];
+      if (co < Cout) {
+        const int64_t off = (int64_t)co * K + tap * Cin + ci0 + b_ch[i] * 8;
+        rb[i] = *reinterpret_cast<const uint4*>(w + off);
+      } else {
+        rb[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < ACH; ++i)
+      *reinterpret_cast<uint4*>(As + (buf * BM + a_row[i]) * BK + swz(a_row[i], a_ch[i]) * 8) = ra[i];
+#pragma unroll
+    for (int i = 0; i < BCH; ++i)
+      *reinterpret_cast<uint4*>(Bs + (buf * BN + b_row[i]) * BK + swz(b_row[i], b_ch[i]) * 8) = rb[i];
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < nk) load(ks + 1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+      const int chunk = kk * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WM + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(As + (buf * BM + row) * BK + swz(row, chunk) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WN + j * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (buf * BN + row) * BK + swz(row, chunk) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    if (ks + 1 < nk) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  // epilogue: C/D map col = lane & 15, row = (lane >> 4) * 4 + r
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * WN + j * 16 + (lane & 15);
+    if (n >= Cout) continue;
+    const float bv = bias ? bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+        if (m < M) {
+          float v = acc[i][j][r] + bv;
+          if (relu) v = fmaxf(v, 0.f);
+          y[(int64_t)m * Cout + n] = f32_to_bf16(v);
+        }
+      }
+    }
+  }
+}
+
+template <int BM, int BN>
+static void launch_fwd(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int NB, int H, int W,
+                       int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int relu,
+                       hipStream_t st) {
+  const int M = NB * Ho * Wo;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (Cout + BN - 1) / BN;
+  const int nwg = tiles_m * tiles_n;
+  conv_igemm_fwd_kernel<BM, BN><<<nwg, 256, 0, st>>>(x, w, bias, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
+                                                     pad, relu, tiles_n, nwg);
+}
+
+int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int NB, int H, int W,
+                   int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, int tile,
+                   hipStream_t st) {
+  if (Cin % BK != 0) return -1;
+  const int64_t M = (int64_t)NB * Ho * Wo;
+  if (tile <= 0) {
+    // pick the largest tile that still puts >= ~2 waves of blocks on the 256 CUs
+    const int64_t b128 = ((M + 127) / 128) * ((Cout + 127) / 128);
+    const int64_t b12864 = ((M + 127) / 128) * ((Cout + 63) / 64);
+    if (b128 >= 512) tile = 1;
+    else if (b12864 >= 384) tile = 2;
+    else tile = 3;
+  }
+  switch (tile) {
+    case 1: launch_fwd<128, 128>(x, w, bias, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, st); break;
+    case 2: launch_fwd<128, 64>(x, w, bias, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, st); break;
+    default: launch_fwd<64, 64>(x, w, bias, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, st); break;
+  }
+  return tile;
+}
+
+}  // namespace mxr

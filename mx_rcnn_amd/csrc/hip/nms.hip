@@ -50,7 +50,7 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
   return ((uint64_t)hi << 32) | lo;
 }
 
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(1024)
 nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ scores,
                   const int32_t* __restrict__ n_valid, const uint64_t* __restrict__ mask, int P, int nb, int post,
                   const float* __restrict__ rand_u, float* __restrict__ rois, float* __restrict__ out_scores,
@@ -99,15 +99,23 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
     __syncthreads();
     const uint64_t kept = s_kept_bits;
     if (kept && s_nkeep < post) {
-      for (int c = rb + 1 + tid; c < nbv; c += blockDim.x) {
-        uint64_t acc = removed[c];
-        uint64_t k = kept;
-        while (k) {
-          const int j = __builtin_ctzll(k);
-          k &= k - 1;
-          acc |= mb[(int64_t)(rb * 64 + j) * nb + c];
+      // column-parallel OR of the kept rows: 4 thread groups each own 16 of the block's 64
+      // rows; loads are unconditional (masked after) so hipcc keeps 16 independent loads in
+      // flight instead of branching around each one
+      const int jq = tid >> 8, cidx = tid & 255;
+      const int nrow = min(64, P - rb * 64);
+      for (int c = rb + 1 + cidx; c < nbv; c += 256) {
+        uint64_t acc = 0;
+        const uint64_t* col = mb + (int64_t)(rb * 64) * nb + c;
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+          const int j = jq * 16 + jj;
+          if (j < nrow) {
+            const uint64_t v = col[(int64_t)j * nb];
+            acc |= ((kept >> j) & 1ull) ? v : 0ull;
+          }
         }
-        removed[c] = acc;
+        if (acc) atomicOr(reinterpret_cast<unsigned long long*>(&removed[c]), (unsigned long long)acc);
       }
     }
     __syncthreads();
@@ -147,7 +155,7 @@ void nms_reduce(const float* boxes, const float* scores, const int32_t* n_valid,
   if (B == 0) return;
   const int nb = div_up(P, 64);
   const size_t lds = 16 + ((nb * 8 + 15) / 16) * 16 + (size_t)post * 4;
-  nms_reduce_kernel<<<B, 256, lds, st>>>(boxes, scores, n_valid, mask, P, nb, post, rand_u, rois, out_scores,
+  nms_reduce_kernel<<<B, 1024, lds, st>>>(boxes, scores, n_valid, mask, P, nb, post, rand_u, rois, out_scores,
                                          keep_idx, n_keep);
 }
 

@@ -87,9 +87,20 @@ void sgd_momentum(float* w, float* mom, const void* grad, int grad_bf16, int64_t
 void bn_relu_fwd(const void* x, int bf16, int64_t M, int C, const float* gamma, const float* beta,
                  const float* mean, const float* var, float eps, int fix_gamma, int relu, void* y,
                  hipStream_t st);
-// dx = dy * [y>0] * s;  dgamma += sum(dy*[y>0]*xhat), dbeta += sum(dy*[y>0]) (fp32, zeroed by caller)
+// dx = dy * [y>0] * s;  dgamma = sum(dy*[y>0]*xhat), dbeta = sum(dy*[y>0]) (fp32; written, not
+// accumulated, on the vector path; the scalar C%4 path accumulates into zeroed buffers).
+// workspace: bn_bwd_workspace_floats(M, C) floats (per-block partial rows, no atomics).
+int bn_bwd_workspace_floats(int64_t M, int C);
 void bn_relu_bwd(const void* x, const void* dy, int bf16, int64_t M, int C, const float* gamma,
                  const float* beta, const float* mean, const float* var, float eps, int fix_gamma, int relu,
-                 void* dx, float* dgamma, float* dbeta, hipStream_t st);
+                 void* dx, float* dgamma, float* dbeta, float* workspace, hipStream_t st);
+
+// ---- implicit-GEMM convolution (conv_igemm.hip) ------------------------------
+// NHWC bf16 x (NB, H, W, Cin), weight (Cout, KH, KW, Cin) bf16, bias fp32 (Cout) or null,
+// y (NB, Ho, Wo, Cout) bf16.  tile: 0 = auto, 1 = 128x128, 2 = 128x64, 3 = 64x64.
+// Returns the tile used, or -1 if the shape is unsupported (Cin % 64 != 0).
+int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int NB, int H, int W,
+                   int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, int tile,
+                   hipStream_t st);
 
 }  // namespace mxr

@@ -44,7 +44,7 @@ class RPNHead(nn.Module):
         nn.init.normal_(self.rpn_bbox_pred.weight, 0, 0.001)
 
     def forward(self, feat):
-        x = F.relu(self.rpn_conv_3x3(feat), inplace=True)
+        x = self.rpn_conv_3x3(feat, relu=True)
         return self.rpn_cls_score(x), self.rpn_bbox_pred(x)
 
 

@@ -12,6 +12,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.bn import frozen_bn_relu
+from ..ops.conv import conv2d
 
 
 class MxLayer(nn.Module):
@@ -38,13 +39,14 @@ class Conv(MxLayer):
         self.bias = nn.Parameter(torch.zeros(cout)) if bias else None
         nn.init.normal_(self.weight, 0, 0.01)
 
-    def forward(self, x):
+    def forward(self, x, relu=False):
         b = None if self.bias is None else _w(self.bias, x)
         w = _w(self.weight, x)
         if self.weight.shape[-1] == 1 and self.pad == 0 and x.is_cuda and \
                 x.is_contiguous(memory_format=torch.channels_last):
-            return conv1x1_nhwc(x, w, b, self.stride)
-        return F.conv2d(x, w, b, stride=self.stride, padding=self.pad)
+            y = conv1x1_nhwc(x, w, b, self.stride)
+            return F.relu(y, inplace=True) if relu else y
+        return conv2d(x, w, b, self.stride, self.pad, relu)
 
 
 class Linear(MxLayer):

@@ -26,7 +26,7 @@ class VGG16Trunk(nn.Module):
 
     def forward(self, x):
         for i, c in enumerate(self.convs):
-            x = F.relu(c(x), inplace=True)
+            x = c(x, relu=True)
             if i in self.pool_after:
                 x = max_pool(x, 2, 2)
         return x

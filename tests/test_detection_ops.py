@@ -33,8 +33,14 @@ def test_batched_nms_separates_classes():
 
 
 def _rpn_inputs(seed, A, H, W, B=1, spread=2.0):
+    """Logits whose fg-bg margins are a permutation of an evenly spaced grid, so fp32 and fp64
+    scores sort identically (no near-ties) and the kernel/oracle orders can be compared."""
     g = torch.Generator().manual_seed(seed)
-    cls = torch.randn(B, 2 * A, H, W, generator=g) * spread
+    n = A * H * W
+    cls = torch.zeros(B, 2 * A, H, W)
+    for b in range(B):
+        margin = (torch.randperm(n, generator=g).float() / n * 2 - 1) * 2 * spread
+        cls[b, A:] = margin.reshape(A, H, W)
     dlt = torch.randn(B, 4 * A, H, W, generator=g) * 0.2
     return cls, dlt
 

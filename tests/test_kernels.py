@@ -242,3 +242,53 @@ def test_sgd_gpu(cuda):
     wg2, mg2 = w.to(cuda), m.to(cuda)
     ops.sgd_momentum_(wg2, mg2, gr.to(cuda), lr.to(cuda), 0.9, 5e-4, 1.0, 1.0)
     assert torch.allclose(wg2.cpu(), wc, atol=1e-6) and torch.allclose(mg2.cpu(), mc, atol=1e-6)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('shape', [
+    # N, Cin, H, W, Cout, k, s, p, bias, relu
+    (1, 64, 23, 37, 64, 3, 1, 1, False, False),
+    (2, 128, 13, 9, 192, 3, 1, 1, True, True),
+    (1, 256, 50, 84, 256, 3, 1, 1, False, False),
+    (1, 128, 31, 40, 128, 3, 2, 1, False, False),
+    (3, 512, 7, 7, 512, 3, 2, 1, False, False),
+    (1, 64, 20, 30, 96, 5, 1, 2, True, False),
+])
+def test_conv_igemm_fwd_vs_fp32(cuda, shape):
+    from mx_rcnn_amd.ops import need_ext
+    N, Cin, H, W, Cout, k, s, p, bias, relu = shape
+    g = torch.Generator().manual_seed(8)
+    x = torch.randn(N, Cin, H, W, generator=g).bfloat16()
+    w = (torch.randn(Cout, Cin, k, k, generator=g) * 0.05).bfloat16()
+    b = torch.randn(Cout, generator=g) if bias else None
+    ref = F.conv2d(x.float(), w.float(), b, stride=s, padding=p)
+    if relu:
+        ref = torch.relu(ref)
+    for tile in (1, 2, 3):
+        y = need_ext().conv_igemm_fwd(x.to(cuda).contiguous(memory_format=torch.channels_last),
+                                      w.to(cuda).contiguous(memory_format=torch.channels_last),
+                                      None if b is None else b.to(cuda), s, p, relu, tile)
+        err = (y.float().cpu() - ref).abs().max().item()
+        scale = ref.abs().max().item()
+        assert err <= 1e-2 * scale + 1e-2, (tile, err, scale)
+
+
+@pytest.mark.gpu
+def test_conv_igemm_autograd(cuda):
+    from mx_rcnn_amd.ops.conv import conv2d
+    g = torch.Generator().manual_seed(9)
+    x = torch.randn(1, 128, 21, 33, generator=g).bfloat16()
+    w = (torch.randn(192, 128, 3, 3, generator=g) * 0.05).bfloat16()
+    b = torch.randn(192, generator=g)
+    xr, wr, br = [t.float().clone().requires_grad_() for t in (x, w, b)]
+    yr = torch.relu(F.conv2d(xr, wr, br, padding=1))
+    dy = torch.randn(yr.shape, generator=g).bfloat16()
+    yr.backward(dy.float())
+    xg = x.to(cuda).contiguous(memory_format=torch.channels_last).requires_grad_()
+    wg = w.to(cuda).contiguous(memory_format=torch.channels_last).requires_grad_()
+    bg = b.to(cuda).requires_grad_()
+    yg = conv2d(xg, wg, bg, 1, 1, relu=True)
+    yg.backward(dy.to(cuda).contiguous(memory_format=torch.channels_last))
+    for a, r in [(yg, yr), (xg.grad, xr.grad), (wg.grad, wr.grad), (bg.grad, br.grad)]:
+        err = (a.float().cpu() - r.detach()).abs().max().item()
+        assert err <= 2e-2 * r.abs().max().item() + 2e-2, err

@@ -291,7 +291,7 @@ std::vector<Tensor> bn_relu_bwd(const Tensor& x, const Tensor& dy, const Tensor&
 
 // ---- implicit-GEMM conv ----------------------------------------------------------------
 Tensor conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::optional<Tensor> bias, int64_t stride, int64_t pad,
-                      bool relu, int64_t tile) {
+                      bool relu, int64_t tile, int64_t splits) {
   CHECK_DEV(x); CHECK_DEV(w);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "bf16 only");
   TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "x must be channels_last (N,C,H,W)");
@@ -310,10 +310,16 @@ Tensor conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::optional<Tensor> bi
   }
   DevGuard g(x.device());
   Tensor y = at::empty({NB, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  int auto_splits = 1;
+  const int t = mxr::conv_igemm_plan(NB, Ho, Wo, Cin, Cout, KH, KW, (int)tile, &auto_splits);
+  const int sp = splits > 0 ? (int)splits : auto_splits;
+  Tensor slab;
+  if (sp > 1) slab = at::empty({(int64_t)sp * NB * Ho * Wo * Cout}, x.options().dtype(at::kFloat));
   const int used = mxr::conv_igemm_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                                        reinterpret_cast<const uint16_t*>(w.data_ptr()), bp,
                                        reinterpret_cast<uint16_t*>(y.data_ptr()), NB, H, W, Cin, Ho, Wo, Cout, KH, KW,
-                                       (int)stride, (int)pad, relu ? 1 : 0, (int)tile, cur_stream());
+                                       (int)stride, (int)pad, relu ? 1 : 0, t, sp,
+                                       sp > 1 ? slab.data_ptr<float>() : nullptr, cur_stream());
   TORCH_CHECK(used > 0, "conv_igemm: unsupported shape");
   return y;
 }
@@ -335,6 +341,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_relu_fwd", &bn_relu_fwd);
   m.def("bn_relu_bwd", &bn_relu_bwd);
   m.def("conv_igemm_fwd", &conv_igemm_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),
-        py::arg("pad"), py::arg("relu"), py::arg("tile") = 0);
+        py::arg("pad"), py::arg("relu"), py::arg("tile") = 0, py::arg("splits") = 0);
   m.attr("arch") = "gfx950";
 }

@@ -115,15 +115,34 @@ bn_relu_bwd_kernel(const void* __restrict__ x, const void* __restrict__ dy, int 
   }
 }
 
+// Stage 2: 64 columns per block (one per lane), the 4 waves split the partial rows and keep
+// 8 independent loads in flight each (a serial per-thread loop over 160 rows was latency
+// bound at ~37 us/call), then combine through LDS.
 __global__ void __launch_bounds__(256)
 bn_part_reduce(const float* __restrict__ part, int nblk, int C, int fix_gamma, float* __restrict__ dgamma,
                float* __restrict__ dbeta) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= 2 * C) return;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + lane;
   float acc = 0.f;
-  for (int b = 0; b < nblk; ++b) acc += part[(int64_t)b * 2 * C + i];
-  if (i < C) { if (dgamma && !fix_gamma) dgamma[i] = acc; }
-  else if (dbeta) dbeta[i - C] = acc;
+  if (i < 2 * C) {
+    int b = wid;
+    for (; b + 28 < nblk; b += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(b + 4 * u) * 2 * C + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; b < nblk; b += 4) acc += part[(int64_t)b * 2 * C + i];
+  }
+  red[wid][lane] = acc;
+  __syncthreads();
+  if (wid == 0 && i < 2 * C) {
+    const float s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    if (i < C) { if (dgamma && !fix_gamma) dgamma[i] = s; }
+    else if (dbeta) dbeta[i - C] = s;
+  }
 }
 
 // Scalar path for channel counts that are not a multiple of 4 (bn_data on the 3-channel
@@ -221,7 +240,7 @@ void bn_relu_bwd(const void* x, const void* dy, int bf16, int64_t M, int C, cons
   float* part = (dgamma || dbeta) ? workspace : nullptr;
   bn_relu_bwd_kernel<<<nblk, 256, 2 * C * sizeof(float), st>>>(x, dy, bf16, M, C, gamma, beta, mean, var, eps,
                                                                fix_gamma, relu, dx, part);
-  if (part) bn_part_reduce<<<(2 * C + 255) / 256, 256, 0, st>>>(part, nblk, C, fix_gamma, dgamma, dbeta);
+  if (part) bn_part_reduce<<<(2 * C + 63) / 64, 256, 0, st>>>(part, nblk, C, fix_gamma, dgamma, dbeta);
 }
 
 }  // namespace mxr

@@ -33,7 +33,8 @@ template <int BM, int BN>
 __global__ void __launch_bounds__(256)
 conv_igemm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, const float* __restrict__ bias,
                       uint16_t* __restrict__ y, int NB, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW,
-                      int stride, int pad, int relu, int tiles_n, int nwg) {
+                      int stride, int pad, int relu, int tiles_n, int nwg, int ntiles, int splits,
+                      float* __restrict__ slab) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int ACH = BM * 8 / 256;  // 16-B chunks of A per thread per K-step
@@ -46,7 +47,8 @@ conv_igemm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
   const int bid = blockIdx.x;
   const int q = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
   const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + bid / 8;
-  const int tm_idx = wgid / tiles_n, tn_idx = wgid % tiles_n;
+  const int split = wgid / ntiles, tile = wgid % ntiles;
+  const int tm_idx = tile / tiles_n, tn_idx = tile % tiles_n;
   const int m0 = tm_idx * BM, n0 = tn_idx * BN;
   const int M = NB * Ho * Wo;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -78,10 +80,15 @@ conv_igemm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
   }
   const int K = KH * KW * Cin;
   const int cin_steps = Cin / BK;
-  const int nk = KH * KW * cin_steps;
+  const int nk_all = KH * KW * cin_steps;
+  const int per = (nk_all + splits - 1) / splits;
+  const int k_begin = split * per;
+  const int k_end = min(nk_all, k_begin + per);
+  const int nk = max(0, k_end - k_begin);
 
   uint4 ra[ACH], rb[BCH];
-  auto load = [&](int ks) {
+  auto load = [&](int kl) {
+    const int ks = k_begin + kl;
     const int tap = ks / cin_steps;
     const int ci0 = (ks % cin_steps) * BK;
     const int fr = tap / KW, fc = tap % KW;
@@ -121,8 +128,10 @@ conv_igemm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  load(0);
-  store(0);
+  if (nk > 0) {
+    load(0);
+    store(0);
+  }
   __syncthreads();
   for (int ks = 0; ks < nk; ++ks) {
     const int buf = ks & 1;
@@ -152,6 +161,22 @@ conv_igemm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
   }
 
   // epilogue: C/D map col = lane & 15, row = (lane >> 4) * 4 + r
+  if (splits > 1) {  // fp32 partial slab; bias/ReLU/cast happen in the reduce kernel
+    float* sp = slab + (int64_t)split * M * Cout;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WN + j * 16 + (lane & 15);
+      if (n >= Cout) continue;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+          if (m < M) sp[(int64_t)m * Cout + n] = acc[i][j][r];
+        }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn * WN + j * 16 + (lane & 15);
@@ -172,34 +197,72 @@ conv_igemm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
   }
 }
 
-template <int BM, int BN>
-static void launch_fwd(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int NB, int H, int W,
-                       int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int relu,
-                       hipStream_t st) {
-  const int M = NB * Ho * Wo;
-  const int tiles_m = (M + BM - 1) / BM, tiles_n = (Cout + BN - 1) / BN;
-  const int nwg = tiles_m * tiles_n;
-  conv_igemm_fwd_kernel<BM, BN><<<nwg, 256, 0, st>>>(x, w, bias, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
-                                                     pad, relu, tiles_n, nwg);
+// split-K reduce: y = act(sum_s slab[s] + bias), 4 outputs per thread (Cout % 4 == 0)
+__global__ void __launch_bounds__(256)
+splitk_reduce_kernel(const float* __restrict__ slab, int splits, int64_t MN, int Cout, const float* __restrict__ bias,
+                     int relu, uint16_t* __restrict__ y) {
+  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+  if (e >= MN) return;
+  float4 a = *reinterpret_cast<const float4*>(slab + e);
+  for (int sidx = 1; sidx < splits; ++sidx) {
+    const float4 b = *reinterpret_cast<const float4*>(slab + (int64_t)sidx * MN + e);
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  float v[4] = {a.x, a.y, a.z, a.w};
+  const int n = (int)(e % Cout);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (bias) v[k] += bias[n + k];
+    if (relu) v[k] = fmaxf(v[k], 0.f);
+  }
+  *reinterpret_cast<ushort4*>(y + e) = make_ushort4(f32_to_bf16(v[0]), f32_to_bf16(v[1]), f32_to_bf16(v[2]),
+                                                    f32_to_bf16(v[3]));
 }
 
-int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int NB, int H, int W,
-                   int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, int tile,
-                   hipStream_t st) {
-  if (Cin % BK != 0) return -1;
+template <int BM, int BN>
+static void launch_fwd(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int NB, int H, int W,
+                       int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, int splits,
+                       float* slab, hipStream_t st) {
+  const int M = NB * Ho * Wo;
+  const int tiles_m = (M + BM - 1) / BM, tiles_n = (Cout + BN - 1) / BN;
+  const int ntiles = tiles_m * tiles_n;
+  const int nwg = ntiles * splits;
+  conv_igemm_fwd_kernel<BM, BN><<<nwg, 256, 0, st>>>(x, w, bias, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
+                                                     pad, relu, tiles_n, nwg, ntiles, splits, slab);
+  if (splits > 1) {
+    const int64_t MN = (int64_t)M * Cout;
+    splitk_reduce_kernel<<<div_up((MN + 3) / 4, 256), 256, 0, st>>>(slab, splits, MN, Cout, bias, relu, y);
+  }
+}
+
+int conv_igemm_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int tile, int* splits_out) {
   const int64_t M = (int64_t)NB * Ho * Wo;
   if (tile <= 0) {
-    // pick the largest tile that still puts >= ~2 waves of blocks on the 256 CUs
     const int64_t b128 = ((M + 127) / 128) * ((Cout + 127) / 128);
     const int64_t b12864 = ((M + 127) / 128) * ((Cout + 63) / 64);
     if (b128 >= 512) tile = 1;
     else if (b12864 >= 384) tile = 2;
     else tile = 3;
   }
+  const int bm = tile == 3 ? 64 : 128, bn = tile == 1 ? 128 : 64;
+  const int64_t blocks = ((M + bm - 1) / bm) * ((Cout + bn - 1) / bn);
+  const int nk = KH * KW * (Cin / BK);
+  int splits = 1;
+  // latency-bound regime (few blocks per CU): split K until ~4 blocks per CU, >= 6 K-steps each
+  while (splits < 8 && blocks * splits * 2 <= 1024 && nk / (splits * 2) >= 6 && Cout % 4 == 0) splits *= 2;
+  *splits_out = splits;
+  return tile;
+}
+
+int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int NB, int H, int W,
+                   int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, int tile,
+                   int splits, float* slab, hipStream_t st) {
+  if (Cin % BK != 0) return -1;
+  if (splits > 1 && (slab == nullptr || Cout % 4 != 0)) return -1;
   switch (tile) {
-    case 1: launch_fwd<128, 128>(x, w, bias, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, st); break;
-    case 2: launch_fwd<128, 64>(x, w, bias, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, st); break;
-    default: launch_fwd<64, 64>(x, w, bias, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, st); break;
+    case 1: launch_fwd<128, 128>(x, w, bias, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, splits, slab, st); break;
+    case 2: launch_fwd<128, 64>(x, w, bias, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, splits, slab, st); break;
+    default: launch_fwd<64, 64>(x, w, bias, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, splits, slab, st); break;
   }
   return tile;
 }

@@ -71,29 +71,45 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
   for (int rb = 0; rb < nbv; ++rb) {
     if (s_nkeep >= post) break;  // uniform: read after a barrier
     if (tid < 64) {
+      // Resolve the 64-box block without a serial scalar chain: lane j holds COLUMN j of the
+      // block's diagonal 64x64 suppression tile (bit i set when box i suppresses box j), and
+      // the wave iterates kept <- {j candidate : no kept i < j suppresses j} to its fixpoint.
+      // Greedy NMS is the unique fixpoint (membership of j depends only on i < j), and the
+      // iteration count is the longest suppression chain in the block (usually a few), not
+      // the number of kept boxes.
       const int i = rb * 64 + tid;
       const uint64_t diag = (i < nv) ? mb[(int64_t)i * nb + rb] : 0ull;
       const int nrow = min(64, nv - rb * 64);
       const uint64_t valid = (nrow == 64) ? ~0ull : ((1ull << nrow) - 1ull);
-      uint64_t rem = removed[rb];
-      uint64_t kept = 0;
+      const uint64_t cand = valid & ~removed[rb];
+      uint64_t col = 0;
+      for (int r = 0; r < 64; ++r) {
+        const uint64_t row = readlane64(diag, r);
+        col |= ((row >> tid) & 1ull) << r;
+      }
+      uint64_t kept = cand;
+      for (int it = 0; it < 65; ++it) {
+        const bool keep_me = ((cand >> tid) & 1ull) && !(col & kept);
+        const uint64_t next = __ballot(keep_me);
+        if (next == kept) break;
+        kept = next;
+      }
       int nk = s_nkeep;
-      uint64_t cand = valid & ~rem;
-      while (cand && nk < post) {  // wave-uniform scalar loop over kept boxes only
-        const int j = __builtin_ctzll(cand);
-        kept |= (1ull << j);
-        ++nk;
-        rem |= readlane64(diag, j);
-        cand = valid & ~rem & ~((2ull << j) - 1ull);
+      const int cnt = __popcll(kept);
+      if (nk + cnt > post) {  // keep only the lowest (post - nk) boxes of this block
+        int need = post - nk;
+        uint64_t trunc = 0, k = kept;
+        while (need-- > 0 && k) { trunc |= k & (~k + 1); k &= k - 1; }
+        kept = trunc;
       }
       if ((kept >> tid) & 1ull) {
-        const int pos = s_nkeep + __popcll(kept & ((1ull << tid) - 1ull));
+        const int pos = nk + __popcll(kept & ((1ull << tid) - 1ull));
         keep_list[pos] = i;
       }
       __builtin_amdgcn_wave_barrier();
       if (tid == 0) {
         s_kept_bits = kept;
-        s_nkeep = nk;
+        s_nkeep = nk + __popcll(kept);
       }
     }
     __syncthreads();

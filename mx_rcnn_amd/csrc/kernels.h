@@ -98,9 +98,11 @@ void bn_relu_bwd(const void* x, const void* dy, int bf16, int64_t M, int C, cons
 // ---- implicit-GEMM convolution (conv_igemm.hip) ------------------------------
 // NHWC bf16 x (NB, H, W, Cin), weight (Cout, KH, KW, Cin) bf16, bias fp32 (Cout) or null,
 // y (NB, Ho, Wo, Cout) bf16.  tile: 0 = auto, 1 = 128x128, 2 = 128x64, 3 = 64x64.
+// conv_igemm_plan picks (tile, splits); splits > 1 needs an fp32 slab of splits*M*Cout floats.
 // Returns the tile used, or -1 if the shape is unsupported (Cin % 64 != 0).
+int conv_igemm_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int tile, int* splits_out);
 int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int NB, int H, int W,
                    int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, int tile,
-                   hipStream_t st);
+                   int splits, float* slab, hipStream_t st);
 
 }  // namespace mxr

@@ -4,22 +4,26 @@ the feature map is used in channels_last memory format, which is the framework's
 activation layout.  CPU: reference loops (test oracle)."""
 import math
 
+import numpy as np
 import torch
 
 from ._ext import need_ext
 
 
 def _bins(roi, PH, PW, H, W, scale):
-    x1 = int(_round(float(roi[1]) * scale)); y1 = int(_round(float(roi[2]) * scale))
-    x2 = int(_round(float(roi[3]) * scale)); y2 = int(_round(float(roi[4]) * scale))
+    """Bin edges with MXNet's float32 arithmetic (static_cast<float>(ph) * bin_size)."""
+    f = np.float32
+    sc = f(scale)
+    x1 = int(_round(float(f(roi[1]) * sc))); y1 = int(_round(float(f(roi[2]) * sc)))
+    x2 = int(_round(float(f(roi[3]) * sc))); y2 = int(_round(float(f(roi[4]) * sc)))
     rw = max(x2 - x1 + 1, 1); rh = max(y2 - y1 + 1, 1)
-    bh = rh / PH; bw = rw / PW
+    bh = f(rh) / f(PH); bw = f(rw) / f(PW)
     for ph in range(PH):
-        hs = min(max(int(math.floor(ph * bh)) + y1, 0), H)
-        he = min(max(int(math.ceil((ph + 1) * bh)) + y1, 0), H)
+        hs = min(max(int(math.floor(f(ph) * bh)) + y1, 0), H)
+        he = min(max(int(math.ceil(f(ph + 1) * bh)) + y1, 0), H)
         for pw in range(PW):
-            ws = min(max(int(math.floor(pw * bw)) + x1, 0), W)
-            we = min(max(int(math.ceil((pw + 1) * bw)) + x1, 0), W)
+            ws = min(max(int(math.floor(f(pw) * bw)) + x1, 0), W)
+            we = min(max(int(math.ceil(f(pw + 1) * bw)) + x1, 0), W)
             yield ph, pw, hs, he, ws, we
 
 
@@ -65,7 +69,6 @@ class _RoIPool(torch.autograd.Function):
             out, arg = roi_pool_ref(feat, rois, PH, PW, scale)
         ctx.save_for_backward(arg, rois)
         ctx.shape = (B, C, H, W)
-        ctx.mark_non_differentiable(arg)
         return out
 
     @staticmethod

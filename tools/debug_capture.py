@@ -1,5 +1,9 @@
 """Find which op of the training step refuses hipGraph stream capture."""
+import os
+import sys
 import traceback
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch
 

@@ -324,6 +324,31 @@ Tensor conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::optional<Tensor> bi
   return y;
 }
 
+Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
+                  int64_t splits) {
+  CHECK_DEV(dy); CHECK_DEV(x);
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "bf16 only");
+  TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "dy/x must be channels_last");
+  const int NB = (int)x.size(0), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int Cout = (int)dy.size(1), Ho = (int)dy.size(2), Wo = (int)dy.size(3);
+  TORCH_CHECK(dy.size(0) == NB, "batch mismatch");
+  TORCH_CHECK(Cin % 64 == 0 && Cout % 8 == 0, "conv_wgrad requires Cin % 64 == 0 and Cout % 8 == 0");
+  TORCH_CHECK(Ho == (H + 2 * pad - KH) / stride + 1 && Wo == (W + 2 * pad - KW) / stride + 1, "geometry mismatch");
+  DevGuard g(x.device());
+  int sp = 1;
+  mxr::conv_wgrad_plan(NB, Ho, Wo, Cin, Cout, (int)KH, (int)KW, &sp);
+  if (splits > 0) sp = (int)splits;
+  Tensor dw = at::empty({Cout, Cin, KH, KW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor slab = at::empty({(int64_t)sp * Cout * KH * KW * Cin}, x.options().dtype(at::kFloat));
+  const int r = mxr::conv_wgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                                reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                reinterpret_cast<uint16_t*>(dw.data_ptr()), slab.data_ptr<float>(), NB, H, W, Cin, Ho,
+                                Wo, Cout, (int)KH, (int)KW, (int)stride, (int)pad, sp, cur_stream());
+  TORCH_CHECK(r > 0, "conv_wgrad: unsupported shape");
+  return dw;
+}
+
 }  // namespace
 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
@@ -342,5 +367,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_relu_bwd", &bn_relu_bwd);
   m.def("conv_igemm_fwd", &conv_igemm_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),
         py::arg("pad"), py::arg("relu"), py::arg("tile") = 0, py::arg("splits") = 0);
+  m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"), py::arg("stride"),
+        py::arg("pad"), py::arg("splits") = 0);
   m.attr("arch") = "gfx950";
 }

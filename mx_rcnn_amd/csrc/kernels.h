@@ -105,4 +105,11 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, const float* bias, uint
                    int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, int tile,
                    int splits, float* slab, hipStream_t st);
 
+// ---- MFMA weight gradient (conv_wgrad.hip) -------------------------------------
+// dy (NB, Ho, Wo, Cout) bf16, x (NB, H, W, Cin) bf16 -> dw (Cout, KH, KW, Cin) bf16.
+// slab: splits * Cout * KH*KW*Cin floats.  Requires Cin % 64 == 0, Cout % 8 == 0.
+int conv_wgrad_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int* splits_out);
+int conv_wgrad(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab, int NB, int H, int W, int Cin,
+               int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int splits, hipStream_t st);
+
 }  // namespace mxr

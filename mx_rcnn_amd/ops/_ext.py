@@ -52,3 +52,19 @@ def check_sync(name):
         torch.cuda.synchronize()
         err = torch.cuda.current_stream()  # touching the stream surfaces async errors
         del err
+
+
+_CONSTS = {}
+
+
+def const_tensor(values, device, dtype=None):
+    """Cached small constant tensor on ``device`` (built once, outside any hipGraph capture:
+    creating it from host data inside a capture would be a forbidden synchronous copy)."""
+    import torch
+    dtype = dtype or torch.float32
+    key = (tuple(float(v) for v in values), str(device), dtype)
+    t = _CONSTS.get(key)
+    if t is None:
+        t = torch.tensor([float(v) for v in values], dtype=dtype, device=device)
+        _CONSTS[key] = t
+    return t

@@ -10,7 +10,7 @@ inside / outside weights (B, 4A, H, W).
 import torch
 
 from ..config import config as _global_cfg
-from ._ext import need_ext
+from ._ext import need_ext, const_tensor
 from .anchors import base_anchors
 from .boxes import bbox_transform, box_iou
 from .sampling import keep_random
@@ -88,7 +88,7 @@ def anchor_target(feat_shape, gt_boxes, n_gt, im_info, feat_stride=16, scales=(8
         bg_keep = keep_random(bg, num_bg, generator)
         label = torch.where(bg & ~bg_keep, torch.full_like(label, -1), label)
         # weights (RPN_POSITIVE_WEIGHT < 0: uniform 1/num_examples)
-        inside_w = torch.tensor(cfg.TRAIN.RPN_BBOX_INSIDE_WEIGHTS, dtype=torch.float32, device=dev)
+        inside_w = const_tensor(cfg.TRAIN.RPN_BBOX_INSIDE_WEIGHTS, dev)
         inside = (label == 1).float()[..., None] * inside_w
         if cfg.TRAIN.RPN_POSITIVE_WEIGHT < 0:
             num_ex = (label >= 0).sum(dim=1).clamp_min(1).float()

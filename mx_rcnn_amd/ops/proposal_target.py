@@ -7,11 +7,13 @@ bg in [BG_LO, BG_HI) (TRAIN fallback [0, BG_HI+0.2) when empty), labels zeroed f
 fg_this onwards, class-specific targets (optionally normalised by BBOX_MEANS/STDS) with
 inside weights on the assigned class slot and outside = (inside > 0).
 """
+import numpy as np
 import torch
 
 from ..config import config as _global_cfg
 from .boxes import bbox_transform, iou_max
 from .sampling import sample_slots
+from ._ext import const_tensor
 
 
 def proposal_target(rois, gt_boxes, n_gt, num_classes, cfg=None, is_train=True, generator=None):
@@ -56,15 +58,15 @@ def proposal_target(rois, gt_boxes, n_gt, num_classes, cfg=None, is_train=True, 
             if G > 0 else torch.zeros(B, R, 4, device=dev)
         t = bbox_transform(out_rois[..., 1:5], gt_sel)
         if cfg.TRAIN.BBOX_NORMALIZATION_PRECOMPUTED:
-            means = torch.tensor(cfg.TRAIN.BBOX_MEANS, dtype=torch.float32, device=dev)
-            stds = torch.tensor(cfg.TRAIN.BBOX_STDS, dtype=torch.float32, device=dev)
+            means = const_tensor(cfg.TRAIN.BBOX_MEANS, dev)
+            stds = const_tensor(cfg.TRAIN.BBOX_STDS, dev)
             t = (t - means) / stds
         pos = labels > 0
         t = torch.where(pos[..., None], t, torch.zeros_like(t))
         cls = labels.long().clamp(0, num_classes - 1)
         onehot = torch.nn.functional.one_hot(cls, num_classes).to(torch.float32) * pos[..., None].float()
         targets = (onehot[..., None] * t[..., None, :]).reshape(B, R, 4 * num_classes)
-        inside_w = torch.tensor(cfg.TRAIN.BBOX_INSIDE_WEIGHTS, dtype=torch.float32, device=dev)
+        inside_w = const_tensor(np.asarray(cfg.TRAIN.BBOX_INSIDE_WEIGHTS).ravel(), dev)
         inside = (onehot[..., None] * inside_w).reshape(B, R, 4 * num_classes)
         outside = (inside > 0).float()
         return {'rois': out_rois.reshape(B * R, 5).contiguous(),

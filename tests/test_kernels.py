@@ -299,3 +299,29 @@ def test_conv_igemm_autograd(cuda):
     for a, r in [(yg, yr), (xg.grad, xr.grad), (wg.grad, wr.grad), (bg.grad, br.grad)]:
         err = (a.float().cpu() - r.detach()).abs().max().item()
         assert err <= 2e-2 * r.abs().max().item() + 2e-2, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('shape', [
+    # N, Cin, H, W, Cout, k, s, p
+    (1, 64, 23, 37, 64, 3, 1, 1),
+    (1, 256, 50, 84, 256, 3, 1, 1),
+    (2, 128, 13, 9, 192, 3, 2, 1),
+    (1, 1024, 50, 84, 512, 3, 1, 1),
+    (1, 128, 20, 30, 64, 1, 1, 0),
+])
+def test_conv_wgrad_vs_fp32(cuda, shape):
+    from mx_rcnn_amd.ops import need_ext
+    N, Cin, H, W, Cout, k, s, p = shape
+    g = torch.Generator().manual_seed(10)
+    x = torch.randn(N, Cin, H, W, generator=g).bfloat16()
+    w = torch.zeros(Cout, Cin, k, k)
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = torch.randn(N, Cout, Ho, Wo, generator=g).bfloat16()
+    ref = torch.ops.aten.convolution_backward(dy.float(), x.float(), w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
+                                              [False, True, False])[1]
+    for splits in (1, 0):
+        dw = need_ext().conv_wgrad(dy.to(cuda).contiguous(memory_format=torch.channels_last),
+                                   x.to(cuda).contiguous(memory_format=torch.channels_last), k, k, s, p, splits)
+        err = (dw.float().cpu() - ref).abs().max().item()
+        assert err <= 1e-2 * ref.abs().max().item() + 1e-2, (splits, err)

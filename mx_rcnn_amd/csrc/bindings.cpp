@@ -157,7 +157,9 @@ Tensor roi_pool_bwd(const Tensor& grad_out, const Tensor& argmax, const Tensor& 
   TORCH_CHECK(argmax.is_contiguous(at::MemoryFormat::ChannelsLast), "argmax must be channels_last");
   DevGuard g(grad_out.device());
   auto st = cur_stream();
-  Tensor gin32 = at::zeros({B, C, H, W}, grad_out.options().dtype(at::kFloat).memory_format(at::MemoryFormat::ChannelsLast));
+  // NOTE: at::zeros ignores a memory_format carried in TensorOptions (returns NCHW); allocate
+  // the NHWC buffer explicitly and view it as logical NCHW.
+  Tensor gin32 = at::zeros({B, H, W, C}, grad_out.options().dtype(at::kFloat)).permute({0, 3, 1, 2});
   mxr::roi_pool_bwd(go.data_ptr(), is_bf16(go), argmax.data_ptr<int32_t>(), rois.contiguous().data_ptr<float>(), R,
                     PH, PW, (int)B, (int)H, (int)W, C, gin32.data_ptr<float>(), st);
   if (grad_out.scalar_type() == at::kFloat) return gin32;

@@ -1,0 +1,269 @@
+"""Data iterators (reference `rcnn/loader.py:9-330`): ``AnchorLoader`` for RPN / end-to-end
+training, ``ROIIter`` for Fast R-CNN on precomputed proposals and for testing.
+
+MI355X-first differences from the reference's single-threaded MXNet DataIter:
+
+* Anchor targets are NOT computed here: the loader ships images + gt boxes and the model
+  step assigns anchors on the device (HIP kernels), so the host never runs the IoU loop.
+* A background thread pool decodes / resizes the next batches while the GPU trains
+  (``prefetch`` batches in flight) into pinned host memory; the trainer copies them with
+  non_blocking H2D transfers.
+* Data parallel: one process per GPU; every rank draws the SAME shuffled order (seeded per
+  epoch) and takes its strided shard of the batches, so aspect-grouped pairs stay together.
+* ``pad_shape`` pads every image to a fixed (H, W) (e.g. the reference's max shape) so the
+  step has static shapes and can replay a hipGraph; otherwise images are padded to the batch
+  max like the reference's ``tensor_vstack``.
+* Multiple images per device are supported (the reference asserts one).
+"""
+import queue
+import threading
+
+import numpy as np
+import torch
+
+from ..config import config
+from ..processing.image_processing import tensor_vstack
+from . import minibatch
+
+
+class _Prefetcher:
+    def __init__(self, make_batch, n_batches, prefetch=2, workers=2):
+        self.make_batch = make_batch
+        self.n = n_batches
+        self.q = queue.Queue(maxsize=max(1, prefetch))
+        self.workers = max(1, workers)
+        self._next = 0
+        self._lock = threading.Lock()
+        self._results = {}
+        self._cv = threading.Condition()
+        self._stop = False
+        self._threads = [threading.Thread(target=self._work, daemon=True) for _ in range(self.workers)]
+        self._sem = threading.Semaphore(max(1, prefetch) + self.workers)
+        for t in self._threads:
+            t.start()
+
+    def _work(self):
+        while True:
+            self._sem.acquire()
+            with self._lock:
+                if self._stop or self._next >= self.n:
+                    self._sem.release()
+                    return
+                i = self._next
+                self._next += 1
+            try:
+                res = self.make_batch(i)
+            except Exception as e:  # surfaced to the consumer
+                res = e
+            with self._cv:
+                self._results[i] = res
+                self._cv.notify_all()
+
+    def get(self, i):
+        with self._cv:
+            while i not in self._results:
+                self._cv.wait()
+            res = self._results.pop(i)
+        self._sem.release()
+        if isinstance(res, Exception):
+            raise res
+        return res
+
+    def close(self):
+        with self._lock:
+            self._stop = True
+        for _ in self._threads:
+            self._sem.release()
+
+
+def _pin(t):
+    t = torch.as_tensor(t)
+    try:
+        return t.pin_memory() if torch.cuda.is_available() else t
+    except RuntimeError:
+        return t
+
+
+def aspect_grouped_order(roidb, rng):
+    """Horizontal vs vertical groups, shuffled pairs (reference `rcnn/loader.py:62-83`)."""
+    widths = np.array([r.get('width', 1) for r in roidb])
+    heights = np.array([r.get('height', 1) for r in roidb])
+    horz = widths >= heights
+    inds = np.hstack((rng.permutation(np.where(horz)[0]), rng.permutation(np.where(~horz)[0])))
+    if inds.shape[0] % 2:
+        pairs = inds[:-1].reshape(-1, 2)
+        inds[:-1] = pairs[rng.permutation(pairs.shape[0])].reshape(-1)
+    else:
+        pairs = inds.reshape(-1, 2)
+        inds = pairs[rng.permutation(pairs.shape[0])].reshape(-1)
+    return inds
+
+
+class _BaseLoader:
+    def __init__(self, roidb, batch_size, shuffle, mode, ctx, work_load_list, rank, world_size, seed, prefetch,
+                 workers):
+        self.roidb = roidb
+        self.batch_size = batch_size
+        self.shuffle = shuffle
+        self.mode = mode
+        self.ctx = ctx
+        self.work_load_list = work_load_list
+        self.rank, self.world_size = rank, world_size
+        self.seed = seed
+        self.epoch = 0
+        self.prefetch, self.workers = prefetch, workers
+        self.size = len(roidb)
+        self.index = np.arange(self.size)
+        self.cur = 0
+        self._pf = None
+        self.reset()
+
+    # -- order / sharding
+    def reset(self):
+        self.cur = 0
+        if self._pf is not None:
+            self._pf.close()
+        if self.shuffle:
+            rng = np.random.RandomState(self.seed + self.epoch)
+            if config.TRAIN.ASPECT_GROUPING and 'width' in self.roidb[0]:
+                self.index = aspect_grouped_order(self.roidb, rng)
+            else:
+                self.index = rng.permutation(self.size)
+        self.epoch += 1
+        self._batches = self._shard_batches()
+        self._pf = _Prefetcher(self._make_batch, len(self._batches), self.prefetch, self.workers)
+
+    def _shard_batches(self):
+        nb = self.size // self.batch_size
+        all_b = [self.index[i * self.batch_size:(i + 1) * self.batch_size] for i in range(nb)]
+        if self.world_size > 1:
+            n = (len(all_b) // self.world_size) * self.world_size  # equal steps on every rank
+            all_b = all_b[self.rank:n:self.world_size]
+        return all_b
+
+    def __len__(self):
+        return len(self._batches)
+
+    def iter_next(self):
+        return self.cur < len(self._batches)
+
+    def getindex(self):
+        return self.cur
+
+    def getpad(self):
+        return 0
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        if not self.iter_next():
+            raise StopIteration
+        b = self._pf.get(self.cur)
+        self.cur += 1
+        return b
+
+    next = __next__
+
+    def get_batch(self):
+        return self._make_batch(min(self.cur, len(self._batches) - 1))
+
+
+class AnchorLoader(_BaseLoader):
+    """RPN / end-to-end loader.  Batches: data (B,3,H,W) fp32, im_info (B,3), gt_boxes (B,G,5)
+    padded with -1, n_gt (B,) int32.  ``feat_sym`` (the model, or anything with
+    ``feat_shape(h, w)``) is kept for API parity and shape reporting."""
+
+    def __init__(self, feat_sym, roidb, batch_size=1, shuffle=False, mode='train', ctx=None, work_load_list=None,
+                 feat_stride=16, anchor_scales=(8, 16, 32), anchor_ratios=(0.5, 1, 2), allowed_border=0,
+                 need_mean=True, rank=0, world_size=1, seed=0, prefetch=2, workers=2, pad_shape=None, max_gt=None):
+        self.feat_sym = feat_sym
+        self.feat_stride, self.anchor_scales, self.anchor_ratios = feat_stride, anchor_scales, anchor_ratios
+        self.allowed_border, self.need_mean = allowed_border, need_mean
+        self.pad_shape, self.max_gt = pad_shape, max_gt
+        self.data_name = ['data', 'im_info']
+        self.label_name = ['gt_boxes', 'n_gt']
+        super().__init__(roidb, batch_size, shuffle, mode, ctx, work_load_list, rank, world_size, seed, prefetch,
+                         workers)
+
+    def _make_batch(self, i):
+        entries = [self.roidb[j] for j in self._batches[i]]
+        data, label = minibatch.get_minibatch(entries, 0, self.mode, need_mean=self.need_mean, has_rpn=True)
+        im = data['data']
+        if self.pad_shape is not None:
+            ph, pw = self.pad_shape
+            if im.shape[2] > ph or im.shape[3] > pw:
+                raise ValueError('image %s larger than pad_shape %s' % (im.shape[2:], self.pad_shape))
+            padded = np.zeros((im.shape[0], 3, ph, pw), np.float32)
+            padded[:, :, :im.shape[2], :im.shape[3]] = im
+            im = padded
+        gts = label.get('gt_boxes', [np.zeros((0, 5), np.float32)] * len(entries))
+        G = max(1, max(g.shape[0] for g in gts)) if self.max_gt is None else self.max_gt
+        gt = np.full((len(entries), G, 5), -1.0, np.float32)
+        n_gt = np.zeros((len(entries),), np.int32)
+        for k, g in enumerate(gts):
+            n = min(g.shape[0], G)
+            gt[k, :n] = g[:n]
+            n_gt[k] = n
+        return {'data': _pin(np.ascontiguousarray(im, dtype=np.float32)), 'im_info': _pin(data['im_info']),
+                'gt_boxes': _pin(gt), 'n_gt': _pin(n_gt)}
+
+    @property
+    def provide_data(self):
+        b = self.get_batch()
+        return [('data', tuple(b['data'].shape)), ('im_info', tuple(b['im_info'].shape))]
+
+    @property
+    def provide_label(self):
+        b = self.get_batch()
+        out = [('gt_boxes', tuple(b['gt_boxes'].shape))]
+        if self.feat_sym is not None and hasattr(self.feat_sym, 'feat_shape'):
+            h, w = self.feat_sym.feat_shape(b['data'].shape[2], b['data'].shape[3])
+            A = len(self.anchor_scales) * len(self.anchor_ratios)
+            out += [('label', (b['data'].shape[0], A * h * w)), ('bbox_target', (b['data'].shape[0], 4 * A, h, w)),
+                    ('bbox_inside_weight', (b['data'].shape[0], 4 * A, h, w)),
+                    ('bbox_outside_weight', (b['data'].shape[0], 4 * A, h, w))]
+        return out
+
+
+class ROIIter(_BaseLoader):
+    """Fast R-CNN loader (offline proposals).  train: data, rois (B*R, 5), label, bbox_target,
+    bbox_inside_weight, bbox_outside_weight; test: data, rois, im_info."""
+
+    def __init__(self, roidb, batch_size=2, shuffle=False, mode='train', ctx=None, work_load_list=None,
+                 rank=0, world_size=1, seed=0, prefetch=2, workers=2, need_mean=True):
+        self.num_classes = roidb[0]['gt_overlaps'].shape[1]
+        self.need_mean = need_mean
+        self.data_name = ['data', 'rois']
+        self.label_name = ['label', 'bbox_target', 'bbox_inside_weight', 'bbox_outside_weight']
+        super().__init__(roidb, batch_size, shuffle, mode, ctx, work_load_list, rank, world_size, seed, prefetch,
+                         workers)
+
+    def _make_batch(self, i):
+        entries = [self.roidb[j] for j in self._batches[i]]
+        data, label = minibatch.get_minibatch(entries, self.num_classes, self.mode, need_mean=self.need_mean,
+                                              has_rpn=False)
+        out = {'data': _pin(np.ascontiguousarray(data['data'], dtype=np.float32))}
+        if self.mode == 'train':
+            out['rois'] = _pin(data['rois'].reshape(-1, 5).astype(np.float32))
+            out['label'] = _pin(label['label'].reshape(-1).astype(np.int32))
+            for k in ('bbox_target', 'bbox_inside_weight', 'bbox_outside_weight'):
+                out[k] = _pin(label[k].reshape(-1, label[k].shape[-1]).astype(np.float32))
+        else:
+            out['rois'] = _pin(data['rois'].astype(np.float32))
+            out['im_info'] = _pin(data['im_info'])
+        return out
+
+    @property
+    def provide_data(self):
+        b = self.get_batch()
+        return [(k, tuple(b[k].shape)) for k in ('data', 'rois')]
+
+    @property
+    def provide_label(self):
+        b = self.get_batch()
+        return [(k, tuple(b[k].shape)) for k in self.label_name if k in b]
+
+
+def tensor_vstack_batches(batches, key, pad=0):
+    return tensor_vstack([b[key] for b in batches], pad=pad)

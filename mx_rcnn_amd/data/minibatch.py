@@ -59,12 +59,13 @@ def sample_rois(roidb, fg_rois_per_image, rois_per_image, num_classes):
     return rois, labels, bbox_targets, bbox_inside, overlaps
 
 
-def get_minibatch(roidb, num_classes, mode='test', need_mean=True):
+def get_minibatch(roidb, num_classes, mode='test', need_mean=True, has_rpn=None):
+    """``has_rpn`` overrides config[TRAIN|TEST].HAS_RPN (thread-safe use from loader workers)."""
     num_images = len(roidb)
     scale_idx = npr.randint(0, high=len(config.SCALES), size=num_images)
     im_array, im_scales = get_image_array(roidb, config.SCALES, scale_idx, need_mean=need_mean)
     cfg_key = 'TRAIN' if mode == 'train' else 'TEST'
-    if config[cfg_key].HAS_RPN:
+    if (config[cfg_key].HAS_RPN if has_rpn is None else has_rpn):
         # per-image im_info (the reference asserts a single image here)
         im_info = np.array([[r_h, r_w, s] for (r_h, r_w), s in
                             zip([_resized_hw(r, s) for r, s in zip(roidb, im_scales)], im_scales)], dtype=np.float32)

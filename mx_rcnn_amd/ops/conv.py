@@ -2,8 +2,9 @@
 
 * k x k, Cin % 64 == 0: hand-written MFMA implicit-GEMM forward (csrc/hip/conv_igemm.hip),
   fused bias + ReLU epilogue.  Backward: the stride-1 data gradient is the same kernel run
-  on dY with the flipped/transposed filter (pad' = k-1-pad); the weight gradient and strided
-  dgrad use ``aten.convolution_backward`` (MIOpen) for now.
+  on dY with the flipped/transposed filter (pad' = k-1-pad); the weight gradient is the MFMA
+  wgrad kernel (csrc/hip/conv_wgrad.hip, transposed LDS reads); strided dgrad still uses
+  ``aten.convolution_backward`` (MIOpen).  ``MXR_CONV_WGRAD=0`` restores MIOpen wgrad.
 * 1x1: one GEMM over the NHWC matrix view (layers.conv1x1_nhwc).
 * Anything else (the 3-channel stem convs): MIOpen.
 
@@ -19,6 +20,10 @@ from ._ext import need_ext
 
 def igemm_enabled():
     return os.environ.get('MXR_CONV_IGEMM', '1') != '0'
+
+
+def wgrad_enabled():
+    return os.environ.get('MXR_CONV_WGRAD', '1') != '0'
 
 
 def _flip_t(w):
@@ -52,7 +57,13 @@ class _ConvIgemm(torch.autograd.Function):
                 dx = torch.ops.aten.convolution_backward(
                     dy, x, w, None, [ctx.stride] * 2, [ctx.pad] * 2, [1, 1], False, [0, 0], 1,
                     [True, False, False])[0]
-        if ctx.needs_input_grad[1] or (ctx.has_bias and ctx.needs_input_grad[2]):
+        need_w = ctx.needs_input_grad[1]
+        need_b = ctx.has_bias and ctx.needs_input_grad[2]
+        if need_w and wgrad_enabled() and w.shape[0] % 8 == 0:
+            dw = need_ext().conv_wgrad(dy, x, w.shape[2], w.shape[3], ctx.stride, ctx.pad)
+            if need_b:
+                db = dy.sum(dim=(0, 2, 3)).to(w.dtype)
+        elif need_w or need_b:
             _, dw, db = torch.ops.aten.convolution_backward(
                 dy, x, w, [w.shape[0]] if ctx.has_bias else None, [ctx.stride] * 2, [ctx.pad] * 2, [1, 1], False,
                 [0, 0], 1, [False, bool(ctx.needs_input_grad[1]), bool(ctx.has_bias and ctx.needs_input_grad[2])])

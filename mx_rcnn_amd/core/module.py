@@ -1,0 +1,256 @@
+"""MutableModule: the reference's training driver API (`rcnn/module.py:13-199` plus the
+inherited MXNet ``BaseModule.fit``) on top of :class:`Trainer`.
+
+* ``symbol`` is a :class:`~mx_rcnn_amd.models.FasterRCNN` (or ``(model, mode)``); the mode
+  (``'e2e'``, ``'rpn'``, ``'rcnn'``) selects the training graph like the reference's symbol
+  builders do.
+* Shape changes: the reference rebinds a new executor sharing memory when the input shape
+  changes (`rcnn/module.py:155-175`).  Here every distinct input shape gets its own captured
+  hipGraph (``use_graph=True``), cached by shape -- the same idea, replayed without any
+  per-step launch overhead.
+* ``fixed_param_prefix`` freezes parameters by SUBSTRING match, exactly like the reference
+  (with a warning when a prefix also matches inside other names).
+* Data parallel: one process per GPU (torch.distributed, RCCL); gradients are SUM-reduced
+  in overlapped buckets; BN moving statistics are averaged across ranks only when params are
+  fetched (checkpointing), mirroring MXNet's ``get_params``; rank 0 runs epoch-end callbacks.
+"""
+import logging
+import time
+
+import numpy as np
+import torch
+
+from ..parallel import dist as pdist
+from .callback import BatchEndParam
+from .lr_scheduler import FactorScheduler
+from .trainer import GraphedStep, Trainer
+
+
+class MutableModule(object):
+    def __init__(self, symbol, data_names=None, label_names=None, logger=logging, context=None, work_load_list=None,
+                 max_data_shapes=None, max_label_shapes=None, fixed_param_prefix=None, mode=None, use_graph=None,
+                 compute_dtype=None):
+        if isinstance(symbol, tuple):
+            symbol, mode = symbol
+        self.symbol = symbol
+        self.model = symbol
+        self.mode = mode or getattr(symbol, 'train_mode', 'e2e')
+        self._data_names = list(data_names or [])
+        self._label_names = list(label_names or [])
+        self.logger = logger
+        ctx = context if context is not None else ('cuda' if torch.cuda.is_available() else 'cpu')
+        if isinstance(ctx, (list, tuple)):
+            ctx = ctx[0]
+        self.context = torch.device(ctx) if not isinstance(ctx, torch.device) else ctx
+        self.work_load_list = work_load_list
+        self.max_data_shapes, self.max_label_shapes = max_data_shapes, max_label_shapes
+        self.fixed_param_prefix = fixed_param_prefix or []
+        self.use_graph = (self.context.type == 'cuda') if use_graph is None else use_graph
+        self.compute_dtype = compute_dtype
+        self.binded = self.params_initialized = self.optimizer_initialized = False
+        self.trainer = None
+        self._graphs = {}
+        self._outputs = None
+        self._batch = None
+        self._monitor = None
+
+    # ------------------------------------------------------------------ properties
+    @property
+    def data_names(self):
+        return self._data_names
+
+    @property
+    def output_names(self):
+        return ['loss', 'rpn_cls_loss', 'rpn_bbox_loss', 'cls_loss', 'bbox_loss', 'cls_prob', 'label']
+
+    @property
+    def data_shapes(self):
+        return self.max_data_shapes
+
+    @property
+    def label_shapes(self):
+        return self.max_label_shapes
+
+    @property
+    def output_shapes(self):
+        if self._outputs is None:
+            return []
+        return [(k, tuple(v.shape)) for k, v in self._outputs.items() if torch.is_tensor(v)]
+
+    # ------------------------------------------------------------------ setup
+    def bind(self, data_shapes=None, label_shapes=None, for_training=True, inputs_need_grad=False,
+             force_rebind=False, shared_module=None, grad_req='write'):
+        if data_shapes is not None:
+            self.max_data_shapes = data_shapes
+        if label_shapes is not None:
+            self.max_label_shapes = label_shapes
+        self.for_training = for_training
+        self.model.to(self.context)
+        self.binded = True
+
+    def init_params(self, initializer=None, arg_params=None, aux_params=None, allow_missing=True, force_init=False):
+        """Load MXNet-named arrays into the model (missing names keep their initialisation)."""
+        if self.params_initialized and not force_init:
+            return
+        if self.trainer is not None:
+            arrays = dict(arg_params or {})
+            self.trainer.store.load_arrays(arrays)
+            self._load_aux(aux_params)
+        else:
+            self._load_model_arrays(arg_params, aux_params, allow_missing)
+        self.params_initialized = True
+
+    def _load_model_arrays(self, arg_params, aux_params, allow_missing=True):
+        cur = self.model.arg_params()
+        missing = []
+        with torch.no_grad():
+            for k, t in cur.items():
+                if arg_params and k in arg_params:
+                    src = torch.as_tensor(np.asarray(arg_params[k]) if not torch.is_tensor(arg_params[k])
+                                          else arg_params[k]).float()
+                    t.copy_(src.reshape(t.shape).to(t.device, t.dtype))
+                else:
+                    missing.append(k)
+        if missing and not allow_missing:
+            raise KeyError('missing arg params: %s' % missing[:10])
+        self._load_aux(aux_params)
+
+    def _load_aux(self, aux_params):
+        if not aux_params:
+            return
+        cur = self.model.aux_params()
+        with torch.no_grad():
+            for k, t in cur.items():
+                if k in aux_params:
+                    src = aux_params[k]
+                    src = src if torch.is_tensor(src) else torch.as_tensor(np.asarray(src))
+                    t.copy_(src.reshape(t.shape).to(t.device, t.dtype))
+
+    def init_optimizer(self, kvstore='device', optimizer='sgd', optimizer_params=None, force_init=False):
+        if self.optimizer_initialized and not force_init:
+            return
+        assert optimizer == 'sgd', 'only SGD (the reference optimizer) is implemented'
+        p = dict(optimizer_params or {})
+        lr = p.get('learning_rate', 0.01)
+        sched = p.get('lr_scheduler')
+        self.trainer = Trainer(self.model, self.mode, fixed_param_prefix=self.fixed_param_prefix, lr=lr,
+                               momentum=p.get('momentum', 0.0), wd=p.get('wd', 0.0),
+                               clip_gradient=p.get('clip_gradient', -1.0) or -1.0,
+                               rescale_grad=p.get('rescale_grad', 1.0), lr_scheduler=sched,
+                               compute_dtype=self.compute_dtype, device=self.context,
+                               bucket_mb=p.get('bucket_mb', 64))
+        self.optimizer_initialized = True
+
+    def install_monitor(self, mon):
+        self._monitor = mon
+        mon.install(self.model)
+
+    # ------------------------------------------------------------------ step API
+    def forward(self, data_batch, is_train=None):
+        is_train = self.for_training if is_train is None else is_train
+        b = self.trainer.prepare_batch(data_batch)
+        self._batch = b
+        self.model.train(is_train)
+        if is_train:
+            self.trainer.store.zero_grad()
+            self.trainer.reducer.prepare()
+            self._outputs = self.trainer.forward(b)
+        else:
+            with torch.no_grad():
+                self._outputs = self.trainer.forward(b)
+
+    def backward(self, out_grads=None):
+        self._outputs['loss'].backward()
+
+    def update(self):
+        t = self.trainer
+        t.reducer.finish()
+        t.update_lr()
+        t.store.sgd_step(t.lr_t, t.momentum, t.wd, t.rescale, t.clip)
+
+    def step(self, data_batch):
+        """forward + backward + update fused (graph-replayed per input shape when enabled)."""
+        if not self.use_graph:
+            self._outputs = self.trainer.step(data_batch)
+            return self._outputs
+        key = tuple((k, tuple(v.shape)) for k, v in sorted(data_batch.items()) if torch.is_tensor(v))
+        g = self._graphs.get(key)
+        if g is None:
+            g = GraphedStep(self.trainer, data_batch)
+            self._graphs[key] = g
+            logging.info('captured hipGraph for input shape %s (%d cached)', key, len(self._graphs))
+        self._outputs = g(data_batch)
+        return self._outputs
+
+    def get_outputs(self, merge_multi_context=True):
+        return self._outputs
+
+    def update_metric(self, eval_metric, labels=None):
+        eval_metric.update(labels, self._outputs)
+
+    def get_params(self):
+        """-> (arg_params, aux_params) as fp32 numpy, BN moving stats averaged over ranks."""
+        if self.trainer is not None:
+            arg = {k: v.detach().float().cpu().numpy() for k, v in self.trainer.store.state_arrays().items()}
+        else:
+            arg = {k: v.detach().float().cpu().numpy() for k, v in self.model.arg_params().items()}
+        aux = {}
+        for k, v in self.model.aux_params().items():
+            t = v.detach().float().clone()
+            if pdist.is_distributed():
+                torch.distributed.all_reduce(t)
+                t /= pdist.get_world_size()
+            aux[k] = t.cpu().numpy()
+        return arg, aux
+
+    def set_params(self, arg_params, aux_params, allow_missing=False, force_init=True):
+        self.init_params(None, arg_params, aux_params, allow_missing=allow_missing, force_init=force_init)
+
+    # ------------------------------------------------------------------ fit
+    def fit(self, train_data, eval_data=None, eval_metric=None, epoch_end_callback=None, batch_end_callback=None,
+            kvstore='device', optimizer='sgd', optimizer_params=None, eval_batch_end_callback=None,
+            initializer=None, arg_params=None, aux_params=None, allow_missing=True, force_rebind=False,
+            force_init=False, begin_epoch=0, num_epoch=None, validation_metric=None, monitor=None,
+            max_steps=None):
+        assert num_epoch is not None, 'please specify number of epochs'
+        self.bind(for_training=True)
+        if monitor is not None:
+            self.install_monitor(monitor)
+        self.init_params(initializer, arg_params, aux_params, allow_missing, force_init)
+        self.init_optimizer(kvstore, optimizer, optimizer_params)
+        rank = pdist.get_rank()
+        cbs_b = batch_end_callback if isinstance(batch_end_callback, (list, tuple)) else \
+            ([batch_end_callback] if batch_end_callback else [])
+        cbs_e = epoch_end_callback if isinstance(epoch_end_callback, (list, tuple)) else \
+            ([epoch_end_callback] if epoch_end_callback else [])
+        steps = 0
+        for epoch in range(begin_epoch, num_epoch):
+            tic = time.time()
+            if eval_metric is not None:
+                eval_metric.reset()
+            for nbatch, batch in enumerate(train_data):
+                self.step(batch)
+                if eval_metric is not None:
+                    self.update_metric(eval_metric)
+                if self._monitor is not None:
+                    self._monitor.toc_print()
+                for cb in cbs_b:
+                    cb(BatchEndParam(epoch, nbatch, eval_metric, locals()))
+                steps += 1
+                if max_steps is not None and steps >= max_steps:
+                    break
+            if eval_metric is not None:
+                for name, val in eval_metric.get_name_value():
+                    logging.info('Epoch[%d] Train-%s=%f', epoch, name, val)
+            logging.info('Epoch[%d] Time cost=%.3f', epoch, time.time() - tic)
+            arg, aux = self.get_params()
+            if rank == 0:
+                for cb in cbs_e:
+                    cb(epoch, self.symbol, arg, aux)
+            train_data.reset()
+            if max_steps is not None and steps >= max_steps:
+                break
+
+
+def default_lr_scheduler(step, factor=0.1):
+    return FactorScheduler(step, factor)

@@ -22,6 +22,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.sgd import sgd_momentum_
+from ..ops import grad_sink
 
 
 def _is_bn_param(name):
@@ -93,6 +94,7 @@ class FlatParamStore:
                         pv.copy_(src.to(compute_dtype))
                     param = nn.Parameter(pv, requires_grad=True)
                     param.grad = self._shaped(g.grad[off:off + numel], shape, cl)
+                    grad_sink.enable_direct(param)
                     m._parameters[attr] = param
                     self.params[n] = param
                     off += numel

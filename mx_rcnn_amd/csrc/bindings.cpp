@@ -71,6 +71,7 @@ std::vector<Tensor> nms_proposals(const Tensor& boxes, const Tensor& scores, con
   DevGuard g(boxes.device());
   const int nb = (P + 63) / 64;
   TORCH_CHECK(16 + (int64_t)nb * 8 + post * 4 <= 160 * 1024, "NMS LDS budget exceeded (P or post too large)");
+  TORCH_CHECK(nb <= 256, "NMS supports at most 16384 pre-NMS boxes per image");
   auto st = cur_stream();
   Tensor mask = at::empty({B, P, nb}, boxes.options().dtype(at::kLong));
   mxr::nms_mask(boxes.data_ptr<float>(), n_valid.data_ptr<int32_t>(), B, P, (float)thresh,
@@ -268,7 +269,8 @@ Tensor bn_relu_fwd(const Tensor& x, const Tensor& gamma, const Tensor& beta, con
 
 std::vector<Tensor> bn_relu_bwd(const Tensor& x, const Tensor& dy, const Tensor& gamma, const Tensor& beta,
                                 const Tensor& mean, const Tensor& var, double eps, bool fix_gamma, bool relu,
-                                bool need_dx, bool need_params) {
+                                bool need_dx, bool need_params, c10::optional<Tensor> dgamma_out,
+                                c10::optional<Tensor> dbeta_out) {
   CHECK_DEV(x); CHECK_DEV(dy);
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "x must be channels_last");
   Tensor g = dy.contiguous(at::MemoryFormat::ChannelsLast);
@@ -277,17 +279,28 @@ std::vector<Tensor> bn_relu_bwd(const Tensor& x, const Tensor& dy, const Tensor&
   DevGuard guard(x.device());
   Tensor dx = need_dx ? at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast) : Tensor();
   const bool vec = (C % 4 == 0);
-  Tensor dgamma = need_params ? (vec ? at::empty({C}, x.options().dtype(at::kFloat))
-                                     : at::zeros({C}, x.options().dtype(at::kFloat))) : Tensor();
-  Tensor dbeta = need_params ? (vec ? at::empty({C}, x.options().dtype(at::kFloat))
-                                    : at::zeros({C}, x.options().dtype(at::kFloat))) : Tensor();
+  // accumulate directly into caller-provided fp32 gradients (flat-buffer views) when given
+  const bool acc = vec && dgamma_out.has_value() && dgamma_out->defined() && dbeta_out.has_value() &&
+                   dbeta_out->defined();
+  Tensor dgamma, dbeta;
+  if (acc) {
+    dgamma = *dgamma_out;
+    dbeta = *dbeta_out;
+    TORCH_CHECK(dgamma.scalar_type() == at::kFloat && dbeta.scalar_type() == at::kFloat && dgamma.is_contiguous() &&
+                    dbeta.is_contiguous() && dgamma.numel() == C && dbeta.numel() == C,
+                "dgamma_out/dbeta_out must be contiguous fp32 (C,)");
+  } else if (need_params) {
+    dgamma = vec ? at::empty({C}, x.options().dtype(at::kFloat)) : at::zeros({C}, x.options().dtype(at::kFloat));
+    dbeta = vec ? at::empty({C}, x.options().dtype(at::kFloat)) : at::zeros({C}, x.options().dtype(at::kFloat));
+  }
+  need_params = need_params || acc;
   Tensor ws;
   if (need_params && vec) ws = at::empty({mxr::bn_bwd_workspace_floats(x.numel() / C, C)}, x.options().dtype(at::kFloat));
   mxr::bn_relu_bwd(x.data_ptr(), g.data_ptr(), is_bf16(x), x.numel() / C, C, gamma.data_ptr<float>(),
                    beta.data_ptr<float>(), mean.data_ptr<float>(), var.data_ptr<float>(), (float)eps,
                    fix_gamma ? 1 : 0, relu ? 1 : 0, need_dx ? dx.data_ptr() : nullptr,
                    need_params ? dgamma.data_ptr<float>() : nullptr, need_params ? dbeta.data_ptr<float>() : nullptr,
-                   ws.defined() ? ws.data_ptr<float>() : nullptr, cur_stream());
+                   ws.defined() ? ws.data_ptr<float>() : nullptr, acc ? 1 : 0, cur_stream());
   return {dx, dgamma, dbeta};
 }
 
@@ -327,7 +340,7 @@ Tensor conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::optional<Tensor> bi
 }
 
 Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
-                  int64_t splits) {
+                  int64_t splits, c10::optional<Tensor> out) {
   CHECK_DEV(dy); CHECK_DEV(x);
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "bf16 only");
   TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) && x.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -341,12 +354,21 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int
   int sp = 1;
   mxr::conv_wgrad_plan(NB, Ho, Wo, Cin, Cout, (int)KH, (int)KW, &sp);
   if (splits > 0) sp = (int)splits;
-  Tensor dw = at::empty({Cout, Cin, KH, KW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor dw;
+  const bool acc = out.has_value() && out->defined();
+  if (acc) {
+    dw = *out;
+    TORCH_CHECK(dw.scalar_type() == at::kBFloat16 && dw.size(0) == Cout && dw.size(1) == Cin && dw.size(2) == KH &&
+                    dw.size(3) == KW && dw.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "out must be a channels_last bf16 (Cout, Cin, KH, KW) tensor");
+  } else {
+    dw = at::empty({Cout, Cin, KH, KW}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  }
   Tensor slab = at::empty({(int64_t)sp * Cout * KH * KW * Cin}, x.options().dtype(at::kFloat));
   const int r = mxr::conv_wgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                                 reinterpret_cast<const uint16_t*>(x.data_ptr()),
                                 reinterpret_cast<uint16_t*>(dw.data_ptr()), slab.data_ptr<float>(), NB, H, W, Cin, Ho,
-                                Wo, Cout, (int)KH, (int)KW, (int)stride, (int)pad, sp, cur_stream());
+                                Wo, Cout, (int)KH, (int)KW, (int)stride, (int)pad, sp, acc ? 1 : 0, cur_stream());
   TORCH_CHECK(r > 0, "conv_wgrad: unsupported shape");
   return dw;
 }
@@ -366,10 +388,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("smooth_l1", &smooth_l1);
   m.def("sgd_momentum", &sgd_momentum);
   m.def("bn_relu_fwd", &bn_relu_fwd);
-  m.def("bn_relu_bwd", &bn_relu_bwd);
+  m.def("bn_relu_bwd", &bn_relu_bwd, py::arg("x"), py::arg("dy"), py::arg("gamma"), py::arg("beta"),
+        py::arg("mean"), py::arg("var"), py::arg("eps"), py::arg("fix_gamma"), py::arg("relu"), py::arg("need_dx"),
+        py::arg("need_params"), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none());
   m.def("conv_igemm_fwd", &conv_igemm_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),
         py::arg("pad"), py::arg("relu"), py::arg("tile") = 0, py::arg("splits") = 0);
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"), py::arg("stride"),
-        py::arg("pad"), py::arg("splits") = 0);
+        py::arg("pad"), py::arg("splits") = 0, py::arg("out") = py::none());
   m.attr("arch") = "gfx950";
 }

@@ -52,7 +52,23 @@ bn_relu_fwd_kernel(const void* __restrict__ x, int bf16, int64_t M, int C, const
   float s[4], t[4];
   for (int k = 0; k < 4; ++k) bn_coeffs(cv * 4 + k, gamma, beta, mean, var, eps, fix_gamma, s[k], t[k]);
   const int64_t total = M * CV;
-  for (int64_t e = tid; e < total; e += T) {
+  // 4 independent 8/16-B loads in flight per thread per trip (latency hiding at low occupancy)
+  int64_t e = tid;
+  for (; e + 3 * T < total; e += 4 * T) {
+    float v[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) load4(x, (e + u * T) * 4, bf16, v[u]);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[u][k] = v[u][k] * s[k] + t[k];
+        if (relu) v[u][k] = fmaxf(v[u][k], 0.f);
+      }
+      store4(y, (e + u * T) * 4, bf16, v[u]);
+    }
+  }
+  for (; e < total; e += T) {
     float v[4];
     load4(x, e * 4, bf16, v);
 #pragma unroll
@@ -64,11 +80,6 @@ bn_relu_fwd_kernel(const void* __restrict__ x, int bf16, int64_t M, int C, const
   }
 }
 
-// Backward, stage 1: each block owns a fixed channel quad per thread (grid*256 % CV == 0),
-// accumulates dgamma/dbeta partials in registers, reduces them through LDS (threads of a
-// block that share a channel quad) and writes ONE partial row per block -- no global
-// atomics (per-thread atomics onto 2C addresses serialised at the memory side and made
-// this kernel 0.3 ms/call in the first profile).  Stage 2 sums the partial rows.
 __global__ void __launch_bounds__(256)
 bn_relu_bwd_kernel(const void* __restrict__ x, const void* __restrict__ dy, int bf16, int64_t M, int C,
                    const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ mean,
@@ -89,10 +100,7 @@ bn_relu_bwd_kernel(const void* __restrict__ x, const void* __restrict__ dy, int 
   }
   float ag[4] = {0.f, 0.f, 0.f, 0.f}, ab[4] = {0.f, 0.f, 0.f, 0.f};
   const int64_t total = M * CV;
-  for (int64_t e = tid; e < total; e += T) {
-    float xv[4], g[4];
-    load4(x, e * 4, bf16, xv);
-    load4(dy, e * 4, bf16, g);
+  auto body = [&](float* xv, float* g, int64_t e) {
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const float pre = xv[k] * s[k] + t[k];
@@ -102,6 +110,23 @@ bn_relu_bwd_kernel(const void* __restrict__ x, const void* __restrict__ dy, int 
       g[k] = gm * s[k];
     }
     if (dx) store4(dx, e * 4, bf16, g);
+  };
+  int64_t e = tid;
+  for (; e + 3 * T < total; e += 4 * T) {  // 8 independent loads in flight per thread
+    float xv[4][4], g[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      load4(x, (e + u * T) * 4, bf16, xv[u]);
+      load4(dy, (e + u * T) * 4, bf16, g[u]);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) body(xv[u], g[u], e + u * T);
+  }
+  for (; e < total; e += T) {
+    float xv[4], g[4];
+    load4(x, e * 4, bf16, xv);
+    load4(dy, e * 4, bf16, g);
+    body(xv, g, e);
   }
   __syncthreads();
   if (part) {
@@ -120,7 +145,7 @@ bn_relu_bwd_kernel(const void* __restrict__ x, const void* __restrict__ dy, int 
 // bound at ~37 us/call), then combine through LDS.
 __global__ void __launch_bounds__(256)
 bn_part_reduce(const float* __restrict__ part, int nblk, int C, int fix_gamma, float* __restrict__ dgamma,
-               float* __restrict__ dbeta) {
+               float* __restrict__ dbeta, int accumulate) {
   __shared__ float red[4][64];
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   const int i = blockIdx.x * 64 + lane;
@@ -140,8 +165,11 @@ bn_part_reduce(const float* __restrict__ part, int nblk, int C, int fix_gamma, f
   __syncthreads();
   if (wid == 0 && i < 2 * C) {
     const float s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
-    if (i < C) { if (dgamma && !fix_gamma) dgamma[i] = s; }
-    else if (dbeta) dbeta[i - C] = s;
+    if (i < C) {
+      if (dgamma && !fix_gamma) dgamma[i] = accumulate ? dgamma[i] + s : s;
+    } else if (dbeta) {
+      dbeta[i - C] = accumulate ? dbeta[i - C] + s : s;
+    }
   }
 }
 
@@ -224,23 +252,23 @@ void bn_relu_fwd(const void* x, int bf16, int64_t M, int C, const float* gamma, 
 
 int bn_bwd_workspace_floats(int64_t M, int C) {
   if (C % 4 != 0) return 0;
-  return bn_grid(M, C, 160) * 2 * C;
+  return bn_grid(M, C, 320) * 2 * C;
 }
 
 void bn_relu_bwd(const void* x, const void* dy, int bf16, int64_t M, int C, const float* gamma, const float* beta,
                  const float* mean, const float* var, float eps, int fix_gamma, int relu, void* dx, float* dgamma,
-                 float* dbeta, float* workspace, hipStream_t st) {
+                 float* dbeta, float* workspace, int accumulate, hipStream_t st) {
   if (M == 0 || C == 0) return;
   if (C % 4 != 0) {
     bn_relu_bwd_scalar<<<bn_grid_scalar(M, C), 256, 2 * C * sizeof(float), st>>>(
         x, dy, bf16, M, C, gamma, beta, mean, var, eps, fix_gamma, relu, dx, dgamma, dbeta);
     return;
   }
-  const int nblk = bn_grid(M, C, 160);
+  const int nblk = bn_grid(M, C, 320);
   float* part = (dgamma || dbeta) ? workspace : nullptr;
   bn_relu_bwd_kernel<<<nblk, 256, 2 * C * sizeof(float), st>>>(x, dy, bf16, M, C, gamma, beta, mean, var, eps,
                                                                fix_gamma, relu, dx, part);
-  if (part) bn_part_reduce<<<(2 * C + 63) / 64, 256, 0, st>>>(part, nblk, C, fix_gamma, dgamma, dbeta);
+  if (part) bn_part_reduce<<<(2 * C + 63) / 64, 256, 0, st>>>(part, nblk, C, fix_gamma, dgamma, dbeta, accumulate);
 }
 
 }  // namespace mxr

@@ -147,13 +147,18 @@ conv_wgrad_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ 
 }
 
 __global__ void __launch_bounds__(256)
-wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int64_t n, uint16_t* __restrict__ out) {
+wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int64_t n, uint16_t* __restrict__ out,
+                    int accumulate) {
   const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (e >= n) return;
   float4 a = *reinterpret_cast<const float4*>(slab + e);
   for (int s = 1; s < splits; ++s) {
     const float4 b = *reinterpret_cast<const float4*>(slab + (int64_t)s * n + e);
     a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  if (accumulate) {  // add into the existing gradient (flat-buffer view), no separate add kernel
+    const ushort4 o = *reinterpret_cast<const ushort4*>(out + e);
+    a.x += bf16_to_f32(o.x); a.y += bf16_to_f32(o.y); a.z += bf16_to_f32(o.z); a.w += bf16_to_f32(o.w);
   }
   *reinterpret_cast<ushort4*>(out + e) = make_ushort4(f32_to_bf16(a.x), f32_to_bf16(a.y), f32_to_bf16(a.z),
                                                       f32_to_bf16(a.w));
@@ -170,7 +175,8 @@ int conv_wgrad_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, i
 }
 
 int conv_wgrad(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab, int NB, int H, int W, int Cin,
-               int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int splits, hipStream_t st) {
+               int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int splits, int accumulate,
+               hipStream_t st) {
   if (Cin % WG_BN != 0 || Cout % 8 != 0) return -1;
   const int P = NB * Ho * Wo;
   const int tiles_m = (Cout + WG_BM - 1) / WG_BM, tiles_n = KH * KW * Cin / WG_BN;
@@ -180,7 +186,7 @@ int conv_wgrad(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab,
   conv_wgrad_kernel<<<ntiles * splits, 256, 0, st>>>(dy, x, slab, NB, H, W, Cin, Ho, Wo, Cout, KW, stride, pad,
                                                      tiles_n, ntiles, splits, per);
   const int64_t n = (int64_t)Cout * KH * KW * Cin;
-  wgrad_reduce_kernel<<<div_up((n + 3) / 4, 256), 256, 0, st>>>(slab, splits, n, dw);
+  wgrad_reduce_kernel<<<div_up((n + 3) / 4, 256), 256, 0, st>>>(slab, splits, n, dw, accumulate);
   return splits;
 }
 

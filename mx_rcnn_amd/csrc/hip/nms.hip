@@ -50,6 +50,25 @@ __device__ __forceinline__ uint64_t readlane64(uint64_t v, int lane) {
   return ((uint64_t)hi << 32) | lo;
 }
 
+__device__ __forceinline__ uint64_t wave_or64(uint64_t v) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lo |= __shfl_xor(lo, o, 64);
+    hi |= __shfl_xor(hi, o, 64);
+  }
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// One workgroup (16 waves) per image.  Per 64-box block rb:
+//  1. wave 0 resolves the block: lane i holds row i's diagonal word (boxes j > i it suppresses);
+//     iterate kept <- cand & ~OR_{i in kept} diag_i to its fixpoint (a wave OR-reduction per
+//     iteration; greedy NMS is the unique fixpoint, reached in "longest suppression chain"
+//     iterations -- typically 1-3);
+//  2. all threads OR the kept rows of block rb into the LDS `removed` bitmap of the later
+//     column blocks.  Thread (jq, c) owns column block c (< 256) and rows jq*16..+15 of the
+//     block; the 16 mask words for block rb+1 are PREFETCHED into registers while block rb is
+//     being resolved, so each iteration's global-load latency overlaps the previous iteration.
 __global__ void __launch_bounds__(1024)
 nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ scores,
                   const int32_t* __restrict__ n_valid, const uint64_t* __restrict__ mask, int P, int nb, int post,
@@ -59,53 +78,63 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
   // single dynamic LDS region (Guideline 17): [kept_bits u64 | nkeep i32 | pad][removed nb*u64][keep_list]
   uint64_t& s_kept_bits = *reinterpret_cast<uint64_t*>(smem);
   int& s_nkeep = *reinterpret_cast<int*>(smem + 8);
-  uint64_t* removed = reinterpret_cast<uint64_t*>(smem + 16);                          // nb words
+  uint64_t* removed = reinterpret_cast<uint64_t*>(smem + 16);                            // nb words
   int32_t* keep_list = reinterpret_cast<int32_t*>(smem + 16 + ((nb * 8 + 15) / 16) * 16);  // post ints
   const int b = blockIdx.x, tid = threadIdx.x;
   const int nv = n_valid[b];
   const uint64_t* mb = mask + (int64_t)b * P * nb;
   for (int c = tid; c < nb; c += blockDim.x) removed[c] = 0;
   if (tid == 0) s_nkeep = 0;
-  __syncthreads();
   const int nbv = (nv + 63) / 64;
+  const int jq = tid >> 8, cidx = tid & 255;
+  // prefetch registers: this thread's 16 words of (row block rb, column cidx)
+  uint64_t pf[16];
+  auto fetch = [&](int rb) {
+    const int nrow = min(64, P - rb * 64);
+    const bool colok = (cidx > rb) && (cidx < nbv);
+    // unconditional loads from clamped (always in-bounds) addresses, masked afterwards, so the
+    // 16 loads issue back to back instead of branching around each one
+    const int col = min(cidx, nb - 1);
+#pragma unroll
+    for (int jj = 0; jj < 16; ++jj) {
+      const int j = jq * 16 + jj;
+      const uint64_t v = mb[(int64_t)min(rb * 64 + j, P - 1) * nb + col];
+      pf[jj] = (colok && j < nrow) ? v : 0ull;
+    }
+  };
+  uint64_t diag_next = 0;
+  if (nbv > 0) {
+    fetch(0);
+    if (tid < 64) diag_next = (tid < nv) ? mb[(int64_t)tid * nb] : 0ull;
+  }
+  __syncthreads();
   for (int rb = 0; rb < nbv; ++rb) {
     if (s_nkeep >= post) break;  // uniform: read after a barrier
     if (tid < 64) {
-      // Resolve the 64-box block without a serial scalar chain: lane j holds COLUMN j of the
-      // block's diagonal 64x64 suppression tile (bit i set when box i suppresses box j), and
-      // the wave iterates kept <- {j candidate : no kept i < j suppresses j} to its fixpoint.
-      // Greedy NMS is the unique fixpoint (membership of j depends only on i < j), and the
-      // iteration count is the longest suppression chain in the block (usually a few), not
-      // the number of kept boxes.
       const int i = rb * 64 + tid;
-      const uint64_t diag = (i < nv) ? mb[(int64_t)i * nb + rb] : 0ull;
+      const uint64_t diag = diag_next;
+      if (rb + 1 < nbv) {
+        const int i2 = i + 64;
+        diag_next = (i2 < nv) ? mb[(int64_t)i2 * nb + rb + 1] : 0ull;
+      }
       const int nrow = min(64, nv - rb * 64);
       const uint64_t valid = (nrow == 64) ? ~0ull : ((1ull << nrow) - 1ull);
       const uint64_t cand = valid & ~removed[rb];
-      uint64_t col = 0;
-      for (int r = 0; r < 64; ++r) {
-        const uint64_t row = readlane64(diag, r);
-        col |= ((row >> tid) & 1ull) << r;
-      }
       uint64_t kept = cand;
       for (int it = 0; it < 65; ++it) {
-        const bool keep_me = ((cand >> tid) & 1ull) && !(col & kept);
-        const uint64_t next = __ballot(keep_me);
+        const uint64_t sup = wave_or64(((kept >> tid) & 1ull) ? diag : 0ull);
+        const uint64_t next = cand & ~sup;
         if (next == kept) break;
         kept = next;
       }
-      int nk = s_nkeep;
-      const int cnt = __popcll(kept);
-      if (nk + cnt > post) {  // keep only the lowest (post - nk) boxes of this block
+      const int nk = s_nkeep;
+      if (nk + __popcll(kept) > post) {  // keep only the lowest (post - nk) boxes of this block
         int need = post - nk;
         uint64_t trunc = 0, k = kept;
         while (need-- > 0 && k) { trunc |= k & (~k + 1); k &= k - 1; }
         kept = trunc;
       }
-      if ((kept >> tid) & 1ull) {
-        const int pos = nk + __popcll(kept & ((1ull << tid) - 1ull));
-        keep_list[pos] = i;
-      }
+      if ((kept >> tid) & 1ull) keep_list[nk + __popcll(kept & ((1ull << tid) - 1ull))] = i;
       __builtin_amdgcn_wave_barrier();
       if (tid == 0) {
         s_kept_bits = kept;
@@ -114,26 +143,11 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
     }
     __syncthreads();
     const uint64_t kept = s_kept_bits;
-    if (kept && s_nkeep < post) {
-      // column-parallel OR of the kept rows: 4 thread groups each own 16 of the block's 64
-      // rows; loads are unconditional (masked after) so hipcc keeps 16 independent loads in
-      // flight instead of branching around each one
-      const int jq = tid >> 8, cidx = tid & 255;
-      const int nrow = min(64, P - rb * 64);
-      for (int c = rb + 1 + cidx; c < nbv; c += 256) {
-        uint64_t acc = 0;
-        const uint64_t* col = mb + (int64_t)(rb * 64) * nb + c;
+    uint64_t acc = 0;
 #pragma unroll
-        for (int jj = 0; jj < 16; ++jj) {
-          const int j = jq * 16 + jj;
-          if (j < nrow) {
-            const uint64_t v = col[(int64_t)j * nb];
-            acc |= ((kept >> j) & 1ull) ? v : 0ull;
-          }
-        }
-        if (acc) atomicOr(reinterpret_cast<unsigned long long*>(&removed[c]), (unsigned long long)acc);
-      }
-    }
+    for (int jj = 0; jj < 16; ++jj) acc |= ((kept >> (jq * 16 + jj)) & 1ull) ? pf[jj] : 0ull;
+    if (acc) atomicOr(reinterpret_cast<unsigned long long*>(&removed[cidx]), (unsigned long long)acc);
+    if (rb + 1 < nbv) fetch(rb + 1);
     __syncthreads();
   }
   const int nk = s_nkeep;

@@ -93,7 +93,7 @@ void bn_relu_fwd(const void* x, int bf16, int64_t M, int C, const float* gamma, 
 int bn_bwd_workspace_floats(int64_t M, int C);
 void bn_relu_bwd(const void* x, const void* dy, int bf16, int64_t M, int C, const float* gamma,
                  const float* beta, const float* mean, const float* var, float eps, int fix_gamma, int relu,
-                 void* dx, float* dgamma, float* dbeta, float* workspace, hipStream_t st);
+                 void* dx, float* dgamma, float* dbeta, float* workspace, int accumulate, hipStream_t st);
 
 // ---- implicit-GEMM convolution (conv_igemm.hip) ------------------------------
 // NHWC bf16 x (NB, H, W, Cin), weight (Cout, KH, KW, Cin) bf16, bias fp32 (Cout) or null,
@@ -110,6 +110,7 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, const float* bias, uint
 // slab: splits * Cout * KH*KW*Cin floats.  Requires Cin % 64 == 0, Cout % 8 == 0.
 int conv_wgrad_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int* splits_out);
 int conv_wgrad(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab, int NB, int H, int W, int Cin,
-               int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int splits, hipStream_t st);
+               int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int splits, int accumulate,
+               hipStream_t st);
 
 }  // namespace mxr

@@ -50,7 +50,7 @@ class RPNHead(nn.Module):
 
 class FasterRCNN(nn.Module):
     def __init__(self, network='vgg16', num_classes=21, cfg=None, bn_mom=0.99, num_anchors=None,
-                 anchor_scales=None, anchor_ratios=RATIOS):
+                 anchor_scales=None, anchor_ratios=RATIOS, resnet_spec=None, train_mode='e2e'):
         super().__init__()
         self.cfg = cfg if cfg is not None else snapshot()
         self.network = network
@@ -60,7 +60,8 @@ class FasterRCNN(nn.Module):
             self.head = VGGHead(num_classes)
             self.anchor_scales = tuple(anchor_scales or VGG_SCALES)
         elif network.startswith('resnet'):
-            depth = int(network.replace('resnet', '').replace('-', '').replace('_', ''))
+            depth = resnet_spec if resnet_spec is not None else \
+                int(network.replace('resnet', '').replace('-', '').replace('_', ''))
             self.trunk = ResNetTrunk(depth, bn_mom=bn_mom)
             self.head = ResNetHead(num_classes, depth, bn_mom=bn_mom)
             self.anchor_scales = tuple(anchor_scales or RESNET_SCALES)
@@ -76,6 +77,7 @@ class FasterRCNN(nn.Module):
         else:
             raise ValueError('unknown network %r' % network)
         self.anchor_ratios = tuple(anchor_ratios)
+        self.train_mode = train_mode
         self.num_anchors = num_anchors or len(self.anchor_scales) * len(self.anchor_ratios)
         self.feat_stride = 16
         self.rpn = RPNHead(self.trunk.out_channels, self.num_anchors)

@@ -41,12 +41,7 @@ class Conv(MxLayer):
 
     def forward(self, x, relu=False):
         b = None if self.bias is None else _w(self.bias, x)
-        w = _w(self.weight, x)
-        if self.weight.shape[-1] == 1 and self.pad == 0 and x.is_cuda and \
-                x.is_contiguous(memory_format=torch.channels_last):
-            y = conv1x1_nhwc(x, w, b, self.stride)
-            return F.relu(y, inplace=True) if relu else y
-        return conv2d(x, w, b, self.stride, self.pad, relu)
+        return conv2d(x, _w(self.weight, x), b, self.stride, self.pad, relu)
 
 
 class Linear(MxLayer):
@@ -96,20 +91,6 @@ class BatchNorm(MxLayer):
                          self.beta.to(x.dtype) if x.dtype != torch.float32 else self.beta, training=True,
                          momentum=1.0 - self.momentum, eps=self.eps)
         return F.relu(y) if self.relu else y
-
-
-def conv1x1_nhwc(x, w, b, stride=1):
-    """1x1 convolution on channels_last activations as ONE GEMM over the (N*H*W, C) matrix
-    view of the NHWC memory (no im2col, no layout change); backward is the two GEMMs
-    dX = dY W and dW = dY^T X produced by autograd.  Strided 1x1 (projection shortcuts)
-    subsamples first.  Measured on MI355X: MIOpen spends ~40 us per 1x1 call at the
-    ResNet stage-3 shapes where the GEMM is ~10 us (tools/microbench/conv_layout.py)."""
-    if stride != 1:
-        x = x[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last)
-    n, c, h, wd = x.shape
-    x2 = x.permute(0, 2, 3, 1).reshape(n * h * wd, c)
-    y2 = F.linear(x2, w.reshape(w.shape[0], c), b)
-    return y2.reshape(n, h, wd, w.shape[0]).permute(0, 3, 1, 2)
 
 
 def max_pool(x, k, s, p=0):

@@ -59,13 +59,23 @@ def _stage(idx, n_units, cin, cout, bottle_neck, bn_mom, bn_global):
     return nn.Sequential(*units)
 
 
+def resolve_depth(depth):
+    """int depth (18..200) or an explicit (units, filter_list, bottle_neck) spec
+    (the reference's generic ``resnet(units, num_stage, filter_list, ...)`` builder)."""
+    if isinstance(depth, (tuple, list)):
+        units, filters, bottle = depth
+        assert len(units) == 4 and len(filters) == 5, 'C4 layout needs 4 stages / 5 filter sizes'
+        return list(units), list(filters), bool(bottle)
+    return DEPTHS[int(depth)]
+
+
 class ResNetTrunk(nn.Module):
     """bn_data -> conv0 -> bn0/relu -> maxpool -> stages 1..3 (stride 16)."""
     feat_stride = 16
 
     def __init__(self, depth=101, bn_mom=0.99, bn_global=True):
         super().__init__()
-        units, filters, bottle = DEPTHS[depth]
+        units, filters, bottle = resolve_depth(depth)
         self.out_channels = filters[3]
         self.bn_data = BatchNorm('bn_data', 3, momentum=bn_mom, fix_gamma=True, use_global_stats=bn_global,
                                  relu=False)
@@ -93,7 +103,7 @@ class ResNetHead(nn.Module):
 
     def __init__(self, num_classes, depth=101, bn_mom=0.99):
         super().__init__()
-        units, filters, bottle = DEPTHS[depth]
+        units, filters, bottle = resolve_depth(depth)
         self.stage4 = _stage(4, units[3], filters[3], filters[4], bottle, bn_mom, False)
         self.bn1 = BatchNorm('bn1', filters[4], momentum=bn_mom, use_global_stats=False)
         self.cls_score = Linear('cls_score', filters[4], num_classes)

@@ -6,6 +6,7 @@ parameters of global-stats BN trainable); the running statistics are constants.
 """
 import torch
 
+from . import grad_sink
 from ._ext import need_ext
 
 
@@ -19,6 +20,7 @@ class _FrozenBnRelu(torch.autograd.Function):
             y = ext.bn_relu_fwd(xc, gamma.float().contiguous(), beta.float().contiguous(), mean.float().contiguous(),
                                 var.float().contiguous(), float(eps), bool(fix_gamma), bool(relu))
             ctx.save_for_backward(xc, gamma, beta, mean, var)
+            ctx.params = (gamma if gamma.is_leaf else None, beta if beta.is_leaf else None)
             return y
         g = torch.ones_like(gamma) if fix_gamma else gamma
         s = g.float() * torch.rsqrt(var.float() + eps)
@@ -36,10 +38,18 @@ class _FrozenBnRelu(torch.autograd.Function):
         need_p = ctx.needs_input_grad[1] or ctx.needs_input_grad[2]
         if x.is_cuda:
             ext = need_ext()
+            tg = grad_sink.target(ctx.params[0]) if ctx.needs_input_grad[1] and not ctx.fix_gamma else None
+            tb = grad_sink.target(ctx.params[1]) if ctx.needs_input_grad[2] else None
+            direct = tg is not None and tb is not None and tg.dtype == torch.float32 and tb.dtype == torch.float32
             dx, dg, db = ext.bn_relu_bwd(x, dy.to(x.dtype), gamma.float().contiguous(), beta.float().contiguous(),
                                          mean.float().contiguous(), var.float().contiguous(), float(ctx.eps),
-                                         bool(ctx.fix_gamma), bool(ctx.relu), bool(need_dx), bool(need_p))
+                                         bool(ctx.fix_gamma), bool(ctx.relu), bool(need_dx), bool(need_p),
+                                         tg if direct else None, tb if direct else None)
             dx = dx if need_dx else None
+            if direct:  # accumulated straight into the flat gradient buffers
+                grad_sink.delivered(ctx.params[0])
+                grad_sink.delivered(ctx.params[1])
+                return dx, None, None, None, None, None, None, None
         else:
             g = torch.ones_like(gamma) if ctx.fix_gamma else gamma
             inv = torch.rsqrt(var.float() + ctx.eps)

@@ -1,21 +1,27 @@
 """Convolution dispatch for channels_last bf16 activations on MI355X.
 
-* k x k, Cin % 64 == 0: hand-written MFMA implicit-GEMM forward (csrc/hip/conv_igemm.hip),
-  fused bias + ReLU epilogue.  Backward: the stride-1 data gradient is the same kernel run
-  on dY with the flipped/transposed filter (pad' = k-1-pad); the weight gradient is the MFMA
-  wgrad kernel (csrc/hip/conv_wgrad.hip, transposed LDS reads); strided dgrad still uses
-  ``aten.convolution_backward`` (MIOpen).  ``MXR_CONV_WGRAD=0`` restores MIOpen wgrad.
-* 1x1: one GEMM over the NHWC matrix view (layers.conv1x1_nhwc).
-* Anything else (the 3-channel stem convs): MIOpen.
-
-``MXR_CONV_IGEMM=0`` disables the custom kernel (A/B switch for profiling).
+* Cin % 64 == 0 (every ResNet/VGG conv except the 3-channel stem): hand-written MFMA
+  implicit-GEMM forward (csrc/hip/conv_igemm.hip) with fused bias + ReLU epilogue and split-K
+  for the latency-bound small-M shapes of 1-image detection.  1x1 convs with M = N*H*W >
+  16384 (frozen stage-1/2 shapes, forward only) use one hipBLASLt GEMM over the NHWC matrix
+  view instead (faster there, tools/microbench/conv_kernels.py); strided 1x1 subsample first.
+* Backward: stride-1 data gradient = the same kernel on dY with the flipped/transposed
+  filter (pad' = k-1-pad); weight gradient = the MFMA wgrad kernel (csrc/hip/conv_wgrad.hip),
+  which ACCUMULATES straight into the parameter's flat-buffer gradient view when the
+  parameter is managed by the FlatParamStore (ops/grad_sink.py: no AccumulateGrad add);
+  strided 3x3 data gradients use ``aten.convolution_backward`` (MIOpen).
+* Anything else: MIOpen.  ``MXR_CONV_IGEMM=0`` / ``MXR_CONV_WGRAD=0`` switch the custom
+  kernels off for A/B runs.
 """
 import os
 
 import torch
 import torch.nn.functional as F
 
+from . import grad_sink
 from ._ext import need_ext
+
+GEMM_1X1_MIN_M = 16384
 
 
 def igemm_enabled():
@@ -28,6 +34,8 @@ def wgrad_enabled():
 
 def _flip_t(w):
     """(O, I, kh, kw) -> (I, O, kh, kw) spatially flipped, channels_last memory."""
+    if w.shape[2] == 1 and w.shape[3] == 1:
+        return w.transpose(0, 1).contiguous(memory_format=torch.channels_last)
     return w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
 
 
@@ -39,6 +47,7 @@ class _ConvIgemm(torch.autograd.Function):
         wc = w.contiguous(memory_format=torch.channels_last)
         y = ext.conv_igemm_fwd(x, wc, b, stride, pad, relu)
         ctx.save_for_backward(x, wc, y if relu else None)
+        ctx.param = w if w.is_leaf else None
         ctx.stride, ctx.pad, ctx.relu, ctx.has_bias = stride, pad, relu, b is not None
         return y
 
@@ -60,20 +69,45 @@ class _ConvIgemm(torch.autograd.Function):
         need_w = ctx.needs_input_grad[1]
         need_b = ctx.has_bias and ctx.needs_input_grad[2]
         if need_w and wgrad_enabled() and w.shape[0] % 8 == 0:
-            dw = need_ext().conv_wgrad(dy, x, w.shape[2], w.shape[3], ctx.stride, ctx.pad)
+            tgt = grad_sink.target(ctx.param)
+            if tgt is not None and tgt.is_contiguous(memory_format=torch.channels_last):
+                need_ext().conv_wgrad(dy, x, w.shape[2], w.shape[3], ctx.stride, ctx.pad, 0, tgt)
+                grad_sink.delivered(ctx.param)
+            else:
+                dw = need_ext().conv_wgrad(dy, x, w.shape[2], w.shape[3], ctx.stride, ctx.pad)
             if need_b:
                 db = dy.sum(dim=(0, 2, 3)).to(w.dtype)
         elif need_w or need_b:
             _, dw, db = torch.ops.aten.convolution_backward(
                 dy, x, w, [w.shape[0]] if ctx.has_bias else None, [ctx.stride] * 2, [ctx.pad] * 2, [1, 1], False,
-                [0, 0], 1, [False, bool(ctx.needs_input_grad[1]), bool(ctx.has_bias and ctx.needs_input_grad[2])])
+                [0, 0], 1, [False, bool(need_w), bool(need_b)])
         return dx, dw, db, None, None, None
+
+
+def conv1x1_gemm(x, w, b, stride=1):
+    """1x1 convolution on channels_last activations as ONE GEMM over the (N*H*W, C) matrix view
+    of the NHWC memory (no im2col, no layout change); backward via autograd (two GEMMs)."""
+    if stride != 1:
+        x = x[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last)
+    n, c, h, wd = x.shape
+    x2 = x.permute(0, 2, 3, 1).reshape(n * h * wd, c)
+    y2 = F.linear(x2, w.reshape(w.shape[0], c), b)
+    return y2.reshape(n, h, wd, w.shape[0]).permute(0, 3, 1, 2)
 
 
 def conv2d(x, w, b=None, stride=1, pad=0, relu=False):
     """Conv (+bias, +optional fused ReLU) on NCHW-logical / channels_last tensors."""
-    if (x.is_cuda and igemm_enabled() and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and
-            x.shape[1] % 64 == 0 and w.shape[2] > 1):
-        return _ConvIgemm.apply(x, w, b, int(stride), int(pad), bool(relu))
+    k = w.shape[2]
+    if (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.shape[1] % 64 == 0 and
+            x.is_contiguous(memory_format=torch.channels_last)):
+        if k == 1 and pad == 0 and stride != 1:
+            x = x[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last)
+            stride = 1
+        m = x.shape[0] * ((x.shape[2] + 2 * pad - k) // stride + 1) * ((x.shape[3] + 2 * pad - k) // stride + 1)
+        if igemm_enabled() and not (k == 1 and m > GEMM_1X1_MIN_M):
+            return _ConvIgemm.apply(x, w, b, int(stride), int(pad), bool(relu))
+        if k == 1 and pad == 0:
+            y = conv1x1_gemm(x, w, b, stride)
+            return F.relu(y, inplace=True) if relu else y
     y = F.conv2d(x, w, b, stride=stride, padding=pad)
     return F.relu(y, inplace=True) if relu else y

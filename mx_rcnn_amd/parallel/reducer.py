@@ -16,6 +16,7 @@ bf16 gradients in 2 buckets and VGG16's fc6 (205 MB bf16) in its own bucket.
 import torch
 import torch.distributed as dist
 
+from ..ops import grad_sink
 from .dist import get_world_size, is_distributed
 
 
@@ -54,7 +55,7 @@ class BucketReducer:
         if self.overlap:
             for n, p in store.params.items():
                 if n in self._param_bucket:
-                    self._hooks.append(p.register_post_accumulate_grad_hook(self._make_hook(n)))
+                    grad_sink.add_hook(p, self._make_hook(n))
 
     def _make_hook(self, name):
         def hook(_p):

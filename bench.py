@@ -85,15 +85,20 @@ def main():
     mode = args.mode if device.type == 'cuda' else 'eager'
     step_fn = None
     if mode == 'graph':
+        ok = 1.0
         try:
             g = GraphedStep(trainer, pool[0], warmup=3)
             step_fn = g
         except Exception as e:  # reported, never silent
-            if rank == 0:
-                print('[bench] hipGraph capture failed (%s: %s); running eager' % (type(e).__name__, str(e)[:300]),
-                      file=sys.stderr)
-            mode = 'eager'
+            ok = 0.0
+            print('[bench] rank %d: hipGraph capture failed (%s: %s)' % (rank, type(e).__name__, str(e)[:300]),
+                  file=sys.stderr)
             torch.cuda.synchronize()
+        # every rank must take the same path (collectives are inside the captured step)
+        if -pdist.all_reduce_max(-ok, device) < 1.0:
+            if rank == 0:
+                print('[bench] falling back to eager execution on all ranks', file=sys.stderr)
+            mode, step_fn = 'eager', None
     if step_fn is None:
         step_fn = trainer.step
 

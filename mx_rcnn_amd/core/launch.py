@@ -1,0 +1,98 @@
+"""Shared plumbing for the CLI entry points (train_end2end.py, train_alternate.py,
+train_widerface*.py, test.py, tools/*): process-group bootstrap, roidb construction (VOC,
+.lst, synthetic), model construction + pretrained loading + new-layer initialisation
+(`train_end2end.py:56-78`), optimizer parameters (`train_end2end.py:98-105`), frozen prefixes.
+
+Multi-GPU: launch one process per GPU with ``torchrun --nproc-per-node N`` (or
+``python -m torch.distributed.run``); ``--gpus`` is accepted for command-line parity but the
+device of each rank is its LOCAL_RANK.  Gradients are summed across ranks like the
+reference's kvstore (rescale_grad 1.0).
+"""
+import logging
+import os
+
+import numpy as np
+import torch
+
+from ..config import config, override, parse_cfg_overrides, snapshot
+from ..models import FasterRCNN
+from ..parallel import dist as pdist
+from ..utils.load_model import load_param
+from .lr_scheduler import FactorScheduler, WarmupScheduler
+
+FIXED_PREFIX = {'vgg': ['conv1', 'conv2'], 'resnet': ['conv0', 'stage1', 'stage2', 'bn_data', 'bn0']}
+
+
+def setup_logging(rank=0):
+    logging.basicConfig(level=logging.INFO if rank == 0 else logging.WARNING,
+                        format='%(asctime)s %(levelname)s %(message)s')
+
+
+def add_common_args(parser):
+    parser.add_argument('--network', default='vgg16', help='vgg16 | resnet18..resnet200')
+    parser.add_argument('--synthetic', type=int, default=0, help='use N synthetic images instead of a dataset')
+    parser.add_argument('--synthetic-shape', default='600x1000')
+    parser.add_argument('--cfg', nargs='*', default=[], help='config overrides key=value (e.g. TRAIN.RPN_MIN_SIZE=10)')
+    parser.add_argument('--max-steps', type=int, default=None, help='stop after this many steps (smoke runs)')
+    parser.add_argument('--eager', action='store_true', help='disable hipGraph step capture')
+    parser.add_argument('--ims-per-gpu', type=int, default=1)
+    parser.add_argument('--seed', type=int, default=0)
+    return parser
+
+
+def init_runtime(args):
+    rank, world, local_rank, device = pdist.init_distributed()
+    setup_logging(rank)
+    if getattr(args, 'cfg', None):
+        override(parse_cfg_overrides(args.cfg))
+    torch.manual_seed(getattr(args, 'seed', 0) + rank)
+    np.random.seed(getattr(args, 'seed', 0) + rank)
+    return rank, world, device
+
+
+def family(network):
+    return 'resnet' if network.startswith('resnet') else 'vgg'
+
+
+def build_model(network, num_classes, pretrained=None, load_epoch=0, resume=False, bn_mom=0.99, train_mode='e2e'):
+    """Model with MXNet names; loads ``pretrained-%04d.params`` when it exists, drops the
+    ImageNet classifier, re-initialises the new detection layers unless resuming."""
+    model = FasterRCNN(network, num_classes, cfg=snapshot(), bn_mom=bn_mom, train_mode=train_mode)
+    arg = aux = None
+    if pretrained and pretrained.lower() != 'none':
+        path = '%s-%04d.params' % (pretrained, load_epoch)
+        if os.path.exists(path):
+            arg, aux, _ = load_param(pretrained, load_epoch, convert=False)
+            for k in ('fc8_weight', 'fc8_bias', 'fc1_weight', 'fc1_bias'):
+                arg.pop(k, None)
+            if not resume:
+                for k in [k for k in arg if k.startswith('rpn_') or k.startswith('cls_score') or
+                          k.startswith('bbox_pred')]:
+                    arg.pop(k)  # keep the fresh N(0, 0.01) / N(0, 0.001) initialisation
+            logging.info('loaded pretrained %s (%d args, %d aux)', path, len(arg), len(aux))
+        else:
+            logging.warning('pretrained %s not found: random initialisation', path)
+    return model, arg, aux
+
+
+def optimizer_params(lr, mom, wd, factor_step, resume, warmup=True):
+    sched = FactorScheduler(factor_step, 0.1) if (resume or not warmup) else \
+        WarmupScheduler(factor_step, 0.1, warmup_lr=0.1 * lr, warmup_step=200)
+    return {'momentum': mom, 'wd': wd, 'learning_rate': lr, 'lr_scheduler': sched, 'clip_gradient': 1.0,
+            'rescale_grad': 1.0}
+
+
+def e2e_config():
+    """Run-time mutation of train_end2end.py:25-32."""
+    config.TRAIN.BG_THRESH_LO = 0.0
+    config.TRAIN.HAS_RPN = True
+    config.END2END = 1
+    config.TRAIN.BBOX_NORMALIZATION_PRECOMPUTED = True
+
+
+def synthetic_roidb(args, num_classes, flip=False):
+    from ..data.load_data import load_synthetic_roidb
+    h, w = [int(v) for v in args.synthetic_shape.lower().split('x')]
+    config.SCALES = (min(h, w),)
+    config.MAX_SIZE = max(h, w)
+    return load_synthetic_roidb(args.synthetic, h, w, num_classes, flip=flip, seed=args.seed)

@@ -124,10 +124,13 @@ class FasterRCNN(nn.Module):
                               sigma=3.0, grad_scale=1.0)
         return cls_loss, bbox_loss, at
 
-    def _head_losses(self, cls_score, bbox_pred, label, bbox_target, inside, outside):
-        cls_loss, cls_prob = softmax_ce(cls_score, label, 'batch')
+    def _head_losses(self, cls_score, bbox_pred, label, bbox_target, inside, outside, e2e=True):
+        """e2e graph: SoftmaxOutput('batch') + MakeLoss(grad_scale=1/BATCH_SIZE) (`rcnn/symbol.py:372-378`);
+        Fast R-CNN graph: normalization 'null', grad_scale 1, the optimizer's rescale_grad =
+        1/BATCH_SIZE does the scaling (`rcnn/symbol.py:105-111`, `tools/train_rcnn.py`)."""
+        cls_loss, cls_prob = softmax_ce(cls_score, label, 'batch' if e2e else 'null')
         bbox_loss = smooth_l1(bbox_pred, bbox_target, inside, outside, sigma=1.0,
-                              grad_scale=1.0 / float(self.cfg.TRAIN.BATCH_SIZE))
+                              grad_scale=1.0 / float(self.cfg.TRAIN.BATCH_SIZE) if e2e else 1.0)
         return cls_loss, bbox_loss, cls_prob
 
     # ------------------------------------------------------------------ modes
@@ -161,7 +164,8 @@ class FasterRCNN(nn.Module):
         feat = self.trunk(data)
         pooled = roi_pool(feat, rois, (7, 7), 1.0 / self.feat_stride)
         cls_score, bbox_pred = self.head(pooled)
-        cls_loss, bbox_loss, cls_prob = self._head_losses(cls_score, bbox_pred, label, bbox_target, inside, outside)
+        cls_loss, bbox_loss, cls_prob = self._head_losses(cls_score, bbox_pred, label, bbox_target, inside, outside,
+                                                          e2e=False)
         return {'loss': cls_loss + bbox_loss, 'cls_loss': cls_loss, 'bbox_loss': bbox_loss, 'cls_prob': cls_prob,
                 'label': label, 'num_images': data.shape[0], 'num_rois': rois.shape[0]}
 

@@ -47,8 +47,6 @@ class _FrozenBnRelu(torch.autograd.Function):
                                          tg if direct else None, tb if direct else None)
             dx = dx if need_dx else None
             if direct:  # accumulated straight into the flat gradient buffers
-                grad_sink.delivered(ctx.params[0])
-                grad_sink.delivered(ctx.params[1])
                 return dx, None, None, None, None, None, None, None
         else:
             g = torch.ones_like(gamma) if ctx.fix_gamma else gamma

@@ -72,7 +72,6 @@ class _ConvIgemm(torch.autograd.Function):
             tgt = grad_sink.target(ctx.param)
             if tgt is not None and tgt.is_contiguous(memory_format=torch.channels_last):
                 need_ext().conv_wgrad(dy, x, w.shape[2], w.shape[3], ctx.stride, ctx.pad, 0, tgt)
-                grad_sink.delivered(ctx.param)
             else:
                 dw = need_ext().conv_wgrad(dy, x, w.shape[2], w.shape[3], ctx.stride, ctx.pad)
             if need_b:

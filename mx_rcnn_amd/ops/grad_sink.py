@@ -3,9 +3,11 @@
 Parameters managed by the FlatParamStore carry a pre-set ``.grad`` that is a view of a flat
 buffer.  Kernels that produce a parameter gradient (MFMA conv wgrad, fused BN backward) can
 ACCUMULATE straight into that view and return ``None`` to autograd, which removes one
-AccumulateGrad ``add`` kernel per parameter per step (~300 launches on ResNet-101).  Because
-autograd then never runs AccumulateGrad for that parameter, the producer calls
-``delivered(param)`` so the readiness hooks (the bucketed all-reduce) still fire.
+AccumulateGrad ``add`` kernel per parameter per step (~300 launches on ResNet-101).  The
+engine still visits the parameter's AccumulateGrad node with an undefined gradient and runs
+its post-accumulate hooks (verified on torch 2.10, tests/test_kernels.py
+test_direct_grad_delivery), so the readiness hooks -- the bucketed all-reduce -- fire exactly
+once per step either way; producers must NOT call ``delivered`` themselves.
 """
 _ENABLED = set()
 _HOOKS = {}

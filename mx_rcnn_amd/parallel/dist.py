@@ -28,7 +28,8 @@ def init_distributed(backend=None, timeout_s=600):
     device = torch.device('cuda', local_rank) if use_gpu else torch.device('cpu')
     if use_gpu:
         torch.cuda.set_device(device)
-    if world > 1 and not is_distributed():
+    force = os.environ.get('MXR_FORCE_DIST', '0') == '1'  # 1-rank process group (tests the RCCL paths)
+    if (world > 1 or force) and not is_distributed():
         os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
         backend = backend or ('nccl' if use_gpu else 'gloo')
         kw = {}

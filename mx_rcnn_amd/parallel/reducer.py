@@ -13,6 +13,8 @@ Semantics: SUM across ranks (MXNet kvstore 'device', rescale_grad=1: `train_end2
 link per hop, so fewer, larger messages win; the default 64 MB keeps ResNet-101's 92 MB of
 bf16 gradients in 2 buckets and VGG16's fc6 (205 MB bf16) in its own bucket.
 """
+import os
+
 import torch
 import torch.distributed as dist
 
@@ -39,7 +41,7 @@ class BucketReducer:
         self.buckets = []
         self._param_bucket = {}
         self._hooks = []
-        if not is_distributed() or self.world == 1:
+        if not is_distributed() or (self.world == 1 and os.environ.get('MXR_FORCE_DIST', '0') != '1'):
             return
         for g in store.groups:
             esize = g.grad.element_size()

@@ -1,0 +1,6 @@
+#!/usr/bin/env python
+"""WIDER FACE training with ResNet-34 (reference `train_widerface_resnet34.py`)."""
+import train_widerface
+
+if __name__ == '__main__':
+    train_widerface.main(train_widerface.parse_args(default_network='resnet34'), default_network='resnet34')

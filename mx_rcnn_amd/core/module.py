@@ -45,7 +45,7 @@ class MutableModule(object):
         self.work_load_list = work_load_list
         self.max_data_shapes, self.max_label_shapes = max_data_shapes, max_label_shapes
         self.fixed_param_prefix = fixed_param_prefix or []
-        self.use_graph = (self.context.type == 'cuda') if use_graph is None else use_graph
+        self.use_graph = (self.context.type == 'cuda') and (use_graph is None or bool(use_graph))
         self.compute_dtype = compute_dtype
         self.binded = self.params_initialized = self.optimizer_initialized = False
         self.trainer = None
@@ -101,7 +101,7 @@ class MutableModule(object):
         self.params_initialized = True
 
     def _load_model_arrays(self, arg_params, aux_params, allow_missing=True):
-        cur = self.model.arg_params()
+        cur = self._model_args()
         missing = []
         with torch.no_grad():
             for k, t in cur.items():
@@ -118,13 +118,28 @@ class MutableModule(object):
     def _load_aux(self, aux_params):
         if not aux_params:
             return
-        cur = self.model.aux_params()
+        cur = self._model_aux()
         with torch.no_grad():
             for k, t in cur.items():
                 if k in aux_params:
                     src = aux_params[k]
                     src = src if torch.is_tensor(src) else torch.as_tensor(np.asarray(src))
                     t.copy_(src.reshape(t.shape).to(t.device, t.dtype))
+
+    def _graph_mode(self):
+        return self.mode if self.mode in ('rpn', 'rcnn') else None
+
+    def _model_args(self):
+        try:
+            return self.model.arg_params(self._graph_mode())
+        except TypeError:
+            return self.model.arg_params()
+
+    def _model_aux(self):
+        try:
+            return self.model.aux_params(self._graph_mode())
+        except TypeError:
+            return self.model.aux_params()
 
     def init_optimizer(self, kvstore='device', optimizer='sgd', optimizer_params=None, force_init=False):
         if self.optimizer_initialized and not force_init:
@@ -193,9 +208,9 @@ class MutableModule(object):
         if self.trainer is not None:
             arg = {k: v.detach().float().cpu().numpy() for k, v in self.trainer.store.state_arrays().items()}
         else:
-            arg = {k: v.detach().float().cpu().numpy() for k, v in self.model.arg_params().items()}
+            arg = {k: v.detach().float().cpu().numpy() for k, v in self._model_args().items()}
         aux = {}
-        for k, v in self.model.aux_params().items():
+        for k, v in self._model_aux().items():
             t = v.detach().float().clone()
             if pdist.is_distributed():
                 torch.distributed.all_reduce(t)
@@ -247,9 +262,11 @@ class MutableModule(object):
             if rank == 0:
                 for cb in cbs_e:
                     cb(epoch, self.symbol, arg, aux)
-            train_data.reset()
             if max_steps is not None and steps >= max_steps:
                 break
+            train_data.reset()
+        if hasattr(train_data, 'close'):
+            train_data.close()
 
 
 def default_lr_scheduler(step, factor=0.1):

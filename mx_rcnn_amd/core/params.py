@@ -50,14 +50,14 @@ class ParamGroup:
 
 class FlatParamStore:
     def __init__(self, model, fixed_param_prefix=None, compute_dtype=torch.bfloat16, device=None,
-                 channels_last=True):
+                 channels_last=True, mode=None):
         self.model = model
         self.compute_dtype = compute_dtype
         dev = torch.device(device) if device is not None else next(model.parameters()).device
         self.device = dev
         lowp_enabled = compute_dtype != torch.float32
         fixed = fixed_param_prefix or []
-        layers = list(model.mx_layers())
+        layers = list(model.mx_layers(mode)) if mode is not None else list(model.mx_layers())
         named = []  # (mx_name, module, attr, param)
         for m in layers:
             for attr, p in m._parameters.items():
@@ -98,9 +98,11 @@ class FlatParamStore:
                     m._parameters[attr] = param
                     self.params[n] = param
                     off += numel
-            # frozen: cast once, no grad
+            # frozen: cast once, no grad (the fp32 original is kept for checkpoints)
+            self.frozen_fp32 = {}
             for n, m, attr, p in named:
                 if n in self.fixed_names:
+                    self.frozen_fp32[n] = p.detach().to(dev, torch.float32).clone()
                     lowp = lowp_enabled and not _is_bn_param(n)
                     t = p.detach().to(dev, compute_dtype if lowp else torch.float32)
                     if channels_last and t.dim() == 4:
@@ -142,8 +144,9 @@ class FlatParamStore:
             for (n, _, _, numel, shape, cl), off in zip(g.entries, g.offsets):
                 if n == name:
                     return self._shaped(g.master[off:off + numel], shape, cl)
-        p = self.params[name]
-        return p.detach().float()
+        if name in self.frozen_fp32:
+            return self.frozen_fp32[name]
+        return self.params[name].detach().float()
 
     def state_arrays(self):
         """fp32 copies of every parameter (trainable from master, frozen from the cast copy)."""
@@ -167,6 +170,8 @@ class FlatParamStore:
                             found = True
                 if not found:
                     p.data.copy_(src.to(p.dtype))
+                    if n in self.frozen_fp32:
+                        self.frozen_fp32[n].copy_(src)
         if strict and missing:
             raise KeyError('missing params: %s' % missing[:10])
         return missing

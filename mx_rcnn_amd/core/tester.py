@@ -38,10 +38,11 @@ def pred_eval(detector, test_data, imdb, vis=False, thresh=0.05, max_per_image=1
                 vis_all_detection(batch['data'].numpy() if torch.is_tensor(batch['data']) else batch['data'],
                                   dets, imdb.classes)
             i += 1
-    cache_folder = os.path.join(imdb.cache_path, imdb.name)
-    os.makedirs(cache_folder, exist_ok=True)
-    np.savez(os.path.join(cache_folder, 'detections.npz'),
-             **{'c%d_i%d' % (j, k): all_boxes[j][k] for j in range(imdb.num_classes) for k in range(num_images)})
+    if getattr(imdb, 'cache_path', None):
+        cache_folder = os.path.join(imdb.cache_path, imdb.name)
+        os.makedirs(cache_folder, exist_ok=True)
+        np.savez(os.path.join(cache_folder, 'detections.npz'),
+                 **{'c%d_i%d' % (j, k): all_boxes[j][k] for j in range(imdb.num_classes) for k in range(num_images)})
     return imdb.evaluate_detections(all_boxes)
 
 

@@ -23,7 +23,8 @@ class Trainer:
         self.device, self.compute_dtype, self.channels_last = dev, compute_dtype, channels_last
         self.model = model.to(dev)
         self.mode = mode
-        self.store = FlatParamStore(self.model, fixed_param_prefix, compute_dtype, dev, channels_last)
+        self.store = FlatParamStore(self.model, fixed_param_prefix, compute_dtype, dev, channels_last,
+                                   mode=mode if mode in ('rpn', 'rcnn') else None)
         self.reducer = BucketReducer(self.store, bucket_mb=bucket_mb, average=average_grads)
         self.momentum, self.wd, self.clip, self.rescale = momentum, wd, clip_gradient, rescale_grad
         self.base_lr = lr

@@ -46,6 +46,11 @@ class DetectionList(IMDB):
         assert os.path.exists(f), 'Path does not exist: {}'.format(f)
         return f
 
+    def evaluate_detections(self, detections):
+        """mAP against the list's own boxes (the reference's list dataset had no evaluator)."""
+        from .voc_eval import eval_in_memory
+        return eval_in_memory(self.gt_roidb(), detections, self.classes)
+
     def gt_roidb(self):
         cache_file = os.path.join(self.cache_path, self.name + '_gt_roidb.npz')
         if os.path.exists(cache_file):

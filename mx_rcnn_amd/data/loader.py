@@ -74,6 +74,8 @@ class _Prefetcher:
             self._stop = True
         for _ in self._threads:
             self._sem.release()
+        for t in self._threads:
+            t.join()
 
 
 def _pin(t):
@@ -131,7 +133,13 @@ class _BaseLoader:
                 self.index = rng.permutation(self.size)
         self.epoch += 1
         self._batches = self._shard_batches()
-        self._pf = _Prefetcher(self._make_batch, len(self._batches), self.prefetch, self.workers)
+        self._pf = None  # started lazily by the first __next__ of the epoch
+
+    def close(self):
+        """Stop the prefetch workers (call before exiting mid-epoch)."""
+        if self._pf is not None:
+            self._pf.close()
+            self._pf = None
 
     def _shard_batches(self):
         nb = self.size // self.batch_size
@@ -159,6 +167,8 @@ class _BaseLoader:
     def __next__(self):
         if not self.iter_next():
             raise StopIteration
+        if self._pf is None:
+            self._pf = _Prefetcher(self._make_batch, len(self._batches), self.prefetch, self.workers)
         b = self._pf.get(self.cur)
         self.cur += 1
         return b

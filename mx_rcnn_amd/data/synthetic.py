@@ -26,6 +26,10 @@ class SyntheticDetection(IMDB):
     def image_size_from_index(self, index):
         return self.height, self.width
 
+    def evaluate_detections(self, detections):
+        from .voc_eval import eval_in_memory
+        return eval_in_memory(self.gt_roidb(), detections, self.classes)
+
     def gt_roidb(self):
         rng = np.random.RandomState(self.seed)
         out = []

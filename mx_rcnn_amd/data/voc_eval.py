@@ -71,6 +71,12 @@ def voc_eval(detpath, annopath, imageset_file, classname, cache_dir, ovthresh=0.
     image_ids = [x[0] for x in split]
     confidence = np.array([float(x[1]) for x in split])
     bbox = np.array([[float(z) for z in x[2:]] for x in split]).reshape(-1, 4)
+    return match_detections(class_recs, image_ids, confidence, bbox, npos, ovthresh, use_07_metric)
+
+
+def match_detections(class_recs, image_ids, confidence, bbox, npos, ovthresh=0.5, use_07_metric=False):
+    """Greedy score-ordered matching of detections to (non-difficult) gt -> (rec, prec, ap).
+    ``class_recs[id] = {'bbox': (n,4), 'difficult': (n,) bool, 'det': [False]*n}``."""
     order = np.argsort(-confidence, kind='stable')
     bbox = bbox[order, :]
     image_ids = [image_ids[x] for x in order]
@@ -110,3 +116,32 @@ def voc_eval(detpath, annopath, imageset_file, classname, cache_dir, ovthresh=0.
     rec = tp / float(max(npos, 1))
     prec = tp / np.maximum(tp + fp, np.finfo(np.float64).eps)
     return rec, prec, voc_ap(rec, prec, use_07_metric)
+
+
+def eval_in_memory(gt_roidb, detections, classes, ovthresh=0.5, use_07_metric=False):
+    """mAP of ``detections[cls][img] = (n, 5)`` against in-memory gt entries (boxes, gt_classes)
+    -- the evaluator for datasets without VOC annotation files (synthetic, .lst lists)."""
+    aps = []
+    for c in range(1, len(classes)):
+        class_recs, npos = {}, 0
+        for i, r in enumerate(gt_roidb):
+            m = np.asarray(r['gt_classes']) == c
+            bb = np.asarray(r['boxes'])[m].astype(float).reshape(-1, 4)
+            class_recs[i] = {'bbox': bb, 'difficult': np.zeros(len(bb), bool), 'det': [False] * len(bb)}
+            npos += len(bb)
+        ids, conf, boxes = [], [], []
+        for i in range(len(gt_roidb)):
+            d = detections[c][i] if len(detections[c]) > i else []
+            d = np.asarray(d, dtype=np.float64).reshape(-1, 5)
+            ids += [i] * len(d)
+            conf.append(d[:, 4])
+            boxes.append(d[:, :4])
+        conf = np.concatenate(conf) if conf else np.zeros(0)
+        boxes = np.concatenate(boxes) if boxes else np.zeros((0, 4))
+        _, _, ap = match_detections(class_recs, ids, conf, boxes, npos, ovthresh, use_07_metric)
+        if npos > 0:
+            aps.append(ap)
+        logging.info('AP for %s = %.4f', classes[c], ap)
+    mean_ap = float(np.mean(aps)) if aps else 0.0
+    logging.info('Mean AP = %.4f', mean_ap)
+    return mean_ap

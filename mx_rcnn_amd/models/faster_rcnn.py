@@ -88,22 +88,48 @@ class FasterRCNN(nn.Module):
             nn.init.normal_(self.head.fc7.weight, 0, 0.005)
 
     # ------------------------------------------------------------------ naming / params
-    def mx_layers(self):
-        for m in self.modules():
+    GRAPH_PARTS = {'rpn': ('trunk', 'rpn'), 'rpn_test': ('trunk', 'rpn'), 'rcnn': ('trunk', 'head')}
+
+    def mx_layers(self, mode=None):
+        """Named layers of the graph ``mode`` builds: the RPN graphs (`rcnn/symbol.py` get_*_rpn)
+        hold no Fast R-CNN head and the RCNN graphs no RPN, so their checkpoints / optimizers
+        only see those parameters; every other mode (e2e, test) holds all of them."""
+        parts = self.GRAPH_PARTS.get(mode)
+        mods = self.modules() if parts is None else (m for p in parts for m in getattr(self, p).modules())
+        for m in mods:
             if hasattr(m, 'mx_args'):
                 yield m
 
-    def arg_params(self):
+    def arg_params(self, mode=None):
         out = {}
-        for m in self.mx_layers():
+        for m in self.mx_layers(mode):
             out.update(m.mx_args())
         return out
 
-    def aux_params(self):
+    def aux_params(self, mode=None):
         out = {}
-        for m in self.mx_layers():
+        for m in self.mx_layers(mode):
             out.update(m.mx_aux())
         return out
+
+    @torch.no_grad()
+    def calibrate_bn(self, data):
+        """Set the trunk's frozen BN moving statistics from one fp32 forward over ``data`` (N,3,H,W).
+        Random-init ResNets have no meaningful frozen statistics; without this their activations
+        grow through 100+ pre-activation units.  Pretrained checkpoints carry real ones (load them
+        after, or skip this)."""
+        bns = [m for m in self.trunk.modules() if hasattr(m, 'moving_var')]
+        was = self.training
+        self.eval()
+        for m in bns:
+            m._calibrate = True
+        try:
+            self.trunk(data.float())
+        finally:
+            for m in bns:
+                m._calibrate = False
+            self.train(was)
+        return len(bns)
 
     def feat_shape(self, h, w):
         return self.trunk.feat_shape(h, w)
@@ -149,7 +175,11 @@ class FasterRCNN(nn.Module):
         B = data.shape[0]
         R = cls_score.shape[0]
         loss = rpn_cls_loss + rpn_bbox_loss + cls_loss + bbox_loss
-        return {'loss': loss, 'rpn_cls_loss': rpn_cls_loss, 'rpn_bbox_loss': rpn_bbox_loss,
+        # 'loss' carries the gradients (each loss applies its own grad_scale in backward); its value
+        # mixes normalised and summed terms like the reference's outputs.  'objective' is the
+        # value of the function actually being minimised.
+        obj = (rpn_cls_loss + rpn_bbox_loss + cls_loss + bbox_loss / float(self.cfg.TRAIN.BATCH_SIZE)).detach()
+        return {'loss': loss, 'objective': obj, 'rpn_cls_loss': rpn_cls_loss, 'rpn_bbox_loss': rpn_bbox_loss,
                 'cls_loss': cls_loss, 'bbox_loss': bbox_loss, 'cls_prob': cls_prob, 'label': pt['label'],
                 'rpn_cls_score': rpn_cls, 'rpn_label': at['label'], 'num_images': B, 'num_rois': R}
 
@@ -157,7 +187,7 @@ class FasterRCNN(nn.Module):
         feat = self.trunk(data)
         rpn_cls, rpn_bbox = self.rpn(feat)
         cls_loss, bbox_loss, at = self._rpn_losses(rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt)
-        return {'loss': cls_loss + bbox_loss, 'rpn_cls_loss': cls_loss, 'rpn_bbox_loss': bbox_loss,
+        return {'loss': cls_loss + bbox_loss, 'objective': (cls_loss + bbox_loss).detach(), 'rpn_cls_loss': cls_loss, 'rpn_bbox_loss': bbox_loss,
                 'rpn_cls_score': rpn_cls, 'rpn_label': at['label'], 'num_images': data.shape[0]}
 
     def train_rcnn(self, data, rois, label, bbox_target, inside, outside):
@@ -166,7 +196,8 @@ class FasterRCNN(nn.Module):
         cls_score, bbox_pred = self.head(pooled)
         cls_loss, bbox_loss, cls_prob = self._head_losses(cls_score, bbox_pred, label, bbox_target, inside, outside,
                                                           e2e=False)
-        return {'loss': cls_loss + bbox_loss, 'cls_loss': cls_loss, 'bbox_loss': bbox_loss, 'cls_prob': cls_prob,
+        return {'loss': cls_loss + bbox_loss,
+                'objective': ((cls_loss + bbox_loss) / float(self.cfg.TRAIN.BATCH_SIZE)).detach(), 'cls_loss': cls_loss, 'bbox_loss': bbox_loss, 'cls_prob': cls_prob,
                 'label': label, 'num_images': data.shape[0], 'num_rois': rois.shape[0]}
 
     @torch.no_grad()

@@ -82,6 +82,17 @@ class BatchNorm(MxLayer):
         return {'%s_moving_mean' % self.mx_name: self.moving_mean, '%s_moving_var' % self.mx_name: self.moving_var}
 
     def forward(self, x):
+        if getattr(self, '_calibrate', False):
+            # data-dependent init: moving stats := statistics of this batch (stand-in for the
+            # ImageNet statistics a pretrained checkpoint carries)
+            xf = x.float()
+            with torch.no_grad():
+                self.moving_mean.copy_(xf.mean(dim=(0, 2, 3)))
+                self.moving_var.copy_(xf.var(dim=(0, 2, 3), unbiased=False))
+            g = torch.ones_like(self.gamma) if self.fix_gamma else self.gamma
+            y = F.batch_norm(xf, self.moving_mean, self.moving_var, g.float(), self.beta.float(), training=False,
+                             eps=self.eps).to(x.dtype)
+            return F.relu(y) if self.relu else y
         if self.use_global_stats or not self.training:
             return frozen_bn_relu(x, self.gamma, self.beta, self.moving_mean, self.moving_var, self.eps,
                                   self.fix_gamma, self.relu)

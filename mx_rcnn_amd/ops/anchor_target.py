@@ -32,7 +32,7 @@ def _assign_ref(H, W, base, feat_stride, im_info, border, gt, n_gt, neg, pos, cl
                   (anchors[:, 2] < im_w + border) & (anchors[:, 3] < im_h + border))
         ng = int(n_gt[b])
         idx = torch.nonzero(inside)[:, 0]
-        if ng == 0:
+        if ng == 0 or idx.numel() == 0:
             labels[b, idx] = 0
             continue
         g = gt[b, :ng, :4].float()

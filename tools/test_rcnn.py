@@ -19,8 +19,12 @@ from mx_rcnn_amd.utils.load_model import load_param  # noqa: E402
 
 
 def test_rcnn(image_set, year, root_path, devkit_path, prefix, epoch, ctx, vis=False, has_rpn=True,
-              proposal='rpn', network='vgg16', end2end=False):
-    if has_rpn:
+              proposal='rpn', network='vgg16', end2end=False, imdb_roidb=None):
+    if imdb_roidb is not None:  # e.g. synthetic set (in-memory evaluation)
+        config.TEST.HAS_RPN = True
+        imdb, roidb = imdb_roidb
+        test_data = AnchorLoader(None, roidb, batch_size=1, shuffle=False, mode='test')
+    elif has_rpn:
         config.TEST.HAS_RPN = True
         config.TEST.RPN_PRE_NMS_TOP_N = 6000
         config.TEST.RPN_POST_NMS_TOP_N = 300
@@ -48,6 +52,7 @@ def parse_args(argv=None):
     p.add_argument('--has_rpn', action='store_true')
     p.add_argument('--end2end', action='store_true')
     p.add_argument('--proposal', default='rpn')
+    p.add_argument('--num-classes', dest='num_classes', type=int, default=21, help='for --synthetic sets')
     launch.add_common_args(p)
     return p.parse_args(argv)
 
@@ -55,5 +60,6 @@ def parse_args(argv=None):
 if __name__ == '__main__':
     a = parse_args()
     rank, world, dev = launch.init_runtime(a)
+    syn = launch.synthetic_roidb(a, a.num_classes) if a.synthetic else None
     test_rcnn(a.image_set, a.year, a.root_path, a.devkit_path, a.prefix, a.epoch, dev, a.vis,
-              a.has_rpn or a.end2end, a.proposal, a.network, a.end2end)
+              a.has_rpn or a.end2end, a.proposal, a.network, a.end2end, imdb_roidb=syn)

@@ -5,6 +5,8 @@ import json
 import logging
 import time
 
+from ..utils import profiler as prof
+
 
 class BatchEndParam(object):
     def __init__(self, epoch, nbatch, eval_metric, locals=None):
@@ -37,10 +39,14 @@ class Speedometer(object):
                 else:
                     names, values = [], []
                     logging.info('Iter[%d] Batch [%d]\tSpeed: %.2f samples/sec', param.epoch, count, speed)
+                stages = prof.report() if prof.enabled() else None
+                if stages:
+                    logging.info('Epoch[%d] Batch [%d]\tStages: %s', param.epoch, count, prof.format_report(stages))
                 if self.jsonl:
                     with open(self.jsonl, 'a') as f:
                         f.write(json.dumps({'epoch': param.epoch, 'batch': count, 'samples_per_sec': speed,
-                                            'metrics': dict(zip(names, values))}) + '\n')
+                                            'metrics': dict(zip(names, values)),
+                                            'stage_ms': stages or {}}) + '\n')
                 self.tic = time.time()
         else:
             self.init = True

@@ -96,3 +96,14 @@ def synthetic_roidb(args, num_classes, flip=False):
     config.SCALES = (min(h, w),)
     config.MAX_SIZE = max(h, w)
     return load_synthetic_roidb(args.synthetic, h, w, num_classes, flip=flip, seed=args.seed)
+
+
+def calibrate_if_random(model, loader, arg_params):
+    """Random-init ResNets get data-dependent BN statistics from the first batch (a pretrained
+    checkpoint carries real ones); without them 100+ pre-activation units blow up."""
+    if arg_params or not model.network.startswith('resnet'):
+        return False
+    b = loader.get_batch()
+    model.calibrate_bn(torch.as_tensor(b['data']))
+    logging.info('no pretrained weights: calibrated %s BN statistics on the first batch', model.network)
+    return True

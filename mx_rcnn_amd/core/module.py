@@ -15,6 +15,7 @@ inherited MXNet ``BaseModule.fit``) on top of :class:`Trainer`.
   fetched (checkpointing), mirroring MXNet's ``get_params``; rank 0 runs epoch-end callbacks.
 """
 import logging
+import os
 import time
 
 import numpy as np
@@ -24,6 +25,7 @@ from ..parallel import dist as pdist
 from .callback import BatchEndParam
 from .lr_scheduler import FactorScheduler
 from .trainer import GraphedStep, Trainer
+from ..utils import profiler as prof
 
 
 class MutableModule(object):
@@ -184,8 +186,12 @@ class MutableModule(object):
         t.store.sgd_step(t.lr_t, t.momentum, t.wd, t.rescale, t.clip)
 
     def step(self, data_batch):
-        """forward + backward + update fused (graph-replayed per input shape when enabled)."""
-        if not self.use_graph:
+        """forward + backward + update fused (graph-replayed per input shape when enabled).
+        Steps watched by a norm monitor or the stage profiler run eagerly (hooks and timing
+        events do not exist inside a replayed graph)."""
+        eager = (not self.use_graph or prof.enabled() or
+                 (self._monitor is not None and self._monitor.activated))
+        if eager:
             self._outputs = self.trainer.step(data_batch)
             return self._outputs
         key = tuple((k, tuple(v.shape)) for k, v in sorted(data_batch.items()) if torch.is_tensor(v))
@@ -218,6 +224,33 @@ class MutableModule(object):
             aux[k] = t.cpu().numpy()
         return arg, aux
 
+    def save_optimizer_states(self, fname):
+        """Momentum + update count (MXNet ``Module.save_optimizer_states``), MXNet .params codec."""
+        from ..utils import ndarray_io
+        st = {'mom:' + k: v.detach().cpu().numpy() for k, v in self.trainer.store.optimizer_state().items()}
+        st['num_update'] = np.array([self.trainer.num_update], np.float32)
+        st['rng_cpu'] = torch.get_rng_state().numpy()
+        if self.context.type == 'cuda':
+            st['rng_cuda'] = torch.cuda.get_rng_state(self.context).numpy()
+        ndarray_io.save(fname, st)
+
+    def load_optimizer_states(self, fname):
+        from ..utils import ndarray_io
+        st = ndarray_io.load(fname)
+        moms = {k[4:]: v for k, v in st.items() if k.startswith('mom:')}
+        missing = self.trainer.store.load_optimizer_state(moms)
+        if 'num_update' in st:
+            self.trainer.num_update = int(np.asarray(st['num_update']).reshape(-1)[0])
+            self.trainer.num_update -= 1
+            self.trainer.update_lr()  # lr tensor matches the schedule position
+        if 'rng_cpu' in st:
+            torch.set_rng_state(torch.from_numpy(np.ascontiguousarray(st['rng_cpu'], dtype=np.uint8)))
+        if 'rng_cuda' in st and self.context.type == 'cuda':
+            torch.cuda.set_rng_state(torch.from_numpy(np.ascontiguousarray(st['rng_cuda'], dtype=np.uint8)),
+                                     self.context)
+        if missing:
+            logging.warning('optimizer state missing for %d params (e.g. %s)', len(missing), missing[0])
+
     def set_params(self, arg_params, aux_params, allow_missing=False, force_init=True):
         self.init_params(None, arg_params, aux_params, allow_missing=allow_missing, force_init=force_init)
 
@@ -226,25 +259,45 @@ class MutableModule(object):
             kvstore='device', optimizer='sgd', optimizer_params=None, eval_batch_end_callback=None,
             initializer=None, arg_params=None, aux_params=None, allow_missing=True, force_rebind=False,
             force_init=False, begin_epoch=0, num_epoch=None, validation_metric=None, monitor=None,
-            max_steps=None):
+            max_steps=None, check_every=20, states_prefix=None, resume_states=None):
+        """MXNet ``BaseModule.fit``.  Extras: ``max_steps`` (smoke runs), ``check_every`` (non-finite
+        guard period), ``states_prefix`` (rank 0 writes ``<prefix>-%04d.states`` = momentum +
+        update count at each epoch end) and ``resume_states`` (a .states file to restore after
+        the optimizer is created; the data order also resumes at ``begin_epoch``)."""
         assert num_epoch is not None, 'please specify number of epochs'
         self.bind(for_training=True)
         if monitor is not None:
             self.install_monitor(monitor)
         self.init_params(initializer, arg_params, aux_params, allow_missing, force_init)
         self.init_optimizer(kvstore, optimizer, optimizer_params)
+        if resume_states:
+            self.load_optimizer_states(resume_states)
+            logging.info('restored optimizer states from %s', resume_states)
+        if begin_epoch > 0 and hasattr(train_data, 'epoch'):
+            train_data.epoch = begin_epoch  # same shuffle as an uninterrupted run
+            train_data.reset()
         rank = pdist.get_rank()
         cbs_b = batch_end_callback if isinstance(batch_end_callback, (list, tuple)) else \
             ([batch_end_callback] if batch_end_callback else [])
         cbs_e = epoch_end_callback if isinstance(epoch_end_callback, (list, tuple)) else \
             ([epoch_end_callback] if epoch_end_callback else [])
         steps = 0
+        fault_step, fault_kind = parse_fault(os.environ.get('MXR_FAULT_INJECT'))
         for epoch in range(begin_epoch, num_epoch):
             tic = time.time()
             if eval_metric is not None:
                 eval_metric.reset()
             for nbatch, batch in enumerate(train_data):
+                if self._monitor is not None:
+                    self._monitor.tic()
+                fault = fault_step is not None and steps == fault_step
+                if fault:
+                    self.trainer.arm_fault(fault_kind)
                 self.step(batch)
+                if fault:
+                    self.trainer.disarm_fault()
+                if (steps + 1) % check_every == 0:
+                    self.trainer.check_finite(steps)
                 if eval_metric is not None:
                     self.update_metric(eval_metric)
                 if self._monitor is not None:
@@ -254,6 +307,7 @@ class MutableModule(object):
                 steps += 1
                 if max_steps is not None and steps >= max_steps:
                     break
+            self.trainer.check_finite(steps)
             if eval_metric is not None:
                 for name, val in eval_metric.get_name_value():
                     logging.info('Epoch[%d] Train-%s=%f', epoch, name, val)
@@ -262,11 +316,21 @@ class MutableModule(object):
             if rank == 0:
                 for cb in cbs_e:
                     cb(epoch, self.symbol, arg, aux)
+                if states_prefix:
+                    self.save_optimizer_states('%s-%04d.states' % (states_prefix, epoch + 1))
             if max_steps is not None and steps >= max_steps:
                 break
             train_data.reset()
         if hasattr(train_data, 'close'):
             train_data.close()
+
+
+def parse_fault(spec):
+    """``MXR_FAULT_INJECT=nan@STEP`` (or ``inf@STEP``) -> (step, kind); None -> (None, None)."""
+    if not spec:
+        return None, None
+    kind, _, at = spec.partition('@')
+    return int(at), kind
 
 
 def default_lr_scheduler(step, factor=0.1):

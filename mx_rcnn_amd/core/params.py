@@ -111,6 +111,44 @@ class FlatParamStore:
                     self.params[n] = m._parameters[attr]
         for b in model.buffers():
             b.data = b.data.to(dev)
+        self._build_dgrad_cache()
+
+    # ------------------------------------------------------------------ dgrad filter cache
+    def _build_dgrad_cache(self):
+        """Flipped/transposed bf16 copies of every trainable conv filter the MFMA dgrad path
+        uses, refreshed by ONE multi-filter kernel after each update (ops/conv.py)."""
+        self._wt_table = None
+        if self.device.type != 'cuda' or self.compute_dtype != torch.bfloat16:
+            return
+        from ..ops import conv as conv_ops
+        from ..ops._ext import need_ext
+        ext = need_ext()
+        srcs, dsts = [], []
+        for g in self.groups:
+            if g.shadow is None:
+                continue
+            for (n, m, attr, numel, shape, cl) in g.entries:
+                if len(shape) != 4 or not cl:
+                    continue
+                o, i, kh, kw = shape
+                if o % 64 != 0 or i % 8 != 0 or kh != kw:
+                    continue
+                p = self.params[n]
+                buf = torch.empty((i, o, kh, kw), dtype=p.dtype, device=self.device,
+                                  memory_format=torch.channels_last)
+                conv_ops.register_dgrad_weight(p, buf)
+                srcs.append(p.detach())
+                dsts.append(buf)
+        if srcs:
+            n_ent, tiles = ext.wt_flip_table_info(srcs)
+            self._wt_table = (ext.wt_flip_build(srcs, dsts), n_ent, tiles, dsts)
+            self.refresh_dgrad_cache()
+
+    def refresh_dgrad_cache(self):
+        if self._wt_table is not None:
+            from ..ops._ext import need_ext
+            table, n_ent, tiles, _ = self._wt_table
+            need_ext().wt_flip_run(table, n_ent, tiles)
 
     @staticmethod
     def _flat_view(t, cl):
@@ -138,6 +176,7 @@ class FlatParamStore:
         for g in self.groups:
             sgd_momentum_(g.master, g.mom, g.grad, lr, momentum, wd if g.decay else 0.0, rescale, clip,
                           g.shadow)
+        self.refresh_dgrad_cache()
 
     def master_param(self, name):
         for g in self.groups:
@@ -147,6 +186,26 @@ class FlatParamStore:
         if name in self.frozen_fp32:
             return self.frozen_fp32[name]
         return self.params[name].detach().float()
+
+    def optimizer_state(self):
+        """Momentum of every trainable parameter (fp32, parameter layout) for exact resume."""
+        out = {}
+        for g in self.groups:
+            for (n, _, _, numel, shape, cl), off in zip(g.entries, g.offsets):
+                out[n] = self._shaped(g.mom[off:off + numel], shape, cl).contiguous()
+        return out
+
+    def load_optimizer_state(self, arrays):
+        missing = []
+        with torch.no_grad():
+            for g in self.groups:
+                for (n, _, _, numel, shape, cl), off in zip(g.entries, g.offsets):
+                    if n not in arrays:
+                        missing.append(n)
+                        continue
+                    src = torch.as_tensor(arrays[n]).to(self.device, torch.float32).reshape(shape)
+                    g.mom[off:off + numel].copy_(self._flat_view(src, cl))
+        return missing
 
     def state_arrays(self):
         """fp32 copies of every parameter (trainable from master, frozen from the cast copy)."""
@@ -172,6 +231,7 @@ class FlatParamStore:
                     p.data.copy_(src.to(p.dtype))
                     if n in self.frozen_fp32:
                         self.frozen_fp32[n].copy_(src)
+        self.refresh_dgrad_cache()
         if strict and missing:
             raise KeyError('missing params: %s' % missing[:10])
         return missing

@@ -5,9 +5,12 @@ One step = forward (mode-specific model entry) -> backward -> bucketed all-reduc
 so ``GraphedStep`` can capture the entire step into one hipGraph and replay it (static
 shapes: the detection ops are designed for it).
 """
+import os
+
 import torch
 
 from ..parallel.reducer import BucketReducer
+from ..utils import profiler as prof
 from .params import FlatParamStore
 
 
@@ -33,6 +36,8 @@ class Trainer:
             lr_scheduler.base_lr = lr
         self.lr_t = torch.full((1,), float(lr), dtype=torch.float32, device=dev)
         self.num_update = 0
+        self.nonfinite = torch.zeros((), dtype=torch.int32, device=dev)
+        self.fault = torch.ones((), dtype=torch.float32, device=dev) if os.environ.get('MXR_FAULT_INJECT') else None
 
     # ------------------------------------------------------------------
     def prepare_batch(self, batch):
@@ -63,10 +68,35 @@ class Trainer:
         self.store.zero_grad()
         self.reducer.prepare()
         out = self.forward(b)
-        out['loss'].backward()
-        self.reducer.finish()
-        self.store.sgd_step(self.lr_t, self.momentum, self.wd, self.rescale, self.clip)
+        if self.fault is not None:  # test hook: multiplies the loss by NaN on the armed step
+            out['loss'] = out['loss'] * self.fault
+            out['objective'] = out['objective'] * self.fault
+        # device-side non-finite guard: no host sync, read every `frequent` steps
+        self.nonfinite.add_((~torch.isfinite(out['objective'])).to(torch.int32))
+        with prof.range('backward+allreduce'):
+            out['loss'].backward()
+        with prof.range('allreduce_wait'):
+            self.reducer.finish()
+        with prof.range('sgd'):
+            self.store.sgd_step(self.lr_t, self.momentum, self.wd, self.rescale, self.clip)
         return out
+
+    def check_finite(self, step=None):
+        """Raise FloatingPointError if any step since the last check produced a non-finite loss
+        (one host read of a device counter)."""
+        n = int(self.nonfinite.item())
+        if n:
+            self.nonfinite.zero_()
+            raise FloatingPointError('non-finite loss in %d step(s) up to step %s' % (n, step))
+
+    def arm_fault(self, kind='nan'):
+        """Fault injection (``MXR_FAULT_INJECT=nan@STEP``): poison the next step's loss."""
+        if self.fault is not None:
+            self.fault.fill_(float('nan') if kind == 'nan' else float('inf'))
+
+    def disarm_fault(self):
+        if self.fault is not None:
+            self.fault.fill_(1.0)
 
     def update_lr(self):
         self.num_update += 1

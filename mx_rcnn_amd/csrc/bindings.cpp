@@ -1,6 +1,7 @@
 // Python bindings for the gfx950 kernels.  Thin: validate shapes/dtypes/devices, allocate
 // outputs through the PyTorch caching allocator, launch on the current HIP stream.  All
 // launches are graph-capturable (no host sync, no allocation inside the launchers).
+#include <cstring>
 #include <torch/extension.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
@@ -270,7 +271,7 @@ Tensor bn_relu_fwd(const Tensor& x, const Tensor& gamma, const Tensor& beta, con
 std::vector<Tensor> bn_relu_bwd(const Tensor& x, const Tensor& dy, const Tensor& gamma, const Tensor& beta,
                                 const Tensor& mean, const Tensor& var, double eps, bool fix_gamma, bool relu,
                                 bool need_dx, bool need_params, c10::optional<Tensor> dgamma_out,
-                                c10::optional<Tensor> dbeta_out) {
+                                c10::optional<Tensor> dbeta_out, c10::optional<Tensor> dres) {
   CHECK_DEV(x); CHECK_DEV(dy);
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "x must be channels_last");
   Tensor g = dy.contiguous(at::MemoryFormat::ChannelsLast);
@@ -294,19 +295,29 @@ std::vector<Tensor> bn_relu_bwd(const Tensor& x, const Tensor& dy, const Tensor&
     dbeta = vec ? at::empty({C}, x.options().dtype(at::kFloat)) : at::zeros({C}, x.options().dtype(at::kFloat));
   }
   need_params = need_params || acc;
+  Tensor rd;
+  if (dres.has_value() && dres->defined()) {
+    TORCH_CHECK(vec && need_dx, "dres needs C % 4 == 0 and need_dx");
+    rd = dres->contiguous(at::MemoryFormat::ChannelsLast);
+    TORCH_CHECK(rd.scalar_type() == x.scalar_type() && rd.sizes() == x.sizes(), "dres must match x");
+  }
   Tensor ws;
   if (need_params && vec) ws = at::empty({mxr::bn_bwd_workspace_floats(x.numel() / C, C)}, x.options().dtype(at::kFloat));
   mxr::bn_relu_bwd(x.data_ptr(), g.data_ptr(), is_bf16(x), x.numel() / C, C, gamma.data_ptr<float>(),
                    beta.data_ptr<float>(), mean.data_ptr<float>(), var.data_ptr<float>(), (float)eps,
                    fix_gamma ? 1 : 0, relu ? 1 : 0, need_dx ? dx.data_ptr() : nullptr,
-                   need_params ? dgamma.data_ptr<float>() : nullptr, need_params ? dbeta.data_ptr<float>() : nullptr,
+                   rd.defined() ? rd.data_ptr() : nullptr, need_params ? dgamma.data_ptr<float>() : nullptr, need_params ? dbeta.data_ptr<float>() : nullptr,
                    ws.defined() ? ws.data_ptr<float>() : nullptr, acc ? 1 : 0, cur_stream());
   return {dx, dgamma, dbeta};
 }
 
 // ---- implicit-GEMM conv ----------------------------------------------------------------
-Tensor conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::optional<Tensor> bias, int64_t stride, int64_t pad,
-                      bool relu, int64_t tile, int64_t splits) {
+// conv_igemm_fwd(x, w, bias, stride, pad, relu, tile, splits, residual, bn, bn_eps, bn_fix_gamma, act_relu)
+//   -> [y] or, when bn = (gamma, beta, mean, var) is given, [y, act(bn(y))]  (see ConvEpi)
+std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::optional<Tensor> bias, int64_t stride,
+                                   int64_t pad, bool relu, int64_t tile, int64_t splits,
+                                   c10::optional<Tensor> residual, c10::optional<std::vector<Tensor>> bn,
+                                   double bn_eps, bool bn_fix_gamma, bool act_relu) {
   CHECK_DEV(x); CHECK_DEV(w);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "bf16 only");
   TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "x must be channels_last (N,C,H,W)");
@@ -316,27 +327,93 @@ Tensor conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::optional<Tensor> bi
   TORCH_CHECK(w.size(1) == Cin, "channel mismatch");
   TORCH_CHECK(Cin % 64 == 0, "conv_igemm requires Cin % 64 == 0");
   const int Ho = (H + 2 * (int)pad - KH) / (int)stride + 1, Wo = (W + 2 * (int)pad - KW) / (int)stride + 1;
-  const float* bp = nullptr;
+  mxr::ConvEpi ep;
+  ep.relu = relu ? 1 : 0;
   Tensor b;
   if (bias.has_value() && bias->defined()) {
     b = bias->to(at::kFloat).contiguous();
     TORCH_CHECK(b.numel() == Cout, "bias size");
-    bp = b.data_ptr<float>();
+    ep.bias = b.data_ptr<float>();
   }
   DevGuard g(x.device());
   Tensor y = at::empty({NB, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (residual.has_value() && residual->defined()) {
+    const Tensor& r = *residual;
+    TORCH_CHECK(r.scalar_type() == at::kBFloat16 && r.sizes() == y.sizes() &&
+                    r.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "residual must be a channels_last bf16 tensor shaped like the output");
+    ep.residual = reinterpret_cast<const uint16_t*>(r.data_ptr());
+  }
+  Tensor y2;
+  std::vector<Tensor> bnf;
+  if (bn.has_value()) {
+    TORCH_CHECK(bn->size() == 4, "bn = (gamma, beta, mean, var)");
+    for (const auto& t : *bn) {
+      TORCH_CHECK(t.numel() == Cout, "bn parameter size");
+      bnf.push_back(t.to(at::kFloat).contiguous());
+    }
+    y2 = at::empty_like(y, y.options(), at::MemoryFormat::ChannelsLast);
+    ep.bn_gamma = bnf[0].data_ptr<float>();
+    ep.bn_beta = bnf[1].data_ptr<float>();
+    ep.bn_mean = bnf[2].data_ptr<float>();
+    ep.bn_var = bnf[3].data_ptr<float>();
+    ep.bn_eps = (float)bn_eps;
+    ep.bn_fix_gamma = bn_fix_gamma ? 1 : 0;
+    ep.act_relu = act_relu ? 1 : 0;
+    ep.y2 = reinterpret_cast<uint16_t*>(y2.data_ptr());
+  }
   int auto_splits = 1;
   const int t = mxr::conv_igemm_plan(NB, Ho, Wo, Cin, Cout, KH, KW, (int)tile, &auto_splits);
   const int sp = splits > 0 ? (int)splits : auto_splits;
   Tensor slab;
   if (sp > 1) slab = at::empty({(int64_t)sp * NB * Ho * Wo * Cout}, x.options().dtype(at::kFloat));
   const int used = mxr::conv_igemm_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
-                                       reinterpret_cast<const uint16_t*>(w.data_ptr()), bp,
+                                       reinterpret_cast<const uint16_t*>(w.data_ptr()),
                                        reinterpret_cast<uint16_t*>(y.data_ptr()), NB, H, W, Cin, Ho, Wo, Cout, KH, KW,
-                                       (int)stride, (int)pad, relu ? 1 : 0, t, sp,
-                                       sp > 1 ? slab.data_ptr<float>() : nullptr, cur_stream());
+                                       (int)stride, (int)pad, ep, t, sp, sp > 1 ? slab.data_ptr<float>() : nullptr,
+                                       cur_stream());
   TORCH_CHECK(used > 0, "conv_igemm: unsupported shape");
-  return y;
+  if (y2.defined()) return {y, y2};
+  return {y};
+}
+
+// dgrad filter cache: table of (src, dst) filters -> device byte tensor, built once
+std::vector<int64_t> wt_flip_table_info(const std::vector<Tensor>& srcs) {
+  int64_t tiles = 0;
+  for (const auto& s : srcs) tiles += (int64_t)s.size(2) * s.size(3) * ((s.size(0) + 63) / 64) * ((s.size(1) + 63) / 64);
+  return {(int64_t)srcs.size(), tiles};
+}
+
+Tensor wt_flip_build(const std::vector<Tensor>& srcs, const std::vector<Tensor>& dsts) {
+  TORCH_CHECK(srcs.size() == dsts.size() && !srcs.empty(), "srcs/dsts mismatch");
+  std::vector<mxr::WtFlipEntry> ents(srcs.size());
+  int tiles = 0;
+  for (size_t k = 0; k < srcs.size(); ++k) {
+    const Tensor &s = srcs[k], &d = dsts[k];
+    CHECK_DEV(s); CHECK_DEV(d);
+    TORCH_CHECK(s.scalar_type() == at::kBFloat16 && d.scalar_type() == at::kBFloat16, "bf16 filters only");
+    TORCH_CHECK(s.is_contiguous(at::MemoryFormat::ChannelsLast) && d.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "filters must be channels_last");
+    const int O = (int)s.size(0), I = (int)s.size(1), KH = (int)s.size(2), KW = (int)s.size(3);
+    TORCH_CHECK(d.size(0) == I && d.size(1) == O && d.size(2) == KH && d.size(3) == KW, "dst must be (I, O, KH, KW)");
+    TORCH_CHECK(O % 8 == 0 && I % 8 == 0, "filter flip needs O % 8 == 0 and I % 8 == 0");
+    ents[k].src = reinterpret_cast<const uint16_t*>(s.data_ptr());
+    ents[k].dst = reinterpret_cast<uint16_t*>(d.data_ptr());
+    ents[k].O = O; ents[k].I = I; ents[k].KH = KH; ents[k].KW = KW;
+    ents[k].tile_begin = tiles;
+    tiles += KH * KW * ((O + 63) / 64) * ((I + 63) / 64);
+  }
+  Tensor host = at::empty({(int64_t)(ents.size() * sizeof(mxr::WtFlipEntry))}, at::TensorOptions().dtype(at::kByte));
+  std::memcpy(host.data_ptr(), ents.data(), ents.size() * sizeof(mxr::WtFlipEntry));
+  return host.to(srcs[0].device());
+}
+
+void wt_flip_run(const Tensor& table, int64_t n_entries, int64_t total_tiles) {
+  CHECK_DEV(table);
+  TORCH_CHECK((int64_t)table.numel() == n_entries * (int64_t)sizeof(mxr::WtFlipEntry), "table size");
+  DevGuard g(table.device());
+  mxr::conv_wt_flip_multi(reinterpret_cast<const mxr::WtFlipEntry*>(table.data_ptr()), (int)n_entries,
+                          (int)total_tiles, cur_stream());
 }
 
 Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
@@ -390,9 +467,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_relu_fwd", &bn_relu_fwd);
   m.def("bn_relu_bwd", &bn_relu_bwd, py::arg("x"), py::arg("dy"), py::arg("gamma"), py::arg("beta"),
         py::arg("mean"), py::arg("var"), py::arg("eps"), py::arg("fix_gamma"), py::arg("relu"), py::arg("need_dx"),
-        py::arg("need_params"), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none());
+        py::arg("need_params"), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(),
+        py::arg("dres") = py::none());
   m.def("conv_igemm_fwd", &conv_igemm_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),
-        py::arg("pad"), py::arg("relu"), py::arg("tile") = 0, py::arg("splits") = 0);
+        py::arg("pad"), py::arg("relu"), py::arg("tile") = 0, py::arg("splits") = 0, py::arg("residual") = py::none(),
+        py::arg("bn") = py::none(), py::arg("bn_eps") = 2e-5, py::arg("bn_fix_gamma") = false,
+        py::arg("act_relu") = true);
+  m.def("wt_flip_table_info", &wt_flip_table_info);
+  m.def("wt_flip_build", &wt_flip_build);
+  m.def("wt_flip_run", &wt_flip_run);
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"), py::arg("stride"),
         py::arg("pad"), py::arg("splits") = 0, py::arg("out") = py::none());
   m.attr("arch") = "gfx950";

@@ -84,7 +84,7 @@ __global__ void __launch_bounds__(256)
 bn_relu_bwd_kernel(const void* __restrict__ x, const void* __restrict__ dy, int bf16, int64_t M, int C,
                    const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ mean,
                    const float* __restrict__ var, float eps, int fix_gamma, int relu, void* __restrict__ dx,
-                   float* __restrict__ part) {
+                   const void* __restrict__ dres, float* __restrict__ part) {
   extern __shared__ __attribute__((aligned(16))) float red[];  // 2*C
   const int CV = C >> 2;
   const int64_t T = (int64_t)gridDim.x * blockDim.x;
@@ -109,7 +109,15 @@ bn_relu_bwd_kernel(const void* __restrict__ x, const void* __restrict__ dy, int 
       ag[k] += gm * (xv[k] - mu[k]) * inv[k];
       g[k] = gm * s[k];
     }
-    if (dx) store4(dx, e * 4, bf16, g);
+    if (dx) {
+      if (dres) {  // fused gradient accumulation: dx = dres + d(bn_relu)
+        float rv[4];
+        load4(dres, e * 4, bf16, rv);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) g[k] += rv[k];
+      }
+      store4(dx, e * 4, bf16, g);
+    }
   };
   int64_t e = tid;
   for (; e + 3 * T < total; e += 4 * T) {  // 8 independent loads in flight per thread
@@ -256,10 +264,11 @@ int bn_bwd_workspace_floats(int64_t M, int C) {
 }
 
 void bn_relu_bwd(const void* x, const void* dy, int bf16, int64_t M, int C, const float* gamma, const float* beta,
-                 const float* mean, const float* var, float eps, int fix_gamma, int relu, void* dx, float* dgamma,
-                 float* dbeta, float* workspace, int accumulate, hipStream_t st) {
+                 const float* mean, const float* var, float eps, int fix_gamma, int relu, void* dx, const void* dres,
+                 float* dgamma, float* dbeta, float* workspace, int accumulate, hipStream_t st) {
   if (M == 0 || C == 0) return;
   if (C % 4 != 0) {
+    if (dres) return;  // not supported on the scalar path (caller checks)
     bn_relu_bwd_scalar<<<bn_grid_scalar(M, C), 256, 2 * C * sizeof(float), st>>>(
         x, dy, bf16, M, C, gamma, beta, mean, var, eps, fix_gamma, relu, dx, dgamma, dbeta);
     return;
@@ -267,7 +276,7 @@ void bn_relu_bwd(const void* x, const void* dy, int bf16, int64_t M, int C, cons
   const int nblk = bn_grid(M, C, 320);
   float* part = (dgamma || dbeta) ? workspace : nullptr;
   bn_relu_bwd_kernel<<<nblk, 256, 2 * C * sizeof(float), st>>>(x, dy, bf16, M, C, gamma, beta, mean, var, eps,
-                                                               fix_gamma, relu, dx, part);
+                                                               fix_gamma, relu, dx, dres, part);
   if (part) bn_part_reduce<<<(2 * C + 63) / 64, 256, 0, st>>>(part, nblk, C, fix_gamma, dgamma, dbeta, accumulate);
 }
 

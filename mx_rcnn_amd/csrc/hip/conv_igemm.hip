@@ -29,12 +29,44 @@ constexpr int BK = 64;  // bf16 elements per K-step (one 128-B row per tile row)
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
+// per-output-channel epilogue constants
+struct EpiCol {
+  float bias, s, t;
+};
+
+__device__ __forceinline__ EpiCol epi_col(const ConvEpi& ep, int n) {
+  EpiCol c;
+  c.bias = ep.bias ? ep.bias[n] : 0.f;
+  c.s = 1.f;
+  c.t = 0.f;
+  if (ep.y2) {
+    const float g = ep.bn_fix_gamma ? 1.f : ep.bn_gamma[n];
+    c.s = g * rsqrtf(ep.bn_var[n] + ep.bn_eps);
+    c.t = ep.bn_beta[n] - ep.bn_mean[n] * c.s;
+  }
+  return c;
+}
+
+__device__ __forceinline__ void epi_store(const ConvEpi& ep, const EpiCol& c, uint16_t* __restrict__ y, int64_t idx,
+                                          float v) {
+  v += c.bias;
+  if (ep.residual) v += bf16_to_f32(ep.residual[idx]);
+  if (ep.relu) v = fmaxf(v, 0.f);
+  const uint16_t yb = f32_to_bf16(v);
+  y[idx] = yb;
+  if (ep.y2) {
+    // the BN reads the STORED (bf16-rounded) conv output, exactly like the unfused pair
+    float a = bf16_to_f32(yb) * c.s + c.t;
+    if (ep.act_relu) a = fmaxf(a, 0.f);
+    ep.y2[idx] = f32_to_bf16(a);
+  }
+}
+
 template <int BM, int BN>
 __global__ void __launch_bounds__(256)
-conv_igemm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, const float* __restrict__ bias,
-                      uint16_t* __restrict__ y, int NB, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW,
-                      int stride, int pad, int relu, int tiles_n, int nwg, int ntiles, int splits,
-                      float* __restrict__ slab) {
+conv_igemm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
+                      int NB, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad,
+                      const ConvEpi ep, int tiles_n, int nwg, int ntiles, int splits, float* __restrict__ slab) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int ACH = BM * 8 / 256;  // 16-B chunks of A per thread per K-step
@@ -181,26 +213,22 @@ conv_igemm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn * WN + j * 16 + (lane & 15);
     if (n >= Cout) continue;
-    const float bv = bias ? bias[n] : 0.f;
+    const EpiCol ec = epi_col(ep, n);
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
-        if (m < M) {
-          float v = acc[i][j][r] + bv;
-          if (relu) v = fmaxf(v, 0.f);
-          y[(int64_t)m * Cout + n] = f32_to_bf16(v);
-        }
+        if (m < M) epi_store(ep, ec, y, (int64_t)m * Cout + n, acc[i][j][r]);
       }
     }
   }
 }
 
-// split-K reduce: y = act(sum_s slab[s] + bias), 4 outputs per thread (Cout % 4 == 0)
+// split-K reduce + the fused epilogue, 4 outputs per thread (Cout % 4 == 0)
 __global__ void __launch_bounds__(256)
-splitk_reduce_kernel(const float* __restrict__ slab, int splits, int64_t MN, int Cout, const float* __restrict__ bias,
-                     int relu, uint16_t* __restrict__ y) {
+splitk_reduce_kernel(const float* __restrict__ slab, int splits, int64_t MN, int Cout, const ConvEpi ep,
+                     uint16_t* __restrict__ y) {
   const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
   if (e >= MN) return;
   float4 a = *reinterpret_cast<const float4*>(slab + e);
@@ -210,28 +238,39 @@ splitk_reduce_kernel(const float* __restrict__ slab, int splits, int64_t MN, int
   }
   float v[4] = {a.x, a.y, a.z, a.w};
   const int n = (int)(e % Cout);
+  float res[4] = {0.f, 0.f, 0.f, 0.f};
+  if (ep.residual) {
+    const ushort4 rv = *reinterpret_cast<const ushort4*>(ep.residual + e);
+    res[0] = bf16_to_f32(rv.x); res[1] = bf16_to_f32(rv.y); res[2] = bf16_to_f32(rv.z); res[3] = bf16_to_f32(rv.w);
+  }
+  uint16_t out[4], out2[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    if (bias) v[k] += bias[n + k];
-    if (relu) v[k] = fmaxf(v[k], 0.f);
+    const EpiCol c = epi_col(ep, n + k);
+    float t = v[k] + c.bias + res[k];
+    if (ep.relu) t = fmaxf(t, 0.f);
+    out[k] = f32_to_bf16(t);
+    float q = bf16_to_f32(out[k]) * c.s + c.t;
+    if (ep.act_relu) q = fmaxf(q, 0.f);
+    out2[k] = f32_to_bf16(q);
   }
-  *reinterpret_cast<ushort4*>(y + e) = make_ushort4(f32_to_bf16(v[0]), f32_to_bf16(v[1]), f32_to_bf16(v[2]),
-                                                    f32_to_bf16(v[3]));
+  *reinterpret_cast<ushort4*>(y + e) = make_ushort4(out[0], out[1], out[2], out[3]);
+  if (ep.y2) *reinterpret_cast<ushort4*>(ep.y2 + e) = make_ushort4(out2[0], out2[1], out2[2], out2[3]);
 }
 
 template <int BM, int BN>
-static void launch_fwd(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int NB, int H, int W,
-                       int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, int splits,
+static void launch_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho,
+                       int Wo, int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int splits,
                        float* slab, hipStream_t st) {
   const int M = NB * Ho * Wo;
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (Cout + BN - 1) / BN;
   const int ntiles = tiles_m * tiles_n;
   const int nwg = ntiles * splits;
-  conv_igemm_fwd_kernel<BM, BN><<<nwg, 256, 0, st>>>(x, w, bias, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
-                                                     pad, relu, tiles_n, nwg, ntiles, splits, slab);
+  conv_igemm_fwd_kernel<BM, BN><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep,
+                                                     tiles_n, nwg, ntiles, splits, slab);
   if (splits > 1) {
     const int64_t MN = (int64_t)M * Cout;
-    splitk_reduce_kernel<<<div_up((MN + 3) / 4, 256), 256, 0, st>>>(slab, splits, MN, Cout, bias, relu, y);
+    splitk_reduce_kernel<<<div_up((MN + 3) / 4, 256), 256, 0, st>>>(slab, splits, MN, Cout, ep, y);
   }
 }
 
@@ -254,17 +293,64 @@ int conv_igemm_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, i
   return tile;
 }
 
-int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int NB, int H, int W,
-                   int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, int tile,
-                   int splits, float* slab, hipStream_t st) {
+int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho, int Wo,
+                   int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int tile, int splits, float* slab,
+                   hipStream_t st) {
   if (Cin % BK != 0) return -1;
   if (splits > 1 && (slab == nullptr || Cout % 4 != 0)) return -1;
+  if (ep.y2 && (!ep.bn_beta || !ep.bn_mean || !ep.bn_var || (!ep.bn_fix_gamma && !ep.bn_gamma))) return -1;
   switch (tile) {
-    case 1: launch_fwd<128, 128>(x, w, bias, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, splits, slab, st); break;
-    case 2: launch_fwd<128, 64>(x, w, bias, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, splits, slab, st); break;
-    default: launch_fwd<64, 64>(x, w, bias, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu, splits, slab, st); break;
+    case 1: launch_fwd<128, 128>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    case 2: launch_fwd<128, 64>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    default: launch_fwd<64, 64>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
   }
   return tile;
+}
+
+// ---- dgrad filter cache: flip + transpose every registered filter in one launch -------------
+// One 256-thread block per (entry, tap, 64-o x 64-i tile).  The tile goes through LDS so both
+// the read (rows of i) and the write (rows of o) are 16-B vectorised and coalesced.
+__global__ void __launch_bounds__(256)
+conv_wt_flip_kernel(const WtFlipEntry* __restrict__ entries, int n_entries) {
+  __shared__ uint16_t t[64][64 + 8];
+  const int b = blockIdx.x;
+  int lo = 0, hi = n_entries - 1;  // last entry with tile_begin <= b
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (entries[mid].tile_begin <= b) lo = mid; else hi = mid - 1;
+  }
+  const WtFlipEntry e = entries[lo];
+  const int local = b - e.tile_begin;
+  const int to = (e.O + 63) / 64, ti = (e.I + 63) / 64;
+  const int tap = local / (to * ti), rem = local % (to * ti);
+  const int o0 = (rem / ti) * 64, i0 = (rem % ti) * 64;
+  const int taps = e.KH * e.KW;
+  const int ftap = taps - 1 - tap;  // (KH-1-r, KW-1-s) flattened
+  const int tid = threadIdx.x;
+  // read: src[o][tap][i], 64 rows of o x 8 chunks of 8 i
+  for (int q = tid; q < 512; q += 256) {
+    const int row = q >> 3, ch = q & 7;
+    const int o = o0 + row, i = i0 + ch * 8;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (o < e.O && i < e.I) v = *reinterpret_cast<const uint4*>(e.src + ((int64_t)o * taps + ftap) * e.I + i);
+    const uint16_t* pv = reinterpret_cast<const uint16_t*>(&v);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) t[ch * 8 + k][row] = pv[k];
+  }
+  __syncthreads();
+  // write: dst[i][tap][o], 64 rows of i x 8 chunks of 8 o
+  for (int q = tid; q < 512; q += 256) {
+    const int row = q >> 3, ch = q & 7;
+    const int i = i0 + row, o = o0 + ch * 8;
+    if (i < e.I && o < e.O)
+      *reinterpret_cast<uint4*>(e.dst + ((int64_t)i * taps + tap) * e.O + o) =
+          *reinterpret_cast<const uint4*>(&t[row][ch * 8]);
+  }
+}
+
+void conv_wt_flip_multi(const WtFlipEntry* entries, int n_entries, int total_tiles, hipStream_t st) {
+  if (n_entries <= 0 || total_tiles <= 0) return;
+  conv_wt_flip_kernel<<<total_tiles, 256, 0, st>>>(entries, n_entries);
 }
 
 }  // namespace mxr

@@ -93,7 +93,8 @@ void bn_relu_fwd(const void* x, int bf16, int64_t M, int C, const float* gamma, 
 int bn_bwd_workspace_floats(int64_t M, int C);
 void bn_relu_bwd(const void* x, const void* dy, int bf16, int64_t M, int C, const float* gamma,
                  const float* beta, const float* mean, const float* var, float eps, int fix_gamma, int relu,
-                 void* dx, float* dgamma, float* dbeta, float* workspace, int accumulate, hipStream_t st);
+                 void* dx, const void* dres, float* dgamma, float* dbeta, float* workspace, int accumulate,
+                 hipStream_t st);
 
 // ---- implicit-GEMM convolution (conv_igemm.hip) ------------------------------
 // NHWC bf16 x (NB, H, W, Cin), weight (Cout, KH, KW, Cin) bf16, bias fp32 (Cout) or null,
@@ -101,9 +102,37 @@ void bn_relu_bwd(const void* x, const void* dy, int bf16, int64_t M, int C, cons
 // conv_igemm_plan picks (tile, splits); splits > 1 needs an fp32 slab of splits*M*Cout floats.
 // Returns the tile used, or -1 if the shape is unsupported (Cin % 64 != 0).
 int conv_igemm_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int tile, int* splits_out);
-int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, const float* bias, uint16_t* y, int NB, int H, int W,
-                   int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int relu, int tile,
-                   int splits, float* slab, hipStream_t st);
+// Fused epilogue of the implicit-GEMM conv (all fields optional):
+//   v  = acc + bias[n] + residual[m][n];  if relu: v = max(v, 0);  y[m][n] = bf16(v)
+//   if y2: y2[m][n] = bf16(act(v * s[n] + t[n])) with the frozen-BN affine
+//          s = gamma * rsqrt(var + eps) (gamma := 1 when fix_gamma), t = beta - mean * s,
+//          act = ReLU when act_relu.  (Conv -> frozen BN -> ReLU of a pre-activation ResNet unit,
+//          keeping the raw conv output y for the BN backward.)
+struct ConvEpi {
+  const float* bias = nullptr;
+  const uint16_t* residual = nullptr;
+  int relu = 0;
+  const float* bn_gamma = nullptr;
+  const float* bn_beta = nullptr;
+  const float* bn_mean = nullptr;
+  const float* bn_var = nullptr;
+  float bn_eps = 2e-5f;
+  int bn_fix_gamma = 0;
+  int act_relu = 1;
+  uint16_t* y2 = nullptr;
+};
+int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho, int Wo,
+                   int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int tile, int splits, float* slab,
+                   hipStream_t st);
+// Flip + transpose many conv filters in ONE launch (dgrad operand cache):
+//   dst[i][r][s][o] = src[o][KH-1-r][KW-1-s][i]   (both channels_last, i.e. (O,KH,KW,I) rows)
+struct WtFlipEntry {
+  const uint16_t* src;
+  uint16_t* dst;
+  int O, I, KH, KW;
+  int tile_begin;  // prefix sum of 64x64 tiles (per tap) over entries
+};
+void conv_wt_flip_multi(const WtFlipEntry* entries, int n_entries, int total_tiles, hipStream_t st);
 
 // ---- MFMA weight gradient (conv_wgrad.hip) -------------------------------------
 // dy (NB, Ho, Wo, Cout) bf16, x (NB, H, W, Cin) bf16 -> dw (Cout, KH, KW, Cin) bf16.

@@ -21,6 +21,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..config import config as _global_cfg, snapshot
+from ..utils import profiler as prof
 from ..ops import anchor_target, proposal, proposal_target, roi_pool
 from ..ops.losses import rpn_softmax_ce, smooth_l1, softmax_ce
 from .layers import Conv
@@ -163,15 +164,23 @@ class FasterRCNN(nn.Module):
     def train_e2e(self, data, im_info, gt_boxes, n_gt):
         """Approximate joint training step forward.  Returns dict with 'loss' (to backward)
         and the metric tensors of the reference's six metrics (rcnn/metric.py)."""
-        feat = self.trunk(data)
-        rpn_cls, rpn_bbox = self.rpn(feat)
-        rpn_cls_loss, rpn_bbox_loss, at = self._rpn_losses(rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt)
-        rois, _ = self._proposal(rpn_cls, rpn_bbox, im_info, 'TRAIN')
-        pt = proposal_target(rois, gt_boxes, n_gt, self.num_classes, cfg=self.cfg, is_train=True)
-        pooled = roi_pool(feat, pt['rois'], (7, 7), 1.0 / self.feat_stride)
-        cls_score, bbox_pred = self.head(pooled)
-        cls_loss, bbox_loss, cls_prob = self._head_losses(cls_score, bbox_pred, pt['label'], pt['bbox_target'],
-                                                          pt['bbox_inside_weight'], pt['bbox_outside_weight'])
+        with prof.range('trunk'):
+            feat = self.trunk(data)
+        with prof.range('rpn'):
+            rpn_cls, rpn_bbox = self.rpn(feat)
+        with prof.range('anchor_target+rpn_loss'):
+            rpn_cls_loss, rpn_bbox_loss, at = self._rpn_losses(rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt)
+        with prof.range('proposal'):
+            rois, _ = self._proposal(rpn_cls, rpn_bbox, im_info, 'TRAIN')
+        with prof.range('proposal_target'):
+            pt = proposal_target(rois, gt_boxes, n_gt, self.num_classes, cfg=self.cfg, is_train=True)
+        with prof.range('roi_pool'):
+            pooled = roi_pool(feat, pt['rois'], (7, 7), 1.0 / self.feat_stride)
+        with prof.range('head'):
+            cls_score, bbox_pred = self.head(pooled)
+        with prof.range('head_loss'):
+            cls_loss, bbox_loss, cls_prob = self._head_losses(cls_score, bbox_pred, pt['label'], pt['bbox_target'],
+                                                              pt['bbox_inside_weight'], pt['bbox_outside_weight'])
         B = data.shape[0]
         R = cls_score.shape[0]
         loss = rpn_cls_loss + rpn_bbox_loss + cls_loss + bbox_loss

@@ -3,10 +3,22 @@
 RPN + RoIPool sit after the last unit of stage 3, stage 4 runs per RoI with batch-statistics
 BN (the reference's ``bn_global_`` switch), then bn1 -> relu -> global avg-pool -> cls/bbox.
 """
+import os
+
 import torch
 import torch.nn as nn
 
+from ..ops.conv import igemm_eligible
+from ..ops.fused import conv_add, conv_add_bn_relu, conv_bn_relu
 from .layers import BatchNorm, Conv, Linear, max_pool
+
+
+def fusion_enabled():
+    return os.environ.get('MXR_FUSE', '1') != '0'
+
+
+def _frozen(bn):
+    return bn.use_global_stats or not bn.training
 
 DEPTHS = {
     18: ([2, 2, 2, 2], [64, 64, 128, 256, 512], False),
@@ -48,6 +60,54 @@ class ResidualUnit(nn.Module):
         sc = x if self.dim_match else self.sc(act1)
         return y + sc
 
+    def can_fuse(self, x):
+        """Frozen BNs and MFMA-eligible convs: run the unit as fused conv+BN+ReLU(+residual) ops."""
+        if not (fusion_enabled() and _frozen(self.bn1) and _frozen(self.bn2) and
+                (not self.bottle_neck or _frozen(self.bn3))):
+            return False
+        c1 = self.conv1
+        return igemm_eligible(x, c1.weight, c1.stride, c1.pad) and c1.weight.dtype == torch.bfloat16
+
+    def forward_fused(self, x, act1=None, next_bn=None):
+        """-> (unit output, next unit's act1 or None).  act1: this unit's bn1(x) if already
+        produced by the previous unit's epilogue."""
+        if act1 is None:
+            act1 = self.bn1(x)
+        a = conv_bn_relu(act1, self.conv1, self.bn2)
+        if self.bottle_neck:
+            c2 = self.conv2
+            if igemm_eligible(a, c2.weight, c2.stride, c2.pad):
+                a = conv_bn_relu(a, c2, self.bn3)
+            else:
+                a = self.bn3(c2(a))
+            last = self.conv3
+        else:
+            last = self.conv2
+        sc = x if self.dim_match else self.sc(act1)
+        if not igemm_eligible(a, last.weight, last.stride, last.pad):
+            out = last(a) + sc
+            return out, (next_bn(out) if next_bn is not None else None)
+        if next_bn is not None and _frozen(next_bn) and next_bn.relu:
+            return conv_add_bn_relu(a, last, sc, next_bn)
+        out = conv_add(a, last, sc)
+        return out, (next_bn(out) if next_bn is not None else None)
+
+
+def run_stage(stage, x):
+    """Run a stage (nn.Sequential of ResidualUnit) through the fused path when possible, chaining
+    each unit's conv3 epilogue into the next unit's bn1."""
+    units = list(stage)
+    if not units[0].can_fuse(x):
+        return stage(x)
+    act1 = None
+    for i, u in enumerate(units):
+        nxt = units[i + 1] if i + 1 < len(units) else None
+        if act1 is None and not u.can_fuse(x):
+            x = u(x)
+            continue
+        x, act1 = u.forward_fused(x, act1, nxt.bn1 if (nxt is not None and _frozen(nxt.bn1)) else None)
+    return x
+
 
 def _stage(idx, n_units, cin, cout, bottle_neck, bn_mom, bn_global):
     units = []
@@ -88,7 +148,9 @@ class ResNetTrunk(nn.Module):
     def forward(self, x):
         x = self.bn0(self.conv0(self.bn_data(x)))
         x = max_pool(x, 3, 2, 1)
-        return self.stage3(self.stage2(self.stage1(x)))
+        for st in (self.stage1, self.stage2, self.stage3):
+            x = run_stage(st, x)
+        return x
 
     def feat_shape(self, h, w):
         h, w = (h + 6 - 7) // 2 + 1, (w + 6 - 7) // 2 + 1  # conv0

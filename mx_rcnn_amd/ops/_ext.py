@@ -28,12 +28,39 @@ def ext_available():
     return _load() is not None
 
 
+class _SyncProxy(object):
+    """RCNN_SYNC=1 (the reference's NaiveEngine debug mode): every kernel launcher
+    is followed by a device synchronisation, so an asynchronous fault is reported at the op
+    that caused it (with its name) instead of at some later API call."""
+
+    def __init__(self, ext):
+        self._ext = ext
+
+    def __getattr__(self, name):
+        fn = getattr(self._ext, name)
+        if not callable(fn):
+            return fn
+
+        def wrapped(*a, **k):
+            import torch
+            out = fn(*a, **k)
+            if torch.cuda.is_available() and not torch.cuda.is_current_stream_capturing():
+                try:
+                    torch.cuda.synchronize()
+                except Exception as e:  # pragma: no cover - only on a faulting kernel
+                    raise RuntimeError('RCNN_SYNC: kernel %s failed: %s' % (name, e)) from e
+            return out
+        return wrapped
+
+
 def need_ext():
     ext = _load()
     if ext is None:
         raise RuntimeError(
             'mx_rcnn_amd HIP extension is not built (%s). Run `python -m mx_rcnn_amd.csrc.build` '
             '(hipcc --offload-arch=gfx950) before using GPU tensors.' % _ERR)
+    if sync_debug():
+        return _SyncProxy(ext)
     return ext
 
 

@@ -32,11 +32,54 @@ def wgrad_enabled():
     return os.environ.get('MXR_CONV_WGRAD', '1') != '0'
 
 
+# dgrad operand cache: id(weight Parameter) -> flipped/transposed bf16 filter, refreshed by the
+# FlatParamStore with ONE multi-filter kernel right after each SGD update (core/params.py),
+# instead of a flip + transpose copy per conv per backward.
+_DGRAD_W = {}
+
+
+def register_dgrad_weight(param, buf):
+    _DGRAD_W[id(param)] = (param, buf)
+
+
+def dgrad_weight(param, w):
+    ent = _DGRAD_W.get(id(param)) if param is not None else None
+    if ent is not None and ent[0] is param:
+        return ent[1]
+    return _flip_t(w)
+
+
 def _flip_t(w):
     """(O, I, kh, kw) -> (I, O, kh, kw) spatially flipped, channels_last memory."""
     if w.shape[2] == 1 and w.shape[3] == 1:
         return w.transpose(0, 1).contiguous(memory_format=torch.channels_last)
     return w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
+
+
+def conv_backward(x, w, param, dy, stride, pad, has_bias, need_x, need_w, need_b):
+    """(dx, dw, db) of an NHWC bf16 conv given the gradient at its (pre-activation) output.
+    dw is None when it was accumulated straight into the parameter's flat gradient view."""
+    kh = w.shape[2]
+    dx = dw = db = None
+    if need_x:
+        if stride == 1 and w.shape[0] % 64 == 0 and 2 * pad == kh - 1:
+            dx = need_ext().conv_igemm_fwd(dy, dgrad_weight(param, w), None, 1, kh - 1 - pad, False)[0]
+        else:
+            dx = torch.ops.aten.convolution_backward(
+                dy, x, w, None, [stride] * 2, [pad] * 2, [1, 1], False, [0, 0], 1, [True, False, False])[0]
+    if need_w and wgrad_enabled() and w.shape[0] % 8 == 0:
+        tgt = grad_sink.target(param)
+        if tgt is not None and tgt.is_contiguous(memory_format=torch.channels_last):
+            need_ext().conv_wgrad(dy, x, w.shape[2], w.shape[3], stride, pad, 0, tgt)
+        else:
+            dw = need_ext().conv_wgrad(dy, x, w.shape[2], w.shape[3], stride, pad)
+        if has_bias and need_b:
+            db = dy.sum(dim=(0, 2, 3)).to(w.dtype)
+    elif need_w or (has_bias and need_b):
+        _, dw, db = torch.ops.aten.convolution_backward(
+            dy, x, w, [w.shape[0]] if has_bias else None, [stride] * 2, [pad] * 2, [1, 1], False,
+            [0, 0], 1, [False, bool(need_w), bool(has_bias and need_b)])
+    return dx, dw, db
 
 
 class _ConvIgemm(torch.autograd.Function):
@@ -45,7 +88,7 @@ class _ConvIgemm(torch.autograd.Function):
         ext = need_ext()
         x = x.contiguous(memory_format=torch.channels_last)
         wc = w.contiguous(memory_format=torch.channels_last)
-        y = ext.conv_igemm_fwd(x, wc, b, stride, pad, relu)
+        y = ext.conv_igemm_fwd(x, wc, b, stride, pad, relu)[0]
         ctx.save_for_backward(x, wc, y if relu else None)
         ctx.param = w if w.is_leaf else None
         ctx.stride, ctx.pad, ctx.relu, ctx.has_bias = stride, pad, relu, b is not None
@@ -57,29 +100,8 @@ class _ConvIgemm(torch.autograd.Function):
         dy = dy.contiguous(memory_format=torch.channels_last)
         if ctx.relu:
             dy = dy * (y > 0)
-        kh = w.shape[2]
-        dx = dw = db = None
-        if ctx.needs_input_grad[0]:
-            if ctx.stride == 1 and w.shape[0] % 64 == 0 and 2 * ctx.pad == kh - 1:
-                dx = need_ext().conv_igemm_fwd(dy, _flip_t(w), None, 1, kh - 1 - ctx.pad, False)
-            else:
-                dx = torch.ops.aten.convolution_backward(
-                    dy, x, w, None, [ctx.stride] * 2, [ctx.pad] * 2, [1, 1], False, [0, 0], 1,
-                    [True, False, False])[0]
-        need_w = ctx.needs_input_grad[1]
-        need_b = ctx.has_bias and ctx.needs_input_grad[2]
-        if need_w and wgrad_enabled() and w.shape[0] % 8 == 0:
-            tgt = grad_sink.target(ctx.param)
-            if tgt is not None and tgt.is_contiguous(memory_format=torch.channels_last):
-                need_ext().conv_wgrad(dy, x, w.shape[2], w.shape[3], ctx.stride, ctx.pad, 0, tgt)
-            else:
-                dw = need_ext().conv_wgrad(dy, x, w.shape[2], w.shape[3], ctx.stride, ctx.pad)
-            if need_b:
-                db = dy.sum(dim=(0, 2, 3)).to(w.dtype)
-        elif need_w or need_b:
-            _, dw, db = torch.ops.aten.convolution_backward(
-                dy, x, w, [w.shape[0]] if ctx.has_bias else None, [ctx.stride] * 2, [ctx.pad] * 2, [1, 1], False,
-                [0, 0], 1, [False, bool(need_w), bool(need_b)])
+        dx, dw, db = conv_backward(x, w, ctx.param, dy, ctx.stride, ctx.pad, ctx.has_bias, ctx.needs_input_grad[0],
+                                   ctx.needs_input_grad[1], ctx.needs_input_grad[2])
         return dx, dw, db, None, None, None
 
 
@@ -92,6 +114,18 @@ def conv1x1_gemm(x, w, b, stride=1):
     x2 = x.permute(0, 2, 3, 1).reshape(n * h * wd, c)
     y2 = F.linear(x2, w.reshape(w.shape[0], c), b)
     return y2.reshape(n, h, wd, w.shape[0]).permute(0, 3, 1, 2)
+
+
+def igemm_eligible(x, w, stride=1, pad=0):
+    """True when the MFMA implicit-GEMM kernel is the path conv2d would take for this conv."""
+    k = w.shape[2]
+    if not (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.shape[1] % 64 == 0 and
+            x.is_contiguous(memory_format=torch.channels_last) and igemm_enabled()):
+        return False
+    if k == 1 and pad == 0 and stride != 1:
+        return False
+    m = x.shape[0] * ((x.shape[2] + 2 * pad - k) // stride + 1) * ((x.shape[3] + 2 * pad - k) // stride + 1)
+    return not (k == 1 and m > GEMM_1X1_MIN_M)
 
 
 def conv2d(x, w, b=None, stride=1, pad=0, relu=False):

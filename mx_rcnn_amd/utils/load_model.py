@@ -116,6 +116,12 @@ def save_states(prefix, epoch, states):
     ndarray_io.save('%s-%04d.states' % (prefix, epoch), states)
 
 
+def states_file(prefix, epoch):
+    """Path of the optimizer-state sidecar if it exists, else None."""
+    path = '%s-%04d.states' % (prefix, epoch)
+    return path if os.path.exists(path) else None
+
+
 def load_states(prefix, epoch):
     path = '%s-%04d.states' % (prefix, epoch)
     return ndarray_io.load(path) if os.path.exists(path) else None

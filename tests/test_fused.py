@@ -1,0 +1,163 @@
+"""Fused conv epilogues (conv + frozen BN + ReLU + residual), the BN backward with fused
+residual gradient, the one-launch dgrad filter cache, and fused-vs-unfused ResNet units.
+Oracles: plain PyTorch fp32 ops on the same bf16 inputs (tests/test_kernels.py convention)."""
+import os
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _cl(t, dev):
+    return t.to(dev).contiguous(memory_format=torch.channels_last)
+
+
+def _bn_ref(y, gamma, beta, mean, var, eps=2e-5):
+    s = gamma * torch.rsqrt(var + eps)
+    return y * s[None, :, None, None] + (beta - mean * s)[None, :, None, None]
+
+
+@pytest.mark.parametrize('shape', [(1, 256, 24, 40, 256, 1, 1, 0), (1, 64, 31, 17, 64, 3, 1, 1),
+                                   (2, 128, 14, 14, 512, 1, 1, 0), (1, 1024, 50, 84, 256, 1, 1, 0)])
+@pytest.mark.parametrize('tile,splits', [(3, 1), (3, 4), (0, 0)])
+def test_conv_epilogue_residual_bn(cuda, shape, tile, splits):
+    from mx_rcnn_amd.ops import need_ext
+    N, Cin, H, W, Cout, k, s, p = shape
+    g = torch.Generator().manual_seed(21)
+    x = torch.randn(N, Cin, H, W, generator=g).bfloat16()
+    w = (torch.randn(Cout, Cin, k, k, generator=g) * 0.05).bfloat16()
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    res = torch.randn(N, Cout, Ho, Wo, generator=g).bfloat16()
+    gamma, beta = torch.rand(Cout, generator=g) + 0.5, torch.randn(Cout, generator=g) * 0.1
+    mean, var = torch.randn(Cout, generator=g) * 0.2, torch.rand(Cout, generator=g) + 0.5
+    y, a = need_ext().conv_igemm_fwd(_cl(x, cuda), _cl(w, cuda), None, s, p, False, tile, splits, _cl(res, cuda),
+                                     [t.to(cuda) for t in (gamma, beta, mean, var)], 2e-5, False, True)
+    ref_y = F.conv2d(x.float(), w.float(), stride=s, padding=p) + res.float()
+    ref_a = torch.relu(_bn_ref(ref_y, gamma, beta, mean, var))
+    for out, ref in ((y, ref_y), (a, ref_a)):
+        err = (out.float().cpu() - ref).abs().max().item()
+        assert err <= 1.5e-2 * ref.abs().max().item() + 1e-2, err
+    # y2 is computed from the STORED bf16 y: exactly the unfused BN of y
+    a2 = need_ext().bn_relu_fwd(y, gamma.to(cuda), beta.to(cuda), mean.to(cuda), var.to(cuda), 2e-5, False, True)
+    assert (a2.float() - a.float()).abs().max().item() <= 1e-2
+
+
+def test_bn_relu_bwd_dres(cuda):
+    from mx_rcnn_amd.ops import need_ext
+    g = torch.Generator().manual_seed(22)
+    C = 256
+    x = torch.randn(1, C, 20, 30, generator=g).bfloat16()
+    dy = torch.randn(1, C, 20, 30, generator=g).bfloat16()
+    dres = torch.randn(1, C, 20, 30, generator=g).bfloat16()
+    gamma, beta = torch.rand(C, generator=g) + 0.5, torch.randn(C, generator=g) * 0.1
+    mean, var = torch.randn(C, generator=g) * 0.2, torch.rand(C, generator=g) + 0.5
+    args = [t.to(cuda) for t in (gamma, beta, mean, var)]
+    dx0, dg0, db0 = need_ext().bn_relu_bwd(_cl(x, cuda), _cl(dy, cuda), *args, 2e-5, False, True, True, True)
+    dx1, dg1, db1 = need_ext().bn_relu_bwd(_cl(x, cuda), _cl(dy, cuda), *args, 2e-5, False, True, True, True,
+                                           None, None, _cl(dres, cuda))
+    ref = dx0.float() + dres.to(cuda).float()
+    assert (dx1.float() - ref).abs().max().item() <= 2e-2 * ref.abs().max().item()
+    assert torch.allclose(dg0, dg1) and torch.allclose(db0, db1)
+
+
+def test_wt_flip_cache(cuda):
+    from mx_rcnn_amd.ops import need_ext
+    from mx_rcnn_amd.ops.conv import _flip_t
+    g = torch.Generator().manual_seed(23)
+    shapes = [(256, 64, 3, 3), (64, 256, 1, 1), (1024, 256, 1, 1), (512, 512, 3, 3), (72, 136, 3, 3)]
+    srcs = [_cl(torch.randn(*s, generator=g).bfloat16(), cuda) for s in shapes]
+    dsts = [torch.empty((s[1], s[0], s[2], s[3]), dtype=torch.bfloat16, device=cuda,
+                        memory_format=torch.channels_last) for s in shapes]
+    ext = need_ext()
+    n, tiles = ext.wt_flip_table_info(srcs)
+    table = ext.wt_flip_build(srcs, dsts)
+    ext.wt_flip_run(table, n, tiles)
+    for s_, d_ in zip(srcs, dsts):
+        assert torch.equal(d_, _flip_t(s_))
+
+
+def _unit(cin, cout, stride, dim_match, dev):
+    from mx_rcnn_amd.models.resnet import ResidualUnit
+    torch.manual_seed(5)
+    u = ResidualUnit('u', cin, cout, stride, dim_match, True, 0.99, True)
+    with torch.no_grad():
+        for m in u.modules():
+            if hasattr(m, 'moving_var'):
+                m.moving_mean.normal_(0, 0.2)
+                m.moving_var.uniform_(0.5, 1.5)
+                m.gamma.uniform_(0.5, 1.5)
+                m.beta.normal_(0, 0.1)
+            elif hasattr(m, 'weight') and m.weight is not None:
+                m.weight.normal_(0, 0.05)
+    u = u.to(dev)
+    for m in u.modules():
+        if hasattr(m, 'weight') and m.weight is not None and m.weight.dim() == 4:
+            m.weight = torch.nn.Parameter(m.weight.detach().bfloat16().contiguous(memory_format=torch.channels_last))
+    return u
+
+
+@pytest.mark.parametrize('cfg', [(1024, 1024, 1, True), (512, 1024, 2, False), (256, 256, 1, True)])
+def test_fused_unit_matches_unfused(cuda, cfg):
+    from mx_rcnn_amd.models.resnet import ResidualUnit  # noqa: F401
+    cin, cout, stride, dim_match = cfg
+    H, W = (24, 40) if stride == 1 else (48, 80)
+    u = _unit(cin, cout, stride, dim_match, cuda)
+    nxt = _unit(cout, cout, 1, True, cuda).bn1
+    g = torch.Generator().manual_seed(6)
+    x0 = torch.randn(1, cin, H, W, generator=g).bfloat16()
+    results = []
+    for fused in (False, True):
+        x = _cl(x0, cuda).requires_grad_()
+        if fused:
+            assert u.can_fuse(x)
+            out, act = u.forward_fused(x, None, nxt)
+        else:
+            out = u(x)
+            act = nxt(out)
+        gen = torch.Generator().manual_seed(7)
+        d_out = torch.randn(out.shape, generator=gen).bfloat16().to(cuda)
+        d_act = torch.randn(act.shape, generator=gen).bfloat16().to(cuda)
+        for p_ in u.parameters():
+            p_.grad = None
+        torch.autograd.backward([out, act], [d_out, d_act])
+        grads = {n: p_.grad.detach().float().clone() for n, p_ in u.named_parameters() if p_.grad is not None}
+        results.append((out.detach().float(), act.detach().float(), x.grad.detach().float(), grads))
+    (o0, a0, x0g, g0), (o1, a1, x1g, g1) = results
+    for t0, t1 in ((o0, o1), (a0, a1), (x0g, x1g)):
+        assert (t0 - t1).abs().max().item() <= 2e-2 * t0.abs().max().item() + 1e-3
+    assert set(g0) == set(g1)
+    for n in g0:
+        err = (g0[n] - g1[n]).abs().max().item()
+        assert err <= 3e-2 * g0[n].abs().max().item() + 1e-3, (n, err)
+
+
+def test_fused_trunk_step_matches_unfused(cuda):
+    """One full e2e step on a small ResNet-50: fused and unfused trunks give the same losses."""
+    from mx_rcnn_amd.config import snapshot
+    from mx_rcnn_amd.core.trainer import Trainer
+    from mx_rcnn_amd.models import FasterRCNN
+    import bench
+    cfg = snapshot()
+    cfg.TRAIN.BG_THRESH_LO = 0.0
+    cfg.END2END = 1
+    cfg.TRAIN.BBOX_NORMALIZATION_PRECOMPUTED = True
+    losses = []
+    for fuse in ('0', '1'):
+        os.environ['MXR_FUSE'] = fuse
+        try:
+            torch.manual_seed(0)
+            m = FasterRCNN('resnet50', 21, cfg=cfg)
+            gen = torch.Generator().manual_seed(1)
+            batch = bench.synthetic_batch(1, 320, 480, 21, cuda, gen)
+            m.to(cuda).calibrate_bn(batch['data'])
+            t = Trainer(m, 'e2e', fixed_param_prefix=['conv0', 'stage1', 'bn_data', 'bn0'], lr=0.001, device=cuda)
+            torch.manual_seed(3)
+            torch.cuda.manual_seed(3)
+            out = [t.step(batch) for _ in range(2)]
+            losses.append([float(o['rpn_cls_loss']) for o in out] + [float(o['cls_loss']) for o in out])
+        finally:
+            os.environ.pop('MXR_FUSE', None)
+    for a, b in zip(*losses):
+        assert abs(a - b) <= 2e-2 * abs(a) + 1e-3, losses

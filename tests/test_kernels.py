@@ -274,7 +274,7 @@ def test_conv_igemm_fwd_vs_fp32(cuda, shape):
     for tile, splits in ((1, 1), (2, 1), (3, 1), (3, 2), (3, 4), (0, 0)):
         y = need_ext().conv_igemm_fwd(x.to(cuda).contiguous(memory_format=torch.channels_last),
                                       w.to(cuda).contiguous(memory_format=torch.channels_last),
-                                      None if b is None else b.to(cuda), s, p, relu, tile, splits)
+                                      None if b is None else b.to(cuda), s, p, relu, tile, splits)[0]
         err = (y.float().cpu() - ref).abs().max().item()
         scale = ref.abs().max().item()
         assert err <= 1e-2 * scale + 1e-2, (tile, splits, err, scale)

@@ -49,7 +49,7 @@ def main():
         fl = 2 * y.numel() * cin * k * k
         r = {'name': name}
         r['fwd_miopen'] = t_ms(lambda: F.conv2d(x, wt, stride=s, padding=p))
-        r['fwd_ours'] = t_ms(lambda: ext.conv_igemm_fwd(x, wt, None, s, p, False))
+        r['fwd_ours'] = t_ms(lambda: ext.conv_igemm_fwd(x, wt, None, s, p, False)[0])
         if k == 1 and s == 1:
             x2 = x.permute(0, 2, 3, 1).reshape(-1, cin)
             r['fwd_gemm'] = t_ms(lambda: F.linear(x2, wt.reshape(cout, cin)))
@@ -64,7 +64,7 @@ def main():
             dy, x, wt, None, [s, s], [p, p], [1, 1], False, [0, 0], 1, [True, False, False]))
         if s == 1 and cout % 64 == 0:
             wf = wt.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
-            r['dgrad_ours'] = t_ms(lambda: ext.conv_igemm_fwd(dy, wf, None, 1, k - 1 - p, False))
+            r['dgrad_ours'] = t_ms(lambda: ext.conv_igemm_fwd(dy, wf, None, 1, k - 1 - p, False)[0])
         for kk in list(r):
             if kk != 'name':
                 r[kk] = round(r[kk] * 1000, 1)  # us

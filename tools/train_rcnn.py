@@ -46,6 +46,7 @@ def train_rcnn(image_set, year, root_path, devkit_path, pretrained, epoch, prefi
     fam = launch.family(network)
     fixed = (['conv1', 'conv2', 'conv3', 'conv4', 'conv5'] if config.TRAIN.FINETUNE else ['conv1', 'conv2']) \
         if fam == 'vgg' else launch.FIXED_PREFIX['resnet']
+    launch.calibrate_if_random(model, train_data, arg)
     mod = MutableModule(model, ['data', 'rois'], ['label', 'bbox_target', 'bbox_inside_weight',
                                                   'bbox_outside_weight'], context=ctx, fixed_param_prefix=fixed,
                         mode='rcnn', use_graph=use_graph)

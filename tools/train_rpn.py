@@ -44,6 +44,7 @@ def train_rpn(image_set, year, root_path, devkit_path, pretrained, epoch, prefix
     fam = launch.family(network)
     fixed = (['conv1', 'conv2', 'conv3', 'conv4', 'conv5'] if config.TRAIN.FINETUNE else ['conv1', 'conv2']) \
         if fam == 'vgg' else launch.FIXED_PREFIX['resnet']
+    launch.calibrate_if_random(model, train_data, arg)
     mod = MutableModule(model, ['data', 'im_info'], ['gt_boxes'], context=ctx, fixed_param_prefix=fixed,
                         mode='rpn', use_graph=use_graph)
     mod.fit(train_data, eval_metric=rpn_metrics(), epoch_end_callback=do_checkpoint(prefix),

@@ -16,7 +16,8 @@ from mx_rcnn_amd.core.module import MutableModule
 from mx_rcnn_amd.data.load_data import load_gt_roidb
 from mx_rcnn_amd.data.loader import AnchorLoader
 from mx_rcnn_amd.parallel import dist as pdist
-from mx_rcnn_amd.utils.load_model import do_checkpoint
+from mx_rcnn_amd.utils.load_model import do_checkpoint, states_file
+from mx_rcnn_amd.utils.monitor import Monitor
 
 
 def end2end_train(args):
@@ -37,14 +38,17 @@ def end2end_train(args):
     train_data = AnchorLoader(model, roidb, batch_size=args.ims_per_gpu, shuffle=True, mode='train',
                               anchor_scales=scales, rank=rank, world_size=world, seed=args.seed,
                               need_mean=fam == 'vgg')
+    launch.calibrate_if_random(model, train_data, arg_params)
     mod = MutableModule(model, data_names=['data', 'im_info'], label_names=['gt_boxes'], context=device,
                         fixed_param_prefix=launch.FIXED_PREFIX[fam], mode='e2e', use_graph=not args.eager)
-    mod.fit(train_data, eval_metric=e2e_metrics(), epoch_end_callback=do_checkpoint(args.prefix),
+    monitor = Monitor(100) if args.monitor else None
+    mod.fit(train_data, eval_metric=e2e_metrics(), epoch_end_callback=do_checkpoint(args.prefix), monitor=monitor,
             batch_end_callback=Speedometer(args.ims_per_gpu * world, frequent=args.frequent),
             kvstore=args.kv_store, optimizer='sgd',
             optimizer_params=launch.optimizer_params(args.lr, args.mom, args.wd, args.factor_step, args.resume),
             arg_params=arg_params, aux_params=aux_params, begin_epoch=args.load_epoch, num_epoch=args.num_epoch,
-            max_steps=args.max_steps)
+            max_steps=args.max_steps, states_prefix=args.prefix,
+            resume_states=states_file(args.pretrained, args.load_epoch) if args.resume else None)
     pdist.destroy()
     return mod
 

@@ -47,6 +47,7 @@ def main(args, default_network=DEFAULT_NETWORK):
     train_data = AnchorLoader(model, roidb, batch_size=args.ims_per_gpu, shuffle=not args.no_shuffle,
                               anchor_scales=model.anchor_scales, rank=rank, world_size=world, seed=args.seed,
                               need_mean=args.need_mean, max_gt=1200)
+    launch.calibrate_if_random(model, train_data, arg_params)
     mod = MutableModule(model, data_names=['data', 'im_info'], label_names=['gt_boxes'], context=device,
                         fixed_param_prefix=launch.FIXED_PREFIX[fam] if fam == 'resnet' else
                         ['conv1', 'conv2', 'conv3'], mode='e2e', use_graph=not args.eager)

@@ -86,6 +86,11 @@ class Detector(object):
         nms_thresh = config.TEST.NMS if nms_thresh is None else nms_thresh
         r, scores, deltas = self.forward(im_array, im_info, rois)
         info = torch.as_tensor(np.asarray(im_info) if not torch.is_tensor(im_info) else im_info).float().to(self.ctx)
+        return self.postprocess(r, scores, deltas, info, nms_thresh, thresh, max_per_image)
+
+    @torch.no_grad()
+    def postprocess(self, r, scores, deltas, info, nms_thresh=0.3, thresh=0.05, max_per_image=100):
+        """Device-side test post-process of ``model.detect`` outputs (see detect_batch)."""
         B = info.shape[0]
         C = scores.shape[1]
         out = []

@@ -317,7 +317,9 @@ std::vector<Tensor> bn_relu_bwd(const Tensor& x, const Tensor& dy, const Tensor&
 std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::optional<Tensor> bias, int64_t stride,
                                    int64_t pad, bool relu, int64_t tile, int64_t splits,
                                    c10::optional<Tensor> residual, c10::optional<std::vector<Tensor>> bn,
-                                   double bn_eps, bool bn_fix_gamma, bool act_relu) {
+                                   double bn_eps, bool bn_fix_gamma, bool act_relu, c10::optional<Tensor> bnb_x,
+                                   c10::optional<Tensor> dadd, c10::optional<Tensor> dgamma_out,
+                                   c10::optional<Tensor> dbeta_out) {
   CHECK_DEV(x); CHECK_DEV(w);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "bf16 only");
   TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "x must be channels_last (N,C,H,W)");
@@ -352,7 +354,6 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
       TORCH_CHECK(t.numel() == Cout, "bn parameter size");
       bnf.push_back(t.to(at::kFloat).contiguous());
     }
-    y2 = at::empty_like(y, y.options(), at::MemoryFormat::ChannelsLast);
     ep.bn_gamma = bnf[0].data_ptr<float>();
     ep.bn_beta = bnf[1].data_ptr<float>();
     ep.bn_mean = bnf[2].data_ptr<float>();
@@ -360,6 +361,34 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
     ep.bn_eps = (float)bn_eps;
     ep.bn_fix_gamma = bn_fix_gamma ? 1 : 0;
     ep.act_relu = act_relu ? 1 : 0;
+  }
+  const bool bwd_mode = bnb_x.has_value() && bnb_x->defined();
+  Tensor dgm, dbt;
+  if (bwd_mode) {
+    TORCH_CHECK(bn.has_value(), "bnb_x needs bn = (gamma, beta, mean, var)");
+    const Tensor& bx = *bnb_x;
+    TORCH_CHECK(bx.scalar_type() == at::kBFloat16 && bx.sizes() == y.sizes() &&
+                    bx.is_contiguous(at::MemoryFormat::ChannelsLast), "bnb_x must be channels_last bf16 like y");
+    ep.bnb_x = reinterpret_cast<const uint16_t*>(bx.data_ptr());
+    if (dadd.has_value() && dadd->defined()) {
+      TORCH_CHECK(dadd->scalar_type() == at::kBFloat16 && dadd->sizes() == y.sizes() &&
+                      dadd->is_contiguous(at::MemoryFormat::ChannelsLast), "dadd must be channels_last bf16 like y");
+      ep.dadd = reinterpret_cast<const uint16_t*>(dadd->data_ptr());
+    }
+    if (dgamma_out.has_value() && dgamma_out->defined()) {
+      dgm = *dgamma_out;
+      dbt = *dbeta_out;
+      TORCH_CHECK(dgm.scalar_type() == at::kFloat && dbt.scalar_type() == at::kFloat && dgm.is_contiguous() &&
+                      dbt.is_contiguous() && dgm.numel() == Cout && dbt.numel() == Cout,
+                  "dgamma_out/dbeta_out must be contiguous fp32 (C,)");
+    } else {
+      dgm = at::zeros({Cout}, x.options().dtype(at::kFloat));
+      dbt = at::zeros({Cout}, x.options().dtype(at::kFloat));
+    }
+    ep.bnb_dgamma = dgm.data_ptr<float>();
+    ep.bnb_dbeta = dbt.data_ptr<float>();
+  } else if (bn.has_value()) {
+    y2 = at::empty_like(y, y.options(), at::MemoryFormat::ChannelsLast);
     ep.y2 = reinterpret_cast<uint16_t*>(y2.data_ptr());
   }
   int auto_splits = 1;
@@ -373,8 +402,61 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
                                        (int)stride, (int)pad, ep, t, sp, sp > 1 ? slab.data_ptr<float>() : nullptr,
                                        cur_stream());
   TORCH_CHECK(used > 0, "conv_igemm: unsupported shape");
+  if (bwd_mode) return {y, dgm, dbt};
   if (y2.defined()) return {y, y2};
   return {y};
+}
+
+// ---- training-mode BN ----------------------------------------------------------------------
+std::vector<Tensor> bn_train_fwd(const Tensor& x, const Tensor& gamma, const Tensor& beta, Tensor rmean, Tensor rvar,
+                                 double momentum, double eps, bool fix_gamma, bool relu) {
+  CHECK_DEV(x);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "x: bf16 NHWC");
+  const int C = (int)x.size(1);
+  TORCH_CHECK(C % 8 == 0, "bn_train needs C % 8 == 0");
+  CHECK_F32(rmean); CHECK_F32(rvar); CHECK_CONTIG(rmean); CHECK_CONTIG(rvar);
+  DevGuard g(x.device());
+  Tensor gf = gamma.to(at::kFloat).contiguous(), bf = beta.to(at::kFloat).contiguous();
+  Tensor y = at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast);
+  Tensor sm = at::empty({C}, x.options().dtype(at::kFloat)), si = at::empty({C}, x.options().dtype(at::kFloat));
+  const int r = mxr::bn_train_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), x.numel() / C, C,
+                                  gf.data_ptr<float>(), bf.data_ptr<float>(), rmean.data_ptr<float>(),
+                                  rvar.data_ptr<float>(), (float)momentum, (float)eps, fix_gamma ? 1 : 0, relu ? 1 : 0,
+                                  reinterpret_cast<uint16_t*>(y.data_ptr()), sm.data_ptr<float>(), si.data_ptr<float>(),
+                                  cur_stream());
+  TORCH_CHECK(r == 0, "bn_train_fwd: unsupported shape");
+  return {y, sm, si};
+}
+
+std::vector<Tensor> bn_train_bwd(const Tensor& x, const Tensor& dy, const Tensor& gamma, const Tensor& beta,
+                                 const Tensor& save_mean, const Tensor& save_invstd, bool fix_gamma, bool relu,
+                                 bool need_dx, c10::optional<Tensor> dgamma_out, c10::optional<Tensor> dbeta_out) {
+  CHECK_DEV(x); CHECK_DEV(dy);
+  const int C = (int)x.size(1);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "x: bf16 NHWC");
+  Tensor g = dy.to(at::kBFloat16).contiguous(at::MemoryFormat::ChannelsLast);
+  DevGuard dg(x.device());
+  Tensor gf = gamma.to(at::kFloat).contiguous(), bf = beta.to(at::kFloat).contiguous();
+  Tensor dx = need_dx ? at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast) : Tensor();
+  const bool acc = dgamma_out.has_value() && dgamma_out->defined() && dbeta_out.has_value() && dbeta_out->defined();
+  Tensor dgm, dbt;
+  if (acc) {
+    dgm = *dgamma_out;
+    dbt = *dbeta_out;
+    TORCH_CHECK(dgm.scalar_type() == at::kFloat && dbt.scalar_type() == at::kFloat && dgm.is_contiguous() &&
+                    dbt.is_contiguous() && dgm.numel() == C && dbt.numel() == C, "dgamma/dbeta out: fp32 (C,)");
+  } else {
+    dgm = at::zeros({C}, x.options().dtype(at::kFloat));
+    dbt = at::zeros({C}, x.options().dtype(at::kFloat));
+  }
+  const int r = mxr::bn_train_bwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                  reinterpret_cast<const uint16_t*>(g.data_ptr()), x.numel() / C, C,
+                                  gf.data_ptr<float>(), bf.data_ptr<float>(), save_mean.data_ptr<float>(),
+                                  save_invstd.data_ptr<float>(), fix_gamma ? 1 : 0, relu ? 1 : 0,
+                                  need_dx ? reinterpret_cast<uint16_t*>(dx.data_ptr()) : nullptr,
+                                  dgm.data_ptr<float>(), dbt.data_ptr<float>(), acc ? 1 : 0, cur_stream());
+  TORCH_CHECK(r == 0, "bn_train_bwd: unsupported shape");
+  return {dx, dgm, dbt};
 }
 
 // dgrad filter cache: table of (src, dst) filters -> device byte tensor, built once
@@ -472,7 +554,12 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_igemm_fwd", &conv_igemm_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),
         py::arg("pad"), py::arg("relu"), py::arg("tile") = 0, py::arg("splits") = 0, py::arg("residual") = py::none(),
         py::arg("bn") = py::none(), py::arg("bn_eps") = 2e-5, py::arg("bn_fix_gamma") = false,
-        py::arg("act_relu") = true);
+        py::arg("act_relu") = true, py::arg("bnb_x") = py::none(), py::arg("dadd") = py::none(),
+        py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none());
+  m.def("bn_train_fwd", &bn_train_fwd);
+  m.def("bn_train_bwd", &bn_train_bwd, py::arg("x"), py::arg("dy"), py::arg("gamma"), py::arg("beta"),
+        py::arg("save_mean"), py::arg("save_invstd"), py::arg("fix_gamma"), py::arg("relu"), py::arg("need_dx"),
+        py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none());
   m.def("wt_flip_table_info", &wt_flip_table_info);
   m.def("wt_flip_build", &wt_flip_build);
   m.def("wt_flip_run", &wt_flip_run);

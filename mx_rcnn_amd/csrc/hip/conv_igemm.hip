@@ -31,7 +31,7 @@ __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >>
 
 // per-output-channel epilogue constants
 struct EpiCol {
-  float bias, s, t;
+  float bias, s, t, mean, inv;
 };
 
 __device__ __forceinline__ EpiCol epi_col(const ConvEpi& ep, int n) {
@@ -39,10 +39,14 @@ __device__ __forceinline__ EpiCol epi_col(const ConvEpi& ep, int n) {
   c.bias = ep.bias ? ep.bias[n] : 0.f;
   c.s = 1.f;
   c.t = 0.f;
-  if (ep.y2) {
+  c.mean = 0.f;
+  c.inv = 1.f;
+  if (ep.y2 || ep.bnb_x) {
     const float g = ep.bn_fix_gamma ? 1.f : ep.bn_gamma[n];
-    c.s = g * rsqrtf(ep.bn_var[n] + ep.bn_eps);
-    c.t = ep.bn_beta[n] - ep.bn_mean[n] * c.s;
+    c.inv = rsqrtf(ep.bn_var[n] + ep.bn_eps);
+    c.mean = ep.bn_mean[n];
+    c.s = g * c.inv;
+    c.t = ep.bn_beta[n] - c.mean * c.s;
   }
   return c;
 }
@@ -60,6 +64,19 @@ __device__ __forceinline__ void epi_store(const ConvEpi& ep, const EpiCol& c, ui
     if (ep.act_relu) a = fmaxf(a, 0.f);
     ep.y2[idx] = f32_to_bf16(a);
   }
+}
+
+// BN-backward epilogue of one element; returns (g, g * xhat) through sg / sgx
+__device__ __forceinline__ void epi_bnb(const ConvEpi& ep, const EpiCol& c, uint16_t* __restrict__ y, int64_t idx,
+                                        float v, float& sg, float& sgx) {
+  if (ep.dadd) v += bf16_to_f32(ep.dadd[idx]);
+  const float xv = bf16_to_f32(ep.bnb_x[idx]);
+  const float g = (!ep.act_relu || xv * c.s + c.t > 0.f) ? v : 0.f;
+  sg += g;
+  sgx += g * (xv - c.mean) * c.inv;
+  float o = g * c.s;
+  if (ep.residual) o += bf16_to_f32(ep.residual[idx]);
+  y[idx] = f32_to_bf16(o);
 }
 
 template <int BM, int BN>
@@ -209,6 +226,34 @@ conv_igemm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
     }
     return;
   }
+  if (ep.bnb_x) {
+    // BN-backward epilogue: per-column sums over this wave's rows, reduced across the four
+    // 16-lane row groups, then one fp32 atomic per (wave, column, stat)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WN + j * 16 + (lane & 15);
+      float sg = 0.f, sgx = 0.f;
+      if (n < Cout) {
+        const EpiCol ec = epi_col(ep, n);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+            if (m < M) epi_bnb(ep, ec, y, (int64_t)m * Cout + n, acc[i][j][r], sg, sgx);
+          }
+      }
+      sg += __shfl_xor(sg, 16, 64);
+      sg += __shfl_xor(sg, 32, 64);
+      sgx += __shfl_xor(sgx, 16, 64);
+      sgx += __shfl_xor(sgx, 32, 64);
+      if (lane < 16 && n < Cout) {
+        if (ep.bnb_dbeta) atomicAdd(ep.bnb_dbeta + n, sg);
+        if (ep.bnb_dgamma && !ep.bn_fix_gamma) atomicAdd(ep.bnb_dgamma + n, sgx);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int n = n0 + wn * WN + j * 16 + (lane & 15);
@@ -221,6 +266,52 @@ conv_igemm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
         const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
         if (m < M) epi_store(ep, ec, y, (int64_t)m * Cout + n, acc[i][j][r]);
       }
+    }
+  }
+}
+
+// split-K reduce for the BN-backward epilogue: column-blocked so the per-column statistics are
+// accumulated in registers over 256 rows and leave the block with one atomic per column.
+// Block = 16 column quads (64 columns) x 16 row lanes; grid = (Cout/64) x ceil(M/256).
+__global__ void __launch_bounds__(256)
+splitk_reduce_bnb_kernel(const float* __restrict__ slab, int splits, int M, int Cout, const ConvEpi ep,
+                         uint16_t* __restrict__ y) {
+  __shared__ float red[2][16][64];
+  const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
+  const int n = blockIdx.x * 64 + cq * 4;
+  const int r0 = blockIdx.y * 256;
+  const int64_t MN = (int64_t)M * Cout;
+  float sg[4] = {0.f, 0.f, 0.f, 0.f}, sgx[4] = {0.f, 0.f, 0.f, 0.f};
+  EpiCol ec[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) ec[k] = epi_col(ep, min(n + k, Cout - 1));
+  if (n < Cout) {
+    for (int r = r0 + rl; r < min(M, r0 + 256); r += 16) {
+      const int64_t e = (int64_t)r * Cout + n;
+      float4 a = *reinterpret_cast<const float4*>(slab + e);
+      for (int sidx = 1; sidx < splits; ++sidx) {
+        const float4 b = *reinterpret_cast<const float4*>(slab + (int64_t)sidx * MN + e);
+        a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+      }
+      const float v[4] = {a.x, a.y, a.z, a.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) epi_bnb(ep, ec[k], y, e + k, v[k], sg[k], sgx[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    red[0][rl][cq * 4 + k] = sg[k];
+    red[1][rl][cq * 4 + k] = sgx[k];
+  }
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    const int stat = threadIdx.x >> 6, col = threadIdx.x & 63;
+    float t = 0.f;
+    for (int q = 0; q < 16; ++q) t += red[stat][q][col];
+    const int nc = blockIdx.x * 64 + col;
+    if (nc < Cout) {
+      if (stat == 0 && ep.bnb_dbeta) atomicAdd(ep.bnb_dbeta + nc, t);
+      if (stat == 1 && ep.bnb_dgamma && !ep.bn_fix_gamma) atomicAdd(ep.bnb_dgamma + nc, t);
     }
   }
 }
@@ -270,7 +361,10 @@ static void launch_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB
                                                      tiles_n, nwg, ntiles, splits, slab);
   if (splits > 1) {
     const int64_t MN = (int64_t)M * Cout;
-    splitk_reduce_kernel<<<div_up((MN + 3) / 4, 256), 256, 0, st>>>(slab, splits, MN, Cout, ep, y);
+    if (ep.bnb_x)
+      splitk_reduce_bnb_kernel<<<dim3(div_up(Cout, 64), div_up(M, 256)), 256, 0, st>>>(slab, splits, M, Cout, ep, y);
+    else
+      splitk_reduce_kernel<<<div_up((MN + 3) / 4, 256), 256, 0, st>>>(slab, splits, MN, Cout, ep, y);
   }
 }
 
@@ -298,7 +392,9 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
                    hipStream_t st) {
   if (Cin % BK != 0) return -1;
   if (splits > 1 && (slab == nullptr || Cout % 4 != 0)) return -1;
-  if (ep.y2 && (!ep.bn_beta || !ep.bn_mean || !ep.bn_var || (!ep.bn_fix_gamma && !ep.bn_gamma))) return -1;
+  if ((ep.y2 || ep.bnb_x) && (!ep.bn_beta || !ep.bn_mean || !ep.bn_var || (!ep.bn_fix_gamma && !ep.bn_gamma)))
+    return -1;
+  if (ep.y2 && ep.bnb_x) return -1;
   switch (tile) {
     case 1: launch_fwd<128, 128>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 2: launch_fwd<128, 64>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;

@@ -120,10 +120,28 @@ struct ConvEpi {
   int bn_fix_gamma = 0;
   int act_relu = 1;
   uint16_t* y2 = nullptr;
+  // BN-ReLU BACKWARD mode (the conv is a dgrad producing d(act) of a frozen BN + ReLU whose
+  // input was bnb_x): v = acc + dadd; g = v * [bn(bnb_x) > 0]; y = g * s + residual;
+  // dgamma += sum_rows g * xhat, dbeta += sum_rows g (fp32 atomics; may be null).
+  const uint16_t* bnb_x = nullptr;
+  const uint16_t* dadd = nullptr;
+  float* bnb_dgamma = nullptr;
+  float* bnb_dbeta = nullptr;
 };
 int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho, int Wo,
                    int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int tile, int splits, float* slab,
                    hipStream_t st);
+// ---- training-mode BatchNorm (bn_train.hip) -----------------------------------------------
+// x/y/dy/dx NHWC bf16 (M rows x C), C % 8 == 0.  fwd updates the running stats in place
+// (moving = momentum * moving + (1 - momentum) * batch, unbiased var) and saves mean / invstd.
+int bn_train_fwd(const uint16_t* x, int64_t M, int C, const float* gamma, const float* beta, float* rmean,
+                 float* rvar, float momentum, float eps, int fix_gamma, int relu, uint16_t* y, float* save_mean,
+                 float* save_invstd, hipStream_t st);
+// dgamma/dbeta: written (accumulate = 0) or added to (accumulate = 1); may be null.
+int bn_train_bwd(const uint16_t* x, const uint16_t* dy, int64_t M, int C, const float* gamma, const float* beta,
+                 const float* save_mean, const float* save_invstd, int fix_gamma, int relu, uint16_t* dx,
+                 float* dgamma, float* dbeta, int accumulate, hipStream_t st);
+
 // Flip + transpose many conv filters in ONE launch (dgrad operand cache):
 //   dst[i][r][s][o] = src[o][KH-1-r][KW-1-s][i]   (both channels_last, i.e. (O,KH,KW,I) rows)
 struct WtFlipEntry {

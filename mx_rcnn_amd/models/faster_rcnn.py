@@ -196,8 +196,8 @@ class FasterRCNN(nn.Module):
         feat = self.trunk(data)
         rpn_cls, rpn_bbox = self.rpn(feat)
         cls_loss, bbox_loss, at = self._rpn_losses(rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt)
-        return {'loss': cls_loss + bbox_loss, 'objective': (cls_loss + bbox_loss).detach(), 'rpn_cls_loss': cls_loss, 'rpn_bbox_loss': bbox_loss,
-                'rpn_cls_score': rpn_cls, 'rpn_label': at['label'], 'num_images': data.shape[0]}
+        return {'loss': cls_loss + bbox_loss, 'objective': (cls_loss + bbox_loss).detach(),
+                'rpn_cls_loss': cls_loss, 'rpn_bbox_loss': bbox_loss, 'rpn_cls_score': rpn_cls, 'rpn_label': at['label'], 'num_images': data.shape[0]}
 
     def train_rcnn(self, data, rois, label, bbox_target, inside, outside):
         feat = self.trunk(data)
@@ -206,7 +206,8 @@ class FasterRCNN(nn.Module):
         cls_loss, bbox_loss, cls_prob = self._head_losses(cls_score, bbox_pred, label, bbox_target, inside, outside,
                                                           e2e=False)
         return {'loss': cls_loss + bbox_loss,
-                'objective': ((cls_loss + bbox_loss) / float(self.cfg.TRAIN.BATCH_SIZE)).detach(), 'cls_loss': cls_loss, 'bbox_loss': bbox_loss, 'cls_prob': cls_prob,
+                'objective': ((cls_loss + bbox_loss) / float(self.cfg.TRAIN.BATCH_SIZE)).detach(),
+                'cls_loss': cls_loss, 'bbox_loss': bbox_loss, 'cls_prob': cls_prob,
                 'label': label, 'num_images': data.shape[0], 'num_rois': rois.shape[0]}
 
     @torch.no_grad()

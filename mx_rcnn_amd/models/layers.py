@@ -7,11 +7,13 @@ the GPU (the native layout of the HIP kernels); weights are cast to the activati
 only when they differ (mixed precision installs bf16 weight views, see
 :mod:`mx_rcnn_amd.core.params`).
 """
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..ops.bn import frozen_bn_relu
+from ..ops.bn import frozen_bn_relu, train_bn_eligible, train_bn_relu
 from ..ops.conv import conv2d
 
 
@@ -96,6 +98,9 @@ class BatchNorm(MxLayer):
         if self.use_global_stats or not self.training:
             return frozen_bn_relu(x, self.gamma, self.beta, self.moving_mean, self.moving_var, self.eps,
                                   self.fix_gamma, self.relu)
+        if train_bn_eligible(x) and os.environ.get('MXR_BN_TRAIN_KERNEL', '1') != '0':
+            return train_bn_relu(x, self.gamma, self.beta, self.moving_mean, self.moving_var, self.momentum,
+                                 self.eps, self.fix_gamma, self.relu)
         g = torch.ones_like(self.gamma) if self.fix_gamma else self.gamma
         # torch running = (1-m)*running + m*batch  <=>  MXNet moving = mom*moving + (1-mom)*batch
         y = F.batch_norm(x, self.moving_mean, self.moving_var, g.to(x.dtype) if x.dtype != torch.float32 else g,

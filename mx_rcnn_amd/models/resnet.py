@@ -9,7 +9,7 @@ import torch
 import torch.nn as nn
 
 from ..ops.conv import igemm_eligible
-from ..ops.fused import conv_add, conv_add_bn_relu, conv_bn_relu
+from ..ops.fused import conv_add, conv_add_bn_relu, conv_bn_relu, fused_unit
 from .layers import BatchNorm, Conv, Linear, max_pool
 
 
@@ -68,9 +68,25 @@ class ResidualUnit(nn.Module):
         c1 = self.conv1
         return igemm_eligible(x, c1.weight, c1.stride, c1.pad) and c1.weight.dtype == torch.bfloat16
 
+    def unit_op_ok(self, x, next_bn):
+        """The whole-unit fused op needs MFMA-eligible 1x1/3x3 shapes and frozen BNs."""
+        if os.environ.get('MXR_FUSE_UNIT', '1') == '0':
+            return False
+        if next_bn is not None and not (_frozen(next_bn) and next_bn.relu):
+            return False
+        convs = [self.conv1, self.conv2] + ([self.conv3] if self.bottle_neck else [])
+        if not all(c.weight.dtype == torch.bfloat16 and c.weight.shape[0] % 64 == 0 and c.weight.shape[1] % 64 == 0
+                   for c in convs):
+            return False
+        if not self.dim_match and not (self.sc.weight.shape[0] % 64 == 0 and self.sc.weight.dtype == torch.bfloat16):
+            return False
+        return x.shape[1] % 64 == 0 and x.shape[1] % 8 == 0
+
     def forward_fused(self, x, act1=None, next_bn=None):
         """-> (unit output, next unit's act1 or None).  act1: this unit's bn1(x) if already
         produced by the previous unit's epilogue."""
+        if self.unit_op_ok(x, next_bn):
+            return fused_unit(self, x, act1, next_bn)
         if act1 is None:
             act1 = self.bn1(x)
         a = conv_bn_relu(act1, self.conv1, self.bn2)
@@ -172,6 +188,6 @@ class ResNetHead(nn.Module):
         self.bbox_pred = Linear('bbox_pred', filters[4], 4 * num_classes)
 
     def forward(self, pooled):
-        x = self.bn1(self.stage4(pooled))
+        x = self.bn1(run_stage(self.stage4, pooled))  # fused when the BNs are frozen (test time)
         x = torch.mean(x, dim=(2, 3))
         return self.cls_score(x), self.bbox_pred(x)

@@ -72,3 +72,45 @@ class _FrozenBnRelu(torch.autograd.Function):
 
 def frozen_bn_relu(x, gamma, beta, mean, var, eps=2e-5, fix_gamma=False, relu=True):
     return _FrozenBnRelu.apply(x, gamma, beta, mean, var, float(eps), bool(fix_gamma), bool(relu))
+
+
+class _TrainBnRelu(torch.autograd.Function):
+    """Batch-statistics BN (+ReLU) of the ResNet head (csrc/hip/bn_train.hip); the running stats
+    are updated in the forward kernel with MXNet's momentum convention."""
+
+    @staticmethod
+    def forward(ctx, x, gamma, beta, rmean, rvar, momentum, eps, fix_gamma, relu):
+        xc = x.contiguous(memory_format=torch.channels_last)
+        y, sm, si = need_ext().bn_train_fwd(xc, gamma, beta, rmean, rvar, float(momentum), float(eps),
+                                            bool(fix_gamma), bool(relu))
+        ctx.save_for_backward(xc, gamma, beta, sm, si)
+        ctx.params = (gamma if gamma.is_leaf else None, beta if beta.is_leaf else None)
+        ctx.fix_gamma, ctx.relu = fix_gamma, relu
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, gamma, beta, sm, si = ctx.saved_tensors
+        need_g = ctx.needs_input_grad[1] and not ctx.fix_gamma
+        need_b = ctx.needs_input_grad[2]
+        tg = grad_sink.target(ctx.params[0]) if need_g else None
+        tb = grad_sink.target(ctx.params[1]) if need_b else None
+        direct = tg is not None and tb is not None and tg.dtype == torch.float32 and tb.dtype == torch.float32
+        dx, dg, db = need_ext().bn_train_bwd(x, dy, gamma, beta, sm, si, bool(ctx.fix_gamma), bool(ctx.relu),
+                                             bool(ctx.needs_input_grad[0]), tg if direct else None,
+                                             tb if direct else None)
+        dx = dx if ctx.needs_input_grad[0] else None
+        if direct:
+            return dx, None, None, None, None, None, None, None, None
+        dg = dg.to(gamma.dtype) if need_g else None
+        db = db.to(beta.dtype) if need_b else None
+        return dx, dg, db, None, None, None, None, None, None
+
+
+def train_bn_relu(x, gamma, beta, rmean, rvar, momentum=0.9, eps=2e-5, fix_gamma=False, relu=True):
+    return _TrainBnRelu.apply(x, gamma, beta, rmean, rvar, float(momentum), float(eps), bool(fix_gamma), bool(relu))
+
+
+def train_bn_eligible(x):
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0 and
+            x.is_contiguous(memory_format=torch.channels_last))

@@ -126,3 +126,210 @@ def conv_add_bn_relu(x, conv, res, bn):
     """(y, relu(bn(y))) with y = conv(x) + res."""
     return _ConvAddBnRelu.apply(x, conv.weight, res, *_bn_args(bn), int(conv.stride), int(conv.pad),
                                 float(bn.eps), bool(bn.fix_gamma))
+
+
+# ---------------------------------------------------------------------------------------------
+# Whole-unit op: forward = the fused epilogues above; backward = a hand-scheduled kernel
+# sequence in which every frozen BN-ReLU backward rides in the epilogue of the data-gradient
+# conv that produces its input gradient (csrc/hip/conv_igemm.hip BN-backward mode):
+#
+#   wgrad3(a3, dOut)                      dY2 = dgrad3(dOut) o bn3'   (+ dgamma3/dbeta3)
+#   wgrad2(a2, dY2)                       dY1 = dgrad2(dY2)  o bn2'   (+ dgamma2/dbeta2)
+#   wgrad1(act1, dY1)  [wgrad_sc, dgrad_sc]
+#   dX = dgrad1(dY1) (+ dgrad_sc) o bn1' + dOut (identity shortcut)   (+ dgamma1/dbeta1)
+#
+# Parameter gradients go straight into the flat gradient buffers (ops/grad_sink.py) when the
+# parameters are store-managed; otherwise they are returned through autograd.  The unit's
+# second output (next unit's act1, produced in conv3's epilogue) is non-differentiable: its
+# gradient is handled inside the next unit, whose bn1 it is.
+# ---------------------------------------------------------------------------------------------
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+class _Unit(object):
+    """Static description of a residual unit for the fused op."""
+
+    def __init__(self, u, next_bn):
+        self.bottle = u.bottle_neck
+        self.dim_match = u.dim_match
+        self.stride = int((u.conv2 if u.bottle_neck else u.conv1).stride)
+        self.bns = [u.bn1, u.bn2] + ([u.bn3] if u.bottle_neck else [])
+        self.next_bn = next_bn
+        self.eps = [float(b.eps) for b in self.bns]
+        self.fix = [bool(b.fix_gamma) for b in self.bns]
+
+
+def _bnp(bn):
+    return [bn.gamma, bn.beta, bn.moving_mean, bn.moving_var]
+
+
+class _FusedUnitFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, spec, x, act1, *t):
+        # t = W1, W2, [W3], [Wsc], bn1(4), bn2(4), [bn3(4)], [next_bn(4)]
+        ext = need_ext()
+        nconv = (3 if spec.bottle else 2) + (0 if spec.dim_match else 1)
+        ws = list(t[:nconv])
+        nb = len(spec.bns)
+        bnps = [list(t[nconv + 4 * i:nconv + 4 * i + 4]) for i in range(nb)]
+        nxt = list(t[nconv + 4 * nb:nconv + 4 * nb + 4]) if spec.next_bn is not None else None
+        x = _cl(x)
+        bn1 = bnps[0]
+        if act1 is None:
+            act1 = ext.bn_relu_fwd(x, *[p.float().contiguous() for p in bn1], spec.eps[0], spec.fix[0], True)
+        # conv1 (stride 1 for bottleneck; 3x3 stride s for basic) -> bn2
+        s1 = 1 if spec.bottle else spec.stride
+        p1 = 0 if spec.bottle else 1
+        y1, a2 = ext.conv_igemm_fwd(act1, ws[0], None, s1, p1, False, 0, 0, None, bnps[1], spec.eps[1],
+                                    spec.fix[1], True)
+        if spec.bottle:
+            y2, a3 = ext.conv_igemm_fwd(a2, ws[1], None, spec.stride, 1, False, 0, 0, None, bnps[2], spec.eps[2],
+                                        spec.fix[2], True)
+            last_in, w_last = a3, ws[2]
+        else:
+            y2, a3 = None, None
+            last_in, w_last = a2, ws[1]
+        sc_in = None
+        if spec.dim_match:
+            res = x
+        else:
+            wsc = ws[-1]
+            sc_in = act1 if spec.stride == 1 else _cl(act1[:, :, ::spec.stride, ::spec.stride])
+            res = ext.conv_igemm_fwd(sc_in, wsc, None, 1, 0, False)[0]
+        if nxt is not None:
+            out, act1n = ext.conv_igemm_fwd(last_in, w_last, None, 1, 0 if spec.bottle else 1, False, 0, 0, res,
+                                            nxt, float(spec.next_bn.eps), bool(spec.next_bn.fix_gamma), True)
+        else:
+            out = ext.conv_igemm_fwd(last_in, w_last, None, 1, 0 if spec.bottle else 1, False, 0, 0, res)[0]
+            act1n = None
+        ctx.spec = spec
+        ctx.nconv = nconv
+        ctx.params = [p if p.is_leaf else None for p in t]
+        ctx.save_for_backward(x, act1, y1, a2, y2, a3, sc_in, *t)
+        if act1n is None:
+            return out, out.new_zeros(())
+        ctx.mark_non_differentiable(act1n)
+        return out, act1n
+
+    @staticmethod
+    def backward(ctx, d_out, _d_act1n):
+        ext = need_ext()
+        spec, nconv = ctx.spec, ctx.nconv
+        saved = ctx.saved_tensors
+        x, act1, y1, a2, y2, a3, sc_in = saved[:7]
+        t = saved[7:]
+        ws = list(t[:nconv])
+        nb = len(spec.bns)
+        bnps = [list(t[nconv + 4 * i:nconv + 4 * i + 4]) for i in range(nb)]
+        need = ctx.needs_input_grad[3:]  # per tensor in t
+        grads = [None] * len(t)
+        d_out = _cl(d_out).to(x.dtype)
+
+        def wgrad(idx, dy, inp, k, stride, pad):
+            if not need[idx]:
+                return
+            tgt = grad_sink.target(ctx.params[idx])
+            if tgt is not None and tgt.is_contiguous(memory_format=torch.channels_last):
+                ext.conv_wgrad(dy, inp, k, k, stride, pad, 0, tgt)
+            else:
+                grads[idx] = ext.conv_wgrad(dy, inp, k, k, stride, pad)
+
+        def bn_targets(i):
+            gi = nconv + 4 * i
+            ng, nbb = need[gi] and not spec.fix[i], need[gi + 1]
+            if not (ng or nbb):
+                return None, None, False
+            tg = grad_sink.target(ctx.params[gi]) if ng else None
+            tb = grad_sink.target(ctx.params[gi + 1]) if nbb else None
+            if (ng and (tg is None or tg.dtype != torch.float32)) or (nbb and (tb is None or tb.dtype != torch.float32)):
+                C = bnps[i][0].numel()
+                tg = torch.zeros(C, device=x.device, dtype=torch.float32)
+                tb = torch.zeros(C, device=x.device, dtype=torch.float32)
+                return tg, tb, True
+            return tg, tb, False
+
+        def finish_bn(i, tg, tb, returned):
+            if returned:
+                gi = nconv + 4 * i
+                if need[gi] and not spec.fix[i]:
+                    grads[gi] = tg.to(bnps[i][0].dtype)
+                if need[gi + 1]:
+                    grads[gi + 1] = tb.to(bnps[i][1].dtype)
+
+        def dgrad_bn(dy, w_idx, k, pad, bn_i, bn_x, dadd=None, dres=None):
+            """dgrad of a stride-1 conv with the BN(bn_i)-ReLU backward of its input in the epilogue."""
+            from .conv import dgrad_weight
+            tg, tb, ret = bn_targets(bn_i)
+            r = ext.conv_igemm_fwd(dy, dgrad_weight(ctx.params[w_idx], ws[w_idx]), None, 1, k - 1 - pad, False, 0, 0,
+                                   dres, bnps[bn_i], spec.eps[bn_i], spec.fix[bn_i], True, bn_x, dadd, tg, tb)
+            finish_bn(bn_i, tg, tb, ret)
+            return r[0]
+
+        def bn_bwd_plain(dy_act, bn_i, bn_x, dres=None):
+            tg, tb, ret = bn_targets(bn_i)
+            p = [q.float().contiguous() for q in bnps[bn_i]]
+            dx, dg, db = ext.bn_relu_bwd(bn_x, dy_act, *p, spec.eps[bn_i], spec.fix[bn_i], True, True,
+                                         tg is not None, tg, tb, dres)
+            finish_bn(bn_i, tg, tb, ret)
+            return dx
+
+        s = spec.stride
+        if spec.bottle:
+            # conv3 (1x1) : wgrad + dgrad with bn3 backward
+            wgrad(2, d_out, a3, 1, 1, 0)
+            d_y2 = dgrad_bn(d_out, 2, 1, 0, 2, y2)
+            # conv2 (3x3, stride s)
+            wgrad(1, d_y2, a2, 3, s, 1)
+            if s == 1:
+                d_y1 = dgrad_bn(d_y2, 1, 3, 1, 1, y1)
+            else:
+                d_a2 = torch.ops.aten.convolution_backward(d_y2, a2, ws[1], None, [s, s], [1, 1], [1, 1], False,
+                                                           [0, 0], 1, [True, False, False])[0]
+                d_y1 = bn_bwd_plain(_cl(d_a2), 1, y1)
+            wgrad(0, d_y1, act1, 1, 1, 0)
+            k1, p1, s1 = 1, 0, 1
+        else:
+            # basic: conv2 (3x3 s1) then conv1 (3x3 stride s)
+            wgrad(1, d_out, a2, 3, 1, 1)
+            d_y1 = dgrad_bn(d_out, 1, 3, 1, 1, y1)
+            wgrad(0, d_y1, act1, 3, s, 1)
+            k1, p1, s1 = 3, 1, s
+        if not ctx.needs_input_grad[1]:
+            if not spec.dim_match:
+                wgrad(nconv - 1, d_out, sc_in, 1, 1, 0)
+            return (None, None, None) + tuple(grads)
+        d_sc = None
+        if not spec.dim_match:
+            wgrad(nconv - 1, d_out, sc_in, 1, 1, 0)
+            from .conv import dgrad_weight
+            d_sub = ext.conv_igemm_fwd(d_out, dgrad_weight(ctx.params[nconv - 1], ws[nconv - 1]), None, 1, 0,
+                                       False)[0]
+            if s == 1:
+                d_sc = d_sub
+            else:
+                d_sc = torch.zeros_like(act1, memory_format=torch.channels_last)
+                d_sc[:, :, ::s, ::s] = d_sub
+        dres = d_out if spec.dim_match else None
+        if s1 == 1 and ws[0].shape[0] % 64 == 0:
+            d_x = dgrad_bn(d_y1, 0, k1, p1, 0, x, dadd=d_sc, dres=dres)
+        else:
+            d_act1 = torch.ops.aten.convolution_backward(d_y1, act1, ws[0], None, [s1, s1], [p1, p1], [1, 1], False,
+                                                         [0, 0], 1, [True, False, False])[0]
+            if d_sc is not None:
+                d_act1 = d_act1 + d_sc
+            d_x = bn_bwd_plain(_cl(d_act1), 0, x, dres)
+        return (None, d_x, None) + tuple(grads)
+
+
+def fused_unit(u, x, act1=None, next_bn=None):
+    """Run ResidualUnit ``u`` (frozen BNs) as one fused op -> (out, next act1 or None)."""
+    spec = _Unit(u, next_bn)
+    ws = [u.conv1.weight, u.conv2.weight] + ([u.conv3.weight] if u.bottle_neck else [])
+    if not u.dim_match:
+        ws.append(u.sc.weight)
+    t = ws + _bnp(u.bn1) + _bnp(u.bn2) + (_bnp(u.bn3) if u.bottle_neck else [])
+    if next_bn is not None:
+        t += [p.detach() for p in _bnp(next_bn)]  # gradients of next_bn are produced by the next unit
+    out, act1n = _FusedUnitFn.apply(spec, x, act1, *t)
+    return out, (act1n if next_bn is not None else None)

@@ -8,5 +8,6 @@ run() { local name=$1 t=$2; shift 2; echo "[r] $name"; timeout -k 10 "$t" "$@" >
 run pytest_fused 600 python -m pytest tests/test_fused.py -x -q -p no:cacheprovider
 run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider -k "not graph"
 run bench_graph 400 python bench.py --steps 20 --warmup 5
+run bench_test 400 python bench_test.py --steps 50 --warmup 5
 run bench_nofuse 400 env MXR_FUSE=0 python bench.py --steps 20 --warmup 5
 cd /tmp && run prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof_r8" -o run -- python "$GRAFT_REPO_ROOT/bench.py" --steps 10 --warmup 3

@@ -78,10 +78,10 @@ def test_wt_flip_cache(cuda):
         assert torch.equal(d_, _flip_t(s_))
 
 
-def _unit(cin, cout, stride, dim_match, dev):
+def _unit(cin, cout, stride, dim_match, dev, bottle=True):
     from mx_rcnn_amd.models.resnet import ResidualUnit
     torch.manual_seed(5)
-    u = ResidualUnit('u', cin, cout, stride, dim_match, True, 0.99, True)
+    u = ResidualUnit('u', cin, cout, stride, dim_match, bottle, 0.99, True)
     with torch.no_grad():
         for m in u.modules():
             if hasattr(m, 'moving_var'):
@@ -98,13 +98,17 @@ def _unit(cin, cout, stride, dim_match, dev):
     return u
 
 
-@pytest.mark.parametrize('cfg', [(1024, 1024, 1, True), (512, 1024, 2, False), (256, 256, 1, True)])
-def test_fused_unit_matches_unfused(cuda, cfg):
-    from mx_rcnn_amd.models.resnet import ResidualUnit  # noqa: F401
-    cin, cout, stride, dim_match = cfg
+@pytest.mark.parametrize('cfg', [(1024, 1024, 1, True, True), (512, 1024, 2, False, True),
+                                 (256, 256, 1, True, True), (256, 512, 1, False, True),
+                                 (128, 128, 1, True, False), (128, 256, 2, False, False)])
+@pytest.mark.parametrize('unit_op', ['1', '0'])
+def test_fused_units_match_unfused(cuda, cfg, unit_op, monkeypatch):
+    """Two chained units (u -> v, v's bn1 fused into u's last epilogue) vs the plain modules."""
+    monkeypatch.setenv('MXR_FUSE_UNIT', unit_op)
+    cin, cout, stride, dim_match, bottle = cfg
     H, W = (24, 40) if stride == 1 else (48, 80)
-    u = _unit(cin, cout, stride, dim_match, cuda)
-    nxt = _unit(cout, cout, 1, True, cuda).bn1
+    u = _unit(cin, cout, stride, dim_match, cuda, bottle)
+    v = _unit(cout, cout, 1, True, cuda, bottle)
     g = torch.Generator().manual_seed(6)
     x0 = torch.randn(1, cin, H, W, generator=g).bfloat16()
     results = []
@@ -112,25 +116,61 @@ def test_fused_unit_matches_unfused(cuda, cfg):
         x = _cl(x0, cuda).requires_grad_()
         if fused:
             assert u.can_fuse(x)
-            out, act = u.forward_fused(x, None, nxt)
+            out_u, act = u.forward_fused(x, None, v.bn1)
+            out, _ = v.forward_fused(out_u, act, None)
         else:
-            out = u(x)
-            act = nxt(out)
+            out = v(u(x))
         gen = torch.Generator().manual_seed(7)
         d_out = torch.randn(out.shape, generator=gen).bfloat16().to(cuda)
-        d_act = torch.randn(act.shape, generator=gen).bfloat16().to(cuda)
-        for p_ in u.parameters():
+        for p_ in list(u.parameters()) + list(v.parameters()):
             p_.grad = None
-        torch.autograd.backward([out, act], [d_out, d_act])
-        grads = {n: p_.grad.detach().float().clone() for n, p_ in u.named_parameters() if p_.grad is not None}
-        results.append((out.detach().float(), act.detach().float(), x.grad.detach().float(), grads))
-    (o0, a0, x0g, g0), (o1, a1, x1g, g1) = results
-    for t0, t1 in ((o0, o1), (a0, a1), (x0g, x1g)):
+        out.backward(d_out)
+        grads = {}
+        for tag, mod in (('u', u), ('v', v)):
+            for n, p_ in mod.named_parameters():
+                if p_.grad is not None:
+                    grads[tag + '.' + n] = p_.grad.detach().float().clone()
+        results.append((out.detach().float(), x.grad.detach().float(), grads))
+    (o0, x0g, g0), (o1, x1g, g1) = results
+    for t0, t1 in ((o0, o1), (x0g, x1g)):
         assert (t0 - t1).abs().max().item() <= 2e-2 * t0.abs().max().item() + 1e-3
-    assert set(g0) == set(g1)
+    assert set(g0) == set(g1), set(g0) ^ set(g1)
     for n in g0:
         err = (g0[n] - g1[n]).abs().max().item()
         assert err <= 3e-2 * g0[n].abs().max().item() + 1e-3, (n, err)
+
+
+def test_bnb_epilogue_vs_reference(cuda):
+    """dgrad conv with the BN-ReLU backward epilogue (+dadd, +dres) vs unfused torch ops."""
+    from mx_rcnn_amd.ops import need_ext
+    from mx_rcnn_amd.ops.conv import _flip_t
+    g = torch.Generator().manual_seed(41)
+    for (Cin, Cout, k, H, W, splits) in ((256, 1024, 1, 24, 40, 1), (256, 1024, 1, 24, 40, 4),
+                                         (256, 256, 3, 20, 30, 1), (256, 256, 3, 20, 30, 2)):
+        w = (torch.randn(Cout, Cin, k, k, generator=g) * 0.05).bfloat16()
+        dy = torch.randn(1, Cout, H, W, generator=g).bfloat16()
+        xr = torch.randn(1, Cin, H, W, generator=g).bfloat16()
+        dadd = torch.randn(1, Cin, H, W, generator=g).bfloat16()
+        dres = torch.randn(1, Cin, H, W, generator=g).bfloat16()
+        gamma, beta = torch.rand(Cin, generator=g) + 0.5, torch.randn(Cin, generator=g) * 0.1
+        mean, var = torch.randn(Cin, generator=g) * 0.2, torch.rand(Cin, generator=g) + 0.5
+        p = k // 2
+        # reference
+        d_act = torch.ops.aten.convolution_backward(dy.float(), xr.float(), w.float(), None, [1, 1], [p, p], [1, 1],
+                                                    False, [0, 0], 1, [True, False, False])[0] + dadd.float()
+        s = gamma * torch.rsqrt(var + 2e-5)
+        pre = xr.float() * s[None, :, None, None] + (beta - mean * s)[None, :, None, None]
+        gm = d_act * (pre > 0).float()
+        ref_dx = gm * s[None, :, None, None] + dres.float()
+        xhat = (xr.float() - mean[None, :, None, None]) * torch.rsqrt(var + 2e-5)[None, :, None, None]
+        ref_dg, ref_db = (gm * xhat).sum(dim=(0, 2, 3)), gm.sum(dim=(0, 2, 3))
+        wt = _flip_t(_cl(w, cuda))
+        dx, dgm, dbt = need_ext().conv_igemm_fwd(_cl(dy, cuda), wt, None, 1, k - 1 - p, False, 0, splits,
+                                                 _cl(dres, cuda), [t.to(cuda) for t in (gamma, beta, mean, var)],
+                                                 2e-5, False, True, _cl(xr, cuda), _cl(dadd, cuda))
+        for a, r in ((dx, ref_dx), (dgm, ref_dg), (dbt, ref_db)):
+            err = (a.float().cpu() - r).abs().max().item()
+            assert err <= 2e-2 * r.abs().max().item() + 2e-2, (Cin, Cout, k, splits, err)
 
 
 def test_fused_trunk_step_matches_unfused(cuda):
@@ -161,3 +201,31 @@ def test_fused_trunk_step_matches_unfused(cuda):
             os.environ.pop('MXR_FUSE', None)
     for a, b in zip(*losses):
         assert abs(a - b) <= 2e-2 * abs(a) + 1e-3, losses
+
+
+@pytest.mark.parametrize('C,M_hw', [(1024, (128, 7, 7)), (2048, (128, 4, 4)), (512, (64, 7, 7)), (8, (3, 5, 5))])
+@pytest.mark.parametrize('relu', [True, False])
+def test_train_bn_relu_vs_torch(cuda, C, M_hw, relu):
+    from mx_rcnn_amd.ops.bn import train_bn_relu
+    N, H, W = M_hw
+    g = torch.Generator().manual_seed(31)
+    x = (torch.randn(N, C, H, W, generator=g) * 2 + 0.5).bfloat16()
+    gamma = (torch.rand(C, generator=g) + 0.5)
+    beta = torch.randn(C, generator=g) * 0.1
+    dy = torch.randn(N, C, H, W, generator=g).bfloat16()
+    # reference: fp32 torch batch norm on the same bf16 input
+    xr = x.float().clone().requires_grad_()
+    gr, br = gamma.clone().requires_grad_(), beta.clone().requires_grad_()
+    rm_r, rv_r = torch.zeros(C), torch.ones(C)
+    yr = F.batch_norm(xr, rm_r, rv_r, gr, br, training=True, momentum=0.1, eps=2e-5)
+    if relu:
+        yr = torch.relu(yr)
+    yr.backward(dy.float())
+    xg = _cl(x, cuda).requires_grad_()
+    gg, bg = gamma.to(cuda).requires_grad_(), beta.to(cuda).requires_grad_()
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    yg = train_bn_relu(xg, gg, bg, rm, rv, 0.9, 2e-5, False, relu)
+    yg.backward(_cl(dy, cuda))
+    for a, r in ((yg, yr), (xg.grad, xr.grad), (gg.grad, gr.grad), (bg.grad, br.grad), (rm, rm_r), (rv, rv_r)):
+        err = (a.float().cpu() - r.detach()).abs().max().item()
+        assert err <= 2e-2 * r.abs().max().item() + 2e-3, err

@@ -393,7 +393,8 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   }
   int auto_splits = 1;
   const int t = mxr::conv_igemm_plan(NB, Ho, Wo, Cin, Cout, KH, KW, (int)tile, &auto_splits);
-  const int sp = splits > 0 ? (int)splits : auto_splits;
+  // BN-backward epilogue: no split-K by default (the statistics are reduced in-tile instead)
+  const int sp = splits > 0 ? (int)splits : (bwd_mode ? 1 : auto_splits);
   Tensor slab;
   if (sp > 1) slab = at::empty({(int64_t)sp * NB * Ho * Wo * Cout}, x.options().dtype(at::kFloat));
   const int used = mxr::conv_igemm_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),

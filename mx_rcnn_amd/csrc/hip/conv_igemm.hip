@@ -271,22 +271,22 @@ conv_igemm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
 }
 
 // split-K reduce for the BN-backward epilogue: column-blocked so the per-column statistics are
-// accumulated in registers over 256 rows and leave the block with one atomic per column.
-// Block = 16 column quads (64 columns) x 16 row lanes; grid = (Cout/64) x ceil(M/256).
+// accumulated in registers over 64 rows and leave the block with one atomic per column.
+// Block = 16 column quads (64 columns) x 16 row lanes; grid = (Cout/64) x ceil(M/64).
 __global__ void __launch_bounds__(256)
 splitk_reduce_bnb_kernel(const float* __restrict__ slab, int splits, int M, int Cout, const ConvEpi ep,
                          uint16_t* __restrict__ y) {
   __shared__ float red[2][16][64];
   const int cq = threadIdx.x & 15, rl = threadIdx.x >> 4;
   const int n = blockIdx.x * 64 + cq * 4;
-  const int r0 = blockIdx.y * 256;
+  const int r0 = blockIdx.y * 64;
   const int64_t MN = (int64_t)M * Cout;
   float sg[4] = {0.f, 0.f, 0.f, 0.f}, sgx[4] = {0.f, 0.f, 0.f, 0.f};
   EpiCol ec[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) ec[k] = epi_col(ep, min(n + k, Cout - 1));
   if (n < Cout) {
-    for (int r = r0 + rl; r < min(M, r0 + 256); r += 16) {
+    for (int r = r0 + rl; r < min(M, r0 + 64); r += 16) {
       const int64_t e = (int64_t)r * Cout + n;
       float4 a = *reinterpret_cast<const float4*>(slab + e);
       for (int sidx = 1; sidx < splits; ++sidx) {
@@ -362,7 +362,7 @@ static void launch_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB
   if (splits > 1) {
     const int64_t MN = (int64_t)M * Cout;
     if (ep.bnb_x)
-      splitk_reduce_bnb_kernel<<<dim3(div_up(Cout, 64), div_up(M, 256)), 256, 0, st>>>(slab, splits, M, Cout, ep, y);
+      splitk_reduce_bnb_kernel<<<dim3(div_up(Cout, 64), div_up(M, 64)), 256, 0, st>>>(slab, splits, M, Cout, ep, y);
     else
       splitk_reduce_kernel<<<div_up((MN + 3) / 4, 256), 256, 0, st>>>(slab, splits, MN, Cout, ep, y);
   }

@@ -68,9 +68,18 @@ class ResidualUnit(nn.Module):
         c1 = self.conv1
         return igemm_eligible(x, c1.weight, c1.stride, c1.pad) and c1.weight.dtype == torch.bfloat16
 
+    def frozen_bns(self):
+        return _frozen(self.bn1) and _frozen(self.bn2) and (not self.bottle_neck or _frozen(self.bn3))
+
     def unit_op_ok(self, x, next_bn):
-        """The whole-unit fused op needs MFMA-eligible 1x1/3x3 shapes and frozen BNs."""
-        if os.environ.get('MXR_FUSE_UNIT', '1') == '0':
+        """The whole-unit fused op needs MFMA-eligible 1x1/3x3 shapes (any M) and frozen BNs."""
+        if not fusion_enabled() or os.environ.get('MXR_FUSE_UNIT', '1') == '0' or not self.frozen_bns():
+            return False
+        if not (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)):
+            return False
+        # forward-only units with large-M 1x1 convs (frozen stages 1-2) run faster on hipBLASLt
+        needs_grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters()))
+        if not needs_grad and not self.can_fuse(x):
             return False
         if next_bn is not None and not (_frozen(next_bn) and next_bn.relu):
             return False
@@ -110,18 +119,20 @@ class ResidualUnit(nn.Module):
 
 
 def run_stage(stage, x):
-    """Run a stage (nn.Sequential of ResidualUnit) through the fused path when possible, chaining
-    each unit's conv3 epilogue into the next unit's bn1."""
+    """Run a stage (nn.Sequential of ResidualUnit) unit by unit through the fused ops where they
+    apply, chaining each unit's last epilogue into the next unit's bn1; units that cannot fuse
+    (e.g. train-mode BN in the RoI head) run as plain modules."""
     units = list(stage)
-    if not units[0].can_fuse(x):
-        return stage(x)
     act1 = None
     for i, u in enumerate(units):
         nxt = units[i + 1] if i + 1 < len(units) else None
-        if act1 is None and not u.can_fuse(x):
+        nbn = nxt.bn1 if (nxt is not None and _frozen(nxt.bn1) and fusion_enabled()) else None
+        if u.unit_op_ok(x, nbn) and u.frozen_bns():
+            x, act1 = fused_unit(u, x, act1, nbn)
+        elif act1 is None and not u.can_fuse(x):
             x = u(x)
-            continue
-        x, act1 = u.forward_fused(x, act1, nxt.bn1 if (nxt is not None and _frozen(nxt.bn1)) else None)
+        else:
+            x, act1 = u.forward_fused(x, act1, nbn)
     return x
 
 

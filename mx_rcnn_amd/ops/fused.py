@@ -205,6 +205,7 @@ class _FusedUnitFn(torch.autograd.Function):
             act1n = None
         ctx.spec = spec
         ctx.nconv = nconv
+        ctx.set_materialize_grads(False)  # the act1n output never receives a gradient
         ctx.params = [p if p.is_leaf else None for p in t]
         ctx.save_for_backward(x, act1, y1, a2, y2, a3, sc_in, *t)
         if act1n is None:

@@ -2,6 +2,7 @@
 // outputs through the PyTorch caching allocator, launch on the current HIP stream.  All
 // launches are graph-capturable (no host sync, no allocation inside the launchers).
 #include <cstring>
+#include <map>
 #include <torch/extension.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
@@ -312,6 +313,7 @@ std::vector<Tensor> bn_relu_bwd(const Tensor& x, const Tensor& dy, const Tensor&
 }
 
 // ---- implicit-GEMM conv ----------------------------------------------------------------
+
 // conv_igemm_fwd(x, w, bias, stride, pad, relu, tile, splits, residual, bn, bn_eps, bn_fix_gamma, act_relu)
 //   -> [y] or, when bn = (gamma, beta, mean, var) is given, [y, act(bn(y))]  (see ConvEpi)
 std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::optional<Tensor> bias, int64_t stride,
@@ -414,17 +416,18 @@ std::vector<Tensor> bn_train_fwd(const Tensor& x, const Tensor& gamma, const Ten
   CHECK_DEV(x);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "x: bf16 NHWC");
   const int C = (int)x.size(1);
-  TORCH_CHECK(C % 8 == 0, "bn_train needs C % 8 == 0");
+  TORCH_CHECK(C % 64 == 0, "bn_train needs C % 64 == 0");
   CHECK_F32(rmean); CHECK_F32(rvar); CHECK_CONTIG(rmean); CHECK_CONTIG(rvar);
   DevGuard g(x.device());
   Tensor gf = gamma.to(at::kFloat).contiguous(), bf = beta.to(at::kFloat).contiguous();
   Tensor y = at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast);
   Tensor sm = at::empty({C}, x.options().dtype(at::kFloat)), si = at::empty({C}, x.options().dtype(at::kFloat));
+  Tensor ws = at::empty({mxr::bn_train_workspace_floats(x.numel() / C, C)}, x.options().dtype(at::kFloat));
   const int r = mxr::bn_train_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), x.numel() / C, C,
                                   gf.data_ptr<float>(), bf.data_ptr<float>(), rmean.data_ptr<float>(),
                                   rvar.data_ptr<float>(), (float)momentum, (float)eps, fix_gamma ? 1 : 0, relu ? 1 : 0,
                                   reinterpret_cast<uint16_t*>(y.data_ptr()), sm.data_ptr<float>(), si.data_ptr<float>(),
-                                  cur_stream());
+                                  ws.data_ptr<float>(), cur_stream());
   TORCH_CHECK(r == 0, "bn_train_fwd: unsupported shape");
   return {y, sm, si};
 }
@@ -450,12 +453,15 @@ std::vector<Tensor> bn_train_bwd(const Tensor& x, const Tensor& dy, const Tensor
     dgm = at::zeros({C}, x.options().dtype(at::kFloat));
     dbt = at::zeros({C}, x.options().dtype(at::kFloat));
   }
+  TORCH_CHECK(C % 64 == 0, "bn_train needs C % 64 == 0");
+  Tensor ws = at::empty({mxr::bn_train_workspace_floats(x.numel() / C, C)}, x.options().dtype(at::kFloat));
   const int r = mxr::bn_train_bwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                                   reinterpret_cast<const uint16_t*>(g.data_ptr()), x.numel() / C, C,
                                   gf.data_ptr<float>(), bf.data_ptr<float>(), save_mean.data_ptr<float>(),
                                   save_invstd.data_ptr<float>(), fix_gamma ? 1 : 0, relu ? 1 : 0,
                                   need_dx ? reinterpret_cast<uint16_t*>(dx.data_ptr()) : nullptr,
-                                  dgm.data_ptr<float>(), dbt.data_ptr<float>(), acc ? 1 : 0, cur_stream());
+                                  dgm.data_ptr<float>(), dbt.data_ptr<float>(), acc ? 1 : 0, ws.data_ptr<float>(),
+                                  cur_stream());
   TORCH_CHECK(r == 0, "bn_train_bwd: unsupported shape");
   return {dx, dgm, dbt};
 }

@@ -1,24 +1,27 @@
 // Training-mode (batch statistics) BatchNorm + optional ReLU for NHWC bf16 activations: the
 // stage-4 / bn1 layers of the ResNet C4 head, which normalise over the 128 sampled RoIs
-// (`rcnn/resnet.py:152,165`, bn_global=False).  M = N*H*W is small (2 K - 6 K rows) and C large
-// (512 - 2048), so one workgroup owns 8 channels (one 16-B load per row) for ALL rows:
-// statistics, the running-average update and the normalisation happen in one launch with no
-// cross-block reduction, and C/8 = 64-256 workgroups cover the chip.  256 row lanes with 4 rows
-// in flight per lane hide the HBM latency; the blocks of neighbouring channel groups read the
-// same cache lines, so L2 serves the 16-B-per-row pattern.  The slab stays L2-resident between
-// the passes.
-// fwd: pass 1 mean, pass 2 centred variance (no E[x^2]-E[x]^2 cancellation), pass 3 y.
-// bwd: pass 1 sum(g), sum(g*xhat) with g = dy * relu_mask, pass 2 dx.
-// Running stats follow MXNet: moving = mom * moving + (1 - mom) * batch (unbiased variance, as
-// the cuDNN path MXNet uses).
-#include <type_traits>
-
+// (`rcnn/resnet.py:152,165`, bn_global=False).  M = N*H*W = 2 K - 6 K rows, C = 512 - 2048.
+//
+// Two kernels per direction, both fully coalesced: a workgroup owns 64 channels (one 128-B
+// line per row, 8 lanes x 16 B) and a chunk of BT_ROWS rows (32 row lanes).
+//   fwd 1: per-chunk partial sum / sum of squares (shifted by the running mean, so the
+//          E[x^2] - E[x]^2 form does not cancel) -> workspace [chunks][2][C]
+//   fwd 2: every block folds the chunk partials of its 64 channels (a few dozen rows),
+//          derives scale/shift, normalises (+ReLU) its chunk; chunk 0 writes the running
+//          stats (moving = mom * moving + (1 - mom) * batch, unbiased var, as MXNet's cuDNN
+//          path) and the saved mean / invstd.
+//   bwd 1: partial sum(g), sum(g * xhat) with g = dy * relu_mask
+//   bwd 2: fold partials -> dgamma / dbeta (chunk 0) and dx for the chunk.
+// An earlier one-block-per-8-channels version read every 128-B line 8 times through L2 and
+// ran ~37 us per call; this layout touches each line once per pass.
 #include "common.h"
 #include "../kernels.h"
 
 namespace mxr {
 
-constexpr int BT_CB = 8;  // channels per block (one 16-B load per row)
+constexpr int BT_C = 64;       // channels per block
+constexpr int BT_ROWS = 256;   // rows per chunk
+constexpr int BT_LANES = 32;   // row lanes per block (8 channel groups x 32 = 256 threads)
 
 __device__ __forceinline__ void ld8(const uint16_t* p, float* v) {
   const uint4 u = *reinterpret_cast<const uint4*>(p);
@@ -38,193 +41,244 @@ __device__ __forceinline__ void st8(uint16_t* p, const float* v) {
   *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// block-wide sum of 8 per-thread values (256 threads) -> out[8] visible to all threads
-__device__ __forceinline__ void block_sum8(float* v, float (*red)[8], float* out) {
+// sum a[8] / b[8] over the 32 row lanes of each channel group; results for channel
+// (cg*8 + k) land in out_a / out_b [64] (visible after the call)
+__device__ __forceinline__ void lane_reduce(const float* a, const float* b, float (*red)[BT_LANES][16],
+                                            float* out_a, float* out_b) {
+  const int cg = threadIdx.x & 7, rl = threadIdx.x >> 3;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) v[k] = wave_sum(v[k]);
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (lane == 0)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) red[wid][k] = v[k];
+  for (int k = 0; k < 8; ++k) {
+    red[cg][rl][k] = a[k];
+    red[cg][rl][8 + k] = b[k];
+  }
   __syncthreads();
-  if (threadIdx.x < 8) out[threadIdx.x] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
-                                          red[3][threadIdx.x];
+  if (threadIdx.x < 128) {
+    const int c = threadIdx.x & 63, which = threadIdx.x >> 6;
+    const int g = c >> 3, k = c & 7;
+    float s = 0.f;
+    for (int r = 0; r < BT_LANES; ++r) s += red[g][r][which * 8 + k];
+    (which ? out_b : out_a)[c] = s;
+  }
   __syncthreads();
-}
-
-// for each of this thread's rows r = tid + i*256: fn(row_ptr_offset)
-template <typename F>
-__device__ __forceinline__ void for_rows(int64_t M, F fn) {
-  int64_t r = threadIdx.x;
-  for (; r + 768 < M; r += 1024) fn(r, std::integral_constant<int, 4>());  // 4 rows in flight
-  for (; r < M; r += 256) fn(r, std::integral_constant<int, 1>());
 }
 
 __global__ void __launch_bounds__(256)
-bn_train_fwd_kernel(const uint16_t* __restrict__ x, int64_t M, int C, const float* __restrict__ gamma,
-                    const float* __restrict__ beta, float* __restrict__ rmean, float* __restrict__ rvar,
-                    float momentum, float eps, int fix_gamma, int relu, uint16_t* __restrict__ y,
-                    float* __restrict__ save_mean, float* __restrict__ save_invstd) {
-  __shared__ float red[4][8];
-  __shared__ float tot[8];
-  const int c0 = blockIdx.x * BT_CB;
-  float acc[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) acc[k] = 0.f;
-  for_rows(M, [&](int64_t r, auto N) {
-    constexpr int n = decltype(N)::value;
-    float v[4][8];
-#pragma unroll
-    for (int u = 0; u < n; ++u) ld8(x + (r + u * 256) * C + c0, v[u]);
-#pragma unroll
-    for (int u = 0; u < n; ++u)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) acc[k] += v[u][k];
-  });
-  block_sum8(acc, red, tot);
-  float mu[8];
+bn_train_stats_kernel(const uint16_t* __restrict__ x, int64_t M, int C, const float* __restrict__ shift,
+                      float* __restrict__ part) {
+  __shared__ float red[8][BT_LANES][16];
+  __shared__ float sa[64], sb[64];
+  const int cg = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c0 = blockIdx.x * BT_C + cg * 8;
+  const int64_t r0 = (int64_t)blockIdx.y * BT_ROWS;
+  const int64_t r1 = r0 + BT_ROWS < M ? r0 + BT_ROWS : M;
+  float sh[8], s1[8], s2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    mu[k] = tot[k] / (float)M;
-    acc[k] = 0.f;
+    sh[k] = shift[c0 + k];
+    s1[k] = s2[k] = 0.f;
   }
-  __syncthreads();
-  for_rows(M, [&](int64_t r, auto N) {
-    constexpr int n = decltype(N)::value;
-    float v[4][8];
+#pragma unroll 4
+  for (int64_t r = r0 + rl; r < r1; r += BT_LANES) {
+    float v[8];
+    ld8(x + r * C + c0, v);
 #pragma unroll
-    for (int u = 0; u < n; ++u) ld8(x + (r + u * 256) * C + c0, v[u]);
-#pragma unroll
-    for (int u = 0; u < n; ++u)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float d = v[u][k] - mu[k];
-        acc[k] += d * d;
-      }
-  });
-  block_sum8(acc, red, tot);
-  float sc[8], sh[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const int c = c0 + k;
-    const float var = tot[k] / (float)M;
+    for (int k = 0; k < 8; ++k) {
+      const float d = v[k] - sh[k];
+      s1[k] += d;
+      s2[k] += d * d;
+    }
+  }
+  lane_reduce(s1, s2, red, sa, sb);
+  if (threadIdx.x < 64) {
+    float* row = part + (int64_t)blockIdx.y * 2 * C;
+    row[blockIdx.x * BT_C + threadIdx.x] = sa[threadIdx.x];
+    row[C + blockIdx.x * BT_C + threadIdx.x] = sb[threadIdx.x];
+  }
+}
+
+__global__ void __launch_bounds__(256)
+bn_train_norm_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int nchunks, const float* __restrict__ part,
+                     const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ rmean,
+                     float* __restrict__ rvar, float momentum, float eps, int fix_gamma, int relu,
+                     uint16_t* __restrict__ y, float* __restrict__ save_mean, float* __restrict__ save_invstd) {
+  __shared__ float scale_sh[64], shift_sh[64];
+  const int tid = threadIdx.x;
+  if (tid < 64) {
+    const int c = blockIdx.x * BT_C + tid;
+    const float sh = rmean[c];  // the shift used by the stats kernel (read before any update)
+    float a = 0.f, b = 0.f;
+    for (int i = 0; i < nchunks; ++i) {
+      a += part[(int64_t)i * 2 * C + c];
+      b += part[(int64_t)i * 2 * C + C + c];
+    }
+    const float dm = a / (float)M;  // mean - shift
+    const float var = fmaxf(b / (float)M - dm * dm, 0.f);
+    const float mu = sh + dm;
     const float inv = rsqrtf(var + eps);
     const float g = fix_gamma ? 1.f : gamma[c];
-    sc[k] = g * inv;
-    sh[k] = beta[c] - mu[k] * sc[k];
-    if (threadIdx.x == 0) {
-      save_mean[c] = mu[k];
+    scale_sh[tid] = g * inv;
+    shift_sh[tid] = beta[c] - mu * g * inv;
+    if (blockIdx.y == 0) {
+      save_mean[c] = mu;
       save_invstd[c] = inv;
-      const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
-      rmean[c] = momentum * rmean[c] + (1.f - momentum) * mu[k];
-      rvar[c] = momentum * rvar[c] + (1.f - momentum) * unb;
     }
   }
-  for_rows(M, [&](int64_t r, auto N) {
-    constexpr int n = decltype(N)::value;
-    float v[4][8];
+  __syncthreads();
+  const int cg = tid & 7, rl = tid >> 3;
+  const int c0 = blockIdx.x * BT_C + cg * 8;
+  float sc[8], sf[8];
 #pragma unroll
-    for (int u = 0; u < n; ++u) ld8(x + (r + u * 256) * C + c0, v[u]);
+  for (int k = 0; k < 8; ++k) {
+    sc[k] = scale_sh[cg * 8 + k];
+    sf[k] = shift_sh[cg * 8 + k];
+  }
+  const int64_t r0 = (int64_t)blockIdx.y * BT_ROWS;
+  const int64_t r1 = r0 + BT_ROWS < M ? r0 + BT_ROWS : M;
+#pragma unroll 4
+  for (int64_t r = r0 + rl; r < r1; r += BT_LANES) {
+    float v[8];
+    ld8(x + r * C + c0, v);
 #pragma unroll
-    for (int u = 0; u < n; ++u) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        v[u][k] = v[u][k] * sc[k] + sh[k];
-        if (relu) v[u][k] = fmaxf(v[u][k], 0.f);
-      }
-      st8(y + (r + u * 256) * C + c0, v[u]);
+    for (int k = 0; k < 8; ++k) {
+      v[k] = v[k] * sc[k] + sf[k];
+      if (relu) v[k] = fmaxf(v[k], 0.f);
     }
-  });
+    st8(y + r * C + c0, v);
+  }
+}
+
+// running-stat update after every block has read the old running mean (separate launch)
+__global__ void bn_train_running_kernel(int64_t M, int C, const float* __restrict__ save_mean,
+                                        const float* __restrict__ save_invstd, float eps, float momentum,
+                                        float* __restrict__ rmean, float* __restrict__ rvar) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const float inv = save_invstd[c];
+  const float var = 1.f / (inv * inv) - eps;
+  const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+  rmean[c] = momentum * rmean[c] + (1.f - momentum) * save_mean[c];
+  rvar[c] = momentum * rvar[c] + (1.f - momentum) * unb;
 }
 
 __global__ void __launch_bounds__(256)
-bn_train_bwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy, int64_t M, int C,
-                    const float* __restrict__ gamma, const float* __restrict__ beta,
-                    const float* __restrict__ save_mean, const float* __restrict__ save_invstd, int fix_gamma,
-                    int relu, uint16_t* __restrict__ dx, float* __restrict__ dgamma, float* __restrict__ dbeta,
-                    int accumulate) {
-  __shared__ float red[4][8];
-  __shared__ float tot_g[8], tot_gx[8];
-  const int c0 = blockIdx.x * BT_CB;
-  float mu[8], inv[8], g[8], b[8];
+bn_train_bstats_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy, int64_t M, int C,
+                       const float* __restrict__ gamma, const float* __restrict__ beta,
+                       const float* __restrict__ save_mean, const float* __restrict__ save_invstd, int fix_gamma,
+                       int relu, float* __restrict__ part) {
+  __shared__ float red[8][BT_LANES][16];
+  __shared__ float sa[64], sb[64];
+  const int cg = threadIdx.x & 7, rl = threadIdx.x >> 3;
+  const int c0 = blockIdx.x * BT_C + cg * 8;
+  float mu[8], inv[8], g[8], b[8], sg[8], sgx[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     mu[k] = save_mean[c0 + k];
     inv[k] = save_invstd[c0 + k];
     g[k] = fix_gamma ? 1.f : gamma[c0 + k];
     b[k] = beta[c0 + k];
+    sg[k] = sgx[k] = 0.f;
   }
-  float sg[8], sgx[8];
+  const int64_t r0 = (int64_t)blockIdx.y * BT_ROWS;
+  const int64_t r1 = r0 + BT_ROWS < M ? r0 + BT_ROWS : M;
+#pragma unroll 4
+  for (int64_t r = r0 + rl; r < r1; r += BT_LANES) {
+    float v[8], d[8];
+    ld8(x + r * C + c0, v);
+    ld8(dy + r * C + c0, d);
 #pragma unroll
-  for (int k = 0; k < 8; ++k) sg[k] = sgx[k] = 0.f;
-  for_rows(M, [&](int64_t r, auto N) {
-    constexpr int n = decltype(N)::value;
-    float v[4][8], d[4][8];
-#pragma unroll
-    for (int u = 0; u < n; ++u) {
-      ld8(x + (r + u * 256) * C + c0, v[u]);
-      ld8(dy + (r + u * 256) * C + c0, d[u]);
+    for (int k = 0; k < 8; ++k) {
+      const float xh = (v[k] - mu[k]) * inv[k];
+      const float gm = (!relu || xh * g[k] + b[k] > 0.f) ? d[k] : 0.f;
+      sg[k] += gm;
+      sgx[k] += gm * xh;
     }
-#pragma unroll
-    for (int u = 0; u < n; ++u)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float xh = (v[u][k] - mu[k]) * inv[k];
-        const float gm = (!relu || xh * g[k] + b[k] > 0.f) ? d[u][k] : 0.f;
-        sg[k] += gm;
-        sgx[k] += gm * xh;
-      }
-  });
-  block_sum8(sg, red, tot_g);
-  block_sum8(sgx, red, tot_gx);
-  float mg[8], mgx[8];
+  }
+  lane_reduce(sg, sgx, red, sa, sb);
+  if (threadIdx.x < 64) {
+    float* row = part + (int64_t)blockIdx.y * 2 * C;
+    row[blockIdx.x * BT_C + threadIdx.x] = sa[threadIdx.x];
+    row[C + blockIdx.x * BT_C + threadIdx.x] = sb[threadIdx.x];
+  }
+}
+
+__global__ void __launch_bounds__(256)
+bn_train_dx_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy, int64_t M, int C, int nchunks,
+                   const float* __restrict__ part, const float* __restrict__ gamma, const float* __restrict__ beta,
+                   const float* __restrict__ save_mean, const float* __restrict__ save_invstd, int fix_gamma,
+                   int relu, uint16_t* __restrict__ dx, float* __restrict__ dgamma, float* __restrict__ dbeta,
+                   int accumulate) {
+  __shared__ float mg_sh[64], mgx_sh[64];
+  const int tid = threadIdx.x;
+  if (tid < 64) {
+    const int c = blockIdx.x * BT_C + tid;
+    float a = 0.f, b = 0.f;
+    for (int i = 0; i < nchunks; ++i) {
+      a += part[(int64_t)i * 2 * C + c];
+      b += part[(int64_t)i * 2 * C + C + c];
+    }
+    mg_sh[tid] = a / (float)M;
+    mgx_sh[tid] = b / (float)M;
+    if (blockIdx.y == 0) {
+      if (dgamma && !fix_gamma) dgamma[c] = accumulate ? dgamma[c] + b : b;
+      if (dbeta) dbeta[c] = accumulate ? dbeta[c] + a : a;
+    }
+  }
+  __syncthreads();
+  if (!dx) return;
+  const int cg = tid & 7, rl = tid >> 3;
+  const int c0 = blockIdx.x * BT_C + cg * 8;
+  float mu[8], inv[8], g[8], b[8], mg[8], mgx[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    mg[k] = tot_g[k] / (float)M;
-    mgx[k] = tot_gx[k] / (float)M;
-    if (threadIdx.x == 0) {
-      const int c = c0 + k;
-      if (dgamma && !fix_gamma) dgamma[c] = accumulate ? dgamma[c] + tot_gx[k] : tot_gx[k];
-      if (dbeta) dbeta[c] = accumulate ? dbeta[c] + tot_g[k] : tot_g[k];
-    }
+    mu[k] = save_mean[c0 + k];
+    inv[k] = save_invstd[c0 + k];
+    g[k] = fix_gamma ? 1.f : gamma[c0 + k];
+    b[k] = beta[c0 + k];
+    mg[k] = mg_sh[cg * 8 + k];
+    mgx[k] = mgx_sh[cg * 8 + k];
   }
-  if (!dx) return;
-  for_rows(M, [&](int64_t r, auto N) {
-    constexpr int n = decltype(N)::value;
-    float v[4][8], d[4][8];
+  const int64_t r0 = (int64_t)blockIdx.y * BT_ROWS;
+  const int64_t r1 = r0 + BT_ROWS < M ? r0 + BT_ROWS : M;
+#pragma unroll 4
+  for (int64_t r = r0 + rl; r < r1; r += BT_LANES) {
+    float v[8], d[8];
+    ld8(x + r * C + c0, v);
+    ld8(dy + r * C + c0, d);
 #pragma unroll
-    for (int u = 0; u < n; ++u) {
-      ld8(x + (r + u * 256) * C + c0, v[u]);
-      ld8(dy + (r + u * 256) * C + c0, d[u]);
+    for (int k = 0; k < 8; ++k) {
+      const float xh = (v[k] - mu[k]) * inv[k];
+      const float gm = (!relu || xh * g[k] + b[k] > 0.f) ? d[k] : 0.f;
+      d[k] = g[k] * inv[k] * (gm - mg[k] - xh * mgx[k]);
     }
-#pragma unroll
-    for (int u = 0; u < n; ++u) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float xh = (v[u][k] - mu[k]) * inv[k];
-        const float gm = (!relu || xh * g[k] + b[k] > 0.f) ? d[u][k] : 0.f;
-        d[u][k] = g[k] * inv[k] * (gm - mg[k] - xh * mgx[k]);
-      }
-      st8(dx + (r + u * 256) * C + c0, d[u]);
-    }
-  });
+    st8(dx + r * C + c0, d);
+  }
 }
+
+int bn_train_workspace_floats(int64_t M, int C) { return (int)(((M + BT_ROWS - 1) / BT_ROWS) * 2 * C); }
 
 int bn_train_fwd(const uint16_t* x, int64_t M, int C, const float* gamma, const float* beta, float* rmean,
                  float* rvar, float momentum, float eps, int fix_gamma, int relu, uint16_t* y, float* save_mean,
-                 float* save_invstd, hipStream_t st) {
-  if (C % BT_CB != 0 || M <= 0) return -1;
-  bn_train_fwd_kernel<<<C / BT_CB, 256, 0, st>>>(x, M, C, gamma, beta, rmean, rvar, momentum, eps, fix_gamma, relu,
-                                                 y, save_mean, save_invstd);
+                 float* save_invstd, float* workspace, hipStream_t st) {
+  if (C % BT_C != 0 || M <= 0) return -1;
+  const int nchunks = (int)((M + BT_ROWS - 1) / BT_ROWS);
+  const dim3 grid(C / BT_C, nchunks);
+  bn_train_stats_kernel<<<grid, 256, 0, st>>>(x, M, C, rmean, workspace);
+  bn_train_norm_kernel<<<grid, 256, 0, st>>>(x, M, C, nchunks, workspace, gamma, beta, rmean, rvar, momentum, eps,
+                                             fix_gamma, relu, y, save_mean, save_invstd);
+  bn_train_running_kernel<<<div_up(C, 256), 256, 0, st>>>(M, C, save_mean, save_invstd, eps, momentum, rmean, rvar);
   return 0;
 }
 
 int bn_train_bwd(const uint16_t* x, const uint16_t* dy, int64_t M, int C, const float* gamma, const float* beta,
                  const float* save_mean, const float* save_invstd, int fix_gamma, int relu, uint16_t* dx,
-                 float* dgamma, float* dbeta, int accumulate, hipStream_t st) {
-  if (C % BT_CB != 0 || M <= 0) return -1;
-  bn_train_bwd_kernel<<<C / BT_CB, 256, 0, st>>>(x, dy, M, C, gamma, beta, save_mean, save_invstd, fix_gamma, relu,
-                                                 dx, dgamma, dbeta, accumulate);
+                 float* dgamma, float* dbeta, int accumulate, float* workspace, hipStream_t st) {
+  if (C % BT_C != 0 || M <= 0) return -1;
+  const int nchunks = (int)((M + BT_ROWS - 1) / BT_ROWS);
+  const dim3 grid(C / BT_C, nchunks);
+  bn_train_bstats_kernel<<<grid, 256, 0, st>>>(x, dy, M, C, gamma, beta, save_mean, save_invstd, fix_gamma, relu,
+                                               workspace);
+  bn_train_dx_kernel<<<grid, 256, 0, st>>>(x, dy, M, C, nchunks, workspace, gamma, beta, save_mean, save_invstd,
+                                           fix_gamma, relu, dx, dgamma, dbeta, accumulate);
   return 0;
 }
 

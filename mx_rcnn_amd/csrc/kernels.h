@@ -132,15 +132,17 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
                    int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int tile, int splits, float* slab,
                    hipStream_t st);
 // ---- training-mode BatchNorm (bn_train.hip) -----------------------------------------------
-// x/y/dy/dx NHWC bf16 (M rows x C), C % 8 == 0.  fwd updates the running stats in place
+// x/y/dy/dx NHWC bf16 (M rows x C), C % 64 == 0.  fwd updates the running stats in place
 // (moving = momentum * moving + (1 - momentum) * batch, unbiased var) and saves mean / invstd.
+// workspace: bn_train_workspace_floats(M, C) floats.
+int bn_train_workspace_floats(int64_t M, int C);
 int bn_train_fwd(const uint16_t* x, int64_t M, int C, const float* gamma, const float* beta, float* rmean,
                  float* rvar, float momentum, float eps, int fix_gamma, int relu, uint16_t* y, float* save_mean,
-                 float* save_invstd, hipStream_t st);
+                 float* save_invstd, float* workspace, hipStream_t st);
 // dgamma/dbeta: written (accumulate = 0) or added to (accumulate = 1); may be null.
 int bn_train_bwd(const uint16_t* x, const uint16_t* dy, int64_t M, int C, const float* gamma, const float* beta,
                  const float* save_mean, const float* save_invstd, int fix_gamma, int relu, uint16_t* dx,
-                 float* dgamma, float* dbeta, int accumulate, hipStream_t st);
+                 float* dgamma, float* dbeta, int accumulate, float* workspace, hipStream_t st);
 
 // Flip + transpose many conv filters in ONE launch (dgrad operand cache):
 //   dst[i][r][s][o] = src[o][KH-1-r][KW-1-s][i]   (both channels_last, i.e. (O,KH,KW,I) rows)

@@ -112,5 +112,5 @@ def train_bn_relu(x, gamma, beta, rmean, rvar, momentum=0.9, eps=2e-5, fix_gamma
 
 
 def train_bn_eligible(x):
-    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0 and
+    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 64 == 0 and
             x.is_contiguous(memory_format=torch.channels_last))

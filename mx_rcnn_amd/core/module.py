@@ -178,6 +178,8 @@ class MutableModule(object):
 
     def backward(self, out_grads=None):
         self._outputs['loss'].backward()
+        # release the autograd graph (see Trainer.step_body: a live graph breaks later captures)
+        self._outputs = {k: (v.detach() if torch.is_tensor(v) else v) for k, v in self._outputs.items()}
 
     def update(self):
         t = self.trainer

@@ -79,7 +79,11 @@ class Trainer:
             self.reducer.finish()
         with prof.range('sgd'):
             self.store.sgd_step(self.lr_t, self.momentum, self.wd, self.rescale, self.clip)
-        return out
+        # Return detached outputs: a caller holding the loss would otherwise keep this step's
+        # autograd graph (and its AccumulateGrad nodes, bound to this step's stream) alive, and a
+        # later hipGraph capture on a side stream then syncs against that stream and dies in
+        # hipStreamEndCapture.
+        return {k: (v.detach() if torch.is_tensor(v) else v) for k, v in out.items()}
 
     def check_finite(self, step=None):
         """Raise FloatingPointError if any step since the last check produced a non-finite loss

@@ -70,12 +70,13 @@ std::vector<Tensor> nms_proposals(const Tensor& boxes, const Tensor& scores, con
   TORCH_CHECK(n_valid.numel() == B, "n_valid shape");
   TORCH_CHECK(rand_u.numel() == (int64_t)B * post, "rand_u must hold B*post values");
   TORCH_CHECK(post > 0, "post must be > 0");
+  TORCH_CHECK(P > 0, "NMS needs at least one box slot");
   DevGuard g(boxes.device());
   const int nb = (P + 63) / 64;
-  TORCH_CHECK(16 + (int64_t)nb * 8 + post * 4 <= 160 * 1024, "NMS LDS budget exceeded (P or post too large)");
+  TORCH_CHECK(mxr::nms_reduce_lds(P, (int)post) <= 160 * 1024, "NMS LDS budget exceeded (P or post too large)");
   TORCH_CHECK(nb <= 256, "NMS supports at most 16384 pre-NMS boxes per image");
   auto st = cur_stream();
-  Tensor mask = at::empty({B, P, nb}, boxes.options().dtype(at::kLong));
+  Tensor mask = at::empty({mxr::nms_mask_words(B, P)}, boxes.options().dtype(at::kLong));
   mxr::nms_mask(boxes.data_ptr<float>(), n_valid.data_ptr<int32_t>(), B, P, (float)thresh,
                 reinterpret_cast<uint64_t*>(mask.data_ptr<int64_t>()), st);
   Tensor rois = at::empty({B, post, 5}, boxes.options());

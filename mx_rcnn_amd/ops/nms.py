@@ -13,6 +13,8 @@ import torch
 
 from ._ext import need_ext
 
+MAX_GPU_BOXES = 16384  # nms_proposals: at most 256 64-box blocks per image
+
 
 def _greedy_ref(boxes, n_valid, thresh, max_keep=None):
     """boxes already score-sorted (P, 4); returns list of kept positions among the first n_valid."""
@@ -71,6 +73,17 @@ def batched_nms(boxes, scores, classes, thresh, max_keep=None):
     """Per-class NMS in one pass: offset each class's boxes by class_id * (max_coord + 1)."""
     if boxes.numel() == 0:
         return torch.zeros(0, dtype=torch.long, device=boxes.device)
+    if boxes.is_cuda and boxes.shape[0] > MAX_GPU_BOXES:
+        # one bitmask pass holds at most MAX_GPU_BOXES boxes: run the classes separately
+        # (classes never interact), then restore the global descending-score order
+        keeps = []
+        for c in torch.unique(classes).tolist():
+            idx = torch.nonzero(classes == c).flatten()
+            keeps.append(idx[nms(boxes[idx], scores[idx], thresh, max_keep)])
+        keep = torch.cat(keeps)
+        order = torch.sort(scores[keep].float(), descending=True, stable=True).indices
+        keep = keep[order]
+        return keep if max_keep is None else keep[:max_keep]
     max_coord = boxes.max()
     offs = classes.to(boxes.dtype) * (max_coord + 1)
     return nms(boxes + offs[:, None], scores, thresh, max_keep)

@@ -161,6 +161,20 @@ def test_nms_gpu_matches_cpu(cuda):
 
 
 @pytest.mark.gpu
+def test_nms_gpu_training_scale(cuda):
+    """12000 -> 6000 (train proposal sizes), the 256-block limit, and post truncation."""
+    g = torch.Generator().manual_seed(9)
+    for n, th, post in [(12000, 0.7, None), (16384, 0.7, None), (5000, 0.5, 700)]:
+        b = rand_boxes(g, n, 1300)
+        s = torch.rand(n, generator=g)
+        k_cpu = ops.nms(b, s, th, max_keep=post)
+        k_gpu = ops.nms(b.to(cuda), s.to(cuda), th, max_keep=post).cpu()
+        assert torch.equal(k_cpu, k_gpu), (n, th, post)
+        if post is not None:
+            assert k_gpu.numel() == post
+
+
+@pytest.mark.gpu
 def test_anchor_target_gpu_matches_cpu(cuda):
     H, W = 50, 84
     g = torch.Generator().manual_seed(11)

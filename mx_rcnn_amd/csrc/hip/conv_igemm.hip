@@ -79,6 +79,71 @@ __device__ __forceinline__ void epi_bnb(const ConvEpi& ep, const EpiCol& c, uint
   y[idx] = f32_to_bf16(o);
 }
 
+// Shared epilogue of the implicit-GEMM kernels: C/D map col = lane & 15, row = (lane >> 4) * 4 + r.
+template <int TM, int TN, int WM, int WN>
+__device__ __forceinline__ void igemm_epilogue(f32x4 (&acc)[TM][TN], int m0, int n0, int wm, int wn, int lane, int M,
+                                               int Cout, const ConvEpi& ep, uint16_t* __restrict__ y, int split,
+                                               int splits, float* __restrict__ slab) {
+  if (splits > 1) {  // fp32 partial slab; bias/ReLU/cast happen in the reduce kernel
+    float* sp = slab + (int64_t)split * M * Cout;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WN + j * 16 + (lane & 15);
+      if (n >= Cout) continue;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+          if (m < M) sp[(int64_t)m * Cout + n] = acc[i][j][r];
+        }
+    }
+    return;
+  }
+  if (ep.bnb_x) {
+    // BN-backward epilogue: per-column sums over this wave's rows, reduced across the four
+    // 16-lane row groups, then one fp32 atomic per (wave, column, stat)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0 + wn * WN + j * 16 + (lane & 15);
+      float sg = 0.f, sgx = 0.f;
+      if (n < Cout) {
+        const EpiCol ec = epi_col(ep, n);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+            if (m < M) epi_bnb(ep, ec, y, (int64_t)m * Cout + n, acc[i][j][r], sg, sgx);
+          }
+      }
+      sg += __shfl_xor(sg, 16, 64);
+      sg += __shfl_xor(sg, 32, 64);
+      sgx += __shfl_xor(sgx, 16, 64);
+      sgx += __shfl_xor(sgx, 32, 64);
+      if (lane < 16 && n < Cout) {
+        if (ep.bnb_dbeta) atomicAdd(ep.bnb_dbeta + n, sg);
+        if (ep.bnb_dgamma && !ep.bn_fix_gamma) atomicAdd(ep.bnb_dgamma + n, sgx);
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * WN + j * 16 + (lane & 15);
+    if (n >= Cout) continue;
+    const EpiCol ec = epi_col(ep, n);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
+        if (m < M) epi_store(ep, ec, y, (int64_t)m * Cout + n, acc[i][j][r]);
+      }
+    }
+  }
+}
+
 template <int BM, int BN>
 __global__ void __launch_bounds__(256)
 conv_igemm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
@@ -209,65 +274,7 @@ conv_igemm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
     __syncthreads();
   }
 
-  // epilogue: C/D map col = lane & 15, row = (lane >> 4) * 4 + r
-  if (splits > 1) {  // fp32 partial slab; bias/ReLU/cast happen in the reduce kernel
-    float* sp = slab + (int64_t)split * M * Cout;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * WN + j * 16 + (lane & 15);
-      if (n >= Cout) continue;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
-          if (m < M) sp[(int64_t)m * Cout + n] = acc[i][j][r];
-        }
-    }
-    return;
-  }
-  if (ep.bnb_x) {
-    // BN-backward epilogue: per-column sums over this wave's rows, reduced across the four
-    // 16-lane row groups, then one fp32 atomic per (wave, column, stat)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * WN + j * 16 + (lane & 15);
-      float sg = 0.f, sgx = 0.f;
-      if (n < Cout) {
-        const EpiCol ec = epi_col(ep, n);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
-            if (m < M) epi_bnb(ep, ec, y, (int64_t)m * Cout + n, acc[i][j][r], sg, sgx);
-          }
-      }
-      sg += __shfl_xor(sg, 16, 64);
-      sg += __shfl_xor(sg, 32, 64);
-      sgx += __shfl_xor(sgx, 16, 64);
-      sgx += __shfl_xor(sgx, 32, 64);
-      if (lane < 16 && n < Cout) {
-        if (ep.bnb_dbeta) atomicAdd(ep.bnb_dbeta + n, sg);
-        if (ep.bnb_dgamma && !ep.bn_fix_gamma) atomicAdd(ep.bnb_dgamma + n, sgx);
-      }
-    }
-    return;
-  }
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * WN + j * 16 + (lane & 15);
-    if (n >= Cout) continue;
-    const EpiCol ec = epi_col(ep, n);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
-        if (m < M) epi_store(ep, ec, y, (int64_t)m * Cout + n, acc[i][j][r]);
-      }
-    }
-  }
+  igemm_epilogue<TM, TN, WM, WN>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab);
 }
 
 // split-K reduce for the BN-backward epilogue: column-blocked so the per-column statistics are
@@ -349,7 +356,298 @@ splitk_reduce_kernel(const float* __restrict__ slab, int splits, int64_t MN, int
   if (ep.y2) *reinterpret_cast<ushort4*>(ep.y2 + e) = make_ushort4(out2[0], out2[1], out2[2], out2[3]);
 }
 
-template <int BM, int BN>
+// ---- S-stage LDS-DMA pipeline (the latency-bound 1-image detection regime) -----------------
+// One image's stage-3/4 convs give M = 2-6 K output rows: a few hundred workgroups, one per CU,
+// 4 waves each.  The register-staged kernel above keeps one K-step in flight, so every K-step
+// pays a full L2/MALL round trip (~1 us under load) for ~8-32 MFMAs.  Here every thread issues
+// its tile chunks as global_load_lds_dwordx4 (LDS-DMA, no VGPRs) S-1 K-steps ahead into an S-deep
+// LDS ring; a counted `s_waitcnt vmcnt` retires exactly the oldest stage and a raw s_barrier
+// publishes it (a __syncthreads() fence would drain every DMA in flight).  The LDS image is
+// written lane-linearly (DMA destination = wave base + lane * 16 B), so the XOR swizzle of the
+// MFMA-operand reads is applied to the per-lane SOURCE chunk instead; out-of-image taps and
+// rows past Cout read a 128-B block of zeros.  The MFMA tile, fragment reads and epilogue are
+// those of conv_igemm_fwd_kernel.
+__device__ __attribute__((aligned(128))) uint16_t g_igemm_zeros[64];
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
+}
+
+template <int BM, int BN, int S>
+__global__ void __launch_bounds__(256)
+conv_igemm_glds_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
+                       int NB, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad,
+                       const ConvEpi ep, int tiles_n, int nwg, int ntiles, int splits, float* __restrict__ slab) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int ACH = BM / 32, BCH = BN / 32;  // DMA instructions per thread per stage (8 rows each)
+  constexpr int LPS = ACH + BCH;
+  static_assert(S >= 2 && S <= 4, "pipeline depth");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[S * (BM + BN) * BK];  // the ONLY __shared__ object
+  uint16_t* As = lds;               // [S][BM][BK]
+  uint16_t* Bs = lds + S * BM * BK;  // [S][BN][BK]
+
+  const int bid = blockIdx.x;
+  const int q = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + bid / 8;
+  const int split = wgid / ntiles, tile = wgid % ntiles;
+  const int tm_idx = tile / tiles_n, tn_idx = tile % tiles_n;
+  const int m0 = tm_idx * BM, n0 = tn_idx * BN;
+  const int M = NB * Ho * Wo;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+
+  // DMA instruction i of wave wid fills tile rows 32 i + 8 wid .. +8; lane -> row + lane/8, slot lane%8
+  const int slot = lane & 7;
+  int a_hi0[ACH], a_wi0[ACH], a_img[ACH], a_lc[ACH];
+#pragma unroll
+  for (int i = 0; i < ACH; ++i) {
+    const int row = 32 * i + 8 * wid + (lane >> 3);
+    a_lc[i] = slot ^ ((row >> 1) & 7);  // logical 16-B chunk stored in this slot (swizzle)
+    const int m = m0 + row;
+    if (m < M) {
+      const int img = m / (Ho * Wo), rem = m % (Ho * Wo);
+      a_img[i] = img;
+      a_hi0[i] = (rem / Wo) * stride - pad;
+      a_wi0[i] = (rem % Wo) * stride - pad;
+    } else {
+      a_img[i] = -1; a_hi0[i] = 0; a_wi0[i] = 0;
+    }
+  }
+  const uint16_t* b_src[BCH];
+#pragma unroll
+  for (int i = 0; i < BCH; ++i) {
+    const int row = 32 * i + 8 * wid + (lane >> 3);
+    const int co = n0 + row;
+    b_src[i] = co < Cout ? w + (int64_t)co * KH * KW * Cin + (slot ^ ((row >> 1) & 7)) * 8 : nullptr;
+  }
+  const int cin_steps = Cin / BK;
+  const int nk_all = KH * KW * cin_steps;
+  const int per = (nk_all + splits - 1) / splits;
+  const int k_begin = split * per;
+  const int k_end = min(nk_all, k_begin + per);
+  const int nk = max(0, k_end - k_begin);
+
+  auto issue = [&](int kl, int buf) {
+    const int ks = k_begin + kl;
+    const int tap = ks / cin_steps;
+    const int ci0 = (ks % cin_steps) * BK;
+    const int fr = tap / KW, fc = tap % KW;
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const int hi = a_hi0[i] + fr, wi = a_wi0[i] + fc;
+      const uint16_t* src = g_igemm_zeros;
+      if (a_img[i] >= 0 && hi >= 0 && hi < H && wi >= 0 && wi < W)
+        src = x + (((int64_t)a_img[i] * H + hi) * W + wi) * Cin + ci0 + a_lc[i] * 8;
+      glds16(src, As + (buf * BM + 32 * i + 8 * wid) * BK);
+    }
+    const int koff = tap * Cin + ci0;
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) {
+      const uint16_t* src = b_src[i] ? b_src[i] + koff : g_igemm_zeros;
+      glds16(src, Bs + (buf * BN + 32 * i + 8 * wid) * BK);
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) issue(s, s);
+  for (int ks = 0; ks < nk; ++ks) {
+    // retire stage ks: the stages issued after it may stay in flight
+    const int ahead = min(S - 2, nk - 1 - ks);
+    if (ahead >= 2) wait_vmcnt<2 * LPS>();
+    else if (ahead == 1) wait_vmcnt<LPS>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();  // every wave's DMA of stage ks landed; stage ks-1 fully read
+    if (ks + S - 1 < nk) issue(ks + S - 1, (ks + S - 1) % S);
+    const int buf = ks % S;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+      const int chunk = kk * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WM + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(As + (buf * BM + row) * BK + swz(row, chunk) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WN + j * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (buf * BN + row) * BK + swz(row, chunk) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  igemm_epilogue<TM, TN, WM, WN>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab);
+}
+
+// ---- buffer-resource LDS-DMA variant: near-zero address arithmetic per K-step ---------------
+// PMC on the two kernels above (s3 3x3, 64x64 tile) shows ~100 VALU + ~80 SALU instructions per
+// K-step per wave against 8 MFMAs: the im2col address math (integer divisions for the tap,
+// 64-bit pixel offsets, four bounds compares per chunk) -- not memory -- paced the loop.  Here
+// each thread precomputes, once, a 32-bit byte offset of its A row at tap (0,0) and a bit mask of
+// the taps that fall inside the image; the per-K-step part is uniform (SGPR soffset = tap and
+// channel-block offset, advanced incrementally) and the per-lane part is one mask test that
+// swaps in an out-of-range offset: buffer loads return zeros past num_records, so padding and
+// rows >= M / Cout need no zero page and no branch.  Loads go straight to LDS
+// (buffer_load_dwordx4 ... lds) S-1 stages ahead, counted vmcnt + raw barrier as above.
+constexpr uint32_t kBufOOB = 0x80000000u;
+
+__device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t rs, void* lds_wave_base, uint32_t voff,
+                                          uint32_t soff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds_wave_base, 16,
+                                           (int)voff, (int)soff, 0, 0);
+}
+
+template <int BM, int BN, int S>
+__global__ void __launch_bounds__(256)
+conv_igemm_buf_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
+                      int NB, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad,
+                      const ConvEpi ep, int tiles_n, int nwg, int ntiles, int splits, float* __restrict__ slab) {
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int ACH = BM / 32, BCH = BN / 32;
+  constexpr int LPS = ACH + BCH;
+  static_assert(S >= 2 && S <= 4, "pipeline depth");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[S * (BM + BN) * BK];  // the ONLY __shared__ object
+  uint16_t* As = lds;
+  uint16_t* Bs = lds + S * BM * BK;
+
+  const int bid = blockIdx.x;
+  const int q = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + bid / 8;
+  const int split = wgid / ntiles, tile = wgid % ntiles;
+  const int tm_idx = tile / tiles_n, tn_idx = tile % tiles_n;
+  const int m0 = tm_idx * BM, n0 = tn_idx * BN;
+  const int M = NB * Ho * Wo;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int K = KH * KW * Cin;
+
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)((int64_t)NB * H * W * Cin * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, (int)((int64_t)Cout * K * 2), 0x00020000);
+
+  const int slot = lane & 7;
+  uint32_t a_off[ACH];
+  uint64_t a_mask[ACH];
+#pragma unroll
+  for (int i = 0; i < ACH; ++i) {
+    const int row = 32 * i + 8 * wid + (lane >> 3);
+    const int lc = slot ^ ((row >> 1) & 7);
+    const int m = m0 + row;
+    a_off[i] = 0;
+    a_mask[i] = 0;
+    if (m < M) {
+      const int img = m / (Ho * Wo), rem = m % (Ho * Wo);
+      const int hi0 = (rem / Wo) * stride - pad, wi0 = (rem % Wo) * stride - pad;
+      a_off[i] = (uint32_t)(((((int64_t)img * H + hi0) * W + wi0) * Cin + lc * 8) * 2);
+      for (int fr = 0; fr < KH; ++fr)
+        for (int fc = 0; fc < KW; ++fc)
+          if ((unsigned)(hi0 + fr) < (unsigned)H && (unsigned)(wi0 + fc) < (unsigned)W)
+            a_mask[i] |= 1ull << (fr * KW + fc);
+    }
+  }
+  uint32_t b_off[BCH];
+#pragma unroll
+  for (int i = 0; i < BCH; ++i) {
+    const int row = 32 * i + 8 * wid + (lane >> 3);
+    const int co = n0 + row;
+    b_off[i] = co < Cout ? (uint32_t)(((int64_t)co * K + (slot ^ ((row >> 1) & 7)) * 8) * 2) : kBufOOB;
+  }
+  const int cin_steps = Cin / BK;
+  const int nk_all = KH * KW * cin_steps;
+  const int per = (nk_all + splits - 1) / splits;
+  const int k_begin = split * per;
+  const int k_end = min(nk_all, k_begin + per);
+  const int nk = max(0, k_end - k_begin);
+
+  // issue cursor (uniform): tap (fr, fc), channel block ci0 of the next stage to load
+  int c_tap = k_begin / cin_steps, c_ci = (k_begin % cin_steps) * BK;
+  int c_fr = c_tap / KW, c_fc = c_tap % KW;
+  auto issue = [&](int buf) {
+    // the buffer range check sees only the VGPR offset, so the tap shift (which can turn a
+    // negative padding-row offset into a valid one) goes there; the channel block is the SGPR part
+    const uint32_t tap_a = (uint32_t)((c_fr * W + c_fc) * Cin * 2);
+    const uint32_t soff_a = (uint32_t)(c_ci * 2);
+    const uint32_t soff_b = (uint32_t)((c_tap * Cin + c_ci) * 2);
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const uint32_t vo = ((a_mask[i] >> c_tap) & 1ull) ? a_off[i] + tap_a : kBufOOB;
+      buf_lds16(xr, As + (buf * BM + 32 * i + 8 * wid) * BK, vo, soff_a);
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) buf_lds16(wr, Bs + (buf * BN + 32 * i + 8 * wid) * BK, b_off[i], soff_b);
+    c_ci += BK;
+    if (c_ci == Cin) {
+      c_ci = 0;
+      ++c_tap;
+      if (++c_fc == KW) {
+        c_fc = 0;
+        ++c_fr;
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) issue(s);
+  for (int ks = 0; ks < nk; ++ks) {
+    const int ahead = min(S - 2, nk - 1 - ks);
+    if (ahead >= 2) wait_vmcnt<2 * LPS>();
+    else if (ahead == 1) wait_vmcnt<LPS>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();
+    if (ks + S - 1 < nk) issue((ks + S - 1) % S);
+    const int buf = ks % S;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+      const int chunk = kk * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WM + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(As + (buf * BM + row) * BK + swz(row, chunk) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WN + j * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (buf * BN + row) * BK + swz(row, chunk) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  igemm_epilogue<TM, TN, WM, WN>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab);
+}
+
+template <int BM, int BN, int S = 0, bool BUF = false>
 static void launch_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho,
                        int Wo, int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int splits,
                        float* slab, hipStream_t st) {
@@ -357,8 +655,15 @@ static void launch_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (Cout + BN - 1) / BN;
   const int ntiles = tiles_m * tiles_n;
   const int nwg = ntiles * splits;
-  conv_igemm_fwd_kernel<BM, BN><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep,
-                                                     tiles_n, nwg, ntiles, splits, slab);
+  if constexpr (BUF)
+    conv_igemm_buf_kernel<BM, BN, S><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
+                                                         ep, tiles_n, nwg, ntiles, splits, slab);
+  else if constexpr (S > 0)
+    conv_igemm_glds_kernel<BM, BN, S><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
+                                                          ep, tiles_n, nwg, ntiles, splits, slab);
+  else
+    conv_igemm_fwd_kernel<BM, BN><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep,
+                                                       tiles_n, nwg, ntiles, splits, slab);
   if (splits > 1) {
     const int64_t MN = (int64_t)M * Cout;
     if (ep.bnb_x)
@@ -370,18 +675,25 @@ static void launch_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB
 
 int conv_igemm_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int tile, int* splits_out) {
   const int64_t M = (int64_t)NB * Ho * Wo;
-  if (tile <= 0) {
-    const int64_t b128 = ((M + 127) / 128) * ((Cout + 127) / 128);
-    const int64_t b12864 = ((M + 127) / 128) * ((Cout + 63) / 64);
-    if (b128 >= 512) tile = 1;
-    else if (b12864 >= 384) tile = 2;
-    else tile = 3;
-  }
-  const int bm = tile == 3 ? 64 : 128, bn = tile == 1 ? 128 : 64;
-  const int64_t blocks = ((M + bm - 1) / bm) * ((Cout + bn - 1) / bn);
   const int nk = KH * KW * (Cin / BK);
+  if (tile <= 0) {
+    // buffer-resource LDS-DMA kernel, 3-deep (tools/microbench/conv_tiles.py sweep on the
+    // ResNet-101 C4 shapes): 64x64 everywhere except many-block, long-K shapes (the 128-RoI
+    // stage-4 convs), where 128x64 halves the operand bytes per FLOP; split-K only for grids
+    // too small to cover the CUs
+    const int64_t b64 = ((M + 63) / 64) * ((Cout + 63) / 64);
+    const int t = (b64 >= 600 && nk >= 16) ? 22 : 23;
+    const int64_t blocks = t == 22 ? ((M + 127) / 128) * ((Cout + 63) / 64) : b64;
+    int splits = 1;
+    while (splits < 4 && blocks * splits < 128 && nk / (splits * 2) >= 8 && Cout % 4 == 0) splits *= 2;
+    *splits_out = splits;
+    return t;
+  }
+  // explicit tile (A/B runs): tile codes -> (BM, BN); split K until ~4 blocks per CU
+  const int code = tile % 10;
+  const int bm = code == 3 ? 64 : 128, bn = code == 1 ? 128 : 64;
+  const int64_t blocks = ((M + bm - 1) / bm) * ((Cout + bn - 1) / bn);
   int splits = 1;
-  // latency-bound regime (few blocks per CU): split K until ~4 blocks per CU, >= 6 K-steps each
   while (splits < 8 && blocks * splits * 2 <= 1024 && nk / (splits * 2) >= 6 && Cout % 4 == 0) splits *= 2;
   *splits_out = splits;
   return tile;
@@ -395,9 +707,27 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
   if ((ep.y2 || ep.bnb_x) && (!ep.bn_beta || !ep.bn_mean || !ep.bn_var || (!ep.bn_fix_gamma && !ep.bn_gamma)))
     return -1;
   if (ep.y2 && ep.bnb_x) return -1;
+  // buffer variants: 32-bit byte offsets below the kBufOOB sentinel, tap mask of 64 bits
+  if (tile >= 21 && ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB ||
+                     (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kBufOOB || KH * KW > 64))
+    tile = 3;
   switch (tile) {
     case 1: launch_fwd<128, 128>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 2: launch_fwd<128, 64>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    // LDS-DMA pipelined variants (tile code 10 + x: x = 1 128x128, 2 128x64, 3 64x64, 4/5/6 the same at depth 3)
+    case 11: launch_fwd<128, 128, 4>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    case 12: launch_fwd<128, 64, 4>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    case 13: launch_fwd<64, 64, 4>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    case 14: launch_fwd<128, 128, 3>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    case 15: launch_fwd<128, 64, 3>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    case 16: launch_fwd<64, 64, 3>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    // buffer-resource LDS-DMA variants: 2x = depth 3, 3x = depth 4 (x as above)
+    case 21: launch_fwd<128, 128, 3, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    case 22: launch_fwd<128, 64, 3, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    case 23: launch_fwd<64, 64, 3, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    case 31: launch_fwd<128, 128, 4, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    case 32: launch_fwd<128, 64, 4, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    case 33: launch_fwd<64, 64, 4, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     default: launch_fwd<64, 64>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
   }
   return tile;

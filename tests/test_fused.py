@@ -25,7 +25,7 @@ def _bn_ref(y, gamma, beta, mean, var, eps=2e-5):
 
 @pytest.mark.parametrize('shape', [(1, 256, 24, 40, 256, 1, 1, 0), (1, 64, 31, 17, 64, 3, 1, 1),
                                    (2, 128, 14, 14, 512, 1, 1, 0), (1, 1024, 50, 84, 256, 1, 1, 0)])
-@pytest.mark.parametrize('tile,splits', [(3, 1), (3, 4), (0, 0)])
+@pytest.mark.parametrize('tile,splits', [(3, 1), (3, 4), (0, 0), (23, 1), (22, 2)])
 def test_conv_epilogue_residual_bn(cuda, shape, tile, splits):
     from mx_rcnn_amd.ops import need_ext
     N, Cin, H, W, Cout, k, s, p = shape

@@ -1,0 +1,86 @@
+"""Tile / pipeline / split-K sweep of the MFMA implicit-GEMM conv (conv_igemm_fwd) on the
+ResNet-101 C4 @800x1333 shapes (forward and the stride-1 dgrad form), one process, CUDA-event
+timing, numerics checked against torch's conv (fp32 accumulate of the same bf16 operands).
+
+    python tools/microbench/conv_tiles.py [--shapes s3_3x3,s3_1x1a] [--tiles 0,11,12,13] [--splits 1,2,4]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+import torch  # noqa: E402
+import torch.nn.functional as F  # noqa: E402
+
+from mx_rcnn_amd.ops import need_ext  # noqa: E402
+
+SHAPES = {
+    # name: (N, Cin, H, W, Cout, k, stride, pad)
+    's1_3x3': (1, 64, 200, 334, 64, 3, 1, 1),
+    's2_3x3': (1, 128, 100, 167, 128, 3, 1, 1),
+    's2_1x1a': (1, 512, 100, 167, 128, 1, 1, 0),
+    's3_3x3': (1, 256, 50, 84, 256, 3, 1, 1),
+    's3_1x1a': (1, 1024, 50, 84, 256, 1, 1, 0),
+    's3_1x1b': (1, 256, 50, 84, 1024, 1, 1, 0),
+    'rpn_3x3': (1, 1024, 50, 84, 512, 3, 1, 1),
+    's4_3x3': (128, 512, 7, 7, 512, 3, 1, 1),
+    's4_1x1a': (128, 2048, 7, 7, 512, 1, 1, 0),
+    's4_1x1b': (128, 512, 7, 7, 2048, 1, 1, 0),
+}
+
+
+def timeit(fn, iters=20, warm=3):
+    for _ in range(warm):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--shapes', default=','.join(SHAPES))
+    ap.add_argument('--tiles', default='0,1,2,3,11,12,13,14,15,16')
+    ap.add_argument('--splits', default='0,1,2,4,8')
+    args = ap.parse_args()
+    ext = need_ext()
+    torch.manual_seed(0)
+    for name in args.shapes.split(','):
+        n, cin, h, w, cout, k, s, p = SHAPES[name]
+        x = torch.randn(n, cin, h, w, device='cuda').bfloat16().contiguous(memory_format=torch.channels_last)
+        wt = (torch.randn(cout, cin, k, k, device='cuda') / (cin * k * k) ** 0.5).bfloat16().contiguous(
+            memory_format=torch.channels_last)
+        ref = F.conv2d(x.float(), wt.float(), stride=s, padding=p)
+        fl = 2.0 * ref.numel() * cin * k * k
+        res = {'name': name, 'gflop': round(fl / 1e9, 2), 'miopen_us': round(timeit(lambda: F.conv2d(x, wt, stride=s, padding=p)), 1)}
+        best = None
+        for tile in [int(t) for t in args.tiles.split(',')]:
+            for sp in [int(v) for v in args.splits.split(',')]:
+                if tile == 0 and sp != 0:
+                    continue
+                try:
+                    y = ext.conv_igemm_fwd(x, wt, None, s, p, False, tile, sp)[0]
+                except RuntimeError as e:
+                    res['t%d_s%d' % (tile, sp)] = 'err'
+                    continue
+                err = (y.float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-6)
+                if err > 2e-2:
+                    res['t%d_s%d' % (tile, sp)] = 'BAD %.3g' % err
+                    continue
+                us = timeit(lambda: ext.conv_igemm_fwd(x, wt, None, s, p, False, tile, sp))
+                res['t%d_s%d' % (tile, sp)] = round(us, 1)
+                if best is None or us < best[0]:
+                    best = (us, tile, sp)
+        if best:
+            res['best'] = '%.1fus t%d s%d %.0f TF/s' % (best[0], best[1], best[2], fl / best[0] / 1e6)
+        print(json.dumps(res), flush=True)
+
+
+if __name__ == '__main__':
+    main()

@@ -24,6 +24,23 @@ __device__ __forceinline__ void st(void* p, int64_t i, float v, int bf16) {
   else static_cast<float*>(p)[i] = v;
 }
 
+// 8 consecutive bf16 <-> fp32 through one 16-B access (p 16-B aligned)
+__device__ __forceinline__ void ld8_bf16(const uint16_t* p, float* v) {
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[2 * k] = __uint_as_float(w[k] << 16);
+    v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
+  }
+}
+__device__ __forceinline__ void st8_bf16(uint16_t* p, const float* v) {
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) w[k] = (uint32_t)f32_to_bf16(v[2 * k]) | ((uint32_t)f32_to_bf16(v[2 * k + 1]) << 16);
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
 // Wave64 reduction (sum) via DPP-backed shuffles.
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

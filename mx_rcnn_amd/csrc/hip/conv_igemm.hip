@@ -144,6 +144,141 @@ __device__ __forceinline__ void igemm_epilogue(f32x4 (&acc)[TM][TN], int m0, int
   }
 }
 
+// LDS-transposed epilogue (Cout % 8 == 0): the MFMA C/D layout gives each lane 4 rows of ONE
+// column, so a direct epilogue issues 2-byte accesses strided by Cout.  Here the fp32 tile is
+// scattered into LDS ([BM][BN+4], conflict-free for the 16-lane column runs), and every thread
+// then owns 8 consecutive columns of a row: residual / BN-input / dY-add reads, y / y2 stores and
+// fp32 split-K slab writes are 16-B vectors, the per-column constants are computed once per
+// thread, and the BN-backward column sums reduce across the lanes sharing a column group
+// (shuffles), across waves (LDS) and leave the workgroup as one atomic per column and stat.
+template <int BM, int BN, int TM, int TN, int WM, int WN>
+__device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* __restrict__ T, int m0, int n0, int wm,
+                                                   int wn, int lane, int tid, int M, int Cout, const ConvEpi& ep,
+                                                   uint16_t* __restrict__ y, int split, int splits,
+                                                   float* __restrict__ slab) {
+  constexpr int LDT = BN + 4;      // fp32 row stride of the staged tile
+  constexpr int VPR = BN / 8;      // 8-column vectors per row
+  constexpr int NV = BM * VPR / 256;  // vectors per thread
+  __syncthreads();  // every wave is done reading the operand ring
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        T[(wm * WM + i * 16 + (lane >> 4) * 4 + r) * LDT + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  const int cv = tid % VPR;  // this thread's column group (the same for all its vectors)
+  const int n = n0 + cv * 8;
+  const bool ncol = n < Cout;
+  if (splits > 1) {
+    float* sp = slab + (int64_t)split * M * Cout;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int row = (tid + v * 256) / VPR, m = m0 + row;
+      if (m >= M || !ncol) continue;
+      const float4* src = reinterpret_cast<const float4*>(T + row * LDT + cv * 8);
+      float4* dst = reinterpret_cast<float4*>(sp + (int64_t)m * Cout + n);
+      dst[0] = src[0];
+      dst[1] = src[1];
+    }
+    return;
+  }
+  EpiCol ec[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ec[k] = epi_col(ep, ncol ? n + k : 0);
+  if (ep.bnb_x) {
+    float sg[8], sgx[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sg[k] = sgx[k] = 0.f;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int row = (tid + v * 256) / VPR, m = m0 + row;
+      if (m >= M || !ncol) continue;
+      const int64_t e = (int64_t)m * Cout + n;
+      float a[8], xv[8], d[8], rs[8];
+      const float4* src = reinterpret_cast<const float4*>(T + row * LDT + cv * 8);
+      const float4 a0 = src[0], a1 = src[1];
+      a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w; a[4] = a1.x; a[5] = a1.y; a[6] = a1.z; a[7] = a1.w;
+      ld8_bf16(ep.bnb_x + e, xv);
+      if (ep.dadd) {
+        ld8_bf16(ep.dadd + e, d);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a[k] += d[k];
+      }
+      if (ep.residual) ld8_bf16(ep.residual + e, rs);
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float g = (!ep.act_relu || xv[k] * ec[k].s + ec[k].t > 0.f) ? a[k] : 0.f;
+        sg[k] += g;
+        sgx[k] += g * (xv[k] - ec[k].mean) * ec[k].inv;
+        o[k] = g * ec[k].s + (ep.residual ? rs[k] : 0.f);
+      }
+      st8_bf16(y + e, o);
+    }
+    // reduce over the lanes of this wave that share the column group, then over the waves
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+#pragma unroll
+      for (int o = VPR; o < 64; o <<= 1) {
+        sg[k] += __shfl_xor(sg[k], o, 64);
+        sgx[k] += __shfl_xor(sgx[k], o, 64);
+      }
+    }
+    __syncthreads();  // T is reused as [4 waves][BN][2] partials
+    const int wid = tid >> 6;
+    if (lane < VPR) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        T[(wid * BN + cv * 8 + k) * 2] = sg[k];
+        T[(wid * BN + cv * 8 + k) * 2 + 1] = sgx[k];
+      }
+    }
+    __syncthreads();
+    if (tid < BN) {
+      const int col = n0 + tid;
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        a += T[(q * BN + tid) * 2];
+        b += T[(q * BN + tid) * 2 + 1];
+      }
+      if (col < Cout) {
+        if (ep.bnb_dbeta) atomicAdd(ep.bnb_dbeta + col, a);
+        if (ep.bnb_dgamma && !ep.bn_fix_gamma) atomicAdd(ep.bnb_dgamma + col, b);
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int row = (tid + v * 256) / VPR, m = m0 + row;
+    if (m >= M || !ncol) continue;
+    const int64_t e = (int64_t)m * Cout + n;
+    const float4* src = reinterpret_cast<const float4*>(T + row * LDT + cv * 8);
+    const float4 a0 = src[0], a1 = src[1];
+    float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    float rs[8];
+    if (ep.residual) ld8_bf16(ep.residual + e, rs);
+    uint16_t yb[8];
+    float y2v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float t = a[k] + ec[k].bias + (ep.residual ? rs[k] : 0.f);
+      if (ep.relu) t = fmaxf(t, 0.f);
+      yb[k] = f32_to_bf16(t);
+      float q = bf16_to_f32(yb[k]) * ec[k].s + ec[k].t;  // the BN reads the STORED conv output
+      if (ep.act_relu) q = fmaxf(q, 0.f);
+      y2v[k] = q;
+    }
+    *reinterpret_cast<uint4*>(y + e) =
+        make_uint4((uint32_t)yb[0] | ((uint32_t)yb[1] << 16), (uint32_t)yb[2] | ((uint32_t)yb[3] << 16),
+                   (uint32_t)yb[4] | ((uint32_t)yb[5] << 16), (uint32_t)yb[6] | ((uint32_t)yb[7] << 16));
+    if (ep.y2) st8_bf16(ep.y2 + e, y2v);
+  }
+}
+
 template <int BM, int BN>
 __global__ void __launch_bounds__(256)
 conv_igemm_fwd_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
@@ -644,7 +779,12 @@ conv_igemm_buf_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   }
-  igemm_epilogue<TM, TN, WM, WN>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab);
+  static_assert(BM * (BN + 4) * 4 <= S * (BM + BN) * BK * 2, "epilogue tile must fit the operand ring");
+  if (Cout % 8 == 0)
+    igemm_epilogue_lds<BM, BN, TM, TN, WM, WN>(acc, reinterpret_cast<float*>(lds), m0, n0, wm, wn, lane, tid, M, Cout,
+                                               ep, y, split, splits, slab);
+  else
+    igemm_epilogue<TM, TN, WM, WN>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab);
 }
 
 template <int BM, int BN, int S = 0, bool BUF = false>

@@ -507,7 +507,7 @@ void wt_flip_run(const Tensor& table, int64_t n_entries, int64_t total_tiles) {
 }
 
 Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
-                  int64_t splits, c10::optional<Tensor> out) {
+                  int64_t splits, c10::optional<Tensor> out, int64_t variant) {
   CHECK_DEV(dy); CHECK_DEV(x);
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "bf16 only");
   TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) && x.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -535,7 +535,8 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int
   const int r = mxr::conv_wgrad(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
                                 reinterpret_cast<const uint16_t*>(x.data_ptr()),
                                 reinterpret_cast<uint16_t*>(dw.data_ptr()), slab.data_ptr<float>(), NB, H, W, Cin, Ho,
-                                Wo, Cout, (int)KH, (int)KW, (int)stride, (int)pad, sp, acc ? 1 : 0, cur_stream());
+                                Wo, Cout, (int)KH, (int)KW, (int)stride, (int)pad, sp, acc ? 1 : 0, cur_stream(),
+                                (int)variant);
   TORCH_CHECK(r > 0, "conv_wgrad: unsupported shape");
   return dw;
 }
@@ -572,6 +573,6 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("wt_flip_build", &wt_flip_build);
   m.def("wt_flip_run", &wt_flip_run);
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"), py::arg("stride"),
-        py::arg("pad"), py::arg("splits") = 0, py::arg("out") = py::none());
+        py::arg("pad"), py::arg("splits") = 0, py::arg("out") = py::none(), py::arg("variant") = 0);
   m.attr("arch") = "gfx950";
 }

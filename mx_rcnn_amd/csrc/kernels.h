@@ -162,6 +162,6 @@ void conv_wt_flip_multi(const WtFlipEntry* entries, int n_entries, int total_til
 int conv_wgrad_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int* splits_out);
 int conv_wgrad(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab, int NB, int H, int W, int Cin,
                int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int splits, int accumulate,
-               hipStream_t st);
+               hipStream_t st, int variant = 0);
 
 }  // namespace mxr

@@ -310,6 +310,7 @@ def test_conv_igemm_autograd(cuda):
     (2, 128, 13, 9, 192, 3, 2, 1),
     (1, 1024, 50, 84, 512, 3, 1, 1),
     (1, 128, 20, 30, 64, 1, 1, 0),
+    (8, 512, 7, 7, 512, 3, 1, 1),
 ])
 def test_conv_wgrad_vs_fp32(cuda, shape):
     from mx_rcnn_amd.ops import need_ext
@@ -321,11 +322,21 @@ def test_conv_wgrad_vs_fp32(cuda, shape):
     dy = torch.randn(N, Cout, Ho, Wo, generator=g).bfloat16()
     ref = torch.ops.aten.convolution_backward(dy.float(), x.float(), w, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
                                               [False, True, False])[1]
-    for splits in (1, 0):
-        dw = need_ext().conv_wgrad(dy.to(cuda).contiguous(memory_format=torch.channels_last),
-                                   x.to(cuda).contiguous(memory_format=torch.channels_last), k, k, s, p, splits)
-        err = (dw.float().cpu() - ref).abs().max().item()
-        assert err <= 1e-2 * ref.abs().max().item() + 1e-2, (splits, err)
+    dyc = dy.to(cuda).contiguous(memory_format=torch.channels_last)
+    xc = x.to(cuda).contiguous(memory_format=torch.channels_last)
+    tol = 1e-2 * ref.abs().max().item() + 1e-2
+    for variant in (0, 1):  # 0: LDS-DMA kernel (default), 1: register-staged kernel
+        for splits in (1, 0, 3):
+            dw = need_ext().conv_wgrad(dyc, xc, k, k, s, p, splits, variant=variant)
+            err = (dw.float().cpu() - ref).abs().max().item()
+            assert err <= tol, (variant, splits, err)
+        # accumulate into an existing gradient (flat-buffer delivery), direct and split paths
+        for splits in (1, 2):
+            base = (torch.randn(ref.shape, generator=g) * ref.abs().max()).bfloat16()
+            out = base.to(cuda).contiguous(memory_format=torch.channels_last)
+            need_ext().conv_wgrad(dyc, xc, k, k, s, p, splits, out, variant=variant)
+            err = (out.float().cpu() - (ref + base.float())).abs().max().item()
+            assert err <= 2 * tol, ('acc', variant, splits, err)
 
 
 @pytest.mark.gpu

@@ -48,6 +48,7 @@ def main():
     ap.add_argument('--shapes', default=','.join(SHAPES))
     ap.add_argument('--tiles', default='0,1,2,3,11,12,13,14,15,16')
     ap.add_argument('--splits', default='0,1,2,4,8')
+    ap.add_argument('--wgrad', action='store_true', help='sweep conv_wgrad (variant x splits) instead')
     args = ap.parse_args()
     ext = need_ext()
     torch.manual_seed(0)
@@ -58,6 +59,29 @@ def main():
             memory_format=torch.channels_last)
         ref = F.conv2d(x.float(), wt.float(), stride=s, padding=p)
         fl = 2.0 * ref.numel() * cin * k * k
+        if args.wgrad:
+            dy = torch.randn_like(ref).bfloat16().contiguous(memory_format=torch.channels_last)
+            wref = torch.ops.aten.convolution_backward(dy.float(), x.float(), wt.float(), None, [s, s], [p, p], [1, 1],
+                                                       False, [0, 0], 1, [False, True, False])[1]
+            res = {'name': name, 'gflop': round(fl / 1e9, 2), 'miopen_us': round(timeit(
+                lambda: torch.ops.aten.convolution_backward(dy, x, wt, None, [s, s], [p, p], [1, 1], False, [0, 0], 1,
+                                                            [False, True, False])), 1)}
+            best = None
+            for var in (0, 1):
+                for sp in [int(v) for v in args.splits.split(',')]:
+                    dw = ext.conv_wgrad(dy, x, k, k, s, p, sp, variant=var)
+                    err = (dw.float() - wref).abs().max().item() / (wref.abs().max().item() + 1e-6)
+                    key = 'v%d_s%d' % (var, sp)
+                    if err > 2e-2:
+                        res[key] = 'BAD %.3g' % err
+                        continue
+                    us = timeit(lambda: ext.conv_wgrad(dy, x, k, k, s, p, sp, variant=var))
+                    res[key] = round(us, 1)
+                    if best is None or us < best[0]:
+                        best = (us, var, sp)
+            res['best'] = '%.1fus v%d s%d %.0f TF/s' % (best[0], best[1], best[2], fl / best[0] / 1e6)
+            print(json.dumps(res), flush=True)
+            continue
         res = {'name': name, 'gflop': round(fl / 1e9, 2), 'miopen_us': round(timeit(lambda: F.conv2d(x, wt, stride=s, padding=p)), 1)}
         best = None
         for tile in [int(t) for t in args.tiles.split(',')]:

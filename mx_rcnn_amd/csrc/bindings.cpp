@@ -90,6 +90,70 @@ std::vector<Tensor> nms_proposals(const Tensor& boxes, const Tensor& scores, con
   return {rois, out_scores, keep, n_keep};
 }
 
+// ---- fused target sampling ------------------------------------------------------------------
+std::vector<Tensor> anchor_sample(const Tensor& label_pre, const Tensor& targets, const Tensor& keys, int64_t A,
+                                  int64_t H, int64_t W, int64_t num_fg, int64_t batch, std::vector<double> inside_w,
+                                  double pos_weight) {
+  CHECK_DEV(label_pre); CHECK_I32(label_pre); CHECK_CONTIG(label_pre);
+  CHECK_DEV(targets); CHECK_F32(targets); CHECK_CONTIG(targets);
+  CHECK_DEV(keys); CHECK_F32(keys); CHECK_CONTIG(keys);
+  const int B = (int)label_pre.size(0);
+  const int64_t N = H * W * A;
+  TORCH_CHECK(label_pre.numel() == B * N && targets.numel() == B * N * 4 && keys.numel() == B * N, "anchor_sample shapes");
+  TORCH_CHECK(inside_w.size() == 4, "inside_w: 4 values");
+  TORCH_CHECK(num_fg >= 0 && batch >= 0 && num_fg <= 1024 && batch <= 1024, "RPN batch must be <= 1024 anchors");
+  DevGuard g(label_pre.device());
+  auto o = targets.options();
+  Tensor kept = at::empty({B, (N + 31) / 32}, o.dtype(at::kInt));
+  Tensor meta = at::empty({B, 4}, o.dtype(at::kInt));
+  Tensor label = at::empty({B, A * H * W}, o.dtype(at::kInt));
+  Tensor bt = at::empty({B, 4 * A, H, W}, o);
+  Tensor iw = at::empty({B, 4 * A, H, W}, o);
+  Tensor ow = at::empty({B, 4 * A, H, W}, o);
+  const float iwf[4] = {(float)inside_w[0], (float)inside_w[1], (float)inside_w[2], (float)inside_w[3]};
+  mxr::anchor_sample(label_pre.data_ptr<int32_t>(), targets.data_ptr<float>(), keys.data_ptr<float>(), B, (int)A,
+                     (int)H, (int)W, (int)num_fg, (int)batch, iwf, (float)pos_weight,
+                     reinterpret_cast<uint32_t*>(kept.data_ptr<int32_t>()), meta.data_ptr<int32_t>(),
+                     label.data_ptr<int32_t>(), bt.data_ptr<float>(), iw.data_ptr<float>(), ow.data_ptr<float>(),
+                     cur_stream());
+  return {label, bt, iw, ow};
+}
+
+std::vector<Tensor> proposal_sample(const Tensor& rois, const Tensor& gt, const Tensor& n_gt, const Tensor& max_ov,
+                                    const Tensor& argmax, const Tensor& rnd, int64_t R, int64_t F, int64_t C,
+                                    double fg_thresh, double bg_hi, double bg_lo, bool is_train, bool normalize,
+                                    std::vector<double> means, std::vector<double> stds,
+                                    std::vector<double> inside_w) {
+  for (const Tensor* t : {&rois, &gt, &max_ov, &rnd}) {
+    CHECK_DEV((*t)); CHECK_F32((*t)); CHECK_CONTIG((*t));
+  }
+  CHECK_DEV(n_gt); CHECK_I32(n_gt); CHECK_CONTIG(n_gt);
+  CHECK_DEV(argmax); CHECK_I32(argmax); CHECK_CONTIG(argmax);
+  TORCH_CHECK(rois.dim() == 3 && rois.size(2) == 5 && gt.dim() == 3 && gt.size(2) == 5, "rois (B,P,5), gt (B,G,5)");
+  const int B = (int)rois.size(0), P = (int)rois.size(1), G = (int)gt.size(1);
+  TORCH_CHECK(gt.size(0) == B && n_gt.numel() == B && max_ov.numel() == (int64_t)B * P && argmax.numel() == (int64_t)B * P,
+              "proposal_sample batch shapes");
+  TORCH_CHECK(rnd.numel() == (int64_t)B * (2 * (P + G) + R), "rnd must hold B * (2 (P + G) + R) draws");
+  TORCH_CHECK(means.size() == 4 && stds.size() == 4 && inside_w.size() == 4, "means/stds/inside_w: 4 values");
+  DevGuard g(rois.device());
+  auto o = rois.options();
+  Tensor out_rois = at::empty({(int64_t)B * R, 5}, o);
+  Tensor label = at::empty({(int64_t)B * R}, o.dtype(at::kInt));
+  Tensor bt = at::empty({(int64_t)B * R, 4 * C}, o);
+  Tensor iw = at::empty({(int64_t)B * R, 4 * C}, o);
+  Tensor ow = at::empty({(int64_t)B * R, 4 * C}, o);
+  float mf[4], sf[4], wf[4];
+  for (int q = 0; q < 4; ++q) { mf[q] = (float)means[q]; sf[q] = (float)stds[q]; wf[q] = (float)inside_w[q]; }
+  const int r = mxr::proposal_sample(rois.data_ptr<float>(), gt.data_ptr<float>(), n_gt.data_ptr<int32_t>(),
+                                     max_ov.data_ptr<float>(), argmax.data_ptr<int32_t>(), rnd.data_ptr<float>(), B, P,
+                                     G, (int)R, (int)F, (int)C, (float)fg_thresh, (float)bg_hi, (float)bg_lo,
+                                     is_train ? 1 : 0, normalize ? 1 : 0, mf, sf, wf, out_rois.data_ptr<float>(),
+                                     label.data_ptr<int32_t>(), bt.data_ptr<float>(), iw.data_ptr<float>(),
+                                     ow.data_ptr<float>(), cur_stream());
+  TORCH_CHECK(r == 0, "proposal_sample: shape beyond the kernel plan (P + G <= 16384, R - F <= 1024)");
+  return {out_rois, label, bt, iw, ow};
+}
+
 // ---- IoU / assignment ------------------------------------------------------------------
 std::vector<Tensor> iou_max(const Tensor& boxes, int64_t off, const Tensor& gt, const Tensor& n_gt,
                             bool want_gt_max) {
@@ -548,6 +612,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("proposal_decode", &proposal_decode);
   m.def("nms_proposals", &nms_proposals);
   m.def("iou_max", &iou_max);
+  m.def("anchor_sample", &anchor_sample);
+  m.def("proposal_sample", &proposal_sample);
   m.def("anchor_target_assign", &anchor_target_assign);
   m.def("roi_pool_fwd", &roi_pool_fwd);
   m.def("roi_pool_bwd", &roi_pool_bwd);

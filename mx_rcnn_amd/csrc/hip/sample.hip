@@ -1,0 +1,385 @@
+// Fused RPN anchor-target subsampling and R-CNN proposal-target sampling (SURVEY §2.11-B/C;
+// reference `rcnn/minibatch.py:319-395` and `rcnn/rpn/proposal_target.py:135-195`).
+//
+// The torch formulation of these two steps (random-rank argsort per pool, where/gather/one-hot
+// chains) was ~120 tiny launches per training step, each a graph node costing a few
+// microseconds regardless of its work.  Here:
+//
+//   anchor_sample  (1 workgroup / image): fg/bg counts, uniform random subsets without
+//                  replacement (fg to RPN_FG_FRACTION * RPN_BATCH_SIZE, bg to the rest), written
+//                  as a kept-anchor bitmap + number of examples
+//   anchor_output  (grid over anchors): final labels in the reference (a, h, w) order and the
+//                  bbox target / inside / outside weights in (4A, H, W) planes
+//   proposal_sample (1 workgroup / image): gt rows appended to the proposals, fg / bg pools with
+//                  the reference fallbacks, fixed-size fg (with-replacement pad prepended) and bg
+//                  samples, labels zeroed past fg_this, class-specific normalised targets and
+//                  weights (R x 4C)
+//
+// Random subsets: "the k smallest random keys among the pool" (ties by index) is a uniform
+// k-subset.  It is found without sorting the pool: collect the pool members whose key is below
+// a threshold t set for ~k + 4 sqrt(k) + 32 expected hits, then rank the (few hundred) hits by
+// counting in LDS; t is widened / narrowed in the rare rounds that catch too few / too many.
+// The keys are a torch.rand draw (graph-safe Philox offsets), so results are reproducible for a
+// fixed generator state; the RNG stream is not numpy's (documented deviation).
+#include "common.h"
+#include "../kernels.h"
+
+namespace mxr {
+
+constexpr int SEL_CAP = 1024;  // LDS candidate list (one element per thread when ranking)
+
+struct SelScratch {
+  float key[SEL_CAP];
+  int idx[SEL_CAP];
+  int cnt;
+};
+
+// Selects take = min(k, count) pool members with the smallest (key, index); writes them in
+// ascending key order to out[0..take).  count = |pool|.  take == count needs count <= SEL_CAP.
+// Block-uniform arguments; all threads must call.
+template <class Pool, class Key>
+__device__ int select_smallest(int n, int count, int k, Pool pool, Key key, SelScratch& s, int* out) {
+  const int take = min(k, count);
+  if (take <= 0) return 0;
+  float t = take >= count ? 2.f : fminf(1.f, ((float)take + 4.f * sqrtf((float)take) + 32.f) / (float)count);
+  for (int round = 0; round < 48; ++round) {
+    if (threadIdx.x == 0) s.cnt = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      if (!pool(i)) continue;
+      const float kv = key(i);
+      if (kv < t) {
+        const int p = atomicAdd(&s.cnt, 1);
+        if (p < SEL_CAP) {
+          s.key[p] = kv;
+          s.idx[p] = i;
+        }
+      }
+    }
+    __syncthreads();
+    const int c = s.cnt;
+    if (c >= take && c <= SEL_CAP) {
+      for (int e = threadIdx.x; e < c; e += blockDim.x) {
+        const float ke = s.key[e];
+        const int ie = s.idx[e];
+        int r = 0;
+        for (int j = 0; j < c; ++j) {
+          const float kj = s.key[j];
+          r += (kj < ke) || (kj == ke && s.idx[j] < ie);
+        }
+        if (r < take) out[r] = ie;
+      }
+      __syncthreads();
+      return take;
+    }
+    __syncthreads();  // every thread has read s.cnt before the next round resets it
+    if (c < take) t = t >= 1.f ? 2.f : fminf(1.f, t * 2.f);
+    else t *= fmaxf(0.05f, ((float)take + 4.f * sqrtf((float)take) + 32.f) / (float)c);
+  }
+  return 0;  // not reached for key distributions in [0, 1)
+}
+
+// ------------------------------------------------------------------------------- anchors
+// label_pre (B, N) int32 in {-1, 0, 1}; keys (B, N) uniform [0,1).  Writes kept (B, NW) uint32
+// bitmap (bit = anchor selected), meta (B, 4) int32 = [all_fg, all_bg, n_fg, n_bg].
+__global__ void __launch_bounds__(1024)
+anchor_sample_kernel(const int32_t* __restrict__ label_pre, const float* __restrict__ keys, int N, int num_fg,
+                     int batch, uint32_t* __restrict__ kept, int32_t* __restrict__ meta) {
+  __shared__ SelScratch s;
+  __shared__ int s_acc;
+  __shared__ int sel[SEL_CAP];
+  const int b = blockIdx.x;
+  const int32_t* lab = label_pre + (int64_t)b * N;
+  const float* key = keys + (int64_t)b * N;
+  const int NW = (N + 31) / 32;
+  uint32_t* kb = kept + (int64_t)b * NW;
+  for (int w = threadIdx.x; w < NW; w += blockDim.x) kb[w] = 0u;
+  int nfg = 0, nbg = 0;
+  {
+    int cf = 0, cb = 0;
+    for (int i = threadIdx.x; i < N; i += blockDim.x) {
+      const int l = lab[i];
+      cf += l == 1;
+      cb += l == 0;
+    }
+    if (threadIdx.x == 0) s_acc = 0;
+    __syncthreads();
+    atomicAdd(&s_acc, cf);
+    __syncthreads();
+    nfg = s_acc;
+    __syncthreads();
+    if (threadIdx.x == 0) s_acc = 0;
+    __syncthreads();
+    atomicAdd(&s_acc, cb);
+    __syncthreads();
+    nbg = s_acc;
+    __syncthreads();
+  }
+  const bool all_fg = nfg <= num_fg;
+  int n_fg = nfg;
+  if (!all_fg) {
+    n_fg = select_smallest(N, nfg, num_fg, [&](int i) { return lab[i] == 1; }, [&](int i) { return key[i]; }, s, sel);
+    for (int e = threadIdx.x; e < n_fg; e += blockDim.x) atomicOr(kb + (sel[e] >> 5), 1u << (sel[e] & 31));
+    __syncthreads();
+  }
+  const int k_bg = max(batch - n_fg, 0);
+  const bool all_bg = nbg <= k_bg;
+  int n_bg = nbg;
+  if (!all_bg) {
+    n_bg = select_smallest(N, nbg, k_bg, [&](int i) { return lab[i] == 0; }, [&](int i) { return key[i]; }, s, sel);
+    for (int e = threadIdx.x; e < n_bg; e += blockDim.x) atomicOr(kb + (sel[e] >> 5), 1u << (sel[e] & 31));
+  }
+  if (threadIdx.x == 0) {
+    meta[b * 4 + 0] = all_fg;
+    meta[b * 4 + 1] = all_bg;
+    meta[b * 4 + 2] = n_fg;
+    meta[b * 4 + 3] = n_bg;
+  }
+}
+
+// One thread per (image, anchor a, position hw): reads the (h, w, a)-ordered assignment, writes
+// label (B, A*H*W) and the (B, 4A, H, W) target / inside / outside planes.
+__global__ void __launch_bounds__(256)
+anchor_output_kernel(const int32_t* __restrict__ label_pre, const float* __restrict__ targets,
+                     const uint32_t* __restrict__ kept, const int32_t* __restrict__ meta, int B, int A, int HW,
+                     float iw0, float iw1, float iw2, float iw3, float pos_weight, int32_t* __restrict__ label,
+                     float* __restrict__ bbox_target, float* __restrict__ inside, float* __restrict__ outside) {
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t per = (int64_t)A * HW;
+  if (t >= (int64_t)B * per) return;
+  const int b = (int)(t / per);
+  const int r = (int)(t % per);
+  const int a = r / HW, hw = r % HW;
+  const int N = HW * A;
+  const int i = hw * A + a;
+  const int NW = (N + 31) / 32;
+  const int l = label_pre[(int64_t)b * N + i];
+  const int32_t* m = meta + b * 4;
+  const bool bit = (kept[(int64_t)b * NW + (i >> 5)] >> (i & 31)) & 1u;
+  int lo = -1;
+  if (l == 1 && (m[0] || bit)) lo = 1;
+  else if (l == 0 && (m[1] || bit)) lo = 0;
+  label[(int64_t)b * per + r] = lo;
+  const float4 tg = *reinterpret_cast<const float4*>(targets + ((int64_t)b * N + i) * 4);
+  float pw, nw;
+  if (pos_weight < 0.f) {
+    const int ne = max(m[2] + m[3], 1);
+    pw = nw = 1.f / (float)ne;
+  } else {
+    pw = pos_weight / (float)max(m[2], 1);
+    nw = (1.f - pos_weight) / (float)max(m[3], 1);
+  }
+  const float ow = lo == 1 ? pw : (lo == 0 ? nw : 0.f);
+  const float fgw = lo == 1 ? 1.f : 0.f;
+  const float tv[4] = {tg.x, tg.y, tg.z, tg.w};
+  const float iw[4] = {iw0, iw1, iw2, iw3};
+  const int64_t base = ((int64_t)b * 4 * A + 4 * a) * HW + hw;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    bbox_target[base + (int64_t)c * HW] = tv[c];
+    inside[base + (int64_t)c * HW] = fgw * iw[c];
+    outside[base + (int64_t)c * HW] = ow;
+  }
+}
+
+void anchor_sample(const int32_t* label_pre, const float* targets, const float* keys, int B, int A, int H, int W,
+                   int num_fg, int batch, const float* inside_w, float pos_weight, uint32_t* kept_ws,
+                   int32_t* meta_ws, int32_t* label, float* bbox_target, float* inside, float* outside,
+                   hipStream_t st) {
+  if (B == 0) return;
+  const int N = H * W * A;
+  anchor_sample_kernel<<<B, 1024, 0, st>>>(label_pre, keys, N, num_fg, batch, kept_ws, meta_ws);
+  const int64_t total = (int64_t)B * N;
+  anchor_output_kernel<<<div_up(total, 256), 256, 0, st>>>(label_pre, targets, kept_ws, meta_ws, B, A, H * W,
+                                                           inside_w[0], inside_w[1], inside_w[2], inside_w[3],
+                                                           pos_weight, label, bbox_target, inside, outside);
+}
+
+// ------------------------------------------------------------------------------- proposals
+// rois (B, P, 5), gt (B, G, 5) (rows >= n_gt[b] padding), max_ov / argmax (B, P) of the proposal
+// rows vs the image's gt (HIP iou_max), rnd (B, 2M + 2R') uniform [0,1) with M = P + G.
+// Outputs: out_rois (B*R, 5), label (B*R) int32, bbox_target / inside / outside (B*R, 4C).
+constexpr int PT_MAX_ROWS = 16384;  // LDS row arrays: 16384 x 8 B = 128 KB
+
+struct PtParams {
+  int P, G, R, F, C;
+  float fg_thresh, bg_hi, bg_lo;
+  int is_train, normalize;
+  float means[4], stds[4], iw[4];
+};
+
+__global__ void __launch_bounds__(1024)
+proposal_sample_kernel(const float* __restrict__ rois, const float* __restrict__ gt, const int32_t* __restrict__ n_gt,
+                       const float* __restrict__ max_ov_p, const int32_t* __restrict__ argmax_p,
+                       const float* __restrict__ rnd, const PtParams prm, float* __restrict__ out_rois,
+                       int32_t* __restrict__ out_label, float* __restrict__ bbox_target, float* __restrict__ inside,
+                       float* __restrict__ outside) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  const int P = prm.P, G = prm.G, R = prm.R, F = prm.F, C = prm.C;
+  const int M = P + G;
+  float* s_ov = reinterpret_cast<float*>(smem);                    // [M]
+  int* s_am = reinterpret_cast<int*>(s_ov + M);                    // [M]
+  SelScratch& s = *reinterpret_cast<SelScratch*>(s_am + M);
+  int* sel_fg = reinterpret_cast<int*>(&s + 1);                    // [F]
+  int* sel_bg = sel_fg + F;                                        // [R - F]
+  int* keep = sel_bg + (R - F);                                    // [R]
+  float* s_t = reinterpret_cast<float*>(keep + R);                 // [R][4]
+  int* s_lab = reinterpret_cast<int*>(s_t + 4 * R);                // [R]
+  int* s_acc = s_lab + R;
+  const int b = blockIdx.x;
+  const int ng = n_gt[b];
+  const float* gb = gt + (int64_t)b * G * 5;
+  const float* rb = rois + (int64_t)b * P * 5;
+  for (int i = threadIdx.x; i < P; i += blockDim.x) {
+    s_ov[i] = max_ov_p[(int64_t)b * P + i];
+    s_am[i] = argmax_p[(int64_t)b * P + i];
+  }
+  for (int g = threadIdx.x; g < G; g += blockDim.x) {  // gt rows vs gt (first max, like numpy)
+    float best = 0.f;
+    int bi = 0;
+    if (g < ng) {
+      const float* q = gb + g * 5;
+      const float qa = (q[2] - q[0] + 1.f) * (q[3] - q[1] + 1.f);
+      best = -1.f;
+      for (int j = 0; j < ng; ++j) {
+        const float* o = gb + j * 5;
+        const float oa = (o[2] - o[0] + 1.f) * (o[3] - o[1] + 1.f);
+        const float v = iou_plus1(q[0], q[1], q[2], q[3], qa, o[0], o[1], o[2], o[3], oa);
+        if (v > best) {
+          best = v;
+          bi = j;
+        }
+      }
+    }
+    s_ov[P + g] = best;
+    s_am[P + g] = bi;
+  }
+  __syncthreads();
+  auto valid = [&](int i) { return i < P || (i - P) < ng; };
+  auto is_fg = [&](int i) { return valid(i) && s_ov[i] >= prm.fg_thresh; };
+  auto is_bg0 = [&](int i) { return valid(i) && s_ov[i] < prm.bg_hi && s_ov[i] >= prm.bg_lo; };
+  auto is_bgfb = [&](int i) { return valid(i) && s_ov[i] < prm.bg_hi + 0.2f && s_ov[i] >= 0.f; };
+  int nfg = 0, nbg0 = 0, nbgfb = 0, nval = 0;
+  {
+    int a0 = 0, a1 = 0, a2 = 0, a3 = 0;
+    for (int i = threadIdx.x; i < M; i += blockDim.x) {
+      a0 += is_fg(i);
+      a1 += is_bg0(i);
+      a2 += is_bgfb(i);
+      a3 += valid(i);
+    }
+    int* acc4 = s_acc;  // 4 counters
+    if (threadIdx.x < 4) acc4[threadIdx.x] = 0;
+    __syncthreads();
+    if (a0) atomicAdd(acc4 + 0, a0);
+    if (a1) atomicAdd(acc4 + 1, a1);
+    if (a2) atomicAdd(acc4 + 2, a2);
+    if (a3) atomicAdd(acc4 + 3, a3);
+    __syncthreads();
+    nfg = acc4[0];
+    nbg0 = acc4[1];
+    nbgfb = acc4[2];
+    nval = acc4[3];
+    __syncthreads();
+  }
+  const bool bg_use_fb = prm.is_train && nbg0 == 0;
+  const int nbg = bg_use_fb ? nbgfb : nbg0;
+  const bool fg_any = nfg > 0, bg_any = nbg > 0;
+  auto fg_pool = [&](int i) { return fg_any ? is_fg(i) : valid(i); };
+  auto bg_pool = [&](int i) { return bg_any ? (bg_use_fb ? is_bgfb(i) : is_bg0(i)) : valid(i); };
+  const float* kf = rnd + (int64_t)b * (2 * M + R);
+  const float* kg = kf + M;
+  const float* ur = kg + M;  // R pad draws: [0, F) fg, [F, R) bg
+  const int cf = fg_any ? nfg : nval, cb = bg_any ? nbg : nval;
+  const int tf = select_smallest(M, cf, F, fg_pool, [&](int i) { return kf[i]; }, s, sel_fg);
+  const int tb = select_smallest(M, cb, R - F, bg_pool, [&](int i) { return kg[i]; }, s, sel_bg);
+  // sample_slots: [0, pad) with-replacement picks from the sample, [pad, n) the sample in key order
+  for (int j = threadIdx.x; j < R; j += blockDim.x) {
+    const bool f = j < F;
+    const int n = f ? F : R - F, take = f ? tf : tb, jj = f ? j : j - F;
+    const int* sl = f ? sel_fg : sel_bg;
+    const int pad = n - take;
+    int idx = 0;
+    if (take > 0) {
+      if (jj < pad) idx = sl[min((int)(ur[j] * (float)take), take - 1)];
+      else idx = sl[jj - pad];
+    }
+    keep[j] = idx;
+  }
+  __syncthreads();
+  const int fg_this = min(nfg, F);
+  for (int j = threadIdx.x; j < R; j += blockDim.x) {
+    const int idx = keep[j];
+    float bx[5];
+    if (idx < P) {
+      for (int q = 0; q < 5; ++q) bx[q] = rb[idx * 5 + q];
+    } else {
+      bx[0] = (float)b;
+      for (int q = 0; q < 4; ++q) bx[q + 1] = gb[(idx - P) * 5 + q];
+    }
+    const int am = s_am[idx];
+    const float* gs = gb + min(am, max(G - 1, 0)) * 5;
+    int lab = (G > 0 && j < fg_this) ? (int)gs[4] : 0;
+    float* ro = out_rois + ((int64_t)b * R + j) * 5;
+    for (int q = 0; q < 5; ++q) ro[q] = bx[q];
+    out_label[(int64_t)b * R + j] = lab;
+    // bbox_transform(ex = roi, gt = assigned gt), optionally (t - mean) / std; zero unless fg
+    float t4[4] = {0.f, 0.f, 0.f, 0.f};
+    if (lab > 0 && G > 0) {
+      const float ew = bx[3] - bx[1] + 1.f, eh = bx[4] - bx[2] + 1.f;
+      const float ex = bx[1] + 0.5f * (ew - 1.f), ey = bx[2] + 0.5f * (eh - 1.f);
+      const float gw = gs[2] - gs[0] + 1.f, gh = gs[3] - gs[1] + 1.f;
+      const float gx = gs[0] + 0.5f * (gw - 1.f), gy = gs[1] + 0.5f * (gh - 1.f);
+      t4[0] = (gx - ex) / (ew + 1e-14f);
+      t4[1] = (gy - ey) / (eh + 1e-14f);
+      t4[2] = logf(gw / ew);
+      t4[3] = logf(gh / eh);
+      if (prm.normalize)
+        for (int q = 0; q < 4; ++q) t4[q] = (t4[q] - prm.means[q]) / prm.stds[q];
+    }
+    for (int q = 0; q < 4; ++q) s_t[j * 4 + q] = t4[q];
+    s_lab[j] = lab;
+  }
+  __syncthreads();
+  const int C4 = 4 * C;
+  const int64_t off = (int64_t)b * R * C4;
+  for (int e = threadIdx.x; e < R * C4; e += blockDim.x) {
+    const int j = e / C4, col = e % C4;
+    const int lab = s_lab[j];
+    const bool hit = lab > 0 && (col >> 2) == lab;
+    const float iwv = hit ? prm.iw[col & 3] : 0.f;
+    bbox_target[off + e] = hit ? s_t[j * 4 + (col & 3)] : 0.f;
+    inside[off + e] = iwv;
+    outside[off + e] = iwv > 0.f ? 1.f : 0.f;
+  }
+}
+
+size_t proposal_sample_lds(int P, int G, int R, int F) {
+  const int M = P + G;
+  return (size_t)M * 8 + sizeof(SelScratch) + (size_t)(F + (R - F) + R) * 4 + (size_t)R * 16 + (size_t)R * 4 + 32;
+}
+
+int proposal_sample(const float* rois, const float* gt, const int32_t* n_gt, const float* max_ov, const int32_t* argmax,
+                    const float* rnd, int B, int P, int G, int R, int F, int C, float fg_thresh, float bg_hi,
+                    float bg_lo, int is_train, int normalize, const float* means, const float* stds,
+                    const float* inside_w, float* out_rois, int32_t* out_label, float* bbox_target, float* inside,
+                    float* outside, hipStream_t st) {
+  if (P + G > PT_MAX_ROWS || F > SEL_CAP || R - F > SEL_CAP || F < 0 || F > R) return -1;
+  const size_t lds = proposal_sample_lds(P, G, R, F);
+  if (lds > 160 * 1024) return -1;
+  if (B == 0) return 0;
+  PtParams prm;
+  prm.P = P; prm.G = G; prm.R = R; prm.F = F; prm.C = C;
+  prm.fg_thresh = fg_thresh; prm.bg_hi = bg_hi; prm.bg_lo = bg_lo;
+  prm.is_train = is_train; prm.normalize = normalize;
+  for (int q = 0; q < 4; ++q) {
+    prm.means[q] = means[q];
+    prm.stds[q] = stds[q];
+    prm.iw[q] = inside_w[q];
+  }
+  proposal_sample_kernel<<<B, 1024, lds, st>>>(rois, gt, n_gt, max_ov, argmax, rnd, prm, out_rois, out_label,
+                                               bbox_target, inside, outside);
+  return 0;
+}
+
+}  // namespace mxr

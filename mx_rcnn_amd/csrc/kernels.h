@@ -50,6 +50,23 @@ void anchor_target_assign(const float* base_anchors, int A, int H, int W, float 
                           float* max_ov, int32_t* argmax, float* gt_max,
                           int32_t* label, float* targets, hipStream_t st);
 
+// ---- fused target sampling (sample.hip) ------------------------------------
+// RPN: label_pre (B, N=H*W*A) in (h, w, a) order from anchor_target_assign, targets (B, N, 4), keys
+// (B, N) uniform [0,1).  Workspaces: kept (B, ceil(N/32)) uint32, meta (B, 4) int32.  Outputs in the
+// reference layout: label (B, A*H*W), bbox_target / inside / outside (B, 4A, H, W).
+void anchor_sample(const int32_t* label_pre, const float* targets, const float* keys, int B, int A, int H, int W,
+                   int num_fg, int batch, const float* inside_w, float pos_weight, uint32_t* kept_ws,
+                   int32_t* meta_ws, int32_t* label, float* bbox_target, float* inside, float* outside,
+                   hipStream_t st);
+// R-CNN: rois (B, P, 5), gt (B, G, 5), n_gt (B), max_ov / argmax (B, P) vs gt, rnd (B, 2(P+G)+R).
+// Returns -1 when the shape exceeds the kernel's LDS plan.
+size_t proposal_sample_lds(int P, int G, int R, int F);
+int proposal_sample(const float* rois, const float* gt, const int32_t* n_gt, const float* max_ov, const int32_t* argmax,
+                    const float* rnd, int B, int P, int G, int R, int F, int C, float fg_thresh, float bg_hi,
+                    float bg_lo, int is_train, int normalize, const float* means, const float* stds,
+                    const float* inside_w, float* out_rois, int32_t* out_label, float* bbox_target, float* inside,
+                    float* outside, hipStream_t st);
+
 // ---- RoI pooling (roi_pool.hip) -------------------------------------------
 // feat NHWC (B, H, W, C) bf16 or fp32; rois (R, 5); out (R, PH, PW, C); argmax (R, PH, PW, C) int32
 // holding h*W + w (or -1).

@@ -7,6 +7,7 @@ inside anchors, label rules, encode); fg/bg subsampling is a device random-rank 
 Output layout matches the reference: label (B, A*H*W) in (a, h, w) order; bbox_target /
 inside / outside weights (B, 4A, H, W).
 """
+import numpy as np
 import torch
 
 from ..config import config as _global_cfg
@@ -68,18 +69,25 @@ def anchor_target(feat_shape, gt_boxes, n_gt, im_info, feat_stride=16, scales=(8
     B = gt_boxes.shape[0]
     n_gt = n_gt.to(torch.int32).contiguous()
     with torch.no_grad():
+        num_fg = int(cfg.TRAIN.RPN_FG_FRACTION * cfg.TRAIN.RPN_BATCH_SIZE)
         if gt_boxes.is_cuda:
             C = need_ext()
             label, targets, _, _ = C.anchor_target_assign(
                 base, H, W, float(feat_stride), im_info.float().contiguous(), int(allowed_border),
                 gt_boxes.float().contiguous(), n_gt, float(cfg.TRAIN.RPN_NEGATIVE_OVERLAP),
                 float(cfg.TRAIN.RPN_POSITIVE_OVERLAP), bool(cfg.TRAIN.RPN_CLOBBER_POSITIVES))
+            # fused subsampling + weights + reference layout (csrc/hip/sample.hip): 3 launches
+            keys = torch.rand(label.shape, device=dev, generator=generator)
+            iw = [float(v) for v in np.asarray(cfg.TRAIN.RPN_BBOX_INSIDE_WEIGHTS, dtype=np.float64).ravel()[:4]]
+            lab, bt, inside, outside = C.anchor_sample(label, targets.contiguous(), keys, A, H, W, num_fg,
+                                                       int(cfg.TRAIN.RPN_BATCH_SIZE), iw,
+                                                       float(cfg.TRAIN.RPN_POSITIVE_WEIGHT))
+            return {'label': lab, 'bbox_target': bt, 'bbox_inside_weight': inside, 'bbox_outside_weight': outside}
         else:
             label, targets = _assign_ref(H, W, base, feat_stride, im_info, allowed_border, gt_boxes, n_gt,
                                          cfg.TRAIN.RPN_NEGATIVE_OVERLAP, cfg.TRAIN.RPN_POSITIVE_OVERLAP,
                                          cfg.TRAIN.RPN_CLOBBER_POSITIVES)
         # subsample: fg to FG_FRACTION*BATCH, bg to BATCH - #fg (rcnn/minibatch.py:319-334)
-        num_fg = int(cfg.TRAIN.RPN_FG_FRACTION * cfg.TRAIN.RPN_BATCH_SIZE)
         fg = label == 1
         fg_keep = keep_random(fg, num_fg, generator)
         label = torch.where(fg & ~fg_keep, torch.full_like(label, -1), label)

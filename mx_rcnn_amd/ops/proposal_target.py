@@ -28,6 +28,22 @@ def proposal_target(rois, gt_boxes, n_gt, num_classes, cfg=None, is_train=True, 
         F = int(round(cfg.TRAIN.FG_FRACTION * R))
         gtf = gt_boxes.float()
         n_gt = n_gt.to(torch.int32)
+        if rois.is_cuda:
+            # fused sampling + targets (csrc/hip/sample.hip): iou_max + one draw + one kernel
+            from ._ext import need_ext
+            rf = rois.float().contiguous()
+            max_ov, argmax = iou_max(rf, gtf, n_gt, off=1)
+            F = int(round(cfg.TRAIN.FG_FRACTION * R))
+            rnd = torch.rand(B, 2 * (P + G) + R, device=dev, generator=generator)
+            out = need_ext().proposal_sample(
+                rf, gtf.contiguous(), n_gt.contiguous(), max_ov.contiguous(), argmax.contiguous(), rnd, R, F,
+                int(num_classes), float(cfg.TRAIN.FG_THRESH), float(cfg.TRAIN.BG_THRESH_HI),
+                float(cfg.TRAIN.BG_THRESH_LO), bool(is_train), bool(cfg.TRAIN.BBOX_NORMALIZATION_PRECOMPUTED),
+                [float(v) for v in np.asarray(cfg.TRAIN.BBOX_MEANS, dtype=np.float64).ravel()[:4]],
+                [float(v) for v in np.asarray(cfg.TRAIN.BBOX_STDS, dtype=np.float64).ravel()[:4]],
+                [float(v) for v in np.asarray(cfg.TRAIN.BBOX_INSIDE_WEIGHTS, dtype=np.float64).ravel()[:4]])
+            return {'rois': out[0], 'label': out[1], 'bbox_target': out[2], 'bbox_inside_weight': out[3],
+                    'bbox_outside_weight': out[4]}
         bidx = torch.arange(B, device=dev, dtype=torch.float32)[:, None, None].expand(B, G, 1)
         all_rois = torch.cat([rois.float(), torch.cat([bidx, gtf[..., :4]], dim=-1)], dim=1).contiguous()
         M = P + G

@@ -222,3 +222,91 @@ def test_proposal_target_gpu(cuda):
         assert nfg >= 1 and torch.all(lab[b, nfg:] == 0)
         assert torch.all(r[b, :, 0] == b)
     assert torch.isfinite(out['bbox_target']).all()
+
+
+@pytest.mark.gpu
+def test_proposal_sample_fused_semantics(cuda):
+    """Fused HIP proposal-target sampling (csrc/hip/sample.hip): structure, pools, targets and
+    weights recomputed independently on the host from the returned RoIs."""
+    cfg = snapshot()
+    cfg.TRAIN.BBOX_NORMALIZATION_PRECOMPUTED = True
+    cfg.TRAIN.BG_THRESH_LO = 0.0
+    g = torch.Generator().manual_seed(5)
+    P, C = 3000, 21
+    rois = torch.zeros(3, P, 5)
+    for b in range(3):
+        rois[b, :, 0] = b
+        rois[b, :, 1:] = rand_boxes(g, P, 700)
+    gt = torch.full((3, 4, 5), -1.0)
+    gt[0, :3] = torch.tensor([[20., 30, 120, 140, 5], [150, 40, 300, 200, 2], [400, 400, 600, 500, 9]])
+    gt[1, :1] = torch.tensor([[50., 60, 350, 300, 7]])
+    n_gt = torch.tensor([3, 1, 0])  # image 2: no gt -> no fg, labels all 0
+    out = ops.proposal_target(rois.to(cuda), gt.to(cuda), n_gt.to(cuda), C, cfg=cfg)
+    lab = out['label'].cpu().reshape(3, 128)
+    r = out['rois'].cpu().reshape(3, 128, 5)
+    bt = out['bbox_target'].cpu().reshape(3, 128, 4 * C)
+    iw = out['bbox_inside_weight'].cpu().reshape(3, 128, 4 * C)
+    ow = out['bbox_outside_weight'].cpu().reshape(3, 128, 4 * C)
+    means, stds = torch.tensor(cfg.TRAIN.BBOX_MEANS), torch.tensor(cfg.TRAIN.BBOX_STDS)
+    for b in range(3):
+        ng = int(n_gt[b])
+        assert torch.all(r[b, :, 0] == b)
+        nfg = int((lab[b] > 0).sum())
+        assert torch.all(lab[b, nfg:] == 0) and nfg <= 32
+        if ng == 0:
+            assert nfg == 0 and torch.all(bt[b] == 0)
+            continue
+        assert nfg >= 1
+        ov = ops.box_iou(r[b, :, 1:], gt[b, :ng, :4])
+        mo, am = ov.max(1)
+        assert torch.all(mo[:nfg] >= 0.5) and torch.all(mo[32:] < 0.5)  # fg slots / bg slots
+        assert torch.equal(lab[b, :nfg].long(), gt[b, am[:nfg], 4].long())
+        t = ops.bbox_transform(r[b, :nfg, 1:], gt[b, am[:nfg], :4])
+        t = (t - means) / stds
+        cols = lab[b, :nfg].long() * 4
+        got = torch.stack([bt[b, j, cols[j]:cols[j] + 4] for j in range(nfg)])
+        assert torch.allclose(got, t.float(), atol=1e-4, rtol=1e-4)
+        assert torch.equal(iw[b].sum(1), (lab[b] > 0).float() * 4)
+        assert torch.equal(ow[b], (iw[b] > 0).float())
+        assert torch.allclose(bt[b].abs().sum(), got.abs().sum(), rtol=1e-5)  # nothing else is set
+
+
+@pytest.mark.gpu
+def test_anchor_sample_fused_counts_and_uniformity(cuda):
+    """Fused RPN subsampling: exact counts, labels only from the pre-sampling pools, reference
+    weights, and uniform selection frequency over many draws."""
+    H, W = 38, 50
+    gt = torch.full((1, 4, 5), -1.0)
+    gt[0, :4, :4] = torch.tensor([[20., 30, 220, 240], [300, 100, 500, 300], [50, 400, 300, 590], [600, 50, 780, 260]])
+    gt[0, :4, 4] = 1
+    n_gt = torch.tensor([4], dtype=torch.int32)
+    im_info = torch.tensor([[600.0, 800.0, 1.0]])
+    base = ops.base_anchors(16, (4, 8, 16, 32), (0.5, 1, 2))
+    from mx_rcnn_amd.ops import need_ext
+    pre, _, _, _ = need_ext().anchor_target_assign(base.to(cuda), H, W, 16.0, im_info.to(cuda), 0, gt.to(cuda),
+                                                    n_gt.to(cuda), 0.3, 0.7, False)
+    A = 12
+    pre_ahw = pre.cpu().reshape(1, H, W, A).permute(0, 3, 1, 2).reshape(1, -1)
+    nfg_pre, nbg_pre = int((pre_ahw == 1).sum()), int((pre_ahw == 0).sum())
+    gen = torch.Generator(device=cuda).manual_seed(0)
+    hits = torch.zeros(pre_ahw.shape[1])
+    trials = 200
+    for _ in range(trials):
+        out = ops.anchor_target((H, W), gt.to(cuda), n_gt.to(cuda), im_info.to(cuda), scales=(4, 8, 16, 32),
+                                generator=gen)
+        lab = out['label'].cpu()
+        nf, nb = int((lab == 1).sum()), int((lab == 0).sum())
+        assert nf == min(nfg_pre, 128) and nb == min(nbg_pre, 256 - nf)
+        assert torch.all(pre_ahw[lab == 1] == 1) and torch.all(pre_ahw[lab == 0] == 0)
+        ow = out['bbox_outside_weight'].cpu()
+        assert torch.allclose(ow.sum(), torch.tensor(4.0), atol=1e-4)  # 4 coords x (1 / num_examples) each
+        hits += (lab == 0).float()[0]
+    # every bg-pool anchor is picked with probability nb / nbg_pre: mean hit rate over the pool
+    bg_pool = (pre_ahw[0] == 0)
+    rate = hits[bg_pool] / trials
+    expect = min(nbg_pre, 256 - min(nfg_pre, 128)) / nbg_pre
+    assert abs(rate.mean().item() - expect) < 0.1 * expect
+    # no anchor is systematically favoured (first vs second half of the pool by index)
+    idx = torch.nonzero(bg_pool).flatten()
+    h1, h2 = rate[: len(idx) // 2].mean().item(), rate[len(idx) // 2:].mean().item()
+    assert abs(h1 - h2) < 0.15 * expect

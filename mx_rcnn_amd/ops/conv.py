@@ -21,7 +21,7 @@ import torch.nn.functional as F
 from . import grad_sink
 from ._ext import need_ext
 
-GEMM_1X1_MIN_M = 16384
+GEMM_1X1_MIN_M = 1 << 40  # the LDS-DMA igemm kernel beats hipBLASLt on every trunk 1x1 shape (tools/microbench/conv_tiles.py)
 
 
 def igemm_enabled():

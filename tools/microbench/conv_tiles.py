@@ -27,6 +27,9 @@ SHAPES = {
     's4_3x3': (128, 512, 7, 7, 512, 3, 1, 1),
     's4_1x1a': (128, 2048, 7, 7, 512, 1, 1, 0),
     's4_1x1b': (128, 512, 7, 7, 2048, 1, 1, 0),
+    's1_1x1a': (1, 256, 200, 334, 64, 1, 1, 0),
+    's1_1x1b': (1, 64, 200, 334, 256, 1, 1, 0),
+    's2_1x1b': (1, 128, 100, 167, 512, 1, 1, 0),
 }
 
 
@@ -83,6 +86,10 @@ def main():
             print(json.dumps(res), flush=True)
             continue
         res = {'name': name, 'gflop': round(fl / 1e9, 2), 'miopen_us': round(timeit(lambda: F.conv2d(x, wt, stride=s, padding=p)), 1)}
+        if k == 1 and s == 1:
+            x2 = x.permute(0, 2, 3, 1).reshape(-1, cin)
+            w2 = wt.reshape(cout, cin)
+            res['hipblaslt_us'] = round(timeit(lambda: F.linear(x2, w2)), 1)
         best = None
         for tile in [int(t) for t in args.tiles.split(',')]:
             for sp in [int(v) for v in args.splits.split(',')]:

@@ -127,11 +127,12 @@ def main():
     imgs = args.ims_per_gpu * world * args.steps
     value = imgs / elapsed
     if rank == 0:
-        rec = {'metric': METRIC, 'value': round(value, 3), 'unit': 'images/s', 'n_gpus': world,
+        metric = METRIC if args.network == 'resnet101' else 'imgs/sec e2e train %s Faster R-CNN' % args.network
+        rec = {'metric': metric, 'value': round(value, 3), 'unit': 'images/s', 'n_gpus': world,
                'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
                'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
                'dtype': 'bf16' if dtype == torch.bfloat16 else 'fp32',
-               'data': 'synthetic (random 800x1333 images, 1-20 random gt boxes, random-init weights)',
+               'data': 'synthetic (random %dx%d images, 1-20 random gt boxes, random-init weights)' % (h, w),
                'config': {'model': '%s-faster-rcnn-c4' % args.network, 'global_batch': args.ims_per_gpu * world,
                           'seq_len': None, 'image_hw': [h, w], 'num_classes': args.num_classes,
                           'ims_per_gpu': args.ims_per_gpu, 'parallelism': 'dp%d' % world,

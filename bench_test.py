@@ -64,6 +64,7 @@ def main():
     ap.add_argument('--num-classes', type=int, default=81)
     ap.add_argument('--image', default='800x1333')
     ap.add_argument('--mode', default='graph', choices=['graph', 'eager'])
+    ap.add_argument('--batch', type=int, default=1, help='images per forward per GPU (BASELINE config 5: 8)')
     args = ap.parse_args()
 
     rank, world, local_rank, device = pdist.init_distributed()
@@ -71,10 +72,11 @@ def main():
     torch.manual_seed(1234 + rank)
     model = FasterRCNN(args.network, args.num_classes, cfg=snapshot(), train_mode='test')
     gen = torch.Generator().manual_seed(99 + rank)
-    pool = [(torch.randn(1, 3, h, w, generator=gen) * 50.0) for _ in range(4)]
-    info = torch.tensor([[float(h), float(w), 1.0]])
+    nb = args.batch
+    pool = [(torch.randn(nb, 3, h, w, generator=gen) * 50.0) for _ in range(4)]
+    info = torch.tensor([[float(h), float(w), 1.0]] * nb)
     if args.network.startswith('resnet'):
-        model.to(device).calibrate_bn(pool[0].to(device))
+        model.to(device).calibrate_bn(pool[0][:1].to(device))
     det = Detector(model, device)
     dev_pool = [det._prep(x) for x in pool]
     dinfo = info.to(device)
@@ -111,15 +113,16 @@ def main():
     pdist.barrier()
     sync()
     elapsed = pdist.all_reduce_max(time.perf_counter() - t0, device)
-    n_det = int(res[0][1].numel())
+    n_det = sum(int(r_[1].numel()) for r_ in res)
     if rank == 0:
-        value = world * args.steps / elapsed
+        value = world * nb * args.steps / elapsed
         print(json.dumps({
             'metric': METRIC if args.network == 'resnet101' else 'test FPS %s Faster R-CNN' % args.network, 'value': round(value, 3), 'unit': 'images/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
             'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16' if device.type == 'cuda' else 'fp32',
             'data': 'synthetic (random %dx%d images, random-init weights, BN calibrated)' % (h, w),
-            'config': {'model': '%s-faster-rcnn-c4' % args.network, 'global_batch': world, 'image_hw': [h, w],
+            'config': {'model': '%s-faster-rcnn-c4' % args.network, 'global_batch': world * nb, 'ims_per_gpu': nb,
+                       'image_hw': [h, w],
                        'num_classes': args.num_classes, 'parallelism': 'dp%d' % world, 'exec': mode,
                        'rpn_pre_post_nms': [config.TEST.RPN_PRE_NMS_TOP_N, config.TEST.RPN_POST_NMS_TOP_N],
                        'detections_last_image': n_det}}), flush=True)

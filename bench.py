@@ -60,7 +60,7 @@ def main():
     ap.add_argument('--ims-per-gpu', type=int, default=1)
     ap.add_argument('--mode', default='graph', choices=['graph', 'eager'])
     ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
-    ap.add_argument('--bucket-mb', type=float, default=64)
+    ap.add_argument('--bucket-mb', type=float, default=25)
     ap.add_argument('--pool', type=int, default=4, help='distinct synthetic batches cycled')
     args = ap.parse_args()
 

@@ -17,7 +17,7 @@ from .params import FlatParamStore
 class Trainer:
     def __init__(self, model, mode='e2e', fixed_param_prefix=None, lr=0.001, momentum=0.9, wd=0.0005,
                  clip_gradient=1.0, rescale_grad=1.0, lr_scheduler=None, compute_dtype=None, device=None,
-                 bucket_mb=64, average_grads=False, channels_last=None):
+                 bucket_mb=25, average_grads=False, channels_last=None):
         dev = torch.device(device) if device is not None else next(model.parameters()).device
         if compute_dtype is None:
             compute_dtype = torch.bfloat16 if dev.type == 'cuda' else torch.float32

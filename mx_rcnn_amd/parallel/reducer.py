@@ -10,8 +10,11 @@ before the optimizer touches the buffers -- no host blocking.
 
 Semantics: SUM across ranks (MXNet kvstore 'device', rescale_grad=1: `train_end2end.py:104`);
 ``average=True`` switches to mean.  Bucket sizing: xGMI is point-to-point, a ring uses one
-link per hop, so fewer, larger messages win; the default 64 MB keeps ResNet-101's 92 MB of
-bf16 gradients in 2 buckets and VGG16's fc6 (205 MB bf16) in its own bucket.
+link per hop, so messages must stay large enough to run at link bandwidth (a 25 MB ring
+all-reduce over 8 GPUs is bandwidth-, not latency-bound), but small enough that the first
+buckets are reduced while most of the backward is still running: the default 25 MB cuts
+ResNet-101's ~90 MB of bf16 gradients into 4 buckets, the last of which is the only exposed one;
+VGG16's fc6 (205 MB bf16) still gets a bucket of its own.
 """
 import os
 
@@ -33,7 +36,7 @@ class _Bucket:
 
 
 class BucketReducer:
-    def __init__(self, store, bucket_mb=64, average=False, overlap=True):
+    def __init__(self, store, bucket_mb=25, average=False, overlap=True):
         self.store = store
         self.world = get_world_size()
         self.average = average

@@ -147,6 +147,29 @@ def _cl(t):
     return t.contiguous(memory_format=torch.channels_last)
 
 
+_SIDE = {}
+
+
+def _side_stream(device):
+    """Per-device side stream for the weight-gradient kernels (MXR_WGRAD_STREAM=0 disables)."""
+    import os
+    if os.environ.get('MXR_WGRAD_STREAM', '1') == '0':
+        return None
+    s = _SIDE.get(device.index)
+    if s is None:
+        s = torch.cuda.Stream(device=device)
+        _SIDE[device.index] = s
+    return s
+
+
+class _nullctx(object):
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 class _Unit(object):
     """Static description of a residual unit for the fused op."""
 
@@ -227,14 +250,23 @@ class _FusedUnitFn(torch.autograd.Function):
         grads = [None] * len(t)
         d_out = _cl(d_out).to(x.dtype)
 
+        # weight gradients run on a side stream, concurrently with the data-gradient chain on the
+        # compute stream (each wgrad only waits for the dY it reads); joined before returning, so
+        # gradient-readiness hooks (DP all-reduce) and later frees see finished writes
+        main = torch.cuda.current_stream() if x.is_cuda else None
+        side = _side_stream(x.device) if main is not None else None
+
         def wgrad(idx, dy, inp, k, stride, pad):
             if not need[idx]:
                 return
             tgt = grad_sink.target(ctx.params[idx])
-            if tgt is not None and tgt.is_contiguous(memory_format=torch.channels_last):
-                ext.conv_wgrad(dy, inp, k, k, stride, pad, 0, tgt)
-            else:
-                grads[idx] = ext.conv_wgrad(dy, inp, k, k, stride, pad)
+            if side is not None:
+                side.wait_stream(main)
+            with torch.cuda.stream(side) if side is not None else _nullctx():
+                if tgt is not None and tgt.is_contiguous(memory_format=torch.channels_last):
+                    ext.conv_wgrad(dy, inp, k, k, stride, pad, 0, tgt)
+                else:
+                    grads[idx] = ext.conv_wgrad(dy, inp, k, k, stride, pad)
 
         def bn_targets(i):
             gi = nconv + 4 * i
@@ -299,6 +331,8 @@ class _FusedUnitFn(torch.autograd.Function):
         if not ctx.needs_input_grad[1]:
             if not spec.dim_match:
                 wgrad(nconv - 1, d_out, sc_in, 1, 1, 0)
+            if side is not None:
+                main.wait_stream(side)
             return (None, None, None) + tuple(grads)
         d_sc = None
         if not spec.dim_match:
@@ -320,6 +354,8 @@ class _FusedUnitFn(torch.autograd.Function):
             if d_sc is not None:
                 d_act1 = d_act1 + d_sc
             d_x = bn_bwd_plain(_cl(d_act1), 0, x, dres)
+        if side is not None:
+            main.wait_stream(side)
         return (None, d_x, None) + tuple(grads)
 
 

@@ -61,12 +61,36 @@ def conv_backward(x, w, param, dy, stride, pad, has_bias, need_x, need_w, need_b
     dw is None when it was accumulated straight into the parameter's flat gradient view."""
     kh = w.shape[2]
     dx = dw = db = None
+    # the weight gradient runs on a side stream concurrently with the data gradient (joined before
+    # returning, so readiness hooks and frees see finished writes)
+    side = main = None
+    if need_w and x.is_cuda and need_x:
+        from .fused import _side_stream
+        side = _side_stream(x.device)
+        if side is not None:
+            main = torch.cuda.current_stream()
+            side.wait_stream(main)
+    if side is not None:
+        with torch.cuda.stream(side):
+            dw, db = _wgrad(x, w, param, dy, stride, pad, has_bias, need_w, need_b)
     if need_x:
         if stride == 1 and w.shape[0] % 64 == 0 and 2 * pad == kh - 1:
             dx = need_ext().conv_igemm_fwd(dy, dgrad_weight(param, w), None, 1, kh - 1 - pad, False)[0]
         else:
             dx = torch.ops.aten.convolution_backward(
                 dy, x, w, None, [stride] * 2, [pad] * 2, [1, 1], False, [0, 0], 1, [True, False, False])[0]
+    if side is None:
+        dw, db = _wgrad(x, w, param, dy, stride, pad, has_bias, need_w, need_b)
+    else:
+        main.wait_stream(side)
+        for t in (dw, db):  # allocated on the side stream, consumed (and freed) on the compute stream
+            if t is not None:
+                t.record_stream(main)
+    return dx, dw, db
+
+
+def _wgrad(x, w, param, dy, stride, pad, has_bias, need_w, need_b):
+    dw = db = None
     if need_w and wgrad_enabled() and w.shape[0] % 8 == 0:
         tgt = grad_sink.target(param)
         if tgt is not None and tgt.is_contiguous(memory_format=torch.channels_last):
@@ -79,7 +103,7 @@ def conv_backward(x, w, param, dy, stride, pad, has_bias, need_x, need_w, need_b
         _, dw, db = torch.ops.aten.convolution_backward(
             dy, x, w, [w.shape[0]] if has_bias else None, [stride] * 2, [pad] * 2, [1, 1], False,
             [0, 0], 1, [False, bool(need_w), bool(has_bias and need_b)])
-    return dx, dw, db
+    return dw, db
 
 
 class _ConvIgemm(torch.autograd.Function):

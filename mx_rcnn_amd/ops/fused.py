@@ -267,6 +267,8 @@ class _FusedUnitFn(torch.autograd.Function):
                     ext.conv_wgrad(dy, inp, k, k, stride, pad, 0, tgt)
                 else:
                     grads[idx] = ext.conv_wgrad(dy, inp, k, k, stride, pad)
+                    if side is not None:  # allocated on the side stream, consumed on the compute stream
+                        grads[idx].record_stream(main)
 
         def bn_targets(i):
             gi = nconv + 4 * i

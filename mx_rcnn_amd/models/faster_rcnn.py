@@ -16,6 +16,8 @@ so the whole step can be captured in a hipGraph (core/graph.py).  Images per dev
 """
 import math
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -142,10 +144,37 @@ class FasterRCNN(nn.Module):
                         self.anchor_ratios, c.RPN_PRE_NMS_TOP_N, c.RPN_POST_NMS_TOP_N, c.RPN_NMS_THRESH,
                         c.RPN_MIN_SIZE, is_train=(key == 'TRAIN'), is_prob=is_prob)
 
-    def _rpn_losses(self, rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt):
+    def _anchor_target_async(self, data, im_info, gt_boxes, n_gt):
+        """Start the RPN anchor-target assignment (which needs only the image shape and the gt
+        boxes) on an auxiliary stream, concurrent with the trunk forward; returns a callable that
+        joins it into the compute stream and yields the targets."""
+        H, W = self.feat_shape(data.shape[2], data.shape[3])
+
+        def run():
+            return anchor_target((H, W), gt_boxes, n_gt, im_info, self.feat_stride, self.anchor_scales,
+                                 self.anchor_ratios, allowed_border=0, cfg=self.cfg)
+        if not data.is_cuda or os.environ.get('MXR_AUX_STREAM', '1') == '0':
+            at = run()
+            return lambda: at
+        main = torch.cuda.current_stream()
+        aux = _aux_stream(data.device)
+        aux.wait_stream(main)
+        with torch.cuda.stream(aux):
+            at = run()
+
+        def join():
+            main.wait_stream(aux)
+            for t in at.values():
+                t.record_stream(main)
+            return at
+        return join
+
+    def _rpn_losses(self, rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt, at=None):
         H, W = rpn_cls.shape[2], rpn_cls.shape[3]
-        at = anchor_target((H, W), gt_boxes, n_gt, im_info, self.feat_stride, self.anchor_scales,
-                           self.anchor_ratios, allowed_border=0, cfg=self.cfg)
+        if at is None:
+            at = anchor_target((H, W), gt_boxes, n_gt, im_info, self.feat_stride, self.anchor_scales,
+                               self.anchor_ratios, allowed_border=0, cfg=self.cfg)
+        assert at['label'].shape[1] == rpn_cls.shape[1] // 2 * H * W, 'anchor grid / RPN map mismatch'
         cls_loss = rpn_softmax_ce(rpn_cls, at['label'])
         bbox_loss = smooth_l1(rpn_bbox, at['bbox_target'], at['bbox_inside_weight'], at['bbox_outside_weight'],
                               sigma=3.0, grad_scale=1.0)
@@ -164,12 +193,14 @@ class FasterRCNN(nn.Module):
     def train_e2e(self, data, im_info, gt_boxes, n_gt):
         """Approximate joint training step forward.  Returns dict with 'loss' (to backward)
         and the metric tensors of the reference's six metrics (rcnn/metric.py)."""
+        at_join = self._anchor_target_async(data, im_info, gt_boxes, n_gt)
         with prof.range('trunk'):
             feat = self.trunk(data)
         with prof.range('rpn'):
             rpn_cls, rpn_bbox = self.rpn(feat)
         with prof.range('anchor_target+rpn_loss'):
-            rpn_cls_loss, rpn_bbox_loss, at = self._rpn_losses(rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt)
+            rpn_cls_loss, rpn_bbox_loss, at = self._rpn_losses(rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt,
+                                                                at_join())
         with prof.range('proposal'):
             rois, _ = self._proposal(rpn_cls, rpn_bbox, im_info, 'TRAIN')
         with prof.range('proposal_target'):
@@ -193,9 +224,10 @@ class FasterRCNN(nn.Module):
                 'rpn_cls_score': rpn_cls, 'rpn_label': at['label'], 'num_images': B, 'num_rois': R}
 
     def train_rpn(self, data, im_info, gt_boxes, n_gt):
+        at_join = self._anchor_target_async(data, im_info, gt_boxes, n_gt)
         feat = self.trunk(data)
         rpn_cls, rpn_bbox = self.rpn(feat)
-        cls_loss, bbox_loss, at = self._rpn_losses(rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt)
+        cls_loss, bbox_loss, at = self._rpn_losses(rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt, at_join())
         return {'loss': cls_loss + bbox_loss, 'objective': (cls_loss + bbox_loss).detach(),
                 'rpn_cls_loss': cls_loss, 'rpn_bbox_loss': bbox_loss, 'rpn_cls_score': rpn_cls, 'rpn_label': at['label'], 'num_images': data.shape[0]}
 
@@ -227,6 +259,17 @@ class FasterRCNN(nn.Module):
         pooled = roi_pool(feat, rois, (7, 7), 1.0 / self.feat_stride)
         cls_score, bbox_pred = self.head(pooled)
         return rois, torch.softmax(cls_score.float(), dim=1), bbox_pred.float()
+
+
+_AUX = {}
+
+
+def _aux_stream(device):
+    s = _AUX.get(device.index)
+    if s is None:
+        s = torch.cuda.Stream(device=device)
+        _AUX[device.index] = s
+    return s
 
 
 def build_model(network='vgg16', num_classes=21, cfg=None, **kw):

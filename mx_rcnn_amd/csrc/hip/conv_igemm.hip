@@ -509,6 +509,20 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// wait until at most `ahead` stages (LPS loads each) are still in flight; ahead <= S - 2 <= 6
+template <int LPS>
+__device__ __forceinline__ void wait_stages(int ahead) {
+  switch (ahead) {
+    case 6: wait_vmcnt<6 * LPS>(); break;
+    case 5: wait_vmcnt<5 * LPS>(); break;
+    case 4: wait_vmcnt<4 * LPS>(); break;
+    case 3: wait_vmcnt<3 * LPS>(); break;
+    case 2: wait_vmcnt<2 * LPS>(); break;
+    case 1: wait_vmcnt<LPS>(); break;
+    default: wait_vmcnt<0>(); break;
+  }
+}
+
 __device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
                                    (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
@@ -659,7 +673,7 @@ conv_igemm_buf_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int ACH = BM / 32, BCH = BN / 32;
   constexpr int LPS = ACH + BCH;
-  static_assert(S >= 2 && S <= 4, "pipeline depth");
+  static_assert(S >= 2 && S <= 8, "pipeline depth");
   __shared__ __attribute__((aligned(16))) uint16_t lds[S * (BM + BN) * BK];  // the ONLY __shared__ object
   uint16_t* As = lds;
   uint16_t* Bs = lds + S * BM * BK;
@@ -751,10 +765,7 @@ conv_igemm_buf_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
   for (int s = 0; s < S - 1; ++s)
     if (s < nk) issue(s);
   for (int ks = 0; ks < nk; ++ks) {
-    const int ahead = min(S - 2, nk - 1 - ks);
-    if (ahead >= 2) wait_vmcnt<2 * LPS>();
-    else if (ahead == 1) wait_vmcnt<LPS>();
-    else wait_vmcnt<0>();
+    wait_stages<LPS>(min(S - 2, nk - 1 - ks));
     __builtin_amdgcn_s_barrier();
     if (ks + S - 1 < nk) issue((ks + S - 1) % S);
     const int buf = ks % S;
@@ -861,7 +872,8 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
     case 14: launch_fwd<128, 128, 3>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 15: launch_fwd<128, 64, 3>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 16: launch_fwd<64, 64, 3>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
-    // buffer-resource LDS-DMA variants: 2x = depth 3, 3x = depth 4 (x as above)
+    // buffer-resource LDS-DMA variants: 2x = depth 3, 3x = depth 4 (x as above).  Depth 6 / 8 were
+    // 1.5-2x slower on every ResNet shape (tools/microbench/conv_tiles.py): 3 is the sweet spot
     case 21: launch_fwd<128, 128, 3, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 22: launch_fwd<128, 64, 3, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 23: launch_fwd<64, 64, 3, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;

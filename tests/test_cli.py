@@ -82,3 +82,13 @@ def test_eval_in_memory_perfect_and_empty():
     assert eval_in_memory(gt, det, classes) == pytest.approx(1.0)
     empty = [[], [np.zeros((0, 5))] * 2, [np.zeros((0, 5))] * 2]
     assert eval_in_memory(gt, empty, classes) == 0.0
+
+
+def test_bench_rpn_cpu_json(tmp_path):
+    """BASELINE config 1 harness (VGG16 RPN-only CPU forward) prints one well-formed JSON line."""
+    import json
+    out = _run([os.path.join(ROOT, 'bench_rpn_cpu.py'), '--image', '224x320', '--steps', '1', '--warmup', '0'],
+               cwd=str(tmp_path))
+    rec = json.loads([ln for ln in out.splitlines() if ln.startswith('{')][-1])
+    assert rec['unit'] == 'ms/image' and rec['higher_is_better'] is False and rec['value'] > 0
+    assert rec['config']['rois'] == [1, 300, 5]

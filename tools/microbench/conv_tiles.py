@@ -30,6 +30,9 @@ SHAPES = {
     's1_1x1a': (1, 256, 200, 334, 64, 1, 1, 0),
     's1_1x1b': (1, 64, 200, 334, 256, 1, 1, 0),
     's2_1x1b': (1, 128, 100, 167, 512, 1, 1, 0),
+    # the stage-3 shapes at M = 4096 (exactly 256 64x64 blocks): wave-quantisation probe
+    's3_3x3_sq': (1, 256, 64, 64, 256, 3, 1, 1),
+    's3_1x1a_sq': (1, 1024, 64, 64, 256, 1, 1, 0),
 }
 
 

@@ -74,7 +74,7 @@ std::vector<Tensor> nms_proposals(const Tensor& boxes, const Tensor& scores, con
   DevGuard g(boxes.device());
   const int nb = (P + 63) / 64;
   TORCH_CHECK(mxr::nms_reduce_lds(P, (int)post) <= 160 * 1024, "NMS LDS budget exceeded (P or post too large)");
-  TORCH_CHECK(nb <= 256, "NMS supports at most 16384 pre-NMS boxes per image");
+  TORCH_CHECK(nb <= 1024, "NMS supports at most 65536 pre-NMS boxes per image");
   auto st = cur_stream();
   Tensor mask = at::empty({mxr::nms_mask_words(B, P)}, boxes.options().dtype(at::kLong));
   mxr::nms_mask(boxes.data_ptr<float>(), n_valid.data_ptr<int32_t>(), B, P, (float)thresh,

@@ -27,7 +27,8 @@
 namespace mxr {
 
 constexpr int NMS_HELPERS = 15;  // helper waves in the 1024-thread reducer
-constexpr int NMS_PF = 18;       // prefetched column blocks per helper lane: 15 * 18 + 2 >= 256 blocks
+constexpr int NMS_PF = 18;       // prefetched column blocks per helper lane (15 * 18 + 2 >= 256 blocks;
+                                 // farther columns take plain loads)
 
 __global__ void __launch_bounds__(256)
 nms_mask_kernel(const float* __restrict__ boxes, const int32_t* __restrict__ n_valid, int P, int nb,
@@ -148,6 +149,14 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
               // ds_or_b64 without return: no LDS round trip on the helper's path
               if (lane == 0 && bits) atomicOr(reinterpret_cast<unsigned long long*>(&removed[c]), bits);
             }
+          }
+          // column blocks beyond the prefetch window (> NMS_HELPERS * NMS_PF ahead: only when
+          // P > ~17K, e.g. the alternate-training proposal dump with pre-NMS = all anchors):
+          // plain loads of row block t-1, same fold
+          for (int c = t + 1 + h + NMS_HELPERS * NMS_PF; c < nbv; c += NMS_HELPERS) {
+            const uint64_t wv = mb[(int64_t)(t - 1) * Pp + (int64_t)c * 64 + lane];
+            const uint64_t bits = __ballot((wv & kp) != 0ull);
+            if (lane == 0 && bits) atomicOr(reinterpret_cast<unsigned long long*>(&removed[c]), bits);
           }
         }
       }

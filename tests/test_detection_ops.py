@@ -162,9 +162,11 @@ def test_nms_gpu_matches_cpu(cuda):
 
 @pytest.mark.gpu
 def test_nms_gpu_training_scale(cuda):
-    """12000 -> 6000 (train proposal sizes), the 256-block limit, and post truncation."""
+    """12000 -> 6000 (train proposal sizes), post truncation, and P beyond the helpers' prefetch
+    window (> 272 blocks: the alternate-training proposal dump keeps every anchor pre-NMS)."""
     g = torch.Generator().manual_seed(9)
-    for n, th, post in [(12000, 0.7, None), (16384, 0.7, None), (5000, 0.5, 700)]:
+    for n, th, post in [(12000, 0.7, None), (16384, 0.7, None), (5000, 0.5, 700), (30000, 0.7, 2000),
+                        (20000, 0.6, None)]:
         b = rand_boxes(g, n, 1300)
         s = torch.rand(n, generator=g)
         k_cpu = ops.nms(b, s, th, max_keep=post)

@@ -27,24 +27,37 @@ class Detector(object):
         return rois[0, :, 1:].cpu().numpy(), scores[0, :, None].cpu().numpy()
 
 
-def generate_detections(detector, test_data, imdb, vis=False):
+def generate_detections(detector, test_data, imdb, vis=False, shard=(0, 1)):
+    """Run the RPN over ``test_data`` and write the proposal dump.  ``shard=(rank, world)``:
+    the iterator holds images ``rank::world`` of the image set; the per-rank lists are gathered
+    (interleaved back into image order) and rank 0 writes the file."""
     assert not test_data.shuffle
+    rank, world = shard
     imdb_boxes = []
     for i, batch in enumerate(test_data):
         if i % 10 == 0:
-            logging.info('generating detections %d/%d', i, imdb.num_images)
+            logging.info('generating detections %d/%d', i * world + rank, imdb.num_images)
         boxes, scores = detector.im_detect(batch['data'], batch['im_info'])
         scale = float(batch['im_info'][0, 2])
         dets = np.hstack((boxes / scale, scores))
         imdb_boxes.append(dets)
         if vis:
             vis_detection(np.asarray(batch['data']), dets, thresh=0.9)
+    if world > 1:
+        import torch.distributed as dist
+        parts = [None] * world
+        dist.all_gather_object(parts, imdb_boxes)
+        imdb_boxes = [parts[i % world][i // world] for i in range(sum(len(p) for p in parts))]
     assert len(imdb_boxes) == imdb.num_images, 'calculations not complete'
     rpn_folder = os.path.join(imdb.root_path, 'rpn_data')
-    os.makedirs(rpn_folder, exist_ok=True)
     rpn_file = os.path.join(rpn_folder, imdb.name + '_rpn.npz')
-    cache_io.save_box_list(rpn_file, imdb_boxes)
-    logging.info('wrote rpn proposals to %s', rpn_file)
+    if rank == 0:
+        os.makedirs(rpn_folder, exist_ok=True)
+        cache_io.save_box_list(rpn_file, imdb_boxes)
+        logging.info('wrote rpn proposals to %s', rpn_file)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
     return imdb_boxes
 
 

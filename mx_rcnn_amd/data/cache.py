@@ -40,7 +40,9 @@ def load_roidb(path):
 
 def save_box_list(path, box_list):
     """RPN proposal dump: list (per image) of (n, 4) or (n, 5) arrays."""
-    np.savez(path, n=np.array([len(box_list)]), **{'b%d' % i: np.asarray(b, np.float32) for i, b in enumerate(box_list)})
+    tmp = '%s.tmp%d.npz' % (path, os.getpid())  # write-then-rename (other ranks may read it next)
+    np.savez(tmp, n=np.array([len(box_list)]), **{'b%d' % i: np.asarray(b, np.float32) for i, b in enumerate(box_list)})
+    os.replace(tmp, path)
 
 
 def load_box_list(path):

@@ -54,7 +54,11 @@ def synthetic_image(entry):
     rng = np.random.RandomState(entry['synthetic_seed'] % (2 ** 31))
     h, w = entry['height'], entry['width']
     im = rng.randint(0, 255, size=(h, w, 3), dtype=np.uint8)
-    for b in entry['boxes']:
+    boxes = np.asarray(entry['boxes'])
+    cls = entry.get('gt_classes')
+    if cls is not None:  # merged roidbs (alternate training) also hold proposal rows: draw the gt only
+        boxes = boxes[np.asarray(cls) > 0]
+    for b in boxes:
         x1, y1, x2, y2 = [int(v) for v in b]
         im[y1:y2 + 1, x1:x2 + 1] = (im[y1:y2 + 1, x1:x2 + 1] // 2 + 120).astype(np.uint8)
     return im

@@ -11,6 +11,7 @@ Checkpoints are only ever parsed as data (no pickle), so loading a foreign file 
 nothing from it.  Compatibility with real MXNet-written files is unverified in this
 environment (no MXNet, no fixture in the reference tree); the layout follows the spec above.
 """
+import os
 import struct
 
 import numpy as np
@@ -38,7 +39,10 @@ def save(fname, data):
         arrays = [data[k] for k in names]
     else:
         names, arrays = [], list(data)
-    with open(fname, 'wb') as f:
+    # write-then-rename: a reader on another rank (alternate training loads the checkpoint the
+    # previous stage wrote) never sees a partial file
+    tmp = '%s.tmp%d' % (fname, os.getpid())
+    with open(tmp, 'wb') as f:
         f.write(struct.pack('<QQQ', LIST_MAGIC, 0, len(arrays)))
         for a in arrays:
             a = _to_numpy(a)
@@ -54,6 +58,7 @@ def save(fname, data):
             b = n.encode('utf-8')
             f.write(struct.pack('<Q', len(b)))
             f.write(b)
+    os.replace(tmp, fname)
 
 
 class _Reader:

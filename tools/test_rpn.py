@@ -11,6 +11,7 @@ from mx_rcnn_amd.core import launch  # noqa: E402
 from mx_rcnn_amd.core.generate import Detector, generate_detections  # noqa: E402
 from mx_rcnn_amd.data.load_data import load_gt_roidb  # noqa: E402
 from mx_rcnn_amd.data.loader import ROIIter  # noqa: E402
+from mx_rcnn_amd.parallel import dist as pdist  # noqa: E402
 from mx_rcnn_amd.utils.load_model import load_param  # noqa: E402
 
 
@@ -23,12 +24,14 @@ def test_rpn(image_set, year, root_path, devkit_path, prefix, epoch, ctx, vis=Fa
         imdb, roidb = load_gt_roidb(image_set, year, root_path, devkit_path)
     else:
         imdb, roidb = imdb_roidb
-    test_data = _rpn_test_iter(roidb)
+    # data parallel: each rank runs images rank::world, the dump is gathered (core/generate.py)
+    rank, world = pdist.get_rank(), pdist.get_world_size()
+    test_data = _rpn_test_iter(roidb[rank::world])
     arg, aux, num_classes = load_param(prefix, epoch, convert=False)
     model, _, _ = launch.build_model(network, num_classes if num_classes != 1000 else imdb.num_classes,
                                      train_mode='rpn_test')
     det = Detector(model, ctx, arg, aux)
-    boxes = generate_detections(det, test_data, imdb, vis=vis)
+    boxes = generate_detections(det, test_data, imdb, vis=vis, shard=(rank, world))
     imdb.evaluate_recall(roidb, candidate_boxes=boxes)
     return boxes
 

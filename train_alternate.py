@@ -13,6 +13,7 @@ from mx_rcnn_amd.config import config
 from mx_rcnn_amd.core import launch
 from mx_rcnn_amd.data.load_data import load_gt_roidb, load_rpn_roidb
 from mx_rcnn_amd.data.roidb import prepare_roidb, add_bbox_regression_targets
+from mx_rcnn_amd.parallel import dist as pdist
 from mx_rcnn_amd.utils.combine_model import combine_model
 from tools.test_rpn import test_rpn
 from tools.train_rcnn import train_rcnn
@@ -49,6 +50,7 @@ def alternate_train(image_set, test_image_set, year, root_path, devkit_path, pre
               frequent, kv_store, work_load_list, network=network,
               synthetic=None if synthetic is None else (synthetic[1], synthetic[0]), max_steps=max_steps,
               rank=rank, world=world)
+    pdist.barrier()
     logging.info('########## GENERATE RPN DETECTION')
     boxes = test_rpn(image_set, year, root_path, devkit_path, p('rpn1'), rpn_epoch, ctx, network=network, imdb_roidb=gt())
     logging.info('########## TRAIN RCNN WITH IMAGENET INIT AND RPN DETECTION')
@@ -57,6 +59,7 @@ def alternate_train(image_set, test_image_set, year, root_path, devkit_path, pre
     train_rcnn(image_set, year, root_path, devkit_path, pretrained, epoch, p('rcnn1'), ctx, begin_epoch,
                rcnn_epoch, frequent, kv_store, work_load_list, network=network, roidb_override=rpn_roidb(boxes),
                max_steps=max_steps, rank=rank, world=world)
+    pdist.barrier()
     logging.info('########## TRAIN RPN WITH RCNN INIT')
     config.TRAIN.FINETUNE = True
     config.TRAIN.BATCH_IMAGES = batch_images
@@ -64,18 +67,24 @@ def alternate_train(image_set, test_image_set, year, root_path, devkit_path, pre
               rpn_epoch, frequent, kv_store, work_load_list, network=network,
               synthetic=None if synthetic is None else (synthetic[1], synthetic[0]), max_steps=max_steps,
               rank=rank, world=world)
+    pdist.barrier()
     logging.info('########## GENERATE RPN DETECTION')
     boxes = test_rpn(image_set, year, root_path, devkit_path, p('rpn2'), rpn_epoch, ctx, network=network, imdb_roidb=gt())
     logging.info('########## COMBINE RPN2 WITH RCNN1')
-    combine_model(p('rpn2'), rpn_epoch, p('rcnn1'), rcnn_epoch, p('rcnn2'), 0)
+    if rank == 0:
+        combine_model(p('rpn2'), rpn_epoch, p('rcnn1'), rcnn_epoch, p('rcnn2'), 0)
+    pdist.barrier()
     logging.info('########## TRAIN RCNN WITH RPN INIT AND DETECTION')
     config.TRAIN.BATCH_SIZE = 128
     config.TRAIN.BATCH_IMAGES = batch_images
     train_rcnn(image_set, year, root_path, devkit_path, p('rcnn2'), 0, p('rcnn2'), ctx, begin_epoch, rcnn_epoch,
                frequent, kv_store, work_load_list, network=network, roidb_override=rpn_roidb(boxes),
                max_steps=max_steps, rank=rank, world=world)
+    pdist.barrier()
     logging.info('########## COMBINE RPN2 WITH RCNN2')
-    combine_model(p('rpn2'), rpn_epoch, p('rcnn2'), rcnn_epoch, p('final'), 0)
+    if rank == 0:
+        combine_model(p('rpn2'), rpn_epoch, p('rcnn2'), rcnn_epoch, p('final'), 0)
+    pdist.barrier()
     return p('final')
 
 

@@ -17,6 +17,8 @@
 //
 // The same kernel computes the stride-1 data gradient (dgrad) as a forward convolution of
 // dY with the flipped / transposed filter (pad' = k-1-pad); see ops/conv.py.
+#include <cstdlib>
+
 #include "common.h"
 #include "../kernels.h"
 
@@ -830,10 +832,12 @@ int conv_igemm_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, i
   if (tile <= 0) {
     // buffer-resource LDS-DMA kernel, 3-deep (tools/microbench/conv_tiles.py sweep on the
     // ResNet-101 C4 shapes): 64x64 everywhere except many-block, long-K shapes (the 128-RoI
-    // stage-4 convs), where 128x64 halves the operand bytes per FLOP; split-K only for grids
+    // stage-4 convs), where 128x64 halves the operand bytes per FLOP -- but not on wide outputs
+    // (the RPN 3x3's dgrad, Cout 1024: 64x64 71 us vs 128x64 89 us); split-K only for grids
     // too small to cover the CUs
     const int64_t b64 = ((M + 63) / 64) * ((Cout + 63) / 64);
-    const int t = (b64 >= 600 && nk >= 16) ? 22 : 23;
+    static const bool wide22 = getenv("MXR_PLAN_WIDE22") != nullptr;  // A/B switch for the rule below
+    const int t = (b64 >= 600 && nk >= 16 && (Cout <= 512 || wide22)) ? 22 : 23;
     const int64_t blocks = t == 22 ? ((M + 127) / 128) * ((Cout + 63) / 64) : b64;
     int splits = 1;
     while (splits < 4 && blocks * splits < 128 && nk / (splits * 2) >= 8 && Cout % 4 == 0) splits *= 2;
@@ -842,7 +846,7 @@ int conv_igemm_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, i
   }
   // explicit tile (A/B runs): tile codes -> (BM, BN); split K until ~4 blocks per CU
   const int code = tile % 10;
-  const int bm = code == 3 ? 64 : 128, bn = code == 1 ? 128 : 64;
+  const int bm = code == 3 || code == 5 ? 64 : code == 4 ? 32 : 128, bn = code == 1 ? 128 : code == 5 ? 32 : 64;
   const int64_t blocks = ((M + bm - 1) / bm) * ((Cout + bn - 1) / bn);
   int splits = 1;
   while (splits < 8 && blocks * splits * 2 <= 1024 && nk / (splits * 2) >= 6 && Cout % 4 == 0) splits *= 2;
@@ -880,6 +884,9 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
     case 31: launch_fwd<128, 128, 4, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 32: launch_fwd<128, 64, 4, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 33: launch_fwd<64, 64, 4, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    // small tiles (2-4 workgroups per CU on the ~4K-row stage-3 GEMMs: more waves to hide latency)
+    case 24: launch_fwd<32, 64, 3, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    case 25: launch_fwd<64, 32, 3, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     default: launch_fwd<64, 64>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
   }
   return tile;

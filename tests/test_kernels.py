@@ -272,7 +272,7 @@ def test_conv_igemm_fwd_vs_fp32(cuda, shape):
     if relu:
         ref = torch.relu(ref)
     for tile, splits in ((1, 1), (2, 1), (3, 1), (3, 2), (3, 4), (0, 0), (21, 1), (22, 1), (23, 1), (23, 2), (31, 2),
-                         (33, 1), (12, 1), (16, 2)):
+                         (33, 1), (12, 1), (16, 2), (24, 1), (25, 1), (24, 2)):
         y = need_ext().conv_igemm_fwd(x.to(cuda).contiguous(memory_format=torch.channels_last),
                                       w.to(cuda).contiguous(memory_format=torch.channels_last),
                                       None if b is None else b.to(cuda), s, p, relu, tile, splits)[0]

@@ -24,6 +24,7 @@ SHAPES = {
     's3_1x1a': (1, 1024, 50, 84, 256, 1, 1, 0),
     's3_1x1b': (1, 256, 50, 84, 1024, 1, 1, 0),
     'rpn_3x3': (1, 1024, 50, 84, 512, 3, 1, 1),
+    'rpn_dgrad': (1, 512, 50, 84, 1024, 3, 1, 1),  # the dgrad of rpn_3x3 as a forward conv
     's4_3x3': (128, 512, 7, 7, 512, 3, 1, 1),
     's4_1x1a': (128, 2048, 7, 7, 512, 1, 1, 0),
     's4_1x1b': (128, 512, 7, 7, 2048, 1, 1, 0),

@@ -252,7 +252,10 @@ class _FusedUnitFn(torch.autograd.Function):
 
         # weight gradients run on a side stream, concurrently with the data-gradient chain on the
         # compute stream (each wgrad only waits for the dY it reads); joined before returning, so
-        # gradient-readiness hooks (DP all-reduce) and later frees see finished writes
+        # gradient-readiness hooks (DP all-reduce) and later frees see finished writes.  Looser
+        # joins measured slower on ResNet-101 (scripts/gpu_ab3.sh, 129 img/s per-unit join vs 119
+        # joining once per backward with record_stream, 118 joining one unit late): the wgrad of
+        # unit k shares dY with unit k's dgrad in L2/MALL, a lagging side stream does not
         main = torch.cuda.current_stream() if x.is_cuda else None
         side = _side_stream(x.device) if main is not None else None
 

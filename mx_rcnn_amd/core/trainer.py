@@ -66,7 +66,8 @@ class Trainer:
     def step_body(self, b):
         """The device work of one step (capturable)."""
         self.store.zero_grad()
-        self.reducer.prepare()
+        # the optimizer runs bucket by bucket under the backward pass (parallel/reducer.py)
+        self.reducer.prepare(sgd=(self.lr_t, self.momentum, self.wd, self.rescale, self.clip))
         out = self.forward(b)
         if self.fault is not None:  # test hook: multiplies the loss by NaN on the armed step
             out['loss'] = out['loss'] * self.fault
@@ -78,7 +79,10 @@ class Trainer:
         with prof.range('allreduce_wait'):
             self.reducer.finish()
         with prof.range('sgd'):
-            self.store.sgd_step(self.lr_t, self.momentum, self.wd, self.rescale, self.clip)
+            if self.reducer.sgd_applied:
+                self.store.refresh_dgrad_cache()
+            else:
+                self.store.sgd_step(self.lr_t, self.momentum, self.wd, self.rescale, self.clip)
         # Return detached outputs: a caller holding the loss would otherwise keep this step's
         # autograd graph (and its AccumulateGrad nodes, bound to this step's stream) alive, and a
         # later hipGraph capture on a side stream then syncs against that stream and dies in

@@ -26,38 +26,60 @@ from .dist import get_world_size, is_distributed
 
 
 class _Bucket:
-    __slots__ = ('buf', 'start', 'end', 'names', 'pending', 'work')
+    __slots__ = ('group', 'buf', 'start', 'end', 'names', 'pending', 'work', 'updated')
 
-    def __init__(self, buf, start, end):
-        self.buf, self.start, self.end = buf, start, end
+    def __init__(self, group, start, end):
+        self.group, self.buf, self.start, self.end = group, group.grad, start, end
         self.names = []
         self.pending = 0
         self.work = None
+        self.updated = False
 
 
 class BucketReducer:
-    def __init__(self, store, bucket_mb=25, average=False, overlap=True):
+    """Gradient buckets with readiness hooks.  Two jobs, either or both:
+
+    * data parallel: all-reduce each bucket as soon as its last gradient lands;
+    * overlapped optimizer (``prepare(sgd=...)``, GPU): run the fused SGD of each bucket on an
+      optimizer stream as soon as the bucket is final (after its all-reduce under DP), so the
+      update of the head / stage-4 / RPN weights runs under the rest of the backward pass instead
+      of after it.  SGD is elementwise per parameter (MXNet clips each element, no global norm),
+      and a parameter's value is not read again once its gradient is final (each weight belongs
+      to one layer; its dgrad and wgrad are both done when the readiness hook fires), so
+      updating it early is exact.  Single-GPU buckets are ``sgd_bucket_mb`` (smaller: only the
+      last one is exposed after the backward).
+    """
+
+    def __init__(self, store, bucket_mb=25, average=False, overlap=True, sgd_bucket_mb=8):
         self.store = store
         self.world = get_world_size()
         self.average = average
-        self.overlap = overlap and is_distributed()
+        self.dp = is_distributed() and (self.world > 1 or os.environ.get('MXR_FORCE_DIST', '0') == '1')
+        self.overlap = overlap and self.dp
+        # off by default: measured 2-3 % slower on 1-GPU ResNet-101 (scripts/gpu_sgd.sh A/B, 125-126
+        # vs 128-129 img/s): the HBM-bound update steals bandwidth from the concurrent backward
+        # convs for less than it hides (the whole update is ~0.16 ms)
+        self.sgd_capable = store.device.type == 'cuda' and os.environ.get('MXR_OVERLAP_SGD', '0') == '1'
         self.buckets = []
         self._param_bucket = {}
-        self._hooks = []
-        if not is_distributed() or (self.world == 1 and os.environ.get('MXR_FORCE_DIST', '0') != '1'):
+        self._sgd = None
+        self._opt_stream = None
+        self.sgd_applied = False
+        if not (self.dp or self.sgd_capable):
             return
+        mb = bucket_mb if self.dp else sgd_bucket_mb
         for g in store.groups:
             esize = g.grad.element_size()
-            cap = max(1, int(bucket_mb * (1 << 20) // esize))
+            cap = max(1, int(mb * (1 << 20) // esize))
             cur = None
             for (n, _, _, numel, _, _), off in zip(g.entries, g.offsets):
                 if cur is None or (off + numel - cur.start > cap and cur.end > cur.start):
-                    cur = _Bucket(g.grad, off, off)
+                    cur = _Bucket(g, off, off)
                     self.buckets.append(cur)
                 cur.end = off + numel
                 cur.names.append(n)
                 self._param_bucket[n] = cur
-        if self.overlap:
+        if self.overlap or self.sgd_capable:
             for n, p in store.params.items():
                 if n in self._param_bucket:
                     grad_sink.add_hook(p, self._make_hook(n))
@@ -67,7 +89,10 @@ class BucketReducer:
             b = self._param_bucket[name]
             b.pending -= 1
             if b.pending == 0:
-                self._launch(b)
+                if self.overlap:
+                    self._launch(b)
+                if self._sgd is not None:
+                    self._update(b)
         return hook
 
     def _launch(self, b):
@@ -76,20 +101,52 @@ class BucketReducer:
             t.div_(self.world)
         b.work = dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
 
-    def prepare(self):
-        """Call before backward: reset per-bucket pending counters."""
+    def _update(self, b):
+        """SGD of one final bucket on the optimizer stream (after its all-reduce under DP)."""
+        from ..ops.sgd import sgd_momentum_
+        if self._opt_stream is None:
+            self._opt_stream = torch.cuda.Stream(device=b.buf.device)
+        os_ = self._opt_stream
+        os_.wait_stream(torch.cuda.current_stream(b.buf.device))
+        g, s, e = b.group, b.start, b.end
+        lr, mu, wd, rescale, clip = self._sgd
+        with torch.cuda.stream(os_):
+            if b.work is not None:
+                b.work.wait()  # the optimizer stream waits for this bucket's collective
+            sgd_momentum_(g.master[s:e], g.mom[s:e], g.grad[s:e], lr, mu, wd if g.decay else 0.0, rescale, clip,
+                          None if g.shadow is None else g.shadow[s:e])
+        b.updated = True
+
+    def prepare(self, sgd=None):
+        """Call before backward: reset per-bucket counters.  ``sgd=(lr_tensor, momentum, wd,
+        rescale, clip)`` enables the overlapped optimizer for this step (GPU only)."""
+        self._sgd = sgd if (sgd is not None and self.sgd_capable and self.buckets) else None
+        self.sgd_applied = False
         for b in self.buckets:
             b.pending = len(b.names)
             b.work = None
+            b.updated = False
 
     def finish(self):
-        """After backward: launch buckets whose params got no gradient, then stream-wait all."""
+        """After backward: launch / update buckets whose params got no gradient, then make the
+        compute stream wait for every collective and the optimizer stream.  ``sgd_applied`` tells
+        the caller whether the update already happened."""
+        if self.dp:
+            for b in self.buckets:
+                if b.work is None:
+                    self._launch(b)
+        if self._sgd is not None:
+            for b in self.buckets:
+                if not b.updated:
+                    self._update(b)
+            self.sgd_applied = True
         for b in self.buckets:
-            if b.work is None:
-                self._launch(b)
-        for b in self.buckets:
-            b.work.wait()
-            b.work = None
+            if b.work is not None:
+                b.work.wait()
+                b.work = None
+        if self._opt_stream is not None and self._sgd is not None:
+            torch.cuda.current_stream(self._opt_stream.device).wait_stream(self._opt_stream)
+        self._sgd = None
 
     def bucket_sizes(self):
         return [(b.end - b.start) * b.buf.element_size() for b in self.buckets]

@@ -102,3 +102,32 @@ def test_e2e_step_gpu_graph(cuda):
         o = g(b)
     torch.cuda.synchronize()
     assert torch.isfinite(o['loss'])
+
+
+@pytest.mark.gpu
+def test_overlapped_sgd_matches_end_of_step_sgd(cuda, monkeypatch):
+    """Bucket-by-bucket SGD under the backward pass (MXR_OVERLAP_SGD=1, parallel/reducer.py) gives the same weights
+    and momenta as one update after the backward (MXR_OVERLAP_SGD=0)."""
+    fixed = ['conv0', 'stage1', 'stage2', 'bn_data', 'bn0']
+    b = {k: v.to(cuda) for k, v in _batch(320, 480).items()}
+
+    def run(overlap):
+        monkeypatch.setenv('MXR_OVERLAP_SGD', '1' if overlap else '0')
+        torch.manual_seed(0)
+        m = FasterRCNN('resnet50', 21, cfg=_cfg())
+        tr = Trainer(m, 'e2e', fixed_param_prefix=fixed, lr=0.01, device=cuda)
+        assert tr.reducer.sgd_capable == overlap
+        for i in range(2):
+            torch.manual_seed(10 + i)
+            tr.step(b)
+        assert tr.reducer.sgd_applied == overlap
+        torch.cuda.synchronize()
+        return tr.store.state_arrays(), tr.store.optimizer_state()
+
+    w1, m1 = run(True)
+    w0, m0 = run(False)
+    for k in w0:
+        assert torch.allclose(w1[k], w0[k], rtol=1e-3, atol=1e-5), k
+    for k in m0:
+        scale = m0[k].abs().max().item() + 1e-12
+        assert (m1[k] - m0[k]).abs().max().item() <= 2e-2 * scale + 1e-7, k

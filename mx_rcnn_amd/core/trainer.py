@@ -38,6 +38,9 @@ class Trainer:
         self.num_update = 0
         self.nonfinite = torch.zeros((), dtype=torch.int32, device=dev)
         self.fault = torch.ones((), dtype=torch.float32, device=dev) if os.environ.get('MXR_FAULT_INJECT') else None
+        # the loss-combine kernel bumps the counter (one launch for loss, objective and guard);
+        # with fault injection the guard must see the poisoned objective, so the trainer keeps it
+        self.model.nonfinite_counter = self.nonfinite if self.fault is None else None
 
     # ------------------------------------------------------------------
     def prepare_batch(self, batch):
@@ -72,8 +75,10 @@ class Trainer:
         if self.fault is not None:  # test hook: multiplies the loss by NaN on the armed step
             out['loss'] = out['loss'] * self.fault
             out['objective'] = out['objective'] * self.fault
-        # device-side non-finite guard: no host sync, read every `frequent` steps
-        self.nonfinite.add_((~torch.isfinite(out['objective'])).to(torch.int32))
+        # device-side non-finite guard: no host sync, read every `frequent` steps;
+        # counted by the model's loss-combine kernel unless fault injection is armed
+        if self.model.nonfinite_counter is None:
+            self.nonfinite.add_((~torch.isfinite(out['objective'])).to(torch.int32))
         with prof.range('backward+allreduce'):
             out['loss'].backward()
         with prof.range('allreduce_wait'):

@@ -116,7 +116,7 @@ std::vector<Tensor> anchor_sample(const Tensor& label_pre, const Tensor& targets
                      reinterpret_cast<uint32_t*>(kept.data_ptr<int32_t>()), meta.data_ptr<int32_t>(),
                      label.data_ptr<int32_t>(), bt.data_ptr<float>(), iw.data_ptr<float>(), ow.data_ptr<float>(),
                      cur_stream());
-  return {label, bt, iw, ow};
+  return {label, bt, iw, ow, meta};
 }
 
 std::vector<Tensor> proposal_sample(const Tensor& rois, const Tensor& gt, const Tensor& n_gt, const Tensor& max_ov,
@@ -238,27 +238,51 @@ Tensor roi_pool_bwd(const Tensor& grad_out, const Tensor& argmax, const Tensor& 
 
 // ---- losses ----------------------------------------------------------------------------
 // returns (grad like logits, loss_sum (1,), prob_fg (B, H*W*A) in (h, w, a) order)
-std::vector<Tensor> rpn_softmax_ce(const Tensor& logits, const Tensor& label, const Tensor& norm, double grad_scale,
-                                   bool want_prob) {
-  CHECK_DEV(logits); CHECK_DEV(label); CHECK_I32(label); CHECK_CONTIG(label); CHECK_DEV(norm); CHECK_F32(norm);
+// Persistent ticket counters of the grid-reduction losses (losses.hip), one slot per call site;
+// zero at allocation and re-armed by the kernels.  Deliberately leaked (no destructor after
+// the HIP runtime has gone at exit).
+static unsigned* loss_ticket(const at::Device& dev, int64_t slot) {
+  static auto* bufs = new std::map<int, Tensor>();
+  TORCH_CHECK(slot >= 0 && slot < 64, "loss ticket slot out of range");
+  auto it = bufs->find(dev.index());
+  if (it == bufs->end())
+    it = bufs->emplace(dev.index(), at::zeros({64}, at::TensorOptions().device(dev).dtype(at::kInt))).first;
+  return reinterpret_cast<unsigned*>(it->second.data_ptr<int32_t>()) + slot;
+}
+
+// returns (grad like logits, loss (1,) already normalised[, prob_fg])
+std::vector<Tensor> rpn_softmax_ce(const Tensor& logits, const Tensor& label, c10::optional<Tensor> norm,
+                                   double grad_scale, bool want_prob, c10::optional<Tensor> meta) {
+  CHECK_DEV(logits); CHECK_DEV(label); CHECK_I32(label); CHECK_CONTIG(label);
   const int B = (int)logits.size(0), C2 = (int)logits.size(1), H = (int)logits.size(2), W = (int)logits.size(3);
   TORCH_CHECK(C2 % 2 == 0, "logits channels must be 2A");
   const int A = C2 / 2;
   TORCH_CHECK(label.numel() == (int64_t)B * A * H * W, "label must be (B, A*H*W)");
+  const bool has_meta = meta.has_value() && meta->defined();
+  if (has_meta) {
+    CHECK_DEV((*meta)); CHECK_I32((*meta)); CHECK_CONTIG((*meta));
+    TORCH_CHECK(meta->numel() == (int64_t)B * 4, "meta must be (B, 4)");
+  } else {
+    TORCH_CHECK(norm.has_value() && norm->defined(), "rpn_softmax_ce: norm or meta required");
+    CHECK_DEV((*norm)); CHECK_F32((*norm));
+  }
   DevGuard g(logits.device());
   Tensor grad = at::empty_like(logits);
   TORCH_CHECK(grad.strides() == logits.strides(), "grad layout must match logits");
-  Tensor loss = at::zeros({1}, logits.options().dtype(at::kFloat));
+  Tensor loss = at::empty({1}, logits.options().dtype(at::kFloat));
+  Tensor partials = at::empty({mxr::loss_blocks_rpn((int64_t)B * A * H * W)}, logits.options().dtype(at::kFloat));
   Tensor prob = want_prob ? at::empty({B, (int64_t)H * W * A}, logits.options().dtype(at::kFloat)) : Tensor();
   mxr::rpn_softmax_ce(logits.data_ptr(), is_bf16(logits), logits.stride(0), logits.stride(1), logits.stride(2),
-                      logits.stride(3), label.data_ptr<int32_t>(), B, A, H, W, norm.data_ptr<float>(),
-                      (float)grad_scale, grad.data_ptr(), loss.data_ptr<float>(),
+                      logits.stride(3), label.data_ptr<int32_t>(), B, A, H, W,
+                      has_meta ? nullptr : norm->data_ptr<float>(), has_meta ? meta->data_ptr<int32_t>() : nullptr,
+                      (float)grad_scale, grad.data_ptr(), partials.data_ptr<float>(),
+                      loss_ticket(logits.device(), 0), loss.data_ptr<float>(),
                       want_prob ? prob.data_ptr<float>() : nullptr, cur_stream());
   if (want_prob) return {grad, loss, prob};
   return {grad, loss};
 }
 
-// returns (grad (R,C) like logits, prob (R,C) fp32, loss_sum (1,))
+// returns (grad (R,C) like logits, prob (R,C) fp32, loss (1,) = sum / norm)
 std::vector<Tensor> row_softmax_ce(const Tensor& logits, const Tensor& label, double norm, double grad_scale,
                                    bool want_grad) {
   CHECK_DEV(logits); CHECK_CONTIG(logits); CHECK_DEV(label); CHECK_I32(label); CHECK_CONTIG(label);
@@ -268,20 +292,25 @@ std::vector<Tensor> row_softmax_ce(const Tensor& logits, const Tensor& label, do
   DevGuard g(logits.device());
   Tensor grad = want_grad ? at::empty_like(logits) : Tensor();
   Tensor prob = at::empty({R, C}, logits.options().dtype(at::kFloat));
-  Tensor loss = at::zeros({1}, logits.options().dtype(at::kFloat));
+  Tensor loss = R > 0 ? at::empty({1}, logits.options().dtype(at::kFloat))
+                      : at::zeros({1}, logits.options().dtype(at::kFloat));  // R == 0 launches nothing
+  Tensor partials = at::empty({std::max(mxr::loss_blocks_row(R), 1)}, logits.options().dtype(at::kFloat));
   mxr::row_softmax_ce(logits.data_ptr(), is_bf16(logits), R, C, label.data_ptr<int32_t>(), (float)norm,
                       (float)grad_scale, want_grad ? grad.data_ptr() : nullptr, prob.data_ptr<float>(),
-                      loss.data_ptr<float>(), cur_stream());
+                      partials.data_ptr<float>(), loss_ticket(logits.device(), 1), loss.data_ptr<float>(),
+                      cur_stream());
   if (want_grad) return {grad, prob, loss};
   return {prob, loss};
 }
 
 // pred (n0,n1,n2,n3) any strides; tgt/in_w/out_w contiguous fp32 of the same logical shape.
+// returns (grad like pred, loss (1,) = sum); `slot`: ticket slot of the call site (2..63)
 std::vector<Tensor> smooth_l1(const Tensor& pred, const Tensor& tgt, const Tensor& in_w, const Tensor& out_w,
-                              double sigma, double grad_scale) {
+                              double sigma, double grad_scale, int64_t slot) {
   CHECK_DEV(pred); CHECK_DEV(tgt); CHECK_F32(tgt); CHECK_CONTIG(tgt);
   CHECK_F32(in_w); CHECK_CONTIG(in_w); CHECK_F32(out_w); CHECK_CONTIG(out_w);
   TORCH_CHECK(pred.dim() <= 4, "pred rank must be <= 4");
+  TORCH_CHECK(slot >= 2, "smooth_l1: ticket slots 0/1 belong to the CE losses");
   Tensor p4 = pred;
   while (p4.dim() < 4) p4 = p4.unsqueeze(0);
   TORCH_CHECK(tgt.numel() == p4.numel() && in_w.numel() == p4.numel() && out_w.numel() == p4.numel(),
@@ -291,12 +320,45 @@ std::vector<Tensor> smooth_l1(const Tensor& pred, const Tensor& tgt, const Tenso
   Tensor g4 = grad;
   while (g4.dim() < 4) g4 = g4.unsqueeze(0);
   TORCH_CHECK(g4.strides() == p4.strides(), "grad layout must match pred");
-  Tensor loss = at::zeros({1}, pred.options().dtype(at::kFloat));
+  Tensor loss = p4.numel() > 0 ? at::empty({1}, pred.options().dtype(at::kFloat))
+                               : at::zeros({1}, pred.options().dtype(at::kFloat));  // empty: no launch
+  Tensor partials = at::empty({std::max(mxr::loss_blocks_rpn(p4.numel()), 1)}, pred.options().dtype(at::kFloat));
   mxr::smooth_l1(p4.data_ptr(), is_bf16(p4), p4.stride(0), p4.stride(1), p4.stride(2), p4.stride(3), (int)p4.size(0),
                  (int)p4.size(1), (int)p4.size(2), (int)p4.size(3), tgt.data_ptr<float>(), in_w.data_ptr<float>(),
-                 out_w.data_ptr<float>(), (float)sigma, (float)grad_scale, g4.data_ptr(), loss.data_ptr<float>(),
-                 cur_stream());
+                 out_w.data_ptr<float>(), (float)sigma, (float)grad_scale, g4.data_ptr(), partials.data_ptr<float>(),
+                 loss_ticket(pred.device(), slot), loss.data_ptr<float>(), cur_stream());
   return {grad, loss};
+}
+
+// x *= s[0] in place
+Tensor scale_by_scalar_(Tensor x, const Tensor& s) {
+  CHECK_DEV(x); CHECK_CONTIG(x); CHECK_DEV(s); CHECK_F32(s);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat, "bf16 / fp32 only");
+  TORCH_CHECK(s.numel() == 1, "scalar expected");
+  DevGuard g(x.device());
+  mxr::scale_by_scalar(x.data_ptr(), is_bf16(x), x.numel(), s.data_ptr<float>(), cur_stream());
+  return x;
+}
+
+// (total, weighted objective) of scalar fp32 loss terms in one launch; nonfinite (int32, 1) += !isfinite(obj)
+Tensor loss_combine(std::vector<Tensor> terms, std::vector<double> weights, c10::optional<Tensor> nonfinite) {
+  TORCH_CHECK(!terms.empty() && terms.size() <= 8 && weights.size() == terms.size(), "1..8 terms with weights");
+  mxr::LossTerms t;
+  t.n = (int)terms.size();
+  for (int i = 0; i < t.n; ++i) {
+    CHECK_DEV(terms[i]); CHECK_F32(terms[i]);
+    TORCH_CHECK(terms[i].numel() == 1, "scalar terms");
+    t.p[i] = terms[i].data_ptr<float>();
+    t.w[i] = (float)weights[i];
+  }
+  if (nonfinite.has_value() && nonfinite->defined()) {
+    CHECK_DEV((*nonfinite)); CHECK_I32((*nonfinite));
+  }
+  DevGuard g(terms[0].device());
+  Tensor out = at::empty({2}, terms[0].options());
+  mxr::loss_combine(t, out.data_ptr<float>(), nonfinite.has_value() && nonfinite->defined() ? nonfinite->data_ptr<int32_t>() : nullptr,
+                    cur_stream());
+  return out;
 }
 
 // ---- optimizer -------------------------------------------------------------------------
@@ -617,9 +679,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("anchor_target_assign", &anchor_target_assign);
   m.def("roi_pool_fwd", &roi_pool_fwd);
   m.def("roi_pool_bwd", &roi_pool_bwd);
-  m.def("rpn_softmax_ce", &rpn_softmax_ce);
+  m.def("rpn_softmax_ce", &rpn_softmax_ce, py::arg("logits"), py::arg("label"), py::arg("norm"), py::arg("grad_scale"),
+        py::arg("want_prob"), py::arg("meta") = py::none());
   m.def("row_softmax_ce", &row_softmax_ce);
-  m.def("smooth_l1", &smooth_l1);
+  m.def("smooth_l1", &smooth_l1, py::arg("pred"), py::arg("tgt"), py::arg("in_w"), py::arg("out_w"), py::arg("sigma"),
+        py::arg("grad_scale"), py::arg("slot") = 2);
+  m.def("scale_by_scalar_", &scale_by_scalar_);
+  m.def("loss_combine", &loss_combine, py::arg("terms"), py::arg("weights"), py::arg("nonfinite") = py::none());
   m.def("sgd_momentum", &sgd_momentum);
   m.def("bn_relu_fwd", &bn_relu_fwd);
   m.def("bn_relu_bwd", &bn_relu_bwd, py::arg("x"), py::arg("dy"), py::arg("gamma"), py::arg("beta"),

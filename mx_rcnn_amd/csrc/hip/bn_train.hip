@@ -9,7 +9,8 @@
 //   fwd 2: every block folds the chunk partials of its 64 channels (a few dozen rows),
 //          derives scale/shift, normalises (+ReLU) its chunk; chunk 0 writes the running
 //          stats (moving = mom * moving + (1 - mom) * batch, unbiased var, as MXNet's cuDNN
-//          path) and the saved mean / invstd.
+//          path) and the saved mean / invstd.  The stats kernel records the shift it used in
+//          the workspace, so no block of this kernel reads the running mean it updates.
 //   bwd 1: partial sum(g), sum(g * xhat) with g = dy * relu_mask
 //   bwd 2: fold partials -> dgamma / dbeta (chunk 0) and dx for the chunk.
 // An earlier one-block-per-8-channels version read every 128-B line 8 times through L2 and
@@ -93,6 +94,8 @@ bn_train_stats_kernel(const uint16_t* __restrict__ x, int64_t M, int C, const fl
     float* row = part + (int64_t)blockIdx.y * 2 * C;
     row[blockIdx.x * BT_C + threadIdx.x] = sa[threadIdx.x];
     row[C + blockIdx.x * BT_C + threadIdx.x] = sb[threadIdx.x];
+    // the shift of these partials, for the norm kernel (which then owns the running stats)
+    if (blockIdx.y == 0) part[(int64_t)gridDim.y * 2 * C + blockIdx.x * BT_C + threadIdx.x] = shift[blockIdx.x * BT_C + threadIdx.x];
   }
 }
 
@@ -105,7 +108,7 @@ bn_train_norm_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int nchun
   const int tid = threadIdx.x;
   if (tid < 64) {
     const int c = blockIdx.x * BT_C + tid;
-    const float sh = rmean[c];  // the shift used by the stats kernel (read before any update)
+    const float sh = part[(int64_t)nchunks * 2 * C + c];  // the shift the stats kernel used
     float a = 0.f, b = 0.f;
     for (int i = 0; i < nchunks; ++i) {
       a += part[(int64_t)i * 2 * C + c];
@@ -121,6 +124,10 @@ bn_train_norm_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int nchun
     if (blockIdx.y == 0) {
       save_mean[c] = mu;
       save_invstd[c] = inv;
+      // running statistics (MXNet cuDNN path: unbiased batch variance); no block reads rmean
+      const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
+      rmean[c] = momentum * rmean[c] + (1.f - momentum) * mu;
+      rvar[c] = momentum * rvar[c] + (1.f - momentum) * unb;
     }
   }
   __syncthreads();
@@ -145,19 +152,6 @@ bn_train_norm_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int nchun
     }
     st8(y + r * C + c0, v);
   }
-}
-
-// running-stat update after every block has read the old running mean (separate launch)
-__global__ void bn_train_running_kernel(int64_t M, int C, const float* __restrict__ save_mean,
-                                        const float* __restrict__ save_invstd, float eps, float momentum,
-                                        float* __restrict__ rmean, float* __restrict__ rvar) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  const float inv = save_invstd[c];
-  const float var = 1.f / (inv * inv) - eps;
-  const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
-  rmean[c] = momentum * rmean[c] + (1.f - momentum) * save_mean[c];
-  rvar[c] = momentum * rvar[c] + (1.f - momentum) * unb;
 }
 
 __global__ void __launch_bounds__(256)
@@ -254,7 +248,7 @@ bn_train_dx_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ 
   }
 }
 
-int bn_train_workspace_floats(int64_t M, int C) { return (int)(((M + BT_ROWS - 1) / BT_ROWS) * 2 * C); }
+int bn_train_workspace_floats(int64_t M, int C) { return (int)(((M + BT_ROWS - 1) / BT_ROWS) * 2 * C + C); }
 
 int bn_train_fwd(const uint16_t* x, int64_t M, int C, const float* gamma, const float* beta, float* rmean,
                  float* rvar, float momentum, float eps, int fix_gamma, int relu, uint16_t* y, float* save_mean,
@@ -265,7 +259,6 @@ int bn_train_fwd(const uint16_t* x, int64_t M, int C, const float* gamma, const 
   bn_train_stats_kernel<<<grid, 256, 0, st>>>(x, M, C, rmean, workspace);
   bn_train_norm_kernel<<<grid, 256, 0, st>>>(x, M, C, nchunks, workspace, gamma, beta, rmean, rvar, momentum, eps,
                                              fix_gamma, relu, y, save_mean, save_invstd);
-  bn_train_running_kernel<<<div_up(C, 256), 256, 0, st>>>(M, C, save_mean, save_invstd, eps, momentum, rmean, rvar);
   return 0;
 }
 

@@ -79,21 +79,39 @@ void roi_pool_bwd(const void* grad_out, int bf16, const int32_t* argmax, const f
 void cast_f32(const float* in, void* out, int out_bf16, int64_t n, hipStream_t st);
 
 // ---- losses (losses.hip) ---------------------------------------------------
+// Every loss kernel writes its final (normalised) value to loss_out[0] itself: blocks store
+// partial sums into `partials` (>= loss_blocks_* floats) and the last block to take a ticket
+// (a persistent counter, zero between launches, re-armed by that block) reduces them.
 // RPN 2-class softmax CE with ignore label -1 ("valid" normalisation).
 // logits (B, 2A, H, W) strided; label (B, A*H*W) int32 in (a, h, w) order.
-// grad written with the same strides as logits; loss_sum[0] += sum of -log p.
-// norm: device float* with the divisor (number of valid labels), read in-kernel.
+// grad written with the same strides as logits.  Divisor: the sampled counts meta (B, 4) =
+// [all_fg, all_bg, n_fg, n_bg] of anchor_sample when given, else *norm (device float).
+int loss_blocks_rpn(int64_t total);
 void rpn_softmax_ce(const void* logits, int bf16, int64_t s0, int64_t s1, int64_t s2, int64_t s3,
-                    const int32_t* label, int B, int A, int H, int W, const float* norm, float grad_scale,
-                    void* grad, float* loss_sum, float* prob_fg, hipStream_t st);
+                    const int32_t* label, int B, int A, int H, int W, const float* norm, const int32_t* meta,
+                    float grad_scale, void* grad, float* partials, unsigned* ticket, float* loss_out,
+                    float* prob_fg, hipStream_t st);
 // Row softmax CE for (R, C) logits, labels int32 (R), ignore < 0; normalisation divisor `norm`.
+int loss_blocks_row(int R);
 void row_softmax_ce(const void* logits, int bf16, int R, int C, const int32_t* label, float norm,
-                    float grad_scale, void* grad, float* prob, float* loss_sum, hipStream_t st);
+                    float grad_scale, void* grad, float* prob, float* partials, unsigned* ticket, float* loss_out,
+                    hipStream_t st);
 // Weighted smooth-L1: out_w * f(in_w * (pred - tgt)), sigma; grad = gs * out_w * f'(.) * in_w.
 // pred strided 4-D (n0, n1, n2, n3); tgt/in_w/out_w contiguous 4-D of the same logical shape.
+// loss_out[0] = sum (blocks: loss_blocks_rpn(n0*n1*n2*n3)).
 void smooth_l1(const void* pred, int bf16, int64_t s0, int64_t s1, int64_t s2, int64_t s3,
                int n0, int n1, int n2, int n3, const float* tgt, const float* in_w, const float* out_w,
-               float sigma, float grad_scale, void* grad, float* loss_sum, hipStream_t st);
+               float sigma, float grad_scale, void* grad, float* partials, unsigned* ticket, float* loss_out,
+               hipStream_t st);
+// x[i] *= s[0] (device scalar), bf16 or fp32, in place.
+void scale_by_scalar(void* x, int bf16, int64_t n, const float* s, hipStream_t st);
+// total / weighted objective of up to 8 scalar loss terms, plus the non-finite step counter.
+struct LossTerms {
+  const float* p[8];
+  float w[8];
+  int n;
+};
+void loss_combine(const LossTerms& t, float* out, int32_t* nonfinite, hipStream_t st);
 
 // ---- optimizer (sgd.hip) ---------------------------------------------------
 // MXNet SGD semantics: g = clip(rescale*g, +-clip) (clip<=0: off); mom = mu*mom - lr*(g + wd*w); w += mom.

@@ -25,7 +25,7 @@ import torch.nn.functional as F
 from ..config import config as _global_cfg, snapshot
 from ..utils import profiler as prof
 from ..ops import anchor_target, proposal, proposal_target, roi_pool
-from ..ops.losses import rpn_softmax_ce, smooth_l1, softmax_ce
+from ..ops.losses import combine_losses, rpn_softmax_ce, smooth_l1, softmax_ce
 from .layers import Conv
 from .resnet import ResNetHead, ResNetTrunk
 from .vgg import VGG16Trunk, VGGHead
@@ -56,6 +56,9 @@ class FasterRCNN(nn.Module):
                  anchor_scales=None, anchor_ratios=RATIOS, resnet_spec=None, train_mode='e2e'):
         super().__init__()
         self.cfg = cfg if cfg is not None else snapshot()
+        # the trainer's device-side non-finite step counter, bumped by the loss-combine kernel
+        # (core/trainer.py hands it over; None = the caller checks the objective itself)
+        self.nonfinite_counter = None
         self.network = network
         self.num_classes = num_classes
         if network == 'vgg16' or network == 'vgg':
@@ -175,9 +178,9 @@ class FasterRCNN(nn.Module):
             at = anchor_target((H, W), gt_boxes, n_gt, im_info, self.feat_stride, self.anchor_scales,
                                self.anchor_ratios, allowed_border=0, cfg=self.cfg)
         assert at['label'].shape[1] == rpn_cls.shape[1] // 2 * H * W, 'anchor grid / RPN map mismatch'
-        cls_loss = rpn_softmax_ce(rpn_cls, at['label'])
+        cls_loss = rpn_softmax_ce(rpn_cls, at['label'], sample_meta=at.get('sample_meta'))
         bbox_loss = smooth_l1(rpn_bbox, at['bbox_target'], at['bbox_inside_weight'], at['bbox_outside_weight'],
-                              sigma=3.0, grad_scale=1.0)
+                              sigma=3.0, grad_scale=1.0, slot=2)
         return cls_loss, bbox_loss, at
 
     def _head_losses(self, cls_score, bbox_pred, label, bbox_target, inside, outside, e2e=True):
@@ -186,7 +189,7 @@ class FasterRCNN(nn.Module):
         1/BATCH_SIZE does the scaling (`rcnn/symbol.py:105-111`, `tools/train_rcnn.py`)."""
         cls_loss, cls_prob = softmax_ce(cls_score, label, 'batch' if e2e else 'null')
         bbox_loss = smooth_l1(bbox_pred, bbox_target, inside, outside, sigma=1.0,
-                              grad_scale=1.0 / float(self.cfg.TRAIN.BATCH_SIZE) if e2e else 1.0)
+                              grad_scale=1.0 / float(self.cfg.TRAIN.BATCH_SIZE) if e2e else 1.0, slot=3)
         return cls_loss, bbox_loss, cls_prob
 
     # ------------------------------------------------------------------ modes
@@ -214,11 +217,12 @@ class FasterRCNN(nn.Module):
                                                               pt['bbox_inside_weight'], pt['bbox_outside_weight'])
         B = data.shape[0]
         R = cls_score.shape[0]
-        loss = rpn_cls_loss + rpn_bbox_loss + cls_loss + bbox_loss
         # 'loss' carries the gradients (each loss applies its own grad_scale in backward); its value
         # mixes normalised and summed terms like the reference's outputs.  'objective' is the
-        # value of the function actually being minimised.
-        obj = (rpn_cls_loss + rpn_bbox_loss + cls_loss + bbox_loss / float(self.cfg.TRAIN.BATCH_SIZE)).detach()
+        # value of the function actually being minimised.  One launch for both (+ the trainer's
+        # non-finite counter when it handed one over).
+        loss, obj = combine_losses([rpn_cls_loss, rpn_bbox_loss, cls_loss, bbox_loss],
+                                   [1.0, 1.0, 1.0, 1.0 / float(self.cfg.TRAIN.BATCH_SIZE)], self.nonfinite_counter)
         return {'loss': loss, 'objective': obj, 'rpn_cls_loss': rpn_cls_loss, 'rpn_bbox_loss': rpn_bbox_loss,
                 'cls_loss': cls_loss, 'bbox_loss': bbox_loss, 'cls_prob': cls_prob, 'label': pt['label'],
                 'rpn_cls_score': rpn_cls, 'rpn_label': at['label'], 'num_images': B, 'num_rois': R}
@@ -228,7 +232,8 @@ class FasterRCNN(nn.Module):
         feat = self.trunk(data)
         rpn_cls, rpn_bbox = self.rpn(feat)
         cls_loss, bbox_loss, at = self._rpn_losses(rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt, at_join())
-        return {'loss': cls_loss + bbox_loss, 'objective': (cls_loss + bbox_loss).detach(),
+        loss, obj = combine_losses([cls_loss, bbox_loss], [1.0, 1.0], self.nonfinite_counter)
+        return {'loss': loss, 'objective': obj,
                 'rpn_cls_loss': cls_loss, 'rpn_bbox_loss': bbox_loss, 'rpn_cls_score': rpn_cls, 'rpn_label': at['label'], 'num_images': data.shape[0]}
 
     def train_rcnn(self, data, rois, label, bbox_target, inside, outside):
@@ -237,8 +242,9 @@ class FasterRCNN(nn.Module):
         cls_score, bbox_pred = self.head(pooled)
         cls_loss, bbox_loss, cls_prob = self._head_losses(cls_score, bbox_pred, label, bbox_target, inside, outside,
                                                           e2e=False)
-        return {'loss': cls_loss + bbox_loss,
-                'objective': ((cls_loss + bbox_loss) / float(self.cfg.TRAIN.BATCH_SIZE)).detach(),
+        k = 1.0 / float(self.cfg.TRAIN.BATCH_SIZE)
+        loss, obj = combine_losses([cls_loss, bbox_loss], [k, k], self.nonfinite_counter)
+        return {'loss': loss, 'objective': obj,
                 'cls_loss': cls_loss, 'bbox_loss': bbox_loss, 'cls_prob': cls_prob,
                 'label': label, 'num_images': data.shape[0], 'num_rois': rois.shape[0]}
 

@@ -79,10 +79,12 @@ def anchor_target(feat_shape, gt_boxes, n_gt, im_info, feat_stride=16, scales=(8
             # fused subsampling + weights + reference layout (csrc/hip/sample.hip): 3 launches
             keys = torch.rand(label.shape, device=dev, generator=generator)
             iw = [float(v) for v in np.asarray(cfg.TRAIN.RPN_BBOX_INSIDE_WEIGHTS, dtype=np.float64).ravel()[:4]]
-            lab, bt, inside, outside = C.anchor_sample(label, targets.contiguous(), keys, A, H, W, num_fg,
-                                                       int(cfg.TRAIN.RPN_BATCH_SIZE), iw,
-                                                       float(cfg.TRAIN.RPN_POSITIVE_WEIGHT))
-            return {'label': lab, 'bbox_target': bt, 'bbox_inside_weight': inside, 'bbox_outside_weight': outside}
+            lab, bt, inside, outside, meta = C.anchor_sample(label, targets.contiguous(), keys, A, H, W, num_fg,
+                                                             int(cfg.TRAIN.RPN_BATCH_SIZE), iw,
+                                                             float(cfg.TRAIN.RPN_POSITIVE_WEIGHT))
+            # meta (B, 4) = [all_fg, all_bg, n_fg, n_bg]: the RPN loss's 'valid' count without a reduction
+            return {'label': lab, 'bbox_target': bt, 'bbox_inside_weight': inside, 'bbox_outside_weight': outside,
+                    'sample_meta': meta}
         else:
             label, targets = _assign_ref(H, W, base, feat_stride, im_info, allowed_border, gt_boxes, n_gt,
                                          cfg.TRAIN.RPN_NEGATIVE_OVERLAP, cfg.TRAIN.RPN_POSITIVE_OVERLAP,

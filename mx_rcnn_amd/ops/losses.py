@@ -17,36 +17,49 @@ from ._ext import need_ext
 
 class _RpnCE(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, logits, label, grad_scale):
+    def forward(ctx, logits, label, grad_scale, meta):
         B, C2, H, W = logits.shape
         A = C2 // 2
         lab = label.to(torch.int32).contiguous()
-        norm = (lab >= 0).sum().float().reshape(1)
         if logits.is_cuda:
             ext = need_ext()
-            grad, loss = ext.rpn_softmax_ce(logits, lab, norm, float(grad_scale), False)
-        else:
-            z = logits.float().reshape(B, 2, A * H, W)
-            p = torch.softmax(z, dim=1)
-            l4 = lab.reshape(B, A * H, W).long()
-            valid = l4 >= 0
-            onehot = torch.stack([(l4 == 0), (l4 == 1)], dim=1).float()
-            g = (p - onehot) * valid[:, None].float() * (grad_scale / norm.clamp_min(1))
-            grad = g.reshape(B, C2, H, W).to(logits.dtype)
-            pl = torch.where(l4 == 1, p[:, 1], p[:, 0]).clamp_min(1e-14)
-            loss = (-(torch.log(pl)) * valid.float()).sum().reshape(1)
+            if meta is not None:  # sampled fg + bg counts from anchor_sample: no count reduction
+                grad, loss = ext.rpn_softmax_ce(logits, lab, None, float(grad_scale), False, meta)
+            else:
+                norm = (lab >= 0).sum().float().reshape(1)
+                grad, loss = ext.rpn_softmax_ce(logits, lab, norm, float(grad_scale), False)
+            ctx.save_for_backward(grad)
+            return loss.reshape(())  # normalised in-kernel
+        norm = (lab >= 0).sum().float().reshape(1)
+        z = logits.float().reshape(B, 2, A * H, W)
+        p = torch.softmax(z, dim=1)
+        l4 = lab.reshape(B, A * H, W).long()
+        valid = l4 >= 0
+        onehot = torch.stack([(l4 == 0), (l4 == 1)], dim=1).float()
+        g = (p - onehot) * valid[:, None].float() * (grad_scale / norm.clamp_min(1))
+        grad = g.reshape(B, C2, H, W).to(logits.dtype)
+        pl = torch.where(l4 == 1, p[:, 1], p[:, 0]).clamp_min(1e-14)
+        loss = (-(torch.log(pl)) * valid.float()).sum().reshape(1)
         ctx.save_for_backward(grad)
         return (loss / norm.clamp_min(1)).reshape(())
 
     @staticmethod
     def backward(ctx, g):
         (grad,) = ctx.saved_tensors
-        return grad * g.to(grad.dtype), None, None
+        return _scale_grad(grad, g), None, None, None
 
 
-def rpn_softmax_ce(logits, label, grad_scale=1.0):
-    """logits (B, 2A, H, W), label (B, A*H*W) in {-1, 0, 1}."""
-    return _RpnCE.apply(logits, label, grad_scale)
+def _scale_grad(grad, g):
+    """The stored loss gradient times the incoming scalar (in place on the GPU: one kernel)."""
+    if grad.is_cuda and grad.is_contiguous() and g.dtype == torch.float32:
+        return need_ext().scale_by_scalar_(grad, g.reshape(1))
+    return grad * g.to(grad.dtype)
+
+
+def rpn_softmax_ce(logits, label, grad_scale=1.0, sample_meta=None):
+    """logits (B, 2A, H, W), label (B, A*H*W) in {-1, 0, 1}.  ``sample_meta`` (B, 4) from the GPU
+    anchor sampler ([all_fg, all_bg, n_fg, n_bg]) supplies the 'valid' count directly."""
+    return _RpnCE.apply(logits, label, grad_scale, sample_meta)
 
 
 class _RowCE(torch.autograd.Function):
@@ -56,14 +69,16 @@ class _RowCE(torch.autograd.Function):
         if logits.is_cuda:
             ext = need_ext()
             grad, prob, loss = ext.row_softmax_ce(logits.contiguous(), lab, float(norm), float(grad_scale), True)
-        else:
-            p = torch.softmax(logits.float(), dim=1)
-            valid = (lab >= 0)
-            onehot = torch.nn.functional.one_hot(lab.long().clamp_min(0), logits.shape[1]).float()
-            grad = ((p - onehot) * valid[:, None].float() * (grad_scale / norm)).to(logits.dtype)
-            prob = p
-            pl = p.gather(1, lab.long().clamp_min(0)[:, None])[:, 0].clamp_min(1e-14)
-            loss = (-torch.log(pl) * valid.float()).sum().reshape(1)
+            ctx.save_for_backward(grad)
+            ctx.mark_non_differentiable(prob)
+            return loss.reshape(()), prob  # divided by norm in-kernel
+        p = torch.softmax(logits.float(), dim=1)
+        valid = (lab >= 0)
+        onehot = torch.nn.functional.one_hot(lab.long().clamp_min(0), logits.shape[1]).float()
+        grad = ((p - onehot) * valid[:, None].float() * (grad_scale / norm)).to(logits.dtype)
+        prob = p
+        pl = p.gather(1, lab.long().clamp_min(0)[:, None])[:, 0].clamp_min(1e-14)
+        loss = (-torch.log(pl) * valid.float()).sum().reshape(1)
         ctx.save_for_backward(grad)
         ctx.mark_non_differentiable(prob)
         return (loss / norm).reshape(()), prob
@@ -71,7 +86,7 @@ class _RowCE(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g, gprob):
         (grad,) = ctx.saved_tensors
-        return grad * g.to(grad.dtype), None, None, None
+        return _scale_grad(grad, g), None, None, None
 
 
 def softmax_ce(logits, label, normalization='batch', grad_scale=1.0):
@@ -88,13 +103,13 @@ def softmax_ce(logits, label, normalization='batch', grad_scale=1.0):
 
 class _SmoothL1(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, pred, target, inside, outside, sigma, grad_scale):
+    def forward(ctx, pred, target, inside, outside, sigma, grad_scale, slot):
         t = target.float().contiguous()
         iw = inside.float().contiguous()
         ow = outside.float().contiguous()
         if pred.is_cuda:
             ext = need_ext()
-            grad, loss = ext.smooth_l1(pred, t, iw, ow, float(sigma), float(grad_scale))
+            grad, loss = ext.smooth_l1(pred, t, iw, ow, float(sigma), float(grad_scale), int(slot))
         else:
             s2 = sigma * sigma
             x = iw * (pred.float() - t)
@@ -110,10 +125,40 @@ class _SmoothL1(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g):
         (grad,) = ctx.saved_tensors
-        return grad * g.to(grad.dtype), None, None, None, None, None
+        return _scale_grad(grad, g), None, None, None, None, None, None
 
 
-def smooth_l1(pred, target, inside_weight, outside_weight, sigma=1.0, grad_scale=1.0):
+def smooth_l1(pred, target, inside_weight, outside_weight, sigma=1.0, grad_scale=1.0, slot=2):
     """Returns sum(outside * f(inside * (pred - target))) (the MakeLoss output summed, i.e. the
-    metric quantity); its autograd gradient is grad_scale * d/dpred of that sum."""
-    return _SmoothL1.apply(pred, target, inside_weight, outside_weight, float(sigma), float(grad_scale))
+    metric quantity); its autograd gradient is grad_scale * d/dpred of that sum.  ``slot``: the
+    GPU kernel's grid-reduction ticket (2..63); calls that may run concurrently need distinct slots."""
+    return _SmoothL1.apply(pred, target, inside_weight, outside_weight, float(sigma), float(grad_scale), int(slot))
+
+
+class _Combine(torch.autograd.Function):
+    """total = sum(terms) (carries the gradient: each term receives the incoming scalar) and
+    objective = sum(w_i * term_i) (detached), plus the non-finite step counter, in one launch."""
+
+    @staticmethod
+    def forward(ctx, weights, nonfinite, *terms):
+        ctx.n = len(terms)
+        if terms[0].is_cuda:
+            out = need_ext().loss_combine([t.reshape(1).float() for t in terms], list(weights), nonfinite)
+            total, obj = out[0], out[1]
+        else:
+            total = sum(terms)
+            obj = sum(w * t for w, t in zip(weights, terms))
+            if nonfinite is not None:
+                nonfinite.add_((~torch.isfinite(obj)).to(nonfinite.dtype))
+        ctx.mark_non_differentiable(obj)
+        return total.reshape(()), obj.reshape(())
+
+    @staticmethod
+    def backward(ctx, g, _gobj):
+        return (None, None) + (g,) * ctx.n
+
+
+def combine_losses(terms, weights, nonfinite=None):
+    """-> (total loss for backward, objective value).  ``nonfinite`` (int32 (1,) or 0-d device
+    counter) is incremented when the objective is not finite (the trainer's guard)."""
+    return _Combine.apply(tuple(float(w) for w in weights), nonfinite, *terms)

@@ -302,6 +302,8 @@ def test_anchor_sample_fused_counts_and_uniformity(cuda):
         assert torch.all(pre_ahw[lab == 1] == 1) and torch.all(pre_ahw[lab == 0] == 0)
         ow = out['bbox_outside_weight'].cpu()
         assert torch.allclose(ow.sum(), torch.tensor(4.0), atol=1e-4)  # 4 coords x (1 / num_examples) each
+        meta = out['sample_meta'].cpu()  # [all_fg, all_bg, n_fg, n_bg]: the RPN loss normaliser
+        assert int(meta[:, 2].sum()) == nf and int(meta[:, 3].sum()) == nb
         hits += (lab == 0).float()[0]
     # every bg-pool anchor is picked with probability nb / nbg_pre: mean hit rate over the pool
     bg_pool = (pre_ahw[0] == 0)

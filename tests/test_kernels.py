@@ -378,3 +378,43 @@ def test_direct_grad_delivery(cuda):
     ops.frozen_bn_relu(xb, gm, bm, mean, var).float().sum().backward()
     assert torch.allclose(gm.grad, gr.grad, atol=1e-2, rtol=1e-3)
     assert torch.allclose(bm.grad, br.grad, atol=1e-2, rtol=1e-3)
+
+
+@pytest.mark.gpu
+def test_loss_grid_reduction_meta_and_combine(cuda):
+    """Losses finalise in-kernel (last-block reduction, ticket re-armed per launch): repeated
+    many-block launches, the anchor-sampler count as normaliser, the backward scale, and the
+    one-launch loss/objective/non-finite combine."""
+    from mx_rcnn_amd.ops.losses import combine_losses
+    g = torch.Generator().manual_seed(5)
+    B, A, H, W = 2, 12, 50, 84
+    lc = torch.randn(B, 2 * A, H, W, generator=g)
+    label = torch.randint(-1, 2, (B, A * H * W), generator=g, dtype=torch.int32)
+    meta = torch.zeros(B, 4, dtype=torch.int32)
+    meta[:, 2] = (label == 1).sum(1)
+    meta[:, 3] = (label == 0).sum(1)
+    lcr = lc.clone().requires_grad_()
+    ref = ops.rpn_softmax_ce(lcr, label)
+    ref.backward(torch.tensor(2.0))
+    for _ in range(3):
+        for m in (None, meta.to(cuda)):
+            lg = lc.to(cuda).requires_grad_()
+            out = ops.rpn_softmax_ce(lg, label.to(cuda), sample_meta=m)
+            out.backward(torch.tensor(2.0, device=cuda))
+            assert abs(out.item() - ref.item()) <= 1e-4 * abs(ref.item()) + 1e-5
+            assert torch.allclose(lg.grad.cpu(), lcr.grad, atol=1e-6, rtol=1e-3)
+    pred = torch.randn(B, 4 * A, H, W, generator=g)
+    tgt, iw, ow = torch.randn_like(pred), (torch.rand_like(pred) > 0.5).float(), torch.rand_like(pred)
+    s_ref = ops.smooth_l1(pred, tgt, iw, ow, 3.0, 1.0)
+    for _ in range(3):
+        s = ops.smooth_l1(pred.to(cuda), tgt.to(cuda), iw.to(cuda), ow.to(cuda), 3.0, 1.0, slot=5)
+        assert abs(s.item() - s_ref.item()) <= 1e-4 * abs(s_ref.item()) + 1e-4
+    nf = torch.zeros((), dtype=torch.int32, device=cuda)
+    a = torch.tensor(1.5, device=cuda, requires_grad=True)
+    b = torch.tensor(4.0, device=cuda, requires_grad=True)
+    tot, obj = combine_losses([a, b], [1.0, 0.25], nf)
+    tot.backward()
+    assert tot.item() == 5.5 and obj.item() == 2.5 and int(nf) == 0
+    assert a.grad.item() == 1.0 and b.grad.item() == 1.0
+    combine_losses([a, torch.tensor(float('nan'), device=cuda)], [1.0, 1.0], nf)
+    assert int(nf) == 1

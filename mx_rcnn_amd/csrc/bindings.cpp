@@ -73,7 +73,8 @@ std::vector<Tensor> nms_proposals(const Tensor& boxes, const Tensor& scores, con
   TORCH_CHECK(P > 0, "NMS needs at least one box slot");
   DevGuard g(boxes.device());
   const int nb = (P + 63) / 64;
-  TORCH_CHECK(mxr::nms_reduce_lds(P, (int)post) <= 160 * 1024, "NMS LDS budget exceeded (P or post too large)");
+  TORCH_CHECK(mxr::nms_reduce_lds(P, (int)post) + 66 * 1024 <= 160 * 1024,
+              "NMS LDS budget exceeded (P or post too large)");  // + the kernel's static DMA rings
   TORCH_CHECK(nb <= 1024, "NMS supports at most 65536 pre-NMS boxes per image");
   auto st = cur_stream();
   Tensor mask = at::empty({mxr::nms_mask_words(B, P)}, boxes.options().dtype(at::kLong));

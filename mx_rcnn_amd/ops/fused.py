@@ -254,8 +254,9 @@ class _FusedUnitFn(torch.autograd.Function):
         # compute stream (each wgrad only waits for the dY it reads); joined before returning, so
         # gradient-readiness hooks (DP all-reduce) and later frees see finished writes.  Looser
         # joins measured slower on ResNet-101 (scripts/gpu_ab3.sh, 129 img/s per-unit join vs 119
-        # joining once per backward with record_stream, 118 joining one unit late): the wgrad of
-        # unit k shares dY with unit k's dgrad in L2/MALL, a lagging side stream does not
+        # joining once per backward with record_stream, 118 joining one unit late, 122 joining after
+        # the next unit's first dgrad kernel -- with the inputs kept referenced, so not the
+        # allocator): any lag of the side stream behind its unit costs more than the hand-off
         main = torch.cuda.current_stream() if x.is_cuda else None
         side = _side_stream(x.device) if main is not None else None
 

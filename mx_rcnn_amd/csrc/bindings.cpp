@@ -9,6 +9,14 @@
 
 #include "kernels.h"
 
+// a rejected launch (e.g. an LDS request over budget) must raise here, not leave the outputs
+// uninitialised for a later gather to fault on
+#define LAUNCH_CHECK(what)                                                                       \
+  do {                                                                                           \
+    const hipError_t e_ = hipGetLastError();                                                     \
+    TORCH_CHECK(e_ == hipSuccess, what, ": kernel launch failed: ", hipGetErrorString(e_));      \
+  } while (0)
+
 namespace {
 
 using at::Tensor;
@@ -73,13 +81,13 @@ std::vector<Tensor> nms_proposals(const Tensor& boxes, const Tensor& scores, con
   TORCH_CHECK(P > 0, "NMS needs at least one box slot");
   DevGuard g(boxes.device());
   const int nb = (P + 63) / 64;
-  TORCH_CHECK(mxr::nms_reduce_lds(P, (int)post) + 66 * 1024 <= 160 * 1024,
-              "NMS LDS budget exceeded (P or post too large)");  // + the kernel's static DMA rings
+  TORCH_CHECK(mxr::nms_reduce_lds(P, (int)post) <= 160 * 1024, "NMS LDS budget exceeded (P or post too large)");
   TORCH_CHECK(nb <= 1024, "NMS supports at most 65536 pre-NMS boxes per image");
   auto st = cur_stream();
   Tensor mask = at::empty({mxr::nms_mask_words(B, P)}, boxes.options().dtype(at::kLong));
   mxr::nms_mask(boxes.data_ptr<float>(), n_valid.data_ptr<int32_t>(), B, P, (float)thresh,
                 reinterpret_cast<uint64_t*>(mask.data_ptr<int64_t>()), st);
+  LAUNCH_CHECK("nms_mask");
   Tensor rois = at::empty({B, post, 5}, boxes.options());
   Tensor out_scores = at::empty({B, post}, boxes.options());
   Tensor keep = at::empty({B, post}, boxes.options().dtype(at::kLong));
@@ -88,6 +96,7 @@ std::vector<Tensor> nms_proposals(const Tensor& boxes, const Tensor& scores, con
                   reinterpret_cast<const uint64_t*>(mask.data_ptr<int64_t>()), B, P, (int)post,
                   rand_u.data_ptr<float>(), rois.data_ptr<float>(), out_scores.data_ptr<float>(),
                   keep.data_ptr<int64_t>(), n_keep.data_ptr<int32_t>(), st);
+  LAUNCH_CHECK("nms_reduce");
   return {rois, out_scores, keep, n_keep};
 }
 

@@ -13,7 +13,7 @@ import torch
 
 from ._ext import need_ext
 
-MAX_GPU_BOXES = 16384  # one bitmask pass: keep list (4 B/box) + prefetch rings within the 160 KB of LDS
+MAX_GPU_BOXES = 32768  # one bitmask pass: 512 64-box blocks, keep list (4 B/box) within LDS
 
 
 def _greedy_ref(boxes, n_valid, thresh, max_keep=None):

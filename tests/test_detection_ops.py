@@ -314,3 +314,40 @@ def test_anchor_sample_fused_counts_and_uniformity(cuda):
     idx = torch.nonzero(bg_pool).flatten()
     h1, h2 = rate[: len(idx) // 2].mean().item(), rate[len(idx) // 2:].mean().item()
     assert abs(h1 - h2) < 0.15 * expect
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('P,post,nv_frac', [(6000, 300, 1.0), (6000, 300, 0.7), (12000, 6000, 1.0), (3000, 2000, 0.5)])
+def test_nms_proposals_graph_replay(cuda, P, post, nv_frac):
+    """The proposal NMS captured in a hipGraph (as in GraphedStep / bench_test's GraphedDetect)
+    and replayed on new inputs gives the eager result (workspace zeroing is a captured memset)."""
+    from mx_rcnn_amd.ops import need_ext
+    C = need_ext()
+    g = torch.Generator().manual_seed(17)
+
+    def inputs():
+        b = rand_boxes(g, P, 1300)
+        s = torch.sort(torch.rand(P, generator=g), descending=True).values
+        nv = torch.tensor([int(P * nv_frac)], dtype=torch.int32)
+        u = torch.rand(1, post, generator=g)
+        return b[None].to(cuda), s[None].to(cuda).contiguous(), nv.to(cuda), u.to(cuda)
+
+    sb, ss, snv, su = inputs()
+    torch.cuda.synchronize()
+    st = torch.cuda.Stream()
+    st.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(st):
+        C.nms_proposals(sb, ss, snv, 0.7, post, su)
+    torch.cuda.current_stream().wait_stream(st)
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        out = C.nms_proposals(sb, ss, snv, 0.7, post, su)
+    for _ in range(3):
+        b, s, nv, u = inputs()
+        sb.copy_(b), ss.copy_(s), snv.copy_(nv), su.copy_(u)
+        graph.replay()
+        torch.cuda.synchronize()
+        ref = C.nms_proposals(b, s, nv, 0.7, post, u)
+        for a, r in zip(out, ref):
+            assert torch.equal(a, r)

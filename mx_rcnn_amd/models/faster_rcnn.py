@@ -94,7 +94,8 @@ class FasterRCNN(nn.Module):
             nn.init.normal_(self.head.fc7.weight, 0, 0.005)
 
     # ------------------------------------------------------------------ naming / params
-    GRAPH_PARTS = {'rpn': ('trunk', 'rpn'), 'rpn_test': ('trunk', 'rpn'), 'rcnn': ('trunk', 'head')}
+    GRAPH_PARTS = {'rpn': ('trunk', 'rpn'), 'rpn_test': ('trunk', 'rpn'), 'rcnn': ('trunk', 'head'),
+                   'rcnn_test': ('trunk', 'head')}
 
     def mx_layers(self, mode=None):
         """Named layers of the graph ``mode`` builds: the RPN graphs (`rcnn/symbol.py` get_*_rpn)

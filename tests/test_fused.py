@@ -139,7 +139,7 @@ def test_fused_units_match_unfused(cuda, cfg, unit_op, monkeypatch):
     # bf16 activations: ReLU masks flip where the two paths round a pre-activation differently
     # (fused adds the residual in fp32 before rounding), so gradients are compared in relative
     # L2 with a bound of the same size as either path's distance to an fp32 oracle (~5%,
-    # tools/debug_fused2.py); outputs must agree to bf16 rounding.
+    # the fused-vs-unfused comparison); outputs must agree to bf16 rounding.
     assert _rel(o1, o0) <= 1e-2
     assert _rel(x1g, x0g) <= 0.1
     assert set(g0) == set(g1), set(g0) ^ set(g1)

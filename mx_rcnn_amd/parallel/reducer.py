@@ -50,7 +50,7 @@ class BucketReducer:
       last one is exposed after the backward).
     """
 
-    def __init__(self, store, bucket_mb=25, average=False, overlap=True, sgd_bucket_mb=8):
+    def __init__(self, store, bucket_mb=25, average=False, overlap=True, sgd_bucket_mb=8, tail_mb=4):
         self.store = store
         self.world = get_world_size()
         self.average = average
@@ -68,17 +68,30 @@ class BucketReducer:
         if not (self.dp or self.sgd_capable):
             return
         mb = bucket_mb if self.dp else sgd_bucket_mb
+        tail = min(tail_mb, mb) if tail_mb else mb
         for g in store.groups:
             esize = g.grad.element_size()
             cap = max(1, int(mb * (1 << 20) // esize))
-            cur = None
-            for (n, _, _, numel, _, _), off in zip(g.entries, g.offsets):
-                if cur is None or (off + numel - cur.start > cap and cur.end > cur.start):
-                    cur = _Bucket(g, off, off)
-                    self.buckets.append(cur)
-                cur.end = off + numel
-                cur.names.append(n)
-                self._param_bucket[n] = cur
+            tail_cap = max(1, int(tail * (1 << 20) // esize))
+            # cut from the LAST-ready end: the bucket that completes when the backward pass ends
+            # is the only one whose collective is fully exposed, so it is capped at ``tail_mb``;
+            # the rest get ``bucket_mb`` (entries are in readiness order)
+            rev = []  # [start, end, names] from the last-ready end
+            for (n, _, _, numel, _, _), off in reversed(list(zip(g.entries, g.offsets))):
+                cur = rev[-1] if rev else None
+                limit = tail_cap if len(rev) == 1 else cap
+                if cur is None or (cur[1] - off > limit and cur[1] > cur[0]):
+                    cur = [off, off + numel, []]
+                    rev.append(cur)
+                cur[0] = off
+                cur[2].append(n)
+            for start, end, names in reversed(rev):
+                bkt = _Bucket(g, start, start)
+                bkt.end = end
+                bkt.names = list(reversed(names))
+                self.buckets.append(bkt)
+                for n in names:
+                    self._param_bucket[n] = bkt
         if self.overlap or self.sgd_capable:
             for n, p in store.params.items():
                 if n in self._param_bucket:

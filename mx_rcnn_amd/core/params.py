@@ -163,6 +163,29 @@ class FlatParamStore:
             return flat.view(o, kh, kw, i).permute(0, 3, 1, 2)
         return flat.view(shape)
 
+    # ------------------------------------------------------------------ data parallel
+    @torch.no_grad()
+    def broadcast_(self, src=0):
+        """Make every rank start from rank ``src``'s weights (the reference's ranks load one
+        checkpoint; random-init or per-rank-calibrated models would otherwise train apart):
+        the flat fp32 masters (bf16 shadows re-derived), the frozen parameters and the model
+        buffers (BN moving statistics), then the dgrad filter cache."""
+        import torch.distributed as dist
+        for g in self.groups:
+            dist.broadcast(g.master, src)
+            if g.shadow is not None:
+                g.shadow.copy_(g.master.to(g.shadow.dtype))
+        for n in self.fixed_names:
+            dist.broadcast(self.frozen_fp32[n], src)
+            self.params[n].data.copy_(self.frozen_fp32[n].to(self.params[n].dtype))
+        for b in self.model.buffers():
+            if b.is_floating_point() or b.dtype in (torch.int32, torch.int64):
+                t = b.data if b.is_contiguous() else b.data.contiguous()
+                dist.broadcast(t, src)
+                if t is not b.data:
+                    b.data.copy_(t)
+        self.refresh_dgrad_cache()
+
     # ------------------------------------------------------------------ step pieces
     def zero_grad(self):
         for g in self.groups:

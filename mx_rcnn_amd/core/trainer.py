@@ -29,6 +29,8 @@ class Trainer:
         self.store = FlatParamStore(self.model, fixed_param_prefix, compute_dtype, dev, channels_last,
                                    mode=mode if mode in ('rpn', 'rcnn') else None)
         self.reducer = BucketReducer(self.store, bucket_mb=bucket_mb, average=average_grads)
+        if self.reducer.dp:
+            self.store.broadcast_(0)  # identical starting weights on every rank
         self.momentum, self.wd, self.clip, self.rescale = momentum, wd, clip_gradient, rescale_grad
         self.base_lr = lr
         self.lr_scheduler = lr_scheduler

@@ -94,3 +94,36 @@ def test_alternate_training_two_ranks(tmp_path):
     from mx_rcnn_amd.data.cache import load_box_list
     boxes = load_box_list(str(tmp_path / 'rpn_data' / 'synthetic_rpn.npz'))
     assert len(boxes) == 5 and all(b.shape[1] == 5 for b in boxes)
+
+
+def _bcast_worker(rank, world, port, out_dir):
+    os.environ.update({'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port), 'RANK': str(rank),
+                       'WORLD_SIZE': str(world), 'LOCAL_RANK': str(rank)})
+    from mx_rcnn_amd.config import snapshot
+    from mx_rcnn_amd.core.trainer import Trainer
+    from mx_rcnn_amd.models import FasterRCNN
+    from mx_rcnn_amd.parallel import dist as pdist
+    pdist.init_distributed(backend='gloo')
+    torch.manual_seed(rank)  # deliberately different initialisations
+    m = FasterRCNN('resnet18', 6, cfg=snapshot())
+    for b in m.buffers():
+        if b.is_floating_point():
+            b.add_(float(rank))
+    tr = Trainer(m, 'e2e', fixed_param_prefix=['conv0', 'stage1'], device='cpu')
+    st = {k: v.clone() for k, v in tr.store.state_arrays().items()}
+    st.update({'buf%d' % i: b.clone() for i, b in enumerate(tr.model.buffers())})
+    torch.save(st, os.path.join(out_dir, 'b%d.pt' % rank))
+    pdist.barrier()
+    pdist.destroy()
+
+
+def test_dp_ranks_start_from_rank0_weights():
+    """Data parallel training starts every rank from rank 0's parameters and buffers."""
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_bcast_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        r0 = torch.load(os.path.join(d, 'b0.pt'), weights_only=True)
+        r1 = torch.load(os.path.join(d, 'b1.pt'), weights_only=True)
+    assert r0.keys() == r1.keys()
+    for k in r0:
+        assert torch.equal(r0[k], r1[k]), k

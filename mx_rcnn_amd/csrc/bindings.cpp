@@ -1,6 +1,7 @@
 // Python bindings for the gfx950 kernels.  Thin: validate shapes/dtypes/devices, allocate
 // outputs through the PyTorch caching allocator, launch on the current HIP stream.  All
 // launches are graph-capturable (no host sync, no allocation inside the launchers).
+#include <algorithm>
 #include <cstring>
 #include <map>
 #include <torch/extension.h>
@@ -679,10 +680,43 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int
 
 }  // namespace
 
+// ---- CPU twin of the proposal NMS (host C++, the CPU configuration and the test oracle's
+// fast path): greedy over score-sorted boxes, suppress j when IoU(i, j) > thresh with +1-pixel
+// areas, stop after max_keep kept (<= 0: no cap).  Returns kept positions (int64).
+Tensor nms_cpu(const Tensor& boxes_in, int64_t n_valid, double thresh, int64_t max_keep) {
+  TORCH_CHECK(!boxes_in.is_cuda(), "nms_cpu takes CPU boxes");
+  TORCH_CHECK(boxes_in.dim() == 2 && boxes_in.size(1) == 4, "boxes must be (P, 4)");
+  const Tensor boxes = boxes_in.to(at::kDouble).contiguous();
+  const int64_t n = std::min<int64_t>(n_valid, boxes.size(0));
+  const double* b = boxes.data_ptr<double>();
+  std::vector<double> area(std::max<int64_t>(n, 0));
+  for (int64_t i = 0; i < n; ++i) area[i] = (b[4 * i + 2] - b[4 * i] + 1.0) * (b[4 * i + 3] - b[4 * i + 1] + 1.0);
+  std::vector<uint8_t> removed(std::max<int64_t>(n, 0), 0);
+  std::vector<int64_t> keep;
+  for (int64_t i = 0; i < n; ++i) {
+    if (removed[i]) continue;
+    keep.push_back(i);
+    if (max_keep > 0 && (int64_t)keep.size() >= max_keep) break;
+    const double x1 = b[4 * i], y1 = b[4 * i + 1], x2 = b[4 * i + 2], y2 = b[4 * i + 3];
+    for (int64_t j = i + 1; j < n; ++j) {
+      if (removed[j]) continue;
+      const double w = std::min(x2, b[4 * j + 2]) - std::max(x1, b[4 * j]) + 1.0;
+      const double h = std::min(y2, b[4 * j + 3]) - std::max(y1, b[4 * j + 1]) + 1.0;
+      if (w <= 0.0 || h <= 0.0) continue;
+      const double inter = w * h;
+      if (inter / (area[i] + area[j] - inter) > thresh) removed[j] = 1;
+    }
+  }
+  Tensor out = at::empty({(int64_t)keep.size()}, at::TensorOptions().dtype(at::kLong));
+  std::copy(keep.begin(), keep.end(), out.data_ptr<int64_t>());
+  return out;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mx_rcnn_amd gfx950 kernels";
   m.def("proposal_decode", &proposal_decode);
   m.def("nms_proposals", &nms_proposals);
+  m.def("nms_cpu", &nms_cpu);
   m.def("iou_max", &iou_max);
   m.def("anchor_sample", &anchor_sample);
   m.def("proposal_sample", &proposal_sample);

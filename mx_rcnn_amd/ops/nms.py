@@ -17,10 +17,19 @@ MAX_GPU_BOXES = 32768  # one bitmask pass: 512 64-box blocks, keep list (4 B/box
 
 
 def _greedy_ref(boxes, n_valid, thresh, max_keep=None):
-    """boxes already score-sorted (P, 4); returns list of kept positions among the first n_valid."""
+    """boxes already score-sorted (P, 4); returns list of kept positions among the first n_valid.
+    Runs the extension's C++ twin when it is built (CPU configuration), else the tensor loop
+    below (the oracle the twin is tested against)."""
     n = int(n_valid)
     if n == 0:
         return []
+    from ._ext import ext_available
+    if ext_available() and not boxes.is_cuda:
+        return need_ext().nms_cpu(boxes[:n], n, float(thresh), -1 if max_keep is None else int(max_keep)).tolist()
+    return _greedy_loop(boxes, n, thresh, max_keep)
+
+
+def _greedy_loop(boxes, n, thresh, max_keep=None):
     b = boxes[:n].double()
     x1, y1, x2, y2 = b[:, 0], b[:, 1], b[:, 2], b[:, 3]
     areas = (x2 - x1 + 1) * (y2 - y1 + 1)

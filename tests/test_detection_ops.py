@@ -351,3 +351,20 @@ def test_nms_proposals_graph_replay(cuda, P, post, nv_frac):
         ref = C.nms_proposals(b, s, nv, 0.7, post, u)
         for a, r in zip(out, ref):
             assert torch.equal(a, r)
+
+
+def test_nms_cpu_twin_matches_tensor_loop():
+    """The C++ CPU twin of the greedy NMS (the CPU configuration's fast path) keeps exactly what
+    the tensor-loop oracle keeps, including duplicate boxes and the max_keep cap."""
+    from mx_rcnn_amd.ops import ext_available, need_ext
+    from mx_rcnn_amd.ops.nms import _greedy_loop
+    if not ext_available():
+        pytest.skip('extension not built')
+    g = torch.Generator().manual_seed(21)
+    for n, th, cap in [(1, 0.5, None), (200, 0.7, None), (1500, 0.5, 100), (3000, 0.3, None), (700, 0.0, None)]:
+        b = rand_boxes(g, n, 600)
+        if n > 10:
+            b[5:10] = b[0]  # exact duplicates
+        ref = _greedy_loop(b, n, th, cap)
+        got = need_ext().nms_cpu(b, n, th, -1 if cap is None else cap).tolist()
+        assert got == ref, (n, th, cap)

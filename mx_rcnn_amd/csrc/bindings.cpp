@@ -2,9 +2,11 @@
 // outputs through the PyTorch caching allocator, launch on the current HIP stream.  All
 // launches are graph-capturable (no host sync, no allocation inside the launchers).
 #include <algorithm>
+#include <cmath>
 #include <cstring>
 #include <map>
 #include <torch/extension.h>
+#include <ATen/Parallel.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 
@@ -712,11 +714,68 @@ Tensor nms_cpu(const Tensor& boxes_in, int64_t n_valid, double thresh, int64_t m
   return out;
 }
 
+// ---- CPU twin of the RoI max-pool forward (MXNet ROIPooling semantics, as roi_pool.hip):
+// roundf RoI corners, float32 bin edges with floor / ceil, first maximum in row-major order
+// (strict '>'), empty bins -> 0 with argmax -1.  feat (B, C, H, W) fp32, rois (R, 5).
+std::vector<Tensor> roi_pool_fwd_cpu(const Tensor& feat_in, const Tensor& rois_in, int64_t PH, int64_t PW,
+                                     double spatial_scale) {
+  TORCH_CHECK(!feat_in.is_cuda() && feat_in.dim() == 4, "feat must be a CPU (B, C, H, W) tensor");
+  const Tensor feat = feat_in.to(at::kFloat).contiguous();
+  const Tensor rois = rois_in.to(at::kFloat).contiguous();
+  TORCH_CHECK(rois.dim() == 2 && rois.size(1) == 5, "rois must be (R, 5)");
+  const int64_t B = feat.size(0), C = feat.size(1), H = feat.size(2), W = feat.size(3), R = rois.size(0);
+  Tensor out = at::zeros({R, C, PH, PW}, feat.options());
+  Tensor arg = at::full({R, C, PH, PW}, -1, feat.options().dtype(at::kInt));
+  const float* f = feat.data_ptr<float>();
+  const float* ro = rois.data_ptr<float>();
+  float* o = out.data_ptr<float>();
+  int32_t* a = arg.data_ptr<int32_t>();
+  const float sc = (float)spatial_scale;
+  at::parallel_for(0, R, 1, [&](int64_t r0, int64_t r1) {
+    for (int64_t r = r0; r < r1; ++r) {
+      const float* roi = ro + r * 5;
+      const int64_t b = (int64_t)roi[0];
+      if (b < 0 || b >= B) continue;
+      const int x1 = (int)std::round(roi[1] * sc), y1 = (int)std::round(roi[2] * sc);
+      const int x2 = (int)std::round(roi[3] * sc), y2 = (int)std::round(roi[4] * sc);
+      const int rw = std::max(x2 - x1 + 1, 1), rh = std::max(y2 - y1 + 1, 1);
+      const float bh = (float)rh / (float)PH, bw = (float)rw / (float)PW;
+      for (int64_t ph = 0; ph < PH; ++ph) {
+        const int hs = (int)std::min<int64_t>(std::max<int64_t>((int64_t)std::floor((float)ph * bh) + y1, 0), H);
+        const int he = (int)std::min<int64_t>(std::max<int64_t>((int64_t)std::ceil((float)(ph + 1) * bh) + y1, 0), H);
+        for (int64_t pw = 0; pw < PW; ++pw) {
+          const int ws = (int)std::min<int64_t>(std::max<int64_t>((int64_t)std::floor((float)pw * bw) + x1, 0), W);
+          const int we = (int)std::min<int64_t>(std::max<int64_t>((int64_t)std::ceil((float)(pw + 1) * bw) + x1, 0), W);
+          if (he <= hs || we <= ws) continue;
+          for (int64_t c = 0; c < C; ++c) {
+            const float* fc = f + ((b * C + c) * H) * W;
+            float best = fc[hs * W + ws];
+            int bi = hs * (int)W + ws;
+            for (int h = hs; h < he; ++h)
+              for (int w = ws; w < we; ++w) {
+                const float v = fc[h * W + w];
+                if (v > best) {
+                  best = v;
+                  bi = h * (int)W + w;
+                }
+              }
+            const int64_t oi = ((r * C + c) * PH + ph) * PW + pw;
+            o[oi] = best;
+            a[oi] = bi;
+          }
+        }
+      }
+    }
+  });
+  return {out, arg};
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mx_rcnn_amd gfx950 kernels";
   m.def("proposal_decode", &proposal_decode);
   m.def("nms_proposals", &nms_proposals);
   m.def("nms_cpu", &nms_cpu);
+  m.def("roi_pool_fwd_cpu", &roi_pool_fwd_cpu);
   m.def("iou_max", &iou_max);
   m.def("anchor_sample", &anchor_sample);
   m.def("proposal_sample", &proposal_sample);

@@ -418,3 +418,21 @@ def test_loss_grid_reduction_meta_and_combine(cuda):
     assert a.grad.item() == 1.0 and b.grad.item() == 1.0
     combine_losses([a, torch.tensor(float('nan'), device=cuda)], [1.0, 1.0], nf)
     assert int(nf) == 1
+
+
+def test_roi_pool_cpu_twin_matches_reference():
+    """C++ CPU RoI max-pool == the loop reference (ties -> first max in row-major order, empty
+    bins, RoIs outside the map and an out-of-range batch index)."""
+    from mx_rcnn_amd.ops import ext_available, need_ext
+    if not ext_available():
+        pytest.skip('extension not built')
+    g = torch.Generator().manual_seed(3)
+    feat = torch.randn(2, 5, 23, 31, generator=g)
+    feat[0, :, 3:8, 4:9] = 1.5  # plateau: tie-breaking
+    rois = torch.tensor([[0, 10, 20, 200, 150], [1, 0, 0, 15, 15], [0, 300, 300, 900, 900],
+                         [1, -40, -40, 40, 40], [5, 0, 0, 100, 100], [0, 64, 48, 64.4, 48.6]])
+    for ph, pw, sc in [(7, 7, 1.0 / 16), (3, 5, 0.125), (14, 14, 0.0625)]:
+        ref_o, ref_a = roi_pool_ref(feat, rois, ph, pw, sc)
+        o, a = need_ext().roi_pool_fwd_cpu(feat, rois, ph, pw, sc)
+        assert torch.equal(a, ref_a), (ph, pw, sc)
+        assert torch.equal(o, ref_o), (ph, pw, sc)

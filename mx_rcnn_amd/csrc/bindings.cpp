@@ -17,7 +17,8 @@
 #define LAUNCH_CHECK(what)                                                                       \
   do {                                                                                           \
     const hipError_t e_ = hipGetLastError();                                                     \
-    TORCH_CHECK(e_ == hipSuccess, what, ": kernel launch failed: ", hipGetErrorString(e_));      \
+    TORCH_CHECK(e_ == hipSuccess || e_ == hipErrorNotReady, what, ": kernel launch failed: ",     \
+                hipGetErrorString(e_));                                                          \
   } while (0)
 
 namespace {

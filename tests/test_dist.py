@@ -127,3 +127,25 @@ def test_dp_ranks_start_from_rank0_weights():
     assert r0.keys() == r1.keys()
     for k in r0:
         assert torch.equal(r0[k], r1[k]), k
+
+
+def test_bench_two_ranks_contract(tmp_path):
+    """bench.py under torchrun with 2 gloo ranks (the driver's N>1 launch shape, on the CPU):
+    one JSON line from rank 0 with the whole-job value and dp2 config."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root, CUDA_VISIBLE_DEVICES='', HIP_VISIBLE_DEVICES='')
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', '2',
+           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), os.path.join(root, 'bench.py'),
+           '--gpus', '2', '--steps', '2', '--warmup', '1', '--network', 'resnet18', '--image', '256x320',
+           '--num-classes', '6']
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, r.stdout[-2000:]
+    rec = json.loads(lines[0])
+    assert rec['n_gpus'] == 2 and rec['steps'] == 2 and rec['warmup'] == 1 and rec['scaling'] == 'weak'
+    assert rec['config']['parallelism'] == 'dp2' and rec['config']['global_batch'] == 2
+    assert abs(rec['value'] - 2 * 2 / (rec['ms_per_step'] * 2 / 1e3)) <= 0.01 * rec['value'] + 1e-3

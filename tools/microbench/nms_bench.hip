@@ -96,18 +96,6 @@ int main(int argc, char** argv) {
   }
   printf("P=%d post=%d  mask %.1f us  reduce %.1f us  n_keep %d (cpu %d)\n", P, post, tm / iters * 1e3,
          tr / iters * 1e3, nk, nk_ref);
-#ifdef NMS_DEBUG
-  int dbg[4];
-  CK(hipMemcpyFromSymbol(dbg, HIP_SYMBOL(mxr::g_nms_dbg), sizeof(dbg)));
-  printf("debug counters: mask_ent %d reduce_ent %d near %d removed %d\n", dbg[0], dbg[1], dbg[2], dbg[3]);
-  {
-    const int nbb = (P + 63) / 64;
-    std::vector<int> cnt(nbb);
-    CK(hipMemcpy(cnt.data(), reinterpret_cast<char*>(d_mask) + (int64_t)nbb * 128 * 8, nbb * 4, hipMemcpyDeviceToHost));
-    long tot = 0;
-    for (int v : cnt) tot += v;
-    printf("row-list counts: row0 %d row1 %d total %ld (cap/row %d)\n", cnt[0], cnt[1], tot, nbb * 64);
-  }
-#endif
+
   return 0;
 }

@@ -6,14 +6,20 @@
 // BM output pixels straight from the NHWC map (out-of-image taps read as zero), so both
 // operands are K-contiguous in memory and land in LDS as [row][64] bf16 tiles (128 B rows)
 // with an XOR swizzle on the 16-B chunk index (chunk ^ ((row >> 1) & 7)), which makes the
-// MFMA-operand ds_read_b128 of 16 consecutive rows conflict-free.  Register-staged loads
-// for step k+1 are issued before the MFMAs of step k and written to the other LDS buffer
-// after them (one barrier per K-step).
+// MFMA-operand ds_read_b128 of 16 consecutive rows conflict-free.  256 threads = 4 wave64 in a
+// 2x2 arrangement, wave tile (BM/2)x(BN/2) of v_mfma_f32_16x16x32_bf16 (fp32 accumulate); 1-D
+// grid with a bijective XCD remap so the column tiles sharing an A row-panel run on one XCD's L2.
 //
-// 256 threads = 4 wave64 in a 2x2 arrangement, wave tile (BM/2)x(BN/2) built from
-// v_mfma_f32_16x16x32_bf16 (fp32 accumulate).  Grid is 1-D with a bijective XCD remap so
-// the column tiles sharing an A row-panel run on one XCD's L2.  Epilogue fuses bias and
-// ReLU and stores bf16.  Requirements (checked by the launcher): Cin % 64 == 0.
+// Variants (tile codes; conv_igemm_plan picks 22 / 23 with split-K only for small grids):
+//   1-3     register-staged loads, double-buffered LDS (the first version; test oracle shapes)
+//   11-16   global_load_lds DMA straight into an S-deep LDS ring, counted vmcnt + raw barrier
+//   21-25   the production path: buffer-resource DMA (buffer_load ... lds).  Per lane a 32-bit
+//           row offset and a 64-bit tap mask are precomputed once, the per-step offsets are
+//           uniform (SGPR), padding comes from the buffer range check returning zeros
+//   26-27   experimental: two 4-wave groups per workgroup split one tile's K-steps
+// Epilogues (ConvEpi): bias, ReLU, residual add, frozen BN+ReLU of the consumer (second output),
+// BN-backward column sums (dgrad fused with the BN backward), fp32 split-K slab + reduce; the
+// LDS-transposed epilogue makes every global access a 16-B vector.  Cin % 64 == 0.
 //
 // The same kernel computes the stride-1 data gradient (dgrad) as a forward convolution of
 // dY with the flipped / transposed filter (pad' = k-1-pad); see ops/conv.py.

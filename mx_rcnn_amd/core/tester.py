@@ -13,9 +13,14 @@ from ..config import config
 from ..processing import image_processing
 
 
-def pred_eval(detector, test_data, imdb, vis=False, thresh=0.05, max_per_image=100):
+def pred_eval(detector, test_data, imdb, vis=False, thresh=0.05, max_per_image=100, shard=(0, 1)):
+    """``shard=(rank, world)``: ``test_data`` holds images ``rank::world`` of the image set (the
+    reference tests on one GPU).  Per-rank detections are gathered and interleaved back into
+    image order; rank 0 writes the cache and evaluates, and the result is broadcast so every
+    rank returns the same value."""
     assert not test_data.shuffle
-    num_images = imdb.num_images
+    rank, world = shard
+    num_images = len(range(rank, imdb.num_images, world))
     all_boxes = [[np.zeros((0, 5), np.float32) for _ in range(num_images)] for _ in range(imdb.num_classes)]
     i = 0
     for batch in test_data:
@@ -38,6 +43,22 @@ def pred_eval(detector, test_data, imdb, vis=False, thresh=0.05, max_per_image=1
                 vis_all_detection(batch['data'].numpy() if torch.is_tensor(batch['data']) else batch['data'],
                                   dets, imdb.classes)
             i += 1
+    if world > 1:
+        import torch.distributed as dist
+        parts = [None] * world
+        dist.all_gather_object(parts, all_boxes)
+        num_images = imdb.num_images
+        all_boxes = [[parts[k % world][j][k // world] for k in range(num_images)] for j in range(imdb.num_classes)]
+        result = [None]
+        if rank == 0:
+            result[0] = _cache_and_evaluate(imdb, all_boxes)
+        dist.broadcast_object_list(result, src=0)
+        return result[0]
+    return _cache_and_evaluate(imdb, all_boxes)
+
+
+def _cache_and_evaluate(imdb, all_boxes):
+    num_images = imdb.num_images
     if getattr(imdb, 'cache_path', None):
         cache_folder = os.path.join(imdb.cache_path, imdb.name)
         os.makedirs(cache_folder, exist_ok=True)

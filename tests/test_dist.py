@@ -149,3 +149,58 @@ def test_bench_two_ranks_contract(tmp_path):
     assert rec['n_gpus'] == 2 and rec['steps'] == 2 and rec['warmup'] == 1 and rec['scaling'] == 'weak'
     assert rec['config']['parallelism'] == 'dp2' and rec['config']['global_batch'] == 2
     assert abs(rec['value'] - 2 * 2 / (rec['ms_per_step'] * 2 / 1e3)) <= 0.01 * rec['value'] + 1e-3
+
+
+class _FakeImdb:
+    num_images, num_classes, name = 5, 3, 'fake'
+
+    def evaluate_detections(self, all_boxes):
+        # image k of class j carries the score k + j / 10; the result encodes the order
+        return [[float(all_boxes[j][k][0, 4]) for k in range(self.num_images)] for j in range(1, self.num_classes)]
+
+
+class _FakeLoader:
+    shuffle = False
+
+    def __init__(self, image_ids):
+        self.ids = image_ids
+
+    def __iter__(self):
+        for k in self.ids:
+            yield {'data': None, 'im_info': None, 'k': k}
+
+
+class _FakeDetector:
+    def __init__(self, loader):
+        self.it = iter(loader.ids)
+
+    def detect_batch(self, data, im_info, thresh, nms, max_per_image, rois=None):
+        k = next(self.it)
+        boxes = torch.tensor([[0., 0, 10, 10], [1., 1, 11, 11]])
+        return [(boxes, torch.tensor([k + 0.1, k + 0.2]), torch.tensor([1, 2]))]
+
+
+def _eval_worker(rank, world, port, out_dir):
+    os.environ.update({'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port), 'RANK': str(rank),
+                       'WORLD_SIZE': str(world), 'LOCAL_RANK': str(rank)})
+    from mx_rcnn_amd.parallel import dist as pdist
+    from mx_rcnn_amd.core.tester import pred_eval
+    from mx_rcnn_amd.config import config
+    pdist.init_distributed(backend='gloo')
+    config.TEST.HAS_RPN = True
+    loader = _FakeLoader(list(range(rank, _FakeImdb.num_images, world)))
+    res = pred_eval(_FakeDetector(loader), loader, _FakeImdb(), shard=(rank, world))
+    torch.save(torch.tensor(res), os.path.join(out_dir, 'e%d.pt' % rank))
+    pdist.barrier()
+    pdist.destroy()
+
+
+def test_sharded_pred_eval_two_ranks():
+    """Images rank::world per rank are gathered back in image order; every rank gets rank 0's
+    evaluation."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_eval_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        e0 = torch.load(os.path.join(d, 'e0.pt'), weights_only=True)
+        e1 = torch.load(os.path.join(d, 'e1.pt'), weights_only=True)
+    want = torch.tensor([[k + 0.1 for k in range(5)], [k + 0.2 for k in range(5)]])
+    assert torch.allclose(e0, want) and torch.equal(e0, e1)

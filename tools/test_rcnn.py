@@ -19,24 +19,27 @@ from mx_rcnn_amd.utils.load_model import load_param  # noqa: E402
 
 
 def test_rcnn(image_set, year, root_path, devkit_path, prefix, epoch, ctx, vis=False, has_rpn=True,
-              proposal='rpn', network='vgg16', end2end=False, imdb_roidb=None):
+              proposal='rpn', network='vgg16', end2end=False, imdb_roidb=None, shard=(0, 1)):
+    """``shard=(rank, world)``: each rank runs images ``rank::world`` and ``pred_eval`` gathers
+    them (one process per GPU under torchrun; the reference tests on a single device)."""
+    rank, world = shard
     if imdb_roidb is not None:  # e.g. synthetic set (in-memory evaluation)
         config.TEST.HAS_RPN = True
         imdb, roidb = imdb_roidb
-        test_data = AnchorLoader(None, roidb, batch_size=1, shuffle=False, mode='test')
+        test_data = AnchorLoader(None, roidb[rank::world], batch_size=1, shuffle=False, mode='test')
     elif has_rpn:
         config.TEST.HAS_RPN = True
         config.TEST.RPN_PRE_NMS_TOP_N = 6000
         config.TEST.RPN_POST_NMS_TOP_N = 300
         imdb, roidb = load_data.load_gt_roidb(image_set, year, root_path, devkit_path)
-        test_data = AnchorLoader(None, roidb, batch_size=1, shuffle=False, mode='test')
+        test_data = AnchorLoader(None, roidb[rank::world], batch_size=1, shuffle=False, mode='test')
     else:
         imdb, roidb = getattr(load_data, 'load_test_%s_roidb' % proposal)(image_set, year, root_path, devkit_path)
-        test_data = ROIIter(roidb, batch_size=1, shuffle=False, mode='test')
+        test_data = ROIIter(roidb[rank::world], batch_size=1, shuffle=False, mode='test')
     arg, aux, num_classes = load_param(prefix, epoch, convert=False)
     model, _, _ = launch.build_model(network, num_classes, train_mode='test')
     det = Detector(model, ctx, arg, aux)
-    return pred_eval(det, test_data, imdb, vis=vis)
+    return pred_eval(det, test_data, imdb, vis=vis, shard=shard)
 
 
 def parse_args(argv=None):
@@ -62,4 +65,4 @@ if __name__ == '__main__':
     rank, world, dev = launch.init_runtime(a)
     syn = launch.synthetic_roidb(a, a.num_classes) if a.synthetic else None
     test_rcnn(a.image_set, a.year, a.root_path, a.devkit_path, a.prefix, a.epoch, dev, a.vis,
-              a.has_rpn or a.end2end, a.proposal, a.network, a.end2end, imdb_roidb=syn)
+              a.has_rpn or a.end2end, a.proposal, a.network, a.end2end, imdb_roidb=syn, shard=(rank, world))

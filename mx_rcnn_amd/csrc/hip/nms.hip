@@ -37,7 +37,7 @@ nms_mask_kernel(const float* __restrict__ boxes, const int32_t* __restrict__ n_v
   if (blockIdx.x * 4 + 3 < rb) return;  // whole group below the diagonal
   const int cb = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const int nv = n_valid[b];
+  const int nv = min(n_valid[b], P);  // a count above P must not walk past the image's boxes
   const int row0 = rb * 64;
   const int64_t Pp = (int64_t)nb * 64;
   __shared__ float4 rbox[64];
@@ -71,20 +71,25 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
                   const float* __restrict__ rand_u, float* __restrict__ rois, float* __restrict__ out_scores,
                   int64_t* __restrict__ keep_idx, int32_t* __restrict__ n_keep_out) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  // single dynamic LDS region (Guideline 17): [nkeep i32 | pad][removed nb u64][keptw nb u64][keep_list post i32]
-  int& s_nkeep = *reinterpret_cast<int*>(smem);
+  // single dynamic LDS region (Guideline 17): [nkeep 2 x i32 | pad][removed nb u64][keptw nb u64][keep_list post i32]
+  // The kept count is double-buffered: iteration t reads s_nk[t & 1] (written in t-1) and wave 0
+  // writes s_nk[(t + 1) & 1].  A single slot let a late helper wave read wave 0's iteration-t
+  // update at the top of iteration t, break out of the loop alone and skip the barrier the
+  // rest of the workgroup waits on (reached whenever `post` boxes are kept, i.e. every
+  // test-time call with post = 300).
+  int* s_nk = reinterpret_cast<int*>(smem);
   uint64_t* removed = reinterpret_cast<uint64_t*>(smem + 16);
   uint64_t* keptw = removed + nb;
   int32_t* keep_list = reinterpret_cast<int32_t*>(keptw + nb);
   const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int nv = n_valid[b];
+  const int nv = min(n_valid[b], P);
   const int64_t Pp = (int64_t)nb * 64;
   const uint64_t* mb = maskT + (int64_t)b * nb * Pp;
   for (int c = tid; c < nb; c += blockDim.x) {
     removed[c] = 0;
     keptw[c] = 0;
   }
-  if (tid == 0) s_nkeep = 0;
+  if (tid < 2) s_nk[tid] = 0;
   const int nbv = (nv + 63) / 64;
   // wave 0: words of block t (diag = maskT[t][j], wprev = maskT[t-1][j]); helpers: words of the
   // column blocks of the next iteration.  Every prefetch is loaded into the variable it is
@@ -96,8 +101,9 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
   for (int k = 0; k < NMS_PF; ++k) pf[k] = 0;
   if (wave == 0 && nbv > 0) diag = mb[lane];
   __syncthreads();
-  for (int t = 0; t < nbv; ++t) {
-    if (s_nkeep >= post) break;  // uniform: read after a barrier
+  int t = 0;
+  for (; t < nbv; ++t) {
+    if (s_nk[t & 1] >= post) break;  // uniform: written before the last barrier, not rewritten until the next
     if (wave == 0) {
       const int j = t * 64 + lane;
       const uint64_t kp = t > 0 ? keptw[t - 1] : 0ull;
@@ -119,7 +125,7 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
       const int tn = min(t + 1, nb - 1);
       diag = mb[(int64_t)tn * Pp + jn];
       wprev = mb[(int64_t)t * Pp + jn];
-      const int nk = s_nkeep;
+      const int nk = s_nk[t & 1];
       if (nk + __popcll(kept) > post) {  // keep only the lowest (post - nk) boxes of this block
         int need = post - nk;
         uint64_t trunc = 0, k = kept;
@@ -132,7 +138,7 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
       if ((kept >> lane) & 1ull) keep_list[nk + __popcll(kept & ((1ull << lane) - 1ull))] = j;
       if (lane == 0) {
         keptw[t] = kept;
-        s_nkeep = nk + __popcll(kept);
+        s_nk[(t + 1) & 1] = nk + __popcll(kept);
       }
     } else {
 #ifndef NMS_ABL_NOHELP  // ablation switch for tools/microbench/nms_bench.hip
@@ -177,7 +183,9 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
     }
     __syncthreads();
   }
-  const int nk = s_nkeep;
+  // the loop ends right after a barrier (break) or after the last one (t == nbv): s_nk[t & 1]
+  // is the final count either way
+  const int nk = min(s_nk[t & 1], post);
   if (tid == 0) n_keep_out[b] = nk;
   const float4* bx = reinterpret_cast<const float4*>(boxes) + (int64_t)b * P;
   for (int s = tid; s < post; s += blockDim.x) {

@@ -83,7 +83,7 @@ nms_mask_kernel(const float* __restrict__ boxes, const int32_t* __restrict__ n_v
   if (blockIdx.x * 4 + 3 < rb) return;  // whole group below the diagonal
   const int cb = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
-  const int nv = n_valid[b];
+  const int nv = min(n_valid[b], P);
   const int row0 = rb * 64;
   __shared__ float4 rbox[64];
   __shared__ float rarea[64];
@@ -164,13 +164,13 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // dynamic LDS: [nkeep i32 | pad][removed nb u64][keptw nb u64][cnt nb i32 (even)][keep_list post i32]
   unsigned char* rest = smem;
-  int& s_nkeep = *reinterpret_cast<int*>(rest);
+  int* s_nk = reinterpret_cast<int*>(rest);  // double-buffered kept count (see csrc/hip/nms.hip)
   uint64_t* removed = reinterpret_cast<uint64_t*>(rest + 16);
   uint64_t* keptw = removed + nb;
   int32_t* s_cnt = reinterpret_cast<int32_t*>(keptw + nb);
   int32_t* keep_list = s_cnt + ((nb + 1) & ~1);
   const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
-  const int nv = n_valid[b];
+  const int nv = min(n_valid[b], P);
   const NmsLayout L = nms_layout(const_cast<uint64_t*>(ws), B, nb);
   const uint64_t* near = L.near + (int64_t)b * nb * 128;
   const NmsEntry* ent = L.ent + (int64_t)b * nb * L.cap;
@@ -179,7 +179,7 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
     keptw[c] = 0;
     s_cnt[c] = L.cnt[(int64_t)b * nb + c];
   }
-  if (tid == 0) s_nkeep = 0;
+  if (tid < 2) s_nk[tid] = 0;
   const int nbv = (nv + 63) / 64;
   const int h = wave - 1;
   // Prefetch distance 2 through LDS-DMA rings (the asynchronous writes land in LDS, never in
@@ -213,8 +213,9 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
   } else if (nbv > 0) {
     issued_prev = h_issue(0);
   }
-  for (int t = 0; t < nbv; ++t) {
-    if (s_nkeep >= post) break;  // uniform: read after a barrier
+  int t = 0;
+  for (; t < nbv; ++t) {
+    if (s_nk[t & 1] >= post) break;  // uniform: not rewritten before the next barrier
     if (wave == 0) {
       nms_wait_vm<1>();  // row t's near words (issued two iterations ago) are in ring_w[t & 3]
       uint64_t diag, wprev;  // (asm reads, as for the helpers' ring; wprev is ANDed with kp = 0 at t = 0)
@@ -238,7 +239,7 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
       }
 #endif
       w0_issue(t + 2);  // into the slot of row t-2, read for the last time in iteration t-1
-      const int nk = s_nkeep;
+      const int nk = s_nk[t & 1];
       if (nk + __popcll(kept) > post) {  // keep only the lowest (post - nk) boxes of this block
         int need = post - nk;
         uint64_t trunc = 0, k = kept;
@@ -251,7 +252,7 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
       if ((kept >> lane) & 1ull) keep_list[nk + __popcll(kept & ((1ull << lane) - 1ull))] = j;
       if (lane == 0) {
         keptw[t] = kept;
-        s_nkeep = nk + __popcll(kept);
+        s_nk[(t + 1) & 1] = nk + __popcll(kept);
       }
     } else {
 #ifndef NMS_ABL_NOHELP  // ablation switch for tools/microbench/nms_bench.hip
@@ -302,7 +303,7 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
   }
   // drain the DMAs still in flight before the block can retire
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int nk = s_nkeep;
+  const int nk = min(s_nk[t & 1], post);
   if (tid == 0) n_keep_out[b] = nk;
   const float4* bx = reinterpret_cast<const float4*>(boxes) + (int64_t)b * P;
   for (int s = tid; s < post; s += blockDim.x) {

@@ -10,6 +10,7 @@
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 
+#include "host_ops.h"
 #include "kernels.h"
 
 // a rejected launch (e.g. an LDS request over budget) must raise here, not leave the outputs
@@ -691,25 +692,8 @@ Tensor nms_cpu(const Tensor& boxes_in, int64_t n_valid, double thresh, int64_t m
   TORCH_CHECK(boxes_in.dim() == 2 && boxes_in.size(1) == 4, "boxes must be (P, 4)");
   const Tensor boxes = boxes_in.to(at::kDouble).contiguous();
   const int64_t n = std::min<int64_t>(n_valid, boxes.size(0));
-  const double* b = boxes.data_ptr<double>();
-  std::vector<double> area(std::max<int64_t>(n, 0));
-  for (int64_t i = 0; i < n; ++i) area[i] = (b[4 * i + 2] - b[4 * i] + 1.0) * (b[4 * i + 3] - b[4 * i + 1] + 1.0);
-  std::vector<uint8_t> removed(std::max<int64_t>(n, 0), 0);
   std::vector<int64_t> keep;
-  for (int64_t i = 0; i < n; ++i) {
-    if (removed[i]) continue;
-    keep.push_back(i);
-    if (max_keep > 0 && (int64_t)keep.size() >= max_keep) break;
-    const double x1 = b[4 * i], y1 = b[4 * i + 1], x2 = b[4 * i + 2], y2 = b[4 * i + 3];
-    for (int64_t j = i + 1; j < n; ++j) {
-      if (removed[j]) continue;
-      const double w = std::min(x2, b[4 * j + 2]) - std::max(x1, b[4 * j]) + 1.0;
-      const double h = std::min(y2, b[4 * j + 3]) - std::max(y1, b[4 * j + 1]) + 1.0;
-      if (w <= 0.0 || h <= 0.0) continue;
-      const double inter = w * h;
-      if (inter / (area[i] + area[j] - inter) > thresh) removed[j] = 1;
-    }
-  }
+  mxr::host::nms_greedy(boxes.data_ptr<double>(), n, thresh, max_keep, keep);
   Tensor out = at::empty({(int64_t)keep.size()}, at::TensorOptions().dtype(at::kLong));
   std::copy(keep.begin(), keep.end(), out.data_ptr<int64_t>());
   return out;
@@ -733,40 +717,7 @@ std::vector<Tensor> roi_pool_fwd_cpu(const Tensor& feat_in, const Tensor& rois_i
   int32_t* a = arg.data_ptr<int32_t>();
   const float sc = (float)spatial_scale;
   at::parallel_for(0, R, 1, [&](int64_t r0, int64_t r1) {
-    for (int64_t r = r0; r < r1; ++r) {
-      const float* roi = ro + r * 5;
-      const int64_t b = (int64_t)roi[0];
-      if (b < 0 || b >= B) continue;
-      const int x1 = (int)std::round(roi[1] * sc), y1 = (int)std::round(roi[2] * sc);
-      const int x2 = (int)std::round(roi[3] * sc), y2 = (int)std::round(roi[4] * sc);
-      const int rw = std::max(x2 - x1 + 1, 1), rh = std::max(y2 - y1 + 1, 1);
-      const float bh = (float)rh / (float)PH, bw = (float)rw / (float)PW;
-      for (int64_t ph = 0; ph < PH; ++ph) {
-        const int hs = (int)std::min<int64_t>(std::max<int64_t>((int64_t)std::floor((float)ph * bh) + y1, 0), H);
-        const int he = (int)std::min<int64_t>(std::max<int64_t>((int64_t)std::ceil((float)(ph + 1) * bh) + y1, 0), H);
-        for (int64_t pw = 0; pw < PW; ++pw) {
-          const int ws = (int)std::min<int64_t>(std::max<int64_t>((int64_t)std::floor((float)pw * bw) + x1, 0), W);
-          const int we = (int)std::min<int64_t>(std::max<int64_t>((int64_t)std::ceil((float)(pw + 1) * bw) + x1, 0), W);
-          if (he <= hs || we <= ws) continue;
-          for (int64_t c = 0; c < C; ++c) {
-            const float* fc = f + ((b * C + c) * H) * W;
-            float best = fc[hs * W + ws];
-            int bi = hs * (int)W + ws;
-            for (int h = hs; h < he; ++h)
-              for (int w = ws; w < we; ++w) {
-                const float v = fc[h * W + w];
-                if (v > best) {
-                  best = v;
-                  bi = h * (int)W + w;
-                }
-              }
-            const int64_t oi = ((r * C + c) * PH + ph) * PW + pw;
-            o[oi] = best;
-            a[oi] = bi;
-          }
-        }
-      }
-    }
+    mxr::host::roi_pool_range(f, B, C, H, W, ro, r0, r1, PH, PW, sc, o, a);
   });
   return {out, arg};
 }

@@ -22,6 +22,7 @@ import numpy as np
 import torch
 
 from ..parallel import dist as pdist
+from ..parallel import watchdog
 from .callback import BatchEndParam
 from .lr_scheduler import FactorScheduler
 from .trainer import GraphedStep, Trainer
@@ -285,6 +286,7 @@ class MutableModule(object):
             ([epoch_end_callback] if epoch_end_callback else [])
         steps = 0
         fault_step, fault_kind = parse_fault(os.environ.get('MXR_FAULT_INJECT'))
+        hb = watchdog.from_env()
         for epoch in range(begin_epoch, num_epoch):
             tic = time.time()
             if eval_metric is not None:
@@ -298,6 +300,8 @@ class MutableModule(object):
                 self.step(batch)
                 if fault:
                     self.trainer.disarm_fault()
+                if hb is not None:
+                    hb.beat(steps)
                 if (steps + 1) % check_every == 0:
                     self.trainer.check_finite(steps)
                 if eval_metric is not None:
@@ -323,6 +327,8 @@ class MutableModule(object):
             if max_steps is not None and steps >= max_steps:
                 break
             train_data.reset()
+        if hb is not None:
+            hb.stop()
         if hasattr(train_data, 'close'):
             train_data.close()
 

@@ -722,12 +722,102 @@ std::vector<Tensor> roi_pool_fwd_cpu(const Tensor& feat_in, const Tensor& rois_i
   return {out, arg};
 }
 
+// ---- CPU twin of the RoI max-pool backward: scatter gout through the forward's argmax,
+// parallel over channels (no atomics, per-channel sums in RoI order).  Returns fp32 (B, C, H, W).
+Tensor roi_pool_bwd_cpu(const Tensor& gout_in, const Tensor& arg_in, const Tensor& rois_in, int64_t B, int64_t H,
+                        int64_t W) {
+  TORCH_CHECK(!gout_in.is_cuda() && gout_in.dim() == 4, "gout must be a CPU (R, C, PH, PW) tensor");
+  const Tensor gout = gout_in.to(at::kFloat).contiguous();
+  const Tensor arg = arg_in.to(at::kInt).contiguous();
+  const Tensor rois = rois_in.to(at::kFloat).contiguous();
+  TORCH_CHECK(arg.sizes() == gout.sizes(), "arg must match gout");
+  const int64_t R = gout.size(0), C = gout.size(1), PHW = gout.size(2) * gout.size(3);
+  TORCH_CHECK(rois.dim() == 2 && rois.size(0) == R && rois.size(1) == 5, "rois must be (R, 5)");
+  Tensor gin = at::zeros({B, C, H, W}, gout.options());
+  const float* g = gout.data_ptr<float>();
+  const int32_t* a = arg.data_ptr<int32_t>();
+  const float* ro = rois.data_ptr<float>();
+  float* o = gin.data_ptr<float>();
+  at::parallel_for(0, C, 1, [&](int64_t c0, int64_t c1) {
+    mxr::host::roi_pool_bwd_channels(g, a, ro, R, B, C, H, W, PHW, c0, c1, o);
+  });
+  return gin;
+}
+
+// ---- CPU twin of the fused proposal decode (proposal.hip): per image, softmax fg + anchors +
+// decode + clip + min-size; rows (h, w, a).  cls (B, 2A, H, W), dlt (B, 4A, H, W), im_info
+// (B, 3), base (A, 4).  Returns boxes (B, N, 4) and keys (B, N) (-inf = filtered).
+std::vector<Tensor> proposal_decode_cpu(const Tensor& cls_in, const Tensor& dlt_in, const Tensor& im_info_in,
+                                        const Tensor& base_in, double stride, double min_size, bool crop,
+                                        bool is_prob) {
+  TORCH_CHECK(!cls_in.is_cuda() && cls_in.dim() == 4 && dlt_in.dim() == 4, "cls / dlt must be CPU NCHW tensors");
+  const Tensor cls = cls_in.to(at::kFloat).contiguous();
+  const Tensor dlt = dlt_in.to(at::kFloat).contiguous();
+  const Tensor im_info = im_info_in.to(at::kFloat).contiguous();
+  const Tensor base = base_in.to(at::kFloat).contiguous();
+  const int64_t B = cls.size(0), A = cls.size(1) / 2, H = cls.size(2), W = cls.size(3), N = H * W * A;
+  TORCH_CHECK(cls.size(1) == 2 * A && dlt.size(0) == B && dlt.size(1) == 4 * A && dlt.size(2) == H &&
+                  dlt.size(3) == W, "dlt must be (B, 4A, H, W) with cls (B, 2A, H, W)");
+  TORCH_CHECK(im_info.dim() == 2 && im_info.size(0) == B && im_info.size(1) >= 3, "im_info must be (B, 3)");
+  TORCH_CHECK(base.numel() == 4 * A, "base must hold A anchors");
+  Tensor boxes = at::empty({B, N, 4}, cls.options());
+  Tensor keys = at::empty({B, N}, cls.options());
+  const float* ii = im_info.data_ptr<float>();
+  const int64_t ist = im_info.size(1);
+  at::parallel_for(0, B, 1, [&](int64_t b0, int64_t b1) {
+    for (int64_t b = b0; b < b1; ++b)
+      mxr::host::proposal_decode_image(cls.data_ptr<float>() + b * 2 * A * H * W,
+                                       dlt.data_ptr<float>() + b * 4 * A * H * W, A, H, W, ii[b * ist],
+                                       ii[b * ist + 1], ii[b * ist + 2], base.data_ptr<float>(), (float)stride,
+                                       (float)min_size, crop, is_prob, boxes.data_ptr<float>() + b * N * 4,
+                                       keys.data_ptr<float>() + b * N);
+  });
+  return {boxes, keys};
+}
+
+// ---- CPU twin of the RPN anchor-target assignment (assign.hip, before subsampling): labels
+// (B, N) int32 in {-1, 0, 1} and targets (B, N, 4), rows (h, w, a).  gt (B, G, >=4) padded
+// past n_gt[b]; im_info (B, >=2).  Pass 1 per image, pass 2 parallel over anchor rows.
+std::vector<Tensor> anchor_assign_cpu(const Tensor& base_in, int64_t H, int64_t W, double stride,
+                                      const Tensor& im_info_in, int64_t border, const Tensor& gt_in,
+                                      const Tensor& n_gt_in, double neg, double pos, bool clobber) {
+  TORCH_CHECK(!gt_in.is_cuda() && gt_in.dim() == 3 && gt_in.size(2) >= 4, "gt must be a CPU (B, G, >=4) tensor");
+  const Tensor base = base_in.to(at::kFloat).contiguous();
+  const Tensor im_info = im_info_in.to(at::kFloat).contiguous();
+  const Tensor gt = gt_in.to(at::kFloat).contiguous();
+  const Tensor n_gt = n_gt_in.to(at::kLong).contiguous();
+  const int64_t A = base.numel() / 4, B = gt.size(0), G = gt.size(1), gs = gt.size(2), N = H * W * A;
+  TORCH_CHECK(base.numel() == 4 * A && im_info.size(0) == B && n_gt.numel() == B, "base / im_info / n_gt shapes");
+  Tensor labels = at::empty({B, N}, gt.options().dtype(at::kInt));
+  Tensor targets = at::empty({B, N, 4}, gt.options());
+  const float* bs = base.data_ptr<float>();
+  const float* ii = im_info.data_ptr<float>();
+  const int64_t ist = im_info.size(1);
+  std::vector<float> gmax(std::max<int64_t>(G, 1));
+  for (int64_t b = 0; b < B; ++b) {
+    const int64_t ng = std::min<int64_t>(std::max<int64_t>(n_gt.data_ptr<int64_t>()[b], 0), G);
+    const float im_h = ii[b * ist], im_w = ii[b * ist + 1];
+    const float* g = gt.data_ptr<float>() + b * G * gs;
+    mxr::host::anchor_gt_max(bs, A, H, W, (float)stride, im_h, im_w, (int)border, g, gs, ng, gmax.data());
+    int32_t* lb = labels.data_ptr<int32_t>() + b * N;
+    float* tg = targets.data_ptr<float>() + b * N * 4;
+    at::parallel_for(0, N, 2048, [&](int64_t n0, int64_t n1) {
+      mxr::host::anchor_assign_range(bs, A, W, (float)stride, im_h, im_w, (int)border, g, gs, ng, gmax.data(),
+                                     (float)neg, (float)pos, clobber, n0, n1, lb, tg);
+    });
+  }
+  return {labels, targets};
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mx_rcnn_amd gfx950 kernels";
   m.def("proposal_decode", &proposal_decode);
   m.def("nms_proposals", &nms_proposals);
   m.def("nms_cpu", &nms_cpu);
   m.def("roi_pool_fwd_cpu", &roi_pool_fwd_cpu);
+  m.def("roi_pool_bwd_cpu", &roi_pool_bwd_cpu);
+  m.def("proposal_decode_cpu", &proposal_decode_cpu);
+  m.def("anchor_assign_cpu", &anchor_assign_cpu);
   m.def("iou_max", &iou_max);
   m.def("anchor_sample", &anchor_sample);
   m.def("proposal_sample", &proposal_sample);

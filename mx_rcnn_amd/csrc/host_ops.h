@@ -1,7 +1,8 @@
-// Host (CPU) twins of the proposal NMS and the RoI max-pool forward, written against raw
-// pointers so the same code is linked into the extension (bindings.cpp wraps it in ATen
-// tensors and at::parallel_for) and into the sanitizer driver tests/native/host_ops_test.cpp
-// (built with -fsanitize=address,undefined and -fsanitize=thread, no torch).
+// Host (CPU) twins of the RPN anchor-target assignment, the proposal decode, the proposal NMS and the RoI max-pool forward /
+// backward, written against raw pointers so the same code is linked into the extension
+// (bindings.cpp wraps it in ATen tensors and at::parallel_for) and into the sanitizer driver
+// tests/native/host_ops_test.cpp (built with -fsanitize=address,undefined and
+// -fsanitize=thread, no torch).
 //
 // Semantics follow the GPU kernels, which follow the reference:
 //   * NMS: greedy over score-sorted boxes, +1-pixel areas, suppress j when IoU(i, j) > thresh
@@ -81,6 +82,155 @@ inline void roi_pool_range(const float* f, int64_t B, int64_t C, int64_t H, int6
         }
       }
     }
+  }
+}
+
+// RoI max-pool backward for channels [c0, c1): gin (B, C, H, W) fp32, pre-zeroed; gout / arg
+// (R, C, PH*PW).  Each channel's gradients are summed in ascending RoI order, so the result is
+// bitwise reproducible and channel ranges can run concurrently without atomics.
+inline void roi_pool_bwd_channels(const float* gout, const int32_t* arg, const float* ro, int64_t R, int64_t B,
+                                  int64_t C, int64_t H, int64_t W, int64_t PHW, int64_t c0, int64_t c1, float* gin) {
+  for (int64_t r = 0; r < R; ++r) {
+    const float bf = ro[r * 5];
+    if (!(bf > -1.f) || bf >= (float)B) continue;
+    const int64_t b = (int64_t)bf;
+    for (int64_t c = c0; c < c1; ++c) {
+      const float* g = gout + (r * C + c) * PHW;
+      const int32_t* a = arg + (r * C + c) * PHW;
+      float* dst = gin + (b * C + c) * H * W;
+      for (int64_t k = 0; k < PHW; ++k)
+        if (a[k] >= 0 && a[k] < H * W) dst[a[k]] += g[k];
+    }
+  }
+}
+
+// One image of the proposal decode (rcnn/rpn/proposal.py:39-149 steps 1-4):
+// fg score (softmax over the (bg, fg) logit pair, or the given probability), anchor at
+// (x * stride, y * stride) + base[a], +1-convention delta decode, clip to the image, min-size
+// filter (filtered / NaN -> key -inf).  cls (2A, H, W), dlt (4A, H, W) NCHW fp32; rows are
+// (h, w, a) over the Hc x Wc grid (crop: int(im / stride) as the TRAIN deltas), the rest of
+// the H*W*A outputs keep key -inf and box 0.
+inline void proposal_decode_image(const float* cls, const float* dlt, int64_t A, int64_t H, int64_t W, float im_h,
+                                  float im_w, float im_scale, const float* base, float stride, float min_size,
+                                  bool crop, bool is_prob, float* boxes, float* keys) {
+  const int64_t N = H * W * A, HW = H * W;
+  for (int64_t i = 0; i < N; ++i) {
+    keys[i] = -INFINITY;
+    boxes[4 * i] = boxes[4 * i + 1] = boxes[4 * i + 2] = boxes[4 * i + 3] = 0.f;
+  }
+  int64_t Hc = H, Wc = W;
+  if (crop) {
+    Hc = std::min<int64_t>(H, (int64_t)(im_h / stride));
+    Wc = std::min<int64_t>(W, (int64_t)(im_w / stride));
+  }
+  const float wmax = im_w - 1.f, hmax = im_h - 1.f, ms = min_size * im_scale;
+  for (int64_t y = 0; y < Hc; ++y)
+    for (int64_t x = 0; x < Wc; ++x)
+      for (int64_t a = 0; a < A; ++a) {
+        const int64_t pix = y * W + x, row = (y * Wc + x) * A + a;
+        float fg;
+        if (is_prob) {
+          fg = cls[(A + a) * HW + pix];
+        } else {
+          const float l0 = cls[a * HW + pix], l1 = cls[(A + a) * HW + pix];
+          const float m = std::max(l0, l1), e0 = std::exp(l0 - m), e1 = std::exp(l1 - m);
+          fg = e1 / (e0 + e1);
+        }
+        const float ax1 = (float)x * stride + base[4 * a], ay1 = (float)y * stride + base[4 * a + 1];
+        const float ax2 = (float)x * stride + base[4 * a + 2], ay2 = (float)y * stride + base[4 * a + 3];
+        const float w = ax2 - ax1 + 1.f, h = ay2 - ay1 + 1.f;
+        const float cx = ax1 + 0.5f * (w - 1.f), cy = ay1 + 0.5f * (h - 1.f);
+        const float* d = dlt + (4 * a) * HW + pix;
+        const float pcx = d[0] * w + cx, pcy = d[HW] * h + cy;
+        const float pw = std::exp(d[2 * HW]) * w, ph = std::exp(d[3 * HW]) * h;
+        float* o = boxes + 4 * row;
+        o[0] = std::max(std::min(pcx - 0.5f * (pw - 1.f), wmax), 0.f);
+        o[1] = std::max(std::min(pcy - 0.5f * (ph - 1.f), hmax), 0.f);
+        o[2] = std::max(std::min(pcx + 0.5f * (pw - 1.f), wmax), 0.f);
+        o[3] = std::max(std::min(pcy + 0.5f * (ph - 1.f), hmax), 0.f);
+        const bool ok = (o[2] - o[0] + 1.f >= ms) && (o[3] - o[1] + 1.f >= ms) && !std::isnan(fg);
+        keys[row] = ok ? fg : -INFINITY;
+      }
+}
+
+// RPN anchor-target assignment (rcnn/minibatch.py assign_anchor, before the
+// fg/bg subsampling), one image.  Anchors are (h, w, a) rows at (x * stride, y * stride) +
+// base[a]; an anchor is inside when it lies within the image grown by `border`.  IoU uses
+// +1-pixel areas.  Pass 1 (anchor_gt_max) takes each gt's best IoU over the inside anchors;
+// pass 2 (anchor_assign_range, anchor rows [n0, n1), runnable concurrently) labels each
+// inside anchor: bg if its best IoU < neg, fg if it ties a gt's best or reaches pos (bg rule
+// last when clobber), and encodes its best gt.  Outside anchors: label -1, target 0.
+inline bool anchor_at(const float* base, int64_t A, int64_t W, float stride, int64_t n, float im_h, float im_w,
+                      int border, float* an) {
+  const int64_t a = n % A, x = (n / A) % W, y = n / (A * W);
+  an[0] = (float)x * stride + base[4 * a];
+  an[1] = (float)y * stride + base[4 * a + 1];
+  an[2] = (float)x * stride + base[4 * a + 2];
+  an[3] = (float)y * stride + base[4 * a + 3];
+  return an[0] >= (float)-border && an[1] >= (float)-border && an[2] < im_w + (float)border &&
+         an[3] < im_h + (float)border;
+}
+
+inline float iou1(const float* a, const float* g) {
+  const float iw = std::min(a[2], g[2]) - std::max(a[0], g[0]) + 1.f;
+  const float ih = std::min(a[3], g[3]) - std::max(a[1], g[1]) + 1.f;
+  if (!(iw > 0.f && ih > 0.f)) return 0.f;
+  const float inter = iw * ih;
+  const float aa = (a[2] - a[0] + 1.f) * (a[3] - a[1] + 1.f), ga = (g[2] - g[0] + 1.f) * (g[3] - g[1] + 1.f);
+  return inter / (aa + ga - inter);
+}
+
+// gt: ng rows of stride gt_stride (x1, y1, x2, y2, ...); gmax: ng floats (0 when no inside anchor)
+inline void anchor_gt_max(const float* base, int64_t A, int64_t H, int64_t W, float stride, float im_h, float im_w,
+                          int border, const float* gt, int64_t gt_stride, int64_t ng, float* gmax) {
+  for (int64_t g = 0; g < ng; ++g) gmax[g] = -INFINITY;
+  float an[4];
+  for (int64_t n = 0; n < H * W * A; ++n) {
+    if (!anchor_at(base, A, W, stride, n, im_h, im_w, border, an)) continue;
+    for (int64_t g = 0; g < ng; ++g) gmax[g] = std::max(gmax[g], iou1(an, gt + g * gt_stride));
+  }
+}
+
+inline void anchor_assign_range(const float* base, int64_t A, int64_t W, float stride, float im_h, float im_w,
+                                int border, const float* gt, int64_t gt_stride, int64_t ng, const float* gmax,
+                                float neg, float pos, bool clobber, int64_t n0, int64_t n1, int32_t* labels,
+                                float* targets) {
+  float an[4];
+  for (int64_t n = n0; n < n1; ++n) {
+    float* t = targets + 4 * n;
+    t[0] = t[1] = t[2] = t[3] = 0.f;
+    labels[n] = -1;
+    if (!anchor_at(base, A, W, stride, n, im_h, im_w, border, an)) continue;
+    if (ng == 0) {
+      labels[n] = 0;
+      continue;
+    }
+    float mo = -INFINITY;
+    int64_t am = 0;
+    bool best = false;
+    for (int64_t g = 0; g < ng; ++g) {
+      const float v = iou1(an, gt + g * gt_stride);
+      if (v > mo) {
+        mo = v;
+        am = g;
+      }
+      best = best || v == gmax[g];
+    }
+    int32_t lab = -1;
+    if (!clobber && mo < neg) lab = 0;
+    if (best) lab = 1;
+    if (mo >= pos) lab = 1;
+    if (clobber && mo < neg) lab = 0;
+    labels[n] = lab;
+    const float* q = gt + am * gt_stride;
+    const float ew = an[2] - an[0] + 1.f, eh = an[3] - an[1] + 1.f;
+    const float ecx = an[0] + 0.5f * (ew - 1.f), ecy = an[1] + 0.5f * (eh - 1.f);
+    const float gw = q[2] - q[0] + 1.f, gh = q[3] - q[1] + 1.f;
+    const float gcx = q[0] + 0.5f * (gw - 1.f), gcy = q[1] + 0.5f * (gh - 1.f);
+    t[0] = (gcx - ecx) / (ew + 1e-14f);
+    t[1] = (gcy - ecy) / (eh + 1e-14f);
+    t[2] = std::log(gw / ew);
+    t[3] = std::log(gh / eh);
   }
 }
 

@@ -11,7 +11,7 @@ import numpy as np
 import torch
 
 from ..config import config as _global_cfg
-from ._ext import need_ext, const_tensor
+from ._ext import ext_available, need_ext, const_tensor
 from .anchors import base_anchors
 from .boxes import bbox_transform, box_iou
 from .sampling import keep_random
@@ -85,6 +85,11 @@ def anchor_target(feat_shape, gt_boxes, n_gt, im_info, feat_stride=16, scales=(8
             # meta (B, 4) = [all_fg, all_bg, n_fg, n_bg]: the RPN loss's 'valid' count without a reduction
             return {'label': lab, 'bbox_target': bt, 'bbox_inside_weight': inside, 'bbox_outside_weight': outside,
                     'sample_meta': meta}
+        elif ext_available():  # C++ twin (host_ops.h); _assign_ref is its test oracle
+            label, targets = need_ext().anchor_assign_cpu(
+                base, H, W, float(feat_stride), im_info.float(), int(allowed_border), gt_boxes.float(), n_gt,
+                float(cfg.TRAIN.RPN_NEGATIVE_OVERLAP), float(cfg.TRAIN.RPN_POSITIVE_OVERLAP),
+                bool(cfg.TRAIN.RPN_CLOBBER_POSITIVES))
         else:
             label, targets = _assign_ref(H, W, base, feat_stride, im_info, allowed_border, gt_boxes, n_gt,
                                          cfg.TRAIN.RPN_NEGATIVE_OVERLAP, cfg.TRAIN.RPN_POSITIVE_OVERLAP,

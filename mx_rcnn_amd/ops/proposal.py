@@ -14,7 +14,7 @@ Deviation (documented): in TRAIN the scores are cropped to the sam
 """
 import torch
 
-from ._ext import need_ext
+from ._ext import ext_available, need_ext
 from .anchors import base_anchors
 from .boxes import bbox_pred, clip_boxes
 from .nms import _greedy_ref
@@ -72,6 +72,9 @@ def proposal(cls, bbox_deltas, im_info, feat_stride=16, scales=(8, 16, 32), rati
             C = need_ext()
             boxes, keys = C.proposal_decode(cls, bbox_deltas, im_info, base, float(feat_stride), float(min_size),
                                             bool(is_train), bool(is_prob))
+        elif ext_available():  # C++ twin (host_ops.h); the tensor version below is its test oracle
+            boxes, keys = need_ext().proposal_decode_cpu(cls, bbox_deltas, im_info, base, float(feat_stride),
+                                                         float(min_size), bool(is_train), bool(is_prob))
         else:
             boxes, keys = _decode_ref(cls, bbox_deltas, im_info, base, feat_stride, min_size, is_train, is_prob)
         N = keys.shape[1]

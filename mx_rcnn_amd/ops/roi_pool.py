@@ -7,7 +7,7 @@ import math
 import numpy as np
 import torch
 
-from ._ext import need_ext
+from ._ext import ext_available, need_ext
 
 
 def _bins(roi, PH, PW, H, W, scale):
@@ -66,7 +66,6 @@ class _RoIPool(torch.autograd.Function):
             ext = need_ext()
             out, arg = ext.roi_pool_fwd(feat.contiguous(memory_format=torch.channels_last), rois, PH, PW, float(scale))
         else:
-            from ._ext import ext_available
             if ext_available():  # C++ twin (the loop reference below is the test oracle)
                 out, arg = need_ext().roi_pool_fwd_cpu(feat, rois, PH, PW, float(scale))
                 out = out.to(feat.dtype)
@@ -83,6 +82,8 @@ class _RoIPool(torch.autograd.Function):
         if gout.is_cuda:
             ext = need_ext()
             gin = ext.roi_pool_bwd(gout, arg, rois, B, H, W)
+        elif ext_available():  # C++ twin: channel-parallel scatter, deterministic sum order
+            gin = need_ext().roi_pool_bwd_cpu(gout, arg, rois, B, H, W).to(gout.dtype)
         else:
             gin = torch.zeros(B, C * H * W, dtype=torch.float32)
             R = gout.shape[0]

@@ -7,6 +7,12 @@
 //     degenerate boxes, bitwise repeatability;
 //   * RoI pool against a per-bin brute-force oracle, including RoIs outside the map, bad
 //     batch indices (negative, >= B, NaN) and 1-pixel RoIs;
+//   * RoI pool backward against a float64 scatter (invalid batch indices, out-of-range
+//     argmax), channel ranges on threads bitwise equal to one pass;
+//   * proposal decode invariants (scores in [0, 1], boxes clipped, min size, crop rows -inf,
+//     NaN score and exp overflow inputs);
+//   * anchor assignment: anchor-row ranges on threads bitwise equal to one pass, label
+//     invariants with 0 / some / all gt (fg present without clobber, none without gt);
 //   * RoI pool ranges run concurrently on std::threads equal the serial result (the
 //     at::parallel_for contract; -fsanitize=thread checks the disjoint-write claim).
 #include <cmath>
@@ -191,11 +197,129 @@ void test_roi_pool() {
   CHECK(std::memcmp(a.data(), a2.data(), a.size() * sizeof(int32_t)) == 0, "threaded roi pool argmax differs");
 }
 
+void test_roi_pool_bwd() {
+  Rng g(13);
+  const int64_t B = 2, C = 6, H = 17, W = 21, PHW = 49, R = 40;
+  std::vector<float> gout(R * C * PHW), rois(R * 5, 0.f);
+  std::vector<int32_t> arg(R * C * PHW);
+  for (auto& v : gout) v = (float)(g.uni() - 0.5);
+  for (auto& v : arg) v = (int32_t)(g.uni() * (H * W + 8)) - 4;  // includes -1..-4 and > H*W: skipped
+  for (int64_t r = 0; r < R; ++r) rois[r * 5] = (float)(r % (B + 1)) - (r % 7 == 0 ? 3.f : 0.f);  // some invalid
+  std::vector<double> ref(B * C * H * W, 0.0);
+  for (int64_t r = 0; r < R; ++r) {
+    const float bf = rois[r * 5];
+    if (!(bf > -1.f) || bf >= (float)B) continue;
+    const int64_t b = (int64_t)bf;
+    for (int64_t c = 0; c < C; ++c)
+      for (int64_t k = 0; k < PHW; ++k) {
+        const int32_t a = arg[(r * C + c) * PHW + k];
+        if (a >= 0 && a < H * W) ref[(b * C + c) * H * W + a] += gout[(r * C + c) * PHW + k];
+      }
+  }
+  std::vector<float> gin(B * C * H * W, 0.f), gin2(B * C * H * W, 0.f);
+  mxr::host::roi_pool_bwd_channels(gout.data(), arg.data(), rois.data(), R, B, C, H, W, PHW, 0, C, gin.data());
+  for (size_t i = 0; i < gin.size(); ++i) CHECK(std::fabs(gin[i] - ref[i]) < 1e-4, "bwd %zu: %f vs %f", i, gin[i], ref[i]);
+  std::vector<std::thread> th;
+  for (int t = 0; t < 3; ++t)
+    th.emplace_back([&, t] {
+      mxr::host::roi_pool_bwd_channels(gout.data(), arg.data(), rois.data(), R, B, C, H, W, PHW, C * t / 3,
+                                       C * (t + 1) / 3, gin2.data());
+    });
+  for (auto& x : th) x.join();
+  CHECK(std::memcmp(gin.data(), gin2.data(), gin.size() * sizeof(float)) == 0, "threaded bwd differs");
+}
+
+void test_proposal_decode() {
+  Rng g(17);
+  const int64_t A = 9, H = 19, W = 25, N = H * W * A;
+  std::vector<float> cls(2 * A * H * W), dlt(4 * A * H * W), base(4 * A);
+  for (auto& v : cls) v = (float)(g.uni() * 6 - 3);
+  for (auto& v : dlt) v = (float)(g.uni() - 0.5);
+  dlt[7] = std::numeric_limits<float>::infinity();  // exp overflow path
+  cls[5] = std::numeric_limits<float>::quiet_NaN();  // NaN score -> filtered
+  for (int64_t a = 0; a < A; ++a) {
+    const float s = 8.f * (float)(1 + a % 3) * 4.f;
+    base[4 * a] = -s;
+    base[4 * a + 1] = -s / (1 + a / 3);
+    base[4 * a + 2] = s + 15.f;
+    base[4 * a + 3] = s / (1 + a / 3) + 15.f;
+  }
+  const float im_h = 250.f, im_w = 330.f;  // crop grid 15 x 20 < 19 x 25
+  for (int crop = 0; crop < 2; ++crop) {
+    std::vector<float> boxes(4 * N), keys(N);
+    mxr::host::proposal_decode_image(cls.data(), dlt.data(), A, H, W, im_h, im_w, 1.f, base.data(), 16.f, 16.f,
+                                     crop != 0, false, boxes.data(), keys.data());
+    const int64_t Hc = crop ? 15 : H, Wc = crop ? 20 : W;
+    int64_t n_fin = 0;
+    for (int64_t i = 0; i < N; ++i) {
+      if (i >= Hc * Wc * A) CHECK(std::isinf(keys[i]) && keys[i] < 0, "row %ld beyond the grid must be -inf", (long)i);
+      if (!std::isfinite(keys[i])) continue;
+      ++n_fin;
+      CHECK(keys[i] >= 0.f && keys[i] <= 1.f, "score %f out of [0, 1]", keys[i]);
+      const float* b = &boxes[4 * i];
+      CHECK(b[0] >= 0 && b[2] <= im_w - 1 && b[1] >= 0 && b[3] <= im_h - 1, "box %ld outside the image", (long)i);
+      CHECK(b[2] - b[0] + 1 >= 16.f && b[3] - b[1] + 1 >= 16.f, "box %ld below min size", (long)i);
+    }
+    CHECK(n_fin > N / 10, "too few boxes survive (%ld)", (long)n_fin);
+  }
+}
+
+void test_anchor_assign() {
+  Rng g(19);
+  const int64_t A = 9, H = 21, W = 27, N = H * W * A, G = 5, gs = 5;
+  std::vector<float> base(4 * A), gt(G * gs, 0.f);
+  for (int64_t a = 0; a < A; ++a) {
+    const float s = 16.f * (float)(1 + a % 3), r = 1.f + (float)(a / 3) * 0.5f;
+    base[4 * a] = -s * r;
+    base[4 * a + 1] = -s / r;
+    base[4 * a + 2] = s * r + 15.f;
+    base[4 * a + 3] = s / r + 15.f;
+  }
+  for (int64_t i = 0; i < G; ++i) {
+    const float x = (float)(g.uni() * 350), y = (float)(g.uni() * 260), w = (float)(g.uni() * 120 + 8);
+    gt[i * gs] = x;
+    gt[i * gs + 1] = y;
+    gt[i * gs + 2] = x + w;
+    gt[i * gs + 3] = y + w * 0.7f;
+  }
+  const float im_h = 330.f, im_w = 430.f;
+  for (int clobber = 0; clobber < 2; ++clobber)
+    for (int64_t ng : {(int64_t)0, (int64_t)2, G}) {
+      std::vector<float> gmax(G), t1(4 * N), t2(4 * N);
+      std::vector<int32_t> l1(N), l2(N);
+      mxr::host::anchor_gt_max(base.data(), A, H, W, 16.f, im_h, im_w, 0, gt.data(), gs, ng, gmax.data());
+      mxr::host::anchor_assign_range(base.data(), A, W, 16.f, im_h, im_w, 0, gt.data(), gs, ng, gmax.data(), 0.3f,
+                                     0.7f, clobber != 0, 0, N, l1.data(), t1.data());
+      std::vector<std::thread> th;
+      for (int t = 0; t < 4; ++t)
+        th.emplace_back([&, t] {
+          mxr::host::anchor_assign_range(base.data(), A, W, 16.f, im_h, im_w, 0, gt.data(), gs, ng, gmax.data(),
+                                         0.3f, 0.7f, clobber != 0, N * t / 4, N * (t + 1) / 4, l2.data(), t2.data());
+        });
+      for (auto& x : th) x.join();
+      CHECK(l1 == l2 && std::memcmp(t1.data(), t2.data(), t1.size() * sizeof(float)) == 0,
+            "threaded anchor assignment differs (ng %ld)", (long)ng);
+      int64_t nfg = 0, nbg = 0;
+      for (int64_t n = 0; n < N; ++n) {
+        CHECK(l1[n] >= -1 && l1[n] <= 1, "label %d", l1[n]);
+        nfg += l1[n] == 1;
+        nbg += l1[n] == 0;
+        if (l1[n] != 1) CHECK(t1[4 * n] == 0.f || ng > 0, "target without gt");
+      }
+      // without clobber every gt's best anchor is fg; with clobber the bg rule may override it
+      CHECK(ng == 0 ? nfg == 0 && nbg > 0 : (clobber || nfg >= 1), "fg %ld bg %ld with %ld gt", (long)nfg, (long)nbg,
+            (long)ng);
+    }
+}
+
 }  // namespace
 
 int main() {
   test_nms();
   test_roi_pool();
+  test_roi_pool_bwd();
+  test_proposal_decode();
+  test_anchor_assign();
   if (g_fail) {
     std::fprintf(stderr, "%d check(s) failed\n", g_fail);
     return 1;

@@ -368,3 +368,50 @@ def test_nms_cpu_twin_matches_tensor_loop():
         ref = _greedy_loop(b, n, th, cap)
         got = need_ext().nms_cpu(b, n, th, -1 if cap is None else cap).tolist()
         assert got == ref, (n, th, cap)
+
+
+@pytest.mark.parametrize('crop,is_prob', [(True, False), (False, False), (True, True)])
+def test_proposal_decode_cpu_twin_matches_tensor_ref(crop, is_prob):
+    """C++ twin (host_ops.h proposal_decode_image) vs the tensor decode: same filter mask,
+    boxes within an ulp of the box magnitude, scores within an ulp."""
+    from mx_rcnn_amd.ops import ext_available, need_ext
+    from mx_rcnn_amd.ops.anchors import base_anchors
+    from mx_rcnn_amd.ops.proposal import _decode_ref
+    if not ext_available():
+        pytest.skip('extension not built')
+    cls, dlt = _rpn_inputs(8, 9, 30, 40, B=2)
+    if is_prob:
+        cls = torch.rand(cls.shape, generator=torch.Generator().manual_seed(2))
+    im = torch.tensor([[470., 630., 1.0], [400., 600., 1.5]])
+    base = base_anchors(16, (8, 16, 32), (0.5, 1, 2), torch.device('cpu'))
+    b1, k1 = _decode_ref(cls, dlt, im, base, 16, 16, crop, is_prob)
+    b2, k2 = need_ext().proposal_decode_cpu(cls, dlt, im, base, 16., 16., crop, is_prob)
+    fin = torch.isfinite(k1)
+    assert torch.equal(fin, torch.isfinite(k2))
+    assert torch.allclose(b1, b2, rtol=0, atol=2e-4)
+    assert torch.allclose(k1[fin], k2[fin], rtol=0, atol=1e-6)
+
+
+@pytest.mark.parametrize('clobber,border', [(False, 0), (True, 0), (False, 10)])
+def test_anchor_assign_cpu_twin_matches_tensor_ref(clobber, border):
+    """C++ twin (host_ops.h anchor_gt_max / anchor_assign_range) vs the tensor assignment:
+    identical labels (incl. gt-best ties and an image without gt) and targets."""
+    from mx_rcnn_amd.ops import ext_available, need_ext
+    from mx_rcnn_amd.ops.anchor_target import _assign_ref
+    from mx_rcnn_amd.ops.anchors import base_anchors
+    if not ext_available():
+        pytest.skip('extension not built')
+    g = torch.Generator().manual_seed(3)
+    base = base_anchors(16, (8, 16, 32), (0.5, 1, 2), torch.device('cpu'))
+    H, W = 38, 50
+    gt = torch.zeros(3, 6, 5)
+    for b in range(3):
+        xy = torch.rand(6, 2, generator=g) * torch.tensor([700., 500.])
+        gt[b, :, :2] = xy
+        gt[b, :, 2:4] = xy + torch.rand(6, 2, generator=g) * 200 + 10
+    n_gt = torch.tensor([6, 2, 0], dtype=torch.int32)
+    im = torch.tensor([[600., 800., 1.], [580., 790., 1.], [600., 800., 1.]])
+    l1, t1 = _assign_ref(H, W, base, 16, im, border, gt, n_gt, 0.3, 0.7, clobber)
+    l2, t2 = need_ext().anchor_assign_cpu(base, H, W, 16., im, border, gt, n_gt, 0.3, 0.7, clobber)
+    assert torch.equal(l1, l2) and torch.allclose(t1, t2, atol=1e-6)
+    assert (l2 == 1).any() and (l2[2] != 1).all()

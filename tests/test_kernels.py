@@ -436,3 +436,26 @@ def test_roi_pool_cpu_twin_matches_reference():
         o, a = need_ext().roi_pool_fwd_cpu(feat, rois, ph, pw, sc)
         assert torch.equal(a, ref_a), (ph, pw, sc)
         assert torch.equal(o, ref_o), (ph, pw, sc)
+
+
+def test_roi_pool_bwd_cpu_twin_matches_scatter():
+    from mx_rcnn_amd.ops import ext_available, need_ext
+    if not ext_available():
+        pytest.skip('extension not built')
+    g = torch.Generator().manual_seed(9)
+    feat = torch.randn(2, 16, 30, 40, generator=g)
+    rois = _rois(g, 64, 2, 30, 40)
+    rois[3, 0] = -1
+    _, arg = roi_pool_ref(feat, rois, 7, 7, 1 / 16)
+    gout = torch.randn(64, 16, 7, 7, generator=g)
+    ref = torch.zeros(2, 16 * 30 * 40, dtype=torch.float64)
+    for r in range(64):
+        b = int(rois[r, 0])
+        if b < 0:
+            continue
+        a = arg[r].reshape(16, -1).long()
+        m = a >= 0
+        ref[b].index_add_(0, (torch.arange(16)[:, None] * 1200 + a.clamp_min(0))[m], gout[r].reshape(16, -1)[m].double())
+    gin = need_ext().roi_pool_bwd_cpu(gout, arg, rois, 2, 30, 40)
+    assert torch.allclose(gin.double(), ref.reshape(2, 16, 30, 40), atol=1e-5)
+    assert torch.equal(gin, need_ext().roi_pool_bwd_cpu(gout, arg, rois, 2, 30, 40))

@@ -809,6 +809,38 @@ std::vector<Tensor> anchor_assign_cpu(const Tensor& base_in, int64_t H, int64_t 
   return {labels, targets};
 }
 
+// ---- CPU twin of iou_max (assign.hip): boxes (B, N, bs) rows [off, off+4), gt (B, G, >=4),
+// n_gt (B,).  Returns max (B, N), argmax (B, N) int32 [, per-gt max over rows of max(IoU, 0)].
+std::vector<Tensor> iou_max_cpu(const Tensor& boxes_in, int64_t off, const Tensor& gt_in, const Tensor& n_gt_in,
+                                bool want_gt_max) {
+  TORCH_CHECK(!boxes_in.is_cuda() && boxes_in.dim() == 3 && boxes_in.size(2) >= off + 4, "boxes must be CPU (B, N, >=off+4)");
+  TORCH_CHECK(gt_in.dim() == 3 && gt_in.size(2) >= 4 && gt_in.size(0) == boxes_in.size(0), "gt must be (B, G, >=4)");
+  const Tensor boxes = boxes_in.to(at::kFloat).contiguous();
+  const Tensor gt = gt_in.to(at::kFloat).contiguous();
+  const Tensor n_gt = n_gt_in.to(at::kLong).contiguous();
+  const int64_t B = boxes.size(0), N = boxes.size(1), bs = boxes.size(2), G = gt.size(1), gs = gt.size(2);
+  TORCH_CHECK(n_gt.numel() == B, "n_gt must be (B,)");
+  Tensor mx = at::empty({B, N}, boxes.options());
+  Tensor am = at::empty({B, N}, boxes.options().dtype(at::kInt));
+  Tensor gm = at::zeros({B, G}, boxes.options());
+  for (int64_t b = 0; b < B; ++b) {
+    const int64_t ng = std::min<int64_t>(std::max<int64_t>(n_gt.data_ptr<int64_t>()[b], 0), G);
+    const float* bx = boxes.data_ptr<float>() + b * N * bs;
+    const float* g = gt.data_ptr<float>() + b * G * gs;
+    at::parallel_for(0, N, 1024, [&](int64_t n0, int64_t n1) {
+      mxr::host::iou_max_rows(bx, bs, off, n0, n1, g, gs, ng, mx.data_ptr<float>() + b * N,
+                              am.data_ptr<int32_t>() + b * N);
+    });
+    if (want_gt_max) {
+      float* gmb = gm.data_ptr<float>() + b * G;
+      for (int64_t n = 0; n < N; ++n)
+        for (int64_t j = 0; j < ng; ++j) gmb[j] = std::max(gmb[j], mxr::host::iou1(bx + n * bs + off, g + j * gs));
+    }
+  }
+  if (want_gt_max) return {mx, am, gm};
+  return {mx, am};
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mx_rcnn_amd gfx950 kernels";
   m.def("proposal_decode", &proposal_decode);
@@ -818,6 +850,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("roi_pool_bwd_cpu", &roi_pool_bwd_cpu);
   m.def("proposal_decode_cpu", &proposal_decode_cpu);
   m.def("anchor_assign_cpu", &anchor_assign_cpu);
+  m.def("iou_max_cpu", &iou_max_cpu);
   m.def("iou_max", &iou_max);
   m.def("anchor_sample", &anchor_sample);
   m.def("proposal_sample", &proposal_sample);

@@ -1,4 +1,5 @@
-// Host (CPU) twins of the RPN anchor-target assignment, the proposal decode, the proposal NMS and the RoI max-pool forward /
+// Host (CPU) twins of the RPN anchor-target assignment, the proposal-target IoU pass, the
+// proposal decode, the proposal NMS and the RoI max-pool forward /
 // backward, written against raw pointers so the same code is linked into the extension
 // (bindings.cpp wraps it in ATen tensors and at::parallel_for) and into the sanitizer driver
 // tests/native/host_ops_test.cpp (built with -fsanitize=address,undefined and
@@ -231,6 +232,27 @@ inline void anchor_assign_range(const float* base, int64_t A, int64_t W, float s
     t[1] = (gcy - ecy) / (eh + 1e-14f);
     t[2] = std::log(gw / ew);
     t[3] = std::log(gh / eh);
+  }
+}
+
+// Row max / first argmax of IoU(boxes[n, off:off+4], gt[:ng]) for rows [n0, n1) (the
+// proposal-target overlap pass, rcnn/rpn/proposal_target.py _sample_rois bbox_overlaps +
+// argmax).  An image without gt gives 0 / 0 (numpy argmax of an all-zero row).
+inline void iou_max_rows(const float* boxes, int64_t bstride, int64_t off, int64_t n0, int64_t n1, const float* gt,
+                         int64_t gt_stride, int64_t ng, float* mx, int32_t* am) {
+  for (int64_t n = n0; n < n1; ++n) {
+    const float* a = boxes + n * bstride + off;
+    float best = ng > 0 ? -INFINITY : 0.f;
+    int32_t bi = 0;
+    for (int64_t g = 0; g < ng; ++g) {
+      const float v = iou1(a, gt + g * gt_stride);
+      if (v > best) {
+        best = v;
+        bi = (int32_t)g;
+      }
+    }
+    mx[n] = best;
+    am[n] = bi;
   }
 }
 

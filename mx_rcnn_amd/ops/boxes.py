@@ -2,7 +2,7 @@
 `bbox_regression.py:11-31`).  ``iou_max`` dispatches to the HIP row-reduction kernel."""
 import torch
 
-from ._ext import need_ext
+from ._ext import ext_available, need_ext
 
 
 def bbox_transform(ex, gt):
@@ -77,6 +77,13 @@ def iou_max(boxes, gt, n_gt, off=0, want_gt_max=False):
         C = need_ext()
         return tuple(C.iou_max(boxes.contiguous().float(), int(off), gt.contiguous().float(),
                                n_gt.to(torch.int32).contiguous(), bool(want_gt_max)))
+    if ext_available():  # C++ twin (host_ops.h iou_max_rows); the tensor version below is its oracle
+        return tuple(need_ext().iou_max_cpu(boxes, int(off), gt, n_gt, bool(want_gt_max)))
+    return iou_max_ref(boxes, gt, n_gt, off, want_gt_max)
+
+
+def iou_max_ref(boxes, gt, n_gt, off=0, want_gt_max=False):
+    """Dense tensor version of :func:`iou_max` (CPU oracle)."""
     b4 = boxes[..., off:off + 4].float()
     ov = box_iou(b4, gt[..., :4].float())  # (B, N, G)
     valid = _gt_valid(gt, n_gt)[:, None, :]

@@ -13,6 +13,7 @@
 //     NaN score and exp overflow inputs);
 //   * anchor assignment: anchor-row ranges on threads bitwise equal to one pass, label
 //     invariants with 0 / some / all gt (fg present without clobber, none without gt);
+//   * IoU row max: ranges on threads equal one pass, IoU 1 for boxes equal to a gt, no-gt rows;
 //   * RoI pool ranges run concurrently on std::threads equal the serial result (the
 //     at::parallel_for contract; -fsanitize=thread checks the disjoint-write claim).
 #include <cmath>
@@ -312,6 +313,41 @@ void test_anchor_assign() {
     }
 }
 
+void test_iou_max() {
+  Rng g(23);
+  const int64_t N = 300, bs = 5, G = 6;
+  std::vector<float> boxes(N * bs), gt(G * 5);
+  for (int64_t n = 0; n < N; ++n) {
+    const float x = (float)(g.uni() * 400), y = (float)(g.uni() * 300);
+    boxes[n * bs] = 0.f;
+    boxes[n * bs + 1] = x;
+    boxes[n * bs + 2] = y;
+    boxes[n * bs + 3] = x + (float)(g.uni() * 120);
+    boxes[n * bs + 4] = y + (float)(g.uni() * 120);
+  }
+  for (int64_t j = 0; j < G; ++j)
+    for (int k = 0; k < 4; ++k) gt[j * 5 + k] = boxes[(j * 37) * bs + 1 + k];  // gt j == box 37 j
+  for (int64_t ng : {(int64_t)0, G}) {
+    std::vector<float> m1(N), m2(N);
+    std::vector<int32_t> a1(N), a2(N);
+    mxr::host::iou_max_rows(boxes.data(), bs, 1, 0, N, gt.data(), 5, ng, m1.data(), a1.data());
+    std::vector<std::thread> th;
+    for (int t = 0; t < 3; ++t)
+      th.emplace_back([&, t] {
+        mxr::host::iou_max_rows(boxes.data(), bs, 1, N * t / 3, N * (t + 1) / 3, gt.data(), 5, ng, m2.data(),
+                                a2.data());
+      });
+    for (auto& x : th) x.join();
+    CHECK(m1 == m2 && a1 == a2, "threaded iou_max differs");
+    for (int64_t n = 0; n < N; ++n) {
+      CHECK(m1[n] >= 0.f && m1[n] <= 1.f && a1[n] >= 0 && a1[n] < std::max<int64_t>(ng, 1), "row %ld", (long)n);
+      if (ng == 0) CHECK(m1[n] == 0.f && a1[n] == 0, "no-gt row %ld", (long)n);
+    }
+    if (ng > 0)
+      for (int64_t j = 0; j < G; ++j) CHECK(m1[j * 37] == 1.f, "box equal to gt %ld must have IoU 1", (long)j);
+  }
+}
+
 }  // namespace
 
 int main() {
@@ -320,6 +356,7 @@ int main() {
   test_roi_pool_bwd();
   test_proposal_decode();
   test_anchor_assign();
+  test_iou_max();
   if (g_fail) {
     std::fprintf(stderr, "%d check(s) failed\n", g_fail);
     return 1;

@@ -415,3 +415,27 @@ def test_anchor_assign_cpu_twin_matches_tensor_ref(clobber, border):
     l2, t2 = need_ext().anchor_assign_cpu(base, H, W, 16., im, border, gt, n_gt, 0.3, 0.7, clobber)
     assert torch.equal(l1, l2) and torch.allclose(t1, t2, atol=1e-6)
     assert (l2 == 1).any() and (l2[2] != 1).all()
+
+
+def test_iou_max_cpu_twin_matches_tensor_ref():
+    """C++ twin (host_ops.h iou_max_rows) vs the dense tensor version: exact max, first argmax
+    on ties, image without gt -> 0 / 0, per-gt column max."""
+    from mx_rcnn_amd.ops import ext_available, need_ext
+    from mx_rcnn_amd.ops.boxes import iou_max_ref
+    if not ext_available():
+        pytest.skip('extension not built')
+    g = torch.Generator().manual_seed(5)
+    B, N, G = 3, 700, 7
+    xy = torch.rand(B, N, 2, generator=g) * 600
+    r = torch.cat([torch.zeros(B, N, 1), xy, xy + torch.rand(B, N, 2, generator=g) * 150], -1)
+    gxy = torch.rand(B, G, 2, generator=g) * 600
+    gt = torch.cat([gxy, gxy + torch.rand(B, G, 2, generator=g) * 150 + 5, torch.ones(B, G, 1)], -1)
+    gt[0, 4, :4] = gt[0, 2, :4]  # duplicate gt: argmax must take the first
+    r[0, 5, 1:] = gt[0, 2, :4]
+    n_gt = torch.tensor([7, 3, 0], dtype=torch.int32)
+    for want in (False, True):
+        a = iou_max_ref(r, gt, n_gt, off=1, want_gt_max=want)
+        b = need_ext().iou_max_cpu(r, 1, gt, n_gt, want)
+        for x, y in zip(a, b):
+            assert torch.equal(x, y)
+    assert int(b[1][0, 5]) == 2 and float(b[0][0, 5]) == 1.0

@@ -151,3 +151,17 @@ def test_exact_resume_from_states(tmp_path):
     b2, _ = load_checkpoint(b_pref, 2)
     for k in a2:
         np.testing.assert_allclose(a2[k], b2[k], rtol=1e-2, atol=1e-5, err_msg=k)
+
+
+def test_watchdog_in_fit_reports_slow_steps_and_stops(monkeypatch):
+    """MXR_WATCHDOG=<s> arms the heartbeat inside Module.fit: CPU steps slower than the stall
+    limit are reported (the loop itself is not disturbed) and the thread ends with fit."""
+    import threading
+    from mx_rcnn_amd.parallel import watchdog
+    seen = []
+    monkeypatch.setattr(watchdog.Heartbeat, '_report', lambda self, *a: seen.append(a))
+    monkeypatch.setenv('MXR_WATCHDOG', '0.02')
+    mod, data = _tiny_module()
+    mod.fit(data, num_epoch=1, max_steps=2, optimizer_params={'learning_rate': 1e-3, 'momentum': 0.9, 'wd': 5e-4})
+    assert seen and all(k == 'local' for k, *_ in seen)
+    assert not any(t.name == 'mxr-heartbeat' for t in threading.enumerate())

@@ -841,6 +841,35 @@ std::vector<Tensor> iou_max_cpu(const Tensor& boxes_in, int64_t off, const Tenso
   return {mx, am};
 }
 
+// ---- CPU twins of the fused losses (losses.hip): value and gradient in one pass.
+std::vector<Tensor> rpn_softmax_ce_cpu(const Tensor& logits_in, const Tensor& label_in, double grad_scale) {
+  TORCH_CHECK(!logits_in.is_cuda() && logits_in.dim() == 4 && logits_in.size(1) % 2 == 0, "logits must be CPU (B, 2A, H, W)");
+  const Tensor logits = logits_in.to(at::kFloat).contiguous();
+  const Tensor label = label_in.to(at::kInt).contiguous();
+  const int64_t B = logits.size(0), AHW = logits.size(1) / 2 * logits.size(2) * logits.size(3);
+  TORCH_CHECK(label.numel() == B * AHW, "label must hold B * A*H*W entries");
+  Tensor grad = at::empty_like(logits);
+  const float loss = mxr::host::rpn_softmax_ce(logits.data_ptr<float>(), label.data_ptr<int32_t>(), B, AHW,
+                                               (float)grad_scale, grad.data_ptr<float>());
+  return {grad, at::full({1}, loss, logits.options())};
+}
+
+std::vector<Tensor> smooth_l1_cpu(const Tensor& pred_in, const Tensor& tgt_in, const Tensor& iw_in,
+                                  const Tensor& ow_in, double sigma, double grad_scale) {
+  TORCH_CHECK(!pred_in.is_cuda(), "smooth_l1_cpu takes CPU tensors");
+  const Tensor pred = pred_in.to(at::kFloat).contiguous();
+  const Tensor tgt = tgt_in.to(at::kFloat).contiguous();
+  const Tensor iw = iw_in.to(at::kFloat).contiguous();
+  const Tensor ow = ow_in.to(at::kFloat).contiguous();
+  TORCH_CHECK(tgt.numel() == pred.numel() && iw.numel() == pred.numel() && ow.numel() == pred.numel(),
+              "pred / target / weights must have the same size");
+  Tensor grad = at::empty_like(pred);
+  const float loss = mxr::host::smooth_l1(pred.data_ptr<float>(), tgt.data_ptr<float>(), iw.data_ptr<float>(),
+                                          ow.data_ptr<float>(), pred.numel(), (float)sigma, (float)grad_scale,
+                                          grad.data_ptr<float>());
+  return {grad, at::full({1}, loss, pred.options())};
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mx_rcnn_amd gfx950 kernels";
   m.def("proposal_decode", &proposal_decode);
@@ -851,6 +880,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("proposal_decode_cpu", &proposal_decode_cpu);
   m.def("anchor_assign_cpu", &anchor_assign_cpu);
   m.def("iou_max_cpu", &iou_max_cpu);
+  m.def("rpn_softmax_ce_cpu", &rpn_softmax_ce_cpu);
+  m.def("smooth_l1_cpu", &smooth_l1_cpu);
   m.def("iou_max", &iou_max);
   m.def("anchor_sample", &anchor_sample);
   m.def("proposal_sample", &proposal_sample);

@@ -1,4 +1,4 @@
-// Host (CPU) twins of the RPN anchor-target assignment, the proposal-target IoU pass, the
+// Host (CPU) twins of the RPN softmax-CE and smooth-L1 losses, the RPN anchor-target assignment, the proposal-target IoU pass, the
 // proposal decode, the proposal NMS and the RoI max-pool forward /
 // backward, written against raw pointers so the same code is linked into the extension
 // (bindings.cpp wraps it in ATen tensors and at::parallel_for) and into the sanitizer driver
@@ -254,6 +254,53 @@ inline void iou_max_rows(const float* boxes, int64_t bstride, int64_t off, int64
     mx[n] = best;
     am[n] = bi;
   }
+}
+
+// RPN SoftmaxOutput(multi_output, use_ignore=-1, normalization='valid') in one pass per
+// element (rcnn/symbol.py:194 rpn_cls_prob): logits (B, 2A, H, W) viewed as (B, 2, A*H*W)
+// (bg = first A channels), label (B, A*H*W) in {-1, 0, 1}.  grad = (p - onehot) * valid *
+// grad_scale / max(#valid, 1); returns the mean -log p over the valid labels.  The loss is
+// accumulated in double in element order (reproducible).
+inline float rpn_softmax_ce(const float* logits, const int32_t* label, int64_t B, int64_t AHW, float grad_scale,
+                            float* grad) {
+  int64_t nvalid = 0;
+  for (int64_t i = 0; i < B * AHW; ++i) nvalid += label[i] >= 0;
+  const float norm = (float)std::max<int64_t>(nvalid, 1), gs = grad_scale / norm;
+  double loss = 0.0;
+  for (int64_t b = 0; b < B; ++b)
+    for (int64_t i = 0; i < AHW; ++i) {
+      const int64_t i0 = b * 2 * AHW + i, i1 = i0 + AHW;
+      const int32_t l = label[b * AHW + i];
+      const float m = std::max(logits[i0], logits[i1]);
+      const float e0 = std::exp(logits[i0] - m), e1 = std::exp(logits[i1] - m), s = e0 + e1;
+      const float p0 = e0 / s, p1 = e1 / s;
+      if (l < 0) {
+        grad[i0] = grad[i1] = 0.f;
+        continue;
+      }
+      grad[i0] = (p0 - (l == 0 ? 1.f : 0.f)) * gs;
+      grad[i1] = (p1 - (l == 1 ? 1.f : 0.f)) * gs;
+      loss -= std::log((double)std::max(l == 1 ? p1 : p0, 1e-14f));
+    }
+  return (float)(loss / norm);
+}
+
+// MakeLoss(outside * smooth_l1(inside * (pred - target), sigma), grad_scale) value and
+// gradient in one pass (rcnn/symbol.py:378 bbox_loss): f(x) = 0.5 (sigma x)^2 if |x| < 1 /
+// sigma^2 else |x| - 0.5 / sigma^2.  Returns sum(outside * f), double-accumulated.
+inline float smooth_l1(const float* pred, const float* tgt, const float* iw, const float* ow, int64_t n, float sigma,
+                       float grad_scale, float* grad) {
+  const float s2 = sigma * sigma;
+  double loss = 0.0;
+  for (int64_t i = 0; i < n; ++i) {
+    const float x = iw[i] * (pred[i] - tgt[i]), ax = std::fabs(x);
+    const bool small = ax < 1.f / s2;
+    const float f = small ? 0.5f * s2 * x * x : ax - 0.5f / s2;
+    const float d = small ? s2 * x : (float)((x > 0.f) - (x < 0.f));
+    grad[i] = grad_scale * ow[i] * d * iw[i];
+    loss += (double)(ow[i] * f);
+  }
+  return (float)loss;
 }
 
 }  // namespace host

@@ -12,7 +12,7 @@ mean -log p over the normalisation count, and grad_scale * sum(elementwise loss)
 """
 import torch
 
-from ._ext import need_ext
+from ._ext import ext_available, need_ext
 
 
 class _RpnCE(torch.autograd.Function):
@@ -30,6 +30,10 @@ class _RpnCE(torch.autograd.Function):
                 grad, loss = ext.rpn_softmax_ce(logits, lab, norm, float(grad_scale), False)
             ctx.save_for_backward(grad)
             return loss.reshape(())  # normalised in-kernel
+        if ext_available():  # C++ twin (host_ops.h); the tensor version below is its oracle
+            grad, loss = need_ext().rpn_softmax_ce_cpu(logits, lab, float(grad_scale))
+            ctx.save_for_backward(grad.to(logits.dtype))
+            return loss.reshape(())
         norm = (lab >= 0).sum().float().reshape(1)
         z = logits.float().reshape(B, 2, A * H, W)
         p = torch.softmax(z, dim=1)
@@ -110,6 +114,9 @@ class _SmoothL1(torch.autograd.Function):
         if pred.is_cuda:
             ext = need_ext()
             grad, loss = ext.smooth_l1(pred, t, iw, ow, float(sigma), float(grad_scale), int(slot))
+        elif ext_available():  # C++ twin (host_ops.h)
+            grad, loss = need_ext().smooth_l1_cpu(pred, t, iw, ow, float(sigma), float(grad_scale))
+            grad = grad.to(pred.dtype)
         else:
             s2 = sigma * sigma
             x = iw * (pred.float() - t)

@@ -14,6 +14,8 @@
 //   * anchor assignment: anchor-row ranges on threads bitwise equal to one pass, label
 //     invariants with 0 / some / all gt (fg present without clobber, none without gt);
 //   * IoU row max: ranges on threads equal one pass, IoU 1 for boxes equal to a gt, no-gt rows;
+//   * losses: softmax-CE gradient pairs cancel, ignored labels carry no gradient, large logits
+//     stay finite; smooth-L1 gradient bounded by the outside weight and masked by inside;
 //   * RoI pool ranges run concurrently on std::threads equal the serial result (the
 //     at::parallel_for contract; -fsanitize=thread checks the disjoint-write claim).
 #include <cmath>
@@ -348,6 +350,39 @@ void test_iou_max() {
   }
 }
 
+void test_losses() {
+  Rng g(29);
+  const int64_t B = 2, AHW = 9 * 5 * 7;
+  std::vector<float> logits(B * 2 * AHW), grad(B * 2 * AHW);
+  std::vector<int32_t> label(B * AHW);
+  for (auto& v : logits) v = (float)(g.uni() * 40 - 20);  // large logits: exp stability
+  for (auto& l : label) l = (int32_t)(g.uni() * 3) - 1;
+  const float loss = mxr::host::rpn_softmax_ce(logits.data(), label.data(), B, AHW, 1.f, grad.data());
+  CHECK(std::isfinite(loss) && loss >= 0.f, "rpn ce loss %f", loss);
+  for (int64_t b = 0; b < B; ++b)
+    for (int64_t i = 0; i < AHW; ++i) {
+      const float g0 = grad[b * 2 * AHW + i], g1 = grad[b * 2 * AHW + AHW + i];
+      CHECK(std::fabs(g0 + g1) < 1e-6f, "softmax grads of one anchor must cancel");
+      if (label[b * AHW + i] < 0) CHECK(g0 == 0.f && g1 == 0.f, "ignored label with gradient");
+    }
+  std::vector<int32_t> none(B * AHW, -1);
+  CHECK(mxr::host::rpn_softmax_ce(logits.data(), none.data(), B, AHW, 1.f, grad.data()) == 0.f, "all ignored");
+  const int64_t n = 4 * 21 * 16;
+  std::vector<float> p(n), t(n), iw(n), ow(n), gr(n);
+  for (int64_t i = 0; i < n; ++i) {
+    p[i] = (float)(g.uni() * 4 - 2);
+    t[i] = (float)(g.uni() * 4 - 2);
+    iw[i] = g.uni() < 0.5 ? 1.f : 0.f;
+    ow[i] = iw[i] / 16.f;
+  }
+  const float sl = mxr::host::smooth_l1(p.data(), t.data(), iw.data(), ow.data(), n, 3.f, 1.f, gr.data());
+  CHECK(std::isfinite(sl) && sl >= 0.f, "smooth l1 %f", sl);
+  for (int64_t i = 0; i < n; ++i) {
+    if (iw[i] == 0.f) CHECK(gr[i] == 0.f, "masked element with gradient");
+    CHECK(std::fabs(gr[i]) <= 1.f / 16.f + 1e-7f, "smooth-L1 gradient not bounded by the outside weight");
+  }
+}
+
 }  // namespace
 
 int main() {
@@ -357,6 +392,7 @@ int main() {
   test_proposal_decode();
   test_anchor_assign();
   test_iou_max();
+  test_losses();
   if (g_fail) {
     std::fprintf(stderr, "%d check(s) failed\n", g_fail);
     return 1;

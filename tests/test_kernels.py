@@ -459,3 +459,34 @@ def test_roi_pool_bwd_cpu_twin_matches_scatter():
     gin = need_ext().roi_pool_bwd_cpu(gout, arg, rois, 2, 30, 40)
     assert torch.allclose(gin.double(), ref.reshape(2, 16, 30, 40), atol=1e-5)
     assert torch.equal(gin, need_ext().roi_pool_bwd_cpu(gout, arg, rois, 2, 30, 40))
+
+
+@pytest.mark.parametrize('which', ['rpn_ce', 'smooth_l1'])
+def test_loss_cpu_twins_match_tensor_path(which, monkeypatch):
+    """C++ loss twins (host_ops.h) vs the tensor path (ext disabled): value and autograd grad."""
+    from mx_rcnn_amd.ops import ext_available
+    from mx_rcnn_amd.ops import losses as L
+    if not ext_available():
+        pytest.skip('extension not built')
+    g = torch.Generator().manual_seed(12)
+    if which == 'rpn_ce':
+        x = torch.randn(2, 18, 7, 9, generator=g) * 3
+        lab = torch.randint(-1, 2, (2, 9 * 7 * 9), generator=g).to(torch.int32)
+        fn = lambda t: L.rpn_softmax_ce(t, lab, grad_scale=1.0)  # noqa: E731
+    else:
+        x = torch.randn(64, 84, generator=g)
+        tgt = torch.randn(64, 84, generator=g)
+        iw = (torch.rand(64, 84, generator=g) > 0.5).float()
+        ow = iw / 64
+        fn = lambda t: L.smooth_l1(t, tgt, iw, ow, sigma=3.0, grad_scale=0.5)  # noqa: E731
+    outs = []
+    for use_ext in (True, False):
+        if not use_ext:
+            monkeypatch.setattr(L, 'ext_available', lambda: False)
+        xi = x.clone().requires_grad_()
+        v = fn(xi)
+        (v * 1.5).backward()
+        outs.append((v.detach(), xi.grad))
+    (v1, g1), (v2, g2) = outs
+    assert torch.allclose(v1, v2, rtol=1e-5, atol=1e-6), (v1, v2)
+    assert torch.allclose(g1, g2, rtol=1e-5, atol=1e-7)

@@ -870,6 +870,23 @@ std::vector<Tensor> smooth_l1_cpu(const Tensor& pred_in, const Tensor& tgt_in, c
   return {grad, at::full({1}, loss, pred.options())};
 }
 
+// ---- CPU twin of the fused SGD-momentum update (sgd.hip), in place on fp32 w / mom.
+void sgd_momentum_cpu(Tensor w, Tensor mom, const Tensor& grad_in, double lr, double momentum, double wd,
+                      double rescale, double clip) {
+  TORCH_CHECK(!w.is_cuda() && w.scalar_type() == at::kFloat && mom.scalar_type() == at::kFloat &&
+                  w.is_contiguous() && mom.is_contiguous() && w.numel() == mom.numel(),
+              "w / mom must be contiguous fp32 CPU tensors of one size");
+  const Tensor grad = grad_in.to(at::kFloat).contiguous();
+  TORCH_CHECK(grad.numel() == w.numel(), "grad size");
+  float* wp = w.data_ptr<float>();
+  float* mp = mom.data_ptr<float>();
+  const float* gp = grad.data_ptr<float>();
+  at::parallel_for(0, w.numel(), 1 << 16, [&](int64_t n0, int64_t n1) {
+    mxr::host::sgd_momentum_range(wp, mp, gp, n0, n1, (float)lr, (float)momentum, (float)wd, (float)rescale,
+                                  (float)clip);
+  });
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mx_rcnn_amd gfx950 kernels";
   m.def("proposal_decode", &proposal_decode);
@@ -882,6 +899,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("iou_max_cpu", &iou_max_cpu);
   m.def("rpn_softmax_ce_cpu", &rpn_softmax_ce_cpu);
   m.def("smooth_l1_cpu", &smooth_l1_cpu);
+  m.def("sgd_momentum_cpu", &sgd_momentum_cpu);
   m.def("iou_max", &iou_max);
   m.def("anchor_sample", &anchor_sample);
   m.def("proposal_sample", &proposal_sample);

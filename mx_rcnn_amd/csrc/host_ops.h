@@ -1,4 +1,4 @@
-// Host (CPU) twins of the RPN softmax-CE and smooth-L1 losses, the RPN anchor-target assignment, the proposal-target IoU pass, the
+// Host (CPU) twins of the SGD-momentum update, the RPN softmax-CE and smooth-L1 losses, the RPN anchor-target assignment, the proposal-target IoU pass, the
 // proposal decode, the proposal NMS and the RoI max-pool forward /
 // backward, written against raw pointers so the same code is linked into the extension
 // (bindings.cpp wraps it in ATen tensors and at::parallel_for) and into the sanitizer driver
@@ -301,6 +301,19 @@ inline float smooth_l1(const float* pred, const float* tgt, const float* iw, con
     loss += (double)(ow[i] * f);
   }
   return (float)loss;
+}
+
+// SGD with momentum, MXNet semantics (SURVEY 2.9 SGD row): g = clip(rescale * grad, +-clip)
+// (clip <= 0: none), mom = momentum * mom - lr * (g + wd * w), w += mom; elements [n0, n1).
+inline void sgd_momentum_range(float* w, float* mom, const float* grad, int64_t n0, int64_t n1, float lr,
+                               float momentum, float wd, float rescale, float clip) {
+  for (int64_t i = n0; i < n1; ++i) {
+    float g = grad[i] * rescale;
+    if (clip > 0.f) g = std::min(std::max(g, -clip), clip);
+    const float m = mom[i] * momentum - lr * (g + wd * w[i]);
+    mom[i] = m;
+    w[i] += m;
+  }
 }
 
 }  // namespace host

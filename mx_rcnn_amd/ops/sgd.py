@@ -2,7 +2,7 @@
 rescale_grad and weight decay, `train_end2end.py:98-105`)."""
 import torch
 
-from ._ext import need_ext
+from ._ext import ext_available, need_ext
 
 
 def sgd_momentum_(w, mom, grad, lr, momentum=0.9, wd=0.0, rescale=1.0, clip=-1.0, w_bf16=None):
@@ -13,6 +13,12 @@ def sgd_momentum_(w, mom, grad, lr, momentum=0.9, wd=0.0, rescale=1.0, clip=-1.0
     """
     if w.is_cuda:
         need_ext().sgd_momentum(w, mom, grad, lr, float(momentum), float(wd), float(rescale), float(clip), w_bf16)
+        return
+    if ext_available() and w.dtype == torch.float32 and w.is_contiguous() and mom.is_contiguous():
+        # C++ twin (host_ops.h): one fused, thread-parallel pass instead of five tensor ops
+        need_ext().sgd_momentum_cpu(w, mom, grad, float(lr), float(momentum), float(wd), float(rescale), float(clip))
+        if w_bf16 is not None:
+            w_bf16.copy_(w.to(torch.bfloat16))
         return
     g = grad.float() * rescale
     if clip > 0:

@@ -16,6 +16,7 @@
 //   * IoU row max: ranges on threads equal one pass, IoU 1 for boxes equal to a gt, no-gt rows;
 //   * losses: softmax-CE gradient pairs cancel, ignored labels carry no gradient, large logits
 //     stay finite; smooth-L1 gradient bounded by the outside weight and masked by inside;
+//   * SGD-momentum: element ranges on threads equal one pass and the hand-written update;
 //   * RoI pool ranges run concurrently on std::threads equal the serial result (the
 //     at::parallel_for contract; -fsanitize=thread checks the disjoint-write claim).
 #include <cmath>
@@ -383,6 +384,32 @@ void test_losses() {
   }
 }
 
+void test_sgd() {
+  Rng g(37);
+  const int64_t n = 10007;
+  std::vector<float> w(n), m(n), gr(n);
+  for (int64_t i = 0; i < n; ++i) {
+    w[i] = (float)(g.uni() - 0.5);
+    m[i] = (float)(g.uni() - 0.5) * 0.1f;
+    gr[i] = (float)(g.uni() * 4 - 2);
+  }
+  std::vector<float> w1 = w, m1 = m, w2 = w, m2 = m;
+  mxr::host::sgd_momentum_range(w1.data(), m1.data(), gr.data(), 0, n, 0.01f, 0.9f, 5e-4f, 0.5f, 0.3f);
+  std::vector<std::thread> th;
+  for (int t = 0; t < 4; ++t)
+    th.emplace_back([&, t] {
+      mxr::host::sgd_momentum_range(w2.data(), m2.data(), gr.data(), n * t / 4, n * (t + 1) / 4, 0.01f, 0.9f, 5e-4f,
+                                    0.5f, 0.3f);
+    });
+  for (auto& x : th) x.join();
+  CHECK(w1 == w2 && m1 == m2, "threaded SGD differs");
+  for (int64_t i = 0; i < n; i += 997) {
+    const float gc = std::min(std::max(gr[i] * 0.5f, -0.3f), 0.3f);
+    const float me = m[i] * 0.9f - 0.01f * (gc + 5e-4f * w[i]);
+    CHECK(m1[i] == me && w1[i] == w[i] + me, "SGD element %ld", (long)i);
+  }
+}
+
 }  // namespace
 
 int main() {
@@ -393,6 +420,7 @@ int main() {
   test_anchor_assign();
   test_iou_max();
   test_losses();
+  test_sgd();
   if (g_fail) {
     std::fprintf(stderr, "%d check(s) failed\n", g_fail);
     return 1;

@@ -490,3 +490,25 @@ def test_loss_cpu_twins_match_tensor_path(which, monkeypatch):
     (v1, g1), (v2, g2) = outs
     assert torch.allclose(v1, v2, rtol=1e-5, atol=1e-6), (v1, v2)
     assert torch.allclose(g1, g2, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize('clip', [-1.0, 0.05])
+def test_sgd_cpu_twin_matches_tensor_path(clip, monkeypatch):
+    from mx_rcnn_amd.ops import ext_available
+    from mx_rcnn_amd.ops import sgd as S
+    if not ext_available():
+        pytest.skip('extension not built')
+    g = torch.Generator().manual_seed(31)
+    n = 300001  # not a multiple of the parallel grain
+    w0, m0, gr = (torch.randn(n, generator=g) for _ in range(3))
+    lr = torch.tensor([0.01])
+    res = []
+    for use_ext in (True, False):
+        if not use_ext:
+            monkeypatch.setattr(S, 'ext_available', lambda: False)
+        w, m = w0.clone(), m0.clone()
+        wb = torch.empty(n, dtype=torch.bfloat16)
+        S.sgd_momentum_(w, m, gr, lr, momentum=0.9, wd=5e-4, rescale=0.5, clip=clip, w_bf16=wb)
+        res.append((w, m, wb))
+    for a, b in zip(*res):
+        assert torch.allclose(a.float(), b.float(), rtol=1e-6, atol=1e-7)

@@ -887,6 +887,30 @@ void sgd_momentum_cpu(Tensor w, Tensor mom, const Tensor& grad_in, double lr, do
   });
 }
 
+// ---- CPU twin of the head softmax-CE (row_softmax_ce in losses.hip).  Returns grad, prob,
+// loss (1,) = sum over valid rows of -log p / norm; per-chunk partial sums are added in chunk
+// order, so the value does not depend on the thread count's scheduling.
+std::vector<Tensor> row_softmax_ce_cpu(const Tensor& logits_in, const Tensor& label_in, double norm,
+                                       double grad_scale) {
+  TORCH_CHECK(!logits_in.is_cuda() && logits_in.dim() == 2, "logits must be a CPU (R, C) tensor");
+  const Tensor logits = logits_in.to(at::kFloat).contiguous();
+  const Tensor label = label_in.to(at::kInt).contiguous();
+  const int64_t R = logits.size(0), C = logits.size(1);
+  TORCH_CHECK(label.numel() == R && C > 0, "label must be (R,)");
+  Tensor prob = at::empty_like(logits), grad = at::empty_like(logits);
+  const int64_t grain = 64, chunks = (R + grain - 1) / grain;
+  std::vector<double> part(std::max<int64_t>(chunks, 1), 0.0);
+  at::parallel_for(0, chunks, 1, [&](int64_t c0, int64_t c1) {
+    for (int64_t k = c0; k < c1; ++k)
+      part[k] = mxr::host::row_softmax_ce_range(logits.data_ptr<float>(), label.data_ptr<int32_t>(), C, k * grain,
+                                                std::min(R, (k + 1) * grain), (float)norm, (float)grad_scale,
+                                                prob.data_ptr<float>(), grad.data_ptr<float>());
+  });
+  double loss = 0.0;
+  for (double v : part) loss += v;
+  return {grad, prob, at::full({1}, (float)(loss / norm), logits.options())};
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mx_rcnn_amd gfx950 kernels";
   m.def("proposal_decode", &proposal_decode);
@@ -900,6 +924,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("rpn_softmax_ce_cpu", &rpn_softmax_ce_cpu);
   m.def("smooth_l1_cpu", &smooth_l1_cpu);
   m.def("sgd_momentum_cpu", &sgd_momentum_cpu);
+  m.def("row_softmax_ce_cpu", &row_softmax_ce_cpu);
   m.def("iou_max", &iou_max);
   m.def("anchor_sample", &anchor_sample);
   m.def("proposal_sample", &proposal_sample);

@@ -1,4 +1,5 @@
-// Host (CPU) twins of the SGD-momentum update, the RPN softmax-CE and smooth-L1 losses, the RPN anchor-target assignment, the proposal-target IoU pass, the
+// Host (CPU) twins of the SGD-momentum update, the RPN / R-CNN softmax-CE and smooth-L1
+// losses, the RPN anchor-target assignment, the proposal-target IoU pass, the
 // proposal decode, the proposal NMS and the RoI max-pool forward /
 // backward, written against raw pointers so the same code is linked into the extension
 // (bindings.cpp wraps it in ATen tensors and at::parallel_for) and into the sanitizer driver
@@ -314,6 +315,33 @@ inline void sgd_momentum_range(float* w, float* mom, const float* grad, int64_t 
     mom[i] = m;
     w[i] += m;
   }
+}
+
+// R-CNN head SoftmaxOutput (normalization 'batch' / 'null', rcnn/symbol.py cls_prob) for rows
+// [r0, r1) of (R, C) logits: prob = softmax(row), grad = (prob - onehot) * valid * grad_scale /
+// norm (label < 0 = ignored row).  Returns the rows' summed -log p (divide by norm outside);
+// rows are independent, so ranges may run concurrently.
+inline double row_softmax_ce_range(const float* logits, const int32_t* label, int64_t C, int64_t r0, int64_t r1,
+                                   float norm, float grad_scale, float* prob, float* grad) {
+  double loss = 0.0;
+  const float gs = grad_scale / norm;
+  for (int64_t r = r0; r < r1; ++r) {
+    const float* x = logits + r * C;
+    float* p = prob + r * C;
+    float m = x[0];
+    for (int64_t c = 1; c < C; ++c) m = std::max(m, x[c]);
+    float s = 0.f;
+    for (int64_t c = 0; c < C; ++c) {
+      p[c] = std::exp(x[c] - m);
+      s += p[c];
+    }
+    for (int64_t c = 0; c < C; ++c) p[c] /= s;
+    const int32_t l = label[r];
+    const bool valid = l >= 0 && l < C;
+    for (int64_t c = 0; c < C; ++c) grad[r * C + c] = valid ? (p[c] - (c == l ? 1.f : 0.f)) * gs : 0.f;
+    if (valid) loss -= std::log((double)std::max(p[l], 1e-14f));
+  }
+  return loss;
 }
 
 }  // namespace host

@@ -76,6 +76,11 @@ class _RowCE(torch.autograd.Function):
             ctx.save_for_backward(grad)
             ctx.mark_non_differentiable(prob)
             return loss.reshape(()), prob  # divided by norm in-kernel
+        if ext_available():  # C++ twin (host_ops.h)
+            grad, prob, loss = need_ext().row_softmax_ce_cpu(logits, lab, float(norm), float(grad_scale))
+            ctx.save_for_backward(grad.to(logits.dtype))
+            ctx.mark_non_differentiable(prob)
+            return loss.reshape(()), prob
         p = torch.softmax(logits.float(), dim=1)
         valid = (lab >= 0)
         onehot = torch.nn.functional.one_hot(lab.long().clamp_min(0), logits.shape[1]).float()

@@ -16,6 +16,7 @@
 //   * IoU row max: ranges on threads equal one pass, IoU 1 for boxes equal to a gt, no-gt rows;
 //   * losses: softmax-CE gradient pairs cancel, ignored labels carry no gradient, large logits
 //     stay finite; smooth-L1 gradient bounded by the outside weight and masked by inside;
+//   * head softmax-CE: row ranges on threads equal one pass, rows sum to 1, gradients to 0;
 //   * SGD-momentum: element ranges on threads equal one pass and the hand-written update;
 //   * RoI pool ranges run concurrently on std::threads equal the serial result (the
 //     at::parallel_for contract; -fsanitize=thread checks the disjoint-write claim).
@@ -410,6 +411,35 @@ void test_sgd() {
   }
 }
 
+void test_row_softmax_ce() {
+  Rng g(41);
+  const int64_t R = 257, C = 21;
+  std::vector<float> x(R * C), p1(R * C), g1(R * C), p2(R * C), g2(R * C);
+  std::vector<int32_t> lab(R);
+  for (auto& v : x) v = (float)(g.uni() * 60 - 30);
+  for (auto& l : lab) l = (int32_t)(g.uni() * (C + 1)) - 1;
+  const double l1 = mxr::host::row_softmax_ce_range(x.data(), lab.data(), C, 0, R, (float)R, 1.f, p1.data(), g1.data());
+  double parts[4];
+  std::vector<std::thread> th;
+  for (int t = 0; t < 4; ++t)
+    th.emplace_back([&, t] {
+      parts[t] = mxr::host::row_softmax_ce_range(x.data(), lab.data(), C, R * t / 4, R * (t + 1) / 4, (float)R, 1.f,
+                                                 p2.data(), g2.data());
+    });
+  for (auto& x_ : th) x_.join();
+  CHECK(p1 == p2 && g1 == g2, "threaded row CE differs");
+  CHECK(std::fabs(l1 - (parts[0] + parts[1] + parts[2] + parts[3])) < 1e-9 * std::max(1.0, l1), "row CE partials");
+  for (int64_t r = 0; r < R; ++r) {
+    double ps = 0.0, gsum = 0.0;
+    for (int64_t c = 0; c < C; ++c) {
+      ps += p1[r * C + c];
+      gsum += g1[r * C + c];
+    }
+    CHECK(std::fabs(ps - 1.0) < 1e-5, "row %ld probabilities sum to %f", (long)r, ps);
+    CHECK(std::fabs(gsum) < 1e-6, "row %ld gradient sums to %g", (long)r, gsum);
+  }
+}
+
 }  // namespace
 
 int main() {
@@ -421,6 +451,7 @@ int main() {
   test_iou_max();
   test_losses();
   test_sgd();
+  test_row_softmax_ce();
   if (g_fail) {
     std::fprintf(stderr, "%d check(s) failed\n", g_fail);
     return 1;

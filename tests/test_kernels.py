@@ -461,7 +461,7 @@ def test_roi_pool_bwd_cpu_twin_matches_scatter():
     assert torch.equal(gin, need_ext().roi_pool_bwd_cpu(gout, arg, rois, 2, 30, 40))
 
 
-@pytest.mark.parametrize('which', ['rpn_ce', 'smooth_l1'])
+@pytest.mark.parametrize('which', ['rpn_ce', 'smooth_l1', 'row_ce'])
 def test_loss_cpu_twins_match_tensor_path(which, monkeypatch):
     """C++ loss twins (host_ops.h) vs the tensor path (ext disabled): value and autograd grad."""
     from mx_rcnn_amd.ops import ext_available
@@ -473,6 +473,10 @@ def test_loss_cpu_twins_match_tensor_path(which, monkeypatch):
         x = torch.randn(2, 18, 7, 9, generator=g) * 3
         lab = torch.randint(-1, 2, (2, 9 * 7 * 9), generator=g).to(torch.int32)
         fn = lambda t: L.rpn_softmax_ce(t, lab, grad_scale=1.0)  # noqa: E731
+    elif which == 'row_ce':
+        x = torch.randn(300, 21, generator=g) * 4
+        lab = torch.randint(-1, 21, (300,), generator=g).to(torch.int32)
+        fn = lambda t: L.softmax_ce(t, lab, 'batch', grad_scale=1.0)[0]  # noqa: E731
     else:
         x = torch.randn(64, 84, generator=g)
         tgt = torch.randn(64, 84, generator=g)

@@ -911,6 +911,28 @@ std::vector<Tensor> row_softmax_ce_cpu(const Tensor& logits_in, const Tensor& la
   return {grad, prob, at::full({1}, (float)(loss / norm), logits.options())};
 }
 
+// ---- CPU twin of the frozen BN+ReLU forward (bn_act.hip): keeps x's memory format
+// (NCHW or channels_last), returns fp32.
+Tensor bn_relu_fwd_cpu(const Tensor& x_in, const Tensor& gamma, const Tensor& beta, const Tensor& mean,
+                       const Tensor& var, double eps, bool fix_gamma, bool relu) {
+  TORCH_CHECK(!x_in.is_cuda() && x_in.dim() == 4, "x must be a CPU (N, C, H, W) tensor");
+  const bool cl = !x_in.is_contiguous() && x_in.is_contiguous(at::MemoryFormat::ChannelsLast);
+  const auto fmt = cl ? at::MemoryFormat::ChannelsLast : at::MemoryFormat::Contiguous;
+  const Tensor x = x_in.to(at::kFloat).contiguous(fmt);
+  const int64_t C = x.size(1), inner = cl ? 1 : x.size(2) * x.size(3);
+  TORCH_CHECK(gamma.numel() == C && beta.numel() == C && mean.numel() == C && var.numel() == C, "per-channel params");
+  const Tensor g = fix_gamma ? at::ones({C}, x.options()) : gamma.to(at::kFloat).contiguous();
+  const Tensor scale = (g * at::rsqrt(var.to(at::kFloat) + eps)).contiguous();
+  const Tensor shift = (beta.to(at::kFloat) - mean.to(at::kFloat) * scale).contiguous();
+  Tensor y = at::empty_like(x);
+  const float* xp = x.data_ptr<float>();
+  float* yp = y.data_ptr<float>();
+  at::parallel_for(0, x.numel(), 1 << 15, [&](int64_t n0, int64_t n1) {
+    mxr::host::bn_frozen_range(xp, yp, n0, n1, C, inner, scale.data_ptr<float>(), shift.data_ptr<float>(), relu);
+  });
+  return y;
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mx_rcnn_amd gfx950 kernels";
   m.def("proposal_decode", &proposal_decode);
@@ -925,6 +947,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("smooth_l1_cpu", &smooth_l1_cpu);
   m.def("sgd_momentum_cpu", &sgd_momentum_cpu);
   m.def("row_softmax_ce_cpu", &row_softmax_ce_cpu);
+  m.def("bn_relu_fwd_cpu", &bn_relu_fwd_cpu);
   m.def("iou_max", &iou_max);
   m.def("anchor_sample", &anchor_sample);
   m.def("proposal_sample", &proposal_sample);

@@ -1,4 +1,4 @@
-// Host (CPU) twins of the SGD-momentum update, the RPN / R-CNN softmax-CE and smooth-L1
+// Host (CPU) twins of the frozen BN+ReLU forward, the SGD-momentum update, the RPN / R-CNN softmax-CE and smooth-L1
 // losses, the RPN anchor-target assignment, the proposal-target IoU pass, the
 // proposal decode, the proposal NMS and the RoI max-pool forward /
 // backward, written against raw pointers so the same code is linked into the extension
@@ -342,6 +342,19 @@ inline double row_softmax_ce_range(const float* logits, const int32_t* label, in
     if (valid) loss -= std::log((double)std::max(p[l], 1e-14f));
   }
   return loss;
+}
+
+// Frozen BatchNorm (+ReLU) forward, use_global_stats semantics (SURVEY 2.9 BatchNorm row:
+// gamma * (x - mean) / sqrt(var + eps) + beta, gamma := 1 with fix_gamma) folded to a
+// per-channel scale / shift, elements [n0, n1) of a tensor whose channel of element i is
+// (i / inner) % C (inner = H*W for NCHW, 1 for channels_last).
+inline void bn_frozen_range(const float* x, float* y, int64_t n0, int64_t n1, int64_t C, int64_t inner,
+                            const float* scale, const float* shift, bool relu) {
+  for (int64_t i = n0; i < n1; ++i) {
+    const int64_t c = (i / inner) % C;
+    const float v = x[i] * scale[c] + shift[c];
+    y[i] = relu ? std::max(v, 0.f) : v;
+  }
 }
 
 }  // namespace host

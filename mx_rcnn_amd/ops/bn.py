@@ -7,7 +7,7 @@ parameters of global-stats BN trainable); the running statistics are constants.
 import torch
 
 from . import grad_sink
-from ._ext import need_ext
+from ._ext import ext_available, need_ext
 
 
 class _FrozenBnRelu(torch.autograd.Function):
@@ -22,13 +22,16 @@ class _FrozenBnRelu(torch.autograd.Function):
             ctx.save_for_backward(xc, gamma, beta, mean, var)
             ctx.params = (gamma if gamma.is_leaf else None, beta if beta.is_leaf else None)
             return y
+        ctx.save_for_backward(x, gamma, beta, mean, var)
+        if ext_available() and x.dim() == 4:  # C++ twin (host_ops.h): one fused pass
+            return need_ext().bn_relu_fwd_cpu(x.detach(), gamma.detach(), beta.detach(), mean, var, float(eps),
+                                              bool(fix_gamma), bool(relu)).to(x.dtype)
         g = torch.ones_like(gamma) if fix_gamma else gamma
         s = g.float() * torch.rsqrt(var.float() + eps)
         t = beta.float() - mean.float() * s
         y = x.float() * s[None, :, None, None] + t[None, :, None, None]
         if relu:
             y = torch.relu(y)
-        ctx.save_for_backward(x, gamma, beta, mean, var)
         return y.to(x.dtype)
 
     @staticmethod

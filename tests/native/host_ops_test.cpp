@@ -17,6 +17,7 @@
 //   * losses: softmax-CE gradient pairs cancel, ignored labels carry no gradient, large logits
 //     stay finite; smooth-L1 gradient bounded by the outside weight and masked by inside;
 //   * head softmax-CE: row ranges on threads equal one pass, rows sum to 1, gradients to 0;
+//   * frozen BN+ReLU: NCHW and channels_last channel indexing, threaded ranges;
 //   * SGD-momentum: element ranges on threads equal one pass and the hand-written update;
 //   * RoI pool ranges run concurrently on std::threads equal the serial result (the
 //     at::parallel_for contract; -fsanitize=thread checks the disjoint-write claim).
@@ -440,6 +441,32 @@ void test_row_softmax_ce() {
   }
 }
 
+void test_bn_frozen() {
+  Rng g(47);
+  const int64_t N = 2, C = 13, HW = 37, n = N * C * HW;
+  std::vector<float> x(n), y1(n), y2(n), sc(C), sh(C);
+  for (auto& v : x) v = (float)(g.uni() * 8 - 4);
+  for (int64_t c = 0; c < C; ++c) {
+    sc[c] = (float)(g.uni() * 2 - 1);
+    sh[c] = (float)(g.uni() - 0.5);
+  }
+  for (int64_t inner : {HW, (int64_t)1}) {  // NCHW, channels_last
+    mxr::host::bn_frozen_range(x.data(), y1.data(), 0, n, C, inner, sc.data(), sh.data(), true);
+    std::vector<std::thread> th;
+    for (int t = 0; t < 3; ++t)
+      th.emplace_back([&, t] {
+        mxr::host::bn_frozen_range(x.data(), y2.data(), n * t / 3, n * (t + 1) / 3, C, inner, sc.data(), sh.data(),
+                                   true);
+      });
+    for (auto& x_ : th) x_.join();
+    CHECK(y1 == y2, "threaded BN differs");
+    for (int64_t i = 0; i < n; ++i) {
+      const int64_t c = (i / inner) % C;
+      CHECK(y1[i] == std::max(x[i] * sc[c] + sh[c], 0.f), "BN element %ld", (long)i);
+    }
+  }
+}
+
 }  // namespace
 
 int main() {
@@ -452,6 +479,7 @@ int main() {
   test_losses();
   test_sgd();
   test_row_softmax_ce();
+  test_bn_frozen();
   if (g_fail) {
     std::fprintf(stderr, "%d check(s) failed\n", g_fail);
     return 1;

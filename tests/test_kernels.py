@@ -516,3 +516,28 @@ def test_sgd_cpu_twin_matches_tensor_path(clip, monkeypatch):
         res.append((w, m, wb))
     for a, b in zip(*res):
         assert torch.allclose(a.float(), b.float(), rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize('channels_last,fix_gamma,relu', [(False, False, True), (True, True, False)])
+def test_bn_relu_cpu_twin_matches_tensor_path(channels_last, fix_gamma, relu, monkeypatch):
+    from mx_rcnn_amd.ops import ext_available
+    from mx_rcnn_amd.ops import bn as BN
+    if not ext_available():
+        pytest.skip('extension not built')
+    g = torch.Generator().manual_seed(43)
+    x = torch.randn(2, 24, 9, 11, generator=g)
+    if channels_last:
+        x = x.contiguous(memory_format=torch.channels_last)
+    gamma, beta, mean = (torch.randn(24, generator=g) for _ in range(3))
+    var = torch.rand(24, generator=g) + 0.1
+    outs = []
+    for use_ext in (True, False):
+        if not use_ext:
+            monkeypatch.setattr(BN, 'ext_available', lambda: False)
+        xi, gi, bi = x.clone().requires_grad_(), gamma.clone().requires_grad_(), beta.clone().requires_grad_()
+        y = BN._FrozenBnRelu.apply(xi, gi, bi, mean, var, 2e-5, fix_gamma, relu)
+        (y * torch.linspace(-1, 1, y.numel()).reshape(y.shape)).sum().backward()
+        outs.append((y.detach(), xi.grad, bi.grad))
+        assert y.is_contiguous(memory_format=torch.channels_last) == channels_last
+    for a, b in zip(*outs):
+        assert torch.allclose(a, b, rtol=1e-5, atol=1e-6)

@@ -8,10 +8,12 @@ full step timed: trunk+RPN fwd/bwd, anchor target, proposal (sort + NMS 12000->6
 proposal target (128 RoIs), RoIPool, stage-4 head, losses, bucketed RCCL all-reduce (N>1),
 fused SGD update.  Weak scaling (fixed per-GPU work).
 
-    python bench.py --gpus N --steps K --warmup W
+    python bench.py --gpus N --steps K --warmup W      # spawns N ranks itself (one per GPU)
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N ...
 
 Rank 0 prints ONE JSON line.  Reference publishes no numbers, so vs_baseline=null.
+With N>1 the line also carries the measured per-bucket all-reduce time (``config.allreduce``:
+each gradient bucket's collective timed in isolation with HIP events after the timed region).
 """
 import argparse
 import json
@@ -19,9 +21,33 @@ import os
 import sys
 import time
 
-import torch
-
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=200)
+    ap.add_argument('--warmup', type=int, default=10)
+    ap.add_argument('--network', default='resnet101')
+    ap.add_argument('--num-classes', type=int, default=81)
+    ap.add_argument('--image', default='800x1333')
+    ap.add_argument('--ims-per-gpu', type=int, default=1)
+    ap.add_argument('--mode', default='graph', choices=['graph', 'eager'])
+    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--bucket-mb', type=float, default=25)
+    ap.add_argument('--grad-comm', default='fp32', choices=['fp32', 'bf16'],
+                    help='all-reduce wire dtype of the gradient buckets (fp32 = the reference kvstore sum)')
+    ap.add_argument('--pool', type=int, default=4, help='distinct synthetic batches cycled')
+    return ap.parse_args(argv)
+
+
+if __name__ == '__main__':
+    # before anything touches the GPU: --gpus N without a launcher -> N fresh rank processes
+    from mx_rcnn_amd.parallel.spawn import maybe_spawn
+    maybe_spawn(parse_args().gpus, os.path.abspath(__file__), sys.argv[1:])
+
+import torch  # noqa: E402
 
 from mx_rcnn_amd.config import snapshot  # noqa: E402
 from mx_rcnn_amd.models import FasterRCNN  # noqa: E402
@@ -50,21 +76,10 @@ def synthetic_batch(n_img, h, w, num_classes, device, gen, max_gt=20):
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
-    ap.add_argument('--warmup', type=int, default=5)
-    ap.add_argument('--network', default='resnet101')
-    ap.add_argument('--num-classes', type=int, default=81)
-    ap.add_argument('--image', default='800x1333')
-    ap.add_argument('--ims-per-gpu', type=int, default=1)
-    ap.add_argument('--mode', default='graph', choices=['graph', 'eager'])
-    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
-    ap.add_argument('--bucket-mb', type=float, default=25)
-    ap.add_argument('--pool', type=int, default=4, help='distinct synthetic batches cycled')
-    args = ap.parse_args()
-
+    args = parse_args()
     rank, world, local_rank, device = pdist.init_distributed()
+    if world != args.gpus:
+        raise SystemExit('--gpus %d but %d ranks were launched' % (args.gpus, world))
     h, w = [int(v) for v in args.image.lower().split('x')]
     cfg = snapshot()
     # end2end config mutation (train_end2end.py:25-32)
@@ -82,7 +97,8 @@ def main():
     fixed = ['conv0', 'stage1', 'stage2', 'bn_data', 'bn0'] if args.network.startswith('resnet') else ['conv1', 'conv2']
     dtype = torch.bfloat16 if (args.dtype == 'bf16' and device.type == 'cuda') else torch.float32
     trainer = Trainer(model, 'e2e', fixed_param_prefix=fixed, lr=0.001, momentum=0.9, wd=0.0005, clip_gradient=1.0,
-                      rescale_grad=1.0, compute_dtype=dtype, device=device, bucket_mb=args.bucket_mb)
+                      rescale_grad=1.0, compute_dtype=dtype, device=device, bucket_mb=args.bucket_mb,
+                      grad_comm_dtype=torch.float32 if args.grad_comm == 'fp32' else torch.bfloat16)
 
     mode = args.mode if device.type == 'cuda' else 'eager'
     step_fn = None
@@ -123,6 +139,8 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed = pdist.all_reduce_max(elapsed, device)
     loss1 = float(out['objective'].float().item())
+    # after the timed region: each gradient bucket's collective in isolation (HIP events)
+    comm = trainer.reducer.measure_collectives() if world > 1 else None
     ms = elapsed / max(args.steps, 1) * 1e3
     imgs = args.ims_per_gpu * world * args.steps
     value = imgs / elapsed
@@ -138,7 +156,8 @@ def main():
                           'ims_per_gpu': args.ims_per_gpu, 'parallelism': 'dp%d' % world,
                           'rpn_pre_post_nms': [cfg.TRAIN.RPN_PRE_NMS_TOP_N, cfg.TRAIN.RPN_POST_NMS_TOP_N],
                           'rois_per_image': cfg.TRAIN.BATCH_SIZE, 'exec': mode,
-                          'objective_first_last': [round(loss0, 4), round(loss1, 4)]}}
+                          'objective_first_last': [round(loss0, 4), round(loss1, 4)],
+                          'backend': pdist.backend_name(), 'allreduce': comm}}
         print(json.dumps(rec), flush=True)
     pdist.destroy()
 

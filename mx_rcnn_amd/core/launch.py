@@ -3,10 +3,11 @@ train_widerface*.py, test.py, tools/*): process-group bootstrap, roidb construct
 .lst, synthetic), model construction + pretrained loading + new-layer initialisation
 (`train_end2end.py:56-78`), optimizer parameters (`train_end2end.py:98-105`), frozen prefixes.
 
-Multi-GPU: launch one process per GPU with ``torchrun --nproc-per-node N`` (or
-``python -m torch.distributed.run``); ``--gpus`` is accepted for command-line parity but the
-device of each rank is its LOCAL_RANK.  Gradients are summed across ranks like the
-reference's kvstore (rescale_grad 1.0).
+Multi-GPU: ``--gpus 0,1,2,3`` (the reference's device list, `train_end2end.py:168`) or
+``--gpus 4`` starts one process per GPU from the single command (parallel/spawn.py: fresh
+child processes, torchrun's environment contract); under ``torchrun --nproc-per-node N`` the
+launcher's ranks are used as they are.  The device of each rank is its LOCAL_RANK.  Gradients
+are summed across ranks like the reference's kvstore (rescale_grad 1.0).
 """
 import logging
 import os
@@ -41,6 +42,15 @@ def add_common_args(parser):
 
 
 def init_runtime(args):
+    """Spawn the per-GPU ranks if ``--gpus`` names more than one device (the parent exits with
+    the job's code and never touches the GPU), then bootstrap this rank."""
+    from ..parallel.spawn import maybe_spawn, parse_gpus
+    import sys
+    spec = getattr(args, 'gpus', None)
+    if spec is None:
+        spec = getattr(args, 'gpu_ids', None)
+    if spec is not None:
+        maybe_spawn(parse_gpus(spec), sys.argv[0], sys.argv[1:])
     rank, world, local_rank, device = pdist.init_distributed()
     setup_logging(rank)
     if getattr(args, 'cfg', None):

@@ -17,6 +17,7 @@ inherited MXNet ``BaseModule.fit``) on top of :class:`Trainer`.
 import logging
 import os
 import time
+import zlib
 
 import numpy as np
 import torch
@@ -56,6 +57,7 @@ class MutableModule(object):
         self._outputs = None
         self._batch = None
         self._monitor = None
+        self._hb = None  # heartbeat of the running fit(), paused across captures
 
     # ------------------------------------------------------------------ properties
     @property
@@ -186,7 +188,7 @@ class MutableModule(object):
         t = self.trainer
         t.reducer.finish()
         t.update_lr()
-        t.store.sgd_step(t.lr_t, t.momentum, t.wd, t.rescale, t.clip)
+        t.store.sgd_step(t.lr_t, t.momentum, t.wd, t.rescale, t.clip, grad_for=t.reducer.grad_for)
 
     def step(self, data_batch):
         """forward + backward + update fused (graph-replayed per input shape when enabled).
@@ -200,11 +202,48 @@ class MutableModule(object):
         key = tuple((k, tuple(v.shape)) for k, v in sorted(data_batch.items()) if torch.is_tensor(v))
         g = self._graphs.get(key)
         if g is None:
-            g = GraphedStep(self.trainer, data_batch)
-            self._graphs[key] = g
-            logging.info('captured hipGraph for input shape %s (%d cached)', key, len(self._graphs))
-        self._outputs = g(data_batch)
+            g = self._capture(key, data_batch)
+        if g == 'eager':
+            self._outputs = self.trainer.step(data_batch)
+        else:
+            self._outputs = g(data_batch)
         return self._outputs
+
+    def _capture(self, key, data_batch):
+        """Capture a hipGraph for a new input shape.  Under data parallelism every rank reaches
+        this on the same step (the loaders pad every rank's batch to the global step's shape,
+        data/loader.py), and the ranks agree on the outcome: if capture failed anywhere, all
+        ranks run this shape eagerly (the captured step contains collectives, so a mixed
+        graphed/eager step would mismatch them)."""
+        ok, g = 1.0, None
+        if self._hb is not None:
+            self._hb.pause()
+        try:
+            g = GraphedStep(self.trainer, data_batch)
+        except Exception as e:  # reported, never silent
+            ok = 0.0
+            logging.warning('hipGraph capture failed for %s (%s: %s)', key, type(e).__name__, str(e)[:300])
+            torch.cuda.synchronize()
+        finally:
+            if self._hb is not None:
+                self._hb.resume()
+        if pdist.is_distributed():
+            if pdist.get_world_size() > 1:
+                h = torch.tensor([float(zlib.crc32(repr(key).encode()))], dtype=torch.float64, device=self.context)
+                lo, hi = h.clone(), h.clone()
+                torch.distributed.all_reduce(lo, op=torch.distributed.ReduceOp.MIN)
+                torch.distributed.all_reduce(hi, op=torch.distributed.ReduceOp.MAX)
+                if float(lo.item()) != float(hi.item()):
+                    raise RuntimeError('ranks reached different input shapes at a capture point (%s); the data '
+                                       'loaders must pad every rank to the global step shape' % (key,))
+            ok = -pdist.all_reduce_max(-ok, self.context)
+        if ok < 1.0:
+            g = 'eager'
+            logging.warning('running input shape %s eagerly on every rank', key)
+        else:
+            logging.info('captured hipGraph for input shape %s (%d cached)', key, len(self._graphs) + 1)
+        self._graphs[key] = g
+        return g
 
     def get_outputs(self, merge_multi_context=True):
         return self._outputs
@@ -284,13 +323,30 @@ class MutableModule(object):
             ([batch_end_callback] if batch_end_callback else [])
         cbs_e = epoch_end_callback if isinstance(epoch_end_callback, (list, tuple)) else \
             ([epoch_end_callback] if epoch_end_callback else [])
+        hb = watchdog.from_env()
+        self._hb = hb
+        try:
+            self._fit_loop(train_data, eval_metric, cbs_b, cbs_e, begin_epoch, num_epoch, max_steps, check_every,
+                           states_prefix, rank, hb)
+        finally:
+            self._hb = None
+            if hb is not None:
+                hb.stop()
+            if hasattr(train_data, 'close'):
+                train_data.close()
+
+    def _fit_loop(self, train_data, eval_metric, cbs_b, cbs_e, begin_epoch, num_epoch, max_steps, check_every,
+                  states_prefix, rank, hb):
+        import contextlib
         steps = 0
         fault_step, fault_kind = parse_fault(os.environ.get('MXR_FAULT_INJECT'))
-        hb = watchdog.from_env()
+        quiet = hb.paused if hb is not None else contextlib.nullcontext
         for epoch in range(begin_epoch, num_epoch):
             tic = time.time()
             if eval_metric is not None:
                 eval_metric.reset()
+            if hb is not None:
+                hb.beat(steps)
             for nbatch, batch in enumerate(train_data):
                 if self._monitor is not None:
                     self._monitor.tic()
@@ -313,24 +369,22 @@ class MutableModule(object):
                 steps += 1
                 if max_steps is not None and steps >= max_steps:
                     break
-            self.trainer.check_finite(steps)
-            if eval_metric is not None:
-                for name, val in eval_metric.get_name_value():
-                    logging.info('Epoch[%d] Train-%s=%f', epoch, name, val)
-            logging.info('Epoch[%d] Time cost=%.3f', epoch, time.time() - tic)
-            arg, aux = self.get_params()
-            if rank == 0:
-                for cb in cbs_e:
-                    cb(epoch, self.symbol, arg, aux)
-                if states_prefix:
-                    self.save_optimizer_states('%s-%04d.states' % (states_prefix, epoch + 1))
-            if max_steps is not None and steps >= max_steps:
-                break
-            train_data.reset()
-        if hb is not None:
-            hb.stop()
-        if hasattr(train_data, 'close'):
-            train_data.close()
+            # epoch-end host phases (gather, checkpoint, reshuffle) are known to be long
+            with quiet():
+                self.trainer.check_finite(steps)
+                if eval_metric is not None:
+                    for name, val in eval_metric.get_name_value():
+                        logging.info('Epoch[%d] Train-%s=%f', epoch, name, val)
+                logging.info('Epoch[%d] Time cost=%.3f', epoch, time.time() - tic)
+                arg, aux = self.get_params()
+                if rank == 0:
+                    for cb in cbs_e:
+                        cb(epoch, self.symbol, arg, aux)
+                    if states_prefix:
+                        self.save_optimizer_states('%s-%04d.states' % (states_prefix, epoch + 1))
+                if max_steps is not None and steps >= max_steps:
+                    break
+                train_data.reset()
 
 
 def parse_fault(spec):

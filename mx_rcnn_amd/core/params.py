@@ -194,11 +194,12 @@ class FlatParamStore:
     def grad_buffers(self):
         return [g.grad for g in self.groups]
 
-    def sgd_step(self, lr, momentum=0.9, wd=0.0005, rescale=1.0, clip=-1.0):
-        """``lr``: 1-element fp32 device tensor."""
+    def sgd_step(self, lr, momentum=0.9, wd=0.0005, rescale=1.0, clip=-1.0, grad_for=None):
+        """``lr``: 1-element fp32 device tensor.  ``grad_for(group)`` picks the gradient source
+        (the reducer's fp32 all-reduce buffer under data parallelism; default ``group.grad``)."""
         for g in self.groups:
-            sgd_momentum_(g.master, g.mom, g.grad, lr, momentum, wd if g.decay else 0.0, rescale, clip,
-                          g.shadow)
+            grad = grad_for(g) if grad_for is not None else g.grad
+            sgd_momentum_(g.master, g.mom, grad, lr, momentum, wd if g.decay else 0.0, rescale, clip, g.shadow)
         self.refresh_dgrad_cache()
 
     def master_param(self, name):

@@ -17,7 +17,7 @@ from .params import FlatParamStore
 class Trainer:
     def __init__(self, model, mode='e2e', fixed_param_prefix=None, lr=0.001, momentum=0.9, wd=0.0005,
                  clip_gradient=1.0, rescale_grad=1.0, lr_scheduler=None, compute_dtype=None, device=None,
-                 bucket_mb=25, average_grads=False, channels_last=None):
+                 bucket_mb=25, average_grads=False, channels_last=None, grad_comm_dtype=None):
         dev = torch.device(device) if device is not None else next(model.parameters()).device
         if compute_dtype is None:
             compute_dtype = torch.bfloat16 if dev.type == 'cuda' else torch.float32
@@ -28,7 +28,8 @@ class Trainer:
         self.mode = mode
         self.store = FlatParamStore(self.model, fixed_param_prefix, compute_dtype, dev, channels_last,
                                    mode=mode if mode in ('rpn', 'rcnn') else None)
-        self.reducer = BucketReducer(self.store, bucket_mb=bucket_mb, average=average_grads)
+        self.reducer = BucketReducer(self.store, bucket_mb=bucket_mb, average=average_grads,
+                                     comm_dtype=grad_comm_dtype)
         if self.reducer.dp:
             self.store.broadcast_(0)  # identical starting weights on every rank
         self.momentum, self.wd, self.clip, self.rescale = momentum, wd, clip_gradient, rescale_grad
@@ -89,7 +90,8 @@ class Trainer:
             if self.reducer.sgd_applied:
                 self.store.refresh_dgrad_cache()
             else:
-                self.store.sgd_step(self.lr_t, self.momentum, self.wd, self.rescale, self.clip)
+                self.store.sgd_step(self.lr_t, self.momentum, self.wd, self.rescale, self.clip,
+                                    grad_for=self.reducer.grad_for)
         # Return detached outputs: a caller holding the loss would otherwise keep this step's
         # autograd graph (and its AccumulateGrad nodes, bound to this step's stream) alive, and a
         # later hipGraph capture on a side stream then syncs against that stream and dies in
@@ -113,6 +115,37 @@ class Trainer:
         if self.fault is not None:
             self.fault.fill_(1.0)
 
+    # ------------------------------------------------------------------ state snapshot
+    @torch.no_grad()
+    def snapshot_state(self):
+        """Copies of everything a step mutates: fp32 masters, momentum, low-precision shadows,
+        model buffers (train-mode BN moving statistics), the non-finite counter and the RNG
+        streams.  Used to make hipGraph warm-up runs side-effect free."""
+        st = {'groups': [(g.master.clone(), g.mom.clone(), None if g.shadow is None else g.shadow.clone())
+                         for g in self.store.groups],
+              'buffers': [b.detach().clone() for b in self.model.buffers()],
+              'nonfinite': self.nonfinite.clone(),
+              'rng_cpu': torch.get_rng_state()}
+        if self.device.type == 'cuda':
+            st['rng_cuda'] = torch.cuda.get_rng_state(self.device)
+        return st
+
+    @torch.no_grad()
+    def restore_state(self, st, rng=True):
+        for g, (m, mo, sh) in zip(self.store.groups, st['groups']):
+            g.master.copy_(m)
+            g.mom.copy_(mo)
+            if sh is not None:
+                g.shadow.copy_(sh)
+        for b, v in zip(self.model.buffers(), st['buffers']):
+            b.copy_(v)
+        self.nonfinite.copy_(st['nonfinite'])
+        self.store.refresh_dgrad_cache()
+        if rng:
+            torch.set_rng_state(st['rng_cpu'])
+            if 'rng_cuda' in st:
+                torch.cuda.set_rng_state(st['rng_cuda'], self.device)
+
     def update_lr(self):
         self.num_update += 1
         if self.lr_scheduler is not None:
@@ -132,6 +165,12 @@ class GraphedStep:
     Static input buffers are filled with copies of each new batch (D2D), the LR lives in a
     device tensor, RNG draws use PyTorch's graph-safe Philox offsets.  Falls back to eager
     if capture fails (reported, not silent).
+
+    The warm-up runs (which allocate the kernels' workspaces and settle the allocator before
+    capture) execute real steps on the example batch; every piece of state they touch --
+    weights, momentum, shadows, BN moving statistics, the non-finite counter, the RNG -- is
+    snapshotted first and restored before capture, so capturing a new shape never applies
+    unscheduled updates (graphed and eager training give the same weights).
     """
 
     def __init__(self, trainer, example_batch, warmup=3):
@@ -139,6 +178,7 @@ class GraphedStep:
         trainer.model.train()
         self.static = trainer.prepare_batch(example_batch)
         self.static = {k: (v.clone() if torch.is_tensor(v) else v) for k, v in self.static.items()}
+        saved = trainer.snapshot_state() if warmup else None
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -146,6 +186,10 @@ class GraphedStep:
                 trainer.step_body(self.static)
         torch.cuda.current_stream().wait_stream(s)
         torch.cuda.synchronize()
+        if saved is not None:
+            trainer.restore_state(saved)
+            del saved
+            torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.out = trainer.step_body(self.static)

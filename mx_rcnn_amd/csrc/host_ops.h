@@ -182,7 +182,9 @@ inline float iou1(const float* a, const float* g) {
   return inter / (aa + ga - inter);
 }
 
-// gt: ng rows of stride gt_stride (x1, y1, x2, y2, ...); gmax: ng floats (0 when no inside anchor)
+// gt: ng rows of stride gt_stride (x1, y1, x2, y2, ...); gmax: ng floats, the best IoU of each gt over
+// the inside anchors (-INFINITY when no anchor is inside: then no anchor ever reads it).  A gt whose best
+// IoU is 0 marks every inside zero-IoU anchor as its foreground, as in the reference.
 inline void anchor_gt_max(const float* base, int64_t A, int64_t H, int64_t W, float stride, float im_h, float im_w,
                           int border, const float* gt, int64_t gt_stride, int64_t ng, float* gmax) {
   for (int64_t g = 0; g < ng; ++g) gmax[g] = -INFINITY;

@@ -9,10 +9,17 @@ MI355X-first differences from the reference's single-threaded MXNet DataIter:
   (``prefetch`` batches in flight) into pinned host memory; the trainer copies them with
   non_blocking H2D transfers.
 * Data parallel: one process per GPU; every rank draws the SAME shuffled order (seeded per
-  epoch) and takes its strided shard of the batches, so aspect-grouped pairs stay together.
-* ``pad_shape`` pads every image to a fixed (H, W) (e.g. the reference's max shape) so the
-  step has static shapes and can replay a hipGraph; otherwise images are padded to the batch
-  max like the reference's ``tensor_vstack``.
+  epoch) and cuts the same GLOBAL batches (``batch_size`` x world images); rank r takes its
+  slice, equal by default or proportional to ``work_load_list`` (MXNet's
+  ``_split_input_slice``, reference `rcnn/loader.py:114-120`).
+* Shapes: like the reference's AnchorLoader, which pads every device's image to the common
+  shape of the step (`rcnn/loader.py:283-286`), every rank pads its batch to the max resized
+  shape over the WHOLE global batch -- computed from roidb metadata, identical on every rank
+  with no communication -- and the gt count to the global max.  Both are rounded up to
+  buckets (``shape_bucket`` px, power-of-two gt counts) so a dataset produces few distinct
+  shapes and each gets one hipGraph; all ranks capture on the same step.  ``pad_shape`` /
+  ``max_gt`` fix them outright.  The per-image scale choice is drawn from a per-(epoch,
+  global batch) seed, so every rank knows every image's resized size.
 * Multiple images per device are supported (the reference asserts one).
 """
 import queue
@@ -101,6 +108,45 @@ def aspect_grouped_order(roidb, rng):
     return inds
 
 
+def split_input_slice(batch_size, work_load_list):
+    """Split ``batch_size`` items over devices proportionally to ``work_load_list`` ->
+    list of (start, stop); every slice must be non-empty (MXNet ``_split_input_slice``)."""
+    total = float(sum(work_load_list))
+    counts = [int(round(w * batch_size / total)) for w in work_load_list]
+    diff = batch_size - sum(counts)
+    counts[-1] += diff
+    if any(c <= 0 for c in counts):
+        raise ValueError('work_load_list %s leaves a device without data at batch size %d'
+                         % (list(work_load_list), batch_size))
+    out, start = [], 0
+    for c in counts:
+        out.append((start, start + c))
+        start += c
+    return out
+
+
+def _parse_work_load(wl, world):
+    if wl is None:
+        return None
+    if isinstance(wl, str):
+        wl = [float(v) for v in wl.strip('[]() ').split(',') if v.strip()]
+    wl = [float(v) for v in wl]
+    if len(wl) != world:
+        raise ValueError('work_load_list has %d entries for %d ranks' % (len(wl), world))
+    return wl
+
+
+def _bucket_up(v, q):
+    return int(-(-v // q) * q) if q and q > 1 else int(v)
+
+
+def _pow2_at_least(n, lo=8):
+    p = lo
+    while p < n:
+        p *= 2
+    return p
+
+
 class _BaseLoader:
     def __init__(self, roidb, batch_size, shuffle, mode, ctx, work_load_list, rank, world_size, seed, prefetch,
                  workers):
@@ -109,7 +155,7 @@ class _BaseLoader:
         self.shuffle = shuffle
         self.mode = mode
         self.ctx = ctx
-        self.work_load_list = work_load_list
+        self.work_load_list = _parse_work_load(work_load_list, world_size)
         self.rank, self.world_size = rank, world_size
         self.seed = seed
         self.epoch = 0
@@ -142,15 +188,48 @@ class _BaseLoader:
             self._pf = None
 
     def _shard_batches(self):
-        nb = self.size // self.batch_size
-        all_b = [self.index[i * self.batch_size:(i + 1) * self.batch_size] for i in range(nb)]
-        if self.world_size > 1:
-            n = (len(all_b) // self.world_size) * self.world_size  # equal steps on every rank
-            all_b = all_b[self.rank:n:self.world_size]
-        return all_b
+        """This rank's slice of every global batch (equal steps on every rank); the global
+        batches themselves are kept for the shape plan."""
+        gb = self.batch_size * self.world_size
+        nb = self.size // gb
+        self._global = [self.index[i * gb:(i + 1) * gb] for i in range(nb)]
+        if self.work_load_list is not None and self.world_size > 1:
+            a, b = split_input_slice(gb, self.work_load_list)[self.rank]
+        else:
+            a, b = self.rank * self.batch_size, (self.rank + 1) * self.batch_size
+        self._slice = (a, b)
+        return [g[a:b] for g in self._global]
+
+    def plan_hw(self, i):
+        """(pad (H, W), this rank's scale indexes) for global batch ``i``: the max resized
+        shape over the global batch rounded up to ``shape_bucket`` (or ``pad_shape``)."""
+        sidx = self._scale_indexes(i)
+        a, b = self._slice
+        if getattr(self, 'pad_shape', None) is not None:
+            return tuple(self.pad_shape), sidx[a:b]
+        hs, ws = [], []
+        for j, si in zip(self._global[i], sidx):
+            h, w = _planned_hw(self.roidb[j], config.SCALES[si])
+            hs.append(h)
+            ws.append(w)
+        q = getattr(self, 'shape_bucket', 1)
+        return (_bucket_up(max(hs), q), _bucket_up(max(ws), q)), sidx[a:b]
+
+    def _scale_indexes(self, i):
+        """Per-image SCALES choice for global batch ``i`` (same on every rank)."""
+        n = len(self._global[i])
+        if len(config.SCALES) == 1:
+            return np.zeros(n, np.int64)
+        rng = np.random.RandomState((self.seed * 1000003 + self.epoch * 7919 + i) % (2 ** 31))
+        return rng.randint(0, len(config.SCALES), size=n)
 
     def __len__(self):
         return len(self._batches)
+
+    @property
+    def global_batch_size(self):
+        """Images per step over all ranks (the Speedometer's batch size)."""
+        return self.batch_size * self.world_size
 
     def iter_next(self):
         return self.cur < len(self._batches)
@@ -186,29 +265,46 @@ class AnchorLoader(_BaseLoader):
 
     def __init__(self, feat_sym, roidb, batch_size=1, shuffle=False, mode='train', ctx=None, work_load_list=None,
                  feat_stride=16, anchor_scales=(8, 16, 32), anchor_ratios=(0.5, 1, 2), allowed_border=0,
-                 need_mean=True, rank=0, world_size=1, seed=0, prefetch=2, workers=2, pad_shape=None, max_gt=None):
+                 need_mean=True, rank=0, world_size=1, seed=0, prefetch=2, workers=2, pad_shape=None, max_gt=None,
+                 shape_bucket=None):
         self.feat_sym = feat_sym
         self.feat_stride, self.anchor_scales, self.anchor_ratios = feat_stride, anchor_scales, anchor_ratios
         self.allowed_border, self.need_mean = allowed_border, need_mean
         self.pad_shape, self.max_gt = pad_shape, max_gt
+        # shape bucketing only pays when shapes are static per bucket (graph replay); with a single
+        # process and no bucket requested, pad to the batch max like the reference's tensor_vstack
+        self.shape_bucket = shape_bucket if shape_bucket is not None else (64 if world_size > 1 else 1)
         self.data_name = ['data', 'im_info']
         self.label_name = ['gt_boxes', 'n_gt']
         super().__init__(roidb, batch_size, shuffle, mode, ctx, work_load_list, rank, world_size, seed, prefetch,
                          workers)
 
+    def step_plan(self, i):
+        """(pad_hw, gt_slots, scale_indexes of this rank's images) for global batch ``i``; the
+        same (pad_hw, gt_slots) on every rank."""
+        hw, sidx = self.plan_hw(i)
+        glob = [self.roidb[j] for j in self._global[i]]
+        if self.max_gt is not None:
+            G = self.max_gt
+        else:
+            G = max(1, max(int((e['gt_classes'] != 0).sum()) for e in glob))
+            if self.shape_bucket > 1:
+                G = _pow2_at_least(G)
+        return hw, G, sidx
+
     def _make_batch(self, i):
         entries = [self.roidb[j] for j in self._batches[i]]
-        data, label = minibatch.get_minibatch(entries, 0, self.mode, need_mean=self.need_mean, has_rpn=True)
+        (ph, pw), G, sidx = self.step_plan(i)
+        data, label = minibatch.get_minibatch(entries, 0, self.mode, need_mean=self.need_mean, has_rpn=True,
+                                              scale_indexes=sidx)
         im = data['data']
-        if self.pad_shape is not None:
-            ph, pw = self.pad_shape
-            if im.shape[2] > ph or im.shape[3] > pw:
-                raise ValueError('image %s larger than pad_shape %s' % (im.shape[2:], self.pad_shape))
+        if im.shape[2] > ph or im.shape[3] > pw:
+            raise ValueError('image %s larger than the planned pad shape %s' % (im.shape[2:], (ph, pw)))
+        if im.shape[2] != ph or im.shape[3] != pw:
             padded = np.zeros((im.shape[0], 3, ph, pw), np.float32)
             padded[:, :, :im.shape[2], :im.shape[3]] = im
             im = padded
         gts = label.get('gt_boxes', [np.zeros((0, 5), np.float32)] * len(entries))
-        G = max(1, max(g.shape[0] for g in gts)) if self.max_gt is None else self.max_gt
         gt = np.full((len(entries), G, 5), -1.0, np.float32)
         n_gt = np.zeros((len(entries),), np.int32)
         for k, g in enumerate(gts):
@@ -241,9 +337,12 @@ class ROIIter(_BaseLoader):
     bbox_inside_weight, bbox_outside_weight; test: data, rois, im_info."""
 
     def __init__(self, roidb, batch_size=2, shuffle=False, mode='train', ctx=None, work_load_list=None,
-                 rank=0, world_size=1, seed=0, prefetch=2, workers=2, need_mean=True):
+                 rank=0, world_size=1, seed=0, prefetch=2, workers=2, need_mean=True, pad_shape=None,
+                 shape_bucket=None):
         self.num_classes = roidb[0]['gt_overlaps'].shape[1]
         self.need_mean = need_mean
+        self.pad_shape = pad_shape
+        self.shape_bucket = shape_bucket if shape_bucket is not None else (64 if world_size > 1 else 1)
         self.data_name = ['data', 'rois']
         self.label_name = ['label', 'bbox_target', 'bbox_inside_weight', 'bbox_outside_weight']
         super().__init__(roidb, batch_size, shuffle, mode, ctx, work_load_list, rank, world_size, seed, prefetch,
@@ -251,9 +350,17 @@ class ROIIter(_BaseLoader):
 
     def _make_batch(self, i):
         entries = [self.roidb[j] for j in self._batches[i]]
+        sidx = None
+        if self.mode == 'train':
+            (ph, pw), sidx = self.plan_hw(i)
         data, label = minibatch.get_minibatch(entries, self.num_classes, self.mode, need_mean=self.need_mean,
-                                              has_rpn=False)
-        out = {'data': _pin(np.ascontiguousarray(data['data'], dtype=np.float32))}
+                                              has_rpn=False, scale_indexes=sidx)
+        im = data['data']
+        if sidx is not None and (im.shape[2] != ph or im.shape[3] != pw):
+            padded = np.zeros((im.shape[0], 3, ph, pw), np.float32)
+            padded[:, :, :im.shape[2], :im.shape[3]] = im
+            im = padded
+        out = {'data': _pin(np.ascontiguousarray(im, dtype=np.float32))}
         if self.mode == 'train':
             out['rois'] = _pin(data['rois'].reshape(-1, 5).astype(np.float32))
             out['label'] = _pin(label['label'].reshape(-1).astype(np.int32))
@@ -273,6 +380,16 @@ class ROIIter(_BaseLoader):
     def provide_label(self):
         b = self.get_batch()
         return [(k, tuple(b[k].shape)) for k in self.label_name if k in b]
+
+
+def _planned_hw(entry, target_size):
+    """Resized (h, w) of a roidb entry at ``target_size`` (image_processing.resize rule)."""
+    from ..processing.image_processing import compute_scale
+    h, w = entry.get('height'), entry.get('width')
+    if h is None or w is None:
+        h, w = minibatch.load_image(entry).shape[:2]
+    s = compute_scale((h, w), target_size, config.MAX_SIZE)
+    return int(round(h * s)), int(round(w * s))
 
 
 def tensor_vstack_batches(batches, key, pad=0):

@@ -59,10 +59,12 @@ def sample_rois(roidb, fg_rois_per_image, rois_per_image, num_classes):
     return rois, labels, bbox_targets, bbox_inside, overlaps
 
 
-def get_minibatch(roidb, num_classes, mode='test', need_mean=True, has_rpn=None):
-    """``has_rpn`` overrides config[TRAIN|TEST].HAS_RPN (thread-safe use from loader workers)."""
+def get_minibatch(roidb, num_classes, mode='test', need_mean=True, has_rpn=None, scale_indexes=None):
+    """``has_rpn`` overrides config[TRAIN|TEST].HAS_RPN (thread-safe use from loader workers);
+    ``scale_indexes`` fixes the per-image SCALES choice (the loaders plan it per global batch)."""
     num_images = len(roidb)
-    scale_idx = npr.randint(0, high=len(config.SCALES), size=num_images)
+    scale_idx = npr.randint(0, high=len(config.SCALES), size=num_images) if scale_indexes is None \
+        else np.asarray(scale_indexes)
     im_array, im_scales = get_image_array(roidb, config.SCALES, scale_idx, need_mean=need_mean)
     cfg_key = 'TRAIN' if mode == 'train' else 'TEST'
     if (config[cfg_key].HAS_RPN if has_rpn is None else has_rpn):

@@ -40,6 +40,11 @@ def init_distributed(backend=None, timeout_s=600):
     return rank, world, local_rank, device
 
 
+def backend_name():
+    """'nccl' (RCCL on ROCm), 'gloo', or None when not distributed."""
+    return dist.get_backend() if is_distributed() else None
+
+
 def barrier():
     if is_distributed():
         if dist.get_backend() == 'nccl':

@@ -9,12 +9,20 @@ backward pass.  ``finish()`` makes the compute stream wait on every outstanding 
 before the optimizer touches the buffers -- no host blocking.
 
 Semantics: SUM across ranks (MXNet kvstore 'device', rescale_grad=1: `train_end2end.py:104`);
-``average=True`` switches to mean.  Bucket sizing: xGMI is point-to-point, a ring uses one
-link per hop, so messages must stay large enough to run at link bandwidth (a 25 MB ring
-all-reduce over 8 GPUs is bandwidth-, not latency-bound), but small enough that the first
-buckets are reduced while most of the backward is still running: the default 25 MB cuts
-ResNet-101's ~90 MB of bf16 gradients into 4 buckets, the last of which is the only exposed one;
-VGG16's fc6 (205 MB bf16) still gets a bucket of its own.
+``average=True`` switches to mean.
+
+Precision: the kvstore sums fp32 gradients.  With bf16 compute the per-rank flat gradient
+buffers are bf16 (the MFMA wgrad kernels round once when they store), so by default
+(``comm_dtype=float32``) each ready bucket is widened into an fp32 communication buffer (one
+cast kernel on the compute stream), the ring sums fp32, and the optimizer reads the fp32 sum
+(:meth:`BucketReducer.grad_for`) -- no per-hop bf16 rounding, at twice the bytes on the wire.
+``comm_dtype=bfloat16`` keeps the half-size wire format (opt-in, measured by bench.py).
+
+Bucket sizing: xGMI is point-to-point, a ring uses one link per hop, so messages must stay
+large enough to run at link bandwidth (a 25 MB ring all-reduce over 8 GPUs is bandwidth-, not
+latency-bound), but small enough that the first buckets are reduced while most of the backward
+is still running.  Sizes are in bytes of the WIRE dtype: 25 MB cuts ResNet-101's ~180 MB of
+fp32 gradient traffic into 8 buckets, the last (capped at ``tail_mb``) is the only exposed one.
 """
 import os
 
@@ -26,10 +34,11 @@ from .dist import get_world_size, is_distributed
 
 
 class _Bucket:
-    __slots__ = ('group', 'buf', 'start', 'end', 'names', 'pending', 'work', 'updated')
+    __slots__ = ('group', 'buf', 'comm', 'start', 'end', 'names', 'pending', 'work', 'updated')
 
-    def __init__(self, group, start, end):
+    def __init__(self, group, start, end, comm=None):
         self.group, self.buf, self.start, self.end = group, group.grad, start, end
+        self.comm = comm  # fp32 flat buffer of the group (wire format), or None (reduce in place)
         self.names = []
         self.pending = 0
         self.work = None
@@ -50,11 +59,16 @@ class BucketReducer:
       last one is exposed after the backward).
     """
 
-    def __init__(self, store, bucket_mb=25, average=False, overlap=True, sgd_bucket_mb=8, tail_mb=4):
+    def __init__(self, store, bucket_mb=25, average=False, overlap=True, sgd_bucket_mb=8, tail_mb=4,
+                 comm_dtype=None):
         self.store = store
         self.world = get_world_size()
         self.average = average
         self.dp = is_distributed() and (self.world > 1 or os.environ.get('MXR_FORCE_DIST', '0') == '1')
+        if comm_dtype is None:
+            comm_dtype = {'bf16': torch.bfloat16, 'fp32': torch.float32}[os.environ.get('MXR_GRAD_COMM', 'fp32')]
+        self.comm_dtype = comm_dtype
+        self._comm = {}  # id(group) -> fp32 wire buffer (DP with low-precision gradient buffers)
         self.overlap = overlap and self.dp
         # off by default: measured 2-3 % slower on 1-GPU ResNet-101 (scripts/gpu_sgd.sh A/B, 125-126
         # vs 128-129 img/s): the HBM-bound update steals bandwidth from the concurrent backward
@@ -70,7 +84,11 @@ class BucketReducer:
         mb = bucket_mb if self.dp else sgd_bucket_mb
         tail = min(tail_mb, mb) if tail_mb else mb
         for g in store.groups:
-            esize = g.grad.element_size()
+            comm = None
+            if self.dp and g.grad.dtype != torch.float32 and self.comm_dtype == torch.float32:
+                comm = torch.zeros(g.numel, dtype=torch.float32, device=g.grad.device)
+                self._comm[id(g)] = comm
+            esize = comm.element_size() if comm is not None else g.grad.element_size()
             cap = max(1, int(mb * (1 << 20) // esize))
             tail_cap = max(1, int(tail * (1 << 20) // esize))
             # cut from the LAST-ready end: the bucket that completes when the backward pass ends
@@ -86,7 +104,7 @@ class BucketReducer:
                 cur[0] = off
                 cur[2].append(n)
             for start, end, names in reversed(rev):
-                bkt = _Bucket(g, start, start)
+                bkt = _Bucket(g, start, start, comm)
                 bkt.end = end
                 bkt.names = list(reversed(names))
                 self.buckets.append(bkt)
@@ -108,8 +126,17 @@ class BucketReducer:
                     self._update(b)
         return hook
 
+    def grad_for(self, group):
+        """The buffer holding ``group``'s reduced gradient after :meth:`finish` (the fp32 wire
+        buffer under DP with fp32 communication, else the group's own gradient buffer)."""
+        return self._comm.get(id(group), group.grad)
+
     def _launch(self, b):
         t = b.buf[b.start:b.end]
+        if b.comm is not None:
+            w = b.comm[b.start:b.end]
+            w.copy_(t)  # widen on the compute stream, ordered after the producers of t
+            t = w
         if self.average:
             t.div_(self.world)
         b.work = dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
@@ -126,8 +153,8 @@ class BucketReducer:
         with torch.cuda.stream(os_):
             if b.work is not None:
                 b.work.wait()  # the optimizer stream waits for this bucket's collective
-            sgd_momentum_(g.master[s:e], g.mom[s:e], g.grad[s:e], lr, mu, wd if g.decay else 0.0, rescale, clip,
-                          None if g.shadow is None else g.shadow[s:e])
+            sgd_momentum_(g.master[s:e], g.mom[s:e], self.grad_for(g)[s:e], lr, mu, wd if g.decay else 0.0, rescale,
+                          clip, None if g.shadow is None else g.shadow[s:e])
         b.updated = True
 
     def prepare(self, sgd=None):
@@ -162,4 +189,46 @@ class BucketReducer:
         self._sgd = None
 
     def bucket_sizes(self):
-        return [(b.end - b.start) * b.buf.element_size() for b in self.buckets]
+        """Bytes each bucket puts on the wire."""
+        return [(b.end - b.start) * (b.comm if b.comm is not None else b.buf).element_size() for b in self.buckets]
+
+    def measure_collectives(self, iters=10, warmup=2):
+        """Time every bucket's all-reduce in isolation (same buffers, dtype and order as the
+        step, outside any graph): -> {'bucket_bytes': [...], 'bucket_ms': [...], 'total_ms',
+        'busbw_GBps'}.  ``total_ms`` is the per-step collective time if nothing overlapped;
+        bus bandwidth uses the ring formula 2(n-1)/n * bytes / time.  Collective call; every
+        rank must call it.  Clobbers the gradient / wire buffers (call between steps)."""
+        if not self.dp or not self.buckets:
+            return None
+        import time
+        cuda = self.store.device.type == 'cuda'
+        tensors = [(b.comm if b.comm is not None else b.buf)[b.start:b.end] for b in self.buckets]
+        out_ms = []
+        for t in tensors:
+            for _ in range(warmup):
+                dist.all_reduce(t)
+            if cuda:
+                ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                torch.cuda.synchronize()
+                ev0.record()
+                for _ in range(iters):
+                    dist.all_reduce(t)
+                ev1.record()
+                ev1.synchronize()
+                ms = ev0.elapsed_time(ev1) / iters
+            else:
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    dist.all_reduce(t)
+                ms = (time.perf_counter() - t0) * 1e3 / iters
+            out_ms.append(ms)
+        # the slowest rank defines the collective time
+        agg = torch.tensor(out_ms, dtype=torch.float64, device=self.store.device)
+        dist.all_reduce(agg, op=dist.ReduceOp.MAX)
+        out_ms = [float(v) for v in agg.tolist()]
+        nbytes = self.bucket_sizes()
+        total = sum(out_ms)
+        n = self.world
+        busbw = (2.0 * (n - 1) / n * sum(nbytes) / (total * 1e-3) / 1e9) if total > 0 and n > 1 else 0.0
+        return {'bucket_bytes': nbytes, 'bucket_ms': [round(v, 4) for v in out_ms], 'total_ms': round(total, 4),
+                'busbw_GBps': round(busbw, 2), 'wire_dtype': str((tensors[0].dtype)).replace('torch.', '')}

@@ -1,0 +1,116 @@
+"""Single-command multi-GPU launch: one fresh child process per GPU.
+
+The reference takes ``--gpus 0,1,2,3`` and builds one MXNet context per device inside a single
+process (`train_end2end.py:168`, `run.sh:7-8`).  On MI355X the engine is one process per GPU
+over RCCL, so the entry points that accept ``--gpus`` re-launch themselves: the parent starts
+N children with ``RANK`` / ``LOCAL_RANK`` / ``WORLD_SIZE`` / ``MASTER_ADDR`` / ``MASTER_PORT``
+set (the torchrun contract), waits for them, and exits with the first failure's code.
+
+The parent NEVER initialises the GPU: call :func:`maybe_spawn` before anything touches HIP
+(importing torch is fine; ``torch.cuda.is_available()`` is not).  Children are started with
+``subprocess`` (no fork of a HIP-initialised process, no exec of the parent).  If one child
+fails, the others are terminated by PID (they would otherwise block in a collective forever).
+
+This module imports nothing heavy so entry scripts can call it before ``import torch``.
+"""
+import os
+import signal
+import socket
+import subprocess
+import sys
+import time
+
+_RANK_VARS = ('RANK', 'LOCAL_RANK', 'WORLD_SIZE', 'LOCAL_WORLD_SIZE', 'GROUP_RANK', 'MASTER_ADDR', 'MASTER_PORT')
+
+
+def free_port(host='127.0.0.1'):
+    s = socket.socket()
+    s.bind((host, 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def parse_gpus(spec):
+    """``'0,1,2'`` (reference device list) or ``'3'`` / ``3`` (a count) -> number of GPUs.
+    A single id ``'0'`` means one GPU, as in the reference."""
+    if isinstance(spec, int):
+        return max(1, spec)
+    spec = str(spec).strip()
+    if ',' in spec:
+        return len([s for s in spec.split(',') if s.strip() != ''])
+    return 1 if spec in ('', '0') else max(1, int(spec))
+
+
+def launched_rank():
+    """True when this process already is one rank of a launched job (torchrun or ours)."""
+    return 'WORLD_SIZE' in os.environ and 'RANK' in os.environ
+
+
+def spawn_local(nprocs, argv, master_addr='127.0.0.1', master_port=None, extra_env=None, poll_s=0.2):
+    """Run ``python argv...`` as ``nprocs`` ranks on this node; returns the job's exit code
+    (0 when every rank exited 0, else the first non-zero code observed)."""
+    port = master_port or free_port(master_addr)
+    procs = []
+    for r in range(nprocs):
+        env = {k: v for k, v in os.environ.items() if k not in _RANK_VARS}
+        env.update(extra_env or {})
+        env.update({'RANK': str(r), 'LOCAL_RANK': str(r), 'WORLD_SIZE': str(nprocs),
+                    'LOCAL_WORLD_SIZE': str(nprocs), 'GROUP_RANK': '0', 'MASTER_ADDR': master_addr,
+                    'MASTER_PORT': str(port)})
+        procs.append(subprocess.Popen([sys.executable] + list(argv), env=env))
+    rc = 0
+
+    def _terminate(sig=signal.SIGTERM):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.send_signal(sig)
+                except ProcessLookupError:
+                    pass
+
+    prev = {}
+    for s in (signal.SIGINT, signal.SIGTERM):
+        try:
+            prev[s] = signal.signal(s, lambda signum, _f: _terminate(signum))
+        except ValueError:  # not the main thread
+            pass
+    try:
+        alive = set(range(nprocs))
+        while alive:
+            for r in sorted(alive):
+                code = procs[r].poll()
+                if code is None:
+                    continue
+                alive.discard(r)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code  # -SIG -> 128+SIG like a shell
+                    sys.stderr.write('[spawn] rank %d exited with %d; stopping the other ranks\n' % (r, code))
+                    _terminate()
+            if alive:
+                time.sleep(poll_s)
+    finally:
+        deadline = time.time() + 30
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.wait(timeout=max(0.1, deadline - time.time()))
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+        for s, h in prev.items():
+            signal.signal(s, h)
+    return rc
+
+
+def maybe_spawn(n_gpus, script, argv):
+    """Entry-script helper.  ``n_gpus`` > 1 and not already a launched rank -> run the job
+    (``script argv``) as ``n_gpus`` children and ``sys.exit`` with its code.  Inside a launched
+    job, check that the launcher's world size agrees with ``--gpus``."""
+    if launched_rank():
+        world = int(os.environ['WORLD_SIZE'])
+        if n_gpus > 1 and world != n_gpus:
+            raise SystemExit('--gpus %d but the launcher started WORLD_SIZE=%d ranks' % (n_gpus, world))
+        return
+    if n_gpus > 1:
+        sys.exit(spawn_local(n_gpus, [script] + list(argv)))

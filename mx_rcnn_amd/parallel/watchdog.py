@@ -55,6 +55,7 @@ class Heartbeat:
         self._last_wall = time.time()
         self._reported_local = None
         self._reported_peer = {}
+        self._paused = 0
         self._stop = threading.Event()
         self._thread = None
         self.stalls = []  # (kind, rank, step, age_s) -- kept for tests and post-mortems
@@ -64,6 +65,28 @@ class Heartbeat:
         self._step = int(step)
         self._last = time.monotonic()
         self._last_wall = time.time()
+
+    def pause(self):
+        """Enter a known long host phase (graph capture, checkpoint write, epoch-end gather):
+        no local stall is reported and peers see this rank as alive until :meth:`resume`."""
+        self._paused += 1
+
+    def resume(self, step=None):
+        self._paused = max(0, self._paused - 1)
+        self.beat(self._step if step is None else step)
+
+    def paused(self):
+        """``with hb.paused(): ...`` -- pause/resume around a block."""
+        import contextlib
+
+        @contextlib.contextmanager
+        def _cm():
+            self.pause()
+            try:
+                yield self
+            finally:
+                self.resume()
+        return _cm()
 
     def start(self):
         if self._thread is None:
@@ -92,6 +115,8 @@ class Heartbeat:
                 logging.debug('heartbeat tick failed: %s', e)
 
     def _tick(self):
+        if self._paused:
+            self._last, self._last_wall = time.monotonic(), time.time()
         step, age = self._step, time.monotonic() - self._last
         if self.store is not None:
             # the time of the last beat, not of this publish: a rank whose loop is stuck but

@@ -146,3 +146,52 @@ def test_voc_ap_fixed_branch():
     prec = np.array([1.0, 0.5])
     assert voc_ap(rec, prec, False) == pytest.approx(0.75)
     assert voc_ap(rec, prec, True) == pytest.approx((6 * 1.0 + 5 * 0.5) / 11)
+
+
+def test_split_input_slice_and_work_load_list():
+    from mx_rcnn_amd.data.loader import split_input_slice
+    assert split_input_slice(4, [1, 1]) == [(0, 2), (2, 4)]
+    assert split_input_slice(6, [1, 2]) == [(0, 2), (2, 6)]
+    assert split_input_slice(5, [1, 1, 1]) == [(0, 2), (2, 4), (4, 5)]
+    with pytest.raises(ValueError):
+        split_input_slice(2, [1, 1, 1])
+    imdb, roidb = load_synthetic_roidb(12, 96, 128, 4)
+    config.SCALES = (96,)
+    config.MAX_SIZE = 128
+    # global batch 2 x 2 = 4 images split 1:3 between the ranks; same steps on every rank
+    r0 = AnchorLoader(None, roidb, 2, True, rank=0, world_size=2, work_load_list='1,3', prefetch=1, workers=1)
+    r1 = AnchorLoader(None, roidb, 2, True, rank=1, world_size=2, work_load_list=[1, 3], prefetch=1, workers=1)
+    assert len(r0) == len(r1) == 3
+    assert all(len(b) == 1 for b in r0._batches) and all(len(b) == 3 for b in r1._batches)
+    for b0, b1, g in zip(r0._batches, r1._batches, r0._global):
+        assert list(b0) + list(b1) == list(g)
+
+
+def test_dp_loaders_agree_on_step_shape():
+    """Every rank pads its batch to the global step's (bucketed) shape and gt count, computed
+    from roidb metadata without communication, so all ranks reach each hipGraph capture on the
+    same step (reference: AnchorLoader pads across devices, rcnn/loader.py:283-286)."""
+    rng = np.random.RandomState(3)
+    imdb, roidb = load_synthetic_roidb(16, 96, 128, 4)
+    for k, r in enumerate(roidb):  # mixed sizes and gt counts
+        r['height'], r['width'] = int(rng.randint(80, 200)), int(rng.randint(80, 200))
+        n = int(rng.randint(1, 6))
+        r['boxes'] = np.tile(np.array([[2, 2, 40, 40]], np.uint16), (n, 1))
+        r['gt_classes'] = np.ones(n, np.int32)
+        r['synthetic_seed'] = k
+    config.SCALES = (100, 120)
+    config.MAX_SIZE = 180
+    ld = [AnchorLoader(None, roidb, 1, True, rank=r, world_size=2, prefetch=1, workers=1) for r in range(2)]
+    shapes = []
+    for b0, b1 in zip(ld[0], ld[1]):
+        assert b0['data'].shape == b1['data'].shape and b0['gt_boxes'].shape == b1['gt_boxes'].shape
+        assert b0['data'].shape[2] % 64 == 0 and b0['data'].shape[3] % 64 == 0
+        G = b0['gt_boxes'].shape[1]
+        assert G >= 8 and (G & (G - 1)) == 0
+        for b in (b0, b1):  # the real image sits inside the padding
+            h, w = b['im_info'][0, :2].tolist()
+            assert h <= b['data'].shape[2] and w <= b['data'].shape[3]
+        shapes.append(tuple(b0['data'].shape))
+    assert len(shapes) == 8
+    config.SCALES = (600,)
+    config.MAX_SIZE = 1000

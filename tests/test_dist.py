@@ -204,3 +204,127 @@ def test_sharded_pred_eval_two_ranks():
         e1 = torch.load(os.path.join(d, 'e1.pt'), weights_only=True)
     want = torch.tensor([[k + 0.1 for k in range(5)], [k + 0.2 for k in range(5)]])
     assert torch.allclose(e0, want) and torch.equal(e0, e1)
+
+
+def test_bench_spawns_ranks_itself(tmp_path):
+    """``python bench.py --gpus 2`` with no launcher starts 2 rank processes itself (the
+    reference's single-command multi-GPU launch) and reports n_gpus from the process group,
+    plus the measured per-bucket all-reduce time."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK', 'MASTER_PORT')}
+    env.update(PYTHONPATH=root, CUDA_VISIBLE_DEVICES='', HIP_VISIBLE_DEVICES='')
+    cmd = [sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2', '--steps', '2', '--warmup', '1',
+           '--network', 'resnet18', '--image', '256x320', '--num-classes', '6']
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, r.stdout[-2000:]
+    rec = json.loads(lines[0])
+    assert rec['n_gpus'] == 2 and rec['config']['parallelism'] == 'dp2' and rec['config']['backend'] == 'gloo'
+    ar = rec['config']['allreduce']
+    assert ar and len(ar['bucket_ms']) == len(ar['bucket_bytes']) >= 1 and ar['total_ms'] > 0
+
+
+def test_bench_rejects_mismatched_world(tmp_path):
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, PYTHONPATH=root, CUDA_VISIBLE_DEVICES='', RANK='0', WORLD_SIZE='1', LOCAL_RANK='0',
+               MASTER_ADDR='127.0.0.1', MASTER_PORT=str(_free_port()))
+    r = subprocess.run([sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2', '--steps', '1'],
+                       cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode != 0 and 'WORLD_SIZE=1' in (r.stderr + r.stdout)
+
+
+class _FakeGroup:
+    def __init__(self, grad):
+        self.grad = grad
+        self.numel = grad.numel()
+        self.entries = [('p%d' % i, None, 'weight', 25, (25,), False) for i in range(grad.numel() // 25)]
+        self.offsets = [25 * i for i in range(grad.numel() // 25)]
+        self.decay = True
+
+
+class _FakeStore:
+    def __init__(self, grad):
+        self.groups = [_FakeGroup(grad)]
+        self.params = {}
+        self.device = grad.device
+
+
+def _wire_worker(rank, world, port, out_dir, comm):
+    os.environ.update({'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port), 'RANK': str(rank),
+                       'WORLD_SIZE': str(world), 'LOCAL_RANK': str(rank)})
+    from mx_rcnn_amd.parallel import dist as pdist
+    from mx_rcnn_amd.parallel.reducer import BucketReducer
+    pdist.init_distributed(backend='gloo')
+    g = torch.Generator().manual_seed(7 + rank)
+    grad = (torch.randn(200, generator=g) * torch.logspace(-3, 3, 200)).to(torch.bfloat16)
+    red = BucketReducer(_FakeStore(grad), bucket_mb=0.0002, tail_mb=0.0001,
+                        comm_dtype=torch.float32 if comm == 'fp32' else torch.bfloat16)
+    assert len(red.buckets) > 1
+    orig = grad.clone()  # the bf16 wire reduces in place
+    red.prepare()
+    red.finish()
+    out = red.grad_for(red.store.groups[0]).clone()
+    torch.save({'grad': orig, 'sum': out}, os.path.join(out_dir, 'w%d.pt' % rank))
+    pdist.barrier()
+    pdist.destroy()
+
+
+@pytest.mark.parametrize('comm', ['fp32', 'bf16'])
+def test_bf16_gradients_summed_in_fp32_on_the_wire(comm):
+    """bf16 gradient buffers are widened per bucket and all-reduced in fp32 (the reference
+    kvstore sums fp32); the optimizer reads the fp32 sum.  bf16 wire is the opt-in."""
+    world = 3
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_wire_worker, args=(world, _free_port(), d, comm), nprocs=world, join=True)
+        rs = [torch.load(os.path.join(d, 'w%d.pt' % r), weights_only=True) for r in range(world)]
+    exact = sum(r['grad'].double() for r in rs)
+    scale = sum(r['grad'].double().abs() for r in rs)  # error bounds scale with sum |g|
+    for r in rs:
+        assert torch.equal(r['sum'], rs[0]['sum'])
+    err = ((rs[0]['sum'].double() - exact).abs() / scale).max().item()
+    if comm == 'fp32':
+        assert rs[0]['sum'].dtype == torch.float32
+        assert err <= 2 ** -22
+    else:
+        assert rs[0]['sum'].dtype == torch.bfloat16
+        assert err <= 2 ** -6
+
+
+def _aux_worker(rank, world, port, out_dir):
+    os.environ.update({'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port), 'RANK': str(rank),
+                       'WORLD_SIZE': str(world), 'LOCAL_RANK': str(rank)})
+    from mx_rcnn_amd.config import snapshot
+    from mx_rcnn_amd.core.module import MutableModule
+    from mx_rcnn_amd.models import FasterRCNN
+    from mx_rcnn_amd.parallel import dist as pdist
+    pdist.init_distributed(backend='gloo')
+    torch.manual_seed(0)
+    m = FasterRCNN('resnet18', 6, cfg=snapshot())
+    mod = MutableModule(m, context='cpu', mode='e2e')
+    mod.bind()
+    with torch.no_grad():  # per-rank train-mode statistics diverge between checkpoints
+        for k, t in mod._model_aux().items():
+            t.fill_(float(rank + 1))
+    _, aux = mod.get_params()
+    torch.save({k: torch.from_numpy(v) for k, v in aux.items()}, os.path.join(out_dir, 'a%d.pt' % rank))
+    pdist.barrier()
+    pdist.destroy()
+
+
+def test_checkpoint_averages_bn_moving_stats_over_ranks():
+    """get_params (the checkpoint source) averages BN moving statistics across ranks, like
+    MXNet's get_params over device copies (rcnn/module.py:84-86)."""
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_aux_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        a0 = torch.load(os.path.join(d, 'a0.pt'), weights_only=True)
+        a1 = torch.load(os.path.join(d, 'a1.pt'), weights_only=True)
+    assert a0 and any('stage4' in k or 'bn1' in k for k in a0)
+    for k in a0:
+        assert torch.allclose(a0[k], torch.full_like(a0[k], 1.5)), k
+        assert torch.equal(a0[k], a1[k])

@@ -131,3 +131,25 @@ def test_overlapped_sgd_matches_end_of_step_sgd(cuda, monkeypatch):
     for k in m0:
         scale = m0[k].abs().max().item() + 1e-12
         assert (m1[k] - m0[k]).abs().max().item() <= 2e-2 * scale + 1e-7, k
+
+
+@pytest.mark.gpu
+def test_graph_capture_has_no_training_side_effects(cuda):
+    """GraphedStep's warm-up runs real steps to settle workspaces; weights, momentum, bf16
+    shadows and BN moving statistics must be exactly as before the capture (a new shape must
+    not apply unscheduled SGD updates), and replaying then trains like eager steps."""
+    from mx_rcnn_amd.core.trainer import GraphedStep
+    torch.manual_seed(0)
+    m = FasterRCNN('resnet50', 21, cfg=_cfg())
+    tr = Trainer(m, 'e2e', fixed_param_prefix=['conv0', 'stage1', 'stage2', 'bn_data', 'bn0'], lr=0.01, device=cuda)
+    b = {k: v.to(cuda) for k, v in _batch(320, 480).items()}
+    tr.step(b)
+    torch.cuda.synchronize()
+    before = tr.snapshot_state()
+    GraphedStep(tr, b, warmup=3)
+    torch.cuda.synchronize()
+    for g, (mst, mom, sh) in zip(tr.store.groups, before['groups']):
+        assert torch.equal(g.master, mst) and torch.equal(g.mom, mom)
+        assert sh is None or torch.equal(g.shadow, sh)
+    for buf, v in zip(tr.model.buffers(), before['buffers']):
+        assert torch.equal(buf, v)

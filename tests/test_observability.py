@@ -165,3 +165,20 @@ def test_watchdog_in_fit_reports_slow_steps_and_stops(monkeypatch):
     mod.fit(data, num_epoch=1, max_steps=2, optimizer_params={'learning_rate': 1e-3, 'momentum': 0.9, 'wd': 5e-4})
     assert seen and all(k == 'local' for k, *_ in seen)
     assert not any(t.name == 'mxr-heartbeat' for t in threading.enumerate())
+
+
+def test_watchdog_pause_covers_long_host_phases():
+    """pause()/resume() brackets known long phases (graph capture, epoch-end checkpointing): no
+    local stall is reported while paused, and the stall clock restarts on resume."""
+    import time
+    from mx_rcnn_amd.parallel.watchdog import Heartbeat
+    seen = []
+    hb = Heartbeat(0.05, period_s=0.01, store=None, on_stall=lambda *a: seen.append(a))
+    hb.start()
+    hb.beat(0)
+    with hb.paused():
+        time.sleep(0.25)
+    assert not seen
+    time.sleep(0.25)  # unpaused and silent: reported
+    hb.stop()
+    assert seen and seen[0][0] == 'local'

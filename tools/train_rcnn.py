@@ -42,7 +42,7 @@ def train_rcnn(image_set, year, root_path, devkit_path, pretrained, epoch, prefi
         except FileNotFoundError:
             logging.warning('pretrained %s-%04d.params not found: random init', pretrained, epoch)
     train_data = ROIIter(roidb, batch_size=config.TRAIN.BATCH_IMAGES, shuffle=True, mode='train', rank=rank,
-                         world_size=world, seed=seed)
+                         world_size=world, seed=seed, work_load_list=work_load_list)
     fam = launch.family(network)
     fixed = (['conv1', 'conv2', 'conv3', 'conv4', 'conv5'] if config.TRAIN.FINETUNE else ['conv1', 'conv2']) \
         if fam == 'vgg' else launch.FIXED_PREFIX['resnet']

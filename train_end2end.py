@@ -37,13 +37,13 @@ def end2end_train(args):
     scales = model.anchor_scales
     train_data = AnchorLoader(model, roidb, batch_size=args.ims_per_gpu, shuffle=True, mode='train',
                               anchor_scales=scales, rank=rank, world_size=world, seed=args.seed,
-                              need_mean=fam == 'vgg')
+                              need_mean=fam == 'vgg', work_load_list=args.work_load_list)
     launch.calibrate_if_random(model, train_data, arg_params)
     mod = MutableModule(model, data_names=['data', 'im_info'], label_names=['gt_boxes'], context=device,
                         fixed_param_prefix=launch.FIXED_PREFIX[fam], mode='e2e', use_graph=not args.eager)
     monitor = Monitor(100) if args.monitor else None
     mod.fit(train_data, eval_metric=e2e_metrics(), epoch_end_callback=do_checkpoint(args.prefix), monitor=monitor,
-            batch_end_callback=Speedometer(args.ims_per_gpu * world, frequent=args.frequent),
+            batch_end_callback=Speedometer(train_data.global_batch_size, frequent=args.frequent),
             kvstore=args.kv_store, optimizer='sgd',
             optimizer_params=launch.optimizer_params(args.lr, args.mom, args.wd, args.factor_step, args.resume),
             arg_params=arg_params, aux_params=aux_params, begin_epoch=args.load_epoch, num_epoch=args.num_epoch,
@@ -65,11 +65,11 @@ def parse_args(argv=None):
     p.add_argument('--pretrained', default='model/vgg16')
     p.add_argument('--load-epoch', dest='load_epoch', type=int, default=0)
     p.add_argument('--prefix', default='model/faster-rcnn')
-    p.add_argument('--gpus', default='0', help='parity flag; use torchrun for multi-GPU')
+    p.add_argument('--gpus', default='0', help='GPU list "0,1,2,3" or count: one process per GPU (or use torchrun)')
     p.add_argument('--num_epoch', type=int, default=7)
     p.add_argument('--frequent', type=int, default=20)
     p.add_argument('--kv_store', default='device')
-    p.add_argument('--work_load_list', default=None)
+    p.add_argument('--work_load_list', default=None, help='per-GPU share of the global batch, e.g. "1,1,2,2"')
     p.add_argument('--lr', type=float, default=0.001)
     p.add_argument('--mom', type=float, default=0.9)
     p.add_argument('--wd', type=float, default=0.0005)

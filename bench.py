@@ -159,6 +159,10 @@ def main():
                           'objective_first_last': [round(loss0, 4), round(loss1, 4)],
                           'backend': pdist.backend_name(), 'allreduce': comm}}
         print(json.dumps(rec), flush=True)
+    if os.environ.get('MXR_BENCH_DUMP_TUNE') and device.type == 'cuda':
+        from mx_rcnn_amd.ops import need_ext
+        for key, tile, sp in need_ext().conv_tune_table():
+            print('[tune] %-48s tile %d splits %d' % (key, tile, sp), file=sys.stderr)
     pdist.destroy()
 
 

@@ -5,6 +5,8 @@
 #include <cmath>
 #include <cstring>
 #include <map>
+#include <mutex>
+#include <string>
 #include <torch/extension.h>
 #include <ATen/Parallel.h>
 #include <c10/core/DeviceGuard.h>
@@ -456,6 +458,41 @@ std::vector<Tensor> bn_relu_bwd(const Tensor& x, const Tensor& dy, const Tensor&
 
 // ---- implicit-GEMM conv ----------------------------------------------------------------
 
+// ---- per-shape conv autotune (MIOpen-find style, MI355X-measured) ------------------------------
+// The best tile configuration of the implicit-GEMM conv depends on the grid's fit to 256 CUs,
+// K depth and output width (tools/microbench/conv_tiles.py, profiles/r2_conv_tiles.txt): e.g. the
+// 128-RoI stage-4 convs run 1.3-1.5x faster on the 16-wave 128x128 ring, the stage-3 1x1s 5-15 %
+// faster on 8-wave tiles.  The first call of a shape (and epilogue kind) times every candidate
+// into scratch outputs on the current stream (hipEvents, 3 runs each) and caches the fastest;
+// graph capture never tunes (a capturing stream uses the cache or the static plan).  All
+// candidates accumulate each output in the same K order, so the choice never changes results.
+// MXR_CONV_TUNE=0 disables it.
+namespace {
+std::mutex g_tune_mu;
+std::map<std::string, std::pair<int, int>> g_tune;
+
+bool conv_tune_enabled() {
+  static const bool on = [] {
+    const char* e = getenv("MXR_CONV_TUNE");
+    return e == nullptr || e[0] != '0';
+  }();
+  return on;
+}
+
+bool stream_capturing(hipStream_t st) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess) return true;  // unknown: be safe
+  return cs != hipStreamCaptureStatusNone;
+}
+}  // namespace
+
+std::vector<std::tuple<std::string, int64_t, int64_t>> conv_tune_table() {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  std::vector<std::tuple<std::string, int64_t, int64_t>> out;
+  for (const auto& kv : g_tune) out.emplace_back(kv.first, kv.second.first, kv.second.second);
+  return out;
+}
+
 // conv_igemm_fwd(x, w, bias, stride, pad, relu, tile, splits, residual, bn, bn_eps, bn_fix_gamma, act_relu)
 //   -> [y] or, when bn = (gamma, beta, mean, var) is given, [y, act(bn(y))]  (see ConvEpi)
 std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::optional<Tensor> bias, int64_t stride,
@@ -536,9 +573,73 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
     ep.y2 = reinterpret_cast<uint16_t*>(y2.data_ptr());
   }
   int auto_splits = 1;
-  const int t = mxr::conv_igemm_plan(NB, Ho, Wo, Cin, Cout, KH, KW, (int)tile, &auto_splits);
+  int t = mxr::conv_igemm_plan(NB, Ho, Wo, Cin, Cout, KH, KW, (int)tile, &auto_splits);
   // BN-backward epilogue: no split-K by default (the statistics are reduced in-tile instead)
-  const int sp = splits > 0 ? (int)splits : (bwd_mode ? 1 : auto_splits);
+  int sp = splits > 0 ? (int)splits : (bwd_mode ? 1 : auto_splits);
+  if (tile <= 0 && splits <= 0 && conv_tune_enabled()) {
+    char kb[256];
+    snprintf(kb, sizeof(kb), "%d,%d,%d,%d,%d,%d,%d,%d,%d|%d%d%d%d%d%d", NB, H, W, Cin, Cout, KH, KW, (int)stride,
+             (int)pad, ep.residual != nullptr, ep.y2 != nullptr || bn.has_value(), bwd_mode, ep.dadd != nullptr,
+             ep.relu, ep.bias != nullptr);
+    const std::string key(kb);
+    std::unique_lock<std::mutex> lk(g_tune_mu);
+    auto it = g_tune.find(key);
+    if (it != g_tune.end()) {
+      t = it->second.first;
+      sp = it->second.second;
+    } else if (!stream_capturing(cur_stream())) {
+      // time the candidates into scratch outputs (no in-place aliasing, no statistics updates)
+      std::vector<std::pair<int, int>> cands = {{t, sp}};
+      for (int c : {23, 22, 101, 104, 105, 106, 108, 109, 110, 111})
+        if (c != t || sp != 1) cands.push_back({c, 1});
+      mxr::ConvEpi et = ep;
+      Tensor ys = at::empty_like(y, y.options(), at::MemoryFormat::ChannelsLast);
+      Tensor y2s, dg2, db2;
+      if (et.y2) {
+        y2s = at::empty_like(y, y.options(), at::MemoryFormat::ChannelsLast);
+        et.y2 = reinterpret_cast<uint16_t*>(y2s.data_ptr());
+      }
+      if (bwd_mode) {
+        dg2 = at::zeros({Cout}, x.options().dtype(at::kFloat));
+        db2 = at::zeros({Cout}, x.options().dtype(at::kFloat));
+        et.bnb_dgamma = dg2.data_ptr<float>();
+        et.bnb_dbeta = db2.data_ptr<float>();
+      }
+      Tensor slab_t;
+      if (sp > 1) slab_t = at::empty({(int64_t)sp * NB * Ho * Wo * Cout}, x.options().dtype(at::kFloat));
+      hipStream_t st = cur_stream();
+      hipEvent_t e0, e1;
+      hipEventCreate(&e0);
+      hipEventCreate(&e1);
+      float best = 1e30f;
+      std::pair<int, int> pick = {t, sp};
+      for (const auto& c : cands) {
+        float* sl = c.second > 1 ? slab_t.data_ptr<float>() : nullptr;
+        auto run = [&]() {
+          return mxr::conv_igemm_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                     reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                                     reinterpret_cast<uint16_t*>(ys.data_ptr()), NB, H, W, Cin, Ho, Wo, Cout, KH, KW,
+                                     (int)stride, (int)pad, et, c.first, c.second, sl, st);
+        };
+        if (run() != c.first) continue;  // fell back to another variant: not this candidate
+        hipEventRecord(e0, st);
+        for (int r = 0; r < 3; ++r) run();
+        hipEventRecord(e1, st);
+        hipEventSynchronize(e1);
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, e0, e1);
+        if (ms < best * 0.98f) {  // prefer the earlier (static-plan) candidate on near ties
+          best = ms;
+          pick = c;
+        }
+      }
+      hipEventDestroy(e0);
+      hipEventDestroy(e1);
+      g_tune[key] = pick;
+      t = pick.first;
+      sp = pick.second;
+    }
+  }
   Tensor slab;
   if (sp > 1) slab = at::empty({(int64_t)sp * NB * Ho * Wo * Cout}, x.options().dtype(at::kFloat));
   const int used = mxr::conv_igemm_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
@@ -967,6 +1068,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mean"), py::arg("var"), py::arg("eps"), py::arg("fix_gamma"), py::arg("relu"), py::arg("need_dx"),
         py::arg("need_params"), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(),
         py::arg("dres") = py::none());
+  m.def("conv_tune_table", &conv_tune_table, "per-shape conv autotune choices: [(key, tile, splits)]");
   m.def("conv_igemm_fwd", &conv_igemm_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),
         py::arg("pad"), py::arg("relu"), py::arg("tile") = 0, py::arg("splits") = 0, py::arg("residual") = py::none(),
         py::arg("bn") = py::none(), py::arg("bn_eps") = 2e-5, py::arg("bn_fix_gamma") = false,

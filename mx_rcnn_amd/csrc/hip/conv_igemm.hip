@@ -975,6 +975,406 @@ conv_igemm_bufks_kernel(const uint16_t* __restrict__ x, const uint16_t* __restri
     igemm_epilogue<TM, TN, WM, WN>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab);
 }
 
+// ---- tile-balanced LDS-DMA ring (the production path) ----------------------------------------
+// Measured on the ResNet-101 C4 stage-3/4 shapes (rocprofv3 --pmc, profiles/r2_conv_pmc.txt): the
+// 64x64 ring above is limited by what ONE CU can pull into LDS (~27 GB/s at two 16 KB stages in
+// flight, 47 % of wave cycles parked on vmcnt/barrier), and by tile quantisation: 4200 x 256 gives
+// 264 tiles for 256 CUs, so 8 CUs carry two tiles and set the kernel time.  This kernel
+//   * sizes the tile so the grid is at most one (or an integer number of) tile(s) per CU
+//     (BM = 16*TM*WGM rows x BN = 16*TN*WGN columns, any wave layout WGM x WGN),
+//   * keeps 5-7 K-steps in flight (S-deep ring, up to ~150 KB of LDS: one workgroup per CU),
+//   * spreads the (BM+BN)/8 DMA instructions of a stage over the waves (a wave issues q or
+//     q+1, and waits for exactly its own count), 1x1 convs skip the tap mask entirely,
+//   * keeps the fragment reads, MFMA and fused epilogues of the kernels above.
+template <int TM, int TN, int WGM, int WGN, int SFIX = 0>
+struct RingCfg {
+  static constexpr int NW = WGM * WGN, NT = 64 * NW;
+  static constexpr int BM = 16 * TM * WGM, BN = 16 * TN * WGN;
+  static constexpr int RA = BM / 8, RB = BN / 8, RT = RA + RB;  // 8-row DMA pieces per stage
+  static constexpr int QL = RT / NW, RL = RT % NW;              // pieces per wave: QL (+1 for wid < RL)
+  static constexpr int QMAX = QL + (RL ? 1 : 0);
+  static constexpr int STAGE_BYTES = (BM + BN) * BK * 2;
+  // deepest ring within ~150 KB of LDS, 3..8 stages, and <= 63 outstanding DMAs per wave
+  static constexpr int S0 = (150 * 1024) / STAGE_BYTES;
+  static constexpr int S1 = S0 > 8 ? 8 : (S0 < 3 ? 3 : S0);
+  static constexpr int S2 = (S1 - 2) * QMAX > 60 ? 60 / QMAX + 2 : S1;
+  static constexpr int S = SFIX ? SFIX : S2;
+};
+
+// wait until this wave has at most `ahead` stages of its own DMAs (n per stage) in flight
+template <int N>
+__device__ __forceinline__ void wait_ring(int ahead) {
+  switch (ahead) {
+    case 6: wait_vmcnt<6 * N>(); break;
+    case 5: wait_vmcnt<5 * N>(); break;
+    case 4: wait_vmcnt<4 * N>(); break;
+    case 3: wait_vmcnt<3 * N>(); break;
+    case 2: wait_vmcnt<2 * N>(); break;
+    case 1: wait_vmcnt<N>(); break;
+    default: wait_vmcnt<0>(); break;
+  }
+}
+
+// Generic LDS-transposed epilogue for NT threads and any wave layout (see igemm_epilogue_lds).
+template <int BM, int BN, int TM, int TN, int NT>
+__device__ __forceinline__ void ring_epilogue(f32x4 (&acc)[TM][TN], float* __restrict__ T, int m0, int n0, int wm,
+                                              int wn, int lane, int tid, int M, int Cout, const ConvEpi& ep,
+                                              uint16_t* __restrict__ y, int split, int splits,
+                                              float* __restrict__ slab) {
+  constexpr int LDT = BN + 4;
+  constexpr int VPR = BN / 8;
+  constexpr int NVEC = BM * VPR;
+  constexpr int WM = 16 * TM, WN = 16 * TN;
+  constexpr int NW = NT / 64;
+  static_assert(64 % VPR == 0 && NT % VPR == 0, "column groups must tile the wave");
+  __syncthreads();  // every wave is done reading the operand ring
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        T[(wm * WM + i * 16 + (lane >> 4) * 4 + r) * LDT + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
+  __syncthreads();
+  const int cv = tid % VPR;
+  const int n = n0 + cv * 8;
+  const bool ncol = n < Cout;
+  if (splits > 1) {
+    float* sp = slab + (int64_t)split * M * Cout;
+    for (int q = tid; q < NVEC; q += NT) {
+      const int row = q / VPR, m = m0 + row;
+      if (m >= M || !ncol) continue;
+      const float4* src = reinterpret_cast<const float4*>(T + row * LDT + cv * 8);
+      float4* dst = reinterpret_cast<float4*>(sp + (int64_t)m * Cout + n);
+      dst[0] = src[0];
+      dst[1] = src[1];
+    }
+    return;
+  }
+  EpiCol ec[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ec[k] = epi_col(ep, ncol ? n + k : 0);
+  if (ep.bnb_x) {
+    float sg[8], sgx[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) sg[k] = sgx[k] = 0.f;
+    for (int q = tid; q < NVEC; q += NT) {
+      const int row = q / VPR, m = m0 + row;
+      if (m >= M || !ncol) continue;
+      const int64_t e = (int64_t)m * Cout + n;
+      float a[8], xv[8], d[8], rs[8];
+      const float4* src = reinterpret_cast<const float4*>(T + row * LDT + cv * 8);
+      const float4 a0 = src[0], a1 = src[1];
+      a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w; a[4] = a1.x; a[5] = a1.y; a[6] = a1.z; a[7] = a1.w;
+      ld8_bf16(ep.bnb_x + e, xv);
+      if (ep.dadd) {
+        ld8_bf16(ep.dadd + e, d);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) a[k] += d[k];
+      }
+      if (ep.residual) ld8_bf16(ep.residual + e, rs);
+      float o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const float g = (!ep.act_relu || xv[k] * ec[k].s + ec[k].t > 0.f) ? a[k] : 0.f;
+        sg[k] += g;
+        sgx[k] += g * (xv[k] - ec[k].mean) * ec[k].inv;
+        o[k] = g * ec[k].s + (ep.residual ? rs[k] : 0.f);
+      }
+      st8_bf16(y + e, o);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+#pragma unroll
+      for (int o = VPR; o < 64; o <<= 1) {
+        sg[k] += __shfl_xor(sg[k], o, 64);
+        sgx[k] += __shfl_xor(sgx[k], o, 64);
+      }
+    }
+    __syncthreads();  // T is reused as [NW waves][BN][2] partials
+    const int wid = tid >> 6;
+    if (lane < VPR) {
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        T[(wid * BN + cv * 8 + k) * 2] = sg[k];
+        T[(wid * BN + cv * 8 + k) * 2 + 1] = sgx[k];
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      const int col = n0 + c;
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        a += T[(q * BN + c) * 2];
+        b += T[(q * BN + c) * 2 + 1];
+      }
+      if (col < Cout) {
+        if (ep.bnb_dbeta) atomicAdd(ep.bnb_dbeta + col, a);
+        if (ep.bnb_dgamma && !ep.bn_fix_gamma) atomicAdd(ep.bnb_dgamma + col, b);
+      }
+    }
+    return;
+  }
+  for (int q = tid; q < NVEC; q += NT) {
+    const int row = q / VPR, m = m0 + row;
+    if (m >= M || !ncol) continue;
+    const int64_t e = (int64_t)m * Cout + n;
+    const float4* src = reinterpret_cast<const float4*>(T + row * LDT + cv * 8);
+    const float4 a0 = src[0], a1 = src[1];
+    float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+    float rs[8];
+    if (ep.residual) ld8_bf16(ep.residual + e, rs);
+    uint16_t yb[8];
+    float y2v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float t = a[k] + ec[k].bias + (ep.residual ? rs[k] : 0.f);
+      if (ep.relu) t = fmaxf(t, 0.f);
+      yb[k] = f32_to_bf16(t);
+      float qv = bf16_to_f32(yb[k]) * ec[k].s + ec[k].t;
+      if (ep.act_relu) qv = fmaxf(qv, 0.f);
+      y2v[k] = qv;
+    }
+    *reinterpret_cast<uint4*>(y + e) =
+        make_uint4((uint32_t)yb[0] | ((uint32_t)yb[1] << 16), (uint32_t)yb[2] | ((uint32_t)yb[3] << 16),
+                   (uint32_t)yb[4] | ((uint32_t)yb[5] << 16), (uint32_t)yb[6] | ((uint32_t)yb[7] << 16));
+    if (ep.y2) st8_bf16(ep.y2 + e, y2v);
+  }
+}
+
+template <int TM, int TN, int WGM, int WGN, int SFIX, bool ONE>
+__global__ void __launch_bounds__(64 * WGM * WGN)
+conv_ring_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int NB,
+                 int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad,
+                 const ConvEpi ep, int tiles_n, int nwg, int ntiles, int splits, float* __restrict__ slab) {
+  using C = RingCfg<TM, TN, WGM, WGN, SFIX>;
+  constexpr int BM = C::BM, BN = C::BN, S = C::S, NT = C::NT, NW = C::NW;
+  static_assert(C::BM * (C::BN + 4) * 4 <= S * (C::BM + C::BN) * BK * 2, "epilogue tile must fit the ring");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[S * (BM + BN) * BK];
+  uint16_t* As = lds;
+  uint16_t* Bs = lds + S * BM * BK;
+
+  const int bid = blockIdx.x;
+  const int q8 = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+  const int wgid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + bid / 8;
+  const int split = wgid / ntiles, tile = wgid % ntiles;
+  const int tm_idx = tile / tiles_n, tn_idx = tile % tiles_n;
+  const int m0 = tm_idx * BM, n0 = tn_idx * BN;
+  const int M = NB * Ho * Wo;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid / WGN, wn = wid % WGN;
+  const int K = KH * KW * Cin;
+
+  const __amdgpu_buffer_rsrc_t xr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)((int64_t)NB * H * W * Cin * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr =
+      __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, (int)((int64_t)Cout * K * 2), 0x00020000);
+
+  // this wave's DMA pieces: d = wid + j * NW (d < RA: A rows 8d.., else B rows 8(d-RA)..)
+  const int nmine = C::QL + (wid < C::RL ? 1 : 0);
+  const int slot = lane & 7;
+  uint32_t off[C::QMAX];
+  uint64_t amask[C::QMAX];
+#pragma unroll
+  for (int j = 0; j < C::QMAX; ++j) {
+    const int d = wid + j * NW;
+    off[j] = kBufOOB;
+    amask[j] = 0;
+    if (j >= nmine) continue;
+    if (d < C::RA) {
+      const int row = 8 * d + (lane >> 3);
+      const int lc = slot ^ ((row >> 1) & 7);
+      const int m = m0 + row;
+      if (m < M) {
+        const int img = m / (Ho * Wo), rem = m % (Ho * Wo);
+        const int hi0 = (rem / Wo) * stride - pad, wi0 = (rem % Wo) * stride - pad;
+        off[j] = (uint32_t)(((((int64_t)img * H + hi0) * W + wi0) * Cin + lc * 8) * 2);
+        if (!ONE) {
+          for (int fr = 0; fr < KH; ++fr)
+            for (int fc = 0; fc < KW; ++fc)
+              if ((unsigned)(hi0 + fr) < (unsigned)H && (unsigned)(wi0 + fc) < (unsigned)W)
+                amask[j] |= 1ull << (fr * KW + fc);
+        }
+      }
+    } else {
+      const int row = 8 * (d - C::RA) + (lane >> 3);
+      const int co = n0 + row;
+      if (co < Cout) off[j] = (uint32_t)(((int64_t)co * K + (slot ^ ((row >> 1) & 7)) * 8) * 2);
+    }
+  }
+  const int cin_steps = Cin / BK;
+  const int nk_all = KH * KW * cin_steps;
+  const int per = (nk_all + splits - 1) / splits;
+  const int k_begin = split * per;
+  const int k_end = min(nk_all, k_begin + per);
+  const int nk = max(0, k_end - k_begin);
+
+  int c_tap = k_begin / cin_steps, c_ci = (k_begin % cin_steps) * BK;
+  int c_fr = c_tap / KW, c_fc = c_tap % KW;
+  auto issue = [&](int buf) {
+    const uint32_t tap_a = (uint32_t)((c_fr * W + c_fc) * Cin * 2);
+    const uint32_t soff_a = (uint32_t)(c_ci * 2);
+    const uint32_t soff_b = (uint32_t)((c_tap * Cin + c_ci) * 2);
+#pragma unroll
+    for (int j = 0; j < C::QMAX; ++j) {
+      if (j >= nmine) break;
+      const int d = wid + j * NW;
+      if (d < C::RA) {
+        uint32_t vo;
+        if (ONE) vo = off[j];
+        else vo = ((amask[j] >> c_tap) & 1ull) ? off[j] + tap_a : kBufOOB;
+        buf_lds16(xr, As + (buf * BM + 8 * d) * BK, vo, soff_a);
+      } else {
+        buf_lds16(wr, Bs + (buf * BN + 8 * (d - C::RA)) * BK, off[j], soff_b);
+      }
+    }
+    c_ci += BK;
+    if (c_ci == Cin) {
+      c_ci = 0;
+      ++c_tap;
+      if (++c_fc == KW) {
+        c_fc = 0;
+        ++c_fr;
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int s = 0; s < S - 1; ++s)
+    if (s < nk) issue(s);
+  for (int ks = 0; ks < nk; ++ks) {
+    const int ahead = min(S - 2, nk - 1 - ks);
+    if (C::RL == 0 || wid < C::RL) wait_ring<C::QMAX>(ahead);
+    else wait_ring<C::QL>(ahead);
+    __builtin_amdgcn_s_barrier();
+    if (ks + S - 1 < nk) issue((ks + S - 1) % S);
+    const int buf = ks % S;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[TM], bfr[TN];
+      const int chunk = kk * 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * 16 * TM + i * 16 + (lane & 15);
+        af[i] = *reinterpret_cast<const bf16x8*>(As + (buf * BM + row) * BK + swz(row, chunk) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * 16 * TN + j * 16 + (lane & 15);
+        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (buf * BN + row) * BK + swz(row, chunk) * 8);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  if (Cout % 8 == 0)
+    ring_epilogue<BM, BN, TM, TN, NT>(acc, reinterpret_cast<float*>(lds), m0, n0, wm, wn, lane, tid, M, Cout, ep, y,
+                                      split, splits, slab);
+  else
+    igemm_epilogue<TM, TN, 16 * TM, 16 * TN>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab);
+}
+
+// ring configurations (tile codes 100 + index)
+struct RingShape {
+  int bm, bn, nt, stage_bytes, s;
+};
+template <int TM, int TN, int WGM, int WGN, int SFIX>
+constexpr RingShape ring_shape() {
+  using C = RingCfg<TM, TN, WGM, WGN, SFIX>;
+  return RingShape{C::BM, C::BN, C::NT, C::STAGE_BYTES, C::S};
+}
+#define MXR_RING_CONFIGS(X)   \
+  X(0, 2, 2, 2, 2, 3)   /* 64x64, 4 waves, S3 */ \
+  X(1, 2, 1, 2, 4, 3)   /* 64x64, 8 waves, S3 */ \
+  X(2, 2, 1, 2, 4, 4)   /* 64x64, 8 waves, S4 */ \
+  X(3, 1, 1, 4, 4, 3)   /* 64x64, 16 waves, S3 */ \
+  X(4, 1, 2, 2, 2, 3)   /* 32x64, 4 waves, S3 */ \
+  X(5, 2, 2, 4, 2, 3)   /* 128x64, 8 waves, S3 */ \
+  X(6, 2, 2, 4, 4, 3)   /* 128x128, 16 waves, S3 */ \
+  X(7, 4, 4, 2, 2, 3)   /* 128x128, 4 waves, S3 */ \
+  X(8, 2, 4, 4, 2, 3)   /* 128x128, 8 waves, S3 */ \
+  X(9, 2, 2, 2, 4, 3)   /* 64x128, 8 waves, S3 */ \
+  X(10, 1, 2, 4, 2, 3)  /* 64x64, 8 waves (4x2), S3 */ \
+  X(11, 2, 2, 2, 2, 2)  /* 64x64, 4 waves, S2 */
+static const RingShape kRingShapes[] = {
+#define MXR_X(i, a, b, c, d, e) ring_shape<a, b, c, d, e>(),
+    MXR_RING_CONFIGS(MXR_X)
+#undef MXR_X
+};
+constexpr int kNumRing = sizeof(kRingShapes) / sizeof(kRingShapes[0]);
+
+template <int TM, int TN, int WGM, int WGN, int SFIX>
+static void launch_ring(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho,
+                        int Wo, int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int splits,
+                        float* slab, hipStream_t st) {
+  using C = RingCfg<TM, TN, WGM, WGN, SFIX>;
+  const int M = NB * Ho * Wo;
+  const int tiles_m = (M + C::BM - 1) / C::BM, tiles_n = (Cout + C::BN - 1) / C::BN;
+  const int ntiles = tiles_m * tiles_n;
+  const int nwg = ntiles * splits;
+  if (KH == 1 && KW == 1 && pad == 0)
+    conv_ring_kernel<TM, TN, WGM, WGN, SFIX, true><<<nwg, C::NT, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW,
+                                                                    stride, pad, ep, tiles_n, nwg, ntiles, splits, slab);
+  else
+    conv_ring_kernel<TM, TN, WGM, WGN, SFIX, false><<<nwg, C::NT, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW,
+                                                                     stride, pad, ep, tiles_n, nwg, ntiles, splits,
+                                                                     slab);
+  if (splits > 1) {
+    const int64_t MN = (int64_t)M * Cout;
+    if (ep.bnb_x)
+      splitk_reduce_bnb_kernel<<<dim3(div_up(Cout, 64), div_up(M, 64)), 256, 0, st>>>(slab, splits, M, Cout, ep, y);
+    else
+      splitk_reduce_kernel<<<div_up((MN + 3) / 4, 256), 256, 0, st>>>(slab, splits, MN, Cout, ep, y);
+  }
+}
+
+static void launch_ring_code(int idx, const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W,
+                             int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep,
+                             int splits, float* slab, hipStream_t st) {
+  switch (idx) {
+#define MXR_X(i, a, b, c, d, e) \
+  case i: launch_ring<a, b, c, d, e>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    MXR_RING_CONFIGS(MXR_X)
+#undef MXR_X
+    default: break;
+  }
+}
+
+// Ring plan: the configuration with the least modelled time.  Model: a CU streams its tiles'
+// operand bytes at a per-CU rate (LDS-DMA, ~70 GB/s) while the MFMA work proceeds at its own
+// rate; the grid takes ceil(tiles / 256) rounds of the slower of the two, plus a per-tile
+// prologue/epilogue latency; output columns wider than the tile cost A re-reads (already in bytes).
+static int ring_plan(int64_t M, int Cout, int nk, int* splits_out) {
+  int best = 0;
+  double best_t = 1e30;
+  for (int i = 0; i < kNumRing; ++i) {
+    const RingShape& r = kRingShapes[i];
+    const int64_t tiles = ((M + r.bm - 1) / r.bm) * ((Cout + r.bn - 1) / r.bn);
+    const int64_t rounds = (tiles + 255) / 256;
+    const double bytes = (double)(r.bm + r.bn) * 128.0 * nk;            // per tile
+    const double flops = 2.0 * r.bm * r.bn * 64.0 * nk;                  // per tile
+    const double t_mem = bytes / 70e3;                                   // us at 70 GB/s per CU
+    const double t_mma = flops / (4.0 * 1024 * 2.1e3);                   // us at 4 SIMDs x 1024 FLOP/clk, 2.1 GHz
+    const double t = rounds * ((t_mem > t_mma ? t_mem : t_mma) + 1.0);
+    if (t < best_t * 0.999) {
+      best_t = t;
+      best = i;
+    }
+  }
+  *splits_out = 1;
+  return 100 + best;
+}
+
 template <int BM, int BN, int S, int KS>
 static void launch_fwd_ks(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho,
                           int Wo, int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int splits,
@@ -1023,6 +1423,11 @@ static void launch_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB
 int conv_igemm_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int tile, int* splits_out) {
   const int64_t M = (int64_t)NB * Ho * Wo;
   const int nk = KH * KW * (Cin / BK);
+  static const bool ring = [] {
+    const char* e = getenv("MXR_CONV_RING");
+    return e != nullptr && e[0] == '1';
+  }();
+  if (tile <= 0 && ring && Cin % BK == 0 && KH * KW <= 64) return ring_plan(M, Cout, nk, splits_out);
   if (tile <= 0) {
     // buffer-resource LDS-DMA kernel, 3-deep (tools/microbench/conv_tiles.py sweep on the
     // ResNet-101 C4 shapes): 64x64 everywhere except many-block, long-K shapes (the 128-RoI
@@ -1058,9 +1463,16 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
     return -1;
   if (ep.y2 && ep.bnb_x) return -1;
   // buffer variants: 32-bit byte offsets below the kBufOOB sentinel, tap mask of 64 bits
+  if (tile >= 100 && ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB ||
+                      (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kBufOOB || KH * KW > 64))
+    tile = 23;
   if (tile >= 21 && ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB ||
                      (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kBufOOB || KH * KW > 64))
     tile = 3;
+  if (tile >= 100 && tile < 100 + kNumRing) {
+    launch_ring_code(tile - 100, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st);
+    return tile;
+  }
   switch (tile) {
     case 1: launch_fwd<128, 128>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 2: launch_fwd<128, 64>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
@@ -1079,6 +1491,11 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
     case 31: launch_fwd<128, 128, 4, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 32: launch_fwd<128, 64, 4, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 33: launch_fwd<64, 64, 4, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    // deeper rings for the one-tile-per-CU grids (probe)
+    case 43: launch_fwd<64, 64, 5, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    case 53: launch_fwd<64, 64, 6, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    case 63: launch_fwd<64, 64, 8, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    case 41: launch_fwd<128, 128, 4, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     // small tiles (2-4 workgroups per CU on the ~4K-row stage-3 GEMMs: more waves to hide latency)
     case 24: launch_fwd<32, 64, 3, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 25: launch_fwd<64, 32, 3, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;

@@ -25,7 +25,8 @@ def _bn_ref(y, gamma, beta, mean, var, eps=2e-5):
 
 @pytest.mark.parametrize('shape', [(1, 256, 24, 40, 256, 1, 1, 0), (1, 64, 31, 17, 64, 3, 1, 1),
                                    (2, 128, 14, 14, 512, 1, 1, 0), (1, 1024, 50, 84, 256, 1, 1, 0)])
-@pytest.mark.parametrize('tile,splits', [(3, 1), (3, 4), (0, 0), (23, 1), (22, 2)])
+@pytest.mark.parametrize('tile,splits', [(3, 1), (3, 4), (0, 0), (23, 1), (22, 2), (101, 1), (105, 1), (106, 1),
+                                         (109, 1), (110, 1), (106, 2)])
 def test_conv_epilogue_residual_bn(cuda, shape, tile, splits):
     from mx_rcnn_amd.ops import need_ext
     N, Cin, H, W, Cout, k, s, p = shape
@@ -152,8 +153,10 @@ def test_bnb_epilogue_vs_reference(cuda):
     from mx_rcnn_amd.ops import need_ext
     from mx_rcnn_amd.ops.conv import _flip_t
     g = torch.Generator().manual_seed(41)
-    for (Cin, Cout, k, H, W, splits) in ((256, 1024, 1, 24, 40, 1), (256, 1024, 1, 24, 40, 4),
-                                         (256, 256, 3, 20, 30, 1), (256, 256, 3, 20, 30, 2)):
+    for (Cin, Cout, k, H, W, splits, tile) in ((256, 1024, 1, 24, 40, 1, 0), (256, 1024, 1, 24, 40, 4, 0),
+                                               (256, 256, 3, 20, 30, 1, 0), (256, 256, 3, 20, 30, 2, 0),
+                                               (256, 1024, 1, 24, 40, 1, 105), (256, 256, 3, 20, 30, 1, 106),
+                                               (256, 256, 3, 20, 30, 1, 109), (256, 1024, 1, 24, 40, 2, 106)):
         w = (torch.randn(Cout, Cin, k, k, generator=g) * 0.05).bfloat16()
         dy = torch.randn(1, Cout, H, W, generator=g).bfloat16()
         xr = torch.randn(1, Cin, H, W, generator=g).bfloat16()
@@ -172,12 +175,12 @@ def test_bnb_epilogue_vs_reference(cuda):
         xhat = (xr.float() - mean[None, :, None, None]) * torch.rsqrt(var + 2e-5)[None, :, None, None]
         ref_dg, ref_db = (gm * xhat).sum(dim=(0, 2, 3)), gm.sum(dim=(0, 2, 3))
         wt = _flip_t(_cl(w, cuda))
-        dx, dgm, dbt = need_ext().conv_igemm_fwd(_cl(dy, cuda), wt, None, 1, k - 1 - p, False, 0, splits,
+        dx, dgm, dbt = need_ext().conv_igemm_fwd(_cl(dy, cuda), wt, None, 1, k - 1 - p, False, tile, splits,
                                                  _cl(dres, cuda), [t.to(cuda) for t in (gamma, beta, mean, var)],
                                                  2e-5, False, True, _cl(xr, cuda), _cl(dadd, cuda))
         for a, r in ((dx, ref_dx), (dgm, ref_dg), (dbt, ref_db)):
             err = (a.float().cpu() - r).abs().max().item()
-            assert err <= 2e-2 * r.abs().max().item() + 2e-2, (Cin, Cout, k, splits, err)
+            assert err <= 2e-2 * r.abs().max().item() + 2e-2, (Cin, Cout, k, splits, tile, err)
 
 
 def test_fused_trunk_step_matches_unfused(cuda):

@@ -272,7 +272,8 @@ def test_conv_igemm_fwd_vs_fp32(cuda, shape):
     if relu:
         ref = torch.relu(ref)
     for tile, splits in ((1, 1), (2, 1), (3, 1), (3, 2), (3, 4), (0, 0), (21, 1), (22, 1), (23, 1), (23, 2), (31, 2),
-                         (33, 1), (12, 1), (16, 2), (24, 1), (25, 1), (24, 2)):
+                         (33, 1), (12, 1), (16, 2), (24, 1), (25, 1), (24, 2)) + \
+            tuple((100 + i, 1) for i in range(12)) + ((105, 2), (106, 4)):
         y = need_ext().conv_igemm_fwd(x.to(cuda).contiguous(memory_format=torch.channels_last),
                                       w.to(cuda).contiguous(memory_format=torch.channels_last),
                                       None if b is None else b.to(cuda), s, p, relu, tile, splits)[0]
@@ -541,3 +542,20 @@ def test_bn_relu_cpu_twin_matches_tensor_path(channels_last, fix_gamma, relu, mo
         assert y.is_contiguous(memory_format=torch.channels_last) == channels_last
     for a, b in zip(*outs):
         assert torch.allclose(a, b, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_conv_autotune_picks_a_candidate_and_matches(cuda, monkeypatch):
+    """The per-shape autotune (first eager call) caches a tile choice; outputs equal the
+    static-plan result bitwise (every candidate accumulates in the same K order)."""
+    from mx_rcnn_amd.ops import need_ext
+    ext = need_ext()
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(1, 256, 38, 61, generator=g).bfloat16().to(cuda).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(256, 256, 3, 3, generator=g) * 0.05).bfloat16().to(cuda).contiguous(
+        memory_format=torch.channels_last)
+    y_tuned = ext.conv_igemm_fwd(x, w, None, 1, 1, False)[0]
+    keys = [k for k, t, s in ext.conv_tune_table() if k.startswith('1,38,61,256,256,3,3,1,1|')]
+    assert len(keys) == 1
+    y_plan = ext.conv_igemm_fwd(x, w, None, 1, 1, False, 23, 1)[0]
+    assert torch.equal(y_tuned, y_plan)

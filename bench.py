@@ -151,7 +151,7 @@ def main():
                'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
                'dtype': 'bf16' if dtype == torch.bfloat16 else 'fp32',
                'data': 'synthetic (random %dx%d images, 1-20 random gt boxes, random-init weights)' % (h, w),
-               'config': {'model': '%s-faster-rcnn-c4' % args.network, 'global_batch': args.ims_per_gpu * world,
+               'config': {'model': '%s-faster-rcnn%s' % (args.network, '-c4' if args.network.startswith('resnet') else ''), 'global_batch': args.ims_per_gpu * world,
                           'seq_len': None, 'image_hw': [h, w], 'num_classes': args.num_classes,
                           'ims_per_gpu': args.ims_per_gpu, 'parallelism': 'dp%d' % world,
                           'rpn_pre_post_nms': [cfg.TRAIN.RPN_PRE_NMS_TOP_N, cfg.TRAIN.RPN_POST_NMS_TOP_N],

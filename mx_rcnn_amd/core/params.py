@@ -128,12 +128,22 @@ class FlatParamStore:
             if g.shadow is None:
                 continue
             for (n, m, attr, numel, shape, cl) in g.entries:
+                p = self.params[n]
+                if len(shape) == 2:  # FullyConnected (out, in): its transpose, for the FC data gradient
+                    o, i = shape
+                    if o % 64 != 0 or i % 64 != 0:
+                        continue
+                    buf = torch.empty((i, o, 1, 1), dtype=p.dtype, device=self.device,
+                                      memory_format=torch.channels_last)
+                    conv_ops.register_dgrad_weight(p, buf)
+                    srcs.append(p.detach().view(o, i, 1, 1))
+                    dsts.append(buf)
+                    continue
                 if len(shape) != 4 or not cl:
                     continue
                 o, i, kh, kw = shape
                 if o % 64 != 0 or i % 8 != 0 or kh != kw:
                     continue
-                p = self.params[n]
                 buf = torch.empty((i, o, kh, kw), dtype=p.dtype, device=self.device,
                                   memory_format=torch.channels_last)
                 conv_ops.register_dgrad_weight(p, buf)

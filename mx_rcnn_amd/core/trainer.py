@@ -39,6 +39,13 @@ class Trainer:
             lr_scheduler.base_lr = lr
         self.lr_t = torch.full((1,), float(lr), dtype=torch.float32, device=dev)
         self.num_update = 0
+        # step counter of the counter-based dropout (ops/fc.py), advanced with the LR tensor so a
+        # replayed graph draws a fresh mask every update
+        self.rng_step = torch.zeros(1, dtype=torch.int64, device=dev)
+        from ..models.layers import Linear
+        for m in self.model.modules():
+            if isinstance(m, Linear):
+                m.rng_step = self.rng_step
         self.nonfinite = torch.zeros((), dtype=torch.int32, device=dev)
         self.fault = torch.ones((), dtype=torch.float32, device=dev) if os.environ.get('MXR_FAULT_INJECT') else None
         # the loss-combine kernel bumps the counter (one launch for loss, objective and guard);
@@ -148,6 +155,7 @@ class Trainer:
 
     def update_lr(self):
         self.num_update += 1
+        self.rng_step.fill_(self.num_update)
         if self.lr_scheduler is not None:
             lr = self.lr_scheduler(self.num_update)
             self.lr_t.fill_(float(lr))

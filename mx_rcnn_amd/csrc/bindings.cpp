@@ -500,7 +500,8 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
                                    c10::optional<Tensor> residual, c10::optional<std::vector<Tensor>> bn,
                                    double bn_eps, bool bn_fix_gamma, bool act_relu, c10::optional<Tensor> bnb_x,
                                    c10::optional<Tensor> dadd, c10::optional<Tensor> dgamma_out,
-                                   c10::optional<Tensor> dbeta_out) {
+                                   c10::optional<Tensor> dbeta_out, double drop_p, int64_t drop_seed,
+                                   c10::optional<Tensor> drop_step) {
   CHECK_DEV(x); CHECK_DEV(w);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "bf16 only");
   TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "x must be channels_last (N,C,H,W)");
@@ -520,6 +521,15 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   }
   DevGuard g(x.device());
   Tensor y = at::empty({NB, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (drop_p > 0.0) {
+    TORCH_CHECK(drop_p < 1.0, "dropout p must be < 1");
+    TORCH_CHECK(drop_step.has_value() && drop_step->defined() && drop_step->scalar_type() == at::kLong &&
+                    drop_step->is_cuda() && drop_step->numel() >= 1,
+                "dropout needs drop_step: an int64 device tensor holding the step");
+    ep.drop_p = (float)drop_p;
+    ep.drop_seed = (uint32_t)drop_seed;
+    ep.drop_step = drop_step->data_ptr<int64_t>();
+  }
   if (residual.has_value() && residual->defined()) {
     const Tensor& r = *residual;
     TORCH_CHECK(r.scalar_type() == at::kBFloat16 && r.sizes() == y.sizes() &&
@@ -578,9 +588,9 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   int sp = splits > 0 ? (int)splits : (bwd_mode ? 1 : auto_splits);
   if (tile <= 0 && splits <= 0 && conv_tune_enabled()) {
     char kb[256];
-    snprintf(kb, sizeof(kb), "%d,%d,%d,%d,%d,%d,%d,%d,%d|%d%d%d%d%d%d", NB, H, W, Cin, Cout, KH, KW, (int)stride,
+    snprintf(kb, sizeof(kb), "%d,%d,%d,%d,%d,%d,%d,%d,%d|%d%d%d%d%d%d%d", NB, H, W, Cin, Cout, KH, KW, (int)stride,
              (int)pad, ep.residual != nullptr, ep.y2 != nullptr || bn.has_value(), bwd_mode, ep.dadd != nullptr,
-             ep.relu, ep.bias != nullptr);
+             ep.relu, ep.bias != nullptr, ep.drop_p > 0.f);
     const std::string key(kb);
     std::unique_lock<std::mutex> lk(g_tune_mu);
     auto it = g_tune.find(key);
@@ -592,6 +602,16 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
       std::vector<std::pair<int, int>> cands = {{t, sp}};
       for (int c : {23, 22, 101, 104, 105, 106, 108, 109, 110, 111})
         if (c != t || sp != 1) cands.push_back({c, 1});
+      // grids far below one tile per CU (the FC head: M = 128 RoIs, K up to 25088): split K
+      const int64_t Mrows = (int64_t)NB * Ho * Wo;
+      const int nkk = KH * KW * (Cin / 64);
+      if (!bwd_mode && Cout % 4 == 0 && ((Mrows + 63) / 64) * ((Cout + 63) / 64) < 128) {
+        for (int c : {23, 22, 106, 109})
+          for (int spl : {2, 4, 8})
+            if (nkk / spl >= 4 && !(c == t && spl == sp)) cands.push_back({c, spl});
+      }
+      int max_sp = sp;
+      for (const auto& c : cands) max_sp = std::max(max_sp, c.second);
       mxr::ConvEpi et = ep;
       Tensor ys = at::empty_like(y, y.options(), at::MemoryFormat::ChannelsLast);
       Tensor y2s, dg2, db2;
@@ -606,7 +626,7 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
         et.bnb_dbeta = db2.data_ptr<float>();
       }
       Tensor slab_t;
-      if (sp > 1) slab_t = at::empty({(int64_t)sp * NB * Ho * Wo * Cout}, x.options().dtype(at::kFloat));
+      if (max_sp > 1) slab_t = at::empty({(int64_t)max_sp * NB * Ho * Wo * Cout}, x.options().dtype(at::kFloat));
       hipStream_t st = cur_stream();
       hipEvent_t e0, e1;
       hipEventCreate(&e0);
@@ -651,6 +671,72 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   if (bwd_mode) return {y, dgm, dbt};
   if (y2.defined()) return {y, y2};
   return {y};
+}
+
+// ---- pooling ---------------------------------------------------------------------------------
+std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t p) {
+  CHECK_DEV(x);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "maxpool: x must be channels_last bf16 (N,C,H,W)");
+  const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  TORCH_CHECK(C % 8 == 0, "maxpool needs C % 8 == 0");
+  const int Ho = (H + 2 * (int)p - (int)k) / (int)s + 1, Wo = (W + 2 * (int)p - (int)k) / (int)s + 1;
+  TORCH_CHECK(Ho > 0 && Wo > 0, "maxpool: empty output");
+  DevGuard g(x.device());
+  Tensor y = at::empty({N, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor arg = at::empty({N, C, Ho, Wo}, x.options().dtype(at::kByte).memory_format(at::MemoryFormat::ChannelsLast));
+  const int rc = mxr::maxpool_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<uint16_t*>(y.data_ptr()),
+                                  arg.data_ptr<uint8_t>(), N, H, W, C, Ho, Wo, (int)k, (int)s, (int)p, cur_stream());
+  TORCH_CHECK(rc == 0, "maxpool_fwd: unsupported shape");
+  return {y, arg};
+}
+
+Tensor maxpool_bwd(const Tensor& dy, const Tensor& arg, int64_t H, int64_t W, int64_t k, int64_t s, int64_t p) {
+  CHECK_DEV(dy); CHECK_DEV(arg);
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  arg.scalar_type() == at::kByte && arg.sizes() == dy.sizes() &&
+                  arg.is_contiguous(at::MemoryFormat::ChannelsLast), "maxpool_bwd: channels_last bf16 dy + byte arg");
+  const int N = (int)dy.size(0), C = (int)dy.size(1), Ho = (int)dy.size(2), Wo = (int)dy.size(3);
+  TORCH_CHECK((H + 2 * p - k) / s + 1 == Ho && (W + 2 * p - k) / s + 1 == Wo, "maxpool_bwd: shape mismatch");
+  DevGuard g(dy.device());
+  Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int rc = mxr::maxpool_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), arg.data_ptr<uint8_t>(),
+                                  reinterpret_cast<uint16_t*>(dx.data_ptr()), N, (int)H, (int)W, C, Ho, Wo, (int)k,
+                                  (int)s, (int)p, cur_stream());
+  TORCH_CHECK(rc == 0, "maxpool_bwd: unsupported shape");
+  return dx;
+}
+
+Tensor avgpool_fwd(const Tensor& x) {
+  CHECK_DEV(x);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "avgpool: x must be channels_last bf16 (N,C,H,W)");
+  const int N = (int)x.size(0), C = (int)x.size(1), HW = (int)(x.size(2) * x.size(3));
+  DevGuard g(x.device());
+  Tensor y = at::empty({N, C}, x.options());
+  TORCH_CHECK(mxr::avgpool_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<uint16_t*>(y.data_ptr()),
+                               N, HW, C, cur_stream()) == 0, "avgpool_fwd: C % 8 != 0");
+  return y;
+}
+
+Tensor avgpool_bwd(const Tensor& dy, int64_t H, int64_t W) {
+  CHECK_DEV(dy);
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.dim() == 2 && dy.is_contiguous(), "avgpool_bwd: dy (N, C) bf16");
+  const int N = (int)dy.size(0), C = (int)dy.size(1);
+  DevGuard g(dy.device());
+  Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  TORCH_CHECK(mxr::avgpool_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<uint16_t*>(dx.data_ptr()),
+                               N, (int)(H * W), C, cur_stream()) == 0, "avgpool_bwd: C % 8 != 0");
+  return dx;
+}
+
+Tensor philox_uniform_cpu(int64_t seed, int64_t step, int64_t n) {
+  Tensor out = at::empty({n}, at::TensorOptions().dtype(at::kFloat));
+  float* o = out.data_ptr<float>();
+  at::parallel_for(0, n, 4096, [&](int64_t b, int64_t e) {
+    for (int64_t i = b; i < e; ++i) o[i] = mxr::philox_uniform_host((uint32_t)seed, (uint64_t)step, (uint64_t)i);
+  });
+  return out;
 }
 
 // ---- training-mode BN ----------------------------------------------------------------------
@@ -1073,7 +1159,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("pad"), py::arg("relu"), py::arg("tile") = 0, py::arg("splits") = 0, py::arg("residual") = py::none(),
         py::arg("bn") = py::none(), py::arg("bn_eps") = 2e-5, py::arg("bn_fix_gamma") = false,
         py::arg("act_relu") = true, py::arg("bnb_x") = py::none(), py::arg("dadd") = py::none(),
-        py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none());
+        py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(), py::arg("drop_p") = 0.0,
+        py::arg("drop_seed") = 0, py::arg("drop_step") = py::none());
+  m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("s"), py::arg("p"));
+  m.def("maxpool_bwd", &maxpool_bwd, py::arg("dy"), py::arg("arg"), py::arg("H"), py::arg("W"), py::arg("k"),
+        py::arg("s"), py::arg("p"));
+  m.def("avgpool_fwd", &avgpool_fwd);
+  m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("philox_uniform", &philox_uniform_cpu, py::arg("seed"), py::arg("step"), py::arg("n"),
+        "host twin of the fused-dropout generator: uniforms of elements 0..n-1 (CPU float tensor)");
   m.def("bn_train_fwd", &bn_train_fwd);
   m.def("bn_train_bwd", &bn_train_bwd, py::arg("x"), py::arg("dy"), py::arg("gamma"), py::arg("beta"),
         py::arg("save_mean"), py::arg("save_invstd"), py::arg("fix_gamma"), py::arg("relu"), py::arg("need_dx"),

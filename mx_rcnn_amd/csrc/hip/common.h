@@ -63,6 +63,27 @@ __device__ __forceinline__ float iou_plus1(float ax1, float ay1, float ax2, floa
   return inter / (aarea + barea - inter);
 }
 
+// Philox-4x32-10 (Salmon et al. 2011), the counter-based generator behind the fused dropout:
+// key = (seed, 0x9E3779B9), counter = (lo(e), hi(e), lo(step), hi(step)); returns the first
+// output word as a uniform in [0, 1) with 24 bits of resolution.  Pure function of its inputs,
+// so every epilogue path (vector, scalar, split-K reduce) and the host twin agree bit for bit.
+__host__ __device__ __forceinline__ float philox_uniform(uint32_t seed, uint64_t step, uint64_t e) {
+  uint32_t c0 = (uint32_t)e, c1 = (uint32_t)(e >> 32), c2 = (uint32_t)step, c3 = (uint32_t)(step >> 32);
+  uint32_t k0 = seed, k1 = 0x9E3779B9u;
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint64_t p0 = (uint64_t)0xD2511F53u * c0, p1 = (uint64_t)0xCD9E8D57u * c2;
+    const uint32_t h0 = (uint32_t)(p0 >> 32), l0 = (uint32_t)p0, h1 = (uint32_t)(p1 >> 32), l1 = (uint32_t)p1;
+    c0 = h1 ^ c1 ^ k0;
+    c1 = l1;
+    c2 = h0 ^ c3 ^ k1;
+    c3 = l0;
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return (float)(c0 >> 8) * (1.0f / 16777216.0f);
+}
+
 inline int div_up(int64_t a, int64_t b) { return static_cast<int>((a + b - 1) / b); }
 
 }  // namespace mxr

@@ -59,11 +59,21 @@ __device__ __forceinline__ EpiCol epi_col(const ConvEpi& ep, int n) {
   return c;
 }
 
+// fused inverted dropout of output element `idx` (see ConvEpi::drop_p)
+__device__ __forceinline__ float epi_dropout(const ConvEpi& ep, int64_t idx, float v) {
+  if (ep.drop_p > 0.f) {
+    const float u = philox_uniform(ep.drop_seed, (uint64_t)*ep.drop_step, (uint64_t)idx);
+    v = u >= ep.drop_p ? v * (1.f / (1.f - ep.drop_p)) : 0.f;
+  }
+  return v;
+}
+
 __device__ __forceinline__ void epi_store(const ConvEpi& ep, const EpiCol& c, uint16_t* __restrict__ y, int64_t idx,
                                           float v) {
   v += c.bias;
   if (ep.residual) v += bf16_to_f32(ep.residual[idx]);
   if (ep.relu) v = fmaxf(v, 0.f);
+  v = epi_dropout(ep, idx, v);
   const uint16_t yb = f32_to_bf16(v);
   y[idx] = yb;
   if (ep.y2) {
@@ -275,6 +285,7 @@ __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* 
     for (int k = 0; k < 8; ++k) {
       float t = a[k] + ec[k].bias + (ep.residual ? rs[k] : 0.f);
       if (ep.relu) t = fmaxf(t, 0.f);
+      t = epi_dropout(ep, e + k, t);
       yb[k] = f32_to_bf16(t);
       float q = bf16_to_f32(yb[k]) * ec[k].s + ec[k].t;  // the BN reads the STORED conv output
       if (ep.act_relu) q = fmaxf(q, 0.f);
@@ -490,6 +501,7 @@ splitk_reduce_kernel(const float* __restrict__ slab, int splits, int64_t MN, int
     const EpiCol c = epi_col(ep, n + k);
     float t = v[k] + c.bias + res[k];
     if (ep.relu) t = fmaxf(t, 0.f);
+    t = epi_dropout(ep, e + k, t);
     out[k] = f32_to_bf16(t);
     float q = bf16_to_f32(out[k]) * c.s + c.t;
     if (ep.act_relu) q = fmaxf(q, 0.f);
@@ -1131,6 +1143,7 @@ __device__ __forceinline__ void ring_epilogue(f32x4 (&acc)[TM][TN], float* __res
     for (int k = 0; k < 8; ++k) {
       float t = a[k] + ec[k].bias + (ep.residual ? rs[k] : 0.f);
       if (ep.relu) t = fmaxf(t, 0.f);
+      t = epi_dropout(ep, e + k, t);
       yb[k] = f32_to_bf16(t);
       float qv = bf16_to_f32(yb[k]) * ec[k].s + ec[k].t;
       if (ep.act_relu) qv = fmaxf(qv, 0.f);
@@ -1419,6 +1432,8 @@ static void launch_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB
       splitk_reduce_kernel<<<div_up((MN + 3) / 4, 256), 256, 0, st>>>(slab, splits, MN, Cout, ep, y);
   }
 }
+
+float philox_uniform_host(uint32_t seed, uint64_t step, uint64_t e) { return philox_uniform(seed, step, e); }
 
 int conv_igemm_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int tile, int* splits_out) {
   const int64_t M = (int64_t)NB * Ho * Wo;

@@ -164,7 +164,15 @@ struct ConvEpi {
   const uint16_t* dadd = nullptr;
   float* bnb_dgamma = nullptr;
   float* bnb_dbeta = nullptr;
+  // inverted dropout AFTER bias/residual/ReLU (the FC head's ReLU -> Dropout, rcnn/symbol.py:98,102):
+  // element e of step s is kept iff philox_uniform(drop_seed, s, e) >= drop_p, kept values are
+  // scaled by 1 / (1 - drop_p).  The step is read from device memory (graph replay safe).
+  float drop_p = 0.f;
+  uint32_t drop_seed = 0;
+  const int64_t* drop_step = nullptr;
 };
+// counter-based uniform in [0, 1) (Philox-4x32-10, key = (seed, 0x9E3779B9), counter = (e, s))
+float philox_uniform_host(uint32_t seed, uint64_t step, uint64_t e);
 int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho, int Wo,
                    int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int tile, int splits, float* slab,
                    hipStream_t st);
@@ -180,6 +188,15 @@ int bn_train_fwd(const uint16_t* x, int64_t M, int C, const float* gamma, const 
 int bn_train_bwd(const uint16_t* x, const uint16_t* dy, int64_t M, int C, const float* gamma, const float* beta,
                  const float* save_mean, const float* save_invstd, int fix_gamma, int relu, uint16_t* dx,
                  float* dgamma, float* dbeta, int accumulate, float* workspace, hipStream_t st);
+
+// ---- pooling (pool.hip): NHWC bf16, C % 8 == 0 ------------------------------------------------
+// arg: one byte per output element, the winning tap (i * k + j) of its window
+int maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int Ho, int Wo, int k,
+                int s, int p, hipStream_t st);
+int maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int H, int W, int C, int Ho, int Wo,
+                int k, int s, int p, hipStream_t st);
+int avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st);
+int avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st);
 
 // Flip + transpose many conv filters in ONE launch (dgrad operand cache):
 //   dst[i][r][s][o] = src[o][KH-1-r][KW-1-s][i]   (both channels_last, i.e. (O,KH,KW,I) rows)

@@ -15,6 +15,8 @@ import torch.nn.functional as F
 
 from ..ops.bn import frozen_bn_relu, train_bn_eligible, train_bn_relu
 from ..ops.conv import conv2d
+from ..ops.fc import fully_connected, layer_seed
+from ..ops.pool import max_pool2d
 
 
 class MxLayer(nn.Module):
@@ -47,7 +49,9 @@ class Conv(MxLayer):
 
 
 class Linear(MxLayer):
-    """MXNet FullyConnected: flattens all but dim 0, y = x W^T + b."""
+    """MXNet FullyConnected: flattens all but dim 0, y = x W^T + b; optionally fused with the
+    following ReLU and Dropout (ops/fc.py).  ``rng_step`` (an int64 device tensor set by the
+    Trainer and advanced every update) drives the counter-based dropout mask."""
 
     def __init__(self, name, cin, cout, bias=True):
         super().__init__()
@@ -55,11 +59,15 @@ class Linear(MxLayer):
         self.weight = nn.Parameter(torch.empty(cout, cin))
         self.bias = nn.Parameter(torch.zeros(cout)) if bias else None
         nn.init.normal_(self.weight, 0, 0.01)
+        self.rng_step = None
+        self._seed = None
 
-    def forward(self, x):
+    def forward(self, x, relu=False, drop_p=0.0):
         x = x.reshape(x.shape[0], -1)
         b = None if self.bias is None else _w(self.bias, x)
-        return F.linear(x, _w(self.weight, x), b)
+        if drop_p and self.training and self._seed is None:
+            self._seed = layer_seed(self.mx_name)
+        return fully_connected(x, _w(self.weight, x), b, relu, drop_p, self._seed or 0, self.rng_step, self.training)
 
 
 class BatchNorm(MxLayer):
@@ -110,4 +118,4 @@ class BatchNorm(MxLayer):
 
 
 def max_pool(x, k, s, p=0):
-    return F.max_pool2d(x, kernel_size=k, stride=s, padding=p)
+    return max_pool2d(x, k, s, p)

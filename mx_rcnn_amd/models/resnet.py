@@ -10,6 +10,7 @@ import torch.nn as nn
 
 from ..ops.conv import igemm_eligible
 from ..ops.fused import conv_add, conv_add_bn_relu, conv_bn_relu, fused_unit
+from ..ops.pool import global_avg_pool
 from .layers import BatchNorm, Conv, Linear, max_pool
 
 
@@ -200,5 +201,5 @@ class ResNetHead(nn.Module):
 
     def forward(self, pooled):
         x = self.bn1(run_stage(self.stage4, pooled))  # fused when the BNs are frozen (test time)
-        x = torch.mean(x, dim=(2, 3))
+        x = global_avg_pool(x)
         return self.cls_score(x), self.bbox_pred(x)

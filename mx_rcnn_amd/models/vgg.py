@@ -4,7 +4,6 @@
 RoIPool 7x7 @ 1/16 -> fc6 4096 -> ReLU -> Dropout .5 -> fc7 -> ReLU -> Dropout -> cls/bbox.
 """
 import torch.nn as nn
-import torch.nn.functional as F
 
 from .layers import Conv, Linear, max_pool
 
@@ -50,6 +49,7 @@ class VGGHead(nn.Module):
 
     def forward(self, pooled):
         x = pooled.reshape(pooled.shape[0], -1)  # MXNet Flatten: (C, H, W) order
-        x = F.dropout(F.relu(self.fc6(x), inplace=True), self.dropout, self.training)
-        x = F.dropout(F.relu(self.fc7(x), inplace=True), self.dropout, self.training)
+        # relu6/drop6 and relu7/drop7 run in the FC kernel's epilogue (ops/fc.py)
+        x = self.fc6(x, relu=True, drop_p=self.dropout)
+        x = self.fc7(x, relu=True, drop_p=self.dropout)
         return self.cls_score(x), self.bbox_pred(x)

@@ -42,6 +42,12 @@ def register_dgrad_weight(param, buf):
     _DGRAD_W[id(param)] = (param, buf)
 
 
+def cached_dgrad_weight(param):
+    """The cached flipped / transposed filter of ``param`` or None."""
+    ent = _DGRAD_W.get(id(param)) if param is not None else None
+    return ent[1] if ent is not None and ent[0] is param else None
+
+
 def dgrad_weight(param, w):
     ent = _DGRAD_W.get(id(param)) if param is not None else None
     if ent is not None and ent[0] is param:

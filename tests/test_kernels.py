@@ -559,3 +559,88 @@ def test_conv_autotune_picks_a_candidate_and_matches(cuda, monkeypatch):
     assert len(keys) == 1
     y_plan = ext.conv_igemm_fwd(x, w, None, 1, 1, False, 23, 1)[0]
     assert torch.equal(y_tuned, y_plan)
+
+
+def test_philox_host_twin_statistics():
+    """The counter-based dropout generator: deterministic, uniform, distinct per step and seed."""
+    from mx_rcnn_amd.ops import need_ext
+    ext = need_ext()
+    u = ext.philox_uniform(7, 3, 1 << 16)
+    assert torch.equal(u, ext.philox_uniform(7, 3, 1 << 16))
+    assert 0.0 <= u.min().item() and u.max().item() < 1.0
+    assert abs(u.mean().item() - 0.5) < 0.01 and abs((u < 0.5).float().mean().item() - 0.5) < 0.01
+    assert (u != ext.philox_uniform(7, 4, 1 << 16)).float().mean() > 0.99
+    assert (u != ext.philox_uniform(8, 3, 1 << 16)).float().mean() > 0.99
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('M,K,N,relu,drop', [(128, 25088, 4096, True, 0.5), (128, 4096, 4096, True, 0.5),
+                                             (128, 4096, 21, False, 0.0), (300, 2048, 324, False, 0.0),
+                                             (96, 512, 256, True, 0.0)])
+def test_fc_fused_vs_fp32(cuda, M, K, N, relu, drop):
+    """FullyConnected on the MFMA kernel (+bias, ReLU, Philox dropout) and its backward vs fp32 torch
+    with the same mask (host twin of the generator)."""
+    from mx_rcnn_amd.ops import need_ext
+    from mx_rcnn_amd.ops.fc import _FC
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(M, K, generator=g).bfloat16()
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).bfloat16()
+    b = torch.randn(N, generator=g).bfloat16()
+    step = torch.tensor([11], dtype=torch.int64, device=cuda)
+    xg = x.to(cuda).requires_grad_(True)
+    wg = w.to(cuda).requires_grad_(True)
+    bg = b.to(cuda).requires_grad_(True)
+    y = _FC.apply(xg, wg, bg, relu, drop, 1234, step)
+    ref = x.float() @ w.float().t() + b.float()
+    if relu:
+        ref = torch.relu(ref)
+    mask = torch.ones(M, N)
+    if drop > 0:
+        mask = (need_ext().philox_uniform(1234, 11, M * N).view(M, N) >= drop).float() / (1 - drop)
+    ref = ref * mask
+    err = (y.float().cpu() - ref).abs().max().item()
+    assert err <= 2e-2 * ref.abs().max().item() + 2e-2, err
+    dy = torch.randn(M, N, generator=g).bfloat16()
+    y.backward(dy.to(cuda))
+    xr, wr, br = x.float().requires_grad_(True), w.float().requires_grad_(True), b.float().requires_grad_(True)
+    r = xr @ wr.t() + br
+    if relu:
+        r = torch.relu(r)
+    (r * mask).backward(dy.float())
+    for got, want in ((xg.grad, xr.grad), (wg.grad, wr.grad), (bg.grad, br.grad)):
+        e = (got.float().cpu() - want).abs().max().item()
+        assert e <= 3e-2 * want.abs().max().item() + 3e-2, (e, want.abs().max().item())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('N,C,H,W,k,s,p', [(1, 64, 61, 97, 2, 2, 0), (1, 512, 75, 125, 2, 2, 0),
+                                           (1, 64, 400, 667, 3, 2, 1), (2, 16, 9, 14, 3, 2, 1)])
+def test_maxpool_vs_torch(cuda, N, C, H, W, k, s, p):
+    from mx_rcnn_amd.ops.pool import max_pool2d
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(N, C, H, W, generator=g).bfloat16()
+    xg = x.to(cuda).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    y = max_pool2d(xg, k, s, p)
+    xr = x.float().requires_grad_(True)
+    ref = F.max_pool2d(xr, k, s, p)
+    assert torch.equal(y.float().cpu(), ref.detach())
+    dy = torch.randn(ref.shape, generator=g).bfloat16()
+    y.backward(dy.to(cuda).contiguous(memory_format=torch.channels_last))
+    ref.backward(dy.float())
+    assert (xg.grad.float().cpu() - xr.grad).abs().max().item() <= 2e-2 * xr.grad.abs().max().item()
+
+
+@pytest.mark.gpu
+def test_global_avgpool_vs_torch(cuda):
+    from mx_rcnn_amd.ops.pool import global_avg_pool
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(128, 2048, 4, 4, generator=g).bfloat16()
+    xg = x.to(cuda).contiguous(memory_format=torch.channels_last).requires_grad_(True)
+    y = global_avg_pool(xg)
+    xr = x.float().requires_grad_(True)
+    ref = xr.mean(dim=(2, 3))
+    assert (y.float().cpu() - ref.detach()).abs().max().item() <= 1e-2
+    dy = torch.randn(128, 2048, generator=g).bfloat16()
+    y.backward(dy.to(cuda))
+    ref.backward(dy.float())
+    assert (xg.grad.float().cpu() - xr.grad).abs().max().item() <= 1e-2

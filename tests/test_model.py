@@ -1,4 +1,5 @@
 """Model families, parameter naming (SURVEY §2.12 counts), trainer step on CPU."""
+import math
 import pytest
 import torch
 
@@ -153,3 +154,24 @@ def test_graph_capture_has_no_training_side_effects(cuda):
         assert sh is None or torch.equal(g.shadow, sh)
     for buf, v in zip(tr.model.buffers(), before['buffers']):
         assert torch.equal(buf, v)
+
+
+@pytest.mark.gpu
+def test_vgg16_e2e_step_gpu_graph(cuda):
+    """VGG16 end-to-end step on the GPU path (MFMA convs, HIP max-pool, fused FC + ReLU + dropout)
+    eager then graph-replayed: finite loss, and dropout draws a new mask every update."""
+    from mx_rcnn_amd.core.trainer import GraphedStep
+    torch.manual_seed(0)
+    m = FasterRCNN('vgg16', 21, cfg=_cfg())
+    tr = Trainer(m, 'e2e', fixed_param_prefix=['conv1', 'conv2'], lr=0.001, device=cuda)
+    b = {k: v.to(cuda) for k, v in _batch(320, 480).items()}
+    out = tr.step(b)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out['loss'])
+    g = GraphedStep(tr, b, warmup=2)
+    losses = []
+    for _ in range(3):
+        o = g(b)
+        losses.append(float(o['loss'].float().item()))
+    assert all(math.isfinite(v) for v in losses)
+    assert int(tr.rng_step.item()) == tr.num_update

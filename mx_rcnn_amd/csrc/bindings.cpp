@@ -501,7 +501,8 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
                                    double bn_eps, bool bn_fix_gamma, bool act_relu, c10::optional<Tensor> bnb_x,
                                    c10::optional<Tensor> dadd, c10::optional<Tensor> dgamma_out,
                                    c10::optional<Tensor> dbeta_out, double drop_p, int64_t drop_seed,
-                                   c10::optional<Tensor> drop_step) {
+                                   c10::optional<Tensor> drop_step, int64_t pad_w, c10::optional<Tensor> out,
+                                   c10::optional<std::vector<int64_t>> out_map) {
   CHECK_DEV(x); CHECK_DEV(w);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "bf16 only");
   TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "x must be channels_last (N,C,H,W)");
@@ -510,9 +511,26 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   const int Cout = (int)w.size(0), KH = (int)w.size(2), KW = (int)w.size(3);
   TORCH_CHECK(w.size(1) == Cin, "channel mismatch");
   TORCH_CHECK(Cin % 64 == 0, "conv_igemm requires Cin % 64 == 0");
-  const int Ho = (H + 2 * (int)pad - KH) / (int)stride + 1, Wo = (W + 2 * (int)pad - KW) / (int)stride + 1;
+  const int padw = pad_w >= 0 ? (int)pad_w : (int)pad;
+  int Ho = (H + 2 * (int)pad - KH) / (int)stride + 1, Wo = (W + 2 * padw - KW) / (int)stride + 1;
   mxr::ConvEpi ep;
   ep.relu = relu ? 1 : 0;
+  ep.pad_w = pad_w >= 0 ? (int)pad_w : -1;
+  const bool mapped = out_map.has_value();
+  if (mapped) {
+    // out_map = (Ho, Wo, o_H, o_W, o_sh, o_sw, o_ph, o_pw): this launch computes an Ho x Wo grid and
+    // scatters it into `out` (N, Cout, o_H, o_W) at rows (i*o_sh + o_ph, j*o_sw + o_pw)
+    const auto& om = *out_map;
+    TORCH_CHECK(om.size() == 8, "out_map = (Ho, Wo, o_H, o_W, o_sh, o_sw, o_ph, o_pw)");
+    Ho = (int)om[0];
+    Wo = (int)om[1];
+    ep.omap = 1;
+    ep.o_H = (int)om[2]; ep.o_W = (int)om[3]; ep.o_sh = (int)om[4]; ep.o_sw = (int)om[5];
+    ep.o_ph = (int)om[6]; ep.o_pw = (int)om[7];
+    TORCH_CHECK(Ho > 0 && Wo > 0 && (Ho - 1) * ep.o_sh + ep.o_ph < ep.o_H && (Wo - 1) * ep.o_sw + ep.o_pw < ep.o_W,
+                "out_map: the grid does not fit the output map");
+    TORCH_CHECK(out.has_value() && out->defined(), "out_map needs out");
+  }
   Tensor b;
   if (bias.has_value() && bias->defined()) {
     b = bias->to(at::kFloat).contiguous();
@@ -520,7 +538,15 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
     ep.bias = b.data_ptr<float>();
   }
   DevGuard g(x.device());
-  Tensor y = at::empty({NB, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor y;
+  if (mapped) {
+    y = *out;
+    TORCH_CHECK(y.scalar_type() == at::kBFloat16 && y.is_contiguous(at::MemoryFormat::ChannelsLast) && y.dim() == 4 &&
+                    y.size(0) == NB && y.size(1) == Cout && y.size(2) == ep.o_H && y.size(3) == ep.o_W,
+                "out must be a channels_last bf16 (N, Cout, o_H, o_W) tensor");
+  } else {
+    y = at::empty({NB, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  }
   if (drop_p > 0.0) {
     TORCH_CHECK(drop_p < 1.0, "dropout p must be < 1");
     TORCH_CHECK(drop_step.has_value() && drop_step->defined() && drop_step->scalar_type() == at::kLong &&
@@ -586,7 +612,11 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   int t = mxr::conv_igemm_plan(NB, Ho, Wo, Cin, Cout, KH, KW, (int)tile, &auto_splits);
   // BN-backward epilogue: no split-K by default (the statistics are reduced in-tile instead)
   int sp = splits > 0 ? (int)splits : (bwd_mode ? 1 : auto_splits);
-  if (tile <= 0 && splits <= 0 && conv_tune_enabled()) {
+  if (mapped || ep.pad_w >= 0) {  // geometry extensions: buffer / ring kernels, no split-K
+    if (!(t == 22 || t == 23 || t >= 100)) t = 23;
+    sp = 1;
+  }
+  if (tile <= 0 && splits <= 0 && !mapped && ep.pad_w < 0 && conv_tune_enabled()) {
     char kb[256];
     snprintf(kb, sizeof(kb), "%d,%d,%d,%d,%d,%d,%d,%d,%d|%d%d%d%d%d%d%d", NB, H, W, Cin, Cout, KH, KW, (int)stride,
              (int)pad, ep.residual != nullptr, ep.y2 != nullptr || bn.has_value(), bwd_mode, ep.dadd != nullptr,
@@ -628,10 +658,13 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
       Tensor slab_t;
       if (max_sp > 1) slab_t = at::empty({(int64_t)max_sp * NB * Ho * Wo * Cout}, x.options().dtype(at::kFloat));
       hipStream_t st = cur_stream();
+      // time in isolation: work still queued on other streams (the side-stream weight gradients)
+      // would otherwise share the CUs with the candidates and randomise the choice
+      hipDeviceSynchronize();
       hipEvent_t e0, e1;
       hipEventCreate(&e0);
       hipEventCreate(&e1);
-      float best = 1e30f;
+      float best = 1e30f, plan_ms = 1e30f;
       std::pair<int, int> pick = {t, sp};
       for (const auto& c : cands) {
         float* sl = c.second > 1 ? slab_t.data_ptr<float>() : nullptr;
@@ -643,16 +676,20 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
         };
         if (run() != c.first) continue;  // fell back to another variant: not this candidate
         hipEventRecord(e0, st);
-        for (int r = 0; r < 3; ++r) run();
+        for (int r = 0; r < 5; ++r) run();
         hipEventRecord(e1, st);
         hipEventSynchronize(e1);
         float ms = 0.f;
         hipEventElapsedTime(&ms, e0, e1);
-        if (ms < best * 0.98f) {  // prefer the earlier (static-plan) candidate on near ties
+        if (c == cands[0]) plan_ms = ms;
+        if (ms < best) {
           best = ms;
           pick = c;
         }
       }
+      // leave the static plan only for a clear win: near ties measured in isolation did not
+      // survive the concurrent streams of the real step (profiles/r2_conv_tune_choices.txt)
+      if (best > 0.9f * plan_ms) pick = cands[0];
       hipEventDestroy(e0);
       hipEventDestroy(e1);
       g_tune[key] = pick;
@@ -1160,7 +1197,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("bn") = py::none(), py::arg("bn_eps") = 2e-5, py::arg("bn_fix_gamma") = false,
         py::arg("act_relu") = true, py::arg("bnb_x") = py::none(), py::arg("dadd") = py::none(),
         py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(), py::arg("drop_p") = 0.0,
-        py::arg("drop_seed") = 0, py::arg("drop_step") = py::none());
+        py::arg("drop_seed") = 0, py::arg("drop_step") = py::none(), py::arg("pad_w") = -1,
+        py::arg("out") = py::none(), py::arg("out_map") = py::none());
   m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("s"), py::arg("p"));
   m.def("maxpool_bwd", &maxpool_bwd, py::arg("dy"), py::arg("arg"), py::arg("H"), py::arg("W"), py::arg("k"),
         py::arg("s"), py::arg("p"));

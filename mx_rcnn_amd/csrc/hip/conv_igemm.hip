@@ -37,6 +37,14 @@ constexpr int BK = 64;  // bf16 elements per K-step (one 128-B row per tile row)
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
 
+// output row of GEMM row m (identity unless the epilogue scatters to a parity class, ConvEpi::omap)
+__device__ __forceinline__ int64_t epi_row(const ConvEpi& ep, int m, int Ho, int Wo) {
+  if (!ep.omap) return m;
+  const int hw = Ho * Wo;
+  const int img = m / hw, r = m - img * hw, i = r / Wo, j = r - (r / Wo) * Wo;
+  return ((int64_t)img * ep.o_H + i * ep.o_sh + ep.o_ph) * ep.o_W + j * ep.o_sw + ep.o_pw;
+}
+
 // per-output-channel epilogue constants
 struct EpiCol {
   float bias, s, t, mean, inv;
@@ -101,7 +109,7 @@ __device__ __forceinline__ void epi_bnb(const ConvEpi& ep, const EpiCol& c, uint
 template <int TM, int TN, int WM, int WN>
 __device__ __forceinline__ void igemm_epilogue(f32x4 (&acc)[TM][TN], int m0, int n0, int wm, int wn, int lane, int M,
                                                int Cout, const ConvEpi& ep, uint16_t* __restrict__ y, int split,
-                                               int splits, float* __restrict__ slab) {
+                                               int splits, float* __restrict__ slab, int Ho = 1, int Wo = 1) {
   if (splits > 1) {  // fp32 partial slab; bias/ReLU/cast happen in the reduce kernel
     float* sp = slab + (int64_t)split * M * Cout;
 #pragma unroll
@@ -132,7 +140,7 @@ __device__ __forceinline__ void igemm_epilogue(f32x4 (&acc)[TM][TN], int m0, int
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
-            if (m < M) epi_bnb(ep, ec, y, (int64_t)m * Cout + n, acc[i][j][r], sg, sgx);
+            if (m < M) epi_bnb(ep, ec, y, epi_row(ep, m, Ho, Wo) * Cout + n, acc[i][j][r], sg, sgx);
           }
       }
       sg += __shfl_xor(sg, 16, 64);
@@ -156,7 +164,7 @@ __device__ __forceinline__ void igemm_epilogue(f32x4 (&acc)[TM][TN], int m0, int
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
-        if (m < M) epi_store(ep, ec, y, (int64_t)m * Cout + n, acc[i][j][r]);
+        if (m < M) epi_store(ep, ec, y, epi_row(ep, m, Ho, Wo) * Cout + n, acc[i][j][r]);
       }
     }
   }
@@ -173,7 +181,7 @@ template <int BM, int BN, int TM, int TN, int WM, int WN>
 __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* __restrict__ T, int m0, int n0, int wm,
                                                    int wn, int lane, int tid, int M, int Cout, const ConvEpi& ep,
                                                    uint16_t* __restrict__ y, int split, int splits,
-                                                   float* __restrict__ slab) {
+                                                   float* __restrict__ slab, int Ho = 1, int Wo = 1) {
   constexpr int LDT = BN + 4;      // fp32 row stride of the staged tile
   constexpr int VPR = BN / 8;      // 8-column vectors per row
   constexpr int NV = BM * VPR / 256;  // vectors per thread
@@ -213,7 +221,7 @@ __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* 
     for (int v = 0; v < NV; ++v) {
       const int row = (tid + v * 256) / VPR, m = m0 + row;
       if (m >= M || !ncol) continue;
-      const int64_t e = (int64_t)m * Cout + n;
+      const int64_t e = epi_row(ep, m, Ho, Wo) * Cout + n;
       float a[8], xv[8], d[8], rs[8];
       const float4* src = reinterpret_cast<const float4*>(T + row * LDT + cv * 8);
       const float4 a0 = src[0], a1 = src[1];
@@ -273,7 +281,7 @@ __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* 
   for (int v = 0; v < NV; ++v) {
     const int row = (tid + v * 256) / VPR, m = m0 + row;
     if (m >= M || !ncol) continue;
-    const int64_t e = (int64_t)m * Cout + n;
+    const int64_t e = epi_row(ep, m, Ho, Wo) * Cout + n;
     const float4* src = reinterpret_cast<const float4*>(T + row * LDT + cv * 8);
     const float4 a0 = src[0], a1 = src[1];
     float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
@@ -726,7 +734,7 @@ conv_igemm_buf_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
     a_mask[i] = 0;
     if (m < M) {
       const int img = m / (Ho * Wo), rem = m % (Ho * Wo);
-      const int hi0 = (rem / Wo) * stride - pad, wi0 = (rem % Wo) * stride - pad;
+      const int hi0 = (rem / Wo) * stride - pad, wi0 = (rem % Wo) * stride - (ep.pad_w >= 0 ? ep.pad_w : pad);
       a_off[i] = (uint32_t)(((((int64_t)img * H + hi0) * W + wi0) * Cin + lc * 8) * 2);
       for (int fr = 0; fr < KH; ++fr)
         for (int fc = 0; fc < KW; ++fc)
@@ -813,9 +821,9 @@ conv_igemm_buf_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
   static_assert(BM * (BN + 4) * 4 <= S * (BM + BN) * BK * 2, "epilogue tile must fit the operand ring");
   if (Cout % 8 == 0)
     igemm_epilogue_lds<BM, BN, TM, TN, WM, WN>(acc, reinterpret_cast<float*>(lds), m0, n0, wm, wn, lane, tid, M, Cout,
-                                               ep, y, split, splits, slab);
+                                               ep, y, split, splits, slab, Ho, Wo);
   else
-    igemm_epilogue<TM, TN, WM, WN>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab);
+    igemm_epilogue<TM, TN, WM, WN>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab, Ho, Wo);
 }
 
 // ---- intra-workgroup split-K variant (tile codes 26 / 27; experimental, not in the plan) -----
@@ -871,7 +879,7 @@ conv_igemm_bufks_kernel(const uint16_t* __restrict__ x, const uint16_t* __restri
     a_mask[i] = 0;
     if (m < M) {
       const int img = m / (Ho * Wo), rem = m % (Ho * Wo);
-      const int hi0 = (rem / Wo) * stride - pad, wi0 = (rem % Wo) * stride - pad;
+      const int hi0 = (rem / Wo) * stride - pad, wi0 = (rem % Wo) * stride - (ep.pad_w >= 0 ? ep.pad_w : pad);
       a_off[i] = (uint32_t)(((((int64_t)img * H + hi0) * W + wi0) * Cin + lc * 8) * 2);
       for (int fr = 0; fr < KH; ++fr)
         for (int fc = 0; fc < KW; ++fc)
@@ -1032,7 +1040,7 @@ template <int BM, int BN, int TM, int TN, int NT>
 __device__ __forceinline__ void ring_epilogue(f32x4 (&acc)[TM][TN], float* __restrict__ T, int m0, int n0, int wm,
                                               int wn, int lane, int tid, int M, int Cout, const ConvEpi& ep,
                                               uint16_t* __restrict__ y, int split, int splits,
-                                              float* __restrict__ slab) {
+                                              float* __restrict__ slab, int Ho = 1, int Wo = 1) {
   constexpr int LDT = BN + 4;
   constexpr int VPR = BN / 8;
   constexpr int NVEC = BM * VPR;
@@ -1073,7 +1081,7 @@ __device__ __forceinline__ void ring_epilogue(f32x4 (&acc)[TM][TN], float* __res
     for (int q = tid; q < NVEC; q += NT) {
       const int row = q / VPR, m = m0 + row;
       if (m >= M || !ncol) continue;
-      const int64_t e = (int64_t)m * Cout + n;
+      const int64_t e = epi_row(ep, m, Ho, Wo) * Cout + n;
       float a[8], xv[8], d[8], rs[8];
       const float4* src = reinterpret_cast<const float4*>(T + row * LDT + cv * 8);
       const float4 a0 = src[0], a1 = src[1];
@@ -1131,7 +1139,7 @@ __device__ __forceinline__ void ring_epilogue(f32x4 (&acc)[TM][TN], float* __res
   for (int q = tid; q < NVEC; q += NT) {
     const int row = q / VPR, m = m0 + row;
     if (m >= M || !ncol) continue;
-    const int64_t e = (int64_t)m * Cout + n;
+    const int64_t e = epi_row(ep, m, Ho, Wo) * Cout + n;
     const float4* src = reinterpret_cast<const float4*>(T + row * LDT + cv * 8);
     const float4 a0 = src[0], a1 = src[1];
     float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
@@ -1201,7 +1209,7 @@ conv_ring_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
       const int m = m0 + row;
       if (m < M) {
         const int img = m / (Ho * Wo), rem = m % (Ho * Wo);
-        const int hi0 = (rem / Wo) * stride - pad, wi0 = (rem % Wo) * stride - pad;
+        const int hi0 = (rem / Wo) * stride - pad, wi0 = (rem % Wo) * stride - (ep.pad_w >= 0 ? ep.pad_w : pad);
         off[j] = (uint32_t)(((((int64_t)img * H + hi0) * W + wi0) * Cin + lc * 8) * 2);
         if (!ONE) {
           for (int fr = 0; fr < KH; ++fr)
@@ -1292,9 +1300,9 @@ conv_ring_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
   }
   if (Cout % 8 == 0)
     ring_epilogue<BM, BN, TM, TN, NT>(acc, reinterpret_cast<float*>(lds), m0, n0, wm, wn, lane, tid, M, Cout, ep, y,
-                                      split, splits, slab);
+                                      split, splits, slab, Ho, Wo);
   else
-    igemm_epilogue<TM, TN, 16 * TM, 16 * TN>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab);
+    igemm_epilogue<TM, TN, 16 * TM, 16 * TN>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab, Ho, Wo);
 }
 
 // ring configurations (tile codes 100 + index)
@@ -1335,7 +1343,7 @@ static void launch_ring(const uint16_t* x, const uint16_t* w, uint16_t* y, int N
   const int tiles_m = (M + C::BM - 1) / C::BM, tiles_n = (Cout + C::BN - 1) / C::BN;
   const int ntiles = tiles_m * tiles_n;
   const int nwg = ntiles * splits;
-  if (KH == 1 && KW == 1 && pad == 0)
+  if (KH == 1 && KW == 1 && pad == 0 && ep.pad_w <= 0)
     conv_ring_kernel<TM, TN, WGM, WGN, SFIX, true><<<nwg, C::NT, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW,
                                                                     stride, pad, ep, tiles_n, nwg, ntiles, splits, slab);
   else
@@ -1477,6 +1485,7 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
   if ((ep.y2 || ep.bnb_x) && (!ep.bn_beta || !ep.bn_mean || !ep.bn_var || (!ep.bn_fix_gamma && !ep.bn_gamma)))
     return -1;
   if (ep.y2 && ep.bnb_x) return -1;
+  if ((ep.omap || ep.pad_w >= 0) && (splits > 1 || !(tile == 22 || tile == 23 || tile >= 100))) return -1;
   // buffer variants: 32-bit byte offsets below the kBufOOB sentinel, tap mask of 64 bits
   if (tile >= 100 && ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB ||
                       (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kBufOOB || KH * KW > 64))

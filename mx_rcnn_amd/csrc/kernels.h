@@ -170,6 +170,13 @@ struct ConvEpi {
   float drop_p = 0.f;
   uint32_t drop_seed = 0;
   const int64_t* drop_step = nullptr;
+  // geometry extensions (ring / buffer kernels only, no split-K): width padding different from the
+  // height padding, and an output row map that scatters output pixel (img, i, j) of the Ho x Wo
+  // grid to row (img, i*o_sh + o_ph, j*o_sw + o_pw) of an o_H x o_W map -- the parity classes of
+  // a strided data gradient each write their own positions of dx (ops/conv.py strided_dgrad)
+  int pad_w = -1;
+  int omap = 0;
+  int o_H = 0, o_W = 0, o_sh = 1, o_sw = 1, o_ph = 0, o_pw = 0;
 };
 // counter-based uniform in [0, 1) (Philox-4x32-10, key = (seed, 0x9E3779B9), counter = (e, s))
 float philox_uniform_host(uint32_t seed, uint64_t step, uint64_t e);

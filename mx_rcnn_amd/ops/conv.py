@@ -9,7 +9,8 @@
   filter (pad' = k-1-pad); weight gradient = the MFMA wgrad kernel (csrc/hip/conv_wgrad.hip),
   which ACCUMULATES straight into the parameter's flat-buffer gradient view when the
   parameter is managed by the FlatParamStore (ops/grad_sink.py: no AccumulateGrad add);
-  strided 3x3 data gradients use ``aten.convolution_backward`` (MIOpen).
+  strided data gradients are parity-decomposed into s*s stride-1 convs of dy written straight
+  into their positions of dx (``strided_dgrad``); anything else uses MIOpen.
 * Anything else: MIOpen.  ``MXR_CONV_IGEMM=0`` / ``MXR_CONV_WGRAD=0`` switch the custom
   kernels off for A/B runs.
 """
@@ -62,6 +63,64 @@ def _flip_t(w):
     return w.flip(2, 3).transpose(0, 1).contiguous(memory_format=torch.channels_last)
 
 
+def _parity_taps(k, s, p, ph):
+    """Filter taps of the flipped filter that reach input rows of parity ``ph`` in the data
+    gradient of a (k, stride s, pad p) conv, and the dy offset of the first one."""
+    q = k - 1 - p
+    taps = [t for t in range(k) if (ph + t - q) % s == 0]
+    off = (ph + taps[0] - q) // s if taps else 0
+    return taps, off
+
+
+def strided_dgrad_ok(k, s, p, H, W):
+    """True when every parity class of the data gradient has taps and starts at or before its
+    dy row (so it is a padded stride-1 conv over dy).  ``MXR_STRIDED_DGRAD=0`` disables the path."""
+    if os.environ.get('MXR_STRIDED_DGRAD', '1') == '0':
+        return False
+    for ph in range(min(s, H)):
+        taps, off = _parity_taps(k, s, p, ph)
+        if not taps or off > 0:
+            return False
+    return True
+
+
+def strided_dgrad(dy, wf, H, W, k, s, p, residual=None, bn=None, bn_eps=2e-5, bn_fix_gamma=False, bnb_x=None,
+                  dadd=None, dgamma=None, dbeta=None):
+    """Data gradient of a stride-``s`` k x k conv (pad p) on the MFMA kernel, by parity
+    decomposition: input rows / columns of parity (ph, pw) receive only the filter taps of matching
+    parity, so each of the s*s classes is a small stride-1 conv of dy with a sub-filter, written
+    straight into its positions of dx by the epilogue's output row map (no dilated dy, no scatter
+    pass).  ``wf`` is the flipped / transposed filter (I, O, k, k) of the dgrad cache.  The
+    optional BN-ReLU backward epilogue (``bn`` + ``bnb_x`` [+ ``dadd``, ``residual``]) accumulates
+    dgamma / dbeta over the classes."""
+    ext = need_ext()
+    N, O, Ho, Wo = dy.shape
+    I = wf.shape[0]
+    dx = torch.empty((N, I, H, W), dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
+    bwd = bnb_x is not None
+    if bwd and dgamma is None:
+        dgamma = torch.zeros(I, dtype=torch.float32, device=dy.device)
+        dbeta = torch.zeros(I, dtype=torch.float32, device=dy.device)
+    for ph in range(s):
+        Hc = (H - ph + s - 1) // s
+        if Hc <= 0:
+            continue
+        th, oh = _parity_taps(k, s, p, ph)
+        for pw in range(s):
+            Wc = (W - pw + s - 1) // s
+            if Wc <= 0:
+                continue
+            tw, ow = _parity_taps(k, s, p, pw)
+            # the taps of one parity are an arithmetic progression of step s: plain slicing (an index
+            # list would be a host-to-device copy, illegal inside graph capture)
+            sub = wf[:, :, th[0]:th[-1] + 1:s, tw[0]:tw[-1] + 1:s].contiguous(memory_format=torch.channels_last)
+            ext.conv_igemm_fwd(dy, sub, None, 1, -oh, False, 0, 0, residual, bn, bn_eps, bn_fix_gamma, True,
+                               bnb_x, dadd, dgamma, dbeta, 0.0, 0, None, -ow, dx, [Hc, Wc, H, W, s, s, ph, pw])
+    if bwd:
+        return dx, dgamma, dbeta
+    return dx
+
+
 def conv_backward(x, w, param, dy, stride, pad, has_bias, need_x, need_w, need_b):
     """(dx, dw, db) of an NHWC bf16 conv given the gradient at its (pre-activation) output.
     dw is None when it was accumulated straight into the parameter's flat gradient view."""
@@ -82,6 +141,9 @@ def conv_backward(x, w, param, dy, stride, pad, has_bias, need_x, need_w, need_b
     if need_x:
         if stride == 1 and w.shape[0] % 64 == 0 and 2 * pad == kh - 1:
             dx = need_ext().conv_igemm_fwd(dy, dgrad_weight(param, w), None, 1, kh - 1 - pad, False)[0]
+        elif (stride > 1 and w.shape[0] % 64 == 0 and w.shape[1] % 8 == 0 and kh == w.shape[3] and
+              strided_dgrad_ok(kh, stride, pad, x.shape[2], x.shape[3])):
+            dx = strided_dgrad(dy, dgrad_weight(param, w), x.shape[2], x.shape[3], kh, stride, pad)
         else:
             dx = torch.ops.aten.convolution_backward(
                 dy, x, w, None, [stride] * 2, [pad] * 2, [1, 1], False, [0, 0], 1, [True, False, False])[0]

@@ -17,6 +17,7 @@ nothing on 288 GB), the weight gradient runs the MFMA wgrad kernel straight into
 gradient buffer (ops/grad_sink.py).  Small outputs (the cls / bbox predictors, N = 21..324) fall
 back to torch matmuls for the parts the kernels do not tile.
 """
+import os
 import zlib
 
 import torch
@@ -35,6 +36,8 @@ def layer_seed(name, base=None):
 
 
 def fc_eligible(x, w):
+    if os.environ.get('MXR_FC_KERNEL', '1') == '0':
+        return False
     return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 2 and
             x.shape[1] % 64 == 0)
 

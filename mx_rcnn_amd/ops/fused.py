@@ -305,6 +305,20 @@ class _FusedUnitFn(torch.autograd.Function):
             finish_bn(bn_i, tg, tb, ret)
             return r[0]
 
+        def strided_dgrad_bn(dy, w_idx, k, stride, pad, bn_i, bn_x, H, W, dadd=None, dres=None):
+            """strided-conv dgrad (parity classes) with the BN(bn_i)-ReLU backward in the epilogue."""
+            from .conv import dgrad_weight, strided_dgrad
+            tg, tb, ret = bn_targets(bn_i)
+            if tg is None:  # statistics not needed: accumulate into scratch
+                C = bnps[bn_i][0].numel()
+                tg = torch.zeros(C, device=dy.device, dtype=torch.float32)
+                tb = torch.zeros(C, device=dy.device, dtype=torch.float32)
+            r = strided_dgrad(dy, dgrad_weight(ctx.params[w_idx], ws[w_idx]), H, W, k, stride, pad, residual=dres,
+                              bn=bnps[bn_i], bn_eps=spec.eps[bn_i], bn_fix_gamma=spec.fix[bn_i], bnb_x=bn_x,
+                              dadd=dadd, dgamma=tg, dbeta=tb)
+            finish_bn(bn_i, tg, tb, ret)
+            return r[0]
+
         def bn_bwd_plain(dy_act, bn_i, bn_x, dres=None):
             tg, tb, ret = bn_targets(bn_i)
             p = [q.float().contiguous() for q in bnps[bn_i]]
@@ -322,6 +336,8 @@ class _FusedUnitFn(torch.autograd.Function):
             wgrad(1, d_y2, a2, 3, s, 1)
             if s == 1:
                 d_y1 = dgrad_bn(d_y2, 1, 3, 1, 1, y1)
+            elif _strided_ok(ws[1], s, a2):
+                d_y1 = strided_dgrad_bn(d_y2, 1, 3, s, 1, 1, y1, a2.shape[2], a2.shape[3])
             else:
                 d_a2 = torch.ops.aten.convolution_backward(d_y2, a2, ws[1], None, [s, s], [1, 1], [1, 1], False,
                                                            [0, 0], 1, [True, False, False])[0]
@@ -354,6 +370,8 @@ class _FusedUnitFn(torch.autograd.Function):
         dres = d_out if spec.dim_match else None
         if s1 == 1 and ws[0].shape[0] % 64 == 0:
             d_x = dgrad_bn(d_y1, 0, k1, p1, 0, x, dadd=d_sc, dres=dres)
+        elif s1 > 1 and _strided_ok(ws[0], s1, act1):
+            d_x = strided_dgrad_bn(d_y1, 0, k1, s1, p1, 0, x, act1.shape[2], act1.shape[3], dadd=d_sc, dres=dres)
         else:
             d_act1 = torch.ops.aten.convolution_backward(d_y1, act1, ws[0], None, [s1, s1], [p1, p1], [1, 1], False,
                                                          [0, 0], 1, [True, False, False])[0]
@@ -363,6 +381,12 @@ class _FusedUnitFn(torch.autograd.Function):
         if side is not None:
             main.wait_stream(side)
         return (None, d_x, None) + tuple(grads)
+
+
+def _strided_ok(w, s, inp):
+    from .conv import strided_dgrad_ok
+    return (w.shape[0] % 64 == 0 and w.shape[1] % 8 == 0 and w.shape[2] == w.shape[3] and
+            strided_dgrad_ok(w.shape[2], s, (w.shape[2] - 1) // 2, inp.shape[2], inp.shape[3]))
 
 
 def fused_unit(u, x, act1=None, next_bn=None):

@@ -6,6 +6,8 @@ convention: VGG pool1..4 2x2/2 (`rcnn/symbol.py:19,28,40,52`), ResNet pool0 3x3/
 predictors (`rcnn/resnet.py:167`).  GPU bf16 channels_last tensors run the HIP kernels (the
 backward gathers through the recorded winning taps, no atomics); anything else runs torch.
 """
+import os
+
 import torch
 import torch.nn.functional as F
 
@@ -13,6 +15,8 @@ from ._ext import need_ext
 
 
 def _eligible(x):
+    if os.environ.get('MXR_POOL_KERNEL', '1') == '0':
+        return False
     return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0 and
             x.is_contiguous(memory_format=torch.channels_last))
 

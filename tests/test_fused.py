@@ -239,3 +239,52 @@ def test_train_bn_relu_vs_torch(cuda, C, M_hw, relu):
     for a, r in ((yg, yr), (xg.grad, xr.grad), (gg.grad, gr.grad), (bg.grad, br.grad), (rm, rm_r), (rv, rv_r)):
         err = (a.float().cpu() - r.detach()).abs().max().item()
         assert err <= 2e-2 * r.abs().max().item() + 2e-3, err
+
+
+@pytest.mark.parametrize('N,Cin,Cout,H,W,k,s,p', [(1, 256, 256, 100, 167, 3, 2, 1), (128, 512, 512, 7, 7, 3, 2, 1),
+                                                 (2, 64, 128, 15, 22, 3, 2, 1), (1, 64, 64, 9, 10, 5, 2, 2),
+                                                 (1, 128, 64, 12, 13, 3, 3, 0)])
+def test_strided_dgrad_parity_classes(cuda, N, Cin, Cout, H, W, k, s, p):
+    """Parity-decomposed stride-s data gradient on the MFMA kernel (output row map) vs fp32 torch."""
+    from mx_rcnn_amd.ops.conv import _flip_t, strided_dgrad, strided_dgrad_ok
+    assert strided_dgrad_ok(k, s, p, H, W)
+    g = torch.Generator().manual_seed(51)
+    x = torch.randn(N, Cin, H, W, generator=g).bfloat16()
+    w = (torch.randn(Cout, Cin, k, k, generator=g) * 0.05).bfloat16()
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = torch.randn(N, Cout, Ho, Wo, generator=g).bfloat16()
+    ref = torch.ops.aten.convolution_backward(dy.float(), x.float(), w.float(), None, [s, s], [p, p], [1, 1], False,
+                                              [0, 0], 1, [True, False, False])[0]
+    dx = strided_dgrad(_cl(dy, cuda), _flip_t(_cl(w, cuda)), H, W, k, s, p)
+    err = (dx.float().cpu() - ref).abs().max().item()
+    assert err <= 1e-2 * ref.abs().max().item() + 1e-2, err
+
+
+def test_strided_dgrad_bnb_epilogue(cuda):
+    """Strided dgrad fused with the BN-ReLU backward (+dadd, +residual): dx and dgamma / dbeta
+    accumulated over the parity classes vs unfused fp32 ops."""
+    from mx_rcnn_amd.ops.conv import _flip_t, strided_dgrad
+    g = torch.Generator().manual_seed(52)
+    Cin, Cout, H, W, k, s, p = 256, 256, 21, 34, 3, 2, 1
+    w = (torch.randn(Cout, Cin, k, k, generator=g) * 0.05).bfloat16()
+    Ho, Wo = (H + 2 * p - k) // s + 1, (W + 2 * p - k) // s + 1
+    dy = torch.randn(1, Cout, Ho, Wo, generator=g).bfloat16()
+    xr = torch.randn(1, Cin, H, W, generator=g).bfloat16()
+    dadd = torch.randn(1, Cin, H, W, generator=g).bfloat16()
+    dres = torch.randn(1, Cin, H, W, generator=g).bfloat16()
+    gamma, beta = torch.rand(Cin, generator=g) + 0.5, torch.randn(Cin, generator=g) * 0.1
+    mean, var = torch.randn(Cin, generator=g) * 0.2, torch.rand(Cin, generator=g) + 0.5
+    d_act = torch.ops.aten.convolution_backward(dy.float(), xr.float(), w.float(), None, [s, s], [p, p], [1, 1],
+                                                False, [0, 0], 1, [True, False, False])[0] + dadd.float()
+    sc = gamma * torch.rsqrt(var + 2e-5)
+    pre = xr.float() * sc[None, :, None, None] + (beta - mean * sc)[None, :, None, None]
+    gm = d_act * (pre > 0).float()
+    ref_dx = gm * sc[None, :, None, None] + dres.float()
+    xhat = (xr.float() - mean[None, :, None, None]) * torch.rsqrt(var + 2e-5)[None, :, None, None]
+    ref_dg, ref_db = (gm * xhat).sum(dim=(0, 2, 3)), gm.sum(dim=(0, 2, 3))
+    dx, dgm, dbt = strided_dgrad(_cl(dy, cuda), _flip_t(_cl(w, cuda)), H, W, k, s, p, residual=_cl(dres, cuda),
+                                 bn=[t.to(cuda) for t in (gamma, beta, mean, var)], bnb_x=_cl(xr, cuda),
+                                 dadd=_cl(dadd, cuda))
+    for a, r in ((dx, ref_dx), (dgm, ref_dg), (dbt, ref_db)):
+        err = (a.float().cpu() - r).abs().max().item()
+        assert err <= 2e-2 * r.abs().max().item() + 2e-2, err

@@ -84,52 +84,69 @@ class IMDB(object):
         self.num_images = len(self.image_set_index)
         return roidb
 
-    def evaluate_recall(self, roidb, candidate_boxes=None, thresholds=None, area='all', limit=None):
-        """Greedy gt<->proposal matching recall over IoU thresholds; returns (ar, recalls, thresholds)."""
-        areas = {'all': 0, 'small': 1, 'medium': 2, 'large': 3, '96-128': 4, '128-256': 5, '256-512': 6,
-                 '512-inf': 7}
-        area_ranges = [[0 ** 2, 1e5 ** 2], [0 ** 2, 32 ** 2], [32 ** 2, 96 ** 2], [96 ** 2, 1e5 ** 2],
-                       [96 ** 2, 128 ** 2], [128 ** 2, 256 ** 2], [256 ** 2, 512 ** 2], [512 ** 2, 1e5 ** 2]]
-        assert area in areas, 'unknown area range: {}'.format(area)
-        area_range = area_ranges[areas[area]]
-        gt_overlaps = np.zeros(0)
-        num_pos = 0
-        for i in range(len(roidb)):
-            max_gt = roidb[i]['gt_overlaps'].toarray().max(axis=1)
-            gt_inds = np.where((roidb[i]['gt_classes'] > 0) & (max_gt == 1))[0]
-            gt_boxes = roidb[i]['boxes'][gt_inds, :]
-            gt_areas = (gt_boxes[:, 2] - gt_boxes[:, 0] + 1) * (gt_boxes[:, 3] - gt_boxes[:, 1] + 1)
-            valid = np.where((gt_areas >= area_range[0]) & (gt_areas <= area_range[1]))[0]
-            gt_boxes = gt_boxes[valid, :]
-            num_pos += len(valid)
-            if candidate_boxes is None:
-                boxes = roidb[i]['boxes'][np.where(roidb[i]['gt_classes'] == 0)[0], :]
-            else:
-                boxes = np.asarray(candidate_boxes[i])[:, :4]
-            if boxes.shape[0] == 0:
+    # gt-area buckets of the recall report (pixel areas, inclusive), keyed like the reference
+    RECALL_AREAS = {'all': (0.0, 1e10), 'small': (0.0, 32.0 ** 2), 'medium': (32.0 ** 2, 96.0 ** 2),
+                    'large': (96.0 ** 2, 1e10), '96-128': (96.0 ** 2, 128.0 ** 2),
+                    '128-256': (128.0 ** 2, 256.0 ** 2), '256-512': (256.0 ** 2, 512.0 ** 2),
+                    '512-inf': (512.0 ** 2, 1e10)}
+
+    @staticmethod
+    def greedy_gt_coverage(overlaps):
+        """One-to-one proposal<->gt matching, best pair first: all (proposal, gt) pairs are visited
+        in decreasing IoU and a pair is taken when neither side is used yet.  Returns, per gt
+        column, the IoU of its matched proposal (0 when it gets none).  Same assignment as the
+        reference's repeated global-argmax loop (`helper/dataset/imdb.py:160-171`), in
+        O(P*G log(P*G)) instead of G full passes, and without its failure when there are fewer
+        proposals than gt boxes."""
+        n_box, n_gt = overlaps.shape
+        cover = np.zeros(n_gt)
+        if n_box == 0 or n_gt == 0:
+            return cover
+        order = np.argsort(-overlaps, axis=None, kind='stable')
+        box_used = np.zeros(n_box, bool)
+        gt_used = np.zeros(n_gt, bool)
+        left = min(n_box, n_gt)
+        for flat in order:
+            b, g = divmod(int(flat), n_gt)
+            if box_used[b] or gt_used[g]:
                 continue
-            if limit is not None and boxes.shape[0] > limit:
-                boxes = boxes[:limit, :]
-            overlaps = bbox_overlaps(boxes.astype(np.float64), gt_boxes.astype(np.float64))
-            _gt = np.zeros((gt_boxes.shape[0]))
-            for j in range(gt_boxes.shape[0]):
-                argmax_ov = overlaps.argmax(axis=0)
-                max_ov = overlaps.max(axis=0)
-                gt_ind = max_ov.argmax()
-                gt_ovr = max_ov.max()
-                assert gt_ovr >= 0
-                box_ind = argmax_ov[gt_ind]
-                _gt[j] = overlaps[box_ind, gt_ind]
-                overlaps[box_ind, :] = -1
-                overlaps[:, gt_ind] = -1
-            gt_overlaps = np.hstack((gt_overlaps, _gt))
-        gt_overlaps = np.sort(gt_overlaps)
-        if thresholds is None:
-            thresholds = np.arange(0.5, 0.95 + 1e-5, 0.05)
-        recalls = np.zeros_like(thresholds, dtype=np.float64)
-        for i, t in enumerate(thresholds):
-            recalls[i] = (gt_overlaps >= t).sum() / float(max(num_pos, 1))
-        ar = recalls.mean()
+            box_used[b] = gt_used[g] = True
+            cover[g] = overlaps[b, g]
+            left -= 1
+            if left == 0:
+                break
+        return cover
+
+    def evaluate_recall(self, roidb, candidate_boxes=None, thresholds=None, area='all', limit=None):
+        """Proposal recall of the gt boxes in an area bucket, over IoU thresholds (default
+        0.5:0.05:0.95); returns (average recall, recalls, thresholds).  Proposals are the roidb's
+        non-gt rows unless ``candidate_boxes`` is given; ``limit`` keeps the first N per image."""
+        if area not in self.RECALL_AREAS:
+            raise ValueError('unknown area range: %s' % area)
+        lo, hi = self.RECALL_AREAS[area]
+        covers, num_pos = [], 0
+        for i, entry in enumerate(roidb):
+            boxes_all = np.asarray(entry['boxes'], dtype=np.float64)
+            is_gt = (entry['gt_classes'] > 0) & (entry['gt_overlaps'].toarray().max(axis=1) == 1)
+            gt = boxes_all[is_gt]
+            a = (gt[:, 2] - gt[:, 0] + 1) * (gt[:, 3] - gt[:, 1] + 1)
+            gt = gt[(a >= lo) & (a <= hi)]
+            num_pos += gt.shape[0]
+            if candidate_boxes is None:
+                props = boxes_all[entry['gt_classes'] == 0]
+            else:
+                props = np.asarray(candidate_boxes[i], dtype=np.float64)[:, :4]
+            if limit is not None:
+                props = props[:limit]
+            if props.shape[0] == 0 or gt.shape[0] == 0:
+                continue
+            covers.append(self.greedy_gt_coverage(bbox_overlaps(props, gt)))
+        cover = np.sort(np.concatenate(covers)) if covers else np.zeros(0)
+        thresholds = np.arange(0.5, 0.95 + 1e-5, 0.05) if thresholds is None else np.asarray(thresholds)
+        # matched gts with IoU >= t, for every t at once
+        hits = cover.size - np.searchsorted(cover, thresholds, side='left')
+        recalls = hits / float(max(num_pos, 1))
+        ar = float(recalls.mean())
         logging.info('average recall: %.3f', ar)
         for t, r in zip(thresholds, recalls):
             logging.info('recall @%.2f: %.3f', t, r)

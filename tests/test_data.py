@@ -195,3 +195,36 @@ def test_dp_loaders_agree_on_step_shape():
     assert len(shapes) == 8
     config.SCALES = (600,)
     config.MAX_SIZE = 1000
+
+
+def _greedy_loop(ov):
+    """Repeated global-argmax matching (oracle for the pair-sorted version)."""
+    ov = ov.copy()
+    out = np.zeros(ov.shape[1])
+    for _ in range(min(ov.shape)):
+        b, g = np.unravel_index(np.argmax(ov), ov.shape)
+        out[g] = ov[b, g]
+        ov[b, :] = -1
+        ov[:, g] = -1
+    return out
+
+
+def test_evaluate_recall_greedy_matching():
+    import scipy.sparse
+    from mx_rcnn_amd.data.imdb import IMDB
+    rng = np.random.RandomState(9)
+    for _ in range(20):
+        ov = rng.rand(rng.randint(1, 12), rng.randint(1, 6))
+        np.testing.assert_allclose(np.sort(IMDB.greedy_gt_coverage(ov)), np.sort(_greedy_loop(ov)))
+    # toy image: 2 gts, proposals hitting one exactly and the other at IoU 0.8
+    gt = np.array([[0, 0, 9, 9], [20, 20, 39, 39]], np.float32)
+    props = np.array([[0, 0, 9, 9], [20, 20, 35, 39], [50, 50, 60, 60]], np.float32)
+    boxes = np.vstack([gt, props])
+    ovl = np.zeros((5, 2), np.float32)
+    ovl[0, 1] = ovl[1, 1] = 1.0
+    roidb = [{'boxes': boxes, 'gt_classes': np.array([1, 1, 0, 0, 0], np.int32),
+              'gt_overlaps': scipy.sparse.csr_matrix(ovl)}]
+    ar, rec, th = IMDB('t').evaluate_recall(roidb, thresholds=[0.5, 0.7, 0.9])
+    np.testing.assert_allclose(rec, [1.0, 1.0, 0.5])  # IoU 1.0 and 0.8
+    ar, rec, th = IMDB('t').evaluate_recall(roidb, thresholds=[0.5], area='large')
+    assert rec[0] == 0.0  # no gt of area >= 96^2

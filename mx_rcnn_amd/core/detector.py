@@ -5,8 +5,8 @@ built once, weights live on the device, and an image batch runs ``model.detect``
 RoI de-duplication (TEST.DEDUP_BOXES, Fast R-CNN mode) hashes rounded RoIs like the
 reference.  ``im_detect`` returns numpy (scores, pred_boxes) for API parity;
 ``detect_batch`` keeps everything on the device and performs the whole test-time
-post-process (decode, clip, per-class score threshold, batched per-class NMS, top-k) in one
-pass per image (SURVEY kernel K18).
+post-process (decode, clip, per-class score threshold, per-class NMS, top-k over classes) as
+two kernel launches for the whole batch (SURVEY kernel K18, csrc/hip/det_post.hip).
 """
 import numpy as np
 import torch
@@ -93,9 +93,38 @@ class Detector(object):
         info = torch.as_tensor(np.asarray(im_info) if not torch.is_tensor(im_info) else im_info).float().to(self.ctx)
         return self.postprocess(r, scores, deltas, info, nms_thresh, thresh, max_per_image)
 
+    @staticmethod
+    def device_postprocess_ok(r, scores, info):
+        B = info.shape[0]
+        if not (r.is_cuda and B > 0 and r.shape[0] % B == 0 and r.shape[0] // B <= 1024 and
+                2 <= scores.shape[1] <= 1025):
+            return False
+        return True
+
+    @torch.no_grad()
+    def postprocess_raw(self, r, scores, deltas, info, nms_thresh=0.3, thresh=0.05, max_per_image=100, cap=None):
+        """The whole test post-process as two device launches, no host sync (csrc/hip/det_post.hip):
+        -> dets (B, cap, 6) [x1 y1 x2 y2 score class] in original-image pixels, counts (B,) int32.
+        Detections are in class order, score-descending within a class."""
+        from ..ops._ext import need_ext
+        cap = cap or max(4 * max_per_image, 512)
+        return need_ext().det_postprocess(r.float().contiguous(), scores.float().contiguous(),
+                                          deltas.float().contiguous(), info.float().contiguous(), float(thresh),
+                                          float(nms_thresh), int(max_per_image), int(cap))
+
     @torch.no_grad()
     def postprocess(self, r, scores, deltas, info, nms_thresh=0.3, thresh=0.05, max_per_image=100):
-        """Device-side test post-process of ``model.detect`` outputs (see detect_batch)."""
+        """Device-side test post-process of ``model.detect`` outputs (see detect_batch).  GPU: the
+        fused kernels plus ONE host read of the per-image counts; CPU: the tensor reference."""
+        if self.device_postprocess_ok(r, scores, info):
+            dets, counts = self.postprocess_raw(r, scores, deltas, info, nms_thresh, thresh, max_per_image)
+            n = counts.cpu().tolist()
+            return [(dets[b, :k, :4], dets[b, :k, 4], dets[b, :k, 5].long()) for b, k in enumerate(n)]
+        return self.postprocess_ref(r, scores, deltas, info, nms_thresh, thresh, max_per_image)
+
+    @torch.no_grad()
+    def postprocess_ref(self, r, scores, deltas, info, nms_thresh=0.3, thresh=0.05, max_per_image=100):
+        """Tensor reference of the post-process (the oracle of the device kernels)."""
         B = info.shape[0]
         C = scores.shape[1]
         out = []

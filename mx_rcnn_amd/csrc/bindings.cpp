@@ -767,6 +767,48 @@ Tensor avgpool_bwd(const Tensor& dy, int64_t H, int64_t W) {
   return dx;
 }
 
+// ---- detection post-process -------------------------------------------------------------------
+std::vector<Tensor> det_postprocess(const Tensor& rois, const Tensor& scores, const Tensor& deltas,
+                                    const Tensor& im_info, double thresh, double nms_thresh, int64_t max_per,
+                                    int64_t cap) {
+  CHECK_DEV(rois); CHECK_DEV(scores); CHECK_DEV(deltas); CHECK_DEV(im_info);
+  for (const Tensor* t : {&rois, &scores, &deltas, &im_info})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->is_contiguous(), "det_postprocess: contiguous fp32 inputs");
+  const int B = (int)im_info.size(0);
+  const int64_t RB = rois.size(0);
+  const int C = (int)scores.size(1);
+  TORCH_CHECK(B > 0 && RB % B == 0, "rois must hold the same number of RoIs per image, grouped by image");
+  const int R = (int)(RB / B);
+  TORCH_CHECK(rois.size(1) == 5 && scores.size(0) == RB && deltas.size(0) == RB && deltas.size(1) == 4 * C,
+              "det_postprocess: shape mismatch");
+  TORCH_CHECK(R <= 1024 && C >= 2 && C <= 1025, "det_postprocess: at most 1024 RoIs per image and 1024 classes");
+  DevGuard g(rois.device());
+  auto fo = rois.options();
+  Tensor ws_s = at::empty({(int64_t)B * (C - 1) * R}, fo);
+  Tensor ws_b = at::empty({(int64_t)B * (C - 1) * R * 4}, fo);
+  Tensor ws_n = at::empty({(int64_t)B * (C - 1)}, fo.dtype(at::kInt));
+  Tensor dets = at::zeros({B, cap, 6}, fo);
+  Tensor counts = at::empty({B}, fo.dtype(at::kInt));
+  const int rc = mxr::det_postprocess(rois.data_ptr<float>(), scores.data_ptr<float>(), deltas.data_ptr<float>(),
+                                      im_info.data_ptr<float>(), B, R, C, (float)thresh, (float)nms_thresh,
+                                      (int)max_per, (int)cap, ws_s.data_ptr<float>(), ws_b.data_ptr<float>(),
+                                      ws_n.data_ptr<int>(), dets.data_ptr<float>(), counts.data_ptr<int>(),
+                                      cur_stream());
+  TORCH_CHECK(rc == 0, "det_postprocess: unsupported shape");
+  return {dets, counts};
+}
+
+Tensor nest_keep(const Tensor& dets, double thresh) {
+  CHECK_DEV(dets);
+  TORCH_CHECK(dets.scalar_type() == at::kFloat && dets.dim() == 2 && dets.size(1) >= 4 && dets.stride(1) == 1,
+              "nest: dets (N, >=4) fp32 with unit column stride");
+  DevGuard g(dets.device());
+  Tensor keep = at::empty({dets.size(0)}, dets.options().dtype(at::kByte));
+  mxr::nest_filter(dets.data_ptr<float>(), (int)dets.size(0), (int)dets.stride(0), (float)thresh,
+                   keep.data_ptr<uint8_t>(), cur_stream());
+  return keep;
+}
+
 Tensor philox_uniform_cpu(int64_t seed, int64_t step, int64_t n) {
   Tensor out = at::empty({n}, at::TensorOptions().dtype(at::kFloat));
   float* o = out.data_ptr<float>();
@@ -1199,6 +1241,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(), py::arg("drop_p") = 0.0,
         py::arg("drop_seed") = 0, py::arg("drop_step") = py::none(), py::arg("pad_w") = -1,
         py::arg("out") = py::none(), py::arg("out_map") = py::none());
+  m.def("det_postprocess", &det_postprocess, py::arg("rois"), py::arg("scores"), py::arg("deltas"),
+        py::arg("im_info"), py::arg("thresh"), py::arg("nms_thresh"), py::arg("max_per"), py::arg("cap"));
+  m.def("nest_keep", &nest_keep, py::arg("dets"), py::arg("thresh"));
   m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("s"), py::arg("p"));
   m.def("maxpool_bwd", &maxpool_bwd, py::arg("dy"), py::arg("arg"), py::arg("H"), py::arg("W"), py::arg("k"),
         py::arg("s"), py::arg("p"));

@@ -205,6 +205,16 @@ int maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int
 int avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st);
 int avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st);
 
+// ---- test-time detection post-process (det_post.hip) ------------------------------------------
+// rois (B*R, 5) grouped by image, scores (B*R, C), deltas (B*R, 4C), im_info (B, 3), all fp32.
+// ws_*: (B, C-1, R) kept scores, (B, C-1, R, 4) kept boxes, (B, C-1) kept counts.
+// dets (B, cap, 6) [x1 y1 x2 y2 score class] in original-image pixels, counts (B,).
+int det_postprocess(const float* rois, const float* scores, const float* deltas, const float* im_info, int B, int R,
+                    int C, float thresh, float nms_thresh, int max_per, int cap, float* ws_scores, float* ws_boxes,
+                    int* ws_counts, float* dets, int* counts, hipStream_t st);
+// keep[i] = 0 when box i lies inside another box by more than `thresh` of its own area
+int nest_filter(const float* dets, int n, int stride, float thresh, uint8_t* keep, hipStream_t st);
+
 // Flip + transpose many conv filters in ONE launch (dgrad operand cache):
 //   dst[i][r][s][o] = src[o][KH-1-r][KW-1-s][i]   (both channels_last, i.e. (O,KH,KW,I) rows)
 struct WtFlipEntry {

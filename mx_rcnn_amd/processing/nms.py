@@ -36,7 +36,16 @@ def nms(dets, thresh):
 
 
 def nest(dets, thresh=0.90):
-    """Drop box i if inter(i, j) / area_i > thresh for any other box j (vectorised O(N^2))."""
+    """Drop box i if inter(i, j) / area_i > thresh for any other box j (vectorised O(N^2));
+    a GPU tensor runs the HIP kernel (csrc/hip/det_post.hip)."""
+    try:
+        import torch
+        if torch.is_tensor(dets) and dets.is_cuda:
+            from ..ops._ext import need_ext
+            keep = need_ext().nest_keep(dets.float().contiguous(), float(thresh))
+            return [int(i) for i in torch.nonzero(keep).flatten().tolist()]
+    except ImportError:  # pragma: no cover
+        pass
     dets = np.asarray(dets)
     n = dets.shape[0]
     if n == 0:

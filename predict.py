@@ -30,7 +30,11 @@ def predict(args, ctx):
     keep = np.where(cls_scores >= args.thresh)[0]
     dets = np.hstack((cls_boxes[keep], cls_scores[keep, None])).astype(np.float32)
     dets = dets[nms(dets, args.nms_thresh), :]
-    dets = dets[nest(dets, thresh=args.nest_thresh), :]
+    if getattr(ctx, 'type', str(ctx)) == 'cuda' and len(dets):
+        import torch
+        dets = dets[nest(torch.as_tensor(dets, device=ctx), thresh=args.nest_thresh), :]  # HIP nest kernel
+    else:
+        dets = dets[nest(dets, thresh=args.nest_thresh), :]
     dets = dets[(dets[:, 2] - dets[:, 0] + 1 >= args.min_size * scale) |
                 (dets[:, 3] - dets[:, 1] + 1 >= args.min_size * scale)] if dets.size else dets
     out = draw_boxes(color, dets[:, :4] / scale, color=(0, 255, 0))

@@ -439,3 +439,58 @@ def test_iou_max_cpu_twin_matches_tensor_ref():
         for x, y in zip(a, b):
             assert torch.equal(x, y)
     assert int(b[1][0, 5]) == 2 and float(b[0][0, 5]) == 1.0
+
+
+def _det_case(B, R, C, seed):
+    g = torch.Generator().manual_seed(seed)
+    H, W = 600.0, 900.0
+    x1 = torch.rand(B * R, generator=g) * (W - 200)
+    y1 = torch.rand(B * R, generator=g) * (H - 200)
+    wh = torch.rand(B * R, 2, generator=g) * 180 + 10
+    rois = torch.stack([torch.arange(B).repeat_interleave(R).float(), x1, y1, x1 + wh[:, 0], y1 + wh[:, 1]], 1)
+    logits = torch.randn(B * R, C, generator=g) * 2
+    logits[:, 1:6] += 3.0  # a few confident classes
+    scores = torch.softmax(logits, 1)
+    deltas = torch.randn(B * R, 4 * C, generator=g) * 0.1
+    info = torch.tensor([[H, W, 1.5]] * B)
+    return rois, scores, deltas, info
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,R,C,maxper', [(1, 300, 81, 100), (8, 300, 81, 100), (2, 1000, 21, 100), (3, 64, 5, 0)])
+def test_device_postprocess_matches_reference(cuda, B, R, C, maxper):
+    """Fused test-time post-process (decode, clip, threshold, per-class NMS, image top-k with the
+    reference's >= tie rule) vs the tensor reference, as per-image sets."""
+    from mx_rcnn_amd.core.detector import Detector
+    rois, scores, deltas, info = _det_case(B, R, C, 17 + B)
+    det = Detector.__new__(Detector)
+    ref = det.postprocess_ref(rois, scores, deltas, info, 0.3, 0.05, maxper)
+    dets, counts = det.postprocess_raw(rois.to(cuda), scores.to(cuda), deltas.to(cuda), info.to(cuda), 0.3, 0.05,
+                                       maxper, cap=4096)
+    dets, counts = dets.cpu(), counts.cpu()
+    for b in range(B):
+        rb, rs, rc = ref[b]
+        n = int(counts[b])
+        assert n == rs.numel(), (b, n, rs.numel())
+        if maxper:
+            assert n >= min(maxper, n)
+        got = dets[b, :n]
+        key_ref = torch.stack([rc.float(), -rs], 1)
+        key_got = torch.stack([got[:, 5], -got[:, 4]], 1)
+        oref = sorted(range(n), key=lambda i: tuple(key_ref[i].tolist()))
+        ogot = sorted(range(n), key=lambda i: tuple(key_got[i].tolist()))
+        assert torch.allclose(got[ogot, 4], rs[oref], atol=1e-6)
+        assert torch.equal(got[ogot, 5].long(), rc[oref])
+        assert torch.allclose(got[ogot, :4], rb[oref].float(), atol=1e-3, rtol=1e-5)
+
+
+@pytest.mark.gpu
+def test_nest_kernel_matches_reference(cuda):
+    from mx_rcnn_amd.processing.nms import nest
+    rng = np.random.RandomState(4)
+    x1 = rng.rand(700) * 500
+    y1 = rng.rand(700) * 500
+    w, h = rng.rand(700) * 120 + 4, rng.rand(700) * 120 + 4
+    dets = np.stack([x1, y1, x1 + w, y1 + h, rng.rand(700)], 1).astype(np.float32)
+    dets[5] = dets[6]  # identical boxes are each nested in the other: both dropped
+    assert nest(torch.as_tensor(dets, device=cuda), 0.8) == nest(dets, 0.8)

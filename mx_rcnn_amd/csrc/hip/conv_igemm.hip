@@ -13,10 +13,11 @@
 // Variants (tile codes; conv_igemm_plan picks 22 / 23 with split-K only for small grids):
 //   1-3     register-staged loads, double-buffered LDS (the first version; test oracle shapes)
 //   11-16   global_load_lds DMA straight into an S-deep LDS ring, counted vmcnt + raw barrier
-//   21-25   the production path: buffer-resource DMA (buffer_load ... lds).  Per lane a 32-bit
-//           row offset and a 64-bit tap mask are precomputed once, the per-step offsets are
-//           uniform (SGPR), padding comes from the buffer range check returning zeros
-//   26-27   experimental: two 4-wave groups per workgroup split one tile's K-steps
+//   21-25   buffer-resource DMA (buffer_load ... lds).  Per lane a 32-bit row offset and a
+//           64-bit tap mask are precomputed once, the per-step offsets are uniform (SGPR),
+//           padding comes from the buffer range check returning zeros
+//   100+    the tile-balanced ring (any wave layout, 4-16 waves, ring depth per config); the
+//           per-shape autotune (bindings.cpp) picks among 22 / 23 / 100+ on first use
 // Epilogues (ConvEpi): bias, ReLU, residual add, frozen BN+ReLU of the consumer (second output),
 // BN-backward column sums (dgrad fused with the BN backward), fp32 split-K slab + reduce; the
 // LDS-transposed epilogue makes every global access a 16-B vector.  Cin % 64 == 0.
@@ -826,175 +827,6 @@ conv_igemm_buf_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
     igemm_epilogue<TM, TN, WM, WN>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab, Ho, Wo);
 }
 
-// ---- intra-workgroup split-K variant (tile codes 26 / 27; experimental, not in the plan) -----
-// The stage-3 GEMMs (M ~ 4200 pixels) give each CU one 64x64 tile, i.e. one wave per SIMD,
-// and run latency-bound: four independent copies on four streams reach ~1.9x the throughput
-// of one (tools/microbench/conv_concurrency.py).  Here KS wave groups of 4 waves share a tile,
-// each streaming every KS-th K-step through its own LDS ring, so a CU has KS times the loads in
-// flight without smaller tiles (same operand bytes per FLOP) or a slab round trip.  The groups
-// stay in lockstep (one raw barrier per step; a group past its last step idles); at the end the
-// other groups hand their accumulators to group 0 through LDS and exit, and group 0 runs the
-// usual epilogue (s_barrier only waits for the surviving waves).
-template <int BM, int BN, int S, int KS>
-__global__ void __launch_bounds__(256 * KS)
-conv_igemm_bufks_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
-                        int NB, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad,
-                        const ConvEpi ep, int tiles_n, int nwg, int ntiles, int splits, float* __restrict__ slab) {
-  constexpr int WM = BM / 2, WN = BN / 2;
-  constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int ACH = BM / 32, BCH = BN / 32;
-  constexpr int LPS = ACH + BCH;
-  constexpr int RING = S * (BM + BN) * BK;  // bf16 elements per group ring
-  static_assert(S >= 2 && S <= 4 && KS >= 2 && KS <= 4, "pipeline depth / groups");
-  __shared__ __attribute__((aligned(16))) uint16_t lds[KS * RING];  // the ONLY __shared__ object
-  const int grp = threadIdx.x >> 8;
-  uint16_t* As = lds + grp * RING;
-  uint16_t* Bs = As + S * BM * BK;
-
-  const int bid = blockIdx.x;
-  const int q = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
-  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + bid / 8;
-  const int split = wgid / ntiles, tile = wgid % ntiles;
-  const int tm_idx = tile / tiles_n, tn_idx = tile % tiles_n;
-  const int m0 = tm_idx * BM, n0 = tn_idx * BN;
-  const int M = NB * Ho * Wo;
-  const int tid = threadIdx.x & 255, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int K = KH * KW * Cin;
-
-  const __amdgpu_buffer_rsrc_t xr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)((int64_t)NB * H * W * Cin * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t wr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, (int)((int64_t)Cout * K * 2), 0x00020000);
-
-  const int slot = lane & 7;
-  uint32_t a_off[ACH];
-  uint64_t a_mask[ACH];
-#pragma unroll
-  for (int i = 0; i < ACH; ++i) {
-    const int row = 32 * i + 8 * wid + (lane >> 3);
-    const int lc = slot ^ ((row >> 1) & 7);
-    const int m = m0 + row;
-    a_off[i] = 0;
-    a_mask[i] = 0;
-    if (m < M) {
-      const int img = m / (Ho * Wo), rem = m % (Ho * Wo);
-      const int hi0 = (rem / Wo) * stride - pad, wi0 = (rem % Wo) * stride - (ep.pad_w >= 0 ? ep.pad_w : pad);
-      a_off[i] = (uint32_t)(((((int64_t)img * H + hi0) * W + wi0) * Cin + lc * 8) * 2);
-      for (int fr = 0; fr < KH; ++fr)
-        for (int fc = 0; fc < KW; ++fc)
-          if ((unsigned)(hi0 + fr) < (unsigned)H && (unsigned)(wi0 + fc) < (unsigned)W)
-            a_mask[i] |= 1ull << (fr * KW + fc);
-    }
-  }
-  uint32_t b_off[BCH];
-#pragma unroll
-  for (int i = 0; i < BCH; ++i) {
-    const int row = 32 * i + 8 * wid + (lane >> 3);
-    const int co = n0 + row;
-    b_off[i] = co < Cout ? (uint32_t)(((int64_t)co * K + (slot ^ ((row >> 1) & 7)) * 8) * 2) : kBufOOB;
-  }
-  const int cin_steps = Cin / BK;
-  const int nk_all = KH * KW * cin_steps;
-  const int per = (nk_all + splits - 1) / splits;
-  const int k_begin = split * per;
-  const int k_end = min(nk_all, k_begin + per);
-  const int nk = max(0, k_end - k_begin);
-  const int nk_g = nk > grp ? (nk - grp + KS - 1) / KS : 0;  // this group's steps: grp, grp+KS, ...
-  const int nk_max = (nk + KS - 1) / KS;                     // the lockstep trip count
-
-  // issue cursor (uniform per group): this group's next K-step
-  int c_k = k_begin + grp;
-  auto issue = [&](int buf) {
-    const int c_tap = c_k / cin_steps, c_ci = (c_k % cin_steps) * BK;
-    const int c_fr = c_tap / KW, c_fc = c_tap % KW;
-    const uint32_t tap_a = (uint32_t)((c_fr * W + c_fc) * Cin * 2);
-    const uint32_t soff_a = (uint32_t)(c_ci * 2);
-    const uint32_t soff_b = (uint32_t)((c_tap * Cin + c_ci) * 2);
-#pragma unroll
-    for (int i = 0; i < ACH; ++i) {
-      const uint32_t vo = ((a_mask[i] >> c_tap) & 1ull) ? a_off[i] + tap_a : kBufOOB;
-      buf_lds16(xr, As + (buf * BM + 32 * i + 8 * wid) * BK, vo, soff_a);
-    }
-#pragma unroll
-    for (int i = 0; i < BCH; ++i) buf_lds16(wr, Bs + (buf * BN + 32 * i + 8 * wid) * BK, b_off[i], soff_b);
-    c_k += KS;
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int st = 0; st < S - 1; ++st)
-    if (st < nk_g) issue(st);
-  for (int ks = 0; ks < nk_max; ++ks) {
-    const bool live = ks < nk_g;
-    if (live) wait_stages<LPS>(min(S - 2, nk_g - 1 - ks));
-    __builtin_amdgcn_s_barrier();
-    if (live) {
-      if (ks + S - 1 < nk_g) issue((ks + S - 1) % S);
-      const int buf = ks % S;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        bf16x8 af[TM], bfr[TN];
-        const int chunk = kk * 4 + (lane >> 4);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const int row = wm * WM + i * 16 + (lane & 15);
-          af[i] = *reinterpret_cast<const bf16x8*>(As + (buf * BM + row) * BK + swz(row, chunk) * 8);
-        }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int row = wn * WN + j * 16 + (lane & 15);
-          bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (buf * BN + row) * BK + swz(row, chunk) * 8);
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-      }
-    }
-  }
-  // hand the other groups' partial sums to group 0 (fp32 through LDS, one [BM][BN] block per
-  // group, laid out per wave-lane like the accumulators so no index math is needed)
-  wait_vmcnt<0>();
-  __syncthreads();
-  constexpr int PART = TM * TN * 4 * 256;  // floats per group
-  static_assert(BM * (BN + 4) + (KS - 1) * PART <= KS * RING / 2, "partials + epilogue tile fit the rings");
-  float* part = reinterpret_cast<float*>(lds) + BM * (BN + 4);  // beyond the epilogue staging tile
-  if (grp > 0) {
-    float* dst = part + (grp - 1) * PART;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) dst[((i * TN + j) * 4 + r) * 256 + tid] = acc[i][j][r];
-  }
-  __syncthreads();
-  if (grp > 0) return;  // later barriers only wait for the surviving group-0 waves
-#pragma unroll
-  for (int g = 1; g < KS; ++g) {
-    const float* src = part + (g - 1) * PART;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][j][r] += src[((i * TN + j) * 4 + r) * 256 + tid];
-  }
-  static_assert(BM * (BN + 4) * 4 <= KS * RING * 2, "epilogue tile must fit the operand rings");
-  if (Cout % 8 == 0)
-    igemm_epilogue_lds<BM, BN, TM, TN, WM, WN>(acc, reinterpret_cast<float*>(lds), m0, n0, wm, wn, lane, tid, M, Cout,
-                                               ep, y, split, splits, slab);
-  else
-    igemm_epilogue<TM, TN, WM, WN>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab);
-}
-
 // ---- tile-balanced LDS-DMA ring (the production path) ----------------------------------------
 // Measured on the ResNet-101 C4 stage-3/4 shapes (rocprofv3 --pmc, profiles/r2_conv_pmc.txt): the
 // 64x64 ring above is limited by what ONE CU can pull into LDS (~27 GB/s at two 16 KB stages in
@@ -1396,25 +1228,6 @@ static int ring_plan(int64_t M, int Cout, int nk, int* splits_out) {
   return 100 + best;
 }
 
-template <int BM, int BN, int S, int KS>
-static void launch_fwd_ks(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho,
-                          int Wo, int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int splits,
-                          float* slab, hipStream_t st) {
-  const int M = NB * Ho * Wo;
-  const int tiles_m = (M + BM - 1) / BM, tiles_n = (Cout + BN - 1) / BN;
-  const int ntiles = tiles_m * tiles_n;
-  const int nwg = ntiles * splits;
-  conv_igemm_bufks_kernel<BM, BN, S, KS><<<nwg, 256 * KS, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW,
-                                                                   stride, pad, ep, tiles_n, nwg, ntiles, splits, slab);
-  if (splits > 1) {
-    const int64_t MN = (int64_t)M * Cout;
-    if (ep.bnb_x)
-      splitk_reduce_bnb_kernel<<<dim3(div_up(Cout, 64), div_up(M, 64)), 256, 0, st>>>(slab, splits, M, Cout, ep, y);
-    else
-      splitk_reduce_kernel<<<div_up((MN + 3) / 4, 256), 256, 0, st>>>(slab, splits, MN, Cout, ep, y);
-  }
-}
-
 template <int BM, int BN, int S = 0, bool BUF = false>
 static void launch_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho,
                        int Wo, int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int splits,
@@ -1515,17 +1328,9 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
     case 31: launch_fwd<128, 128, 4, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 32: launch_fwd<128, 64, 4, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 33: launch_fwd<64, 64, 4, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
-    // deeper rings for the one-tile-per-CU grids (probe)
-    case 43: launch_fwd<64, 64, 5, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
-    case 53: launch_fwd<64, 64, 6, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
-    case 63: launch_fwd<64, 64, 8, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
-    case 41: launch_fwd<128, 128, 4, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     // small tiles (2-4 workgroups per CU on the ~4K-row stage-3 GEMMs: more waves to hide latency)
     case 24: launch_fwd<32, 64, 3, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 25: launch_fwd<64, 32, 3, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
-    // intra-workgroup split-K (2 wave groups share a 64x64 / 128x64 tile; experimental)
-    case 26: launch_fwd_ks<64, 64, 3, 2>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
-    case 27: launch_fwd_ks<128, 64, 3, 2>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     default: launch_fwd<64, 64>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
   }
   return tile;

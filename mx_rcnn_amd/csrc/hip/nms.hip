@@ -112,14 +112,12 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
       const uint64_t valid = nrow >= 64 ? ~0ull : ((1ull << nrow) - 1ull);
       const uint64_t cand = valid & ~(removed[t] | sp);
       uint64_t kept = cand;
-#ifndef NMS_ABL_NOFIX  // ablation switch for tools/microbench/nms_bench.hip
       for (int it = 0; it < 65; ++it) {
         const uint64_t sup = __ballot((diag & kept) != 0ull);
         const uint64_t next = cand & ~sup;
         if (next == kept) break;
         kept = next;
       }
-#endif
       // prefetch block t+1 (clamped in-range address on the last block)
       const int jn = min(j + 64, (int)Pp - 1);
       const int tn = min(t + 1, nb - 1);
@@ -141,7 +139,6 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
         s_nk[(t + 1) & 1] = nk + __popcll(kept);
       }
     } else {
-#ifndef NMS_ABL_NOHELP  // ablation switch for tools/microbench/nms_bench.hip
       const int h = wave - 1;
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the asm prefetch is invisible to hipcc
       if (t >= 1) {
@@ -179,7 +176,6 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
           asm volatile("global_load_dwordx2 %0, %1, off" : "+v"(pf[k]) : "v"(src) : "memory");
         }
       }
-#endif
     }
     __syncthreads();
   }

@@ -2,9 +2,9 @@
 
 * Cin % 64 == 0 (every ResNet/VGG conv except the 3-channel stem): hand-written MFMA
   implicit-GEMM forward (csrc/hip/conv_igemm.hip) with fused bias + ReLU epilogue and split-K
-  for the latency-bound small-M shapes of 1-image detection.  1x1 convs with M = N*H*W >
-  16384 (frozen stage-1/2 shapes, forward only) use one hipBLASLt GEMM over the NHWC matrix
-  view instead (faster there, tools/microbench/conv_kernels.py); strided 1x1 subsample first.
+  for the latency-bound small-M shapes of 1-image detection (the LDS-DMA kernel beats
+  hipBLASLt on every trunk 1x1 shape, tools/microbench/conv_tiles.py); strided 1x1 convs
+  subsample first.
 * Backward: stride-1 data gradient = the same kernel on dY with the flipped/transposed
   filter (pad' = k-1-pad); weight gradient = the MFMA wgrad kernel (csrc/hip/conv_wgrad.hip),
   which ACCUMULATES straight into the parameter's flat-buffer gradient view when the
@@ -21,9 +21,6 @@ import torch.nn.functional as F
 
 from . import grad_sink
 from ._ext import need_ext
-
-GEMM_1X1_MIN_M = 1 << 40  # the LDS-DMA igemm kernel beats hipBLASLt on every trunk 1x1 shape (tools/microbench/conv_tiles.py)
-
 
 def igemm_enabled():
     return os.environ.get('MXR_CONV_IGEMM', '1') != '0'
@@ -197,17 +194,6 @@ class _ConvIgemm(torch.autograd.Function):
         return dx, dw, db, None, None, None
 
 
-def conv1x1_gemm(x, w, b, stride=1):
-    """1x1 convolution on channels_last activations as ONE GEMM over the (N*H*W, C) matrix view
-    of the NHWC memory (no im2col, no layout change); backward via autograd (two GEMMs)."""
-    if stride != 1:
-        x = x[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last)
-    n, c, h, wd = x.shape
-    x2 = x.permute(0, 2, 3, 1).reshape(n * h * wd, c)
-    y2 = F.linear(x2, w.reshape(w.shape[0], c), b)
-    return y2.reshape(n, h, wd, w.shape[0]).permute(0, 3, 1, 2)
-
-
 def igemm_eligible(x, w, stride=1, pad=0):
     """True when the MFMA implicit-GEMM kernel is the path conv2d would take for this conv."""
     k = w.shape[2]
@@ -216,8 +202,7 @@ def igemm_eligible(x, w, stride=1, pad=0):
         return False
     if k == 1 and pad == 0 and stride != 1:
         return False
-    m = x.shape[0] * ((x.shape[2] + 2 * pad - k) // stride + 1) * ((x.shape[3] + 2 * pad - k) // stride + 1)
-    return not (k == 1 and m > GEMM_1X1_MIN_M)
+    return True
 
 
 def conv2d(x, w, b=None, stride=1, pad=0, relu=False):
@@ -228,11 +213,7 @@ def conv2d(x, w, b=None, stride=1, pad=0, relu=False):
         if k == 1 and pad == 0 and stride != 1:
             x = x[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last)
             stride = 1
-        m = x.shape[0] * ((x.shape[2] + 2 * pad - k) // stride + 1) * ((x.shape[3] + 2 * pad - k) // stride + 1)
-        if igemm_enabled() and not (k == 1 and m > GEMM_1X1_MIN_M):
+        if igemm_enabled():
             return _ConvIgemm.apply(x, w, b, int(stride), int(pad), bool(relu))
-        if k == 1 and pad == 0:
-            y = conv1x1_gemm(x, w, b, stride)
-            return F.relu(y, inplace=True) if relu else y
     y = F.conv2d(x, w, b, stride=stride, padding=pad)
     return F.relu(y, inplace=True) if relu else y

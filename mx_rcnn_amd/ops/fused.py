@@ -350,7 +350,11 @@ class _FusedUnitFn(torch.autograd.Function):
             d_y1 = dgrad_bn(d_out, 1, 3, 1, 1, y1)
             wgrad(0, d_y1, act1, 3, s, 1)
             k1, p1, s1 = 3, 1, s
-        if not ctx.needs_input_grad[1]:
+        # bn1 (the unit's input BN) gets its gamma / beta gradients from the d_x pass below; when
+        # the unit input needs no gradient (first trainable unit after frozen stages) that pass
+        # still runs if bn1's own parameters are trainable (its dx is then discarded)
+        bn1_trainable = need[nconv] or need[nconv + 1]
+        if not ctx.needs_input_grad[1] and not bn1_trainable:
             if not spec.dim_match:
                 wgrad(nconv - 1, d_out, sc_in, 1, 1, 0)
             if side is not None:
@@ -380,7 +384,7 @@ class _FusedUnitFn(torch.autograd.Function):
             d_x = bn_bwd_plain(_cl(d_act1), 0, x, dres)
         if side is not None:
             main.wait_stream(side)
-        return (None, d_x, None) + tuple(grads)
+        return (None, d_x if ctx.needs_input_grad[1] else None, None) + tuple(grads)
 
 
 def _strided_ok(w, s, inp):

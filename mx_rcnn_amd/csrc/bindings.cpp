@@ -767,6 +767,29 @@ Tensor avgpool_bwd(const Tensor& dy, int64_t H, int64_t W) {
   return dx;
 }
 
+// ---- proposal top-k ----------------------------------------------------------------------------
+std::vector<Tensor> proposal_topk(const Tensor& keys, const Tensor& boxes, int64_t P) {
+  CHECK_DEV(keys); CHECK_DEV(boxes);
+  TORCH_CHECK(keys.scalar_type() == at::kFloat && boxes.scalar_type() == at::kFloat && keys.is_contiguous() &&
+                  boxes.is_contiguous() && keys.dim() == 2 && boxes.dim() == 3 && boxes.size(2) == 4 &&
+                  boxes.size(0) == keys.size(0) && boxes.size(1) == keys.size(1),
+              "proposal_topk: keys (B, N) and boxes (B, N, 4), contiguous fp32");
+  const int B = (int)keys.size(0), N = (int)keys.size(1);
+  TORCH_CHECK(P > 0 && P <= N, "proposal_topk: 0 < P <= N");
+  DevGuard g(keys.device());
+  auto o = keys.options();
+  Tensor wk = at::empty({(int64_t)B * P}, o.dtype(at::kInt));
+  Tensor wi = at::empty({(int64_t)B * P}, o.dtype(at::kInt));
+  Tensor sk = at::empty({B, P}, o);
+  Tensor sb = at::empty({B, P, 4}, o);
+  Tensor nv = at::empty({B}, o.dtype(at::kInt));
+  TORCH_CHECK(mxr::proposal_topk(keys.data_ptr<float>(), boxes.data_ptr<float>(), B, N, (int)P,
+                                 reinterpret_cast<uint32_t*>(wk.data_ptr<int>()), wi.data_ptr<int>(),
+                                 sk.data_ptr<float>(), sb.data_ptr<float>(), nv.data_ptr<int>(), cur_stream()) == 0,
+              "proposal_topk failed");
+  return {sk, sb, nv};
+}
+
 // ---- detection post-process -------------------------------------------------------------------
 std::vector<Tensor> det_postprocess(const Tensor& rois, const Tensor& scores, const Tensor& deltas,
                                     const Tensor& im_info, double thresh, double nms_thresh, int64_t max_per,
@@ -1241,6 +1264,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(), py::arg("drop_p") = 0.0,
         py::arg("drop_seed") = 0, py::arg("drop_step") = py::none(), py::arg("pad_w") = -1,
         py::arg("out") = py::none(), py::arg("out_map") = py::none());
+  m.def("proposal_topk", &proposal_topk, py::arg("keys"), py::arg("boxes"), py::arg("P"));
   m.def("det_postprocess", &det_postprocess, py::arg("rois"), py::arg("scores"), py::arg("deltas"),
         py::arg("im_info"), py::arg("thresh"), py::arg("nms_thresh"), py::arg("max_per"), py::arg("cap"));
   m.def("nest_keep", &nest_keep, py::arg("dets"), py::arg("thresh"));

@@ -205,6 +205,11 @@ int maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int
 int avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st);
 int avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st);
 
+// ---- proposal pre-NMS top-k (topk.hip): keys (B, N), boxes (B, N, 4) -> the P best in stable
+// descending order; ws_key / ws_idx: B * P each
+int proposal_topk(const float* keys, const float* boxes, int B, int N, int P, uint32_t* ws_key, int* ws_idx,
+                  float* skeys, float* sboxes, int* n_valid, hipStream_t st);
+
 // ---- test-time detection post-process (det_post.hip) ------------------------------------------
 // rois (B*R, 5) grouped by image, scores (B*R, C), deltas (B*R, 4C), im_info (B, 3), all fp32.
 // ws_*: (B, C-1, R) kept scores, (B, C-1, R, 4) kept boxes, (B, C-1) kept counts.

@@ -3,7 +3,9 @@ over images with static output shapes so the whole training step can be captured
 hipGraph (no host synchronisation):
 
   1. fused softmax(fg) + anchors + decode + clip + min-size   -> HIP `proposal_decode`
-  2. stable descending sort, truncate to PRE_NMS_TOP_N        -> device radix sort
+  2. stable descending sort, truncate to PRE_NMS_TOP_N        -> device merge sort (the HIP
+                                                                 `proposal_topk` select+rank kernel
+                                                                 is opt-in: MXR_TOPK=1, slower here)
   3. bitmask NMS (IoU > thresh suppresses), keep POST_NMS_TOP_N,
      random pad (choice with replacement from keep), assemble (post, 5) RoIs
                                                               -> HIP `nms_proposals`
@@ -12,6 +14,8 @@ Deviation (documented): in TRAIN the scores are cropped to the sam
 (int(im_h/16), int(im_w/16)) grid as the deltas.  Tie order among equal scores is
 "lower anchor index first" (numpy's unstable argsort leaves it unspecified).
 """
+import os
+
 import torch
 
 from ._ext import ext_available, need_ext
@@ -79,11 +83,18 @@ def proposal(cls, bbox_deltas, im_info, feat_stride=16, scales=(8, 16, 32), rati
             boxes, keys = _decode_ref(cls, bbox_deltas, im_info, base, feat_stride, min_size, is_train, is_prob)
         N = keys.shape[1]
         P = N if pre_nms_top_n <= 0 else min(int(pre_nms_top_n), N)
-        skeys, order = torch.sort(keys, dim=1, descending=True, stable=True)
-        skeys = skeys[:, :P].contiguous()
-        order = order[:, :P]
-        sboxes = torch.gather(boxes, 1, order[..., None].expand(-1, -1, 4)).contiguous()
-        n_valid = (skeys > float('-inf')).sum(dim=1).to(torch.int32)
+        if cls.is_cuda and N <= 65536 and os.environ.get('MXR_TOPK', '0') == '1':
+            # radix-select + rank-by-counting top-P in stable descending order (csrc/hip/topk.hip).
+            # Off by default: on one image (50 400 clustered RPN scores) it measured 160-340 us against
+            # 60 us for the device merge sort (tools/microbench/topk_bench.py): one workgroup's LDS
+            # histogram atomics serialise when most scores share their top bytes.
+            skeys, sboxes, n_valid = C.proposal_topk(keys.contiguous(), boxes.contiguous(), P)
+        else:
+            skeys, order = torch.sort(keys, dim=1, descending=True, stable=True)
+            skeys = skeys[:, :P].contiguous()
+            order = order[:, :P]
+            sboxes = torch.gather(boxes, 1, order[..., None].expand(-1, -1, 4)).contiguous()
+            n_valid = (skeys > float('-inf')).sum(dim=1).to(torch.int32)
         post = int(post_nms_top_n) if post_nms_top_n > 0 else P
         rand_u = torch.rand(B, post, device=dev, generator=generator)
         if cls.is_cuda:

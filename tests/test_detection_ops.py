@@ -494,3 +494,25 @@ def test_nest_kernel_matches_reference(cuda):
     dets = np.stack([x1, y1, x1 + w, y1 + h, rng.rand(700)], 1).astype(np.float32)
     dets[5] = dets[6]  # identical boxes are each nested in the other: both dropped
     assert nest(torch.as_tensor(dets, device=cuda), 0.8) == nest(dets, 0.8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('B,N,P,ties', [(1, 50400, 12000, False), (2, 50400, 6000, True), (3, 1000, 1000, True),
+                                        (1, 7000, 6000, False)])
+def test_proposal_topk_matches_stable_sort(cuda, B, N, P, ties):
+    """Radix-select + rank-by-counting top-P == stable descending sort truncated to P (keys, boxes,
+    valid count), with heavy ties and -inf (filtered) entries."""
+    from mx_rcnn_amd.ops import need_ext
+    g = torch.Generator().manual_seed(N + P)
+    keys = torch.rand(B, N, generator=g)
+    if ties:
+        keys = (keys * 64).floor() / 64  # 64 distinct values
+    keys[torch.rand(B, N, generator=g) < 0.3] = float('-inf')
+    boxes = torch.rand(B, N, 4, generator=g) * 500
+    sk, sb, nv = need_ext().proposal_topk(keys.to(cuda), boxes.to(cuda), P)
+    rk, order = torch.sort(keys, dim=1, descending=True, stable=True)
+    rk, order = rk[:, :P], order[:, :P]
+    rb = torch.gather(boxes, 1, order[..., None].expand(-1, -1, 4))
+    assert torch.equal(sk.cpu(), rk)
+    assert torch.equal(sb.cpu(), rb)
+    assert torch.equal(nv.cpu(), (rk > float('-inf')).sum(1).to(torch.int32))

@@ -30,6 +30,8 @@ def parse_args(argv=None):
     ap.add_argument('--image', default='800x1333')
     ap.add_argument('--mode', default='graph', choices=['graph', 'eager'])
     ap.add_argument('--batch', type=int, default=1, help='images per forward per GPU (BASELINE config 5: 8)')
+    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp16'],
+                    help='activation / MFMA operand dtype of the test graph (fp16: BASELINE config 5)')
     ap.add_argument('--plant', type=int, default=10,
                     help='classes whose cls_score bias is raised so random-init weights produce detections above '
                          'the 0.05 threshold (the NMS / top-k post-process then has real work); 0 = off')
@@ -93,7 +95,8 @@ def main():
     if args.plant:
         with torch.no_grad():  # synthetic "confident" classes: softmax mass well above 0.05 on them
             model.head.cls_score.bias[1:1 + args.plant] += 6.0
-    det = Detector(model, device)
+    cdt = {'bf16': torch.bfloat16, 'fp16': torch.float16}[args.dtype] if device.type == 'cuda' else torch.float32
+    det = Detector(model, device, compute_dtype=cdt)
     dev_pool = [det._prep(x) for x in pool]
     dinfo = info.to(device)
     run = None
@@ -144,7 +147,7 @@ def main():
         print(json.dumps({
             'metric': METRIC if args.network == 'resnet101' else 'test FPS %s Faster R-CNN' % args.network, 'value': round(value, 3), 'unit': 'images/s', 'n_gpus': world, 'steps': args.steps,
             'warmup': args.warmup, 'ms_per_step': round(elapsed / args.steps * 1e3, 3), 'higher_is_better': True,
-            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'bf16' if device.type == 'cuda' else 'fp32',
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': args.dtype if device.type == 'cuda' else 'fp32',
             'data': 'synthetic (random %dx%d images, random-init weights, BN calibrated, %d planted classes)' % (
                 h, w, args.plant),
             'config': {'model': '%s-faster-rcnn%s' % (args.network, '-c4' if args.network.startswith('resnet') else ''), 'global_batch': world * nb, 'ims_per_gpu': nb,

@@ -28,11 +28,12 @@ class Detector(object):
         self.model.to(self.ctx).eval()
         if compute_dtype is None:
             compute_dtype = torch.bfloat16 if self.ctx.type == 'cuda' else torch.float32
-        # The GPU kernels take bf16 or fp32 activations.  BASELINE config 5 names an fp16 MFMA path:
-        # on CDNA4 bf16 MFMA has the fp16 rate and operand width with fp32's exponent range, so
-        # inference runs bf16 (the reference itself runs fp32).
-        if compute_dtype not in (torch.bfloat16, torch.float32):
-            raise ValueError('compute_dtype must be torch.bfloat16 or torch.float32 (got %s)' % compute_dtype)
+        # bf16 (default), fp16 (BASELINE config 5's "fp16 MFMA path": v_mfma_f32_16x16x32_f16 in the
+        # conv / FC kernels, fp16 activations through BN, pooling, RoIPool and the proposal decode,
+        # fp32 accumulation and epilogue math) or fp32 (PyTorch ops; the reference runs fp32)
+        if compute_dtype not in (torch.bfloat16, torch.float16, torch.float32):
+            raise ValueError('compute_dtype must be torch.bfloat16, torch.float16 or torch.float32 (got %s)'
+                             % compute_dtype)
         self.dtype = compute_dtype
         if self.ctx.type == 'cuda' and compute_dtype != torch.float32:
             self._to_lowp()

@@ -42,6 +42,13 @@ struct DevGuard {
 #define CHECK_I32(t) TORCH_CHECK((t).scalar_type() == at::kInt, #t " must be int32")
 #define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
 
+// 16-bit storage code of the dtype-generic kernels: 0 fp32, 1 bf16, 2 fp16
+int dcode(const Tensor& t) {
+  TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat || t.scalar_type() == at::kHalf,
+              "expected bf16, fp16 or fp32 tensor");
+  return t.scalar_type() == at::kBFloat16 ? 1 : t.scalar_type() == at::kHalf ? 2 : 0;
+}
+
 int is_bf16(const Tensor& t) {
   TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat, "expected bf16 or fp32 tensor");
   return t.scalar_type() == at::kBFloat16 ? 1 : 0;
@@ -64,8 +71,8 @@ std::vector<Tensor> proposal_decode(const Tensor& cls, const Tensor& dlt, const 
   auto opts = cls.options().dtype(at::kFloat);
   Tensor boxes = at::empty({B, N, 4}, opts);
   Tensor keys = at::empty({B, N}, opts);
-  mxr::proposal_decode(cls.data_ptr(), is_bf16(cls), cls.stride(0), cls.stride(1), cls.stride(2), cls.stride(3),
-                       dlt.data_ptr(), is_bf16(dlt), dlt.stride(0), dlt.stride(1), dlt.stride(2), dlt.stride(3),
+  mxr::proposal_decode(cls.data_ptr(), dcode(cls), cls.stride(0), cls.stride(1), cls.stride(2), cls.stride(3),
+                       dlt.data_ptr(), dcode(dlt), dlt.stride(0), dlt.stride(1), dlt.stride(2), dlt.stride(3),
                        is_prob ? 1 : 0, im_info.data_ptr<float>(), base_anchors.data_ptr<float>(), A, B, H, W,
                        (float)feat_stride, (float)min_size, crop_to_im ? 1 : 0, boxes.data_ptr<float>(),
                        keys.data_ptr<float>(), cur_stream());
@@ -229,7 +236,7 @@ std::vector<Tensor> roi_pool_fwd(const Tensor& feat, const Tensor& rois, int64_t
   DevGuard g(feat.device());
   Tensor out = at::empty({R, C, PH, PW}, feat.options().memory_format(at::MemoryFormat::ChannelsLast));
   Tensor argmax = at::empty({R, C, PH, PW}, feat.options().dtype(at::kInt).memory_format(at::MemoryFormat::ChannelsLast));
-  mxr::roi_pool_fwd(feat.data_ptr(), is_bf16(feat), B, H, W, C, rois.data_ptr<float>(), R, (int)PH, (int)PW,
+  mxr::roi_pool_fwd(feat.data_ptr(), dcode(feat), B, H, W, C, rois.data_ptr<float>(), R, (int)PH, (int)PW,
                     (float)scale, out.data_ptr(), argmax.data_ptr<int32_t>(), cur_stream());
   return {out, argmax};
 }
@@ -407,7 +414,7 @@ Tensor bn_relu_fwd(const Tensor& x, const Tensor& gamma, const Tensor& beta, con
   }
   DevGuard g(x.device());
   Tensor y = at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast);
-  mxr::bn_relu_fwd(x.data_ptr(), is_bf16(x), x.numel() / C, C, gamma.data_ptr<float>(), beta.data_ptr<float>(),
+  mxr::bn_relu_fwd(x.data_ptr(), dcode(x), x.numel() / C, C, gamma.data_ptr<float>(), beta.data_ptr<float>(),
                    mean.data_ptr<float>(), var.data_ptr<float>(), (float)eps, fix_gamma ? 1 : 0, relu ? 1 : 0,
                    y.data_ptr(), cur_stream());
   return y;
@@ -504,7 +511,9 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
                                    c10::optional<Tensor> drop_step, int64_t pad_w, c10::optional<Tensor> out,
                                    c10::optional<std::vector<int64_t>> out_map) {
   CHECK_DEV(x); CHECK_DEV(w);
-  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16, "bf16 only");
+  TORCH_CHECK((x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf) && w.scalar_type() == x.scalar_type(),
+              "conv_igemm: bf16 or fp16 activations and weights of the same dtype");
+  const bool f16 = x.scalar_type() == at::kHalf;
   TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "x must be channels_last (N,C,H,W)");
   TORCH_CHECK(w.dim() == 4 && w.is_contiguous(at::MemoryFormat::ChannelsLast), "w must be channels_last (O,I,kh,kw)");
   const int NB = (int)x.size(0), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
@@ -515,6 +524,7 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   int Ho = (H + 2 * (int)pad - KH) / (int)stride + 1, Wo = (W + 2 * padw - KW) / (int)stride + 1;
   mxr::ConvEpi ep;
   ep.relu = relu ? 1 : 0;
+  ep.f16 = f16 ? 1 : 0;
   ep.pad_w = pad_w >= 0 ? (int)pad_w : -1;
   const bool mapped = out_map.has_value();
   if (mapped) {
@@ -558,9 +568,9 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   }
   if (residual.has_value() && residual->defined()) {
     const Tensor& r = *residual;
-    TORCH_CHECK(r.scalar_type() == at::kBFloat16 && r.sizes() == y.sizes() &&
+    TORCH_CHECK(r.scalar_type() == x.scalar_type() && r.sizes() == y.sizes() &&
                     r.is_contiguous(at::MemoryFormat::ChannelsLast),
-                "residual must be a channels_last bf16 tensor shaped like the output");
+                "residual must be a channels_last tensor of the activation dtype shaped like the output");
     ep.residual = reinterpret_cast<const uint16_t*>(r.data_ptr());
   }
   Tensor y2;
@@ -612,6 +622,7 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   int t = mxr::conv_igemm_plan(NB, Ho, Wo, Cin, Cout, KH, KW, (int)tile, &auto_splits);
   // BN-backward epilogue: no split-K by default (the statistics are reduced in-tile instead)
   int sp = splits > 0 ? (int)splits : (bwd_mode ? 1 : auto_splits);
+  if (f16 && !(t == 21 || t == 22 || t == 23 || t >= 100)) t = 23;  // fp16 MFMA: buffer / ring kernels
   if (mapped || ep.pad_w >= 0) {  // geometry extensions: buffer / ring kernels, no split-K
     if (!(t == 22 || t == 23 || t >= 100)) t = 23;
     sp = 1;
@@ -713,8 +724,9 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
 // ---- pooling ---------------------------------------------------------------------------------
 std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t p) {
   CHECK_DEV(x);
-  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "maxpool: x must be channels_last bf16 (N,C,H,W)");
+  TORCH_CHECK((x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf) && x.dim() == 4 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "maxpool: x must be channels_last bf16 / fp16 (N,C,H,W)");
   const int N = (int)x.size(0), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
   TORCH_CHECK(C % 8 == 0, "maxpool needs C % 8 == 0");
   const int Ho = (H + 2 * (int)p - (int)k) / (int)s + 1, Wo = (W + 2 * (int)p - (int)k) / (int)s + 1;
@@ -723,15 +735,16 @@ std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t p
   Tensor y = at::empty({N, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   Tensor arg = at::empty({N, C, Ho, Wo}, x.options().dtype(at::kByte).memory_format(at::MemoryFormat::ChannelsLast));
   const int rc = mxr::maxpool_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<uint16_t*>(y.data_ptr()),
-                                  arg.data_ptr<uint8_t>(), N, H, W, C, Ho, Wo, (int)k, (int)s, (int)p, cur_stream());
+                                  arg.data_ptr<uint8_t>(), N, H, W, C, Ho, Wo, (int)k, (int)s, (int)p, dcode(x),
+                                  cur_stream());
   TORCH_CHECK(rc == 0, "maxpool_fwd: unsupported shape");
   return {y, arg};
 }
 
 Tensor maxpool_bwd(const Tensor& dy, const Tensor& arg, int64_t H, int64_t W, int64_t k, int64_t s, int64_t p) {
   CHECK_DEV(dy); CHECK_DEV(arg);
-  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.is_contiguous(at::MemoryFormat::ChannelsLast) &&
-                  arg.scalar_type() == at::kByte && arg.sizes() == dy.sizes() &&
+  TORCH_CHECK((dy.scalar_type() == at::kBFloat16 || dy.scalar_type() == at::kHalf) &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast) && arg.scalar_type() == at::kByte && arg.sizes() == dy.sizes() &&
                   arg.is_contiguous(at::MemoryFormat::ChannelsLast), "maxpool_bwd: channels_last bf16 dy + byte arg");
   const int N = (int)dy.size(0), C = (int)dy.size(1), Ho = (int)dy.size(2), Wo = (int)dy.size(3);
   TORCH_CHECK((H + 2 * p - k) / s + 1 == Ho && (W + 2 * p - k) / s + 1 == Wo, "maxpool_bwd: shape mismatch");
@@ -739,31 +752,33 @@ Tensor maxpool_bwd(const Tensor& dy, const Tensor& arg, int64_t H, int64_t W, in
   Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   const int rc = mxr::maxpool_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), arg.data_ptr<uint8_t>(),
                                   reinterpret_cast<uint16_t*>(dx.data_ptr()), N, (int)H, (int)W, C, Ho, Wo, (int)k,
-                                  (int)s, (int)p, cur_stream());
+                                  (int)s, (int)p, dcode(dy), cur_stream());
   TORCH_CHECK(rc == 0, "maxpool_bwd: unsupported shape");
   return dx;
 }
 
 Tensor avgpool_fwd(const Tensor& x) {
   CHECK_DEV(x);
-  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
-              "avgpool: x must be channels_last bf16 (N,C,H,W)");
+  TORCH_CHECK((x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf) && x.dim() == 4 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "avgpool: x must be channels_last bf16 / fp16 (N,C,H,W)");
   const int N = (int)x.size(0), C = (int)x.size(1), HW = (int)(x.size(2) * x.size(3));
   DevGuard g(x.device());
   Tensor y = at::empty({N, C}, x.options());
   TORCH_CHECK(mxr::avgpool_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<uint16_t*>(y.data_ptr()),
-                               N, HW, C, cur_stream()) == 0, "avgpool_fwd: C % 8 != 0");
+                               N, HW, C, dcode(x), cur_stream()) == 0, "avgpool_fwd: C % 8 != 0");
   return y;
 }
 
 Tensor avgpool_bwd(const Tensor& dy, int64_t H, int64_t W) {
   CHECK_DEV(dy);
-  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.dim() == 2 && dy.is_contiguous(), "avgpool_bwd: dy (N, C) bf16");
+  TORCH_CHECK((dy.scalar_type() == at::kBFloat16 || dy.scalar_type() == at::kHalf) && dy.dim() == 2 && dy.is_contiguous(),
+              "avgpool_bwd: dy (N, C) bf16 / fp16");
   const int N = (int)dy.size(0), C = (int)dy.size(1);
   DevGuard g(dy.device());
   Tensor dx = at::empty({N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   TORCH_CHECK(mxr::avgpool_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<uint16_t*>(dx.data_ptr()),
-                               N, (int)(H * W), C, cur_stream()) == 0, "avgpool_bwd: C % 8 != 0");
+                               N, (int)(H * W), C, dcode(dy), cur_stream()) == 0, "avgpool_bwd: C % 8 != 0");
   return dx;
 }
 

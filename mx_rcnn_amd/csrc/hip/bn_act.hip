@@ -27,7 +27,7 @@ __device__ __forceinline__ void bn_coeffs(int c, const float* gamma, const float
 __device__ __forceinline__ void load4(const void* p, int64_t i, int bf16, float v[4]) {
   if (bf16) {
     const ushort4 u = *reinterpret_cast<const ushort4*>(static_cast<const uint16_t*>(p) + i);
-    v[0] = bf16_to_f32(u.x); v[1] = bf16_to_f32(u.y); v[2] = bf16_to_f32(u.z); v[3] = bf16_to_f32(u.w);
+    v[0] = h16_to_f32(u.x, bf16); v[1] = h16_to_f32(u.y, bf16); v[2] = h16_to_f32(u.z, bf16); v[3] = h16_to_f32(u.w, bf16);
   } else {
     const float4 f = *reinterpret_cast<const float4*>(static_cast<const float*>(p) + i);
     v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
@@ -36,7 +36,7 @@ __device__ __forceinline__ void load4(const void* p, int64_t i, int bf16, float 
 __device__ __forceinline__ void store4(void* p, int64_t i, int bf16, const float v[4]) {
   if (bf16)
     *reinterpret_cast<ushort4*>(static_cast<uint16_t*>(p) + i) =
-        make_ushort4(f32_to_bf16(v[0]), f32_to_bf16(v[1]), f32_to_bf16(v[2]), f32_to_bf16(v[3]));
+        make_ushort4(f32_to_h16(v[0], bf16), f32_to_h16(v[1], bf16), f32_to_h16(v[2], bf16), f32_to_h16(v[3], bf16));
   else
     *reinterpret_cast<float4*>(static_cast<float*>(p) + i) = make_float4(v[0], v[1], v[2], v[3]);
 }

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
+#include <hip/hip_fp16.h>
 #include <cstdint>
 #include <cfloat>
 
@@ -16,11 +17,21 @@ __device__ __forceinline__ uint16_t f32_to_bf16(float f) {
   __hip_bfloat16 h = __float2bfloat16(f);  // v_cvt_pk_bf16_f32 (RNE, NaN-preserving)
   return *reinterpret_cast<uint16_t*>(&h);
 }
-__device__ __forceinline__ float ld(const void* p, int64_t i, int bf16) {
-  return bf16 ? bf16_to_f32(static_cast<const uint16_t*>(p)[i]) : static_cast<const float*>(p)[i];
+__device__ __forceinline__ float f16_to_f32(uint16_t v) { return __half2float(__ushort_as_half(v)); }
+__device__ __forceinline__ uint16_t f32_to_f16(float f) { return __half_as_ushort(__float2half(f)); }
+
+// 16-bit storage codes used by the kernels' dtype flags: 0 = fp32, 1 = bf16, 2 = fp16
+__device__ __forceinline__ float h16_to_f32(uint16_t v, int code) {
+  return code == 2 ? f16_to_f32(v) : bf16_to_f32(v);
 }
-__device__ __forceinline__ void st(void* p, int64_t i, float v, int bf16) {
-  if (bf16) static_cast<uint16_t*>(p)[i] = f32_to_bf16(v);
+__device__ __forceinline__ uint16_t f32_to_h16(float f, int code) {
+  return code == 2 ? f32_to_f16(f) : f32_to_bf16(f);
+}
+__device__ __forceinline__ float ld(const void* p, int64_t i, int code) {
+  return code ? h16_to_f32(static_cast<const uint16_t*>(p)[i], code) : static_cast<const float*>(p)[i];
+}
+__device__ __forceinline__ void st(void* p, int64_t i, float v, int code) {
+  if (code) static_cast<uint16_t*>(p)[i] = f32_to_h16(v, code);
   else static_cast<float*>(p)[i] = v;
 }
 
@@ -38,6 +49,31 @@ __device__ __forceinline__ void st8_bf16(uint16_t* p, const float* v) {
   uint32_t w[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k) w[k] = (uint32_t)f32_to_bf16(v[2 * k]) | ((uint32_t)f32_to_bf16(v[2 * k + 1]) << 16);
+  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+// 8 consecutive 16-bit values (bf16 or fp16 by code) <-> fp32 through one 16-B access
+__device__ __forceinline__ void ld8_h16(const uint16_t* p, float* v, int code) {
+  if (code != 2) {
+    ld8_bf16(p, v);
+    return;
+  }
+  const uint4 u = *reinterpret_cast<const uint4*>(p);
+  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    v[2 * k] = f16_to_f32((uint16_t)(w[k] & 0xffffu));
+    v[2 * k + 1] = f16_to_f32((uint16_t)(w[k] >> 16));
+  }
+}
+__device__ __forceinline__ void st8_h16(uint16_t* p, const float* v, int code) {
+  if (code != 2) {
+    st8_bf16(p, v);
+    return;
+  }
+  uint32_t w[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) w[k] = (uint32_t)f32_to_f16(v[2 * k]) | ((uint32_t)f32_to_f16(v[2 * k + 1]) << 16);
   *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 

@@ -29,10 +29,33 @@
 #include "common.h"
 #include "../kernels.h"
 
+// epilogue storage code: fp16 when the conv runs on fp16 activations (inference), else bf16
+#define EPC (ep.f16 ? 2 : 1)
+
 namespace mxr {
 
+__device__ __forceinline__ uint16_t f32_to_h16c(int code, float f) { return f32_to_h16(f, code); }
+__device__ __forceinline__ float h16_to_f32c(int code, uint16_t v) { return h16_to_f32(v, code); }
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// MFMA 16x16x32 on bf16 or fp16 operands (same rate, same fragment layout)
+template <bool F16> struct Mfma16;
+template <> struct Mfma16<false> {
+  typedef bf16x8 T;
+  __device__ static __forceinline__ f32x4 mma(T a, T b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+template <> struct Mfma16<true> {
+  typedef f16x8 T;
+  __device__ static __forceinline__ f32x4 mma(T a, T b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
 
 constexpr int BK = 64;  // bf16 elements per K-step (one 128-B row per tile row)
 
@@ -80,30 +103,30 @@ __device__ __forceinline__ float epi_dropout(const ConvEpi& ep, int64_t idx, flo
 __device__ __forceinline__ void epi_store(const ConvEpi& ep, const EpiCol& c, uint16_t* __restrict__ y, int64_t idx,
                                           float v) {
   v += c.bias;
-  if (ep.residual) v += bf16_to_f32(ep.residual[idx]);
+  if (ep.residual) v += h16_to_f32c(EPC, ep.residual[idx]);
   if (ep.relu) v = fmaxf(v, 0.f);
   v = epi_dropout(ep, idx, v);
-  const uint16_t yb = f32_to_bf16(v);
+  const uint16_t yb = f32_to_h16c(EPC, v);
   y[idx] = yb;
   if (ep.y2) {
     // the BN reads the STORED (bf16-rounded) conv output, exactly like the unfused pair
-    float a = bf16_to_f32(yb) * c.s + c.t;
+    float a = h16_to_f32c(EPC, yb) * c.s + c.t;
     if (ep.act_relu) a = fmaxf(a, 0.f);
-    ep.y2[idx] = f32_to_bf16(a);
+    ep.y2[idx] = f32_to_h16c(EPC, a);
   }
 }
 
 // BN-backward epilogue of one element; returns (g, g * xhat) through sg / sgx
 __device__ __forceinline__ void epi_bnb(const ConvEpi& ep, const EpiCol& c, uint16_t* __restrict__ y, int64_t idx,
                                         float v, float& sg, float& sgx) {
-  if (ep.dadd) v += bf16_to_f32(ep.dadd[idx]);
-  const float xv = bf16_to_f32(ep.bnb_x[idx]);
+  if (ep.dadd) v += h16_to_f32c(EPC, ep.dadd[idx]);
+  const float xv = h16_to_f32c(EPC, ep.bnb_x[idx]);
   const float g = (!ep.act_relu || xv * c.s + c.t > 0.f) ? v : 0.f;
   sg += g;
   sgx += g * (xv - c.mean) * c.inv;
   float o = g * c.s;
-  if (ep.residual) o += bf16_to_f32(ep.residual[idx]);
-  y[idx] = f32_to_bf16(o);
+  if (ep.residual) o += h16_to_f32c(EPC, ep.residual[idx]);
+  y[idx] = f32_to_h16c(EPC, o);
 }
 
 // Shared epilogue of the implicit-GEMM kernels: C/D map col = lane & 15, row = (lane >> 4) * 4 + r.
@@ -227,13 +250,13 @@ __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* 
       const float4* src = reinterpret_cast<const float4*>(T + row * LDT + cv * 8);
       const float4 a0 = src[0], a1 = src[1];
       a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w; a[4] = a1.x; a[5] = a1.y; a[6] = a1.z; a[7] = a1.w;
-      ld8_bf16(ep.bnb_x + e, xv);
+      ld8_h16(ep.bnb_x + e, xv, EPC);
       if (ep.dadd) {
-        ld8_bf16(ep.dadd + e, d);
+        ld8_h16(ep.dadd + e, d, EPC);
 #pragma unroll
         for (int k = 0; k < 8; ++k) a[k] += d[k];
       }
-      if (ep.residual) ld8_bf16(ep.residual + e, rs);
+      if (ep.residual) ld8_h16(ep.residual + e, rs, EPC);
       float o[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -242,7 +265,7 @@ __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* 
         sgx[k] += g * (xv[k] - ec[k].mean) * ec[k].inv;
         o[k] = g * ec[k].s + (ep.residual ? rs[k] : 0.f);
       }
-      st8_bf16(y + e, o);
+      st8_h16(y + e, o, EPC);
     }
     // reduce over the lanes of this wave that share the column group, then over the waves
 #pragma unroll
@@ -287,7 +310,7 @@ __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* 
     const float4 a0 = src[0], a1 = src[1];
     float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
     float rs[8];
-    if (ep.residual) ld8_bf16(ep.residual + e, rs);
+    if (ep.residual) ld8_h16(ep.residual + e, rs, EPC);
     uint16_t yb[8];
     float y2v[8];
 #pragma unroll
@@ -295,15 +318,15 @@ __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* 
       float t = a[k] + ec[k].bias + (ep.residual ? rs[k] : 0.f);
       if (ep.relu) t = fmaxf(t, 0.f);
       t = epi_dropout(ep, e + k, t);
-      yb[k] = f32_to_bf16(t);
-      float q = bf16_to_f32(yb[k]) * ec[k].s + ec[k].t;  // the BN reads the STORED conv output
+      yb[k] = f32_to_h16c(EPC, t);
+      float q = h16_to_f32c(EPC, yb[k]) * ec[k].s + ec[k].t;  // the BN reads the STORED conv output
       if (ep.act_relu) q = fmaxf(q, 0.f);
       y2v[k] = q;
     }
     *reinterpret_cast<uint4*>(y + e) =
         make_uint4((uint32_t)yb[0] | ((uint32_t)yb[1] << 16), (uint32_t)yb[2] | ((uint32_t)yb[3] << 16),
                    (uint32_t)yb[4] | ((uint32_t)yb[5] << 16), (uint32_t)yb[6] | ((uint32_t)yb[7] << 16));
-    if (ep.y2) st8_bf16(ep.y2 + e, y2v);
+    if (ep.y2) st8_h16(ep.y2 + e, y2v, EPC);
   }
 }
 
@@ -502,7 +525,7 @@ splitk_reduce_kernel(const float* __restrict__ slab, int splits, int64_t MN, int
   float res[4] = {0.f, 0.f, 0.f, 0.f};
   if (ep.residual) {
     const ushort4 rv = *reinterpret_cast<const ushort4*>(ep.residual + e);
-    res[0] = bf16_to_f32(rv.x); res[1] = bf16_to_f32(rv.y); res[2] = bf16_to_f32(rv.z); res[3] = bf16_to_f32(rv.w);
+    res[0] = h16_to_f32c(EPC, rv.x); res[1] = h16_to_f32c(EPC, rv.y); res[2] = h16_to_f32c(EPC, rv.z); res[3] = h16_to_f32c(EPC, rv.w);
   }
   uint16_t out[4], out2[4];
 #pragma unroll
@@ -511,10 +534,10 @@ splitk_reduce_kernel(const float* __restrict__ slab, int splits, int64_t MN, int
     float t = v[k] + c.bias + res[k];
     if (ep.relu) t = fmaxf(t, 0.f);
     t = epi_dropout(ep, e + k, t);
-    out[k] = f32_to_bf16(t);
-    float q = bf16_to_f32(out[k]) * c.s + c.t;
+    out[k] = f32_to_h16c(EPC, t);
+    float q = h16_to_f32c(EPC, out[k]) * c.s + c.t;
     if (ep.act_relu) q = fmaxf(q, 0.f);
-    out2[k] = f32_to_bf16(q);
+    out2[k] = f32_to_h16c(EPC, q);
   }
   *reinterpret_cast<ushort4*>(y + e) = make_ushort4(out[0], out[1], out[2], out[3]);
   if (ep.y2) *reinterpret_cast<ushort4*>(ep.y2 + e) = make_ushort4(out2[0], out2[1], out2[2], out2[3]);
@@ -693,7 +716,7 @@ __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t rs, void* lds_w
                                            (int)voff, (int)soff, 0, 0);
 }
 
-template <int BM, int BN, int S>
+template <int BM, int BN, int S, bool F16 = false>
 __global__ void __launch_bounds__(256)
 conv_igemm_buf_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
                       int NB, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad,
@@ -800,23 +823,23 @@ conv_igemm_buf_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
     const int buf = ks % S;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[TM], bfr[TN];
+      typename Mfma16<F16>::T af[TM], bfr[TN];
       const int chunk = kk * 4 + (lane >> 4);
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * WM + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const bf16x8*>(As + (buf * BM + row) * BK + swz(row, chunk) * 8);
+        af[i] = *reinterpret_cast<const typename Mfma16<F16>::T*>(As + (buf * BM + row) * BK + swz(row, chunk) * 8);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * WN + j * 16 + (lane & 15);
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (buf * BN + row) * BK + swz(row, chunk) * 8);
+        bfr[j] = *reinterpret_cast<const typename Mfma16<F16>::T*>(Bs + (buf * BN + row) * BK + swz(row, chunk) * 8);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = Mfma16<F16>::mma(af[i], bfr[j], acc[i][j]);
     }
   }
   static_assert(BM * (BN + 4) * 4 <= S * (BM + BN) * BK * 2, "epilogue tile must fit the operand ring");
@@ -918,13 +941,13 @@ __device__ __forceinline__ void ring_epilogue(f32x4 (&acc)[TM][TN], float* __res
       const float4* src = reinterpret_cast<const float4*>(T + row * LDT + cv * 8);
       const float4 a0 = src[0], a1 = src[1];
       a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w; a[4] = a1.x; a[5] = a1.y; a[6] = a1.z; a[7] = a1.w;
-      ld8_bf16(ep.bnb_x + e, xv);
+      ld8_h16(ep.bnb_x + e, xv, EPC);
       if (ep.dadd) {
-        ld8_bf16(ep.dadd + e, d);
+        ld8_h16(ep.dadd + e, d, EPC);
 #pragma unroll
         for (int k = 0; k < 8; ++k) a[k] += d[k];
       }
-      if (ep.residual) ld8_bf16(ep.residual + e, rs);
+      if (ep.residual) ld8_h16(ep.residual + e, rs, EPC);
       float o[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -933,7 +956,7 @@ __device__ __forceinline__ void ring_epilogue(f32x4 (&acc)[TM][TN], float* __res
         sgx[k] += g * (xv[k] - ec[k].mean) * ec[k].inv;
         o[k] = g * ec[k].s + (ep.residual ? rs[k] : 0.f);
       }
-      st8_bf16(y + e, o);
+      st8_h16(y + e, o, EPC);
     }
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -976,7 +999,7 @@ __device__ __forceinline__ void ring_epilogue(f32x4 (&acc)[TM][TN], float* __res
     const float4 a0 = src[0], a1 = src[1];
     float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
     float rs[8];
-    if (ep.residual) ld8_bf16(ep.residual + e, rs);
+    if (ep.residual) ld8_h16(ep.residual + e, rs, EPC);
     uint16_t yb[8];
     float y2v[8];
 #pragma unroll
@@ -984,19 +1007,19 @@ __device__ __forceinline__ void ring_epilogue(f32x4 (&acc)[TM][TN], float* __res
       float t = a[k] + ec[k].bias + (ep.residual ? rs[k] : 0.f);
       if (ep.relu) t = fmaxf(t, 0.f);
       t = epi_dropout(ep, e + k, t);
-      yb[k] = f32_to_bf16(t);
-      float qv = bf16_to_f32(yb[k]) * ec[k].s + ec[k].t;
+      yb[k] = f32_to_h16c(EPC, t);
+      float qv = h16_to_f32c(EPC, yb[k]) * ec[k].s + ec[k].t;
       if (ep.act_relu) qv = fmaxf(qv, 0.f);
       y2v[k] = qv;
     }
     *reinterpret_cast<uint4*>(y + e) =
         make_uint4((uint32_t)yb[0] | ((uint32_t)yb[1] << 16), (uint32_t)yb[2] | ((uint32_t)yb[3] << 16),
                    (uint32_t)yb[4] | ((uint32_t)yb[5] << 16), (uint32_t)yb[6] | ((uint32_t)yb[7] << 16));
-    if (ep.y2) st8_bf16(ep.y2 + e, y2v);
+    if (ep.y2) st8_h16(ep.y2 + e, y2v, EPC);
   }
 }
 
-template <int TM, int TN, int WGM, int WGN, int SFIX, bool ONE>
+template <int TM, int TN, int WGM, int WGN, int SFIX, bool ONE, bool F16 = false>
 __global__ void __launch_bounds__(64 * WGM * WGN)
 conv_ring_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int NB,
                  int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad,
@@ -1111,23 +1134,23 @@ conv_ring_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
     const int buf = ks % S;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[TM], bfr[TN];
+      typename Mfma16<F16>::T af[TM], bfr[TN];
       const int chunk = kk * 4 + (lane >> 4);
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         const int row = wm * 16 * TM + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const bf16x8*>(As + (buf * BM + row) * BK + swz(row, chunk) * 8);
+        af[i] = *reinterpret_cast<const typename Mfma16<F16>::T*>(As + (buf * BM + row) * BK + swz(row, chunk) * 8);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * 16 * TN + j * 16 + (lane & 15);
-        bfr[j] = *reinterpret_cast<const bf16x8*>(Bs + (buf * BN + row) * BK + swz(row, chunk) * 8);
+        bfr[j] = *reinterpret_cast<const typename Mfma16<F16>::T*>(Bs + (buf * BN + row) * BK + swz(row, chunk) * 8);
       }
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = Mfma16<F16>::mma(af[i], bfr[j], acc[i][j]);
     }
   }
   if (Cout % 8 == 0)
@@ -1175,13 +1198,19 @@ static void launch_ring(const uint16_t* x, const uint16_t* w, uint16_t* y, int N
   const int tiles_m = (M + C::BM - 1) / C::BM, tiles_n = (Cout + C::BN - 1) / C::BN;
   const int ntiles = tiles_m * tiles_n;
   const int nwg = ntiles * splits;
-  if (KH == 1 && KW == 1 && pad == 0 && ep.pad_w <= 0)
-    conv_ring_kernel<TM, TN, WGM, WGN, SFIX, true><<<nwg, C::NT, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW,
-                                                                    stride, pad, ep, tiles_n, nwg, ntiles, splits, slab);
-  else
-    conv_ring_kernel<TM, TN, WGM, WGN, SFIX, false><<<nwg, C::NT, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW,
-                                                                     stride, pad, ep, tiles_n, nwg, ntiles, splits,
-                                                                     slab);
+  const bool one = KH == 1 && KW == 1 && pad == 0 && ep.pad_w <= 0;
+#define MXR_RING_LAUNCH(ONE_, F16_)                                                                              \
+  conv_ring_kernel<TM, TN, WGM, WGN, SFIX, ONE_, F16_><<<nwg, C::NT, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, \
+                                                                             KH, KW, stride, pad, ep, tiles_n, nwg,  \
+                                                                             ntiles, splits, slab)
+  if (ep.f16) {
+    if (one) MXR_RING_LAUNCH(true, true);
+    else MXR_RING_LAUNCH(false, true);
+  } else {
+    if (one) MXR_RING_LAUNCH(true, false);
+    else MXR_RING_LAUNCH(false, false);
+  }
+#undef MXR_RING_LAUNCH
   if (splits > 1) {
     const int64_t MN = (int64_t)M * Cout;
     if (ep.bnb_x)
@@ -1236,9 +1265,14 @@ static void launch_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB
   const int tiles_m = (M + BM - 1) / BM, tiles_n = (Cout + BN - 1) / BN;
   const int ntiles = tiles_m * tiles_n;
   const int nwg = ntiles * splits;
-  if constexpr (BUF)
-    conv_igemm_buf_kernel<BM, BN, S><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
-                                                         ep, tiles_n, nwg, ntiles, splits, slab);
+  if constexpr (BUF) {
+    if (ep.f16)
+      conv_igemm_buf_kernel<BM, BN, S, true><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
+                                                                 pad, ep, tiles_n, nwg, ntiles, splits, slab);
+    else
+      conv_igemm_buf_kernel<BM, BN, S, false><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
+                                                                  pad, ep, tiles_n, nwg, ntiles, splits, slab);
+  }
   else if constexpr (S > 0)
     conv_igemm_glds_kernel<BM, BN, S><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
                                                           ep, tiles_n, nwg, ntiles, splits, slab);
@@ -1299,6 +1333,7 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
     return -1;
   if (ep.y2 && ep.bnb_x) return -1;
   if ((ep.omap || ep.pad_w >= 0) && (splits > 1 || !(tile == 22 || tile == 23 || tile >= 100))) return -1;
+  if (ep.f16 && !(tile == 21 || tile == 22 || tile == 23 || tile >= 100)) return -1;
   // buffer variants: 32-bit byte offsets below the kBufOOB sentinel, tap mask of 64 bits
   if (tile >= 100 && ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB ||
                       (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kBufOOB || KH * KW > 64))

@@ -1,4 +1,5 @@
-// Max-pool forward / backward and global average pool on NHWC bf16 maps (SURVEY kernel K14).
+// Max-pool forward / backward and global average pool on NHWC bf16 / fp16 maps (SURVEY kernel K14;
+// `code` = 1 bf16, 2 fp16).
 //
 // Reference ops: VGG pool1..pool4 2x2/2 (`rcnn/symbol.py:19,28,40,52`), ResNet pool0 3x3/2 pad 1
 // (`rcnn/resnet.py:150`), global average pool before the predictors (`rcnn/resnet.py:167`).
@@ -19,7 +20,7 @@ namespace mxr {
 
 __global__ void __launch_bounds__(256)
 maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, uint8_t* __restrict__ arg, int N, int H,
-                   int W, int C, int Ho, int Wo, int k, int s, int p) {
+                   int W, int C, int Ho, int Wo, int k, int s, int p, int code) {
   const int cv = C / 8;
   const int64_t total = (int64_t)N * Ho * Wo * cv;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -42,7 +43,7 @@ maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, uin
       const int w = w0 + j;
       if ((unsigned)w >= (unsigned)W) continue;
       float v[8];
-      ld8_bf16(x + (((int64_t)n * H + h) * W + w) * C + c8 * 8, v);
+      ld8_h16(x + (((int64_t)n * H + h) * W + w) * C + c8 * 8, v, code);
 #pragma unroll
       for (int q = 0; q < 8; ++q)
         if (v[q] > best[q] || bi[q] == 255) {  // strict: the first maximum wins
@@ -51,7 +52,7 @@ maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, uin
         }
     }
   }
-  st8_bf16(y + pix * C + c8 * 8, best);
+  st8_h16(y + pix * C + c8 * 8, best, code);
   uint32_t lo = 0, hi = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -63,7 +64,7 @@ maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, uin
 
 __global__ void __launch_bounds__(256)
 maxpool_bwd_kernel(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ arg, uint16_t* __restrict__ dx,
-                   int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p) {
+                   int N, int H, int W, int C, int Ho, int Wo, int k, int s, int p, int code) {
   const int cv = C / 8;
   const int64_t total = (int64_t)N * H * W * cv;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -84,7 +85,7 @@ maxpool_bwd_kernel(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ 
       const int64_t o = (((int64_t)n * Ho + ho) * Wo + wo) * C + c8 * 8;
       const uint2 a = *reinterpret_cast<const uint2*>(arg + o);
       float g[8];
-      ld8_bf16(dy + o, g);
+      ld8_h16(dy + o, g, code);
       const int tap = i * k + j;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -93,11 +94,11 @@ maxpool_bwd_kernel(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ 
       }
     }
   }
-  st8_bf16(dx + pix * C + c8 * 8, acc);
+  st8_h16(dx + pix * C + c8 * 8, acc, code);
 }
 
 __global__ void __launch_bounds__(64)
-avgpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int HW, int C) {
+avgpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int HW, int C, int code) {
   const int n = blockIdx.y;
   const int c = (blockIdx.x * 64 + threadIdx.x) * 8;
   if (c >= C) return;
@@ -105,18 +106,18 @@ avgpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int
   const uint16_t* base = x + (int64_t)n * HW * C + c;
   for (int i = 0; i < HW; ++i) {
     float v[8];
-    ld8_bf16(base + (int64_t)i * C, v);
+    ld8_h16(base + (int64_t)i * C, v, code);
 #pragma unroll
     for (int q = 0; q < 8; ++q) acc[q] += v[q];
   }
   const float inv = 1.f / (float)HW;
 #pragma unroll
   for (int q = 0; q < 8; ++q) acc[q] *= inv;
-  st8_bf16(y + (int64_t)n * C + c, acc);
+  st8_h16(y + (int64_t)n * C + c, acc, code);
 }
 
 __global__ void __launch_bounds__(256)
-avgpool_bwd_kernel(const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx, int N, int HW, int C) {
+avgpool_bwd_kernel(const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx, int N, int HW, int C, int code) {
   const int cv = C / 8;
   const int64_t total = (int64_t)N * HW * cv;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -124,42 +125,42 @@ avgpool_bwd_kernel(const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx, i
   const int c8 = (int)(t % cv);
   const int n = (int)(t / ((int64_t)HW * cv));
   float g[8];
-  ld8_bf16(dy + (int64_t)n * C + c8 * 8, g);
+  ld8_h16(dy + (int64_t)n * C + c8 * 8, g, code);
   const float inv = 1.f / (float)HW;
 #pragma unroll
   for (int q = 0; q < 8; ++q) g[q] *= inv;
-  st8_bf16(dx + (t / cv) * C + c8 * 8, g);
+  st8_h16(dx + (t / cv) * C + c8 * 8, g, code);
 }
 
 int maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int Ho, int Wo, int k,
-                int s, int p, hipStream_t st) {
+                int s, int p, int code, hipStream_t st) {
   if (C % 8 != 0 || k > 15 || k <= 0 || s <= 0) return -1;
   const int64_t total = (int64_t)N * Ho * Wo * (C / 8);
   if (total == 0) return 0;
-  maxpool_fwd_kernel<<<div_up(total, 256), 256, 0, st>>>(x, y, arg, N, H, W, C, Ho, Wo, k, s, p);
+  maxpool_fwd_kernel<<<div_up(total, 256), 256, 0, st>>>(x, y, arg, N, H, W, C, Ho, Wo, k, s, p, code);
   return 0;
 }
 
 int maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int H, int W, int C, int Ho, int Wo,
-                int k, int s, int p, hipStream_t st) {
+                int k, int s, int p, int code, hipStream_t st) {
   if (C % 8 != 0 || k > 15 || k <= 0 || s <= 0) return -1;
   const int64_t total = (int64_t)N * H * W * (C / 8);
   if (total == 0) return 0;
-  maxpool_bwd_kernel<<<div_up(total, 256), 256, 0, st>>>(dy, arg, dx, N, H, W, C, Ho, Wo, k, s, p);
+  maxpool_bwd_kernel<<<div_up(total, 256), 256, 0, st>>>(dy, arg, dx, N, H, W, C, Ho, Wo, k, s, p, code);
   return 0;
 }
 
-int avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st) {
+int avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, int code, hipStream_t st) {
   if (C % 8 != 0 || N == 0) return -1;
-  avgpool_fwd_kernel<<<dim3(div_up(C / 8, 64), N), 64, 0, st>>>(x, y, HW, C);
+  avgpool_fwd_kernel<<<dim3(div_up(C / 8, 64), N), 64, 0, st>>>(x, y, HW, C, code);
   return 0;
 }
 
-int avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st) {
+int avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, int code, hipStream_t st) {
   if (C % 8 != 0) return -1;
   const int64_t total = (int64_t)N * HW * (C / 8);
   if (total == 0) return 0;
-  avgpool_bwd_kernel<<<div_up(total, 256), 256, 0, st>>>(dy, dx, N, HW, C);
+  avgpool_bwd_kernel<<<div_up(total, 256), 256, 0, st>>>(dy, dx, N, HW, C, code);
   return 0;
 }
 

@@ -17,8 +17,8 @@ template <typename T> struct Vec4;
 template <> struct Vec4<float> { using type = float4; };
 template <> struct Vec4<uint16_t> { using type = ushort4; };
 
-__device__ __forceinline__ float to_f(float v) { return v; }
-__device__ __forceinline__ float to_f(uint16_t v) { return bf16_to_f32(v); }
+__device__ __forceinline__ float to_f(float v, int) { return v; }
+__device__ __forceinline__ float to_f(uint16_t v, int code) { return h16_to_f32(v, code); }
 
 struct Bin {
   int b, hs, he, ws, we;
@@ -44,7 +44,7 @@ __device__ __forceinline__ Bin roi_bin(const float* __restrict__ rois, int r, in
 
 template <typename T>
 __global__ void __launch_bounds__(256)
-roi_pool_fwd_vec4(const T* __restrict__ feat, int B, int H, int W, int C, const float* __restrict__ rois, int R,
+roi_pool_fwd_vec4(const T* __restrict__ feat, int code, int B, int H, int W, int C, const float* __restrict__ rois, int R,
                   int PH, int PW, float scale, T* __restrict__ out, int32_t* __restrict__ argmax) {
   using V = typename Vec4<T>::type;
   const int CV = C >> 2;
@@ -68,7 +68,7 @@ roi_pool_fwd_vec4(const T* __restrict__ feat, int B, int H, int W, int C, const 
       for (int w = bin.ws; w < bin.we; ++w) {
         const int idx = h * W + w;
         const V v = *reinterpret_cast<const V*>(fb + (int64_t)idx * C);
-        const float f0 = to_f(v.x), f1 = to_f(v.y), f2 = to_f(v.z), f3 = to_f(v.w);
+        const float f0 = to_f(v.x, code), f1 = to_f(v.y, code), f2 = to_f(v.z, code), f3 = to_f(v.w, code);
         if (f0 > m0) { m0 = f0; a0 = idx; }
         if (f1 > m1) { m1 = f1; a1 = idx; }
         if (f2 > m2) { m2 = f2; a2 = idx; }
@@ -78,7 +78,7 @@ roi_pool_fwd_vec4(const T* __restrict__ feat, int B, int H, int W, int C, const 
   }
   const int64_t o = t * 4;
   if constexpr (sizeof(T) == 2) {
-    ushort4 ov = make_ushort4(f32_to_bf16(m0), f32_to_bf16(m1), f32_to_bf16(m2), f32_to_bf16(m3));
+    ushort4 ov = make_ushort4(f32_to_h16(m0, code), f32_to_h16(m1, code), f32_to_h16(m2, code), f32_to_h16(m3, code));
     *reinterpret_cast<ushort4*>(out + o) = ov;
   } else {
     *reinterpret_cast<float4*>(out + o) = make_float4(m0, m1, m2, m3);
@@ -88,7 +88,7 @@ roi_pool_fwd_vec4(const T* __restrict__ feat, int B, int H, int W, int C, const 
 
 template <typename T>
 __global__ void __launch_bounds__(256)
-roi_pool_fwd_scalar(const T* __restrict__ feat, int B, int H, int W, int C, const float* __restrict__ rois, int R,
+roi_pool_fwd_scalar(const T* __restrict__ feat, int code, int B, int H, int W, int C, const float* __restrict__ rois, int R,
                     int PH, int PW, float scale, T* __restrict__ out, int32_t* __restrict__ argmax) {
   const int64_t total = (int64_t)R * PH * PW * C;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -107,11 +107,11 @@ roi_pool_fwd_scalar(const T* __restrict__ feat, int B, int H, int W, int C, cons
     for (int h = bin.hs; h < bin.he; ++h)
       for (int w = bin.ws; w < bin.we; ++w) {
         const int idx = h * W + w;
-        const float f = to_f(fb[(int64_t)idx * C]);
+        const float f = to_f(fb[(int64_t)idx * C], code);
         if (f > m) { m = f; a = idx; }
       }
   }
-  if constexpr (sizeof(T) == 2) out[t] = f32_to_bf16(m); else out[t] = m;
+  if constexpr (sizeof(T) == 2) out[t] = f32_to_h16(m, code); else out[t] = m;
   argmax[t] = a;
 }
 
@@ -128,7 +128,7 @@ roi_pool_bwd_kernel(const T* __restrict__ gout, const int32_t* __restrict__ argm
   const int r = (int)(t / ((int64_t)PH * PW * C));
   const int b = (int)rois[(int64_t)r * 5];
   if (b < 0 || b >= B) return;
-  const float g = to_f(gout[t]);
+  const float g = to_f(gout[t], 1);
   if (g != 0.f) atomicAdd(gin + ((int64_t)b * HW + a) * C + c, g);  // no-return global_atomic_add_f32
 }
 
@@ -139,18 +139,18 @@ void roi_pool_fwd(const void* feat, int bf16, int B, int H, int W, int C, const 
     const int64_t total = (int64_t)R * PH * PW * (C / 4);
     if (bf16)
       roi_pool_fwd_vec4<uint16_t><<<div_up(total, 256), 256, 0, st>>>(
-          (const uint16_t*)feat, B, H, W, C, rois, R, PH, PW, spatial_scale, (uint16_t*)out, argmax);
+          (const uint16_t*)feat, bf16, B, H, W, C, rois, R, PH, PW, spatial_scale, (uint16_t*)out, argmax);
     else
       roi_pool_fwd_vec4<float><<<div_up(total, 256), 256, 0, st>>>(
-          (const float*)feat, B, H, W, C, rois, R, PH, PW, spatial_scale, (float*)out, argmax);
+          (const float*)feat, 0, B, H, W, C, rois, R, PH, PW, spatial_scale, (float*)out, argmax);
   } else {
     const int64_t total = (int64_t)R * PH * PW * C;
     if (bf16)
       roi_pool_fwd_scalar<uint16_t><<<div_up(total, 256), 256, 0, st>>>(
-          (const uint16_t*)feat, B, H, W, C, rois, R, PH, PW, spatial_scale, (uint16_t*)out, argmax);
+          (const uint16_t*)feat, bf16, B, H, W, C, rois, R, PH, PW, spatial_scale, (uint16_t*)out, argmax);
     else
       roi_pool_fwd_scalar<float><<<div_up(total, 256), 256, 0, st>>>(
-          (const float*)feat, B, H, W, C, rois, R, PH, PW, spatial_scale, (float*)out, argmax);
+          (const float*)feat, 0, B, H, W, C, rois, R, PH, PW, spatial_scale, (float*)out, argmax);
   }
 }
 

@@ -177,6 +177,8 @@ struct ConvEpi {
   int pad_w = -1;
   int omap = 0;
   int o_H = 0, o_W = 0, o_sh = 1, o_sw = 1, o_ph = 0, o_pw = 0;
+  // fp16 activations / weights (inference): MFMA f16 operands, fp16 epilogue loads / stores
+  int f16 = 0;
 };
 // counter-based uniform in [0, 1) (Philox-4x32-10, key = (seed, 0x9E3779B9), counter = (e, s))
 float philox_uniform_host(uint32_t seed, uint64_t step, uint64_t e);
@@ -199,11 +201,11 @@ int bn_train_bwd(const uint16_t* x, const uint16_t* dy, int64_t M, int C, const 
 // ---- pooling (pool.hip): NHWC bf16, C % 8 == 0 ------------------------------------------------
 // arg: one byte per output element, the winning tap (i * k + j) of its window
 int maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int Ho, int Wo, int k,
-                int s, int p, hipStream_t st);
+                int s, int p, int code, hipStream_t st);
 int maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int H, int W, int C, int Ho, int Wo,
-                int k, int s, int p, hipStream_t st);
-int avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, hipStream_t st);
-int avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, hipStream_t st);
+                int k, int s, int p, int code, hipStream_t st);
+int avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, int code, hipStream_t st);
+int avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, int code, hipStream_t st);
 
 // ---- proposal pre-NMS top-k (topk.hip): keys (B, N), boxes (B, N, 4) -> the P best in stable
 // descending order; ws_key / ws_idx: B * P each

@@ -67,7 +67,7 @@ class ResidualUnit(nn.Module):
                 (not self.bottle_neck or _frozen(self.bn3))):
             return False
         c1 = self.conv1
-        return igemm_eligible(x, c1.weight, c1.stride, c1.pad) and c1.weight.dtype == torch.bfloat16
+        return igemm_eligible(x, c1.weight, c1.stride, c1.pad) and c1.weight.dtype == x.dtype
 
     def frozen_bns(self):
         return _frozen(self.bn1) and _frozen(self.bn2) and (not self.bottle_neck or _frozen(self.bn3))
@@ -76,7 +76,7 @@ class ResidualUnit(nn.Module):
         """The whole-unit fused op needs MFMA-eligible 1x1/3x3 shapes (any M) and frozen BNs."""
         if not fusion_enabled() or os.environ.get('MXR_FUSE_UNIT', '1') == '0' or not self.frozen_bns():
             return False
-        if not (x.is_cuda and x.dtype == torch.bfloat16 and x.is_contiguous(memory_format=torch.channels_last)):
+        if not (x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and x.is_contiguous(memory_format=torch.channels_last)):
             return False
         # forward-only units with large-M 1x1 convs (frozen stages 1-2) run faster on hipBLASLt
         needs_grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters()))
@@ -85,10 +85,10 @@ class ResidualUnit(nn.Module):
         if next_bn is not None and not (_frozen(next_bn) and next_bn.relu):
             return False
         convs = [self.conv1, self.conv2] + ([self.conv3] if self.bottle_neck else [])
-        if not all(c.weight.dtype == torch.bfloat16 and c.weight.shape[0] % 64 == 0 and c.weight.shape[1] % 64 == 0
+        if not all(c.weight.dtype == x.dtype and c.weight.shape[0] % 64 == 0 and c.weight.shape[1] % 64 == 0
                    for c in convs):
             return False
-        if not self.dim_match and not (self.sc.weight.shape[0] % 64 == 0 and self.sc.weight.dtype == torch.bfloat16):
+        if not self.dim_match and not (self.sc.weight.shape[0] % 64 == 0 and self.sc.weight.dtype == x.dtype):
             return False
         return x.shape[1] % 64 == 0 and x.shape[1] % 8 == 0
 

@@ -22,6 +22,8 @@ import torch.nn.functional as F
 from . import grad_sink
 from ._ext import need_ext
 
+LOWP = (torch.bfloat16, torch.float16)  # MFMA operand dtypes (fp16: the inference path)
+
 def igemm_enabled():
     return os.environ.get('MXR_CONV_IGEMM', '1') != '0'
 
@@ -197,7 +199,7 @@ class _ConvIgemm(torch.autograd.Function):
 def igemm_eligible(x, w, stride=1, pad=0):
     """True when the MFMA implicit-GEMM kernel is the path conv2d would take for this conv."""
     k = w.shape[2]
-    if not (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.shape[1] % 64 == 0 and
+    if not (x.is_cuda and x.dtype in LOWP and w.dtype == x.dtype and x.shape[1] % 64 == 0 and
             x.is_contiguous(memory_format=torch.channels_last) and igemm_enabled()):
         return False
     if k == 1 and pad == 0 and stride != 1:
@@ -208,7 +210,7 @@ def igemm_eligible(x, w, stride=1, pad=0):
 def conv2d(x, w, b=None, stride=1, pad=0, relu=False):
     """Conv (+bias, +optional fused ReLU) on NCHW-logical / channels_last tensors."""
     k = w.shape[2]
-    if (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.shape[1] % 64 == 0 and
+    if (x.is_cuda and x.dtype in LOWP and w.dtype == x.dtype and x.shape[1] % 64 == 0 and
             x.is_contiguous(memory_format=torch.channels_last)):
         if k == 1 and pad == 0 and stride != 1:
             x = x[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last)

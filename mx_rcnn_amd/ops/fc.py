@@ -25,7 +25,7 @@ import torch.nn.functional as F
 
 from . import grad_sink
 from ._ext import need_ext
-from .conv import cached_dgrad_weight, wgrad_enabled
+from .conv import LOWP, cached_dgrad_weight, wgrad_enabled
 
 
 def layer_seed(name, base=None):
@@ -38,7 +38,7 @@ def layer_seed(name, base=None):
 def fc_eligible(x, w):
     if os.environ.get('MXR_FC_KERNEL', '1') == '0':
         return False
-    return (x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.dim() == 2 and
+    return (x.is_cuda and x.dtype in LOWP and w.dtype == x.dtype and x.dim() == 2 and
             x.shape[1] % 64 == 0)
 
 

@@ -17,7 +17,7 @@ from ._ext import need_ext
 def _eligible(x):
     if os.environ.get('MXR_POOL_KERNEL', '1') == '0':
         return False
-    return (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and x.shape[1] % 8 == 0 and
+    return (x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and x.dim() == 4 and x.shape[1] % 8 == 0 and
             x.is_contiguous(memory_format=torch.channels_last))
 
 

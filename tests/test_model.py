@@ -175,3 +175,44 @@ def test_vgg16_e2e_step_gpu_graph(cuda):
         losses.append(float(o['loss'].float().item()))
     assert all(math.isfinite(v) for v in losses)
     assert int(tr.rng_step.item()) == tr.num_update
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('net', ['resnet50', 'vgg16'])
+def test_fp16_inference_matches_fp32(cuda, net):
+    """The fp16 test graph (MFMA f16 convs / FC, fp16 BN, pooling, RoIPool) vs the fp32 graph on
+    fixed RoIs: fp16 keeps 3 more mantissa bits than bf16, so with activations inside fp16's range it
+    must land closer to fp32."""
+    import copy
+    from mx_rcnn_amd.core.detector import Detector
+    torch.manual_seed(0)
+    m = FasterRCNN(net, 21, cfg=_cfg(), train_mode='test')
+    g = torch.Generator().manual_seed(1)
+    data = torch.randn(1, 3, 224, 320, generator=g) * 50
+    if net.startswith('resnet'):
+        m.calibrate_bn(data)
+    else:  # He init keeps a BN-free VGG's activations O(1) (the 0.01-std init shrinks them into fp16 subnormals)
+        with torch.no_grad():
+            for c in m.trunk.convs:
+                c.weight.normal_(0, (2.0 / (c.weight[0].numel())) ** 0.5, generator=g)
+            data = data / 50.0
+    with torch.no_grad():
+        m.head.cls_score.weight.normal_(0, 0.05, generator=g)
+        m.head.bbox_pred.weight.normal_(0, 0.05, generator=g)
+    info = torch.tensor([[224., 320., 1.0]])
+    x1 = torch.rand(64, generator=g) * 250
+    y1 = torch.rand(64, generator=g) * 150
+    rois = torch.stack([torch.zeros(64), x1, y1, x1 + 60, y1 + 60], 1)
+    outs = {}
+    for name, dt in (('fp32', torch.float32), ('bf16', torch.bfloat16), ('fp16', torch.float16)):
+        det = Detector(copy.deepcopy(m), cuda, compute_dtype=dt)
+        _, prob, box = det.forward(data, info, rois)
+        outs[name] = (prob.float().cpu(), box.float().cpu())
+    ref_p, ref_b = outs['fp32']
+
+    def err(k):
+        p, b = outs[k]
+        return ((p - ref_p).abs().max().item(), ((b - ref_b).norm() / ref_b.norm()).item())
+    e16, eb = err('fp16'), err('bf16')
+    assert e16[0] <= 0.02 and e16[1] <= 0.02, e16
+    assert e16[1] <= eb[1], (e16, eb)

@@ -3,6 +3,7 @@
 // launches are graph-capturable (no host sync, no allocation inside the launchers).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -543,9 +544,13 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   }
   Tensor b;
   if (bias.has_value() && bias->defined()) {
-    b = bias->to(at::kFloat).contiguous();
-    TORCH_CHECK(b.numel() == Cout, "bias size");
-    ep.bias = b.data_ptr<float>();
+    TORCH_CHECK(bias->numel() == Cout, "bias size");
+    if (bias->scalar_type() == x.scalar_type() && bias->is_contiguous()) {
+      ep.bias_h = reinterpret_cast<const uint16_t*>(bias->data_ptr());  // no per-call fp32 cast kernel
+    } else {
+      b = bias->to(at::kFloat).contiguous();
+      ep.bias = b.data_ptr<float>();
+    }
   }
   DevGuard g(x.device());
   Tensor y;
@@ -631,7 +636,7 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
     char kb[256];
     snprintf(kb, sizeof(kb), "%d,%d,%d,%d,%d,%d,%d,%d,%d|%d%d%d%d%d%d%d", NB, H, W, Cin, Cout, KH, KW, (int)stride,
              (int)pad, ep.residual != nullptr, ep.y2 != nullptr || bn.has_value(), bwd_mode, ep.dadd != nullptr,
-             ep.relu, ep.bias != nullptr, ep.drop_p > 0.f);
+             ep.relu, ep.bias != nullptr || ep.bias_h != nullptr, ep.drop_p > 0.f);
     const std::string key(kb);
     std::unique_lock<std::mutex> lk(g_tune_mu);
     auto it = g_tune.find(key);
@@ -780,6 +785,96 @@ Tensor avgpool_bwd(const Tensor& dy, int64_t H, int64_t W) {
   TORCH_CHECK(mxr::avgpool_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<uint16_t*>(dx.data_ptr()),
                                N, (int)(H * W), C, dcode(dy), cur_stream()) == 0, "avgpool_bwd: C % 8 != 0");
   return dx;
+}
+
+// ---- small-head backward / channel sum (head_bwd.hip) --------------------------------------------
+bool al16(const Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0; }
+
+// x (M, K) bf16 rows shared by 1-2 heads; dys[h] (M, N_h), ws[h] (N_h, K), dws[h] (N_h, K) bf16 targets
+// (accumulated when dw_acc[h]); dbs[h] (N_h) fp32 / bf16 targets (accumulated when db_acc[h]) or
+// empty (skipped).  Returns dx (M, K), ReLU-masked by x > 0 when relu_mask (empty unless need_dx).
+Tensor head_bwd(const Tensor& x, const std::vector<Tensor>& dys, const std::vector<Tensor>& ws,
+                const std::vector<Tensor>& dws, const std::vector<bool>& dw_acc, const std::vector<Tensor>& dbs,
+                const std::vector<bool>& db_acc, bool need_dx, bool relu_mask) {
+  CHECK_DEV(x);
+  const int nh = (int)dys.size();
+  TORCH_CHECK(nh >= 1 && nh <= 2 && (int)ws.size() == nh && (int)dws.size() == nh && (int)dw_acc.size() == nh &&
+                  (int)dbs.size() == nh && (int)db_acc.size() == nh, "head_bwd: 1 or 2 heads, one entry per head");
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.dim() == 2 && x.is_contiguous() && al16(x),
+              "head_bwd: x must be a contiguous 16-B aligned bf16 (M, K) matrix");
+  const int M = (int)x.size(0), K = (int)x.size(1);
+  TORCH_CHECK(K % 64 == 0, "head_bwd: K % 64 == 0");
+  mxr::HeadBwdArgs a;
+  a.nheads = nh;
+  for (int h = 0; h < nh; ++h) {
+    const Tensor &dy = dys[h], &w = ws[h], &dw = dws[h], &db = dbs[h];
+    CHECK_DEV(dy); CHECK_DEV(w); CHECK_DEV(dw);
+    TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && dy.dim() == 2 && dy.size(0) == M && dy.is_contiguous(),
+                "head_bwd: dy must be contiguous bf16 (M, N)");
+    const int N = (int)dy.size(1);
+    TORCH_CHECK(w.scalar_type() == at::kBFloat16 && w.is_contiguous() && w.numel() == (int64_t)N * K && al16(w),
+                "head_bwd: w must be a contiguous 16-B aligned bf16 (N, K) matrix");
+    TORCH_CHECK(dw.scalar_type() == at::kBFloat16 && dw.is_contiguous() && dw.numel() == (int64_t)N * K && al16(dw),
+                "head_bwd: dw must be a contiguous 16-B aligned bf16 (N, K) matrix");
+    a.dy[h] = reinterpret_cast<const uint16_t*>(dy.data_ptr());
+    a.w[h] = reinterpret_cast<const uint16_t*>(w.data_ptr());
+    a.N[h] = N;
+    a.dw[h] = reinterpret_cast<uint16_t*>(dw.data_ptr());
+    a.dw_acc[h] = dw_acc[h] ? 1 : 0;
+    if (db.defined() && db.numel() > 0) {
+      CHECK_DEV(db);
+      TORCH_CHECK(db.numel() == N && db.is_contiguous(), "head_bwd: db must be contiguous (N,)");
+      a.db[h] = db.data_ptr();
+      a.db_code[h] = dcode(db);
+      a.db_acc[h] = db_acc[h] ? 1 : 0;
+    }
+  }
+  DevGuard g(x.device());
+  Tensor dx;
+  if (need_dx) {
+    dx = at::empty({M, K}, x.options());
+    a.dx = reinterpret_cast<uint16_t*>(dx.data_ptr());
+    a.relu_mask = relu_mask ? 1 : 0;
+  }
+  a.rs = mxr::head_bwd_splits(M, K, a.N, nh);
+  Tensor wsp;
+  if (a.rs > 1) {
+    int64_t tot = 0;
+    for (int h = 0; h < nh; ++h) tot += (int64_t)a.rs * a.N[h] * (K + 1);
+    wsp = at::empty({tot}, x.options().dtype(at::kFloat));
+    float* p = wsp.data_ptr<float>();
+    for (int h = 0; h < nh; ++h) {
+      a.ws_dw[h] = p;
+      p += (int64_t)a.rs * a.N[h] * K;
+      a.ws_db[h] = p;
+      p += (int64_t)a.rs * a.N[h];
+    }
+  }
+  TORCH_CHECK(mxr::head_bwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), M, K, a, cur_stream()) == 0,
+              "head_bwd: unsupported shape");
+  return dx;
+}
+
+// per-channel sum of a channels_last map or (M, C) matrix into out (C,) fp32 / bf16 (+= when accumulate)
+void chan_sum(const Tensor& x, Tensor out, bool accumulate) {
+  CHECK_DEV(x); CHECK_DEV(out);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "chan_sum: bf16 / fp16 input");
+  int64_t C;
+  if (x.dim() == 4) {
+    TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "chan_sum: 4-D input must be channels_last");
+    C = x.size(1);
+  } else {
+    TORCH_CHECK(x.dim() == 2 && x.is_contiguous(), "chan_sum: 2-D input must be contiguous");
+    C = x.size(1);
+  }
+  TORCH_CHECK(C % 8 == 0 && al16(x), "chan_sum: C % 8 == 0 and 16-B aligned rows");
+  TORCH_CHECK(out.numel() == C && out.is_contiguous(), "chan_sum: out (C,) contiguous");
+  const int64_t M = x.numel() / C;
+  DevGuard g(x.device());
+  Tensor part = at::empty({(int64_t)mxr::chan_sum_chunks(M, (int)C) * C}, x.options().dtype(at::kFloat));
+  TORCH_CHECK(mxr::chan_sum(reinterpret_cast<const uint16_t*>(x.data_ptr()), M, (int)C, dcode(x),
+                            part.data_ptr<float>(), out.data_ptr(), dcode(out), accumulate ? 1 : 0, cur_stream()) == 0,
+              "chan_sum: unsupported shape");
 }
 
 // ---- proposal top-k ----------------------------------------------------------------------------
@@ -965,6 +1060,11 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int
   DevGuard g(x.device());
   int sp = 1;
   mxr::conv_wgrad_plan(NB, Ho, Wo, Cin, Cout, (int)KH, (int)KW, &sp);
+  static const int max_sp = [] {  // A/B knob: cap the pixel split (fewer reduce launches)
+    const char* e = std::getenv("MXR_WGRAD_MAX_SPLITS");
+    return e ? std::max(1, std::atoi(e)) : 1 << 30;
+  }();
+  sp = std::min(sp, max_sp);
   if (splits > 0) sp = (int)splits;
   Tensor dw;
   const bool acc = out.has_value() && out->defined();
@@ -1280,6 +1380,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("drop_seed") = 0, py::arg("drop_step") = py::none(), py::arg("pad_w") = -1,
         py::arg("out") = py::none(), py::arg("out_map") = py::none());
   m.def("proposal_topk", &proposal_topk, py::arg("keys"), py::arg("boxes"), py::arg("P"));
+  m.def("head_bwd", &head_bwd, py::arg("x"), py::arg("dys"), py::arg("ws"), py::arg("dws"), py::arg("dw_acc"),
+        py::arg("dbs"), py::arg("db_acc"), py::arg("need_dx"), py::arg("relu_mask"));
+  m.def("chan_sum", &chan_sum, py::arg("x"), py::arg("out"), py::arg("accumulate"));
   m.def("det_postprocess", &det_postprocess, py::arg("rois"), py::arg("scores"), py::arg("deltas"),
         py::arg("im_info"), py::arg("thresh"), py::arg("nms_thresh"), py::arg("max_per"), py::arg("cap"));
   m.def("nest_keep", &nest_keep, py::arg("dets"), py::arg("thresh"));

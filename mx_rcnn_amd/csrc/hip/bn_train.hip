@@ -3,7 +3,10 @@
 // (`rcnn/resnet.py:152,165`, bn_global=False).  M = N*H*W = 2 K - 6 K rows, C = 512 - 2048.
 //
 // Two kernels per direction, both fully coalesced: a workgroup owns 64 channels (one 128-B
-// line per row, 8 lanes x 16 B) and a chunk of BT_ROWS rows (32 row lanes).
+// line per row, 8 lanes x 16 B) and a chunk of `rows` rows (32 row lanes).  The chunk height
+// (32-256, bn_train_rows) is picked per shape so the grid has >= 512 workgroups: at 128 RoIs
+// the stage-4 maps are only 2 K - 6 K rows x 8 - 32 channel blocks, and one 256-row chunk per
+// workgroup left most of the 256 CUs idle (64-256 workgroups, 5-12 us per launch).
 //   fwd 1: per-chunk partial sum / sum of squares (shifted by the running mean, so the
 //          E[x^2] - E[x]^2 form does not cancel) -> workspace [chunks][2][C]
 //   fwd 2: every block folds the chunk partials of its 64 channels (a few dozen rows),
@@ -21,8 +24,37 @@
 namespace mxr {
 
 constexpr int BT_C = 64;       // channels per block
-constexpr int BT_ROWS = 256;   // rows per chunk
 constexpr int BT_LANES = 32;   // row lanes per block (8 channel groups x 32 = 256 threads)
+
+int bn_train_rows(int64_t M, int C) {
+  int rows = 256;
+  while (rows > BT_LANES && (int64_t)(C / BT_C) * ((M + rows - 1) / rows) < 512) rows >>= 1;
+  return rows;
+}
+
+// fold the per-chunk partials [nchunks][2][C] of this block's 64 channels: 4 threads per channel
+// each sum every 4th chunk, combined through LDS -> out_a / out_b [64] (visible after the call)
+__device__ __forceinline__ void fold_partials(const float* __restrict__ part, int nchunks, int C, float* red4,
+                                              float* out_a, float* out_b) {
+  const int tid = threadIdx.x, c = tid & 63, q = tid >> 6;
+  const int cc = blockIdx.x * BT_C + c;
+  float a = 0.f, b = 0.f;
+  for (int i = q; i < nchunks; i += 4) {
+    a += part[(int64_t)i * 2 * C + cc];
+    b += part[(int64_t)i * 2 * C + C + cc];
+  }
+  red4[q * 128 + c] = a;
+  red4[q * 128 + 64 + c] = b;
+  __syncthreads();
+  if (tid < 128) {
+    const int k = tid & 63, w = tid >> 6;
+    float s = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) s += red4[j * 128 + w * 64 + k];
+    (w ? out_b : out_a)[k] = s;
+  }
+  __syncthreads();
+}
 
 __device__ __forceinline__ void ld8(const uint16_t* p, float* v) {
   const uint4 u = *reinterpret_cast<const uint4*>(p);
@@ -64,14 +96,14 @@ __device__ __forceinline__ void lane_reduce(const float* a, const float* b, floa
 }
 
 __global__ void __launch_bounds__(256)
-bn_train_stats_kernel(const uint16_t* __restrict__ x, int64_t M, int C, const float* __restrict__ shift,
+bn_train_stats_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int rows, const float* __restrict__ shift,
                       float* __restrict__ part) {
   __shared__ float red[8][BT_LANES][16];
   __shared__ float sa[64], sb[64];
   const int cg = threadIdx.x & 7, rl = threadIdx.x >> 3;
   const int c0 = blockIdx.x * BT_C + cg * 8;
-  const int64_t r0 = (int64_t)blockIdx.y * BT_ROWS;
-  const int64_t r1 = r0 + BT_ROWS < M ? r0 + BT_ROWS : M;
+  const int64_t r0 = (int64_t)blockIdx.y * rows;
+  const int64_t r1 = r0 + rows < M ? r0 + rows : M;
   float sh[8], s1[8], s2[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -100,20 +132,17 @@ bn_train_stats_kernel(const uint16_t* __restrict__ x, int64_t M, int C, const fl
 }
 
 __global__ void __launch_bounds__(256)
-bn_train_norm_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int nchunks, const float* __restrict__ part,
+bn_train_norm_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int rows, int nchunks, const float* __restrict__ part,
                      const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ rmean,
                      float* __restrict__ rvar, float momentum, float eps, int fix_gamma, int relu,
                      uint16_t* __restrict__ y, float* __restrict__ save_mean, float* __restrict__ save_invstd) {
-  __shared__ float scale_sh[64], shift_sh[64];
+  __shared__ float scale_sh[64], shift_sh[64], red4[512], fa[64], fb[64];
   const int tid = threadIdx.x;
+  fold_partials(part, nchunks, C, red4, fa, fb);
   if (tid < 64) {
     const int c = blockIdx.x * BT_C + tid;
     const float sh = part[(int64_t)nchunks * 2 * C + c];  // the shift the stats kernel used
-    float a = 0.f, b = 0.f;
-    for (int i = 0; i < nchunks; ++i) {
-      a += part[(int64_t)i * 2 * C + c];
-      b += part[(int64_t)i * 2 * C + C + c];
-    }
+    const float a = fa[tid], b = fb[tid];
     const float dm = a / (float)M;  // mean - shift
     const float var = fmaxf(b / (float)M - dm * dm, 0.f);
     const float mu = sh + dm;
@@ -139,8 +168,8 @@ bn_train_norm_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int nchun
     sc[k] = scale_sh[cg * 8 + k];
     sf[k] = shift_sh[cg * 8 + k];
   }
-  const int64_t r0 = (int64_t)blockIdx.y * BT_ROWS;
-  const int64_t r1 = r0 + BT_ROWS < M ? r0 + BT_ROWS : M;
+  const int64_t r0 = (int64_t)blockIdx.y * rows;
+  const int64_t r1 = r0 + rows < M ? r0 + rows : M;
 #pragma unroll 4
   for (int64_t r = r0 + rl; r < r1; r += BT_LANES) {
     float v[8];
@@ -158,7 +187,7 @@ __global__ void __launch_bounds__(256)
 bn_train_bstats_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy, int64_t M, int C,
                        const float* __restrict__ gamma, const float* __restrict__ beta,
                        const float* __restrict__ save_mean, const float* __restrict__ save_invstd, int fix_gamma,
-                       int relu, float* __restrict__ part) {
+                       int relu, int rows, float* __restrict__ part) {
   __shared__ float red[8][BT_LANES][16];
   __shared__ float sa[64], sb[64];
   const int cg = threadIdx.x & 7, rl = threadIdx.x >> 3;
@@ -172,8 +201,8 @@ bn_train_bstats_kernel(const uint16_t* __restrict__ x, const uint16_t* __restric
     b[k] = beta[c0 + k];
     sg[k] = sgx[k] = 0.f;
   }
-  const int64_t r0 = (int64_t)blockIdx.y * BT_ROWS;
-  const int64_t r1 = r0 + BT_ROWS < M ? r0 + BT_ROWS : M;
+  const int64_t r0 = (int64_t)blockIdx.y * rows;
+  const int64_t r1 = r0 + rows < M ? r0 + rows : M;
 #pragma unroll 4
   for (int64_t r = r0 + rl; r < r1; r += BT_LANES) {
     float v[8], d[8];
@@ -196,20 +225,17 @@ bn_train_bstats_kernel(const uint16_t* __restrict__ x, const uint16_t* __restric
 }
 
 __global__ void __launch_bounds__(256)
-bn_train_dx_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy, int64_t M, int C, int nchunks,
+bn_train_dx_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy, int64_t M, int C, int rows, int nchunks,
                    const float* __restrict__ part, const float* __restrict__ gamma, const float* __restrict__ beta,
                    const float* __restrict__ save_mean, const float* __restrict__ save_invstd, int fix_gamma,
                    int relu, uint16_t* __restrict__ dx, float* __restrict__ dgamma, float* __restrict__ dbeta,
                    int accumulate) {
-  __shared__ float mg_sh[64], mgx_sh[64];
+  __shared__ float mg_sh[64], mgx_sh[64], red4[512], fa[64], fb[64];
   const int tid = threadIdx.x;
+  fold_partials(part, nchunks, C, red4, fa, fb);
   if (tid < 64) {
     const int c = blockIdx.x * BT_C + tid;
-    float a = 0.f, b = 0.f;
-    for (int i = 0; i < nchunks; ++i) {
-      a += part[(int64_t)i * 2 * C + c];
-      b += part[(int64_t)i * 2 * C + C + c];
-    }
+    const float a = fa[tid], b = fb[tid];
     mg_sh[tid] = a / (float)M;
     mgx_sh[tid] = b / (float)M;
     if (blockIdx.y == 0) {
@@ -231,8 +257,8 @@ bn_train_dx_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ 
     mg[k] = mg_sh[cg * 8 + k];
     mgx[k] = mgx_sh[cg * 8 + k];
   }
-  const int64_t r0 = (int64_t)blockIdx.y * BT_ROWS;
-  const int64_t r1 = r0 + BT_ROWS < M ? r0 + BT_ROWS : M;
+  const int64_t r0 = (int64_t)blockIdx.y * rows;
+  const int64_t r1 = r0 + rows < M ? r0 + rows : M;
 #pragma unroll 4
   for (int64_t r = r0 + rl; r < r1; r += BT_LANES) {
     float v[8], d[8];
@@ -248,16 +274,20 @@ bn_train_dx_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ 
   }
 }
 
-int bn_train_workspace_floats(int64_t M, int C) { return (int)(((M + BT_ROWS - 1) / BT_ROWS) * 2 * C + C); }
+int bn_train_workspace_floats(int64_t M, int C) {
+  const int rows = bn_train_rows(M, C);
+  return (int)(((M + rows - 1) / rows) * 2 * C + C);
+}
 
 int bn_train_fwd(const uint16_t* x, int64_t M, int C, const float* gamma, const float* beta, float* rmean,
                  float* rvar, float momentum, float eps, int fix_gamma, int relu, uint16_t* y, float* save_mean,
                  float* save_invstd, float* workspace, hipStream_t st) {
   if (C % BT_C != 0 || M <= 0) return -1;
-  const int nchunks = (int)((M + BT_ROWS - 1) / BT_ROWS);
+  const int rows = bn_train_rows(M, C);
+  const int nchunks = (int)((M + rows - 1) / rows);
   const dim3 grid(C / BT_C, nchunks);
-  bn_train_stats_kernel<<<grid, 256, 0, st>>>(x, M, C, rmean, workspace);
-  bn_train_norm_kernel<<<grid, 256, 0, st>>>(x, M, C, nchunks, workspace, gamma, beta, rmean, rvar, momentum, eps,
+  bn_train_stats_kernel<<<grid, 256, 0, st>>>(x, M, C, rows, rmean, workspace);
+  bn_train_norm_kernel<<<grid, 256, 0, st>>>(x, M, C, rows, nchunks, workspace, gamma, beta, rmean, rvar, momentum, eps,
                                              fix_gamma, relu, y, save_mean, save_invstd);
   return 0;
 }
@@ -266,11 +296,12 @@ int bn_train_bwd(const uint16_t* x, const uint16_t* dy, int64_t M, int C, const 
                  const float* save_mean, const float* save_invstd, int fix_gamma, int relu, uint16_t* dx,
                  float* dgamma, float* dbeta, int accumulate, float* workspace, hipStream_t st) {
   if (C % BT_C != 0 || M <= 0) return -1;
-  const int nchunks = (int)((M + BT_ROWS - 1) / BT_ROWS);
+  const int rows = bn_train_rows(M, C);
+  const int nchunks = (int)((M + rows - 1) / rows);
   const dim3 grid(C / BT_C, nchunks);
   bn_train_bstats_kernel<<<grid, 256, 0, st>>>(x, dy, M, C, gamma, beta, save_mean, save_invstd, fix_gamma, relu,
-                                               workspace);
-  bn_train_dx_kernel<<<grid, 256, 0, st>>>(x, dy, M, C, nchunks, workspace, gamma, beta, save_mean, save_invstd,
+                                               rows, workspace);
+  bn_train_dx_kernel<<<grid, 256, 0, st>>>(x, dy, M, C, rows, nchunks, workspace, gamma, beta, save_mean, save_invstd,
                                            fix_gamma, relu, dx, dgamma, dbeta, accumulate);
   return 0;
 }

@@ -76,7 +76,7 @@ struct EpiCol {
 
 __device__ __forceinline__ EpiCol epi_col(const ConvEpi& ep, int n) {
   EpiCol c;
-  c.bias = ep.bias ? ep.bias[n] : 0.f;
+  c.bias = ep.bias ? ep.bias[n] : (ep.bias_h ? h16_to_f32c(EPC, ep.bias_h[n]) : 0.f);
   c.s = 1.f;
   c.t = 0.f;
   c.mean = 0.f;

@@ -17,6 +17,9 @@
 //
 // Split-K over pixels with fp32 slab partials (the output is small, the reduction long);
 // the shared split-K reduce kernel of conv_igemm.hip casts to bf16.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 #include "../kernels.h"
 
@@ -344,8 +347,12 @@ int conv_wgrad_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, i
   const int P = NB * Ho * Wo;
   const int tiles = ((Cout + WG_BM - 1) / WG_BM) * (KH * KW * Cin / WG_BN);
   const int steps = (P + WG_BK - 1) / WG_BK;
+  static const int min_steps = [] {  // A/B knob MXR_WGRAD_MIN_STEPS: 64-pixel steps kept per split
+    const char* e = std::getenv("MXR_WGRAD_MIN_STEPS");
+    return e ? std::max(1, std::atoi(e)) : 16;
+  }();
   int splits = 1;
-  while (splits < 64 && tiles * splits * 2 <= 2304 && steps / (splits * 2) >= 16) splits *= 2;
+  while (splits < 64 && tiles * splits * 2 <= 2304 && steps / (splits * 2) >= min_steps) splits *= 2;
   *splits_out = splits;
   return splits;
 }

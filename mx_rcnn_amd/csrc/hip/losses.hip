@@ -66,10 +66,10 @@ rpn_softmax_ce_kernel(const void* __restrict__ logits, int bf16, int64_t s0, int
                       float* __restrict__ partials, unsigned* __restrict__ ticket, float* __restrict__ loss_out,
                       float* __restrict__ prob_fg) {
   const int64_t total = (int64_t)B * H * W * A;
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const float nrm = rpn_norm(norm, meta, B);
   float loss = 0.f;
-  if (t < total) {
+  // grid-stride over a capped grid (loss_blocks_rpn): fewer partials / ticket arrivals to fold
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
     const int a = (int)(t % A);
     int64_t rest = t / A;
     const int w = (int)(rest % W); rest /= W;
@@ -88,7 +88,7 @@ rpn_softmax_ce_kernel(const void* __restrict__ logits, int bf16, int64_t s0, int
       const float sc = grad_scale / nrm;
       gb = (pb - (lab == 0 ? 1.f : 0.f)) * sc;
       gf = (pf - (lab == 1 ? 1.f : 0.f)) * sc;
-      loss = -logf(fmaxf(lab == 1 ? pf : pb, 1e-14f));
+      loss += -logf(fmaxf(lab == 1 ? pf : pb, 1e-14f));
     }
     st(grad, ibg, gb, bf16);
     st(grad, ifg, gf, bf16);
@@ -97,14 +97,16 @@ rpn_softmax_ce_kernel(const void* __restrict__ logits, int bf16, int64_t s0, int
   block_reduce_final(loss, partials, ticket, 1.f / nrm, loss_out);
 }
 
-int loss_blocks_rpn(int64_t total) { return (int)div_up(total, 256); }
+// grid of the element-wise grid-reduction losses: at most 128 blocks (a few elements per thread
+// at RPN sizes), so the last-block fold and the ticket see 128 arrivals, not ~800
+int loss_blocks_rpn(int64_t total) { return (int)std::min<int64_t>(div_up(total, 256), 128); }
 
 void rpn_softmax_ce(const void* logits, int bf16, int64_t s0, int64_t s1, int64_t s2, int64_t s3, const int32_t* label,
                     int B, int A, int H, int W, const float* norm, const int32_t* meta, float grad_scale, void* grad,
                     float* partials, unsigned* ticket, float* loss_out, float* prob_fg, hipStream_t st) {
   const int64_t total = (int64_t)B * H * W * A;
   if (total == 0) return;
-  rpn_softmax_ce_kernel<<<div_up(total, 256), 256, 0, st>>>(logits, bf16, s0, s1, s2, s3, label, B, A, H, W, norm, meta,
+  rpn_softmax_ce_kernel<<<loss_blocks_rpn(total), 256, 0, st>>>(logits, bf16, s0, s1, s2, s3, label, B, A, H, W, norm, meta,
                                                             grad_scale, grad, partials, ticket, loss_out, prob_fg);
 }
 
@@ -152,9 +154,8 @@ smooth_l1_kernel(const void* __restrict__ pred, int bf16, int64_t s0, int64_t s1
                  int n2, int n3, int64_t total, const float* __restrict__ tgt, const float* __restrict__ in_w,
                  const float* __restrict__ out_w, float sigma2, float grad_scale, void* __restrict__ grad,
                  float* __restrict__ partials, unsigned* __restrict__ ticket, float* __restrict__ loss_out) {
-  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   float loss = 0.f;
-  if (t < total) {
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x) {
     const int i3 = (int)(t % n3);
     int64_t rest = t / n3;
     const int i2 = (int)(rest % n2); rest /= n2;
@@ -167,7 +168,7 @@ smooth_l1_kernel(const void* __restrict__ pred, int bf16, int64_t s0, int64_t s1
     float f, d;
     if (ax < 1.f / sigma2) { f = 0.5f * sigma2 * x * x; d = sigma2 * x; }
     else { f = ax - 0.5f / sigma2; d = x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f); }
-    loss = ow * f;
+    loss += ow * f;
     if (grad) st(grad, pi, grad_scale * ow * d * iw, bf16);
   }
   block_reduce_final(loss, partials, ticket, 1.f, loss_out);
@@ -178,7 +179,7 @@ void smooth_l1(const void* pred, int bf16, int64_t s0, int64_t s1, int64_t s2, i
                void* grad, float* partials, unsigned* ticket, float* loss_out, hipStream_t st) {
   const int64_t total = (int64_t)n0 * n1 * n2 * n3;
   if (total == 0) return;
-  smooth_l1_kernel<<<div_up(total, 256), 256, 0, st>>>(pred, bf16, s0, s1, s2, s3, n1, n2, n3, total, tgt, in_w,
+  smooth_l1_kernel<<<loss_blocks_rpn(total), 256, 0, st>>>(pred, bf16, s0, s1, s2, s3, n1, n2, n3, total, tgt, in_w,
                                                        out_w, sigma * sigma, grad_scale, grad, partials, ticket,
                                                        loss_out);
 }

@@ -147,6 +147,7 @@ int conv_igemm_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, i
 //          keeping the raw conv output y for the BN backward.)
 struct ConvEpi {
   const float* bias = nullptr;
+  const uint16_t* bias_h = nullptr;  // bias in the activation dtype (bf16 / fp16), instead of `bias`
   const uint16_t* residual = nullptr;
   int relu = 0;
   const float* bn_gamma = nullptr;
@@ -239,5 +240,34 @@ int conv_wgrad_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, i
 int conv_wgrad(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab, int NB, int H, int W, int Cin,
                int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int splits, int accumulate,
                hipStream_t st, int variant = 0);
+
+// ---- small-head backward (head_bwd.hip) ---------------------------------------------------------
+// One or two heads y_h = X W_h^T (+b_h) over the same X (M, K) bf16, K % 64 == 0, dY_h (M, N_h):
+// dX (optional, ReLU-masked by X > 0 when relu_mask), dW_h (N_h, K) bf16 (+= when dw_acc), db_h (N_h)
+// fp32 / bf16 by db_code (+= when db_acc; null: skipped).  rs > 1 splits the dW rows M and needs
+// ws_dw[h] (rs * N_h * K floats) and ws_db[h] (rs * N_h floats).
+struct HeadBwdArgs {
+  const uint16_t* dy[2] = {nullptr, nullptr};
+  const uint16_t* w[2] = {nullptr, nullptr};
+  int N[2] = {0, 0};
+  uint16_t* dw[2] = {nullptr, nullptr};
+  int dw_acc[2] = {0, 0};
+  void* db[2] = {nullptr, nullptr};
+  int db_code[2] = {0, 0};
+  int db_acc[2] = {0, 0};
+  float* ws_dw[2] = {nullptr, nullptr};
+  float* ws_db[2] = {nullptr, nullptr};
+  uint16_t* dx = nullptr;
+  int relu_mask = 0;
+  int nheads = 1;
+  int rs = 1;
+};
+int head_bwd_splits(int M, int K, const int* N, int nheads);
+int head_bwd(const uint16_t* x, int M, int K, const HeadBwdArgs& a, hipStream_t st);
+// per-channel sum of x (M, C) (bf16 / fp16 by code) into out (C) fp32 / bf16 by out_code (+= when
+// accumulate); part: chan_sum_chunks(M, C) * C floats
+int chan_sum_chunks(int64_t M, int C);
+int chan_sum(const uint16_t* x, int64_t M, int C, int code, float* part, void* out, int out_code, int accumulate,
+             hipStream_t st);
 
 }  // namespace mxr

@@ -25,6 +25,7 @@ import torch.nn.functional as F
 from ..config import config as _global_cfg, snapshot
 from ..utils import profiler as prof
 from ..ops import anchor_target, proposal, proposal_target, roi_pool
+from ..ops.head import rpn_head
 from ..ops.losses import combine_losses, rpn_softmax_ce, smooth_l1, softmax_ce
 from .layers import Conv
 from .resnet import ResNetHead, ResNetTrunk
@@ -47,8 +48,9 @@ class RPNHead(nn.Module):
         nn.init.normal_(self.rpn_bbox_pred.weight, 0, 0.001)
 
     def forward(self, feat):
-        x = self.rpn_conv_3x3(feat, relu=True)
-        return self.rpn_cls_score(x), self.rpn_bbox_pred(x)
+        # conv + ReLU + both predictors as one op: its backward is one kernel for the two 1x1 heads
+        # with the ReLU backward fused (ops/head.py); falls back to the three modules elsewhere
+        return rpn_head(feat, self.rpn_conv_3x3, self.rpn_cls_score, self.rpn_bbox_pred)
 
 
 class FasterRCNN(nn.Module):
@@ -171,6 +173,30 @@ class FasterRCNN(nn.Module):
             for t in at.values():
                 t.record_stream(main)
             return at
+        join.stream, join.at = aux, at  # for _rpn_losses_async: the losses can stay on this stream
+        return join
+
+    def _rpn_losses_async(self, rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt, at_join):
+        """The RPN losses on the auxiliary stream that holds the anchor targets, issued right after
+        the RPN forward: the proposal chain (decode, top-k, NMS -> sampling -> RoI pooling), the
+        step's serial critical path, then starts without waiting for them.  Returns a callable that
+        joins the stream and yields (cls_loss, bbox_loss, anchor targets)."""
+        aux = getattr(at_join, 'stream', None)
+        if aux is None:
+            res = self._rpn_losses(rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt, at_join())
+            return lambda: res
+        main = torch.cuda.current_stream()
+        aux.wait_stream(main)  # the RPN outputs (nothing later on main is waited for)
+        rpn_cls.record_stream(aux)
+        rpn_bbox.record_stream(aux)
+        with torch.cuda.stream(aux):
+            res = self._rpn_losses(rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt, at_join.at)
+
+        def join():
+            main.wait_stream(aux)
+            for t in (res[0], res[1]) + tuple(res[2].values()):
+                t.record_stream(main)
+            return res
         return join
 
     def _rpn_losses(self, rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt, at=None):
@@ -203,8 +229,7 @@ class FasterRCNN(nn.Module):
         with prof.range('rpn'):
             rpn_cls, rpn_bbox = self.rpn(feat)
         with prof.range('anchor_target+rpn_loss'):
-            rpn_cls_loss, rpn_bbox_loss, at = self._rpn_losses(rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt,
-                                                                at_join())
+            rpn_losses = self._rpn_losses_async(rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt, at_join)
         with prof.range('proposal'):
             rois, _ = self._proposal(rpn_cls, rpn_bbox, im_info, 'TRAIN')
         with prof.range('proposal_target'):
@@ -216,6 +241,7 @@ class FasterRCNN(nn.Module):
         with prof.range('head_loss'):
             cls_loss, bbox_loss, cls_prob = self._head_losses(cls_score, bbox_pred, pt['label'], pt['bbox_target'],
                                                               pt['bbox_inside_weight'], pt['bbox_outside_weight'])
+        rpn_cls_loss, rpn_bbox_loss, at = rpn_losses()
         B = data.shape[0]
         R = cls_score.shape[0]
         # 'loss' carries the gradients (each loss applies its own grad_scale in backward); its value

@@ -10,6 +10,7 @@ import torch.nn as nn
 
 from ..ops.conv import igemm_eligible
 from ..ops.fused import conv_add, conv_add_bn_relu, conv_bn_relu, fused_unit
+from ..ops.head import fc_pair
 from ..ops.pool import global_avg_pool
 from .layers import BatchNorm, Conv, Linear, max_pool
 
@@ -55,11 +56,13 @@ class ResidualUnit(nn.Module):
     def forward(self, x):
         act1 = self.bn1(x)
         if self.bottle_neck:
-            y = self.conv3(self.bn3(self.conv2(self.bn2(self.conv1(act1)))))
+            a, last = self.bn3(self.conv2(self.bn2(self.conv1(act1)))), self.conv3
         else:
-            y = self.conv2(self.bn2(self.conv1(act1)))
+            a, last = self.bn2(self.conv1(act1)), self.conv2
         sc = x if self.dim_match else self.sc(act1)
-        return y + sc
+        if fusion_enabled() and igemm_eligible(a, last.weight, last.stride, last.pad) and last.weight.dtype == a.dtype:
+            return conv_add(a, last, sc)  # residual add in the conv epilogue (train-mode BN head units)
+        return last(a) + sc
 
     def can_fuse(self, x):
         """Frozen BNs and MFMA-eligible convs: run the unit as fused conv+BN+ReLU(+residual) ops."""
@@ -202,4 +205,4 @@ class ResNetHead(nn.Module):
     def forward(self, pooled):
         x = self.bn1(run_stage(self.stage4, pooled))  # fused when the BNs are frozen (test time)
         x = global_avg_pool(x)
-        return self.cls_score(x), self.bbox_pred(x)
+        return fc_pair(x, self.cls_score, self.bbox_pred)

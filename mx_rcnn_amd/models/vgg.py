@@ -6,6 +6,7 @@ RoIPool 7x7 @ 1/16 -> fc6 4096 -> ReLU -> Dropout .5 -> fc7 -> ReLU -> Dropout -
 import torch.nn as nn
 
 from .layers import Conv, Linear, max_pool
+from ..ops.head import fc_pair
 
 VGG_CFG = [(1, 2, 3, 64), (2, 2, 64, 128), (3, 3, 128, 256), (4, 3, 256, 512), (5, 3, 512, 512)]
 
@@ -52,4 +53,4 @@ class VGGHead(nn.Module):
         # relu6/drop6 and relu7/drop7 run in the FC kernel's epilogue (ops/fc.py)
         x = self.fc6(x, relu=True, drop_p=self.dropout)
         x = self.fc7(x, relu=True, drop_p=self.dropout)
-        return self.cls_score(x), self.bbox_pred(x)
+        return fc_pair(x, self.cls_score, self.bbox_pred)

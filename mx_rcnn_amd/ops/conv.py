@@ -120,7 +120,7 @@ def strided_dgrad(dy, wf, H, W, k, s, p, residual=None, bn=None, bn_eps=2e-5, bn
     return dx
 
 
-def conv_backward(x, w, param, dy, stride, pad, has_bias, need_x, need_w, need_b):
+def conv_backward(x, w, param, dy, stride, pad, has_bias, need_x, need_w, need_b, bparam=None):
     """(dx, dw, db) of an NHWC bf16 conv given the gradient at its (pre-activation) output.
     dw is None when it was accumulated straight into the parameter's flat gradient view."""
     kh = w.shape[2]
@@ -136,7 +136,7 @@ def conv_backward(x, w, param, dy, stride, pad, has_bias, need_x, need_w, need_b
             side.wait_stream(main)
     if side is not None:
         with torch.cuda.stream(side):
-            dw, db = _wgrad(x, w, param, dy, stride, pad, has_bias, need_w, need_b)
+            dw, db = _wgrad(x, w, param, dy, stride, pad, has_bias, need_w, need_b, bparam)
     if need_x:
         if stride == 1 and w.shape[0] % 64 == 0 and 2 * pad == kh - 1:
             dx = need_ext().conv_igemm_fwd(dy, dgrad_weight(param, w), None, 1, kh - 1 - pad, False)[0]
@@ -147,7 +147,7 @@ def conv_backward(x, w, param, dy, stride, pad, has_bias, need_x, need_w, need_b
             dx = torch.ops.aten.convolution_backward(
                 dy, x, w, None, [stride] * 2, [pad] * 2, [1, 1], False, [0, 0], 1, [True, False, False])[0]
     if side is None:
-        dw, db = _wgrad(x, w, param, dy, stride, pad, has_bias, need_w, need_b)
+        dw, db = _wgrad(x, w, param, dy, stride, pad, has_bias, need_w, need_b, bparam)
     else:
         main.wait_stream(side)
         for t in (dw, db):  # allocated on the side stream, consumed (and freed) on the compute stream
@@ -156,7 +156,19 @@ def conv_backward(x, w, param, dy, stride, pad, has_bias, need_x, need_w, need_b
     return dx, dw, db
 
 
-def _wgrad(x, w, param, dy, stride, pad, has_bias, need_w, need_b):
+def _bias_grad(dy, w, bparam):
+    """Per-channel sum of dy (HIP two-pass column sum, accumulated straight into the bias's flat
+    gradient view when it has one) -> db or None."""
+    tb = grad_sink.target(bparam)
+    if tb is not None and tb.is_contiguous():
+        need_ext().chan_sum(dy, tb, True)
+        return None
+    db = torch.empty(w.shape[0], dtype=w.dtype, device=dy.device)
+    need_ext().chan_sum(dy, db, False)
+    return db
+
+
+def _wgrad(x, w, param, dy, stride, pad, has_bias, need_w, need_b, bparam=None):
     dw = db = None
     if need_w and wgrad_enabled() and w.shape[0] % 8 == 0:
         tgt = grad_sink.target(param)
@@ -165,7 +177,7 @@ def _wgrad(x, w, param, dy, stride, pad, has_bias, need_w, need_b):
         else:
             dw = need_ext().conv_wgrad(dy, x, w.shape[2], w.shape[3], stride, pad)
         if has_bias and need_b:
-            db = dy.sum(dim=(0, 2, 3)).to(w.dtype)
+            db = _bias_grad(dy, w, bparam)
     elif need_w or (has_bias and need_b):
         _, dw, db = torch.ops.aten.convolution_backward(
             dy, x, w, [w.shape[0]] if has_bias else None, [stride] * 2, [pad] * 2, [1, 1], False,
@@ -182,6 +194,7 @@ class _ConvIgemm(torch.autograd.Function):
         y = ext.conv_igemm_fwd(x, wc, b, stride, pad, relu)[0]
         ctx.save_for_backward(x, wc, y if relu else None)
         ctx.param = w if w.is_leaf else None
+        ctx.bparam = b if (b is not None and b.is_leaf) else None
         ctx.stride, ctx.pad, ctx.relu, ctx.has_bias = stride, pad, relu, b is not None
         return y
 
@@ -192,7 +205,7 @@ class _ConvIgemm(torch.autograd.Function):
         if ctx.relu:
             dy = dy * (y > 0)
         dx, dw, db = conv_backward(x, w, ctx.param, dy, ctx.stride, ctx.pad, ctx.has_bias, ctx.needs_input_grad[0],
-                                   ctx.needs_input_grad[1], ctx.needs_input_grad[2])
+                                   ctx.needs_input_grad[1], ctx.needs_input_grad[2], ctx.bparam)
         return dx, dw, db, None, None, None
 
 

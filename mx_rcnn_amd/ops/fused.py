@@ -217,9 +217,8 @@ class _FusedUnitFn(torch.autograd.Function):
         if spec.dim_match:
             res = x
         else:
-            wsc = ws[-1]
-            sc_in = act1 if spec.stride == 1 else _cl(act1[:, :, ::spec.stride, ::spec.stride])
-            res = ext.conv_igemm_fwd(sc_in, wsc, None, 1, 0, False)[0]
+            # strided 1x1 projection read straight from act1 by the kernel (no subsampled copy)
+            res = ext.conv_igemm_fwd(act1, ws[-1], None, spec.stride, 0, False)[0]
         if nxt is not None:
             out, act1n = ext.conv_igemm_fwd(last_in, w_last, None, 1, 0 if spec.bottle else 1, False, 0, 0, res,
                                             nxt, float(spec.next_bn.eps), bool(spec.next_bn.fix_gamma), True)
@@ -356,13 +355,13 @@ class _FusedUnitFn(torch.autograd.Function):
         bn1_trainable = need[nconv] or need[nconv + 1]
         if not ctx.needs_input_grad[1] and not bn1_trainable:
             if not spec.dim_match:
-                wgrad(nconv - 1, d_out, sc_in, 1, 1, 0)
+                wgrad(nconv - 1, d_out, act1, 1, s, 0)
             if side is not None:
                 main.wait_stream(side)
             return (None, None, None) + tuple(grads)
         d_sc = None
         if not spec.dim_match:
-            wgrad(nconv - 1, d_out, sc_in, 1, 1, 0)
+            wgrad(nconv - 1, d_out, act1, 1, s, 0)
             from .conv import dgrad_weight
             d_sub = ext.conv_igemm_fwd(d_out, dgrad_weight(ctx.params[nconv - 1], ws[nconv - 1]), None, 1, 0,
                                        False)[0]

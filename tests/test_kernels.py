@@ -644,3 +644,93 @@ def test_global_avgpool_vs_torch(cuda):
     y.backward(dy.to(cuda))
     ref.backward(dy.float())
     assert (xg.grad.float().cpu() - xr.grad).abs().max().item() <= 1e-2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('M,K,N1,N2,relu_mask', [(128, 2048, 81, 324, False), (128, 4096, 21, 84, False),
+                                                (4200, 512, 24, 48, True), (333, 256, 18, 36, True)])
+def test_head_pair_bwd_vs_fp32(cuda, M, K, N1, N2, relu_mask):
+    """csrc/hip/head_bwd.hip: dX (ReLU-masked), both dW (accumulated) and db (fp32 / bf16 targets,
+    accumulated) of a head pair vs fp32 torch; row-split (rs > 1) and single-pass shapes."""
+    from mx_rcnn_amd.ops import need_ext
+    g = torch.Generator(device='cpu').manual_seed(3)
+    x = torch.randn(M, K, generator=g)
+    if relu_mask:
+        x = x.clamp(min=0)  # a ReLU output: the mask is x > 0
+    dys = [torch.randn(M, n, generator=g) for n in (N1, N2)]
+    ws = [torch.randn(n, K, generator=g) * 0.05 for n in (N1, N2)]
+    xb, dyb, wb = x.bfloat16(), [d.bfloat16() for d in dys], [w.bfloat16() for w in ws]
+    xf, dyf, wf = xb.float(), [d.float() for d in dyb], [w.float() for w in wb]
+    dw0 = [torch.randn(n, K, generator=g).bfloat16() for n in (N1, N2)]
+    db0 = [torch.randn(N1, generator=g), torch.randn(N2, generator=g).bfloat16()]
+    dws = [d.clone().to(cuda) for d in dw0]
+    dbs = [d.clone().to(cuda) for d in db0]
+    dx = need_ext().head_bwd(xb.to(cuda), [d.to(cuda) for d in dyb], [w.to(cuda) for w in wb], dws, [True, True],
+                             dbs, [True, True], True, relu_mask)
+    ref_dx = dyf[0] @ wf[0] + dyf[1] @ wf[1]
+    if relu_mask:
+        ref_dx = ref_dx * (xf > 0)
+    assert torch.allclose(dx.float().cpu(), ref_dx, rtol=2e-2, atol=2e-2 * ref_dx.abs().max().item())
+    for h in range(2):
+        ref_dw = dw0[h].float() + dyf[h].t() @ xf
+        got = dws[h].float().cpu()
+        assert torch.allclose(got, ref_dw, rtol=2e-2, atol=1e-2 * ref_dw.abs().max().item()), h
+        ref_db = db0[h].float() + dyf[h].sum(0)
+        assert torch.allclose(dbs[h].float().cpu(), ref_db, rtol=1e-2, atol=1e-2 * ref_db.abs().max().item()), h
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('N,C,H,W', [(1, 512, 50, 84), (2, 24, 7, 9), (128, 1024, 1, 1)])
+def test_chan_sum_vs_torch(cuda, N, C, H, W):
+    from mx_rcnn_amd.ops import need_ext
+    x = torch.randn(N, C, H, W).bfloat16().contiguous(memory_format=torch.channels_last)
+    ref = x.float().sum((0, 2, 3))
+    out = torch.zeros(C, device=cuda)
+    need_ext().chan_sum(x.to(cuda), out, False)
+    assert torch.allclose(out.cpu(), ref, rtol=1e-4, atol=1e-3)
+    acc = torch.ones(C, device=cuda).bfloat16()
+    need_ext().chan_sum(x.to(cuda), acc, True)
+    assert torch.allclose(acc.float().cpu(), ref + 1, rtol=1e-2, atol=1e-2 * (ref.abs().max().item() + 1))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('network', ['resnet', 'vgg'])
+def test_head_pair_ops_match_modules(cuda, network):
+    """ops/head.py: the fused RPN head / FC pair (forward + one-kernel backward) against the same
+    modules run separately (MXR_HEAD_KERNEL path off), gradients of every input and parameter."""
+    import copy
+    import os
+    from mx_rcnn_amd.models.faster_rcnn import RPNHead
+    from mx_rcnn_amd.models.layers import Linear
+    from mx_rcnn_amd.ops.head import fc_pair
+    torch.manual_seed(0)
+    if network == 'resnet':
+        mod = RPNHead(1024, 12).to(cuda).bfloat16()
+        for p in mod.parameters():
+            p.data = p.data.contiguous(memory_format=torch.channels_last) if p.dim() == 4 else p.data
+            p.data.normal_(0, 0.02)
+        inp = torch.randn(1, 1024, 20, 31, device=cuda).bfloat16().contiguous(memory_format=torch.channels_last)
+        run = lambda m, x: m(x)  # noqa: E731
+    else:
+        mod = torch.nn.ModuleList([Linear('cls_score', 2048, 81), Linear('bbox_pred', 2048, 324)]).to(cuda).bfloat16()
+        for p in mod.parameters():
+            p.data.normal_(0, 0.02)
+        inp = torch.randn(128, 2048, device=cuda).bfloat16()
+        run = lambda m, x: fc_pair(x, m[0], m[1])  # noqa: E731
+    ref_mod = copy.deepcopy(mod)
+    outs = []
+    for m, env in ((mod, '1'), (ref_mod, '0')):
+        os.environ['MXR_HEAD_KERNEL'] = env
+        try:
+            x = inp.clone().requires_grad_(True)
+            y1, y2 = run(m, x)
+            g = torch.Generator(device='cpu').manual_seed(1)
+            loss = (y1.float() * torch.randn(y1.shape, generator=g).to(cuda)).sum() + \
+                (y2.float() * torch.randn(y2.shape, generator=g).to(cuda)).sum()
+            loss.backward()
+            outs.append([y1.float(), y2.float(), x.grad.float()] + [p.grad.float() for p in m.parameters()])
+        finally:
+            os.environ.pop('MXR_HEAD_KERNEL', None)
+    for a, b in zip(*outs):
+        scale = b.abs().max().item() + 1e-6
+        assert (a - b).abs().max().item() <= 3e-2 * scale, (a.shape, (a - b).abs().max().item(), scale)

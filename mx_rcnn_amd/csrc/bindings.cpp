@@ -726,6 +726,83 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   return {y};
 }
 
+// Grouped backward of a stride-1 conv of a fused unit (conv_igemm.hip conv_dgrad_wgrad): the data
+// gradient dgrad = conv(dy, wf, pad) with the BN-ReLU backward epilogue (bn, bnb_x, optional dadd /
+// residual, dgamma/dbeta fp32 accumulators) AND the weight gradient of (wg_dy, wg_x) accumulated into
+// wg_out, in one launch.  Returns [dx, dgamma, dbeta]; throws when a role's shape is unsupported
+// (the caller checks conv_dgrad_wgrad_ok first).
+std::vector<Tensor> conv_dgrad_wgrad(const Tensor& x, const Tensor& w, int64_t pad, c10::optional<Tensor> residual,
+                                     const std::vector<Tensor>& bn, double bn_eps, bool bn_fix_gamma,
+                                     const Tensor& bnb_x, c10::optional<Tensor> dadd, Tensor dgamma, Tensor dbeta,
+                                     const Tensor& wg_dy, const Tensor& wg_x, int64_t KH, int64_t KW, int64_t wg_stride,
+                                     int64_t wg_pad, Tensor wg_out) {
+  CHECK_DEV(x); CHECK_DEV(w); CHECK_DEV(wg_dy); CHECK_DEV(wg_x); CHECK_DEV(wg_out);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast) && w.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_dgrad_wgrad: channels_last bf16 x / w");
+  const int NB = (int)x.size(0), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int Cout = (int)w.size(0), kh = (int)w.size(2), kw = (int)w.size(3);
+  TORCH_CHECK(w.size(1) == Cin && Cin % 64 == 0 && Cout % 8 == 0, "conv_dgrad_wgrad: dgrad channels");
+  const int Ho = H + 2 * (int)pad - kh + 1, Wo = W + 2 * (int)pad - kw + 1;
+  mxr::ConvEpi ep;
+  Tensor y = at::empty({NB, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  if (residual.has_value() && residual->defined()) {
+    TORCH_CHECK(residual->scalar_type() == at::kBFloat16 && residual->sizes() == y.sizes() &&
+                    residual->is_contiguous(at::MemoryFormat::ChannelsLast), "residual like y");
+    ep.residual = reinterpret_cast<const uint16_t*>(residual->data_ptr());
+  }
+  TORCH_CHECK(bn.size() == 4, "bn = (gamma, beta, mean, var)");
+  std::vector<Tensor> bnf;
+  for (const auto& t : bn) {
+    TORCH_CHECK(t.numel() == Cout, "bn parameter size");
+    bnf.push_back(t.to(at::kFloat).contiguous());
+  }
+  ep.bn_gamma = bnf[0].data_ptr<float>();
+  ep.bn_beta = bnf[1].data_ptr<float>();
+  ep.bn_mean = bnf[2].data_ptr<float>();
+  ep.bn_var = bnf[3].data_ptr<float>();
+  ep.bn_eps = (float)bn_eps;
+  ep.bn_fix_gamma = bn_fix_gamma ? 1 : 0;
+  ep.act_relu = 1;
+  TORCH_CHECK(bnb_x.scalar_type() == at::kBFloat16 && bnb_x.sizes() == y.sizes() &&
+                  bnb_x.is_contiguous(at::MemoryFormat::ChannelsLast), "bnb_x like y");
+  ep.bnb_x = reinterpret_cast<const uint16_t*>(bnb_x.data_ptr());
+  if (dadd.has_value() && dadd->defined()) {
+    TORCH_CHECK(dadd->scalar_type() == at::kBFloat16 && dadd->sizes() == y.sizes() &&
+                    dadd->is_contiguous(at::MemoryFormat::ChannelsLast), "dadd like y");
+    ep.dadd = reinterpret_cast<const uint16_t*>(dadd->data_ptr());
+  }
+  TORCH_CHECK(dgamma.scalar_type() == at::kFloat && dbeta.scalar_type() == at::kFloat && dgamma.is_contiguous() &&
+                  dbeta.is_contiguous() && dgamma.numel() == Cout && dbeta.numel() == Cout,
+              "dgamma / dbeta: contiguous fp32 (C,)");
+  ep.bnb_dgamma = dgamma.data_ptr<float>();
+  ep.bnb_dbeta = dbeta.data_ptr<float>();
+  // weight-gradient role
+  TORCH_CHECK(wg_dy.scalar_type() == at::kBFloat16 && wg_x.scalar_type() == at::kBFloat16 &&
+                  wg_dy.is_contiguous(at::MemoryFormat::ChannelsLast) && wg_x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "conv_dgrad_wgrad: channels_last bf16 wg_dy / wg_x");
+  const int gNB = (int)wg_x.size(0), gCin = (int)wg_x.size(1), gH = (int)wg_x.size(2), gW = (int)wg_x.size(3);
+  const int gCout = (int)wg_dy.size(1), gHo = (int)wg_dy.size(2), gWo = (int)wg_dy.size(3);
+  TORCH_CHECK(wg_dy.size(0) == gNB && gCin % 64 == 0 && gCout % 8 == 0, "conv_dgrad_wgrad: wgrad channels");
+  TORCH_CHECK(gHo == (gH + 2 * wg_pad - KH) / wg_stride + 1 && gWo == (gW + 2 * wg_pad - KW) / wg_stride + 1,
+              "conv_dgrad_wgrad: wgrad geometry");
+  TORCH_CHECK(wg_out.scalar_type() == at::kBFloat16 && wg_out.size(0) == gCout && wg_out.size(1) == gCin &&
+                  wg_out.size(2) == KH && wg_out.size(3) == KW && wg_out.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "wg_out: channels_last bf16 (Cout, Cin, KH, KW)");
+  DevGuard g(x.device());
+  int sp = 1;
+  mxr::conv_wgrad_plan(gNB, gHo, gWo, gCin, gCout, (int)KH, (int)KW, &sp);
+  Tensor slab = at::empty({sp > 1 ? (int64_t)sp * gCout * KH * KW * gCin : 1}, x.options().dtype(at::kFloat));
+  const int r = mxr::conv_dgrad_wgrad(
+      reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
+      reinterpret_cast<uint16_t*>(y.data_ptr()), NB, H, W, Cin, Ho, Wo, Cout, kh, kw, (int)pad, ep,
+      reinterpret_cast<const uint16_t*>(wg_dy.data_ptr()), reinterpret_cast<const uint16_t*>(wg_x.data_ptr()),
+      reinterpret_cast<uint16_t*>(wg_out.data_ptr()), slab.data_ptr<float>(), gNB, gH, gW, gCin, gHo, gWo, gCout,
+      (int)KH, (int)KW, (int)wg_stride, (int)wg_pad, sp, 1, cur_stream());
+  TORCH_CHECK(r == 0, "conv_dgrad_wgrad: unsupported shape");
+  return {y, dgamma, dbeta};
+}
+
 // ---- pooling ---------------------------------------------------------------------------------
 std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t p) {
   CHECK_DEV(x);
@@ -1380,6 +1457,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("drop_seed") = 0, py::arg("drop_step") = py::none(), py::arg("pad_w") = -1,
         py::arg("out") = py::none(), py::arg("out_map") = py::none());
   m.def("proposal_topk", &proposal_topk, py::arg("keys"), py::arg("boxes"), py::arg("P"));
+  m.def("conv_dgrad_wgrad", &conv_dgrad_wgrad, py::arg("x"), py::arg("w"), py::arg("pad"), py::arg("residual"),
+        py::arg("bn"), py::arg("bn_eps"), py::arg("bn_fix_gamma"), py::arg("bnb_x"), py::arg("dadd"), py::arg("dgamma"),
+        py::arg("dbeta"), py::arg("wg_dy"), py::arg("wg_x"), py::arg("KH"), py::arg("KW"), py::arg("wg_stride"),
+        py::arg("wg_pad"), py::arg("wg_out"));
   m.def("head_bwd", &head_bwd, py::arg("x"), py::arg("dys"), py::arg("ws"), py::arg("dws"), py::arg("dw_acc"),
         py::arg("dbs"), py::arg("db_acc"), py::arg("need_dx"), py::arg("relu_mask"));
   m.def("chan_sum", &chan_sum, py::arg("x"), py::arg("out"), py::arg("accumulate"));

@@ -28,6 +28,7 @@
 
 #include "common.h"
 #include "../kernels.h"
+#include "wgrad_body.h"
 
 // epilogue storage code: fp16 when the conv runs on fp16 activations (inference), else bf16
 #define EPC (ep.f16 ? 2 : 1)
@@ -716,21 +717,23 @@ __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t rs, void* lds_w
                                            (int)voff, (int)soff, 0, 0);
 }
 
+// body of the buffer kernel for workgroup `bid` of an `nwg`-workgroup launch; `lds`: S*(BM+BN)*BK
+// elements, the block's ONLY LDS (the grouped data + weight gradient launch below shares it with
+// the wgrad role)
 template <int BM, int BN, int S, bool F16 = false>
-__global__ void __launch_bounds__(256)
-conv_igemm_buf_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
-                      int NB, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad,
-                      const ConvEpi ep, int tiles_n, int nwg, int ntiles, int splits, float* __restrict__ slab) {
+__device__ __forceinline__ void igemm_buf_body(uint16_t* __restrict__ lds, int bid, const uint16_t* __restrict__ x,
+                                               const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int NB, int H,
+                                               int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride,
+                                               int pad, const ConvEpi& ep, int tiles_n, int nwg, int ntiles, int splits,
+                                               float* __restrict__ slab) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int ACH = BM / 32, BCH = BN / 32;
   constexpr int LPS = ACH + BCH;
   static_assert(S >= 2 && S <= 8, "pipeline depth");
-  __shared__ __attribute__((aligned(16))) uint16_t lds[S * (BM + BN) * BK];  // the ONLY __shared__ object
   uint16_t* As = lds;
   uint16_t* Bs = lds + S * BM * BK;
 
-  const int bid = blockIdx.x;
   const int q = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
   const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + bid / 8;
   const int split = wgid / ntiles, tile = wgid % ntiles;
@@ -848,6 +851,16 @@ conv_igemm_buf_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
                                                ep, y, split, splits, slab, Ho, Wo);
   else
     igemm_epilogue<TM, TN, WM, WN>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab, Ho, Wo);
+}
+
+template <int BM, int BN, int S, bool F16 = false>
+__global__ void __launch_bounds__(256)
+conv_igemm_buf_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
+                      int NB, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad,
+                      const ConvEpi ep, int tiles_n, int nwg, int ntiles, int splits, float* __restrict__ slab) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[S * (BM + BN) * BK];
+  igemm_buf_body<BM, BN, S, F16>(lds, blockIdx.x, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, tiles_n,
+                                 nwg, ntiles, splits, slab);
 }
 
 // ---- tile-balanced LDS-DMA ring (the production path) ----------------------------------------
@@ -1415,6 +1428,52 @@ conv_wt_flip_kernel(const WtFlipEntry* __restrict__ entries, int n_entries) {
 void conv_wt_flip_multi(const WtFlipEntry* entries, int n_entries, int total_tiles, hipStream_t st) {
   if (n_entries <= 0 || total_tiles <= 0) return;
   conv_wt_flip_kernel<<<total_tiles, 256, 0, st>>>(entries, n_entries);
+}
+
+// ---- grouped data + weight gradient launch -----------------------------------------------------
+// The backward of a stride-1 conv inside a fused residual unit as ONE launch: workgroups
+// [0, nwg_d) run the data gradient (the 64x64 buffer kernel above over dY with the flipped filter,
+// any ConvEpi epilogue -- the BN-ReLU backward of the fused units), workgroups [nwg_d, ...) the
+// weight gradient (conv_wgrad.hip's LDS-DMA body, split over pixels into fp32 slabs).  Both roles
+// read the same dY and use one 48 KB LDS ring, so a CU holds up to three blocks of either role.
+// Replaces the two-stream schedule (wgrad on a side stream, one cross-queue wait per wgrad and a
+// join per unit): every cross-queue edge of a replayed graph cost ~10 us of idle time, four per
+// unit (profiles/r2_resnet101_stage3_unit_timeline.txt).
+__global__ void __launch_bounds__(256)
+conv_dgrad_wgrad_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
+                        int NB, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int pad,
+                        const ConvEpi ep, int tiles_n, int nwg_d, int ntiles, WgradParams wp) {
+  static_assert(3 * (64 + 64) * BK == kWgradLdsElems, "both roles use the same 48 KB ring");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[3 * (64 + 64) * BK];
+  if ((int)blockIdx.x < nwg_d)
+    igemm_buf_body<64, 64, 3, false>(lds, blockIdx.x, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, 1, pad, ep, tiles_n,
+                                     nwg_d, ntiles, 1, nullptr);
+  else
+    wgrad_buf_body<3>(lds, (int)blockIdx.x - nwg_d, wp);
+}
+
+int conv_dgrad_wgrad(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho, int Wo,
+                     int Cout, int KH, int KW, int pad, const ConvEpi& ep, const uint16_t* wg_dy,
+                     const uint16_t* wg_x, uint16_t* dw, float* slab, int wg_NB, int wg_H, int wg_W, int wg_Cin,
+                     int wg_Ho, int wg_Wo, int wg_Cout, int wg_KH, int wg_KW, int wg_stride, int wg_pad, int wg_splits,
+                     int accumulate, hipStream_t st) {
+  if (Cin % BK != 0 || Cout % 8 != 0 || ep.f16 || ep.omap || ep.pad_w >= 0) return -1;
+  if ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB || (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kBufOOB)
+    return -1;
+  if (wg_Cin % WG_BN != 0 || wg_Cout % 8 != 0 || wg_splits < 1) return -1;
+  if ((int64_t)wg_NB * wg_Ho * wg_Wo * wg_Cout * 2 >= (int64_t)kWgOOB ||
+      (int64_t)wg_NB * wg_H * wg_W * wg_Cin * 2 >= (int64_t)kWgOOB)
+    return -1;
+  const int M = NB * Ho * Wo;
+  const int tiles_n = (Cout + 63) / 64;
+  const int ntiles = ((M + 63) / 64) * tiles_n;
+  const WgradParams wp = wgrad_params(wg_dy, wg_x, dw, slab, wg_NB, wg_H, wg_W, wg_Cin, wg_Ho, wg_Wo, wg_Cout, wg_KH,
+                                      wg_KW, wg_stride, wg_pad, wg_splits, accumulate);
+  conv_dgrad_wgrad_kernel<<<ntiles + wp.nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, pad, ep,
+                                                            tiles_n, ntiles, ntiles, wp);
+  if (wg_splits > 1)
+    wgrad_reduce(slab, wg_splits, (int64_t)wg_Cout * wg_KH * wg_KW * wg_Cin, dw, accumulate, st);
+  return 0;
 }
 
 }  // namespace mxr

@@ -22,28 +22,9 @@
 
 #include "common.h"
 #include "../kernels.h"
+#include "wgrad_body.h"
 
 namespace mxr {
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef short s16x4 __attribute__((ext_vector_type(4)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int WG_BM = 64, WG_BN = 64, WG_BK = 64;  // co x k-cols x pixels per step
-constexpr int WG_ROW = 80;                         // padded LDS row, in bf16 elements (160 B)
-
-__device__ __forceinline__ s16x4 tr_read(const uint16_t* p) {
-  return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-      (__attribute__((address_space(3))) s16x4*)(reinterpret_cast<uintptr_t>(p)));
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt_wg() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// LDS row holding MFMA k-index (kk*32) + 8g + j, for the first (j<4) / second (j>=4) read
-__device__ __forceinline__ int krow(int kk, int g, int second) { return kk * 32 + (second ? 16 : 0) + 4 * g; }
 
 __global__ void __launch_bounds__(256)
 conv_wgrad_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, float* __restrict__ slab, int NB,
@@ -154,173 +135,10 @@ conv_wgrad_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ 
       }
 }
 
-// ---- LDS-DMA variant ------------------------------------------------------------------------
-// Same GEMM and transposed fragment reads, restructured like conv_igemm_buf_kernel: both
-// operands arrive by buffer_load_dwordx4 ... lds (S-deep ring, counted vmcnt, raw barrier), so
-// the per-step VALU is the pixel -> (img, ho, wo) split of two rows (multiply-high divisions by
-// precomputed magic numbers instead of integer division) and the per-lane validity selects.
-// DMA writes LDS lane-linearly, so the 160-B row padding of the kernel above becomes an XOR
-// swizzle of the 16-B chunk, chunk ^ ((row >> 1) & 3) * 2: the 8 rows x 32 B read by each
-// half-wave of ds_read_b64_tr_b16 then fall on 16 distinct 16-B bank slots (conflict-free).
-// The epilogue goes through LDS as well: with one split the tile is written straight to the
-// bf16 gradient (accumulating into it when asked), otherwise as float4 slab rows.
-struct FastDiv {
-  uint32_t mul, shift;
-};
-
-static FastDiv make_fastdiv(uint32_t d) {  // n / d == (mulhi(n, mul) + n) >> shift for n < 2^31
-  uint32_t l = 0;
-  while ((1u << l) < d) ++l;
-  FastDiv f;
-  f.shift = l;
-  f.mul = (uint32_t)(((((uint64_t)1 << l) - d) << 32) / d + 1);
-  return f;
-}
-
-__device__ __forceinline__ uint32_t fdiv(uint32_t n, FastDiv f) { return (__umulhi(n, f.mul) + n) >> f.shift; }
-
-__device__ __forceinline__ int wsw(int row) { return ((row >> 1) & 3) << 1; }
-
-constexpr uint32_t kWgOOB = 0x80000000u;
-
 template <int S>
-__global__ void __launch_bounds__(256)
-conv_wgrad_buf_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ x, float* __restrict__ slab,
-                      uint16_t* __restrict__ dw, int accumulate, int NB, int H, int W, int Cin, int Ho, int Wo,
-                      int Cout, int KW, int stride, int pad, int tiles_n, int ntiles, int splits, int per,
-                      FastDiv fd_hw, FastDiv fd_w) {
-  constexpr int LPS = 4;  // DMA instructions per thread per stage (2 dY rows + 2 X rows)
-  static_assert(S >= 2 && S <= 4, "pipeline depth");
+__global__ void __launch_bounds__(256) conv_wgrad_buf_kernel(WgradParams p) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[S * 2 * WG_BK * 64];  // [S][dY|X][64 px][64 ch]
-  const int wgid = blockIdx.x;
-  const int split = wgid / ntiles, tile = wgid % ntiles;
-  const int tm = tile / tiles_n, tn = tile % tiles_n;
-  const int co0 = tm * WG_BM, k0 = tn * WG_BN;
-  const int tap = k0 / Cin, ci0 = k0 % Cin;
-  const int fr = tap / KW, fc = tap % KW;
-  const int P = NB * Ho * Wo, HWo = Ho * Wo;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int steps_all = (P + WG_BK - 1) / WG_BK;
-  const int s_begin = split * per, s_end = min(steps_all, s_begin + per);
-  const int nsteps = max(0, s_end - s_begin);
-
-  const __amdgpu_buffer_rsrc_t dyr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)dy, (short)0, (int)((int64_t)P * Cout * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t xr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)((int64_t)NB * H * W * Cin * 2), 0x00020000);
-  int rowi[2], chk[2];
-  uint32_t a_off[2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    rowi[i] = 32 * i + 8 * wid + (lane >> 3);
-    chk[i] = (lane & 7) ^ wsw(rowi[i]);
-    a_off[i] = co0 + chk[i] * 8 < Cout ? (uint32_t)((rowi[i] * Cout + co0 + chk[i] * 8) * 2) : kWgOOB;
-  }
-  auto issue = [&](int sl, int buf) {
-    const int p0 = (s_begin + sl) * WG_BK;
-    uint16_t* Ab = lds + buf * 2 * WG_BK * 64;
-    uint16_t* Bb = Ab + WG_BK * 64;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int p = p0 + rowi[i];
-      const uint32_t va = p < P ? a_off[i] : kWgOOB;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(dyr, (__attribute__((address_space(3))) void*)(Ab + (32 * i + 8 * wid) * 64),
-                                               16, (int)va, (int)((uint32_t)p0 * Cout * 2), 0, 0);
-      uint32_t vb = kWgOOB;
-      if (p < P) {
-        const int img = (int)fdiv((uint32_t)p, fd_hw), rem = p - img * HWo;
-        const int ho = (int)fdiv((uint32_t)rem, fd_w), wo = rem - ho * Wo;
-        const int hi = ho * stride - pad + fr, wi = wo * stride - pad + fc;
-        if ((unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W)
-          vb = (uint32_t)(((((int64_t)img * H + hi) * W + wi) * Cin + ci0 + chk[i] * 8) * 2);
-      }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(Bb + (32 * i + 8 * wid) * 64),
-                                               16, (int)vb, 0, 0, 0);
-    }
-  };
-
-  f32x4 acc[2][2];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const int g = lane >> 4, q = (lane & 15) >> 2, pcol = (lane & 3) * 4;
-  // swizzled element offset of (row, col), col a multiple of 4 inside one 16-B chunk
-  auto lidx = [](int row, int col) { return row * 64 + (((col >> 3) ^ wsw(row)) << 3) + (col & 7); };
-
-#pragma unroll
-  for (int s = 0; s < S - 1; ++s)
-    if (s < nsteps) issue(s, s);
-  for (int st = 0; st < nsteps; ++st) {
-    const int ahead = min(S - 2, nsteps - 1 - st);
-    if (ahead >= 2) wait_vmcnt_wg<2 * LPS>();
-    else if (ahead == 1) wait_vmcnt_wg<LPS>();
-    else wait_vmcnt_wg<0>();
-    __builtin_amdgcn_s_barrier();
-    if (st + S - 1 < nsteps) issue(st + S - 1, (st + S - 1) % S);
-    const uint16_t* Ab = lds + (st % S) * 2 * WG_BK * 64;
-    const uint16_t* Bb = Ab + WG_BK * 64;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[2], bfr[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int col = wm * 32 + i * 16 + pcol;
-        const s16x4 lo = tr_read(Ab + lidx(krow(kk, g, 0) + q, col));
-        const s16x4 hi = tr_read(Ab + lidx(krow(kk, g, 1) + q, col));
-        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-      }
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int col = wn * 32 + j * 16 + pcol;
-        const s16x4 lo = tr_read(Bb + lidx(krow(kk, g, 0) + q, col));
-        const s16x4 hi = tr_read(Bb + lidx(krow(kk, g, 1) + q, col));
-        bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
-    }
-  }
-
-  // epilogue through LDS: T[co][k] fp32 (row stride 68), then 8-column vectors per thread
-  float* T = reinterpret_cast<float*>(lds);
-  __syncthreads();
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        T[(wm * 32 + i * 16 + (lane >> 4) * 4 + r) * 68 + wn * 32 + j * 16 + (lane & 15)] = acc[i][j][r];
-  __syncthreads();
-  const int ldk = tiles_n * WG_BN;
-#pragma unroll
-  for (int v = 0; v < 2; ++v) {
-    const int e = tid + v * 256, row = e >> 3, cv = e & 7;
-    const int co = co0 + row;
-    if (co >= Cout) continue;
-    const float4* src = reinterpret_cast<const float4*>(T + row * 68 + cv * 8);
-    const float4 a0 = src[0], a1 = src[1];
-    const int64_t o = (int64_t)co * ldk + k0 + cv * 8;
-    if (splits > 1) {
-      float4* d = reinterpret_cast<float4*>(slab + (int64_t)split * Cout * ldk + o);
-      d[0] = a0;
-      d[1] = a1;
-    } else {
-      float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-      if (accumulate) {
-        float prev[8];
-        ld8_bf16(dw + o, prev);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) a[k] += prev[k];
-      }
-      st8_bf16(dw + o, a);
-    }
-  }
+  wgrad_buf_body<S>(lds, blockIdx.x, p);
 }
 
 __global__ void __launch_bounds__(256)
@@ -339,6 +157,28 @@ wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int64_t n, uint1
   }
   *reinterpret_cast<ushort4*>(out + e) = make_ushort4(f32_to_bf16(a.x), f32_to_bf16(a.y), f32_to_bf16(a.z),
                                                       f32_to_bf16(a.w));
+}
+
+WgradParams wgrad_params(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab, int NB, int H, int W,
+                         int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int splits,
+                         int accumulate) {
+  WgradParams p;
+  p.dy = dy; p.x = x; p.slab = slab; p.dw = dw; p.accumulate = accumulate;
+  p.NB = NB; p.H = H; p.W = W; p.Cin = Cin; p.Ho = Ho; p.Wo = Wo; p.Cout = Cout; p.KW = KW;
+  p.stride = stride; p.pad = pad;
+  p.tiles_n = KH * KW * Cin / WG_BN;
+  p.ntiles = ((Cout + WG_BM - 1) / WG_BM) * p.tiles_n;
+  p.splits = splits;
+  const int steps = (NB * Ho * Wo + WG_BK - 1) / WG_BK;
+  p.per = (steps + splits - 1) / splits;
+  p.nwg = p.ntiles * splits;
+  p.fd_hw = make_fastdiv(Ho * Wo);
+  p.fd_w = make_fastdiv(Wo);
+  return p;
+}
+
+void wgrad_reduce(const float* slab, int splits, int64_t n, uint16_t* dw, int accumulate, hipStream_t st) {
+  wgrad_reduce_kernel<<<div_up((n + 3) / 4, 256), 256, 0, st>>>(slab, splits, n, dw, accumulate);
 }
 
 int conv_wgrad_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int* splits_out) {
@@ -369,9 +209,8 @@ int conv_wgrad(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab,
   const int64_t n = (int64_t)Cout * KH * KW * Cin;
   const bool buf_ok = (int64_t)P * Cout * 2 < (int64_t)kWgOOB && (int64_t)NB * H * W * Cin * 2 < (int64_t)kWgOOB;
   if (variant == 0 && buf_ok) {
-    conv_wgrad_buf_kernel<3><<<ntiles * splits, 256, 0, st>>>(dy, x, slab, dw, accumulate, NB, H, W, Cin, Ho, Wo, Cout,
-                                                              KW, stride, pad, tiles_n, ntiles, splits, per,
-                                                              make_fastdiv(Ho * Wo), make_fastdiv(Wo));
+    conv_wgrad_buf_kernel<3><<<ntiles * splits, 256, 0, st>>>(
+        wgrad_params(dy, x, dw, slab, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, splits, accumulate));
     if (splits > 1) wgrad_reduce_kernel<<<div_up((n + 3) / 4, 256), 256, 0, st>>>(slab, splits, n, dw, accumulate);
     return splits;
   }

@@ -237,6 +237,14 @@ void conv_wt_flip_multi(const WtFlipEntry* entries, int n_entries, int total_til
 // dy (NB, Ho, Wo, Cout) bf16, x (NB, H, W, Cin) bf16 -> dw (Cout, KH, KW, Cin) bf16.
 // slab: splits * Cout * KH*KW*Cin floats.  Requires Cin % 64 == 0, Cout % 8 == 0.
 int conv_wgrad_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int* splits_out);
+// Grouped launch (conv_igemm.hip): the stride-1 implicit-GEMM conv (x, w) -> y with epilogue `ep`
+// (64x64 buffer kernel, no split) AND the weight gradient (wg_*: as conv_wgrad) in ONE launch, plus
+// the wgrad split-K reduce when wg_splits > 1.  Returns 0, or -1 when a role's shape is unsupported.
+int conv_dgrad_wgrad(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho, int Wo,
+                     int Cout, int KH, int KW, int pad, const ConvEpi& ep, const uint16_t* wg_dy,
+                     const uint16_t* wg_x, uint16_t* dw, float* slab, int wg_NB, int wg_H, int wg_W, int wg_Cin,
+                     int wg_Ho, int wg_Wo, int wg_Cout, int wg_KH, int wg_KW, int wg_stride, int wg_pad, int wg_splits,
+                     int accumulate, hipStream_t st);
 int conv_wgrad(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab, int NB, int H, int W, int Cin,
                int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int splits, int accumulate,
                hipStream_t st, int variant = 0);

@@ -150,6 +150,13 @@ def _cl(t):
 _SIDE = {}
 
 
+def grouped_enabled():
+    """One launch per conv for data + weight gradient in the fused units (MXR_GROUPED_BWD=0: the
+    weight gradient on the side stream instead)."""
+    import os
+    return os.environ.get('MXR_GROUPED_BWD', '1') != '0'
+
+
 def _side_stream(device):
     """Per-device side stream for the weight-gradient kernels (MXR_WGRAD_STREAM=0 disables)."""
     import os
@@ -258,6 +265,7 @@ class _FusedUnitFn(torch.autograd.Function):
         # allocator): any lag of the side stream behind its unit costs more than the hand-off
         main = torch.cuda.current_stream() if x.is_cuda else None
         side = _side_stream(x.device) if main is not None else None
+        used_side = [False]
 
         def wgrad(idx, dy, inp, k, stride, pad):
             if not need[idx]:
@@ -265,6 +273,7 @@ class _FusedUnitFn(torch.autograd.Function):
             tgt = grad_sink.target(ctx.params[idx])
             if side is not None:
                 side.wait_stream(main)
+                used_side[0] = True
             with torch.cuda.stream(side) if side is not None else _nullctx():
                 if tgt is not None and tgt.is_contiguous(memory_format=torch.channels_last):
                     ext.conv_wgrad(dy, inp, k, k, stride, pad, 0, tgt)
@@ -295,12 +304,37 @@ class _FusedUnitFn(torch.autograd.Function):
                 if need[gi + 1]:
                     grads[gi + 1] = tb.to(bnps[i][1].dtype)
 
-        def dgrad_bn(dy, w_idx, k, pad, bn_i, bn_x, dadd=None, dres=None):
-            """dgrad of a stride-1 conv with the BN(bn_i)-ReLU backward of its input in the epilogue."""
+        def grouped_target(wg):
+            """The flat-gradient target of pending weight gradient ``wg`` = (idx, dy, inp, k, stride,
+            pad) when it can ride in the grouped dgrad launch, else None."""
+            if wg is None or not grouped_enabled() or not need[wg[0]] or not wg[1].is_cuda:
+                return None
+            tgt = grad_sink.target(ctx.params[wg[0]])
+            if tgt is None or not tgt.is_contiguous(memory_format=torch.channels_last) or tgt.dtype != torch.bfloat16:
+                return None
+            return tgt
+
+        def dgrad_bn(dy, w_idx, k, pad, bn_i, bn_x, dadd=None, dres=None, wg=None):
+            """dgrad of a stride-1 conv with the BN(bn_i)-ReLU backward of its input in the epilogue;
+            with ``wg`` the weight gradient of a conv (idx, dy, inp, k, stride, pad) in the SAME launch
+            (csrc/hip/conv_igemm.hip conv_dgrad_wgrad), otherwise on the side stream."""
             from .conv import dgrad_weight
             tg, tb, ret = bn_targets(bn_i)
-            r = ext.conv_igemm_fwd(dy, dgrad_weight(ctx.params[w_idx], ws[w_idx]), None, 1, k - 1 - pad, False, 0, 0,
-                                   dres, bnps[bn_i], spec.eps[bn_i], spec.fix[bn_i], True, bn_x, dadd, tg, tb)
+            wf = dgrad_weight(ctx.params[w_idx], ws[w_idx])
+            tgt = grouped_target(wg)
+            if tgt is not None and dy.dtype == torch.bfloat16 and wf.dtype == torch.bfloat16:
+                if tg is None:  # statistics not needed: accumulate into scratch
+                    C = bnps[bn_i][0].numel()
+                    tg = torch.zeros(C, device=dy.device, dtype=torch.float32)
+                    tb = torch.zeros(C, device=dy.device, dtype=torch.float32)
+                idx, wdy, winp, wk, wstride, wpad = wg
+                r = ext.conv_dgrad_wgrad(dy, wf, k - 1 - pad, dres, bnps[bn_i], spec.eps[bn_i], spec.fix[bn_i], bn_x,
+                                         dadd, tg, tb, wdy, winp, wk, wk, wstride, wpad, tgt)
+            else:
+                if wg is not None:
+                    wgrad(*wg)
+                r = ext.conv_igemm_fwd(dy, wf, None, 1, k - 1 - pad, False, 0, 0, dres, bnps[bn_i], spec.eps[bn_i],
+                                       spec.fix[bn_i], True, bn_x, dadd, tg, tb)
             finish_bn(bn_i, tg, tb, ret)
             return r[0]
 
@@ -327,36 +361,39 @@ class _FusedUnitFn(torch.autograd.Function):
             return dx
 
         s = spec.stride
+        # each conv's weight gradient rides in the launch of a data gradient that reads the same
+        # dY (grouped), or runs on the side stream (wgrad(...)); wg0 (conv1's) is issued with the
+        # unit's input gradient below
         if spec.bottle:
             # conv3 (1x1) : wgrad + dgrad with bn3 backward
-            wgrad(2, d_out, a3, 1, 1, 0)
-            d_y2 = dgrad_bn(d_out, 2, 1, 0, 2, y2)
+            d_y2 = dgrad_bn(d_out, 2, 1, 0, 2, y2, wg=(2, d_out, a3, 1, 1, 0))
             # conv2 (3x3, stride s)
-            wgrad(1, d_y2, a2, 3, s, 1)
             if s == 1:
-                d_y1 = dgrad_bn(d_y2, 1, 3, 1, 1, y1)
+                d_y1 = dgrad_bn(d_y2, 1, 3, 1, 1, y1, wg=(1, d_y2, a2, 3, s, 1))
             elif _strided_ok(ws[1], s, a2):
+                wgrad(1, d_y2, a2, 3, s, 1)
                 d_y1 = strided_dgrad_bn(d_y2, 1, 3, s, 1, 1, y1, a2.shape[2], a2.shape[3])
             else:
+                wgrad(1, d_y2, a2, 3, s, 1)
                 d_a2 = torch.ops.aten.convolution_backward(d_y2, a2, ws[1], None, [s, s], [1, 1], [1, 1], False,
                                                            [0, 0], 1, [True, False, False])[0]
                 d_y1 = bn_bwd_plain(_cl(d_a2), 1, y1)
-            wgrad(0, d_y1, act1, 1, 1, 0)
+            wg0 = (0, d_y1, act1, 1, 1, 0)
             k1, p1, s1 = 1, 0, 1
         else:
             # basic: conv2 (3x3 s1) then conv1 (3x3 stride s)
-            wgrad(1, d_out, a2, 3, 1, 1)
-            d_y1 = dgrad_bn(d_out, 1, 3, 1, 1, y1)
-            wgrad(0, d_y1, act1, 3, s, 1)
+            d_y1 = dgrad_bn(d_out, 1, 3, 1, 1, y1, wg=(1, d_out, a2, 3, 1, 1))
+            wg0 = (0, d_y1, act1, 3, s, 1)
             k1, p1, s1 = 3, 1, s
         # bn1 (the unit's input BN) gets its gamma / beta gradients from the d_x pass below; when
         # the unit input needs no gradient (first trainable unit after frozen stages) that pass
         # still runs if bn1's own parameters are trainable (its dx is then discarded)
         bn1_trainable = need[nconv] or need[nconv + 1]
         if not ctx.needs_input_grad[1] and not bn1_trainable:
+            wgrad(*wg0)
             if not spec.dim_match:
                 wgrad(nconv - 1, d_out, act1, 1, s, 0)
-            if side is not None:
+            if used_side[0]:
                 main.wait_stream(side)
             return (None, None, None) + tuple(grads)
         d_sc = None
@@ -372,16 +409,18 @@ class _FusedUnitFn(torch.autograd.Function):
                 d_sc[:, :, ::s, ::s] = d_sub
         dres = d_out if spec.dim_match else None
         if s1 == 1 and ws[0].shape[0] % 64 == 0:
-            d_x = dgrad_bn(d_y1, 0, k1, p1, 0, x, dadd=d_sc, dres=dres)
+            d_x = dgrad_bn(d_y1, 0, k1, p1, 0, x, dadd=d_sc, dres=dres, wg=wg0)
         elif s1 > 1 and _strided_ok(ws[0], s1, act1):
+            wgrad(*wg0)
             d_x = strided_dgrad_bn(d_y1, 0, k1, s1, p1, 0, x, act1.shape[2], act1.shape[3], dadd=d_sc, dres=dres)
         else:
+            wgrad(*wg0)
             d_act1 = torch.ops.aten.convolution_backward(d_y1, act1, ws[0], None, [s1, s1], [p1, p1], [1, 1], False,
                                                          [0, 0], 1, [True, False, False])[0]
             if d_sc is not None:
                 d_act1 = d_act1 + d_sc
             d_x = bn_bwd_plain(_cl(d_act1), 0, x, dres)
-        if side is not None:
+        if used_side[0]:
             main.wait_stream(side)
         return (None, d_x if ctx.needs_input_grad[1] else None, None) + tuple(grads)
 

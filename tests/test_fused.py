@@ -288,3 +288,81 @@ def test_strided_dgrad_bnb_epilogue(cuda):
     for a, r in ((dx, ref_dx), (dgm, ref_dg), (dbt, ref_db)):
         err = (a.float().cpu() - r).abs().max().item()
         assert err <= 2e-2 * r.abs().max().item() + 2e-2, err
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('geo', [(256, 1024, 1, 24, 40, 1024, 256, 1, 1, 0), (256, 256, 3, 20, 30, 256, 256, 3, 1, 1),
+                                 (1024, 256, 1, 50, 84, 256, 1024, 1, 1, 0), (256, 256, 3, 50, 84, 256, 512, 1, 1, 0)])
+def test_grouped_dgrad_wgrad_matches_separate(cuda, geo):
+    """conv_dgrad_wgrad (one launch: BN-backward dgrad role + split-K wgrad role) against the same
+    two computations as separate launches (buffer kernel tile 23, conv_wgrad): same bodies, so the
+    data gradient and the weight gradient agree to rounding; dgamma / dbeta to atomic order."""
+    from mx_rcnn_amd.ops import need_ext
+    from mx_rcnn_amd.ops.conv import _flip_t
+    Cin, Cout, k, H, W, wCo, wCi, wk, ws, wp = geo
+    g = torch.Generator().manual_seed(5)
+    ext = need_ext()
+    w = (torch.randn(Cout, Cin, k, k, generator=g) * 0.05).bfloat16()
+    dy = _cl(torch.randn(1, Cout, H, W, generator=g).bfloat16(), cuda)
+    xr = _cl(torch.randn(1, Cin, H, W, generator=g).bfloat16(), cuda)
+    dres = _cl(torch.randn(1, Cin, H, W, generator=g).bfloat16(), cuda)
+    bn = [t.to(cuda) for t in (torch.rand(Cin, generator=g) + 0.5, torch.randn(Cin, generator=g) * 0.1,
+                               torch.randn(Cin, generator=g) * 0.2, torch.rand(Cin, generator=g) + 0.5)]
+    Ho, Wo = (H + 2 * wp - wk) // ws + 1, (W + 2 * wp - wk) // ws + 1
+    wdy = _cl(torch.randn(1, wCo, Ho, Wo, generator=g).bfloat16(), cuda)
+    wx = _cl(torch.randn(1, wCi, H, W, generator=g).bfloat16(), cuda)
+    dw0 = _cl((torch.randn(wCo, wCi, wk, wk, generator=g) * 0.1).bfloat16(), cuda)
+    wt = _flip_t(_cl(w, cuda))
+    p = k // 2
+    tg, tb = torch.zeros(Cin, device=cuda), torch.zeros(Cin, device=cuda)
+    dw = dw0.clone()
+    dx, dgm, dbt = ext.conv_dgrad_wgrad(dy, wt, k - 1 - p, dres, bn, 2e-5, False, xr, None, tg, tb, wdy, wx, wk, wk, ws,
+                                        wp, dw)
+    rdx, rdg, rdb = ext.conv_igemm_fwd(dy, wt, None, 1, k - 1 - p, False, 23, 1, dres, bn, 2e-5, False, True, xr, None)
+    rdw = dw0.clone()
+    ext.conv_wgrad(wdy, wx, wk, wk, ws, wp, 0, rdw)
+    torch.cuda.synchronize()
+    assert torch.equal(dx, rdx)
+    assert torch.allclose(dw.float(), rdw.float(), rtol=1e-2, atol=1e-2 * rdw.float().abs().max().item())
+    for a, r in ((dgm, rdg), (dbt, rdb)):
+        assert torch.allclose(a, r, rtol=1e-4, atol=1e-4 * r.abs().max().item() + 1e-5)
+
+
+@pytest.mark.gpu
+def test_grouped_unit_backward_matches_side_stream(cuda, monkeypatch):
+    """A fused stage-3 style unit pair under the FlatParamStore (direct gradient sinks, so the
+    grouped launches run) against MXR_GROUPED_BWD=0 (weight gradients on the side stream)."""
+    import copy
+    from mx_rcnn_amd.core.params import FlatParamStore
+    from mx_rcnn_amd.models.resnet import run_stage, _stage
+    class _Holder(torch.nn.Module):
+        def __init__(self, st):
+            super().__init__()
+            self.st = st
+
+        def mx_layers(self, mode=None):
+            return (m for m in self.modules() if hasattr(m, 'mx_args'))
+
+    torch.manual_seed(0)
+    stage = _stage(3, 3, 512, 1024, True, 0.99, True).to(cuda)
+    for mod in stage.modules():
+        if hasattr(mod, 'moving_var'):
+            mod.moving_var.uniform_(0.5, 1.5)
+            mod.moving_mean.normal_(0, 0.1)
+    x0 = torch.randn(1, 512, 50, 84).bfloat16()
+    res = []
+    for grouped in ('1', '0'):
+        monkeypatch.setenv('MXR_GROUPED_BWD', grouped)
+        st = copy.deepcopy(stage)
+        store = FlatParamStore(_Holder(st), device=cuda)
+        store.zero_grad()
+        x = _cl(x0, cuda).requires_grad_()
+        out = run_stage(st, x)
+        gen = torch.Generator().manual_seed(7)
+        out.backward(torch.randn(out.shape, generator=gen).bfloat16().to(cuda).contiguous(memory_format=torch.channels_last))
+        torch.cuda.synchronize()
+        res.append((x.grad.float(), {n: p.grad.float().clone() for n, p in store.params.items()}))
+    (xa, ga), (xb, gb) = res
+    assert _rel(xa, xb) <= 1e-2
+    for n in ga:
+        assert _rel(ga[n], gb[n]) <= 2e-2, (n, _rel(ga[n], gb[n]))

@@ -726,16 +726,20 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   return {y};
 }
 
-// Grouped backward of a stride-1 conv of a fused unit (conv_igemm.hip conv_dgrad_wgrad): the data
-// gradient dgrad = conv(dy, wf, pad) with the BN-ReLU backward epilogue (bn, bnb_x, optional dadd /
-// residual, dgamma/dbeta fp32 accumulators) AND the weight gradient of (wg_dy, wg_x) accumulated into
-// wg_out, in one launch.  Returns [dx, dgamma, dbeta]; throws when a role's shape is unsupported
-// (the caller checks conv_dgrad_wgrad_ok first).
+// Grouped backward of a stride-1 conv (conv_igemm.hip conv_dgrad_wgrad): the data gradient
+// dgrad = conv(x = dY, w = flipped filter, pad) -- with the BN-ReLU backward epilogue when `bn` is
+// given (bnb_x, optional dadd / residual, dgamma / dbeta fp32 accumulators), else plain (+residual)
+// -- AND the weight gradient of (wg_dy, wg_x) accumulated into wg_out, in one launch.  With
+// `defer` the weight gradient's split-K reduce is not launched: the returned slab (and wg_out)
+// go to the NEXT grouped launch as prev_slab / prev_out, whose first workgroups run it.
+// Returns [dx, dgamma, dbeta, slab] (dgamma / dbeta / slab empty when unused).
 std::vector<Tensor> conv_dgrad_wgrad(const Tensor& x, const Tensor& w, int64_t pad, c10::optional<Tensor> residual,
-                                     const std::vector<Tensor>& bn, double bn_eps, bool bn_fix_gamma,
-                                     const Tensor& bnb_x, c10::optional<Tensor> dadd, Tensor dgamma, Tensor dbeta,
-                                     const Tensor& wg_dy, const Tensor& wg_x, int64_t KH, int64_t KW, int64_t wg_stride,
-                                     int64_t wg_pad, Tensor wg_out) {
+                                     c10::optional<std::vector<Tensor>> bn, double bn_eps, bool bn_fix_gamma,
+                                     c10::optional<Tensor> bnb_x, c10::optional<Tensor> dadd,
+                                     c10::optional<Tensor> dgamma, c10::optional<Tensor> dbeta, const Tensor& wg_dy,
+                                     const Tensor& wg_x, int64_t KH, int64_t KW, int64_t wg_stride, int64_t wg_pad,
+                                     Tensor wg_out, bool defer, c10::optional<Tensor> prev_slab,
+                                     c10::optional<Tensor> prev_out) {
   CHECK_DEV(x); CHECK_DEV(w); CHECK_DEV(wg_dy); CHECK_DEV(wg_x); CHECK_DEV(wg_out);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast) && w.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -751,32 +755,39 @@ std::vector<Tensor> conv_dgrad_wgrad(const Tensor& x, const Tensor& w, int64_t p
                     residual->is_contiguous(at::MemoryFormat::ChannelsLast), "residual like y");
     ep.residual = reinterpret_cast<const uint16_t*>(residual->data_ptr());
   }
-  TORCH_CHECK(bn.size() == 4, "bn = (gamma, beta, mean, var)");
   std::vector<Tensor> bnf;
-  for (const auto& t : bn) {
-    TORCH_CHECK(t.numel() == Cout, "bn parameter size");
-    bnf.push_back(t.to(at::kFloat).contiguous());
+  Tensor dgm, dbt;
+  if (bn.has_value()) {
+    TORCH_CHECK(bn->size() == 4, "bn = (gamma, beta, mean, var)");
+    for (const auto& t : *bn) {
+      TORCH_CHECK(t.numel() == Cout, "bn parameter size");
+      bnf.push_back(t.to(at::kFloat).contiguous());
+    }
+    ep.bn_gamma = bnf[0].data_ptr<float>();
+    ep.bn_beta = bnf[1].data_ptr<float>();
+    ep.bn_mean = bnf[2].data_ptr<float>();
+    ep.bn_var = bnf[3].data_ptr<float>();
+    ep.bn_eps = (float)bn_eps;
+    ep.bn_fix_gamma = bn_fix_gamma ? 1 : 0;
+    ep.act_relu = 1;
+    TORCH_CHECK(bnb_x.has_value() && bnb_x->defined() && bnb_x->scalar_type() == at::kBFloat16 &&
+                    bnb_x->sizes() == y.sizes() && bnb_x->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "bn needs bnb_x like y");
+    ep.bnb_x = reinterpret_cast<const uint16_t*>(bnb_x->data_ptr());
+    if (dadd.has_value() && dadd->defined()) {
+      TORCH_CHECK(dadd->scalar_type() == at::kBFloat16 && dadd->sizes() == y.sizes() &&
+                      dadd->is_contiguous(at::MemoryFormat::ChannelsLast), "dadd like y");
+      ep.dadd = reinterpret_cast<const uint16_t*>(dadd->data_ptr());
+    }
+    TORCH_CHECK(dgamma.has_value() && dbeta.has_value() && dgamma->scalar_type() == at::kFloat &&
+                    dbeta->scalar_type() == at::kFloat && dgamma->is_contiguous() && dbeta->is_contiguous() &&
+                    dgamma->numel() == Cout && dbeta->numel() == Cout,
+                "dgamma / dbeta: contiguous fp32 (C,)");
+    dgm = *dgamma;
+    dbt = *dbeta;
+    ep.bnb_dgamma = dgm.data_ptr<float>();
+    ep.bnb_dbeta = dbt.data_ptr<float>();
   }
-  ep.bn_gamma = bnf[0].data_ptr<float>();
-  ep.bn_beta = bnf[1].data_ptr<float>();
-  ep.bn_mean = bnf[2].data_ptr<float>();
-  ep.bn_var = bnf[3].data_ptr<float>();
-  ep.bn_eps = (float)bn_eps;
-  ep.bn_fix_gamma = bn_fix_gamma ? 1 : 0;
-  ep.act_relu = 1;
-  TORCH_CHECK(bnb_x.scalar_type() == at::kBFloat16 && bnb_x.sizes() == y.sizes() &&
-                  bnb_x.is_contiguous(at::MemoryFormat::ChannelsLast), "bnb_x like y");
-  ep.bnb_x = reinterpret_cast<const uint16_t*>(bnb_x.data_ptr());
-  if (dadd.has_value() && dadd->defined()) {
-    TORCH_CHECK(dadd->scalar_type() == at::kBFloat16 && dadd->sizes() == y.sizes() &&
-                    dadd->is_contiguous(at::MemoryFormat::ChannelsLast), "dadd like y");
-    ep.dadd = reinterpret_cast<const uint16_t*>(dadd->data_ptr());
-  }
-  TORCH_CHECK(dgamma.scalar_type() == at::kFloat && dbeta.scalar_type() == at::kFloat && dgamma.is_contiguous() &&
-                  dbeta.is_contiguous() && dgamma.numel() == Cout && dbeta.numel() == Cout,
-              "dgamma / dbeta: contiguous fp32 (C,)");
-  ep.bnb_dgamma = dgamma.data_ptr<float>();
-  ep.bnb_dbeta = dbeta.data_ptr<float>();
   // weight-gradient role
   TORCH_CHECK(wg_dy.scalar_type() == at::kBFloat16 && wg_x.scalar_type() == at::kBFloat16 &&
                   wg_dy.is_contiguous(at::MemoryFormat::ChannelsLast) && wg_x.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -789,6 +800,19 @@ std::vector<Tensor> conv_dgrad_wgrad(const Tensor& x, const Tensor& w, int64_t p
   TORCH_CHECK(wg_out.scalar_type() == at::kBFloat16 && wg_out.size(0) == gCout && wg_out.size(1) == gCin &&
                   wg_out.size(2) == KH && wg_out.size(3) == KW && wg_out.is_contiguous(at::MemoryFormat::ChannelsLast),
               "wg_out: channels_last bf16 (Cout, Cin, KH, KW)");
+  const float* pslab = nullptr;
+  uint16_t* pout = nullptr;
+  int psplits = 0;
+  int64_t pn = 0;
+  if (prev_slab.has_value() && prev_slab->defined() && prev_slab->numel() > 0) {
+    TORCH_CHECK(prev_out.has_value() && prev_out->defined() && prev_out->scalar_type() == at::kBFloat16 &&
+                    prev_slab->scalar_type() == at::kFloat && prev_slab->numel() % prev_out->numel() == 0,
+                "prev_slab (splits * n fp32) / prev_out (n bf16)");
+    pn = prev_out->numel();
+    psplits = (int)(prev_slab->numel() / pn);
+    pslab = prev_slab->data_ptr<float>();
+    pout = reinterpret_cast<uint16_t*>(prev_out->data_ptr());
+  }
   DevGuard g(x.device());
   int sp = 1;
   mxr::conv_wgrad_plan(gNB, gHo, gWo, gCin, gCout, (int)KH, (int)KW, &sp);
@@ -798,9 +822,20 @@ std::vector<Tensor> conv_dgrad_wgrad(const Tensor& x, const Tensor& w, int64_t p
       reinterpret_cast<uint16_t*>(y.data_ptr()), NB, H, W, Cin, Ho, Wo, Cout, kh, kw, (int)pad, ep,
       reinterpret_cast<const uint16_t*>(wg_dy.data_ptr()), reinterpret_cast<const uint16_t*>(wg_x.data_ptr()),
       reinterpret_cast<uint16_t*>(wg_out.data_ptr()), slab.data_ptr<float>(), gNB, gH, gW, gCin, gHo, gWo, gCout,
-      (int)KH, (int)KW, (int)wg_stride, (int)wg_pad, sp, 1, cur_stream());
+      (int)KH, (int)KW, (int)wg_stride, (int)wg_pad, sp, 1, cur_stream(), defer ? 1 : 0, pslab, psplits, pn, pout);
   TORCH_CHECK(r == 0, "conv_dgrad_wgrad: unsupported shape");
-  return {y, dgamma, dbeta};
+  const Tensor none = at::empty({0}, x.options().dtype(at::kFloat));
+  return {y, dgm.defined() ? dgm : none, dbt.defined() ? dbt : none, (defer && sp > 1) ? slab : none};
+}
+
+// split-K reduce of a deferred grouped weight gradient: out (bf16, n) += sum of slab's splits
+void wgrad_reduce_run(const Tensor& slab, Tensor out) {
+  CHECK_DEV(slab); CHECK_DEV(out);
+  TORCH_CHECK(slab.scalar_type() == at::kFloat && out.scalar_type() == at::kBFloat16 && out.numel() % 4 == 0 &&
+                  slab.numel() % out.numel() == 0, "wgrad_reduce_run: slab (splits * n fp32), out (n bf16)");
+  DevGuard g(out.device());
+  mxr::wgrad_reduce_run(slab.data_ptr<float>(), (int)(slab.numel() / out.numel()), out.numel(),
+                        reinterpret_cast<uint16_t*>(out.data_ptr()), cur_stream());
 }
 
 // ---- pooling ---------------------------------------------------------------------------------
@@ -1460,7 +1495,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("conv_dgrad_wgrad", &conv_dgrad_wgrad, py::arg("x"), py::arg("w"), py::arg("pad"), py::arg("residual"),
         py::arg("bn"), py::arg("bn_eps"), py::arg("bn_fix_gamma"), py::arg("bnb_x"), py::arg("dadd"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("wg_dy"), py::arg("wg_x"), py::arg("KH"), py::arg("KW"), py::arg("wg_stride"),
-        py::arg("wg_pad"), py::arg("wg_out"));
+        py::arg("wg_pad"), py::arg("wg_out"), py::arg("defer") = false, py::arg("prev_slab") = py::none(),
+        py::arg("prev_out") = py::none());
+  m.def("wgrad_reduce_run", &wgrad_reduce_run, py::arg("slab"), py::arg("out"));
   m.def("head_bwd", &head_bwd, py::arg("x"), py::arg("dys"), py::arg("ws"), py::arg("dws"), py::arg("dw_acc"),
         py::arg("dbs"), py::arg("db_acc"), py::arg("need_dx"), py::arg("relu_mask"));
   m.def("chan_sum", &chan_sum, py::arg("x"), py::arg("out"), py::arg("accumulate"));

@@ -1442,21 +1442,29 @@ void conv_wt_flip_multi(const WtFlipEntry* entries, int n_entries, int total_til
 __global__ void __launch_bounds__(256)
 conv_dgrad_wgrad_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
                         int NB, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int pad,
-                        const ConvEpi ep, int tiles_n, int nwg_d, int ntiles, WgradParams wp) {
+                        const ConvEpi ep, int tiles_n, int nwg_d, int ntiles, WgradParams wp, WgradReduceParams rp) {
   static_assert(3 * (64 + 64) * BK == kWgradLdsElems, "both roles use the same 48 KB ring");
   __shared__ __attribute__((aligned(16))) uint16_t lds[3 * (64 + 64) * BK];
-  if ((int)blockIdx.x < nwg_d)
-    igemm_buf_body<64, 64, 3, false>(lds, blockIdx.x, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, 1, pad, ep, tiles_n,
+  // roles: [0, rp.nwg) the previous grouped launch's deferred split-K reduce (short, dispatched
+  // first; rp.nwg is a multiple of 8 so the dgrad role keeps its XCD-aware tile order), then the
+  // data gradient, then the weight gradient
+  const int b = (int)blockIdx.x;
+  if (b < rp.nwg) {
+    wgrad_reduce_body(b, rp.slab, rp.splits, rp.n, rp.dw, rp.accumulate);
+  } else if (b < rp.nwg + nwg_d) {
+    igemm_buf_body<64, 64, 3, false>(lds, b - rp.nwg, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, 1, pad, ep, tiles_n,
                                      nwg_d, ntiles, 1, nullptr);
-  else
-    wgrad_buf_body<3>(lds, (int)blockIdx.x - nwg_d, wp);
+  } else {
+    wgrad_buf_body<3>(lds, b - rp.nwg - nwg_d, wp);
+  }
 }
 
 int conv_dgrad_wgrad(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho, int Wo,
                      int Cout, int KH, int KW, int pad, const ConvEpi& ep, const uint16_t* wg_dy,
                      const uint16_t* wg_x, uint16_t* dw, float* slab, int wg_NB, int wg_H, int wg_W, int wg_Cin,
                      int wg_Ho, int wg_Wo, int wg_Cout, int wg_KH, int wg_KW, int wg_stride, int wg_pad, int wg_splits,
-                     int accumulate, hipStream_t st) {
+                     int accumulate, hipStream_t st, int defer_reduce, const float* prev_slab, int prev_splits,
+                     int64_t prev_n, uint16_t* prev_dw) {
   if (Cin % BK != 0 || Cout % 8 != 0 || ep.f16 || ep.omap || ep.pad_w >= 0) return -1;
   if ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB || (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kBufOOB)
     return -1;
@@ -1464,14 +1472,24 @@ int conv_dgrad_wgrad(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, 
   if ((int64_t)wg_NB * wg_Ho * wg_Wo * wg_Cout * 2 >= (int64_t)kWgOOB ||
       (int64_t)wg_NB * wg_H * wg_W * wg_Cin * 2 >= (int64_t)kWgOOB)
     return -1;
+  if (prev_slab != nullptr && (prev_splits < 2 || prev_n % 4 != 0 || prev_dw == nullptr)) return -1;
   const int M = NB * Ho * Wo;
   const int tiles_n = (Cout + 63) / 64;
   const int ntiles = ((M + 63) / 64) * tiles_n;
   const WgradParams wp = wgrad_params(wg_dy, wg_x, dw, slab, wg_NB, wg_H, wg_W, wg_Cin, wg_Ho, wg_Wo, wg_Cout, wg_KH,
                                       wg_KW, wg_stride, wg_pad, wg_splits, accumulate);
-  conv_dgrad_wgrad_kernel<<<ntiles + wp.nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, pad, ep,
-                                                            tiles_n, ntiles, ntiles, wp);
-  if (wg_splits > 1)
+  WgradReduceParams rp;
+  if (prev_slab != nullptr) {
+    rp.slab = prev_slab;
+    rp.dw = prev_dw;
+    rp.n = prev_n;
+    rp.splits = prev_splits;
+    rp.accumulate = 1;
+    rp.nwg = (int)((div_up(prev_n / 4, 256) + 7) / 8 * 8);
+  }
+  conv_dgrad_wgrad_kernel<<<rp.nwg + ntiles + wp.nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, pad, ep,
+                                                                    tiles_n, ntiles, ntiles, wp, rp);
+  if (wg_splits > 1 && !defer_reduce)
     wgrad_reduce(slab, wg_splits, (int64_t)wg_Cout * wg_KH * wg_KW * wg_Cin, dw, accumulate, st);
   return 0;
 }

@@ -144,19 +144,7 @@ __global__ void __launch_bounds__(256) conv_wgrad_buf_kernel(WgradParams p) {
 __global__ void __launch_bounds__(256)
 wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int64_t n, uint16_t* __restrict__ out,
                     int accumulate) {
-  const int64_t e = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
-  if (e >= n) return;
-  float4 a = *reinterpret_cast<const float4*>(slab + e);
-  for (int s = 1; s < splits; ++s) {
-    const float4 b = *reinterpret_cast<const float4*>(slab + (int64_t)s * n + e);
-    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-  }
-  if (accumulate) {  // add into the existing gradient (flat-buffer view), no separate add kernel
-    const ushort4 o = *reinterpret_cast<const ushort4*>(out + e);
-    a.x += bf16_to_f32(o.x); a.y += bf16_to_f32(o.y); a.z += bf16_to_f32(o.z); a.w += bf16_to_f32(o.w);
-  }
-  *reinterpret_cast<ushort4*>(out + e) = make_ushort4(f32_to_bf16(a.x), f32_to_bf16(a.y), f32_to_bf16(a.z),
-                                                      f32_to_bf16(a.w));
+  wgrad_reduce_body((int)blockIdx.x, slab, splits, n, out, accumulate);
 }
 
 WgradParams wgrad_params(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab, int NB, int H, int W,
@@ -179,6 +167,10 @@ WgradParams wgrad_params(const uint16_t* dy, const uint16_t* x, uint16_t* dw, fl
 
 void wgrad_reduce(const float* slab, int splits, int64_t n, uint16_t* dw, int accumulate, hipStream_t st) {
   wgrad_reduce_kernel<<<div_up((n + 3) / 4, 256), 256, 0, st>>>(slab, splits, n, dw, accumulate);
+}
+
+void wgrad_reduce_run(const float* slab, int splits, int64_t n, uint16_t* dw, hipStream_t st) {
+  wgrad_reduce(slab, splits, n, dw, 1, st);
 }
 
 int conv_wgrad_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int* splits_out) {

@@ -210,6 +210,33 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* __restrict__ lds, int w
   }
 }
 
+// sum of the split-K slabs (+ the existing gradient when accumulating) -> bf16; 1024 elements per
+// 256-thread workgroup `gid` (the wgrad_reduce kernel, or a role of the grouped launch)
+__device__ __forceinline__ void wgrad_reduce_body(int gid, const float* __restrict__ slab, int splits, int64_t n,
+                                                  uint16_t* __restrict__ out, int accumulate) {
+  const int64_t e = ((int64_t)gid * 256 + threadIdx.x) * 4;
+  if (e >= n) return;
+  float4 a = *reinterpret_cast<const float4*>(slab + e);
+  for (int s = 1; s < splits; ++s) {
+    const float4 b = *reinterpret_cast<const float4*>(slab + (int64_t)s * n + e);
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  if (accumulate) {  // add into the existing gradient (flat-buffer view), no separate add kernel
+    const ushort4 o = *reinterpret_cast<const ushort4*>(out + e);
+    a.x += bf16_to_f32(o.x); a.y += bf16_to_f32(o.y); a.z += bf16_to_f32(o.z); a.w += bf16_to_f32(o.w);
+  }
+  *reinterpret_cast<ushort4*>(out + e) = make_ushort4(f32_to_bf16(a.x), f32_to_bf16(a.y), f32_to_bf16(a.z),
+                                                      f32_to_bf16(a.w));
+}
+
+// a deferred split-K reduce carried into the next grouped launch (role 0 there)
+struct WgradReduceParams {
+  const float* slab = nullptr;
+  uint16_t* dw = nullptr;
+  int64_t n = 0;
+  int splits = 0, accumulate = 1, nwg = 0;
+};
+
 // host helpers (conv_wgrad.hip)
 WgradParams wgrad_params(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab, int NB, int H, int W,
                          int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int splits,

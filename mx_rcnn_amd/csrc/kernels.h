@@ -244,7 +244,10 @@ int conv_dgrad_wgrad(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, 
                      int Cout, int KH, int KW, int pad, const ConvEpi& ep, const uint16_t* wg_dy,
                      const uint16_t* wg_x, uint16_t* dw, float* slab, int wg_NB, int wg_H, int wg_W, int wg_Cin,
                      int wg_Ho, int wg_Wo, int wg_Cout, int wg_KH, int wg_KW, int wg_stride, int wg_pad, int wg_splits,
-                     int accumulate, hipStream_t st);
+                     int accumulate, hipStream_t st, int defer_reduce = 0, const float* prev_slab = nullptr,
+                     int prev_splits = 0, int64_t prev_n = 0, uint16_t* prev_dw = nullptr);
+// standalone split-K reduce of a deferred grouped weight gradient (accumulates into dw)
+void wgrad_reduce_run(const float* slab, int splits, int64_t n, uint16_t* dw, hipStream_t st);
 int conv_wgrad(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab, int NB, int H, int W, int Cin,
                int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int splits, int accumulate,
                hipStream_t st, int variant = 0);

@@ -120,11 +120,35 @@ def strided_dgrad(dy, wf, H, W, k, s, p, residual=None, bn=None, bn_eps=2e-5, bn
     return dx
 
 
+def _grouped_target(x, w, param, dy, stride, pad):
+    """The flat-gradient target when this conv's data + weight gradient can run as ONE grouped
+    launch (csrc/hip/conv_igemm.hip conv_dgrad_wgrad: stride 1, same padding, bf16), else None."""
+    if os.environ.get('MXR_GROUPED_CONV', '1') == '0' or not wgrad_enabled():
+        return None
+    kh = w.shape[2]
+    if not (stride == 1 and 2 * pad == kh - 1 and kh == w.shape[3] and x.dtype == torch.bfloat16 and
+            dy.dtype == torch.bfloat16 and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0):
+        return None
+    tgt = grad_sink.target(param)
+    if tgt is None or tgt.dtype != torch.bfloat16 or not tgt.is_contiguous(memory_format=torch.channels_last):
+        return None
+    return tgt
+
+
 def conv_backward(x, w, param, dy, stride, pad, has_bias, need_x, need_w, need_b, bparam=None):
     """(dx, dw, db) of an NHWC bf16 conv given the gradient at its (pre-activation) output.
     dw is None when it was accumulated straight into the parameter's flat gradient view."""
     kh = w.shape[2]
     dx = dw = db = None
+    tgt = _grouped_target(x, w, param, dy, stride, pad) if (need_x and need_w and x.is_cuda) else None
+    if tgt is not None:
+        x = x.contiguous(memory_format=torch.channels_last)
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        dx = need_ext().conv_dgrad_wgrad(dy, dgrad_weight(param, w), kh - 1 - pad, None, None, 0.0, False, None,
+                                         None, None, None, dy, x, kh, kh, 1, pad, tgt)[0]
+        if has_bias and need_b:
+            db = _bias_grad(dy, w, bparam)
+        return dx, None, db
     # the weight gradient runs on a side stream concurrently with the data gradient (joined before
     # returning, so readiness hooks and frees see finished writes)
     side = main = None

@@ -266,6 +266,14 @@ class _FusedUnitFn(torch.autograd.Function):
         main = torch.cuda.current_stream() if x.is_cuda else None
         side = _side_stream(x.device) if main is not None else None
         used_side = [False]
+        # split-K reduce of the last grouped weight gradient, run by the next grouped launch's first
+        # workgroups (or flushed before returning: the gradient hooks read the flat buffer)
+        pending = [None]
+
+        def flush_pending():
+            if pending[0] is not None:
+                ext.wgrad_reduce_run(*pending[0])
+                pending[0] = None
 
         def wgrad(idx, dy, inp, k, stride, pad):
             if not need[idx]:
@@ -328,8 +336,11 @@ class _FusedUnitFn(torch.autograd.Function):
                     tg = torch.zeros(C, device=dy.device, dtype=torch.float32)
                     tb = torch.zeros(C, device=dy.device, dtype=torch.float32)
                 idx, wdy, winp, wk, wstride, wpad = wg
+                prev = pending[0]
                 r = ext.conv_dgrad_wgrad(dy, wf, k - 1 - pad, dres, bnps[bn_i], spec.eps[bn_i], spec.fix[bn_i], bn_x,
-                                         dadd, tg, tb, wdy, winp, wk, wk, wstride, wpad, tgt)
+                                         dadd, tg, tb, wdy, winp, wk, wk, wstride, wpad, tgt, True,
+                                         prev[0] if prev else None, prev[1] if prev else None)
+                pending[0] = (r[3], tgt) if r[3].numel() > 0 else None
             else:
                 if wg is not None:
                     wgrad(*wg)
@@ -393,6 +404,7 @@ class _FusedUnitFn(torch.autograd.Function):
             wgrad(*wg0)
             if not spec.dim_match:
                 wgrad(nconv - 1, d_out, act1, 1, s, 0)
+            flush_pending()
             if used_side[0]:
                 main.wait_stream(side)
             return (None, None, None) + tuple(grads)
@@ -420,6 +432,7 @@ class _FusedUnitFn(torch.autograd.Function):
             if d_sc is not None:
                 d_act1 = d_act1 + d_sc
             d_x = bn_bwd_plain(_cl(d_act1), 0, x, dres)
+        flush_pending()
         if used_side[0]:
             main.wait_stream(side)
         return (None, d_x if ctx.needs_input_grad[1] else None, None) + tuple(grads)

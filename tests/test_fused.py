@@ -293,7 +293,8 @@ def test_strided_dgrad_bnb_epilogue(cuda):
 @pytest.mark.gpu
 @pytest.mark.parametrize('geo', [(256, 1024, 1, 24, 40, 1024, 256, 1, 1, 0), (256, 256, 3, 20, 30, 256, 256, 3, 1, 1),
                                  (1024, 256, 1, 50, 84, 256, 1024, 1, 1, 0), (256, 256, 3, 50, 84, 256, 512, 1, 1, 0)])
-def test_grouped_dgrad_wgrad_matches_separate(cuda, geo):
+@pytest.mark.parametrize('with_bn,defer', [(True, False), (False, False), (True, True)])
+def test_grouped_dgrad_wgrad_matches_separate(cuda, geo, with_bn, defer):
     """conv_dgrad_wgrad (one launch: BN-backward dgrad role + split-K wgrad role) against the same
     two computations as separate launches (buffer kernel tile 23, conv_wgrad): same bodies, so the
     data gradient and the weight gradient agree to rounding; dgamma / dbeta to atomic order."""
@@ -316,16 +317,28 @@ def test_grouped_dgrad_wgrad_matches_separate(cuda, geo):
     p = k // 2
     tg, tb = torch.zeros(Cin, device=cuda), torch.zeros(Cin, device=cuda)
     dw = dw0.clone()
-    dx, dgm, dbt = ext.conv_dgrad_wgrad(dy, wt, k - 1 - p, dres, bn, 2e-5, False, xr, None, tg, tb, wdy, wx, wk, wk, ws,
-                                        wp, dw)
-    rdx, rdg, rdb = ext.conv_igemm_fwd(dy, wt, None, 1, k - 1 - p, False, 23, 1, dres, bn, 2e-5, False, True, xr, None)
+    if with_bn:
+        dx, dgm, dbt, slab = ext.conv_dgrad_wgrad(dy, wt, k - 1 - p, dres, bn, 2e-5, False, xr, None, tg, tb, wdy, wx,
+                                                  wk, wk, ws, wp, dw, defer)
+        rdx, rdg, rdb = ext.conv_igemm_fwd(dy, wt, None, 1, k - 1 - p, False, 23, 1, dres, bn, 2e-5, False, True, xr,
+                                           None)
+    else:
+        dx, _, _, slab = ext.conv_dgrad_wgrad(dy, wt, k - 1 - p, dres, None, 0.0, False, None, None, None, None, wdy,
+                                              wx, wk, wk, ws, wp, dw, defer)
+        rdx = ext.conv_igemm_fwd(dy, wt, None, 1, k - 1 - p, False, 23, 1, dres)[0]
+    if defer and slab.numel() > 0:
+        # the deferred reduce runs as role 0 of the next grouped launch: a second (throw-away) one
+        dw2 = dw0.clone()
+        ext.conv_dgrad_wgrad(dy, wt, k - 1 - p, None, None, 0.0, False, None, None, None, None, wdy, wx, wk, wk, ws,
+                             wp, dw2, False, slab, dw)
     rdw = dw0.clone()
     ext.conv_wgrad(wdy, wx, wk, wk, ws, wp, 0, rdw)
     torch.cuda.synchronize()
     assert torch.equal(dx, rdx)
     assert torch.allclose(dw.float(), rdw.float(), rtol=1e-2, atol=1e-2 * rdw.float().abs().max().item())
-    for a, r in ((dgm, rdg), (dbt, rdb)):
-        assert torch.allclose(a, r, rtol=1e-4, atol=1e-4 * r.abs().max().item() + 1e-5)
+    if with_bn:
+        for a, r in ((dgm, rdg), (dbt, rdb)):
+            assert torch.allclose(a, r, rtol=1e-4, atol=1e-4 * r.abs().max().item() + 1e-5)
 
 
 @pytest.mark.gpu

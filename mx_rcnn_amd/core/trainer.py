@@ -90,7 +90,10 @@ class Trainer:
         if self.model.nonfinite_counter is None:
             self.nonfinite.add_((~torch.isfinite(out['objective'])).to(torch.int32))
         with prof.range('backward+allreduce'):
-            out['loss'].backward()
+            from ..ops.fused import defer_reduces
+            # no gradient hook reads the flat buffers mid-backward: split-K reduces may cross units
+            with defer_reduces(not (self.reducer.overlap or self.reducer.sgd_capable)):
+                out['loss'].backward()
         with prof.range('allreduce_wait'):
             self.reducer.finish()
         with prof.range('sgd'):

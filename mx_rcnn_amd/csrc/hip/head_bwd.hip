@@ -245,12 +245,14 @@ head_bwd_fold_kernel(int K, HeadBwdArgs a, int h) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
   if (e < nw) {
     float s = 0.f;
+#pragma unroll 8
     for (int r = 0; r < a.rs; ++r) s += a.ws_dw[h][(int64_t)r * nw + e];
     if (a.dw_acc[h]) s += bf16_to_f32(a.dw[h][e]);
     a.dw[h][e] = f32_to_bf16(s);
   } else if (e < nw + Nh && a.db[h] != nullptr) {
     const int n = (int)(e - nw);
     float s = 0.f;
+#pragma unroll 8
     for (int r = 0; r < a.rs; ++r) s += a.ws_db[h][(int64_t)r * Nh + n];
     if (a.db_acc[h]) s += ld(a.db[h], n, a.db_code[h]);
     st(a.db[h], n, s, a.db_code[h]);
@@ -311,15 +313,26 @@ chan_sum_part_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int rows,
   }
 }
 
+// one workgroup per 64 channels, 4 threads per channel over interleaved chunks (loads in flight
+// instead of one thread walking ~100 dependent L2 loads)
 __global__ void __launch_bounds__(256)
 chan_sum_fold_kernel(const float* __restrict__ part, int nchunks, int C, void* __restrict__ out, int out_code,
                      int accumulate) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= C) return;
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float s = 0.f;
-  for (int i = 0; i < nchunks; ++i) s += part[(int64_t)i * C + c];
-  if (accumulate) s += ld(out, c, out_code);
-  st(out, c, s, out_code);
+  if (c < C) {
+#pragma unroll 8
+    for (int i = q; i < nchunks; i += 4) s += part[(int64_t)i * C + c];
+  }
+  red[q][cl] = s;
+  __syncthreads();
+  if (q == 0 && c < C) {
+    float t = red[0][cl] + red[1][cl] + red[2][cl] + red[3][cl];
+    if (accumulate) t += ld(out, c, out_code);
+    st(out, c, t, out_code);
+  }
 }
 
 int chan_sum_chunks(int64_t M, int C) {
@@ -334,7 +347,7 @@ int chan_sum(const uint16_t* x, int64_t M, int C, int code, float* part, void* o
   const int nchunks = chan_sum_chunks(M, C);
   const int rows = (int)((M + nchunks - 1) / nchunks);
   chan_sum_part_kernel<<<dim3(div_up(C, 64), nchunks), 256, 0, st>>>(x, M, C, rows, code, part);
-  chan_sum_fold_kernel<<<div_up(C, 256), 256, 0, st>>>(part, nchunks, C, out, out_code, accumulate);
+  chan_sum_fold_kernel<<<div_up(C, 64), 256, 0, st>>>(part, nchunks, C, out, out_code, accumulate);
   return 0;
 }
 

@@ -217,6 +217,7 @@ __device__ __forceinline__ void wgrad_reduce_body(int gid, const float* __restri
   const int64_t e = ((int64_t)gid * 256 + threadIdx.x) * 4;
   if (e >= n) return;
   float4 a = *reinterpret_cast<const float4*>(slab + e);
+#pragma unroll 4
   for (int s = 1; s < splits; ++s) {
     const float4 b = *reinterpret_cast<const float4*>(slab + (int64_t)s * n + e);
     a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;

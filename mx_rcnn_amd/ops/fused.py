@@ -150,6 +150,34 @@ def _cl(t):
 _SIDE = {}
 
 
+# Cross-unit deferral of the last grouped weight-gradient reduce of each unit into the NEXT unit's
+# first grouped launch.  Only inside ``defer_reduces()`` (the trainer's backward when no gradient
+# hook reads the flat buffers mid-backward, i.e. no overlapped all-reduce / optimizer), which
+# flushes whatever is still pending on exit.
+_XUNIT = {'on': False, 'pending': None}
+
+
+class defer_reduces(object):
+    def __init__(self, enabled=True):
+        self.enabled = enabled
+
+    def __enter__(self):
+        _XUNIT['on'] = bool(self.enabled)
+        return self
+
+    def __exit__(self, *a):
+        _XUNIT['on'] = False
+        flush_deferred()
+        return False
+
+
+def flush_deferred():
+    p = _XUNIT['pending']
+    if p is not None:
+        need_ext().wgrad_reduce_run(*p)
+        _XUNIT['pending'] = None
+
+
 def grouped_enabled():
     """One launch per conv for data + weight gradient in the fused units (MXR_GROUPED_BWD=0: the
     weight gradient on the side stream instead)."""
@@ -268,11 +296,15 @@ class _FusedUnitFn(torch.autograd.Function):
         used_side = [False]
         # split-K reduce of the last grouped weight gradient, run by the next grouped launch's first
         # workgroups (or flushed before returning: the gradient hooks read the flat buffer)
-        pending = [None]
+        pending = [_XUNIT['pending']]  # a previous unit's deferred reduce, if any
+        _XUNIT['pending'] = None
 
         def flush_pending():
             if pending[0] is not None:
-                ext.wgrad_reduce_run(*pending[0])
+                if _XUNIT['on']:  # hand it to the next unit's first grouped launch
+                    _XUNIT['pending'] = pending[0]
+                else:
+                    ext.wgrad_reduce_run(*pending[0])
                 pending[0] = None
 
         def wgrad(idx, dy, inp, k, stride, pad):

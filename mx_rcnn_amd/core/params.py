@@ -157,8 +157,26 @@ class FlatParamStore:
     def refresh_dgrad_cache(self):
         if self._wt_table is not None:
             from ..ops._ext import need_ext
+            from ..ops.conv import refresh_sub_filters
             table, n_ent, tiles, _ = self._wt_table
             need_ext().wt_flip_run(table, n_ent, tiles)
+            refresh_sub_filters()
+
+    def refresh_dgrad_cache_async(self):
+        """Rebuild the dgrad cache from the current weights on a side stream (concurrent with the
+        forward pass, which does not read it); returns a callable that joins it into the compute
+        stream (call before the backward pass)."""
+        if self._wt_table is None or self.device.type != 'cuda':
+            self.refresh_dgrad_cache()
+            return lambda: None
+        main = torch.cuda.current_stream(self.device)
+        if getattr(self, '_cache_stream', None) is None:
+            self._cache_stream = torch.cuda.Stream(device=self.device)
+        side = self._cache_stream
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            self.refresh_dgrad_cache()
+        return lambda: main.wait_stream(side)
 
     @staticmethod
     def _flat_view(t, cl):
@@ -204,13 +222,16 @@ class FlatParamStore:
     def grad_buffers(self):
         return [g.grad for g in self.groups]
 
-    def sgd_step(self, lr, momentum=0.9, wd=0.0005, rescale=1.0, clip=-1.0, grad_for=None):
+    def sgd_step(self, lr, momentum=0.9, wd=0.0005, rescale=1.0, clip=-1.0, grad_for=None, refresh=True):
         """``lr``: 1-element fp32 device tensor.  ``grad_for(group)`` picks the gradient source
-        (the reducer's fp32 all-reduce buffer under data parallelism; default ``group.grad``)."""
+        (the reducer's fp32 all-reduce buffer under data parallelism; default ``group.grad``).
+        ``refresh=False``: the caller rebuilds the dgrad cache itself (Trainer.step_body does, at
+        the start of the next step, concurrently with its forward pass)."""
         for g in self.groups:
             grad = grad_for(g) if grad_for is not None else g.grad
             sgd_momentum_(g.master, g.mom, grad, lr, momentum, wd if g.decay else 0.0, rescale, clip, g.shadow)
-        self.refresh_dgrad_cache()
+        if refresh:
+            self.refresh_dgrad_cache()
 
     def master_param(self, name):
         for g in self.groups:

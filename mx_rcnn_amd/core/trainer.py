@@ -78,6 +78,8 @@ class Trainer:
 
     def step_body(self, b):
         """The device work of one step (capturable)."""
+        # the dgrad filter cache of the current weights, built beside the forward pass
+        cache_join = self.store.refresh_dgrad_cache_async()
         self.store.zero_grad()
         # the optimizer runs bucket by bucket under the backward pass (parallel/reducer.py)
         self.reducer.prepare(sgd=(self.lr_t, self.momentum, self.wd, self.rescale, self.clip))
@@ -89,6 +91,7 @@ class Trainer:
         # counted by the model's loss-combine kernel unless fault injection is armed
         if self.model.nonfinite_counter is None:
             self.nonfinite.add_((~torch.isfinite(out['objective'])).to(torch.int32))
+        cache_join()
         with prof.range('backward+allreduce'):
             from ..ops.fused import defer_reduces
             # no gradient hook reads the flat buffers mid-backward: split-K reduces may cross units
@@ -97,11 +100,9 @@ class Trainer:
         with prof.range('allreduce_wait'):
             self.reducer.finish()
         with prof.range('sgd'):
-            if self.reducer.sgd_applied:
-                self.store.refresh_dgrad_cache()
-            else:
+            if not self.reducer.sgd_applied:
                 self.store.sgd_step(self.lr_t, self.momentum, self.wd, self.rescale, self.clip,
-                                    grad_for=self.reducer.grad_for)
+                                    grad_for=self.reducer.grad_for, refresh=False)
         # Return detached outputs: a caller holding the loss would otherwise keep this step's
         # autograd graph (and its AccumulateGrad nodes, bound to this step's stream) alive, and a
         # later hipGraph capture on a side stream then syncs against that stream and dies in

@@ -250,6 +250,16 @@ Tensor roi_pool_bwd(const Tensor& grad_out, const Tensor& argmax, const Tensor& 
   TORCH_CHECK(argmax.is_contiguous(at::MemoryFormat::ChannelsLast), "argmax must be channels_last");
   DevGuard g(grad_out.device());
   auto st = cur_stream();
+  static const bool lds_path = [] {
+    const char* e = std::getenv("MXR_ROIPOOL_BWD_LDS");
+    return e == nullptr || e[0] != '0';
+  }();
+  if (lds_path) {
+    Tensor gin = at::empty({B, C, H, W}, grad_out.options().memory_format(at::MemoryFormat::ChannelsLast));
+    if (mxr::roi_pool_bwd_lds(go.data_ptr(), dcode(go), argmax.data_ptr<int32_t>(), rois.contiguous().data_ptr<float>(),
+                              R, PH, PW, (int)B, (int)H, (int)W, C, gin.data_ptr(), st) == 0)
+      return gin;
+  }
   // NOTE: at::zeros ignores a memory_format carried in TensorOptions (returns NCHW); allocate
   // the NHWC buffer explicitly and view it as logical NCHW.
   Tensor gin32 = at::zeros({B, H, W, C}, grad_out.options().dtype(at::kFloat)).permute({0, 3, 1, 2});

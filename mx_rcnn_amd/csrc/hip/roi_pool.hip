@@ -154,6 +154,82 @@ void roi_pool_fwd(const void* feat, int bf16, int B, int H, int W, int C, const 
   }
 }
 
+// Atomic-free (in global memory) backward: one workgroup per (image, CW-channel slab) accumulates
+// the whole H x W x CW gradient slab in LDS (fp32, LDS float atomics), walking every bin of the
+// image's RoIs once (argmax + dY: 16 + 8 B per bin for CW = 4), then writes its channels of every
+// pixel in the output dtype.  Replaces: a zero fill of an fp32 (B, H, W, C) buffer, 6.4 M global
+// fp32 atomics (~120 us at 128 RoIs x 49 bins x 1024 ch) and the cast to bf16.
+template <int CW, typename T>
+__global__ void __launch_bounds__(256)
+roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ argmax, const float* __restrict__ rois,
+                        int R, int PHW, int HW, int C, int code, T* __restrict__ gin) {
+  extern __shared__ float acc[];  // [HW][CW]
+  const int c0 = blockIdx.x * CW, b = blockIdx.y;
+  for (int i = threadIdx.x; i < HW * CW; i += blockDim.x) acc[i] = 0.f;
+  __syncthreads();
+  const int nb = R * PHW;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+    const int r = i / PHW;
+    if ((int)rois[(int64_t)r * 5] != b) continue;
+    const int64_t base = (int64_t)i * C + c0;
+    int a[CW];
+    float g[CW];
+#pragma unroll
+    for (int k = 0; k < CW; ++k) {
+      a[k] = argmax[base + k];
+      g[k] = to_f(gout[base + k], code);
+    }
+#pragma unroll
+    for (int k = 0; k < CW; ++k)
+      if (a[k] >= 0 && a[k] < HW && g[k] != 0.f) atomicAdd(&acc[a[k] * CW + k], g[k]);
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < HW; p += blockDim.x) {
+    T* o = gin + ((int64_t)b * HW + p) * C + c0;
+#pragma unroll
+    for (int k = 0; k < CW; ++k) {
+      if constexpr (sizeof(T) == 2) o[k] = f32_to_h16(acc[p * CW + k], code);
+      else o[k] = acc[p * CW + k];
+    }
+  }
+}
+
+constexpr int kRoiBwdLds = 150 * 1024;
+
+int roi_pool_bwd_lds(const void* grad_out, int code, const int32_t* argmax, const float* rois, int R, int PH, int PW,
+                     int B, int H, int W, int C, void* grad_in, hipStream_t st) {
+  const int HW = H * W;
+  int cw = 0;
+  if (C % 4 == 0 && (int64_t)HW * 4 * 4 <= kRoiBwdLds) cw = 4;
+  else if (C % 2 == 0 && (int64_t)HW * 2 * 4 <= kRoiBwdLds) cw = 2;
+  else if ((int64_t)HW * 4 <= kRoiBwdLds) cw = 1;
+  if (cw == 0 || B <= 0) return -1;
+  const size_t lds = (size_t)HW * cw * 4;
+  const dim3 grid(C / cw, B);
+#define MXR_ROI_BWD(CW_, T_)                                                                                   \
+  do {                                                                                                        \
+    static bool attr = false;                                                                                 \
+    if (!attr) {                                                                                              \
+      (void)hipFuncSetAttribute((const void*)roi_pool_bwd_lds_kernel<CW_, T_>,                                \
+                                hipFuncAttributeMaxDynamicSharedMemorySize, kRoiBwdLds);                      \
+      attr = true;                                                                                            \
+    }                                                                                                         \
+    roi_pool_bwd_lds_kernel<CW_, T_><<<grid, 256, lds, st>>>((const T_*)grad_out, argmax, rois, R, PH * PW, HW, C, \
+                                                             code, (T_*)grad_in);                            \
+  } while (0)
+  if (code) {
+    if (cw == 4) MXR_ROI_BWD(4, uint16_t);
+    else if (cw == 2) MXR_ROI_BWD(2, uint16_t);
+    else MXR_ROI_BWD(1, uint16_t);
+  } else {
+    if (cw == 4) MXR_ROI_BWD(4, float);
+    else if (cw == 2) MXR_ROI_BWD(2, float);
+    else MXR_ROI_BWD(1, float);
+  }
+#undef MXR_ROI_BWD
+  return 0;
+}
+
 void roi_pool_bwd(const void* grad_out, int bf16, const int32_t* argmax, const float* rois, int R, int PH, int PW,
                   int B, int H, int W, int C, float* grad_in, hipStream_t st) {
   const int64_t total = (int64_t)R * PH * PW * C;

@@ -18,7 +18,14 @@ def _load():
         return _EXT
     try:
         import torch  # noqa: F401  (loads libc10_hip / libamdhip64 first)
-        _EXT = importlib.import_module('mx_rcnn_amd._C')
+        path = os.environ.get('MXR_EXT_PATH')  # A/B of two builds on one box (scripts/gpu_ab_prof.sh)
+        if path:
+            import importlib.util
+            spec = importlib.util.spec_from_file_location('mx_rcnn_amd._C', path)
+            _EXT = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(_EXT)
+        else:
+            _EXT = importlib.import_module('mx_rcnn_amd._C')
     except ImportError as e:  # pragma: no cover - depends on build state
         _ERR = e
     return _EXT

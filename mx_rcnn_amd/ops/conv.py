@@ -42,6 +42,35 @@ def register_dgrad_weight(param, buf):
     _DGRAD_W[id(param)] = (param, buf)
 
 
+# parity sub-filters of the cached flipped filters (strided dgrad): (id(param), taps) -> (param,
+# source view builder, buffer); rebuilt with the cache (FlatParamStore.refresh_dgrad_cache)
+_SUBW = {}
+
+
+def sub_filter(param, wf, th, tw, s):
+    """The (I, O, |th|, |tw|) channels_last slice of the flipped filter ``wf`` at taps th[0]::s /
+    tw[0]::s; cached per parameter and refreshed with the dgrad cache, so the strided data
+    gradient does not copy sub-filters on the critical path."""
+    def view(w):
+        return w[:, :, th[0]:th[-1] + 1:s, tw[0]:tw[-1] + 1:s]
+    if param is None or cached_dgrad_weight(param) is not wf:
+        return view(wf).contiguous(memory_format=torch.channels_last)
+    key = (id(param), th[0], th[-1], tw[0], tw[-1], s)
+    ent = _SUBW.get(key)
+    if ent is None or ent[0] is not param:
+        buf = view(wf).contiguous(memory_format=torch.channels_last)
+        _SUBW[key] = (param, view, buf)
+        return buf
+    return ent[2]
+
+
+def refresh_sub_filters():
+    for param, view, buf in list(_SUBW.values()):
+        wf = cached_dgrad_weight(param)
+        if wf is not None:
+            buf.copy_(view(wf))
+
+
 def cached_dgrad_weight(param):
     """The cached flipped / transposed filter of ``param`` or None."""
     ent = _DGRAD_W.get(id(param)) if param is not None else None
@@ -84,7 +113,7 @@ def strided_dgrad_ok(k, s, p, H, W):
 
 
 def strided_dgrad(dy, wf, H, W, k, s, p, residual=None, bn=None, bn_eps=2e-5, bn_fix_gamma=False, bnb_x=None,
-                  dadd=None, dgamma=None, dbeta=None):
+                  dadd=None, dgamma=None, dbeta=None, param=None):
     """Data gradient of a stride-``s`` k x k conv (pad p) on the MFMA kernel, by parity
     decomposition: input rows / columns of parity (ph, pw) receive only the filter taps of matching
     parity, so each of the s*s classes is a small stride-1 conv of dy with a sub-filter, written
@@ -112,7 +141,7 @@ def strided_dgrad(dy, wf, H, W, k, s, p, residual=None, bn=None, bn_eps=2e-5, bn
             tw, ow = _parity_taps(k, s, p, pw)
             # the taps of one parity are an arithmetic progression of step s: plain slicing (an index
             # list would be a host-to-device copy, illegal inside graph capture)
-            sub = wf[:, :, th[0]:th[-1] + 1:s, tw[0]:tw[-1] + 1:s].contiguous(memory_format=torch.channels_last)
+            sub = sub_filter(param, wf, th, tw, s)
             ext.conv_igemm_fwd(dy, sub, None, 1, -oh, False, 0, 0, residual, bn, bn_eps, bn_fix_gamma, True,
                                bnb_x, dadd, dgamma, dbeta, 0.0, 0, None, -ow, dx, [Hc, Wc, H, W, s, s, ph, pw])
     if bwd:
@@ -166,7 +195,7 @@ def conv_backward(x, w, param, dy, stride, pad, has_bias, need_x, need_w, need_b
             dx = need_ext().conv_igemm_fwd(dy, dgrad_weight(param, w), None, 1, kh - 1 - pad, False)[0]
         elif (stride > 1 and w.shape[0] % 64 == 0 and w.shape[1] % 8 == 0 and kh == w.shape[3] and
               strided_dgrad_ok(kh, stride, pad, x.shape[2], x.shape[3])):
-            dx = strided_dgrad(dy, dgrad_weight(param, w), x.shape[2], x.shape[3], kh, stride, pad)
+            dx = strided_dgrad(dy, dgrad_weight(param, w), x.shape[2], x.shape[3], kh, stride, pad, param=param)
         else:
             dx = torch.ops.aten.convolution_backward(
                 dy, x, w, None, [stride] * 2, [pad] * 2, [1, 1], False, [0, 0], 1, [True, False, False])[0]

@@ -391,7 +391,7 @@ class _FusedUnitFn(torch.autograd.Function):
                 tb = torch.zeros(C, device=dy.device, dtype=torch.float32)
             r = strided_dgrad(dy, dgrad_weight(ctx.params[w_idx], ws[w_idx]), H, W, k, stride, pad, residual=dres,
                               bn=bnps[bn_i], bn_eps=spec.eps[bn_i], bn_fix_gamma=spec.fix[bn_i], bnb_x=bn_x,
-                              dadd=dadd, dgamma=tg, dbeta=tb)
+                              dadd=dadd, dgamma=tg, dbeta=tb, param=ctx.params[w_idx])
             finish_bn(bn_i, tg, tb, ret)
             return r[0]
 

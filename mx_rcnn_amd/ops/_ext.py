@@ -6,6 +6,7 @@ GPU box); a CPU tensor runs the PyTorch reference implementation, which is also 
 numerics oracle in tests.
 """
 import importlib
+import importlib.util
 import os
 
 _EXT = None
@@ -20,7 +21,6 @@ def _load():
         import torch  # noqa: F401  (loads libc10_hip / libamdhip64 first)
         path = os.environ.get('MXR_EXT_PATH')  # A/B of two builds on one box (scripts/gpu_ab_prof.sh)
         if path:
-            import importlib.util
             spec = importlib.util.spec_from_file_location('mx_rcnn_amd._C', path)
             _EXT = importlib.util.module_from_spec(spec)
             spec.loader.exec_module(_EXT)

@@ -721,7 +721,7 @@ __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t rs, void* lds_w
 // elements, the block's ONLY LDS (the grouped data + weight gradient launch below shares it with
 // the wgrad role)
 template <int BM, int BN, int S, bool F16 = false>
-__device__ __forceinline__ void igemm_buf_body(uint16_t* __restrict__ lds, int bid, const uint16_t* __restrict__ x,
+__device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uint16_t* __restrict__ x,
                                                const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int NB, int H,
                                                int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride,
                                                int pad, const ConvEpi& ep, int tiles_n, int nwg, int ntiles, int splits,

@@ -69,7 +69,7 @@ constexpr int kWgradLdsElems = 3 * 2 * WG_BK * 64;  // the S = 3 ring: [S][dY|X]
 
 // workgroup `wgid` of the launch; `lds`: S * 2 * 64 * 64 bf16 (16-B aligned)
 template <int S>
-__device__ __forceinline__ void wgrad_buf_body(uint16_t* __restrict__ lds, int wgid, const WgradParams& p) {
+__device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const WgradParams& p) {
   constexpr int LPS = 4;  // DMA instructions per thread per stage (2 dY rows + 2 X rows)
   static_assert(S >= 2 && S <= 4, "pipeline depth");
   const uint16_t* __restrict__ dy = p.dy;
@@ -148,23 +148,52 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* __restrict__ lds, int w
     if (st + S - 1 < nsteps) issue(st + S - 1, (st + S - 1) % S);
     const uint16_t* Ab = lds + (st % S) * 2 * WG_BK * 64;
     const uint16_t* Bb = Ab + WG_BK * 64;
+    // all 16 transposed fragment reads of the step in ONE asm block: through the builtin, the
+    // compiler cannot tell the ring slot being read from the slots the in-flight LDS-DMA loads
+    // fill, and drained EVERY load (s_waitcnt vmcnt(0)) before the reads -- no pipelining at
+    // all; the counted vmcnt wait above is the real dependency
+    uint32_t ad[16];
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          ad[kk * 8 + i * 2 + h] = (uint32_t)reinterpret_cast<uintptr_t>(
+              Ab + lidx(krow(kk, g, h) + q, wm * 32 + i * 16 + pcol));
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          ad[kk * 8 + 4 + j * 2 + h] = (uint32_t)reinterpret_cast<uintptr_t>(
+              Bb + lidx(krow(kk, g, h) + q, wn * 32 + j * 16 + pcol));
+      }
+    s16x4 fr[16];
+    asm volatile(
+        "ds_read_b64_tr_b16 %0, %16\n\tds_read_b64_tr_b16 %1, %17\n\t"
+        "ds_read_b64_tr_b16 %2, %18\n\tds_read_b64_tr_b16 %3, %19\n\t"
+        "ds_read_b64_tr_b16 %4, %20\n\tds_read_b64_tr_b16 %5, %21\n\t"
+        "ds_read_b64_tr_b16 %6, %22\n\tds_read_b64_tr_b16 %7, %23\n\t"
+        "ds_read_b64_tr_b16 %8, %24\n\tds_read_b64_tr_b16 %9, %25\n\t"
+        "ds_read_b64_tr_b16 %10, %26\n\tds_read_b64_tr_b16 %11, %27\n\t"
+        "ds_read_b64_tr_b16 %12, %28\n\tds_read_b64_tr_b16 %13, %29\n\t"
+        "ds_read_b64_tr_b16 %14, %30\n\tds_read_b64_tr_b16 %15, %31\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=&v"(fr[0]), "=&v"(fr[1]), "=&v"(fr[2]), "=&v"(fr[3]), "=&v"(fr[4]), "=&v"(fr[5]), "=&v"(fr[6]),
+          "=&v"(fr[7]), "=&v"(fr[8]), "=&v"(fr[9]), "=&v"(fr[10]), "=&v"(fr[11]), "=&v"(fr[12]), "=&v"(fr[13]),
+          "=&v"(fr[14]), "=&v"(fr[15])
+        : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]), "v"(ad[5]), "v"(ad[6]), "v"(ad[7]),
+          "v"(ad[8]), "v"(ad[9]), "v"(ad[10]), "v"(ad[11]), "v"(ad[12]), "v"(ad[13]), "v"(ad[14]), "v"(ad[15])
+        : "memory");
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       bf16x8 af[2], bfr[2];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int col = wm * 32 + i * 16 + pcol;
-        const s16x4 lo = tr_read(Ab + lidx(krow(kk, g, 0) + q, col));
-        const s16x4 hi = tr_read(Ab + lidx(krow(kk, g, 1) + q, col));
-        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-      }
+      for (int i = 0; i < 2; ++i)
+        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(fr[kk * 8 + i * 2], fr[kk * 8 + i * 2 + 1], 0, 1, 2,
+                                                                   3, 4, 5, 6, 7));
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int col = wn * 32 + j * 16 + pcol;
-        const s16x4 lo = tr_read(Bb + lidx(krow(kk, g, 0) + q, col));
-        const s16x4 hi = tr_read(Bb + lidx(krow(kk, g, 1) + q, col));
-        bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-      }
+      for (int j = 0; j < 2; ++j)
+        bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(fr[kk * 8 + 4 + j * 2],
+                                                                    fr[kk * 8 + 4 + j * 2 + 1], 0, 1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll

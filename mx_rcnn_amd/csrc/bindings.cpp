@@ -367,7 +367,8 @@ std::vector<Tensor> smooth_l1(const Tensor& pred, const Tensor& tgt, const Tenso
 
 // x *= s[0] in place
 Tensor scale_by_scalar_(Tensor x, const Tensor& s) {
-  CHECK_DEV(x); CHECK_CONTIG(x); CHECK_DEV(s); CHECK_F32(s);
+  CHECK_DEV(x); CHECK_DEV(s); CHECK_F32(s);
+  TORCH_CHECK(x.is_contiguous() || x.is_contiguous(at::MemoryFormat::ChannelsLast), "x must be dense");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kFloat, "bf16 / fp32 only");
   TORCH_CHECK(s.numel() == 1, "scalar expected");
   DevGuard g(x.device());

@@ -1439,12 +1439,14 @@ void conv_wt_flip_multi(const WtFlipEntry* entries, int n_entries, int total_til
 // Replaces the two-stream schedule (wgrad on a side stream, one cross-queue wait per wgrad and a
 // join per unit): every cross-queue edge of a replayed graph cost ~10 us of idle time, four per
 // unit (profiles/r2_resnet101_stage3_unit_timeline.txt).
+template <int S>
 __global__ void __launch_bounds__(256)
 conv_dgrad_wgrad_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
                         int NB, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int pad,
                         const ConvEpi ep, int tiles_n, int nwg_d, int ntiles, WgradParams wp, WgradReduceParams rp) {
-  static_assert(3 * (64 + 64) * BK == kWgradLdsElems, "both roles use the same 48 KB ring");
-  __shared__ __attribute__((aligned(16))) uint16_t lds[3 * (64 + 64) * BK];
+  // both roles run an S-deep ring over the same LDS: S * (64 + 64) * 64 bf16 (48 KB at S = 3)
+  static_assert(S * (64 + 64) * BK == S * 2 * WG_BK * 64, "both roles use the same ring");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[S * (64 + 64) * BK];
   // roles: [0, rp.nwg) the previous grouped launch's deferred split-K reduce (short, dispatched
   // first; rp.nwg is a multiple of 8 so the dgrad role keeps its XCD-aware tile order), then the
   // data gradient, then the weight gradient
@@ -1452,10 +1454,10 @@ conv_dgrad_wgrad_kernel(const uint16_t* __restrict__ x, const uint16_t* __restri
   if (b < rp.nwg) {
     wgrad_reduce_body(b, rp.slab, rp.splits, rp.n, rp.dw, rp.accumulate);
   } else if (b < rp.nwg + nwg_d) {
-    igemm_buf_body<64, 64, 3, false>(lds, b - rp.nwg, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, 1, pad, ep, tiles_n,
+    igemm_buf_body<64, 64, S, false>(lds, b - rp.nwg, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, 1, pad, ep, tiles_n,
                                      nwg_d, ntiles, 1, nullptr);
   } else {
-    wgrad_buf_body<3>(lds, b - rp.nwg - nwg_d, wp);
+    wgrad_buf_body<S>(lds, b - rp.nwg - nwg_d, wp);
   }
 }
 
@@ -1487,8 +1489,16 @@ int conv_dgrad_wgrad(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, 
     rp.accumulate = 1;
     rp.nwg = (int)((div_up(prev_n / 4, 256) + 7) / 8 * 8);
   }
-  conv_dgrad_wgrad_kernel<<<rp.nwg + ntiles + wp.nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, pad, ep,
-                                                                    tiles_n, ntiles, ntiles, wp, rp);
+  static const int depth = [] {  // A/B knob MXR_GROUPED_S: ring depth of both roles (3: 48 KB, 4: 64 KB)
+    const char* e = getenv("MXR_GROUPED_S");
+    return e != nullptr && e[0] == '4' ? 4 : 3;
+  }();
+  if (depth == 4)
+    conv_dgrad_wgrad_kernel<4><<<rp.nwg + ntiles + wp.nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW,
+                                                                         pad, ep, tiles_n, ntiles, ntiles, wp, rp);
+  else
+    conv_dgrad_wgrad_kernel<3><<<rp.nwg + ntiles + wp.nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW,
+                                                                         pad, ep, tiles_n, ntiles, ntiles, wp, rp);
   if (wg_splits > 1 && !defer_reduce)
     wgrad_reduce(slab, wg_splits, (int64_t)wg_Cout * wg_KH * wg_KW * wg_Cin, dw, accumulate, st);
   return 0;

@@ -55,7 +55,8 @@ class _RpnCE(torch.autograd.Function):
 
 def _scale_grad(grad, g):
     """The stored loss gradient times the incoming scalar (in place on the GPU: one kernel)."""
-    if grad.is_cuda and grad.is_contiguous() and g.dtype == torch.float32:
+    if (grad.is_cuda and g.dtype == torch.float32 and
+            (grad.is_contiguous() or grad.is_contiguous(memory_format=torch.channels_last))):
         return need_ext().scale_by_scalar_(grad, g.reshape(1))
     return grad * g.to(grad.dtype)
 

@@ -521,7 +521,8 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
                                    c10::optional<Tensor> dadd, c10::optional<Tensor> dgamma_out,
                                    c10::optional<Tensor> dbeta_out, double drop_p, int64_t drop_seed,
                                    c10::optional<Tensor> drop_step, int64_t pad_w, c10::optional<Tensor> out,
-                                   c10::optional<std::vector<int64_t>> out_map) {
+                                   c10::optional<std::vector<int64_t>> out_map, c10::optional<Tensor> stat_shift,
+                                   c10::optional<Tensor> bnb_part, int64_t bnb_row0) {
   CHECK_DEV(x); CHECK_DEV(w);
   TORCH_CHECK((x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf) && w.scalar_type() == x.scalar_type(),
               "conv_igemm: bf16 or fp16 activations and weights of the same dtype");
@@ -618,7 +619,16 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
                       dadd->is_contiguous(at::MemoryFormat::ChannelsLast), "dadd must be channels_last bf16 like y");
       ep.dadd = reinterpret_cast<const uint16_t*>(dadd->data_ptr());
     }
-    if (dgamma_out.has_value() && dgamma_out->defined()) {
+    const bool det = bnb_part.has_value() && bnb_part->defined();
+    if (det) {
+      // deterministic column sums: 64-row tiles (tile 23) write rows bnb_row0 .. + ceil(M / 64)
+      const int64_t rows = ((int64_t)NB * Ho * Wo + 63) / 64;
+      TORCH_CHECK(bnb_part->scalar_type() == at::kFloat && bnb_part->is_contiguous() && Cout % 8 == 0 &&
+                      bnb_part->numel() >= (bnb_row0 + rows) * 2 * Cout && bnb_row0 >= 0,
+                  "bnb_part: contiguous fp32 with (bnb_row0 + ceil(M / 64)) * 2 * Cout elements");
+      ep.bnb_part = bnb_part->data_ptr<float>();
+      ep.bnb_row0 = (int)bnb_row0;
+    } else if (dgamma_out.has_value() && dgamma_out->defined()) {
       dgm = *dgamma_out;
       dbt = *dbeta_out;
       TORCH_CHECK(dgm.scalar_type() == at::kFloat && dbt.scalar_type() == at::kFloat && dgm.is_contiguous() &&
@@ -628,26 +638,49 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
       dgm = at::zeros({Cout}, x.options().dtype(at::kFloat));
       dbt = at::zeros({Cout}, x.options().dtype(at::kFloat));
     }
-    ep.bnb_dgamma = dgm.data_ptr<float>();
-    ep.bnb_dbeta = dbt.data_ptr<float>();
+    if (!det) {
+      ep.bnb_dgamma = dgm.data_ptr<float>();
+      ep.bnb_dbeta = dbt.data_ptr<float>();
+    }
   } else if (bn.has_value()) {
     y2 = at::empty_like(y, y.options(), at::MemoryFormat::ChannelsLast);
     ep.y2 = reinterpret_cast<uint16_t*>(y2.data_ptr());
   }
+  // training-BN statistics of y in the epilogue (ConvEpi::st_part): partial rows for the smallest
+  // row tile any candidate uses (32), the used tile's rows are returned as a view
+  const bool stats = stat_shift.has_value() && stat_shift->defined();
+  Tensor part;
+  if (stats) {
+    TORCH_CHECK(!bwd_mode && !bn.has_value() && !mapped && Cout % 8 == 0, "stat_shift: plain forward epilogue only");
+    TORCH_CHECK(stat_shift->scalar_type() == at::kFloat && stat_shift->is_contiguous() && stat_shift->numel() == Cout,
+                "stat_shift: fp32 (Cout,)");
+    const int64_t Mr = (int64_t)NB * Ho * Wo;
+    part = at::empty({((Mr + 31) / 32) * 2 + 1, Cout}, x.options().dtype(at::kFloat));
+    ep.st_part = part.data_ptr<float>();
+    ep.st_shift = stat_shift->data_ptr<float>();
+  }
   int auto_splits = 1;
   int t = mxr::conv_igemm_plan(NB, Ho, Wo, Cin, Cout, KH, KW, (int)tile, &auto_splits);
   // BN-backward epilogue: no split-K by default (the statistics are reduced in-tile instead)
-  int sp = splits > 0 ? (int)splits : (bwd_mode ? 1 : auto_splits);
+  int sp = splits > 0 ? (int)splits : ((bwd_mode || stats) ? 1 : auto_splits);
+  if (stats) {
+    TORCH_CHECK(sp == 1, "stat_shift: no split-K");
+    if (!(t == 21 || t == 22 || t == 23 || t >= 100)) t = 23;
+  }
+  if (ep.bnb_part) {  // the caller sized the partial rows for 64-row tiles
+    t = 23;
+    sp = 1;
+  }
   if (f16 && !(t == 21 || t == 22 || t == 23 || t >= 100)) t = 23;  // fp16 MFMA: buffer / ring kernels
   if (mapped || ep.pad_w >= 0) {  // geometry extensions: buffer / ring kernels, no split-K
     if (!(t == 22 || t == 23 || t >= 100)) t = 23;
     sp = 1;
   }
-  if (tile <= 0 && splits <= 0 && !mapped && ep.pad_w < 0 && conv_tune_enabled()) {
+  if (tile <= 0 && splits <= 0 && !mapped && ep.pad_w < 0 && !ep.bnb_part && conv_tune_enabled()) {
     char kb[256];
     snprintf(kb, sizeof(kb), "%d,%d,%d,%d,%d,%d,%d,%d,%d|%d%d%d%d%d%d%d", NB, H, W, Cin, Cout, KH, KW, (int)stride,
              (int)pad, ep.residual != nullptr, ep.y2 != nullptr || bn.has_value(), bwd_mode, ep.dadd != nullptr,
-             ep.relu, ep.bias != nullptr || ep.bias_h != nullptr, ep.drop_p > 0.f);
+             ep.relu, ep.bias != nullptr || ep.bias_h != nullptr, (ep.drop_p > 0.f ? 1 : 0) + (stats ? 2 : 0));
     const std::string key(kb);
     std::unique_lock<std::mutex> lk(g_tune_mu);
     auto it = g_tune.find(key);
@@ -662,7 +695,7 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
       // grids far below one tile per CU (the FC head: M = 128 RoIs, K up to 25088): split K
       const int64_t Mrows = (int64_t)NB * Ho * Wo;
       const int nkk = KH * KW * (Cin / 64);
-      if (!bwd_mode && Cout % 4 == 0 && ((Mrows + 63) / 64) * ((Cout + 63) / 64) < 128) {
+      if (!bwd_mode && !stats && Cout % 4 == 0 && ((Mrows + 63) / 64) * ((Cout + 63) / 64) < 128) {
         for (int c : {23, 22, 106, 109})
           for (int spl : {2, 4, 8})
             if (nkk / spl >= 4 && !(c == t && spl == sp)) cands.push_back({c, spl});
@@ -732,6 +765,13 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
                                        (int)stride, (int)pad, ep, t, sp, sp > 1 ? slab.data_ptr<float>() : nullptr,
                                        cur_stream());
   TORCH_CHECK(used > 0, "conv_igemm: unsupported shape");
+  if (stats) {
+    const int bm = mxr::conv_tile_bm(used);
+    TORCH_CHECK(bm >= 32, "stat_shift: unexpected tile");
+    const int64_t nparts = ((int64_t)NB * Ho * Wo + bm - 1) / bm;
+    return {y, part.narrow(0, 0, nparts * 2 + 1)};
+  }
+  if (bwd_mode && ep.bnb_part) return {y};
   if (bwd_mode) return {y, dgm, dbt};
   if (y2.defined()) return {y, y2};
   return {y};
@@ -750,7 +790,7 @@ std::vector<Tensor> conv_dgrad_wgrad(const Tensor& x, const Tensor& w, int64_t p
                                      c10::optional<Tensor> dgamma, c10::optional<Tensor> dbeta, const Tensor& wg_dy,
                                      const Tensor& wg_x, int64_t KH, int64_t KW, int64_t wg_stride, int64_t wg_pad,
                                      Tensor wg_out, bool defer, c10::optional<Tensor> prev_slab,
-                                     c10::optional<Tensor> prev_out) {
+                                     c10::optional<Tensor> prev_out, c10::optional<Tensor> bnb_part) {
   CHECK_DEV(x); CHECK_DEV(w); CHECK_DEV(wg_dy); CHECK_DEV(wg_x); CHECK_DEV(wg_out);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast) && w.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -790,14 +830,21 @@ std::vector<Tensor> conv_dgrad_wgrad(const Tensor& x, const Tensor& w, int64_t p
                       dadd->is_contiguous(at::MemoryFormat::ChannelsLast), "dadd like y");
       ep.dadd = reinterpret_cast<const uint16_t*>(dadd->data_ptr());
     }
-    TORCH_CHECK(dgamma.has_value() && dbeta.has_value() && dgamma->scalar_type() == at::kFloat &&
-                    dbeta->scalar_type() == at::kFloat && dgamma->is_contiguous() && dbeta->is_contiguous() &&
-                    dgamma->numel() == Cout && dbeta->numel() == Cout,
-                "dgamma / dbeta: contiguous fp32 (C,)");
-    dgm = *dgamma;
-    dbt = *dbeta;
-    ep.bnb_dgamma = dgm.data_ptr<float>();
-    ep.bnb_dbeta = dbt.data_ptr<float>();
+    if (bnb_part.has_value() && bnb_part->defined()) {  // deterministic sums, 64-row dgrad tiles
+      TORCH_CHECK(bnb_part->scalar_type() == at::kFloat && bnb_part->is_contiguous() &&
+                      bnb_part->numel() >= (((int64_t)NB * Ho * Wo + 63) / 64) * 2 * Cout,
+                  "bnb_part: contiguous fp32 with ceil(M / 64) * 2 * Cout elements");
+      ep.bnb_part = bnb_part->data_ptr<float>();
+    } else {
+      TORCH_CHECK(dgamma.has_value() && dbeta.has_value() && dgamma->scalar_type() == at::kFloat &&
+                      dbeta->scalar_type() == at::kFloat && dgamma->is_contiguous() && dbeta->is_contiguous() &&
+                      dgamma->numel() == Cout && dbeta->numel() == Cout,
+                  "dgamma / dbeta: contiguous fp32 (C,)");
+      dgm = *dgamma;
+      dbt = *dbeta;
+      ep.bnb_dgamma = dgm.data_ptr<float>();
+      ep.bnb_dbeta = dbt.data_ptr<float>();
+    }
   }
   // weight-gradient role
   TORCH_CHECK(wg_dy.scalar_type() == at::kBFloat16 && wg_x.scalar_type() == at::kBFloat16 &&
@@ -1085,15 +1132,80 @@ std::vector<Tensor> bn_train_fwd(const Tensor& x, const Tensor& gamma, const Ten
   DevGuard g(x.device());
   Tensor gf = gamma.to(at::kFloat).contiguous(), bf = beta.to(at::kFloat).contiguous();
   Tensor y = at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast);
-  Tensor sm = at::empty({C}, x.options().dtype(at::kFloat)), si = at::empty({C}, x.options().dtype(at::kFloat));
+  // save rows: mean, invstd, var + eps
+  Tensor save = at::empty({3, C}, x.options().dtype(at::kFloat));
+  float* sv = save.data_ptr<float>();
   Tensor ws = at::empty({mxr::bn_train_workspace_floats(x.numel() / C, C)}, x.options().dtype(at::kFloat));
   const int r = mxr::bn_train_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), x.numel() / C, C,
                                   gf.data_ptr<float>(), bf.data_ptr<float>(), rmean.data_ptr<float>(),
                                   rvar.data_ptr<float>(), (float)momentum, (float)eps, fix_gamma ? 1 : 0, relu ? 1 : 0,
-                                  reinterpret_cast<uint16_t*>(y.data_ptr()), sm.data_ptr<float>(), si.data_ptr<float>(),
-                                  ws.data_ptr<float>(), cur_stream());
+                                  reinterpret_cast<uint16_t*>(y.data_ptr()), sv, sv + C, ws.data_ptr<float>(),
+                                  cur_stream(), sv + 2 * C);
   TORCH_CHECK(r == 0, "bn_train_fwd: unsupported shape");
-  return {y, sm, si};
+  return {y, save};
+}
+
+// normalisation from conv-epilogue statistics partials (conv_igemm_fwd(..., stat_shift=rmean)[1])
+std::vector<Tensor> bn_train_apply(const Tensor& x, const Tensor& part, const Tensor& gamma, const Tensor& beta,
+                                   Tensor rmean, Tensor rvar, double momentum, double eps, bool fix_gamma, bool relu) {
+  CHECK_DEV(x); CHECK_DEV(part);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "x: bf16 NHWC");
+  const int C = (int)x.size(1);
+  TORCH_CHECK(C % 64 == 0, "bn_train needs C % 64 == 0");
+  CHECK_F32(rmean); CHECK_F32(rvar); CHECK_CONTIG(rmean); CHECK_CONTIG(rvar);
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 2 && part.size(1) == C &&
+                  part.size(0) % 2 == 1 && part.size(0) >= 3, "part: fp32 (2 * nparts + 1, C)");
+  DevGuard g(x.device());
+  Tensor gf = gamma.to(at::kFloat).contiguous(), bf = beta.to(at::kFloat).contiguous();
+  Tensor y = at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast);
+  Tensor save = at::empty({3, C}, x.options().dtype(at::kFloat));
+  const int r = mxr::bn_train_apply(reinterpret_cast<const uint16_t*>(x.data_ptr()), x.numel() / C, C,
+                                    part.data_ptr<float>(), (int)((part.size(0) - 1) / 2), gf.data_ptr<float>(),
+                                    bf.data_ptr<float>(), rmean.data_ptr<float>(), rvar.data_ptr<float>(),
+                                    (float)momentum, (float)eps, fix_gamma ? 1 : 0, relu ? 1 : 0,
+                                    reinterpret_cast<uint16_t*>(y.data_ptr()), save.data_ptr<float>(), cur_stream());
+  TORCH_CHECK(r == 0, "bn_train_apply: unsupported shape");
+  return {y, save};
+}
+
+// finish of a training-BN backward whose BN-backward epilogue (a dgrad conv with bnb_x = x,
+// bn = (gamma_eff, beta, save[0], save[2]), eps 0, bnb_part = part) produced o; nparts partial rows
+Tensor bn_train_dx_apply(Tensor o, const Tensor& x, const Tensor& save, const Tensor& gamma_eff, const Tensor& part,
+                         int64_t nparts, c10::optional<Tensor> dres, c10::optional<Tensor> dgamma,
+                         c10::optional<Tensor> dbeta) {
+  CHECK_DEV(o); CHECK_DEV(x); CHECK_DEV(part);
+  const int C = (int)x.size(1);
+  TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  o.scalar_type() == at::kBFloat16 && o.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  o.sizes() == x.sizes(), "o / x: bf16 NHWC of one shape");
+  TORCH_CHECK(save.scalar_type() == at::kFloat && save.is_contiguous() && save.numel() == 3 * C, "save: fp32 (3, C)");
+  TORCH_CHECK(gamma_eff.scalar_type() == at::kFloat && gamma_eff.is_contiguous() && gamma_eff.numel() == C,
+              "gamma_eff: fp32 (C,)");
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && nparts > 0 &&
+                  part.numel() >= nparts * 2 * C, "part: fp32 with nparts * 2 * C elements");
+  const uint16_t* rp = nullptr;
+  if (dres.has_value() && dres->defined()) {
+    TORCH_CHECK(dres->scalar_type() == at::kBFloat16 && dres->is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                    dres->sizes() == x.sizes(), "dres: bf16 NHWC like x");
+    rp = reinterpret_cast<const uint16_t*>(dres->data_ptr());
+  }
+  float* dg = nullptr;
+  float* db = nullptr;
+  for (auto* p : {&dgamma, &dbeta}) {
+    if (p->has_value() && (*p)->defined())
+      TORCH_CHECK((*p)->scalar_type() == at::kFloat && (*p)->is_contiguous() && (*p)->numel() == C,
+                  "dgamma / dbeta: fp32 (C,)");
+  }
+  if (dgamma.has_value() && dgamma->defined()) dg = dgamma->data_ptr<float>();
+  if (dbeta.has_value() && dbeta->defined()) db = dbeta->data_ptr<float>();
+  DevGuard g(x.device());
+  const int r = mxr::bn_train_dx_apply(reinterpret_cast<const uint16_t*>(o.data_ptr()),
+                                       reinterpret_cast<const uint16_t*>(x.data_ptr()), x.numel() / C, C,
+                                       part.data_ptr<float>(), (int)nparts, gamma_eff.data_ptr<float>(),
+                                       save.data_ptr<float>(), rp, reinterpret_cast<uint16_t*>(o.data_ptr()), dg, db,
+                                       cur_stream());
+  TORCH_CHECK(r == 0, "bn_train_dx_apply: unsupported shape");
+  return o;
 }
 
 std::vector<Tensor> bn_train_bwd(const Tensor& x, const Tensor& dy, const Tensor& gamma, const Tensor& beta,
@@ -1501,13 +1613,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("act_relu") = true, py::arg("bnb_x") = py::none(), py::arg("dadd") = py::none(),
         py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(), py::arg("drop_p") = 0.0,
         py::arg("drop_seed") = 0, py::arg("drop_step") = py::none(), py::arg("pad_w") = -1,
-        py::arg("out") = py::none(), py::arg("out_map") = py::none());
+        py::arg("out") = py::none(), py::arg("out_map") = py::none(), py::arg("stat_shift") = py::none(),
+        py::arg("bnb_part") = py::none(), py::arg("bnb_row0") = 0);
   m.def("proposal_topk", &proposal_topk, py::arg("keys"), py::arg("boxes"), py::arg("P"));
   m.def("conv_dgrad_wgrad", &conv_dgrad_wgrad, py::arg("x"), py::arg("w"), py::arg("pad"), py::arg("residual"),
         py::arg("bn"), py::arg("bn_eps"), py::arg("bn_fix_gamma"), py::arg("bnb_x"), py::arg("dadd"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("wg_dy"), py::arg("wg_x"), py::arg("KH"), py::arg("KW"), py::arg("wg_stride"),
         py::arg("wg_pad"), py::arg("wg_out"), py::arg("defer") = false, py::arg("prev_slab") = py::none(),
-        py::arg("prev_out") = py::none());
+        py::arg("prev_out") = py::none(), py::arg("bnb_part") = py::none());
   m.def("wgrad_reduce_run", &wgrad_reduce_run, py::arg("slab"), py::arg("out"));
   m.def("head_bwd", &head_bwd, py::arg("x"), py::arg("dys"), py::arg("ws"), py::arg("dws"), py::arg("dw_acc"),
         py::arg("dbs"), py::arg("db_acc"), py::arg("need_dx"), py::arg("relu_mask"));
@@ -1523,6 +1636,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("philox_uniform", &philox_uniform_cpu, py::arg("seed"), py::arg("step"), py::arg("n"),
         "host twin of the fused-dropout generator: uniforms of elements 0..n-1 (CPU float tensor)");
   m.def("bn_train_fwd", &bn_train_fwd);
+  m.def("bn_train_apply", &bn_train_apply);
+  m.def("bn_train_dx_apply", &bn_train_dx_apply, py::arg("o"), py::arg("x"), py::arg("save"), py::arg("gamma_eff"),
+        py::arg("part"), py::arg("nparts"), py::arg("dres") = py::none(), py::arg("dgamma") = py::none(),
+        py::arg("dbeta") = py::none());
   m.def("bn_train_bwd", &bn_train_bwd, py::arg("x"), py::arg("dy"), py::arg("gamma"), py::arg("beta"),
         py::arg("save_mean"), py::arg("save_invstd"), py::arg("fix_gamma"), py::arg("relu"), py::arg("need_dx"),
         py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none());

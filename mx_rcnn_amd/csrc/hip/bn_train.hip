@@ -151,7 +151,8 @@ __global__ void __launch_bounds__(256)
 bn_train_norm_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int rows, int nchunks, const float* __restrict__ part,
                      const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ rmean,
                      float* __restrict__ rvar, float momentum, float eps, int fix_gamma, int relu,
-                     uint16_t* __restrict__ y, float* __restrict__ save_mean, float* __restrict__ save_invstd) {
+                     uint16_t* __restrict__ y, float* __restrict__ save_mean, float* __restrict__ save_invstd,
+                     float* __restrict__ save_veps) {
   __shared__ float scale_sh[64], shift_sh[64], red4[512], fa[64], fb[64];
   const int tid = threadIdx.x;
   fold_partials(part, nchunks, C, red4, fa, fb);
@@ -169,6 +170,8 @@ bn_train_norm_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int rows,
     if (blockIdx.y == 0) {
       save_mean[c] = mu;
       save_invstd[c] = inv;
+      // var + eps: a BN-backward conv epilogue given (mean, veps, eps = 0) recomputes exactly inv
+      if (save_veps) save_veps[c] = var + eps;
       // running statistics (MXNet cuDNN path: unbiased batch variance); no block reads rmean
       const float unb = M > 1 ? var * (float)M / (float)(M - 1) : var;
       rmean[c] = momentum * rmean[c] + (1.f - momentum) * mu;
@@ -297,14 +300,78 @@ int bn_train_workspace_floats(int64_t M, int C) {
 
 int bn_train_fwd(const uint16_t* x, int64_t M, int C, const float* gamma, const float* beta, float* rmean,
                  float* rvar, float momentum, float eps, int fix_gamma, int relu, uint16_t* y, float* save_mean,
-                 float* save_invstd, float* workspace, hipStream_t st) {
+                 float* save_invstd, float* workspace, hipStream_t st, float* save_veps) {
   if (C % BT_C != 0 || M <= 0) return -1;
   const int rows = bn_train_rows(M, C);
   const int nchunks = (int)((M + rows - 1) / rows);
   const dim3 grid(C / BT_C, nchunks);
   bn_train_stats_kernel<<<grid, 256, 0, st>>>(x, M, C, rows, rmean, workspace);
   bn_train_norm_kernel<<<grid, 256, 0, st>>>(x, M, C, rows, nchunks, workspace, gamma, beta, rmean, rvar, momentum, eps,
-                                             fix_gamma, relu, y, save_mean, save_invstd);
+                                             fix_gamma, relu, y, save_mean, save_invstd, save_veps);
+  return 0;
+}
+
+int bn_train_apply(const uint16_t* x, int64_t M, int C, const float* part, int nparts, const float* gamma,
+                   const float* beta, float* rmean, float* rvar, float momentum, float eps, int fix_gamma, int relu,
+                   uint16_t* y, float* save, hipStream_t st) {
+  if (C % BT_C != 0 || M <= 0 || nparts <= 0) return -1;
+  const int rows = bn_train_rows(M, C);
+  const dim3 grid(C / BT_C, (int)((M + rows - 1) / rows));
+  bn_train_norm_kernel<<<grid, 256, 0, st>>>(x, M, C, rows, nparts, part, gamma, beta, rmean, rvar, momentum, eps,
+                                             fix_gamma, relu, y, save, save + C, save + 2 * C);
+  return 0;
+}
+
+// dx = s * (g - mean(g) - xhat * mean(g * xhat)) (+ dres), from o = g * s written by a BN-backward
+// conv epilogue that left per-row-tile partial rows [nparts][sum g | sum g * xhat][C] (ConvEpi::
+// bnb_part; folded here in a fixed order, so the step is deterministic).  o and dx may alias
+// (each element is read then written by the same thread).
+__global__ void __launch_bounds__(256)
+bn_train_dx_apply_kernel(const uint16_t* o, const uint16_t* __restrict__ x, int64_t M, int C, int rows,
+                         const float* __restrict__ part, int nparts, const float* __restrict__ gamma,
+                         const float* __restrict__ save, const uint16_t* __restrict__ dres, uint16_t* dx,
+                         float* __restrict__ dgamma, float* __restrict__ dbeta) {
+  __shared__ float red4[512], fa[64], fb[64];
+  const int tid = threadIdx.x, cg = tid & 7, rl = tid >> 3;
+  fold_partials(part, nparts, C, red4, fa, fb);
+  if (blockIdx.y == 0 && tid < 64) {
+    const int c = blockIdx.x * BT_C + tid;
+    if (dbeta) dbeta[c] += fa[tid];
+    if (dgamma) dgamma[c] += fb[tid];
+  }
+  const int c0 = blockIdx.x * BT_C + cg * 8;
+  const float invM = 1.f / (float)M;
+  float a[8], b[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float mu = save[c0 + k], inv = save[C + c0 + k];
+    const float s = gamma[c0 + k] * inv;
+    // dx = o - s * mg - s * mgx * (x - mu) * inv = o - a - b * x
+    const float mg = fa[cg * 8 + k] * invM, mgx = fb[cg * 8 + k] * invM;
+    b[k] = s * mgx * inv;
+    a[k] = s * mg - b[k] * mu;
+  }
+  const int64_t r0 = (int64_t)blockIdx.y * rows;
+  const int64_t r1 = r0 + rows < M ? r0 + rows : M;
+#pragma unroll 4
+  for (int64_t r = r0 + rl; r < r1; r += BT_LANES) {
+    float v[8], d[8], rr[8];
+    ld8(x + r * C + c0, v);
+    ld8(o + r * C + c0, d);
+    if (dres) ld8(dres + r * C + c0, rr);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) d[k] = d[k] - a[k] - b[k] * v[k] + (dres ? rr[k] : 0.f);
+    st8(dx + r * C + c0, d);
+  }
+}
+
+int bn_train_dx_apply(const uint16_t* o, const uint16_t* x, int64_t M, int C, const float* part, int nparts,
+                      const float* gamma, const float* save, const uint16_t* dres, uint16_t* dx, float* dgamma,
+                      float* dbeta, hipStream_t st) {
+  if (C % BT_C != 0 || M <= 0 || nparts <= 0) return -1;
+  const int rows = bn_train_rows(M, C);
+  const dim3 grid(C / BT_C, (int)((M + rows - 1) / rows));
+  bn_train_dx_apply_kernel<<<grid, 256, 0, st>>>(o, x, M, C, rows, part, nparts, gamma, save, dres, dx, dgamma, dbeta);
   return 0;
 }
 

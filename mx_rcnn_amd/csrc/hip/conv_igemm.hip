@@ -130,6 +130,79 @@ __device__ __forceinline__ void epi_bnb(const ConvEpi& ep, const EpiCol& c, uint
   y[idx] = f32_to_h16c(EPC, o);
 }
 
+// Per-column statistics of an LDS-transposed epilogue (thread = 8 consecutive columns cv*8.. of
+// some rows): sum over the lanes of each wave sharing the column group (shuffles), then over the
+// NW waves through T ([NW][BN][2] floats; the caller has finished reading T), one value per
+// column and stat.  With `atomic` the two sums are added to out_a / out_b (fp32 atomics), else
+// written to out_a[col] / out_b[col] (a per-row-tile partial row).
+template <int BN, int NT>
+__device__ __forceinline__ void epi_col_stats(float (&sa)[8], float (&sb)[8], float* __restrict__ T, int tid, int n0,
+                                              int Cout, float* out_a, float* out_b, bool atomic, bool skip_b) {
+  constexpr int VPR = BN / 8;
+  constexpr int NW = NT / 64;
+  const int lane = tid & 63, wid = tid >> 6, cv = tid % VPR;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+#pragma unroll
+    for (int o = VPR; o < 64; o <<= 1) {
+      sa[k] += __shfl_xor(sa[k], o, 64);
+      sb[k] += __shfl_xor(sb[k], o, 64);
+    }
+  }
+  __syncthreads();  // T is reused as [NW waves][BN][2] partials
+  if (lane < VPR) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      T[(wid * BN + cv * 8 + k) * 2] = sa[k];
+      T[(wid * BN + cv * 8 + k) * 2 + 1] = sb[k];
+    }
+  }
+  __syncthreads();
+  for (int c = tid; c < BN; c += NT) {
+    const int col = n0 + c;
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      a += T[(q * BN + c) * 2];
+      b += T[(q * BN + c) * 2 + 1];
+    }
+    if (col < Cout) {
+      if (atomic) {
+        if (out_a) atomicAdd(out_a + col, a);
+        if (out_b && !skip_b) atomicAdd(out_b + col, b);
+      } else {
+        out_a[col] = a;
+        out_b[col] = b;
+      }
+    }
+  }
+}
+
+// BN-backward column sums sum(g) / sum(g * xhat): fp32 atomics into dbeta / dgamma, or (bnb_part,
+// deterministic) this row tile's partial row bnb_row0 + m0 / BM of [rows][2][Cout]
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void epi_bnb_sums(float (&sg)[8], float (&sgx)[8], float* __restrict__ T, int tid, int m0,
+                                             int n0, int Cout, const ConvEpi& ep) {
+  if (ep.bnb_part) {
+    float* row = ep.bnb_part + (int64_t)(ep.bnb_row0 + m0 / BM) * 2 * Cout;
+    epi_col_stats<BN, NT>(sg, sgx, T, tid, n0, Cout, row, row + Cout, false, false);
+  } else {
+    epi_col_stats<BN, NT>(sg, sgx, T, tid, n0, Cout, ep.bnb_dbeta, ep.bnb_dgamma, true, ep.bn_fix_gamma);
+  }
+}
+
+// training-BN statistics epilogue (ConvEpi::st_part): this row tile's partial row, and the shift row
+template <int BM, int BN, int NT>
+__device__ __forceinline__ void epi_bn_stats(float (&s1)[8], float (&s2)[8], float* __restrict__ T, int tid, int m0,
+                                             int n0, int M, int Cout, const ConvEpi& ep) {
+  const int tm = m0 / BM, tiles_m = (M + BM - 1) / BM;
+  float* row = ep.st_part + (int64_t)tm * 2 * Cout;
+  epi_col_stats<BN, NT>(s1, s2, T, tid, n0, Cout, row, row + Cout, false, false);
+  if (tm == 0)
+    for (int c = tid; c < BN; c += NT)
+      if (n0 + c < Cout) ep.st_part[(int64_t)tiles_m * 2 * Cout + n0 + c] = ep.st_shift[n0 + c];
+}
+
 // Shared epilogue of the implicit-GEMM kernels: C/D map col = lane & 15, row = (lane >> 4) * 4 + r.
 template <int TM, int TN, int WM, int WN>
 __device__ __forceinline__ void igemm_epilogue(f32x4 (&acc)[TM][TN], int m0, int n0, int wm, int wn, int lane, int M,
@@ -268,39 +341,14 @@ __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* 
       }
       st8_h16(y + e, o, EPC);
     }
-    // reduce over the lanes of this wave that share the column group, then over the waves
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-#pragma unroll
-      for (int o = VPR; o < 64; o <<= 1) {
-        sg[k] += __shfl_xor(sg[k], o, 64);
-        sgx[k] += __shfl_xor(sgx[k], o, 64);
-      }
-    }
-    __syncthreads();  // T is reused as [4 waves][BN][2] partials
-    const int wid = tid >> 6;
-    if (lane < VPR) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        T[(wid * BN + cv * 8 + k) * 2] = sg[k];
-        T[(wid * BN + cv * 8 + k) * 2 + 1] = sgx[k];
-      }
-    }
-    __syncthreads();
-    if (tid < BN) {
-      const int col = n0 + tid;
-      float a = 0.f, b = 0.f;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        a += T[(q * BN + tid) * 2];
-        b += T[(q * BN + tid) * 2 + 1];
-      }
-      if (col < Cout) {
-        if (ep.bnb_dbeta) atomicAdd(ep.bnb_dbeta + col, a);
-        if (ep.bnb_dgamma && !ep.bn_fix_gamma) atomicAdd(ep.bnb_dgamma + col, b);
-      }
-    }
+    epi_bnb_sums<BM, BN, 256>(sg, sgx, T, tid, m0, n0, Cout, ep);
     return;
+  }
+  float s1[8], s2[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    s1[k] = s2[k] = 0.f;
+    sh[k] = (ep.st_part && ncol) ? ep.st_shift[n + k] : 0.f;
   }
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
@@ -320,15 +368,20 @@ __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* 
       if (ep.relu) t = fmaxf(t, 0.f);
       t = epi_dropout(ep, e + k, t);
       yb[k] = f32_to_h16c(EPC, t);
-      float q = h16_to_f32c(EPC, yb[k]) * ec[k].s + ec[k].t;  // the BN reads the STORED conv output
+      const float ys = h16_to_f32c(EPC, yb[k]);  // the BN reads the STORED conv output
+      float q = ys * ec[k].s + ec[k].t;
       if (ep.act_relu) q = fmaxf(q, 0.f);
       y2v[k] = q;
+      const float d = ys - sh[k];
+      s1[k] += d;
+      s2[k] += d * d;
     }
     *reinterpret_cast<uint4*>(y + e) =
         make_uint4((uint32_t)yb[0] | ((uint32_t)yb[1] << 16), (uint32_t)yb[2] | ((uint32_t)yb[3] << 16),
                    (uint32_t)yb[4] | ((uint32_t)yb[5] << 16), (uint32_t)yb[6] | ((uint32_t)yb[7] << 16));
     if (ep.y2) st8_h16(ep.y2 + e, y2v, EPC);
   }
+  if (ep.st_part) epi_bn_stats<BM, BN, 256>(s1, s2, T, tid, m0, n0, M, Cout, ep);
 }
 
 template <int BM, int BN>
@@ -971,38 +1024,14 @@ __device__ __forceinline__ void ring_epilogue(f32x4 (&acc)[TM][TN], float* __res
       }
       st8_h16(y + e, o, EPC);
     }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-#pragma unroll
-      for (int o = VPR; o < 64; o <<= 1) {
-        sg[k] += __shfl_xor(sg[k], o, 64);
-        sgx[k] += __shfl_xor(sgx[k], o, 64);
-      }
-    }
-    __syncthreads();  // T is reused as [NW waves][BN][2] partials
-    const int wid = tid >> 6;
-    if (lane < VPR) {
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        T[(wid * BN + cv * 8 + k) * 2] = sg[k];
-        T[(wid * BN + cv * 8 + k) * 2 + 1] = sgx[k];
-      }
-    }
-    __syncthreads();
-    for (int c = tid; c < BN; c += NT) {
-      const int col = n0 + c;
-      float a = 0.f, b = 0.f;
-#pragma unroll
-      for (int q = 0; q < NW; ++q) {
-        a += T[(q * BN + c) * 2];
-        b += T[(q * BN + c) * 2 + 1];
-      }
-      if (col < Cout) {
-        if (ep.bnb_dbeta) atomicAdd(ep.bnb_dbeta + col, a);
-        if (ep.bnb_dgamma && !ep.bn_fix_gamma) atomicAdd(ep.bnb_dgamma + col, b);
-      }
-    }
+    epi_bnb_sums<BM, BN, NT>(sg, sgx, T, tid, m0, n0, Cout, ep);
     return;
+  }
+  float s1[8], s2[8], sh[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    s1[k] = s2[k] = 0.f;
+    sh[k] = (ep.st_part && ncol) ? ep.st_shift[n + k] : 0.f;
   }
   for (int q = tid; q < NVEC; q += NT) {
     const int row = q / VPR, m = m0 + row;
@@ -1021,15 +1050,20 @@ __device__ __forceinline__ void ring_epilogue(f32x4 (&acc)[TM][TN], float* __res
       if (ep.relu) t = fmaxf(t, 0.f);
       t = epi_dropout(ep, e + k, t);
       yb[k] = f32_to_h16c(EPC, t);
-      float qv = h16_to_f32c(EPC, yb[k]) * ec[k].s + ec[k].t;
+      const float ys = h16_to_f32c(EPC, yb[k]);
+      float qv = ys * ec[k].s + ec[k].t;
       if (ep.act_relu) qv = fmaxf(qv, 0.f);
       y2v[k] = qv;
+      const float d = ys - sh[k];
+      s1[k] += d;
+      s2[k] += d * d;
     }
     *reinterpret_cast<uint4*>(y + e) =
         make_uint4((uint32_t)yb[0] | ((uint32_t)yb[1] << 16), (uint32_t)yb[2] | ((uint32_t)yb[3] << 16),
                    (uint32_t)yb[4] | ((uint32_t)yb[5] << 16), (uint32_t)yb[6] | ((uint32_t)yb[7] << 16));
     if (ep.y2) st8_h16(ep.y2 + e, y2v, EPC);
   }
+  if (ep.st_part) epi_bn_stats<BM, BN, NT>(s1, s2, T, tid, m0, n0, M, Cout, ep);
 }
 
 template <int TM, int TN, int WGM, int WGN, int SFIX, bool ONE, bool F16 = false>
@@ -1303,6 +1337,15 @@ static void launch_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB
 
 float philox_uniform_host(uint32_t seed, uint64_t step, uint64_t e) { return philox_uniform(seed, step, e); }
 
+int conv_tile_bm(int tile) {
+  if (tile >= 100 && tile < 100 + kNumRing) return kRingShapes[tile - 100].bm;
+  switch (tile) {
+    case 1: case 2: case 11: case 12: case 14: case 15: case 21: case 22: case 31: case 32: return 128;
+    case 24: return 32;
+    default: return 64;
+  }
+}
+
 int conv_igemm_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int tile, int* splits_out) {
   const int64_t M = (int64_t)NB * Ho * Wo;
   const int nk = KH * KW * (Cin / BK);
@@ -1347,6 +1390,9 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
   if (ep.y2 && ep.bnb_x) return -1;
   if ((ep.omap || ep.pad_w >= 0) && (splits > 1 || !(tile == 22 || tile == 23 || tile >= 100))) return -1;
   if (ep.f16 && !(tile == 21 || tile == 22 || tile == 23 || tile >= 100)) return -1;
+  // BN statistics: LDS-epilogue kernels (buffer / ring), whole K per workgroup
+  if (ep.st_part && (splits > 1 || Cout % 8 != 0 || !(tile == 21 || tile == 22 || tile == 23 || tile >= 100)))
+    return -1;
   // buffer variants: 32-bit byte offsets below the kBufOOB sentinel, tap mask of 64 bits
   if (tile >= 100 && ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB ||
                       (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kBufOOB || KH * KW > 64))
@@ -1354,6 +1400,8 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
   if (tile >= 21 && ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB ||
                      (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kBufOOB || KH * KW > 64))
     tile = 3;
+  if ((ep.st_part || ep.bnb_part) && tile < 21) return -1;  // needs the buffer / ring epilogue
+  if (ep.bnb_part && (splits > 1 || Cout % 8 != 0)) return -1;
   if (tile >= 100 && tile < 100 + kNumRing) {
     launch_ring_code(tile - 100, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st);
     return tile;

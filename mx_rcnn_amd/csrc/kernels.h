@@ -184,9 +184,22 @@ struct ConvEpi {
   int o_H = 0, o_W = 0, o_sh = 1, o_sw = 1, o_ph = 0, o_pw = 0;
   // fp16 activations / weights (inference): MFMA f16 operands, fp16 epilogue loads / stores
   int f16 = 0;
+  // batch statistics of the STORED output for a training-mode BN that consumes it (LDS-epilogue
+  // kernels, no split-K): row tile t writes sum(y - shift) / sum((y - shift)^2) of its rows to
+  // st_part[t][0][:] / st_part[t][1][:]; row tile 0 also copies the shift to st_part[tiles_m][0][:]
+  // (the bn_train.hip partial layout, folded by bn_train_apply)
+  float* st_part = nullptr;
+  const float* st_shift = nullptr;
+  // BN-backward mode, deterministic sums (batch-statistics BNs, whose dx needs them): instead of
+  // atomics into bnb_dgamma / bnb_dbeta, row tile t writes [sum g | sum g * xhat] of its rows to
+  // bnb_part[bnb_row0 + t][0 / 1][:] (LDS-epilogue kernels, no split-K)
+  float* bnb_part = nullptr;
+  int bnb_row0 = 0;
 };
 // counter-based uniform in [0, 1) (Philox-4x32-10, key = (seed, 0x9E3779B9), counter = (e, s))
 float philox_uniform_host(uint32_t seed, uint64_t step, uint64_t e);
+// output rows per workgroup tile (BM) of a tile code
+int conv_tile_bm(int tile);
 int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho, int Wo,
                    int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int tile, int splits, float* slab,
                    hipStream_t st);
@@ -197,7 +210,19 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
 int bn_train_workspace_floats(int64_t M, int C);
 int bn_train_fwd(const uint16_t* x, int64_t M, int C, const float* gamma, const float* beta, float* rmean,
                  float* rvar, float momentum, float eps, int fix_gamma, int relu, uint16_t* y, float* save_mean,
-                 float* save_invstd, float* workspace, hipStream_t st);
+                 float* save_invstd, float* workspace, hipStream_t st, float* save_veps = nullptr);
+// the same normalisation from statistics partials produced elsewhere (a conv epilogue's
+// ConvEpi::st_part, nparts row tiles + the shift row).  save: [3][C] = mean, invstd, var + eps
+int bn_train_apply(const uint16_t* x, int64_t M, int C, const float* part, int nparts, const float* gamma,
+                   const float* beta, float* rmean, float* rvar, float momentum, float eps, int fix_gamma, int relu,
+                   uint16_t* y, float* save, hipStream_t st);
+// BN-ReLU backward finish after a BN-backward conv epilogue wrote o = g * s and the partial rows
+// part[nparts][sum g | sum g * xhat][C] (ConvEpi::bnb_part): dx = o - s * (mean g + xhat *
+// mean(g xhat)) (+ dres); o may alias dx; dgamma / dbeta (nullable) += the folded sums.
+// gamma: the effective gamma (ones under fix_gamma)
+int bn_train_dx_apply(const uint16_t* o, const uint16_t* x, int64_t M, int C, const float* part, int nparts,
+                      const float* gamma, const float* save, const uint16_t* dres, uint16_t* dx, float* dgamma,
+                      float* dbeta, hipStream_t st);
 // dgamma/dbeta: written (accumulate = 0) or added to (accumulate = 1); may be null.
 int bn_train_bwd(const uint16_t* x, const uint16_t* dy, int64_t M, int C, const float* gamma, const float* beta,
                  const float* save_mean, const float* save_invstd, int fix_gamma, int relu, uint16_t* dx,

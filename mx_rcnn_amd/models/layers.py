@@ -91,7 +91,8 @@ class BatchNorm(MxLayer):
     def mx_aux(self):
         return {'%s_moving_mean' % self.mx_name: self.moving_mean, '%s_moving_var' % self.mx_name: self.moving_var}
 
-    def forward(self, x):
+    def forward(self, x, parts=None):
+        """parts: statistics partials of x produced by its conv's epilogue (train mode only)."""
         if getattr(self, '_calibrate', False):
             # data-dependent init: moving stats := statistics of this batch (stand-in for the
             # ImageNet statistics a pretrained checkpoint carries)
@@ -108,7 +109,7 @@ class BatchNorm(MxLayer):
                                   self.fix_gamma, self.relu)
         if train_bn_eligible(x) and os.environ.get('MXR_BN_TRAIN_KERNEL', '1') != '0':
             return train_bn_relu(x, self.gamma, self.beta, self.moving_mean, self.moving_var, self.momentum,
-                                 self.eps, self.fix_gamma, self.relu)
+                                 self.eps, self.fix_gamma, self.relu, parts=parts)
         g = torch.ones_like(self.gamma) if self.fix_gamma else self.gamma
         # torch running = (1-m)*running + m*batch  <=>  MXNet moving = mom*moving + (1-mom)*batch
         y = F.batch_norm(x, self.moving_mean, self.moving_var, g.to(x.dtype) if x.dtype != torch.float32 else g,

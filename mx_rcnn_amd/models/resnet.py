@@ -95,6 +95,24 @@ class ResidualUnit(nn.Module):
             return False
         return x.shape[1] % 64 == 0 and x.shape[1] % 8 == 0
 
+    def train_unit_ok(self, x, next_bn):
+        """Batch-statistics unit (the RoI head in training): one fused op whose convs produce the
+        statistics of their outputs in the epilogue (ops/fused.py _forward_train)."""
+        if not fusion_enabled() or os.environ.get('MXR_TRAIN_UNIT', '1') == '0':
+            return False
+        if any(_frozen(b) for b in ([self.bn1, self.bn2] + ([self.bn3] if self.bottle_neck else []))):
+            return False
+        if not (x.is_cuda and x.dtype == torch.bfloat16 and x.dim() == 4 and
+                x.is_contiguous(memory_format=torch.channels_last) and x.shape[1] % 64 == 0):
+            return False
+        if next_bn is not None and not _train_bn_ok(next_bn):
+            return False
+        convs = [self.conv1, self.conv2] + ([self.conv3] if self.bottle_neck else [])
+        if not self.dim_match:
+            convs.append(self.sc)
+        return all(c.weight.dtype == x.dtype and c.weight.shape[0] % 64 == 0 and c.weight.shape[1] % 64 == 0 and
+                   igemm_eligible(x, c.weight, c.stride, c.pad) for c in convs)
+
     def forward_fused(self, x, act1=None, next_bn=None):
         """-> (unit output, next unit's act1 or None).  act1: this unit's bn1(x) if already
         produced by the previous unit's epilogue."""
@@ -122,14 +140,28 @@ class ResidualUnit(nn.Module):
         return out, (next_bn(out) if next_bn is not None else None)
 
 
-def run_stage(stage, x):
+def _train_bn_ok(bn):
+    return not _frozen(bn) and bn.relu and bn.gamma.shape[0] % 64 == 0
+
+
+def run_stage_parts(stage, x, tail_bn=None):
     """Run a stage (nn.Sequential of ResidualUnit) unit by unit through the fused ops where they
-    apply, chaining each unit's last epilogue into the next unit's bn1; units that cannot fuse
-    (e.g. train-mode BN in the RoI head) run as plain modules."""
+    apply, chaining each unit's last epilogue into the next unit's bn1; units that cannot fuse run
+    as plain modules.  Frozen-BN units hand the next unit its bn1 activation; batch-statistics
+    units (the RoI head in training) hand it the statistics partials of their output, and the last
+    one those of ``tail_bn``'s input -> (x, partials for tail_bn or None)."""
     units = list(stage)
-    act1 = None
+    act1, parts = None, None
     for i, u in enumerate(units):
         nxt = units[i + 1] if i + 1 < len(units) else None
+        tbn = nxt.bn1 if nxt is not None else tail_bn
+        tbn = tbn if (tbn is not None and fusion_enabled() and _train_bn_ok(tbn)) else None
+        if u.train_unit_ok(x, tbn):
+            x, parts = fused_unit(u, x, parts, tbn, train=True)
+            parts = parts if tbn is not None else None
+            act1 = None
+            continue
+        parts = None
         nbn = nxt.bn1 if (nxt is not None and _frozen(nxt.bn1) and fusion_enabled()) else None
         if u.unit_op_ok(x, nbn) and u.frozen_bns():
             x, act1 = fused_unit(u, x, act1, nbn)
@@ -137,7 +169,11 @@ def run_stage(stage, x):
             x = u(x)
         else:
             x, act1 = u.forward_fused(x, act1, nbn)
-    return x
+    return x, parts
+
+
+def run_stage(stage, x):
+    return run_stage_parts(stage, x)[0]
 
 
 def _stage(idx, n_units, cin, cout, bottle_neck, bn_mom, bn_global):
@@ -203,6 +239,9 @@ class ResNetHead(nn.Module):
         self.bbox_pred = Linear('bbox_pred', filters[4], 4 * num_classes)
 
     def forward(self, pooled):
-        x = self.bn1(run_stage(self.stage4, pooled))  # fused when the BNs are frozen (test time)
+        # fused units either way: frozen BNs (test time) or batch statistics (training), where the
+        # last unit's conv epilogue also produces bn1's statistics partials
+        x, parts = run_stage_parts(self.stage4, pooled, self.bn1)
+        x = self.bn1(x, parts=parts)
         x = global_avg_pool(x)
         return fc_pair(x, self.cls_score, self.bbox_pred)

@@ -82,10 +82,15 @@ class _TrainBnRelu(torch.autograd.Function):
     are updated in the forward kernel with MXNet's momentum convention."""
 
     @staticmethod
-    def forward(ctx, x, gamma, beta, rmean, rvar, momentum, eps, fix_gamma, relu):
+    def forward(ctx, x, gamma, beta, rmean, rvar, momentum, eps, fix_gamma, relu, parts=None):
         xc = x.contiguous(memory_format=torch.channels_last)
-        y, sm, si = need_ext().bn_train_fwd(xc, gamma, beta, rmean, rvar, float(momentum), float(eps),
-                                            bool(fix_gamma), bool(relu))
+        if parts is not None:  # statistics partials from the producing conv's epilogue
+            y, save = need_ext().bn_train_apply(xc, parts, gamma, beta, rmean, rvar, float(momentum), float(eps),
+                                                bool(fix_gamma), bool(relu))
+        else:
+            y, save = need_ext().bn_train_fwd(xc, gamma, beta, rmean, rvar, float(momentum), float(eps),
+                                              bool(fix_gamma), bool(relu))
+        sm, si = save[0], save[1]
         ctx.save_for_backward(xc, gamma, beta, sm, si)
         ctx.params = (gamma if gamma.is_leaf else None, beta if beta.is_leaf else None)
         ctx.fix_gamma, ctx.relu = fix_gamma, relu
@@ -104,14 +109,17 @@ class _TrainBnRelu(torch.autograd.Function):
                                              tb if direct else None)
         dx = dx if ctx.needs_input_grad[0] else None
         if direct:
-            return dx, None, None, None, None, None, None, None, None
+            return dx, None, None, None, None, None, None, None, None, None
         dg = dg.to(gamma.dtype) if need_g else None
         db = db.to(beta.dtype) if need_b else None
-        return dx, dg, db, None, None, None, None, None, None
+        return dx, dg, db, None, None, None, None, None, None, None
 
 
-def train_bn_relu(x, gamma, beta, rmean, rvar, momentum=0.9, eps=2e-5, fix_gamma=False, relu=True):
-    return _TrainBnRelu.apply(x, gamma, beta, rmean, rvar, float(momentum), float(eps), bool(fix_gamma), bool(relu))
+def train_bn_relu(x, gamma, beta, rmean, rvar, momentum=0.9, eps=2e-5, fix_gamma=False, relu=True, parts=None):
+    """parts: the (2 * nparts + 1, C) statistics partials of x from its conv's epilogue
+    (conv_igemm_fwd(..., stat_shift=rmean)), which replace the statistics pass."""
+    return _TrainBnRelu.apply(x, gamma, beta, rmean, rvar, float(momentum), float(eps), bool(fix_gamma), bool(relu),
+                              parts)
 
 
 def train_bn_eligible(x):

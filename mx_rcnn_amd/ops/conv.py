@@ -112,21 +112,32 @@ def strided_dgrad_ok(k, s, p, H, W):
     return True
 
 
+def strided_dgrad_parts(N, H, W, s):
+    """Partial rows the parity-class launches of strided_dgrad write with ``bnb_part`` (one per
+    64-row tile of each class grid)."""
+    return sum((N * ((H - ph + s - 1) // s) * ((W - pw + s - 1) // s) + 63) // 64
+               for ph in range(s) for pw in range(s) if H > ph and W > pw)
+
+
 def strided_dgrad(dy, wf, H, W, k, s, p, residual=None, bn=None, bn_eps=2e-5, bn_fix_gamma=False, bnb_x=None,
-                  dadd=None, dgamma=None, dbeta=None, param=None):
+                  dadd=None, dgamma=None, dbeta=None, param=None, bnb_part=None):
     """Data gradient of a stride-``s`` k x k conv (pad p) on the MFMA kernel, by parity
     decomposition: input rows / columns of parity (ph, pw) receive only the filter taps of matching
     parity, so each of the s*s classes is a small stride-1 conv of dy with a sub-filter, written
     straight into its positions of dx by the epilogue's output row map (no dilated dy, no scatter
     pass).  ``wf`` is the flipped / transposed filter (I, O, k, k) of the dgrad cache.  The
     optional BN-ReLU backward epilogue (``bn`` + ``bnb_x`` [+ ``dadd``, ``residual``]) accumulates
-    dgamma / dbeta over the classes."""
+    dgamma / dbeta over the classes, or with ``bnb_part`` writes their deterministic partial rows
+    (the classes in order, strided_dgrad_parts rows in all)."""
     ext = need_ext()
     N, O, Ho, Wo = dy.shape
     I = wf.shape[0]
     dx = torch.empty((N, I, H, W), dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
     bwd = bnb_x is not None
-    if bwd and dgamma is None:
+    row0 = 0
+    if bwd and bnb_part is not None:
+        dgamma = dbeta = None
+    elif bwd and dgamma is None:
         dgamma = torch.zeros(I, dtype=torch.float32, device=dy.device)
         dbeta = torch.zeros(I, dtype=torch.float32, device=dy.device)
     for ph in range(s):
@@ -143,7 +154,9 @@ def strided_dgrad(dy, wf, H, W, k, s, p, residual=None, bn=None, bn_eps=2e-5, bn
             # list would be a host-to-device copy, illegal inside graph capture)
             sub = sub_filter(param, wf, th, tw, s)
             ext.conv_igemm_fwd(dy, sub, None, 1, -oh, False, 0, 0, residual, bn, bn_eps, bn_fix_gamma, True,
-                               bnb_x, dadd, dgamma, dbeta, 0.0, 0, None, -ow, dx, [Hc, Wc, H, W, s, s, ph, pw])
+                               bnb_x, dadd, dgamma, dbeta, 0.0, 0, None, -ow, dx, [Hc, Wc, H, W, s, s, ph, pw],
+                               bnb_part=bnb_part, bnb_row0=row0)
+            row0 += (N * Hc * Wc + 63) // 64
     if bwd:
         return dx, dgamma, dbeta
     return dx

@@ -208,7 +208,7 @@ class _nullctx(object):
 class _Unit(object):
     """Static description of a residual unit for the fused op."""
 
-    def __init__(self, u, next_bn):
+    def __init__(self, u, next_bn, train=False):
         self.bottle = u.bottle_neck
         self.dim_match = u.dim_match
         self.stride = int((u.conv2 if u.bottle_neck else u.conv1).stride)
@@ -216,6 +216,10 @@ class _Unit(object):
         self.next_bn = next_bn
         self.eps = [float(b.eps) for b in self.bns]
         self.fix = [bool(b.fix_gamma) for b in self.bns]
+        # batch-statistics BNs (the RoI head, stage 4): conv epilogues produce the statistics
+        # partials, a normalisation kernel applies them; next_bn (if any) is also batch-statistics
+        self.train = bool(train)
+        self.mom = [float(b.momentum) for b in self.bns]
 
 
 def _bnp(bn):
@@ -224,9 +228,63 @@ def _bnp(bn):
 
 class _FusedUnitFn(torch.autograd.Function):
     @staticmethod
+    def _forward_train(ctx, spec, x, parts1, t, nconv, ws, bnps, nxt):
+        """Batch-statistics unit: every conv's epilogue also writes the statistics partials of its
+        output for the BN that consumes it (ConvEpi::st_part), so each BN is ONE normalisation pass
+        (bn_train_apply); the unit's input BN uses the partials the previous unit's last conv
+        produced (parts1) or a statistics pass.  Saved per BN: [mean, invstd, var+eps, 0, 0] --
+        the zero rows are the backward's column-sum accumulators."""
+        ext = need_ext()
+        x = _cl(x)
+
+        def norm(inp, parts, i):
+            g, b, rm, rv = bnps[i]
+            if parts is None:
+                return ext.bn_train_fwd(inp, g, b, rm, rv, spec.mom[i], spec.eps[i], spec.fix[i], True)
+            return ext.bn_train_apply(inp, parts, g, b, rm, rv, spec.mom[i], spec.eps[i], spec.fix[i], True)
+
+        act1, sv1 = norm(x, parts1, 0)
+        s1 = 1 if spec.bottle else spec.stride
+        p1 = 0 if spec.bottle else 1
+        y1, pt = ext.conv_igemm_fwd(act1, ws[0], None, s1, p1, False, stat_shift=bnps[1][2])
+        a2, sv2 = norm(y1, pt, 1)
+        saves = [sv1, sv2]
+        if spec.bottle:
+            y2, pt = ext.conv_igemm_fwd(a2, ws[1], None, spec.stride, 1, False, stat_shift=bnps[2][2])
+            a3, sv3 = norm(y2, pt, 2)
+            saves.append(sv3)
+            last_in, w_last = a3, ws[2]
+        else:
+            y2, a3 = None, None
+            last_in, w_last = a2, ws[1]
+        res = x if spec.dim_match else ext.conv_igemm_fwd(act1, ws[-1], None, spec.stride, 0, False)[0]
+        pl = 0 if spec.bottle else 1
+        if nxt is not None:
+            out, parts_n = ext.conv_igemm_fwd(last_in, w_last, None, 1, pl, False, 0, 0, res,
+                                              stat_shift=nxt[2].float().contiguous())
+        else:
+            out, parts_n = ext.conv_igemm_fwd(last_in, w_last, None, 1, pl, False, 0, 0, res)[0], None
+        ctx.spec = spec
+        ctx.nconv = nconv
+        ctx.set_materialize_grads(False)
+        ctx.params = [p if p.is_leaf else None for p in t]
+        ctx.saves = saves
+        ctx.save_for_backward(x, act1, y1, a2, y2, a3, None, *t)
+        if parts_n is None:
+            return out, out.new_empty(0)
+        ctx.mark_non_differentiable(parts_n)
+        return out, parts_n
+
+    @staticmethod
     def forward(ctx, spec, x, act1, *t):
         # t = W1, W2, [W3], [Wsc], bn1(4), bn2(4), [bn3(4)], [next_bn(4)]
         ext = need_ext()
+        if spec.train:
+            nconv = (3 if spec.bottle else 2) + (0 if spec.dim_match else 1)
+            nb = len(spec.bns)
+            bnps = [list(t[nconv + 4 * i:nconv + 4 * i + 4]) for i in range(nb)]
+            nxt = list(t[nconv + 4 * nb:nconv + 4 * nb + 4]) if spec.next_bn is not None else None
+            return _FusedUnitFn._forward_train(ctx, spec, x, act1, t, nconv, list(t[:nconv]), bnps, nxt)
         nconv = (3 if spec.bottle else 2) + (0 if spec.dim_match else 1)
         ws = list(t[:nconv])
         nb = len(spec.bns)
@@ -283,6 +341,44 @@ class _FusedUnitFn(torch.autograd.Function):
         need = ctx.needs_input_grad[3:]  # per tensor in t
         grads = [None] * len(t)
         d_out = _cl(d_out).to(x.dtype)
+        # BN parameters of the BN-backward epilogues.  Batch-statistics BNs: (effective gamma, beta,
+        # batch mean, var + eps) with eps 0 reproduce the forward's invstd exactly; the epilogue's
+        # column sums land in the saved zero rows and bn_train_dx_apply finishes the backward
+        train = spec.train
+        if train:
+            saves = ctx.saves
+            geff = [torch.ones_like(saves[i][0]) if spec.fix[i] else bnps[i][0].float().contiguous()
+                    for i in range(nb)]
+            bwp = [[geff[i], bnps[i][1], saves[i][0], saves[i][2]] for i in range(nb)]
+            beps, bfix = [0.0] * nb, [False] * nb
+        else:
+            bwp, beps, bfix = bnps, spec.eps, spec.fix
+
+        def train_part(bn_x, nparts):
+            return torch.empty(nparts * 2 * bn_x.shape[1], device=bn_x.device, dtype=torch.float32)
+
+        def train_finish(i, o, bn_x, dres, part, nparts):
+            """o = g * s from the BN-backward epilogue -> the batch-statistics BN's dx (+ dres), in
+            place; gamma / beta gradients from the epilogue's column-sum partial rows (folded in a
+            fixed order: deterministic)."""
+            gi = nconv + 4 * i
+            ng, nbb = need[gi] and not spec.fix[i], need[gi + 1]
+            tg = grad_sink.target(ctx.params[gi]) if ng else None
+            tb = grad_sink.target(ctx.params[gi + 1]) if nbb else None
+            own_g = ng and (tg is None or tg.dtype != torch.float32 or not tg.is_contiguous())
+            own_b = nbb and (tb is None or tb.dtype != torch.float32 or not tb.is_contiguous())
+            C = saves[i].shape[1]
+            if own_g:
+                tg = torch.zeros(C, device=o.device, dtype=torch.float32)
+            if own_b:
+                tb = torch.zeros(C, device=o.device, dtype=torch.float32)
+            dx = ext.bn_train_dx_apply(o, bn_x, saves[i], geff[i], part, nparts, dres, tg if ng else None,
+                                       tb if nbb else None)
+            if own_g:
+                grads[gi] = tg.to(bnps[i][0].dtype)
+            if own_b:
+                grads[gi + 1] = tb.to(bnps[i][1].dtype)
+            return dx
 
         # weight gradients run on a side stream, concurrently with the data-gradient chain on the
         # compute stream (each wgrad only waits for the dY it reads); joined before returning, so
@@ -323,6 +419,8 @@ class _FusedUnitFn(torch.autograd.Function):
                         grads[idx].record_stream(main)
 
         def bn_targets(i):
+            if train:  # column sums go to partial rows (bnb_part), gamma / beta grads via train_finish
+                return None, None, False
             gi = nconv + 4 * i
             ng, nbb = need[gi] and not spec.fix[i], need[gi + 1]
             if not (ng or nbb):
@@ -362,40 +460,59 @@ class _FusedUnitFn(torch.autograd.Function):
             tg, tb, ret = bn_targets(bn_i)
             wf = dgrad_weight(ctx.params[w_idx], ws[w_idx])
             tgt = grouped_target(wg)
+            part, nparts = None, 0
+            if train:
+                nparts = (bn_x.numel() // bn_x.shape[1] + 63) // 64
+                part = train_part(bn_x, nparts)
             if tgt is not None and dy.dtype == torch.bfloat16 and wf.dtype == torch.bfloat16:
-                if tg is None:  # statistics not needed: accumulate into scratch
+                if tg is None and not train:  # statistics not needed: accumulate into scratch
                     C = bnps[bn_i][0].numel()
                     tg = torch.zeros(C, device=dy.device, dtype=torch.float32)
                     tb = torch.zeros(C, device=dy.device, dtype=torch.float32)
                 idx, wdy, winp, wk, wstride, wpad = wg
                 prev = pending[0]
-                r = ext.conv_dgrad_wgrad(dy, wf, k - 1 - pad, dres, bnps[bn_i], spec.eps[bn_i], spec.fix[bn_i], bn_x,
-                                         dadd, tg, tb, wdy, winp, wk, wk, wstride, wpad, tgt, True,
-                                         prev[0] if prev else None, prev[1] if prev else None)
+                r = ext.conv_dgrad_wgrad(dy, wf, k - 1 - pad, None if train else dres, bwp[bn_i], beps[bn_i],
+                                         bfix[bn_i], bn_x, dadd, tg, tb, wdy, winp, wk, wk, wstride, wpad, tgt, True,
+                                         prev[0] if prev else None, prev[1] if prev else None, part)
                 pending[0] = (r[3], tgt) if r[3].numel() > 0 else None
             else:
                 if wg is not None:
                     wgrad(*wg)
-                r = ext.conv_igemm_fwd(dy, wf, None, 1, k - 1 - pad, False, 0, 0, dres, bnps[bn_i], spec.eps[bn_i],
-                                       spec.fix[bn_i], True, bn_x, dadd, tg, tb)
+                r = ext.conv_igemm_fwd(dy, wf, None, 1, k - 1 - pad, False, 0, 0, None if train else dres, bwp[bn_i],
+                                       beps[bn_i], bfix[bn_i], True, bn_x, dadd, tg, tb, bnb_part=part)
             finish_bn(bn_i, tg, tb, ret)
-            return r[0]
+            return train_finish(bn_i, r[0], bn_x, dres, part, nparts) if train else r[0]
 
         def strided_dgrad_bn(dy, w_idx, k, stride, pad, bn_i, bn_x, H, W, dadd=None, dres=None):
             """strided-conv dgrad (parity classes) with the BN(bn_i)-ReLU backward in the epilogue."""
-            from .conv import dgrad_weight, strided_dgrad
+            from .conv import dgrad_weight, strided_dgrad, strided_dgrad_parts
             tg, tb, ret = bn_targets(bn_i)
-            if tg is None:  # statistics not needed: accumulate into scratch
+            part, nparts = None, 0
+            if train:
+                nparts = strided_dgrad_parts(bn_x.shape[0], H, W, stride)
+                part = train_part(bn_x, nparts)
+            elif tg is None:  # statistics not needed: accumulate into scratch
                 C = bnps[bn_i][0].numel()
                 tg = torch.zeros(C, device=dy.device, dtype=torch.float32)
                 tb = torch.zeros(C, device=dy.device, dtype=torch.float32)
-            r = strided_dgrad(dy, dgrad_weight(ctx.params[w_idx], ws[w_idx]), H, W, k, stride, pad, residual=dres,
-                              bn=bnps[bn_i], bn_eps=spec.eps[bn_i], bn_fix_gamma=spec.fix[bn_i], bnb_x=bn_x,
-                              dadd=dadd, dgamma=tg, dbeta=tb, param=ctx.params[w_idx])
+            r = strided_dgrad(dy, dgrad_weight(ctx.params[w_idx], ws[w_idx]), H, W, k, stride, pad,
+                              residual=None if train else dres, bn=bwp[bn_i], bn_eps=beps[bn_i],
+                              bn_fix_gamma=bfix[bn_i], bnb_x=bn_x, dadd=dadd, dgamma=tg, dbeta=tb,
+                              param=ctx.params[w_idx], bnb_part=part)
             finish_bn(bn_i, tg, tb, ret)
-            return r[0]
+            return train_finish(bn_i, r[0], bn_x, dres, part, nparts) if train else r[0]
 
         def bn_bwd_plain(dy_act, bn_i, bn_x, dres=None):
+            if train:  # BN-ReLU backward on the batch statistics (bn_train.hip), then the shortcut
+                gi = nconv + 4 * bn_i
+                ng, nbb = need[gi] and not spec.fix[bn_i], need[gi + 1]
+                dx, dg, db = ext.bn_train_bwd(bn_x, dy_act, bnps[bn_i][0], bnps[bn_i][1], saves[bn_i][0],
+                                              saves[bn_i][1], spec.fix[bn_i], True, True)
+                if ng:
+                    grads[gi] = dg.to(bnps[bn_i][0].dtype)
+                if nbb:
+                    grads[gi + 1] = db.to(bnps[bn_i][1].dtype)
+                return dx + dres if dres is not None else dx
             tg, tb, ret = bn_targets(bn_i)
             p = [q.float().contiguous() for q in bnps[bn_i]]
             dx, dg, db = ext.bn_relu_bwd(bn_x, dy_act, *p, spec.eps[bn_i], spec.fix[bn_i], True, True,
@@ -476,9 +593,11 @@ def _strided_ok(w, s, inp):
             strided_dgrad_ok(w.shape[2], s, (w.shape[2] - 1) // 2, inp.shape[2], inp.shape[3]))
 
 
-def fused_unit(u, x, act1=None, next_bn=None):
-    """Run ResidualUnit ``u`` (frozen BNs) as one fused op -> (out, next act1 or None)."""
-    spec = _Unit(u, next_bn)
+def fused_unit(u, x, act1=None, next_bn=None, train=False):
+    """Run ResidualUnit ``u`` as one fused op -> (out, next act1 or None).  Frozen BNs: act1 /
+    the second output are the unit's / next unit's bn1 activation.  train=True (batch-statistics
+    BNs): they are the statistics partials of the unit input / output for its / the next bn1."""
+    spec = _Unit(u, next_bn, train)
     ws = [u.conv1.weight, u.conv2.weight] + ([u.conv3.weight] if u.bottle_neck else [])
     if not u.dim_match:
         ws.append(u.sc.weight)

@@ -379,3 +379,149 @@ def test_grouped_unit_backward_matches_side_stream(cuda, monkeypatch):
     assert _rel(xa, xb) <= 1e-2
     for n in ga:
         assert _rel(ga[n], gb[n]) <= 2e-2, (n, _rel(ga[n], gb[n]))
+
+
+@pytest.mark.parametrize('shape', [(16, 512, 4, 4, 512, 3, 1, 1), (16, 1024, 7, 7, 256, 1, 1, 0),
+                                   (16, 256, 7, 7, 1024, 1, 2, 0), (1, 256, 50, 84, 1024, 1, 1, 0)])
+@pytest.mark.parametrize('tile', [0, 23, 22, 101, 104, 106, 109])
+def test_conv_stats_epilogue(cuda, shape, tile):
+    """Training-BN statistics partials written by the conv epilogue (ConvEpi::st_part): folded
+    they equal the fp32 column sums of the STORED output, shifted by the given shift."""
+    from mx_rcnn_amd.ops import need_ext
+    ext = need_ext()
+    N, Cin, H, W, Cout, k, s, p = shape
+    g = torch.Generator().manual_seed(11)
+    x = _cl(torch.randn(N, Cin, H, W, generator=g).bfloat16(), cuda)
+    w = _cl((torch.randn(Cout, Cin, k, k, generator=g) * 0.05).bfloat16(), cuda)
+    shift = (torch.randn(Cout, generator=g) * 0.1).to(cuda)
+    res = None
+    if s == 1 and k == 1:
+        res = _cl(torch.randn(N, Cout, H, W, generator=g).bfloat16(), cuda)
+    y, part = ext.conv_igemm_fwd(x, w, None, s, p, False, tile, 0, res, stat_shift=shift)
+    assert part.dim() == 2 and part.shape[1] == Cout and part.shape[0] % 2 == 1
+    nparts = (part.shape[0] - 1) // 2
+    pr = part[:2 * nparts].view(nparts, 2, Cout).sum(0)
+    yf = y.float().permute(0, 2, 3, 1).reshape(-1, Cout) - shift[None]
+    assert torch.allclose(pr[0], yf.sum(0), rtol=1e-4, atol=1e-3)
+    assert torch.allclose(pr[1], (yf * yf).sum(0), rtol=1e-4, atol=1e-3)
+    assert torch.equal(part[2 * nparts], shift)
+    # the output itself is unchanged by the statistics epilogue
+    y0 = ext.conv_igemm_fwd(x, w, None, s, p, False, tile, 1, res)[0]
+    assert torch.equal(y, y0) if tile else _rel(y, y0) <= 1e-3
+
+
+def test_bn_train_apply_and_dx_apply(cuda):
+    """bn_train_apply (normalisation from conv-epilogue partials) and bn_train_dx_apply (the
+    backward finish after a BN-backward dgrad epilogue) vs fp32 torch batch-norm."""
+    from mx_rcnn_amd.ops import need_ext
+    ext = need_ext()
+    g = torch.Generator().manual_seed(12)
+    N, Cin, H, W, C = 32, 256, 4, 4, 512
+    x = _cl(torch.randn(N, Cin, H, W, generator=g).bfloat16(), cuda)
+    w = _cl((torch.randn(C, Cin, 1, 1, generator=g) * 0.1).bfloat16(), cuda)
+    gamma = (torch.rand(C, generator=g) + 0.5).to(cuda)
+    beta = (torch.randn(C, generator=g) * 0.1).to(cuda)
+    rm = (torch.randn(C, generator=g) * 0.1).to(cuda)
+    rv = (torch.rand(C, generator=g) + 0.5).to(cuda)
+    rm0, rv0 = rm.clone(), rv.clone()
+    y, part = ext.conv_igemm_fwd(x, w, None, 1, 0, False, stat_shift=rm)
+    a, save = ext.bn_train_apply(y, part, gamma, beta, rm, rv, 0.9, 2e-5, False, True)
+    yf = y.float()
+    mu = yf.mean(dim=(0, 2, 3))
+    var = yf.var(dim=(0, 2, 3), unbiased=False)
+    ref = torch.relu((yf - mu[None, :, None, None]) * (gamma * torch.rsqrt(var + 2e-5))[None, :, None, None] +
+                     beta[None, :, None, None])
+    assert _rel(a.float(), ref) <= 1e-2
+    assert torch.allclose(save[0], mu, atol=1e-4, rtol=1e-4)
+    assert torch.allclose(save[2], var + 2e-5, atol=1e-4, rtol=1e-4)
+    Mr = N * H * W
+    assert torch.allclose(rm, 0.9 * rm0 + 0.1 * mu, atol=1e-4)
+    assert torch.allclose(rv, 0.9 * rv0 + 0.1 * var * Mr / (Mr - 1), atol=1e-4, rtol=1e-4)
+    # backward: d_a (gradient at the BN-ReLU output) comes from a dgrad conv in the real unit; here
+    # the BN-backward epilogue is driven by a 1x1 "dgrad" of a random dY through the conv weight
+    w2 = _cl((torch.randn(1024, C, 1, 1, generator=g) * 0.05).bfloat16(), cuda)  # the next conv: C -> 1024
+    dy = _cl(torch.randn(N, 1024, H, W, generator=g).bfloat16(), cuda)
+    from mx_rcnn_amd.ops.conv import _flip_t
+    wf = _cl(_flip_t(w2), cuda)
+    dres = _cl(torch.randn(N, C, H, W, generator=g).bfloat16(), cuda)
+    nparts = (N * H * W + 63) // 64
+    part = torch.empty(nparts * 2 * C, device=cuda)
+    o = ext.conv_igemm_fwd(dy, wf, None, 1, 0, False, 0, 0, None, [gamma, beta, save[0], save[2]], 0.0, False,
+                           True, y, bnb_part=part)[0]
+    dgam = torch.zeros(C, device=cuda)
+    dbet = torch.zeros(C, device=cuda)
+    dx = ext.bn_train_dx_apply(o, y, save, gamma, part, nparts, dres, dgam, dbet)
+    # fp32 oracle
+    yr = yf.clone().requires_grad_()
+    out = torch.relu(F.batch_norm(yr, None, None, gamma, beta, training=True, eps=2e-5))
+    d_act = F.conv2d(dy.float(), w2.float().permute(1, 0, 2, 3))
+    out.backward(d_act)
+    assert _rel(dx.float() - dres.float(), yr.grad) <= 3e-2
+    assert _rel(dgam, _ref_dgamma(yf, d_act, gamma, beta)) <= 1e-2
+    assert _rel(dbet, (d_act * (out > 0)).sum(dim=(0, 2, 3))) <= 1e-2
+
+
+def _ref_dgamma(yf, d_act, gamma, beta):
+    mu = yf.mean(dim=(0, 2, 3), keepdim=True)
+    var = yf.var(dim=(0, 2, 3), unbiased=False, keepdim=True)
+    xh = (yf - mu) * torch.rsqrt(var + 2e-5)
+    mask = (xh * gamma[None, :, None, None] + beta[None, :, None, None]) > 0
+    return (d_act * mask * xh).sum(dim=(0, 2, 3))
+
+
+def _train_stage(cuda, n_units=3, cin=512, cout=1024):
+    from mx_rcnn_amd.models.resnet import _stage
+    from mx_rcnn_amd.models.layers import BatchNorm
+    torch.manual_seed(3)
+    st = _stage(4, n_units, cin, cout, True, 0.9, False)
+    tail = BatchNorm('bn1', cout, momentum=0.9, use_global_stats=False)
+    with torch.no_grad():
+        for m in list(st.modules()) + [tail]:
+            if hasattr(m, 'moving_var'):
+                m.moving_mean.normal_(0, 0.2)
+                m.moving_var.uniform_(0.5, 1.5)
+                m.gamma.uniform_(0.5, 1.5)
+                m.beta.normal_(0, 0.1)
+            elif hasattr(m, 'weight') and m.weight is not None:
+                m.weight.normal_(0, 0.03)
+    st, tail = st.to(cuda).train(), tail.to(cuda).train()
+    for m in st.modules():
+        if hasattr(m, 'weight') and m.weight is not None and m.weight.dim() == 4:
+            m.weight = torch.nn.Parameter(m.weight.detach().bfloat16().contiguous(memory_format=torch.channels_last))
+    return st, tail
+
+
+def test_train_units_match_module_path(cuda, monkeypatch):
+    """The RoI-head stage (batch-statistics BNs) through the fused train-unit op -- statistics
+    in the conv epilogues, BN backward in the dgrad epilogues + dx_apply -- vs the per-module
+    path (MXR_TRAIN_UNIT=0), including the head bn1 fed by the last unit's partials."""
+    import copy
+    from mx_rcnn_amd.models.resnet import run_stage_parts
+    st0, tail0 = _train_stage(cuda)
+    g = torch.Generator().manual_seed(9)
+    x0 = torch.randn(16, 512, 8, 8, generator=g).bfloat16()
+    res = []
+    for flag in ('0', '1'):
+        monkeypatch.setenv('MXR_TRAIN_UNIT', flag)
+        st, tail = copy.deepcopy(st0), copy.deepcopy(tail0)
+        x = _cl(x0, cuda).requires_grad_()
+        y, parts = run_stage_parts(st, x, tail)
+        assert (parts is not None) == (flag == '1')
+        out = tail(y, parts=parts)
+        gen = torch.Generator().manual_seed(7)
+        out.backward(_cl(torch.randn(out.shape, generator=gen).bfloat16(), cuda))
+        torch.cuda.synchronize()
+        grads = {n: p.grad.float().clone() for n, p in list(st.named_parameters()) + [('tail.' + n, p) for n, p in
+                                                                                      tail.named_parameters()]
+                 if p.grad is not None}
+        stats = {n: b.float().clone() for n, b in list(st.named_buffers()) + [('tail.' + n, b) for n, b in
+                                                                              tail.named_buffers()]}
+        res.append((out.detach().float(), x.grad.float(), grads, stats))
+    (oa, xa, ga, sa), (ob, xb, gb, sb) = res
+    assert _rel(ob, oa) <= 2e-2
+    assert _rel(xb, xa) <= 0.1
+    assert set(ga) == set(gb), set(ga) ^ set(gb)
+    for n in ga:
+        assert _rel(gb[n], ga[n]) <= 0.1, (n, _rel(gb[n], ga[n]))
+    for n in sa:
+        assert _rel(sb[n], sa[n]) <= 1e-2, (n, _rel(sb[n], sa[n]))

@@ -83,7 +83,13 @@ class Trainer:
         self.store.zero_grad()
         # the optimizer runs bucket by bucket under the backward pass (parallel/reducer.py)
         self.reducer.prepare(sgd=(self.lr_t, self.momentum, self.wd, self.rescale, self.clip))
-        out = self.forward(b)
+        # a model that starts part of its backward inside forward (the e2e graph's early RPN
+        # backward) joins the filter cache first
+        self.model.pre_backward = cache_join
+        try:
+            out = self.forward(b)
+        finally:
+            self.model.pre_backward = None
         if self.fault is not None:  # test hook: multiplies the loss by NaN on the armed step
             out['loss'] = out['loss'] * self.fault
             out['objective'] = out['objective'] * self.fault

@@ -82,7 +82,7 @@ std::vector<Tensor> proposal_decode(const Tensor& cls, const Tensor& dlt, const 
 
 // NMS over score-sorted boxes; returns (rois (B,post,5), scores (B,post), keep (B,post) int64, n_keep (B))
 std::vector<Tensor> nms_proposals(const Tensor& boxes, const Tensor& scores, const Tensor& n_valid, double thresh,
-                                  int64_t post, const Tensor& rand_u) {
+                                  int64_t post, const Tensor& rand_u, c10::optional<Tensor> mask_in) {
   CHECK_DEV(boxes); CHECK_F32(boxes); CHECK_CONTIG(boxes);
   CHECK_DEV(scores); CHECK_F32(scores); CHECK_CONTIG(scores);
   CHECK_DEV(n_valid); CHECK_I32(n_valid); CHECK_CONTIG(n_valid);
@@ -99,10 +99,17 @@ std::vector<Tensor> nms_proposals(const Tensor& boxes, const Tensor& scores, con
   TORCH_CHECK(mxr::nms_reduce_lds(P, (int)post) <= 160 * 1024, "NMS LDS budget exceeded (P or post too large)");
   TORCH_CHECK(nb <= 1024, "NMS supports at most 65536 pre-NMS boxes per image");
   auto st = cur_stream();
-  Tensor mask = at::empty({mxr::nms_mask_words(B, P)}, boxes.options().dtype(at::kLong));
-  mxr::nms_mask(boxes.data_ptr<float>(), n_valid.data_ptr<int32_t>(), B, P, (float)thresh,
-                reinterpret_cast<uint64_t*>(mask.data_ptr<int64_t>()), st);
-  LAUNCH_CHECK("nms_mask");
+  Tensor mask;
+  if (mask_in.has_value() && mask_in->defined()) {  // built by nms_mask_build (the two-phase path)
+    mask = *mask_in;
+    TORCH_CHECK(mask.scalar_type() == at::kLong && mask.is_contiguous() && mask.numel() == mxr::nms_mask_words(B, P),
+                "mask: the nms_mask_build output for these boxes");
+  } else {
+    mask = at::empty({mxr::nms_mask_words(B, P)}, boxes.options().dtype(at::kLong));
+    mxr::nms_mask(boxes.data_ptr<float>(), n_valid.data_ptr<int32_t>(), B, P, (float)thresh,
+                  reinterpret_cast<uint64_t*>(mask.data_ptr<int64_t>()), st);
+    LAUNCH_CHECK("nms_mask");
+  }
   Tensor rois = at::empty({B, post, 5}, boxes.options());
   Tensor out_scores = at::empty({B, post}, boxes.options());
   Tensor keep = at::empty({B, post}, boxes.options().dtype(at::kLong));
@@ -113,6 +120,22 @@ std::vector<Tensor> nms_proposals(const Tensor& boxes, const Tensor& scores, con
                   keep.data_ptr<int64_t>(), n_keep.data_ptr<int32_t>(), st);
   LAUNCH_CHECK("nms_reduce");
   return {rois, out_scores, keep, n_keep};
+}
+
+// phase 1 of nms_proposals alone: the suppression bitmask (a caller can order other work between
+// the data-parallel mask and the serial reduce)
+Tensor nms_mask_build(const Tensor& boxes, const Tensor& n_valid, double thresh) {
+  CHECK_DEV(boxes); CHECK_F32(boxes); CHECK_CONTIG(boxes);
+  CHECK_DEV(n_valid); CHECK_I32(n_valid); CHECK_CONTIG(n_valid);
+  TORCH_CHECK(boxes.dim() == 3 && boxes.size(2) == 4, "boxes must be (B, P, 4)");
+  const int B = (int)boxes.size(0), P = (int)boxes.size(1);
+  TORCH_CHECK(n_valid.numel() == B && P > 0 && (P + 63) / 64 <= 1024, "nms_mask_build: shape");
+  DevGuard g(boxes.device());
+  Tensor mask = at::empty({mxr::nms_mask_words(B, P)}, boxes.options().dtype(at::kLong));
+  mxr::nms_mask(boxes.data_ptr<float>(), n_valid.data_ptr<int32_t>(), B, P, (float)thresh,
+                reinterpret_cast<uint64_t*>(mask.data_ptr<int64_t>()), cur_stream());
+  LAUNCH_CHECK("nms_mask");
+  return mask;
 }
 
 // ---- fused target sampling ------------------------------------------------------------------
@@ -243,7 +266,7 @@ std::vector<Tensor> roi_pool_fwd(const Tensor& feat, const Tensor& rois, int64_t
 }
 
 Tensor roi_pool_bwd(const Tensor& grad_out, const Tensor& argmax, const Tensor& rois, int64_t B, int64_t H,
-                    int64_t W) {
+                    int64_t W, c10::optional<Tensor> grad_add) {
   CHECK_DEV(grad_out); CHECK_DEV(argmax); CHECK_I32(argmax); CHECK_DEV(rois); CHECK_F32(rois);
   const int R = (int)grad_out.size(0), C = (int)grad_out.size(1), PH = (int)grad_out.size(2), PW = (int)grad_out.size(3);
   Tensor go = grad_out.contiguous(at::MemoryFormat::ChannelsLast);
@@ -254,10 +277,17 @@ Tensor roi_pool_bwd(const Tensor& grad_out, const Tensor& argmax, const Tensor& 
     const char* e = std::getenv("MXR_ROIPOOL_BWD_LDS");
     return e == nullptr || e[0] != '0';
   }();
+  const bool add = grad_add.has_value() && grad_add->defined();
+  if (add)
+    TORCH_CHECK(grad_add->scalar_type() == grad_out.scalar_type() && grad_add->dim() == 4 && grad_add->size(0) == B &&
+                    grad_add->size(1) == C && grad_add->size(2) == H && grad_add->size(3) == W &&
+                    grad_add->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "grad_add: channels_last (B, C, H, W) of the gradient dtype");
   if (lds_path) {
     Tensor gin = at::empty({B, C, H, W}, grad_out.options().memory_format(at::MemoryFormat::ChannelsLast));
     if (mxr::roi_pool_bwd_lds(go.data_ptr(), dcode(go), argmax.data_ptr<int32_t>(), rois.contiguous().data_ptr<float>(),
-                              R, PH, PW, (int)B, (int)H, (int)W, C, gin.data_ptr(), st) == 0)
+                              R, PH, PW, (int)B, (int)H, (int)W, C, gin.data_ptr(), st,
+                              add ? grad_add->data_ptr() : nullptr) == 0)
       return gin;
   }
   // NOTE: at::zeros ignores a memory_format carried in TensorOptions (returns NCHW); allocate
@@ -265,6 +295,7 @@ Tensor roi_pool_bwd(const Tensor& grad_out, const Tensor& argmax, const Tensor& 
   Tensor gin32 = at::zeros({B, H, W, C}, grad_out.options().dtype(at::kFloat)).permute({0, 3, 1, 2});
   mxr::roi_pool_bwd(go.data_ptr(), is_bf16(go), argmax.data_ptr<int32_t>(), rois.contiguous().data_ptr<float>(), R,
                     PH, PW, (int)B, (int)H, (int)W, C, gin32.data_ptr<float>(), st);
+  if (add) gin32.add_(*grad_add);
   if (grad_out.scalar_type() == at::kFloat) return gin32;
   Tensor gin = at::empty({B, C, H, W}, grad_out.options().memory_format(at::MemoryFormat::ChannelsLast));
   mxr::cast_f32(gin32.data_ptr<float>(), gin.data_ptr(), 1, gin.numel(), st);
@@ -1575,7 +1606,9 @@ Tensor bn_relu_fwd_cpu(const Tensor& x_in, const Tensor& gamma, const Tensor& be
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mx_rcnn_amd gfx950 kernels";
   m.def("proposal_decode", &proposal_decode);
-  m.def("nms_proposals", &nms_proposals);
+  m.def("nms_proposals", &nms_proposals, py::arg("boxes"), py::arg("scores"), py::arg("n_valid"), py::arg("thresh"),
+        py::arg("post"), py::arg("rand_u"), py::arg("mask") = py::none());
+  m.def("nms_mask_build", &nms_mask_build);
   m.def("nms_cpu", &nms_cpu);
   m.def("roi_pool_fwd_cpu", &roi_pool_fwd_cpu);
   m.def("roi_pool_bwd_cpu", &roi_pool_bwd_cpu);
@@ -1592,7 +1625,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("proposal_sample", &proposal_sample);
   m.def("anchor_target_assign", &anchor_target_assign);
   m.def("roi_pool_fwd", &roi_pool_fwd);
-  m.def("roi_pool_bwd", &roi_pool_bwd);
+  m.def("roi_pool_bwd", &roi_pool_bwd, py::arg("grad_out"), py::arg("argmax"), py::arg("rois"), py::arg("B"),
+        py::arg("H"), py::arg("W"), py::arg("grad_add") = py::none());
   m.def("rpn_softmax_ce", &rpn_softmax_ce, py::arg("logits"), py::arg("label"), py::arg("norm"), py::arg("grad_scale"),
         py::arg("want_prob"), py::arg("meta") = py::none());
   m.def("row_softmax_ce", &row_softmax_ce);

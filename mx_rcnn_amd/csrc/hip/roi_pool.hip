@@ -159,13 +159,62 @@ void roi_pool_fwd(const void* feat, int bf16, int B, int H, int W, int C, const 
 // image's RoIs once (argmax + dY: 16 + 8 B per bin for CW = 4), then writes its channels of every
 // pixel in the output dtype.  Replaces: a zero fill of an fp32 (B, H, W, C) buffer, 6.4 M global
 // fp32 atomics (~120 us at 128 RoIs x 49 bins x 1024 ch) and the cast to bf16.
+// CW consecutive channels of one pixel as one vector access (8 B for 4 bf16 / fp16)
+template <int CW>
+__device__ __forceinline__ void ldv(const uint16_t* p, float* v, int code) {
+  if constexpr (CW == 4) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    const uint16_t h[4] = {(uint16_t)(u.x & 0xffff), (uint16_t)(u.x >> 16), (uint16_t)(u.y & 0xffff),
+                           (uint16_t)(u.y >> 16)};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = to_f(h[k], code);
+  } else {
+#pragma unroll
+    for (int k = 0; k < CW; ++k) v[k] = to_f(p[k], code);
+  }
+}
+template <int CW>
+__device__ __forceinline__ void ldv(const float* p, float* v, int) {
+#pragma unroll
+  for (int k = 0; k < CW; ++k) v[k] = p[k];
+}
+template <int CW>
+__device__ __forceinline__ void stv(uint16_t* p, const float* v, int code) {
+  if constexpr (CW == 4) {
+    uint16_t h[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) h[k] = f32_to_h16(v[k], code);
+    *reinterpret_cast<uint2*>(p) = make_uint2((uint32_t)h[0] | ((uint32_t)h[1] << 16),
+                                              (uint32_t)h[2] | ((uint32_t)h[3] << 16));
+  } else {
+#pragma unroll
+    for (int k = 0; k < CW; ++k) p[k] = f32_to_h16(v[k], code);
+  }
+}
+template <int CW>
+__device__ __forceinline__ void stv(float* p, const float* v, int) {
+#pragma unroll
+  for (int k = 0; k < CW; ++k) p[k] = v[k];
+}
+
 template <int CW, typename T>
 __global__ void __launch_bounds__(256)
 roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ argmax, const float* __restrict__ rois,
-                        int R, int PHW, int HW, int C, int code, T* __restrict__ gin) {
+                        int R, int PHW, int HW, int C, int code, const T* __restrict__ gadd, T* __restrict__ gin) {
   extern __shared__ float acc[];  // [HW][CW]
   const int c0 = blockIdx.x * CW, b = blockIdx.y;
-  for (int i = threadIdx.x; i < HW * CW; i += blockDim.x) acc[i] = 0.f;
+  // the slab starts from the feature map's other gradient (gadd: the RPN head's), if any; one
+  // pixel (CW channels, one vector access) per thread and iteration
+#pragma unroll 4
+  for (int p = threadIdx.x; p < HW; p += blockDim.x) {
+    float v[CW];
+    if (gadd) ldv<CW>(gadd + ((int64_t)b * HW + p) * C + c0, v, code);
+    else
+#pragma unroll
+      for (int k = 0; k < CW; ++k) v[k] = 0.f;
+#pragma unroll
+    for (int k = 0; k < CW; ++k) acc[p * CW + k] = v[k];
+  }
   __syncthreads();
   const int nb = R * PHW;
   for (int i = threadIdx.x; i < nb; i += blockDim.x) {
@@ -184,20 +233,19 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
       if (a[k] >= 0 && a[k] < HW && g[k] != 0.f) atomicAdd(&acc[a[k] * CW + k], g[k]);
   }
   __syncthreads();
+#pragma unroll 4
   for (int p = threadIdx.x; p < HW; p += blockDim.x) {
-    T* o = gin + ((int64_t)b * HW + p) * C + c0;
+    float v[CW];
 #pragma unroll
-    for (int k = 0; k < CW; ++k) {
-      if constexpr (sizeof(T) == 2) o[k] = f32_to_h16(acc[p * CW + k], code);
-      else o[k] = acc[p * CW + k];
-    }
+    for (int k = 0; k < CW; ++k) v[k] = acc[p * CW + k];
+    stv<CW>(gin + ((int64_t)b * HW + p) * C + c0, v, code);
   }
 }
 
 constexpr int kRoiBwdLds = 150 * 1024;
 
 int roi_pool_bwd_lds(const void* grad_out, int code, const int32_t* argmax, const float* rois, int R, int PH, int PW,
-                     int B, int H, int W, int C, void* grad_in, hipStream_t st) {
+                     int B, int H, int W, int C, void* grad_in, hipStream_t st, const void* grad_add) {
   const int HW = H * W;
   int cw = 0;
   if (C % 4 == 0 && (int64_t)HW * 4 * 4 <= kRoiBwdLds) cw = 4;
@@ -215,7 +263,7 @@ int roi_pool_bwd_lds(const void* grad_out, int code, const int32_t* argmax, cons
       attr = true;                                                                                            \
     }                                                                                                         \
     roi_pool_bwd_lds_kernel<CW_, T_><<<grid, 256, lds, st>>>((const T_*)grad_out, argmax, rois, R, PH * PW, HW, C, \
-                                                             code, (T_*)grad_in);                            \
+                                                             code, (const T_*)grad_add, (T_*)grad_in);       \
   } while (0)
   if (code) {
     if (cw == 4) MXR_ROI_BWD(4, uint16_t);

@@ -75,8 +75,9 @@ void roi_pool_fwd(const void* feat, int bf16, int B, int H, int W, int C, const 
 // grad_in fp32 NHWC (B, H, W, C), must be zeroed; grad_out (R, PH, PW, C) bf16/fp32.
 // LDS-accumulated backward straight into grad_in (B, H, W, C) of the grad_out dtype (code: 0 fp32,
 // 1 bf16, 2 fp16); -1 when the H x W slab does not fit LDS (use roi_pool_bwd)
+// grad_add (nullable, NHWC like grad_in): another gradient of the feature map, added in the kernel
 int roi_pool_bwd_lds(const void* grad_out, int code, const int32_t* argmax, const float* rois, int R, int PH, int PW,
-                     int B, int H, int W, int C, void* grad_in, hipStream_t st);
+                     int B, int H, int W, int C, void* grad_in, hipStream_t st, const void* grad_add = nullptr);
 void roi_pool_bwd(const void* grad_out, int bf16, const int32_t* argmax, const float* rois, int R,
                   int PH, int PW, int B, int H, int W, int C, float* grad_in, hipStream_t st);
 // fp32 -> bf16 / fp32 copy-convert helper (n elements)

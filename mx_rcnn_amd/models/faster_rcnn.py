@@ -25,6 +25,7 @@ import torch.nn.functional as F
 from ..config import config as _global_cfg, snapshot
 from ..utils import profiler as prof
 from ..ops import anchor_target, proposal, proposal_target, roi_pool
+from ..ops._ext import const_tensor
 from ..ops.head import rpn_head
 from ..ops.losses import combine_losses, rpn_softmax_ce, smooth_l1, softmax_ce
 from .layers import Conv
@@ -144,11 +145,11 @@ class FasterRCNN(nn.Module):
         return self.trunk.feat_shape(h, w)
 
     # ------------------------------------------------------------------ pieces
-    def _proposal(self, rpn_cls, rpn_bbox, im_info, key, is_prob=False):
+    def _proposal(self, rpn_cls, rpn_bbox, im_info, key, is_prob=False, after_mask=None):
         c = self.cfg[key]
         return proposal(rpn_cls.detach(), rpn_bbox.detach(), im_info, self.feat_stride, self.anchor_scales,
                         self.anchor_ratios, c.RPN_PRE_NMS_TOP_N, c.RPN_POST_NMS_TOP_N, c.RPN_NMS_THRESH,
-                        c.RPN_MIN_SIZE, is_train=(key == 'TRAIN'), is_prob=is_prob)
+                        c.RPN_MIN_SIZE, is_train=(key == 'TRAIN'), is_prob=is_prob, after_mask=after_mask)
 
     def _anchor_target_async(self, data, im_info, gt_boxes, n_gt):
         """Start the RPN anchor-target assignment (which needs only the image shape and the gt
@@ -220,35 +221,88 @@ class FasterRCNN(nn.Module):
         return cls_loss, bbox_loss, cls_prob
 
     # ------------------------------------------------------------------ modes
+    def _early_rpn_backward(self, data):
+        """Run the RPN branch's backward before the proposal chain finishes (e2e training on the
+        GPU).  The proposal chain -- decode, top-k, NMS, RoI sampling -- is a few hundred us of
+        single-workgroup kernels with the rest of the chip idle, and nothing in the RPN losses'
+        backward depends on it (proposals are not differentiable), so it runs on its own stream
+        while the compute stream does the RPN head's backward; the head's feature gradient then
+        enters the trunk through the RoI-pooling backward kernel (``grad_add``)."""
+        return (data.is_cuda and torch.is_grad_enabled() and os.environ.get('MXR_EARLY_RPN_BWD', '1') != '0'
+                and os.environ.get('MXR_AUX_STREAM', '1') != '0')
+
+    def _proposal_target_async(self, rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt):
+        """Proposal + proposal target on the proposal stream; returns a join -> targets dict."""
+        main = torch.cuda.current_stream()
+        ps = _aux_stream(rpn_cls.device, 'proposal')
+        ps.wait_stream(main)
+
+        def mask_done():
+            # the compute stream resumes once the (all-CU) NMS bitmask is built: its RPN backward
+            # then shares the chip only with the single-workgroup NMS reduce and RoI sampling
+            main.wait_stream(ps)
+        with torch.cuda.stream(ps):
+            rois, _ = self._proposal(rpn_cls, rpn_bbox, im_info, 'TRAIN', after_mask=mask_done)
+            pt = proposal_target(rois, gt_boxes, n_gt, self.num_classes, cfg=self.cfg, is_train=True)
+
+        def join():
+            main.wait_stream(ps)
+            for t in pt.values():
+                if torch.is_tensor(t):
+                    t.record_stream(main)
+            return pt
+        return join
+
     def train_e2e(self, data, im_info, gt_boxes, n_gt):
         """Approximate joint training step forward.  Returns dict with 'loss' (to backward)
         and the metric tensors of the reference's six metrics (rcnn/metric.py)."""
         at_join = self._anchor_target_async(data, im_info, gt_boxes, n_gt)
+        early = self._early_rpn_backward(data)
         with prof.range('trunk'):
             feat = self.trunk(data)
+        # early RPN backward: the RPN head reads a detached alias of the feature map, so the main
+        # backward (from the R-CNN losses) does not revisit it
+        feat_rpn = feat.detach().requires_grad_() if early else feat
         with prof.range('rpn'):
-            rpn_cls, rpn_bbox = self.rpn(feat)
+            rpn_cls, rpn_bbox = self.rpn(feat_rpn)
         with prof.range('anchor_target+rpn_loss'):
             rpn_losses = self._rpn_losses_async(rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt, at_join)
-        with prof.range('proposal'):
-            rois, _ = self._proposal(rpn_cls, rpn_bbox, im_info, 'TRAIN')
-        with prof.range('proposal_target'):
-            pt = proposal_target(rois, gt_boxes, n_gt, self.num_classes, cfg=self.cfg, is_train=True)
+        d_feat = None
+        if early:
+            with prof.range('proposal'):  # issue only: the chain runs on the proposal stream
+                pt_join = self._proposal_target_async(rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt)
+            rpn_cls_loss, rpn_bbox_loss, at = rpn_losses()
+            with prof.range('rpn_backward'):
+                pre = getattr(self, 'pre_backward', None)
+                if pre is not None:
+                    pre()  # e.g. the trainer's dgrad filter-cache join
+                one = const_tensor([1.0], data.device).reshape(())
+                torch.autograd.backward([rpn_cls_loss, rpn_bbox_loss], [one, one])
+                d_feat = feat_rpn.grad
+            pt = pt_join()
+        else:
+            with prof.range('proposal'):
+                rois, _ = self._proposal(rpn_cls, rpn_bbox, im_info, 'TRAIN')
+            with prof.range('proposal_target'):
+                pt = proposal_target(rois, gt_boxes, n_gt, self.num_classes, cfg=self.cfg, is_train=True)
         with prof.range('roi_pool'):
-            pooled = roi_pool(feat, pt['rois'], (7, 7), 1.0 / self.feat_stride)
+            pooled = roi_pool(feat, pt['rois'], (7, 7), 1.0 / self.feat_stride, grad_add=d_feat)
         with prof.range('head'):
             cls_score, bbox_pred = self.head(pooled)
         with prof.range('head_loss'):
             cls_loss, bbox_loss, cls_prob = self._head_losses(cls_score, bbox_pred, pt['label'], pt['bbox_target'],
                                                               pt['bbox_inside_weight'], pt['bbox_outside_weight'])
-        rpn_cls_loss, rpn_bbox_loss, at = rpn_losses()
+        if not early:
+            rpn_cls_loss, rpn_bbox_loss, at = rpn_losses()
         B = data.shape[0]
         R = cls_score.shape[0]
         # 'loss' carries the gradients (each loss applies its own grad_scale in backward); its value
         # mixes normalised and summed terms like the reference's outputs.  'objective' is the
         # value of the function actually being minimised.  One launch for both (+ the trainer's
-        # non-finite counter when it handed one over).
-        loss, obj = combine_losses([rpn_cls_loss, rpn_bbox_loss, cls_loss, bbox_loss],
+        # non-finite counter when it handed one over).  After an early RPN backward the RPN terms
+        # enter only the value.
+        r_terms = [rpn_cls_loss.detach(), rpn_bbox_loss.detach()] if early else [rpn_cls_loss, rpn_bbox_loss]
+        loss, obj = combine_losses(r_terms + [cls_loss, bbox_loss],
                                    [1.0, 1.0, 1.0, 1.0 / float(self.cfg.TRAIN.BATCH_SIZE)], self.nonfinite_counter)
         return {'loss': loss, 'objective': obj, 'rpn_cls_loss': rpn_cls_loss, 'rpn_bbox_loss': rpn_bbox_loss,
                 'cls_loss': cls_loss, 'bbox_loss': bbox_loss, 'cls_prob': cls_prob, 'label': pt['label'],
@@ -297,11 +351,11 @@ class FasterRCNN(nn.Module):
 _AUX = {}
 
 
-def _aux_stream(device):
-    s = _AUX.get(device.index)
+def _aux_stream(device, role='aux'):
+    s = _AUX.get((device.index, role))
     if s is None:
         s = torch.cuda.Stream(device=device)
-        _AUX[device.index] = s
+        _AUX[(device.index, role)] = s
     return s
 
 

@@ -109,9 +109,9 @@ class ResidualUnit(nn.Module):
             return False
         convs = [self.conv1, self.conv2] + ([self.conv3] if self.bottle_neck else [])
         if not self.dim_match:
-            convs.append(self.sc)
-        return all(c.weight.dtype == x.dtype and c.weight.shape[0] % 64 == 0 and c.weight.shape[1] % 64 == 0 and
-                   igemm_eligible(x, c.weight, c.stride, c.pad) for c in convs)
+            convs.append(self.sc)  # the strided 1x1 projection reads act1 directly (no subsampled copy)
+        return igemm_eligible(x, self.conv1.weight, self.conv1.stride, self.conv1.pad) and all(
+            c.weight.dtype == x.dtype and c.weight.shape[0] % 64 == 0 and c.weight.shape[1] % 64 == 0 for c in convs)
 
     def forward_fused(self, x, act1=None, next_bn=None):
         """-> (unit output, next unit's act1 or None).  act1: this unit's bn1(x) if already

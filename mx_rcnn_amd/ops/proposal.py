@@ -60,12 +60,13 @@ def _decode_ref(cls, dlt, im_info, base, feat_stride, min_size, crop, is_prob):
 
 def proposal(cls, bbox_deltas, im_info, feat_stride=16, scales=(8, 16, 32), ratios=(0.5, 1, 2),
              pre_nms_top_n=12000, post_nms_top_n=6000, nms_thresh=0.7, min_size=16, is_train=False,
-             is_prob=False, generator=None):
+             is_prob=False, generator=None, after_mask=None):
     """RPN outputs -> (rois (B, post, 5) fp32 [b, x1, y1, x2, y2], scores (B, post)).
 
     cls: (B, 2A, H, W) logits (or probabilities with is_prob=True), bbox_deltas (B, 4A, H, W),
     im_info (B, 3) = [height, width, scale] on the same device.  No gradient flows back
-    (the reference's backward writes zeros).
+    (the reference's backward writes zeros).  after_mask: called (GPU) between the NMS bitmask
+    and the serial NMS reduce, e.g. to record an event other streams start from.
     """
     with torch.no_grad():
         dev = cls.device
@@ -98,7 +99,11 @@ def proposal(cls, bbox_deltas, im_info, feat_stride=16, scales=(8, 16, 32), rati
         post = int(post_nms_top_n) if post_nms_top_n > 0 else P
         rand_u = torch.rand(B, post, device=dev, generator=generator)
         if cls.is_cuda:
-            rois, scores, _, _ = C.nms_proposals(sboxes, skeys, n_valid, float(nms_thresh), post, rand_u)
+            mask = None
+            if after_mask is not None:
+                mask = C.nms_mask_build(sboxes, n_valid, float(nms_thresh))
+                after_mask()
+            rois, scores, _, _ = C.nms_proposals(sboxes, skeys, n_valid, float(nms_thresh), post, rand_u, mask)
             return rois, scores
         rois = torch.zeros(B, post, 5)
         scores = torch.zeros(B, post)

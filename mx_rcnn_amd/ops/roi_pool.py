@@ -59,8 +59,9 @@ def roi_pool_ref(feat, rois, PH, PW, scale):
 
 class _RoIPool(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, feat, rois, PH, PW, scale):
+    def forward(ctx, feat, rois, PH, PW, scale, grad_add=None):
         B, C, H, W = feat.shape
+        ctx.grad_add = grad_add
         rois = rois.float().contiguous()
         if feat.is_cuda:
             ext = need_ext()
@@ -79,9 +80,13 @@ class _RoIPool(torch.autograd.Function):
     def backward(ctx, gout):
         arg, rois = ctx.saved_tensors
         B, C, H, W = ctx.shape
+        ga = ctx.grad_add
         if gout.is_cuda:
             ext = need_ext()
-            gin = ext.roi_pool_bwd(gout, arg, rois, B, H, W)
+            if ga is not None:
+                ga = ga.to(gout.dtype).contiguous(memory_format=torch.channels_last)
+            gin = ext.roi_pool_bwd(gout, arg, rois, B, H, W, ga)
+            ga = None  # added in the kernel
         elif ext_available():  # C++ twin: channel-parallel scatter, deterministic sum order
             gin = need_ext().roi_pool_bwd_cpu(gout, arg, rois, B, H, W).to(gout.dtype)
         else:
@@ -97,9 +102,14 @@ class _RoIPool(torch.autograd.Function):
                 flat = (torch.arange(C)[:, None] * H * W + a[r].clamp_min(0))[m]
                 gin[b].index_add_(0, flat, g[r][m])
             gin = gin.reshape(B, C, H, W).to(gout.dtype)
-        return gin, None, None, None, None
+        if ga is not None:
+            gin = gin + ga.to(gin.dtype)
+        ctx.grad_add = None
+        return gin, None, None, None, None, None
 
 
-def roi_pool(feat, rois, pooled_size=(7, 7), spatial_scale=0.0625):
-    """feat (B, C, H, W), rois (R, 5) -> (R, C, PH, PW) (channels_last on GPU)."""
-    return _RoIPool.apply(feat, rois, int(pooled_size[0]), int(pooled_size[1]), float(spatial_scale))
+def roi_pool(feat, rois, pooled_size=(7, 7), spatial_scale=0.0625, grad_add=None):
+    """feat (B, C, H, W), rois (R, 5) -> (R, C, PH, PW) (channels_last on GPU).  grad_add: a
+    gradient of ``feat`` from elsewhere (B, C, H, W), added to the pooling's input gradient in
+    the backward kernel -- the early RPN-head backward's (models/faster_rcnn.py)."""
+    return _RoIPool.apply(feat, rois, int(pooled_size[0]), int(pooled_size[1]), float(spatial_scale), grad_add)

@@ -494,34 +494,46 @@ def _train_stage(cuda, n_units=3, cin=512, cout=1024):
 def test_train_units_match_module_path(cuda, monkeypatch):
     """The RoI-head stage (batch-statistics BNs) through the fused train-unit op -- statistics
     in the conv epilogues, BN backward in the dgrad epilogues + dx_apply -- vs the per-module
-    path (MXR_TRAIN_UNIT=0), including the head bn1 fed by the last unit's partials."""
+    path (MXR_TRAIN_UNIT=0), including the head bn1 fed by the last unit's partials.  Both bf16
+    paths are scored against an fp32 CPU run of the same stage: the fused path's error may not
+    exceed the module path's by more than bf16 noise."""
     import copy
     from mx_rcnn_amd.models.resnet import run_stage_parts
     st0, tail0 = _train_stage(cuda)
     g = torch.Generator().manual_seed(9)
     x0 = torch.randn(16, 512, 8, 8, generator=g).bfloat16()
+    d0 = torch.randn(16, 1024, 4, 4, generator=torch.Generator().manual_seed(7)).bfloat16()
+
+    def run(st, tail, dev, dtype):
+        x = x0.to(dev, dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
+        y, parts = run_stage_parts(st, x, tail)
+        out = tail(y, parts=parts)
+        out.backward(d0.to(dev, out.dtype).contiguous(memory_format=torch.channels_last))
+        grads = {n: p.grad.float().cpu().clone() for n, p in list(st.named_parameters()) +
+                 [('tail.' + n, p) for n, p in tail.named_parameters()] if p.grad is not None}
+        stats = {n: b.float().cpu().clone() for n, b in list(st.named_buffers()) +
+                 [('tail.' + n, b) for n, b in tail.named_buffers()]}
+        return out.detach().float().cpu(), x.grad.float().cpu(), grads, stats, parts
+
+    ref = run(copy.deepcopy(st0).cpu().float(), copy.deepcopy(tail0).cpu().float(), 'cpu', torch.float32)
     res = []
     for flag in ('0', '1'):
         monkeypatch.setenv('MXR_TRAIN_UNIT', flag)
-        st, tail = copy.deepcopy(st0), copy.deepcopy(tail0)
-        x = _cl(x0, cuda).requires_grad_()
-        y, parts = run_stage_parts(st, x, tail)
-        assert (parts is not None) == (flag == '1')
-        out = tail(y, parts=parts)
-        gen = torch.Generator().manual_seed(7)
-        out.backward(_cl(torch.randn(out.shape, generator=gen).bfloat16(), cuda))
+        r = run(copy.deepcopy(st0), copy.deepcopy(tail0), cuda, torch.bfloat16)
+        assert (r[4] is not None) == (flag == '1')
         torch.cuda.synchronize()
-        grads = {n: p.grad.float().clone() for n, p in list(st.named_parameters()) + [('tail.' + n, p) for n, p in
-                                                                                      tail.named_parameters()]
-                 if p.grad is not None}
-        stats = {n: b.float().clone() for n, b in list(st.named_buffers()) + [('tail.' + n, b) for n, b in
-                                                                              tail.named_buffers()]}
-        res.append((out.detach().float(), x.grad.float(), grads, stats))
-    (oa, xa, ga, sa), (ob, xb, gb, sb) = res
-    assert _rel(ob, oa) <= 2e-2
-    assert _rel(xb, xa) <= 0.1
-    assert set(ga) == set(gb), set(ga) ^ set(gb)
+        res.append(r)
+    (oa, xa, ga, sa, _), (ob, xb, gb, sb, _) = res
+    o_r, x_r, g_r, s_r, _ = ref
+
+    def close(b, a, r, what):
+        ea, eb = _rel(a, r), _rel(b, r)
+        assert eb <= max(1.25 * ea, 0.03), (what, eb, ea)
+
+    close(ob, oa, o_r, 'out')
+    close(xb, xa, x_r, 'dx')
+    assert set(ga) == set(gb) == set(g_r), set(ga) ^ set(gb)
     for n in ga:
-        assert _rel(gb[n], ga[n]) <= 0.1, (n, _rel(gb[n], ga[n]))
+        close(gb[n], ga[n], g_r[n], n)
     for n in sa:
-        assert _rel(sb[n], sa[n]) <= 1e-2, (n, _rel(sb[n], sa[n]))
+        close(sb[n], sa[n], s_r[n], n)

@@ -39,6 +39,9 @@ def parse_args(argv=None):
     ap.add_argument('--grad-comm', default='fp32', choices=['fp32', 'bf16'],
                     help='all-reduce wire dtype of the gradient buckets (fp32 = the reference kvstore sum)')
     ap.add_argument('--pool', type=int, default=4, help='distinct synthetic batches cycled')
+    ap.add_argument('--train-mode', default='e2e', choices=['e2e', 'rpn', 'rcnn'],
+                    help='e2e (headline) or one stage of 4-step alternate training (BASELINE config 4): '
+                         'rpn = RPN-only step, rcnn = Fast R-CNN step on 128 given RoIs per image')
     return ap.parse_args(argv)
 
 
@@ -75,6 +78,32 @@ def synthetic_batch(n_img, h, w, num_classes, device, gen, max_gt=20):
             'n_gt': n_gt.to(device)}
 
 
+def rcnn_batch(b, num_classes, rois_per_image, gen, fg_fraction=0.25):
+    """A Fast R-CNN step input of the alternate scheme's shape (tools/train_rcnn.py): per image
+    ``rois_per_image`` RoIs (the proposal-target sample of precomputed proposals), fg first with
+    one class-specific regression target each, background after."""
+    n, _, h, w = b['data'].shape
+    R = n * rois_per_image
+    wh = torch.rand(R, 2, generator=gen) * min(300.0, 0.5 * min(h, w)) + 16
+    x1 = torch.rand(R, generator=gen) * (w - wh[:, 0] - 1)
+    y1 = torch.rand(R, generator=gen) * (h - wh[:, 1] - 1)
+    img = torch.arange(n).repeat_interleave(rois_per_image).float()
+    rois = torch.stack([img, x1, y1, x1 + wh[:, 0], y1 + wh[:, 1]], 1)
+    label = torch.zeros(n, rois_per_image, dtype=torch.int32)
+    nfg = int(rois_per_image * fg_fraction)
+    label[:, :nfg] = torch.randint(1, num_classes, (n, nfg), generator=gen).to(torch.int32)
+    label = label.reshape(-1)
+    tgt = torch.zeros(R, 4 * num_classes)
+    inside = torch.zeros(R, 4 * num_classes)
+    fg = (label > 0).nonzero().reshape(-1)
+    cols = (4 * label[fg].long()).unsqueeze(1) + torch.arange(4)
+    tgt[fg.unsqueeze(1), cols] = torch.randn(len(fg), 4, generator=gen) * 0.5
+    inside[fg.unsqueeze(1), cols] = 1.0
+    dev = b['data'].device
+    return {'data': b['data'], 'rois': rois.to(dev), 'label': label.to(dev), 'bbox_target': tgt.to(dev),
+            'bbox_inside_weight': inside.to(dev), 'bbox_outside_weight': inside.clone().to(dev)}
+
+
 def main():
     args = parse_args()
     rank, world, local_rank, device = pdist.init_distributed()
@@ -83,20 +112,26 @@ def main():
     h, w = [int(v) for v in args.image.lower().split('x')]
     cfg = snapshot()
     # end2end config mutation (train_end2end.py:25-32)
-    cfg.TRAIN.BG_THRESH_LO = 0.0
-    cfg.TRAIN.HAS_RPN = True
-    cfg.END2END = 1
-    cfg.TRAIN.BBOX_NORMALIZATION_PRECOMPUTED = True
+    if args.train_mode == 'e2e':
+        cfg.TRAIN.BG_THRESH_LO = 0.0
+        cfg.TRAIN.HAS_RPN = True
+        cfg.END2END = 1
+        cfg.TRAIN.BBOX_NORMALIZATION_PRECOMPUTED = True
+    elif args.train_mode == 'rpn':  # tools/train_rpn.py
+        cfg.TRAIN.HAS_RPN = True
+        cfg.END2END = 0
     cfg.TRAIN.IMS_PER_BATCH = args.ims_per_gpu
     torch.manual_seed(1234 + rank)
     model = FasterRCNN(args.network, args.num_classes, cfg=cfg)
     gen = torch.Generator().manual_seed(4321 + rank)
     pool = [synthetic_batch(args.ims_per_gpu, h, w, args.num_classes, device, gen) for _ in range(args.pool)]
+    if args.train_mode == 'rcnn':
+        pool = [rcnn_batch(b, args.num_classes, cfg.TRAIN.BATCH_SIZE, gen) for b in pool]
     if args.network.startswith('resnet'):
         model.to(device).calibrate_bn(pool[0]['data'])  # stand-in for pretrained BN statistics
     fixed = ['conv0', 'stage1', 'stage2', 'bn_data', 'bn0'] if args.network.startswith('resnet') else ['conv1', 'conv2']
     dtype = torch.bfloat16 if (args.dtype == 'bf16' and device.type == 'cuda') else torch.float32
-    trainer = Trainer(model, 'e2e', fixed_param_prefix=fixed, lr=0.001, momentum=0.9, wd=0.0005, clip_gradient=1.0,
+    trainer = Trainer(model, args.train_mode, fixed_param_prefix=fixed, lr=0.001, momentum=0.9, wd=0.0005, clip_gradient=1.0,
                       rescale_grad=1.0, compute_dtype=dtype, device=device, bucket_mb=args.bucket_mb,
                       grad_comm_dtype=torch.float32 if args.grad_comm == 'fp32' else torch.bfloat16)
 
@@ -146,6 +181,8 @@ def main():
     value = imgs / elapsed
     if rank == 0:
         metric = METRIC if args.network == 'resnet101' else 'imgs/sec e2e train %s Faster R-CNN' % args.network
+        if args.train_mode != 'e2e':
+            metric = 'imgs/sec alternate-stage %s train %s' % (args.train_mode, args.network)
         rec = {'metric': metric, 'value': round(value, 3), 'unit': 'images/s', 'n_gpus': world,
                'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
                'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
@@ -153,7 +190,7 @@ def main():
                'data': 'synthetic (random %dx%d images, 1-20 random gt boxes, random-init weights)' % (h, w),
                'config': {'model': '%s-faster-rcnn%s' % (args.network, '-c4' if args.network.startswith('resnet') else ''), 'global_batch': args.ims_per_gpu * world,
                           'seq_len': None, 'image_hw': [h, w], 'num_classes': args.num_classes,
-                          'ims_per_gpu': args.ims_per_gpu, 'parallelism': 'dp%d' % world,
+                          'ims_per_gpu': args.ims_per_gpu, 'train_mode': args.train_mode, 'parallelism': 'dp%d' % world,
                           'rpn_pre_post_nms': [cfg.TRAIN.RPN_PRE_NMS_TOP_N, cfg.TRAIN.RPN_POST_NMS_TOP_N],
                           'rois_per_image': cfg.TRAIN.BATCH_SIZE, 'exec': mode,
                           'objective_first_last': [round(loss0, 4), round(loss1, 4)],

@@ -988,6 +988,38 @@ Tensor avgpool_bwd(const Tensor& dy, int64_t H, int64_t W) {
   return dx;
 }
 
+// ---- stem conv (stem.hip) ------------------------------------------------------------------------
+Tensor stem_conv(const Tensor& x, const Tensor& in_scale, const Tensor& in_shift, const Tensor& wp,
+                 const Tensor& oscale, const Tensor& oshift, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
+                 bool relu) {
+  CHECK_DEV(x); CHECK_DEV(in_scale); CHECK_DEV(in_shift); CHECK_DEV(wp); CHECK_DEV(oscale); CHECK_DEV(oshift);
+  TORCH_CHECK((x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf) && x.dim() == 4 && x.size(1) == 3 &&
+                  x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "stem_conv: x must be channels_last bf16 / fp16 (N,3,H,W)");
+  const int64_t K = KH * KW * 3, KP = (K + 31) / 32 * 32;
+  TORCH_CHECK(wp.scalar_type() == x.scalar_type() && wp.dim() == 2 && wp.size(0) == 64 && wp.size(1) == KP &&
+                  wp.is_contiguous(),
+              "stem_conv: wp must be a contiguous (64, KP) filter of x's dtype");
+  for (const Tensor* t : {&in_scale, &in_shift})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() == 3 && t->is_contiguous(), "stem_conv: in affine fp32 (3)");
+  for (const Tensor* t : {&oscale, &oshift})
+    TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() == 64 && t->is_contiguous(), "stem_conv: out affine fp32 (64)");
+  TORCH_CHECK(pad >= 0 && pad < KH && pad < KW, "stem_conv: pad");
+  const int N = (int)x.size(0), H = (int)x.size(2), W = (int)x.size(3);
+  const int Ho = (int)((H + 2 * pad - KH) / stride + 1), Wo = (int)((W + 2 * pad - KW) / stride + 1);
+  TORCH_CHECK(Ho > 0 && Wo > 0, "stem_conv: empty output");
+  DevGuard g(x.device());
+  Tensor y = at::empty({N, 64, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  const int rc = mxr::stem_conv(reinterpret_cast<const uint16_t*>(x.data_ptr()), in_scale.data_ptr<float>(),
+                                in_shift.data_ptr<float>(), reinterpret_cast<const uint16_t*>(wp.data_ptr()),
+                                oscale.data_ptr<float>(), oshift.data_ptr<float>(),
+                                reinterpret_cast<uint16_t*>(y.data_ptr()), N, H, W, Ho, Wo, (int)KH, (int)KW,
+                                (int)stride, (int)pad, relu ? 1 : 0, dcode(x), cur_stream());
+  TORCH_CHECK(rc == 0, "stem_conv: unsupported geometry (7x7/2 and 3x3/1 only) or grid too large");
+  LAUNCH_CHECK("stem_conv");
+  return y;
+}
+
 // ---- small-head backward / channel sum (head_bwd.hip) --------------------------------------------
 bool al16(const Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) & 15) == 0; }
 
@@ -1667,6 +1699,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("s"), py::arg("p"));
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("stem_conv", &stem_conv, py::arg("x"), py::arg("in_scale"), py::arg("in_shift"), py::arg("wp"),
+        py::arg("oscale"), py::arg("oshift"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
+        py::arg("relu"));
   m.def("philox_uniform", &philox_uniform_cpu, py::arg("seed"), py::arg("step"), py::arg("n"),
         "host twin of the fused-dropout generator: uniforms of elements 0..n-1 (CPU float tensor)");
   m.def("bn_train_fwd", &bn_train_fwd);

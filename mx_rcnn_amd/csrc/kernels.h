@@ -237,6 +237,11 @@ int maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int
                 int k, int s, int p, int code, hipStream_t st);
 int avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, int code, hipStream_t st);
 int avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, int code, hipStream_t st);
+// stem conv (stem.hip): x (N,H,W,3) 16-bit NHWC, wp (64, KP) packed filter, k = (fr*KW+fc)*3+c;
+// y (N,Ho,Wo,64) = relu?(conv(x*in_scale+in_shift) * oscale + oshift).  Geometries 7x7/2, 3x3/1.
+int stem_conv(const uint16_t* x, const float* in_scale, const float* in_shift, const uint16_t* wp, const float* oscale,
+              const float* oshift, uint16_t* y, int N, int H, int W, int Ho, int Wo, int KH, int KW, int stride,
+              int pad, int relu, int code, hipStream_t st);
 
 // ---- proposal pre-NMS top-k (topk.hip): keys (B, N), boxes (B, N, 4) -> the P best in stable
 // descending order; ws_key / ws_idx: B * P each

@@ -12,6 +12,7 @@ from ..ops.conv import igemm_eligible
 from ..ops.fused import conv_add, conv_add_bn_relu, conv_bn_relu, fused_unit
 from ..ops.head import fc_pair
 from ..ops.pool import global_avg_pool
+from ..ops.stem import stem_fusable, stem_conv
 from .layers import BatchNorm, Conv, Linear, max_pool
 
 
@@ -212,8 +213,19 @@ class ResNetTrunk(nn.Module):
         self.stage2 = _stage(2, units[1], filters[1], filters[2], bottle, bn_mom, bn_global)
         self.stage3 = _stage(3, units[2], filters[2], filters[3], bottle, bn_mom, bn_global)
 
+    def _stem_fused(self, x):
+        bd, b0 = self.bn_data, self.bn0
+        if getattr(bd, '_calibrate', False) or getattr(b0, '_calibrate', False):
+            return False
+        if self.training and not (bd.use_global_stats and b0.use_global_stats):
+            return False
+        return stem_fusable(x, self.conv0.weight, bd.gamma, bd.beta, b0.gamma, b0.beta)
+
     def forward(self, x):
-        x = self.bn0(self.conv0(self.bn_data(x)))
+        if self._stem_fused(x):  # one HIP launch (ops/stem.py)
+            x = stem_conv(x, self.conv0.weight, 2, 3, in_bn=self.bn_data, out_bn=self.bn0, relu=True)
+        else:
+            x = self.bn0(self.conv0(self.bn_data(x)))
         x = max_pool(x, 3, 2, 1)
         for st in (self.stage1, self.stage2, self.stage3):
             x = run_stage(st, x)

@@ -7,6 +7,7 @@ import torch.nn as nn
 
 from .layers import Conv, Linear, max_pool
 from ..ops.head import fc_pair
+from ..ops.stem import stem_fusable, stem_conv
 
 VGG_CFG = [(1, 2, 3, 64), (2, 2, 64, 128), (3, 3, 128, 256), (4, 3, 256, 512), (5, 3, 512, 512)]
 
@@ -26,7 +27,10 @@ class VGG16Trunk(nn.Module):
 
     def forward(self, x):
         for i, c in enumerate(self.convs):
-            x = c(x, relu=True)
+            if i == 0 and stem_fusable(x, c.weight, c.bias):  # one HIP launch (ops/stem.py)
+                x = stem_conv(x, c.weight, 1, 1, bias=c.bias, relu=True)
+            else:
+                x = c(x, relu=True)
             if i in self.pool_after:
                 x = max_pool(x, 2, 2)
         return x

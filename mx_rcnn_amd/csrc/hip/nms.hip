@@ -3,7 +3,12 @@
 // +1-pixel areas, boxes visited in descending score order).
 //
 // The suppression matrix is stored TRANSPOSED, one 64-bit word per (row block, box):
-//   maskT[rb][j] bit i  <=>  box rb*64+i (higher score, rb*64+i < j) suppresses box j.
+//   maskT[rb][j] bit i  <=>  box rb*64+i (higher score, rb*64+i < j) suppresses box j,
+// with the columns of each row block PAIRED: the words of boxes cb*64+l and (cb^1)*64+l sit
+// side by side (word index (cb>>1)*128 + 2l + (cb&1)), so one 16-B load per lane fetches lane l's
+// words of two column blocks.  The reducer streams the whole upper triangle through ONE CU,
+// whose address path costs about the same per wave-load at 8 and 16 B per lane: 16-B loads
+// halve the wave-loads (and the per-iteration time, which that path sets).
 // With lane = box j, "is j suppressed by any kept box of block rb" is a single
 // `ballot((maskT[rb][j] & kept[rb]) != 0)` -- the 64-bit word width IS the wave width, so the
 // serial part of greedy NMS runs on wave-wide bit operations instead of shuffles or atomics.
@@ -27,8 +32,16 @@
 namespace mxr {
 
 constexpr int NMS_HELPERS = 15;  // helper waves in the 1024-thread reducer
-constexpr int NMS_PF = 18;       // prefetched column blocks per helper lane (15 * 18 + 2 >= 256 blocks;
-                                 // farther columns take plain loads)
+constexpr int NMS_PF = 7;        // prefetched column-block PAIRS per helper lane (15 * 7 = 105 pairs
+                                 // >= 188 blocks of the 12000-box training NMS; farther pairs take
+                                 // plain loads)
+
+typedef unsigned long long u64x2 __attribute__((ext_vector_type(2)));
+
+// words per row block (column blocks padded to an even count)
+__host__ __device__ __forceinline__ int64_t nms_row_words(int nb) { return (int64_t)((nb + 1) >> 1) * 128; }
+// index of lane l's word of column block cb within a row block
+__device__ __forceinline__ int64_t nms_col(int cb, int l) { return (int64_t)(cb >> 1) * 128 + l * 2 + (cb & 1); }
 
 __global__ void __launch_bounds__(256)
 nms_mask_kernel(const float* __restrict__ boxes, const int32_t* __restrict__ n_valid, int P, int nb,
@@ -39,7 +52,7 @@ nms_mask_kernel(const float* __restrict__ boxes, const int32_t* __restrict__ n_v
   const int lane = threadIdx.x & 63;
   const int nv = min(n_valid[b], P);  // a count above P must not walk past the image's boxes
   const int row0 = rb * 64;
-  const int64_t Pp = (int64_t)nb * 64;
+  const int64_t Pp = nms_row_words(nb);
   __shared__ float4 rbox[64];
   __shared__ float rarea[64];
   const float4* bx = reinterpret_cast<const float4*>(boxes) + (int64_t)b * P;
@@ -62,7 +75,7 @@ nms_mask_kernel(const float* __restrict__ boxes, const int32_t* __restrict__ n_v
       if (iou_plus1(r.x, r.y, r.z, r.w, rarea[i], c.x, c.y, c.z, c.w, carea) > thresh) bits |= (1ull << i);
     }
   }
-  maskT[((int64_t)b * nb + rb) * Pp + j] = bits;
+  maskT[((int64_t)b * nb + rb) * Pp + nms_col(cb, lane)] = bits;
 }
 
 __global__ void __launch_bounds__(1024)
@@ -83,7 +96,7 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
   int32_t* keep_list = reinterpret_cast<int32_t*>(keptw + nb);
   const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int nv = min(n_valid[b], P);
-  const int64_t Pp = (int64_t)nb * 64;
+  const int64_t Pp = nms_row_words(nb);
   const uint64_t* mb = maskT + (int64_t)b * nb * Pp;
   for (int c = tid; c < nb; c += blockDim.x) {
     removed[c] = 0;
@@ -91,15 +104,15 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
   }
   if (tid < 2) s_nk[tid] = 0;
   const int nbv = (nv + 63) / 64;
-  // wave 0: words of block t (diag = maskT[t][j], wprev = maskT[t-1][j]); helpers: words of the
-  // column blocks of the next iteration.  Every prefetch is loaded into the variable it is
+  // wave 0: words of block t (diag = maskT[t][j], wprev = maskT[t-1][j]); helpers: the column
+  // block pairs of the next iteration.  Every prefetch is loaded into the variable it is
   // consumed from, AFTER the consumption: a loop-carried copy (x = x_next) would make the
   // compiler wait for the prefetch at the end of every iteration.
   uint64_t diag = 0, wprev = 0;
-  uint64_t pf[NMS_PF];
+  u64x2 pf[NMS_PF];
 #pragma unroll
-  for (int k = 0; k < NMS_PF; ++k) pf[k] = 0;
-  if (wave == 0 && nbv > 0) diag = mb[lane];
+  for (int k = 0; k < NMS_PF; ++k) pf[k] = u64x2{0ull, 0ull};
+  if (wave == 0 && nbv > 0) diag = mb[nms_col(0, lane)];
   __syncthreads();
   int t = 0;
   for (; t < nbv; ++t) {
@@ -118,11 +131,10 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
         if (next == kept) break;
         kept = next;
       }
-      // prefetch block t+1 (clamped in-range address on the last block)
-      const int jn = min(j + 64, (int)Pp - 1);
+      // prefetch block t+1 (clamped to an in-range word on the last block)
       const int tn = min(t + 1, nb - 1);
-      diag = mb[(int64_t)tn * Pp + jn];
-      wprev = mb[(int64_t)t * Pp + jn];
+      diag = mb[(int64_t)tn * Pp + nms_col(tn, lane)];
+      wprev = mb[(int64_t)t * Pp + nms_col(tn, lane)];
       const int nk = s_nk[t & 1];
       if (nk + __popcll(kept) > post) {  // keep only the lowest (post - nk) boxes of this block
         int need = post - nk;
@@ -144,36 +156,51 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
       if (t >= 1) {
         const uint64_t kp = keptw[t - 1];
         if (kp) {
+          // fold kept rows of block t-1 into columns c >= t+1 (c = t is wave 0's, via wprev);
+          // pair q holds columns 2q, 2q+1; the first pair may start at column t
+          const int q0 = (t + 1) >> 1;
 #pragma unroll
           for (int k = 0; k < NMS_PF; ++k) {
-            const int c = t + 1 + h + NMS_HELPERS * k;
-            if (c < nbv) {
-              const uint64_t bits = __ballot((pf[k] & kp) != 0ull);
+            const int c0 = 2 * (q0 + h + NMS_HELPERS * k);
+            if (c0 >= t + 1 && c0 < nbv) {
+              const uint64_t bits = __ballot((pf[k].x & kp) != 0ull);
               // ds_or_b64 without return: no LDS round trip on the helper's path
-              if (lane == 0 && bits) atomicOr(reinterpret_cast<unsigned long long*>(&removed[c]), bits);
+              if (lane == 0 && bits) atomicOr(reinterpret_cast<unsigned long long*>(&removed[c0]), bits);
+            }
+            if (c0 + 1 < nbv) {
+              const uint64_t bits = __ballot((pf[k].y & kp) != 0ull);
+              if (lane == 0 && bits) atomicOr(reinterpret_cast<unsigned long long*>(&removed[c0 + 1]), bits);
             }
           }
-          // column blocks beyond the prefetch window (> NMS_HELPERS * NMS_PF ahead: only when
-          // P > ~17K, e.g. the alternate-training proposal dump with pre-NMS = all anchors):
-          // plain loads of row block t-1, same fold
-          for (int c = t + 1 + h + NMS_HELPERS * NMS_PF; c < nbv; c += NMS_HELPERS) {
-            const uint64_t wv = mb[(int64_t)(t - 1) * Pp + (int64_t)c * 64 + lane];
-            const uint64_t bits = __ballot((wv & kp) != 0ull);
-            if (lane == 0 && bits) atomicOr(reinterpret_cast<unsigned long long*>(&removed[c]), bits);
+          // pairs beyond the prefetch window (only when P > ~13K, e.g. the alternate-training
+          // proposal dump with pre-NMS = all anchors): plain loads of row block t-1, same fold
+          for (int q = q0 + h + NMS_HELPERS * NMS_PF; 2 * q < nbv; q += NMS_HELPERS) {
+            const u64x2 wv = *reinterpret_cast<const u64x2*>(mb + (int64_t)(t - 1) * Pp + (int64_t)q * 128 + lane * 2);
+            const int c0 = 2 * q;
+            if (c0 >= t + 1) {
+              const uint64_t bits = __ballot((wv.x & kp) != 0ull);
+              if (lane == 0 && bits) atomicOr(reinterpret_cast<unsigned long long*>(&removed[c0]), bits);
+            }
+            if (c0 + 1 < nbv) {
+              const uint64_t bits = __ballot((wv.y & kp) != 0ull);
+              if (lane == 0 && bits) atomicOr(reinterpret_cast<unsigned long long*>(&removed[c0 + 1]), bits);
+            }
           }
         }
       }
-      // prefetch row block t for iteration t+1: only the columns t+2+h+15k < nbv.  One CU
-      // streams the whole triangle and every wave-load costs the CU's address path ~16 cycles,
-      // so unneeded slots must not issue at all.  hipcc waits vmcnt(0) after each guarded C++
-      // load, so the loads are inline asm ("+v": the slot keeps its register on the skipped path,
-      // no phi copy) and the helper waits for them explicitly before consuming (above).
-      const uint64_t* rowp = mb + (int64_t)t * Pp + (t + 2 + h) * 64 + lane;
+      // prefetch row block t for iteration t+1: the pairs q0' + h + 15k (q0' = (t+2)/2) whose
+      // first column is < nbv.  One CU streams the whole triangle and every wave-load costs the
+      // CU's address path about the same at 8 and 16 B per lane, so a slot fetches two column
+      // blocks and unneeded slots do not issue at all.  hipcc waits vmcnt(0) after each guarded
+      // C++ load, so the loads are inline asm ("+v": the slot keeps its registers on the skipped
+      // path, no phi copy) and the helper waits for them explicitly before consuming (above).
+      const int q0n = (t + 2) >> 1;
+      const uint64_t* rowp = mb + (int64_t)t * Pp + (int64_t)(q0n + h) * 128 + lane * 2;
 #pragma unroll
       for (int k = 0; k < NMS_PF; ++k) {
-        if (t + 2 + h + NMS_HELPERS * k < nbv) {
-          const uint64_t* src = rowp + NMS_HELPERS * 64 * k;
-          asm volatile("global_load_dwordx2 %0, %1, off" : "+v"(pf[k]) : "v"(src) : "memory");
+        if (2 * (q0n + h + NMS_HELPERS * k) < nbv) {
+          const uint64_t* src = rowp + NMS_HELPERS * 128 * k;
+          asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(pf[k]) : "v"(src) : "memory");
         }
       }
     }
@@ -204,8 +231,8 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
 }
 
 int64_t nms_mask_words(int B, int P) {
-  const int64_t nb = div_up(P, 64);
-  return (int64_t)B * nb * nb * 64;
+  const int nb = div_up(P, 64);
+  return (int64_t)B * nb * nms_row_words(nb);
 }
 
 void nms_mask(const float* boxes, const int32_t* n_valid, int B, int P, float thresh, uint64_t* mask,

@@ -22,7 +22,7 @@ void proposal_decode(const void* cls, int cls_bf16, int64_t cs0, int64_t cs1, in
 
 // ---- NMS (nms.hip) ----------------------------------------------------------
 // boxes (B, P, 4) sorted by descending score, n_valid (B) int32 on device.
-// mask workspace: nms_mask_words(B, P) uint64 (transposed: [B][nb][nb*64], nb = ceil(P/64)).
+// mask workspace: nms_mask_words(B, P) uint64 (transposed, column blocks paired: [B][nb][ceil(nb/2)*128], nb = ceil(P/64)).
 int64_t nms_mask_words(int B, int P);
 size_t nms_reduce_lds(int P, int post);
 void nms_mask(const float* boxes, const int32_t* n_valid, int B, int P, float thresh,

@@ -162,11 +162,15 @@ class FlatParamStore:
             need_ext().wt_flip_run(table, n_ent, tiles)
             refresh_sub_filters()
 
-    def refresh_dgrad_cache_async(self):
+    def refresh_dgrad_cache_async(self, zero_grad=False):
         """Rebuild the dgrad cache from the current weights on a side stream (concurrent with the
         forward pass, which does not read it); returns a callable that joins it into the compute
-        stream (call before the backward pass)."""
+        stream (call before the backward pass).  ``zero_grad``: clear the flat gradient buffers on
+        that side stream too, so the forward pass's first kernel depends on nothing issued in this
+        step (the gradients are first written after the join)."""
         if self._wt_table is None or self.device.type != 'cuda':
+            if zero_grad:
+                self.zero_grad()
             self.refresh_dgrad_cache()
             return lambda: None
         main = torch.cuda.current_stream(self.device)
@@ -175,6 +179,8 @@ class FlatParamStore:
         side = self._cache_stream
         side.wait_stream(main)
         with torch.cuda.stream(side):
+            if zero_grad:
+                self.zero_grad()
             self.refresh_dgrad_cache()
         return lambda: main.wait_stream(side)
 

@@ -79,8 +79,11 @@ class Trainer:
     def step_body(self, b):
         """The device work of one step (capturable)."""
         # the dgrad filter cache of the current weights, built beside the forward pass
-        cache_join = self.store.refresh_dgrad_cache_async()
-        self.store.zero_grad()
+        # (and the gradient clear), joined before the first backward kernel
+        zg_side = os.environ.get('MXR_ZERO_GRAD_SIDE', '1') != '0'
+        cache_join = self.store.refresh_dgrad_cache_async(zero_grad=zg_side)
+        if not zg_side:
+            self.store.zero_grad()
         # the optimizer runs bucket by bucket under the backward pass (parallel/reducer.py)
         self.reducer.prepare(sgd=(self.lr_t, self.momentum, self.wd, self.rescale, self.clip))
         # a model that starts part of its backward inside forward (the e2e graph's early RPN

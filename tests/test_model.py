@@ -135,6 +135,37 @@ def test_overlapped_sgd_matches_end_of_step_sgd(cuda, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_side_stream_grad_clear_matches_inline(cuda, monkeypatch):
+    """Clearing the flat gradients on the dgrad-cache side stream (MXR_ZERO_GRAD_SIDE=1, joined
+    before the first backward kernel) trains exactly like clearing them on the compute stream
+    before the forward pass, eager and graph-replayed."""
+    from mx_rcnn_amd.core.trainer import GraphedStep
+    fixed = ['conv0', 'stage1', 'stage2', 'bn_data', 'bn0']
+    b = {k: v.to(cuda) for k, v in _batch(320, 480).items()}
+
+    def run(side):
+        monkeypatch.setenv('MXR_ZERO_GRAD_SIDE', '1' if side else '0')
+        torch.manual_seed(0)
+        m = FasterRCNN('resnet50', 21, cfg=_cfg())
+        tr = Trainer(m, 'e2e', fixed_param_prefix=fixed, lr=0.01, device=cuda)
+        torch.manual_seed(10)
+        tr.step(b)
+        g = GraphedStep(tr, b, warmup=1)
+        for _ in range(2):
+            g(b)
+        torch.cuda.synchronize()
+        return tr.store.state_arrays(), [gr.grad.float().clone() for gr in tr.store.groups]
+
+    w1, g1 = run(True)
+    w0, g0 = run(False)
+    for k in w0:
+        assert torch.allclose(w1[k], w0[k], rtol=1e-3, atol=1e-5), k
+    for a, c in zip(g1, g0):
+        scale = c.abs().max().item() + 1e-12
+        assert (a - c).abs().max().item() <= 2e-2 * scale + 1e-7
+
+
+@pytest.mark.gpu
 def test_graph_capture_has_no_training_side_effects(cuda):
     """GraphedStep's warm-up runs real steps to settle workspaces; weights, momentum, bf16
     shadows and BN moving statistics must be exactly as before the capture (a new shape must

@@ -17,6 +17,7 @@ Design (MI355X-first):
   ``_gamma`` are decayed.
 """
 import logging
+import os
 
 import torch
 import torch.nn as nn
@@ -168,7 +169,7 @@ class FlatParamStore:
         stream (call before the backward pass).  ``zero_grad``: clear the flat gradient buffers on
         that side stream too, so the forward pass's first kernel depends on nothing issued in this
         step (the gradients are first written after the join)."""
-        if self._wt_table is None or self.device.type != 'cuda':
+        if self._wt_table is None or self.device.type != 'cuda' or os.environ.get('MXR_CACHE_SIDE', '1') == '0':
             if zero_grad:
                 self.zero_grad()
             self.refresh_dgrad_cache()

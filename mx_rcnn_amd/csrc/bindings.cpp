@@ -989,30 +989,52 @@ Tensor avgpool_bwd(const Tensor& dy, int64_t H, int64_t W) {
 }
 
 // ---- stem conv (stem.hip) ------------------------------------------------------------------------
-Tensor stem_conv(const Tensor& x, const Tensor& in_scale, const Tensor& in_shift, const Tensor& wp,
-                 const Tensor& oscale, const Tensor& oshift, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
-                 bool relu) {
-  CHECK_DEV(x); CHECK_DEV(in_scale); CHECK_DEV(in_shift); CHECK_DEV(wp); CHECK_DEV(oscale); CHECK_DEV(oshift);
+Tensor stem_conv(const Tensor& x, const Tensor& w, const std::vector<Tensor>& in_bn, double in_eps, bool in_fixg,
+                 const std::vector<Tensor>& out_bn, double out_eps, bool out_fixg, const c10::optional<Tensor>& bias,
+                 int64_t stride, int64_t pad, bool relu) {
+  CHECK_DEV(x); CHECK_DEV(w);
   TORCH_CHECK((x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf) && x.dim() == 4 && x.size(1) == 3 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "stem_conv: x must be channels_last bf16 / fp16 (N,3,H,W)");
-  const int64_t K = KH * KW * 3, KP = (K + 31) / 32 * 32;
-  TORCH_CHECK(wp.scalar_type() == x.scalar_type() && wp.dim() == 2 && wp.size(0) == 64 && wp.size(1) == KP &&
-                  wp.is_contiguous(),
-              "stem_conv: wp must be a contiguous (64, KP) filter of x's dtype");
-  for (const Tensor* t : {&in_scale, &in_shift})
-    TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() == 3 && t->is_contiguous(), "stem_conv: in affine fp32 (3)");
-  for (const Tensor* t : {&oscale, &oshift})
-    TORCH_CHECK(t->scalar_type() == at::kFloat && t->numel() == 64 && t->is_contiguous(), "stem_conv: out affine fp32 (64)");
+  TORCH_CHECK(w.scalar_type() == x.scalar_type() && w.dim() == 4 && w.size(0) == 64 && w.size(1) == 3,
+              "stem_conv: w must be a (64, 3, KH, KW) filter of x's dtype");
+  const int64_t KH = w.size(2), KW = w.size(3);
+  mxr::StemArgs a{};
+  a.w_sco = w.stride(0); a.w_sci = w.stride(1); a.w_skh = w.stride(2); a.w_skw = w.stride(3);
+  TORCH_CHECK(in_bn.empty() || in_bn.size() == 4, "stem_conv: in_bn = [] or [gamma, beta, mean, var]");
+  TORCH_CHECK(out_bn.empty() || out_bn.size() == 4, "stem_conv: out_bn = [] or [gamma, beta, mean, var]");
+  for (const Tensor& t : in_bn) {
+    CHECK_DEV(t);
+    TORCH_CHECK(t.scalar_type() == at::kFloat && t.numel() == 3 && t.is_contiguous(), "stem_conv: in_bn fp32 (3)");
+  }
+  for (const Tensor& t : out_bn) {
+    CHECK_DEV(t);
+    TORCH_CHECK(t.scalar_type() == at::kFloat && t.numel() == 64 && t.is_contiguous(), "stem_conv: out_bn fp32 (64)");
+  }
+  if (!in_bn.empty()) {
+    a.in_g = in_bn[0].data_ptr<float>(); a.in_b = in_bn[1].data_ptr<float>();
+    a.in_m = in_bn[2].data_ptr<float>(); a.in_v = in_bn[3].data_ptr<float>();
+  }
+  a.in_eps = (float)in_eps; a.in_fixg = in_fixg ? 1 : 0;
+  if (!out_bn.empty()) {
+    a.out_g = out_bn[0].data_ptr<float>(); a.out_b = out_bn[1].data_ptr<float>();
+    a.out_m = out_bn[2].data_ptr<float>(); a.out_v = out_bn[3].data_ptr<float>();
+  }
+  a.out_eps = (float)out_eps; a.out_fixg = out_fixg ? 1 : 0;
+  if (bias.has_value() && bias->defined()) {
+    CHECK_DEV((*bias));
+    TORCH_CHECK(bias->numel() == 64 && bias->is_contiguous(), "stem_conv: bias (64)");
+    a.bias = bias->data_ptr();
+    a.bias_code = dcode(*bias);
+  }
   TORCH_CHECK(pad >= 0 && pad < KH && pad < KW, "stem_conv: pad");
   const int N = (int)x.size(0), H = (int)x.size(2), W = (int)x.size(3);
   const int Ho = (int)((H + 2 * pad - KH) / stride + 1), Wo = (int)((W + 2 * pad - KW) / stride + 1);
   TORCH_CHECK(Ho > 0 && Wo > 0, "stem_conv: empty output");
   DevGuard g(x.device());
   Tensor y = at::empty({N, 64, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  const int rc = mxr::stem_conv(reinterpret_cast<const uint16_t*>(x.data_ptr()), in_scale.data_ptr<float>(),
-                                in_shift.data_ptr<float>(), reinterpret_cast<const uint16_t*>(wp.data_ptr()),
-                                oscale.data_ptr<float>(), oshift.data_ptr<float>(),
+  const int rc = mxr::stem_conv(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                reinterpret_cast<const uint16_t*>(w.data_ptr()), a,
                                 reinterpret_cast<uint16_t*>(y.data_ptr()), N, H, W, Ho, Wo, (int)KH, (int)KW,
                                 (int)stride, (int)pad, relu ? 1 : 0, dcode(x), cur_stream());
   TORCH_CHECK(rc == 0, "stem_conv: unsupported geometry (7x7/2 and 3x3/1 only) or grid too large");
@@ -1699,8 +1721,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("s"), py::arg("p"));
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
-  m.def("stem_conv", &stem_conv, py::arg("x"), py::arg("in_scale"), py::arg("in_shift"), py::arg("wp"),
-        py::arg("oscale"), py::arg("oshift"), py::arg("KH"), py::arg("KW"), py::arg("stride"), py::arg("pad"),
+  m.def("stem_conv", &stem_conv, py::arg("x"), py::arg("w"), py::arg("in_bn"), py::arg("in_eps"), py::arg("in_fixg"),
+        py::arg("out_bn"), py::arg("out_eps"), py::arg("out_fixg"), py::arg("bias"), py::arg("stride"), py::arg("pad"),
         py::arg("relu"));
   m.def("philox_uniform", &philox_uniform_cpu, py::arg("seed"), py::arg("step"), py::arg("n"),
         "host twin of the fused-dropout generator: uniforms of elements 0..n-1 (CPU float tensor)");

@@ -9,9 +9,11 @@
 //     with the frozen input affine applied (bn_data; identity for VGG) and zero padding AFTER
 //     the affine (the unfused path pads the normalised tensor), rounded to the storage type;
 //   * the im2col A fragments are gathered from the LDS patch through a per-k offset table
-//     (k = (fr*KW + fc)*3 + c, padded to a multiple of 32 with zeros), the packed [64][KP]
-//     filter is read straight from global memory (20 KB, L1/L2 resident);
-//   * 16x16x32 MFMA, fp32 accumulation; epilogue y = relu?(acc*oscale[n] + oshift[n]) (the
+//     (k = (fr*KW + fc)*3 + c, padded to a multiple of 32 with zeros); the filter is read from
+//     the parameter itself (any strides) into a zero-padded [64][KP] LDS tile, and the frozen
+//     BN affines are folded from gamma / beta / moving statistics in the kernel: no packed or
+//     folded copies to keep in sync with the parameters, nothing launched besides the conv;
+//   * 16x16x32 MFMA, fp32 accumulation; epilogue y = relu?(acc*scale[n] + shift[n]) (the
 //     frozen bn0, or the bias), staged through LDS and written as 16-B row vectors.
 // It replaces three launches of the unfused path (input BN, vendor conv, BN+ReLU) with one.
 #include "common.h"
@@ -42,16 +44,17 @@ constexpr int STEM_LDT = STEM_CO + 8;  // 16-bit row stride of the staged output
 
 template <int KH, int KW, int S, bool F16>
 __global__ void __launch_bounds__(256)
-stem_conv_kernel(const uint16_t* __restrict__ x, const float* __restrict__ in_scale, const float* __restrict__ in_shift,
-                 const uint16_t* __restrict__ wp, const float* __restrict__ oscale, const float* __restrict__ oshift,
-                 uint16_t* __restrict__ y, int N, int H, int W, int Ho, int Wo, int pad, int relu, int strips,
-                 int nwg) {
+stem_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, const StemArgs a,
+                 uint16_t* __restrict__ y, int N, int H, int W, int Ho, int Wo, int pad, int relu, int strips, int nwg) {
   constexpr int K = KH * KW * 3;
   constexpr int KP = (K + 31) / 32 * 32;
+  constexpr int LDB = KP + 8;                 // 16-bit row stride of the LDS filter tile
   constexpr int PW = (STEM_BM - 1) * S + KW;  // patch columns
   constexpr int code = F16 ? 2 : 1;
   __shared__ __attribute__((aligned(16))) uint16_t patch[KH * PW * 4];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[STEM_CO * LDB];
   __shared__ int koff[KP];
+  __shared__ float in_aff[6], out_aff[2 * STEM_CO];
   __shared__ __attribute__((aligned(16))) uint16_t T[STEM_BM * STEM_LDT];
 
   // XCD-aware order: consecutive tiles (neighbouring output rows share KH-S input rows) on one XCD
@@ -63,9 +66,58 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const float* __restrict__ in_sc
   const int wo0 = strip * STEM_BM;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
+  // phase 1: folded affines, im2col offset table, zero-padded filter tile
+  if (tid < 3) {
+    float sc = 1.f, sh = 0.f;
+    if (a.in_m) {
+      sc = (a.in_fixg ? 1.f : a.in_g[tid]) * rsqrtf(a.in_v[tid] + a.in_eps);
+      sh = a.in_b[tid] - a.in_m[tid] * sc;
+    }
+    in_aff[tid] = sc;
+    in_aff[3 + tid] = sh;
+  }
+  if (tid < STEM_CO) {
+    float sc = 1.f, sh = 0.f;
+    if (a.out_m) {
+      sc = (a.out_fixg ? 1.f : a.out_g[tid]) * rsqrtf(a.out_v[tid] + a.out_eps);
+      sh = a.out_b[tid] - a.out_m[tid] * sc;
+    } else if (a.bias) {
+      sh = ld(a.bias, tid, a.bias_code);
+    }
+    out_aff[tid] = sc;
+    out_aff[STEM_CO + tid] = sh;
+  }
+  for (int k = tid; k < KP; k += 256) {
+    if (k < K) {
+      const int tap = k / 3, c = k - 3 * tap, fr = tap / KW, fc = tap - fr * KW;
+      koff[k] = (fr * PW + fc) * 4 + c;
+    } else {
+      koff[k] = -1;
+    }
+  }
+  if (a.w_sci == 1 && a.w_skw == 3 && a.w_skh == 3 * KW) {
+    // channels_last filter (the parameter store's layout): row co is k-contiguous
+    for (int e = tid; e < STEM_CO * KP; e += 256) {
+      const int co = e / KP, k = e - co * KP;
+      Bs[co * LDB + k] = k < K ? w[co * a.w_sco + k] : (uint16_t)0;
+    }
+  } else {
+    for (int e = tid; e < STEM_CO * KP; e += 256) {
+      const int co = e / KP, k = e - co * KP;
+      uint16_t v = 0;
+      if (k < K) {
+        const int tap = k / 3, c = k - 3 * tap, fr = tap / KW, fc = tap - fr * KW;
+        v = w[co * a.w_sco + c * a.w_sci + fr * a.w_skh + fc * a.w_skw];
+      }
+      Bs[co * LDB + k] = v;
+    }
+  }
+  __syncthreads();
+
+  // phase 2: the strip's input patch, input affine applied, zero padding after it
   const int hi0 = ho * S - pad, wi0 = wo0 * S - pad;
-  const float s0 = in_scale[0], s1 = in_scale[1], s2 = in_scale[2];
-  const float b0 = in_shift[0], b1 = in_shift[1], b2 = in_shift[2];
+  const float s0 = in_aff[0], s1 = in_aff[1], s2 = in_aff[2];
+  const float b0 = in_aff[3], b1 = in_aff[4], b2 = in_aff[5];
   for (int e = tid; e < KH * PW; e += 256) {
     const int r = e / PW, c = e - r * PW;
     const int hi = hi0 + r, wi = wi0 + c;
@@ -78,14 +130,6 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const float* __restrict__ in_sc
       v = make_uint2(c0 | (c1 << 16), c2);
     }
     *reinterpret_cast<uint2*>(patch + e * 4) = v;
-  }
-  for (int k = tid; k < KP; k += 256) {
-    if (k < K) {
-      const int tap = k / 3, c = k - 3 * tap, fr = tap / KW, fc = tap - fr * KW;
-      koff[k] = (fr * PW + fc) * 4 + c;
-    } else {
-      koff[k] = -1;
-    }
   }
   __syncthreads();
 
@@ -107,11 +151,11 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const float* __restrict__ in_sc
       const uint32_t hi = o1 >= 0 ? patch[o1 + pbase] : 0u;
       aw[e] = lo | (hi << 16);
     }
-    const uint4 a = make_uint4(aw[0], aw[1], aw[2], aw[3]);
+    const uint4 af = make_uint4(aw[0], aw[1], aw[2], aw[3]);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint4 b = *reinterpret_cast<const uint4*>(wp + (int64_t)(j * 16 + (lane & 15)) * KP + k0);
-      acc[j] = stem_mfma<F16>(a, b, acc[j]);
+      const uint4 bf = *reinterpret_cast<const uint4*>(Bs + (j * 16 + (lane & 15)) * LDB + k0);
+      acc[j] = stem_mfma<F16>(af, bf, acc[j]);
     }
   }
 
@@ -119,7 +163,7 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const float* __restrict__ in_sc
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
     const int co = j * 16 + (lane & 15);
-    const float sc = oscale[co], sh = oshift[co];
+    const float sc = out_aff[co], sh = out_aff[STEM_CO + co];
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float v = acc[j][r] * sc + sh;
@@ -140,9 +184,8 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const float* __restrict__ in_sc
   }
 }
 
-int stem_conv(const uint16_t* x, const float* in_scale, const float* in_shift, const uint16_t* wp, const float* oscale,
-              const float* oshift, uint16_t* y, int N, int H, int W, int Ho, int Wo, int KH, int KW, int stride,
-              int pad, int relu, int code, hipStream_t st) {
+int stem_conv(const uint16_t* x, const uint16_t* w, const StemArgs& a, uint16_t* y, int N, int H, int W, int Ho,
+              int Wo, int KH, int KW, int stride, int pad, int relu, int code, hipStream_t st) {
   const int strips = div_up(Wo, STEM_BM);
   const int64_t nwg64 = (int64_t)N * Ho * strips;
   if (nwg64 <= 0) return 0;
@@ -151,11 +194,9 @@ int stem_conv(const uint16_t* x, const float* in_scale, const float* in_shift, c
 #define MXR_STEM(KH_, KW_, S_)                                                                                   \
   if (KH == KH_ && KW == KW_ && stride == S_) {                                                                \
     if (code == 2)                                                                                             \
-      stem_conv_kernel<KH_, KW_, S_, true><<<nwg, 256, 0, st>>>(x, in_scale, in_shift, wp, oscale, oshift, y, N, H, \
-                                                                W, Ho, Wo, pad, relu, strips, nwg);            \
+      stem_conv_kernel<KH_, KW_, S_, true><<<nwg, 256, 0, st>>>(x, w, a, y, N, H, W, Ho, Wo, pad, relu, strips, nwg); \
     else                                                                                                       \
-      stem_conv_kernel<KH_, KW_, S_, false><<<nwg, 256, 0, st>>>(x, in_scale, in_shift, wp, oscale, oshift, y, N, H, \
-                                                                 W, Ho, Wo, pad, relu, strips, nwg);           \
+      stem_conv_kernel<KH_, KW_, S_, false><<<nwg, 256, 0, st>>>(x, w, a, y, N, H, W, Ho, Wo, pad, relu, strips, nwg); \
     return 0;                                                                                                  \
   }
   MXR_STEM(7, 7, 2)

@@ -237,11 +237,21 @@ int maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int
                 int k, int s, int p, int code, hipStream_t st);
 int avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, int code, hipStream_t st);
 int avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, int code, hipStream_t st);
-// stem conv (stem.hip): x (N,H,W,3) 16-bit NHWC, wp (64, KP) packed filter, k = (fr*KW+fc)*3+c;
-// y (N,Ho,Wo,64) = relu?(conv(x*in_scale+in_shift) * oscale + oshift).  Geometries 7x7/2, 3x3/1.
-int stem_conv(const uint16_t* x, const float* in_scale, const float* in_shift, const uint16_t* wp, const float* oscale,
-              const float* oshift, uint16_t* y, int N, int H, int W, int Ho, int Wo, int KH, int KW, int stride,
-              int pad, int relu, int code, hipStream_t st);
+// stem conv (stem.hip): x (N,H,W,3) 16-bit NHWC, w (64,3,KH,KW) 16-bit with element strides;
+// y (N,Ho,Wo,64) = relu?(conv(in_bn(x)) -> out_bn | + bias).  Geometries 7x7/2, 3x3/1.
+struct StemArgs {
+  int64_t w_sco, w_sci, w_skh, w_skw;        // filter element strides (co, ci, kh, kw)
+  const float *in_g, *in_b, *in_m, *in_v;    // frozen input BN (in_m == nullptr: identity)
+  float in_eps;
+  int in_fixg;
+  const float *out_g, *out_b, *out_m, *out_v;  // frozen output BN (out_m == nullptr: bias or none)
+  float out_eps;
+  int out_fixg;
+  const void* bias;                          // per-channel bias (bias_code: 0 fp32, 1 bf16, 2 fp16)
+  int bias_code;
+};
+int stem_conv(const uint16_t* x, const uint16_t* w, const StemArgs& a, uint16_t* y, int N, int H, int W, int Ho,
+              int Wo, int KH, int KW, int stride, int pad, int relu, int code, hipStream_t st);
 
 // ---- proposal pre-NMS top-k (topk.hip): keys (B, N), boxes (B, N, 4) -> the P best in stable
 // descending order; ws_key / ws_idx: B * P each

@@ -124,6 +124,28 @@ std::vector<Tensor> nms_proposals(const Tensor& boxes, const Tensor& scores, con
 
 // phase 1 of nms_proposals alone: the suppression bitmask (a caller can order other work between
 // the data-parallel mask and the serial reduce)
+// (skeys, order) of a descending sort over (B, N) keys, boxes (B, N, 4) fp32 -> (keys (B, P), boxes (B, P, 4),
+// n_valid (B) int32)
+std::vector<Tensor> proposal_gather(const Tensor& skeys, const Tensor& order, const Tensor& boxes, int64_t P) {
+  CHECK_DEV(skeys); CHECK_DEV(order); CHECK_DEV(boxes);
+  TORCH_CHECK(skeys.scalar_type() == at::kFloat && skeys.dim() == 2 && skeys.is_contiguous(), "proposal_gather: skeys");
+  TORCH_CHECK(order.scalar_type() == at::kLong && order.sizes() == skeys.sizes() && order.is_contiguous(),
+              "proposal_gather: order (B, N) int64");
+  const int64_t B = skeys.size(0), N = skeys.size(1);
+  TORCH_CHECK(boxes.scalar_type() == at::kFloat && boxes.dim() == 3 && boxes.size(0) == B && boxes.size(1) == N &&
+                  boxes.size(2) == 4 && boxes.is_contiguous(),
+              "proposal_gather: boxes (B, N, 4) fp32");
+  TORCH_CHECK(P > 0 && P <= N, "proposal_gather: 0 < P <= N");
+  DevGuard g(skeys.device());
+  Tensor ok = at::empty({B, P}, skeys.options());
+  Tensor ob = at::empty({B, P, 4}, boxes.options());
+  Tensor nv = at::empty({B}, skeys.options().dtype(at::kInt));
+  mxr::proposal_gather(skeys.data_ptr<float>(), order.data_ptr<int64_t>(), boxes.data_ptr<float>(), (int)B, N, (int)P,
+                       ok.data_ptr<float>(), ob.data_ptr<float>(), nv.data_ptr<int32_t>(), cur_stream());
+  LAUNCH_CHECK("proposal_gather");
+  return {ok, ob, nv};
+}
+
 Tensor nms_mask_build(const Tensor& boxes, const Tensor& n_valid, double thresh) {
   CHECK_DEV(boxes); CHECK_F32(boxes); CHECK_CONTIG(boxes);
   CHECK_DEV(n_valid); CHECK_I32(n_valid); CHECK_CONTIG(n_valid);
@@ -1721,6 +1743,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("s"), py::arg("p"));
   m.def("avgpool_fwd", &avgpool_fwd);
   m.def("avgpool_bwd", &avgpool_bwd);
+  m.def("proposal_gather", &proposal_gather);
   m.def("stem_conv", &stem_conv, py::arg("x"), py::arg("w"), py::arg("in_bn"), py::arg("in_eps"), py::arg("in_fixg"),
         py::arg("out_bn"), py::arg("out_eps"), py::arg("out_fixg"), py::arg("bias"), py::arg("stride"), py::arg("pad"),
         py::arg("relu"));

@@ -91,3 +91,44 @@ void proposal_decode(const void* cls, int cls_bf16, int64_t cs0, int64_t cs1, in
 }
 
 }  // namespace mxr
+
+namespace mxr {
+
+// Post-sort assembly of the top-P proposals (one workgroup per image): the first P sorted keys,
+// the boxes gathered by the sort order, and the count of valid (finite-key) proposals.  Sorted
+// descending, the valid keys form a prefix, so n_valid is the count over the first P.  Replaces
+// the slice copy, the gather and the compare / sum / cast chain (five launches) on the proposal
+// chain's serial path.
+__global__ void __launch_bounds__(1024)
+proposal_gather_kernel(const float* __restrict__ skeys, const int64_t* __restrict__ order,
+                       const float* __restrict__ boxes, int64_t N, int P, float* __restrict__ out_keys,
+                       float* __restrict__ out_boxes, int32_t* __restrict__ n_valid) {
+  __shared__ int s_cnt;
+  const int b = blockIdx.x;
+  if (threadIdx.x == 0) s_cnt = 0;
+  __syncthreads();
+  const float* kb = skeys + (int64_t)b * N;
+  const int64_t* ob = order + (int64_t)b * N;
+  const float4* bb = reinterpret_cast<const float4*>(boxes) + (int64_t)b * N;
+  int cnt = 0;
+  for (int i = threadIdx.x; i < P; i += blockDim.x) {
+    const float k = kb[i];
+    int64_t o = ob[i];
+    o = o < 0 ? 0 : (o >= N ? N - 1 : o);
+    out_keys[(int64_t)b * P + i] = k;
+    reinterpret_cast<float4*>(out_boxes)[(int64_t)b * P + i] = bb[o];
+    cnt += k > -INFINITY;
+  }
+  for (int off = 32; off > 0; off >>= 1) cnt += __shfl_xor(cnt, off, 64);
+  if ((threadIdx.x & 63) == 0 && cnt) atomicAdd(&s_cnt, cnt);
+  __syncthreads();
+  if (threadIdx.x == 0) n_valid[b] = s_cnt;
+}
+
+void proposal_gather(const float* skeys, const int64_t* order, const float* boxes, int B, int64_t N, int P,
+                     float* out_keys, float* out_boxes, int32_t* n_valid, hipStream_t st) {
+  if (B == 0) return;
+  proposal_gather_kernel<<<B, 1024, 0, st>>>(skeys, order, boxes, N, P, out_keys, out_boxes, n_valid);
+}
+
+}  // namespace mxr

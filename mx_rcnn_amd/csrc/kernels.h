@@ -14,6 +14,10 @@ namespace mxr {
 // is_prob: cls already holds softmax probabilities (test graph) instead of logits.
 // Writes boxes (B, N, 4) and keys (B, N) where N = Hc*Wc*A, order (h*Wc+w)*A+a.
 // Filtered boxes get key = -inf.  Hc/Wc are per-image crops (device arrays, may be null).
+// skeys / order (B, N) from a descending sort, boxes (B, N, 4) -> out_keys (B, P), out_boxes (B, P, 4),
+// n_valid (B) = number of finite keys among the first P
+void proposal_gather(const float* skeys, const int64_t* order, const float* boxes, int B, int64_t N, int P,
+                     float* out_keys, float* out_boxes, int32_t* n_valid, hipStream_t st);
 void proposal_decode(const void* cls, int cls_bf16, int64_t cs0, int64_t cs1, int64_t cs2, int64_t cs3,
                      const void* dlt, int dlt_bf16, int64_t ds0, int64_t ds1, int64_t ds2, int64_t ds3,
                      int is_prob, const float* im_info, const float* base_anchors, int A,

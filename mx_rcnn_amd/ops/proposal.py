@@ -92,10 +92,13 @@ def proposal(cls, bbox_deltas, im_info, feat_stride=16, scales=(8, 16, 32), rati
             skeys, sboxes, n_valid = C.proposal_topk(keys.contiguous(), boxes.contiguous(), P)
         else:
             skeys, order = torch.sort(keys, dim=1, descending=True, stable=True)
-            skeys = skeys[:, :P].contiguous()
-            order = order[:, :P]
-            sboxes = torch.gather(boxes, 1, order[..., None].expand(-1, -1, 4)).contiguous()
-            n_valid = (skeys > float('-inf')).sum(dim=1).to(torch.int32)
+            if cls.is_cuda and os.environ.get('MXR_PROPOSAL_GATHER', '1') != '0':  # one launch: keys, boxes, count
+                skeys, sboxes, n_valid = C.proposal_gather(skeys, order, boxes.contiguous(), P)
+            else:
+                skeys = skeys[:, :P].contiguous()
+                order = order[:, :P]
+                sboxes = torch.gather(boxes, 1, order[..., None].expand(-1, -1, 4)).contiguous()
+                n_valid = (skeys > float('-inf')).sum(dim=1).to(torch.int32)
         post = int(post_nms_top_n) if post_nms_top_n > 0 else P
         rand_u = torch.rand(B, post, device=dev, generator=generator)
         if cls.is_cuda:

@@ -516,3 +516,22 @@ def test_proposal_topk_matches_stable_sort(cuda, B, N, P, ties):
     assert torch.equal(sk.cpu(), rk)
     assert torch.equal(sb.cpu(), rb)
     assert torch.equal(nv.cpu(), (rk > float('-inf')).sum(1).to(torch.int32))
+
+
+@pytest.mark.gpu
+def test_proposal_gather_matches_torch(cuda):
+    """Post-sort top-P assembly kernel == slice + gather + valid count."""
+    from mx_rcnn_amd.ops import need_ext
+    g = torch.Generator().manual_seed(7)
+    B, N, P = 2, 5000, 3000
+    keys = torch.rand(B, N, generator=g)
+    keys[0, torch.randperm(N, generator=g)[:2500]] = float('-inf')  # image 0: 2500 valid
+    keys[1, torch.randperm(N, generator=g)[:200]] = float('-inf')   # image 1: all P valid
+    boxes = torch.rand(B, N, 4, generator=g) * 500
+    keys, boxes = keys.to(cuda), boxes.to(cuda)
+    sk, order = torch.sort(keys, dim=1, descending=True, stable=True)
+    ok, ob, nv = need_ext().proposal_gather(sk, order, boxes, P)
+    torch.testing.assert_close(ok, sk[:, :P])
+    ref_b = torch.gather(boxes, 1, order[:, :P, None].expand(-1, -1, 4))
+    torch.testing.assert_close(ob, ref_b)
+    assert nv.tolist() == [2500, P]

@@ -202,7 +202,13 @@ __global__ void __launch_bounds__(256)
 roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ argmax, const float* __restrict__ rois,
                         int R, int PHW, int HW, int C, int code, const T* __restrict__ gadd, T* __restrict__ gin) {
   extern __shared__ float acc[];  // [HW][CW]
-  const int c0 = blockIdx.x * CW, b = blockIdx.y;
+  // XCD-aware channel groups: workgroups are dealt round-robin over the 8 XCDs, so consecutive
+  // block ids would put neighbouring channel groups -- which read and write the same cache lines
+  // of the NHWC argmax / gradient rows -- on different L2s.  Consecutive groups share an XCD.
+  const int nx = gridDim.x, bx = blockIdx.x;
+  const int q = nx / 8, r8 = nx % 8, xcd = bx % 8;
+  const int grp = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + bx / 8;
+  const int c0 = grp * CW, b = blockIdx.y;
   // the slab starts from the feature map's other gradient (gadd: the RPN head's), if any; one
   // pixel (CW channels, one vector access) per thread and iteration
 #pragma unroll 4

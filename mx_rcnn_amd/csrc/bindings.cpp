@@ -1013,16 +1013,16 @@ Tensor avgpool_bwd(const Tensor& dy, int64_t H, int64_t W) {
 // ---- stem conv (stem.hip) ------------------------------------------------------------------------
 Tensor stem_conv(const Tensor& x, const Tensor& w, const std::vector<Tensor>& in_bn, double in_eps, bool in_fixg,
                  const std::vector<Tensor>& out_bn, double out_eps, bool out_fixg, const c10::optional<Tensor>& bias,
-                 int64_t stride, int64_t pad, bool relu) {
+                 int64_t KH, int64_t KW, int64_t stride, int64_t pad, bool relu) {
   CHECK_DEV(x); CHECK_DEV(w);
   TORCH_CHECK((x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf) && x.dim() == 4 && x.size(1) == 3 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "stem_conv: x must be channels_last bf16 / fp16 (N,3,H,W)");
-  TORCH_CHECK(w.scalar_type() == x.scalar_type() && w.dim() == 4 && w.size(0) == 64 && w.size(1) == 3,
-              "stem_conv: w must be a (64, 3, KH, KW) filter of x's dtype");
-  const int64_t KH = w.size(2), KW = w.size(3);
+  const int64_t KP = (KH * KW * 3 + 31) / 32 * 32;
+  TORCH_CHECK(w.scalar_type() == x.scalar_type() && w.dim() == 2 && w.size(0) == 64 && w.size(1) == KP &&
+                  w.is_contiguous(),
+              "stem_conv: w must be the packed contiguous (64, KP) filter of x's dtype");
   mxr::StemArgs a{};
-  a.w_sco = w.stride(0); a.w_sci = w.stride(1); a.w_skh = w.stride(2); a.w_skw = w.stride(3);
   TORCH_CHECK(in_bn.empty() || in_bn.size() == 4, "stem_conv: in_bn = [] or [gamma, beta, mean, var]");
   TORCH_CHECK(out_bn.empty() || out_bn.size() == 4, "stem_conv: out_bn = [] or [gamma, beta, mean, var]");
   for (const Tensor& t : in_bn) {
@@ -1745,8 +1745,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("avgpool_bwd", &avgpool_bwd);
   m.def("proposal_gather", &proposal_gather);
   m.def("stem_conv", &stem_conv, py::arg("x"), py::arg("w"), py::arg("in_bn"), py::arg("in_eps"), py::arg("in_fixg"),
-        py::arg("out_bn"), py::arg("out_eps"), py::arg("out_fixg"), py::arg("bias"), py::arg("stride"), py::arg("pad"),
-        py::arg("relu"));
+        py::arg("out_bn"), py::arg("out_eps"), py::arg("out_fixg"), py::arg("bias"), py::arg("KH"), py::arg("KW"),
+        py::arg("stride"), py::arg("pad"), py::arg("relu"));
   m.def("philox_uniform", &philox_uniform_cpu, py::arg("seed"), py::arg("step"), py::arg("n"),
         "host twin of the fused-dropout generator: uniforms of elements 0..n-1 (CPU float tensor)");
   m.def("bn_train_fwd", &bn_train_fwd);

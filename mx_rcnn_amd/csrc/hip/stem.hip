@@ -9,10 +9,10 @@
 //     with the frozen input affine applied (bn_data; identity for VGG) and zero padding AFTER
 //     the affine (the unfused path pads the normalised tensor), rounded to the storage type;
 //   * the im2col A fragments are gathered from the LDS patch through a per-k offset table
-//     (k = (fr*KW + fc)*3 + c, padded to a multiple of 32 with zeros); the filter is read from
-//     the parameter itself (any strides) into a zero-padded [64][KP] LDS tile, and the frozen
-//     BN affines are folded from gamma / beta / moving statistics in the kernel: no packed or
-//     folded copies to keep in sync with the parameters, nothing launched besides the conv;
+//     (k = (fr*KW + fc)*3 + c, padded to a multiple of 32 with zeros); the B fragments are 16-B
+//     reads of the packed [64][KP] filter (20 KB, L1/L2 resident: staging it per workgroup cost
+//     2x the kernel time), and the frozen BN affines are folded from gamma / beta / moving
+//     statistics in the kernel (no folded copies to keep in sync with the BN buffers);
 //   * 16x16x32 MFMA, fp32 accumulation; epilogue y = relu?(acc*scale[n] + shift[n]) (the
 //     frozen bn0, or the bias), staged through LDS and written as 16-B row vectors.
 // It replaces three launches of the unfused path (input BN, vendor conv, BN+ReLU) with one.
@@ -48,11 +48,9 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                  uint16_t* __restrict__ y, int N, int H, int W, int Ho, int Wo, int pad, int relu, int strips, int nwg) {
   constexpr int K = KH * KW * 3;
   constexpr int KP = (K + 31) / 32 * 32;
-  constexpr int LDB = KP + 8;                 // 16-bit row stride of the LDS filter tile
   constexpr int PW = (STEM_BM - 1) * S + KW;  // patch columns
   constexpr int code = F16 ? 2 : 1;
   __shared__ __attribute__((aligned(16))) uint16_t patch[KH * PW * 4];
-  __shared__ __attribute__((aligned(16))) uint16_t Bs[STEM_CO * LDB];
   __shared__ int koff[KP];
   __shared__ float in_aff[6], out_aff[2 * STEM_CO];
   __shared__ __attribute__((aligned(16))) uint16_t T[STEM_BM * STEM_LDT];
@@ -66,7 +64,7 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
   const int wo0 = strip * STEM_BM;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
-  // phase 1: folded affines, im2col offset table, zero-padded filter tile
+  // phase 1: folded affines, im2col offset table
   if (tid < 3) {
     float sc = 1.f, sh = 0.f;
     if (a.in_m) {
@@ -93,23 +91,6 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
       koff[k] = (fr * PW + fc) * 4 + c;
     } else {
       koff[k] = -1;
-    }
-  }
-  if (a.w_sci == 1 && a.w_skw == 3 && a.w_skh == 3 * KW) {
-    // channels_last filter (the parameter store's layout): row co is k-contiguous
-    for (int e = tid; e < STEM_CO * KP; e += 256) {
-      const int co = e / KP, k = e - co * KP;
-      Bs[co * LDB + k] = k < K ? w[co * a.w_sco + k] : (uint16_t)0;
-    }
-  } else {
-    for (int e = tid; e < STEM_CO * KP; e += 256) {
-      const int co = e / KP, k = e - co * KP;
-      uint16_t v = 0;
-      if (k < K) {
-        const int tap = k / 3, c = k - 3 * tap, fr = tap / KW, fc = tap - fr * KW;
-        v = w[co * a.w_sco + c * a.w_sci + fr * a.w_skh + fc * a.w_skw];
-      }
-      Bs[co * LDB + k] = v;
     }
   }
   __syncthreads();
@@ -154,7 +135,7 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
     const uint4 af = make_uint4(aw[0], aw[1], aw[2], aw[3]);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      const uint4 bf = *reinterpret_cast<const uint4*>(Bs + (j * 16 + (lane & 15)) * LDB + k0);
+      const uint4 bf = *reinterpret_cast<const uint4*>(w + (j * 16 + (lane & 15)) * KP + k0);
       acc[j] = stem_mfma<F16>(af, bf, acc[j]);
     }
   }

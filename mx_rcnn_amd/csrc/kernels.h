@@ -241,10 +241,10 @@ int maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int
                 int k, int s, int p, int code, hipStream_t st);
 int avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, int code, hipStream_t st);
 int avgpool_bwd(const uint16_t* dy, uint16_t* dx, int N, int HW, int C, int code, hipStream_t st);
-// stem conv (stem.hip): x (N,H,W,3) 16-bit NHWC, w (64,3,KH,KW) 16-bit with element strides;
+// stem conv (stem.hip): x (N,H,W,3) 16-bit NHWC, w the packed (64, KP) filter, k = (fr*KW+fc)*3+c,
+// zero-padded to KP = roundup(3*KH*KW, 32);
 // y (N,Ho,Wo,64) = relu?(conv(in_bn(x)) -> out_bn | + bias).  Geometries 7x7/2, 3x3/1.
 struct StemArgs {
-  int64_t w_sco, w_sci, w_skh, w_skw;        // filter element strides (co, ci, kh, kw)
   const float *in_g, *in_b, *in_m, *in_v;    // frozen input BN (in_m == nullptr: identity)
   float in_eps;
   int in_fixg;

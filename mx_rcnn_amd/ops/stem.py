@@ -7,9 +7,11 @@ unfused path is three launches (input BN, a vendor conv -- the MFMA implicit-GEM
 
 Forward-only: used when nothing upstream of the stem output needs a gradient (the reference
 freezes conv0 / bn_data / bn0 and conv1_x: FIXED_PARAMS, `rcnn/config.py`), i.e. in training with
-those parameters fixed and at test time.  The kernel reads the filter parameter and the BN
-parameters / moving statistics themselves (folding the BN affines in-kernel), so there is no
-derived copy to invalidate and a captured step contains the conv launch only.
+those parameters fixed and at test time.  The kernel folds the BN affines from the BN
+parameters / moving statistics in-kernel (no derived copy to invalidate: the graph warm-up's
+state restore rewrites those buffers), and reads the filter from a packed (64, KP) copy cached
+per parameter and rebuilt when the parameter's version counter moves (a checkpoint load).  A
+captured step contains the conv launch only.
 """
 import os
 
@@ -17,6 +19,19 @@ import torch
 import torch.nn.functional as F
 
 from ._ext import need_ext
+
+
+_PACKED = {}
+
+
+def _packed_filter(w, dtype):
+    key = (id(w), dtype)
+    ver = (w.data_ptr(), w._version, tuple(w.shape))
+    hit = _PACKED.get(key)
+    if hit is None or hit[0] != ver:
+        hit = (ver, pack_filter(w, dtype))
+        _PACKED[key] = hit
+    return hit[1]
 
 
 def stem_fusable(x, *params):
@@ -32,7 +47,7 @@ def stem_fusable(x, *params):
 
 def pack_filter(w, dtype):
     """(64, 3, KH, KW) filter -> contiguous (64, KP) in ``dtype``, k = (fr*KW + fc)*3 + c,
-    zero-padded to a multiple of 32 (the MFMA K step): the kernel's LDS filter tile."""
+    zero-padded to a multiple of 32 (the MFMA K step): the kernel's B operand."""
     co, ci, kh, kw = w.shape
     k = kh * kw * ci
     kp = (k + 31) // 32 * 32
@@ -58,16 +73,14 @@ def _bn_args(bn):
 
 def stem_conv(x, weight, stride, pad, in_bn=None, out_bn=None, bias=None, relu=True):
     """relu?(conv(in_bn(x), weight) -> out_bn or + bias), x (N,3,H,W) channels_last 16-bit."""
-    co, ci = weight.shape[:2]
+    co, ci, kh, kw = weight.shape
     assert co == 64 and ci == 3, 'stem_conv: 3 -> 64 channels'
-    w = weight.detach()
-    if w.dtype != x.dtype:
-        w = w.to(x.dtype)
+    wp = _packed_filter(weight, x.dtype)
     ib, ieps, ifix = _bn_args(in_bn)
     ob, oeps, ofix = _bn_args(out_bn)
     b = bias.detach() if (bias is not None and out_bn is None) else None
     xc = x.contiguous(memory_format=torch.channels_last)
-    return need_ext().stem_conv(xc, w, ib, ieps, ifix, ob, oeps, ofix, b, int(stride), int(pad), bool(relu))
+    return need_ext().stem_conv(xc, wp, ib, ieps, ifix, ob, oeps, ofix, b, kh, kw, int(stride), int(pad), bool(relu))
 
 
 def stem_conv_reference(x, weight, stride, pad, in_bn=None, out_bn=None, bias=None, relu=True):

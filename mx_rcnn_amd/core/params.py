@@ -150,18 +150,56 @@ class FlatParamStore:
                 conv_ops.register_dgrad_weight(p, buf)
                 srcs.append(p.detach())
                 dsts.append(buf)
+        self._wt_params = []
         if srcs:
+            self._wt_params = [p for p in self._dgrad_params(srcs)]
+            self._wt_srcs, self._wt_dsts = srcs, dsts
+            self._sub_in_table = set()
             n_ent, tiles = ext.wt_flip_table_info(srcs)
             self._wt_table = (ext.wt_flip_build(srcs, dsts), n_ent, tiles, dsts)
             self.refresh_dgrad_cache()
+
+    def _dgrad_params(self, srcs):
+        """The parameter behind each flip-table source (same order)."""
+        by_ptr = {p.data_ptr(): p for p in self.params.values()}
+        return [by_ptr.get(s.data_ptr()) for s in srcs]
+
+    def _maybe_add_sub_filters(self):
+        """Fold the parity sub-filters registered since the table was built (the strided data
+        gradient registers them on its first backward) into the flip kernel's table, so they are
+        written in the same pass instead of one copy kernel each.  Never while capturing: the
+        table upload is a host-to-device copy."""
+        from ..ops import conv as conv_ops
+        if not conv_ops._SUBW or os.environ.get('MXR_SUBFILTER_FOLD', '1') == '0':
+            return
+        if torch.cuda.is_current_stream_capturing():
+            return
+        subs, have = [], set()
+        for p in self._wt_params:
+            lst = conv_ops.sub_filters_of(p) if p is not None else []
+            rows = {tuple(r) for _, r, _ in lst}
+            cols = {tuple(c) for _, _, c in lst}
+            kh = p.shape[2] if (p is not None and p.dim() == 4) else 0
+            full = (lst and len(lst) == len(rows) * len(cols) and len(rows) <= 2 and len(cols) <= 2 and
+                    sum(len(r) for r in rows) == kh and sum(len(c) for c in cols) == p.shape[3])
+            subs.append(lst if full else [])
+            if full:
+                have.add(id(p))
+        if have == self._sub_in_table:
+            return
+        from ..ops._ext import need_ext
+        _, n_ent, tiles, dsts = self._wt_table
+        self._wt_table = (need_ext().wt_flip_build(self._wt_srcs, self._wt_dsts, subs), n_ent, tiles, dsts)
+        self._sub_in_table = have
 
     def refresh_dgrad_cache(self):
         if self._wt_table is not None:
             from ..ops._ext import need_ext
             from ..ops.conv import refresh_sub_filters
+            self._maybe_add_sub_filters()
             table, n_ent, tiles, _ = self._wt_table
             need_ext().wt_flip_run(table, n_ent, tiles)
-            refresh_sub_filters()
+            refresh_sub_filters(skip=self._sub_in_table)
 
     def refresh_dgrad_cache_async(self, zero_grad=False):
         """Rebuild the dgrad cache from the current weights on a side stream (concurrent with the

@@ -1356,9 +1356,15 @@ std::vector<int64_t> wt_flip_table_info(const std::vector<Tensor>& srcs) {
   return {(int64_t)srcs.size(), tiles};
 }
 
-Tensor wt_flip_build(const std::vector<Tensor>& srcs, const std::vector<Tensor>& dsts) {
+// subs (optional, one list per entry): (buffer, row taps, col taps) parity sub-filters of the flipped
+// filter -- the (I, O, |rows|, |cols|) channels_last slice at those taps (ops/conv.py sub_filter)
+Tensor wt_flip_build(const std::vector<Tensor>& srcs, const std::vector<Tensor>& dsts,
+                     const std::vector<std::vector<std::tuple<Tensor, std::vector<int64_t>, std::vector<int64_t>>>>&
+                         subs) {
   TORCH_CHECK(srcs.size() == dsts.size() && !srcs.empty(), "srcs/dsts mismatch");
+  TORCH_CHECK(subs.empty() || subs.size() == srcs.size(), "subs: one list per entry");
   std::vector<mxr::WtFlipEntry> ents(srcs.size());
+  std::memset(ents.data(), 0, ents.size() * sizeof(mxr::WtFlipEntry));
   int tiles = 0;
   for (size_t k = 0; k < srcs.size(); ++k) {
     const Tensor &s = srcs[k], &d = dsts[k];
@@ -1373,6 +1379,52 @@ Tensor wt_flip_build(const std::vector<Tensor>& srcs, const std::vector<Tensor>&
     ents[k].dst = reinterpret_cast<uint16_t*>(d.data_ptr());
     ents[k].O = O; ents[k].I = I; ents[k].KH = KH; ents[k].KW = KW;
     ents[k].tile_begin = tiles;
+    if (!subs.empty() && !subs[k].empty()) {
+      TORCH_CHECK(KH <= 8 && KW <= 8, "sub-filters: KH, KW <= 8");
+      // classes are numbered by first appearance along each axis
+      std::vector<std::vector<int64_t>> rsets, csets;
+      auto cls_of = [](std::vector<std::vector<int64_t>>& sets, const std::vector<int64_t>& taps) {
+        for (size_t q = 0; q < sets.size(); ++q)
+          if (sets[q] == taps) return (int)q;
+        sets.push_back(taps);
+        return (int)sets.size() - 1;
+      };
+      for (int q = 0; q < 8; ++q) ents[k].rcls[q] = ents[k].ccls[q] = ents[k].ridx[q] = ents[k].cidx[q] = 0;
+      for (const auto& sb : subs[k]) {
+        const Tensor& buf = std::get<0>(sb);
+        const auto& rt = std::get<1>(sb);
+        const auto& ct = std::get<2>(sb);
+        const int rc = cls_of(rsets, rt), cc = cls_of(csets, ct);
+        TORCH_CHECK(rc < 2 && cc < 2, "sub-filters: at most two parity classes per axis");
+        CHECK_DEV(buf);
+        TORCH_CHECK(buf.scalar_type() == at::kBFloat16 && buf.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                        buf.size(0) == I && buf.size(1) == O && buf.size(2) == (int64_t)rt.size() &&
+                        buf.size(3) == (int64_t)ct.size(),
+                    "sub-filter buffer must be a channels_last bf16 (I, O, |rows|, |cols|) tensor");
+        ents[k].sub[2 * rc + cc] = reinterpret_cast<uint16_t*>(buf.data_ptr());
+        ents[k].rcnt[rc] = (int8_t)rt.size();
+        ents[k].ccnt[cc] = (int8_t)ct.size();
+        for (size_t j = 0; j < rt.size(); ++j) {
+          TORCH_CHECK(rt[j] >= 0 && rt[j] < KH, "sub-filter row tap out of range");
+          ents[k].rcls[rt[j]] = (int8_t)rc; ents[k].ridx[rt[j]] = (int8_t)j;
+        }
+        for (size_t j = 0; j < ct.size(); ++j) {
+          TORCH_CHECK(ct[j] >= 0 && ct[j] < KW, "sub-filter col tap out of range");
+          ents[k].ccls[ct[j]] = (int8_t)cc; ents[k].cidx[ct[j]] = (int8_t)j;
+        }
+      }
+      // every flipped tap must land in exactly one registered class pair, or the kernel would write
+      // a tap into a sub-filter it does not belong to: require a full partition
+      int covered = 0;
+      for (const auto& r : rsets) covered += (int)r.size();
+      TORCH_CHECK(covered == KH, "sub-filters must partition the row taps");
+      covered = 0;
+      for (const auto& c : csets) covered += (int)c.size();
+      TORCH_CHECK(covered == KW, "sub-filters must partition the col taps");
+      for (size_t rc = 0; rc < rsets.size(); ++rc)
+        for (size_t cc = 0; cc < csets.size(); ++cc)
+          TORCH_CHECK(ents[k].sub[2 * rc + cc] != nullptr, "sub-filters: every (row, col) class pair is needed");
+    }
     tiles += KH * KW * ((O + 63) / 64) * ((I + 63) / 64);
   }
   Tensor host = at::empty({(int64_t)(ents.size() * sizeof(mxr::WtFlipEntry))}, at::TensorOptions().dtype(at::kByte));
@@ -1758,7 +1810,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("save_mean"), py::arg("save_invstd"), py::arg("fix_gamma"), py::arg("relu"), py::arg("need_dx"),
         py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none());
   m.def("wt_flip_table_info", &wt_flip_table_info);
-  m.def("wt_flip_build", &wt_flip_build);
+  m.def("wt_flip_build", &wt_flip_build, py::arg("srcs"), py::arg("dsts"),
+        py::arg("subs") = std::vector<std::vector<std::tuple<Tensor, std::vector<int64_t>, std::vector<int64_t>>>>());
   m.def("wt_flip_run", &wt_flip_run);
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"), py::arg("stride"),
         py::arg("pad"), py::arg("splits") = 0, py::arg("out") = py::none(), py::arg("variant") = 0);

@@ -1463,13 +1463,23 @@ conv_wt_flip_kernel(const WtFlipEntry* __restrict__ entries, int n_entries) {
     for (int k = 0; k < 8; ++k) t[ch * 8 + k][row] = pv[k];
   }
   __syncthreads();
-  // write: dst[i][tap][o], 64 rows of i x 8 chunks of 8 o
+  // write: dst[i][tap][o], 64 rows of i x 8 chunks of 8 o (and the tap's parity sub-filter)
+  const int tr = tap / e.KW, tc = tap % e.KW;
+  uint16_t* sd = nullptr;
+  int sub_taps = 0, sub_tap = 0;
+  if (tr < 8 && tc < 8) {
+    sd = e.sub[2 * e.rcls[tr] + e.ccls[tc]];
+    sub_taps = e.rcnt[e.rcls[tr]] * e.ccnt[e.ccls[tc]];
+    sub_tap = e.ridx[tr] * e.ccnt[e.ccls[tc]] + e.cidx[tc];
+  }
   for (int q = tid; q < 512; q += 256) {
     const int row = q >> 3, ch = q & 7;
     const int i = i0 + row, o = o0 + ch * 8;
-    if (i < e.I && o < e.O)
-      *reinterpret_cast<uint4*>(e.dst + ((int64_t)i * taps + tap) * e.O + o) =
-          *reinterpret_cast<const uint4*>(&t[row][ch * 8]);
+    if (i < e.I && o < e.O) {
+      const uint4 v = *reinterpret_cast<const uint4*>(&t[row][ch * 8]);
+      *reinterpret_cast<uint4*>(e.dst + ((int64_t)i * taps + tap) * e.O + o) = v;
+      if (sd) *reinterpret_cast<uint4*>(sd + ((int64_t)i * sub_taps + sub_tap) * e.O + o) = v;
+    }
   }
 }
 

@@ -279,6 +279,12 @@ struct WtFlipEntry {
   uint16_t* dst;
   int O, I, KH, KW;
   int tile_begin;  // prefix sum of 64x64 tiles (per tap) over entries
+  // parity sub-filters of the flipped filter (strided data gradient, ops/conv.py sub_filter):
+  // flipped tap (r, c) also goes to sub[2 * rcls[r] + ccls[c]] (I, O, rcnt, ccnt channels_last)
+  // at sub-tap (ridx[r], cidx[c]); a null sub entry is skipped
+  uint16_t* sub[4];
+  int8_t rcls[8], ridx[8], ccls[8], cidx[8];
+  int8_t rcnt[2], ccnt[2];
 };
 void conv_wt_flip_multi(const WtFlipEntry* entries, int n_entries, int total_tiles, hipStream_t st);
 

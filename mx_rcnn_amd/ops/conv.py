@@ -64,8 +64,22 @@ def sub_filter(param, wf, th, tw, s):
     return ent[2]
 
 
-def refresh_sub_filters():
+def sub_filters_of(param):
+    """[(buf, row taps, col taps)] registered for ``param`` (the flip kernel's table writes them
+    in the same pass as the flipped filter, core/params.py)."""
+    out = []
+    for (pid, r0, r1, c0, c1, s), (p, _view, buf) in _SUBW.items():
+        if p is param:
+            out.append((buf, list(range(r0, r1 + 1, s)), list(range(c0, c1 + 1, s))))
+    return out
+
+
+def refresh_sub_filters(skip=()):
+    """Copy the sub-filters of every parameter not in ``skip`` (ids whose sub-filters the flip
+    kernel already wrote)."""
     for param, view, buf in list(_SUBW.values()):
+        if id(param) in skip:
+            continue
         wf = cached_dgrad_weight(param)
         if wf is not None:
             buf.copy_(view(wf))

@@ -166,6 +166,32 @@ def test_side_stream_grad_clear_matches_inline(cuda, monkeypatch):
 
 
 @pytest.mark.gpu
+def test_flip_kernel_writes_parity_sub_filters(cuda):
+    """After the first backward registers the strided data gradient's parity sub-filters, the
+    multi-filter flip kernel writes them in its own pass: every sub-filter equals its slice of the
+    flipped filter after later updates, and the copy path is skipped for them."""
+    from mx_rcnn_amd.ops import conv as conv_ops
+    torch.manual_seed(0)
+    m = FasterRCNN('resnet50', 21, cfg=_cfg())
+    tr = Trainer(m, 'e2e', fixed_param_prefix=['conv0', 'stage1', 'stage2', 'bn_data', 'bn0'], lr=0.01, device=cuda)
+    b = {k: v.to(cuda) for k, v in _batch(320, 480).items()}
+    for _ in range(3):
+        tr.step(b)
+    torch.cuda.synchronize()
+    assert tr.store._sub_in_table, 'no parity sub-filter was folded into the flip table'
+    tr.store.refresh_dgrad_cache()
+    torch.cuda.synchronize()
+    checked = 0
+    for (pid, r0, r1, c0, c1, st), (p, view, buf) in conv_ops._SUBW.items():
+        if id(p) not in tr.store._sub_in_table:
+            continue
+        wf = conv_ops.cached_dgrad_weight(p)
+        assert torch.equal(buf, view(wf).contiguous(memory_format=torch.channels_last))
+        checked += 1
+    assert checked >= 4
+
+
+@pytest.mark.gpu
 def test_graph_capture_has_no_training_side_effects(cuda):
     """GraphedStep's warm-up runs real steps to settle workspaces; weights, momentum, bf16
     shadows and BN moving statistics must be exactly as before the capture (a new shape must

@@ -328,3 +328,26 @@ def test_checkpoint_averages_bn_moving_stats_over_ranks():
     for k in a0:
         assert torch.allclose(a0[k], torch.full_like(a0[k], 1.5)), k
         assert torch.equal(a0[k], a1[k])
+
+
+@pytest.mark.parametrize('mode', ['rpn', 'rcnn'])
+def test_bench_alternate_stage_modes_two_ranks(tmp_path, mode):
+    """``bench.py --train-mode rpn|rcnn`` (BASELINE config 4: the alternate scheme's stages) with
+    2 self-spawned gloo ranks: one JSON line with the stage metric, n_gpus 2, finite objective."""
+    import json
+    import math
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ('RANK', 'WORLD_SIZE', 'LOCAL_RANK', 'MASTER_PORT')}
+    env.update(PYTHONPATH=root, CUDA_VISIBLE_DEVICES='', HIP_VISIBLE_DEVICES='')
+    cmd = [sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2', '--steps', '2', '--warmup', '1',
+           '--network', 'resnet18', '--image', '256x320', '--num-classes', '6', '--train-mode', mode]
+    r = subprocess.run(cmd, cwd=str(tmp_path), env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith('{')]
+    assert len(lines) == 1, r.stdout[-2000:]
+    rec = json.loads(lines[0])
+    assert rec['metric'] == 'imgs/sec alternate-stage %s train resnet18' % mode
+    assert rec['n_gpus'] == 2 and rec['config']['train_mode'] == mode
+    assert all(math.isfinite(v) for v in rec['config']['objective_first_last'])

@@ -105,7 +105,8 @@ class Trainer:
             from ..ops.fused import defer_reduces
             # no gradient hook reads the flat buffers mid-backward: split-K reduces may cross units
             with defer_reduces(not (self.reducer.overlap or self.reducer.sgd_capable)):
-                out['loss'].backward()
+                from ..ops._ext import unit_grad
+                out['loss'].backward(unit_grad(out['loss'].device))
         with prof.range('allreduce_wait'):
             self.reducer.finish()
         with prof.range('sgd'):

@@ -25,7 +25,7 @@ import torch.nn.functional as F
 from ..config import config as _global_cfg, snapshot
 from ..utils import profiler as prof
 from ..ops import anchor_target, proposal, proposal_target, roi_pool
-from ..ops._ext import const_tensor
+from ..ops._ext import unit_grad
 from ..ops.head import rpn_head
 from ..ops.losses import combine_losses, rpn_softmax_ce, smooth_l1, softmax_ce
 from .layers import Conv
@@ -276,7 +276,7 @@ class FasterRCNN(nn.Module):
                 pre = getattr(self, 'pre_backward', None)
                 if pre is not None:
                     pre()  # e.g. the trainer's dgrad filter-cache join
-                one = const_tensor([1.0], data.device).reshape(())
+                one = unit_grad(data.device)  # recognised by the loss ops: no scale kernels
                 torch.autograd.backward([rpn_cls_loss, rpn_bbox_loss], [one, one])
                 d_feat = feat_rpn.grad
             pt = pt_join()

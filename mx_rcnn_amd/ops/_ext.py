@@ -91,6 +91,29 @@ def check_sync(name):
 _CONSTS = {}
 
 
+_UNIT = {}
+
+
+def unit_grad(device):
+    """The cached 0-d fp32 one that seeds a backward pass (``loss.backward(unit_grad(dev))``).  The
+    loss ops recognise it by identity and hand back their stored gradients unscaled -- no ones
+    fill for the seed and no scale-by-1 kernel per loss term.  Never written in place."""
+    import torch
+    key = str(device)
+    t = _UNIT.get(key)
+    if t is None:
+        t = torch.ones((), dtype=torch.float32, device=device)
+        _UNIT[key] = t
+    return t
+
+
+def is_unit_grad(g):
+    if os.environ.get('MXR_UNIT_SEED', '1') == '0':
+        return False
+    t = _UNIT.get(str(g.device))
+    return t is not None and g is t
+
+
 def const_tensor(values, device, dtype=None):
     """Cached small constant tensor on ``device`` (built once, outside any hipGraph capture:
     creating it from host data inside a capture would be a forbidden synchronous copy)."""

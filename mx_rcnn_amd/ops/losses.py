@@ -12,7 +12,7 @@ mean -log p over the normalisation count, and grad_scale * sum(elementwise loss)
 """
 import torch
 
-from ._ext import ext_available, need_ext
+from ._ext import ext_available, is_unit_grad, need_ext
 
 
 class _RpnCE(torch.autograd.Function):
@@ -54,7 +54,10 @@ class _RpnCE(torch.autograd.Function):
 
 
 def _scale_grad(grad, g):
-    """The stored loss gradient times the incoming scalar (in place on the GPU: one kernel)."""
+    """The stored loss gradient times the incoming scalar (in place on the GPU: one kernel; none
+    when the backward was seeded with ``unit_grad`` and the one arrives unchanged)."""
+    if is_unit_grad(g):
+        return grad
     if (grad.is_cuda and g.dtype == torch.float32 and
             (grad.is_contiguous() or grad.is_contiguous(memory_format=torch.channels_last))):
         return need_ext().scale_by_scalar_(grad, g.reshape(1))

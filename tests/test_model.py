@@ -273,3 +273,32 @@ def test_fp16_inference_matches_fp32(cuda, net):
     e16, eb = err('fp16'), err('bf16')
     assert e16[0] <= 0.02 and e16[1] <= 0.02, e16
     assert e16[1] <= eb[1], (e16, eb)
+
+
+def test_unit_seed_backward_matches_default():
+    """A backward seeded with ops._ext.unit_grad (loss ops skip their scale-by-1) gives the same
+    gradients as the default seed, and a non-unit seed still scales."""
+    from mx_rcnn_amd.ops._ext import unit_grad
+    from mx_rcnn_amd.ops.losses import combine_losses, smooth_l1, softmax_ce
+    g = torch.Generator().manual_seed(3)
+    pred0 = torch.randn(16, 8, generator=g)
+    logits0 = torch.randn(16, 5, generator=g)
+    tgt = torch.randn(16, 8, generator=g)
+    w = torch.ones(16, 8)
+    lab = torch.randint(0, 5, (16,), generator=g)
+
+    def grads(seed):
+        pred = pred0.clone().requires_grad_()
+        logits = logits0.clone().requires_grad_()
+        l1 = smooth_l1(pred, tgt, w, w, sigma=1.0, grad_scale=0.5, slot=2)
+        ce, _ = softmax_ce(logits, lab)
+        loss, _ = combine_losses([l1, ce], [1.0, 1.0])
+        loss.backward(seed)
+        return pred.grad.clone(), logits.grad.clone()
+
+    a = grads(unit_grad(torch.device('cpu')))
+    b = grads(torch.ones(()))
+    c = grads(torch.full((), 2.0))
+    for x, y, z in zip(a, b, c):
+        assert torch.equal(x, y)
+        assert torch.allclose(z, 2 * y)

@@ -565,6 +565,26 @@ std::vector<std::tuple<std::string, int64_t, int64_t>> conv_tune_table() {
   return out;
 }
 
+// dadd either shaped like y, or the stride-s subsampled grid (N, C, ceil(Ho/s), ceil(Wo/s)) of an
+// unmapped launch (a strided projection shortcut's gradient): sets ep.dadd / ep.dadd_s
+void set_dadd(mxr::ConvEpi& ep, const Tensor& dadd, const Tensor& y, int Ho, int Wo, bool mapped) {
+  TORCH_CHECK(dadd.scalar_type() == at::kBFloat16 && dadd.is_contiguous(at::MemoryFormat::ChannelsLast) &&
+                  dadd.dim() == 4 && dadd.size(0) == y.size(0) && dadd.size(1) == y.size(1),
+              "dadd must be a channels_last bf16 (N, C, ., .) tensor like y");
+  ep.dadd = reinterpret_cast<const uint16_t*>(dadd.data_ptr());
+  if (dadd.sizes() == y.sizes()) return;
+  TORCH_CHECK(!mapped, "a subsampled dadd needs an unmapped launch");
+  for (int s = 2; s <= 8; ++s) {
+    if (dadd.size(2) == (Ho + s - 1) / s && dadd.size(3) == (Wo + s - 1) / s) {
+      ep.dadd_s = s;
+      ep.dadd_gh = Ho;
+      ep.dadd_gw = Wo;
+      return;
+    }
+  }
+  TORCH_CHECK(false, "dadd must be shaped like y or its stride-s subsampled grid");
+}
+
 // conv_igemm_fwd(x, w, bias, stride, pad, relu, tile, splits, residual, bn, bn_eps, bn_fix_gamma, act_relu)
 //   -> [y] or, when bn = (gamma, beta, mean, var) is given, [y, act(bn(y))]  (see ConvEpi)
 std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::optional<Tensor> bias, int64_t stride,
@@ -667,11 +687,7 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
     TORCH_CHECK(bx.scalar_type() == at::kBFloat16 && bx.sizes() == y.sizes() &&
                     bx.is_contiguous(at::MemoryFormat::ChannelsLast), "bnb_x must be channels_last bf16 like y");
     ep.bnb_x = reinterpret_cast<const uint16_t*>(bx.data_ptr());
-    if (dadd.has_value() && dadd->defined()) {
-      TORCH_CHECK(dadd->scalar_type() == at::kBFloat16 && dadd->sizes() == y.sizes() &&
-                      dadd->is_contiguous(at::MemoryFormat::ChannelsLast), "dadd must be channels_last bf16 like y");
-      ep.dadd = reinterpret_cast<const uint16_t*>(dadd->data_ptr());
-    }
+    if (dadd.has_value() && dadd->defined()) set_dadd(ep, *dadd, y, Ho, Wo, mapped);
     const bool det = bnb_part.has_value() && bnb_part->defined();
     if (det) {
       // deterministic column sums: 64-row tiles (tile 23) write rows bnb_row0 .. + ceil(M / 64)
@@ -878,11 +894,7 @@ std::vector<Tensor> conv_dgrad_wgrad(const Tensor& x, const Tensor& w, int64_t p
                     bnb_x->sizes() == y.sizes() && bnb_x->is_contiguous(at::MemoryFormat::ChannelsLast),
                 "bn needs bnb_x like y");
     ep.bnb_x = reinterpret_cast<const uint16_t*>(bnb_x->data_ptr());
-    if (dadd.has_value() && dadd->defined()) {
-      TORCH_CHECK(dadd->scalar_type() == at::kBFloat16 && dadd->sizes() == y.sizes() &&
-                      dadd->is_contiguous(at::MemoryFormat::ChannelsLast), "dadd like y");
-      ep.dadd = reinterpret_cast<const uint16_t*>(dadd->data_ptr());
-    }
+    if (dadd.has_value() && dadd->defined()) set_dadd(ep, *dadd, y, Ho, Wo, false);
     if (bnb_part.has_value() && bnb_part->defined()) {  // deterministic sums, 64-row dgrad tiles
       TORCH_CHECK(bnb_part->scalar_type() == at::kFloat && bnb_part->is_contiguous() &&
                       bnb_part->numel() >= (((int64_t)NB * Ho * Wo + 63) / 64) * 2 * Cout,

@@ -70,6 +70,15 @@ __device__ __forceinline__ int64_t epi_row(const ConvEpi& ep, int m, int Ho, int
   return ((int64_t)img * ep.o_H + i * ep.o_sh + ep.o_ph) * ep.o_W + j * ep.o_sw + ep.o_pw;
 }
 
+// dadd element row for output row m of the launch grid (-1: dadd has nothing there)
+__device__ __forceinline__ int64_t dadd_row(const ConvEpi& ep, int m, int64_t out_row) {
+  if (ep.dadd_s <= 1) return out_row;
+  const int s = ep.dadd_s, Ho = ep.dadd_gh, Wo = ep.dadd_gw, hw = Ho * Wo;
+  const int img = m / hw, r = m - img * hw, i = r / Wo, j = r - i * Wo;
+  if (i % s || j % s) return -1;
+  return ((int64_t)img * ((Ho + s - 1) / s) + i / s) * ((Wo + s - 1) / s) + j / s;
+}
+
 // per-output-channel epilogue constants
 struct EpiCol {
   float bias, s, t, mean, inv;
@@ -119,8 +128,8 @@ __device__ __forceinline__ void epi_store(const ConvEpi& ep, const EpiCol& c, ui
 
 // BN-backward epilogue of one element; returns (g, g * xhat) through sg / sgx
 __device__ __forceinline__ void epi_bnb(const ConvEpi& ep, const EpiCol& c, uint16_t* __restrict__ y, int64_t idx,
-                                        float v, float& sg, float& sgx) {
-  if (ep.dadd) v += h16_to_f32c(EPC, ep.dadd[idx]);
+                                        float v, float& sg, float& sgx, int64_t didx) {
+  if (ep.dadd && didx >= 0) v += h16_to_f32c(EPC, ep.dadd[didx]);
   const float xv = h16_to_f32c(EPC, ep.bnb_x[idx]);
   const float g = (!ep.act_relu || xv * c.s + c.t > 0.f) ? v : 0.f;
   sg += g;
@@ -238,7 +247,10 @@ __device__ __forceinline__ void igemm_epilogue(f32x4 (&acc)[TM][TN], int m0, int
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
-            if (m < M) epi_bnb(ep, ec, y, epi_row(ep, m, Ho, Wo) * Cout + n, acc[i][j][r], sg, sgx);
+            if (m < M) {
+              const int64_t orow = epi_row(ep, m, Ho, Wo), drow = dadd_row(ep, m, orow);
+              epi_bnb(ep, ec, y, orow * Cout + n, acc[i][j][r], sg, sgx, drow < 0 ? -1 : drow * Cout + n);
+            }
           }
       }
       sg += __shfl_xor(sg, 16, 64);
@@ -325,8 +337,9 @@ __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* 
       const float4 a0 = src[0], a1 = src[1];
       a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w; a[4] = a1.x; a[5] = a1.y; a[6] = a1.z; a[7] = a1.w;
       ld8_h16(ep.bnb_x + e, xv, EPC);
-      if (ep.dadd) {
-        ld8_h16(ep.dadd + e, d, EPC);
+      const int64_t drow = ep.dadd ? dadd_row(ep, m, e / Cout) : -1;
+      if (drow >= 0) {
+        ld8_h16(ep.dadd + drow * Cout + n, d, EPC);
 #pragma unroll
         for (int k = 0; k < 8; ++k) a[k] += d[k];
       }
@@ -541,8 +554,9 @@ splitk_reduce_bnb_kernel(const float* __restrict__ slab, int splits, int M, int 
         a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
       }
       const float v[4] = {a.x, a.y, a.z, a.w};
+      const int64_t drow = dadd_row(ep, r, r);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) epi_bnb(ep, ec[k], y, e + k, v[k], sg[k], sgx[k]);
+      for (int k = 0; k < 4; ++k) epi_bnb(ep, ec[k], y, e + k, v[k], sg[k], sgx[k], drow < 0 ? -1 : drow * Cout + n + k);
     }
   }
 #pragma unroll
@@ -1008,8 +1022,9 @@ __device__ __forceinline__ void ring_epilogue(f32x4 (&acc)[TM][TN], float* __res
       const float4 a0 = src[0], a1 = src[1];
       a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w; a[4] = a1.x; a[5] = a1.y; a[6] = a1.z; a[7] = a1.w;
       ld8_h16(ep.bnb_x + e, xv, EPC);
-      if (ep.dadd) {
-        ld8_h16(ep.dadd + e, d, EPC);
+      const int64_t drow = ep.dadd ? dadd_row(ep, m, e / Cout) : -1;
+      if (drow >= 0) {
+        ld8_h16(ep.dadd + drow * Cout + n, d, EPC);
 #pragma unroll
         for (int k = 0; k < 8; ++k) a[k] += d[k];
       }

@@ -172,6 +172,11 @@ struct ConvEpi {
   // dgamma += sum_rows g * xhat, dbeta += sum_rows g (fp32 atomics; may be null).
   const uint16_t* bnb_x = nullptr;
   const uint16_t* dadd = nullptr;
+  // dadd_s > 1: dadd is the stride-dadd_s subsampled grid (ceil(Ho/s) x ceil(Wo/s)) of this
+  // launch's Ho x Wo grid and adds only at rows (img, i*s, j*s) -- a strided projection
+  // shortcut's gradient, without scattering it into a zero-filled full-size map first
+  int dadd_s = 0;
+  int dadd_gh = 0, dadd_gw = 0;  // the launch grid (Ho, Wo) the subsampled dadd refers to
   float* bnb_dgamma = nullptr;
   float* bnb_dbeta = nullptr;
   // inverted dropout AFTER bias/residual/ReLU (the FC head's ReLU -> Dropout, rcnn/symbol.py:98,102):

@@ -15,6 +15,8 @@ gradient buffers; for ``conv_add_bn_relu`` that kernel also adds the residual-pa
 (``dres``), replacing autograd's gradient-accumulation add.  Numerics equal the unfused
 sequence: the BN reads the bf16-rounded conv output, exactly like the separate kernels.
 """
+import os
+
 import torch
 
 from . import grad_sink
@@ -563,7 +565,10 @@ class _FusedUnitFn(torch.autograd.Function):
             from .conv import dgrad_weight
             d_sub = ext.conv_igemm_fwd(d_out, dgrad_weight(ctx.params[nconv - 1], ws[nconv - 1]), None, 1, 0,
                                        False)[0]
-            if s == 1:
+            if s == 1 or (s1 == 1 and ws[0].shape[0] % 64 == 0 and
+                          os.environ.get('MXR_SUB_DADD', '1') != '0'):
+                # stride s > 1: the stride-1 dgrad below adds d_sub at rows (i*s, j*s) itself
+                # (subsampled dadd epilogue), no zero-filled full-size scatter
                 d_sc = d_sub
             else:
                 d_sc = torch.zeros_like(act1, memory_format=torch.channels_last)

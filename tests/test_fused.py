@@ -183,6 +183,36 @@ def test_bnb_epilogue_vs_reference(cuda):
             assert err <= 2e-2 * r.abs().max().item() + 2e-2, (Cin, Cout, k, splits, tile, err)
 
 
+@pytest.mark.gpu
+def test_bnb_epilogue_subsampled_dadd(cuda):
+    """A stride-s subsampled dadd (a strided projection shortcut's gradient) added by the BN-backward
+    epilogue at rows (i*s, j*s) == the same dadd scattered into a zero-filled full-size map, for the
+    direct, LDS, ring and split-K epilogues and the grouped dgrad+wgrad launch."""
+    from mx_rcnn_amd.ops import need_ext
+    from mx_rcnn_amd.ops.conv import _flip_t
+    ext = need_ext()
+    g = torch.Generator().manual_seed(43)
+    for (Cin, Cout, k, H, W, splits, tile, st) in ((256, 1024, 1, 24, 40, 1, 0, 2), (256, 1024, 1, 23, 37, 4, 0, 2),
+                                                   (256, 1024, 1, 24, 40, 1, 105, 2), (256, 256, 3, 20, 30, 1, 106, 2),
+                                                   (256, 1024, 1, 25, 31, 2, 106, 2)):
+        w = (torch.randn(Cout, Cin, k, k, generator=g) * 0.05).bfloat16()
+        dy = _cl(torch.randn(1, Cout, H, W, generator=g).bfloat16(), cuda)
+        xr = _cl(torch.randn(1, Cin, H, W, generator=g).bfloat16(), cuda)
+        sub = _cl(torch.randn(1, Cin, (H + st - 1) // st, (W + st - 1) // st, generator=g).bfloat16(), cuda)
+        full = torch.zeros(1, Cin, H, W, dtype=torch.bfloat16, device=cuda).contiguous(memory_format=torch.channels_last)
+        full[:, :, ::st, ::st] = sub
+        bn = [t.to(cuda) for t in (torch.rand(Cin, generator=g) + 0.5, torch.randn(Cin, generator=g) * 0.1,
+                                   torch.randn(Cin, generator=g) * 0.2, torch.rand(Cin, generator=g) + 0.5)]
+        wt = _flip_t(_cl(w, cuda))
+        p = k // 2
+        outs = [ext.conv_igemm_fwd(dy, wt, None, 1, k - 1 - p, False, tile, splits, None, bn, 2e-5, False, True,
+                                   xr, d) for d in (sub, full)]
+        # dx bitwise; dgamma / dbeta are fp32 atomic sums (summation order varies run to run)
+        torch.testing.assert_close(outs[0][0].float(), outs[1][0].float(), rtol=0, atol=0)
+        for a, b in zip(outs[0][1:], outs[1][1:]):
+            torch.testing.assert_close(a.float(), b.float(), rtol=1e-4, atol=1e-4)
+
+
 def test_fused_trunk_step_matches_unfused(cuda):
     """One full e2e step on a small ResNet-50: fused and unfused trunks give the same losses."""
     from mx_rcnn_amd.config import snapshot

@@ -9,8 +9,9 @@
 //   det_class_nms_kernel  grid (B, C-1): one workgroup per (image, class).  Threshold-collect
 //       the class scores into LDS (LDS atomic slot counter), bitonic-sort them (score desc, RoI
 //       index asc on ties -> the reference's stable order), decode + clip the survivors, greedy
-//       NMS over the sorted list (suppression flags in LDS, one barrier per kept box), write the
-//       kept (score, box) list of the class.
+//       NMS over the sorted list (a suppression bitmask resolved by one wave; above 512
+//       candidates suppression flags with one barrier per kept box), write the kept (score, box)
+//       list of the class.
 //   det_topk_kernel       grid B: one workgroup per image.  Radix-select the max_per_image-th
 //       largest kept score (4 passes of 8-bit LDS histograms over the float bits; scores are
 //       positive so their bits order like the values), then compact the detections scoring >= it
@@ -26,6 +27,7 @@
 namespace mxr {
 
 constexpr int kDetMaxR = 1024;  // RoIs per image handled by one (image, class) workgroup
+constexpr int kDetBits = 512;   // classes with up to this many candidates take the bitmask NMS
 
 __device__ __forceinline__ bool det_before(float sa, int ia, float sb, int ib) {
   return sa > sb || (sa == sb && ia < ib);
@@ -39,6 +41,7 @@ det_class_nms_kernel(const float* __restrict__ rois, const float* __restrict__ s
   __shared__ int idx[kDetMaxR];
   __shared__ float box[kDetMaxR][4];
   __shared__ unsigned char sup[kDetMaxR];
+  __shared__ uint64_t smask[kDetBits * (kDetBits / 64)];
   __shared__ int n_s, kept_s;
   const int b = blockIdx.x, c = blockIdx.y + 1, tid = threadIdx.x;
   if (tid == 0) n_s = 0;
@@ -99,6 +102,36 @@ det_class_nms_kernel(const float* __restrict__ rois, const float* __restrict__ s
     sup[i] = 0;
   }
   __syncthreads();
+  if (n <= kDetBits) {
+    // greedy NMS in score order as a suppression bitmask: every thread fills words of
+    // mask[i][w] (bit t: box i suppresses box 64w + t > i), then ONE wave resolves the boxes in
+    // order with the removed set held one 64-bit word per lane -- no barrier per kept box (the
+    // loop below pays one per kept box: ~100 us for a class with a few hundred survivors)
+    const int nw = (n + 63) >> 6;
+    for (int e = tid; e < n * nw; e += 256) {
+      const int i = e / nw, w = e - i * nw;
+      const float ax1 = box[i][0], ay1 = box[i][1], ax2 = box[i][2], ay2 = box[i][3];
+      const float aa = (ax2 - ax1 + 1.f) * (ay2 - ay1 + 1.f);
+      uint64_t bits = 0;
+      const int j1 = min(n, 64 * w + 64);
+      for (int j = max(64 * w, i + 1); j < j1; ++j) {
+        const float bb = (box[j][2] - box[j][0] + 1.f) * (box[j][3] - box[j][1] + 1.f);
+        if (iou_plus1(ax1, ay1, ax2, ay2, aa, box[j][0], box[j][1], box[j][2], box[j][3], bb) > nms_thresh)
+          bits |= 1ull << (j - 64 * w);
+      }
+      smask[e] = bits;
+    }
+    __syncthreads();
+    if (tid < 64) {
+      uint64_t rem = 0;  // lane l: removed bits of boxes 64l .. 64l + 63
+      for (int i = 0; i < n; ++i) {
+        const uint64_t wi = __shfl(rem, i >> 6, 64);
+        if (!((wi >> (i & 63)) & 1ull) && tid < nw) rem |= smask[i * nw + tid];
+      }
+      for (int j = tid; j < n; j += 64) sup[j] = (unsigned char)((__shfl(rem, j >> 6, 64) >> (j & 63)) & 1ull);
+    }
+    __syncthreads();
+  } else {
   // greedy NMS in score order
   for (int i = 0; i < n; ++i) {
     if (sup[i]) continue;  // uniform: every thread reads the same LDS flag after the barrier
@@ -110,6 +143,7 @@ det_class_nms_kernel(const float* __restrict__ rois, const float* __restrict__ s
       if (iou_plus1(ax1, ay1, ax2, ay2, aa, box[j][0], box[j][1], box[j][2], box[j][3], bb) > nms_thresh) sup[j] = 1;
     }
     __syncthreads();
+  }
   }
   // compact the kept list (order preserved): one wave ballots 64 flags at a time
   if (tid < 64) {

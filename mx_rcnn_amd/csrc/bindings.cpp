@@ -96,7 +96,6 @@ std::vector<Tensor> nms_proposals(const Tensor& boxes, const Tensor& scores, con
   TORCH_CHECK(P > 0, "NMS needs at least one box slot");
   DevGuard g(boxes.device());
   const int nb = (P + 63) / 64;
-  TORCH_CHECK(mxr::nms_reduce_lds(P, (int)post) <= 160 * 1024, "NMS LDS budget exceeded (P or post too large)");
   TORCH_CHECK(nb <= 1024, "NMS supports at most 65536 pre-NMS boxes per image");
   auto st = cur_stream();
   Tensor mask;
@@ -114,10 +113,13 @@ std::vector<Tensor> nms_proposals(const Tensor& boxes, const Tensor& scores, con
   Tensor out_scores = at::empty({B, post}, boxes.options());
   Tensor keep = at::empty({B, post}, boxes.options().dtype(at::kLong));
   Tensor n_keep = at::empty({B}, boxes.options().dtype(at::kInt));
+  Tensor keep_ws;  // keep list beyond the LDS budget (post = all boxes of a > 32K-box image)
+  if (!mxr::nms_keep_in_lds(P, (int)post)) keep_ws = at::empty({B, post}, boxes.options().dtype(at::kInt));
   mxr::nms_reduce(boxes.data_ptr<float>(), scores.data_ptr<float>(), n_valid.data_ptr<int32_t>(),
                   reinterpret_cast<const uint64_t*>(mask.data_ptr<int64_t>()), B, P, (int)post,
                   rand_u.data_ptr<float>(), rois.data_ptr<float>(), out_scores.data_ptr<float>(),
-                  keep.data_ptr<int64_t>(), n_keep.data_ptr<int32_t>(), st);
+                  keep.data_ptr<int64_t>(), n_keep.data_ptr<int32_t>(),
+                  keep_ws.defined() ? keep_ws.data_ptr<int32_t>() : nullptr, st);
   LAUNCH_CHECK("nms_reduce");
   return {rois, out_scores, keep, n_keep};
 }
@@ -144,6 +146,26 @@ std::vector<Tensor> proposal_gather(const Tensor& skeys, const Tensor& order, co
                        ok.data_ptr<float>(), ob.data_ptr<float>(), nv.data_ptr<int32_t>(), cur_stream());
   LAUNCH_CHECK("proposal_gather");
   return {ok, ob, nv};
+}
+
+// MXR_NMS_CHECK: recompute greedy NMS on the device with a plain flag loop and compare with the
+// reducer's keep list; returns (B, 2) int32 {first differing keep position or -1, greedy kept count}
+Tensor nms_check(const Tensor& boxes, const Tensor& n_valid, double thresh, int64_t post, const Tensor& keep,
+                 const Tensor& n_keep) {
+  CHECK_DEV(boxes); CHECK_F32(boxes); CHECK_CONTIG(boxes);
+  CHECK_DEV(n_valid); CHECK_I32(n_valid); CHECK_CONTIG(n_valid);
+  CHECK_DEV(n_keep); CHECK_I32(n_keep); CHECK_CONTIG(n_keep);
+  TORCH_CHECK(boxes.dim() == 3 && boxes.size(2) == 4, "boxes must be (B, P, 4)");
+  const int B = (int)boxes.size(0), P = (int)boxes.size(1);
+  TORCH_CHECK(keep.scalar_type() == at::kLong && keep.is_contiguous() && keep.dim() == 2 && keep.size(0) == B &&
+                  keep.size(1) == post, "keep must be (B, post) int64");
+  TORCH_CHECK(n_valid.numel() == B && n_keep.numel() == B && P > 0 && P <= 65536, "nms_check: shape");
+  DevGuard g(boxes.device());
+  Tensor res = at::empty({B, 2}, boxes.options().dtype(at::kInt));
+  mxr::nms_check(boxes.data_ptr<float>(), n_valid.data_ptr<int32_t>(), B, P, (float)thresh, (int)post,
+                 keep.data_ptr<int64_t>(), n_keep.data_ptr<int32_t>(), res.data_ptr<int32_t>(), cur_stream());
+  LAUNCH_CHECK("nms_check");
+  return res;
 }
 
 Tensor nms_mask_build(const Tensor& boxes, const Tensor& n_valid, double thresh) {
@@ -1749,6 +1771,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nms_proposals", &nms_proposals, py::arg("boxes"), py::arg("scores"), py::arg("n_valid"), py::arg("thresh"),
         py::arg("post"), py::arg("rand_u"), py::arg("mask") = py::none());
   m.def("nms_mask_build", &nms_mask_build);
+  m.def("nms_check", &nms_check);
   m.def("nms_cpu", &nms_cpu);
   m.def("roi_pool_fwd_cpu", &roi_pool_fwd_cpu);
   m.def("roi_pool_bwd_cpu", &roi_pool_bwd_cpu);

@@ -82,9 +82,11 @@ __global__ void __launch_bounds__(1024)
 nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ scores,
                   const int32_t* __restrict__ n_valid, const uint64_t* __restrict__ maskT, int P, int nb, int post,
                   const float* __restrict__ rand_u, float* __restrict__ rois, float* __restrict__ out_scores,
-                  int64_t* __restrict__ keep_idx, int32_t* __restrict__ n_keep_out) {
+                  int64_t* __restrict__ keep_idx, int32_t* __restrict__ n_keep_out, int32_t* keep_ws) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  // single dynamic LDS region (Guideline 17): [nkeep 2 x i32 | pad][removed nb u64][keptw nb u64][keep_list post i32]
+  // single dynamic LDS region (Guideline 17): [nkeep 2 x i32 | pad][removed nb u64][keptw nb u64][keep_list post i32];
+  // the keep list moves to global memory (keep_ws, (B, post) int32) when it does not fit in LDS
+  // (post = all boxes of a > 32K-box image)
   // The kept count is double-buffered: iteration t reads s_nk[t & 1] (written in t-1) and wave 0
   // writes s_nk[(t + 1) & 1].  A single slot let a late helper wave read wave 0's iteration-t
   // update at the top of iteration t, break out of the loop alone and skip the barrier the
@@ -93,8 +95,8 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
   int* s_nk = reinterpret_cast<int*>(smem);
   uint64_t* removed = reinterpret_cast<uint64_t*>(smem + 16);
   uint64_t* keptw = removed + nb;
-  int32_t* keep_list = reinterpret_cast<int32_t*>(keptw + nb);
   const int b = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  int32_t* keep_list = keep_ws ? keep_ws + (int64_t)b * post : reinterpret_cast<int32_t*>(keptw + nb);
   const int nv = min(n_valid[b], P);
   const int64_t Pp = nms_row_words(nb);
   const uint64_t* mb = maskT + (int64_t)b * nb * Pp;
@@ -152,7 +154,11 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
       }
     } else {
       const int h = wave - 1;
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the asm prefetch is invisible to hipcc
+      // vmcnt(0) through the builtin, which the compiler's wait-count pass sees: it then knows the
+      // previous iteration's prefetch has landed, and issues this iteration's guarded prefetch
+      // loads back to back instead of draining before each (the skipped-slot path could otherwise
+      // still have a load in flight into the same registers).
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15 (no wait)
       if (t >= 1) {
         const uint64_t kp = keptw[t - 1];
         if (kp) {
@@ -191,17 +197,16 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
       // prefetch row block t for iteration t+1: the pairs q0' + h + 15k (q0' = (t+2)/2) whose
       // first column is < nbv.  One CU streams the whole triangle and every wave-load costs the
       // CU's address path about the same at 8 and 16 B per lane, so a slot fetches two column
-      // blocks and unneeded slots do not issue at all.  hipcc waits vmcnt(0) after each guarded
-      // C++ load, so the loads are inline asm ("+v": the slot keeps its registers on the skipped
-      // path, no phi copy) and the helper waits for them explicitly before consuming (above).
+      // blocks and unneeded slots do not issue at all.  These are ordinary loads: the compiler
+      // tracks them, so a wave leaving the loop with a prefetch in flight waits before any
+      // register of it is reused.  (Round 2 issued them as inline asm, invisible to the compiler's
+      // wait-count pass: after an early exit at `post` kept boxes, a late prefetch could land in
+      // registers the epilogue had reused for the kept count, corrupting the keep list.)
       const int q0n = (t + 2) >> 1;
       const uint64_t* rowp = mb + (int64_t)t * Pp + (int64_t)(q0n + h) * 128 + lane * 2;
 #pragma unroll
       for (int k = 0; k < NMS_PF; ++k) {
-        if (2 * (q0n + h + NMS_HELPERS * k) < nbv) {
-          const uint64_t* src = rowp + NMS_HELPERS * 128 * k;
-          asm volatile("global_load_dwordx4 %0, %1, off" : "+v"(pf[k]) : "v"(src) : "memory");
-        }
+        if (2 * (q0n + h + NMS_HELPERS * k) < nbv) pf[k] = *reinterpret_cast<const u64x2*>(rowp + NMS_HELPERS * 128 * k);
       }
     }
     __syncthreads();
@@ -230,6 +235,55 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
   }
 }
 
+// MXR_NMS_CHECK=1 oracle: the plain greedy flag loop on the device (one 1024-thread workgroup per
+// image, a suppression bit per box in LDS, one barrier per visited box), with the same IoU
+// arithmetic as nms_mask_kernel, so it checks the reducer's logic rather than float rounding.
+// result[b] = {first keep position where the reducer differs (-1 if none), greedy kept count}.
+__global__ void __launch_bounds__(1024)
+nms_check_kernel(const float* __restrict__ boxes, const int32_t* __restrict__ n_valid, int P, float thresh, int post,
+                 const int64_t* __restrict__ keep_idx, const int32_t* __restrict__ n_keep, int32_t* __restrict__ result) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint32_t* removed = reinterpret_cast<uint32_t*>(smem);  // ceil(P / 32) words
+  __shared__ int s_bad;
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const int nv = min(n_valid[b], P);
+  const int nw = (P + 31) / 32;
+  for (int w = tid; w < nw; w += blockDim.x) removed[w] = 0u;
+  if (tid == 0) s_bad = -1;
+  __syncthreads();
+  const float4* bx = reinterpret_cast<const float4*>(boxes) + (int64_t)b * P;
+  const int64_t* kp = keep_idx + (int64_t)b * post;
+  const int nk_dev = n_keep[b];
+  int cnt = 0;
+  for (int i = 0; i < nv && cnt < post; ++i) {
+    if ((removed[i >> 5] >> (i & 31)) & 1u) continue;  // uniform: read after the last barrier
+    if (tid == 0 && s_bad < 0 && (cnt >= nk_dev || kp[cnt] != i)) s_bad = cnt;
+    ++cnt;
+    const float4 r = bx[i];
+    const float ra = (r.z - r.x + 1.f) * (r.w - r.y + 1.f);
+    for (int j = i + 1 + tid; j < nv; j += blockDim.x) {
+      const float4 c = bx[j];
+      const float ca = (c.z - c.x + 1.f) * (c.w - c.y + 1.f);
+      if (iou_plus1(r.x, r.y, r.z, r.w, ra, c.x, c.y, c.z, c.w, ca) > thresh) atomicOr(&removed[j >> 5], 1u << (j & 31));
+    }
+    __syncthreads();
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int bad = s_bad;
+    if (bad < 0 && nk_dev != cnt) bad = min(cnt, nk_dev);
+    result[2 * b] = bad;
+    result[2 * b + 1] = cnt;
+  }
+}
+
+void nms_check(const float* boxes, const int32_t* n_valid, int B, int P, float thresh, int post,
+               const int64_t* keep_idx, const int32_t* n_keep, int32_t* result, hipStream_t st) {
+  if (B == 0 || P == 0) return;
+  nms_check_kernel<<<B, 1024, (size_t)((P + 31) / 32) * 4, st>>>(boxes, n_valid, P, thresh, post, keep_idx, n_keep,
+                                                                 result);
+}
+
 int64_t nms_mask_words(int B, int P) {
   const int nb = div_up(P, 64);
   return (int64_t)B * nb * nms_row_words(nb);
@@ -248,13 +302,16 @@ size_t nms_reduce_lds(int P, int post) {
   return 16 + (size_t)nb * 16 + (size_t)post * 4;
 }
 
+bool nms_keep_in_lds(int P, int post) { return nms_reduce_lds(P, post) <= 160 * 1024; }
+
 void nms_reduce(const float* boxes, const float* scores, const int32_t* n_valid, const uint64_t* mask, int B,
                 int P, int post, const float* rand_u, float* rois, float* out_scores, int64_t* keep_idx,
-                int32_t* n_keep, hipStream_t st) {
+                int32_t* n_keep, int32_t* keep_ws, hipStream_t st) {
   if (B == 0) return;
   const int nb = div_up(P, 64);
-  nms_reduce_kernel<<<B, 1024, nms_reduce_lds(P, post), st>>>(boxes, scores, n_valid, mask, P, nb, post, rand_u,
-                                                             rois, out_scores, keep_idx, n_keep);
+  const size_t lds = keep_ws ? nms_reduce_lds(P, 0) : nms_reduce_lds(P, post);
+  nms_reduce_kernel<<<B, 1024, lds, st>>>(boxes, scores, n_valid, mask, P, nb, post, rand_u, rois, out_scores,
+                                          keep_idx, n_keep, keep_ws);
 }
 
 }  // namespace mxr

@@ -29,6 +29,8 @@ void proposal_decode(const void* cls, int cls_bf16, int64_t cs0, int64_t cs1, in
 // mask workspace: nms_mask_words(B, P) uint64 (transposed, column blocks paired: [B][nb][ceil(nb/2)*128], nb = ceil(P/64)).
 int64_t nms_mask_words(int B, int P);
 size_t nms_reduce_lds(int P, int post);
+// the reducer keeps its keep list in LDS when this holds, else in a (B, post) int32 global workspace
+bool nms_keep_in_lds(int P, int post);
 void nms_mask(const float* boxes, const int32_t* n_valid, int B, int P, float thresh,
               uint64_t* mask, hipStream_t st);
 // Greedy reduction + output assembly: keep up to `post` boxes per image; slots
@@ -36,7 +38,10 @@ void nms_mask(const float* boxes, const int32_t* n_valid, int B, int P, float th
 // rois (B, post, 5) = [b, x1, y1, x2, y2], out_scores (B, post), n_keep (B).
 void nms_reduce(const float* boxes, const float* scores, const int32_t* n_valid, const uint64_t* mask,
                 int B, int P, int post, const float* rand_u, float* rois, float* out_scores,
-                int64_t* keep_idx, int32_t* n_keep, hipStream_t st);
+                int64_t* keep_idx, int32_t* n_keep, int32_t* keep_ws, hipStream_t st);
+// device greedy-NMS oracle (MXR_NMS_CHECK): result (B, 2) int32 = {first differing keep position or -1, kept count}
+void nms_check(const float* boxes, const int32_t* n_valid, int B, int P, float thresh, int post,
+               const int64_t* keep_idx, const int32_t* n_keep, int32_t* result, hipStream_t st);
 
 // ---- IoU / target assignment (assign.hip) ----------------------------------
 // boxes (B, N, bs) with box at [off..off+4), gt (B, G, 5) padded with -1 rows, n_gt (B).

@@ -9,11 +9,13 @@
 GPU tensors run the two-stage bitmask kernel (csrc/hip/nms.hip); CPU tensors a
 vectorised greedy loop with the same visiting order and suppression rule (IoU > thresh).
 """
+import os
+
 import torch
 
 from ._ext import need_ext
 
-MAX_GPU_BOXES = 32768  # one bitmask pass: 512 64-box blocks, keep list (4 B/box) within LDS
+MAX_GPU_BOXES = 65536  # one bitmask pass: at most 1024 64-box blocks (keep list in LDS or, if larger, global)
 
 
 def _greedy_ref(boxes, n_valid, thresh, max_keep=None):
@@ -54,6 +56,22 @@ def _greedy_loop(boxes, n, thresh, max_keep=None):
     return keep
 
 
+def nms_debug_check(sboxes, n_valid, thresh, post, keep, n_keep):
+    """``MXR_NMS_CHECK=1``: recompute the greedy keep list on the device with a plain flag loop
+    (csrc/hip/nms.hip ``nms_check_kernel``) and raise on the first position where the bitmask
+    reducer differs.  Synchronises, so it is skipped while a graph is being captured."""
+    if os.environ.get('MXR_NMS_CHECK', '0') != '1' or torch.cuda.is_current_stream_capturing():
+        return
+    res = need_ext().nms_check(sboxes, n_valid, float(thresh), int(post), keep, n_keep).cpu()
+    for b in range(res.shape[0]):
+        bad, cnt = int(res[b, 0]), int(res[b, 1])
+        if bad >= 0:
+            got = keep[b, max(bad - 2, 0):bad + 3].tolist()
+            raise RuntimeError('MXR_NMS_CHECK: image %d: NMS reducer differs from the device greedy oracle at keep '
+                               'position %d (oracle kept %d, reducer %d; reducer keep[%d:%d] = %s)'
+                               % (b, bad, cnt, int(n_keep[b]), max(bad - 2, 0), bad + 3, got))
+
+
 def sort_desc(scores):
     """Descending stable order (ties -> lower index first)."""
     return torch.sort(scores, dim=-1, descending=True, stable=True)
@@ -72,6 +90,7 @@ def nms(boxes, scores, thresh, max_keep=None):
         nv = torch.full((1,), n, dtype=torch.int32, device=boxes.device)
         u = torch.zeros(1, post, device=boxes.device)
         _, _, keep, n_keep = C.nms_proposals(b[None], s[None].contiguous(), nv, float(thresh), post, u)
+        nms_debug_check(b[None], nv, thresh, post, keep, n_keep)
         k = int(n_keep.item())  # host read: test-time API returns a variable-length list
         return order[keep[0, :k]]
     keep = _greedy_ref(b, n, thresh, max_keep)

@@ -21,7 +21,7 @@ import torch
 from ._ext import ext_available, need_ext
 from .anchors import base_anchors
 from .boxes import bbox_pred, clip_boxes
-from .nms import _greedy_ref
+from .nms import _greedy_ref, nms_debug_check
 
 
 def _decode_ref(cls, dlt, im_info, base, feat_stride, min_size, crop, is_prob):
@@ -106,7 +106,9 @@ def proposal(cls, bbox_deltas, im_info, feat_stride=16, scales=(8, 16, 32), rati
             if after_mask is not None:
                 mask = C.nms_mask_build(sboxes, n_valid, float(nms_thresh))
                 after_mask()
-            rois, scores, _, _ = C.nms_proposals(sboxes, skeys, n_valid, float(nms_thresh), post, rand_u, mask)
+            rois, scores, keep, n_keep = C.nms_proposals(sboxes, skeys, n_valid, float(nms_thresh), post, rand_u,
+                                                         mask)
+            nms_debug_check(sboxes, n_valid, nms_thresh, post, keep, n_keep)
             return rois, scores
         rois = torch.zeros(B, post, 5)
         scores = torch.zeros(B, post)

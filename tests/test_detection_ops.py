@@ -171,9 +171,91 @@ def test_nms_gpu_training_scale(cuda):
         s = torch.rand(n, generator=g)
         k_cpu = ops.nms(b, s, th, max_keep=post)
         k_gpu = ops.nms(b.to(cuda), s.to(cuda), th, max_keep=post).cpu()
-        assert torch.equal(k_cpu, k_gpu), (n, th, post)
+        assert torch.equal(k_cpu, k_gpu), nms_mismatch_report(b, k_cpu, k_gpu, th, (n, th, post))
         if post is not None:
             assert k_gpu.numel() == post
+
+
+def nms_mismatch_report(boxes, k_ref, k_got, th, tag):
+    """First differing keep position, the two boxes there, their IoU (fp32 and fp64) against th,
+    and whether the GPU dropped the oracle's box or kept an extra one."""
+    n = min(k_ref.numel(), k_got.numel())
+    diff = (k_ref[:n] != k_got[:n]).nonzero()
+    pos = int(diff[0]) if diff.numel() else n
+    msg = ['%s: keep lists differ at position %d (oracle %d kept, GPU %d)' % (tag, pos, k_ref.numel(), k_got.numel())]
+    if pos < n:
+        i, j = int(k_ref[pos]), int(k_got[pos])
+        for dt in (torch.float32, torch.float64):
+            a, c = boxes[i].to(dt), boxes[j].to(dt)
+            iw = (torch.minimum(a[2], c[2]) - torch.maximum(a[0], c[0]) + 1).clamp_min(0)
+            ih = (torch.minimum(a[3], c[3]) - torch.maximum(a[1], c[1]) + 1).clamp_min(0)
+            inter = iw * ih
+            area = lambda q: (q[2] - q[0] + 1) * (q[3] - q[1] + 1)
+            msg.append('%s IoU(oracle box %d, GPU box %d) = %.9g vs %g' % (dt, i, j, float(inter / (area(a) + area(c) - inter)), th))
+        msg.append('GPU %s' % ('dropped oracle box %d' % i if i not in set(k_got.tolist()) else 'kept extra box %d' % j))
+    return '; '.join(msg)
+
+
+def rpn_like_boxes(g, P, H=50, W=84, stride=16, im=(800, 1333)):
+    """P proposal-shaped boxes: anchors of 4 scales x 3 ratios on the stride-16 grid of an
+    800x1333 image with small random deltas, clipped, in descending-score order (the layout
+    the proposal layer hands to NMS; heavy overlap, unlike uniform random boxes)."""
+    base = ops.base_anchors(16, (4, 8, 16, 32), (0.5, 1, 2))
+    sy, sx = torch.meshgrid(torch.arange(H) * stride, torch.arange(W) * stride, indexing='ij')
+    shifts = torch.stack([sx, sy, sx, sy], -1).reshape(-1, 1, 4).float()
+    anchors = (shifts + base[None]).reshape(-1, 4)
+    idx = torch.randperm(anchors.shape[0], generator=g)[:P]
+    a = anchors[idx]
+    w, h = a[:, 2] - a[:, 0] + 1, a[:, 3] - a[:, 1] + 1
+    d = torch.randn(P, 4, generator=g) * torch.tensor([0.1, 0.1, 0.2, 0.2])
+    cx, cy = a[:, 0] + 0.5 * (w - 1) + d[:, 0] * w, a[:, 1] + 0.5 * (h - 1) + d[:, 1] * h
+    pw, ph = w * torch.exp(d[:, 2]), h * torch.exp(d[:, 3])
+    b = torch.stack([cx - 0.5 * (pw - 1), cy - 0.5 * (ph - 1), cx + 0.5 * (pw - 1), cy + 0.5 * (ph - 1)], 1)
+    b[:, 0::2] = b[:, 0::2].clamp(0, im[1] - 1)
+    b[:, 1::2] = b[:, 1::2].clamp(0, im[0] - 1)
+    return b.contiguous()
+
+
+def test_nms_cpu_twin_on_proposal_shaped_boxes():
+    """The C++ twin (CPU oracle of the GPU tests below) against the tensor greedy loop on the
+    heavily overlapping proposal-shaped boxes, with and without truncation."""
+    from mx_rcnn_amd.ops.nms import _greedy_loop, _greedy_ref
+    g = torch.Generator().manual_seed(3)
+    b = rpn_like_boxes(g, 3000)
+    for post in (None, 500):
+        ref = _greedy_loop(b, 3000, 0.7, post)
+        assert _greedy_ref(b, 3000, 0.7, post) == ref
+        assert len(ref) < 3000 and (post is None or len(ref) == post)
+
+
+# the RPN-dump shapes of tools/test_rpn.py (pre-NMS = all anchors): VGG 600x1000, 30000, ResNet 800x1333
+LARGE_NMS = [(20646, 2000), (20646, 6000), (20646, -1), (30000, 2000), (30000, 6000), (30000, -1), (50400, 2000),
+             (50400, 6000), (50400, -1)]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('P,post', LARGE_NMS)
+def test_nms_gpu_large_matches_oracles(cuda, P, post):
+    """Beyond the helpers' prefetch window, with and without early exit at `post`: the reducer's
+    keep list equals the device flag-loop oracle (MXR_NMS_CHECK's kernel) and the CPU greedy
+    oracle, on proposal-shaped (heavily overlapping) boxes."""
+    from mx_rcnn_amd.ops import need_ext
+    C = need_ext()
+    g = torch.Generator().manual_seed(P + post)
+    b = rpn_like_boxes(g, P)
+    s = torch.sort(torch.rand(P, generator=g), descending=True).values
+    pst = P if post < 0 else post
+    nv = torch.tensor([P], dtype=torch.int32, device=cuda)
+    u = torch.rand(1, pst, generator=g).to(cuda)
+    bd, sd = b[None].to(cuda), s[None].to(cuda)
+    _, _, keep, n_keep = C.nms_proposals(bd, sd, nv, 0.7, pst, u)
+    res = C.nms_check(bd, nv, 0.7, pst, keep, n_keep).cpu()
+    nk = int(n_keep[0])
+    assert int(res[0, 0]) == -1 and int(res[0, 1]) == nk, (res.tolist(), nk)
+    from mx_rcnn_amd.ops.nms import _greedy_ref
+    ref = torch.tensor(_greedy_ref(b, P, 0.7, pst), dtype=torch.long)
+    got = keep[0, :nk].cpu()
+    assert torch.equal(ref, got), nms_mismatch_report(b, ref, got, 0.7, (P, post))
 
 
 @pytest.mark.gpu

@@ -10,7 +10,7 @@ import pytest
 import torch
 
 from mx_rcnn_amd import ops
-from tests.test_detection_ops import _rpn_inputs, rand_boxes
+from tests.test_detection_ops import LARGE_NMS, _rpn_inputs, rand_boxes, rpn_like_boxes
 from tests.test_kernels import _rois
 
 KW = dict(feat_stride=16, scales=(8, 16, 32), ratios=(0.5, 1, 2), pre_nms_top_n=6000, post_nms_top_n=300,
@@ -65,6 +65,26 @@ def test_nms_proposals_gpu_repeatable(cuda):
     u = torch.rand(1, post, generator=g).to(cuda)
     out1 = [t.clone() for t in C.nms_proposals(b, s, nv, 0.7, post, u)]
     out2 = C.nms_proposals(b, s, nv, 0.7, post, u)
+    torch.cuda.synchronize()
+    for x, y in zip(out1, out2):
+        assert torch.equal(x, y)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('P,post', LARGE_NMS)
+def test_nms_proposals_gpu_repeatable_large(cuda, P, post):
+    """The RPN-dump shapes (tools/test_rpn.py: pre-NMS = all anchors) reach the reducer's
+    beyond-window fold and, with post < kept, its early exit: run twice, bitwise equal."""
+    from mx_rcnn_amd.ops import need_ext
+    C = need_ext()
+    g = torch.Generator().manual_seed(7 * P + post)
+    pst = P if post < 0 else post
+    b = rpn_like_boxes(g, P)[None].to(cuda)
+    s = torch.sort(torch.rand(P, generator=g), descending=True).values[None].to(cuda).contiguous()
+    nv = torch.tensor([P], dtype=torch.int32, device=cuda)
+    u = torch.rand(1, pst, generator=g).to(cuda)
+    out1 = [t.clone() for t in C.nms_proposals(b, s, nv, 0.7, pst, u)]
+    out2 = C.nms_proposals(b, s, nv, 0.7, pst, u)
     torch.cuda.synchronize()
     for x, y in zip(out1, out2):
         assert torch.equal(x, y)

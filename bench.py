@@ -3,7 +3,10 @@
 
 BASELINE.json metric "imgs/sec e2e train ResNet-101 Faster R-CNN at 1/2/4/8 MI355X": ResNet-101
 C4 Faster R-CNN, COCO-shaped synthetic images 800x1333 (81 classes), random-init weights,
-1 image per GPU per step (the reference's only mode), bf16 compute with fp32 master weights,
+1 image per GPU per step (the reference's only mode), at the reference's precision class by default
+(--dtype fp32: every MFMA operand a bf16 hi / lo pair, products as three bf16 MFMAs with fp32
+accumulation, fp32 gradients / masters / SGD, mx_rcnn_amd/ops/precision.py); the bf16 mode is
+timed after it and reported as the extra field ``config.bf16`` (--dtype bf16: bf16 only),
 full step timed: trunk+RPN fwd/bwd, anchor target, proposal (sort + NMS 12000->6000),
 proposal target (128 RoIs), RoIPool, stage-4 head, losses, bucketed RCCL all-reduce (N>1),
 fused SGD update.  Weak scaling (fixed per-GPU work).
@@ -34,7 +37,10 @@ def parse_args(argv=None):
     ap.add_argument('--image', default='800x1333')
     ap.add_argument('--ims-per-gpu', type=int, default=1)
     ap.add_argument('--mode', default='graph', choices=['graph', 'eager'])
-    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--dtype', default='fp32', choices=['bf16', 'fp32'],
+                    help='fp32 (default): the reference precision class on the x2 pair kernels, followed by a bf16 '
+                         'run reported as config.bf16; bf16: the bf16 mode alone')
+    ap.add_argument('--no-bf16-extra', action='store_true', help='fp32 only: skip the extra bf16 run')
     ap.add_argument('--bucket-mb', type=float, default=25)
     ap.add_argument('--grad-comm', default='fp32', choices=['fp32', 'bf16'],
                     help='all-reduce wire dtype of the gradient buckets (fp32 = the reference kvstore sum)')
@@ -109,6 +115,25 @@ def main():
     rank, world, local_rank, device = pdist.init_distributed()
     if world != args.gpus:
         raise SystemExit('--gpus %d but %d ranks were launched' % (args.gpus, world))
+    rec = run(args, args.dtype, rank, world, device)
+    if args.dtype == 'fp32' and not args.no_bf16_extra and device.type == 'cuda':
+        torch.cuda.empty_cache()
+        extra = run(args, 'bf16', rank, world, device)
+        if rec is not None:
+            rec['config']['bf16'] = {'value': extra['value'], 'ms_per_step': extra['ms_per_step'],
+                                     'exec': extra['config']['exec'],
+                                     'objective_first_last': extra['config']['objective_first_last']}
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if os.environ.get('MXR_BENCH_DUMP_TUNE') and device.type == 'cuda':
+        from mx_rcnn_amd.ops import need_ext
+        for key, tile, sp in need_ext().conv_tune_table():
+            print('[tune] %-48s tile %d splits %d' % (key, tile, sp), file=sys.stderr)
+    pdist.destroy()
+
+
+def run(args, precision, rank, world, device):
+    """One timed run at ``precision`` ('fp32': x2 pairs, 'bf16') -> the JSON record (every rank)."""
     h, w = [int(v) for v in args.image.lower().split('x')]
     cfg = snapshot()
     # end2end config mutation (train_end2end.py:25-32)
@@ -130,9 +155,8 @@ def main():
     if args.network.startswith('resnet'):
         model.to(device).calibrate_bn(pool[0]['data'])  # stand-in for pretrained BN statistics
     fixed = ['conv0', 'stage1', 'stage2', 'bn_data', 'bn0'] if args.network.startswith('resnet') else ['conv1', 'conv2']
-    dtype = torch.bfloat16 if (args.dtype == 'bf16' and device.type == 'cuda') else torch.float32
     trainer = Trainer(model, args.train_mode, fixed_param_prefix=fixed, lr=0.001, momentum=0.9, wd=0.0005, clip_gradient=1.0,
-                      rescale_grad=1.0, compute_dtype=dtype, device=device, bucket_mb=args.bucket_mb,
+                      rescale_grad=1.0, device=device, bucket_mb=args.bucket_mb, precision=precision,
                       grad_comm_dtype=torch.float32 if args.grad_comm == 'fp32' else torch.bfloat16)
 
     mode = args.mode if device.type == 'cuda' else 'eager'
@@ -179,28 +203,29 @@ def main():
     ms = elapsed / max(args.steps, 1) * 1e3
     imgs = args.ims_per_gpu * world * args.steps
     value = imgs / elapsed
-    if rank == 0:
-        metric = METRIC if args.network == 'resnet101' else 'imgs/sec e2e train %s Faster R-CNN' % args.network
-        if args.train_mode != 'e2e':
-            metric = 'imgs/sec alternate-stage %s train %s' % (args.train_mode, args.network)
-        rec = {'metric': metric, 'value': round(value, 3), 'unit': 'images/s', 'n_gpus': world,
-               'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
-               'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-               'dtype': 'bf16' if dtype == torch.bfloat16 else 'fp32',
-               'data': 'synthetic (random %dx%d images, 1-20 random gt boxes, random-init weights)' % (h, w),
-               'config': {'model': '%s-faster-rcnn%s' % (args.network, '-c4' if args.network.startswith('resnet') else ''), 'global_batch': args.ims_per_gpu * world,
-                          'seq_len': None, 'image_hw': [h, w], 'num_classes': args.num_classes,
-                          'ims_per_gpu': args.ims_per_gpu, 'train_mode': args.train_mode, 'parallelism': 'dp%d' % world,
-                          'rpn_pre_post_nms': [cfg.TRAIN.RPN_PRE_NMS_TOP_N, cfg.TRAIN.RPN_POST_NMS_TOP_N],
-                          'rois_per_image': cfg.TRAIN.BATCH_SIZE, 'exec': mode,
-                          'objective_first_last': [round(loss0, 4), round(loss1, 4)],
-                          'backend': pdist.backend_name(), 'allreduce': comm}}
-        print(json.dumps(rec), flush=True)
-    if os.environ.get('MXR_BENCH_DUMP_TUNE') and device.type == 'cuda':
-        from mx_rcnn_amd.ops import need_ext
-        for key, tile, sp in need_ext().conv_tune_table():
-            print('[tune] %-48s tile %d splits %d' % (key, tile, sp), file=sys.stderr)
-    pdist.destroy()
+    metric = METRIC if args.network == 'resnet101' else 'imgs/sec e2e train %s Faster R-CNN' % args.network
+    if args.train_mode != 'e2e':
+        metric = 'imgs/sec alternate-stage %s train %s' % (args.train_mode, args.network)
+    x2 = trainer.x2
+    rec = {'metric': metric, 'value': round(value, 3), 'unit': 'images/s', 'n_gpus': world,
+           'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
+           'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+           'dtype': trainer.precision,
+           'data': 'synthetic (random %dx%d images, 1-20 random gt boxes, random-init weights)' % (h, w),
+           'config': {'model': '%s-faster-rcnn%s' % (args.network, '-c4' if args.network.startswith('resnet') else ''), 'global_batch': args.ims_per_gpu * world,
+                      'seq_len': None, 'image_hw': [h, w], 'num_classes': args.num_classes,
+                      'ims_per_gpu': args.ims_per_gpu, 'train_mode': args.train_mode, 'parallelism': 'dp%d' % world,
+                      'precision': ('fp32-class: MFMA operands as bf16 hi/lo pairs (16 significant bits), '
+                                    'hi*hi+hi*lo+lo*hi bf16 MFMA with fp32 accumulation, fp32 grads/masters/SGD')
+                      if x2 else ('bf16 operands, fp32 accumulation and masters' if trainer.precision == 'bf16'
+                                  else 'fp32'),
+                      'rpn_pre_post_nms': [cfg.TRAIN.RPN_PRE_NMS_TOP_N, cfg.TRAIN.RPN_POST_NMS_TOP_N],
+                      'rois_per_image': cfg.TRAIN.BATCH_SIZE, 'exec': mode,
+                      'objective_first_last': [round(loss0, 4), round(loss1, 4)],
+                      'backend': pdist.backend_name(), 'allreduce': comm,
+                      'rccl': pdist.rccl_env() if pdist.backend_name() == 'nccl' else None}}
+    del step_fn, trainer
+    return rec
 
 
 if __name__ == '__main__':

@@ -44,13 +44,14 @@ def add_common_args(parser):
 def init_runtime(args):
     """Spawn the per-GPU ranks if ``--gpus`` names more than one device (the parent exits with
     the job's code and never touches the GPU), then bootstrap this rank."""
-    from ..parallel.spawn import maybe_spawn, parse_gpus
+    from ..parallel.spawn import maybe_spawn, parse_gpus, select_devices
     import sys
     spec = getattr(args, 'gpus', None)
     if spec is None:
         spec = getattr(args, 'gpu_ids', None)
     if spec is not None:
-        maybe_spawn(parse_gpus(spec), sys.argv[0], sys.argv[1:])
+        # --gpus names DEVICES as in the reference ('2,3' runs on GPUs 2 and 3, '3' on GPU 3)
+        maybe_spawn(parse_gpus(spec), sys.argv[0], sys.argv[1:], visible=select_devices(spec))
     rank, world, local_rank, device = pdist.init_distributed()
     setup_logging(rank)
     if getattr(args, 'cfg', None):

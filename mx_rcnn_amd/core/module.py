@@ -30,6 +30,15 @@ from .trainer import GraphedStep, Trainer
 from ..utils import profiler as prof
 
 
+def sync_key(key):
+    """The part of a step's input-shape key that every rank shares: the shapes without their
+    leading (batch / RoI-count) dimension.  With an uneven ``work_load_list`` each rank's slice of
+    the global batch has its own, fixed size (data/loader.py split_input_slice), so the ranks'
+    full keys differ while their capture points -- a new padded image shape of the global step --
+    still coincide."""
+    return tuple((k, tuple(s[1:])) for k, s in key)
+
+
 class MutableModule(object):
     def __init__(self, symbol, data_names=None, label_names=None, logger=logging, context=None, work_load_list=None,
                  max_data_shapes=None, max_label_shapes=None, fixed_param_prefix=None, mode=None, use_graph=None,
@@ -209,7 +218,7 @@ class MutableModule(object):
             self._outputs = g(data_batch)
         return self._outputs
 
-    def _capture(self, key, data_batch):
+    def _capture(self, key, data_batch):  # noqa: C901
         """Capture a hipGraph for a new input shape.  Under data parallelism every rank reaches
         this on the same step (the loaders pad every rank's batch to the global step's shape,
         data/loader.py), and the ranks agree on the outcome: if capture failed anywhere, all
@@ -221,6 +230,11 @@ class MutableModule(object):
         try:
             g = GraphedStep(self.trainer, data_batch)
         except Exception as e:  # reported, never silent
+            if pdist.is_distributed() and pdist.get_world_size() > 1:
+                # the failed warm-up may have issued fewer bucket all-reduces than the peers' did:
+                # negotiating an eager fallback would pair mismatched collectives -> job error
+                raise RuntimeError('hipGraph capture failed on rank %d under data parallelism (%s: %s)'
+                                   % (pdist.get_rank(), type(e).__name__, str(e)[:300]))
             ok = 0.0
             logging.warning('hipGraph capture failed for %s (%s: %s)', key, type(e).__name__, str(e)[:300])
             torch.cuda.synchronize()
@@ -229,7 +243,8 @@ class MutableModule(object):
                 self._hb.resume()
         if pdist.is_distributed():
             if pdist.get_world_size() > 1:
-                h = torch.tensor([float(zlib.crc32(repr(key).encode()))], dtype=torch.float64, device=self.context)
+                h = torch.tensor([float(zlib.crc32(repr(sync_key(key)).encode()))], dtype=torch.float64,
+                                 device=self.context)
                 lo, hi = h.clone(), h.clone()
                 torch.distributed.all_reduce(lo, op=torch.distributed.ReduceOp.MIN)
                 torch.distributed.all_reduce(hi, op=torch.distributed.ReduceOp.MAX)

@@ -35,7 +35,7 @@ def match_fixed(name, prefixes):
 
 
 class ParamGroup:
-    def __init__(self, key, entries, device, compute_dtype):
+    def __init__(self, key, entries, device, compute_dtype, x2=False):
         self.key = key  # (lowp: bool, decay: bool)
         lowp, decay = key
         self.decay = decay
@@ -43,20 +43,40 @@ class ParamGroup:
         self.numel = sum(e[3] for e in entries)
         self.master = torch.zeros(self.numel, dtype=torch.float32, device=device)
         self.mom = torch.zeros(self.numel, dtype=torch.float32, device=device)
-        gd = compute_dtype if lowp else torch.float32
-        self.shadow = torch.zeros(self.numel, dtype=gd, device=device) if lowp else None
+        # x2 (fp32-class mode, ops/precision.py): the parameters ARE the fp32 masters, gradients are
+        # fp32, and the shadow is the bf16 pair the MFMA kernels read: hi plane [0, n), lo plane
+        # [n, 2n), rewritten by the SGD kernel in the same pass as the update
+        self.x2 = bool(x2 and lowp)
+        gd = compute_dtype if (lowp and not self.x2) else torch.float32
+        if self.x2:
+            self.shadow = torch.zeros(2 * self.numel, dtype=torch.bfloat16, device=device)
+        else:
+            self.shadow = torch.zeros(self.numel, dtype=gd, device=device) if lowp else None
         self.grad = torch.zeros(self.numel, dtype=gd, device=device)
         self.offsets = []
+
+    def sync_shadow(self):
+        """Re-derive the shadow from the fp32 masters (after a load / broadcast)."""
+        if self.shadow is None:
+            return
+        if self.x2:
+            hi = self.master.to(torch.bfloat16)
+            self.shadow[:self.numel].copy_(hi)
+            self.shadow[self.numel:].copy_((self.master - hi.float()).to(torch.bfloat16))
+        else:
+            self.shadow.copy_(self.master.to(self.shadow.dtype))
 
 
 class FlatParamStore:
     def __init__(self, model, fixed_param_prefix=None, compute_dtype=torch.bfloat16, device=None,
-                 channels_last=True, mode=None):
+                 channels_last=True, mode=None, x2=False):
         self.model = model
         self.compute_dtype = compute_dtype
         dev = torch.device(device) if device is not None else next(model.parameters()).device
         self.device = dev
-        lowp_enabled = compute_dtype != torch.float32
+        # x2: fp32-class training on the bf16 MFMA (ops/precision.py); compute_dtype is then fp32
+        self.x2 = bool(x2)
+        lowp_enabled = compute_dtype != torch.float32 or self.x2
         fixed = fixed_param_prefix or []
         layers = list(model.mx_layers(mode)) if mode is not None else list(model.mx_layers())
         named = []  # (mx_name, module, attr, param)
@@ -79,8 +99,9 @@ class FlatParamStore:
             decay = n.endswith('_weight') or n.endswith('_gamma')
             cl = channels_last and p.dim() == 4
             groups.setdefault((lowp, decay), []).append((n, m, attr, p.numel(), tuple(p.shape), cl))
-        self.groups = [ParamGroup(k, v, dev, compute_dtype) for k, v in sorted(groups.items())]
+        self.groups = [ParamGroup(k, v, dev, compute_dtype, self.x2) for k, v in sorted(groups.items())]
         self.params = {}
+        from ..ops import precision
         with torch.no_grad():
             for g in self.groups:
                 off = 0
@@ -88,7 +109,7 @@ class FlatParamStore:
                     src = m._parameters[attr].detach().to(dev, torch.float32)
                     g.offsets.append(off)
                     g.master[off:off + numel].copy_(self._flat_view(src, cl))
-                    lowp = g.shadow is not None
+                    lowp = g.shadow is not None and not g.x2
                     storage = g.shadow if lowp else g.master
                     pv = self._shaped(storage[off:off + numel], shape, cl)
                     if lowp:
@@ -98,13 +119,19 @@ class FlatParamStore:
                     grad_sink.enable_direct(param)
                     m._parameters[attr] = param
                     self.params[n] = param
+                    if g.x2:  # the kernels' pair of this weight: hi view + the group's lo-plane offset
+                        precision.register_weight(param, self._shaped(g.shadow[off:off + numel], shape, cl),
+                                                  g.numel)
                     off += numel
-            # frozen: cast once, no grad (the fp32 original is kept for checkpoints)
+                if g.x2:
+                    g.sync_shadow()
+            # frozen: cast once, no grad (the fp32 original is kept for checkpoints; the x2 mode
+            # keeps them fp32 and the ops build their pairs once, ops/precision.py weight_pair)
             self.frozen_fp32 = {}
             for n, m, attr, p in named:
                 if n in self.fixed_names:
                     self.frozen_fp32[n] = p.detach().to(dev, torch.float32).clone()
-                    lowp = lowp_enabled and not _is_bn_param(n)
+                    lowp = lowp_enabled and not _is_bn_param(n) and not self.x2
                     t = p.detach().to(dev, compute_dtype if lowp else torch.float32)
                     if channels_last and t.dim() == 4:
                         t = t.contiguous(memory_format=torch.channels_last)
@@ -119,7 +146,7 @@ class FlatParamStore:
         """Flipped/transposed bf16 copies of every trainable conv filter the MFMA dgrad path
         uses, refreshed by ONE multi-filter kernel after each update (ops/conv.py)."""
         self._wt_table = None
-        if self.device.type != 'cuda' or self.compute_dtype != torch.bfloat16:
+        if self.device.type != 'cuda' or (self.compute_dtype != torch.bfloat16 and not self.x2):
             return
         from ..ops import conv as conv_ops
         from ..ops._ext import need_ext
@@ -128,8 +155,11 @@ class FlatParamStore:
         for g in self.groups:
             if g.shadow is None:
                 continue
-            for (n, m, attr, numel, shape, cl) in g.entries:
+            for (n, m, attr, numel, shape, cl), off in zip(g.entries, g.offsets):
                 p = self.params[n]
+                if g.x2:
+                    self._x2_dgrad_entry(g, p, off, numel, shape, cl, srcs, dsts)
+                    continue
                 if len(shape) == 2:  # FullyConnected (out, in): its transpose, for the FC data gradient
                     o, i = shape
                     if o % 64 != 0 or i % 64 != 0:
@@ -159,6 +189,31 @@ class FlatParamStore:
             self._wt_table = (ext.wt_flip_build(srcs, dsts), n_ent, tiles, dsts)
             self.refresh_dgrad_cache()
 
+    def _x2_dgrad_entry(self, g, p, off, numel, shape, cl, srcs, dsts):
+        """x2 mode: the flipped / transposed filter of ``p`` as a PAIR buffer (2I, O, kh, kw), filled
+        by two flip-table entries (hi plane from the shadow's hi view, lo from its lo view)."""
+        from ..ops import conv as conv_ops
+        if len(shape) == 2:
+            o, i = shape
+            if o % 64 != 0 or i % 64 != 0:
+                return
+            views = [g.shadow[pl + off:pl + off + numel].view(o, i, 1, 1) for pl in (0, g.numel)]
+            buf = torch.empty((2 * i, o, 1, 1), dtype=torch.bfloat16, device=self.device,
+                              memory_format=torch.channels_last)
+        else:
+            if len(shape) != 4 or not cl:
+                return
+            o, i, kh, kw = shape
+            if o % 64 != 0 or i % 8 != 0 or kh != kw:
+                return
+            views = [self._shaped(g.shadow[pl + off:pl + off + numel], shape, cl) for pl in (0, g.numel)]
+            buf = torch.empty((2 * i, o, kh, kw), dtype=torch.bfloat16, device=self.device,
+                              memory_format=torch.channels_last)
+        conv_ops.register_dgrad_weight(p, buf)
+        for v, d in zip(views, (buf[:i], buf[i:])):
+            srcs.append(v)
+            dsts.append(d)
+
     def _dgrad_params(self, srcs):
         """The parameter behind each flip-table source (same order)."""
         by_ptr = {p.data_ptr(): p for p in self.params.values()}
@@ -170,8 +225,8 @@ class FlatParamStore:
         written in the same pass instead of one copy kernel each.  Never while capturing: the
         table upload is a host-to-device copy."""
         from ..ops import conv as conv_ops
-        if not conv_ops._SUBW or os.environ.get('MXR_SUBFILTER_FOLD', '1') == '0':
-            return
+        if not conv_ops._SUBW or os.environ.get('MXR_SUBFILTER_FOLD', '1') == '0' or self.x2:
+            return  # (x2: the pair sub-filters are refreshed by slicing copies)
         if torch.cuda.is_current_stream_capturing():
             return
         subs, have = [], set()
@@ -246,8 +301,7 @@ class FlatParamStore:
         import torch.distributed as dist
         for g in self.groups:
             dist.broadcast(g.master, src)
-            if g.shadow is not None:
-                g.shadow.copy_(g.master.to(g.shadow.dtype))
+            g.sync_shadow()
         for n in self.fixed_names:
             dist.broadcast(self.frozen_fp32[n], src)
             self.params[n].data.copy_(self.frozen_fp32[n].to(self.params[n].dtype))
@@ -327,6 +381,8 @@ class FlatParamStore:
                             g.master[off:off + numel].copy_(self._flat_view(src, cl))
                             p.data.copy_(src.to(p.dtype))
                             found = True
+                            if g.x2:
+                                g.sync_shadow()
                 if not found:
                     p.data.copy_(src.to(p.dtype))
                     if n in self.frozen_fp32:

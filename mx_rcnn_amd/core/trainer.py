@@ -17,17 +17,27 @@ from .params import FlatParamStore
 class Trainer:
     def __init__(self, model, mode='e2e', fixed_param_prefix=None, lr=0.001, momentum=0.9, wd=0.0005,
                  clip_gradient=1.0, rescale_grad=1.0, lr_scheduler=None, compute_dtype=None, device=None,
-                 bucket_mb=25, average_grads=False, channels_last=None, grad_comm_dtype=None):
+                 bucket_mb=25, average_grads=False, channels_last=None, grad_comm_dtype=None, precision=None):
+        """precision: 'bf16' (bf16 operands, fp32 accumulation / masters), or 'fp32': the reference's
+        precision class on the GPU -- every MFMA operand an x2 hi / lo bf16 pair, products as three
+        bf16 MFMAs with fp32 accumulation, fp32 gradients (ops/precision.py).  Default: bf16 on the
+        GPU unless compute_dtype says fp32; the CPU path is plain fp32."""
         dev = torch.device(device) if device is not None else next(model.parameters()).device
+        if precision is None:
+            precision = 'fp32' if (compute_dtype == torch.float32 and dev.type == 'cuda') else 'bf16'
+        self.x2 = precision == 'fp32' and dev.type == 'cuda'
+        if self.x2:
+            compute_dtype = torch.float32
         if compute_dtype is None:
             compute_dtype = torch.bfloat16 if dev.type == 'cuda' else torch.float32
         if channels_last is None:
             channels_last = dev.type == 'cuda'
         self.device, self.compute_dtype, self.channels_last = dev, compute_dtype, channels_last
+        self.precision = 'fp32' if (self.x2 or compute_dtype == torch.float32) else 'bf16'
         self.model = model.to(dev)
         self.mode = mode
         self.store = FlatParamStore(self.model, fixed_param_prefix, compute_dtype, dev, channels_last,
-                                   mode=mode if mode in ('rpn', 'rcnn') else None)
+                                   mode=mode if mode in ('rpn', 'rcnn') else None, x2=self.x2)
         self.reducer = BucketReducer(self.store, bucket_mb=bucket_mb, average=average_grads,
                                      comm_dtype=grad_comm_dtype)
         if self.reducer.dp:
@@ -78,6 +88,11 @@ class Trainer:
 
     def step_body(self, b):
         """The device work of one step (capturable)."""
+        from ..ops.precision import x2_mode
+        with x2_mode(self.x2):
+            return self._step_body(b)
+
+    def _step_body(self, b):
         # the dgrad filter cache of the current weights, built beside the forward pass
         # (and the gradient clear), joined before the first backward kernel
         zg_side = os.environ.get('MXR_ZERO_GRAD_SIDE', '1') != '0'
@@ -203,15 +218,19 @@ class GraphedStep:
         saved = trainer.snapshot_state() if warmup else None
         s = torch.cuda.Stream()
         s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            for _ in range(warmup):
-                trainer.step_body(self.static)
-        torch.cuda.current_stream().wait_stream(s)
-        torch.cuda.synchronize()
-        if saved is not None:
-            trainer.restore_state(saved)
-            del saved
+        try:
+            with torch.cuda.stream(s):
+                for _ in range(warmup):
+                    trainer.step_body(self.static)
+        finally:
+            # a warm-up step that raised must not leave its updates behind (an eager fallback
+            # would start from weights no schedule produced)
+            torch.cuda.current_stream().wait_stream(s)
             torch.cuda.synchronize()
+            if saved is not None:
+                trainer.restore_state(saved)
+                del saved
+                torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph):
             self.out = trainer.step_body(self.static)

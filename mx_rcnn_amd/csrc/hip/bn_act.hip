@@ -24,21 +24,12 @@ __device__ __forceinline__ void bn_coeffs(int c, const float* gamma, const float
   t = beta[c] - mean[c] * s;
 }
 
-__device__ __forceinline__ void load4(const void* p, int64_t i, int bf16, float v[4]) {
-  if (bf16) {
-    const ushort4 u = *reinterpret_cast<const ushort4*>(static_cast<const uint16_t*>(p) + i);
-    v[0] = h16_to_f32(u.x, bf16); v[1] = h16_to_f32(u.y, bf16); v[2] = h16_to_f32(u.z, bf16); v[3] = h16_to_f32(u.w, bf16);
-  } else {
-    const float4 f = *reinterpret_cast<const float4*>(static_cast<const float*>(p) + i);
-    v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
-  }
+// `bf16` is the storage code (common.h: 0 fp32, 1 bf16, 2 fp16, 3 x2 pair with plane = M * C)
+__device__ __forceinline__ void load4(const void* p, int64_t i, int code, float v[4], int64_t plane) {
+  ld4c(p, i, code, plane, v);
 }
-__device__ __forceinline__ void store4(void* p, int64_t i, int bf16, const float v[4]) {
-  if (bf16)
-    *reinterpret_cast<ushort4*>(static_cast<uint16_t*>(p) + i) =
-        make_ushort4(f32_to_h16(v[0], bf16), f32_to_h16(v[1], bf16), f32_to_h16(v[2], bf16), f32_to_h16(v[3], bf16));
-  else
-    *reinterpret_cast<float4*>(static_cast<float*>(p) + i) = make_float4(v[0], v[1], v[2], v[3]);
+__device__ __forceinline__ void store4(void* p, int64_t i, int code, const float v[4], int64_t plane) {
+  st4c(p, i, code, plane, v);
 }
 
 __global__ void __launch_bounds__(256)
@@ -57,7 +48,7 @@ bn_relu_fwd_kernel(const void* __restrict__ x, int bf16, int64_t M, int C, const
   for (; e + 3 * T < total; e += 4 * T) {
     float v[4][4];
 #pragma unroll
-    for (int u = 0; u < 4; ++u) load4(x, (e + u * T) * 4, bf16, v[u]);
+    for (int u = 0; u < 4; ++u) load4(x, (e + u * T) * 4, bf16, v[u], (int64_t)M * C);
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
 #pragma unroll
@@ -65,18 +56,18 @@ bn_relu_fwd_kernel(const void* __restrict__ x, int bf16, int64_t M, int C, const
         v[u][k] = v[u][k] * s[k] + t[k];
         if (relu) v[u][k] = fmaxf(v[u][k], 0.f);
       }
-      store4(y, (e + u * T) * 4, bf16, v[u]);
+      store4(y, (e + u * T) * 4, bf16, v[u], (int64_t)M * C);
     }
   }
   for (; e < total; e += T) {
     float v[4];
-    load4(x, e * 4, bf16, v);
+    load4(x, e * 4, bf16, v, (int64_t)M * C);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       v[k] = v[k] * s[k] + t[k];
       if (relu) v[k] = fmaxf(v[k], 0.f);
     }
-    store4(y, e * 4, bf16, v);
+    store4(y, e * 4, bf16, v, (int64_t)M * C);
   }
 }
 
@@ -112,11 +103,11 @@ bn_relu_bwd_kernel(const void* __restrict__ x, const void* __restrict__ dy, int 
     if (dx) {
       if (dres) {  // fused gradient accumulation: dx = dres + d(bn_relu)
         float rv[4];
-        load4(dres, e * 4, bf16, rv);
+        load4(dres, e * 4, bf16, rv, (int64_t)M * C);
 #pragma unroll
         for (int k = 0; k < 4; ++k) g[k] += rv[k];
       }
-      store4(dx, e * 4, bf16, g);
+      store4(dx, e * 4, bf16, g, (int64_t)M * C);
     }
   };
   int64_t e = tid;
@@ -124,16 +115,16 @@ bn_relu_bwd_kernel(const void* __restrict__ x, const void* __restrict__ dy, int 
     float xv[4][4], g[4][4];
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      load4(x, (e + u * T) * 4, bf16, xv[u]);
-      load4(dy, (e + u * T) * 4, bf16, g[u]);
+      load4(x, (e + u * T) * 4, bf16, xv[u], (int64_t)M * C);
+      load4(dy, (e + u * T) * 4, bf16, g[u], (int64_t)M * C);
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) body(xv[u], g[u], e + u * T);
   }
   for (; e < total; e += T) {
     float xv[4], g[4];
-    load4(x, e * 4, bf16, xv);
-    load4(dy, e * 4, bf16, g);
+    load4(x, e * 4, bf16, xv, (int64_t)M * C);
+    load4(dy, e * 4, bf16, g, (int64_t)M * C);
     body(xv, g, e);
   }
   __syncthreads();
@@ -194,9 +185,9 @@ bn_relu_fwd_scalar(const void* __restrict__ x, int bf16, int64_t M, int C, const
   float s, t;
   bn_coeffs(c, gamma, beta, mean, var, eps, fix_gamma, s, t);
   for (int64_t e = tid; e < M * C; e += T) {
-    float v = ld(x, e, bf16) * s + t;
+    float v = ldc(x, e, bf16, M * C) * s + t;
     if (relu) v = fmaxf(v, 0.f);
-    st(y, e, v, bf16);
+    stc(y, e, v, bf16, M * C);
   }
 }
 
@@ -216,12 +207,12 @@ bn_relu_bwd_scalar(const void* __restrict__ x, const void* __restrict__ dy, int 
   const float inv = rsqrtf(var[c] + eps), mu = mean[c];
   float ag = 0.f, ab = 0.f;
   for (int64_t e = tid; e < M * C; e += T) {
-    const float xv = ld(x, e, bf16);
-    const float g = ld(dy, e, bf16);
+    const float xv = ldc(x, e, bf16, M * C);
+    const float g = ldc(dy, e, bf16, M * C);
     const float gm = (!relu || xv * s + t > 0.f) ? g : 0.f;
     ab += gm;
     ag += gm * (xv - mu) * inv;
-    if (dx) st(dx, e, gm * s, bf16);
+    if (dx) stc(dx, e, gm * s, bf16, M * C);
   }
   atomicAdd(&red[c], ag);
   atomicAdd(&red[C + c], ab);

@@ -72,22 +72,19 @@ __device__ __forceinline__ void fold_partials(const float* __restrict__ part, in
   __syncthreads();
 }
 
-__device__ __forceinline__ void ld8(const uint16_t* p, float* v) {
-  const uint4 u = *reinterpret_cast<const uint4*>(p);
-  const uint32_t w[4] = {u.x, u.y, u.z, u.w};
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    v[2 * k] = __uint_as_float(w[k] << 16);
-    v[2 * k + 1] = __uint_as_float(w[k] & 0xffff0000u);
-  }
+// 8 channels of one row; pl > 0: an x2 hi / lo pair (common.h), the lo plane pl elements further
+__device__ __forceinline__ void ld8(const uint16_t* p, float* v, int64_t pl) {
+  if (pl) ld8x(p, pl, v);
+  else ld8_bf16(p, v);
 }
 
-__device__ __forceinline__ void st8(uint16_t* p, const float* v) {
-  uint32_t w[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k)
-    w[k] = (uint32_t)f32_to_bf16(v[2 * k]) | ((uint32_t)f32_to_bf16(v[2 * k + 1]) << 16);
-  *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
+__device__ __forceinline__ void st8(uint16_t* p, const float* v, int64_t pl) {
+  if (pl) {
+    float t[8];
+    st8x(p, pl, v, t);
+  } else {
+    st8_bf16(p, v);
+  }
 }
 
 // sum a[8] / b[8] over the 32 row lanes of each channel group; results for channel
@@ -113,7 +110,8 @@ __device__ __forceinline__ void lane_reduce(const float* a, const float* b, floa
 
 __global__ void __launch_bounds__(256)
 bn_train_stats_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int rows, const float* __restrict__ shift,
-                      float* __restrict__ part) {
+                      float* __restrict__ part, int x2) {
+  const int64_t pl = x2 ? M * C : 0;  // x2 pairs: every (M, C) operand's lo plane
   __shared__ float red[8][BT_LANES][16];
   __shared__ float sa[64], sb[64];
   const int cg = threadIdx.x & 7, rl = threadIdx.x >> 3;
@@ -129,7 +127,7 @@ bn_train_stats_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int rows
 #pragma unroll 4
   for (int64_t r = r0 + rl; r < r1; r += BT_LANES) {
     float v[8];
-    ld8(x + r * C + c0, v);
+    ld8(x + r * C + c0, v, pl);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float d = v[k] - sh[k];
@@ -152,7 +150,8 @@ bn_train_norm_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int rows,
                      const float* __restrict__ gamma, const float* __restrict__ beta, float* __restrict__ rmean,
                      float* __restrict__ rvar, float momentum, float eps, int fix_gamma, int relu,
                      uint16_t* __restrict__ y, float* __restrict__ save_mean, float* __restrict__ save_invstd,
-                     float* __restrict__ save_veps) {
+                     float* __restrict__ save_veps, int x2) {
+  const int64_t pl = x2 ? M * C : 0;  // x2 pairs: every (M, C) operand's lo plane
   __shared__ float scale_sh[64], shift_sh[64], red4[512], fa[64], fb[64];
   const int tid = threadIdx.x;
   fold_partials(part, nchunks, C, red4, fa, fb);
@@ -192,13 +191,13 @@ bn_train_norm_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int rows,
 #pragma unroll 4
   for (int64_t r = r0 + rl; r < r1; r += BT_LANES) {
     float v[8];
-    ld8(x + r * C + c0, v);
+    ld8(x + r * C + c0, v, pl);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       v[k] = v[k] * sc[k] + sf[k];
       if (relu) v[k] = fmaxf(v[k], 0.f);
     }
-    st8(y + r * C + c0, v);
+    st8(y + r * C + c0, v, pl);
   }
 }
 
@@ -206,7 +205,8 @@ __global__ void __launch_bounds__(256)
 bn_train_bstats_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ dy, int64_t M, int C,
                        const float* __restrict__ gamma, const float* __restrict__ beta,
                        const float* __restrict__ save_mean, const float* __restrict__ save_invstd, int fix_gamma,
-                       int relu, int rows, float* __restrict__ part) {
+                       int relu, int rows, float* __restrict__ part, int x2) {
+  const int64_t pl = x2 ? M * C : 0;  // x2 pairs: every (M, C) operand's lo plane
   __shared__ float red[8][BT_LANES][16];
   __shared__ float sa[64], sb[64];
   const int cg = threadIdx.x & 7, rl = threadIdx.x >> 3;
@@ -225,8 +225,8 @@ bn_train_bstats_kernel(const uint16_t* __restrict__ x, const uint16_t* __restric
 #pragma unroll 4
   for (int64_t r = r0 + rl; r < r1; r += BT_LANES) {
     float v[8], d[8];
-    ld8(x + r * C + c0, v);
-    ld8(dy + r * C + c0, d);
+    ld8(x + r * C + c0, v, pl);
+    ld8(dy + r * C + c0, d, pl);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float xh = (v[k] - mu[k]) * inv[k];
@@ -248,7 +248,8 @@ bn_train_dx_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ 
                    const float* __restrict__ part, const float* __restrict__ gamma, const float* __restrict__ beta,
                    const float* __restrict__ save_mean, const float* __restrict__ save_invstd, int fix_gamma,
                    int relu, uint16_t* __restrict__ dx, float* __restrict__ dgamma, float* __restrict__ dbeta,
-                   int accumulate) {
+                   int accumulate, int x2) {
+  const int64_t pl = x2 ? M * C : 0;  // x2 pairs: every (M, C) operand's lo plane
   __shared__ float mg_sh[64], mgx_sh[64], red4[512], fa[64], fb[64];
   const int tid = threadIdx.x;
   fold_partials(part, nchunks, C, red4, fa, fb);
@@ -281,15 +282,15 @@ bn_train_dx_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ 
 #pragma unroll 4
   for (int64_t r = r0 + rl; r < r1; r += BT_LANES) {
     float v[8], d[8];
-    ld8(x + r * C + c0, v);
-    ld8(dy + r * C + c0, d);
+    ld8(x + r * C + c0, v, pl);
+    ld8(dy + r * C + c0, d, pl);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float xh = (v[k] - mu[k]) * inv[k];
       const float gm = (!relu || xh * g[k] + b[k] > 0.f) ? d[k] : 0.f;
       d[k] = g[k] * inv[k] * (gm - mg[k] - xh * mgx[k]);
     }
-    st8(dx + r * C + c0, d);
+    st8(dx + r * C + c0, d, pl);
   }
 }
 
@@ -300,25 +301,25 @@ int bn_train_workspace_floats(int64_t M, int C) {
 
 int bn_train_fwd(const uint16_t* x, int64_t M, int C, const float* gamma, const float* beta, float* rmean,
                  float* rvar, float momentum, float eps, int fix_gamma, int relu, uint16_t* y, float* save_mean,
-                 float* save_invstd, float* workspace, hipStream_t st, float* save_veps) {
+                 float* save_invstd, float* workspace, hipStream_t st, float* save_veps, int x2) {
   if (C % BT_C != 0 || M <= 0) return -1;
   const int rows = bn_train_rows(M, C);
   const int nchunks = (int)((M + rows - 1) / rows);
   const dim3 grid(C / BT_C, nchunks);
-  bn_train_stats_kernel<<<grid, 256, 0, st>>>(x, M, C, rows, rmean, workspace);
+  bn_train_stats_kernel<<<grid, 256, 0, st>>>(x, M, C, rows, rmean, workspace, x2);
   bn_train_norm_kernel<<<grid, 256, 0, st>>>(x, M, C, rows, nchunks, workspace, gamma, beta, rmean, rvar, momentum, eps,
-                                             fix_gamma, relu, y, save_mean, save_invstd, save_veps);
+                                             fix_gamma, relu, y, save_mean, save_invstd, save_veps, x2);
   return 0;
 }
 
 int bn_train_apply(const uint16_t* x, int64_t M, int C, const float* part, int nparts, const float* gamma,
                    const float* beta, float* rmean, float* rvar, float momentum, float eps, int fix_gamma, int relu,
-                   uint16_t* y, float* save, hipStream_t st) {
+                   uint16_t* y, float* save, hipStream_t st, int x2) {
   if (C % BT_C != 0 || M <= 0 || nparts <= 0) return -1;
   const int rows = bn_train_rows(M, C);
   const dim3 grid(C / BT_C, (int)((M + rows - 1) / rows));
   bn_train_norm_kernel<<<grid, 256, 0, st>>>(x, M, C, rows, nparts, part, gamma, beta, rmean, rvar, momentum, eps,
-                                             fix_gamma, relu, y, save, save + C, save + 2 * C);
+                                             fix_gamma, relu, y, save, save + C, save + 2 * C, x2);
   return 0;
 }
 
@@ -330,7 +331,8 @@ __global__ void __launch_bounds__(256)
 bn_train_dx_apply_kernel(const uint16_t* o, const uint16_t* __restrict__ x, int64_t M, int C, int rows,
                          const float* __restrict__ part, int nparts, const float* __restrict__ gamma,
                          const float* __restrict__ save, const uint16_t* __restrict__ dres, uint16_t* dx,
-                         float* __restrict__ dgamma, float* __restrict__ dbeta) {
+                         float* __restrict__ dgamma, float* __restrict__ dbeta, int x2) {
+  const int64_t pl = x2 ? M * C : 0;  // x2 pairs: every (M, C) operand's lo plane
   __shared__ float red4[512], fa[64], fb[64];
   const int tid = threadIdx.x, cg = tid & 7, rl = tid >> 3;
   fold_partials(part, nparts, C, red4, fa, fb);
@@ -356,36 +358,36 @@ bn_train_dx_apply_kernel(const uint16_t* o, const uint16_t* __restrict__ x, int6
 #pragma unroll 4
   for (int64_t r = r0 + rl; r < r1; r += BT_LANES) {
     float v[8], d[8], rr[8];
-    ld8(x + r * C + c0, v);
-    ld8(o + r * C + c0, d);
-    if (dres) ld8(dres + r * C + c0, rr);
+    ld8(x + r * C + c0, v, pl);
+    ld8(o + r * C + c0, d, pl);
+    if (dres) ld8(dres + r * C + c0, rr, pl);
 #pragma unroll
     for (int k = 0; k < 8; ++k) d[k] = d[k] - a[k] - b[k] * v[k] + (dres ? rr[k] : 0.f);
-    st8(dx + r * C + c0, d);
+    st8(dx + r * C + c0, d, pl);
   }
 }
 
 int bn_train_dx_apply(const uint16_t* o, const uint16_t* x, int64_t M, int C, const float* part, int nparts,
                       const float* gamma, const float* save, const uint16_t* dres, uint16_t* dx, float* dgamma,
-                      float* dbeta, hipStream_t st) {
+                      float* dbeta, hipStream_t st, int x2) {
   if (C % BT_C != 0 || M <= 0 || nparts <= 0) return -1;
   const int rows = bn_train_rows(M, C);
   const dim3 grid(C / BT_C, (int)((M + rows - 1) / rows));
-  bn_train_dx_apply_kernel<<<grid, 256, 0, st>>>(o, x, M, C, rows, part, nparts, gamma, save, dres, dx, dgamma, dbeta);
+  bn_train_dx_apply_kernel<<<grid, 256, 0, st>>>(o, x, M, C, rows, part, nparts, gamma, save, dres, dx, dgamma, dbeta, x2);
   return 0;
 }
 
 int bn_train_bwd(const uint16_t* x, const uint16_t* dy, int64_t M, int C, const float* gamma, const float* beta,
                  const float* save_mean, const float* save_invstd, int fix_gamma, int relu, uint16_t* dx,
-                 float* dgamma, float* dbeta, int accumulate, float* workspace, hipStream_t st) {
+                 float* dgamma, float* dbeta, int accumulate, float* workspace, hipStream_t st, int x2) {
   if (C % BT_C != 0 || M <= 0) return -1;
   const int rows = bn_train_rows(M, C);
   const int nchunks = (int)((M + rows - 1) / rows);
   const dim3 grid(C / BT_C, nchunks);
   bn_train_bstats_kernel<<<grid, 256, 0, st>>>(x, dy, M, C, gamma, beta, save_mean, save_invstd, fix_gamma, relu,
-                                               rows, workspace);
+                                               rows, workspace, x2);
   bn_train_dx_kernel<<<grid, 256, 0, st>>>(x, dy, M, C, rows, nchunks, workspace, gamma, beta, save_mean, save_invstd,
-                                           fix_gamma, relu, dx, dgamma, dbeta, accumulate);
+                                           fix_gamma, relu, dx, dgamma, dbeta, accumulate, x2);
   return 0;
 }
 

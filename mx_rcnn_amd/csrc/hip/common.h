@@ -77,6 +77,120 @@ __device__ __forceinline__ void st8_h16(uint16_t* p, const float* v, int code) {
   *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
+// ---- fp32-class "x2" storage ------------------------------------------------------------------
+// The fp32 training mode keeps every MFMA operand as a PAIR of bf16 planes `plane` elements apart:
+// value = hi + lo with hi = RNE(v), lo = RNE(v - hi) -- 16 significant bits, relative error
+// <= 2^-17 -- so a product is hi*hi + hi*lo + lo*hi on the bf16 MFMA with fp32 accumulation (the
+// dropped lo*lo term is below 2^-16 relative).  Activation tensors are (2N, C, H, W) with the hi
+// plane first; weights carry their lo plane at a per-buffer offset.
+__device__ __forceinline__ void split_bf16(float v, uint16_t& hi, uint16_t& lo) {
+  hi = f32_to_bf16(v);
+  lo = f32_to_bf16(v - bf16_to_f32(hi));
+}
+__device__ __forceinline__ float ldx(const uint16_t* p, int64_t i, int64_t plane) {
+  return bf16_to_f32(p[i]) + bf16_to_f32(p[i + plane]);
+}
+// stores v as a pair and returns the stored value (what a consumer reading it back sees)
+__device__ __forceinline__ float stx(uint16_t* p, int64_t i, int64_t plane, float v) {
+  uint16_t h, l;
+  split_bf16(v, h, l);
+  p[i] = h;
+  p[i + plane] = l;
+  return bf16_to_f32(h) + bf16_to_f32(l);
+}
+__device__ __forceinline__ void ld8x(const uint16_t* p, int64_t plane, float* v) {
+  float t[8];
+  ld8_bf16(p, v);
+  ld8_bf16(p + plane, t);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] += t[k];
+}
+// 8 values -> hi / lo planes; `stored` (may alias v) receives the stored values
+__device__ __forceinline__ void st8x(uint16_t* p, int64_t plane, const float* v, float* stored) {
+  float h[8], l[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    h[k] = bf16_to_f32(f32_to_bf16(v[k]));
+    l[k] = v[k] - h[k];
+  }
+  st8_bf16(p, h);      // exact: h is already bf16
+  st8_bf16(p + plane, l);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) stored[k] = h[k] + bf16_to_f32(f32_to_bf16(l[k]));
+}
+
+// Storage-code access for the elementwise kernels: 0 fp32, 1 bf16, 2 fp16, 3 x2 pair (bf16 hi
+// plane + lo plane `plane` elements further; a kernel over an (M, C) activation passes M * C)
+constexpr int kCodeX2 = 3;
+__device__ __forceinline__ float ldc(const void* p, int64_t i, int code, int64_t plane) {
+  if (code == kCodeX2) return ldx(static_cast<const uint16_t*>(p), i, plane);
+  return ld(p, i, code);
+}
+__device__ __forceinline__ void stc(void* p, int64_t i, float v, int code, int64_t plane) {
+  if (code == kCodeX2) stx(static_cast<uint16_t*>(p), i, plane, v);
+  else st(p, i, v, code);
+}
+// 4 consecutive values (i % 4 == 0)
+__device__ __forceinline__ void ld4c(const void* p, int64_t i, int code, int64_t plane, float v[4]) {
+  if (code == 0) {
+    const float4 f = *reinterpret_cast<const float4*>(static_cast<const float*>(p) + i);
+    v[0] = f.x; v[1] = f.y; v[2] = f.z; v[3] = f.w;
+    return;
+  }
+  const uint16_t* q = static_cast<const uint16_t*>(p);
+  const ushort4 u = *reinterpret_cast<const ushort4*>(q + i);
+  const int c = code == kCodeX2 ? 1 : code;
+  v[0] = h16_to_f32(u.x, c); v[1] = h16_to_f32(u.y, c); v[2] = h16_to_f32(u.z, c); v[3] = h16_to_f32(u.w, c);
+  if (code == kCodeX2) {
+    const ushort4 l = *reinterpret_cast<const ushort4*>(q + i + plane);
+    v[0] += bf16_to_f32(l.x); v[1] += bf16_to_f32(l.y); v[2] += bf16_to_f32(l.z); v[3] += bf16_to_f32(l.w);
+  }
+}
+__device__ __forceinline__ void st4c(void* p, int64_t i, int code, int64_t plane, const float v[4]) {
+  if (code == 0) {
+    *reinterpret_cast<float4*>(static_cast<float*>(p) + i) = make_float4(v[0], v[1], v[2], v[3]);
+    return;
+  }
+  uint16_t* q = static_cast<uint16_t*>(p);
+  if (code == kCodeX2) {
+    uint16_t h[4], l[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) split_bf16(v[k], h[k], l[k]);
+    *reinterpret_cast<ushort4*>(q + i) = make_ushort4(h[0], h[1], h[2], h[3]);
+    *reinterpret_cast<ushort4*>(q + i + plane) = make_ushort4(l[0], l[1], l[2], l[3]);
+    return;
+  }
+  *reinterpret_cast<ushort4*>(q + i) =
+      make_ushort4(f32_to_h16(v[0], code), f32_to_h16(v[1], code), f32_to_h16(v[2], code), f32_to_h16(v[3], code));
+}
+// 8 consecutive values (i % 8 == 0)
+__device__ __forceinline__ void ld8c(const void* p, int64_t i, int code, int64_t plane, float v[8]) {
+  if (code == 0) {
+    const float4* f = reinterpret_cast<const float4*>(static_cast<const float*>(p) + i);
+    const float4 a = f[0], b = f[1];
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    return;
+  }
+  const uint16_t* q = static_cast<const uint16_t*>(p) + i;
+  if (code == kCodeX2) ld8x(q, plane, v);
+  else ld8_h16(q, v, code);
+}
+__device__ __forceinline__ void st8c(void* p, int64_t i, int code, int64_t plane, const float v[8]) {
+  if (code == 0) {
+    float4* f = reinterpret_cast<float4*>(static_cast<float*>(p) + i);
+    f[0] = make_float4(v[0], v[1], v[2], v[3]);
+    f[1] = make_float4(v[4], v[5], v[6], v[7]);
+    return;
+  }
+  uint16_t* q = static_cast<uint16_t*>(p) + i;
+  if (code == kCodeX2) {
+    float s[8];
+    st8x(q, plane, v, s);
+  } else {
+    st8_h16(q, v, code);
+  }
+}
+
 // Wave64 reduction (sum) via DPP-backed shuffles.
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

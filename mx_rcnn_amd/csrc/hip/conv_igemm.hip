@@ -38,6 +38,47 @@ namespace mxr {
 __device__ __forceinline__ uint16_t f32_to_h16c(int code, float f) { return f32_to_h16(f, code); }
 __device__ __forceinline__ float h16_to_f32c(int code, uint16_t v) { return h16_to_f32(v, code); }
 
+// epilogue element access in the launch's storage format: one 16-bit value (bf16 / fp16), or (X2)
+// an x2 hi / lo pair `plane` elements apart (ConvEpi::x2).  Stores return the STORED value, which
+// the fused consumers (BN of the next unit, statistics) must read, exactly like the unfused pair.
+// X2 is a template flag so the bf16 / fp16 epilogues compile exactly as before (unrolled loops).
+template <bool X2>
+__device__ __forceinline__ float epi_ld1(const ConvEpi& ep, const uint16_t* p, int64_t i, int64_t plane) {
+  if constexpr (X2) return ldx(p, i, plane);
+  return h16_to_f32c(ep.f16 ? 2 : 1, p[i]);
+}
+template <bool X2>
+__device__ __forceinline__ float epi_st1(const ConvEpi& ep, uint16_t* p, int64_t i, int64_t plane, float v) {
+  if constexpr (X2) return stx(p, i, plane, v);
+  const uint16_t h = f32_to_h16c(ep.f16 ? 2 : 1, v);
+  p[i] = h;
+  return h16_to_f32c(ep.f16 ? 2 : 1, h);
+}
+template <bool X2>
+__device__ __forceinline__ void epi_ld8(const ConvEpi& ep, const uint16_t* p, int64_t i, int64_t plane, float* v) {
+  if constexpr (X2) ld8x(p + i, plane, v);
+  else ld8_h16(p + i, v, ep.f16 ? 2 : 1);
+}
+// 8 consecutive outputs; `stored` receives the stored values
+template <bool X2>
+__device__ __forceinline__ void epi_st8(const ConvEpi& ep, uint16_t* p, int64_t i, int64_t plane, const float* v,
+                                        float* stored) {
+  if constexpr (X2) {
+    st8x(p + i, plane, v, stored);
+    return;
+  }
+  const int code = ep.f16 ? 2 : 1;
+  uint16_t b[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    b[k] = f32_to_h16c(code, v[k]);
+    stored[k] = h16_to_f32c(code, b[k]);
+  }
+  *reinterpret_cast<uint4*>(p + i) =
+      make_uint4((uint32_t)b[0] | ((uint32_t)b[1] << 16), (uint32_t)b[2] | ((uint32_t)b[3] << 16),
+                 (uint32_t)b[4] | ((uint32_t)b[5] << 16), (uint32_t)b[6] | ((uint32_t)b[7] << 16));
+}
+
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
@@ -110,33 +151,38 @@ __device__ __forceinline__ float epi_dropout(const ConvEpi& ep, int64_t idx, flo
   return v;
 }
 
+template <bool X2>
 __device__ __forceinline__ void epi_store(const ConvEpi& ep, const EpiCol& c, uint16_t* __restrict__ y, int64_t idx,
                                           float v) {
   v += c.bias;
-  if (ep.residual) v += h16_to_f32c(EPC, ep.residual[idx]);
+  if (ep.residual) v += epi_ld1<X2>(ep, ep.residual, idx, ep.x2_py);
   if (ep.relu) v = fmaxf(v, 0.f);
   v = epi_dropout(ep, idx, v);
-  const uint16_t yb = f32_to_h16c(EPC, v);
-  y[idx] = yb;
+  if (X2 && ep.yf) {
+    ep.yf[idx] = v;
+    return;
+  }
+  const float ys = epi_st1<X2>(ep, y, idx, ep.x2_py, v);
   if (ep.y2) {
     // the BN reads the STORED (bf16-rounded) conv output, exactly like the unfused pair
-    float a = h16_to_f32c(EPC, yb) * c.s + c.t;
+    float a = ys * c.s + c.t;
     if (ep.act_relu) a = fmaxf(a, 0.f);
-    ep.y2[idx] = f32_to_h16c(EPC, a);
+    epi_st1<X2>(ep, ep.y2, idx, ep.x2_py, a);
   }
 }
 
 // BN-backward epilogue of one element; returns (g, g * xhat) through sg / sgx
+template <bool X2>
 __device__ __forceinline__ void epi_bnb(const ConvEpi& ep, const EpiCol& c, uint16_t* __restrict__ y, int64_t idx,
                                         float v, float& sg, float& sgx, int64_t didx) {
-  if (ep.dadd && didx >= 0) v += h16_to_f32c(EPC, ep.dadd[didx]);
-  const float xv = h16_to_f32c(EPC, ep.bnb_x[idx]);
+  if (ep.dadd && didx >= 0) v += epi_ld1<X2>(ep, ep.dadd, didx, ep.x2_pd);
+  const float xv = epi_ld1<X2>(ep, ep.bnb_x, idx, ep.x2_py);
   const float g = (!ep.act_relu || xv * c.s + c.t > 0.f) ? v : 0.f;
   sg += g;
   sgx += g * (xv - c.mean) * c.inv;
   float o = g * c.s;
-  if (ep.residual) o += h16_to_f32c(EPC, ep.residual[idx]);
-  y[idx] = f32_to_h16c(EPC, o);
+  if (ep.residual) o += epi_ld1<X2>(ep, ep.residual, idx, ep.x2_py);
+  epi_st1<X2>(ep, y, idx, ep.x2_py, o);
 }
 
 // Per-column statistics of an LDS-transposed epilogue (thread = 8 consecutive columns cv*8.. of
@@ -213,7 +259,7 @@ __device__ __forceinline__ void epi_bn_stats(float (&s1)[8], float (&s2)[8], flo
 }
 
 // Shared epilogue of the implicit-GEMM kernels: C/D map col = lane & 15, row = (lane >> 4) * 4 + r.
-template <int TM, int TN, int WM, int WN>
+template <int TM, int TN, int WM, int WN, bool X2 = false>
 __device__ __forceinline__ void igemm_epilogue(f32x4 (&acc)[TM][TN], int m0, int n0, int wm, int wn, int lane, int M,
                                                int Cout, const ConvEpi& ep, uint16_t* __restrict__ y, int split,
                                                int splits, float* __restrict__ slab, int Ho = 1, int Wo = 1) {
@@ -249,7 +295,7 @@ __device__ __forceinline__ void igemm_epilogue(f32x4 (&acc)[TM][TN], int m0, int
             const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
             if (m < M) {
               const int64_t orow = epi_row(ep, m, Ho, Wo), drow = dadd_row(ep, m, orow);
-              epi_bnb(ep, ec, y, orow * Cout + n, acc[i][j][r], sg, sgx, drow < 0 ? -1 : drow * Cout + n);
+              epi_bnb<X2>(ep, ec, y, orow * Cout + n, acc[i][j][r], sg, sgx, drow < 0 ? -1 : drow * Cout + n);
             }
           }
       }
@@ -274,7 +320,7 @@ __device__ __forceinline__ void igemm_epilogue(f32x4 (&acc)[TM][TN], int m0, int
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
-        if (m < M) epi_store(ep, ec, y, epi_row(ep, m, Ho, Wo) * Cout + n, acc[i][j][r]);
+        if (m < M) epi_store<X2>(ep, ec, y, epi_row(ep, m, Ho, Wo) * Cout + n, acc[i][j][r]);
       }
     }
   }
@@ -287,7 +333,7 @@ __device__ __forceinline__ void igemm_epilogue(f32x4 (&acc)[TM][TN], int m0, int
 // fp32 split-K slab writes are 16-B vectors, the per-column constants are computed once per
 // thread, and the BN-backward column sums reduce across the lanes sharing a column group
 // (shuffles), across waves (LDS) and leave the workgroup as one atomic per column and stat.
-template <int BM, int BN, int TM, int TN, int WM, int WN>
+template <int BM, int BN, int TM, int TN, int WM, int WN, bool X2 = false>
 __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* __restrict__ T, int m0, int n0, int wm,
                                                    int wn, int lane, int tid, int M, int Cout, const ConvEpi& ep,
                                                    uint16_t* __restrict__ y, int split, int splits,
@@ -336,14 +382,14 @@ __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* 
       const float4* src = reinterpret_cast<const float4*>(T + row * LDT + cv * 8);
       const float4 a0 = src[0], a1 = src[1];
       a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w; a[4] = a1.x; a[5] = a1.y; a[6] = a1.z; a[7] = a1.w;
-      ld8_h16(ep.bnb_x + e, xv, EPC);
+      epi_ld8<X2>(ep, ep.bnb_x, e, ep.x2_py, xv);
       const int64_t drow = ep.dadd ? dadd_row(ep, m, e / Cout) : -1;
       if (drow >= 0) {
-        ld8_h16(ep.dadd + drow * Cout + n, d, EPC);
+        epi_ld8<X2>(ep, ep.dadd, drow * Cout + n, ep.x2_pd, d);
 #pragma unroll
         for (int k = 0; k < 8; ++k) a[k] += d[k];
       }
-      if (ep.residual) ld8_h16(ep.residual + e, rs, EPC);
+      if (ep.residual) epi_ld8<X2>(ep, ep.residual, e, ep.x2_py, rs);
       float o[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
@@ -352,7 +398,7 @@ __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* 
         sgx[k] += g * (xv[k] - ec[k].mean) * ec[k].inv;
         o[k] = g * ec[k].s + (ep.residual ? rs[k] : 0.f);
       }
-      st8_h16(y + e, o, EPC);
+      epi_st8<X2>(ep, y, e, ep.x2_py, o, o);
     }
     epi_bnb_sums<BM, BN, 256>(sg, sgx, T, tid, m0, n0, Cout, ep);
     return;
@@ -372,27 +418,32 @@ __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* 
     const float4 a0 = src[0], a1 = src[1];
     float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
     float rs[8];
-    if (ep.residual) ld8_h16(ep.residual + e, rs, EPC);
-    uint16_t yb[8];
+    if (ep.residual) epi_ld8<X2>(ep, ep.residual, e, ep.x2_py, rs);
+    float t[8], ys[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      t[k] = a[k] + ec[k].bias + (ep.residual ? rs[k] : 0.f);
+      if (ep.relu) t[k] = fmaxf(t[k], 0.f);
+      t[k] = epi_dropout(ep, e + k, t[k]);
+    }
+    if (X2 && ep.yf) {  // fp32 output (prediction heads of the x2 mode)
+      float4* dst = reinterpret_cast<float4*>(ep.yf + e);
+      dst[0] = make_float4(t[0], t[1], t[2], t[3]);
+      dst[1] = make_float4(t[4], t[5], t[6], t[7]);
+      continue;
+    }
+    epi_st8<X2>(ep, y, e, ep.x2_py, t, ys);  // the BN reads the STORED conv output
     float y2v[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-      float t = a[k] + ec[k].bias + (ep.residual ? rs[k] : 0.f);
-      if (ep.relu) t = fmaxf(t, 0.f);
-      t = epi_dropout(ep, e + k, t);
-      yb[k] = f32_to_h16c(EPC, t);
-      const float ys = h16_to_f32c(EPC, yb[k]);  // the BN reads the STORED conv output
-      float q = ys * ec[k].s + ec[k].t;
+      float q = ys[k] * ec[k].s + ec[k].t;
       if (ep.act_relu) q = fmaxf(q, 0.f);
       y2v[k] = q;
-      const float d = ys - sh[k];
+      const float d = ys[k] - sh[k];
       s1[k] += d;
       s2[k] += d * d;
     }
-    *reinterpret_cast<uint4*>(y + e) =
-        make_uint4((uint32_t)yb[0] | ((uint32_t)yb[1] << 16), (uint32_t)yb[2] | ((uint32_t)yb[3] << 16),
-                   (uint32_t)yb[4] | ((uint32_t)yb[5] << 16), (uint32_t)yb[6] | ((uint32_t)yb[7] << 16));
-    if (ep.y2) st8_h16(ep.y2 + e, y2v, EPC);
+    if (ep.y2) epi_st8<X2>(ep, ep.y2, e, ep.x2_py, y2v, y2v);
   }
   if (ep.st_part) epi_bn_stats<BM, BN, 256>(s1, s2, T, tid, m0, n0, M, Cout, ep);
 }
@@ -556,7 +607,10 @@ splitk_reduce_bnb_kernel(const float* __restrict__ slab, int splits, int M, int 
       const float v[4] = {a.x, a.y, a.z, a.w};
       const int64_t drow = dadd_row(ep, r, r);
 #pragma unroll
-      for (int k = 0; k < 4; ++k) epi_bnb(ep, ec[k], y, e + k, v[k], sg[k], sgx[k], drow < 0 ? -1 : drow * Cout + n + k);
+      for (int k = 0; k < 4; ++k) {
+        if (ep.x2) epi_bnb<true>(ep, ec[k], y, e + k, v[k], sg[k], sgx[k], drow < 0 ? -1 : drow * Cout + n + k);
+        else epi_bnb<false>(ep, ec[k], y, e + k, v[k], sg[k], sgx[k], drow < 0 ? -1 : drow * Cout + n + k);
+      }
     }
   }
 #pragma unroll
@@ -592,8 +646,29 @@ splitk_reduce_kernel(const float* __restrict__ slab, int splits, int64_t MN, int
   const int n = (int)(e % Cout);
   float res[4] = {0.f, 0.f, 0.f, 0.f};
   if (ep.residual) {
-    const ushort4 rv = *reinterpret_cast<const ushort4*>(ep.residual + e);
-    res[0] = h16_to_f32c(EPC, rv.x); res[1] = h16_to_f32c(EPC, rv.y); res[2] = h16_to_f32c(EPC, rv.z); res[3] = h16_to_f32c(EPC, rv.w);
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      res[k] = ep.x2 ? epi_ld1<true>(ep, ep.residual, e + k, ep.x2_py) : epi_ld1<false>(ep, ep.residual, e + k, 0);
+  }
+  if (ep.x2 || ep.yf) {  // scalar pair / fp32 stores (the packed 16-bit path below is the common one)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const EpiCol c = epi_col(ep, n + k);
+      float t = v[k] + c.bias + res[k];
+      if (ep.relu) t = fmaxf(t, 0.f);
+      t = epi_dropout(ep, e + k, t);
+      if (ep.yf) {
+        ep.yf[e + k] = t;
+        continue;
+      }
+      const float ys = epi_st1<true>(ep, y, e + k, ep.x2_py, t);
+      if (ep.y2) {
+        float q = ys * c.s + c.t;
+        if (ep.act_relu) q = fmaxf(q, 0.f);
+        epi_st1<true>(ep, ep.y2, e + k, ep.x2_py, q);
+      }
+    }
+    return;
   }
   uint16_t out[4], out2[4];
 #pragma unroll
@@ -811,10 +886,12 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
   const int wm = wid >> 1, wn = wid & 1;
   const int K = KH * KW * Cin;
 
-  const __amdgpu_buffer_rsrc_t xr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)((int64_t)NB * H * W * Cin * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t wr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, (int)((int64_t)Cout * K * 2), 0x00020000);
+  // the range check covers voffset + soffset: with x2 pairs the records reach through the lo planes
+  // (the kBufOOB sentinel of padding taps stays beyond them: operands are < 1 GB per plane)
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)x, (short)0, (int)((int64_t)NB * H * W * Cin * 2 + (ep.x2 ? ep.x2_pa : 0u)), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)w, (short)0, (int)((int64_t)Cout * K * 2 + (ep.x2 ? ep.x2_pb : 0u)), 0x00020000);
 
   const int slot = lane & 7;
   uint32_t a_off[ACH];
@@ -844,21 +921,25 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
     b_off[i] = co < Cout ? (uint32_t)(((int64_t)co * K + (slot ^ ((row >> 1) & 7)) * 8) * 2) : kBufOOB;
   }
   const int cin_steps = Cin / BK;
-  const int nk_all = KH * KW * cin_steps;
+  const int nk_base = KH * KW * cin_steps;
+  // x2 (fp32-class) operands: three K phases over the same taps / channel blocks, A_hi B_hi,
+  // A_hi B_lo, A_lo B_hi, the lo planes reached through the (range-check-free) SGPR offset
+  const int nk_all = ep.x2 ? 3 * nk_base : nk_base;
   const int per = (nk_all + splits - 1) / splits;
   const int k_begin = split * per;
   const int k_end = min(nk_all, k_begin + per);
   const int nk = max(0, k_end - k_begin);
 
-  // issue cursor (uniform): tap (fr, fc), channel block ci0 of the next stage to load
-  int c_tap = k_begin / cin_steps, c_ci = (k_begin % cin_steps) * BK;
+  // issue cursor (uniform): phase, tap (fr, fc), channel block ci0 of the next stage to load
+  int c_ph = k_begin / nk_base;
+  int c_tap = (k_begin % nk_base) / cin_steps, c_ci = (k_begin % cin_steps) * BK;
   int c_fr = c_tap / KW, c_fc = c_tap % KW;
   auto issue = [&](int buf) {
     // the buffer range check sees only the VGPR offset, so the tap shift (which can turn a
     // negative padding-row offset into a valid one) goes there; the channel block is the SGPR part
     const uint32_t tap_a = (uint32_t)((c_fr * W + c_fc) * Cin * 2);
-    const uint32_t soff_a = (uint32_t)(c_ci * 2);
-    const uint32_t soff_b = (uint32_t)((c_tap * Cin + c_ci) * 2);
+    const uint32_t soff_a = (uint32_t)(c_ci * 2) + (c_ph == 2 ? ep.x2_pa : 0u);
+    const uint32_t soff_b = (uint32_t)((c_tap * Cin + c_ci) * 2) + (c_ph == 1 ? ep.x2_pb : 0u);
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       const uint32_t vo = ((a_mask[i] >> c_tap) & 1ull) ? a_off[i] + tap_a : kBufOOB;
@@ -872,7 +953,11 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
       ++c_tap;
       if (++c_fc == KW) {
         c_fc = 0;
-        ++c_fr;
+        if (++c_fr == KH) {  // next phase (x2)
+          c_fr = 0;
+          c_tap = 0;
+          ++c_ph;
+        }
       }
     }
   };
@@ -913,11 +998,18 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
     }
   }
   static_assert(BM * (BN + 4) * 4 <= S * (BM + BN) * BK * 2, "epilogue tile must fit the operand ring");
-  if (Cout % 8 == 0)
+  if (ep.x2 || ep.yf) {  // fp32-class pairs (separate instantiation: the 16-bit loops stay unrolled)
+    if (Cout % 8 == 0)
+      igemm_epilogue_lds<BM, BN, TM, TN, WM, WN, true>(acc, reinterpret_cast<float*>(lds), m0, n0, wm, wn, lane, tid, M,
+                                                       Cout, ep, y, split, splits, slab, Ho, Wo);
+    else
+      igemm_epilogue<TM, TN, WM, WN, true>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab, Ho, Wo);
+  } else if (Cout % 8 == 0) {
     igemm_epilogue_lds<BM, BN, TM, TN, WM, WN>(acc, reinterpret_cast<float*>(lds), m0, n0, wm, wn, lane, tid, M, Cout,
                                                ep, y, split, splits, slab, Ho, Wo);
-  else
+  } else {
     igemm_epilogue<TM, TN, WM, WN>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab, Ho, Wo);
+  }
 }
 
 template <int BM, int BN, int S, bool F16 = false>
@@ -1417,6 +1509,14 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
     tile = 3;
   if ((ep.st_part || ep.bnb_part) && tile < 21) return -1;  // needs the buffer / ring epilogue
   if (ep.bnb_part && (splits > 1 || Cout % 8 != 0)) return -1;
+  if (ep.x2 || ep.yf) {
+    // pairs / fp32 outputs: the buffer kernels only (their epilogue and K-phase loop carry x2)
+    if (!(tile == 22 || tile == 23)) tile = 23;
+    if ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB || (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kBufOOB ||
+        KH * KW > 64 || ep.f16)
+      return -1;
+    if (ep.yf && (ep.y2 || ep.bnb_x || ep.st_part)) return -1;
+  }
   if (tile >= 100 && tile < 100 + kNumRing) {
     launch_ring_code(tile - 100, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st);
     return tile;
@@ -1525,7 +1625,7 @@ conv_dgrad_wgrad_kernel(const uint16_t* __restrict__ x, const uint16_t* __restri
   // data gradient, then the weight gradient
   const int b = (int)blockIdx.x;
   if (b < rp.nwg) {
-    wgrad_reduce_body(b, rp.slab, rp.splits, rp.n, rp.dw, rp.accumulate);
+    wgrad_reduce_body(b, rp.slab, rp.splits, rp.n, rp.dw, rp.accumulate, rp.dwf);
   } else if (b < rp.nwg + nwg_d) {
     igemm_buf_body<64, 64, S, false>(lds, b - rp.nwg, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, 1, pad, ep, tiles_n,
                                      nwg_d, ntiles, 1, nullptr);
@@ -1539,7 +1639,7 @@ int conv_dgrad_wgrad(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, 
                      const uint16_t* wg_x, uint16_t* dw, float* slab, int wg_NB, int wg_H, int wg_W, int wg_Cin,
                      int wg_Ho, int wg_Wo, int wg_Cout, int wg_KH, int wg_KW, int wg_stride, int wg_pad, int wg_splits,
                      int accumulate, hipStream_t st, int defer_reduce, const float* prev_slab, int prev_splits,
-                     int64_t prev_n, uint16_t* prev_dw) {
+                     int64_t prev_n, uint16_t* prev_dw, const WgradX2& wx2, float* prev_dwf) {
   if (Cin % BK != 0 || Cout % 8 != 0 || ep.f16 || ep.omap || ep.pad_w >= 0) return -1;
   if ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB || (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kBufOOB)
     return -1;
@@ -1547,16 +1647,23 @@ int conv_dgrad_wgrad(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, 
   if ((int64_t)wg_NB * wg_Ho * wg_Wo * wg_Cout * 2 >= (int64_t)kWgOOB ||
       (int64_t)wg_NB * wg_H * wg_W * wg_Cin * 2 >= (int64_t)kWgOOB)
     return -1;
-  if (prev_slab != nullptr && (prev_splits < 2 || prev_n % 4 != 0 || prev_dw == nullptr)) return -1;
+  if (prev_slab != nullptr && (prev_splits < 2 || prev_n % 4 != 0 || (prev_dw == nullptr && prev_dwf == nullptr)))
+    return -1;
+  if (ep.x2 != wx2.x2) return -1;  // both roles read the same dY: one storage format
   const int M = NB * Ho * Wo;
   const int tiles_n = (Cout + 63) / 64;
   const int ntiles = ((M + 63) / 64) * tiles_n;
-  const WgradParams wp = wgrad_params(wg_dy, wg_x, dw, slab, wg_NB, wg_H, wg_W, wg_Cin, wg_Ho, wg_Wo, wg_Cout, wg_KH,
-                                      wg_KW, wg_stride, wg_pad, wg_splits, accumulate);
+  WgradParams wp = wgrad_params(wg_dy, wg_x, dw, slab, wg_NB, wg_H, wg_W, wg_Cin, wg_Ho, wg_Wo, wg_Cout, wg_KH,
+                                wg_KW, wg_stride, wg_pad, wg_splits, accumulate);
+  wp.x2 = wx2.x2;
+  wp.x2_pdy = wx2.pdy;
+  wp.x2_px = wx2.px;
+  wp.dwf = wx2.dwf;
   WgradReduceParams rp;
   if (prev_slab != nullptr) {
     rp.slab = prev_slab;
     rp.dw = prev_dw;
+    rp.dwf = prev_dwf;
     rp.n = prev_n;
     rp.splits = prev_splits;
     rp.accumulate = 1;
@@ -1573,7 +1680,7 @@ int conv_dgrad_wgrad(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, 
     conv_dgrad_wgrad_kernel<3><<<rp.nwg + ntiles + wp.nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW,
                                                                          pad, ep, tiles_n, ntiles, ntiles, wp, rp);
   if (wg_splits > 1 && !defer_reduce)
-    wgrad_reduce(slab, wg_splits, (int64_t)wg_Cout * wg_KH * wg_KW * wg_Cin, dw, accumulate, st);
+    wgrad_reduce(slab, wg_splits, (int64_t)wg_Cout * wg_KH * wg_KW * wg_Cin, dw, accumulate, st, wx2.dwf);
   return 0;
 }
 

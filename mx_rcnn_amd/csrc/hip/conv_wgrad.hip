@@ -143,8 +143,8 @@ __global__ void __launch_bounds__(256) conv_wgrad_buf_kernel(WgradParams p) {
 
 __global__ void __launch_bounds__(256)
 wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int64_t n, uint16_t* __restrict__ out,
-                    int accumulate) {
-  wgrad_reduce_body((int)blockIdx.x, slab, splits, n, out, accumulate);
+                    int accumulate, float* __restrict__ outf) {
+  wgrad_reduce_body((int)blockIdx.x, slab, splits, n, out, accumulate, outf);
 }
 
 WgradParams wgrad_params(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab, int NB, int H, int W,
@@ -165,12 +165,13 @@ WgradParams wgrad_params(const uint16_t* dy, const uint16_t* x, uint16_t* dw, fl
   return p;
 }
 
-void wgrad_reduce(const float* slab, int splits, int64_t n, uint16_t* dw, int accumulate, hipStream_t st) {
-  wgrad_reduce_kernel<<<div_up((n + 3) / 4, 256), 256, 0, st>>>(slab, splits, n, dw, accumulate);
+void wgrad_reduce(const float* slab, int splits, int64_t n, uint16_t* dw, int accumulate, hipStream_t st,
+                  float* dwf) {
+  wgrad_reduce_kernel<<<div_up((n + 3) / 4, 256), 256, 0, st>>>(slab, splits, n, dw, accumulate, dwf);
 }
 
-void wgrad_reduce_run(const float* slab, int splits, int64_t n, uint16_t* dw, hipStream_t st) {
-  wgrad_reduce(slab, splits, n, dw, 1, st);
+void wgrad_reduce_run(const float* slab, int splits, int64_t n, uint16_t* dw, hipStream_t st, float* dwf) {
+  wgrad_reduce(slab, splits, n, dw, 1, st, dwf);
 }
 
 int conv_wgrad_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int* splits_out) {
@@ -191,7 +192,7 @@ int conv_wgrad_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, i
 
 int conv_wgrad(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab, int NB, int H, int W, int Cin,
                int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int splits, int accumulate,
-               hipStream_t st, int variant) {
+               hipStream_t st, int variant, const WgradX2& x2) {
   if (Cin % WG_BN != 0 || Cout % 8 != 0) return -1;
   const int P = NB * Ho * Wo;
   const int tiles_m = (Cout + WG_BM - 1) / WG_BM, tiles_n = KH * KW * Cin / WG_BN;
@@ -200,15 +201,21 @@ int conv_wgrad(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab,
   const int per = (steps + splits - 1) / splits;
   const int64_t n = (int64_t)Cout * KH * KW * Cin;
   const bool buf_ok = (int64_t)P * Cout * 2 < (int64_t)kWgOOB && (int64_t)NB * H * W * Cin * 2 < (int64_t)kWgOOB;
+  if (x2.x2 && !(variant == 0 && buf_ok)) return -1;  // pairs: the LDS-DMA kernel only
   if (variant == 0 && buf_ok) {
-    conv_wgrad_buf_kernel<3><<<ntiles * splits, 256, 0, st>>>(
-        wgrad_params(dy, x, dw, slab, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, splits, accumulate));
-    if (splits > 1) wgrad_reduce_kernel<<<div_up((n + 3) / 4, 256), 256, 0, st>>>(slab, splits, n, dw, accumulate);
+    WgradParams p = wgrad_params(dy, x, dw, slab, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, splits, accumulate);
+    p.x2 = x2.x2;
+    p.x2_pdy = x2.pdy;
+    p.x2_px = x2.px;
+    p.dwf = x2.dwf;
+    conv_wgrad_buf_kernel<3><<<ntiles * splits, 256, 0, st>>>(p);
+    if (splits > 1)
+      wgrad_reduce_kernel<<<div_up((n + 3) / 4, 256), 256, 0, st>>>(slab, splits, n, dw, accumulate, x2.dwf);
     return splits;
   }
   conv_wgrad_kernel<<<ntiles * splits, 256, 0, st>>>(dy, x, slab, NB, H, W, Cin, Ho, Wo, Cout, KW, stride, pad,
                                                      tiles_n, ntiles, splits, per);
-  wgrad_reduce_kernel<<<div_up((n + 3) / 4, 256), 256, 0, st>>>(slab, splits, n, dw, accumulate);
+  wgrad_reduce_kernel<<<div_up((n + 3) / 4, 256), 256, 0, st>>>(slab, splits, n, dw, accumulate, nullptr);
   return splits;
 }
 

@@ -8,7 +8,9 @@
 //
 //   det_class_nms_kernel  grid (B, C-1): one workgroup per (image, class).  Threshold-collect
 //       the class scores into LDS (LDS atomic slot counter), bitonic-sort them (score desc, RoI
-//       index asc on ties -> the reference's stable order), decode + clip the survivors, greedy
+//       index asc on ties: a fixed, deterministic tie rule -- the reference's `argsort()[::-1]`
+//       (helper/processing/nms.py:19) orders tied scores by DESCENDING index after numpy's
+//       unstable quicksort, so tied-score parity is unpinned), decode + clip the survivors, greedy
 //       NMS over the sorted list (a suppression bitmask resolved by one wave; above 512
 //       candidates suppression flags with one barrier per kept box), write the kept (score, box)
 //       list of the class.

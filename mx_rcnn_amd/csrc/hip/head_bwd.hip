@@ -36,11 +36,16 @@ struct HeadStep {
   int h, r0;  // head, first reduction index of this step
 };
 
+// X2: the fp32-class variant (HeadBwdArgs::x2): dY fp32 split into hi / lo in registers, X / W
+// read as hi / lo planes, both halves staged in LDS, three MFMAs per fragment pair
+template <bool X2>
 __global__ void __launch_bounds__(256)
 head_bwd_kernel(const uint16_t* __restrict__ x, int M, int K, HeadBwdArgs a) {
-  __shared__ __attribute__((aligned(16))) uint16_t As[64 * HB_LD];
-  __shared__ __attribute__((aligned(16))) uint16_t Bs[64 * HB_LD];
+  constexpr int NP = X2 ? 2 : 1;  // operand planes staged per step
+  __shared__ __attribute__((aligned(16))) uint16_t As[NP][64 * HB_LD];
+  __shared__ __attribute__((aligned(16))) uint16_t Bs[NP][64 * HB_LD];
   __shared__ __attribute__((aligned(16))) float T[64 * 68];
+  const int64_t xplane = (int64_t)M * K;
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int wm = wid >> 1, wn = wid & 1;
   const int tk_n = K / 64;
@@ -85,13 +90,21 @@ head_bwd_kernel(const uint16_t* __restrict__ x, int M, int K, HeadBwdArgs a) {
     return st;
   };
 
-  // ---- register stage: 8 A values + one 16-B B vector per thread ----------------------------
-  uint16_t ra[8];
-  uint4 rbv;
+  // ---- register stage: 8 A values + one 16-B B vector per thread (per plane) ---------------
+  uint16_t ra[NP][8];
+  uint4 rbv[NP];
+  // dY element (m, n) of head h as (hi, lo) bf16 (lo unused unless X2)
+  auto dy_at = [&](int hh, int Nh, int64_t idx, uint16_t& hi, uint16_t& lo) {
+    if constexpr (X2) {
+      split_bf16(a.dyf[hh][idx], hi, lo);
+    } else {
+      hi = a.dy[hh][idx];
+      lo = 0;
+    }
+  };
   auto load = [&](int s) {
     const HeadStep st = step_of(s);
     const int Nh = a.N[st.h];
-    const uint16_t* dy = a.dy[st.h];
     if (dx_role) {
       // A(i = m, r = n) = dY[m][n]: thread -> row i, 8 consecutive r
       const int i = tid >> 2, rq = (tid & 3) * 8;
@@ -99,12 +112,18 @@ head_bwd_kernel(const uint16_t* __restrict__ x, int M, int K, HeadBwdArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int n = st.r0 + rq + e;
-        ra[e] = (m < M && n < Nh) ? dy[(int64_t)m * Nh + n] : (uint16_t)0;
+        uint16_t hi = 0, lo = 0;
+        if (m < M && n < Nh) dy_at(st.h, Nh, (int64_t)m * Nh + n, hi, lo);
+        ra[0][e] = hi;
+        if constexpr (X2) ra[1][e] = lo;
       }
       // B(r = n, j = k) = W[n][k]
       const int r = tid >> 3, jq = (tid & 7) * 8;
       const int n = st.r0 + r;
-      rbv = n < Nh ? *reinterpret_cast<const uint4*>(a.w[st.h] + (int64_t)n * K + k0 + jq) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int pl = 0; pl < NP; ++pl)
+        rbv[pl] = n < Nh ? *reinterpret_cast<const uint4*>(a.w[st.h] + (pl ? a.w_plane[st.h] : 0) + (int64_t)n * K + k0 + jq)
+                         : make_uint4(0, 0, 0, 0);
     } else {
       // A(i = n, r = m) = dY[m][n]: thread -> row r, 8 consecutive i
       const int r = tid >> 3, iq = (tid & 7) * 8;
@@ -112,32 +131,41 @@ head_bwd_kernel(const uint16_t* __restrict__ x, int M, int K, HeadBwdArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int n = i0 + iq + e;
-        ra[e] = (m < re && n < Nh) ? dy[(int64_t)m * Nh + n] : (uint16_t)0;
+        uint16_t hi = 0, lo = 0;
+        if (m < re && n < Nh) dy_at(st.h, Nh, (int64_t)m * Nh + n, hi, lo);
+        ra[0][e] = hi;
+        if constexpr (X2) ra[1][e] = lo;
       }
       // B(r = m, j = k) = X[m][k]
-      rbv = m < re ? *reinterpret_cast<const uint4*>(x + (int64_t)m * K + k0 + (tid & 7) * 8) : make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int pl = 0; pl < NP; ++pl)
+        rbv[pl] = m < re ? *reinterpret_cast<const uint4*>(x + (pl ? xplane : 0) + (int64_t)m * K + k0 + (tid & 7) * 8)
+                         : make_uint4(0, 0, 0, 0);
     }
   };
   auto store = [&]() {
-    if (dx_role) {
-      const int i = tid >> 2, rq = (tid & 3) * 8;
-      uint4 v;
-      v.x = (uint32_t)ra[0] | ((uint32_t)ra[1] << 16);
-      v.y = (uint32_t)ra[2] | ((uint32_t)ra[3] << 16);
-      v.z = (uint32_t)ra[4] | ((uint32_t)ra[5] << 16);
-      v.w = (uint32_t)ra[6] | ((uint32_t)ra[7] << 16);
-      *reinterpret_cast<uint4*>(As + i * HB_LD + rq) = v;
-    } else {
-      const int r = tid >> 3, iq = (tid & 7) * 8;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) As[(iq + e) * HB_LD + r] = ra[e];
-    }
-    const int r = tid >> 3, jq = (tid & 7) * 8;
-    const uint32_t bw[4] = {rbv.x, rbv.y, rbv.z, rbv.w};
+    for (int pl = 0; pl < NP; ++pl) {
+      if (dx_role) {
+        const int i = tid >> 2, rq = (tid & 3) * 8;
+        uint4 v;
+        v.x = (uint32_t)ra[pl][0] | ((uint32_t)ra[pl][1] << 16);
+        v.y = (uint32_t)ra[pl][2] | ((uint32_t)ra[pl][3] << 16);
+        v.z = (uint32_t)ra[pl][4] | ((uint32_t)ra[pl][5] << 16);
+        v.w = (uint32_t)ra[pl][6] | ((uint32_t)ra[pl][7] << 16);
+        *reinterpret_cast<uint4*>(As[pl] + i * HB_LD + rq) = v;
+      } else {
+        const int r = tid >> 3, iq = (tid & 7) * 8;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      Bs[(jq + 2 * e) * HB_LD + r] = (uint16_t)(bw[e] & 0xffffu);
-      Bs[(jq + 2 * e + 1) * HB_LD + r] = (uint16_t)(bw[e] >> 16);
+        for (int e = 0; e < 8; ++e) As[pl][(iq + e) * HB_LD + r] = ra[pl][e];
+      }
+      const int r = tid >> 3, jq = (tid & 7) * 8;
+      const uint32_t bw[4] = {rbv[pl].x, rbv[pl].y, rbv[pl].z, rbv[pl].w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        Bs[pl][(jq + 2 * e) * HB_LD + r] = (uint16_t)(bw[e] & 0xffffu);
+        Bs[pl][(jq + 2 * e + 1) * HB_LD + r] = (uint16_t)(bw[e] >> 16);
+      }
     }
   };
 
@@ -153,17 +181,26 @@ head_bwd_kernel(const uint16_t* __restrict__ x, int M, int K, HeadBwdArgs a) {
     __syncthreads();
     if (s + 1 < nsteps) load(s + 1);  // in flight during the MFMAs
     const int kc = (lane >> 4) * 8;
-    hb16x8 af[2], bf[2];
+    hb16x8 af[NP][2], bf[NP][2];
+#pragma unroll
+    for (int pl = 0; pl < NP; ++pl) {
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        af[pl][p] = *reinterpret_cast<const hb16x8*>(As[pl] + (wm * 32 + p * 16 + (lane & 15)) * HB_LD + kc);
+#pragma unroll
+      for (int q = 0; q < 2; ++q)
+        bf[pl][q] = *reinterpret_cast<const hb16x8*>(Bs[pl] + (wn * 32 + q * 16 + (lane & 15)) * HB_LD + kc);
+    }
 #pragma unroll
     for (int p = 0; p < 2; ++p)
-      af[p] = *reinterpret_cast<const hb16x8*>(As + (wm * 32 + p * 16 + (lane & 15)) * HB_LD + kc);
 #pragma unroll
-    for (int q = 0; q < 2; ++q)
-      bf[q] = *reinterpret_cast<const hb16x8*>(Bs + (wn * 32 + q * 16 + (lane & 15)) * HB_LD + kc);
-#pragma unroll
-    for (int p = 0; p < 2; ++p)
-#pragma unroll
-      for (int q = 0; q < 2; ++q) acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[p], bf[q], acc[p][q], 0, 0, 0);
+      for (int q = 0; q < 2; ++q) {
+        acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][p], bf[0][q], acc[p][q], 0, 0, 0);
+        if constexpr (X2) {
+          acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][p], bf[1][q], acc[p][q], 0, 0, 0);
+          acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][p], bf[0][q], acc[p][q], 0, 0, 0);
+        }
+      }
   }
 
   // ---- epilogue through LDS: T[i][j] fp32, then 8-wide rows ---------------------------------
@@ -189,12 +226,14 @@ head_bwd_kernel(const uint16_t* __restrict__ x, int M, int K, HeadBwdArgs a) {
       const int64_t o = (int64_t)i * K + k0 + cv;
       if (a.relu_mask) {
         float xv[8];
-        ld8_bf16(x + o, xv);
+        if constexpr (X2) ld8x(x + o, xplane, xv);
+        else ld8_bf16(x + o, xv);
 #pragma unroll
         for (int q = 0; q < 8; ++q)
           if (!(xv[q] > 0.f)) v8[q] = 0.f;
       }
-      st8_bf16(a.dx + o, v8);
+      if constexpr (X2) st8x(a.dx + o, xplane, v8, v8);
+      else st8_bf16(a.dx + o, v8);
     } else {
       if (i >= Nh) continue;
       const int64_t o = (int64_t)i * K + k0 + cv;
@@ -202,6 +241,16 @@ head_bwd_kernel(const uint16_t* __restrict__ x, int M, int K, HeadBwdArgs a) {
         float* wp = a.ws_dw[h] + (int64_t)split * Nh * K + o;
         *reinterpret_cast<float4*>(wp) = p0;
         *reinterpret_cast<float4*>(wp + 4) = p1;
+      } else if constexpr (X2) {  // fp32 dW
+        float4* d = reinterpret_cast<float4*>(a.dwf[h] + o);
+        if (a.dw_acc[h]) {
+          const float4 q0 = d[0], q1 = d[1];
+          d[0] = make_float4(p0.x + q0.x, p0.y + q0.y, p0.z + q0.z, p0.w + q0.w);
+          d[1] = make_float4(p1.x + q1.x, p1.y + q1.y, p1.z + q1.z, p1.w + q1.w);
+        } else {
+          d[0] = p0;
+          d[1] = p1;
+        }
       } else {
         if (a.dw_acc[h]) {
           float prev[8];
@@ -222,7 +271,10 @@ head_bwd_kernel(const uint16_t* __restrict__ x, int M, int K, HeadBwdArgs a) {
     const int n = i0 + i;
     float s = 0.f;
     if (n < Nh)
-      for (int m = rb + qq; m < re; m += 4) s += bf16_to_f32(a.dy[h][(int64_t)m * Nh + n]);
+      for (int m = rb + qq; m < re; m += 4) {
+        if constexpr (X2) s += a.dyf[h][(int64_t)m * Nh + n];
+        else s += bf16_to_f32(a.dy[h][(int64_t)m * Nh + n]);
+      }
     red[qq * 64 + i] = s;
     __syncthreads();
     if (tid < 64 && n < Nh) {
@@ -247,8 +299,13 @@ head_bwd_fold_kernel(int K, HeadBwdArgs a, int h) {
     float s = 0.f;
 #pragma unroll 8
     for (int r = 0; r < a.rs; ++r) s += a.ws_dw[h][(int64_t)r * nw + e];
-    if (a.dw_acc[h]) s += bf16_to_f32(a.dw[h][e]);
-    a.dw[h][e] = f32_to_bf16(s);
+    if (a.x2) {
+      if (a.dw_acc[h]) s += a.dwf[h][e];
+      a.dwf[h][e] = s;
+    } else {
+      if (a.dw_acc[h]) s += bf16_to_f32(a.dw[h][e]);
+      a.dw[h][e] = f32_to_bf16(s);
+    }
   } else if (e < nw + Nh && a.db[h] != nullptr) {
     const int n = (int)(e - nw);
     float s = 0.f;
@@ -276,7 +333,8 @@ int head_bwd(const uint16_t* x, int M, int K, const HeadBwdArgs& a, hipStream_t 
     if (a.N[h] <= 0) return -1;
     nwg += (int64_t)((a.N[h] + 63) / 64) * tk_n * a.rs;
   }
-  head_bwd_kernel<<<(unsigned)nwg, 256, 0, st>>>(x, M, K, a);
+  if (a.x2) head_bwd_kernel<true><<<(unsigned)nwg, 256, 0, st>>>(x, M, K, a);
+  else head_bwd_kernel<false><<<(unsigned)nwg, 256, 0, st>>>(x, M, K, a);
   if (a.rs > 1)
     for (int h = 0; h < a.nheads; ++h)
       head_bwd_fold_kernel<<<div_up((int64_t)a.N[h] * K + a.N[h], 256), 256, 0, st>>>(K, a, h);
@@ -298,7 +356,7 @@ chan_sum_part_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int rows,
   if (c0 < C)
     for (int64_t r = r0 + rl; r < r1; r += 32) {
       float v[8];
-      ld8_h16(x + r * C + c0, v, code);
+      ld8c(x, r * C + c0, code, M * C, v);  // code 3: x2 pairs, lo plane M * C on
 #pragma unroll
       for (int k = 0; k < 8; ++k) s[k] += v[k];
     }

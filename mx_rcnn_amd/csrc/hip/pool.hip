@@ -1,5 +1,5 @@
 // Max-pool forward / backward and global average pool on NHWC bf16 / fp16 maps (SURVEY kernel K14;
-// `code` = 1 bf16, 2 fp16).
+// `code` = 1 bf16, 2 fp16, 3 x2 hi / lo pairs: the fp32-class training mode, common.h).
 //
 // Reference ops: VGG pool1..pool4 2x2/2 (`rcnn/symbol.py:19,28,40,52`), ResNet pool0 3x3/2 pad 1
 // (`rcnn/resnet.py:150`), global average pool before the predictors (`rcnn/resnet.py:167`).
@@ -43,7 +43,7 @@ maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, uin
       const int w = w0 + j;
       if ((unsigned)w >= (unsigned)W) continue;
       float v[8];
-      ld8_h16(x + (((int64_t)n * H + h) * W + w) * C + c8 * 8, v, code);
+      ld8c(x, (((int64_t)n * H + h) * W + w) * C + c8 * 8, code, (int64_t)N * H * W * C, v);
 #pragma unroll
       for (int q = 0; q < 8; ++q)
         if (v[q] > best[q] || bi[q] == 255) {  // strict: the first maximum wins
@@ -52,7 +52,7 @@ maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, uin
         }
     }
   }
-  st8_h16(y + pix * C + c8 * 8, best, code);
+  st8c(y, pix * C + c8 * 8, code, (int64_t)N * Ho * Wo * C, best);
   uint32_t lo = 0, hi = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -85,7 +85,7 @@ maxpool_bwd_kernel(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ 
       const int64_t o = (((int64_t)n * Ho + ho) * Wo + wo) * C + c8 * 8;
       const uint2 a = *reinterpret_cast<const uint2*>(arg + o);
       float g[8];
-      ld8_h16(dy + o, g, code);
+      ld8c(dy, o, code, (int64_t)N * Ho * Wo * C, g);
       const int tap = i * k + j;
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -94,26 +94,26 @@ maxpool_bwd_kernel(const uint16_t* __restrict__ dy, const uint8_t* __restrict__ 
       }
     }
   }
-  st8_h16(dx + pix * C + c8 * 8, acc, code);
+  st8c(dx, pix * C + c8 * 8, code, (int64_t)N * H * W * C, acc);
 }
 
 __global__ void __launch_bounds__(64)
 avgpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, int HW, int C, int code) {
   const int n = blockIdx.y;
+  const int64_t N = gridDim.y;
   const int c = (blockIdx.x * 64 + threadIdx.x) * 8;
   if (c >= C) return;
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  const uint16_t* base = x + (int64_t)n * HW * C + c;
   for (int i = 0; i < HW; ++i) {
     float v[8];
-    ld8_h16(base + (int64_t)i * C, v, code);
+    ld8c(x, ((int64_t)n * HW + i) * C + c, code, N * HW * C, v);
 #pragma unroll
     for (int q = 0; q < 8; ++q) acc[q] += v[q];
   }
   const float inv = 1.f / (float)HW;
 #pragma unroll
   for (int q = 0; q < 8; ++q) acc[q] *= inv;
-  st8_h16(y + (int64_t)n * C + c, acc, code);
+  st8c(y, (int64_t)n * C + c, code, N * C, acc);
 }
 
 __global__ void __launch_bounds__(256)
@@ -125,11 +125,11 @@ avgpool_bwd_kernel(const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx, i
   const int c8 = (int)(t % cv);
   const int n = (int)(t / ((int64_t)HW * cv));
   float g[8];
-  ld8_h16(dy + (int64_t)n * C + c8 * 8, g, code);
+  ld8c(dy, (int64_t)n * C + c8 * 8, code, (int64_t)N * C, g);
   const float inv = 1.f / (float)HW;
 #pragma unroll
   for (int q = 0; q < 8; ++q) g[q] *= inv;
-  st8_h16(dx + (t / cv) * C + c8 * 8, g, code);
+  st8c(dx, (t / cv) * C + c8 * 8, code, (int64_t)N * HW * C, g);
 }
 
 int maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int Ho, int Wo, int k,

@@ -46,6 +46,8 @@ template <typename T>
 __global__ void __launch_bounds__(256)
 roi_pool_fwd_vec4(const T* __restrict__ feat, int code, int B, int H, int W, int C, const float* __restrict__ rois, int R,
                   int PH, int PW, float scale, T* __restrict__ out, int32_t* __restrict__ argmax) {
+  // code 3 (x2 pairs, T = uint16_t): lo planes one (B, H, W, C) / (R, PH, PW, C) block further
+  const int64_t fplane = (int64_t)B * H * W * C, oplane = (int64_t)R * PH * PW * C;
   using V = typename Vec4<T>::type;
   const int CV = C >> 2;
   const int64_t total = (int64_t)R * PH * PW * CV;
@@ -68,7 +70,14 @@ roi_pool_fwd_vec4(const T* __restrict__ feat, int code, int B, int H, int W, int
       for (int w = bin.ws; w < bin.we; ++w) {
         const int idx = h * W + w;
         const V v = *reinterpret_cast<const V*>(fb + (int64_t)idx * C);
-        const float f0 = to_f(v.x, code), f1 = to_f(v.y, code), f2 = to_f(v.z, code), f3 = to_f(v.w, code);
+        float f0 = to_f(v.x, code == 3 ? 1 : code), f1 = to_f(v.y, code == 3 ? 1 : code);
+        float f2 = to_f(v.z, code == 3 ? 1 : code), f3 = to_f(v.w, code == 3 ? 1 : code);
+        if constexpr (sizeof(T) == 2) {
+          if (code == 3) {
+            const V l = *reinterpret_cast<const V*>(fb + fplane + (int64_t)idx * C);
+            f0 += to_f(l.x, 1); f1 += to_f(l.y, 1); f2 += to_f(l.z, 1); f3 += to_f(l.w, 1);
+          }
+        }
         if (f0 > m0) { m0 = f0; a0 = idx; }
         if (f1 > m1) { m1 = f1; a1 = idx; }
         if (f2 > m2) { m2 = f2; a2 = idx; }
@@ -78,8 +87,13 @@ roi_pool_fwd_vec4(const T* __restrict__ feat, int code, int B, int H, int W, int
   }
   const int64_t o = t * 4;
   if constexpr (sizeof(T) == 2) {
-    ushort4 ov = make_ushort4(f32_to_h16(m0, code), f32_to_h16(m1, code), f32_to_h16(m2, code), f32_to_h16(m3, code));
-    *reinterpret_cast<ushort4*>(out + o) = ov;
+    if (code == 3) {
+      const float mv[4] = {m0, m1, m2, m3};
+      st4c(out, o, 3, oplane, mv);
+    } else {
+      ushort4 ov = make_ushort4(f32_to_h16(m0, code), f32_to_h16(m1, code), f32_to_h16(m2, code), f32_to_h16(m3, code));
+      *reinterpret_cast<ushort4*>(out + o) = ov;
+    }
   } else {
     *reinterpret_cast<float4*>(out + o) = make_float4(m0, m1, m2, m3);
   }
@@ -202,6 +216,8 @@ __global__ void __launch_bounds__(256)
 roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ argmax, const float* __restrict__ rois,
                         int R, int PHW, int HW, int C, int code, const T* __restrict__ gadd, T* __restrict__ gin) {
   extern __shared__ float acc[];  // [HW][CW]
+  // code 3 (x2 pairs): gout's lo plane one (R, PH, PW, C) block further, gadd's / gin's one (B, H, W, C)
+  const int64_t oplane = (int64_t)R * PHW * C, iplane = (int64_t)gridDim.y * HW * C;
   // XCD-aware channel groups: workgroups are dealt round-robin over the 8 XCDs, so consecutive
   // block ids would put neighbouring channel groups -- which read and write the same cache lines
   // of the NHWC argmax / gradient rows -- on different L2s.  Consecutive groups share an XCD.
@@ -214,7 +230,10 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
 #pragma unroll 4
   for (int p = threadIdx.x; p < HW; p += blockDim.x) {
     float v[CW];
-    if (gadd) ldv<CW>(gadd + ((int64_t)b * HW + p) * C + c0, v, code);
+    if (gadd && code == 3) {
+#pragma unroll
+      for (int k = 0; k < CW; ++k) v[k] = ldc(gadd, ((int64_t)b * HW + p) * C + c0 + k, 3, iplane);
+    } else if (gadd) ldv<CW>(gadd + ((int64_t)b * HW + p) * C + c0, v, code);
     else
 #pragma unroll
       for (int k = 0; k < CW; ++k) v[k] = 0.f;
@@ -232,7 +251,7 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
 #pragma unroll
     for (int k = 0; k < CW; ++k) {
       a[k] = argmax[base + k];
-      g[k] = to_f(gout[base + k], code);
+      g[k] = code == 3 ? ldc(gout, base + k, 3, oplane) : to_f(gout[base + k], code);
     }
 #pragma unroll
     for (int k = 0; k < CW; ++k)
@@ -244,7 +263,12 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
     float v[CW];
 #pragma unroll
     for (int k = 0; k < CW; ++k) v[k] = acc[p * CW + k];
-    stv<CW>(gin + ((int64_t)b * HW + p) * C + c0, v, code);
+    if (code == 3) {
+#pragma unroll
+      for (int k = 0; k < CW; ++k) stc(gin, ((int64_t)b * HW + p) * C + c0 + k, v[k], 3, iplane);
+    } else {
+      stv<CW>(gin + ((int64_t)b * HW + p) * C + c0, v, code);
+    }
   }
 }
 

@@ -21,7 +21,8 @@ __device__ __forceinline__ float sgd_one(float w, float& m, float g, float lr, f
 template <bool GBF16>
 __global__ void __launch_bounds__(256)
 sgd_kernel(float* __restrict__ w, float* __restrict__ mom, const void* __restrict__ grad, int64_t n,
-           const float* __restrict__ lr_p, float mu, float wd, float rescale, float clip, uint16_t* __restrict__ wb) {
+           const float* __restrict__ lr_p, float mu, float wd, float rescale, float clip, uint16_t* __restrict__ wb,
+           int64_t x2_plane) {
   const float lr = *lr_p;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
   for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
@@ -41,9 +42,13 @@ sgd_kernel(float* __restrict__ w, float* __restrict__ mom, const void* __restric
       wv.w = sgd_one(wv.w, mv.w, gv.w, lr, mu, wd, rescale, clip);
       *reinterpret_cast<float4*>(w + i) = wv;
       *reinterpret_cast<float4*>(mom + i) = mv;
-      if (wb)
+      if (wb && x2_plane) {  // fp32-class shadow: hi / lo pair planes (common.h x2)
+        const float v4[4] = {wv.x, wv.y, wv.z, wv.w};
+        st4c(wb, i, kCodeX2, x2_plane, v4);
+      } else if (wb) {
         *reinterpret_cast<ushort4*>(wb + i) =
             make_ushort4(f32_to_bf16(wv.x), f32_to_bf16(wv.y), f32_to_bf16(wv.z), f32_to_bf16(wv.w));
+      }
     } else {
       for (int64_t k = i; k < n; ++k) {
         const float g = GBF16 ? bf16_to_f32(static_cast<const uint16_t*>(grad)[k]) : static_cast<const float*>(grad)[k];
@@ -51,20 +56,21 @@ sgd_kernel(float* __restrict__ w, float* __restrict__ mom, const void* __restric
         const float nw = sgd_one(w[k], m, g, lr, mu, wd, rescale, clip);
         w[k] = nw;
         mom[k] = m;
-        if (wb) wb[k] = f32_to_bf16(nw);
+        if (wb && x2_plane) stx(wb, k, x2_plane, nw);
+        else if (wb) wb[k] = f32_to_bf16(nw);
       }
     }
   }
 }
 
 void sgd_momentum(float* w, float* mom, const void* grad, int grad_bf16, int64_t n, const float* lr, float momentum,
-                  float wd, float rescale, float clip, uint16_t* w_bf16, hipStream_t st) {
+                  float wd, float rescale, float clip, uint16_t* w_bf16, hipStream_t st, int64_t x2_plane) {
   if (n == 0) return;
   const int blocks = (int)std::min<int64_t>(div_up((n + 3) / 4, 256), 256 * 8);
   if (grad_bf16)
-    sgd_kernel<true><<<blocks, 256, 0, st>>>(w, mom, grad, n, lr, momentum, wd, rescale, clip, w_bf16);
+    sgd_kernel<true><<<blocks, 256, 0, st>>>(w, mom, grad, n, lr, momentum, wd, rescale, clip, w_bf16, x2_plane);
   else
-    sgd_kernel<false><<<blocks, 256, 0, st>>>(w, mom, grad, n, lr, momentum, wd, rescale, clip, w_bf16);
+    sgd_kernel<false><<<blocks, 256, 0, st>>>(w, mom, grad, n, lr, momentum, wd, rescale, clip, w_bf16, x2_plane);
 }
 
 }  // namespace mxr

@@ -42,7 +42,9 @@ constexpr int STEM_BM = 64;   // output pixels per workgroup (one row strip)
 constexpr int STEM_CO = 64;   // output channels (all of them)
 constexpr int STEM_LDT = STEM_CO + 8;  // 16-bit row stride of the staged output tile
 
-template <int KH, int KW, int S, bool F16>
+// X2 (fp32-class mode): x is the fp32 image, the patch is kept as hi / lo bf16 planes, the packed
+// filter is an x2 pair (lo plane 64 * KP on), three MFMAs per fragment pair, y an x2 pair
+template <int KH, int KW, int S, bool F16, bool X2 = false>
 __global__ void __launch_bounds__(256)
 stem_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, const StemArgs a,
                  uint16_t* __restrict__ y, int N, int H, int W, int Ho, int Wo, int pad, int relu, int strips, int nwg) {
@@ -50,10 +52,11 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
   constexpr int KP = (K + 31) / 32 * 32;
   constexpr int PW = (STEM_BM - 1) * S + KW;  // patch columns
   constexpr int code = F16 ? 2 : 1;
-  __shared__ __attribute__((aligned(16))) uint16_t patch[KH * PW * 4];
+  constexpr int NP = X2 ? 2 : 1;  // planes
+  __shared__ __attribute__((aligned(16))) uint16_t patch[NP][KH * PW * 4];
   __shared__ int koff[KP];
   __shared__ float in_aff[6], out_aff[2 * STEM_CO];
-  __shared__ __attribute__((aligned(16))) uint16_t T[STEM_BM * STEM_LDT];
+  __shared__ __attribute__((aligned(16))) uint16_t T[NP][STEM_BM * STEM_LDT];
 
   // XCD-aware order: consecutive tiles (neighbouring output rows share KH-S input rows) on one XCD
   const int bid = blockIdx.x;
@@ -102,15 +105,26 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
   for (int e = tid; e < KH * PW; e += 256) {
     const int r = e / PW, c = e - r * PW;
     const int hi = hi0 + r, wi = wi0 + c;
-    uint2 v = make_uint2(0u, 0u);
+    uint2 v = make_uint2(0u, 0u), vl = make_uint2(0u, 0u);
     if ((unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W) {
-      const uint16_t* px = x + (((int64_t)n * H + hi) * W + wi) * 3;
-      const uint32_t c0 = f32_to_h16(h16_to_f32(px[0], code) * s0 + b0, code);
-      const uint32_t c1 = f32_to_h16(h16_to_f32(px[1], code) * s1 + b1, code);
-      const uint32_t c2 = f32_to_h16(h16_to_f32(px[2], code) * s2 + b2, code);
-      v = make_uint2(c0 | (c1 << 16), c2);
+      if constexpr (X2) {
+        const float* px = reinterpret_cast<const float*>(x) + (((int64_t)n * H + hi) * W + wi) * 3;
+        uint16_t h0, l0, h1, l1, h2, l2;
+        split_bf16(px[0] * s0 + b0, h0, l0);
+        split_bf16(px[1] * s1 + b1, h1, l1);
+        split_bf16(px[2] * s2 + b2, h2, l2);
+        v = make_uint2((uint32_t)h0 | ((uint32_t)h1 << 16), h2);
+        vl = make_uint2((uint32_t)l0 | ((uint32_t)l1 << 16), l2);
+      } else {
+        const uint16_t* px = x + (((int64_t)n * H + hi) * W + wi) * 3;
+        const uint32_t c0 = f32_to_h16(h16_to_f32(px[0], code) * s0 + b0, code);
+        const uint32_t c1 = f32_to_h16(h16_to_f32(px[1], code) * s1 + b1, code);
+        const uint32_t c2 = f32_to_h16(h16_to_f32(px[2], code) * s2 + b2, code);
+        v = make_uint2(c0 | (c1 << 16), c2);
+      }
     }
-    *reinterpret_cast<uint2*>(patch + e * 4) = v;
+    *reinterpret_cast<uint2*>(patch[0] + e * 4) = v;
+    if constexpr (X2) *reinterpret_cast<uint2*>(patch[NP - 1] + e * 4) = vl;
   }
   __syncthreads();
 
@@ -124,19 +138,28 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
 #pragma unroll
   for (int ks = 0; ks < KP / 32; ++ks) {
     const int k0 = ks * 32 + chunk * 8;
-    uint32_t aw[4];
+    uint4 af[NP];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int o0 = koff[k0 + 2 * e], o1 = koff[k0 + 2 * e + 1];
-      const uint32_t lo = o0 >= 0 ? patch[o0 + pbase] : 0u;
-      const uint32_t hi = o1 >= 0 ? patch[o1 + pbase] : 0u;
-      aw[e] = lo | (hi << 16);
+    for (int pl = 0; pl < NP; ++pl) {
+      uint32_t aw[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int o0 = koff[k0 + 2 * e], o1 = koff[k0 + 2 * e + 1];
+        const uint32_t lo = o0 >= 0 ? patch[pl][o0 + pbase] : 0u;
+        const uint32_t hi = o1 >= 0 ? patch[pl][o1 + pbase] : 0u;
+        aw[e] = lo | (hi << 16);
+      }
+      af[pl] = make_uint4(aw[0], aw[1], aw[2], aw[3]);
     }
-    const uint4 af = make_uint4(aw[0], aw[1], aw[2], aw[3]);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint4 bf = *reinterpret_cast<const uint4*>(w + (j * 16 + (lane & 15)) * KP + k0);
-      acc[j] = stem_mfma<F16>(af, bf, acc[j]);
+      acc[j] = stem_mfma<F16>(af[0], bf, acc[j]);
+      if constexpr (X2) {  // A_hi B_lo + A_lo B_hi
+        const uint4 bl = *reinterpret_cast<const uint4*>(w + STEM_CO * KP + (j * 16 + (lane & 15)) * KP + k0);
+        acc[j] = stem_mfma<F16>(af[0], bl, acc[j]);
+        acc[j] = stem_mfma<F16>(af[1], bf, acc[j]);
+      }
     }
   }
 
@@ -149,7 +172,14 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
     for (int r = 0; r < 4; ++r) {
       float v = acc[j][r] * sc + sh;
       if (relu) v = fmaxf(v, 0.f);
-      T[(wave * 16 + chunk * 4 + r) * STEM_LDT + co] = f32_to_h16(v, code);
+      if constexpr (X2) {
+        uint16_t h, l;
+        split_bf16(v, h, l);
+        T[0][(wave * 16 + chunk * 4 + r) * STEM_LDT + co] = h;
+        T[NP - 1][(wave * 16 + chunk * 4 + r) * STEM_LDT + co] = l;
+      } else {
+        T[0][(wave * 16 + chunk * 4 + r) * STEM_LDT + co] = f32_to_h16(v, code);
+      }
     }
   }
   __syncthreads();
@@ -159,9 +189,13 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
     const int idx = tid + v * 256;
     const int px = idx >> 3, cv = idx & 7;
     const int wo = wo0 + px;
-    if (wo < Wo)
-      *reinterpret_cast<uint4*>(y + (((int64_t)n * Ho + ho) * Wo + wo) * STEM_CO + cv * 8) =
-          *reinterpret_cast<const uint4*>(T + px * STEM_LDT + cv * 8);
+    if (wo < Wo) {
+      const int64_t o = (((int64_t)n * Ho + ho) * Wo + wo) * STEM_CO + cv * 8;
+      *reinterpret_cast<uint4*>(y + o) = *reinterpret_cast<const uint4*>(T[0] + px * STEM_LDT + cv * 8);
+      if constexpr (X2)  // lo plane: one (N, Ho, Wo, 64) block further
+        *reinterpret_cast<uint4*>(y + (int64_t)N * Ho * Wo * STEM_CO + o) =
+            *reinterpret_cast<const uint4*>(T[NP - 1] + px * STEM_LDT + cv * 8);
+    }
   }
 }
 
@@ -174,7 +208,10 @@ int stem_conv(const uint16_t* x, const uint16_t* w, const StemArgs& a, uint16_t*
   const int nwg = (int)nwg64;
 #define MXR_STEM(KH_, KW_, S_)                                                                                   \
   if (KH == KH_ && KW == KW_ && stride == S_) {                                                                \
-    if (code == 2)                                                                                             \
+    if (code == 3)                                                                                             \
+      stem_conv_kernel<KH_, KW_, S_, false, true><<<nwg, 256, 0, st>>>(x, w, a, y, N, H, W, Ho, Wo, pad, relu,     \
+                                                                       strips, nwg);                            \
+    else if (code == 2)                                                                                        \
       stem_conv_kernel<KH_, KW_, S_, true><<<nwg, 256, 0, st>>>(x, w, a, y, N, H, W, Ho, Wo, pad, relu, strips, nwg); \
     else                                                                                                       \
       stem_conv_kernel<KH_, KW_, S_, false><<<nwg, 256, 0, st>>>(x, w, a, y, N, H, W, Ho, Wo, pad, relu, strips, nwg); \

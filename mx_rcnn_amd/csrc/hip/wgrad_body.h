@@ -63,6 +63,11 @@ struct WgradParams {
   uint16_t* dw;
   int accumulate, NB, H, W, Cin, Ho, Wo, Cout, KW, stride, pad, tiles_n, ntiles, splits, per, nwg;
   FastDiv fd_hw, fd_w;
+  // fp32-class operands (common.h x2): dY and X are hi / lo plane pairs; the pixel loop runs three
+  // phases (dY_hi X_hi, dY_hi X_lo, dY_lo X_hi) and the gradient is fp32 (dwf instead of dw)
+  int x2 = 0;
+  uint32_t x2_pdy = 0, x2_px = 0;  // lo-plane offsets, bytes
+  float* dwf = nullptr;
 };
 
 constexpr int kWgradLdsElems = 3 * 2 * WG_BK * 64;  // the S = 3 ring: [S][dY|X][64 px][64 ch] (48 KB)
@@ -91,11 +96,13 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
   const int steps_all = (P + WG_BK - 1) / WG_BK;
   const int s_begin = split * per, s_end = min(steps_all, s_begin + per);
   const int nsteps = max(0, s_end - s_begin);
+  const int nloop = p.x2 ? 3 * nsteps : nsteps;  // x2: the pixel range once per product phase
 
-  const __amdgpu_buffer_rsrc_t dyr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)dy, (short)0, (int)((int64_t)P * Cout * 2), 0x00020000);
-  const __amdgpu_buffer_rsrc_t xr =
-      __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, (int)((int64_t)NB * H * W * Cin * 2), 0x00020000);
+  // records through the lo planes for x2 pairs (the range check covers voffset + soffset)
+  const __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)dy, (short)0, (int)((int64_t)P * Cout * 2 + (p.x2 ? p.x2_pdy : 0u)), 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)x, (short)0, (int)((int64_t)NB * H * W * Cin * 2 + (p.x2 ? p.x2_px : 0u)), 0x00020000);
   int rowi[2], chk[2];
   uint32_t a_off[2];
 #pragma unroll
@@ -104,8 +111,10 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
     chk[i] = (lane & 7) ^ wsw(rowi[i]);
     a_off[i] = co0 + chk[i] * 8 < Cout ? (uint32_t)((rowi[i] * Cout + co0 + chk[i] * 8) * 2) : kWgOOB;
   }
-  auto issue = [&](int sl, int buf) {
+  auto issue = [&](int it, int buf) {
+    const int ph = it / nsteps, sl = it - ph * nsteps;  // x2 phase, step within the range
     const int p0 = (s_begin + sl) * WG_BK;
+    const uint32_t pdy = ph == 2 ? p.x2_pdy : 0u, px = ph == 1 ? p.x2_px : 0u;
     uint16_t* Ab = lds + buf * 2 * WG_BK * 64;
     uint16_t* Bb = Ab + WG_BK * 64;
 #pragma unroll
@@ -113,7 +122,7 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
       const int p = p0 + rowi[i];
       const uint32_t va = p < P ? a_off[i] : kWgOOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(dyr, (__attribute__((address_space(3))) void*)(Ab + (32 * i + 8 * wid) * 64),
-                                               16, (int)va, (int)((uint32_t)p0 * Cout * 2), 0, 0);
+                                               16, (int)va, (int)((uint32_t)p0 * Cout * 2 + pdy), 0, 0);
       uint32_t vb = kWgOOB;
       if (p < P) {
         const int img = (int)fdiv((uint32_t)p, fd_hw), rem = p - img * HWo;
@@ -123,7 +132,7 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
           vb = (uint32_t)(((((int64_t)img * H + hi) * W + wi) * Cin + ci0 + chk[i] * 8) * 2);
       }
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(Bb + (32 * i + 8 * wid) * 64),
-                                               16, (int)vb, 0, 0, 0);
+                                               16, (int)vb, (int)px, 0, 0);
     }
   };
 
@@ -138,14 +147,14 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
 
 #pragma unroll
   for (int s = 0; s < S - 1; ++s)
-    if (s < nsteps) issue(s, s);
-  for (int st = 0; st < nsteps; ++st) {
-    const int ahead = min(S - 2, nsteps - 1 - st);
+    if (s < nloop) issue(s, s);
+  for (int st = 0; st < nloop; ++st) {
+    const int ahead = min(S - 2, nloop - 1 - st);
     if (ahead >= 2) wait_vmcnt_wg<2 * LPS>();
     else if (ahead == 1) wait_vmcnt_wg<LPS>();
     else wait_vmcnt_wg<0>();
     __builtin_amdgcn_s_barrier();
-    if (st + S - 1 < nsteps) issue(st + S - 1, (st + S - 1) % S);
+    if (st + S - 1 < nloop) issue(st + S - 1, (st + S - 1) % S);
     const uint16_t* Ab = lds + (st % S) * 2 * WG_BK * 64;
     const uint16_t* Bb = Ab + WG_BK * 64;
     // all 16 transposed fragment reads of the step in ONE asm block: through the builtin, the
@@ -226,6 +235,16 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
       float4* d = reinterpret_cast<float4*>(slab + (int64_t)split * Cout * ldk + o);
       d[0] = a0;
       d[1] = a1;
+    } else if (p.dwf) {  // fp32 gradient (x2 mode)
+      float4* d = reinterpret_cast<float4*>(p.dwf + o);
+      if (accumulate) {
+        const float4 q0 = d[0], q1 = d[1];
+        d[0] = make_float4(a0.x + q0.x, a0.y + q0.y, a0.z + q0.z, a0.w + q0.w);
+        d[1] = make_float4(a1.x + q1.x, a1.y + q1.y, a1.z + q1.z, a1.w + q1.w);
+      } else {
+        d[0] = a0;
+        d[1] = a1;
+      }
     } else {
       float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
       if (accumulate) {
@@ -242,7 +261,7 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
 // sum of the split-K slabs (+ the existing gradient when accumulating) -> bf16; 1024 elements per
 // 256-thread workgroup `gid` (the wgrad_reduce kernel, or a role of the grouped launch)
 __device__ __forceinline__ void wgrad_reduce_body(int gid, const float* __restrict__ slab, int splits, int64_t n,
-                                                  uint16_t* __restrict__ out, int accumulate) {
+                                                  uint16_t* __restrict__ out, int accumulate, float* outf = nullptr) {
   const int64_t e = ((int64_t)gid * 256 + threadIdx.x) * 4;
   if (e >= n) return;
   float4 a = *reinterpret_cast<const float4*>(slab + e);
@@ -250,6 +269,15 @@ __device__ __forceinline__ void wgrad_reduce_body(int gid, const float* __restri
   for (int s = 1; s < splits; ++s) {
     const float4 b = *reinterpret_cast<const float4*>(slab + (int64_t)s * n + e);
     a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  if (outf) {  // fp32 gradient (x2 mode)
+    float4* d = reinterpret_cast<float4*>(outf + e);
+    if (accumulate) {
+      const float4 q = *d;
+      a.x += q.x; a.y += q.y; a.z += q.z; a.w += q.w;
+    }
+    *d = a;
+    return;
   }
   if (accumulate) {  // add into the existing gradient (flat-buffer view), no separate add kernel
     const ushort4 o = *reinterpret_cast<const ushort4*>(out + e);
@@ -263,6 +291,7 @@ __device__ __forceinline__ void wgrad_reduce_body(int gid, const float* __restri
 struct WgradReduceParams {
   const float* slab = nullptr;
   uint16_t* dw = nullptr;
+  float* dwf = nullptr;  // fp32 gradient instead of dw (x2 mode)
   int64_t n = 0;
   int splits = 0, accumulate = 1, nwg = 0;
 };
@@ -271,6 +300,7 @@ struct WgradReduceParams {
 WgradParams wgrad_params(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab, int NB, int H, int W,
                          int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int splits,
                          int accumulate);
-void wgrad_reduce(const float* slab, int splits, int64_t n, uint16_t* dw, int accumulate, hipStream_t st);
+void wgrad_reduce(const float* slab, int splits, int64_t n, uint16_t* dw, int accumulate, hipStream_t st,
+                  float* dwf = nullptr);
 
 }  // namespace mxr

@@ -24,23 +24,27 @@ namespace host {
 
 // boxes: n x 4 (x1, y1, x2, y2) in descending-score order.  Kept positions are appended to
 // `keep`; max_keep <= 0 means no cap.
-inline void nms_greedy(const double* b, int64_t n, double thresh, int64_t max_keep, std::vector<int64_t>& keep) {
+// T = double: the reference's float64 proposal arithmetic; T = float: bit-identical to the GPU
+// mask kernel's fp32 IoU (iou_plus1), i.e. the oracle of the device reducer's logic
+template <typename T>
+inline void nms_greedy(const T* b, int64_t n, double thresh, int64_t max_keep, std::vector<int64_t>& keep) {
   if (n <= 0) return;
-  std::vector<double> area(n);
-  for (int64_t i = 0; i < n; ++i) area[i] = (b[4 * i + 2] - b[4 * i] + 1.0) * (b[4 * i + 3] - b[4 * i + 1] + 1.0);
+  const T th = (T)thresh;
+  std::vector<T> area(n);
+  for (int64_t i = 0; i < n; ++i) area[i] = (b[4 * i + 2] - b[4 * i] + (T)1) * (b[4 * i + 3] - b[4 * i + 1] + (T)1);
   std::vector<uint8_t> removed(n, 0);
   for (int64_t i = 0; i < n; ++i) {
     if (removed[i]) continue;
     keep.push_back(i);
     if (max_keep > 0 && (int64_t)keep.size() >= max_keep) break;
-    const double x1 = b[4 * i], y1 = b[4 * i + 1], x2 = b[4 * i + 2], y2 = b[4 * i + 3];
+    const T x1 = b[4 * i], y1 = b[4 * i + 1], x2 = b[4 * i + 2], y2 = b[4 * i + 3];
     for (int64_t j = i + 1; j < n; ++j) {
       if (removed[j]) continue;
-      const double w = std::min(x2, b[4 * j + 2]) - std::max(x1, b[4 * j]) + 1.0;
-      const double h = std::min(y2, b[4 * j + 3]) - std::max(y1, b[4 * j + 1]) + 1.0;
-      if (w <= 0.0 || h <= 0.0) continue;
-      const double inter = w * h;
-      if (inter / (area[i] + area[j] - inter) > thresh) removed[j] = 1;
+      const T w = std::min(x2, b[4 * j + 2]) - std::max(x1, b[4 * j]) + (T)1;
+      const T h = std::min(y2, b[4 * j + 3]) - std::max(y1, b[4 * j + 1]) + (T)1;
+      if (w <= (T)0 || h <= (T)0) continue;
+      const T inter = w * h;
+      if (inter / (area[i] + area[j] - inter) > th) removed[j] = 1;
     }
   }
 }

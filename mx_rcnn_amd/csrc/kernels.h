@@ -131,7 +131,8 @@ void loss_combine(const LossTerms& t, float* out, int32_t* nonfinite, hipStream_
 // MXNet SGD semantics: g = clip(rescale*g, +-clip) (clip<=0: off); mom = mu*mom - lr*(g + wd*w); w += mom.
 // grad fp32 or bf16; lr read from device pointer; optional bf16 shadow copy of w.
 void sgd_momentum(float* w, float* mom, const void* grad, int grad_bf16, int64_t n, const float* lr,
-                  float momentum, float wd, float rescale, float clip, uint16_t* w_bf16, hipStream_t st);
+                  float momentum, float wd, float rescale, float clip, uint16_t* w_bf16, hipStream_t st,
+                  int64_t x2_plane = 0);  // x2_plane > 0: w_bf16 is an x2 hi / lo pair, lo x2_plane elements on
 
 // ---- frozen BN + ReLU (bn_act.hip) -----------------------------------------
 // NHWC x (M rows, C channels) bf16/fp32; y = relu((x-mean)*rsqrt(var+eps)*gamma + beta).
@@ -210,6 +211,15 @@ struct ConvEpi {
   // bnb_part[bnb_row0 + t][0 / 1][:] (LDS-epilogue kernels, no split-K)
   float* bnb_part = nullptr;
   int bnb_row0 = 0;
+  // fp32-class mode (common.h "x2"): every 16-bit operand and output is a hi / lo bf16 plane pair.
+  // The main loop runs three K phases (A_hi B_hi, A_hi B_lo, A_lo B_hi) with the lo planes reached
+  // through plane byte offsets; the epilogue reads pairs and stores pairs (buffer kernels 22 / 23
+  // and the grouped launch only)
+  int x2 = 0;
+  uint32_t x2_pa = 0, x2_pb = 0;  // lo-plane offsets of the A (activation) / B (filter) operands, bytes
+  int64_t x2_py = 0;              // lo-plane offset of y, y2, residual and bnb_x, elements
+  int64_t x2_pd = 0;              // lo-plane offset of dadd, elements
+  float* yf = nullptr;            // fp32 output instead of y (no y2): the x2 mode's prediction heads
 };
 // counter-based uniform in [0, 1) (Philox-4x32-10, key = (seed, 0x9E3779B9), counter = (e, s))
 float philox_uniform_host(uint32_t seed, uint64_t step, uint64_t e);
@@ -219,29 +229,30 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
                    int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int tile, int splits, float* slab,
                    hipStream_t st);
 // ---- training-mode BatchNorm (bn_train.hip) -----------------------------------------------
+// (x2 = 1: every bf16 (M, C) operand is an x2 hi / lo pair, lo plane M * C elements on)
 // x/y/dy/dx NHWC bf16 (M rows x C), C % 64 == 0.  fwd updates the running stats in place
 // (moving = momentum * moving + (1 - momentum) * batch, unbiased var) and saves mean / invstd.
 // workspace: bn_train_workspace_floats(M, C) floats.
 int bn_train_workspace_floats(int64_t M, int C);
 int bn_train_fwd(const uint16_t* x, int64_t M, int C, const float* gamma, const float* beta, float* rmean,
                  float* rvar, float momentum, float eps, int fix_gamma, int relu, uint16_t* y, float* save_mean,
-                 float* save_invstd, float* workspace, hipStream_t st, float* save_veps = nullptr);
+                 float* save_invstd, float* workspace, hipStream_t st, float* save_veps = nullptr, int x2 = 0);
 // the same normalisation from statistics partials produced elsewhere (a conv epilogue's
 // ConvEpi::st_part, nparts row tiles + the shift row).  save: [3][C] = mean, invstd, var + eps
 int bn_train_apply(const uint16_t* x, int64_t M, int C, const float* part, int nparts, const float* gamma,
                    const float* beta, float* rmean, float* rvar, float momentum, float eps, int fix_gamma, int relu,
-                   uint16_t* y, float* save, hipStream_t st);
+                   uint16_t* y, float* save, hipStream_t st, int x2 = 0);
 // BN-ReLU backward finish after a BN-backward conv epilogue wrote o = g * s and the partial rows
 // part[nparts][sum g | sum g * xhat][C] (ConvEpi::bnb_part): dx = o - s * (mean g + xhat *
 // mean(g xhat)) (+ dres); o may alias dx; dgamma / dbeta (nullable) += the folded sums.
 // gamma: the effective gamma (ones under fix_gamma)
 int bn_train_dx_apply(const uint16_t* o, const uint16_t* x, int64_t M, int C, const float* part, int nparts,
                       const float* gamma, const float* save, const uint16_t* dres, uint16_t* dx, float* dgamma,
-                      float* dbeta, hipStream_t st);
+                      float* dbeta, hipStream_t st, int x2 = 0);
 // dgamma/dbeta: written (accumulate = 0) or added to (accumulate = 1); may be null.
 int bn_train_bwd(const uint16_t* x, const uint16_t* dy, int64_t M, int C, const float* gamma, const float* beta,
                  const float* save_mean, const float* save_invstd, int fix_gamma, int relu, uint16_t* dx,
-                 float* dgamma, float* dbeta, int accumulate, float* workspace, hipStream_t st);
+                 float* dgamma, float* dbeta, int accumulate, float* workspace, hipStream_t st, int x2 = 0);
 
 // ---- pooling (pool.hip): NHWC bf16, C % 8 == 0 ------------------------------------------------
 // arg: one byte per output element, the winning tap (i * k + j) of its window
@@ -302,6 +313,13 @@ void conv_wt_flip_multi(const WtFlipEntry* entries, int n_entries, int total_til
 // dy (NB, Ho, Wo, Cout) bf16, x (NB, H, W, Cin) bf16 -> dw (Cout, KH, KW, Cin) bf16.
 // slab: splits * Cout * KH*KW*Cin floats.  Requires Cin % 64 == 0, Cout % 8 == 0.
 int conv_wgrad_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int* splits_out);
+// fp32-class (x2) weight gradient: dY / X are hi / lo plane pairs (lo planes pdy / px bytes after the
+// hi ones), the gradient dwf is fp32 (dw unused)
+struct WgradX2 {
+  int x2 = 0;
+  uint32_t pdy = 0, px = 0;
+  float* dwf = nullptr;
+};
 // Grouped launch (conv_igemm.hip): the stride-1 implicit-GEMM conv (x, w) -> y with epilogue `ep`
 // (64x64 buffer kernel, no split) AND the weight gradient (wg_*: as conv_wgrad) in ONE launch, plus
 // the wgrad split-K reduce when wg_splits > 1.  Returns 0, or -1 when a role's shape is unsupported.
@@ -310,12 +328,13 @@ int conv_dgrad_wgrad(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, 
                      const uint16_t* wg_x, uint16_t* dw, float* slab, int wg_NB, int wg_H, int wg_W, int wg_Cin,
                      int wg_Ho, int wg_Wo, int wg_Cout, int wg_KH, int wg_KW, int wg_stride, int wg_pad, int wg_splits,
                      int accumulate, hipStream_t st, int defer_reduce = 0, const float* prev_slab = nullptr,
-                     int prev_splits = 0, int64_t prev_n = 0, uint16_t* prev_dw = nullptr);
-// standalone split-K reduce of a deferred grouped weight gradient (accumulates into dw)
-void wgrad_reduce_run(const float* slab, int splits, int64_t n, uint16_t* dw, hipStream_t st);
+                     int prev_splits = 0, int64_t prev_n = 0, uint16_t* prev_dw = nullptr,
+                     const WgradX2& wx2 = WgradX2(), float* prev_dwf = nullptr);
+// standalone split-K reduce of a deferred grouped weight gradient (accumulates into dw, or dwf)
+void wgrad_reduce_run(const float* slab, int splits, int64_t n, uint16_t* dw, hipStream_t st, float* dwf = nullptr);
 int conv_wgrad(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab, int NB, int H, int W, int Cin,
                int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int splits, int accumulate,
-               hipStream_t st, int variant = 0);
+               hipStream_t st, int variant = 0, const WgradX2& x2 = WgradX2());
 
 // ---- small-head backward (head_bwd.hip) ---------------------------------------------------------
 // One or two heads y_h = X W_h^T (+b_h) over the same X (M, K) bf16, K % 64 == 0, dY_h (M, N_h):
@@ -337,6 +356,12 @@ struct HeadBwdArgs {
   int relu_mask = 0;
   int nheads = 1;
   int rs = 1;
+  // fp32-class mode: X / W / dX are x2 hi / lo pairs (X's and dX's lo planes M * K on, W_h's w_plane[h]
+  // on), dY is fp32 (dyf), dW fp32 (dwf); products hi*hi + hi*lo + lo*hi on the bf16 MFMA
+  int x2 = 0;
+  const float* dyf[2] = {nullptr, nullptr};
+  float* dwf[2] = {nullptr, nullptr};
+  int64_t w_plane[2] = {0, 0};
 };
 int head_bwd_splits(int M, int K, const int* N, int nheads);
 int head_bwd(const uint16_t* x, int M, int K, const HeadBwdArgs& a, hipStream_t st);

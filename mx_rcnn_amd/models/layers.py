@@ -31,6 +31,9 @@ class MxLayer(nn.Module):
 
 
 def _w(t, ref):
+    from ..ops import precision
+    if precision.x2_enabled():  # the fp32 parameter: the ops take its pair from the store
+        return t
     return t if t.dtype == ref.dtype else t.to(ref.dtype)
 
 

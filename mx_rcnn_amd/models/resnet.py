@@ -8,7 +8,7 @@ import os
 import torch
 import torch.nn as nn
 
-from ..ops.conv import igemm_eligible
+from ..ops.conv import igemm_eligible, weight_ok
 from ..ops.fused import conv_add, conv_add_bn_relu, conv_bn_relu, fused_unit
 from ..ops.head import fc_pair
 from ..ops.pool import global_avg_pool
@@ -61,7 +61,7 @@ class ResidualUnit(nn.Module):
         else:
             a, last = self.bn2(self.conv1(act1)), self.conv2
         sc = x if self.dim_match else self.sc(act1)
-        if fusion_enabled() and igemm_eligible(a, last.weight, last.stride, last.pad) and last.weight.dtype == a.dtype:
+        if fusion_enabled() and igemm_eligible(a, last.weight, last.stride, last.pad) and weight_ok(a, last.weight):
             return conv_add(a, last, sc)  # residual add in the conv epilogue (train-mode BN head units)
         return last(a) + sc
 
@@ -71,7 +71,7 @@ class ResidualUnit(nn.Module):
                 (not self.bottle_neck or _frozen(self.bn3))):
             return False
         c1 = self.conv1
-        return igemm_eligible(x, c1.weight, c1.stride, c1.pad) and c1.weight.dtype == x.dtype
+        return igemm_eligible(x, c1.weight, c1.stride, c1.pad) and weight_ok(x, c1.weight)
 
     def frozen_bns(self):
         return _frozen(self.bn1) and _frozen(self.bn2) and (not self.bottle_neck or _frozen(self.bn3))
@@ -84,15 +84,16 @@ class ResidualUnit(nn.Module):
             return False
         # forward-only units with large-M 1x1 convs (frozen stages 1-2) run faster on hipBLASLt
         needs_grad = torch.is_grad_enabled() and (x.requires_grad or any(p.requires_grad for p in self.parameters()))
-        if not needs_grad and not self.can_fuse(x):
+        from ..ops import precision
+        if not needs_grad and not self.can_fuse(x) and not precision.x2_enabled():
             return False
         if next_bn is not None and not (_frozen(next_bn) and next_bn.relu):
             return False
         convs = [self.conv1, self.conv2] + ([self.conv3] if self.bottle_neck else [])
-        if not all(c.weight.dtype == x.dtype and c.weight.shape[0] % 64 == 0 and c.weight.shape[1] % 64 == 0
+        if not all(weight_ok(x, c.weight) and c.weight.shape[0] % 64 == 0 and c.weight.shape[1] % 64 == 0
                    for c in convs):
             return False
-        if not self.dim_match and not (self.sc.weight.shape[0] % 64 == 0 and self.sc.weight.dtype == x.dtype):
+        if not self.dim_match and not (self.sc.weight.shape[0] % 64 == 0 and weight_ok(x, self.sc.weight)):
             return False
         return x.shape[1] % 64 == 0 and x.shape[1] % 8 == 0
 
@@ -112,7 +113,7 @@ class ResidualUnit(nn.Module):
         if not self.dim_match:
             convs.append(self.sc)  # the strided 1x1 projection reads act1 directly (no subsampled copy)
         return igemm_eligible(x, self.conv1.weight, self.conv1.stride, self.conv1.pad) and all(
-            c.weight.dtype == x.dtype and c.weight.shape[0] % 64 == 0 and c.weight.shape[1] % 64 == 0 for c in convs)
+            weight_ok(x, c.weight) and c.weight.shape[0] % 64 == 0 and c.weight.shape[1] % 64 == 0 for c in convs)
 
     def forward_fused(self, x, act1=None, next_bn=None):
         """-> (unit output, next unit's act1 or None).  act1: this unit's bn1(x) if already

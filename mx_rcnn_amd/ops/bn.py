@@ -7,6 +7,7 @@ parameters of global-stats BN trainable); the running statistics are constants.
 import torch
 
 from . import grad_sink
+from . import precision
 from ._ext import ext_available, need_ext
 
 
@@ -14,11 +15,12 @@ class _FrozenBnRelu(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, mean, var, eps, fix_gamma, relu):
         ctx.eps, ctx.fix_gamma, ctx.relu = eps, fix_gamma, relu
+        ctx.x2 = precision.is_pair(x)  # fp32-class pairs (ops/precision.py)
         if x.is_cuda:
             ext = need_ext()
             xc = x.contiguous(memory_format=torch.channels_last)
             y = ext.bn_relu_fwd(xc, gamma.float().contiguous(), beta.float().contiguous(), mean.float().contiguous(),
-                                var.float().contiguous(), float(eps), bool(fix_gamma), bool(relu))
+                                var.float().contiguous(), float(eps), bool(fix_gamma), bool(relu), ctx.x2)
             ctx.save_for_backward(xc, gamma, beta, mean, var)
             ctx.params = (gamma if gamma.is_leaf else None, beta if beta.is_leaf else None)
             return y
@@ -47,7 +49,7 @@ class _FrozenBnRelu(torch.autograd.Function):
             dx, dg, db = ext.bn_relu_bwd(x, dy.to(x.dtype), gamma.float().contiguous(), beta.float().contiguous(),
                                          mean.float().contiguous(), var.float().contiguous(), float(ctx.eps),
                                          bool(ctx.fix_gamma), bool(ctx.relu), bool(need_dx), bool(need_p),
-                                         tg if direct else None, tb if direct else None)
+                                         tg if direct else None, tb if direct else None, None, ctx.x2)
             dx = dx if need_dx else None
             if direct:  # accumulated straight into the flat gradient buffers
                 return dx, None, None, None, None, None, None, None
@@ -84,12 +86,13 @@ class _TrainBnRelu(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, gamma, beta, rmean, rvar, momentum, eps, fix_gamma, relu, parts=None):
         xc = x.contiguous(memory_format=torch.channels_last)
+        ctx.x2 = x2 = precision.is_pair(x)
         if parts is not None:  # statistics partials from the producing conv's epilogue
             y, save = need_ext().bn_train_apply(xc, parts, gamma, beta, rmean, rvar, float(momentum), float(eps),
-                                                bool(fix_gamma), bool(relu))
+                                                bool(fix_gamma), bool(relu), x2)
         else:
             y, save = need_ext().bn_train_fwd(xc, gamma, beta, rmean, rvar, float(momentum), float(eps),
-                                              bool(fix_gamma), bool(relu))
+                                              bool(fix_gamma), bool(relu), x2)
         sm, si = save[0], save[1]
         ctx.save_for_backward(xc, gamma, beta, sm, si)
         ctx.params = (gamma if gamma.is_leaf else None, beta if beta.is_leaf else None)
@@ -104,9 +107,10 @@ class _TrainBnRelu(torch.autograd.Function):
         tg = grad_sink.target(ctx.params[0]) if need_g else None
         tb = grad_sink.target(ctx.params[1]) if need_b else None
         direct = tg is not None and tb is not None and tg.dtype == torch.float32 and tb.dtype == torch.float32
-        dx, dg, db = need_ext().bn_train_bwd(x, dy, gamma, beta, sm, si, bool(ctx.fix_gamma), bool(ctx.relu),
+        dx, dg, db = need_ext().bn_train_bwd(x, dy.contiguous(memory_format=torch.channels_last), gamma, beta, sm,
+                                             si, bool(ctx.fix_gamma), bool(ctx.relu),
                                              bool(ctx.needs_input_grad[0]), tg if direct else None,
-                                             tb if direct else None)
+                                             tb if direct else None, ctx.x2)
         dx = dx if ctx.needs_input_grad[0] else None
         if direct:
             return dx, None, None, None, None, None, None, None, None, None

@@ -20,6 +20,7 @@ import torch
 import torch.nn.functional as F
 
 from . import grad_sink
+from . import precision
 from ._ext import need_ext
 
 LOWP = (torch.bfloat16, torch.float16)  # MFMA operand dtypes (fp16: the inference path)
@@ -95,7 +96,15 @@ def dgrad_weight(param, w):
     ent = _DGRAD_W.get(id(param)) if param is not None else None
     if ent is not None and ent[0] is param:
         return ent[1]
+    if precision.x2_enabled():  # the flipped fp32 filter as a pair
+        return precision.split(_flip_t(w.detach().float()))
     return _flip_t(w)
+
+
+def pair_args(wpair):
+    """x2 mode: a filter PAIR (2O, ...) -> (hi view, plane) for the kernels' w / w_plane."""
+    n = wpair.shape[0] // 2
+    return wpair[:n], wpair.numel() // 2
 
 
 def _flip_t(w):
@@ -145,7 +154,8 @@ def strided_dgrad(dy, wf, H, W, k, s, p, residual=None, bn=None, bn_eps=2e-5, bn
     (the classes in order, strided_dgrad_parts rows in all)."""
     ext = need_ext()
     N, O, Ho, Wo = dy.shape
-    I = wf.shape[0]
+    x2 = precision.x2_enabled()
+    I = wf.shape[0] // 2 if x2 else wf.shape[0]  # x2: wf is the flipped filter's pair
     dx = torch.empty((N, I, H, W), dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
     bwd = bnb_x is not None
     row0 = 0
@@ -167,10 +177,14 @@ def strided_dgrad(dy, wf, H, W, k, s, p, residual=None, bn=None, bn_eps=2e-5, bn
             # the taps of one parity are an arithmetic progression of step s: plain slicing (an index
             # list would be a host-to-device copy, illegal inside graph capture)
             sub = sub_filter(param, wf, th, tw, s)
+            wk = {}
+            if x2:
+                sub, wpl = pair_args(sub)
+                wk = dict(x2=True, w_plane=wpl)
             ext.conv_igemm_fwd(dy, sub, None, 1, -oh, False, 0, 0, residual, bn, bn_eps, bn_fix_gamma, True,
                                bnb_x, dadd, dgamma, dbeta, 0.0, 0, None, -ow, dx, [Hc, Wc, H, W, s, s, ph, pw],
-                               bnb_part=bnb_part, bnb_row0=row0)
-            row0 += (N * Hc * Wc + 63) // 64
+                               bnb_part=bnb_part, bnb_row0=row0, **wk)
+            row0 += ((N // 2 if x2 else N) * Hc * Wc + 63) // 64
     if bwd:
         return dx, dgamma, dbeta
     return dx
@@ -178,7 +192,8 @@ def strided_dgrad(dy, wf, H, W, k, s, p, residual=None, bn=None, bn_eps=2e-5, bn
 
 def _grouped_target(x, w, param, dy, stride, pad):
     """The flat-gradient target when this conv's data + weight gradient can run as ONE grouped
-    launch (csrc/hip/conv_igemm.hip conv_dgrad_wgrad: stride 1, same padding, bf16), else None."""
+    launch (csrc/hip/conv_igemm.hip conv_dgrad_wgrad: stride 1, same padding, bf16 / x2 pairs),
+    else None."""
     if os.environ.get('MXR_GROUPED_CONV', '1') == '0' or not wgrad_enabled():
         return None
     kh = w.shape[2]
@@ -186,7 +201,8 @@ def _grouped_target(x, w, param, dy, stride, pad):
             dy.dtype == torch.bfloat16 and w.shape[0] % 64 == 0 and w.shape[1] % 64 == 0):
         return None
     tgt = grad_sink.target(param)
-    if tgt is None or tgt.dtype != torch.bfloat16 or not tgt.is_contiguous(memory_format=torch.channels_last):
+    gdt = torch.float32 if precision.x2_enabled() else torch.bfloat16
+    if tgt is None or tgt.dtype != gdt or not tgt.is_contiguous(memory_format=torch.channels_last):
         return None
     return tgt
 
@@ -196,12 +212,18 @@ def conv_backward(x, w, param, dy, stride, pad, has_bias, need_x, need_w, need_b
     dw is None when it was accumulated straight into the parameter's flat gradient view."""
     kh = w.shape[2]
     dx = dw = db = None
+    x2 = precision.x2_enabled()
     tgt = _grouped_target(x, w, param, dy, stride, pad) if (need_x and need_w and x.is_cuda) else None
     if tgt is not None:
         x = x.contiguous(memory_format=torch.channels_last)
         dy = dy.contiguous(memory_format=torch.channels_last)
-        dx = need_ext().conv_dgrad_wgrad(dy, dgrad_weight(param, w), kh - 1 - pad, None, None, 0.0, False, None,
-                                         None, None, None, dy, x, kh, kh, 1, pad, tgt)[0]
+        wf = dgrad_weight(param, w)
+        wk = {}
+        if x2:
+            wf, wpl = pair_args(wf)
+            wk = dict(x2=True, w_plane=wpl)
+        dx = need_ext().conv_dgrad_wgrad(dy, wf, kh - 1 - pad, None, None, 0.0, False, None,
+                                         None, None, None, dy, x, kh, kh, 1, pad, tgt, **wk)[0]
         if has_bias and need_b:
             db = _bias_grad(dy, w, bparam)
         return dx, None, db
@@ -219,11 +241,17 @@ def conv_backward(x, w, param, dy, stride, pad, has_bias, need_x, need_w, need_b
             dw, db = _wgrad(x, w, param, dy, stride, pad, has_bias, need_w, need_b, bparam)
     if need_x:
         if stride == 1 and w.shape[0] % 64 == 0 and 2 * pad == kh - 1:
-            dx = need_ext().conv_igemm_fwd(dy, dgrad_weight(param, w), None, 1, kh - 1 - pad, False)[0]
+            wf = dgrad_weight(param, w)
+            wk = {}
+            if x2:
+                wf, wpl = pair_args(wf)
+                wk = dict(x2=True, w_plane=wpl)
+            dx = need_ext().conv_igemm_fwd(dy, wf, None, 1, kh - 1 - pad, False, **wk)[0]
         elif (stride > 1 and w.shape[0] % 64 == 0 and w.shape[1] % 8 == 0 and kh == w.shape[3] and
               strided_dgrad_ok(kh, stride, pad, x.shape[2], x.shape[3])):
             dx = strided_dgrad(dy, dgrad_weight(param, w), x.shape[2], x.shape[3], kh, stride, pad, param=param)
         else:
+            assert not x2, 'fp32 (x2) mode: no MFMA data gradient for this conv shape'
             dx = torch.ops.aten.convolution_backward(
                 dy, x, w, None, [stride] * 2, [pad] * 2, [1, 1], False, [0, 0], 1, [True, False, False])[0]
     if side is None:
@@ -240,25 +268,29 @@ def _bias_grad(dy, w, bparam):
     """Per-channel sum of dy (HIP two-pass column sum, accumulated straight into the bias's flat
     gradient view when it has one) -> db or None."""
     tb = grad_sink.target(bparam)
+    x2 = precision.x2_enabled()
     if tb is not None and tb.is_contiguous():
-        need_ext().chan_sum(dy, tb, True)
+        need_ext().chan_sum(dy, tb, True, x2)
         return None
-    db = torch.empty(w.shape[0], dtype=w.dtype, device=dy.device)
-    need_ext().chan_sum(dy, db, False)
+    db = torch.empty(w.shape[0], dtype=torch.float32 if x2 else w.dtype, device=dy.device)
+    need_ext().chan_sum(dy, db, False, x2)
     return db
 
 
 def _wgrad(x, w, param, dy, stride, pad, has_bias, need_w, need_b, bparam=None):
     dw = db = None
-    if need_w and wgrad_enabled() and w.shape[0] % 8 == 0:
+    x2 = precision.x2_enabled()
+    if need_w and (wgrad_enabled() or x2) and w.shape[0] % 8 == 0:
         tgt = grad_sink.target(param)
-        if tgt is not None and tgt.is_contiguous(memory_format=torch.channels_last):
-            need_ext().conv_wgrad(dy, x, w.shape[2], w.shape[3], stride, pad, 0, tgt)
+        if tgt is not None and tgt.is_contiguous(memory_format=torch.channels_last) and \
+                tgt.dtype == (torch.float32 if x2 else torch.bfloat16):
+            need_ext().conv_wgrad(dy, x, w.shape[2], w.shape[3], stride, pad, 0, tgt, x2=x2)
         else:
-            dw = need_ext().conv_wgrad(dy, x, w.shape[2], w.shape[3], stride, pad)
+            dw = need_ext().conv_wgrad(dy, x, w.shape[2], w.shape[3], stride, pad, x2=x2)
         if has_bias and need_b:
             db = _bias_grad(dy, w, bparam)
     elif need_w or (has_bias and need_b):
+        assert not x2, 'fp32 (x2) mode: no MFMA weight gradient for this conv shape'
         _, dw, db = torch.ops.aten.convolution_backward(
             dy, x, w, [w.shape[0]] if has_bias else None, [stride] * 2, [pad] * 2, [1, 1], False,
             [0, 0], 1, [False, bool(need_w), bool(has_bias and need_b)])
@@ -270,8 +302,13 @@ class _ConvIgemm(torch.autograd.Function):
     def forward(ctx, x, w, b, stride, pad, relu):
         ext = need_ext()
         x = x.contiguous(memory_format=torch.channels_last)
-        wc = w.contiguous(memory_format=torch.channels_last)
-        y = ext.conv_igemm_fwd(x, wc, b, stride, pad, relu)[0]
+        if precision.x2_enabled():  # x: a pair, w: the fp32 parameter (its pair from the store)
+            wc = w
+            wh, wpl = precision.weight_pair(w)
+            y = ext.conv_igemm_fwd(x, wh, b, stride, pad, relu, x2=True, w_plane=wpl)[0]
+        else:
+            wc = w.contiguous(memory_format=torch.channels_last)
+            y = ext.conv_igemm_fwd(x, wc, b, stride, pad, relu)[0]
         ctx.save_for_backward(x, wc, y if relu else None)
         ctx.param = w if w.is_leaf else None
         ctx.bparam = b if (b is not None and b.is_leaf) else None
@@ -282,18 +319,31 @@ class _ConvIgemm(torch.autograd.Function):
     def backward(ctx, dy):
         x, w, y = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
-        if ctx.relu:
+        if ctx.relu and precision.x2_enabled():
+            # the hi plane carries the sign (hi = RNE(v)): mask both planes by it
+            n = y.shape[0] // 2
+            m = y[:n] > 0
+            dy = dy * torch.cat([m, m], 0)
+        elif ctx.relu:
             dy = dy * (y > 0)
         dx, dw, db = conv_backward(x, w, ctx.param, dy, ctx.stride, ctx.pad, ctx.has_bias, ctx.needs_input_grad[0],
                                    ctx.needs_input_grad[1], ctx.needs_input_grad[2], ctx.bparam)
         return dx, dw, db, None, None, None
 
 
+def weight_ok(x, w):
+    """The filter dtype the MFMA path takes with activation ``x``: the activation dtype, or in the
+    fp32 (x2) mode the fp32 parameter (whose pair the store keeps)."""
+    if precision.x2_enabled():
+        return x.dtype == torch.bfloat16 and w.dtype == torch.float32
+    return w.dtype == x.dtype
+
+
 def igemm_eligible(x, w, stride=1, pad=0):
     """True when the MFMA implicit-GEMM kernel is the path conv2d would take for this conv."""
     k = w.shape[2]
-    if not (x.is_cuda and x.dtype in LOWP and w.dtype == x.dtype and x.shape[1] % 64 == 0 and
-            x.is_contiguous(memory_format=torch.channels_last) and igemm_enabled()):
+    if not (x.is_cuda and x.dtype in LOWP and weight_ok(x, w) and x.shape[1] % 64 == 0 and
+            x.is_contiguous(memory_format=torch.channels_last) and (igemm_enabled() or precision.x2_enabled())):
         return False
     if k == 1 and pad == 0 and stride != 1:
         return False
@@ -303,12 +353,13 @@ def igemm_eligible(x, w, stride=1, pad=0):
 def conv2d(x, w, b=None, stride=1, pad=0, relu=False):
     """Conv (+bias, +optional fused ReLU) on NCHW-logical / channels_last tensors."""
     k = w.shape[2]
-    if (x.is_cuda and x.dtype in LOWP and w.dtype == x.dtype and x.shape[1] % 64 == 0 and
+    if (x.is_cuda and x.dtype in LOWP and weight_ok(x, w) and x.shape[1] % 64 == 0 and
             x.is_contiguous(memory_format=torch.channels_last)):
         if k == 1 and pad == 0 and stride != 1:
             x = x[:, :, ::stride, ::stride].contiguous(memory_format=torch.channels_last)
             stride = 1
-        if igemm_enabled():
+        if igemm_enabled() or precision.x2_enabled():
             return _ConvIgemm.apply(x, w, b, int(stride), int(pad), bool(relu))
+    assert not precision.x2_enabled(), 'fp32 (x2) mode: conv shape without an MFMA path'
     y = F.conv2d(x, w, b, stride=stride, padding=pad)
     return F.relu(y, inplace=True) if relu else y

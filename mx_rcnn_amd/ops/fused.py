@@ -20,8 +20,32 @@ import os
 import torch
 
 from . import grad_sink
+from . import precision
 from ._ext import need_ext
-from .conv import conv_backward
+from .conv import conv_backward, pair_args
+
+
+def _wargs(w):
+    """(filter for the kernel, extra conv kwargs): in the fp32 (x2) mode the store's pair of the
+    fp32 parameter ``w``; otherwise ``w`` itself."""
+    if precision.x2_enabled():
+        wh, wpl = precision.weight_pair(w)
+        return wh, {'x2': True, 'w_plane': wpl}
+    return w, {}
+
+
+def _dargs(wf):
+    """The same for a flipped dgrad filter (a pair in the x2 mode)."""
+    if precision.x2_enabled():
+        wh, wpl = pair_args(wf)
+        return wh, {'x2': True, 'w_plane': wpl}
+    return wf, {}
+
+
+def _rows(t):
+    """Logical rows (N*H*W) of an activation (pairs: half the tensor)."""
+    n = t.numel() // t.shape[1]
+    return n // 2 if precision.x2_enabled() else n
 
 
 def _bn_args(bn):
@@ -41,7 +65,7 @@ def _bn_backward(ctx, y, d_act, gamma, beta, mean, var, gi, dres=None):
     dy, dg, db = need_ext().bn_relu_bwd(y, d_act, gamma.float().contiguous(), beta.float().contiguous(),
                                        mean.float().contiguous(), var.float().contiguous(), float(ctx.eps),
                                        bool(ctx.fix_gamma), True, True, bool(need_g or need_b),
-                                       tg if direct else None, tb if direct else None, dres)
+                                       tg if direct else None, tb if direct else None, dres, precision.x2_enabled())
     if direct:
         return dy, None, None
     dg = dg.to(gamma.dtype) if (need_g and dg is not None) else None
@@ -53,8 +77,9 @@ class _ConvBnRelu(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, gamma, beta, mean, var, stride, pad, eps, fix_gamma):
         x = x.contiguous(memory_format=torch.channels_last)
-        y, a = need_ext().conv_igemm_fwd(x, w, None, stride, pad, False, 0, 0, None, [gamma, beta, mean, var],
-                                         eps, fix_gamma, True)
+        wk, kw = _wargs(w)
+        y, a = need_ext().conv_igemm_fwd(x, wk, None, stride, pad, False, 0, 0, None, [gamma, beta, mean, var],
+                                         eps, fix_gamma, True, **kw)
         ctx.save_for_backward(x, w, y, gamma, beta, mean, var)
         ctx.param = w if w.is_leaf else None
         ctx.bn_params = (gamma if gamma.is_leaf else None, beta if beta.is_leaf else None)
@@ -75,7 +100,8 @@ class _ConvAdd(torch.autograd.Function):
     def forward(ctx, x, w, res, stride, pad):
         x = x.contiguous(memory_format=torch.channels_last)
         res = res.contiguous(memory_format=torch.channels_last)
-        y = need_ext().conv_igemm_fwd(x, w, None, stride, pad, False, 0, 0, res)[0]
+        wk, kw = _wargs(w)
+        y = need_ext().conv_igemm_fwd(x, wk, None, stride, pad, False, 0, 0, res, **kw)[0]
         ctx.save_for_backward(x, w)
         ctx.param = w if w.is_leaf else None
         ctx.stride, ctx.pad = stride, pad
@@ -95,8 +121,9 @@ class _ConvAddBnRelu(torch.autograd.Function):
     def forward(ctx, x, w, res, gamma, beta, mean, var, stride, pad, eps, fix_gamma):
         x = x.contiguous(memory_format=torch.channels_last)
         res = res.contiguous(memory_format=torch.channels_last)
-        y, a = need_ext().conv_igemm_fwd(x, w, None, stride, pad, False, 0, 0, res, [gamma, beta, mean, var],
-                                         eps, fix_gamma, True)
+        wk, kw = _wargs(w)
+        y, a = need_ext().conv_igemm_fwd(x, wk, None, stride, pad, False, 0, 0, res, [gamma, beta, mean, var],
+                                         eps, fix_gamma, True, **kw)
         ctx.save_for_backward(x, w, y, gamma, beta, mean, var)
         ctx.param = w if w.is_leaf else None
         ctx.bn_params = (gamma if gamma.is_leaf else None, beta if beta.is_leaf else None)
@@ -238,34 +265,37 @@ class _FusedUnitFn(torch.autograd.Function):
         the zero rows are the backward's column-sum accumulators."""
         ext = need_ext()
         x = _cl(x)
+        x2 = precision.x2_enabled()
 
         def norm(inp, parts, i):
             g, b, rm, rv = bnps[i]
             if parts is None:
-                return ext.bn_train_fwd(inp, g, b, rm, rv, spec.mom[i], spec.eps[i], spec.fix[i], True)
-            return ext.bn_train_apply(inp, parts, g, b, rm, rv, spec.mom[i], spec.eps[i], spec.fix[i], True)
+                return ext.bn_train_fwd(inp, g, b, rm, rv, spec.mom[i], spec.eps[i], spec.fix[i], True, x2)
+            return ext.bn_train_apply(inp, parts, g, b, rm, rv, spec.mom[i], spec.eps[i], spec.fix[i], True, x2)
 
+        wa = [_wargs(w) for w in ws]
         act1, sv1 = norm(x, parts1, 0)
         s1 = 1 if spec.bottle else spec.stride
         p1 = 0 if spec.bottle else 1
-        y1, pt = ext.conv_igemm_fwd(act1, ws[0], None, s1, p1, False, stat_shift=bnps[1][2])
+        y1, pt = ext.conv_igemm_fwd(act1, wa[0][0], None, s1, p1, False, stat_shift=bnps[1][2], **wa[0][1])
         a2, sv2 = norm(y1, pt, 1)
         saves = [sv1, sv2]
         if spec.bottle:
-            y2, pt = ext.conv_igemm_fwd(a2, ws[1], None, spec.stride, 1, False, stat_shift=bnps[2][2])
+            y2, pt = ext.conv_igemm_fwd(a2, wa[1][0], None, spec.stride, 1, False, stat_shift=bnps[2][2], **wa[1][1])
             a3, sv3 = norm(y2, pt, 2)
             saves.append(sv3)
-            last_in, w_last = a3, ws[2]
+            last_in, w_last = a3, wa[2]
         else:
             y2, a3 = None, None
-            last_in, w_last = a2, ws[1]
-        res = x if spec.dim_match else ext.conv_igemm_fwd(act1, ws[-1], None, spec.stride, 0, False)[0]
+            last_in, w_last = a2, wa[1]
+        res = x if spec.dim_match else ext.conv_igemm_fwd(act1, wa[-1][0], None, spec.stride, 0, False,
+                                                          **wa[-1][1])[0]
         pl = 0 if spec.bottle else 1
         if nxt is not None:
-            out, parts_n = ext.conv_igemm_fwd(last_in, w_last, None, 1, pl, False, 0, 0, res,
-                                              stat_shift=nxt[2].float().contiguous())
+            out, parts_n = ext.conv_igemm_fwd(last_in, w_last[0], None, 1, pl, False, 0, 0, res,
+                                              stat_shift=nxt[2].float().contiguous(), **w_last[1])
         else:
-            out, parts_n = ext.conv_igemm_fwd(last_in, w_last, None, 1, pl, False, 0, 0, res)[0], None
+            out, parts_n = ext.conv_igemm_fwd(last_in, w_last[0], None, 1, pl, False, 0, 0, res, **w_last[1])[0], None
         ctx.spec = spec
         ctx.nconv = nconv
         ctx.set_materialize_grads(False)
@@ -294,31 +324,35 @@ class _FusedUnitFn(torch.autograd.Function):
         nxt = list(t[nconv + 4 * nb:nconv + 4 * nb + 4]) if spec.next_bn is not None else None
         x = _cl(x)
         bn1 = bnps[0]
+        x2 = precision.x2_enabled()
+        wa = [_wargs(w) for w in ws]
         if act1 is None:
-            act1 = ext.bn_relu_fwd(x, *[p.float().contiguous() for p in bn1], spec.eps[0], spec.fix[0], True)
+            act1 = ext.bn_relu_fwd(x, *[p.float().contiguous() for p in bn1], spec.eps[0], spec.fix[0], True, x2)
         # conv1 (stride 1 for bottleneck; 3x3 stride s for basic) -> bn2
         s1 = 1 if spec.bottle else spec.stride
         p1 = 0 if spec.bottle else 1
-        y1, a2 = ext.conv_igemm_fwd(act1, ws[0], None, s1, p1, False, 0, 0, None, bnps[1], spec.eps[1],
-                                    spec.fix[1], True)
+        y1, a2 = ext.conv_igemm_fwd(act1, wa[0][0], None, s1, p1, False, 0, 0, None, bnps[1], spec.eps[1],
+                                    spec.fix[1], True, **wa[0][1])
         if spec.bottle:
-            y2, a3 = ext.conv_igemm_fwd(a2, ws[1], None, spec.stride, 1, False, 0, 0, None, bnps[2], spec.eps[2],
-                                        spec.fix[2], True)
-            last_in, w_last = a3, ws[2]
+            y2, a3 = ext.conv_igemm_fwd(a2, wa[1][0], None, spec.stride, 1, False, 0, 0, None, bnps[2], spec.eps[2],
+                                        spec.fix[2], True, **wa[1][1])
+            last_in, w_last = a3, wa[2]
         else:
             y2, a3 = None, None
-            last_in, w_last = a2, ws[1]
+            last_in, w_last = a2, wa[1]
         sc_in = None
         if spec.dim_match:
             res = x
         else:
             # strided 1x1 projection read straight from act1 by the kernel (no subsampled copy)
-            res = ext.conv_igemm_fwd(act1, ws[-1], None, spec.stride, 0, False)[0]
+            res = ext.conv_igemm_fwd(act1, wa[-1][0], None, spec.stride, 0, False, **wa[-1][1])[0]
         if nxt is not None:
-            out, act1n = ext.conv_igemm_fwd(last_in, w_last, None, 1, 0 if spec.bottle else 1, False, 0, 0, res,
-                                            nxt, float(spec.next_bn.eps), bool(spec.next_bn.fix_gamma), True)
+            out, act1n = ext.conv_igemm_fwd(last_in, w_last[0], None, 1, 0 if spec.bottle else 1, False, 0, 0, res,
+                                            nxt, float(spec.next_bn.eps), bool(spec.next_bn.fix_gamma), True,
+                                            **w_last[1])
         else:
-            out = ext.conv_igemm_fwd(last_in, w_last, None, 1, 0 if spec.bottle else 1, False, 0, 0, res)[0]
+            out = ext.conv_igemm_fwd(last_in, w_last[0], None, 1, 0 if spec.bottle else 1, False, 0, 0, res,
+                                     **w_last[1])[0]
             act1n = None
         ctx.spec = spec
         ctx.nconv = nconv
@@ -356,6 +390,9 @@ class _FusedUnitFn(torch.autograd.Function):
         else:
             bwp, beps, bfix = bnps, spec.eps, spec.fix
 
+        x2 = precision.x2_enabled()
+        gdt = torch.float32 if x2 else torch.bfloat16  # weight-gradient dtype of the kernels
+
         def train_part(bn_x, nparts):
             return torch.empty(nparts * 2 * bn_x.shape[1], device=bn_x.device, dtype=torch.float32)
 
@@ -375,7 +412,7 @@ class _FusedUnitFn(torch.autograd.Function):
             if own_b:
                 tb = torch.zeros(C, device=o.device, dtype=torch.float32)
             dx = ext.bn_train_dx_apply(o, bn_x, saves[i], geff[i], part, nparts, dres, tg if ng else None,
-                                       tb if nbb else None)
+                                       tb if nbb else None, x2)
             if own_g:
                 grads[gi] = tg.to(bnps[i][0].dtype)
             if own_b:
@@ -413,10 +450,10 @@ class _FusedUnitFn(torch.autograd.Function):
                 side.wait_stream(main)
                 used_side[0] = True
             with torch.cuda.stream(side) if side is not None else _nullctx():
-                if tgt is not None and tgt.is_contiguous(memory_format=torch.channels_last):
-                    ext.conv_wgrad(dy, inp, k, k, stride, pad, 0, tgt)
+                if tgt is not None and tgt.is_contiguous(memory_format=torch.channels_last) and tgt.dtype == gdt:
+                    ext.conv_wgrad(dy, inp, k, k, stride, pad, 0, tgt, x2=x2)
                 else:
-                    grads[idx] = ext.conv_wgrad(dy, inp, k, k, stride, pad)
+                    grads[idx] = ext.conv_wgrad(dy, inp, k, k, stride, pad, x2=x2)
                     if side is not None:  # allocated on the side stream, consumed on the compute stream
                         grads[idx].record_stream(main)
 
@@ -450,7 +487,7 @@ class _FusedUnitFn(torch.autograd.Function):
             if wg is None or not grouped_enabled() or not need[wg[0]] or not wg[1].is_cuda:
                 return None
             tgt = grad_sink.target(ctx.params[wg[0]])
-            if tgt is None or not tgt.is_contiguous(memory_format=torch.channels_last) or tgt.dtype != torch.bfloat16:
+            if tgt is None or not tgt.is_contiguous(memory_format=torch.channels_last) or tgt.dtype != gdt:
                 return None
             return tgt
 
@@ -460,11 +497,11 @@ class _FusedUnitFn(torch.autograd.Function):
             (csrc/hip/conv_igemm.hip conv_dgrad_wgrad), otherwise on the side stream."""
             from .conv import dgrad_weight
             tg, tb, ret = bn_targets(bn_i)
-            wf = dgrad_weight(ctx.params[w_idx], ws[w_idx])
+            wf, wkw = _dargs(dgrad_weight(ctx.params[w_idx], ws[w_idx]))
             tgt = grouped_target(wg)
             part, nparts = None, 0
             if train:
-                nparts = (bn_x.numel() // bn_x.shape[1] + 63) // 64
+                nparts = (_rows(bn_x) + 63) // 64
                 part = train_part(bn_x, nparts)
             if tgt is not None and dy.dtype == torch.bfloat16 and wf.dtype == torch.bfloat16:
                 if tg is None and not train:  # statistics not needed: accumulate into scratch
@@ -475,13 +512,13 @@ class _FusedUnitFn(torch.autograd.Function):
                 prev = pending[0]
                 r = ext.conv_dgrad_wgrad(dy, wf, k - 1 - pad, None if train else dres, bwp[bn_i], beps[bn_i],
                                          bfix[bn_i], bn_x, dadd, tg, tb, wdy, winp, wk, wk, wstride, wpad, tgt, True,
-                                         prev[0] if prev else None, prev[1] if prev else None, part)
+                                         prev[0] if prev else None, prev[1] if prev else None, part, **wkw)
                 pending[0] = (r[3], tgt) if r[3].numel() > 0 else None
             else:
                 if wg is not None:
                     wgrad(*wg)
                 r = ext.conv_igemm_fwd(dy, wf, None, 1, k - 1 - pad, False, 0, 0, None if train else dres, bwp[bn_i],
-                                       beps[bn_i], bfix[bn_i], True, bn_x, dadd, tg, tb, bnb_part=part)
+                                       beps[bn_i], bfix[bn_i], True, bn_x, dadd, tg, tb, bnb_part=part, **wkw)
             finish_bn(bn_i, tg, tb, ret)
             return train_finish(bn_i, r[0], bn_x, dres, part, nparts) if train else r[0]
 
@@ -491,7 +528,7 @@ class _FusedUnitFn(torch.autograd.Function):
             tg, tb, ret = bn_targets(bn_i)
             part, nparts = None, 0
             if train:
-                nparts = strided_dgrad_parts(bn_x.shape[0], H, W, stride)
+                nparts = strided_dgrad_parts(bn_x.shape[0] // (2 if x2 else 1), H, W, stride)
                 part = train_part(bn_x, nparts)
             elif tg is None:  # statistics not needed: accumulate into scratch
                 C = bnps[bn_i][0].numel()
@@ -509,7 +546,7 @@ class _FusedUnitFn(torch.autograd.Function):
                 gi = nconv + 4 * bn_i
                 ng, nbb = need[gi] and not spec.fix[bn_i], need[gi + 1]
                 dx, dg, db = ext.bn_train_bwd(bn_x, dy_act, bnps[bn_i][0], bnps[bn_i][1], saves[bn_i][0],
-                                              saves[bn_i][1], spec.fix[bn_i], True, True)
+                                              saves[bn_i][1], spec.fix[bn_i], True, True, None, None, x2)
                 if ng:
                     grads[gi] = dg.to(bnps[bn_i][0].dtype)
                 if nbb:
@@ -518,7 +555,7 @@ class _FusedUnitFn(torch.autograd.Function):
             tg, tb, ret = bn_targets(bn_i)
             p = [q.float().contiguous() for q in bnps[bn_i]]
             dx, dg, db = ext.bn_relu_bwd(bn_x, dy_act, *p, spec.eps[bn_i], spec.fix[bn_i], True, True,
-                                         tg is not None, tg, tb, dres)
+                                         tg is not None, tg, tb, dres, x2)
             finish_bn(bn_i, tg, tb, ret)
             return dx
 
@@ -563,8 +600,8 @@ class _FusedUnitFn(torch.autograd.Function):
         if not spec.dim_match:
             wgrad(nconv - 1, d_out, act1, 1, s, 0)
             from .conv import dgrad_weight
-            d_sub = ext.conv_igemm_fwd(d_out, dgrad_weight(ctx.params[nconv - 1], ws[nconv - 1]), None, 1, 0,
-                                       False)[0]
+            wsc, wkw = _dargs(dgrad_weight(ctx.params[nconv - 1], ws[nconv - 1]))
+            d_sub = ext.conv_igemm_fwd(d_out, wsc, None, 1, 0, False, **wkw)[0]
             if s == 1 or (s1 == 1 and ws[0].shape[0] % 64 == 0 and
                           os.environ.get('MXR_SUB_DADD', '1') != '0'):
                 # stride s > 1: the stride-1 dgrad below adds d_sub at rows (i*s, j*s) itself

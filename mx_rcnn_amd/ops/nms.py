@@ -18,21 +18,23 @@ from ._ext import need_ext
 MAX_GPU_BOXES = 65536  # one bitmask pass: at most 1024 64-box blocks (keep list in LDS or, if larger, global)
 
 
-def _greedy_ref(boxes, n_valid, thresh, max_keep=None):
+def _greedy_ref(boxes, n_valid, thresh, max_keep=None, fp32=False):
     """boxes already score-sorted (P, 4); returns list of kept positions among the first n_valid.
     Runs the extension's C++ twin when it is built (CPU configuration), else the tensor loop
-    below (the oracle the twin is tested against)."""
+    below (the oracle the twin is tested against).  fp32=True: IoU in float32, bit-identical to
+    the GPU bitmask kernel (the default float64 can differ from it on exact-threshold ties)."""
     n = int(n_valid)
     if n == 0:
         return []
     from ._ext import ext_available
     if ext_available() and not boxes.is_cuda:
-        return need_ext().nms_cpu(boxes[:n], n, float(thresh), -1 if max_keep is None else int(max_keep)).tolist()
-    return _greedy_loop(boxes, n, thresh, max_keep)
+        return need_ext().nms_cpu(boxes[:n], n, float(thresh), -1 if max_keep is None else int(max_keep),
+                                  bool(fp32)).tolist()
+    return _greedy_loop(boxes, n, thresh, max_keep, fp32)
 
 
-def _greedy_loop(boxes, n, thresh, max_keep=None):
-    b = boxes[:n].double()
+def _greedy_loop(boxes, n, thresh, max_keep=None, fp32=False):
+    b = boxes[:n].float() if fp32 else boxes[:n].double()
     x1, y1, x2, y2 = b[:, 0], b[:, 1], b[:, 2], b[:, 3]
     areas = (x2 - x1 + 1) * (y2 - y1 + 1)
     removed = torch.zeros(n, dtype=torch.bool)

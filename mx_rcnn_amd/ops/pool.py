@@ -11,6 +11,7 @@ import os
 import torch
 import torch.nn.functional as F
 
+from . import precision
 from ._ext import need_ext
 
 
@@ -24,7 +25,8 @@ def _eligible(x):
 class _MaxPool(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, k, s, p):
-        y, arg = need_ext().maxpool_fwd(x, k, s, p)
+        ctx.x2 = x2 = precision.is_pair(x)  # fp32-class pairs (ops/precision.py)
+        y, arg = need_ext().maxpool_fwd(x, k, s, p, x2)
         ctx.save_for_backward(arg)
         ctx.geo = (x.shape[2], x.shape[3], k, s, p)
         return y
@@ -33,7 +35,7 @@ class _MaxPool(torch.autograd.Function):
     def backward(ctx, dy):
         arg, = ctx.saved_tensors
         H, W, k, s, p = ctx.geo
-        dx = need_ext().maxpool_bwd(dy.contiguous(memory_format=torch.channels_last), arg, H, W, k, s, p)
+        dx = need_ext().maxpool_bwd(dy.contiguous(memory_format=torch.channels_last), arg, H, W, k, s, p, ctx.x2)
         return dx, None, None, None
 
 
@@ -41,21 +43,22 @@ class _AvgPool(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x):
         ctx.hw = (x.shape[2], x.shape[3])
-        return need_ext().avgpool_fwd(x)
+        ctx.x2 = x2 = precision.is_pair(x)
+        return need_ext().avgpool_fwd(x, x2)
 
     @staticmethod
     def backward(ctx, dy):
-        return need_ext().avgpool_bwd(dy.contiguous(), *ctx.hw)
+        return need_ext().avgpool_bwd(dy.contiguous(), ctx.hw[0], ctx.hw[1], ctx.x2)
 
 
 def max_pool2d(x, k, s, p=0):
-    if _eligible(x):
+    if _eligible(x) or precision.is_pair(x):
         return _MaxPool.apply(x, int(k), int(s), int(p))
     return F.max_pool2d(x, kernel_size=k, stride=s, padding=p)
 
 
 def global_avg_pool(x):
     """(N, C, H, W) -> (N, C)."""
-    if _eligible(x):
+    if _eligible(x) or precision.is_pair(x):
         return _AvgPool.apply(x)
     return torch.mean(x, dim=(2, 3))

@@ -7,6 +7,7 @@ import math
 import numpy as np
 import torch
 
+from . import precision
 from ._ext import ext_available, need_ext
 
 
@@ -63,9 +64,13 @@ class _RoIPool(torch.autograd.Function):
         B, C, H, W = feat.shape
         ctx.grad_add = grad_add
         rois = rois.float().contiguous()
+        ctx.x2 = x2 = precision.is_pair(feat)
+        if x2:
+            B = B // 2  # (2B, C, H, W) pair
         if feat.is_cuda:
             ext = need_ext()
-            out, arg = ext.roi_pool_fwd(feat.contiguous(memory_format=torch.channels_last), rois, PH, PW, float(scale))
+            out, arg = ext.roi_pool_fwd(feat.contiguous(memory_format=torch.channels_last), rois, PH, PW, float(scale),
+                                        x2)
         else:
             if ext_available():  # C++ twin (the loop reference below is the test oracle)
                 out, arg = need_ext().roi_pool_fwd_cpu(feat, rois, PH, PW, float(scale))
@@ -85,7 +90,7 @@ class _RoIPool(torch.autograd.Function):
             ext = need_ext()
             if ga is not None:
                 ga = ga.to(gout.dtype).contiguous(memory_format=torch.channels_last)
-            gin = ext.roi_pool_bwd(gout, arg, rois, B, H, W, ga)
+            gin = ext.roi_pool_bwd(gout.contiguous(memory_format=torch.channels_last), arg, rois, B, H, W, ga, ctx.x2)
             ga = None  # added in the kernel
         elif ext_available():  # C++ twin: channel-parallel scatter, deterministic sum order
             gin = need_ext().roi_pool_bwd_cpu(gout, arg, rois, B, H, W).to(gout.dtype)

@@ -18,6 +18,7 @@ import os
 import torch
 import torch.nn.functional as F
 
+from . import precision
 from ._ext import need_ext
 
 
@@ -25,11 +26,13 @@ _PACKED = {}
 
 
 def _packed_filter(w, dtype):
+    """dtype torch.float32: the fp32-class mode's (128, KP) bf16 pair of the packed filter."""
     key = (id(w), dtype)
     ver = (w.data_ptr(), w._version, tuple(w.shape))
     hit = _PACKED.get(key)
     if hit is None or hit[0] != ver:
-        hit = (ver, pack_filter(w, dtype))
+        pf = precision.split(pack_filter(w, torch.float32)) if dtype == torch.float32 else pack_filter(w, dtype)
+        hit = (ver, pf)
         _PACKED[key] = hit
     return hit[1]
 
@@ -38,7 +41,8 @@ def stem_fusable(x, *params):
     """True when the fused stem kernel can replace the unfused layers for input ``x``."""
     if os.environ.get('MXR_STEM', '1') == '0':
         return False
-    if not (x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and x.dim() == 4 and x.shape[1] == 3):
+    ok_dtype = (torch.float32,) if precision.x2_enabled() else (torch.bfloat16, torch.float16)
+    if not (x.is_cuda and x.dtype in ok_dtype and x.dim() == 4 and x.shape[1] == 3):
         return False
     if torch.is_grad_enabled() and (x.requires_grad or any(p is not None and p.requires_grad for p in params)):
         return False
@@ -72,7 +76,8 @@ def _bn_args(bn):
 
 
 def stem_conv(x, weight, stride, pad, in_bn=None, out_bn=None, bias=None, relu=True):
-    """relu?(conv(in_bn(x), weight) -> out_bn or + bias), x (N,3,H,W) channels_last 16-bit."""
+    """relu?(conv(in_bn(x), weight) -> out_bn or + bias), x (N,3,H,W) channels_last 16-bit (or the fp32
+    image in the fp32-class mode, whose output is a (2N, 64, Ho, Wo) pair)."""
     co, ci, kh, kw = weight.shape
     assert co == 64 and ci == 3, 'stem_conv: 3 -> 64 channels'
     wp = _packed_filter(weight, x.dtype)

@@ -19,7 +19,29 @@ def get_world_size():
     return dist.get_world_size() if is_distributed() else 1
 
 
-def init_distributed(backend=None, timeout_s=600):
+# RCCL / torch ProcessGroup defaults for one 8 x MI355X node (set before the communicator is created;
+# a value already in the environment wins):
+# * NCCL_MIN_NCHANNELS=16: every GPU has 7 point-to-point xGMI links (~153 GB/s each); one RCCL
+#   channel drives one ring, i.e. one link per hop.  The gradient buckets are 4-25 MB all-reduces
+#   (parallel/reducer.py), large enough to be bandwidth-bound, so at least two channels per link
+#   keep all 7 links busy; each channel costs one workgroup (16 of 256 CUs) that the overlapped
+#   backward kernels lose while a collective runs.
+# * TORCH_NCCL_ASYNC_ERROR_HANDLING=1: a failed or timed-out collective aborts the communicator
+#   and raises on every rank (torchrun then tears the job down) instead of hanging the step.
+# * collective timeout MXR_COLL_TIMEOUT (default 600 s) for init_process_group.
+RCCL_DEFAULTS = {
+    'NCCL_MIN_NCHANNELS': '16',
+    'TORCH_NCCL_ASYNC_ERROR_HANDLING': '1',
+}
+
+
+def rccl_env():
+    """The effective RCCL settings (recorded in bench.py's JSON line)."""
+    keys = list(RCCL_DEFAULTS) + ['NCCL_MAX_NCHANNELS', 'NCCL_ALGO', 'NCCL_PROTO', 'MXR_COLL_TIMEOUT']
+    return {k: os.environ[k] for k in keys if k in os.environ}
+
+
+def init_distributed(backend=None, timeout_s=None):
     """Initialise from env if WORLD_SIZE > 1.  Returns (rank, world_size, local_rank, device)."""
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
@@ -35,6 +57,10 @@ def init_distributed(backend=None, timeout_s=600):
         kw = {}
         if backend == 'nccl':
             kw['device_id'] = device
+            for k, v in RCCL_DEFAULTS.items():
+                os.environ.setdefault(k, v)
+        if timeout_s is None:
+            timeout_s = int(os.environ.get('MXR_COLL_TIMEOUT', '600'))
         dist.init_process_group(backend=backend, rank=rank, world_size=world,
                                 timeout=datetime.timedelta(seconds=timeout_s), **kw)
     return rank, world, local_rank, device

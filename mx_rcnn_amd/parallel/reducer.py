@@ -73,7 +73,10 @@ class BucketReducer:
         # off by default: measured 2-3 % slower on 1-GPU ResNet-101 (scripts/gpu_sgd.sh A/B, 125-126
         # vs 128-129 img/s): the HBM-bound update steals bandwidth from the concurrent backward
         # convs for less than it hides (the whole update is ~0.16 ms)
-        self.sgd_capable = store.device.type == 'cuda' and os.environ.get('MXR_OVERLAP_SGD', '0') == '1'
+        # (not with the fp32-class x2 store: its shadow's lo plane is one group further, not sliceable
+        # per bucket)
+        self.sgd_capable = (store.device.type == 'cuda' and os.environ.get('MXR_OVERLAP_SGD', '0') == '1'
+                            and not getattr(store, 'x2', False))
         self.buckets = []
         self._param_bucket = {}
         self._sgd = None

@@ -32,14 +32,33 @@ def free_port(host='127.0.0.1'):
 
 
 def parse_gpus(spec):
-    """``'0,1,2'`` (reference device list) or ``'3'`` / ``3`` (a count) -> number of GPUs.
-    A single id ``'0'`` means one GPU, as in the reference."""
+    """Number of ranks for ``--gpus``: the length of the reference's device list (``'0,1,2'`` -> 3,
+    ``'3'`` -> 1: device 3), or an int count (bench.py)."""
+    return len(device_ids(spec))
+
+
+def device_ids(spec):
+    """The reference's ``--gpus`` device list (`train_end2end.py:168`): ``'0,1,2'`` -> [0, 1, 2],
+    ``'3'`` -> [3] (one device, the one named), ``''`` -> [0].  An int (bench.py's ``--gpus N``)
+    is a count: [0 .. N-1]."""
     if isinstance(spec, int):
-        return max(1, spec)
+        return list(range(max(1, spec)))
     spec = str(spec).strip()
-    if ',' in spec:
-        return len([s for s in spec.split(',') if s.strip() != ''])
-    return 1 if spec in ('', '0') else max(1, int(spec))
+    ids = [int(t) for t in spec.split(',') if t.strip() != '']
+    return ids or [0]
+
+
+def select_devices(spec):
+    """Make this job run on the devices ``spec`` names.  More than one: returns the
+    ``HIP_VISIBLE_DEVICES`` list for the rank children (rank r uses visible device r).  One:
+    restricts THIS process to it (before anything touches the GPU) and returns None."""
+    ids = device_ids(spec)
+    vis = ','.join(str(i) for i in ids)
+    if len(ids) > 1:
+        return vis
+    if ids != [0] and not launched_rank():
+        os.environ['HIP_VISIBLE_DEVICES'] = vis
+    return None
 
 
 def launched_rank():
@@ -103,14 +122,17 @@ def spawn_local(nprocs, argv, master_addr='127.0.0.1', master_port=None, extra_e
     return rc
 
 
-def maybe_spawn(n_gpus, script, argv):
+def maybe_spawn(n_gpus, script, argv, visible=None):
     """Entry-script helper.  ``n_gpus`` > 1 and not already a launched rank -> run the job
-    (``script argv``) as ``n_gpus`` children and ``sys.exit`` with its code.  Inside a launched
-    job, check that the launcher's world size agrees with ``--gpus``."""
+    (``script argv``) as ``n_gpus`` children and ``sys.exit`` with its code.  ``visible``: the
+    ``HIP_VISIBLE_DEVICES`` list the children get (the user's ``--gpus`` device ids), so rank r
+    runs on the r-th named device.  Inside a launched job, check that the launcher's world size
+    agrees with ``--gpus``."""
     if launched_rank():
         world = int(os.environ['WORLD_SIZE'])
         if n_gpus > 1 and world != n_gpus:
             raise SystemExit('--gpus %d but the launcher started WORLD_SIZE=%d ranks' % (n_gpus, world))
         return
     if n_gpus > 1:
-        sys.exit(spawn_local(n_gpus, [script] + list(argv)))
+        extra = {'HIP_VISIBLE_DEVICES': visible} if visible else None
+        sys.exit(spawn_local(n_gpus, [script] + list(argv), extra_env=extra))

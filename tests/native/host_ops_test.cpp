@@ -111,7 +111,7 @@ void test_nms() {
     if (cap > 0) CHECK((int64_t)k1.size() <= cap, "nms cap exceeded");
   }
   std::vector<int64_t> k;
-  mxr::host::nms_greedy(nullptr, 0, 0.7, -1, k);
+  mxr::host::nms_greedy<float>(nullptr, 0, 0.7, -1, k);
   CHECK(k.empty(), "nms n=0");
   const double one[4] = {1, 2, 3, 4};
   mxr::host::nms_greedy(one, 1, 0.7, -1, k);

@@ -351,3 +351,29 @@ def test_bench_alternate_stage_modes_two_ranks(tmp_path, mode):
     assert rec['metric'] == 'imgs/sec alternate-stage %s train resnet18' % mode
     assert rec['n_gpus'] == 2 and rec['config']['train_mode'] == mode
     assert all(math.isfinite(v) for v in rec['config']['objective_first_last'])
+
+
+def test_gpus_names_devices_like_the_reference(monkeypatch):
+    """--gpus is a device list as in the reference (train_end2end.py:168): '2,3' runs two ranks
+    on GPUs 2 and 3 (HIP_VISIBLE_DEVICES for the children), '3' one process on GPU 3."""
+    from mx_rcnn_amd.parallel import spawn
+    for k in ('RANK', 'WORLD_SIZE', 'HIP_VISIBLE_DEVICES'):
+        monkeypatch.delenv(k, raising=False)
+    assert spawn.device_ids('2,3') == [2, 3] and spawn.device_ids('3') == [3] and spawn.device_ids(4) == [0, 1, 2, 3]
+    assert spawn.parse_gpus('2,3') == 2 and spawn.parse_gpus('0') == 1
+    assert spawn.select_devices('2,3') == '2,3'
+    assert 'HIP_VISIBLE_DEVICES' not in os.environ
+    assert spawn.select_devices('0') is None and 'HIP_VISIBLE_DEVICES' not in os.environ
+    assert spawn.select_devices('3') is None
+    assert os.environ['HIP_VISIBLE_DEVICES'] == '3'
+
+
+def test_capture_sync_key_ignores_uneven_slices():
+    """an uneven work_load_list gives ranks different batch sizes; the cross-rank
+    capture check must compare only the slice-independent dims (module.sync_key)."""
+    from mx_rcnn_amd.core.module import sync_key
+    k1 = (('data', (1, 3, 608, 1024)), ('gt_boxes', (1, 20, 5)), ('im_info', (1, 3)))
+    k3 = (('data', (3, 3, 608, 1024)), ('gt_boxes', (3, 20, 5)), ('im_info', (3, 3)))
+    assert k1 != k3 and sync_key(k1) == sync_key(k3)
+    k_other = (('data', (1, 3, 600, 1024)), ('gt_boxes', (1, 20, 5)), ('im_info', (1, 3)))
+    assert sync_key(k_other) != sync_key(k1)

@@ -1,0 +1,303 @@
+"""fp32-class ("x2") kernels: every MFMA operand as a bf16 hi / lo pair, products as three MFMAs
+with fp32 accumulation (ops/precision.py).  Each kernel is checked against a plain PyTorch fp32
+computation of the same op on the SAME fp32 inputs: the pair representation keeps 16 significant
+bits (relative error <= 2^-17 per stored value), so results must agree to ~1e-5 relative -- four
+orders of magnitude tighter than the bf16 kernels' tolerances.
+
+The CPU tests cover the pair helpers; the kernel tests run on the GPU.
+"""
+import pytest
+import torch
+import torch.nn.functional as F
+
+from mx_rcnn_amd.ops import precision
+
+TOL = 2e-5  # relative (to the output's max magnitude)
+
+
+def _err(a, b):
+    a, b = a.float().cpu(), b.float().cpu()
+    return float((a - b).abs().max() / b.abs().max().clamp_min(1e-20))
+
+
+def test_split_join_roundtrip_cpu():
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(3, 8, 5, 7, generator=g) * 100
+    p = precision.split(x)
+    assert p.dtype == torch.bfloat16 and p.shape == (6, 8, 5, 7)
+    j = precision.join(p)
+    rel = ((j - x).abs() / x.abs().clamp_min(1e-30)).max()
+    assert float(rel) <= 2.0 ** -16, float(rel)
+    xc = x.contiguous(memory_format=torch.channels_last)
+    pc = precision.split(xc)
+    assert pc.is_contiguous(memory_format=torch.channels_last)
+    assert torch.equal(precision.join(pc), j)
+
+
+def test_x2_mode_switch_cpu():
+    assert not precision.x2_enabled()
+    with precision.x2_mode(True):
+        assert precision.x2_enabled()
+        assert precision.is_pair(torch.zeros(2, dtype=torch.bfloat16))
+        assert not precision.is_pair(torch.zeros(2))
+    assert not precision.x2_enabled()
+
+
+def test_weight_pair_cache_cpu():
+    w = torch.nn.Parameter(torch.randn(64, 32, 3, 3).contiguous(memory_format=torch.channels_last))
+    hi, pl = precision.weight_pair(w)
+    assert hi.shape == (64, 32, 3, 3) and pl == w.numel()
+    assert hi.is_contiguous(memory_format=torch.channels_last)
+    full = hi.reshape(-1)  # noqa: F841  (the hi view is a real tensor)
+    with torch.no_grad():
+        w.mul_(2)
+    hi2, _ = precision.weight_pair(w)
+    assert not torch.equal(hi.float(), hi2.float())  # rebuilt after the version bump
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last) if t.dim() == 4 else t.contiguous()
+
+
+def _pair(t, dev):
+    return _cl(precision.split(_cl(t.to(dev))))
+
+
+def _unpair(p):
+    return precision.join(p)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('k,stride,pad,N,C,H,W,O', [
+    (1, 1, 0, 1, 64, 20, 30, 128),     # 1x1
+    (3, 1, 1, 1, 128, 17, 23, 64),     # 3x3 s1
+    (3, 2, 1, 2, 64, 21, 19, 64),      # 3x3 s2
+    (1, 1, 0, 1, 256, 6, 7, 64),       # small grid: split-K
+])
+def test_conv_fwd_x2_matches_fp32(cuda, k, stride, pad, N, C, H, W, O):
+    from mx_rcnn_amd.ops import need_ext
+    g = torch.Generator().manual_seed(k * 100 + C)
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(O, C, k, k, generator=g) * (2.0 / (C * k * k)) ** 0.5
+    b = torch.randn(O, generator=g)
+    ref = F.conv2d(x.double(), w.double(), b.double(), stride=stride, padding=pad)
+    wp = _pair(w, cuda)
+    y = need_ext().conv_igemm_fwd(_pair(x, cuda), wp[:O], b.to(cuda), stride, pad, False, x2=True,
+                                  w_plane=wp.numel() // 2)[0]
+    assert y.shape == (2 * N, O, ref.shape[2], ref.shape[3])
+    assert _err(_unpair(y), ref) <= TOL
+    # fp32 output (the prediction heads) and the frozen-BN + ReLU second output
+    yf = need_ext().conv_igemm_fwd(_pair(x, cuda), wp[:O], b.to(cuda), stride, pad, False, x2=True,
+                                   w_plane=wp.numel() // 2, out_f32=True)[0]
+    assert yf.dtype == torch.float32 and _err(yf, ref) <= TOL
+    gam, bet = torch.rand(O) + 0.5, torch.randn(O)
+    mu, var = torch.randn(O), torch.rand(O) + 0.5
+    bn = [t.to(cuda) for t in (gam, bet, mu, var)]
+    res = torch.randn(ref.shape, generator=g)
+    y1, y2 = need_ext().conv_igemm_fwd(_pair(x, cuda), wp[:O], None, stride, pad, False, 0, 0, _pair(res, cuda), bn,
+                                       2e-5, False, True, x2=True, w_plane=wp.numel() // 2)
+    r1 = ref - b.double().view(1, -1, 1, 1) + res.double()
+    r2 = torch.relu((r1 - mu.double().view(1, -1, 1, 1)) / torch.sqrt(var.double().view(1, -1, 1, 1) + 2e-5)
+                    * gam.double().view(1, -1, 1, 1) + bet.double().view(1, -1, 1, 1))
+    assert _err(_unpair(y1), r1) <= TOL
+    assert _err(_unpair(y2), r2) <= 4 * TOL
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('k,stride,pad', [(1, 1, 0), (3, 1, 1), (3, 2, 1)])
+def test_conv_wgrad_x2_matches_fp32(cuda, k, stride, pad):
+    from mx_rcnn_amd.ops import need_ext
+    g = torch.Generator().manual_seed(7 + k + stride)
+    N, C, H, W, O = 1, 64, 19, 26, 128
+    x = torch.randn(N, C, H, W, generator=g)
+    Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    dy = torch.randn(N, O, Ho, Wo, generator=g)
+    ref = torch.nn.grad.conv2d_weight(x.double(), (O, C, k, k), dy.double(), stride=stride, padding=pad)
+    dw = need_ext().conv_wgrad(_pair(dy, cuda), _pair(x, cuda), k, k, stride, pad, x2=True)
+    assert dw.dtype == torch.float32
+    assert _err(dw, ref) <= TOL
+    acc = _cl(torch.ones(O, C, k, k, device=cuda))
+    need_ext().conv_wgrad(_pair(dy, cuda), _pair(x, cuda), k, k, stride, pad, 0, acc, x2=True)
+    assert _err(acc - 1, ref) <= TOL
+
+
+@pytest.mark.gpu
+def test_grouped_dgrad_wgrad_x2_matches_fp32(cuda):
+    """The fused unit backward's grouped launch: dgrad with the frozen BN-ReLU backward epilogue
+    plus the weight gradient of another conv reading the same dY."""
+    from mx_rcnn_amd.ops import need_ext
+    from mx_rcnn_amd.ops.conv import _flip_t
+    g = torch.Generator().manual_seed(3)
+    N, C, H, W, O = 1, 64, 14, 18, 128
+    dy = torch.randn(N, O, H, W, generator=g)
+    w = torch.randn(O, C, 3, 3, generator=g) * 0.05
+    xbn = torch.randn(N, C, H, W, generator=g)  # the BN input (bnb_x)
+    gam, bet, mu, var = torch.rand(C) + 0.5, torch.randn(C) * 0.1, torch.randn(C) * 0.1, torch.rand(C) + 0.5
+    # reference: d(act) = conv_transpose(dy, w); g = d(act) * [bn(x) > 0]; d(x) = g * s
+    dact = torch.nn.grad.conv2d_input((N, C, H, W), w.double(), dy.double(), padding=1)
+    s = gam.double() / torch.sqrt(var.double() + 2e-5)
+    pre = (xbn.double() - mu.double().view(1, -1, 1, 1)) * s.view(1, -1, 1, 1) + bet.double().view(1, -1, 1, 1)
+    gm = dact * (pre > 0)
+    ref_dx = gm * s.view(1, -1, 1, 1)
+    ref_db = gm.sum((0, 2, 3))
+    # the wgrad role: the same dy against an input of its conv (a 1x1 here)
+    xin = torch.randn(N, 256, H, W, generator=g)
+    ref_dw = torch.nn.grad.conv2d_weight(xin.double(), (O, 256, 1, 1), dy.double())
+    wf = _pair(_flip_t(w), cuda)
+    dgm = torch.zeros(C, device=cuda)
+    dbt = torch.zeros(C, device=cuda)
+    wg = _cl(torch.zeros(O, 256, 1, 1, device=cuda))
+    bn = [t.to(cuda) for t in (gam, bet, mu, var)]
+    out = need_ext().conv_dgrad_wgrad(_pair(dy, cuda), wf[:C], 1, None, bn, 2e-5, False, _pair(xbn, cuda), None, dgm,
+                                      dbt, _pair(dy, cuda), _pair(xin, cuda), 1, 1, 1, 0, wg, x2=True,
+                                      w_plane=wf.numel() // 2)
+    assert _err(_unpair(out[0]), ref_dx) <= 4 * TOL
+    assert _err(dbt, ref_db) <= 4 * TOL
+    assert _err(wg, ref_dw) <= TOL
+
+
+@pytest.mark.gpu
+def test_elementwise_x2_kernels_match_fp32(cuda):
+    from mx_rcnn_amd.ops import need_ext
+    ext = need_ext()
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(2, 64, 17, 23, generator=g) * 3
+    C = 64
+    gam, bet, mu, var = torch.rand(C) + 0.5, torch.randn(C), torch.randn(C), torch.rand(C) + 0.5
+    bn = [t.to(cuda) for t in (gam, bet, mu, var)]
+    # frozen BN + ReLU
+    y = ext.bn_relu_fwd(_pair(x, cuda), *bn, 2e-5, False, True, True)
+    ref = torch.relu((x.double() - mu.double().view(1, -1, 1, 1)) / torch.sqrt(var.double().view(1, -1, 1, 1) + 2e-5)
+                     * gam.double().view(1, -1, 1, 1) + bet.double().view(1, -1, 1, 1))
+    assert _err(_unpair(y), ref) <= TOL
+    # max pool 3x3/2 pad 1 (values, winners) and its backward
+    ym, arg = ext.maxpool_fwd(_pair(x, cuda), 3, 2, 1, True)
+    refm = F.max_pool2d(x.double(), 3, 2, 1)
+    assert _err(_unpair(ym), refm) <= TOL
+    dym = torch.randn(refm.shape, generator=g)
+    xr = x.double().requires_grad_()
+    F.max_pool2d(xr, 3, 2, 1).backward(dym.double())
+    dxm = ext.maxpool_bwd(_pair(dym, cuda), arg, 17, 23, 3, 2, 1, True)
+    assert _err(_unpair(dxm), xr.grad) <= TOL
+    # global average pool and its backward
+    ya = ext.avgpool_fwd(_pair(x, cuda), True)
+    assert _err(_unpair(ya), x.double().mean((2, 3))) <= TOL
+    dya = torch.randn(2, C, generator=g)
+    dxa = ext.avgpool_bwd(_pair(dya, cuda).contiguous(), 17, 23, True)
+    assert _err(_unpair(dxa), (dya.double() / (17 * 23)).view(2, C, 1, 1).expand(2, C, 17, 23)) <= TOL
+    # channel sum (conv bias gradient)
+    out = torch.zeros(C, device=cuda)
+    ext.chan_sum(_pair(x, cuda), out, False, True)
+    assert _err(out, x.double().sum((0, 2, 3))) <= TOL
+
+
+@pytest.mark.gpu
+def test_bn_train_x2_matches_fp32(cuda):
+    from mx_rcnn_amd.ops import need_ext
+    ext = need_ext()
+    g = torch.Generator().manual_seed(12)
+    N, C, H, W = 16, 128, 7, 7
+    x = torch.randn(N, C, H, W, generator=g) * 2 + 0.5
+    gam, bet = torch.rand(C) + 0.5, torch.randn(C)
+    rm, rv = torch.zeros(C, device=cuda), torch.ones(C, device=cuda)
+    y, save = ext.bn_train_fwd(_pair(x, cuda), gam.to(cuda), bet.to(cuda), rm, rv, 0.9, 2e-5, False, True, True)
+    xd = x.double().requires_grad_()
+    mean = xd.mean((0, 2, 3), keepdim=True)
+    var = ((xd - mean) ** 2).mean((0, 2, 3), keepdim=True)
+    ref = torch.relu((xd - mean) / torch.sqrt(var + 2e-5) * gam.double().view(1, -1, 1, 1) + bet.double().view(1, -1, 1, 1))
+    assert _err(_unpair(y), ref.detach()) <= 4 * TOL
+    dy = torch.randn(N, C, H, W, generator=g)
+    ref.backward(dy.double())
+    dx, dg, db = ext.bn_train_bwd(_pair(x, cuda), _pair(dy, cuda), gam.to(cuda), bet.to(cuda), save[0], save[1],
+                                  False, True, True, None, None, True)
+    assert _err(_unpair(dx), xd.grad) <= 8 * TOL
+
+
+@pytest.mark.gpu
+def test_roi_pool_x2_matches_fp32(cuda):
+    from mx_rcnn_amd.ops import need_ext
+    from mx_rcnn_amd.ops.roi_pool import roi_pool_ref
+    ext = need_ext()
+    g = torch.Generator().manual_seed(13)
+    feat = torch.randn(1, 64, 30, 40, generator=g)
+    R = 32
+    xy = torch.rand(R, 2, generator=g) * 300
+    wh = torch.rand(R, 2, generator=g) * 200 + 16
+    rois = torch.cat([torch.zeros(R, 1), xy, xy + wh], 1)
+    out, arg = ext.roi_pool_fwd(_pair(feat, cuda), rois.to(cuda), 7, 7, 1 / 16, True)
+    ref, ref_arg = roi_pool_ref(feat, rois, 7, 7, 1 / 16)
+    assert _err(_unpair(out), ref) <= TOL
+    gout = torch.randn(R, 64, 7, 7, generator=g)
+    gadd = torch.randn(1, 64, 30, 40, generator=g)
+    gin = ext.roi_pool_bwd(_pair(gout, cuda), arg, rois.to(cuda), 1, 30, 40, _pair(gadd, cuda), True)
+    refg = gadd.double().clone().reshape(64, -1)
+    a = ref_arg.reshape(R, 64, -1).long()
+    gg = gout.double().reshape(R, 64, -1)
+    for r in range(R):
+        m = a[r] >= 0
+        refg.view(-1).index_add_(0, (torch.arange(64)[:, None] * 1200 + a[r].clamp_min(0))[m], gg[r][m])
+    assert _err(_unpair(gin), refg.view(1, 64, 30, 40)) <= TOL
+
+
+@pytest.mark.gpu
+def test_head_bwd_x2_matches_fp32(cuda):
+    from mx_rcnn_amd.ops import need_ext
+    g = torch.Generator().manual_seed(14)
+    M, K = 300, 512
+    x = torch.relu(torch.randn(M, K, generator=g))
+    ws = [torch.randn(24, K, generator=g) * 0.02, torch.randn(48, K, generator=g) * 0.02]
+    dys = [torch.randn(M, 24, generator=g), torch.randn(M, 48, generator=g)]
+    wps = [precision.split(w.to(cuda)) for w in ws]
+    dws = [torch.zeros(w.shape, device=cuda) for w in ws]
+    dbs = [torch.zeros(w.shape[0], device=cuda) for w in ws]
+    dx = need_ext().head_bwd(precision.split(x.to(cuda)), [d.to(cuda) for d in dys], [p[:p.shape[0] // 2] for p in wps],
+                             dws, [False, False], dbs, [False, False], True, True, True,
+                             [p.numel() // 2 for p in wps])
+    ref_dx = (dys[0].double() @ ws[0].double() + dys[1].double() @ ws[1].double()) * (x > 0)
+    assert _err(_unpair(dx), ref_dx) <= TOL
+    for h in range(2):
+        assert _err(dws[h], dys[h].double().t() @ x.double()) <= TOL
+        assert _err(dbs[h], dys[h].double().sum(0)) <= TOL
+
+
+@pytest.mark.gpu
+def test_stem_x2_matches_fp32(cuda):
+    from mx_rcnn_amd.ops.stem import stem_conv
+    from mx_rcnn_amd.models.layers import BatchNorm
+    g = torch.Generator().manual_seed(15)
+    x = torch.randn(1, 3, 64, 96, generator=g) * 50
+    w = torch.randn(64, 3, 7, 7, generator=g) * 0.05
+    bn_in = BatchNorm('bn_data', 3, fix_gamma=True, relu=False)
+    bn_out = BatchNorm('bn0', 64)
+    with torch.no_grad():
+        bn_in.moving_mean.copy_(torch.randn(3)); bn_in.moving_var.copy_(torch.rand(3) * 100 + 50)
+        bn_out.moving_mean.copy_(torch.randn(64)); bn_out.moving_var.copy_(torch.rand(64) + 0.5)
+        bn_out.gamma.copy_(torch.rand(64) + 0.5); bn_out.beta.copy_(torch.randn(64))
+    bn_in, bn_out = bn_in.to(cuda), bn_out.to(cuda)
+    with precision.x2_mode(True):
+        y = stem_conv(_cl(x.to(cuda)), w.to(cuda), 2, 3, in_bn=bn_in, out_bn=bn_out, relu=True)
+    xs = (x.double() - bn_in.moving_mean.cpu().double().view(1, -1, 1, 1)) / torch.sqrt(
+        bn_in.moving_var.cpu().double().view(1, -1, 1, 1) + bn_in.eps)
+    ref = F.conv2d(xs, w.double(), stride=2, padding=3)
+    s = bn_out.gamma.detach().cpu().double() / torch.sqrt(bn_out.moving_var.cpu().double() + bn_out.eps)
+    ref = torch.relu((ref - bn_out.moving_mean.cpu().double().view(1, -1, 1, 1)) * s.view(1, -1, 1, 1)
+                     + bn_out.beta.detach().cpu().double().view(1, -1, 1, 1))
+    assert y.shape == (2, 64, 32, 48)
+    assert _err(_unpair(y), ref) <= 4 * TOL
+
+
+@pytest.mark.gpu
+def test_sgd_x2_shadow(cuda):
+    from mx_rcnn_amd.ops import need_ext
+    g = torch.Generator().manual_seed(16)
+    n = 1000
+    w = torch.randn(n, generator=g).to(cuda)
+    mom = torch.zeros(n, device=cuda)
+    grad = torch.randn(n, generator=g).to(cuda)
+    sh = torch.zeros(2 * n, dtype=torch.bfloat16, device=cuda)
+    lr = torch.full((1,), 0.1, device=cuda)
+    w0 = w.clone()
+    need_ext().sgd_momentum(w, mom, grad, lr, 0.9, 0.0, 1.0, -1.0, sh)
+    assert torch.allclose(w, w0 - 0.1 * grad)
+    j = sh[:n].float() + sh[n:].float()
+    assert float(((j - w).abs() / w.abs().clamp_min(1e-30)).max()) <= 2.0 ** -16

@@ -152,11 +152,16 @@ class FlatParamStore:
         from ..ops._ext import need_ext
         ext = need_ext()
         srcs, dsts = [], []
+        # stride-1 data gradients (and the FC's) read the forward filter transposed in-kernel
+        # (ops/conv.py dgrad_args): only the strided k x k convs' parity sub-filters need the copy
+        bt = conv_ops.dgrad_bt_enabled()
         for g in self.groups:
             if g.shadow is None:
                 continue
             for (n, m, attr, numel, shape, cl), off in zip(g.entries, g.offsets):
                 p = self.params[n]
+                if bt and not (len(shape) == 4 and shape[2] > 1 and int(getattr(m, 'stride', 1)) > 1):
+                    continue
                 if g.x2:
                     self._x2_dgrad_entry(g, p, off, numel, shape, cl, srcs, dsts)
                     continue

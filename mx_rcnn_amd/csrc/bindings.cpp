@@ -211,6 +211,53 @@ std::vector<Tensor> anchor_sample(const Tensor& label_pre, const Tensor& targets
   return {label, bt, iw, ow, meta};
 }
 
+// Anchor assignment + subsampling + reference-layout outputs in four grid-wide launches (assign
+// pass 1, pass 2 with the key histograms, mark with the last-workgroup boundary ranking, output):
+// the same result as anchor_target_assign + anchor_sample, without the one-workgroup pass.
+std::vector<Tensor> anchor_target_fused(const Tensor& base_anchors, int64_t H, int64_t W, double feat_stride,
+                                        const Tensor& im_info, int64_t allowed_border, const Tensor& gt,
+                                        const Tensor& n_gt, double neg_thresh, double pos_thresh, bool clobber,
+                                        const Tensor& keys, int64_t num_fg, int64_t batch, std::vector<double> inside_w,
+                                        double pos_weight) {
+  CHECK_DEV(base_anchors); CHECK_F32(base_anchors); CHECK_CONTIG(base_anchors);
+  CHECK_DEV(im_info); CHECK_F32(im_info); CHECK_CONTIG(im_info);
+  CHECK_DEV(gt); CHECK_F32(gt); CHECK_CONTIG(gt);
+  CHECK_DEV(n_gt); CHECK_I32(n_gt); CHECK_CONTIG(n_gt);
+  CHECK_DEV(keys); CHECK_F32(keys); CHECK_CONTIG(keys);
+  const int A = (int)base_anchors.size(0), B = (int)gt.size(0), G = (int)gt.size(1);
+  const int64_t N = H * W * A;
+  TORCH_CHECK(im_info.size(0) == B && n_gt.numel() == B && keys.numel() == B * N, "anchor_target_fused shapes");
+  TORCH_CHECK(inside_w.size() == 4, "inside_w: 4 values");
+  TORCH_CHECK(num_fg >= 0 && batch >= 0 && num_fg <= 1024 && batch <= 1024, "RPN batch must be <= 1024 anchors");
+  DevGuard g(gt.device());
+  auto o = gt.options();
+  // one zeroed workspace: gt_max (B, G) | key histograms (B, 2, bins) | mark workspace
+  const int64_t n_gm = (int64_t)B * std::max(G, 1), n_h = (int64_t)B * 2 * mxr::kSampleBins;
+  Tensor ws = at::zeros({n_gm + n_h + mxr::anchor_mark_ws_ints(B, N)}, o.dtype(at::kInt));
+  int32_t* wsp = ws.data_ptr<int32_t>();
+  Tensor max_ov = at::empty({B, N}, o);
+  Tensor argmax = at::empty({B, N}, o.dtype(at::kInt));
+  Tensor label_pre = at::empty({B, N}, o.dtype(at::kInt));
+  Tensor targets = at::empty({B, N, 4}, o);
+  mxr::anchor_target_assign(base_anchors.data_ptr<float>(), A, (int)H, (int)W, (float)feat_stride,
+                            im_info.data_ptr<float>(), (int)allowed_border, gt.data_ptr<float>(),
+                            n_gt.data_ptr<int32_t>(), G, B, (float)neg_thresh, (float)pos_thresh, clobber ? 1 : 0,
+                            max_ov.data_ptr<float>(), argmax.data_ptr<int32_t>(), reinterpret_cast<float*>(wsp),
+                            label_pre.data_ptr<int32_t>(), targets.data_ptr<float>(), cur_stream(),
+                            keys.data_ptr<float>(), wsp + n_gm);
+  Tensor meta = at::empty({B, 4}, o.dtype(at::kInt));
+  Tensor label = at::empty({B, A * H * W}, o.dtype(at::kInt));
+  Tensor bt = at::empty({B, 4 * A, H, W}, o);
+  Tensor iw = at::empty({B, 4 * A, H, W}, o);
+  Tensor ow = at::empty({B, 4 * A, H, W}, o);
+  const float iwf[4] = {(float)inside_w[0], (float)inside_w[1], (float)inside_w[2], (float)inside_w[3]};
+  mxr::anchor_sample_hist(label_pre.data_ptr<int32_t>(), targets.data_ptr<float>(), keys.data_ptr<float>(),
+                          wsp + n_gm, B, A, (int)H, (int)W, (int)num_fg, (int)batch, iwf, (float)pos_weight,
+                          wsp + n_gm + n_h, meta.data_ptr<int32_t>(), label.data_ptr<int32_t>(), bt.data_ptr<float>(),
+                          iw.data_ptr<float>(), ow.data_ptr<float>(), cur_stream());
+  return {label, bt, iw, ow, meta};
+}
+
 std::vector<Tensor> proposal_sample(const Tensor& rois, const Tensor& gt, const Tensor& n_gt, const Tensor& max_ov,
                                     const Tensor& argmax, const Tensor& rnd, int64_t R, int64_t F, int64_t C,
                                     double fg_thresh, double bg_hi, double bg_lo, bool is_train, bool normalize,
@@ -627,6 +674,21 @@ void set_dadd(mxr::ConvEpi& ep, const Tensor& dadd, const Tensor& y, int Ho, int
   TORCH_CHECK(false, "dadd must be shaped like y or its stride-s subsampled grid");
 }
 
+// ReLU (+ dropout) backward: dy * [y > 0] * scale; x2: dy (2N, ...) pairs, y the ReLU output pair
+Tensor relu_mask_bwd(const Tensor& dy, const Tensor& y, double scale, bool x2) {
+  CHECK_DEV(dy); CHECK_DEV(y);
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16 && dy.sizes() == y.sizes() &&
+                  dy.is_contiguous(at::MemoryFormat::ChannelsLast) && y.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "relu_mask_bwd: bf16 channels_last dy / y of one shape");
+  const int64_t n = x2 ? dy.numel() / 2 : dy.numel();
+  TORCH_CHECK(n % 8 == 0 && (!x2 || dy.size(0) % 2 == 0), "relu_mask_bwd: numel % 8 (pairs: 2N rows)");
+  DevGuard g(dy.device());
+  Tensor out = at::empty_like(dy, dy.options(), at::MemoryFormat::ChannelsLast);
+  mxr::relu_mask(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(y.data_ptr()),
+                 reinterpret_cast<uint16_t*>(out.data_ptr()), n, x2 ? n : 0, (float)scale, cur_stream());
+  return out;
+}
+
 // conv_igemm_fwd(x, w, bias, stride, pad, relu, tile, splits, residual, bn, bn_eps, bn_fix_gamma, act_relu)
 //   -> [y] or, when bn = (gamma, beta, mean, var) is given, [y, act(bn(y))]  (see ConvEpi)
 std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::optional<Tensor> bias, int64_t stride,
@@ -638,7 +700,7 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
                                    c10::optional<Tensor> drop_step, int64_t pad_w, c10::optional<Tensor> out,
                                    c10::optional<std::vector<int64_t>> out_map, c10::optional<Tensor> stat_shift,
                                    c10::optional<Tensor> bnb_part, int64_t bnb_row0, bool x2, int64_t w_plane,
-                                   bool out_f32) {
+                                   bool out_f32, bool bt, c10::optional<Tensor> rmask, double rmask_scale) {
   CHECK_DEV(x); CHECK_DEV(w);
   TORCH_CHECK((x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf) && w.scalar_type() == x.scalar_type(),
               "conv_igemm: bf16 or fp16 activations and weights of the same dtype");
@@ -650,14 +712,18 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   TORCH_CHECK(!x2 || (!f16 && x.size(0) % 2 == 0 && w_plane >= w.numel()), "x2: bf16 pairs (2N, ...) and w_plane");
   TORCH_CHECK(!out_f32 || x2, "out_f32 needs x2");
   const int NB = (int)(x2 ? x.size(0) / 2 : x.size(0)), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
-  const int Cout = (int)w.size(0), KH = (int)w.size(2), KW = (int)w.size(3);
-  TORCH_CHECK(w.size(1) == Cin, "channel mismatch");
+  // bt: a data gradient reading the forward filter w (Cout_f, Cin_f, kh, kw) directly -- this launch's
+  // input channels are the filter's outputs and its outputs the filter's inputs (taps flipped in-kernel)
+  const int Cout = (int)(bt ? w.size(1) : w.size(0)), KH = (int)w.size(2), KW = (int)w.size(3);
+  TORCH_CHECK((bt ? w.size(0) : w.size(1)) == Cin, "channel mismatch");
   TORCH_CHECK(Cin % 64 == 0, "conv_igemm requires Cin % 64 == 0");
+  TORCH_CHECK(!bt || (!f16 && stride == 1 && Cout % 8 == 0), "bt: bf16 stride-1 data gradient, Cout % 8 == 0");
   const int padw = pad_w >= 0 ? (int)pad_w : (int)pad;
   int Ho = (H + 2 * (int)pad - KH) / (int)stride + 1, Wo = (W + 2 * padw - KW) / (int)stride + 1;
   mxr::ConvEpi ep;
   ep.relu = relu ? 1 : 0;
   ep.f16 = f16 ? 1 : 0;
+  ep.bt = bt ? 1 : 0;
   ep.pad_w = pad_w >= 0 ? (int)pad_w : -1;
   const bool mapped = out_map.has_value();
   if (mapped) {
@@ -720,6 +786,14 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
                     r.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "residual must be a channels_last tensor of the activation dtype shaped like the output");
     ep.residual = reinterpret_cast<const uint16_t*>(r.data_ptr());
+  }
+  if (rmask.has_value() && rmask->defined()) {  // ReLU / dropout backward of the layer below (ConvEpi::rmask)
+    const Tensor& r = *rmask;
+    TORCH_CHECK(!f16 && !out_f32 && r.scalar_type() == at::kBFloat16 && r.sizes() == y.sizes() &&
+                    r.is_contiguous(at::MemoryFormat::ChannelsLast),
+                "rmask: a channels_last bf16 tensor shaped like the output (pairs in x2)");
+    ep.rmask = reinterpret_cast<const uint16_t*>(r.data_ptr());
+    ep.rmask_s = (float)rmask_scale;
   }
   Tensor y2;
   std::vector<Tensor> bnf;
@@ -806,9 +880,10 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   }
   if (tile <= 0 && splits <= 0 && !mapped && ep.pad_w < 0 && !ep.bnb_part && conv_tune_enabled()) {
     char kb[256];
-    snprintf(kb, sizeof(kb), "%d,%d,%d,%d,%d,%d,%d,%d,%d|%d%d%d%d%d%d%d", NB, H, W, Cin, Cout, KH, KW, (int)stride,
+    snprintf(kb, sizeof(kb), "%d,%d,%d,%d,%d,%d,%d,%d,%d|%d%d%d%d%d%d%d%d%d%d", NB, H, W, Cin, Cout, KH, KW, (int)stride,
              (int)pad, ep.residual != nullptr, ep.y2 != nullptr || bn.has_value(), bwd_mode, ep.dadd != nullptr,
-             ep.relu, ep.bias != nullptr || ep.bias_h != nullptr, (ep.drop_p > 0.f ? 1 : 0) + (stats ? 2 : 0));
+             ep.relu, ep.bias != nullptr || ep.bias_h != nullptr, (ep.drop_p > 0.f ? 1 : 0) + (stats ? 2 : 0), ep.bt,
+             ep.rmask != nullptr, ep.x2);
     const std::string key(kb);
     std::unique_lock<std::mutex> lk(g_tune_mu);
     auto it = g_tune.find(key);
@@ -920,7 +995,7 @@ std::vector<Tensor> conv_dgrad_wgrad(const Tensor& x, const Tensor& w, int64_t p
                                      const Tensor& wg_x, int64_t KH, int64_t KW, int64_t wg_stride, int64_t wg_pad,
                                      Tensor wg_out, bool defer, c10::optional<Tensor> prev_slab,
                                      c10::optional<Tensor> prev_out, c10::optional<Tensor> bnb_part, bool x2,
-                                     int64_t w_plane) {
+                                     int64_t w_plane, bool bt, c10::optional<Tensor> rmask, double rmask_scale) {
   CHECK_DEV(x); CHECK_DEV(w); CHECK_DEV(wg_dy); CHECK_DEV(wg_x); CHECK_DEV(wg_out);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast) && w.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -929,10 +1004,12 @@ std::vector<Tensor> conv_dgrad_wgrad(const Tensor& x, const Tensor& w, int64_t p
   // the weight gradient wg_out fp32
   TORCH_CHECK(!x2 || (x.size(0) % 2 == 0 && w_plane >= w.numel()), "x2: (2N, ...) pairs and w_plane");
   const int NB = (int)(x2 ? x.size(0) / 2 : x.size(0)), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
-  const int Cout = (int)w.size(0), kh = (int)w.size(2), kw = (int)w.size(3);
-  TORCH_CHECK(w.size(1) == Cin && Cin % 64 == 0 && Cout % 8 == 0, "conv_dgrad_wgrad: dgrad channels");
+  // bt: the dgrad reads the forward filter w (Cin, Cout, kh, kw) directly (see conv_igemm_fwd)
+  const int Cout = (int)(bt ? w.size(1) : w.size(0)), kh = (int)w.size(2), kw = (int)w.size(3);
+  TORCH_CHECK((bt ? w.size(0) : w.size(1)) == Cin && Cin % 64 == 0 && Cout % 8 == 0, "conv_dgrad_wgrad: dgrad channels");
   const int Ho = H + 2 * (int)pad - kh + 1, Wo = W + 2 * (int)pad - kw + 1;
   mxr::ConvEpi ep;
+  ep.bt = bt ? 1 : 0;
   Tensor y = at::empty({x2 ? 2 * NB : NB, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   if (x2) {
     TORCH_CHECK(x.numel() < (int64_t)0x40000000 && w_plane + w.numel() < (int64_t)0x40000000,
@@ -946,6 +1023,13 @@ std::vector<Tensor> conv_dgrad_wgrad(const Tensor& x, const Tensor& w, int64_t p
     TORCH_CHECK(residual->scalar_type() == at::kBFloat16 && residual->sizes() == y.sizes() &&
                     residual->is_contiguous(at::MemoryFormat::ChannelsLast), "residual like y");
     ep.residual = reinterpret_cast<const uint16_t*>(residual->data_ptr());
+  }
+  if (rmask.has_value() && rmask->defined()) {  // ReLU / dropout backward of the layer below (ConvEpi::rmask)
+    TORCH_CHECK(!bn.has_value() && rmask->scalar_type() == at::kBFloat16 && rmask->sizes() == y.sizes() &&
+                    rmask->is_contiguous(at::MemoryFormat::ChannelsLast),
+                "rmask: channels_last bf16 like y, no BN epilogue");
+    ep.rmask = reinterpret_cast<const uint16_t*>(rmask->data_ptr());
+    ep.rmask_s = (float)rmask_scale;
   }
   std::vector<Tensor> bnf;
   Tensor dgm, dbt;
@@ -1182,7 +1266,7 @@ bool al16(const Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) &
 Tensor head_bwd(const Tensor& x, const std::vector<Tensor>& dys, const std::vector<Tensor>& ws,
                 const std::vector<Tensor>& dws, const std::vector<bool>& dw_acc, const std::vector<Tensor>& dbs,
                 const std::vector<bool>& db_acc, bool need_dx, bool relu_mask, bool x2,
-                const std::vector<int64_t>& w_planes) {
+                const std::vector<int64_t>& w_planes, double mask_scale) {
   CHECK_DEV(x);
   const int nh = (int)dys.size();
   TORCH_CHECK(nh >= 1 && nh <= 2 && (int)ws.size() == nh && (int)dws.size() == nh && (int)dw_acc.size() == nh &&
@@ -1234,6 +1318,7 @@ Tensor head_bwd(const Tensor& x, const std::vector<Tensor>& dys, const std::vect
     dx = at::empty({x2 ? 2 * M : M, K}, x.options());
     a.dx = reinterpret_cast<uint16_t*>(dx.data_ptr());
     a.relu_mask = relu_mask ? 1 : 0;
+    a.mask_scale = (float)mask_scale;
   }
   a.rs = mxr::head_bwd_splits(M, K, a.N, nh);
   Tensor wsp;
@@ -1899,6 +1984,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_relu_fwd_cpu", &bn_relu_fwd_cpu);
   m.def("iou_max", &iou_max);
   m.def("anchor_sample", &anchor_sample);
+  m.def("anchor_target_fused", &anchor_target_fused);
   m.def("proposal_sample", &proposal_sample);
   m.def("anchor_target_assign", &anchor_target_assign);
   m.def("roi_pool_fwd", &roi_pool_fwd, py::arg("feat"), py::arg("rois"), py::arg("PH"), py::arg("PW"),
@@ -1928,18 +2014,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("drop_seed") = 0, py::arg("drop_step") = py::none(), py::arg("pad_w") = -1,
         py::arg("out") = py::none(), py::arg("out_map") = py::none(), py::arg("stat_shift") = py::none(),
         py::arg("bnb_part") = py::none(), py::arg("bnb_row0") = 0, py::arg("x2") = false, py::arg("w_plane") = 0,
-        py::arg("out_f32") = false);
+        py::arg("out_f32") = false, py::arg("bt") = false, py::arg("rmask") = py::none(), py::arg("rmask_scale") = 1.0);
+  m.def("relu_mask_bwd", &relu_mask_bwd, py::arg("dy"), py::arg("y"), py::arg("scale") = 1.0, py::arg("x2") = false);
   m.def("proposal_topk", &proposal_topk, py::arg("keys"), py::arg("boxes"), py::arg("P"));
   m.def("conv_dgrad_wgrad", &conv_dgrad_wgrad, py::arg("x"), py::arg("w"), py::arg("pad"), py::arg("residual"),
         py::arg("bn"), py::arg("bn_eps"), py::arg("bn_fix_gamma"), py::arg("bnb_x"), py::arg("dadd"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("wg_dy"), py::arg("wg_x"), py::arg("KH"), py::arg("KW"), py::arg("wg_stride"),
         py::arg("wg_pad"), py::arg("wg_out"), py::arg("defer") = false, py::arg("prev_slab") = py::none(),
         py::arg("prev_out") = py::none(), py::arg("bnb_part") = py::none(), py::arg("x2") = false,
-        py::arg("w_plane") = 0);
+        py::arg("w_plane") = 0, py::arg("bt") = false, py::arg("rmask") = py::none(), py::arg("rmask_scale") = 1.0);
   m.def("wgrad_reduce_run", &wgrad_reduce_run, py::arg("slab"), py::arg("out"));
   m.def("head_bwd", &head_bwd, py::arg("x"), py::arg("dys"), py::arg("ws"), py::arg("dws"), py::arg("dw_acc"),
         py::arg("dbs"), py::arg("db_acc"), py::arg("need_dx"), py::arg("relu_mask"), py::arg("x2") = false,
-        py::arg("w_planes") = std::vector<int64_t>());
+        py::arg("w_planes") = std::vector<int64_t>(), py::arg("mask_scale") = 1.0);
   m.def("chan_sum", &chan_sum, py::arg("x"), py::arg("out"), py::arg("accumulate"), py::arg("x2") = false);
   m.def("det_postprocess", &det_postprocess, py::arg("rois"), py::arg("scores"), py::arg("deltas"),
         py::arg("im_info"), py::arg("thresh"), py::arg("nms_thresh"), py::arg("max_per"), py::arg("cap"));

@@ -141,7 +141,8 @@ anchor_pass2_kernel(const float* __restrict__ base, int A, int H, int W, float s
                     const float* __restrict__ gt, const int32_t* __restrict__ n_gt, int G,
                     float neg_thresh, float pos_thresh, int clobber, const float* __restrict__ max_ov,
                     const int32_t* __restrict__ argmax, const float* __restrict__ gt_max,
-                    int32_t* __restrict__ label, float* __restrict__ targets) {
+                    int32_t* __restrict__ label, float* __restrict__ targets, const float* __restrict__ keys,
+                    int32_t* __restrict__ hist) {
   __shared__ float4 sg[kGtTile];
   __shared__ float sa[kGtTile];
   __shared__ float sm[kGtTile];
@@ -198,19 +199,25 @@ anchor_pass2_kernel(const float* __restrict__ base, int A, int H, int W, float s
   }
   label[(int64_t)b * N + t] = lab;
   reinterpret_cast<float4*>(targets)[(int64_t)b * N + t] = tg;
+  // subsampling histograms (sample.hip anchor_mark): per image and pool (fg, bg), the count of
+  // labelled anchors per key bin
+  if (hist != nullptr && lab >= 0)
+    atomicAdd(hist + ((int64_t)b * 2 + (lab == 1 ? 0 : 1)) * kSampleBins + sample_bin(keys[(int64_t)b * N + t]), 1);
 }
 
 void anchor_target_assign(const float* base_anchors, int A, int H, int W, float feat_stride,
                           const float* im_info, int allowed_border, const float* gt, const int32_t* n_gt, int G,
                           int B, float neg_thresh, float pos_thresh, int clobber_positives, float* max_ov,
-                          int32_t* argmax, float* gt_max, int32_t* label, float* targets, hipStream_t st) {
+                          int32_t* argmax, float* gt_max, int32_t* label, float* targets, hipStream_t st,
+                          const float* keys, int32_t* hist) {
   const int64_t N = (int64_t)H * W * A;
   if (B == 0 || N == 0) return;
   dim3 grid(div_up(N, 256), B);
   anchor_pass1_kernel<<<grid, 256, 0, st>>>(base_anchors, A, H, W, feat_stride, im_info, allowed_border, gt, n_gt,
                                             G, max_ov, argmax, gt_max);
   anchor_pass2_kernel<<<grid, 256, 0, st>>>(base_anchors, A, H, W, feat_stride, gt, n_gt, G, neg_thresh,
-                                            pos_thresh, clobber_positives, max_ov, argmax, gt_max, label, targets);
+                                            pos_thresh, clobber_positives, max_ov, argmax, gt_max, label, targets,
+                                            keys, hist);
 }
 
 }  // namespace mxr

@@ -151,6 +151,16 @@ __device__ __forceinline__ float epi_dropout(const ConvEpi& ep, int64_t idx, flo
   return v;
 }
 
+// ReLU(-and-dropout) backward of the layer whose output is this data gradient's forward input
+// (ConvEpi::rmask): keep v where that activation is positive, scaled by rmask_s
+__device__ __forceinline__ float epi_rmask(const ConvEpi& ep, int64_t idx, float v) {
+  if (ep.rmask) {
+    const uint16_t h = ep.rmask[idx];  // bf16 (x2: the hi plane carries the sign)
+    v = ((h & 0x8000u) == 0 && (h & 0x7fffu) != 0) ? v * ep.rmask_s : 0.f;
+  }
+  return v;
+}
+
 template <bool X2>
 __device__ __forceinline__ void epi_store(const ConvEpi& ep, const EpiCol& c, uint16_t* __restrict__ y, int64_t idx,
                                           float v) {
@@ -158,6 +168,7 @@ __device__ __forceinline__ void epi_store(const ConvEpi& ep, const EpiCol& c, ui
   if (ep.residual) v += epi_ld1<X2>(ep, ep.residual, idx, ep.x2_py);
   if (ep.relu) v = fmaxf(v, 0.f);
   v = epi_dropout(ep, idx, v);
+  v = epi_rmask(ep, idx, v);
   if (X2 && ep.yf) {
     ep.yf[idx] = v;
     return;
@@ -424,7 +435,7 @@ __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* 
     for (int k = 0; k < 8; ++k) {
       t[k] = a[k] + ec[k].bias + (ep.residual ? rs[k] : 0.f);
       if (ep.relu) t[k] = fmaxf(t[k], 0.f);
-      t[k] = epi_dropout(ep, e + k, t[k]);
+      t[k] = epi_rmask(ep, e + k, epi_dropout(ep, e + k, t[k]));
     }
     if (X2 && ep.yf) {  // fp32 output (prediction heads of the x2 mode)
       float4* dst = reinterpret_cast<float4*>(ep.yf + e);
@@ -656,7 +667,7 @@ splitk_reduce_kernel(const float* __restrict__ slab, int splits, int64_t MN, int
       const EpiCol c = epi_col(ep, n + k);
       float t = v[k] + c.bias + res[k];
       if (ep.relu) t = fmaxf(t, 0.f);
-      t = epi_dropout(ep, e + k, t);
+      t = epi_rmask(ep, e + k, epi_dropout(ep, e + k, t));
       if (ep.yf) {
         ep.yf[e + k] = t;
         continue;
@@ -676,7 +687,7 @@ splitk_reduce_kernel(const float* __restrict__ slab, int splits, int64_t MN, int
     const EpiCol c = epi_col(ep, n + k);
     float t = v[k] + c.bias + res[k];
     if (ep.relu) t = fmaxf(t, 0.f);
-    t = epi_dropout(ep, e + k, t);
+    t = epi_rmask(ep, e + k, epi_dropout(ep, e + k, t));
     out[k] = f32_to_h16c(EPC, t);
     float q = h16_to_f32c(EPC, out[k]) * c.s + c.t;
     if (ep.act_relu) q = fmaxf(q, 0.f);
@@ -862,7 +873,21 @@ __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t rs, void* lds_w
 // body of the buffer kernel for workgroup `bid` of an `nwg`-workgroup launch; `lds`: S*(BM+BN)*BK
 // elements, the block's ONLY LDS (the grouped data + weight gradient launch below shares it with
 // the wgrad role)
-template <int BM, int BN, int S, bool F16 = false>
+//
+// x2 (fp32-class pairs, X2 = true): a stage holds 32 channels of BOTH planes -- logical 16-B chunks
+// 0-3 of a 128-B LDS row are the hi plane's channels c..c+31, chunks 4-7 the lo plane's same
+// channels -- so the fragment reads are the bf16 ones (chunk lane>>4 and 4 + lane>>4) and a stage
+// runs three MFMAs per fragment pair (A_hi B_hi + A_hi B_lo + A_lo B_hi): 2/3 of the operand
+// bytes of three separate K phases for the same MFMA work.  The lo planes sit x2_pa / x2_pb bytes
+// further, added to the per-lane offsets of the lo chunks.
+//
+// BT (data gradient straight from the forward filter, no flipped / transposed copy): B is the
+// filter W (Cin_d, taps, Cout_d) itself -- GEMM row k = (tap, channel c) is filter row
+// c * taps + (taps - 1 - tap) with its Cout_d outputs contiguous, i.e. B arrives [k][n] instead of
+// [n][k].  The stage's B tile is stored k-major (64 rows of 64 outputs, wgrad's chunk swizzle) and
+// its fragments are read with ds_read_b64_tr_b16 (rows 8g + 4h + 0..3 of each 32-row half for lane
+// group g: the same k order as the A fragments' 16-B chunks).  BN must be 64.
+template <int BM, int BN, int S, bool F16 = false, bool X2 = false, bool BT = false>
 __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uint16_t* __restrict__ x,
                                                const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int NB, int H,
                                                int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride,
@@ -894,6 +919,9 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
       (void*)w, (short)0, (int)((int64_t)Cout * K * 2 + (ep.x2 ? ep.x2_pb : 0u)), 0x00020000);
 
   const int slot = lane & 7;
+  // logical chunk lc of a row: channels lc*8 (16-bit), or (X2) channels (lc&3)*8 of plane lc>>2
+  auto chan_bytes = [&](int lc) { return X2 ? (lc & 3) * 16 : lc * 16; };
+  auto plane_a = [&](int lc) { return X2 && lc >= 4 ? ep.x2_pa : 0u; };
   uint32_t a_off[ACH];
   uint64_t a_mask[ACH];
 #pragma unroll
@@ -906,40 +934,49 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
     if (m < M) {
       const int img = m / (Ho * Wo), rem = m % (Ho * Wo);
       const int hi0 = (rem / Wo) * stride - pad, wi0 = (rem % Wo) * stride - (ep.pad_w >= 0 ? ep.pad_w : pad);
-      a_off[i] = (uint32_t)(((((int64_t)img * H + hi0) * W + wi0) * Cin + lc * 8) * 2);
+      a_off[i] = (uint32_t)((((int64_t)img * H + hi0) * W + wi0) * Cin * 2 + chan_bytes(lc)) + plane_a(lc);
       for (int fr = 0; fr < KH; ++fr)
         for (int fc = 0; fc < KW; ++fc)
           if ((unsigned)(hi0 + fr) < (unsigned)H && (unsigned)(wi0 + fc) < (unsigned)W)
             a_mask[i] |= 1ull << (fr * KW + fc);
     }
   }
+  static_assert(!BT || (BN == 64 && !F16), "BT: 64-column 16-bit bf16 tiles");
+  const int taps = KH * KW;
   uint32_t b_off[BCH];
 #pragma unroll
   for (int i = 0; i < BCH; ++i) {
     const int row = 32 * i + 8 * wid + (lane >> 3);
-    const int co = n0 + row;
-    b_off[i] = co < Cout ? (uint32_t)(((int64_t)co * K + (slot ^ ((row >> 1) & 7)) * 8) * 2) : kBufOOB;
+    if constexpr (BT) {  // row = k within the stage (x2: rows 32.. are the lo plane of the same channels)
+      const int n = n0 + (slot ^ wsw(row)) * 8;
+      const int crow = X2 ? (row & 31) : row;
+      b_off[i] = n < Cout ? (uint32_t)(((int64_t)crow * taps * Cout + n) * 2) + (X2 && row >= 32 ? ep.x2_pb : 0u)
+                          : kBufOOB;
+    } else {
+      const int co = n0 + row;
+      const int lc = slot ^ ((row >> 1) & 7);
+      b_off[i] = co < Cout ? (uint32_t)((int64_t)co * K * 2 + chan_bytes(lc)) + (X2 && lc >= 4 ? ep.x2_pb : 0u)
+                           : kBufOOB;
+    }
   }
-  const int cin_steps = Cin / BK;
-  const int nk_base = KH * KW * cin_steps;
-  // x2 (fp32-class) operands: three K phases over the same taps / channel blocks, A_hi B_hi,
-  // A_hi B_lo, A_lo B_hi, the lo planes reached through the (range-check-free) SGPR offset
-  const int nk_all = ep.x2 ? 3 * nk_base : nk_base;
+  constexpr int KC = X2 ? BK / 2 : BK;  // channels per stage (x2: 32 of each plane)
+  const int cin_steps = Cin / KC;
+  const int nk_all = KH * KW * cin_steps;
   const int per = (nk_all + splits - 1) / splits;
   const int k_begin = split * per;
   const int k_end = min(nk_all, k_begin + per);
   const int nk = max(0, k_end - k_begin);
 
-  // issue cursor (uniform): phase, tap (fr, fc), channel block ci0 of the next stage to load
-  int c_ph = k_begin / nk_base;
-  int c_tap = (k_begin % nk_base) / cin_steps, c_ci = (k_begin % cin_steps) * BK;
+  // issue cursor (uniform): tap (fr, fc), channel block ci0 of the next stage to load
+  int c_tap = k_begin / cin_steps, c_ci = (k_begin % cin_steps) * KC;
   int c_fr = c_tap / KW, c_fc = c_tap % KW;
   auto issue = [&](int buf) {
     // the buffer range check sees only the VGPR offset, so the tap shift (which can turn a
     // negative padding-row offset into a valid one) goes there; the channel block is the SGPR part
     const uint32_t tap_a = (uint32_t)((c_fr * W + c_fc) * Cin * 2);
-    const uint32_t soff_a = (uint32_t)(c_ci * 2) + (c_ph == 2 ? ep.x2_pa : 0u);
-    const uint32_t soff_b = (uint32_t)((c_tap * Cin + c_ci) * 2) + (c_ph == 1 ? ep.x2_pb : 0u);
+    const uint32_t soff_a = (uint32_t)(c_ci * 2);
+    const uint32_t soff_b = BT ? (uint32_t)(((int64_t)c_ci * taps + (taps - 1 - c_tap)) * Cout * 2)
+                               : (uint32_t)((c_tap * Cin + c_ci) * 2);
 #pragma unroll
     for (int i = 0; i < ACH; ++i) {
       const uint32_t vo = ((a_mask[i] >> c_tap) & 1ull) ? a_off[i] + tap_a : kBufOOB;
@@ -947,17 +984,13 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) buf_lds16(wr, Bs + (buf * BN + 32 * i + 8 * wid) * BK, b_off[i], soff_b);
-    c_ci += BK;
+    c_ci += KC;
     if (c_ci == Cin) {
       c_ci = 0;
       ++c_tap;
       if (++c_fc == KW) {
         c_fc = 0;
-        if (++c_fr == KH) {  // next phase (x2)
-          c_fr = 0;
-          c_tap = 0;
-          ++c_ph;
-        }
+        ++c_fr;
       }
     }
   };
@@ -976,6 +1009,90 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
     __builtin_amdgcn_s_barrier();
     if (ks + S - 1 < nk) issue((ks + S - 1) % S);
     const int buf = ks % S;
+    if constexpr (BT) {
+      // A: 16-B chunk reads (chunk 4*kk + g); B: transposed reads of the k-major tile, all in one
+      // asm block (through the builtin the compiler drains the in-flight DMA ring first)
+      static_assert(TN == 2, "BT: two 16-column fragments per wave");
+      bf16x8 af[2][TM], bfr[2][TN];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = wm * WM + i * 16 + (lane & 15);
+          af[kk][i] = *reinterpret_cast<const bf16x8*>(As + (buf * BM + row) * BK + swz(row, kk * 4 + (lane >> 4)) * 8);
+        }
+      const int g = lane >> 4, q = (lane & 15) >> 2, pcol = (lane & 3) * 4;
+      uint32_t ad[8];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int row = kk * 32 + 8 * g + 4 * h + q, col = wn * WN + j * 16 + pcol;
+            ad[kk * 4 + j * 2 + h] = (uint32_t)reinterpret_cast<uintptr_t>(
+                Bs + (buf * BN + row) * BK + (((col >> 3) ^ wsw(row)) << 3) + (col & 7));
+          }
+      s16x4 fr[8];
+      asm volatile(
+          "ds_read_b64_tr_b16 %0, %8\n\tds_read_b64_tr_b16 %1, %9\n\t"
+          "ds_read_b64_tr_b16 %2, %10\n\tds_read_b64_tr_b16 %3, %11\n\t"
+          "ds_read_b64_tr_b16 %4, %12\n\tds_read_b64_tr_b16 %5, %13\n\t"
+          "ds_read_b64_tr_b16 %6, %14\n\tds_read_b64_tr_b16 %7, %15\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(fr[0]), "=&v"(fr[1]), "=&v"(fr[2]), "=&v"(fr[3]), "=&v"(fr[4]), "=&v"(fr[5]), "=&v"(fr[6]),
+            "=&v"(fr[7])
+          : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]), "v"(ad[5]), "v"(ad[6]), "v"(ad[7])
+          : "memory");
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          bfr[kk][j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(fr[kk * 4 + j * 2], fr[kk * 4 + j * 2 + 1], 0,
+                                                                          1, 2, 3, 4, 5, 6, 7));
+      // products per pass: bf16 (k-half 0) (k-half 1); x2 (hi,hi) (hi,lo) (lo,hi)
+      constexpr int NPASS = X2 ? 3 : 2;
+#pragma unroll
+      for (int ps = 0; ps < NPASS; ++ps) {
+        const int ka = X2 ? (ps == 2) : ps, kb = X2 ? (ps == 1) : ps;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ka][i], bfr[kb][j], acc[i][j], 0, 0, 0);
+      }
+      continue;
+    }
+    if constexpr (X2) {
+      bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+      const int ch = lane >> 4, cl = 4 + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WM + i * 16 + (lane & 15);
+        ah[i] = *reinterpret_cast<const bf16x8*>(As + (buf * BM + row) * BK + swz(row, ch) * 8);
+        al[i] = *reinterpret_cast<const bf16x8*>(As + (buf * BM + row) * BK + swz(row, cl) * 8);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WN + j * 16 + (lane & 15);
+        bh[j] = *reinterpret_cast<const bf16x8*>(Bs + (buf * BN + row) * BK + swz(row, ch) * 8);
+        bl[j] = *reinterpret_cast<const bf16x8*>(Bs + (buf * BN + row) * BK + swz(row, cl) * 8);
+      }
+      // three passes over the accumulator tile (independent MFMAs back to back)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+      continue;
+    }
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
       typename Mfma16<F16>::T af[TM], bfr[TN];
@@ -998,7 +1115,7 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
     }
   }
   static_assert(BM * (BN + 4) * 4 <= S * (BM + BN) * BK * 2, "epilogue tile must fit the operand ring");
-  if (ep.x2 || ep.yf) {  // fp32-class pairs (separate instantiation: the 16-bit loops stay unrolled)
+  if (X2 || ep.yf) {  // fp32-class pairs (separate instantiation: the 16-bit loops stay unrolled)
     if (Cout % 8 == 0)
       igemm_epilogue_lds<BM, BN, TM, TN, WM, WN, true>(acc, reinterpret_cast<float*>(lds), m0, n0, wm, wn, lane, tid, M,
                                                        Cout, ep, y, split, splits, slab, Ho, Wo);
@@ -1012,14 +1129,14 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
   }
 }
 
-template <int BM, int BN, int S, bool F16 = false>
+template <int BM, int BN, int S, bool F16 = false, bool X2 = false, bool BT = false>
 __global__ void __launch_bounds__(256)
 conv_igemm_buf_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
                       int NB, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad,
                       const ConvEpi ep, int tiles_n, int nwg, int ntiles, int splits, float* __restrict__ slab) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[S * (BM + BN) * BK];
-  igemm_buf_body<BM, BN, S, F16>(lds, blockIdx.x, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, tiles_n,
-                                 nwg, ntiles, splits, slab);
+  igemm_buf_body<BM, BN, S, F16, X2, BT>(lds, blockIdx.x, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep,
+                                         tiles_n, nwg, ntiles, splits, slab);
 }
 
 // ---- tile-balanced LDS-DMA ring (the production path) ----------------------------------------
@@ -1155,7 +1272,7 @@ __device__ __forceinline__ void ring_epilogue(f32x4 (&acc)[TM][TN], float* __res
     for (int k = 0; k < 8; ++k) {
       float t = a[k] + ec[k].bias + (ep.residual ? rs[k] : 0.f);
       if (ep.relu) t = fmaxf(t, 0.f);
-      t = epi_dropout(ep, e + k, t);
+      t = epi_rmask(ep, e + k, epi_dropout(ep, e + k, t));
       yb[k] = f32_to_h16c(EPC, t);
       const float ys = h16_to_f32c(EPC, yb[k]);
       float qv = ys * ec[k].s + ec[k].t;
@@ -1423,7 +1540,17 @@ static void launch_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB
     if (ep.f16)
       conv_igemm_buf_kernel<BM, BN, S, true><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
                                                                  pad, ep, tiles_n, nwg, ntiles, splits, slab);
-    else
+    else if (ep.x2 || ep.bt) {
+      if constexpr (S == 3 && BN == 64 && (BM == 64 || BM == 128)) {
+#define MXR_BUF_LAUNCH(X, B)                                                                                        \
+  conv_igemm_buf_kernel<BM, BN, S, false, X, B><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, \
+                                                                     stride, pad, ep, tiles_n, nwg, ntiles, splits, slab)
+        if (ep.x2 && ep.bt) MXR_BUF_LAUNCH(true, true);
+        else if (ep.x2) MXR_BUF_LAUNCH(true, false);
+        else MXR_BUF_LAUNCH(false, true);
+#undef MXR_BUF_LAUNCH
+      }
+    } else
       conv_igemm_buf_kernel<BM, BN, S, false><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
                                                                   pad, ep, tiles_n, nwg, ntiles, splits, slab);
   }
@@ -1495,6 +1622,7 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
   if ((ep.y2 || ep.bnb_x) && (!ep.bn_beta || !ep.bn_mean || !ep.bn_var || (!ep.bn_fix_gamma && !ep.bn_gamma)))
     return -1;
   if (ep.y2 && ep.bnb_x) return -1;
+  if (ep.rmask && (ep.bnb_x || ep.y2 || ep.f16)) return -1;
   if ((ep.omap || ep.pad_w >= 0) && (splits > 1 || !(tile == 22 || tile == 23 || tile >= 100))) return -1;
   if (ep.f16 && !(tile == 21 || tile == 22 || tile == 23 || tile >= 100)) return -1;
   // BN statistics: LDS-epilogue kernels (buffer / ring), whole K per workgroup
@@ -1509,8 +1637,9 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
     tile = 3;
   if ((ep.st_part || ep.bnb_part) && tile < 21) return -1;  // needs the buffer / ring epilogue
   if (ep.bnb_part && (splits > 1 || Cout % 8 != 0)) return -1;
-  if (ep.x2 || ep.yf) {
-    // pairs / fp32 outputs: the buffer kernels only (their epilogue and K-phase loop carry x2)
+  if (ep.bt && (ep.f16 || Cout % 8 != 0)) return -1;
+  if (ep.x2 || ep.yf || ep.bt) {
+    // pairs / fp32 outputs / filter read transposed: the buffer kernels only
     if (!(tile == 22 || tile == 23)) tile = 23;
     if ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB || (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kBufOOB ||
         KH * KW > 64 || ep.f16)
@@ -1612,7 +1741,7 @@ void conv_wt_flip_multi(const WtFlipEntry* entries, int n_entries, int total_til
 // Replaces the two-stream schedule (wgrad on a side stream, one cross-queue wait per wgrad and a
 // join per unit): every cross-queue edge of a replayed graph cost ~10 us of idle time, four per
 // unit (profiles/r2_resnet101_stage3_unit_timeline.txt).
-template <int S>
+template <int S, bool X2 = false, bool BT = false>
 __global__ void __launch_bounds__(256)
 conv_dgrad_wgrad_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
                         int NB, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int pad,
@@ -1627,10 +1756,10 @@ conv_dgrad_wgrad_kernel(const uint16_t* __restrict__ x, const uint16_t* __restri
   if (b < rp.nwg) {
     wgrad_reduce_body(b, rp.slab, rp.splits, rp.n, rp.dw, rp.accumulate, rp.dwf);
   } else if (b < rp.nwg + nwg_d) {
-    igemm_buf_body<64, 64, S, false>(lds, b - rp.nwg, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, 1, pad, ep, tiles_n,
-                                     nwg_d, ntiles, 1, nullptr);
+    igemm_buf_body<64, 64, S, false, X2, BT>(lds, b - rp.nwg, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, 1, pad, ep,
+                                             tiles_n, nwg_d, ntiles, 1, nullptr);
   } else {
-    wgrad_buf_body<S>(lds, b - rp.nwg - nwg_d, wp);
+    wgrad_buf_body<S, X2>(lds, b - rp.nwg - nwg_d, wp);
   }
 }
 
@@ -1673,7 +1802,15 @@ int conv_dgrad_wgrad(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, 
     const char* e = getenv("MXR_GROUPED_S");
     return e != nullptr && e[0] == '4' ? 4 : 3;
   }();
-  if (depth == 4)
+  const int nwg_all = rp.nwg + ntiles + wp.nwg;
+#define MXR_GROUPED(S_, X, B) \
+  conv_dgrad_wgrad_kernel<S_, X, B><<<nwg_all, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, pad, ep, \
+                                                            tiles_n, ntiles, ntiles, wp, rp)
+  if (wx2.x2 && ep.bt) MXR_GROUPED(3, true, true);
+  else if (wx2.x2) MXR_GROUPED(3, true, false);
+  else if (ep.bt) MXR_GROUPED(3, false, true);
+#undef MXR_GROUPED
+  else if (depth == 4)
     conv_dgrad_wgrad_kernel<4><<<rp.nwg + ntiles + wp.nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW,
                                                                          pad, ep, tiles_n, ntiles, ntiles, wp, rp);
   else

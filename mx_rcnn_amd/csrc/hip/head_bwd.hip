@@ -229,8 +229,7 @@ head_bwd_kernel(const uint16_t* __restrict__ x, int M, int K, HeadBwdArgs a) {
         if constexpr (X2) ld8x(x + o, xplane, xv);
         else ld8_bf16(x + o, xv);
 #pragma unroll
-        for (int q = 0; q < 8; ++q)
-          if (!(xv[q] > 0.f)) v8[q] = 0.f;
+        for (int q = 0; q < 8; ++q) v8[q] = xv[q] > 0.f ? v8[q] * a.mask_scale : 0.f;
       }
       if constexpr (X2) st8x(a.dx + o, xplane, v8, v8);
       else st8_bf16(a.dx + o, v8);

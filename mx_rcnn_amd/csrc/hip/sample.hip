@@ -143,7 +143,8 @@ __global__ void __launch_bounds__(256)
 anchor_output_kernel(const int32_t* __restrict__ label_pre, const float* __restrict__ targets,
                      const uint32_t* __restrict__ kept, const int32_t* __restrict__ meta, int B, int A, int HW,
                      float iw0, float iw1, float iw2, float iw3, float pos_weight, int32_t* __restrict__ label,
-                     float* __restrict__ bbox_target, float* __restrict__ inside, float* __restrict__ outside) {
+                     float* __restrict__ bbox_target, float* __restrict__ inside, float* __restrict__ outside,
+                     int64_t kept_stride) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t per = (int64_t)A * HW;
   if (t >= (int64_t)B * per) return;
@@ -155,7 +156,7 @@ anchor_output_kernel(const int32_t* __restrict__ label_pre, const float* __restr
   const int NW = (N + 31) / 32;
   const int l = label_pre[(int64_t)b * N + i];
   const int32_t* m = meta + b * 4;
-  const bool bit = (kept[(int64_t)b * NW + (i >> 5)] >> (i & 31)) & 1u;
+  const bool bit = (kept[(int64_t)b * (kept_stride > 0 ? kept_stride : NW) + (i >> 5)] >> (i & 31)) & 1u;
   int lo = -1;
   if (l == 1 && (m[0] || bit)) lo = 1;
   else if (l == 0 && (m[1] || bit)) lo = 0;
@@ -192,7 +193,194 @@ void anchor_sample(const int32_t* label_pre, const float* targets, const float* 
   const int64_t total = (int64_t)B * N;
   anchor_output_kernel<<<div_up(total, 256), 256, 0, st>>>(label_pre, targets, kept_ws, meta_ws, B, A, H * W,
                                                            inside_w[0], inside_w[1], inside_w[2], inside_w[3],
-                                                           pos_weight, label, bbox_target, inside, outside);
+                                                           pos_weight, label, bbox_target, inside, outside, 0);
+}
+
+// ---- multi-workgroup subsampling -------------------------------------------------------------
+// anchor_sample above runs the whole image on one workgroup (~115 us on ResNet-101's 50 400
+// anchors, ~400 us on VGG16): every pass over the anchors is one CU's bandwidth.  Here the key
+// histograms of the fg / bg pools come from the assignment pass (grid-wide atomics), and one
+// grid-wide mark pass selects: with the pool's k-th smallest key in bin T, every member in a bin
+// below T is taken, members of bin T are collected into a short list, and the grid's last
+// workgroup per image (device-scope counter, release / acquire fences) takes the `rem` smallest
+// (key, index) of that list -- exactly the set select_smallest picks, at ~N / 4096 boundary
+// candidates instead of N.  An overfull boundary list (pathological key repeats) falls back to
+// select_smallest restricted to bin T.
+constexpr int kBoundCap = 2048;
+
+struct AnchorThr {
+  int tbin[2], rem[2];
+  int all_fg, all_bg, n_fg, n_bg;
+};
+
+// Block-wide (256 threads): in histogram h (kSampleBins bins), the bin holding the k-th smallest
+// key (k >= 1) and how many of that bin's members are taken; total = sum of h.  part: 512 ints LDS.
+__device__ void hist_kth(const int32_t* __restrict__ h, int k, int* part, int* res, int& total) {
+  const int tid = threadIdx.x;
+  constexpr int PER = kSampleBins / 256;
+  int v[PER], sum = 0;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    v[j] = h[tid * PER + j];
+    sum += v[j];
+  }
+  part[tid] = sum;
+  __syncthreads();
+  int* a = part;
+  int* bb = part + 256;
+  for (int off = 1; off < 256; off <<= 1) {  // inclusive scan (Hillis-Steele, double-buffered)
+    bb[tid] = a[tid] + (tid >= off ? a[tid - off] : 0);
+    __syncthreads();
+    int* t = a;
+    a = bb;
+    bb = t;
+  }
+  const int incl = a[tid], excl = incl - sum;
+  total = a[255];
+  if (k >= 1 && excl < k && k <= incl) {
+    int c = excl;
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      if (c + v[j] >= k) {
+        res[0] = tid * PER + j;
+        res[1] = k - c;
+        break;
+      }
+      c += v[j];
+    }
+  }
+  __syncthreads();
+}
+
+// thresholds of both pools (block-uniform result in s)
+__device__ void anchor_thresholds(const int32_t* __restrict__ hist, int num_fg, int batch, int* part, AnchorThr& s) {
+  int nfg = 0, nbg = 0;
+  if (threadIdx.x == 0) {
+    s.tbin[0] = s.tbin[1] = kSampleBins;  // "take every member"
+    s.rem[0] = s.rem[1] = 0;
+  }
+  __syncthreads();
+  __shared__ int sres[2];
+  hist_kth(hist, num_fg, part, sres, nfg);  // writes sres only when num_fg < nfg somewhere
+  const bool all_fg = nfg <= num_fg;
+  const int n_fg = all_fg ? nfg : num_fg;
+  if (threadIdx.x == 0 && !all_fg) {
+    s.tbin[0] = num_fg > 0 ? sres[0] : 0;
+    s.rem[0] = num_fg > 0 ? sres[1] : 0;
+  }
+  __syncthreads();
+  const int k_bg = max(batch - n_fg, 0);
+  hist_kth(hist + kSampleBins, k_bg, part, sres, nbg);
+  const bool all_bg = nbg <= k_bg;
+  if (threadIdx.x == 0) {
+    if (!all_bg) {
+      s.tbin[1] = k_bg > 0 ? sres[0] : 0;
+      s.rem[1] = k_bg > 0 ? sres[1] : 0;
+    }
+    s.all_fg = all_fg;
+    s.all_bg = all_bg;
+    s.n_fg = n_fg;
+    s.n_bg = all_bg ? nbg : k_bg;
+  }
+  __syncthreads();
+}
+
+// grid (ceil(N / 256), B) x 256.  ws per image: [kept NW words | bcnt fg, bcnt bg, done, pad | list fg | list bg]
+__global__ void __launch_bounds__(256)
+anchor_mark_kernel(const int32_t* __restrict__ label_pre, const float* __restrict__ keys,
+                   const int32_t* __restrict__ hist, int N, int num_fg, int batch, int32_t* __restrict__ ws,
+                   int64_t per, int NW, int32_t* __restrict__ meta) {
+  __shared__ int part[512];
+  __shared__ AnchorThr thr;
+  __shared__ int s_last;
+  __shared__ SelScratch sc;
+  __shared__ int sel[SEL_CAP];
+  const int b = blockIdx.y, tid = threadIdx.x, lane = tid & 63;
+  const int32_t* h = hist + (int64_t)b * 2 * kSampleBins;
+  anchor_thresholds(h, num_fg, batch, part, thr);
+  int32_t* base = ws + (int64_t)b * per;
+  uint32_t* kept = reinterpret_cast<uint32_t*>(base);
+  int32_t* cnt = base + NW;  // [0] fg boundary count, [1] bg, [2] done blocks
+  int32_t* list = cnt + 4;   // [2][kBoundCap]
+  const int32_t* lab = label_pre + (int64_t)b * N;
+  const float* key = keys + (int64_t)b * N;
+  const int t = blockIdx.x * 256 + tid;
+  bool take = false;
+  if (t < N) {
+    const int l = lab[t];
+    if (l == 0 || l == 1) {
+      const int p = l == 1 ? 0 : 1;
+      const int bin = sample_bin(key[t]);
+      if (bin < thr.tbin[p]) {
+        take = true;
+      } else if (bin == thr.tbin[p] && thr.rem[p] > 0) {
+        const int pos = atomicAdd(cnt + p, 1);
+        if (pos < kBoundCap) list[p * kBoundCap + pos] = t;
+      }
+    }
+  }
+  const unsigned long long m = __ballot(take);
+  if ((lane & 31) == 0 && t < N) {
+    const uint32_t wbits = (uint32_t)(m >> (lane & 32));
+    if (wbits) atomicOr(kept + (t >> 5), wbits);
+  }
+  // the last workgroup of this image resolves the boundary bins
+  __threadfence();
+  __syncthreads();
+  if (tid == 0) s_last = atomicAdd(cnt + 2, 1) == (int)gridDim.x - 1;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  for (int p = 0; p < 2; ++p) {
+    const int rem = thr.rem[p];
+    if (rem <= 0) continue;
+    const int c = atomicAdd(cnt + p, 0);
+    const int32_t* lp = list + p * kBoundCap;
+    if (c <= kBoundCap) {
+      for (int e = tid; e < c; e += 256) {
+        const int ie = lp[e];
+        const float ke = key[ie];
+        int r = 0;
+        for (int j = 0; j < c; ++j) {
+          const int ij = lp[j];
+          const float kj = key[ij];
+          r += (kj < ke) || (kj == ke && ij < ie);
+        }
+        if (r < rem) atomicOr(kept + (ie >> 5), 1u << (ie & 31));
+      }
+    } else {
+      const int lv = p == 0 ? 1 : 0, tb = thr.tbin[p];
+      const int got = select_smallest(N, c, rem, [&](int i) { return lab[i] == lv && sample_bin(key[i]) == tb; },
+                                      [&](int i) { return key[i]; }, sc, sel);
+      for (int e = tid; e < got; e += 256) atomicOr(kept + (sel[e] >> 5), 1u << (sel[e] & 31));
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    meta[b * 4 + 0] = thr.all_fg;
+    meta[b * 4 + 1] = thr.all_bg;
+    meta[b * 4 + 2] = thr.n_fg;
+    meta[b * 4 + 3] = thr.n_bg;
+  }
+}
+
+int64_t anchor_mark_ws_ints(int B, int64_t N) { return (int64_t)B * (div_up(N, 32) + 4 + 2 * kBoundCap); }
+
+void anchor_sample_hist(const int32_t* label_pre, const float* targets, const float* keys, const int32_t* hist,
+                        int B, int A, int H, int W, int num_fg, int batch, const float* inside_w, float pos_weight,
+                        int32_t* ws, int32_t* meta, int32_t* label, float* bbox_target, float* inside, float* outside,
+                        hipStream_t st) {
+  if (B == 0) return;
+  const int N = H * W * A;
+  const int NW = (int)div_up(N, 32);
+  const int64_t per = NW + 4 + 2 * kBoundCap;
+  anchor_mark_kernel<<<dim3((unsigned)div_up(N, 256), B), 256, 0, st>>>(label_pre, keys, hist, N, num_fg, batch, ws,
+                                                                        per, NW, meta);
+  const int64_t total = (int64_t)B * N;
+  anchor_output_kernel<<<div_up(total, 256), 256, 0, st>>>(label_pre, targets, reinterpret_cast<const uint32_t*>(ws),
+                                                           meta, B, A, H * W, inside_w[0], inside_w[1], inside_w[2],
+                                                           inside_w[3], pos_weight, label, bbox_target, inside,
+                                                           outside, per);
 }
 
 // ------------------------------------------------------------------------------- proposals

@@ -63,8 +63,10 @@ struct WgradParams {
   uint16_t* dw;
   int accumulate, NB, H, W, Cin, Ho, Wo, Cout, KW, stride, pad, tiles_n, ntiles, splits, per, nwg;
   FastDiv fd_hw, fd_w;
-  // fp32-class operands (common.h x2): dY and X are hi / lo plane pairs; the pixel loop runs three
-  // phases (dY_hi X_hi, dY_hi X_lo, dY_lo X_hi) and the gradient is fp32 (dwf instead of dw)
+  // fp32-class operands (common.h x2): dY and X are hi / lo plane pairs.  A stage then holds 32
+  // pixels of both planes (LDS rows 0-31 hi, 32-63 lo, the same pixels), read by the same
+  // fragment loads as a 64-pixel bf16 stage, and runs three MFMAs per fragment pair (dY_hi X_hi +
+  // dY_hi X_lo + dY_lo X_hi); the gradient is fp32 (dwf instead of dw)
   int x2 = 0;
   uint32_t x2_pdy = 0, x2_px = 0;  // lo-plane offsets, bytes
   float* dwf = nullptr;
@@ -72,8 +74,8 @@ struct WgradParams {
 
 constexpr int kWgradLdsElems = 3 * 2 * WG_BK * 64;  // the S = 3 ring: [S][dY|X][64 px][64 ch] (48 KB)
 
-// workgroup `wgid` of the launch; `lds`: S * 2 * 64 * 64 bf16 (16-B aligned)
-template <int S>
+// workgroup `wgid` of the launch; `lds`: S * 2 * 64 * 64 bf16 (16-B aligned); X2 must equal p.x2
+template <int S, bool X2 = false>
 __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const WgradParams& p) {
   constexpr int LPS = 4;  // DMA instructions per thread per stage (2 dY rows + 2 X rows)
   static_assert(S >= 2 && S <= 4, "pipeline depth");
@@ -96,30 +98,31 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
   const int steps_all = (P + WG_BK - 1) / WG_BK;
   const int s_begin = split * per, s_end = min(steps_all, s_begin + per);
   const int nsteps = max(0, s_end - s_begin);
-  const int nloop = p.x2 ? 3 * nsteps : nsteps;  // x2: the pixel range once per product phase
+  constexpr int PX = X2 ? WG_BK / 2 : WG_BK;  // pixels per stage
+  const int nloop = X2 ? 2 * nsteps : nsteps;
 
   // records through the lo planes for x2 pairs (the range check covers voffset + soffset)
   const __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)dy, (short)0, (int)((int64_t)P * Cout * 2 + (p.x2 ? p.x2_pdy : 0u)), 0x00020000);
+      (void*)dy, (short)0, (int)((int64_t)P * Cout * 2 + (X2 ? p.x2_pdy : 0u)), 0x00020000);
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)x, (short)0, (int)((int64_t)NB * H * W * Cin * 2 + (p.x2 ? p.x2_px : 0u)), 0x00020000);
-  int rowi[2], chk[2];
+      (void*)x, (short)0, (int)((int64_t)NB * H * W * Cin * 2 + (X2 ? p.x2_px : 0u)), 0x00020000);
+  int rowi[2], chk[2], prow[2];
   uint32_t a_off[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
-    rowi[i] = 32 * i + 8 * wid + (lane >> 3);
+    rowi[i] = 32 * i + 8 * wid + (lane >> 3);  // LDS row
+    prow[i] = X2 ? rowi[i] - 32 * i : rowi[i];  // pixel within the stage (x2: row 32 + r is pixel r's lo)
     chk[i] = (lane & 7) ^ wsw(rowi[i]);
-    a_off[i] = co0 + chk[i] * 8 < Cout ? (uint32_t)((rowi[i] * Cout + co0 + chk[i] * 8) * 2) : kWgOOB;
+    a_off[i] = co0 + chk[i] * 8 < Cout ? (uint32_t)((prow[i] * Cout + co0 + chk[i] * 8) * 2) : kWgOOB;
   }
   auto issue = [&](int it, int buf) {
-    const int ph = it / nsteps, sl = it - ph * nsteps;  // x2 phase, step within the range
-    const int p0 = (s_begin + sl) * WG_BK;
-    const uint32_t pdy = ph == 2 ? p.x2_pdy : 0u, px = ph == 1 ? p.x2_px : 0u;
+    const int p0 = s_begin * WG_BK + it * PX;
     uint16_t* Ab = lds + buf * 2 * WG_BK * 64;
     uint16_t* Bb = Ab + WG_BK * 64;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const int p = p0 + rowi[i];
+      const uint32_t pdy = X2 && i ? p.x2_pdy : 0u, px = X2 && i ? p.x2_px : 0u;
+      const int p = p0 + prow[i];
       const uint32_t va = p < P ? a_off[i] : kWgOOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(dyr, (__attribute__((address_space(3))) void*)(Ab + (32 * i + 8 * wid) * 64),
                                                16, (int)va, (int)((uint32_t)p0 * Cout * 2 + pdy), 0, 0);
@@ -192,22 +195,29 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
         : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]), "v"(ad[5]), "v"(ad[6]), "v"(ad[7]),
           "v"(ad[8]), "v"(ad[9]), "v"(ad[10]), "v"(ad[11]), "v"(ad[12]), "v"(ad[13]), "v"(ad[14]), "v"(ad[15])
         : "memory");
+    bf16x8 af[2][2], bfr[2][2];  // [kk][i]: x2 kk = plane (hi / lo of the same 32 pixels)
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[2], bfr[2];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
-        af[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(fr[kk * 8 + i * 2], fr[kk * 8 + i * 2 + 1], 0, 1, 2,
-                                                                   3, 4, 5, 6, 7));
+        af[kk][i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(fr[kk * 8 + i * 2], fr[kk * 8 + i * 2 + 1], 0,
+                                                                       1, 2, 3, 4, 5, 6, 7));
 #pragma unroll
       for (int j = 0; j < 2; ++j)
-        bfr[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(fr[kk * 8 + 4 + j * 2],
-                                                                    fr[kk * 8 + 4 + j * 2 + 1], 0, 1, 2, 3, 4, 5, 6, 7));
+        bfr[kk][j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(fr[kk * 8 + 4 + j * 2],
+                                                                        fr[kk * 8 + 4 + j * 2 + 1], 0, 1, 2, 3, 4, 5,
+                                                                        6, 7));
+    }
+    // products (a, b) per pass: bf16 (0,0) (1,1); x2 (hi,hi) (hi,lo) (lo,hi)
+    constexpr int NPASS = X2 ? 3 : 2;
+#pragma unroll
+    for (int ps = 0; ps < NPASS; ++ps) {
+      const int ka = X2 ? (ps == 2) : ps, kb = X2 ? (ps == 1) : ps;
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < 2; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ka][i], bfr[kb][j], acc[i][j], 0, 0, 0);
     }
   }
 

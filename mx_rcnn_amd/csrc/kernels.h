@@ -57,7 +57,8 @@ void anchor_target_assign(const float* base_anchors, int A, int H, int W, float 
                           const float* gt, const int32_t* n_gt, int G, int B,
                           float neg_thresh, float pos_thresh, int clobber_positives,
                           float* max_ov, int32_t* argmax, float* gt_max,
-                          int32_t* label, float* targets, hipStream_t st);
+                          int32_t* label, float* targets, hipStream_t st, const float* keys = nullptr,
+                          int32_t* hist = nullptr);
 
 // ---- fused target sampling (sample.hip) ------------------------------------
 // RPN: label_pre (B, N=H*W*A) in (h, w, a) order from anchor_target_assign, targets (B, N, 4), keys
@@ -67,6 +68,21 @@ void anchor_sample(const int32_t* label_pre, const float* targets, const float* 
                    int num_fg, int batch, const float* inside_w, float pos_weight, uint32_t* kept_ws,
                    int32_t* meta_ws, int32_t* label, float* bbox_target, float* inside, float* outside,
                    hipStream_t st);
+// Multi-workgroup form of anchor_sample (the same selection: the k smallest (key, index) of each
+// pool): `hist` (B, 2, kSampleBins) key histograms of the fg / bg pools from anchor_target_assign's
+// second pass (keys + hist given); `ws`: anchor_mark_ws_ints(B, N) zeroed int32 (kept bitmap,
+// boundary lists, counters).  Launches the mark kernel (its last workgroup per image ranks the
+// boundary bin) and the output kernel.
+constexpr int kSampleBins = 4096;
+__host__ __device__ inline int sample_bin(float key) {
+  const int b = (int)(key * (float)kSampleBins);
+  return b < 0 ? 0 : (b >= kSampleBins ? kSampleBins - 1 : b);
+}
+int64_t anchor_mark_ws_ints(int B, int64_t N);
+void anchor_sample_hist(const int32_t* label_pre, const float* targets, const float* keys, const int32_t* hist,
+                        int B, int A, int H, int W, int num_fg, int batch, const float* inside_w, float pos_weight,
+                        int32_t* ws, int32_t* meta, int32_t* label, float* bbox_target, float* inside, float* outside,
+                        hipStream_t st);
 // R-CNN: rois (B, P, 5), gt (B, G, 5), n_gt (B), max_ov / argmax (B, P) vs gt, rnd (B, 2(P+G)+R).
 // Returns -1 when the shape exceeds the kernel's LDS plan.
 size_t proposal_sample_lds(int P, int G, int R, int F);
@@ -220,6 +236,15 @@ struct ConvEpi {
   int64_t x2_py = 0;              // lo-plane offset of y, y2, residual and bnb_x, elements
   int64_t x2_pd = 0;              // lo-plane offset of dadd, elements
   float* yf = nullptr;            // fp32 output instead of y (no y2): the x2 mode's prediction heads
+  // data gradient straight from the forward filter (Cin, KH, KW, Cout) -- no flipped / transposed
+  // copy; the launch's Cin / Cout are the dgrad's (the filter's output / input channels), the taps
+  // are flipped in-kernel (buffer kernels 22 / 23 and the grouped launch)
+  int bt = 0;
+  // ReLU (+ inverted dropout) backward fused into a data gradient: y = v * [rmask > 0] * rmask_s, where
+  // rmask (shaped like y, bf16; x2: its hi plane) is the ReLU / dropout OUTPUT of the previous layer,
+  // i.e. this data gradient's forward input (plain epilogue only: no bnb_x / y2)
+  const uint16_t* rmask = nullptr;
+  float rmask_s = 1.f;
 };
 // counter-based uniform in [0, 1) (Philox-4x32-10, key = (seed, 0x9E3779B9), counter = (e, s))
 float philox_uniform_host(uint32_t seed, uint64_t step, uint64_t e);
@@ -354,6 +379,7 @@ struct HeadBwdArgs {
   float* ws_db[2] = {nullptr, nullptr};
   uint16_t* dx = nullptr;
   int relu_mask = 0;
+  float mask_scale = 1.f;  // kept dX values are scaled (inverted dropout after the masked ReLU)
   int nheads = 1;
   int rs = 1;
   // fp32-class mode: X / W / dX are x2 hi / lo pairs (X's and dX's lo planes M * K on, W_h's w_plane[h]
@@ -363,6 +389,9 @@ struct HeadBwdArgs {
   float* dwf[2] = {nullptr, nullptr};
   int64_t w_plane[2] = {0, 0};
 };
+// out = dy * [y > 0] * scale (bf16, n % 8 == 0; x2: plane = n, dy / out hold both planes)
+void relu_mask(const uint16_t* dy, const uint16_t* y, uint16_t* out, int64_t n, int64_t plane, float scale,
+               hipStream_t st);
 int head_bwd_splits(int M, int K, const int* N, int nheads);
 int head_bwd(const uint16_t* x, int M, int K, const HeadBwdArgs& a, hipStream_t st);
 // per-channel sum of x (M, C) (bf16 / fp16 by code) into out (C) fp32 / bf16 by out_code (+= when

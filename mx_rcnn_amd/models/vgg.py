@@ -8,6 +8,7 @@ import torch.nn as nn
 from .layers import Conv, Linear, max_pool
 from ..ops.head import fc_pair
 from ..ops.stem import stem_fusable, stem_conv
+from ..ops import vgg_fused
 
 VGG_CFG = [(1, 2, 3, 64), (2, 2, 64, 128), (3, 3, 128, 256), (4, 3, 256, 512), (5, 3, 512, 512)]
 
@@ -26,6 +27,8 @@ class VGG16Trunk(nn.Module):
             self.pool_after.append(len(self.convs) - 1 if g < 5 else -1)
 
     def forward(self, x):
+        if vgg_fused.trunk_ok(x, self.convs):  # one autograd node, ReLU backward in the dgrad epilogues
+            return vgg_fused.vgg_trunk(x, self.convs, self.pool_after)
         for i, c in enumerate(self.convs):
             if i == 0 and stem_fusable(x, c.weight, c.bias):  # one HIP launch (ops/stem.py)
                 x = stem_conv(x, c.weight, 1, 1, bias=c.bias, relu=True)
@@ -54,6 +57,8 @@ class VGGHead(nn.Module):
 
     def forward(self, pooled):
         x = pooled.reshape(pooled.shape[0], -1)  # MXNet Flatten: (C, H, W) order
+        if vgg_fused.head_ok(x, self):
+            return vgg_fused.vgg_head(x, self)
         # relu6/drop6 and relu7/drop7 run in the FC kernel's epilogue (ops/fc.py)
         x = self.fc6(x, relu=True, drop_p=self.dropout)
         x = self.fc7(x, relu=True, drop_p=self.dropout)

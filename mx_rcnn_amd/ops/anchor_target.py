@@ -7,6 +7,8 @@ inside anchors, label rules, encode); fg/bg subsampling is a device random-rank 
 Output layout matches the reference: label (B, A*H*W) in (a, h, w) order; bbox_target /
 inside / outside weights (B, 4A, H, W).
 """
+import os
+
 import numpy as np
 import torch
 
@@ -70,6 +72,19 @@ def anchor_target(feat_shape, gt_boxes, n_gt, im_info, feat_stride=16, scales=(8
     n_gt = n_gt.to(torch.int32).contiguous()
     with torch.no_grad():
         num_fg = int(cfg.TRAIN.RPN_FG_FRACTION * cfg.TRAIN.RPN_BATCH_SIZE)
+        if gt_boxes.is_cuda and os.environ.get('MXR_ANCHOR_FUSED', '1') != '0':
+            # assignment + subsampling + layout in four grid-wide launches (csrc/hip/sample.hip
+            # anchor_mark: histogram thresholds instead of a one-workgroup selection pass)
+            C = need_ext()
+            keys = torch.rand((B, H * W * A), device=dev, generator=generator)
+            iw = [float(v) for v in np.asarray(cfg.TRAIN.RPN_BBOX_INSIDE_WEIGHTS, dtype=np.float64).ravel()[:4]]
+            lab, bt, inside, outside, meta = C.anchor_target_fused(
+                base, H, W, float(feat_stride), im_info.float().contiguous(), int(allowed_border),
+                gt_boxes.float().contiguous(), n_gt, float(cfg.TRAIN.RPN_NEGATIVE_OVERLAP),
+                float(cfg.TRAIN.RPN_POSITIVE_OVERLAP), bool(cfg.TRAIN.RPN_CLOBBER_POSITIVES), keys, num_fg,
+                int(cfg.TRAIN.RPN_BATCH_SIZE), iw, float(cfg.TRAIN.RPN_POSITIVE_WEIGHT))
+            return {'label': lab, 'bbox_target': bt, 'bbox_inside_weight': inside, 'bbox_outside_weight': outside,
+                    'sample_meta': meta}
         if gt_boxes.is_cuda:
             C = need_ext()
             label, targets, _, _ = C.anchor_target_assign(

@@ -5,8 +5,8 @@
   for the latency-bound small-M shapes of 1-image detection (the LDS-DMA kernel beats
   hipBLASLt on every trunk 1x1 shape, tools/microbench/conv_tiles.py); strided 1x1 convs
   subsample first.
-* Backward: stride-1 data gradient = the same kernel on dY with the flipped/transposed
-  filter (pad' = k-1-pad); weight gradient = the MFMA wgrad kernel (csrc/hip/conv_wgrad.hip),
+* Backward: stride-1 data gradient = the same kernel on dY reading the forward filter
+  transposed with flipped taps (pad' = k-1-pad, ConvEpi::bt); weight gradient = the MFMA wgrad kernel (csrc/hip/conv_wgrad.hip),
   which ACCUMULATES straight into the parameter's flat-buffer gradient view when the
   parameter is managed by the FlatParamStore (ops/grad_sink.py: no AccumulateGrad add);
   strided data gradients are parity-decomposed into s*s stride-1 convs of dy written straight
@@ -99,6 +99,28 @@ def dgrad_weight(param, w):
     if precision.x2_enabled():  # the flipped fp32 filter as a pair
         return precision.split(_flip_t(w.detach().float()))
     return _flip_t(w)
+
+
+def dgrad_bt_enabled():
+    """Stride-1 data gradients read the forward filter transposed in-kernel (ConvEpi::bt) instead
+    of a flipped / transposed copy rebuilt after every update (``MXR_DGRAD_BT=0``: the copy)."""
+    return os.environ.get('MXR_DGRAD_BT', '1') != '0'
+
+
+def dgrad_args(param, w):
+    """(filter, conv kwargs) of a stride-1 data-gradient launch for the conv with weight ``w``
+    (the tensor its forward used: the bf16 shadow, or in the x2 mode the fp32 parameter)."""
+    x2 = precision.x2_enabled()
+    if dgrad_bt_enabled():
+        if x2:
+            wh, wpl = precision.weight_pair(w)
+            return wh, {'x2': True, 'w_plane': wpl, 'bt': True}
+        return w.contiguous(memory_format=torch.channels_last), {'bt': True}
+    wf = dgrad_weight(param, w)
+    if x2:
+        wh, wpl = pair_args(wf)
+        return wh, {'x2': True, 'w_plane': wpl}
+    return wf, {}
 
 
 def pair_args(wpair):
@@ -217,11 +239,7 @@ def conv_backward(x, w, param, dy, stride, pad, has_bias, need_x, need_w, need_b
     if tgt is not None:
         x = x.contiguous(memory_format=torch.channels_last)
         dy = dy.contiguous(memory_format=torch.channels_last)
-        wf = dgrad_weight(param, w)
-        wk = {}
-        if x2:
-            wf, wpl = pair_args(wf)
-            wk = dict(x2=True, w_plane=wpl)
+        wf, wk = dgrad_args(param, w)
         dx = need_ext().conv_dgrad_wgrad(dy, wf, kh - 1 - pad, None, None, 0.0, False, None,
                                          None, None, None, dy, x, kh, kh, 1, pad, tgt, **wk)[0]
         if has_bias and need_b:
@@ -241,11 +259,7 @@ def conv_backward(x, w, param, dy, stride, pad, has_bias, need_x, need_w, need_b
             dw, db = _wgrad(x, w, param, dy, stride, pad, has_bias, need_w, need_b, bparam)
     if need_x:
         if stride == 1 and w.shape[0] % 64 == 0 and 2 * pad == kh - 1:
-            wf = dgrad_weight(param, w)
-            wk = {}
-            if x2:
-                wf, wpl = pair_args(wf)
-                wk = dict(x2=True, w_plane=wpl)
+            wf, wk = dgrad_args(param, w)
             dx = need_ext().conv_igemm_fwd(dy, wf, None, 1, kh - 1 - pad, False, **wk)[0]
         elif (stride > 1 and w.shape[0] % 64 == 0 and w.shape[1] % 8 == 0 and kh == w.shape[3] and
               strided_dgrad_ok(kh, stride, pad, x.shape[2], x.shape[3])):

@@ -34,14 +34,6 @@ def _wargs(w):
     return w, {}
 
 
-def _dargs(wf):
-    """The same for a flipped dgrad filter (a pair in the x2 mode)."""
-    if precision.x2_enabled():
-        wh, wpl = pair_args(wf)
-        return wh, {'x2': True, 'w_plane': wpl}
-    return wf, {}
-
-
 def _rows(t):
     """Logical rows (N*H*W) of an activation (pairs: half the tensor)."""
     n = t.numel() // t.shape[1]
@@ -495,9 +487,9 @@ class _FusedUnitFn(torch.autograd.Function):
             """dgrad of a stride-1 conv with the BN(bn_i)-ReLU backward of its input in the epilogue;
             with ``wg`` the weight gradient of a conv (idx, dy, inp, k, stride, pad) in the SAME launch
             (csrc/hip/conv_igemm.hip conv_dgrad_wgrad), otherwise on the side stream."""
-            from .conv import dgrad_weight
+            from .conv import dgrad_args
             tg, tb, ret = bn_targets(bn_i)
-            wf, wkw = _dargs(dgrad_weight(ctx.params[w_idx], ws[w_idx]))
+            wf, wkw = dgrad_args(ctx.params[w_idx], ws[w_idx])
             tgt = grouped_target(wg)
             part, nparts = None, 0
             if train:
@@ -599,8 +591,8 @@ class _FusedUnitFn(torch.autograd.Function):
         d_sc = None
         if not spec.dim_match:
             wgrad(nconv - 1, d_out, act1, 1, s, 0)
-            from .conv import dgrad_weight
-            wsc, wkw = _dargs(dgrad_weight(ctx.params[nconv - 1], ws[nconv - 1]))
+            from .conv import dgrad_args
+            wsc, wkw = dgrad_args(ctx.params[nconv - 1], ws[nconv - 1])
             d_sub = ext.conv_igemm_fwd(d_out, wsc, None, 1, 0, False, **wkw)[0]
             if s == 1 or (s1 == 1 and ws[0].shape[0] % 64 == 0 and
                           os.environ.get('MXR_SUB_DADD', '1') != '0'):

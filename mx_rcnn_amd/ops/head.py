@@ -58,7 +58,7 @@ def _mat_w(w):
     return w.reshape(w.shape[0], -1), 0
 
 
-def _pair_backward(x2, dys, ws, wparams, bparams, need_w, need_b, need_dx, relu_mask):
+def _pair_backward(x2, dys, ws, wparams, bparams, need_w, need_b, need_dx, relu_mask, mask_scale=1.0):
     """-> (dx (M, K) or None, [dW_h or None], [db_h or None]); gradients with a flat-buffer target
     are accumulated there and returned as None (grad_sink)."""
     ext = need_ext()
@@ -95,7 +95,7 @@ def _pair_backward(x2, dys, ws, wparams, bparams, need_w, need_b, need_dx, relu_
             db_ret.append(None)
     wm = [_mat_w(w) for w in ws]
     dx = ext.head_bwd(x2, [_mat(d).to(gdt) for d in dys], [m[0] for m in wm], dws, dw_acc, dbs, db_acc, bool(need_dx),
-                      bool(relu_mask), xp, [m[1] for m in wm])
+                      bool(relu_mask), xp, [m[1] for m in wm], float(mask_scale))
     db_ret = [d.to(bparams[h].dtype) if (d is not None and bparams[h] is not None) else d
               for h, d in enumerate(db_ret)]
     return (dx if need_dx else None), dw_ret, db_ret

@@ -359,6 +359,38 @@ def test_proposal_sample_fused_semantics(cuda):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('H,W,A,ngt,batch', [(50, 84, 12, 6, 256), (38, 63, 9, 3, 256), (20, 30, 9, 30, 1024),
+                                             (12, 16, 9, 2, 1024), (50, 84, 12, 0, 256)])
+def test_anchor_target_multi_workgroup_matches_single(cuda, H, W, A, ngt, batch, monkeypatch):
+    """The grid-wide histogram / mark selection (MXR_ANCHOR_FUSED=1) picks exactly the anchors of the
+    one-workgroup select_smallest path for the same keys: bitwise equal outputs, over seeds, ResNet
+    (12 anchors) and VGG (9) maps, all-bg / all-fg pools (RPN batch 1024) and images without gt."""
+    from mx_rcnn_amd.config import snapshot
+    cfg = snapshot()
+    cfg.TRAIN.RPN_BATCH_SIZE = batch
+    g = torch.Generator().manual_seed(H * W + ngt)
+    gt = torch.full((2, max(ngt, 1), 5), -1.0)
+    if ngt:
+        xy = torch.rand(2, ngt, 2, generator=g) * torch.tensor([W * 16 - 100, H * 16 - 100])
+        wh = torch.rand(2, ngt, 2, generator=g) * 200 + 40
+        gt[:, :ngt, :2] = xy
+        gt[:, :ngt, 2:4] = xy + wh
+        gt[:, :ngt, 4] = 1
+    n_gt = torch.tensor([ngt, max(ngt - 1, 0)], dtype=torch.int32)
+    im_info = torch.tensor([[H * 16.0, W * 16.0, 1.0], [H * 16.0 - 40, W * 16.0 - 60, 1.0]])
+    scales = (4, 8, 16, 32) if A == 12 else (8, 16, 32)
+    for seed in range(3):
+        outs = []
+        for fused in ('1', '0'):
+            monkeypatch.setenv('MXR_ANCHOR_FUSED', fused)
+            gen = torch.Generator(device=cuda).manual_seed(seed)
+            outs.append(ops.anchor_target((H, W), gt.to(cuda), n_gt.to(cuda), im_info.to(cuda), scales=scales,
+                                          cfg=cfg, generator=gen))
+        for k in ('label', 'bbox_target', 'bbox_inside_weight', 'bbox_outside_weight', 'sample_meta'):
+            assert torch.equal(outs[0][k], outs[1][k]), (seed, k)
+
+
+@pytest.mark.gpu
 def test_anchor_sample_fused_counts_and_uniformity(cuda):
     """Fused RPN subsampling: exact counts, labels only from the pre-sampling pools, reference
     weights, and uniform selection frequency over many draws."""

@@ -1,0 +1,71 @@
+"""The data-parallel step on the GPU: a 1-rank RCCL (backend 'nccl') process group, with every
+gradient bucket all-reduced inside the captured hipGraph (fp32 wire), must produce the same
+weights as the same graphed step without a process group (reference semantics: kvstore 'device'
+sums gradients, `train_end2end.py:150`; one rank sums one term).
+
+Each configuration runs in its own process (tools/dp_step_check.py): a process group cannot be
+torn down and re-created cleanly inside one process, and the non-DP step must not see one.
+"""
+import os
+import subprocess
+import sys
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run(tmp_path, name, precision, dp, port, steps):
+    out = str(tmp_path / (name + '.pt'))
+    env = dict(os.environ)
+    for k in ('MXR_FORCE_DIST', 'WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
+        env.pop(k, None)
+    # the per-shape conv autotune picks split-K variants by timing, i.e. per process: fix the plan
+    env['MXR_CONV_TUNE'] = '0'
+    if dp:
+        env.update({'MXR_FORCE_DIST': '1', 'WORLD_SIZE': '1', 'RANK': '0', 'LOCAL_RANK': '0',
+                    'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port)})
+    r = subprocess.run([sys.executable, os.path.join(ROOT, 'tools', 'dp_step_check.py'), out, '--precision', precision,
+                        '--steps', str(steps)],
+                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:]
+    return torch.load(out, weights_only=True), r.stdout
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('precision', ['bf16', 'fp32'])
+def test_rccl_one_rank_graphed_step_matches_single_process(tmp_path, precision):
+    """One graphed step (fresh momentum: the update is lr * clip(grad) + wd term, so any gradient
+    difference shows directly).  Every weight whose plain step is bitwise reproducible must match
+    bitwise (bf16: all weights); BN gamma / beta (fp32 atomics in the conv epilogues' column sums)
+    and, in fp32-class mode, the layers below the RoI pooling (LDS float atomics in its backward)
+    within the plain run-to-run spread.  The conv autotune is off (its timing-based split-K choices
+    differ between processes)."""
+    a, _ = _run(tmp_path, 'plain', precision, False, 0, 1)
+    b, _ = _run(tmp_path, 'plain2', precision, False, 0, 1)
+    d, log = _run(tmp_path, 'dp', precision, True, 29650 + (precision == 'fp32'), 1)
+    assert int(a['_dp'][0]) == 0
+    assert int(d['_dp'][0]) == 1 and int(d['_dp'][1]) >= 1, log  # the reducer really ran its buckets
+    keys = [k for k in a if not k.startswith('_')]
+    assert keys and set(keys) == {k for k in d if not k.startswith('_')}
+    # BN gamma / beta gradients of the frozen-statistics units are column sums accumulated with
+    # fp32 atomics in the conv epilogues: their order (and last bit) varies run to run
+    atomic = [k for k in keys if k.endswith(('_gamma', '_beta'))]
+    exact = [k for k in keys if k not in atomic]
+    # fp32-class: the RoI-pool backward sums its LDS gradient slab with float atomics, so everything
+    # below the RoI pooling varies in the last bits run to run (the bf16 store rounds that away)
+    nondet = [k for k in exact if not torch.equal(a[k], b[k])]
+    print('%s: %d arrays, %d atomics-summed, plain run-to-run differences outside them: %d %s' % (
+        precision, len(keys), len(atomic), len(nondet), nondet[:4]))
+    if precision == 'bf16':
+        assert not nondet
+    det = [k for k in exact if k not in nondet]
+    assert len(det) > 20
+    diff = [k for k in det if not torch.equal(a[k], d[k])]
+    assert not diff, 'DP step differs: %s (max abs %s)' % (
+        diff[:5], [float((a[k].float() - d[k].float()).abs().max()) for k in diff[:5]])
+    for k in atomic + nondet:
+        spread = float((a[k] - b[k]).abs().max())
+        tol = 4 * spread + 1e-6 * (1.0 + float(a[k].abs().max()))
+        assert float((a[k] - d[k]).abs().max()) <= tol, k

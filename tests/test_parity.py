@@ -149,7 +149,7 @@ def test_rcnn_step_bf16_gpu_matches_fp32_cpu(cuda):
     _check_grads(gc, gg, 0.30)
 
 
-def _check_grads_tight(gc, gg, cos_min=0.99, rel_max=0.02):
+def _check_grads_tight(gc, gg, cos_min=0.99, rel_max=0.02, min_layers=10):
     """fp32-class contract: EVERY layer with a non-negligible gradient has cosine >= cos_min and
     norm within rel_max of the fp32 CPU step.  (The R-CNN step's deepest BN betas sit at cosine
     ~0.998 / norm ~1 %: a ReLU whose pre-activation is within rounding of zero flips between ANY
@@ -167,7 +167,7 @@ def _check_grads_tight(gc, gg, cos_min=0.99, rel_max=0.02):
         assert cos >= cos_min and rel <= rel_max, (n, cos, rel)
     worst.sort()
     print('fp32 mode: %d layers, worst cosine %s' % (len(worst), worst[:3]))
-    assert len(worst) > 10
+    assert len(worst) >= min_layers
 
 
 def test_rpn_step_fp32_gpu_matches_fp32_cpu(cuda):

@@ -878,6 +878,19 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
     if (!(t == 22 || t == 23 || t >= 100)) t = 23;
     sp = 1;
   }
+  // fp32-class pairs: a grid of about one 64-row tile per CU (the batch-1 stage-3 convs) leaves each
+  // CU latency-bound on its operand ring; MXR_X2_SPLITK=s splits K s ways while the grid has fewer
+  // than two tiles per CU (A/B knob)
+  static const int x2_split = [] {
+    const char* e = getenv("MXR_X2_SPLITK");
+    return e != nullptr ? std::max(1, atoi(e)) : 1;
+  }();
+  if (x2 && x2_split > 1 && tile <= 0 && splits <= 0 && !bwd_mode && !stats && !mapped && ep.pad_w < 0 &&
+      Cout % 4 == 0) {
+    const int bm = t == 22 ? 128 : 64;
+    const int64_t blocks = (((int64_t)NB * Ho * Wo + bm - 1) / bm) * ((Cout + 63) / 64);
+    if (blocks < 512 && KH * KW * Cin / 32 >= 8 * x2_split) sp = std::max(sp, x2_split);
+  }
   if (tile <= 0 && splits <= 0 && !mapped && ep.pad_w < 0 && !ep.bnb_part && conv_tune_enabled()) {
     char kb[256];
     snprintf(kb, sizeof(kb), "%d,%d,%d,%d,%d,%d,%d,%d,%d|%d%d%d%d%d%d%d%d%d%d", NB, H, W, Cin, Cout, KH, KW, (int)stride,

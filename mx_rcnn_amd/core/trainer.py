@@ -20,13 +20,14 @@ class Trainer:
                  bucket_mb=25, average_grads=False, channels_last=None, grad_comm_dtype=None, precision=None):
         """precision: 'bf16' (bf16 operands, fp32 accumulation / masters), or 'fp32': the reference's
         precision class on the GPU -- every MFMA operand an x2 hi / lo bf16 pair, products as three
-        bf16 MFMAs with fp32 accumulation, fp32 gradients (ops/precision.py).  Default: bf16 on the
+        bf16 MFMAs with fp32 accumulation, fp32 gradients (ops/precision.py); 'torch': plain fp32
+        PyTorch / vendor ops on the GPU (a reference arm for precision probes).  Default: bf16 on the
         GPU unless compute_dtype says fp32; the CPU path is plain fp32."""
         dev = torch.device(device) if device is not None else next(model.parameters()).device
         if precision is None:
             precision = 'fp32' if (compute_dtype == torch.float32 and dev.type == 'cuda') else 'bf16'
         self.x2 = precision == 'fp32' and dev.type == 'cuda'
-        if self.x2:
+        if self.x2 or precision == 'torch':
             compute_dtype = torch.float32
         if compute_dtype is None:
             compute_dtype = torch.bfloat16 if dev.type == 'cuda' else torch.float32

@@ -1139,167 +1139,6 @@ conv_igemm_buf_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
                                          tiles_n, nwg, ntiles, splits, slab);
 }
 
-// ---- register-pipelined kernel: operands straight from memory into MFMA fragments ----------
-// The LDS-DMA kernels above keep at most two 16 KB stages in flight per CU; on the batch-1
-// stage-3 grids (about one 64x64 tile per CU) every stage then waits out a full memory round trip
-// (~2 us under load) for 8-12 MFMAs per wave.  The MFMA 16x16x32 operand of a lane is 8
-// consecutive channels of one pixel (A) or one output channel (B) -- 16 contiguous bytes of the
-// NHWC activation / the K-contiguous filter -- so each wave can fetch its fragments itself with one
-// 16-B buffer load each, no LDS, no barriers, and keep D K-steps of them in flight in VGPRs (D * 8
-// KB per wave, four waves per workgroup).  Waves sharing rows / columns re-read them through L1 /
-// L2.  A K-step is 64 channels (two 32-channel halves), or in the x2 mode 32 channels of both
-// planes (three MFMAs per fragment pair).  Padding taps and rows / columns beyond the grid use the
-// buffer range check as in the buffer kernel.  The epilogue stages the tile through LDS.
-typedef int32_t i32x4v __attribute__((ext_vector_type(4)));
-
-template <int TM, int TN, int D, bool X2>
-__global__ void __launch_bounds__(256)
-conv_reg_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int NB,
-                int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad,
-                const ConvEpi ep, int tiles_n, int nwg, int ntiles, int splits, float* __restrict__ slab) {
-  constexpr int WM = 16 * TM, WN = 16 * TN, BM = 2 * WM, BN = 2 * WN;
-  __shared__ __attribute__((aligned(16))) float T[BM * (BN + 4)];
-  const int bid = blockIdx.x;
-  const int q = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
-  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + bid / 8;
-  const int split = wgid / ntiles, tile = wgid % ntiles;
-  const int m0 = (tile / tiles_n) * BM, n0 = (tile % tiles_n) * BN;
-  const int M = NB * Ho * Wo;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int K = KH * KW * Cin;
-  const int g = lane >> 4;
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)x, (short)0, (int)((int64_t)NB * H * W * Cin * 2 + (X2 ? ep.x2_pa : 0u)), 0x00020000);
-  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)w, (short)0, (int)((int64_t)Cout * K * 2 + (X2 ? ep.x2_pb : 0u)), 0x00020000);
-  // per lane: TM A rows (pixel offset at tap (0, 0) + channel chunk g, tap mask), TN B rows
-  uint32_t a_off[TM];
-  uint64_t a_mask[TM];
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = m0 + wm * WM + i * 16 + (lane & 15);
-    a_off[i] = 0;
-    a_mask[i] = 0;
-    if (m < M) {
-      const int img = m / (Ho * Wo), rem = m % (Ho * Wo);
-      const int hi0 = (rem / Wo) * stride - pad, wi0 = (rem % Wo) * stride - (ep.pad_w >= 0 ? ep.pad_w : pad);
-      a_off[i] = (uint32_t)(((((int64_t)img * H + hi0) * W + wi0) * Cin + g * 8) * 2);
-      for (int fr = 0; fr < KH; ++fr)
-        for (int fc = 0; fc < KW; ++fc)
-          if ((unsigned)(hi0 + fr) < (unsigned)H && (unsigned)(wi0 + fc) < (unsigned)W)
-            a_mask[i] |= 1ull << (fr * KW + fc);
-    }
-  }
-  uint32_t b_off[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * WN + j * 16 + (lane & 15);
-    b_off[j] = n < Cout ? (uint32_t)(((int64_t)n * K + g * 8) * 2) : kBufOOB;
-  }
-  constexpr int KC = X2 ? 32 : 64;  // channels per K-step
-  const uint32_t da = X2 ? ep.x2_pa : 64u, db = X2 ? ep.x2_pb : 64u;  // second half of a step's fragment
-  const int cin_steps = Cin / KC;
-  const int nk_all = KH * KW * cin_steps;
-  const int per = (nk_all + splits - 1) / splits;
-  const int k_begin = split * per;
-  const int nk = max(0, min(nk_all, k_begin + per) - k_begin);
-  int c_tap = k_begin / cin_steps, c_ci = (k_begin % cin_steps) * KC;
-  int c_fr = c_tap / KW, c_fc = c_tap % KW;
-
-  // every step issues the same loads unconditionally (steps past the range read zeros through the
-  // range check): the compiler's vmcnt accounting then stays exact across the unrolled ring -- with
-  // conditional issue it must assume the fewest loads in flight and waits for all of them
-  i32x4v ra[D][2][TM], rb[D][2][TN];
-  auto issue = [&](i32x4v (&fa)[2][TM], i32x4v (&fb)[2][TN], bool valid) {
-    // offsets by mask arithmetic, not selects: the compiler turns selects feeding loads into
-    // branches around the loads, and a load on one path only forces a full vmcnt drain at the join
-    const uint32_t tap_a = (uint32_t)((c_fr * W + c_fc) * Cin * 2);
-    const uint32_t soff_a = (uint32_t)(c_ci * 2), soff_b = (uint32_t)((c_tap * Cin + c_ci) * 2);
-    const uint32_t vm = 0u - (uint32_t)valid;  // all ones when the step is in range
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const uint32_t m = vm & (0u - (uint32_t)((a_mask[i] >> c_tap) & 1ull));
-      const uint32_t vo = ((a_off[i] + tap_a) & m) | (kBufOOB & ~m);
-      fa[0][i] = __builtin_amdgcn_raw_buffer_load_b128(xr, (int)vo, (int)soff_a, 0);
-      fa[1][i] = __builtin_amdgcn_raw_buffer_load_b128(xr, (int)(vo + (da & m)), (int)soff_a, 0);
-    }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const uint32_t m = vm & (0u - (uint32_t)(b_off[j] != kBufOOB));
-      const uint32_t vb = (b_off[j] & m) | (kBufOOB & ~m);
-      fb[0][j] = __builtin_amdgcn_raw_buffer_load_b128(wr, (int)vb, (int)soff_b, 0);
-      fb[1][j] = __builtin_amdgcn_raw_buffer_load_b128(wr, (int)(vb + (db & m)), (int)soff_b, 0);
-    }
-    if (!valid) return;
-    c_ci += KC;
-    if (c_ci == Cin) {
-      c_ci = 0;
-      ++c_tap;
-      if (++c_fc == KW) {
-        c_fc = 0;
-        ++c_fr;
-      }
-    }
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int s = 0; s < D - 1; ++s) issue(ra[s], rb[s], s < nk);
-  const int nk_pad = (nk + D - 1) / D * D;  // zero steps past nk add nothing
-  for (int k0 = 0; k0 < nk_pad; k0 += D) {
-#pragma unroll
-    for (int u = 0; u < D; ++u) {
-      issue(ra[(u + D - 1) % D], rb[(u + D - 1) % D], k0 + u + D - 1 < nk);
-      // products per step: bf16 (half 0)(half 1); x2 (hi,hi) (hi,lo) (lo,hi)
-      constexpr int NPASS = X2 ? 3 : 2;
-#pragma unroll
-      for (int ps = 0; ps < NPASS; ++ps) {
-        const int ka = X2 ? (ps == 2) : ps, kb = X2 ? (ps == 1) : ps;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ra[u][ka][i]),
-                                                                __builtin_bit_cast(bf16x8, rb[u][kb][j]), acc[i][j], 0,
-                                                                0, 0);
-      }
-    }
-  }
-  if (Cout % 8 == 0)
-    igemm_epilogue_lds<BM, BN, TM, TN, WM, WN, X2>(acc, T, m0, n0, wm, wn, lane, tid, M, Cout, ep, y, split, splits,
-                                                   slab, Ho, Wo);
-  else
-    igemm_epilogue<TM, TN, WM, WN, X2>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab, Ho, Wo);
-}
-
-template <int TM, int TN, int D>
-static void launch_reg(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho,
-                       int Wo, int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int splits,
-                       float* slab, hipStream_t st) {
-  constexpr int BM = 32 * TM, BN = 32 * TN;
-  const int M = NB * Ho * Wo;
-  const int tiles_n = (Cout + BN - 1) / BN, ntiles = ((M + BM - 1) / BM) * tiles_n, nwg = ntiles * splits;
-  if (ep.x2)
-    conv_reg_kernel<TM, TN, D, true><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
-                                                          ep, tiles_n, nwg, ntiles, splits, slab);
-  else
-    conv_reg_kernel<TM, TN, D, false><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad,
-                                                           ep, tiles_n, nwg, ntiles, splits, slab);
-  if (splits > 1) {
-    const int64_t MN = (int64_t)M * Cout;
-    if (ep.bnb_x)
-      splitk_reduce_bnb_kernel<<<dim3(div_up(Cout, 64), div_up(M, 64)), 256, 0, st>>>(slab, splits, M, Cout, ep, y);
-    else
-      splitk_reduce_kernel<<<div_up((MN + 3) / 4, 256), 256, 0, st>>>(slab, splits, MN, Cout, ep, y);
-  }
-}
-
 // ---- tile-balanced LDS-DMA ring (the production path) ----------------------------------------
 // Measured on the ResNet-101 C4 stage-3/4 shapes (rocprofv3 --pmc, profiles/r2_conv_pmc.txt): the
 // 64x64 ring above is limited by what ONE CU can pull into LDS (~27 GB/s at two 16 KB stages in
@@ -1701,7 +1540,11 @@ static void launch_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB
     if (ep.f16)
       conv_igemm_buf_kernel<BM, BN, S, true><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
                                                                  pad, ep, tiles_n, nwg, ntiles, splits, slab);
-    else if (ep.x2 || ep.bt) {
+    else if (ep.x2 && !ep.bt && ((S == 3 && BN == 128) || S == 4)) {
+      if constexpr ((S == 3 && BN == 128 && BM == 128) || (S == 4 && BN == 64 && (BM == 64 || BM == 128)))
+        conv_igemm_buf_kernel<BM, BN, S, false, true, false><<<nwg, 256, 0, st>>>(
+            x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, tiles_n, nwg, ntiles, splits, slab);
+    } else if (ep.x2 || ep.bt) {
       if constexpr (S == 3 && BN == 64 && (BM == 64 || BM == 128)) {
 #define MXR_BUF_LAUNCH(X, B)                                                                                        \
   conv_igemm_buf_kernel<BM, BN, S, false, X, B><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, \
@@ -1735,7 +1578,7 @@ float philox_uniform_host(uint32_t seed, uint64_t step, uint64_t e) { return phi
 int conv_tile_bm(int tile) {
   if (tile >= 100 && tile < 100 + kNumRing) return kRingShapes[tile - 100].bm;
   switch (tile) {
-    case 1: case 2: case 11: case 12: case 14: case 15: case 21: case 22: case 31: case 32: case 41: return 128;
+    case 1: case 2: case 11: case 12: case 14: case 15: case 21: case 22: case 31: case 32: return 128;
     case 24: return 32;
     default: return 64;
   }
@@ -1799,11 +1642,11 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
   if ((ep.st_part || ep.bnb_part) && tile < 21) return -1;  // needs the buffer / ring epilogue
   if (ep.bnb_part && (splits > 1 || Cout % 8 != 0)) return -1;
   if (ep.bt && (ep.f16 || Cout % 8 != 0)) return -1;
-  const bool reg = tile == 40 || tile == 41 || tile == 42;
-  if (reg && (ep.bt || ep.f16 || KH * KW > 64)) tile = 23;
-  if ((ep.x2 || ep.yf || ep.bt) && !(tile == 40 || tile == 41 || tile == 42)) {
-    // pairs / fp32 outputs / filter read transposed: the buffer / register kernels only
-    if (!(tile == 22 || tile == 23)) tile = 23;
+  if (ep.x2 || ep.yf || ep.bt) {
+    // pairs / fp32 outputs / filter read transposed: the buffer kernels (x2 also at depth 4 and
+    // 128x128, A/B tiles 21 / 32 / 33)
+    const bool x2_ok = !ep.bt && (tile == 21 || tile == 32 || tile == 33);
+    if (!(tile == 22 || tile == 23 || x2_ok)) tile = 23;
     if ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB || (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kBufOOB ||
         KH * KW > 64 || ep.f16)
       return -1;
@@ -1814,10 +1657,6 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
     return tile;
   }
   switch (tile) {
-    // register-pipelined kernels (4 waves of 32x32 / 64x32 / 32x64, D K-steps in flight)
-    case 40: launch_reg<2, 2, 4>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
-    case 41: launch_reg<4, 2, 3>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
-    case 42: launch_reg<2, 2, 6>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 1: launch_fwd<128, 128>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 2: launch_fwd<128, 64>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     // LDS-DMA pipelined variants (tile code 10 + x: x = 1 128x128, 2 128x64, 3 64x64, 4/5/6 the same at depth 3)

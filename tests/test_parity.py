@@ -95,9 +95,12 @@ NEAR = ('rpn_', 'cls_score_', 'bbox_pred_', 'bn1_')  # layers adjacent to a loss
 def _check_grads(gc, gg, median_floor):
     """Loss-adjacent layers: cosine >= 0.97 and norm within 5 %.  All non-negligible layers together:
     total gradient norm within 5 %, median per-layer norm error <= 10 %.
-    Median cosine over all layers >= ``median_floor`` (deep layers of this random-init network are
-    chaotic: fp32 math on merely bf16-ROUNDED inputs and weights already gives a median cosine of
-    0.98 (RPN) / 0.71 (R-CNN) vs exact fp32, tools/parity_probe.py, profiles/r2_parity_probe.txt)."""
+    Median cosine over all layers >= ``median_floor``, set 0.05 below the bf16-STORAGE floor: exact
+    fp32 arithmetic with bf16-rounded inputs, weights, layer outputs and layer-output gradients gives
+    a median cosine of 0.956 (RPN) / 0.521 (R-CNN) vs the fp32 step on this random-init network
+    (deep-layer gradient directions are chaotic under any rounding); the HIP bf16 path measures
+    0.962 / 0.563, i.e. it loses nothing beyond bf16 storage (tools/parity_probe.py,
+    profiles/r3_parity_probe.txt).  The fp32-class mode removes the storage loss (the *_fp32_* tests)."""
     norms = {n: float(v.norm()) for n, v in gc.items()}
     big = max(norms.values())
     rows = []
@@ -136,7 +139,7 @@ def test_rpn_step_bf16_gpu_matches_fp32_cpu(cuda):
     assert torch.equal(og['rpn_label'].cpu(), oc['rpn_label'])
     for k in ('rpn_cls_loss', 'rpn_bbox_loss'):
         assert _rel(og[k].float().cpu().sum(), oc[k].float().sum()) <= 0.03, (k, og[k], oc[k])
-    _check_grads(gc, gg, 0.90)
+    _check_grads(gc, gg, 0.91)
 
 
 def test_rcnn_step_bf16_gpu_matches_fp32_cpu(cuda):
@@ -146,7 +149,7 @@ def test_rcnn_step_bf16_gpu_matches_fp32_cpu(cuda):
     og, gg = _fwd_bwd(gpu, b)
     for k in ('cls_loss', 'bbox_loss'):
         assert _rel(og[k].float().cpu().sum(), oc[k].float().sum()) <= 0.03, (k, og[k], oc[k])
-    _check_grads(gc, gg, 0.30)
+    _check_grads(gc, gg, 0.47)
 
 
 def _check_grads_tight(gc, gg, cos_min=0.99, rel_max=0.02, min_layers=10):

@@ -1,8 +1,14 @@
-"""Register-pipelined conv kernel (tiles 40-42) against the LDS-DMA buffer kernels (22 / 23) on the
-ResNet-101 C4 @800x1333 shapes, bf16 and fp32-class (x2) pairs: device time per call (graph-replayed)
-and bitwise agreement (same K order).
+"""Buffer-kernel tile / depth sweep for bf16 and fp32-class (x2) pairs on the ResNet-101 C4
+@800x1333 shapes: device time per call (graph-replayed) and bitwise agreement between tiles (the
+same K order).  Tiles: 23 = 64x64 depth 3, 33 = 64x64 depth 4, 22 / 32 = 128x64 depth 3 / 4,
+21 = 128x128 depth 3.
 
-    python tools/microbench/conv_reg.py [--shapes s3_1x1a,s3_3x3] [--tiles 23,40,41,42] [--splits 1]
+Round-3 finding kept here: a register-pipelined variant (each wave loading its MFMA fragments
+straight from memory, 3-6 K-steps in VGPRs, no LDS) ran 2.5-3x slower than tile 23 on every
+shape -- the scattered 16-B-per-lane row loads cost far more L1 / L2 throughput than one LDS-DMA
+stage shared by four waves.
+
+    python tools/microbench/conv_reg.py [--shapes s3_1x1a,s3_3x3] [--tiles 23,33] [--splits 1]
 """
 import argparse
 import json
@@ -19,7 +25,7 @@ from tools.microbench.conv_tiles import SHAPES, timeit  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--shapes', default='s3_1x1a,s3_3x3,s3_1x1b,s2_1x1a,s2_3x3,rpn_3x3,s4_1x1a,s4_3x3')
-    ap.add_argument('--tiles', default='23,22,40,41,42')
+    ap.add_argument('--tiles', default='23,33,22,32,21')
     ap.add_argument('--splits', default='1')
     args = ap.parse_args()
     ext = need_ext()

@@ -6,7 +6,11 @@ Arms (same weights, same deterministic samples as the test):
   gpu_bf16      the production path (HIP kernels, bf16 activations / weights, fp32 accumulation)
   gpu_fp32      the same model in fp32 on the GPU (PyTorch / MIOpen ops: order-of-summation noise only)
   cpu_bf16in    fp32 CPU math on bf16-ROUNDED input image and weights (sensitivity of the random-init
-                network to input rounding alone: the noise floor any bf16 path inherits)
+                network to input rounding alone)
+  cpu_bf16act   cpu_bf16in plus every layer output and every layer-output gradient rounded to bf16
+                (forward / tensor hooks on the leaf modules): what bf16 STORAGE of activations and
+                gradients costs with exact fp32 arithmetic in between -- the floor of any bf16 path
+  gpu_x2        the fp32-class GPU mode (bf16 hi / lo pairs, three MFMAs per product)
 
     python tools/parity_probe.py [--mode rpn|rcnn]
 """
@@ -43,6 +47,29 @@ def stats(ref, got):
     return cs[len(cs) // 2], rows[:4], sorted(near)
 
 
+def _bf(t):
+    return t.to(torch.bfloat16).float() if torch.is_tensor(t) and t.is_floating_point() else t
+
+
+def _round_storage(model):
+    """Round every leaf module's output (forward) and the gradient arriving at it (backward) to
+    bf16, as bf16 activation / gradient storage between kernels would."""
+    def fwd_hook(mod, inp, out):
+        def one(t):
+            if not (torch.is_tensor(t) and t.is_floating_point()):
+                return t
+            r = _bf(t)
+            if r.requires_grad:
+                r.register_hook(_bf)
+            return r
+        if isinstance(out, tuple):
+            return tuple(one(t) for t in out)
+        return one(out)
+    for mod in model.modules():
+        if len(list(mod.children())) == 0:
+            mod.register_forward_hook(fwd_hook)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--mode', default='rpn', choices=['rpn', 'rcnn'])
@@ -60,15 +87,20 @@ def main():
         dev = torch.device('cuda', 0)
         arms['gpu_bf16'] = Trainer(copy.deepcopy(base), mode, fixed_param_prefix=tp.FIXED, lr=0.0, device=dev)
         arms['gpu_fp32'] = Trainer(copy.deepcopy(base), mode, fixed_param_prefix=tp.FIXED, lr=0.0, device=dev,
-                                   compute_dtype=torch.float32, channels_last=False)
+                                   channels_last=False, precision='torch')
+        arms['gpu_x2'] = Trainer(copy.deepcopy(base), mode, fixed_param_prefix=tp.FIXED, lr=0.0, device=dev,
+                                 precision='fp32')
     q = copy.deepcopy(base)
     with torch.no_grad():
         for p in q.parameters():
             p.copy_(p.to(torch.bfloat16).float())
     arms['cpu_bf16in'] = Trainer(q, mode, fixed_param_prefix=tp.FIXED, lr=0.0, device='cpu')
+    qa = copy.deepcopy(q)
+    _round_storage(qa)
+    arms['cpu_bf16act'] = Trainer(qa, mode, fixed_param_prefix=tp.FIXED, lr=0.0, device='cpu')
     for name, tr in arms.items():
         b = dict(batch)
-        if name == 'cpu_bf16in':
+        if name.startswith('cpu_bf16'):
             b['data'] = b['data'].to(torch.bfloat16).float()
         _, g = tp._fwd_bwd(tr, b)
         med, worst, near = stats(g_ref, g)

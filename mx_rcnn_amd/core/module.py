@@ -181,6 +181,9 @@ class MutableModule(object):
         self._batch = b
         self.model.train(is_train)
         if is_train:
+            # step() leaves the strided convs' dgrad filter cache for the next step_body to rebuild
+            # (sgd_step(refresh=False)); a backward through this API must see the updated filters
+            self.trainer.store.refresh_dgrad_cache()
             self.trainer.store.zero_grad()
             self.trainer.reducer.prepare()
             self._outputs = self.trainer.forward(b)

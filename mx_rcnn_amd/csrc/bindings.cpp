@@ -908,6 +908,9 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
       std::vector<std::pair<int, int>> cands = {{t, sp}};
       for (int c : {23, 22, 101, 104, 105, 106, 108, 109, 110, 111})
         if (c != t || sp != 1) cands.push_back({c, 1});
+      // large grids: the 256-row tiles of conv_big.hip (512 threads, 4-tile LDS ring)
+      if ((int64_t)NB * Ho * Wo >= 16384 && !ep.x2 && getenv("MXR_NO_BIG") == nullptr)
+        for (int c : {200, 201}) cands.push_back({c, 1});
       // grids far below one tile per CU (the FC head: M = 128 RoIs, K up to 25088): split K
       const int64_t Mrows = (int64_t)NB * Ho * Wo;
       const int nkk = KH * KW * (Cin / 64);
@@ -915,6 +918,14 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
         for (int c : {23, 22, 106, 109})
           for (int spl : {2, 4, 8})
             if (nkk / spl >= 4 && !(c == t && spl == sp)) cands.push_back({c, spl});
+      } else if (!bwd_mode && !stats && Cout % 4 == 0 && nkk >= 64 && getenv("MXR_TUNE_DEEPK") == nullptr &&
+                 ((Mrows + 63) / 64) * ((Cout + 63) / 64) <= 1024) {
+        // deep K (the RPN 3x3 over 1024 channels: K = 9216) on about one tile per CU: K slices give
+        // each CU several workgroups to overlap (fp32-class RPN conv 219 -> 179 us at split 8,
+        // tools/microbench/conv_x2_tiles.py)
+        for (int c : {23, 22})
+          for (int spl : {2, 4, 8})
+            if (!(c == t && spl == sp)) cands.push_back({c, spl});
       }
       int max_sp = sp;
       for (const auto& c : cands) max_sp = std::max(max_sp, c.second);

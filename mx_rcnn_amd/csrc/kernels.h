@@ -250,6 +250,10 @@ struct ConvEpi {
 float philox_uniform_host(uint32_t seed, uint64_t step, uint64_t e);
 // output rows per workgroup tile (BM) of a tile code
 int conv_tile_bm(int tile);
+// large-tile conv (conv_big.hip): tile 200 = 256x256, 201 = 256x128, 512 threads, bf16 / fp16, plain
+// epilogues (bias, residual, ReLU, frozen-BN second output); -1 when unsupported
+int conv_big_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho, int Wo,
+                 int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int tile, hipStream_t st);
 int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho, int Wo,
                    int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int tile, int splits, float* slab,
                    hipStream_t st);

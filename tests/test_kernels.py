@@ -273,13 +273,43 @@ def test_conv_igemm_fwd_vs_fp32(cuda, shape):
         ref = torch.relu(ref)
     for tile, splits in ((1, 1), (2, 1), (3, 1), (3, 2), (3, 4), (0, 0), (21, 1), (22, 1), (23, 1), (23, 2), (31, 2),
                          (33, 1), (12, 1), (16, 2), (24, 1), (25, 1), (24, 2)) + \
-            tuple((100 + i, 1) for i in range(12)) + ((105, 2), (106, 4)):
+            tuple((100 + i, 1) for i in range(12)) + ((105, 2), (106, 4), (200, 1), (201, 1)):
         y = need_ext().conv_igemm_fwd(x.to(cuda).contiguous(memory_format=torch.channels_last),
                                       w.to(cuda).contiguous(memory_format=torch.channels_last),
                                       None if b is None else b.to(cuda), s, p, relu, tile, splits)[0]
         err = (y.float().cpu() - ref).abs().max().item()
         scale = ref.abs().max().item()
         assert err <= 1e-2 * scale + 1e-2, (tile, splits, err, scale)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize('tile', [200, 201])
+def test_conv_big_epilogue_vs_fp32(cuda, dtype, tile):
+    """The 256-row large-tile kernel (conv_big.hip) with its full epilogue -- bias, residual, ReLU and
+    the frozen BN + ReLU second output -- against the fp32 reference of the same 16-bit operands;
+    M = 2 * 37 * 53 (not a multiple of 256) and Cout = 320 (a partial column tile)."""
+    from mx_rcnn_amd.ops import need_ext
+    g = torch.Generator().manual_seed(21)
+    N, Cin, H, W, Cout = 2, 128, 37, 53, 320
+    x = torch.randn(N, Cin, H, W, generator=g).to(dtype)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) * 0.05).to(dtype)
+    b = torch.randn(Cout, generator=g)
+    res = torch.randn(N, Cout, H, W, generator=g).to(dtype)
+    gamma, beta = torch.rand(Cout, generator=g) + 0.5, torch.randn(Cout, generator=g)
+    mean, var = torch.randn(Cout, generator=g), torch.rand(Cout, generator=g) + 0.5
+    ref = torch.relu(F.conv2d(x.float(), w.float(), b, padding=1) + res.float())
+    cl = dict(memory_format=torch.channels_last)
+    y1, y2 = need_ext().conv_igemm_fwd(x.to(cuda).contiguous(**cl), w.to(cuda).contiguous(**cl), b.to(cuda), 1, 1,
+                                       True, tile, 1, res.to(cuda).contiguous(**cl),
+                                       [t.to(cuda) for t in (gamma, beta, mean, var)], 2e-5, False, True)
+    scale = ref.abs().max().item()
+    assert (y1.float().cpu() - ref).abs().max().item() <= 1e-2 * scale
+    # the BN reads the STORED 16-bit output
+    ys = y1.float().cpu()
+    ref2 = torch.relu((ys - mean[:, None, None]) / torch.sqrt(var[:, None, None] + 2e-5) * gamma[:, None, None] +
+                      beta[:, None, None])
+    assert (y2.float().cpu() - ref2).abs().max().item() <= 1e-2 * ref2.abs().max().item()
 
 
 @pytest.mark.gpu

@@ -34,6 +34,13 @@ SHAPES = {
     # the stage-3 shapes at M = 4096 (exactly 256 64x64 blocks): wave-quantisation probe
     's3_3x3_sq': (1, 256, 64, 64, 256, 3, 1, 1),
     's3_1x1a_sq': (1, 1024, 64, 64, 256, 1, 1, 0),
+    # batch-8 inference (BASELINE config 5) and VGG16 600x1000 trunk: the large-M GEMMs
+    'b8_s3_1x1a': (8, 1024, 50, 84, 256, 1, 1, 0),
+    'b8_s3_3x3': (8, 256, 50, 84, 256, 3, 1, 1),
+    'b8_s3_1x1b': (8, 256, 50, 84, 1024, 1, 1, 0),
+    'b8_rpn_3x3': (8, 1024, 50, 84, 512, 3, 1, 1),
+    'vgg_c3': (1, 256, 150, 250, 256, 3, 1, 1),
+    'vgg_c2': (1, 128, 300, 500, 128, 3, 1, 1),
 }
 
 

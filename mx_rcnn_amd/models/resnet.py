@@ -146,16 +146,19 @@ def _train_bn_ok(bn):
     return not _frozen(bn) and bn.relu and bn.gamma.shape[0] % 64 == 0
 
 
-def run_stage_parts(stage, x, tail_bn=None):
+def run_stage_parts(stage, x, tail_bn=None, tail_act=False):
     """Run a stage (nn.Sequential of ResidualUnit) unit by unit through the fused ops where they
     apply, chaining each unit's last epilogue into the next unit's bn1; units that cannot fuse run
     as plain modules.  Frozen-BN units hand the next unit its bn1 activation; batch-statistics
     units (the RoI head in training) hand it the statistics partials of their output, and the last
-    one those of ``tail_bn``'s input -> (x, partials for tail_bn or None)."""
+    one those of ``tail_bn``'s input -> (x, partials for tail_bn or None).  ``tail_act``: a frozen
+    ``tail_bn`` (+ReLU) is applied in the last unit's epilogue as well (the RoI head at test time:
+    no separate BN pass over the stage-4 output) -> (x, None, relu(tail_bn(x)) or None)."""
     units = list(stage)
-    act1, parts = None, None
+    act1, parts, nxt, nbn = None, None, None, None
     for i, u in enumerate(units):
         nxt = units[i + 1] if i + 1 < len(units) else None
+        nbn = None
         tbn = nxt.bn1 if nxt is not None else tail_bn
         tbn = tbn if (tbn is not None and fusion_enabled() and _train_bn_ok(tbn)) else None
         if u.train_unit_ok(x, tbn):
@@ -165,12 +168,17 @@ def run_stage_parts(stage, x, tail_bn=None):
             continue
         parts = None
         nbn = nxt.bn1 if (nxt is not None and _frozen(nxt.bn1) and fusion_enabled()) else None
+        if nxt is None and tail_act and tail_bn is not None and _frozen(tail_bn) and tail_bn.relu and \
+                fusion_enabled():
+            nbn = tail_bn
         if u.unit_op_ok(x, nbn) and u.frozen_bns():
             x, act1 = fused_unit(u, x, act1, nbn)
         elif act1 is None and not u.can_fuse(x):
-            x = u(x)
+            x, act1 = u(x), None
         else:
             x, act1 = u.forward_fused(x, act1, nbn)
+    if tail_act:
+        return x, parts, (act1 if (nxt is None and nbn is tail_bn) else None)
     return x, parts
 
 
@@ -254,7 +262,7 @@ class ResNetHead(nn.Module):
     def forward(self, pooled):
         # fused units either way: frozen BNs (test time) or batch statistics (training), where the
         # last unit's conv epilogue also produces bn1's statistics partials
-        x, parts = run_stage_parts(self.stage4, pooled, self.bn1)
-        x = self.bn1(x, parts=parts)
+        x, parts, act = run_stage_parts(self.stage4, pooled, self.bn1, tail_act=True)
+        x = act if act is not None else self.bn1(x, parts=parts)
         x = global_avg_pool(x)
         return fc_pair(x, self.cls_score, self.bbox_pred)

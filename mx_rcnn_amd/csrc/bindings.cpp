@@ -908,6 +908,10 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
       std::vector<std::pair<int, int>> cands = {{t, sp}};
       for (int c : {23, 22, 101, 104, 105, 106, 108, 109, 110, 111})
         if (c != t || sp != 1) cands.push_back({c, 1});
+      // fp32-class pairs: the wide-stage kernel (64 channels of both planes per LDS stage) is an
+      // A/B candidate only (MXR_X2W=1): 13-26 % faster in isolation on the stage-3/4 and RPN convs,
+      // but the headline step measured 1 % slower with it in the autotune (same-box interleaved)
+      if (ep.x2 && getenv("MXR_X2W") != nullptr) cands.push_back({26, 1});
       // large grids: the 256-row tiles of conv_big.hip (512 threads, 4-tile LDS ring)
       if ((int64_t)NB * Ho * Wo >= 16384 && !ep.x2 && getenv("MXR_NO_BIG") == nullptr)
         for (int c : {200, 201}) cands.push_back({c, 1});

@@ -1139,6 +1139,161 @@ conv_igemm_buf_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
                                          tiles_n, nwg, ntiles, splits, slab);
 }
 
+// ---- fp32-class pairs, wide stages (tile code 26) ---------------------------------------------
+// The x2 buffer kernel above stages 32 channels of both planes per K step (128-B LDS rows): a
+// stage-3 conv at batch 1 then runs 32-72 barrier-separated steps of 16 KB, and the per-step DMA
+// round trip sets its pace (profiles/r3_conv_study.md: the isolated load + fragment-read + MFMA
+// loop at 32 KB stages is 18 % faster than at 16 KB).  Here a stage is 64 channels of BOTH planes:
+// 256-B LDS rows, logical 16-B chunks 0-7 the hi plane's channels c..c+63, 8-15 the lo plane's,
+// stored at chunk lc ^ (row & 15) (16 rows of one logical chunk -> 16 distinct bank slots, also
+// across the ds_read_b128 lane groups, which pair chunk c with c+1 for even c).  Two stages deep
+// (64 KB for 64x64: two workgroups fit a CU, so a 264-tile grid runs in one round), one barrier per
+// 64 channels, 2 k-halves x 3 products per stage.  Forward (non-BT) convs, plain and BN epilogues
+// as the buffer kernel (same epilogue code).
+template <int BM, int BN>
+__device__ __forceinline__ void igemm_x2w_body(uint16_t* lds, int bid, const uint16_t* __restrict__ x,
+                                               const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int NB, int H,
+                                               int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride,
+                                               int pad, const ConvEpi& ep, int tiles_n, int nwg, int ntiles) {
+  constexpr int S = 2;
+  constexpr int RB = 2 * BK;  // LDS row: 64 channels x 2 planes
+  constexpr int WM = BM / 2, WN = BN / 2;
+  constexpr int TM = WM / 16, TN = WN / 16;
+  constexpr int ACH = BM / 16, BCH = BN / 16;  // DMA instructions per wave per stage (4 rows each)
+  static_assert(BM % 64 == 0 && BN % 64 == 0, "whole 16-row blocks per wave");
+  uint16_t* As = lds;
+  uint16_t* Bs = lds + S * BM * RB;
+
+  const int q = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
+  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + bid / 8;
+  const int tm_idx = wgid / tiles_n, tn_idx = wgid % tiles_n;
+  const int m0 = tm_idx * BM, n0 = tn_idx * BN;
+  const int M = NB * Ho * Wo;
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wm = wid >> 1, wn = wid & 1;
+  const int K = KH * KW * Cin;
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)x, (short)0, (int)((int64_t)NB * H * W * Cin * 2 + ep.x2_pa), 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)w, (short)0, (int)((int64_t)Cout * K * 2 + ep.x2_pb), 0x00020000);
+
+  // instruction i of wave w loads rows (BM / 4) * w + 4 * i .. + 3, lane -> row + (lane >> 4),
+  // physical chunk lane & 15 = logical chunk (lane & 15) ^ (row & 15)
+  constexpr int RPW_A = BM / 4, RPW_B = BN / 4;  // rows per wave
+  const int pch = lane & 15;
+  uint32_t a_off[ACH];
+  uint64_t a_mask[ACH];
+#pragma unroll
+  for (int i = 0; i < ACH; ++i) {
+    const int row = RPW_A * wid + 4 * i + (lane >> 4);
+    const int lc = pch ^ (row & 15);
+    const int m = m0 + row;
+    a_off[i] = 0;
+    a_mask[i] = 0;
+    if (m < M) {
+      const int img = m / (Ho * Wo), rem = m % (Ho * Wo);
+      const int hi0 = (rem / Wo) * stride - pad, wi0 = (rem % Wo) * stride - pad;
+      a_off[i] = (uint32_t)((((int64_t)img * H + hi0) * W + wi0) * Cin * 2 + (lc & 7) * 16) + (lc >= 8 ? ep.x2_pa : 0u);
+      for (int fr = 0; fr < KH; ++fr)
+        for (int fc = 0; fc < KW; ++fc)
+          if ((unsigned)(hi0 + fr) < (unsigned)H && (unsigned)(wi0 + fc) < (unsigned)W) a_mask[i] |= 1ull << (fr * KW + fc);
+    }
+  }
+  uint32_t b_off[BCH];
+#pragma unroll
+  for (int i = 0; i < BCH; ++i) {
+    const int row = RPW_B * wid + 4 * i + (lane >> 4);
+    const int lc = pch ^ (row & 15);
+    const int co = n0 + row;
+    b_off[i] = co < Cout ? (uint32_t)((int64_t)co * K * 2 + (lc & 7) * 16) + (lc >= 8 ? ep.x2_pb : 0u) : kBufOOB;
+  }
+  const int cin_steps = Cin / 64;
+  const int nk = KH * KW * cin_steps;
+  int c_tap = 0, c_ci = 0, c_fr = 0, c_fc = 0;
+  auto issue = [&](int buf) {
+    const uint32_t tap_a = (uint32_t)((c_fr * W + c_fc) * Cin * 2);
+    const uint32_t soff_a = (uint32_t)(c_ci * 2);
+    const uint32_t soff_b = (uint32_t)((c_tap * Cin + c_ci) * 2);
+#pragma unroll
+    for (int i = 0; i < ACH; ++i) {
+      const uint32_t vo = ((a_mask[i] >> c_tap) & 1ull) ? a_off[i] + tap_a : kBufOOB;
+      buf_lds16(xr, As + (buf * BM + RPW_A * wid + 4 * i) * RB, vo, soff_a);
+    }
+#pragma unroll
+    for (int i = 0; i < BCH; ++i) buf_lds16(wr, Bs + (buf * BN + RPW_B * wid + 4 * i) * RB, b_off[i], soff_b);
+    c_ci += 64;
+    if (c_ci == Cin) {
+      c_ci = 0;
+      ++c_tap;
+      if (++c_fc == KW) {
+        c_fc = 0;
+        ++c_fr;
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nk > 0) issue(0);
+  for (int ks = 0; ks < nk; ++ks) {
+    wait_vmcnt<0>();
+    __builtin_amdgcn_s_barrier();  // stage ks landed for every wave; stage ks-1's buffer is free
+    if (ks + 1 < nk) issue((ks + 1) & 1);
+    const int buf = ks & 1;
+    const int g = lane >> 4;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WM + i * 16 + (lane & 15);
+        const uint16_t* r = As + (buf * BM + row) * RB;
+        ah[i] = *reinterpret_cast<const bf16x8*>(r + (((kk * 4 + g) ^ (row & 15)) << 3));
+        al[i] = *reinterpret_cast<const bf16x8*>(r + (((8 + kk * 4 + g) ^ (row & 15)) << 3));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WN + j * 16 + (lane & 15);
+        const uint16_t* r = Bs + (buf * BN + row) * RB;
+        bh[j] = *reinterpret_cast<const bf16x8*>(r + (((kk * 4 + g) ^ (row & 15)) << 3));
+        bl[j] = *reinterpret_cast<const bf16x8*>(r + (((8 + kk * 4 + g) ^ (row & 15)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  static_assert(BM * (BN + 4) * 4 <= S * (BM + BN) * RB * 2, "epilogue tile must fit the operand ring");
+  if (Cout % 8 == 0)
+    igemm_epilogue_lds<BM, BN, TM, TN, WM, WN, true>(acc, reinterpret_cast<float*>(lds), m0, n0, wm, wn, lane, tid, M,
+                                                     Cout, ep, y, 0, 1, nullptr, Ho, Wo);
+  else
+    igemm_epilogue<TM, TN, WM, WN, true>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, 0, 1, nullptr, Ho, Wo);
+}
+
+template <int BM, int BN>
+__global__ void __launch_bounds__(256)
+conv_x2w_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int NB,
+                int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, const ConvEpi ep,
+                int tiles_n, int nwg, int ntiles) {
+  __shared__ __attribute__((aligned(16))) uint16_t lds[2 * (BM + BN) * 2 * BK];
+  igemm_x2w_body<BM, BN>(lds, blockIdx.x, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, tiles_n, nwg,
+                         ntiles);
+}
+
 // ---- tile-balanced LDS-DMA ring (the production path) ----------------------------------------
 // Measured on the ResNet-101 C4 stage-3/4 shapes (rocprofv3 --pmc, profiles/r2_conv_pmc.txt): the
 // 64x64 ring above is limited by what ONE CU can pull into LDS (~27 GB/s at two 16 KB stages in
@@ -1645,6 +1800,17 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
   if ((ep.st_part || ep.bnb_part) && tile < 21) return -1;  // needs the buffer / ring epilogue
   if (ep.bnb_part && (splits > 1 || Cout % 8 != 0)) return -1;
   if (ep.bt && (ep.f16 || Cout % 8 != 0)) return -1;
+  if (tile == 26) {  // fp32-class pairs, wide stages: x2 forward only, whole K per workgroup
+    if (!ep.x2 || ep.bt || ep.f16 || splits > 1 || ep.omap || ep.pad_w >= 0 || Cin % 64 != 0 || KH * KW > 64 ||
+        (int64_t)NB * H * W * Cin * 2 + ep.x2_pa >= (int64_t)kBufOOB ||
+        (int64_t)Cout * KH * KW * Cin * 2 + ep.x2_pb >= (int64_t)kBufOOB)
+      return -1;
+    const int M = NB * Ho * Wo;
+    const int tiles_n = (Cout + 63) / 64, ntiles = ((M + 63) / 64) * tiles_n;
+    conv_x2w_kernel<64, 64><<<ntiles, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep,
+                                                    tiles_n, ntiles, ntiles);
+    return tile;
+  }
   if (ep.x2 || ep.yf || ep.bt) {
     // pairs / fp32 outputs / filter read transposed: the buffer kernels (x2 also at depth 4 and
     // 128x128, A/B tiles 21 / 32 / 33)

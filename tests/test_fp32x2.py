@@ -301,3 +301,31 @@ def test_sgd_x2_shadow(cuda):
     assert torch.allclose(w, w0 - 0.1 * grad)
     j = sh[:n].float() + sh[n:].float()
     assert float(((j - w).abs() / w.abs().clamp_min(1e-30)).max()) <= 2.0 ** -16
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('k,stride,pad,N,C,H,W,O', [(1, 1, 0, 1, 1024, 50, 84, 256), (3, 1, 1, 1, 256, 25, 42, 256),
+                                                    (3, 2, 1, 2, 128, 17, 23, 96), (1, 2, 0, 1, 512, 13, 21, 1024)])
+def test_conv_x2_wide_stage_equals_narrow(cuda, k, stride, pad, N, C, H, W, O):
+    """The wide-stage fp32-class kernel (tile 26: 64 channels of both planes per LDS stage) sums in
+    the same K order as the 32-channel buffer kernel (tile 23): bitwise equal outputs, plain and
+    with the residual + frozen-BN second-output epilogue, and within TOL of fp64."""
+    from mx_rcnn_amd.ops import need_ext
+    g = torch.Generator().manual_seed(k * 1000 + C + O)
+    x = torch.randn(N, C, H, W, generator=g)
+    w = torch.randn(O, C, k, k, generator=g) * (2.0 / (C * k * k)) ** 0.5
+    b = torch.randn(O, generator=g)
+    ref = F.conv2d(x.double(), w.double(), b.double(), stride=stride, padding=pad)
+    xp, wp = _pair(x, cuda), _pair(w, cuda)
+    ext = need_ext()
+    ya = ext.conv_igemm_fwd(xp, wp[:O], b.to(cuda), stride, pad, False, 23, 1, x2=True, w_plane=wp.numel() // 2)[0]
+    yb = ext.conv_igemm_fwd(xp, wp[:O], b.to(cuda), stride, pad, False, 26, 1, x2=True, w_plane=wp.numel() // 2)[0]
+    assert torch.equal(ya, yb)
+    assert _err(_unpair(yb), ref) <= TOL
+    bn = [t.to(cuda) for t in (torch.rand(O) + 0.5, torch.randn(O), torch.randn(O), torch.rand(O) + 0.5)]
+    res = _pair(torch.randn(ref.shape, generator=g), cuda)
+    a1, a2 = ext.conv_igemm_fwd(xp, wp[:O], None, stride, pad, False, 23, 1, res, bn, 2e-5, False, True, x2=True,
+                                w_plane=wp.numel() // 2)
+    b1, b2 = ext.conv_igemm_fwd(xp, wp[:O], None, stride, pad, False, 26, 1, res, bn, 2e-5, False, True, x2=True,
+                                w_plane=wp.numel() // 2)
+    assert torch.equal(a1, b1) and torch.equal(a2, b2)

@@ -230,7 +230,9 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
 #pragma unroll 4
   for (int p = threadIdx.x; p < HW; p += blockDim.x) {
     float v[CW];
-    if (gadd && code == 3) {
+    if (gadd && code == 3 && CW == 4) {
+      ld4c(gadd, ((int64_t)b * HW + p) * C + c0, 3, iplane, v);  // one 8-B load per plane
+    } else if (gadd && code == 3) {
 #pragma unroll
       for (int k = 0; k < CW; ++k) v[k] = ldc(gadd, ((int64_t)b * HW + p) * C + c0 + k, 3, iplane);
     } else if (gadd) ldv<CW>(gadd + ((int64_t)b * HW + p) * C + c0, v, code);
@@ -248,10 +250,19 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
     const int64_t base = (int64_t)i * C + c0;
     int a[CW];
     float g[CW];
+    if constexpr (CW == 4) {  // c0 and C are multiples of 4: 16-B argmax / 8-B (per plane) gradient loads
+      const int4 av = *reinterpret_cast<const int4*>(argmax + base);
+      a[0] = av.x; a[1] = av.y; a[2] = av.z; a[3] = av.w;
+      if (code == 3) ld4c(gout, base, 3, oplane, g);
+      else
 #pragma unroll
-    for (int k = 0; k < CW; ++k) {
-      a[k] = argmax[base + k];
-      g[k] = code == 3 ? ldc(gout, base + k, 3, oplane) : to_f(gout[base + k], code);
+        for (int k = 0; k < CW; ++k) g[k] = to_f(gout[base + k], code);
+    } else {
+#pragma unroll
+      for (int k = 0; k < CW; ++k) {
+        a[k] = argmax[base + k];
+        g[k] = code == 3 ? ldc(gout, base + k, 3, oplane) : to_f(gout[base + k], code);
+      }
     }
 #pragma unroll
     for (int k = 0; k < CW; ++k)
@@ -263,7 +274,9 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
     float v[CW];
 #pragma unroll
     for (int k = 0; k < CW; ++k) v[k] = acc[p * CW + k];
-    if (code == 3) {
+    if (code == 3 && CW == 4) {
+      st4c(gin, ((int64_t)b * HW + p) * C + c0, 3, iplane, v);
+    } else if (code == 3) {
 #pragma unroll
       for (int k = 0; k < CW; ++k) stc(gin, ((int64_t)b * HW + p) * C + c0 + k, v[k], 3, iplane);
     } else {

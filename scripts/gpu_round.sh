@@ -17,4 +17,4 @@ run bench_test_b1 300 python bench_test.py --steps 100 --warmup 5
 run bench_test_b8 400 python bench_test.py --steps 30 --warmup 3 --batch 8
 run bench_test_f16_b8 400 python bench_test.py --steps 30 --warmup 3 --batch 8 --dtype fp16
 run prof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof_round" -o run -- \
-    python bench.py --steps 10 --warmup 3
+    python bench.py --steps 10 --warmup 3 --no-bf16-extra

@@ -146,16 +146,18 @@ def _train_bn_ok(bn):
     return not _frozen(bn) and bn.relu and bn.gamma.shape[0] % 64 == 0
 
 
-def run_stage_parts(stage, x, tail_bn=None, tail_act=False):
+def run_stage_parts(stage, x, tail_bn=None, tail_act=False, act1_in=None):
     """Run a stage (nn.Sequential of ResidualUnit) unit by unit through the fused ops where they
     apply, chaining each unit's last epilogue into the next unit's bn1; units that cannot fuse run
     as plain modules.  Frozen-BN units hand the next unit its bn1 activation; batch-statistics
     units (the RoI head in training) hand it the statistics partials of their output, and the last
     one those of ``tail_bn``'s input -> (x, partials for tail_bn or None).  ``tail_act``: a frozen
     ``tail_bn`` (+ReLU) is applied in the last unit's epilogue as well (the RoI head at test time:
-    no separate BN pass over the stage-4 output) -> (x, None, relu(tail_bn(x)) or None)."""
+    no separate BN pass over the stage-4 output, or the next stage's first bn1 in the trunk) -> (x,
+    None, relu(tail_bn(x)) or None).  ``act1_in``: the first unit's bn1 activation when the previous
+    stage's last epilogue produced it."""
     units = list(stage)
-    act1, parts, nxt, nbn = None, None, None, None
+    act1, parts, nxt, nbn = act1_in, None, None, None
     for i, u in enumerate(units):
         nxt = units[i + 1] if i + 1 < len(units) else None
         nbn = None
@@ -236,8 +238,13 @@ class ResNetTrunk(nn.Module):
         else:
             x = self.bn0(self.conv0(self.bn_data(x)))
         x = max_pool(x, 3, 2, 1)
-        for st in (self.stage1, self.stage2, self.stage3):
-            x = run_stage(st, x)
+        # each stage's last unit also produces the next stage's first bn1 activation in its epilogue
+        # (no separate BN + ReLU pass at the stage boundaries)
+        stages = (self.stage1, self.stage2, self.stage3)
+        act = None
+        for i, st in enumerate(stages):
+            nxt_bn = stages[i + 1][0].bn1 if i + 1 < len(stages) else None
+            x, _, act = run_stage_parts(st, x, nxt_bn, tail_act=True, act1_in=act)
         return x
 
     def feat_shape(self, h, w):

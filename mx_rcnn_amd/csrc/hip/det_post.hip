@@ -174,12 +174,18 @@ det_topk_kernel(const float* __restrict__ ks, const float* __restrict__ kb, cons
   __shared__ unsigned int hist[256];
   __shared__ unsigned int prefix_s, remain_s;
   __shared__ int off[1024 + 1];
-  const int b = blockIdx.x, tid = threadIdx.x;
+  __shared__ int kn_s[1024];
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int nc = C - 1;
   const int64_t cbase = (int64_t)b * nc;
+  // per-class kept counts staged in LDS once: the passes below walk the classes wave-parallel
+  // (one class per wave at a time, its scores lane-parallel) instead of every thread stepping
+  // through all classes in order behind a dependent count load each (4 x 80 serial round trips)
+  for (int c = tid; c < nc; c += 256) kn_s[c] = kn[cbase + c];
+  __syncthreads();
   // image threshold: the max_per-th largest kept score (0 when fewer are kept)
   int total = 0;
-  for (int c = 0; c < nc; ++c) total += kn[cbase + c];
+  for (int c = 0; c < nc; ++c) total += kn_s[c];
   unsigned int th_bits = 0;
   if (max_per > 0 && total > max_per) {
     if (tid == 0) {
@@ -191,10 +197,10 @@ det_topk_kernel(const float* __restrict__ ks, const float* __restrict__ kb, cons
       __syncthreads();
       const unsigned int pre = prefix_s;
       const unsigned int hi_mask = pass == 3 ? 0u : (0xffffffffu << (8 * (pass + 1)));
-      for (int c = 0; c < nc; ++c) {
-        const int cnt = kn[cbase + c];
+      for (int c = wid; c < nc; c += 4) {
+        const int cnt = kn_s[c];
         const float* s = ks + (cbase + c) * R;
-        for (int i = tid; i < cnt; i += 256) {
+        for (int i = lane; i < cnt; i += 64) {
           const unsigned int u = __float_as_uint(s[i]);
           if ((u & hi_mask) == (pre & hi_mask)) atomicAdd(&hist[(u >> (8 * pass)) & 255u], 1u);
         }
@@ -216,7 +222,7 @@ det_topk_kernel(const float* __restrict__ ks, const float* __restrict__ kb, cons
   }
   // per-class selected counts (the kept lists are score-sorted: the selection is a prefix)
   for (int c = tid; c < nc; c += 256) {
-    const int cnt = kn[cbase + c];
+    const int cnt = kn_s[c];
     const float* s = ks + (cbase + c) * R;
     int lo = 0, hi = cnt;  // first index with bits < th_bits
     while (lo < hi) {
@@ -233,9 +239,9 @@ det_topk_kernel(const float* __restrict__ ks, const float* __restrict__ kb, cons
   }
   __syncthreads();
   const float inv = 1.f / im_info[b * 3 + 2];
-  for (int c = 0; c < nc; ++c) {
+  for (int c = wid; c < nc; c += 4) {
     const int o0 = off[c], cnt = off[c + 1] - off[c];
-    for (int i = tid; i < cnt; i += 256) {
+    for (int i = lane; i < cnt; i += 64) {
       const int dst = o0 + i;
       if (dst >= cap) break;
       const int64_t src = (cbase + c) * R + i;

@@ -152,6 +152,7 @@ class FlatParamStore:
         from ..ops._ext import need_ext
         ext = need_ext()
         srcs, dsts = [], []
+        self._x2_entries = {}  # table entry -> (param, plane) of the x2 pair entries
         # stride-1 data gradients (and the FC's) read the forward filter transposed in-kernel
         # (ops/conv.py dgrad_args): only the strided k x k convs' parity sub-filters need the copy
         bt = conv_ops.dgrad_bt_enabled()
@@ -187,7 +188,12 @@ class FlatParamStore:
                 dsts.append(buf)
         self._wt_params = []
         if srcs:
+            # the parameter (and, x2, the plane) behind each table entry: x2 entries are views of
+            # the shadow, so they are recorded by _x2_dgrad_entry rather than found by pointer
             self._wt_params = [p for p in self._dgrad_params(srcs)]
+            for k, (pp, pl) in self._x2_entries.items():
+                self._wt_params[k] = pp
+            self._wt_planes = [self._x2_entries.get(k, (None, -1))[1] for k in range(len(srcs))]
             self._wt_srcs, self._wt_dsts = srcs, dsts
             self._sub_in_table = set()
             n_ent, tiles = ext.wt_flip_table_info(srcs)
@@ -215,7 +221,8 @@ class FlatParamStore:
             buf = torch.empty((2 * i, o, kh, kw), dtype=torch.bfloat16, device=self.device,
                               memory_format=torch.channels_last)
         conv_ops.register_dgrad_weight(p, buf)
-        for v, d in zip(views, (buf[:i], buf[i:])):
+        for pl, (v, d) in enumerate(zip(views, (buf[:i], buf[i:]))):
+            self._x2_entries[len(srcs)] = (p, pl)
             srcs.append(v)
             dsts.append(d)
 
@@ -230,13 +237,17 @@ class FlatParamStore:
         written in the same pass instead of one copy kernel each.  Never while capturing: the
         table upload is a host-to-device copy."""
         from ..ops import conv as conv_ops
-        if not conv_ops._SUBW or os.environ.get('MXR_SUBFILTER_FOLD', '1') == '0' or self.x2:
-            return  # (x2: the pair sub-filters are refreshed by slicing copies)
+        if not conv_ops._SUBW or os.environ.get('MXR_SUBFILTER_FOLD', '1') == '0':
+            return
         if torch.cuda.is_current_stream_capturing():
             return
         subs, have = [], set()
-        for p in self._wt_params:
+        for k, p in enumerate(self._wt_params):
             lst = conv_ops.sub_filters_of(p) if p is not None else []
+            plane = self._wt_planes[k] if self.x2 else -1
+            if plane >= 0 and lst:  # x2: this entry writes one plane of the (2I, ...) pair sub-filters
+                half = p.shape[1]
+                lst = [((b[:half] if plane == 0 else b[half:]), r, c) for b, r, c in lst]
             rows = {tuple(r) for _, r, _ in lst}
             cols = {tuple(c) for _, _, c in lst}
             kh = p.shape[2] if (p is not None and p.dim() == 4) else 0

@@ -166,14 +166,17 @@ def test_side_stream_grad_clear_matches_inline(cuda, monkeypatch):
 
 
 @pytest.mark.gpu
-def test_flip_kernel_writes_parity_sub_filters(cuda):
+@pytest.mark.parametrize('precision', ['bf16', 'fp32'])
+def test_flip_kernel_writes_parity_sub_filters(cuda, precision):
     """After the first backward registers the strided data gradient's parity sub-filters, the
     multi-filter flip kernel writes them in its own pass: every sub-filter equals its slice of the
-    flipped filter after later updates, and the copy path is skipped for them."""
+    flipped filter after later updates, and the copy path is skipped for them (fp32-class pairs:
+    one table entry per plane writes that plane's half of the pair sub-filter)."""
     from mx_rcnn_amd.ops import conv as conv_ops
     torch.manual_seed(0)
     m = FasterRCNN('resnet50', 21, cfg=_cfg())
-    tr = Trainer(m, 'e2e', fixed_param_prefix=['conv0', 'stage1', 'stage2', 'bn_data', 'bn0'], lr=0.01, device=cuda)
+    tr = Trainer(m, 'e2e', fixed_param_prefix=['conv0', 'stage1', 'stage2', 'bn_data', 'bn0'], lr=0.01, device=cuda,
+                 precision=precision)
     b = {k: v.to(cuda) for k, v in _batch(320, 480).items()}
     for _ in range(3):
         tr.step(b)

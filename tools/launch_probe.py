@@ -3,10 +3,12 @@
 Times, for the bench.py ResNet-101 step under GraphedStep:
   * gpu     -- ms/step of back-to-back replays (synchronised once at the end);
   * host    -- ms/step the host spends inside the replay calls of that same loop;
-  * single  -- ms of one replay synchronised on its own (launch latency + GPU time).
+  * single  -- ms of one replay synchronised on its own (launch latency + GPU time);
+  * enqueue_behind_busy -- host ms of one replay call issued while the GPU is busy (submission
+    cost alone, no back-pressure from the previous replay).
 A host time close to the gpu time means the step is submission-bound.
 
-    python tools/launch_probe.py [--steps 50]
+    python tools/launch_probe.py [--steps 50] [--precision fp32|bf16]
 """
 import argparse
 import json
@@ -28,6 +30,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--steps', type=int, default=50)
     ap.add_argument('--network', default='resnet101')
+    ap.add_argument('--precision', default='fp32', choices=['fp32', 'bf16'],
+                    help="'fp32': the fp32-class x2 step (bench.py's default), 'bf16'")
     args = ap.parse_args()
     dev = torch.device('cuda:0')
     cfg = snapshot()
@@ -41,8 +45,7 @@ def main():
     batch = bench.synthetic_batch(1, 800, 1333, 81, dev, gen)
     model.to(dev).calibrate_bn(batch['data'])
     tr = Trainer(model, 'e2e', fixed_param_prefix=['conv0', 'stage1', 'stage2', 'bn_data', 'bn0'], lr=0.001,
-                 momentum=0.9, wd=0.0005, clip_gradient=1.0, rescale_grad=1.0, compute_dtype=torch.bfloat16,
-                 device=dev)
+                 momentum=0.9, wd=0.0005, clip_gradient=1.0, rescale_grad=1.0, device=dev, precision=args.precision)
     g = GraphedStep(tr, batch, warmup=3)
     for _ in range(5):
         g(batch)
@@ -72,7 +75,18 @@ def main():
         h2 += time.perf_counter() - a
     torch.cuda.synchronize()
     gpu2 = (time.perf_counter() - t1) / args.steps
-    print(json.dumps({'gpu_ms': round(gpu * 1e3, 3), 'host_ms': round(host / args.steps * 1e3, 3),
+    # pure submission cost: one replay enqueued behind a long spin kernel (the GPU is busy, so
+    # the call cannot block on the previous replay's completion)
+    enq = []
+    for _ in range(5):
+        torch.cuda.synchronize()
+        torch.cuda._sleep(50_000_000)
+        a = time.perf_counter()
+        g.graph.replay()
+        enq.append(time.perf_counter() - a)
+        torch.cuda.synchronize()
+    print(json.dumps({'precision': args.precision, 'enqueue_behind_busy_ms': round(min(enq) * 1e3, 3),
+                      'gpu_ms': round(gpu * 1e3, 3), 'host_ms': round(host / args.steps * 1e3, 3),
                       'single_ms': round(min(singles) * 1e3, 3), 'replay_only_gpu_ms': round(gpu2 * 1e3, 3),
                       'replay_only_host_ms': round(h2 / args.steps * 1e3, 3),
                       'env': {k: v for k, v in os.environ.items() if k.startswith(('DEBUG_', 'HIP_', 'MXR_'))}}))

@@ -7,6 +7,7 @@
 #include "common.h"
 #include "../kernels.h"
 #include <algorithm>
+#include <cstdlib>
 
 namespace mxr {
 
@@ -63,9 +64,107 @@ sgd_kernel(float* __restrict__ w, float* __restrict__ mom, const void* __restric
   }
 }
 
+// 8 elements per lane: two 16-B loads of each fp32 stream issued before any use, the shadow pair
+// written as full 16-B rows (8 bf16 per plane).  NT: master / momentum / gradient accesses are
+// nontemporal (each byte is touched once per step; keeps the shadow the next forward reads in the
+// caches).  Needs x2_plane % 8 == 0 for the aligned lo-plane rows (host checks).
+typedef float sgd_f4 __attribute__((ext_vector_type(4)));
+typedef unsigned int sgd_u4 __attribute__((ext_vector_type(4)));
+
+template <bool NT, typename T>
+__device__ __forceinline__ T sgd_ld(const T* p) {
+  if (NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
+template <bool NT, typename T>
+__device__ __forceinline__ void sgd_st(T* p, T v) {
+  if (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+template <bool GBF16, bool NT>
+__global__ void __launch_bounds__(256)
+sgd8_kernel(float* __restrict__ w, float* __restrict__ mom, const void* __restrict__ grad, int64_t n,
+            const float* __restrict__ lr_p, float mu, float wd, float rescale, float clip, uint16_t* __restrict__ wb,
+            int64_t x2_plane) {
+  const float lr = *lr_p;
+  const int64_t n8 = n & ~(int64_t)7;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
+  for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 8; i < n8; i += stride) {
+    const sgd_f4 w0 = sgd_ld<NT>(reinterpret_cast<const sgd_f4*>(w + i));
+    const sgd_f4 w1 = sgd_ld<NT>(reinterpret_cast<const sgd_f4*>(w + i + 4));
+    const sgd_f4 m0 = sgd_ld<NT>(reinterpret_cast<const sgd_f4*>(mom + i));
+    const sgd_f4 m1 = sgd_ld<NT>(reinterpret_cast<const sgd_f4*>(mom + i + 4));
+    float g[8];
+    if (GBF16) {
+      const sgd_u4 u = sgd_ld<NT>(reinterpret_cast<const sgd_u4*>(static_cast<const uint16_t*>(grad) + i));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        g[2 * k] = __uint_as_float(u[k] << 16);
+        g[2 * k + 1] = __uint_as_float(u[k] & 0xffff0000u);
+      }
+    } else {
+      const sgd_f4 g0 = sgd_ld<NT>(reinterpret_cast<const sgd_f4*>(static_cast<const float*>(grad) + i));
+      const sgd_f4 g1 = sgd_ld<NT>(reinterpret_cast<const sgd_f4*>(static_cast<const float*>(grad) + i + 4));
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        g[k] = g0[k];
+        g[k + 4] = g1[k];
+      }
+    }
+    float wv[8], mv[8];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      wv[k] = w0[k]; wv[k + 4] = w1[k];
+      mv[k] = m0[k]; mv[k + 4] = m1[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) wv[k] = sgd_one(wv[k], mv[k], g[k], lr, mu, wd, rescale, clip);
+    sgd_st<NT>(reinterpret_cast<sgd_f4*>(w + i), sgd_f4{wv[0], wv[1], wv[2], wv[3]});
+    sgd_st<NT>(reinterpret_cast<sgd_f4*>(w + i + 4), sgd_f4{wv[4], wv[5], wv[6], wv[7]});
+    sgd_st<NT>(reinterpret_cast<sgd_f4*>(mom + i), sgd_f4{mv[0], mv[1], mv[2], mv[3]});
+    sgd_st<NT>(reinterpret_cast<sgd_f4*>(mom + i + 4), sgd_f4{mv[4], mv[5], mv[6], mv[7]});
+    if (wb && x2_plane) {
+      float stored[8];
+      st8x(wb + i, x2_plane, wv, stored);
+    } else if (wb) {
+      st8_bf16(wb + i, wv);
+    }
+  }
+  if (blockIdx.x == 0 && threadIdx.x < n - n8) {  // the < 8 trailing elements
+    const int64_t k = n8 + threadIdx.x;
+    const float gk = GBF16 ? bf16_to_f32(static_cast<const uint16_t*>(grad)[k]) : static_cast<const float*>(grad)[k];
+    float m = mom[k];
+    const float nw = sgd_one(w[k], m, gk, lr, mu, wd, rescale, clip);
+    w[k] = nw;
+    mom[k] = m;
+    if (wb && x2_plane) stx(wb, k, x2_plane, nw);
+    else if (wb) wb[k] = f32_to_bf16(nw);
+  }
+}
+
+// MXR_SGD: 0 = the 4-wide kernel (default), 1 = 8-wide, 2 = 8-wide nontemporal
+static int sgd_variant() {
+  static const int v = [] {
+    const char* e = getenv("MXR_SGD");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
 void sgd_momentum(float* w, float* mom, const void* grad, int grad_bf16, int64_t n, const float* lr, float momentum,
                   float wd, float rescale, float clip, uint16_t* w_bf16, hipStream_t st, int64_t x2_plane) {
   if (n == 0) return;
+  const int var = sgd_variant();
+  const auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
+  if (var > 0 && x2_plane % 8 == 0 && a16(w) && a16(mom) && a16(grad) && (w_bf16 == nullptr || a16(w_bf16))) {
+    const int blocks = (int)std::min<int64_t>(std::max<int64_t>(div_up((n + 7) / 8, 256), 1), 256 * 8);
+#define MXR_SGD8(GB, NT) sgd8_kernel<GB, NT><<<blocks, 256, 0, st>>>(w, mom, grad, n, lr, momentum, wd, rescale, clip, w_bf16, x2_plane)
+    if (grad_bf16) { if (var == 2) MXR_SGD8(true, true); else MXR_SGD8(true, false); }
+    else { if (var == 2) MXR_SGD8(false, true); else MXR_SGD8(false, false); }
+#undef MXR_SGD8
+    return;
+  }
   const int blocks = (int)std::min<int64_t>(div_up((n + 3) / 4, 256), 256 * 8);
   if (grad_bf16)
     sgd_kernel<true><<<blocks, 256, 0, st>>>(w, mom, grad, n, lr, momentum, wd, rescale, clip, w_bf16, x2_plane);

@@ -287,10 +287,11 @@ def test_stem_x2_matches_fp32(cuda):
 
 
 @pytest.mark.gpu
-def test_sgd_x2_shadow(cuda):
+@pytest.mark.parametrize('n', [1000, 1003, 65536 + 8])
+def test_sgd_x2_shadow(cuda, n):
+    """n % 8 == 0 takes the 8-wide kernel (16-B rows of both shadow planes), otherwise the 4-wide one."""
     from mx_rcnn_amd.ops import need_ext
     g = torch.Generator().manual_seed(16)
-    n = 1000
     w = torch.randn(n, generator=g).to(cuda)
     mom = torch.zeros(n, device=cuda)
     grad = torch.randn(n, generator=g).to(cuda)

@@ -3,10 +3,12 @@
 
 BASELINE.json metric "imgs/sec e2e train ResNet-101 Faster R-CNN at 1/2/4/8 MI355X": ResNet-101
 C4 Faster R-CNN, COCO-shaped synthetic images 800x1333 (81 classes), random-init weights,
-1 image per GPU per step (the reference's only mode), at the reference's precision class by default
-(--dtype fp32: every MFMA operand a bf16 hi / lo pair, products as three bf16 MFMAs with fp32
-accumulation, fp32 gradients / masters / SGD, mx_rcnn_amd/ops/precision.py); the bf16 mode is
-timed after it and reported as the extra field ``config.bf16`` (--dtype bf16: bf16 only),
+1 image per GPU per step (the reference's only mode), at the reference's precision by default
+(--dtype fp32: every tensor between kernels is the exact fp32 value as a (mid, hi, lo) bf16 triple,
+products as six bf16 MFMAs hh+hm+mh+hl+lh+mm with fp32 accumulation, fp32 gradients / BN statistics
+/ masters / SGD, mx_rcnn_amd/ops/precision.py); the faster, lower-precision modes are timed after it
+and reported as extra fields: ``config.bf16x3`` (16-bit hi / lo pairs, three products) and
+``config.bf16`` (bf16 operands) (--dtype bf16x3 / bf16: that mode alone),
 full step timed: trunk+RPN fwd/bwd, anchor target, proposal (sort + NMS 12000->6000),
 proposal target (128 RoIs), RoIPool, stage-4 head, losses, bucketed RCCL all-reduce (N>1),
 fused SGD update.  Weak scaling (fixed per-GPU work).
@@ -37,10 +39,10 @@ def parse_args(argv=None):
     ap.add_argument('--image', default='800x1333')
     ap.add_argument('--ims-per-gpu', type=int, default=1)
     ap.add_argument('--mode', default='graph', choices=['graph', 'eager'])
-    ap.add_argument('--dtype', default='fp32', choices=['bf16', 'fp32'],
-                    help='fp32 (default): the reference precision class on the x2 pair kernels, followed by a bf16 '
-                         'run reported as config.bf16; bf16: the bf16 mode alone')
-    ap.add_argument('--no-bf16-extra', action='store_true', help='fp32 only: skip the extra bf16 run')
+    ap.add_argument('--dtype', default='fp32', choices=['fp32', 'bf16x3', 'bf16'],
+                    help='fp32 (default): the reference precision (exact fp32 triples), followed by bf16x3 and bf16 '
+                         'runs reported as config.bf16x3 / config.bf16; bf16x3 / bf16: that mode alone')
+    ap.add_argument('--no-bf16-extra', action='store_true', help='fp32 only: skip the extra bf16x3 / bf16 runs')
     ap.add_argument('--bucket-mb', type=float, default=25)
     ap.add_argument('--grad-comm', default='fp32', choices=['fp32', 'bf16'],
                     help='all-reduce wire dtype of the gradient buckets (fp32 = the reference kvstore sum)')
@@ -64,6 +66,14 @@ from mx_rcnn_amd.parallel import dist as pdist  # noqa: E402
 from mx_rcnn_amd.core.trainer import Trainer, GraphedStep  # noqa: E402
 
 METRIC = 'imgs/sec e2e train ResNet-101 Faster R-CNN'
+PRECISION_NOTE = {
+    'fp32': 'fp32: every tensor between kernels is the exact fp32 value as a (mid, hi, lo) bf16 triple (24 '
+            'significant bits), products hh+hm+mh+hl+lh+mm on the bf16 MFMA with fp32 accumulation, fp32 '
+            'grads/BN statistics/masters/SGD',
+    'bf16x3': 'bf16x3: MFMA operands and stored tensors as bf16 hi/lo pairs (16 significant bits), '
+              'hi*hi+hi*lo+lo*hi with fp32 accumulation, fp32 grads/masters/SGD',
+    'bf16': 'bf16 operands, fp32 accumulation and masters',
+}
 
 
 def synthetic_batch(n_img, h, w, num_classes, device, gen, max_gt=20):
@@ -117,12 +127,12 @@ def main():
         raise SystemExit('--gpus %d but %d ranks were launched' % (args.gpus, world))
     rec = run(args, args.dtype, rank, world, device)
     if args.dtype == 'fp32' and not args.no_bf16_extra and device.type == 'cuda':
-        torch.cuda.empty_cache()
-        extra = run(args, 'bf16', rank, world, device)
-        if rec is not None:
-            rec['config']['bf16'] = {'value': extra['value'], 'ms_per_step': extra['ms_per_step'],
-                                     'exec': extra['config']['exec'],
-                                     'objective_first_last': extra['config']['objective_first_last']}
+        for name in ('bf16x3', 'bf16'):
+            torch.cuda.empty_cache()
+            extra = run(args, name, rank, world, device)
+            rec['config'][name] = {'value': extra['value'], 'ms_per_step': extra['ms_per_step'],
+                                   'exec': extra['config']['exec'],
+                                   'objective_first_last': extra['config']['objective_first_last']}
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if os.environ.get('MXR_BENCH_DUMP_TUNE') and device.type == 'cuda':
@@ -133,7 +143,7 @@ def main():
 
 
 def run(args, precision, rank, world, device):
-    """One timed run at ``precision`` ('fp32': x2 pairs, 'bf16') -> the JSON record (every rank)."""
+    """One timed run at ``precision`` ('fp32' triples, 'bf16x3' pairs, 'bf16') -> the JSON record."""
     h, w = [int(v) for v in args.image.lower().split('x')]
     cfg = snapshot()
     # end2end config mutation (train_end2end.py:25-32)
@@ -206,7 +216,6 @@ def run(args, precision, rank, world, device):
     metric = METRIC if args.network == 'resnet101' else 'imgs/sec e2e train %s Faster R-CNN' % args.network
     if args.train_mode != 'e2e':
         metric = 'imgs/sec alternate-stage %s train %s' % (args.train_mode, args.network)
-    x2 = trainer.x2
     rec = {'metric': metric, 'value': round(value, 3), 'unit': 'images/s', 'n_gpus': world,
            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
@@ -215,10 +224,7 @@ def run(args, precision, rank, world, device):
            'config': {'model': '%s-faster-rcnn%s' % (args.network, '-c4' if args.network.startswith('resnet') else ''), 'global_batch': args.ims_per_gpu * world,
                       'seq_len': None, 'image_hw': [h, w], 'num_classes': args.num_classes,
                       'ims_per_gpu': args.ims_per_gpu, 'train_mode': args.train_mode, 'parallelism': 'dp%d' % world,
-                      'precision': ('fp32-class: MFMA operands as bf16 hi/lo pairs (16 significant bits), '
-                                    'hi*hi+hi*lo+lo*hi bf16 MFMA with fp32 accumulation, fp32 grads/masters/SGD')
-                      if x2 else ('bf16 operands, fp32 accumulation and masters' if trainer.precision == 'bf16'
-                                  else 'fp32'),
+                      'precision': PRECISION_NOTE.get(trainer.precision, trainer.precision),
                       'rpn_pre_post_nms': [cfg.TRAIN.RPN_PRE_NMS_TOP_N, cfg.TRAIN.RPN_POST_NMS_TOP_N],
                       'rois_per_image': cfg.TRAIN.BATCH_SIZE, 'exec': mode,
                       'objective_first_last': [round(loss0, 4), round(loss1, 4)],

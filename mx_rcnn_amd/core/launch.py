@@ -3,10 +3,12 @@ train_widerface*.py, test.py, tools/*): process-group bootstrap, roidb construct
 .lst, synthetic), model construction + pretrained loading + new-layer initialisation
 (`train_end2end.py:56-78`), optimizer parameters (`train_end2end.py:98-105`), frozen prefixes.
 
-Multi-GPU: ``--gpus 0,1,2,3`` (the reference's device list, `train_end2end.py:168`) or
-``--gpus 4`` starts one process per GPU from the single command (parallel/spawn.py: fresh
-child processes, torchrun's environment contract); under ``torchrun --nproc-per-node N`` the
-launcher's ranks are used as they are.  The device of each rank is its LOCAL_RANK.  Gradients
+Multi-GPU: ``--gpus 0,1,2,3`` names DEVICES, as the reference's device list does
+(`train_end2end.py:168`): one process per listed device from the single command
+(parallel/spawn.py: fresh child processes, torchrun's environment contract), ``--gpus 3`` one
+process on device 3.  The ids index the devices the job can see: under an existing
+HIP_VISIBLE_DEVICES mask, id i is the mask's i-th entry.  Under ``torchrun --nproc-per-node N``
+the launcher's ranks are used as they are.  The device of each rank is its LOCAL_RANK.  Gradients
 are summed across ranks like the reference's kvstore (rescale_grad 1.0).
 """
 import logging
@@ -38,6 +40,10 @@ def add_common_args(parser):
     parser.add_argument('--eager', action='store_true', help='disable hipGraph step capture')
     parser.add_argument('--ims-per-gpu', type=int, default=1)
     parser.add_argument('--seed', type=int, default=0)
+    parser.add_argument('--dtype', default='fp32', choices=('fp32', 'bf16x3', 'bf16'),
+                        help='training precision on the GPU (ops/precision.py): fp32 = the reference '
+                             'precision (exact fp32 triples, six bf16 products), bf16x3 = 16-bit pairs, '
+                             'bf16 = bf16 operands; fp32 accumulation, gradients and masters in all')
     return parser
 
 
@@ -54,6 +60,9 @@ def init_runtime(args):
         maybe_spawn(parse_gpus(spec), sys.argv[0], sys.argv[1:], visible=select_devices(spec))
     rank, world, local_rank, device = pdist.init_distributed()
     setup_logging(rank)
+    if getattr(args, 'dtype', None):
+        from ..ops import precision
+        precision.set_default(args.dtype)
     if getattr(args, 'cfg', None):
         override(parse_cfg_overrides(args.cfg))
     torch.manual_seed(getattr(args, 'seed', 0) + rank)

@@ -42,7 +42,10 @@ def sync_key(key):
 class MutableModule(object):
     def __init__(self, symbol, data_names=None, label_names=None, logger=logging, context=None, work_load_list=None,
                  max_data_shapes=None, max_label_shapes=None, fixed_param_prefix=None, mode=None, use_graph=None,
-                 compute_dtype=None):
+                 compute_dtype=None, precision=None):
+        """precision: 'fp32' (default on the GPU: the reference's precision, exact fp32 triples on
+        the bf16 MFMA, ops/precision.py), 'bf16x3' or 'bf16' (core/trainer.py); compute_dtype is the
+        older spelling (bf16 -> 'bf16', fp32 -> 'fp32')."""
         if isinstance(symbol, tuple):
             symbol, mode = symbol
         self.symbol = symbol
@@ -60,6 +63,11 @@ class MutableModule(object):
         self.fixed_param_prefix = fixed_param_prefix or []
         self.use_graph = (self.context.type == 'cuda') and (use_graph is None or bool(use_graph))
         self.compute_dtype = compute_dtype
+        if precision is None:
+            from ..ops.precision import default_name
+            precision = 'bf16' if compute_dtype == torch.bfloat16 else ('fp32' if compute_dtype == torch.float32
+                                                                        else default_name())
+        self.precision = precision
         self.binded = self.params_initialized = self.optimizer_initialized = False
         self.trainer = None
         self._graphs = {}
@@ -167,7 +175,8 @@ class MutableModule(object):
                                clip_gradient=p.get('clip_gradient', -1.0) or -1.0,
                                rescale_grad=p.get('rescale_grad', 1.0), lr_scheduler=sched,
                                compute_dtype=self.compute_dtype, device=self.context,
-                               bucket_mb=p.get('bucket_mb', 64))
+                               bucket_mb=p.get('bucket_mb', 64),
+                               precision=self.precision if self.context.type == 'cuda' else None)
         self.optimizer_initialized = True
 
     def install_monitor(self, mon):
@@ -180,19 +189,25 @@ class MutableModule(object):
         b = self.trainer.prepare_batch(data_batch)
         self._batch = b
         self.model.train(is_train)
-        if is_train:
-            # step() leaves the strided convs' dgrad filter cache for the next step_body to rebuild
-            # (sgd_step(refresh=False)); a backward through this API must see the updated filters
-            self.trainer.store.refresh_dgrad_cache()
-            self.trainer.store.zero_grad()
-            self.trainer.reducer.prepare()
-            self._outputs = self.trainer.forward(b)
-        else:
-            with torch.no_grad():
+        from ..ops.precision import x2_mode
+        # the step API runs in the trainer's precision mode, like step() / graph replay (the
+        # multi-plane autograd functions read the mode at backward time too)
+        with x2_mode(self.trainer.x2):
+            if is_train:
+                # step() leaves the strided convs' dgrad filter cache for the next step_body to rebuild
+                # (sgd_step(refresh=False)); a backward through this API must see the updated filters
+                self.trainer.store.refresh_dgrad_cache()
+                self.trainer.store.zero_grad()
+                self.trainer.reducer.prepare()
                 self._outputs = self.trainer.forward(b)
+            else:
+                with torch.no_grad():
+                    self._outputs = self.trainer.forward(b)
 
     def backward(self, out_grads=None):
-        self._outputs['loss'].backward()
+        from ..ops.precision import x2_mode
+        with x2_mode(self.trainer.x2):
+            self._outputs['loss'].backward()
         # release the autograd graph (see Trainer.step_body: a live graph breaks later captures)
         self._outputs = {k: (v.detach() if torch.is_tensor(v) else v) for k, v in self._outputs.items()}
 

@@ -24,6 +24,7 @@ import torch.nn as nn
 
 from ..ops.sgd import sgd_momentum_
 from ..ops import grad_sink
+from ..ops import precision
 
 
 def _is_bn_param(name):
@@ -43,13 +44,16 @@ class ParamGroup:
         self.numel = sum(e[3] for e in entries)
         self.master = torch.zeros(self.numel, dtype=torch.float32, device=device)
         self.mom = torch.zeros(self.numel, dtype=torch.float32, device=device)
-        # x2 (fp32-class mode, ops/precision.py): the parameters ARE the fp32 masters, gradients are
-        # fp32, and the shadow is the bf16 pair the MFMA kernels read: hi plane [0, n), lo plane
-        # [n, 2n), rewritten by the SGD kernel in the same pass as the update
-        self.x2 = bool(x2 and lowp)
+        # x2 = plane count of the fp32 modes (ops/precision.py: 2 bf16x3 pairs, 3 fp32 triples): the
+        # parameters ARE the fp32 masters, gradients are fp32, and the shadow holds the bf16 planes
+        # the MFMA kernels read -- plane k at [k * plane, k * plane + n), plane = n rounded up to a
+        # multiple of 8 so every plane's rows stay 16-B aligned -- rewritten by the SGD kernel in
+        # the same pass as the update
+        self.x2 = (3 if x2 == 3 else 2) if (x2 and lowp) else 0
+        self.plane = (self.numel + 7) // 8 * 8
         gd = compute_dtype if (lowp and not self.x2) else torch.float32
         if self.x2:
-            self.shadow = torch.zeros(2 * self.numel, dtype=torch.bfloat16, device=device)
+            self.shadow = torch.zeros(self.x2 * self.plane, dtype=torch.bfloat16, device=device)
         else:
             self.shadow = torch.zeros(self.numel, dtype=gd, device=device) if lowp else None
         self.grad = torch.zeros(self.numel, dtype=gd, device=device)
@@ -60,9 +64,11 @@ class ParamGroup:
         if self.shadow is None:
             return
         if self.x2:
-            hi = self.master.to(torch.bfloat16)
-            self.shadow[:self.numel].copy_(hi)
-            self.shadow[self.numel:].copy_((self.master - hi.float()).to(torch.bfloat16))
+            from ..ops import precision
+            parts = precision.split(self.master, self.x2)
+            n, pl = self.numel, self.plane
+            for k in range(self.x2):
+                self.shadow[k * pl:k * pl + n].copy_(parts[k * n:(k + 1) * n])
         else:
             self.shadow.copy_(self.master.to(self.shadow.dtype))
 
@@ -74,8 +80,9 @@ class FlatParamStore:
         self.compute_dtype = compute_dtype
         dev = torch.device(device) if device is not None else next(model.parameters()).device
         self.device = dev
-        # x2: fp32-class training on the bf16 MFMA (ops/precision.py); compute_dtype is then fp32
-        self.x2 = bool(x2)
+        # x2: plane count of the fp32 training modes on the bf16 MFMA (ops/precision.py: 2 = bf16x3,
+        # 3 = fp32); compute_dtype is then fp32
+        self.x2 = (3 if x2 == 3 else 2) if x2 else 0
         lowp_enabled = compute_dtype != torch.float32 or self.x2
         fixed = fixed_param_prefix or []
         layers = list(model.mx_layers(mode)) if mode is not None else list(model.mx_layers())
@@ -101,7 +108,6 @@ class FlatParamStore:
             groups.setdefault((lowp, decay), []).append((n, m, attr, p.numel(), tuple(p.shape), cl))
         self.groups = [ParamGroup(k, v, dev, compute_dtype, self.x2) for k, v in sorted(groups.items())]
         self.params = {}
-        from ..ops import precision
         with torch.no_grad():
             for g in self.groups:
                 off = 0
@@ -119,9 +125,9 @@ class FlatParamStore:
                     grad_sink.enable_direct(param)
                     m._parameters[attr] = param
                     self.params[n] = param
-                    if g.x2:  # the kernels' pair of this weight: hi view + the group's lo-plane offset
+                    if g.x2:  # the kernels' planes of this weight: plane-0 view + the group's plane spacing
                         precision.register_weight(param, self._shaped(g.shadow[off:off + numel], shape, cl),
-                                                  g.numel)
+                                                  g.plane, g.x2)
                     off += numel
                 if g.x2:
                     g.sync_shadow()
@@ -201,15 +207,17 @@ class FlatParamStore:
             self.refresh_dgrad_cache()
 
     def _x2_dgrad_entry(self, g, p, off, numel, shape, cl, srcs, dsts):
-        """x2 mode: the flipped / transposed filter of ``p`` as a PAIR buffer (2I, O, kh, kw), filled
-        by two flip-table entries (hi plane from the shadow's hi view, lo from its lo view)."""
+        """Multi-plane modes: the flipped / transposed filter of ``p`` as a planes buffer
+        (P*I, O, kh, kw), filled by one flip-table entry per plane (from the shadow's plane views)."""
         from ..ops import conv as conv_ops
+        P = g.x2
+        starts = [k * g.plane for k in range(P)]
         if len(shape) == 2:
             o, i = shape
             if o % 64 != 0 or i % 64 != 0:
                 return
-            views = [g.shadow[pl + off:pl + off + numel].view(o, i, 1, 1) for pl in (0, g.numel)]
-            buf = torch.empty((2 * i, o, 1, 1), dtype=torch.bfloat16, device=self.device,
+            views = [g.shadow[pl + off:pl + off + numel].view(o, i, 1, 1) for pl in starts]
+            buf = torch.empty((P * i, o, 1, 1), dtype=torch.bfloat16, device=self.device,
                               memory_format=torch.channels_last)
         else:
             if len(shape) != 4 or not cl:
@@ -217,11 +225,11 @@ class FlatParamStore:
             o, i, kh, kw = shape
             if o % 64 != 0 or i % 8 != 0 or kh != kw:
                 return
-            views = [self._shaped(g.shadow[pl + off:pl + off + numel], shape, cl) for pl in (0, g.numel)]
-            buf = torch.empty((2 * i, o, kh, kw), dtype=torch.bfloat16, device=self.device,
+            views = [self._shaped(g.shadow[pl + off:pl + off + numel], shape, cl) for pl in starts]
+            buf = torch.empty((P * i, o, kh, kw), dtype=torch.bfloat16, device=self.device,
                               memory_format=torch.channels_last)
         conv_ops.register_dgrad_weight(p, buf)
-        for pl, (v, d) in enumerate(zip(views, (buf[:i], buf[i:]))):
+        for pl, (v, d) in enumerate(zip(views, [buf[k * i:(k + 1) * i] for k in range(P)])):
             self._x2_entries[len(srcs)] = (p, pl)
             srcs.append(v)
             dsts.append(d)
@@ -245,9 +253,9 @@ class FlatParamStore:
         for k, p in enumerate(self._wt_params):
             lst = conv_ops.sub_filters_of(p) if p is not None else []
             plane = self._wt_planes[k] if self.x2 else -1
-            if plane >= 0 and lst:  # x2: this entry writes one plane of the (2I, ...) pair sub-filters
-                half = p.shape[1]
-                lst = [((b[:half] if plane == 0 else b[half:]), r, c) for b, r, c in lst]
+            if plane >= 0 and lst:  # planes: this entry writes one plane of the (P*I, ...) sub-filters
+                part = p.shape[1]
+                lst = [(b[plane * part:(plane + 1) * part], r, c) for b, r, c in lst]
             rows = {tuple(r) for _, r, _ in lst}
             cols = {tuple(c) for _, _, c in lst}
             kh = p.shape[2] if (p is not None and p.dim() == 4) else 0
@@ -321,6 +329,7 @@ class FlatParamStore:
         for n in self.fixed_names:
             dist.broadcast(self.frozen_fp32[n], src)
             self.params[n].data.copy_(self.frozen_fp32[n].to(self.params[n].dtype))
+            precision.forget_weight(self.params[n])  # .data writes do not move the version counter
         for b in self.model.buffers():
             if b.is_floating_point() or b.dtype in (torch.int32, torch.int64):
                 t = b.data if b.is_contiguous() else b.data.contiguous()
@@ -344,7 +353,8 @@ class FlatParamStore:
         the start of the next step, concurrently with its forward pass)."""
         for g in self.groups:
             grad = grad_for(g) if grad_for is not None else g.grad
-            sgd_momentum_(g.master, g.mom, grad, lr, momentum, wd if g.decay else 0.0, rescale, clip, g.shadow)
+            sgd_momentum_(g.master, g.mom, grad, lr, momentum, wd if g.decay else 0.0, rescale, clip, g.shadow,
+                          planes=g.x2 or 1)
         if refresh:
             self.refresh_dgrad_cache()
 
@@ -401,6 +411,7 @@ class FlatParamStore:
                                 g.sync_shadow()
                 if not found:
                     p.data.copy_(src.to(p.dtype))
+                    precision.forget_weight(p)  # .data writes do not move the version counter
                     if n in self.frozen_fp32:
                         self.frozen_fp32[n].copy_(src)
         self.refresh_dgrad_cache()

@@ -18,15 +18,23 @@ class Trainer:
     def __init__(self, model, mode='e2e', fixed_param_prefix=None, lr=0.001, momentum=0.9, wd=0.0005,
                  clip_gradient=1.0, rescale_grad=1.0, lr_scheduler=None, compute_dtype=None, device=None,
                  bucket_mb=25, average_grads=False, channels_last=None, grad_comm_dtype=None, precision=None):
-        """precision: 'bf16' (bf16 operands, fp32 accumulation / masters), or 'fp32': the reference's
-        precision class on the GPU -- every MFMA operand an x2 hi / lo bf16 pair, products as three
-        bf16 MFMAs with fp32 accumulation, fp32 gradients (ops/precision.py); 'torch': plain fp32
-        PyTorch / vendor ops on the GPU (a reference arm for precision probes).  Default: bf16 on the
-        GPU unless compute_dtype says fp32; the CPU path is plain fp32."""
+        """precision (ops/precision.py):
+        'fp32'   -- the reference's precision on the GPU: every MFMA operand and every tensor stored
+                    between kernels is an EXACT (mid, hi, lo) bf16 triple of the fp32 value, products
+                    as six bf16 MFMAs (hh + hm + mh + hl + lh + mm) with fp32 accumulation, fp32
+                    gradients, BN statistics, SGD state and masters;
+        'bf16x3' -- hi / lo pairs (16 significant bits), three products: faster, below fp32;
+        'bf16'   -- bf16 operands, fp32 accumulation / masters;
+        'torch'  -- plain fp32 PyTorch / vendor ops on the GPU (a reference arm for precision probes).
+        Default: bf16 on the GPU unless compute_dtype says fp32 (then 'fp32'); the CPU path is plain
+        fp32 whatever the name."""
         dev = torch.device(device) if device is not None else next(model.parameters()).device
         if precision is None:
             precision = 'fp32' if (compute_dtype == torch.float32 and dev.type == 'cuda') else 'bf16'
-        self.x2 = precision == 'fp32' and dev.type == 'cuda'
+        if precision not in ('fp32', 'bf16x3', 'bf16', 'torch'):
+            raise ValueError('precision must be fp32, bf16x3, bf16 or torch, not %r' % (precision,))
+        # plane count of the multi-plane mode (0: off)
+        self.x2 = {'fp32': 3, 'bf16x3': 2}.get(precision, 0) if dev.type == 'cuda' else 0
         if self.x2 or precision == 'torch':
             compute_dtype = torch.float32
         if compute_dtype is None:
@@ -34,7 +42,10 @@ class Trainer:
         if channels_last is None:
             channels_last = dev.type == 'cuda'
         self.device, self.compute_dtype, self.channels_last = dev, compute_dtype, channels_last
-        self.precision = 'fp32' if (self.x2 or compute_dtype == torch.float32) else 'bf16'
+        if self.x2:
+            self.precision = precision
+        else:
+            self.precision = 'fp32' if compute_dtype == torch.float32 else 'bf16'
         self.model = model.to(dev)
         self.mode = mode
         self.store = FlatParamStore(self.model, fixed_param_prefix, compute_dtype, dev, channels_last,

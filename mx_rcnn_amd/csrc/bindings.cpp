@@ -44,6 +44,11 @@ struct DevGuard {
 #define CHECK_CONTIG(t) TORCH_CHECK((t).is_contiguous(), #t " must be contiguous")
 
 // 16-bit storage code of the dtype-generic kernels: 0 fp32, 1 bf16, 2 fp16
+// planes of a multi-plane fp32-mode flag: 0 off, 2 x2 pairs (True / 1 / 2), 3 x3 triples (common.h)
+inline int npl(int64_t x2) { return x2 <= 0 ? 0 : (x2 == 3 ? 3 : 2); }
+// the elementwise kernels' storage code of those planes (common.h: 3 x2, 4 x3)
+inline int pcode(int64_t x2) { return npl(x2) == 3 ? 4 : 3; }
+
 int dcode(const Tensor& t) {
   TORCH_CHECK(t.scalar_type() == at::kBFloat16 || t.scalar_type() == at::kFloat || t.scalar_type() == at::kHalf,
               "expected bf16, fp16 or fp32 tensor");
@@ -342,30 +347,30 @@ std::vector<Tensor> anchor_target_assign(const Tensor& base_anchors, int64_t H, 
 // ---- RoI pooling -----------------------------------------------------------------------
 // feat must be channels-last in memory: logical (B, C, H, W) with NHWC strides.
 // x2: feat is a (2B, C, H, W) hi / lo pair, the pooled output (2R, C, PH, PW) a pair too
-std::vector<Tensor> roi_pool_fwd(const Tensor& feat, const Tensor& rois, int64_t PH, int64_t PW, double scale, bool x2) {
+std::vector<Tensor> roi_pool_fwd(const Tensor& feat, const Tensor& rois, int64_t PH, int64_t PW, double scale, int64_t x2) {
   CHECK_DEV(feat); CHECK_DEV(rois); CHECK_F32(rois); CHECK_CONTIG(rois);
   TORCH_CHECK(feat.dim() == 4 && feat.is_contiguous(at::MemoryFormat::ChannelsLast),
               "feat must be (B,C,H,W) channels_last");
   TORCH_CHECK(rois.dim() == 2 && rois.size(1) == 5, "rois must be (R, 5)");
-  TORCH_CHECK(!x2 || (feat.scalar_type() == at::kBFloat16 && feat.size(0) % 2 == 0 && feat.size(1) % 4 == 0),
+  TORCH_CHECK(!x2 || (feat.scalar_type() == at::kBFloat16 && feat.size(0) % npl(x2) == 0 && feat.size(1) % 4 == 0),
               "x2: bf16 (2B, C, H, W) pairs, C % 4 == 0");
-  const int B = (int)(x2 ? feat.size(0) / 2 : feat.size(0)), C = (int)feat.size(1), H = (int)feat.size(2),
+  const int B = (int)(x2 ? feat.size(0) / npl(x2) : feat.size(0)), C = (int)feat.size(1), H = (int)feat.size(2),
             W = (int)feat.size(3);
   const int R = (int)rois.size(0);
   DevGuard g(feat.device());
-  Tensor out = at::empty({x2 ? 2 * R : R, C, PH, PW}, feat.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor out = at::empty({x2 ? npl(x2) * R : R, C, PH, PW}, feat.options().memory_format(at::MemoryFormat::ChannelsLast));
   Tensor argmax = at::empty({R, C, PH, PW}, feat.options().dtype(at::kInt).memory_format(at::MemoryFormat::ChannelsLast));
-  mxr::roi_pool_fwd(feat.data_ptr(), x2 ? 3 : dcode(feat), B, H, W, C, rois.data_ptr<float>(), R, (int)PH, (int)PW,
+  mxr::roi_pool_fwd(feat.data_ptr(), x2 ? pcode(x2) : dcode(feat), B, H, W, C, rois.data_ptr<float>(), R, (int)PH, (int)PW,
                     (float)scale, out.data_ptr(), argmax.data_ptr<int32_t>(), cur_stream());
   return {out, argmax};
 }
 
 Tensor roi_pool_bwd(const Tensor& grad_out, const Tensor& argmax, const Tensor& rois, int64_t B, int64_t H,
-                    int64_t W, c10::optional<Tensor> grad_add, bool x2) {
+                    int64_t W, c10::optional<Tensor> grad_add, int64_t x2) {
   CHECK_DEV(grad_out); CHECK_DEV(argmax); CHECK_I32(argmax); CHECK_DEV(rois); CHECK_F32(rois);
-  const int R = (int)(x2 ? grad_out.size(0) / 2 : grad_out.size(0)), C = (int)grad_out.size(1),
+  const int R = (int)(x2 ? grad_out.size(0) / npl(x2) : grad_out.size(0)), C = (int)grad_out.size(1),
             PH = (int)grad_out.size(2), PW = (int)grad_out.size(3);
-  TORCH_CHECK(!x2 || (grad_out.scalar_type() == at::kBFloat16 && grad_out.size(0) % 2 == 0 && argmax.size(0) == R),
+  TORCH_CHECK(!x2 || (grad_out.scalar_type() == at::kBFloat16 && grad_out.size(0) % npl(x2) == 0 && argmax.size(0) == R),
               "x2: bf16 (2R, C, PH, PW) gradient pairs");
   Tensor go = grad_out.contiguous(at::MemoryFormat::ChannelsLast);
   TORCH_CHECK(argmax.is_contiguous(at::MemoryFormat::ChannelsLast), "argmax must be channels_last");
@@ -378,13 +383,13 @@ Tensor roi_pool_bwd(const Tensor& grad_out, const Tensor& argmax, const Tensor& 
   const bool add = grad_add.has_value() && grad_add->defined();
   if (add)
     TORCH_CHECK(grad_add->scalar_type() == grad_out.scalar_type() && grad_add->dim() == 4 &&
-                    grad_add->size(0) == (x2 ? 2 * B : B) &&
+                    grad_add->size(0) == (x2 ? npl(x2) * B : B) &&
                     grad_add->size(1) == C && grad_add->size(2) == H && grad_add->size(3) == W &&
                     grad_add->is_contiguous(at::MemoryFormat::ChannelsLast),
                 "grad_add: channels_last (B, C, H, W) of the gradient dtype");
   if (lds_path || x2) {
-    Tensor gin = at::empty({x2 ? 2 * B : B, C, H, W}, grad_out.options().memory_format(at::MemoryFormat::ChannelsLast));
-    if (mxr::roi_pool_bwd_lds(go.data_ptr(), x2 ? 3 : dcode(go), argmax.data_ptr<int32_t>(),
+    Tensor gin = at::empty({x2 ? npl(x2) * B : B, C, H, W}, grad_out.options().memory_format(at::MemoryFormat::ChannelsLast));
+    if (mxr::roi_pool_bwd_lds(go.data_ptr(), x2 ? pcode(x2) : dcode(go), argmax.data_ptr<int32_t>(),
                               rois.contiguous().data_ptr<float>(), R, PH, PW, (int)B, (int)H, (int)W, C, gin.data_ptr(),
                               st, add ? grad_add->data_ptr() : nullptr) == 0)
       return gin;
@@ -530,32 +535,34 @@ Tensor loss_combine(std::vector<Tensor> terms, std::vector<double> weights, c10:
 
 // ---- optimizer -------------------------------------------------------------------------
 void sgd_momentum(Tensor w, Tensor mom, const Tensor& grad, const Tensor& lr, double momentum, double wd,
-                  double rescale, double clip, c10::optional<Tensor> w_bf16) {
+                  double rescale, double clip, c10::optional<Tensor> w_bf16, int64_t planes) {
   CHECK_DEV(w); CHECK_F32(w); CHECK_CONTIG(w); CHECK_DEV(mom); CHECK_F32(mom); CHECK_CONTIG(mom);
   CHECK_DEV(grad); CHECK_CONTIG(grad); CHECK_DEV(lr); CHECK_F32(lr);
   TORCH_CHECK(w.numel() == mom.numel() && w.numel() == grad.numel(), "size mismatch");
   uint16_t* wb = nullptr;
   int64_t x2_plane = 0;
   if (w_bf16.has_value() && w_bf16->defined()) {
-    // a shadow of 2n elements is the fp32-class x2 pair: hi plane, then the lo plane n elements on
-    TORCH_CHECK(w_bf16->scalar_type() == at::kBFloat16 && w_bf16->is_contiguous() &&
-                    (w_bf16->numel() == w.numel() || w_bf16->numel() == 2 * w.numel()),
-                "w_bf16 must be contiguous bf16 of the same size (or twice it: an x2 pair)");
+    // planes 2 / 3: the shadow is the x2 pair / x3 triple of the fp32 modes (common.h), its planes
+    // numel / planes elements apart (>= n, a multiple of 8 so every plane's rows stay 16-B aligned)
+    TORCH_CHECK(w_bf16->scalar_type() == at::kBFloat16 && w_bf16->is_contiguous() && planes >= 1 && planes <= 3 &&
+                    w_bf16->numel() % planes == 0 && w_bf16->numel() / planes >= w.numel() &&
+                    (planes == 1 || (w_bf16->numel() / planes) % 8 == 0),
+                "w_bf16 must be contiguous bf16 of `planes` planes of >= numel elements (multiples of 8)");
     wb = reinterpret_cast<uint16_t*>(w_bf16->data_ptr());
-    if (w_bf16->numel() == 2 * w.numel()) x2_plane = w.numel();
+    if (planes > 1) x2_plane = w_bf16->numel() / planes;
   }
   DevGuard g(w.device());
   mxr::sgd_momentum(w.data_ptr<float>(), mom.data_ptr<float>(), grad.data_ptr(), is_bf16(grad), w.numel(),
                     lr.data_ptr<float>(), (float)momentum, (float)wd, (float)rescale, (float)clip, wb, cur_stream(),
-                    x2_plane);
+                    x2_plane, planes == 3 ? 1 : 0);
 }
 
 // ---- BN + ReLU -------------------------------------------------------------------------
 Tensor bn_relu_fwd(const Tensor& x, const Tensor& gamma, const Tensor& beta, const Tensor& mean, const Tensor& var,
-                   double eps, bool fix_gamma, bool relu, bool x2) {
+                   double eps, bool fix_gamma, bool relu, int64_t x2) {
   CHECK_DEV(x);
   TORCH_CHECK(x.dim() == 4 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "x must be channels_last 4-D");
-  TORCH_CHECK(!x2 || (x.scalar_type() == at::kBFloat16 && x.size(0) % 2 == 0 && x.size(1) % 4 == 0),
+  TORCH_CHECK(!x2 || (x.scalar_type() == at::kBFloat16 && x.size(0) % npl(x2) == 0 && x.size(1) % 4 == 0),
               "bn_relu x2: bf16 (2N, C, H, W) pairs, C % 4 == 0");
   const int C = (int)x.size(1);
   TORCH_CHECK(C <= 4096 || C % 4 == 0, "C must be a multiple of 4 or <= 4096");
@@ -564,7 +571,7 @@ Tensor bn_relu_fwd(const Tensor& x, const Tensor& gamma, const Tensor& beta, con
   }
   DevGuard g(x.device());
   Tensor y = at::empty_like(x, x.options(), at::MemoryFormat::ChannelsLast);
-  mxr::bn_relu_fwd(x.data_ptr(), x2 ? 3 : dcode(x), x.numel() / C / (x2 ? 2 : 1), C, gamma.data_ptr<float>(),
+  mxr::bn_relu_fwd(x.data_ptr(), x2 ? pcode(x2) : dcode(x), x.numel() / C / (x2 ? npl(x2) : 1), C, gamma.data_ptr<float>(),
                    beta.data_ptr<float>(),
                    mean.data_ptr<float>(), var.data_ptr<float>(), (float)eps, fix_gamma ? 1 : 0, relu ? 1 : 0,
                    y.data_ptr(), cur_stream());
@@ -574,9 +581,9 @@ Tensor bn_relu_fwd(const Tensor& x, const Tensor& gamma, const Tensor& beta, con
 std::vector<Tensor> bn_relu_bwd(const Tensor& x, const Tensor& dy, const Tensor& gamma, const Tensor& beta,
                                 const Tensor& mean, const Tensor& var, double eps, bool fix_gamma, bool relu,
                                 bool need_dx, bool need_params, c10::optional<Tensor> dgamma_out,
-                                c10::optional<Tensor> dbeta_out, c10::optional<Tensor> dres, bool x2) {
+                                c10::optional<Tensor> dbeta_out, c10::optional<Tensor> dres, int64_t x2) {
   CHECK_DEV(x); CHECK_DEV(dy);
-  TORCH_CHECK(!x2 || (x.scalar_type() == at::kBFloat16 && x.size(0) % 2 == 0 && x.size(1) % 4 == 0),
+  TORCH_CHECK(!x2 || (x.scalar_type() == at::kBFloat16 && x.size(0) % npl(x2) == 0 && x.size(1) % 4 == 0),
               "bn_relu_bwd x2: bf16 (2N, C, H, W) pairs, C % 4 == 0");
   TORCH_CHECK(x.is_contiguous(at::MemoryFormat::ChannelsLast), "x must be channels_last");
   Tensor g = dy.contiguous(at::MemoryFormat::ChannelsLast);
@@ -607,9 +614,9 @@ std::vector<Tensor> bn_relu_bwd(const Tensor& x, const Tensor& dy, const Tensor&
     TORCH_CHECK(rd.scalar_type() == x.scalar_type() && rd.sizes() == x.sizes(), "dres must match x");
   }
   Tensor ws;
-  const int64_t M = x.numel() / C / (x2 ? 2 : 1);
+  const int64_t M = x.numel() / C / (x2 ? npl(x2) : 1);
   if (need_params && vec) ws = at::empty({mxr::bn_bwd_workspace_floats(M, C)}, x.options().dtype(at::kFloat));
-  mxr::bn_relu_bwd(x.data_ptr(), g.data_ptr(), x2 ? 3 : dcode(x), M, C, gamma.data_ptr<float>(),
+  mxr::bn_relu_bwd(x.data_ptr(), g.data_ptr(), x2 ? pcode(x2) : dcode(x), M, C, gamma.data_ptr<float>(),
                    beta.data_ptr<float>(), mean.data_ptr<float>(), var.data_ptr<float>(), (float)eps,
                    fix_gamma ? 1 : 0, relu ? 1 : 0, need_dx ? dx.data_ptr() : nullptr,
                    rd.defined() ? rd.data_ptr() : nullptr, need_params ? dgamma.data_ptr<float>() : nullptr, need_params ? dbeta.data_ptr<float>() : nullptr,
@@ -675,17 +682,20 @@ void set_dadd(mxr::ConvEpi& ep, const Tensor& dadd, const Tensor& y, int Ho, int
 }
 
 // ReLU (+ dropout) backward: dy * [y > 0] * scale; x2: dy (2N, ...) pairs, y the ReLU output pair
-Tensor relu_mask_bwd(const Tensor& dy, const Tensor& y, double scale, bool x2) {
+Tensor relu_mask_bwd(const Tensor& dy, const Tensor& y, double scale, int64_t x2) {
   CHECK_DEV(dy); CHECK_DEV(y);
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && y.scalar_type() == at::kBFloat16 && dy.sizes() == y.sizes() &&
                   dy.is_contiguous(at::MemoryFormat::ChannelsLast) && y.is_contiguous(at::MemoryFormat::ChannelsLast),
               "relu_mask_bwd: bf16 channels_last dy / y of one shape");
-  const int64_t n = x2 ? dy.numel() / 2 : dy.numel();
-  TORCH_CHECK(n % 8 == 0 && (!x2 || dy.size(0) % 2 == 0), "relu_mask_bwd: numel % 8 (pairs: 2N rows)");
+  const int64_t n = x2 ? dy.numel() / npl(x2) : dy.numel();
+  TORCH_CHECK(n % 8 == 0 && (!x2 || dy.size(0) % npl(x2) == 0), "relu_mask_bwd: numel % 8 (pairs: 2N rows)");
   DevGuard g(dy.device());
   Tensor out = at::empty_like(dy, dy.options(), at::MemoryFormat::ChannelsLast);
-  mxr::relu_mask(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<const uint16_t*>(y.data_ptr()),
-                 reinterpret_cast<uint16_t*>(out.data_ptr()), n, x2 ? n : 0, (float)scale, cur_stream());
+  // the sign of a multi-plane value is its hi plane's: plane 0 of a pair, plane 1 of a triple
+  mxr::relu_mask(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                 reinterpret_cast<const uint16_t*>(y.data_ptr()) + (npl(x2) == 3 ? n : 0),
+                 reinterpret_cast<uint16_t*>(out.data_ptr()), n, x2 ? n : 0, (float)scale, cur_stream(),
+                 x2 ? npl(x2) : 1);
   return out;
 }
 
@@ -699,7 +709,7 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
                                    c10::optional<Tensor> dbeta_out, double drop_p, int64_t drop_seed,
                                    c10::optional<Tensor> drop_step, int64_t pad_w, c10::optional<Tensor> out,
                                    c10::optional<std::vector<int64_t>> out_map, c10::optional<Tensor> stat_shift,
-                                   c10::optional<Tensor> bnb_part, int64_t bnb_row0, bool x2, int64_t w_plane,
+                                   c10::optional<Tensor> bnb_part, int64_t bnb_row0, int64_t x2, int64_t w_plane,
                                    bool out_f32, bool bt, c10::optional<Tensor> rmask, double rmask_scale) {
   CHECK_DEV(x); CHECK_DEV(w);
   TORCH_CHECK((x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf) && w.scalar_type() == x.scalar_type(),
@@ -709,9 +719,9 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   TORCH_CHECK(w.dim() == 4 && w.is_contiguous(at::MemoryFormat::ChannelsLast), "w must be channels_last (O,I,kh,kw)");
   // x2 (fp32-class): x / y / residual / bnb_x / dadd are (2N, ...) hi / lo plane pairs, w's lo plane
   // sits w_plane elements after it (the flat shadow or the dgrad cache); out_f32: fp32 (N, ...) output
-  TORCH_CHECK(!x2 || (!f16 && x.size(0) % 2 == 0 && w_plane >= w.numel()), "x2: bf16 pairs (2N, ...) and w_plane");
+  TORCH_CHECK(!x2 || (!f16 && x.size(0) % npl(x2) == 0 && w_plane >= w.numel()), "x2: bf16 pairs (2N, ...) and w_plane");
   TORCH_CHECK(!out_f32 || x2, "out_f32 needs x2");
-  const int NB = (int)(x2 ? x.size(0) / 2 : x.size(0)), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int NB = (int)(x2 ? x.size(0) / npl(x2) : x.size(0)), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
   // bt: a data gradient reading the forward filter w (Cout_f, Cin_f, kh, kw) directly -- this launch's
   // input channels are the filter's outputs and its outputs the filter's inputs (taps flipped in-kernel)
   const int Cout = (int)(bt ? w.size(1) : w.size(0)), KH = (int)w.size(2), KW = (int)w.size(3);
@@ -752,7 +762,7 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   }
   DevGuard g(x.device());
   Tensor y;
-  const int NY = x2 && !out_f32 ? 2 * NB : NB;  // leading dim of y (pairs: 2N)
+  const int NY = x2 && !out_f32 ? npl(x2) * NB : NB;  // leading dim of y (pairs: 2N, triples: 3N)
   if (mapped) {
     y = *out;
     TORCH_CHECK(!out_f32 && y.scalar_type() == at::kBFloat16 && y.is_contiguous(at::MemoryFormat::ChannelsLast) &&
@@ -764,12 +774,13 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   }
   if (x2) {
     ep.x2 = 1;
-    ep.x2_pa = (uint32_t)(x.numel() / 2 * 2);
+    ep.x3 = npl(x2) == 3 ? 1 : 0;
+    ep.x2_pa = (uint32_t)(x.numel() / npl(x2) * 2);
     ep.x2_pb = (uint32_t)(w_plane * 2);
-    TORCH_CHECK(x.numel() < (int64_t)0x40000000 && w_plane + w.numel() < (int64_t)0x40000000,
+    TORCH_CHECK(x.numel() < (int64_t)0x40000000 && (npl(x2) - 1) * w_plane + w.numel() < (int64_t)0x40000000,
                 "x2: operand planes beyond 2 GB (buffer records)");
     if (out_f32) ep.yf = y.data_ptr<float>();
-    else ep.x2_py = y.numel() / 2;
+    else ep.x2_py = y.numel() / npl(x2);
   }
   if (drop_p > 0.0) {
     TORCH_CHECK(drop_p < 1.0, "dropout p must be < 1");
@@ -792,7 +803,8 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
     TORCH_CHECK(!f16 && !out_f32 && r.scalar_type() == at::kBFloat16 && r.sizes() == y.sizes() &&
                     r.is_contiguous(at::MemoryFormat::ChannelsLast),
                 "rmask: a channels_last bf16 tensor shaped like the output (pairs in x2)");
-    ep.rmask = reinterpret_cast<const uint16_t*>(r.data_ptr());
+    // the hi plane carries the sign: plane 0 of a pair, plane 1 of a triple
+    ep.rmask = reinterpret_cast<const uint16_t*>(r.data_ptr()) + (ep.x3 ? r.numel() / 3 : 0);
     ep.rmask_s = (float)rmask_scale;
   }
   Tensor y2;
@@ -820,7 +832,7 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
                     bx.is_contiguous(at::MemoryFormat::ChannelsLast), "bnb_x must be channels_last bf16 like y");
     ep.bnb_x = reinterpret_cast<const uint16_t*>(bx.data_ptr());
     if (dadd.has_value() && dadd->defined()) set_dadd(ep, *dadd, y, Ho, Wo, mapped);
-    if (x2 && ep.dadd) ep.x2_pd = dadd->numel() / 2;
+    if (x2 && ep.dadd) ep.x2_pd = dadd->numel() / npl(x2);
     const bool det = bnb_part.has_value() && bnb_part->defined();
     if (det) {
       // deterministic column sums: 64-row tiles (tile 23) write rows bnb_row0 .. + ceil(M / 64)
@@ -908,6 +920,9 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
       std::vector<std::pair<int, int>> cands = {{t, sp}};
       for (int c : {23, 22, 101, 104, 105, 106, 108, 109, 110, 111})
         if (c != t || sp != 1) cands.push_back({c, 1});
+      // K groups (conv_kg.hip): 2-4 four-wave groups per 64x64 tile, each over a slice of K
+      if (!f16 && Cout % 8 == 0 && getenv("MXR_NO_KG") == nullptr)
+        for (int c : {27, 28, 29}) cands.push_back({c, 1});
       // fp32-class pairs: the wide-stage kernel (64 channels of both planes per LDS stage) is an
       // A/B candidate only (MXR_X2W=1): 13-26 % faster in isolation on the stage-3/4 and RPN convs,
       // but the headline step measured 1 % slower with it in the autotune (same-box interleaved)
@@ -1022,7 +1037,7 @@ std::vector<Tensor> conv_dgrad_wgrad(const Tensor& x, const Tensor& w, int64_t p
                                      c10::optional<Tensor> dgamma, c10::optional<Tensor> dbeta, const Tensor& wg_dy,
                                      const Tensor& wg_x, int64_t KH, int64_t KW, int64_t wg_stride, int64_t wg_pad,
                                      Tensor wg_out, bool defer, c10::optional<Tensor> prev_slab,
-                                     c10::optional<Tensor> prev_out, c10::optional<Tensor> bnb_part, bool x2,
+                                     c10::optional<Tensor> prev_out, c10::optional<Tensor> bnb_part, int64_t x2,
                                      int64_t w_plane, bool bt, c10::optional<Tensor> rmask, double rmask_scale) {
   CHECK_DEV(x); CHECK_DEV(w); CHECK_DEV(wg_dy); CHECK_DEV(wg_x); CHECK_DEV(wg_out);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && w.scalar_type() == at::kBFloat16 &&
@@ -1030,22 +1045,23 @@ std::vector<Tensor> conv_dgrad_wgrad(const Tensor& x, const Tensor& w, int64_t p
               "conv_dgrad_wgrad: channels_last bf16 x / w");
   // x2: dY / x / residual / bnb_x / dadd / wg_x are (2N, ...) pairs, w's lo plane w_plane elements on,
   // the weight gradient wg_out fp32
-  TORCH_CHECK(!x2 || (x.size(0) % 2 == 0 && w_plane >= w.numel()), "x2: (2N, ...) pairs and w_plane");
-  const int NB = (int)(x2 ? x.size(0) / 2 : x.size(0)), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  TORCH_CHECK(!x2 || (x.size(0) % npl(x2) == 0 && w_plane >= w.numel()), "x2: (2N, ...) pairs and w_plane");
+  const int NB = (int)(x2 ? x.size(0) / npl(x2) : x.size(0)), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
   // bt: the dgrad reads the forward filter w (Cin, Cout, kh, kw) directly (see conv_igemm_fwd)
   const int Cout = (int)(bt ? w.size(1) : w.size(0)), kh = (int)w.size(2), kw = (int)w.size(3);
   TORCH_CHECK((bt ? w.size(0) : w.size(1)) == Cin && Cin % 64 == 0 && Cout % 8 == 0, "conv_dgrad_wgrad: dgrad channels");
   const int Ho = H + 2 * (int)pad - kh + 1, Wo = W + 2 * (int)pad - kw + 1;
   mxr::ConvEpi ep;
   ep.bt = bt ? 1 : 0;
-  Tensor y = at::empty({x2 ? 2 * NB : NB, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor y = at::empty({x2 ? npl(x2) * NB : NB, Cout, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   if (x2) {
     TORCH_CHECK(x.numel() < (int64_t)0x40000000 && w_plane + w.numel() < (int64_t)0x40000000,
                 "x2: operand planes beyond 2 GB (buffer records)");
     ep.x2 = 1;
-    ep.x2_pa = (uint32_t)(x.numel() / 2 * 2);
+    ep.x3 = npl(x2) == 3 ? 1 : 0;
+    ep.x2_pa = (uint32_t)(x.numel() / npl(x2) * 2);
     ep.x2_pb = (uint32_t)(w_plane * 2);
-    ep.x2_py = y.numel() / 2;
+    ep.x2_py = y.numel() / npl(x2);
   }
   if (residual.has_value() && residual->defined()) {
     TORCH_CHECK(residual->scalar_type() == at::kBFloat16 && residual->sizes() == y.sizes() &&
@@ -1056,7 +1072,7 @@ std::vector<Tensor> conv_dgrad_wgrad(const Tensor& x, const Tensor& w, int64_t p
     TORCH_CHECK(!bn.has_value() && rmask->scalar_type() == at::kBFloat16 && rmask->sizes() == y.sizes() &&
                     rmask->is_contiguous(at::MemoryFormat::ChannelsLast),
                 "rmask: channels_last bf16 like y, no BN epilogue");
-    ep.rmask = reinterpret_cast<const uint16_t*>(rmask->data_ptr());
+    ep.rmask = reinterpret_cast<const uint16_t*>(rmask->data_ptr()) + (ep.x3 ? rmask->numel() / 3 : 0);
     ep.rmask_s = (float)rmask_scale;
   }
   std::vector<Tensor> bnf;
@@ -1079,7 +1095,7 @@ std::vector<Tensor> conv_dgrad_wgrad(const Tensor& x, const Tensor& w, int64_t p
                 "bn needs bnb_x like y");
     ep.bnb_x = reinterpret_cast<const uint16_t*>(bnb_x->data_ptr());
     if (dadd.has_value() && dadd->defined()) set_dadd(ep, *dadd, y, Ho, Wo, false);
-    if (x2 && ep.dadd) ep.x2_pd = dadd->numel() / 2;
+    if (x2 && ep.dadd) ep.x2_pd = dadd->numel() / npl(x2);
     if (bnb_part.has_value() && bnb_part->defined()) {  // deterministic sums, 64-row dgrad tiles
       TORCH_CHECK(bnb_part->scalar_type() == at::kFloat && bnb_part->is_contiguous() &&
                       bnb_part->numel() >= (((int64_t)NB * Ho * Wo + 63) / 64) * 2 * Cout,
@@ -1100,8 +1116,8 @@ std::vector<Tensor> conv_dgrad_wgrad(const Tensor& x, const Tensor& w, int64_t p
   TORCH_CHECK(wg_dy.scalar_type() == at::kBFloat16 && wg_x.scalar_type() == at::kBFloat16 &&
                   wg_dy.is_contiguous(at::MemoryFormat::ChannelsLast) && wg_x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "conv_dgrad_wgrad: channels_last bf16 wg_dy / wg_x");
-  TORCH_CHECK(!x2 || (wg_x.size(0) % 2 == 0 && wg_dy.size(0) % 2 == 0), "x2: wg_dy / wg_x pairs");
-  const int gNB = (int)(x2 ? wg_x.size(0) / 2 : wg_x.size(0)), gCin = (int)wg_x.size(1), gH = (int)wg_x.size(2),
+  TORCH_CHECK(!x2 || (wg_x.size(0) % npl(x2) == 0 && wg_dy.size(0) % npl(x2) == 0), "x2: wg_dy / wg_x pairs");
+  const int gNB = (int)(x2 ? wg_x.size(0) / npl(x2) : wg_x.size(0)), gCin = (int)wg_x.size(1), gH = (int)wg_x.size(2),
             gW = (int)wg_x.size(3);
   const int gCout = (int)wg_dy.size(1), gHo = (int)wg_dy.size(2), gWo = (int)wg_dy.size(3);
   TORCH_CHECK(wg_dy.size(0) == wg_x.size(0) && gCin % 64 == 0 && gCout % 8 == 0, "conv_dgrad_wgrad: wgrad channels");
@@ -1114,8 +1130,9 @@ std::vector<Tensor> conv_dgrad_wgrad(const Tensor& x, const Tensor& w, int64_t p
   mxr::WgradX2 wx2;
   if (x2) {
     wx2.x2 = 1;
-    wx2.pdy = (uint32_t)(wg_dy.numel() / 2 * 2);
-    wx2.px = (uint32_t)(wg_x.numel() / 2 * 2);
+    wx2.x3 = npl(x2) == 3 ? 1 : 0;
+    wx2.pdy = (uint32_t)(wg_dy.numel() / npl(x2) * 2);
+    wx2.px = (uint32_t)(wg_x.numel() / npl(x2) * 2);
     wx2.dwf = wg_out.data_ptr<float>();
   }
   const float* pslab = nullptr;
@@ -1162,69 +1179,69 @@ void wgrad_reduce_run(const Tensor& slab, Tensor out) {
 }
 
 // ---- pooling ---------------------------------------------------------------------------------
-std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t p, bool x2) {
+std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t p, int64_t x2) {
   CHECK_DEV(x);
   TORCH_CHECK((x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf) && x.dim() == 4 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "maxpool: x must be channels_last bf16 / fp16 (N,C,H,W)");
-  TORCH_CHECK(!x2 || (x.scalar_type() == at::kBFloat16 && x.size(0) % 2 == 0), "maxpool x2: bf16 (2N, ...) pairs");
-  const int N = (int)(x2 ? x.size(0) / 2 : x.size(0)), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  TORCH_CHECK(!x2 || (x.scalar_type() == at::kBFloat16 && x.size(0) % npl(x2) == 0), "maxpool x2: bf16 (2N, ...) pairs");
+  const int N = (int)(x2 ? x.size(0) / npl(x2) : x.size(0)), C = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
   TORCH_CHECK(C % 8 == 0, "maxpool needs C % 8 == 0");
   const int Ho = (H + 2 * (int)p - (int)k) / (int)s + 1, Wo = (W + 2 * (int)p - (int)k) / (int)s + 1;
   TORCH_CHECK(Ho > 0 && Wo > 0, "maxpool: empty output");
   DevGuard g(x.device());
-  Tensor y = at::empty({x2 ? 2 * N : N, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor y = at::empty({x2 ? npl(x2) * N : N, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   Tensor arg = at::empty({N, C, Ho, Wo}, x.options().dtype(at::kByte).memory_format(at::MemoryFormat::ChannelsLast));
   const int rc = mxr::maxpool_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<uint16_t*>(y.data_ptr()),
                                   arg.data_ptr<uint8_t>(), N, H, W, C, Ho, Wo, (int)k, (int)s, (int)p,
-                                  x2 ? 3 : dcode(x), cur_stream());
+                                  x2 ? pcode(x2) : dcode(x), cur_stream());
   TORCH_CHECK(rc == 0, "maxpool_fwd: unsupported shape");
   return {y, arg};
 }
 
 Tensor maxpool_bwd(const Tensor& dy, const Tensor& arg, int64_t H, int64_t W, int64_t k, int64_t s, int64_t p,
-                   bool x2) {
+                   int64_t x2) {
   CHECK_DEV(dy); CHECK_DEV(arg);
   TORCH_CHECK((dy.scalar_type() == at::kBFloat16 || dy.scalar_type() == at::kHalf) &&
                   dy.is_contiguous(at::MemoryFormat::ChannelsLast) && arg.scalar_type() == at::kByte &&
-                  arg.size(0) * (x2 ? 2 : 1) == dy.size(0) && arg.size(1) == dy.size(1) && arg.size(2) == dy.size(2) &&
+                  arg.size(0) * (x2 ? npl(x2) : 1) == dy.size(0) && arg.size(1) == dy.size(1) && arg.size(2) == dy.size(2) &&
                   arg.size(3) == dy.size(3) && arg.is_contiguous(at::MemoryFormat::ChannelsLast),
               "maxpool_bwd: channels_last bf16 dy (2N: x2 pairs) + byte arg (N, ...)");
   const int N = (int)arg.size(0), C = (int)dy.size(1), Ho = (int)dy.size(2), Wo = (int)dy.size(3);
   TORCH_CHECK((H + 2 * p - k) / s + 1 == Ho && (W + 2 * p - k) / s + 1 == Wo, "maxpool_bwd: shape mismatch");
   DevGuard g(dy.device());
-  Tensor dx = at::empty({x2 ? 2 * N : N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor dx = at::empty({x2 ? npl(x2) * N : N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   const int rc = mxr::maxpool_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), arg.data_ptr<uint8_t>(),
                                   reinterpret_cast<uint16_t*>(dx.data_ptr()), N, (int)H, (int)W, C, Ho, Wo, (int)k,
-                                  (int)s, (int)p, x2 ? 3 : dcode(dy), cur_stream());
+                                  (int)s, (int)p, x2 ? pcode(x2) : dcode(dy), cur_stream());
   TORCH_CHECK(rc == 0, "maxpool_bwd: unsupported shape");
   return dx;
 }
 
-Tensor avgpool_fwd(const Tensor& x, bool x2) {
+Tensor avgpool_fwd(const Tensor& x, int64_t x2) {
   CHECK_DEV(x);
   TORCH_CHECK((x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf) && x.dim() == 4 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "avgpool: x must be channels_last bf16 / fp16 (N,C,H,W)");
-  TORCH_CHECK(!x2 || (x.scalar_type() == at::kBFloat16 && x.size(0) % 2 == 0), "avgpool x2: bf16 (2N, ...) pairs");
-  const int N = (int)(x2 ? x.size(0) / 2 : x.size(0)), C = (int)x.size(1), HW = (int)(x.size(2) * x.size(3));
+  TORCH_CHECK(!x2 || (x.scalar_type() == at::kBFloat16 && x.size(0) % npl(x2) == 0), "avgpool x2: bf16 (2N, ...) pairs");
+  const int N = (int)(x2 ? x.size(0) / npl(x2) : x.size(0)), C = (int)x.size(1), HW = (int)(x.size(2) * x.size(3));
   DevGuard g(x.device());
-  Tensor y = at::empty({x2 ? 2 * N : N, C}, x.options());
+  Tensor y = at::empty({x2 ? npl(x2) * N : N, C}, x.options());
   TORCH_CHECK(mxr::avgpool_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<uint16_t*>(y.data_ptr()),
-                               N, HW, C, x2 ? 3 : dcode(x), cur_stream()) == 0, "avgpool_fwd: C % 8 != 0");
+                               N, HW, C, x2 ? pcode(x2) : dcode(x), cur_stream()) == 0, "avgpool_fwd: C % 8 != 0");
   return y;
 }
 
-Tensor avgpool_bwd(const Tensor& dy, int64_t H, int64_t W, bool x2) {
+Tensor avgpool_bwd(const Tensor& dy, int64_t H, int64_t W, int64_t x2) {
   CHECK_DEV(dy);
   TORCH_CHECK((dy.scalar_type() == at::kBFloat16 || dy.scalar_type() == at::kHalf) && dy.dim() == 2 && dy.is_contiguous(),
               "avgpool_bwd: dy (N, C) bf16 / fp16");
-  TORCH_CHECK(!x2 || (dy.scalar_type() == at::kBFloat16 && dy.size(0) % 2 == 0), "avgpool_bwd x2: bf16 (2N, C) pairs");
-  const int N = (int)(x2 ? dy.size(0) / 2 : dy.size(0)), C = (int)dy.size(1);
+  TORCH_CHECK(!x2 || (dy.scalar_type() == at::kBFloat16 && dy.size(0) % npl(x2) == 0), "avgpool_bwd x2: bf16 (2N, C) pairs");
+  const int N = (int)(x2 ? dy.size(0) / npl(x2) : dy.size(0)), C = (int)dy.size(1);
   DevGuard g(dy.device());
-  Tensor dx = at::empty({x2 ? 2 * N : N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor dx = at::empty({x2 ? npl(x2) * N : N, C, H, W}, dy.options().memory_format(at::MemoryFormat::ChannelsLast));
   TORCH_CHECK(mxr::avgpool_bwd(reinterpret_cast<const uint16_t*>(dy.data_ptr()), reinterpret_cast<uint16_t*>(dx.data_ptr()),
-                               N, (int)(H * W), C, x2 ? 3 : dcode(dy), cur_stream()) == 0, "avgpool_bwd: C % 8 != 0");
+                               N, (int)(H * W), C, x2 ? pcode(x2) : dcode(dy), cur_stream()) == 0, "avgpool_bwd: C % 8 != 0");
   return dx;
 }
 
@@ -1233,14 +1250,16 @@ Tensor stem_conv(const Tensor& x, const Tensor& w, const std::vector<Tensor>& in
                  const std::vector<Tensor>& out_bn, double out_eps, bool out_fixg, const c10::optional<Tensor>& bias,
                  int64_t KH, int64_t KW, int64_t stride, int64_t pad, bool relu) {
   CHECK_DEV(x); CHECK_DEV(w);
-  // fp32-class mode: an fp32 image, the packed filter an x2 pair (128, KP) and the output x2 pairs
+  // fp32 modes: an fp32 image, the packed filter an x2 pair (128, KP) / x3 triple (192, KP) in the
+  // logical plane order (hi, lo) / (hi, mid, lo), and the output x2 pairs / x3 triples
   const bool x2 = x.scalar_type() == at::kFloat;
+  const int sp = x2 ? (w.size(0) == 192 ? 3 : 2) : 1;
   TORCH_CHECK((x2 || x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf) && x.dim() == 4 &&
                   x.size(1) == 3 && x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "stem_conv: x must be channels_last fp32 / bf16 / fp16 (N,3,H,W)");
   const int64_t KP = (KH * KW * 3 + 31) / 32 * 32;
   TORCH_CHECK(w.scalar_type() == (x2 ? at::kBFloat16 : x.scalar_type()) && w.dim() == 2 &&
-                  w.size(0) == (x2 ? 128 : 64) && w.size(1) == KP && w.is_contiguous(),
+                  w.size(0) == 64 * sp && w.size(1) == KP && w.is_contiguous(),
               "stem_conv: w must be the packed contiguous (64, KP) filter of x's dtype ((128, KP) x2 pair for fp32)");
   mxr::StemArgs a{};
   TORCH_CHECK(in_bn.empty() || in_bn.size() == 4, "stem_conv: in_bn = [] or [gamma, beta, mean, var]");
@@ -1274,12 +1293,12 @@ Tensor stem_conv(const Tensor& x, const Tensor& w, const std::vector<Tensor>& in
   const int Ho = (int)((H + 2 * pad - KH) / stride + 1), Wo = (int)((W + 2 * pad - KW) / stride + 1);
   TORCH_CHECK(Ho > 0 && Wo > 0, "stem_conv: empty output");
   DevGuard g(x.device());
-  Tensor y = at::empty({x2 ? 2 * N : N, 64, Ho, Wo},
+  Tensor y = at::empty({sp * N, 64, Ho, Wo},
                        x.options().dtype(x2 ? at::kBFloat16 : x.scalar_type()).memory_format(at::MemoryFormat::ChannelsLast));
   const int rc = mxr::stem_conv(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                                 reinterpret_cast<const uint16_t*>(w.data_ptr()), a,
                                 reinterpret_cast<uint16_t*>(y.data_ptr()), N, H, W, Ho, Wo, (int)KH, (int)KW,
-                                (int)stride, (int)pad, relu ? 1 : 0, x2 ? 3 : dcode(x), cur_stream());
+                                (int)stride, (int)pad, relu ? 1 : 0, x2 ? (sp == 3 ? 4 : 3) : dcode(x), cur_stream());
   TORCH_CHECK(rc == 0, "stem_conv: unsupported geometry (7x7/2 and 3x3/1 only) or grid too large");
   LAUNCH_CHECK("stem_conv");
   return y;
@@ -1293,7 +1312,7 @@ bool al16(const Tensor& t) { return (reinterpret_cast<uintptr_t>(t.data_ptr()) &
 // empty (skipped).  Returns dx (M, K), ReLU-masked by x > 0 when relu_mask (empty unless need_dx).
 Tensor head_bwd(const Tensor& x, const std::vector<Tensor>& dys, const std::vector<Tensor>& ws,
                 const std::vector<Tensor>& dws, const std::vector<bool>& dw_acc, const std::vector<Tensor>& dbs,
-                const std::vector<bool>& db_acc, bool need_dx, bool relu_mask, bool x2,
+                const std::vector<bool>& db_acc, bool need_dx, bool relu_mask, int64_t x2,
                 const std::vector<int64_t>& w_planes, double mask_scale) {
   CHECK_DEV(x);
   const int nh = (int)dys.size();
@@ -1303,12 +1322,13 @@ Tensor head_bwd(const Tensor& x, const std::vector<Tensor>& dys, const std::vect
               "head_bwd: x must be a contiguous 16-B aligned bf16 (M, K) matrix");
   // x2 (fp32-class): x (2M, K) and dx are hi / lo pairs, each w_h a pair with its lo plane
   // w_planes[h] elements on, dy / dw fp32
-  TORCH_CHECK(!x2 || (x.size(0) % 2 == 0 && (int)w_planes.size() == nh), "head_bwd x2: (2M, K) x and w_planes");
-  const int M = (int)(x2 ? x.size(0) / 2 : x.size(0)), K = (int)x.size(1);
+  TORCH_CHECK(!x2 || (x.size(0) % npl(x2) == 0 && (int)w_planes.size() == nh), "head_bwd x2: (2M, K) x and w_planes");
+  const int M = (int)(x2 ? x.size(0) / npl(x2) : x.size(0)), K = (int)x.size(1);
   TORCH_CHECK(K % 64 == 0, "head_bwd: K % 64 == 0");
   mxr::HeadBwdArgs a;
   a.nheads = nh;
   a.x2 = x2 ? 1 : 0;
+  a.x3 = npl(x2) == 3 ? 1 : 0;
   const auto adt = x2 ? at::kFloat : at::kBFloat16;  // dy / dw dtype
   for (int h = 0; h < nh; ++h) {
     const Tensor &dy = dys[h], &w = ws[h], &dw = dws[h], &db = dbs[h];
@@ -1343,7 +1363,7 @@ Tensor head_bwd(const Tensor& x, const std::vector<Tensor>& dys, const std::vect
   DevGuard g(x.device());
   Tensor dx;
   if (need_dx) {
-    dx = at::empty({x2 ? 2 * M : M, K}, x.options());
+    dx = at::empty({x2 ? npl(x2) * M : M, K}, x.options());
     a.dx = reinterpret_cast<uint16_t*>(dx.data_ptr());
     a.relu_mask = relu_mask ? 1 : 0;
     a.mask_scale = (float)mask_scale;
@@ -1368,9 +1388,9 @@ Tensor head_bwd(const Tensor& x, const std::vector<Tensor>& dys, const std::vect
 }
 
 // per-channel sum of a channels_last map or (M, C) matrix into out (C,) fp32 / bf16 (+= when accumulate)
-void chan_sum(const Tensor& x, Tensor out, bool accumulate, bool x2) {
+void chan_sum(const Tensor& x, Tensor out, bool accumulate, int64_t x2) {
   CHECK_DEV(x); CHECK_DEV(out);
-  TORCH_CHECK(!x2 || (x.scalar_type() == at::kBFloat16 && x.size(0) % 2 == 0), "chan_sum x2: bf16 (2N, ...) pairs");
+  TORCH_CHECK(!x2 || (x.scalar_type() == at::kBFloat16 && x.size(0) % npl(x2) == 0), "chan_sum x2: bf16 (2N, ...) pairs");
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf, "chan_sum: bf16 / fp16 input");
   int64_t C;
   if (x.dim() == 4) {
@@ -1382,10 +1402,10 @@ void chan_sum(const Tensor& x, Tensor out, bool accumulate, bool x2) {
   }
   TORCH_CHECK(C % 8 == 0 && al16(x), "chan_sum: C % 8 == 0 and 16-B aligned rows");
   TORCH_CHECK(out.numel() == C && out.is_contiguous(), "chan_sum: out (C,) contiguous");
-  const int64_t M = x.numel() / C / (x2 ? 2 : 1);
+  const int64_t M = x.numel() / C / (x2 ? npl(x2) : 1);
   DevGuard g(x.device());
   Tensor part = at::empty({(int64_t)mxr::chan_sum_chunks(M, (int)C) * C}, x.options().dtype(at::kFloat));
-  TORCH_CHECK(mxr::chan_sum(reinterpret_cast<const uint16_t*>(x.data_ptr()), M, (int)C, x2 ? 3 : dcode(x),
+  TORCH_CHECK(mxr::chan_sum(reinterpret_cast<const uint16_t*>(x.data_ptr()), M, (int)C, x2 ? pcode(x2) : dcode(x),
                             part.data_ptr<float>(), out.data_ptr(), dcode(out), accumulate ? 1 : 0, cur_stream()) == 0,
               "chan_sum: unsupported shape");
 }
@@ -1466,12 +1486,12 @@ Tensor philox_uniform_cpu(int64_t seed, int64_t step, int64_t n) {
 
 // ---- training-mode BN ----------------------------------------------------------------------
 std::vector<Tensor> bn_train_fwd(const Tensor& x, const Tensor& gamma, const Tensor& beta, Tensor rmean, Tensor rvar,
-                                 double momentum, double eps, bool fix_gamma, bool relu, bool x2) {
+                                 double momentum, double eps, bool fix_gamma, bool relu, int64_t x2) {
   CHECK_DEV(x);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "x: bf16 NHWC");
-  TORCH_CHECK(!x2 || x.size(0) % 2 == 0, "x2: (2N, ...) pairs");
+  TORCH_CHECK(!x2 || x.size(0) % npl(x2) == 0, "x2: (2N, ...) pairs");
   const int C = (int)x.size(1);
-  const int64_t M = x.numel() / C / (x2 ? 2 : 1);
+  const int64_t M = x.numel() / C / (x2 ? npl(x2) : 1);
   TORCH_CHECK(C % 64 == 0, "bn_train needs C % 64 == 0");
   CHECK_F32(rmean); CHECK_F32(rvar); CHECK_CONTIG(rmean); CHECK_CONTIG(rvar);
   DevGuard g(x.device());
@@ -1485,7 +1505,7 @@ std::vector<Tensor> bn_train_fwd(const Tensor& x, const Tensor& gamma, const Ten
                                   gf.data_ptr<float>(), bf.data_ptr<float>(), rmean.data_ptr<float>(),
                                   rvar.data_ptr<float>(), (float)momentum, (float)eps, fix_gamma ? 1 : 0, relu ? 1 : 0,
                                   reinterpret_cast<uint16_t*>(y.data_ptr()), sv, sv + C, ws.data_ptr<float>(),
-                                  cur_stream(), sv + 2 * C, x2 ? 1 : 0);
+                                  cur_stream(), sv + 2 * C, x2 ? npl(x2) : 0);
   TORCH_CHECK(r == 0, "bn_train_fwd: unsupported shape");
   return {y, save};
 }
@@ -1493,12 +1513,12 @@ std::vector<Tensor> bn_train_fwd(const Tensor& x, const Tensor& gamma, const Ten
 // normalisation from conv-epilogue statistics partials (conv_igemm_fwd(..., stat_shift=rmean)[1])
 std::vector<Tensor> bn_train_apply(const Tensor& x, const Tensor& part, const Tensor& gamma, const Tensor& beta,
                                    Tensor rmean, Tensor rvar, double momentum, double eps, bool fix_gamma, bool relu,
-                                   bool x2) {
+                                   int64_t x2) {
   CHECK_DEV(x); CHECK_DEV(part);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "x: bf16 NHWC");
-  TORCH_CHECK(!x2 || x.size(0) % 2 == 0, "x2: (2N, ...) pairs");
+  TORCH_CHECK(!x2 || x.size(0) % npl(x2) == 0, "x2: (2N, ...) pairs");
   const int C = (int)x.size(1);
-  const int64_t M = x.numel() / C / (x2 ? 2 : 1);
+  const int64_t M = x.numel() / C / (x2 ? npl(x2) : 1);
   TORCH_CHECK(C % 64 == 0, "bn_train needs C % 64 == 0");
   CHECK_F32(rmean); CHECK_F32(rvar); CHECK_CONTIG(rmean); CHECK_CONTIG(rvar);
   TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && part.dim() == 2 && part.size(1) == C &&
@@ -1512,7 +1532,7 @@ std::vector<Tensor> bn_train_apply(const Tensor& x, const Tensor& part, const Te
                                     bf.data_ptr<float>(), rmean.data_ptr<float>(), rvar.data_ptr<float>(),
                                     (float)momentum, (float)eps, fix_gamma ? 1 : 0, relu ? 1 : 0,
                                     reinterpret_cast<uint16_t*>(y.data_ptr()), save.data_ptr<float>(), cur_stream(),
-                                    x2 ? 1 : 0);
+                                    x2 ? npl(x2) : 0);
   TORCH_CHECK(r == 0, "bn_train_apply: unsupported shape");
   return {y, save};
 }
@@ -1521,11 +1541,11 @@ std::vector<Tensor> bn_train_apply(const Tensor& x, const Tensor& part, const Te
 // bn = (gamma_eff, beta, save[0], save[2]), eps 0, bnb_part = part) produced o; nparts partial rows
 Tensor bn_train_dx_apply(Tensor o, const Tensor& x, const Tensor& save, const Tensor& gamma_eff, const Tensor& part,
                          int64_t nparts, c10::optional<Tensor> dres, c10::optional<Tensor> dgamma,
-                         c10::optional<Tensor> dbeta, bool x2) {
+                         c10::optional<Tensor> dbeta, int64_t x2) {
   CHECK_DEV(o); CHECK_DEV(x); CHECK_DEV(part);
-  TORCH_CHECK(!x2 || x.size(0) % 2 == 0, "x2: (2N, ...) pairs");
+  TORCH_CHECK(!x2 || x.size(0) % npl(x2) == 0, "x2: (2N, ...) pairs");
   const int C = (int)x.size(1);
-  const int64_t M = x.numel() / C / (x2 ? 2 : 1);
+  const int64_t M = x.numel() / C / (x2 ? npl(x2) : 1);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous(at::MemoryFormat::ChannelsLast) &&
                   o.scalar_type() == at::kBFloat16 && o.is_contiguous(at::MemoryFormat::ChannelsLast) &&
                   o.sizes() == x.sizes(), "o / x: bf16 NHWC of one shape");
@@ -1554,7 +1574,7 @@ Tensor bn_train_dx_apply(Tensor o, const Tensor& x, const Tensor& save, const Te
                                        reinterpret_cast<const uint16_t*>(x.data_ptr()), M, C,
                                        part.data_ptr<float>(), (int)nparts, gamma_eff.data_ptr<float>(),
                                        save.data_ptr<float>(), rp, reinterpret_cast<uint16_t*>(o.data_ptr()), dg, db,
-                                       cur_stream(), x2 ? 1 : 0);
+                                       cur_stream(), x2 ? npl(x2) : 0);
   TORCH_CHECK(r == 0, "bn_train_dx_apply: unsupported shape");
   return o;
 }
@@ -1562,12 +1582,12 @@ Tensor bn_train_dx_apply(Tensor o, const Tensor& x, const Tensor& save, const Te
 std::vector<Tensor> bn_train_bwd(const Tensor& x, const Tensor& dy, const Tensor& gamma, const Tensor& beta,
                                  const Tensor& save_mean, const Tensor& save_invstd, bool fix_gamma, bool relu,
                                  bool need_dx, c10::optional<Tensor> dgamma_out, c10::optional<Tensor> dbeta_out,
-                                 bool x2) {
+                                 int64_t x2) {
   CHECK_DEV(x); CHECK_DEV(dy);
-  TORCH_CHECK(!x2 || (x.size(0) % 2 == 0 && dy.scalar_type() == at::kBFloat16 && dy.sizes() == x.sizes()),
+  TORCH_CHECK(!x2 || (x.size(0) % npl(x2) == 0 && dy.scalar_type() == at::kBFloat16 && dy.sizes() == x.sizes()),
               "x2: (2N, ...) bf16 pairs");
   const int C = (int)x.size(1);
-  const int64_t M = x.numel() / C / (x2 ? 2 : 1);
+  const int64_t M = x.numel() / C / (x2 ? npl(x2) : 1);
   TORCH_CHECK(x.scalar_type() == at::kBFloat16 && x.is_contiguous(at::MemoryFormat::ChannelsLast), "x: bf16 NHWC");
   Tensor g = dy.to(at::kBFloat16).contiguous(at::MemoryFormat::ChannelsLast);
   DevGuard dg(x.device());
@@ -1592,7 +1612,7 @@ std::vector<Tensor> bn_train_bwd(const Tensor& x, const Tensor& dy, const Tensor
                                   save_invstd.data_ptr<float>(), fix_gamma ? 1 : 0, relu ? 1 : 0,
                                   need_dx ? reinterpret_cast<uint16_t*>(dx.data_ptr()) : nullptr,
                                   dgm.data_ptr<float>(), dbt.data_ptr<float>(), acc ? 1 : 0, ws.data_ptr<float>(),
-                                  cur_stream(), x2 ? 1 : 0);
+                                  cur_stream(), x2 ? npl(x2) : 0);
   TORCH_CHECK(r == 0, "bn_train_bwd: unsupported shape");
   return {dx, dgm, dbt};
 }
@@ -1689,14 +1709,14 @@ void wt_flip_run(const Tensor& table, int64_t n_entries, int64_t total_tiles) {
 }
 
 Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int64_t stride, int64_t pad,
-                  int64_t splits, c10::optional<Tensor> out, int64_t variant, bool x2) {
+                  int64_t splits, c10::optional<Tensor> out, int64_t variant, int64_t x2) {
   CHECK_DEV(dy); CHECK_DEV(x);
   TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "bf16 only");
   TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) && x.is_contiguous(at::MemoryFormat::ChannelsLast),
               "dy/x must be channels_last");
   // x2: dy / x are (2N, ...) pairs and the gradient is fp32
-  TORCH_CHECK(!x2 || x.size(0) % 2 == 0, "x2: (2N, ...) pairs");
-  const int NB = (int)(x2 ? x.size(0) / 2 : x.size(0)), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  TORCH_CHECK(!x2 || x.size(0) % npl(x2) == 0, "x2: (2N, ...) pairs");
+  const int NB = (int)(x2 ? x.size(0) / npl(x2) : x.size(0)), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
   const int Cout = (int)dy.size(1), Ho = (int)dy.size(2), Wo = (int)dy.size(3);
   TORCH_CHECK(dy.size(0) == x.size(0), "batch mismatch");
   TORCH_CHECK(Cin % 64 == 0 && Cout % 8 == 0, "conv_wgrad requires Cin % 64 == 0 and Cout % 8 == 0");
@@ -1725,8 +1745,9 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int
   if (x2) {
     TORCH_CHECK(x.numel() < (int64_t)0x40000000 && dy.numel() < (int64_t)0x40000000, "x2: planes beyond 2 GB");
     wx2.x2 = 1;
-    wx2.pdy = (uint32_t)(dy.numel() / 2 * 2);
-    wx2.px = (uint32_t)(x.numel() / 2 * 2);
+    wx2.x3 = npl(x2) == 3 ? 1 : 0;
+    wx2.pdy = (uint32_t)(dy.numel() / npl(x2) * 2);
+    wx2.px = (uint32_t)(x.numel() / npl(x2) * 2);
     wx2.dwf = dw.data_ptr<float>();
   }
   Tensor slab = at::empty({(int64_t)sp * Cout * KH * KW * Cin}, x.options().dtype(at::kFloat));
@@ -2016,9 +2037,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("proposal_sample", &proposal_sample);
   m.def("anchor_target_assign", &anchor_target_assign);
   m.def("roi_pool_fwd", &roi_pool_fwd, py::arg("feat"), py::arg("rois"), py::arg("PH"), py::arg("PW"),
-        py::arg("scale"), py::arg("x2") = false);
+        py::arg("scale"), py::arg("x2") = 0);
   m.def("roi_pool_bwd", &roi_pool_bwd, py::arg("grad_out"), py::arg("argmax"), py::arg("rois"), py::arg("B"),
-        py::arg("H"), py::arg("W"), py::arg("grad_add") = py::none(), py::arg("x2") = false);
+        py::arg("H"), py::arg("W"), py::arg("grad_add") = py::none(), py::arg("x2") = 0);
   m.def("rpn_softmax_ce", &rpn_softmax_ce, py::arg("logits"), py::arg("label"), py::arg("norm"), py::arg("grad_scale"),
         py::arg("want_prob"), py::arg("meta") = py::none());
   m.def("row_softmax_ce", &row_softmax_ce);
@@ -2026,13 +2047,15 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("grad_scale"), py::arg("slot") = 2);
   m.def("scale_by_scalar_", &scale_by_scalar_);
   m.def("loss_combine", &loss_combine, py::arg("terms"), py::arg("weights"), py::arg("nonfinite") = py::none());
-  m.def("sgd_momentum", &sgd_momentum);
+  m.def("sgd_momentum", &sgd_momentum, py::arg("w"), py::arg("mom"), py::arg("grad"), py::arg("lr"),
+        py::arg("momentum"), py::arg("wd"), py::arg("rescale"), py::arg("clip"), py::arg("w_bf16") = py::none(),
+        py::arg("planes") = 1);
   m.def("bn_relu_fwd", &bn_relu_fwd, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("mean"), py::arg("var"),
-        py::arg("eps"), py::arg("fix_gamma"), py::arg("relu"), py::arg("x2") = false);
+        py::arg("eps"), py::arg("fix_gamma"), py::arg("relu"), py::arg("x2") = 0);
   m.def("bn_relu_bwd", &bn_relu_bwd, py::arg("x"), py::arg("dy"), py::arg("gamma"), py::arg("beta"),
         py::arg("mean"), py::arg("var"), py::arg("eps"), py::arg("fix_gamma"), py::arg("relu"), py::arg("need_dx"),
         py::arg("need_params"), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(),
-        py::arg("dres") = py::none(), py::arg("x2") = false);
+        py::arg("dres") = py::none(), py::arg("x2") = 0);
   m.def("conv_tune_table", &conv_tune_table, "per-shape conv autotune choices: [(key, tile, splits)]");
   m.def("conv_igemm_fwd", &conv_igemm_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),
         py::arg("pad"), py::arg("relu"), py::arg("tile") = 0, py::arg("splits") = 0, py::arg("residual") = py::none(),
@@ -2041,29 +2064,29 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(), py::arg("drop_p") = 0.0,
         py::arg("drop_seed") = 0, py::arg("drop_step") = py::none(), py::arg("pad_w") = -1,
         py::arg("out") = py::none(), py::arg("out_map") = py::none(), py::arg("stat_shift") = py::none(),
-        py::arg("bnb_part") = py::none(), py::arg("bnb_row0") = 0, py::arg("x2") = false, py::arg("w_plane") = 0,
+        py::arg("bnb_part") = py::none(), py::arg("bnb_row0") = 0, py::arg("x2") = 0, py::arg("w_plane") = 0,
         py::arg("out_f32") = false, py::arg("bt") = false, py::arg("rmask") = py::none(), py::arg("rmask_scale") = 1.0);
-  m.def("relu_mask_bwd", &relu_mask_bwd, py::arg("dy"), py::arg("y"), py::arg("scale") = 1.0, py::arg("x2") = false);
+  m.def("relu_mask_bwd", &relu_mask_bwd, py::arg("dy"), py::arg("y"), py::arg("scale") = 1.0, py::arg("x2") = 0);
   m.def("proposal_topk", &proposal_topk, py::arg("keys"), py::arg("boxes"), py::arg("P"));
   m.def("conv_dgrad_wgrad", &conv_dgrad_wgrad, py::arg("x"), py::arg("w"), py::arg("pad"), py::arg("residual"),
         py::arg("bn"), py::arg("bn_eps"), py::arg("bn_fix_gamma"), py::arg("bnb_x"), py::arg("dadd"), py::arg("dgamma"),
         py::arg("dbeta"), py::arg("wg_dy"), py::arg("wg_x"), py::arg("KH"), py::arg("KW"), py::arg("wg_stride"),
         py::arg("wg_pad"), py::arg("wg_out"), py::arg("defer") = false, py::arg("prev_slab") = py::none(),
-        py::arg("prev_out") = py::none(), py::arg("bnb_part") = py::none(), py::arg("x2") = false,
+        py::arg("prev_out") = py::none(), py::arg("bnb_part") = py::none(), py::arg("x2") = 0,
         py::arg("w_plane") = 0, py::arg("bt") = false, py::arg("rmask") = py::none(), py::arg("rmask_scale") = 1.0);
   m.def("wgrad_reduce_run", &wgrad_reduce_run, py::arg("slab"), py::arg("out"));
   m.def("head_bwd", &head_bwd, py::arg("x"), py::arg("dys"), py::arg("ws"), py::arg("dws"), py::arg("dw_acc"),
-        py::arg("dbs"), py::arg("db_acc"), py::arg("need_dx"), py::arg("relu_mask"), py::arg("x2") = false,
+        py::arg("dbs"), py::arg("db_acc"), py::arg("need_dx"), py::arg("relu_mask"), py::arg("x2") = 0,
         py::arg("w_planes") = std::vector<int64_t>(), py::arg("mask_scale") = 1.0);
-  m.def("chan_sum", &chan_sum, py::arg("x"), py::arg("out"), py::arg("accumulate"), py::arg("x2") = false);
+  m.def("chan_sum", &chan_sum, py::arg("x"), py::arg("out"), py::arg("accumulate"), py::arg("x2") = 0);
   m.def("det_postprocess", &det_postprocess, py::arg("rois"), py::arg("scores"), py::arg("deltas"),
         py::arg("im_info"), py::arg("thresh"), py::arg("nms_thresh"), py::arg("max_per"), py::arg("cap"));
   m.def("nest_keep", &nest_keep, py::arg("dets"), py::arg("thresh"));
-  m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("s"), py::arg("p"), py::arg("x2") = false);
+  m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("s"), py::arg("p"), py::arg("x2") = 0);
   m.def("maxpool_bwd", &maxpool_bwd, py::arg("dy"), py::arg("arg"), py::arg("H"), py::arg("W"), py::arg("k"),
-        py::arg("s"), py::arg("p"), py::arg("x2") = false);
-  m.def("avgpool_fwd", &avgpool_fwd, py::arg("x"), py::arg("x2") = false);
-  m.def("avgpool_bwd", &avgpool_bwd, py::arg("dy"), py::arg("H"), py::arg("W"), py::arg("x2") = false);
+        py::arg("s"), py::arg("p"), py::arg("x2") = 0);
+  m.def("avgpool_fwd", &avgpool_fwd, py::arg("x"), py::arg("x2") = 0);
+  m.def("avgpool_bwd", &avgpool_bwd, py::arg("dy"), py::arg("H"), py::arg("W"), py::arg("x2") = 0);
   m.def("proposal_gather", &proposal_gather);
   m.def("stem_conv", &stem_conv, py::arg("x"), py::arg("w"), py::arg("in_bn"), py::arg("in_eps"), py::arg("in_fixg"),
         py::arg("out_bn"), py::arg("out_eps"), py::arg("out_fixg"), py::arg("bias"), py::arg("KH"), py::arg("KW"),
@@ -2072,22 +2095,22 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "host twin of the fused-dropout generator: uniforms of elements 0..n-1 (CPU float tensor)");
   m.def("bn_train_fwd", &bn_train_fwd, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("rmean"),
         py::arg("rvar"), py::arg("momentum"), py::arg("eps"), py::arg("fix_gamma"), py::arg("relu"),
-        py::arg("x2") = false);
+        py::arg("x2") = 0);
   m.def("bn_train_apply", &bn_train_apply, py::arg("x"), py::arg("part"), py::arg("gamma"), py::arg("beta"),
         py::arg("rmean"), py::arg("rvar"), py::arg("momentum"), py::arg("eps"), py::arg("fix_gamma"), py::arg("relu"),
-        py::arg("x2") = false);
+        py::arg("x2") = 0);
   m.def("bn_train_dx_apply", &bn_train_dx_apply, py::arg("o"), py::arg("x"), py::arg("save"), py::arg("gamma_eff"),
         py::arg("part"), py::arg("nparts"), py::arg("dres") = py::none(), py::arg("dgamma") = py::none(),
-        py::arg("dbeta") = py::none(), py::arg("x2") = false);
+        py::arg("dbeta") = py::none(), py::arg("x2") = 0);
   m.def("bn_train_bwd", &bn_train_bwd, py::arg("x"), py::arg("dy"), py::arg("gamma"), py::arg("beta"),
         py::arg("save_mean"), py::arg("save_invstd"), py::arg("fix_gamma"), py::arg("relu"), py::arg("need_dx"),
-        py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(), py::arg("x2") = false);
+        py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(), py::arg("x2") = 0);
   m.def("wt_flip_table_info", &wt_flip_table_info);
   m.def("wt_flip_build", &wt_flip_build, py::arg("srcs"), py::arg("dsts"),
         py::arg("subs") = std::vector<std::vector<std::tuple<Tensor, std::vector<int64_t>, std::vector<int64_t>>>>());
   m.def("wt_flip_run", &wt_flip_run);
   m.def("conv_wgrad", &conv_wgrad, py::arg("dy"), py::arg("x"), py::arg("kh"), py::arg("kw"), py::arg("stride"),
         py::arg("pad"), py::arg("splits") = 0, py::arg("out") = py::none(), py::arg("variant") = 0,
-        py::arg("x2") = false);
+        py::arg("x2") = 0);
   m.attr("arch") = "gfx950";
 }

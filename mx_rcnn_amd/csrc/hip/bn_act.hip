@@ -272,30 +272,29 @@ void bn_relu_bwd(const void* x, const void* dy, int bf16, int64_t M, int C, cons
 }
 
 // ReLU (+ inverted dropout) backward on its own: out = dy * [y > 0] * scale over n 16-bit elements
-// (8 per thread), y the ReLU output; x2 pairs: the mask of hi-plane element i applies to both
-// planes (`plane` = n, both tensors 2n long).  The VGG trunk's top gradient (ops/vgg_fused.py);
+// (8 per thread), y the ReLU output (its hi plane with planes); x2 / x3: the mask of element i applies
+// to every plane of dy (`np` planes `plane` = n apart).  The VGG trunk's top gradient (ops/vgg_fused.py);
 // every other ReLU backward rides in a data-gradient epilogue (ConvEpi::rmask).
 __global__ void __launch_bounds__(256)
 relu_mask_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ y, uint16_t* __restrict__ out,
-                 int64_t n, int64_t plane, float scale) {
+                 int64_t n, int64_t plane, int np, float scale) {
   const int64_t e = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
   if (e >= n) return;
   const uint4 yv = *reinterpret_cast<const uint4*>(y + e);
   const uint16_t* yh = reinterpret_cast<const uint16_t*>(&yv);
-  for (int64_t pl = 0; pl <= plane; pl += (plane > 0 ? plane : 1)) {
+  for (int q = 0; q < np; ++q) {
     float d[8];
-    ld8_bf16(dy + pl + e, d);
+    ld8_bf16(dy + q * plane + e, d);
 #pragma unroll
     for (int k = 0; k < 8; ++k) d[k] = ((yh[k] & 0x8000u) == 0 && (yh[k] & 0x7fffu) != 0) ? d[k] * scale : 0.f;
-    st8_bf16(out + pl + e, d);
-    if (plane == 0) break;
+    st8_bf16(out + q * plane + e, d);
   }
 }
 
 void relu_mask(const uint16_t* dy, const uint16_t* y, uint16_t* out, int64_t n, int64_t plane, float scale,
-               hipStream_t st) {
+               hipStream_t st, int np) {
   if (n <= 0) return;
-  relu_mask_kernel<<<(unsigned)((n / 8 + 255) / 256), 256, 0, st>>>(dy, y, out, n, plane, scale);
+  relu_mask_kernel<<<(unsigned)((n / 8 + 255) / 256), 256, 0, st>>>(dy, y, out, n, plane, np < 1 ? 1 : np, scale);
 }
 
 }  // namespace mxr

@@ -72,16 +72,16 @@ __device__ __forceinline__ void fold_partials(const float* __restrict__ part, in
   __syncthreads();
 }
 
-// 8 channels of one row; pl > 0: an x2 hi / lo pair (common.h), the lo plane pl elements further
-__device__ __forceinline__ void ld8(const uint16_t* p, float* v, int64_t pl) {
-  if (pl) ld8x(p, pl, v);
+// 8 channels of one row; pl > 0: x2 / x3 planes (common.h) pl elements apart
+__device__ __forceinline__ void ld8(const uint16_t* p, float* v, int64_t pl, bool x3) {
+  if (pl) ld8x(p, pl, v, x3);
   else ld8_bf16(p, v);
 }
 
-__device__ __forceinline__ void st8(uint16_t* p, const float* v, int64_t pl) {
+__device__ __forceinline__ void st8(uint16_t* p, const float* v, int64_t pl, bool x3) {
   if (pl) {
     float t[8];
-    st8x(p, pl, v, t);
+    st8x(p, pl, v, t, x3);
   } else {
     st8_bf16(p, v);
   }
@@ -111,7 +111,7 @@ __device__ __forceinline__ void lane_reduce(const float* a, const float* b, floa
 __global__ void __launch_bounds__(256)
 bn_train_stats_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int rows, const float* __restrict__ shift,
                       float* __restrict__ part, int x2) {
-  const int64_t pl = x2 ? M * C : 0;  // x2 pairs: every (M, C) operand's lo plane
+  const int64_t pl = x2 ? M * C : 0;  // x2 (2) / x3 (3) planes of every (M, C) operand
   __shared__ float red[8][BT_LANES][16];
   __shared__ float sa[64], sb[64];
   const int cg = threadIdx.x & 7, rl = threadIdx.x >> 3;
@@ -127,7 +127,7 @@ bn_train_stats_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int rows
 #pragma unroll 4
   for (int64_t r = r0 + rl; r < r1; r += BT_LANES) {
     float v[8];
-    ld8(x + r * C + c0, v, pl);
+    ld8(x + r * C + c0, v, pl, x2 == 3);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float d = v[k] - sh[k];
@@ -151,7 +151,7 @@ bn_train_norm_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int rows,
                      float* __restrict__ rvar, float momentum, float eps, int fix_gamma, int relu,
                      uint16_t* __restrict__ y, float* __restrict__ save_mean, float* __restrict__ save_invstd,
                      float* __restrict__ save_veps, int x2) {
-  const int64_t pl = x2 ? M * C : 0;  // x2 pairs: every (M, C) operand's lo plane
+  const int64_t pl = x2 ? M * C : 0;  // x2 (2) / x3 (3) planes of every (M, C) operand
   __shared__ float scale_sh[64], shift_sh[64], red4[512], fa[64], fb[64];
   const int tid = threadIdx.x;
   fold_partials(part, nchunks, C, red4, fa, fb);
@@ -191,13 +191,13 @@ bn_train_norm_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int rows,
 #pragma unroll 4
   for (int64_t r = r0 + rl; r < r1; r += BT_LANES) {
     float v[8];
-    ld8(x + r * C + c0, v, pl);
+    ld8(x + r * C + c0, v, pl, x2 == 3);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       v[k] = v[k] * sc[k] + sf[k];
       if (relu) v[k] = fmaxf(v[k], 0.f);
     }
-    st8(y + r * C + c0, v, pl);
+    st8(y + r * C + c0, v, pl, x2 == 3);
   }
 }
 
@@ -206,7 +206,7 @@ bn_train_bstats_kernel(const uint16_t* __restrict__ x, const uint16_t* __restric
                        const float* __restrict__ gamma, const float* __restrict__ beta,
                        const float* __restrict__ save_mean, const float* __restrict__ save_invstd, int fix_gamma,
                        int relu, int rows, float* __restrict__ part, int x2) {
-  const int64_t pl = x2 ? M * C : 0;  // x2 pairs: every (M, C) operand's lo plane
+  const int64_t pl = x2 ? M * C : 0;  // x2 (2) / x3 (3) planes of every (M, C) operand
   __shared__ float red[8][BT_LANES][16];
   __shared__ float sa[64], sb[64];
   const int cg = threadIdx.x & 7, rl = threadIdx.x >> 3;
@@ -225,8 +225,8 @@ bn_train_bstats_kernel(const uint16_t* __restrict__ x, const uint16_t* __restric
 #pragma unroll 4
   for (int64_t r = r0 + rl; r < r1; r += BT_LANES) {
     float v[8], d[8];
-    ld8(x + r * C + c0, v, pl);
-    ld8(dy + r * C + c0, d, pl);
+    ld8(x + r * C + c0, v, pl, x2 == 3);
+    ld8(dy + r * C + c0, d, pl, x2 == 3);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float xh = (v[k] - mu[k]) * inv[k];
@@ -249,7 +249,7 @@ bn_train_dx_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ 
                    const float* __restrict__ save_mean, const float* __restrict__ save_invstd, int fix_gamma,
                    int relu, uint16_t* __restrict__ dx, float* __restrict__ dgamma, float* __restrict__ dbeta,
                    int accumulate, int x2) {
-  const int64_t pl = x2 ? M * C : 0;  // x2 pairs: every (M, C) operand's lo plane
+  const int64_t pl = x2 ? M * C : 0;  // x2 (2) / x3 (3) planes of every (M, C) operand
   __shared__ float mg_sh[64], mgx_sh[64], red4[512], fa[64], fb[64];
   const int tid = threadIdx.x;
   fold_partials(part, nchunks, C, red4, fa, fb);
@@ -282,15 +282,15 @@ bn_train_dx_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ 
 #pragma unroll 4
   for (int64_t r = r0 + rl; r < r1; r += BT_LANES) {
     float v[8], d[8];
-    ld8(x + r * C + c0, v, pl);
-    ld8(dy + r * C + c0, d, pl);
+    ld8(x + r * C + c0, v, pl, x2 == 3);
+    ld8(dy + r * C + c0, d, pl, x2 == 3);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const float xh = (v[k] - mu[k]) * inv[k];
       const float gm = (!relu || xh * g[k] + b[k] > 0.f) ? d[k] : 0.f;
       d[k] = g[k] * inv[k] * (gm - mg[k] - xh * mgx[k]);
     }
-    st8(dx + r * C + c0, d, pl);
+    st8(dx + r * C + c0, d, pl, x2 == 3);
   }
 }
 
@@ -332,7 +332,7 @@ bn_train_dx_apply_kernel(const uint16_t* o, const uint16_t* __restrict__ x, int6
                          const float* __restrict__ part, int nparts, const float* __restrict__ gamma,
                          const float* __restrict__ save, const uint16_t* __restrict__ dres, uint16_t* dx,
                          float* __restrict__ dgamma, float* __restrict__ dbeta, int x2) {
-  const int64_t pl = x2 ? M * C : 0;  // x2 pairs: every (M, C) operand's lo plane
+  const int64_t pl = x2 ? M * C : 0;  // x2 (2) / x3 (3) planes of every (M, C) operand
   __shared__ float red4[512], fa[64], fb[64];
   const int tid = threadIdx.x, cg = tid & 7, rl = tid >> 3;
   fold_partials(part, nparts, C, red4, fa, fb);
@@ -358,12 +358,12 @@ bn_train_dx_apply_kernel(const uint16_t* o, const uint16_t* __restrict__ x, int6
 #pragma unroll 4
   for (int64_t r = r0 + rl; r < r1; r += BT_LANES) {
     float v[8], d[8], rr[8];
-    ld8(x + r * C + c0, v, pl);
-    ld8(o + r * C + c0, d, pl);
-    if (dres) ld8(dres + r * C + c0, rr, pl);
+    ld8(x + r * C + c0, v, pl, x2 == 3);
+    ld8(o + r * C + c0, d, pl, x2 == 3);
+    if (dres) ld8(dres + r * C + c0, rr, pl, x2 == 3);
 #pragma unroll
     for (int k = 0; k < 8; ++k) d[k] = d[k] - a[k] - b[k] * v[k] + (dres ? rr[k] : 0.f);
-    st8(dx + r * C + c0, d, pl);
+    st8(dx + r * C + c0, d, pl, x2 == 3);
   }
 }
 

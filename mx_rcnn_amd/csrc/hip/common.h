@@ -77,41 +77,83 @@ __device__ __forceinline__ void st8_h16(uint16_t* p, const float* v, int code) {
   *reinterpret_cast<uint4*>(p) = make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-// ---- fp32-class "x2" storage ------------------------------------------------------------------
-// The fp32 training mode keeps every MFMA operand as a PAIR of bf16 planes `plane` elements apart:
-// value = hi + lo with hi = RNE(v), lo = RNE(v - hi) -- 16 significant bits, relative error
-// <= 2^-17 -- so a product is hi*hi + hi*lo + lo*hi on the bf16 MFMA with fp32 accumulation (the
-// dropped lo*lo term is below 2^-16 relative).  Activation tensors are (2N, C, H, W) with the hi
-// plane first; weights carry their lo plane at a per-buffer offset.
+// ---- multi-plane bf16 storage of the fp32 training modes --------------------------------------
+// x2 ("bf16x3" mode): every MFMA operand is a PAIR of bf16 planes `plane` elements apart, value =
+// hi + lo with hi = RNE(v), lo = RNE(v - hi) -- 16 significant bits -- and a product is
+// hi*hi + hi*lo + lo*hi on the bf16 MFMA with fp32 accumulation.  Tensors are (2N, C, H, W), hi
+// plane first.
+// x3 (the fp32 mode): THREE planes [mid | hi | lo] `plane` apart, hi = RNE(v), mid = RNE(v - hi),
+// lo = RNE(v - hi - mid): hi + mid + lo == v exactly (24 significant bits, IEEE fp32 storage), and
+// a product is the six terms hh + hm + mh + hl + lh + mm (the dropped ml + lm + ll are below 2^-23
+// relative, the size of one fp32 rounding).  Tensors are (3N, C, H, W).  The plane order makes the
+// MFMA kernels' two K phases uniform shifts of one operand base: phase (hi, lo) reads planes 1 / 2
+// = the pair kernel's (first, second) one plane further on than phase (mid, hi), planes 0 / 1, so a
+// pair kernel runs x3 with its K loop twice and a per-phase SGPR offset (hh + hl + lh, then
+// mm + mh + hm).  The sign of v is the sign of hi (plane 1).
 __device__ __forceinline__ void split_bf16(float v, uint16_t& hi, uint16_t& lo) {
   hi = f32_to_bf16(v);
   lo = f32_to_bf16(v - bf16_to_f32(hi));
 }
-__device__ __forceinline__ float ldx(const uint16_t* p, int64_t i, int64_t plane) {
-  return bf16_to_f32(p[i]) + bf16_to_f32(p[i + plane]);
+__device__ __forceinline__ void split3_bf16(float v, uint16_t& hi, uint16_t& mid, uint16_t& lo) {
+  hi = f32_to_bf16(v);
+  const float r = v - bf16_to_f32(hi);
+  mid = f32_to_bf16(r);
+  lo = f32_to_bf16(r - bf16_to_f32(mid));
 }
-// stores v as a pair and returns the stored value (what a consumer reading it back sees)
-__device__ __forceinline__ float stx(uint16_t* p, int64_t i, int64_t plane, float v) {
+// x3 = false: a pair (planes 0, 1); true: a triple (planes 0, 1, 2); the sum is exact either way
+__device__ __forceinline__ float ldx(const uint16_t* p, int64_t i, int64_t plane, bool x3 = false) {
+  const float v = bf16_to_f32(p[i]) + bf16_to_f32(p[i + plane]);
+  return x3 ? v + bf16_to_f32(p[i + 2 * plane]) : v;
+}
+// stores v in the planes and returns the stored value (what a consumer reading it back sees)
+__device__ __forceinline__ float stx(uint16_t* p, int64_t i, int64_t plane, float v, bool x3 = false) {
+  if (x3) {
+    uint16_t h, m, l;
+    split3_bf16(v, h, m, l);
+    p[i] = m;
+    p[i + plane] = h;
+    p[i + 2 * plane] = l;
+    return (bf16_to_f32(m) + bf16_to_f32(h)) + bf16_to_f32(l);
+  }
   uint16_t h, l;
   split_bf16(v, h, l);
   p[i] = h;
   p[i + plane] = l;
   return bf16_to_f32(h) + bf16_to_f32(l);
 }
-__device__ __forceinline__ void ld8x(const uint16_t* p, int64_t plane, float* v) {
+__device__ __forceinline__ void ld8x(const uint16_t* p, int64_t plane, float* v, bool x3 = false) {
   float t[8];
   ld8_bf16(p, v);
   ld8_bf16(p + plane, t);
 #pragma unroll
   for (int k = 0; k < 8; ++k) v[k] += t[k];
+  if (x3) {
+    ld8_bf16(p + 2 * plane, t);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] += t[k];
+  }
 }
-// 8 values -> hi / lo planes; `stored` (may alias v) receives the stored values
-__device__ __forceinline__ void st8x(uint16_t* p, int64_t plane, const float* v, float* stored) {
+// 8 values -> planes; `stored` (may alias v) receives the stored values
+__device__ __forceinline__ void st8x(uint16_t* p, int64_t plane, const float* v, float* stored, bool x3 = false) {
   float h[8], l[8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     h[k] = bf16_to_f32(f32_to_bf16(v[k]));
     l[k] = v[k] - h[k];
+  }
+  if (x3) {
+    float m[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      m[k] = bf16_to_f32(f32_to_bf16(l[k]));
+      l[k] -= m[k];
+    }
+    st8_bf16(p, m);  // exact: m and h are already bf16
+    st8_bf16(p + plane, h);
+    st8_bf16(p + 2 * plane, l);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) stored[k] = (m[k] + h[k]) + bf16_to_f32(f32_to_bf16(l[k]));
+    return;
   }
   st8_bf16(p, h);      // exact: h is already bf16
   st8_bf16(p + plane, l);
@@ -120,14 +162,17 @@ __device__ __forceinline__ void st8x(uint16_t* p, int64_t plane, const float* v,
 }
 
 // Storage-code access for the elementwise kernels: 0 fp32, 1 bf16, 2 fp16, 3 x2 pair (bf16 hi
-// plane + lo plane `plane` elements further; a kernel over an (M, C) activation passes M * C)
+// plane + lo plane `plane` elements further; a kernel over an (M, C) activation passes M * C),
+// 4 x3 triple (planes mid, hi, lo `plane` apart)
 constexpr int kCodeX2 = 3;
+constexpr int kCodeX3 = 4;
+__device__ __forceinline__ bool code_planes(int code) { return code >= kCodeX2; }
 __device__ __forceinline__ float ldc(const void* p, int64_t i, int code, int64_t plane) {
-  if (code == kCodeX2) return ldx(static_cast<const uint16_t*>(p), i, plane);
+  if (code >= kCodeX2) return ldx(static_cast<const uint16_t*>(p), i, plane, code == kCodeX3);
   return ld(p, i, code);
 }
 __device__ __forceinline__ void stc(void* p, int64_t i, float v, int code, int64_t plane) {
-  if (code == kCodeX2) stx(static_cast<uint16_t*>(p), i, plane, v);
+  if (code >= kCodeX2) stx(static_cast<uint16_t*>(p), i, plane, v, code == kCodeX3);
   else st(p, i, v, code);
 }
 // 4 consecutive values (i % 4 == 0)
@@ -139,10 +184,10 @@ __device__ __forceinline__ void ld4c(const void* p, int64_t i, int code, int64_t
   }
   const uint16_t* q = static_cast<const uint16_t*>(p);
   const ushort4 u = *reinterpret_cast<const ushort4*>(q + i);
-  const int c = code == kCodeX2 ? 1 : code;
+  const int c = code >= kCodeX2 ? 1 : code;
   v[0] = h16_to_f32(u.x, c); v[1] = h16_to_f32(u.y, c); v[2] = h16_to_f32(u.z, c); v[3] = h16_to_f32(u.w, c);
-  if (code == kCodeX2) {
-    const ushort4 l = *reinterpret_cast<const ushort4*>(q + i + plane);
+  for (int pl = 1; pl <= code - 2; ++pl) {  // x2: plane 1; x3: planes 1, 2
+    const ushort4 l = *reinterpret_cast<const ushort4*>(q + i + pl * plane);
     v[0] += bf16_to_f32(l.x); v[1] += bf16_to_f32(l.y); v[2] += bf16_to_f32(l.z); v[3] += bf16_to_f32(l.w);
   }
 }
@@ -152,6 +197,15 @@ __device__ __forceinline__ void st4c(void* p, int64_t i, int code, int64_t plane
     return;
   }
   uint16_t* q = static_cast<uint16_t*>(p);
+  if (code == kCodeX3) {
+    uint16_t h[4], m[4], l[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) split3_bf16(v[k], h[k], m[k], l[k]);
+    *reinterpret_cast<ushort4*>(q + i) = make_ushort4(m[0], m[1], m[2], m[3]);
+    *reinterpret_cast<ushort4*>(q + i + plane) = make_ushort4(h[0], h[1], h[2], h[3]);
+    *reinterpret_cast<ushort4*>(q + i + 2 * plane) = make_ushort4(l[0], l[1], l[2], l[3]);
+    return;
+  }
   if (code == kCodeX2) {
     uint16_t h[4], l[4];
 #pragma unroll
@@ -172,7 +226,7 @@ __device__ __forceinline__ void ld8c(const void* p, int64_t i, int code, int64_t
     return;
   }
   const uint16_t* q = static_cast<const uint16_t*>(p) + i;
-  if (code == kCodeX2) ld8x(q, plane, v);
+  if (code >= kCodeX2) ld8x(q, plane, v, code == kCodeX3);
   else ld8_h16(q, v, code);
 }
 __device__ __forceinline__ void st8c(void* p, int64_t i, int code, int64_t plane, const float v[8]) {
@@ -183,9 +237,9 @@ __device__ __forceinline__ void st8c(void* p, int64_t i, int code, int64_t plane
     return;
   }
   uint16_t* q = static_cast<uint16_t*>(p) + i;
-  if (code == kCodeX2) {
+  if (code >= kCodeX2) {
     float s[8];
-    st8x(q, plane, v, s);
+    st8x(q, plane, v, s, code == kCodeX3);
   } else {
     st8_h16(q, v, code);
   }

@@ -26,438 +26,9 @@
 // dY with the flipped / transposed filter (pad' = k-1-pad); see ops/conv.py.
 #include <cstdlib>
 
-#include "common.h"
-#include "../kernels.h"
-#include "wgrad_body.h"
-
-// epilogue storage code: fp16 when the conv runs on fp16 activations (inference), else bf16
-#define EPC (ep.f16 ? 2 : 1)
+#include "igemm_body.h"
 
 namespace mxr {
-
-__device__ __forceinline__ uint16_t f32_to_h16c(int code, float f) { return f32_to_h16(f, code); }
-__device__ __forceinline__ float h16_to_f32c(int code, uint16_t v) { return h16_to_f32(v, code); }
-
-// epilogue element access in the launch's storage format: one 16-bit value (bf16 / fp16), or (X2)
-// an x2 hi / lo pair `plane` elements apart (ConvEpi::x2).  Stores return the STORED value, which
-// the fused consumers (BN of the next unit, statistics) must read, exactly like the unfused pair.
-// X2 is a template flag so the bf16 / fp16 epilogues compile exactly as before (unrolled loops).
-template <bool X2>
-__device__ __forceinline__ float epi_ld1(const ConvEpi& ep, const uint16_t* p, int64_t i, int64_t plane) {
-  if constexpr (X2) return ldx(p, i, plane);
-  return h16_to_f32c(ep.f16 ? 2 : 1, p[i]);
-}
-template <bool X2>
-__device__ __forceinline__ float epi_st1(const ConvEpi& ep, uint16_t* p, int64_t i, int64_t plane, float v) {
-  if constexpr (X2) return stx(p, i, plane, v);
-  const uint16_t h = f32_to_h16c(ep.f16 ? 2 : 1, v);
-  p[i] = h;
-  return h16_to_f32c(ep.f16 ? 2 : 1, h);
-}
-template <bool X2>
-__device__ __forceinline__ void epi_ld8(const ConvEpi& ep, const uint16_t* p, int64_t i, int64_t plane, float* v) {
-  if constexpr (X2) ld8x(p + i, plane, v);
-  else ld8_h16(p + i, v, ep.f16 ? 2 : 1);
-}
-// 8 consecutive outputs; `stored` receives the stored values
-template <bool X2>
-__device__ __forceinline__ void epi_st8(const ConvEpi& ep, uint16_t* p, int64_t i, int64_t plane, const float* v,
-                                        float* stored) {
-  if constexpr (X2) {
-    st8x(p + i, plane, v, stored);
-    return;
-  }
-  const int code = ep.f16 ? 2 : 1;
-  uint16_t b[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    b[k] = f32_to_h16c(code, v[k]);
-    stored[k] = h16_to_f32c(code, b[k]);
-  }
-  *reinterpret_cast<uint4*>(p + i) =
-      make_uint4((uint32_t)b[0] | ((uint32_t)b[1] << 16), (uint32_t)b[2] | ((uint32_t)b[3] << 16),
-                 (uint32_t)b[4] | ((uint32_t)b[5] << 16), (uint32_t)b[6] | ((uint32_t)b[7] << 16));
-}
-
-typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-
-typedef float f32x4 __attribute__((ext_vector_type(4)));
-
-// MFMA 16x16x32 on bf16 or fp16 operands (same rate, same fragment layout)
-template <bool F16> struct Mfma16;
-template <> struct Mfma16<false> {
-  typedef bf16x8 T;
-  __device__ static __forceinline__ f32x4 mma(T a, T b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
-  }
-};
-template <> struct Mfma16<true> {
-  typedef f16x8 T;
-  __device__ static __forceinline__ f32x4 mma(T a, T b, f32x4 c) {
-    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
-  }
-};
-
-constexpr int BK = 64;  // bf16 elements per K-step (one 128-B row per tile row)
-
-__device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ ((row >> 1) & 7); }
-
-// output row of GEMM row m (identity unless the epilogue scatters to a parity class, ConvEpi::omap)
-__device__ __forceinline__ int64_t epi_row(const ConvEpi& ep, int m, int Ho, int Wo) {
-  if (!ep.omap) return m;
-  const int hw = Ho * Wo;
-  const int img = m / hw, r = m - img * hw, i = r / Wo, j = r - (r / Wo) * Wo;
-  return ((int64_t)img * ep.o_H + i * ep.o_sh + ep.o_ph) * ep.o_W + j * ep.o_sw + ep.o_pw;
-}
-
-// dadd element row for output row m of the launch grid (-1: dadd has nothing there)
-__device__ __forceinline__ int64_t dadd_row(const ConvEpi& ep, int m, int64_t out_row) {
-  if (ep.dadd_s <= 1) return out_row;
-  const int s = ep.dadd_s, Ho = ep.dadd_gh, Wo = ep.dadd_gw, hw = Ho * Wo;
-  const int img = m / hw, r = m - img * hw, i = r / Wo, j = r - i * Wo;
-  if (i % s || j % s) return -1;
-  return ((int64_t)img * ((Ho + s - 1) / s) + i / s) * ((Wo + s - 1) / s) + j / s;
-}
-
-// per-output-channel epilogue constants
-struct EpiCol {
-  float bias, s, t, mean, inv;
-};
-
-__device__ __forceinline__ EpiCol epi_col(const ConvEpi& ep, int n) {
-  EpiCol c;
-  c.bias = ep.bias ? ep.bias[n] : (ep.bias_h ? h16_to_f32c(EPC, ep.bias_h[n]) : 0.f);
-  c.s = 1.f;
-  c.t = 0.f;
-  c.mean = 0.f;
-  c.inv = 1.f;
-  if (ep.y2 || ep.bnb_x) {
-    const float g = ep.bn_fix_gamma ? 1.f : ep.bn_gamma[n];
-    c.inv = rsqrtf(ep.bn_var[n] + ep.bn_eps);
-    c.mean = ep.bn_mean[n];
-    c.s = g * c.inv;
-    c.t = ep.bn_beta[n] - c.mean * c.s;
-  }
-  return c;
-}
-
-// fused inverted dropout of output element `idx` (see ConvEpi::drop_p)
-__device__ __forceinline__ float epi_dropout(const ConvEpi& ep, int64_t idx, float v) {
-  if (ep.drop_p > 0.f) {
-    const float u = philox_uniform(ep.drop_seed, (uint64_t)*ep.drop_step, (uint64_t)idx);
-    v = u >= ep.drop_p ? v * (1.f / (1.f - ep.drop_p)) : 0.f;
-  }
-  return v;
-}
-
-// ReLU(-and-dropout) backward of the layer whose output is this data gradient's forward input
-// (ConvEpi::rmask): keep v where that activation is positive, scaled by rmask_s
-__device__ __forceinline__ float epi_rmask(const ConvEpi& ep, int64_t idx, float v) {
-  if (ep.rmask) {
-    const uint16_t h = ep.rmask[idx];  // bf16 (x2: the hi plane carries the sign)
-    v = ((h & 0x8000u) == 0 && (h & 0x7fffu) != 0) ? v * ep.rmask_s : 0.f;
-  }
-  return v;
-}
-
-template <bool X2>
-__device__ __forceinline__ void epi_store(const ConvEpi& ep, const EpiCol& c, uint16_t* __restrict__ y, int64_t idx,
-                                          float v) {
-  v += c.bias;
-  if (ep.residual) v += epi_ld1<X2>(ep, ep.residual, idx, ep.x2_py);
-  if (ep.relu) v = fmaxf(v, 0.f);
-  v = epi_dropout(ep, idx, v);
-  v = epi_rmask(ep, idx, v);
-  if (X2 && ep.yf) {
-    ep.yf[idx] = v;
-    return;
-  }
-  const float ys = epi_st1<X2>(ep, y, idx, ep.x2_py, v);
-  if (ep.y2) {
-    // the BN reads the STORED (bf16-rounded) conv output, exactly like the unfused pair
-    float a = ys * c.s + c.t;
-    if (ep.act_relu) a = fmaxf(a, 0.f);
-    epi_st1<X2>(ep, ep.y2, idx, ep.x2_py, a);
-  }
-}
-
-// BN-backward epilogue of one element; returns (g, g * xhat) through sg / sgx
-template <bool X2>
-__device__ __forceinline__ void epi_bnb(const ConvEpi& ep, const EpiCol& c, uint16_t* __restrict__ y, int64_t idx,
-                                        float v, float& sg, float& sgx, int64_t didx) {
-  if (ep.dadd && didx >= 0) v += epi_ld1<X2>(ep, ep.dadd, didx, ep.x2_pd);
-  const float xv = epi_ld1<X2>(ep, ep.bnb_x, idx, ep.x2_py);
-  const float g = (!ep.act_relu || xv * c.s + c.t > 0.f) ? v : 0.f;
-  sg += g;
-  sgx += g * (xv - c.mean) * c.inv;
-  float o = g * c.s;
-  if (ep.residual) o += epi_ld1<X2>(ep, ep.residual, idx, ep.x2_py);
-  epi_st1<X2>(ep, y, idx, ep.x2_py, o);
-}
-
-// Per-column statistics of an LDS-transposed epilogue (thread = 8 consecutive columns cv*8.. of
-// some rows): sum over the lanes of each wave sharing the column group (shuffles), then over the
-// NW waves through T ([NW][BN][2] floats; the caller has finished reading T), one value per
-// column and stat.  With `atomic` the two sums are added to out_a / out_b (fp32 atomics), else
-// written to out_a[col] / out_b[col] (a per-row-tile partial row).
-template <int BN, int NT>
-__device__ __forceinline__ void epi_col_stats(float (&sa)[8], float (&sb)[8], float* __restrict__ T, int tid, int n0,
-                                              int Cout, float* out_a, float* out_b, bool atomic, bool skip_b) {
-  constexpr int VPR = BN / 8;
-  constexpr int NW = NT / 64;
-  const int lane = tid & 63, wid = tid >> 6, cv = tid % VPR;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-#pragma unroll
-    for (int o = VPR; o < 64; o <<= 1) {
-      sa[k] += __shfl_xor(sa[k], o, 64);
-      sb[k] += __shfl_xor(sb[k], o, 64);
-    }
-  }
-  __syncthreads();  // T is reused as [NW waves][BN][2] partials
-  if (lane < VPR) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      T[(wid * BN + cv * 8 + k) * 2] = sa[k];
-      T[(wid * BN + cv * 8 + k) * 2 + 1] = sb[k];
-    }
-  }
-  __syncthreads();
-  for (int c = tid; c < BN; c += NT) {
-    const int col = n0 + c;
-    float a = 0.f, b = 0.f;
-#pragma unroll
-    for (int q = 0; q < NW; ++q) {
-      a += T[(q * BN + c) * 2];
-      b += T[(q * BN + c) * 2 + 1];
-    }
-    if (col < Cout) {
-      if (atomic) {
-        if (out_a) atomicAdd(out_a + col, a);
-        if (out_b && !skip_b) atomicAdd(out_b + col, b);
-      } else {
-        out_a[col] = a;
-        out_b[col] = b;
-      }
-    }
-  }
-}
-
-// BN-backward column sums sum(g) / sum(g * xhat): fp32 atomics into dbeta / dgamma, or (bnb_part,
-// deterministic) this row tile's partial row bnb_row0 + m0 / BM of [rows][2][Cout]
-template <int BM, int BN, int NT>
-__device__ __forceinline__ void epi_bnb_sums(float (&sg)[8], float (&sgx)[8], float* __restrict__ T, int tid, int m0,
-                                             int n0, int Cout, const ConvEpi& ep) {
-  if (ep.bnb_part) {
-    float* row = ep.bnb_part + (int64_t)(ep.bnb_row0 + m0 / BM) * 2 * Cout;
-    epi_col_stats<BN, NT>(sg, sgx, T, tid, n0, Cout, row, row + Cout, false, false);
-  } else {
-    epi_col_stats<BN, NT>(sg, sgx, T, tid, n0, Cout, ep.bnb_dbeta, ep.bnb_dgamma, true, ep.bn_fix_gamma);
-  }
-}
-
-// training-BN statistics epilogue (ConvEpi::st_part): this row tile's partial row, and the shift row
-template <int BM, int BN, int NT>
-__device__ __forceinline__ void epi_bn_stats(float (&s1)[8], float (&s2)[8], float* __restrict__ T, int tid, int m0,
-                                             int n0, int M, int Cout, const ConvEpi& ep) {
-  const int tm = m0 / BM, tiles_m = (M + BM - 1) / BM;
-  float* row = ep.st_part + (int64_t)tm * 2 * Cout;
-  epi_col_stats<BN, NT>(s1, s2, T, tid, n0, Cout, row, row + Cout, false, false);
-  if (tm == 0)
-    for (int c = tid; c < BN; c += NT)
-      if (n0 + c < Cout) ep.st_part[(int64_t)tiles_m * 2 * Cout + n0 + c] = ep.st_shift[n0 + c];
-}
-
-// Shared epilogue of the implicit-GEMM kernels: C/D map col = lane & 15, row = (lane >> 4) * 4 + r.
-template <int TM, int TN, int WM, int WN, bool X2 = false>
-__device__ __forceinline__ void igemm_epilogue(f32x4 (&acc)[TM][TN], int m0, int n0, int wm, int wn, int lane, int M,
-                                               int Cout, const ConvEpi& ep, uint16_t* __restrict__ y, int split,
-                                               int splits, float* __restrict__ slab, int Ho = 1, int Wo = 1) {
-  if (splits > 1) {  // fp32 partial slab; bias/ReLU/cast happen in the reduce kernel
-    float* sp = slab + (int64_t)split * M * Cout;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * WN + j * 16 + (lane & 15);
-      if (n >= Cout) continue;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
-          if (m < M) sp[(int64_t)m * Cout + n] = acc[i][j][r];
-        }
-    }
-    return;
-  }
-  if (ep.bnb_x) {
-    // BN-backward epilogue: per-column sums over this wave's rows, reduced across the four
-    // 16-lane row groups, then one fp32 atomic per (wave, column, stat)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = n0 + wn * WN + j * 16 + (lane & 15);
-      float sg = 0.f, sgx = 0.f;
-      if (n < Cout) {
-        const EpiCol ec = epi_col(ep, n);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
-            if (m < M) {
-              const int64_t orow = epi_row(ep, m, Ho, Wo), drow = dadd_row(ep, m, orow);
-              epi_bnb<X2>(ep, ec, y, orow * Cout + n, acc[i][j][r], sg, sgx, drow < 0 ? -1 : drow * Cout + n);
-            }
-          }
-      }
-      sg += __shfl_xor(sg, 16, 64);
-      sg += __shfl_xor(sg, 32, 64);
-      sgx += __shfl_xor(sgx, 16, 64);
-      sgx += __shfl_xor(sgx, 32, 64);
-      if (lane < 16 && n < Cout) {
-        if (ep.bnb_dbeta) atomicAdd(ep.bnb_dbeta + n, sg);
-        if (ep.bnb_dgamma && !ep.bn_fix_gamma) atomicAdd(ep.bnb_dgamma + n, sgx);
-      }
-    }
-    return;
-  }
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int n = n0 + wn * WN + j * 16 + (lane & 15);
-    if (n >= Cout) continue;
-    const EpiCol ec = epi_col(ep, n);
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int m = m0 + wm * WM + i * 16 + (lane >> 4) * 4 + r;
-        if (m < M) epi_store<X2>(ep, ec, y, epi_row(ep, m, Ho, Wo) * Cout + n, acc[i][j][r]);
-      }
-    }
-  }
-}
-
-// LDS-transposed epilogue (Cout % 8 == 0): the MFMA C/D layout gives each lane 4 rows of ONE
-// column, so a direct epilogue issues 2-byte accesses strided by Cout.  Here the fp32 tile is
-// scattered into LDS ([BM][BN+4], conflict-free for the 16-lane column runs), and every thread
-// then owns 8 consecutive columns of a row: residual / BN-input / dY-add reads, y / y2 stores and
-// fp32 split-K slab writes are 16-B vectors, the per-column constants are computed once per
-// thread, and the BN-backward column sums reduce across the lanes sharing a column group
-// (shuffles), across waves (LDS) and leave the workgroup as one atomic per column and stat.
-template <int BM, int BN, int TM, int TN, int WM, int WN, bool X2 = false>
-__device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* __restrict__ T, int m0, int n0, int wm,
-                                                   int wn, int lane, int tid, int M, int Cout, const ConvEpi& ep,
-                                                   uint16_t* __restrict__ y, int split, int splits,
-                                                   float* __restrict__ slab, int Ho = 1, int Wo = 1) {
-  constexpr int LDT = BN + 4;      // fp32 row stride of the staged tile
-  constexpr int VPR = BN / 8;      // 8-column vectors per row
-  constexpr int NV = BM * VPR / 256;  // vectors per thread
-  __syncthreads();  // every wave is done reading the operand ring
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r)
-        T[(wm * WM + i * 16 + (lane >> 4) * 4 + r) * LDT + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
-  __syncthreads();
-  const int cv = tid % VPR;  // this thread's column group (the same for all its vectors)
-  const int n = n0 + cv * 8;
-  const bool ncol = n < Cout;
-  if (splits > 1) {
-    float* sp = slab + (int64_t)split * M * Cout;
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int row = (tid + v * 256) / VPR, m = m0 + row;
-      if (m >= M || !ncol) continue;
-      const float4* src = reinterpret_cast<const float4*>(T + row * LDT + cv * 8);
-      float4* dst = reinterpret_cast<float4*>(sp + (int64_t)m * Cout + n);
-      dst[0] = src[0];
-      dst[1] = src[1];
-    }
-    return;
-  }
-  EpiCol ec[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) ec[k] = epi_col(ep, ncol ? n + k : 0);
-  if (ep.bnb_x) {
-    float sg[8], sgx[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) sg[k] = sgx[k] = 0.f;
-#pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int row = (tid + v * 256) / VPR, m = m0 + row;
-      if (m >= M || !ncol) continue;
-      const int64_t e = epi_row(ep, m, Ho, Wo) * Cout + n;
-      float a[8], xv[8], d[8], rs[8];
-      const float4* src = reinterpret_cast<const float4*>(T + row * LDT + cv * 8);
-      const float4 a0 = src[0], a1 = src[1];
-      a[0] = a0.x; a[1] = a0.y; a[2] = a0.z; a[3] = a0.w; a[4] = a1.x; a[5] = a1.y; a[6] = a1.z; a[7] = a1.w;
-      epi_ld8<X2>(ep, ep.bnb_x, e, ep.x2_py, xv);
-      const int64_t drow = ep.dadd ? dadd_row(ep, m, e / Cout) : -1;
-      if (drow >= 0) {
-        epi_ld8<X2>(ep, ep.dadd, drow * Cout + n, ep.x2_pd, d);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) a[k] += d[k];
-      }
-      if (ep.residual) epi_ld8<X2>(ep, ep.residual, e, ep.x2_py, rs);
-      float o[8];
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        const float g = (!ep.act_relu || xv[k] * ec[k].s + ec[k].t > 0.f) ? a[k] : 0.f;
-        sg[k] += g;
-        sgx[k] += g * (xv[k] - ec[k].mean) * ec[k].inv;
-        o[k] = g * ec[k].s + (ep.residual ? rs[k] : 0.f);
-      }
-      epi_st8<X2>(ep, y, e, ep.x2_py, o, o);
-    }
-    epi_bnb_sums<BM, BN, 256>(sg, sgx, T, tid, m0, n0, Cout, ep);
-    return;
-  }
-  float s1[8], s2[8], sh[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    s1[k] = s2[k] = 0.f;
-    sh[k] = (ep.st_part && ncol) ? ep.st_shift[n + k] : 0.f;
-  }
-#pragma unroll
-  for (int v = 0; v < NV; ++v) {
-    const int row = (tid + v * 256) / VPR, m = m0 + row;
-    if (m >= M || !ncol) continue;
-    const int64_t e = epi_row(ep, m, Ho, Wo) * Cout + n;
-    const float4* src = reinterpret_cast<const float4*>(T + row * LDT + cv * 8);
-    const float4 a0 = src[0], a1 = src[1];
-    float a[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
-    float rs[8];
-    if (ep.residual) epi_ld8<X2>(ep, ep.residual, e, ep.x2_py, rs);
-    float t[8], ys[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      t[k] = a[k] + ec[k].bias + (ep.residual ? rs[k] : 0.f);
-      if (ep.relu) t[k] = fmaxf(t[k], 0.f);
-      t[k] = epi_rmask(ep, e + k, epi_dropout(ep, e + k, t[k]));
-    }
-    if (X2 && ep.yf) {  // fp32 output (prediction heads of the x2 mode)
-      float4* dst = reinterpret_cast<float4*>(ep.yf + e);
-      dst[0] = make_float4(t[0], t[1], t[2], t[3]);
-      dst[1] = make_float4(t[4], t[5], t[6], t[7]);
-      continue;
-    }
-    epi_st8<X2>(ep, y, e, ep.x2_py, t, ys);  // the BN reads the STORED conv output
-    float y2v[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float q = ys[k] * ec[k].s + ec[k].t;
-      if (ep.act_relu) q = fmaxf(q, 0.f);
-      y2v[k] = q;
-      const float d = ys[k] - sh[k];
-      s1[k] += d;
-      s2[k] += d * d;
-    }
-    if (ep.y2) epi_st8<X2>(ep, ep.y2, e, ep.x2_py, y2v, y2v);
-  }
-  if (ep.st_part) epi_bn_stats<BM, BN, 256>(s1, s2, T, tid, m0, n0, M, Cout, ep);
-}
 
 template <int BM, int BN>
 __global__ void __launch_bounds__(256)
@@ -697,6 +268,15 @@ splitk_reduce_kernel(const float* __restrict__ slab, int splits, int64_t MN, int
   if (ep.y2) *reinterpret_cast<ushort4*>(ep.y2 + e) = make_ushort4(out2[0], out2[1], out2[2], out2[3]);
 }
 
+void splitk_reduce_launch(const float* slab, int splits, int M, int Cout, const ConvEpi& ep, uint16_t* y,
+                          hipStream_t st) {
+  const int64_t MN = (int64_t)M * Cout;
+  if (ep.bnb_x)
+    splitk_reduce_bnb_kernel<<<dim3(div_up(Cout, 64), div_up(M, 64)), 256, 0, st>>>(slab, splits, M, Cout, ep, y);
+  else
+    splitk_reduce_kernel<<<div_up((MN + 3) / 4, 256), 256, 0, st>>>(slab, splits, MN, Cout, ep, y);
+}
+
 // ---- S-stage LDS-DMA pipeline (the latency-bound 1-image detection regime) -----------------
 // One image's stage-3/4 convs give M = 2-6 K output rows: a few hundred workgroups, one per CU,
 // 4 waves each.  The register-staged kernel above keeps one K-step in flight, so every K-step
@@ -709,30 +289,6 @@ splitk_reduce_kernel(const float* __restrict__ slab, int splits, int64_t MN, int
 // rows past Cout read a 128-B block of zeros.  The MFMA tile, fragment reads and epilogue are
 // those of conv_igemm_fwd_kernel.
 __device__ __attribute__((aligned(128))) uint16_t g_igemm_zeros[64];
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// wait until at most `ahead` stages (LPS loads each) are still in flight; ahead <= S - 2 <= 6
-template <int LPS>
-__device__ __forceinline__ void wait_stages(int ahead) {
-  switch (ahead) {
-    case 6: wait_vmcnt<6 * LPS>(); break;
-    case 5: wait_vmcnt<5 * LPS>(); break;
-    case 4: wait_vmcnt<4 * LPS>(); break;
-    case 3: wait_vmcnt<3 * LPS>(); break;
-    case 2: wait_vmcnt<2 * LPS>(); break;
-    case 1: wait_vmcnt<LPS>(); break;
-    default: wait_vmcnt<0>(); break;
-  }
-}
-
-__device__ __forceinline__ void glds16(const void* src, void* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                   (__attribute__((address_space(3))) void*)lds_wave_base, 16, 0, 0);
-}
 
 template <int BM, int BN, int S>
 __global__ void __launch_bounds__(256)
@@ -850,283 +406,6 @@ conv_igemm_glds_kernel(const uint16_t* __restrict__ x, const uint16_t* __restric
     }
   }
   igemm_epilogue<TM, TN, WM, WN>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab);
-}
-
-// ---- buffer-resource LDS-DMA variant: near-zero address arithmetic per K-step ---------------
-// PMC on the two kernels above (s3 3x3, 64x64 tile) shows ~100 VALU + ~80 SALU instructions per
-// K-step per wave against 8 MFMAs: the im2col address math (integer divisions for the tap,
-// 64-bit pixel offsets, four bounds compares per chunk) -- not memory -- paced the loop.  Here
-// each thread precomputes, once, a 32-bit byte offset of its A row at tap (0,0) and a bit mask of
-// the taps that fall inside the image; the per-K-step part is uniform (SGPR soffset = tap and
-// channel-block offset, advanced incrementally) and the per-lane part is one mask test that
-// swaps in an out-of-range offset: buffer loads return zeros past num_records, so padding and
-// rows >= M / Cout need no zero page and no branch.  Loads go straight to LDS
-// (buffer_load_dwordx4 ... lds) S-1 stages ahead, counted vmcnt + raw barrier as above.
-constexpr uint32_t kBufOOB = 0x80000000u;
-
-__device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t rs, void* lds_wave_base, uint32_t voff,
-                                          uint32_t soff) {
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(rs, (__attribute__((address_space(3))) void*)lds_wave_base, 16,
-                                           (int)voff, (int)soff, 0, 0);
-}
-
-// body of the buffer kernel for workgroup `bid` of an `nwg`-workgroup launch; `lds`: S*(BM+BN)*BK
-// elements, the block's ONLY LDS (the grouped data + weight gradient launch below shares it with
-// the wgrad role)
-//
-// x2 (fp32-class pairs, X2 = true): a stage holds 32 channels of BOTH planes -- logical 16-B chunks
-// 0-3 of a 128-B LDS row are the hi plane's channels c..c+31, chunks 4-7 the lo plane's same
-// channels -- so the fragment reads are the bf16 ones (chunk lane>>4 and 4 + lane>>4) and a stage
-// runs three MFMAs per fragment pair (A_hi B_hi + A_hi B_lo + A_lo B_hi): 2/3 of the operand
-// bytes of three separate K phases for the same MFMA work.  The lo planes sit x2_pa / x2_pb bytes
-// further, added to the per-lane offsets of the lo chunks.
-//
-// BT (data gradient straight from the forward filter, no flipped / transposed copy): B is the
-// filter W (Cin_d, taps, Cout_d) itself -- GEMM row k = (tap, channel c) is filter row
-// c * taps + (taps - 1 - tap) with its Cout_d outputs contiguous, i.e. B arrives [k][n] instead of
-// [n][k].  The stage's B tile is stored k-major (64 rows of 64 outputs, wgrad's chunk swizzle) and
-// its fragments are read with ds_read_b64_tr_b16 (rows 8g + 4h + 0..3 of each 32-row half for lane
-// group g: the same k order as the A fragments' 16-B chunks).  BN must be 64.
-template <int BM, int BN, int S, bool F16 = false, bool X2 = false, bool BT = false>
-__device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uint16_t* __restrict__ x,
-                                               const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int NB, int H,
-                                               int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride,
-                                               int pad, const ConvEpi& ep, int tiles_n, int nwg, int ntiles, int splits,
-                                               float* __restrict__ slab) {
-  constexpr int WM = BM / 2, WN = BN / 2;
-  constexpr int TM = WM / 16, TN = WN / 16;
-  constexpr int ACH = BM / 32, BCH = BN / 32;
-  constexpr int LPS = ACH + BCH;
-  static_assert(S >= 2 && S <= 8, "pipeline depth");
-  uint16_t* As = lds;
-  uint16_t* Bs = lds + S * BM * BK;
-
-  const int q = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
-  const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + bid / 8;
-  const int split = wgid / ntiles, tile = wgid % ntiles;
-  const int tm_idx = tile / tiles_n, tn_idx = tile % tiles_n;
-  const int m0 = tm_idx * BM, n0 = tn_idx * BN;
-  const int M = NB * Ho * Wo;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int wm = wid >> 1, wn = wid & 1;
-  const int K = KH * KW * Cin;
-
-  // the range check covers voffset + soffset: with x2 pairs the records reach through the lo planes
-  // (the kBufOOB sentinel of padding taps stays beyond them: operands are < 1 GB per plane)
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)x, (short)0, (int)((int64_t)NB * H * W * Cin * 2 + (ep.x2 ? ep.x2_pa : 0u)), 0x00020000);
-  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)w, (short)0, (int)((int64_t)Cout * K * 2 + (ep.x2 ? ep.x2_pb : 0u)), 0x00020000);
-
-  const int slot = lane & 7;
-  // logical chunk lc of a row: channels lc*8 (16-bit), or (X2) channels (lc&3)*8 of plane lc>>2
-  auto chan_bytes = [&](int lc) { return X2 ? (lc & 3) * 16 : lc * 16; };
-  auto plane_a = [&](int lc) { return X2 && lc >= 4 ? ep.x2_pa : 0u; };
-  uint32_t a_off[ACH];
-  uint64_t a_mask[ACH];
-#pragma unroll
-  for (int i = 0; i < ACH; ++i) {
-    const int row = 32 * i + 8 * wid + (lane >> 3);
-    const int lc = slot ^ ((row >> 1) & 7);
-    const int m = m0 + row;
-    a_off[i] = 0;
-    a_mask[i] = 0;
-    if (m < M) {
-      const int img = m / (Ho * Wo), rem = m % (Ho * Wo);
-      const int hi0 = (rem / Wo) * stride - pad, wi0 = (rem % Wo) * stride - (ep.pad_w >= 0 ? ep.pad_w : pad);
-      a_off[i] = (uint32_t)((((int64_t)img * H + hi0) * W + wi0) * Cin * 2 + chan_bytes(lc)) + plane_a(lc);
-      for (int fr = 0; fr < KH; ++fr)
-        for (int fc = 0; fc < KW; ++fc)
-          if ((unsigned)(hi0 + fr) < (unsigned)H && (unsigned)(wi0 + fc) < (unsigned)W)
-            a_mask[i] |= 1ull << (fr * KW + fc);
-    }
-  }
-  static_assert(!BT || (BN == 64 && !F16), "BT: 64-column 16-bit bf16 tiles");
-  const int taps = KH * KW;
-  uint32_t b_off[BCH];
-#pragma unroll
-  for (int i = 0; i < BCH; ++i) {
-    const int row = 32 * i + 8 * wid + (lane >> 3);
-    if constexpr (BT) {  // row = k within the stage (x2: rows 32.. are the lo plane of the same channels)
-      const int n = n0 + (slot ^ wsw(row)) * 8;
-      const int crow = X2 ? (row & 31) : row;
-      b_off[i] = n < Cout ? (uint32_t)(((int64_t)crow * taps * Cout + n) * 2) + (X2 && row >= 32 ? ep.x2_pb : 0u)
-                          : kBufOOB;
-    } else {
-      const int co = n0 + row;
-      const int lc = slot ^ ((row >> 1) & 7);
-      b_off[i] = co < Cout ? (uint32_t)((int64_t)co * K * 2 + chan_bytes(lc)) + (X2 && lc >= 4 ? ep.x2_pb : 0u)
-                           : kBufOOB;
-    }
-  }
-  constexpr int KC = X2 ? BK / 2 : BK;  // channels per stage (x2: 32 of each plane)
-  const int cin_steps = Cin / KC;
-  const int nk_all = KH * KW * cin_steps;
-  const int per = (nk_all + splits - 1) / splits;
-  const int k_begin = split * per;
-  const int k_end = min(nk_all, k_begin + per);
-  const int nk = max(0, k_end - k_begin);
-
-  // issue cursor (uniform): tap (fr, fc), channel block ci0 of the next stage to load
-  int c_tap = k_begin / cin_steps, c_ci = (k_begin % cin_steps) * KC;
-  int c_fr = c_tap / KW, c_fc = c_tap % KW;
-  auto issue = [&](int buf) {
-    // the buffer range check sees only the VGPR offset, so the tap shift (which can turn a
-    // negative padding-row offset into a valid one) goes there; the channel block is the SGPR part
-    const uint32_t tap_a = (uint32_t)((c_fr * W + c_fc) * Cin * 2);
-    const uint32_t soff_a = (uint32_t)(c_ci * 2);
-    const uint32_t soff_b = BT ? (uint32_t)(((int64_t)c_ci * taps + (taps - 1 - c_tap)) * Cout * 2)
-                               : (uint32_t)((c_tap * Cin + c_ci) * 2);
-#pragma unroll
-    for (int i = 0; i < ACH; ++i) {
-      const uint32_t vo = ((a_mask[i] >> c_tap) & 1ull) ? a_off[i] + tap_a : kBufOOB;
-      buf_lds16(xr, As + (buf * BM + 32 * i + 8 * wid) * BK, vo, soff_a);
-    }
-#pragma unroll
-    for (int i = 0; i < BCH; ++i) buf_lds16(wr, Bs + (buf * BN + 32 * i + 8 * wid) * BK, b_off[i], soff_b);
-    c_ci += KC;
-    if (c_ci == Cin) {
-      c_ci = 0;
-      ++c_tap;
-      if (++c_fc == KW) {
-        c_fc = 0;
-        ++c_fr;
-      }
-    }
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int s = 0; s < S - 1; ++s)
-    if (s < nk) issue(s);
-  for (int ks = 0; ks < nk; ++ks) {
-    wait_stages<LPS>(min(S - 2, nk - 1 - ks));
-    __builtin_amdgcn_s_barrier();
-    if (ks + S - 1 < nk) issue((ks + S - 1) % S);
-    const int buf = ks % S;
-    if constexpr (BT) {
-      // A: 16-B chunk reads (chunk 4*kk + g); B: transposed reads of the k-major tile, all in one
-      // asm block (through the builtin the compiler drains the in-flight DMA ring first)
-      static_assert(TN == 2, "BT: two 16-column fragments per wave");
-      bf16x8 af[2][TM], bfr[2][TN];
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const int row = wm * WM + i * 16 + (lane & 15);
-          af[kk][i] = *reinterpret_cast<const bf16x8*>(As + (buf * BM + row) * BK + swz(row, kk * 4 + (lane >> 4)) * 8);
-        }
-      const int g = lane >> 4, q = (lane & 15) >> 2, pcol = (lane & 3) * 4;
-      uint32_t ad[8];
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int row = kk * 32 + 8 * g + 4 * h + q, col = wn * WN + j * 16 + pcol;
-            ad[kk * 4 + j * 2 + h] = (uint32_t)reinterpret_cast<uintptr_t>(
-                Bs + (buf * BN + row) * BK + (((col >> 3) ^ wsw(row)) << 3) + (col & 7));
-          }
-      s16x4 fr[8];
-      asm volatile(
-          "ds_read_b64_tr_b16 %0, %8\n\tds_read_b64_tr_b16 %1, %9\n\t"
-          "ds_read_b64_tr_b16 %2, %10\n\tds_read_b64_tr_b16 %3, %11\n\t"
-          "ds_read_b64_tr_b16 %4, %12\n\tds_read_b64_tr_b16 %5, %13\n\t"
-          "ds_read_b64_tr_b16 %6, %14\n\tds_read_b64_tr_b16 %7, %15\n\t"
-          "s_waitcnt lgkmcnt(0)"
-          : "=&v"(fr[0]), "=&v"(fr[1]), "=&v"(fr[2]), "=&v"(fr[3]), "=&v"(fr[4]), "=&v"(fr[5]), "=&v"(fr[6]),
-            "=&v"(fr[7])
-          : "v"(ad[0]), "v"(ad[1]), "v"(ad[2]), "v"(ad[3]), "v"(ad[4]), "v"(ad[5]), "v"(ad[6]), "v"(ad[7])
-          : "memory");
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          bfr[kk][j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(fr[kk * 4 + j * 2], fr[kk * 4 + j * 2 + 1], 0,
-                                                                          1, 2, 3, 4, 5, 6, 7));
-      // products per pass: bf16 (k-half 0) (k-half 1); x2 (hi,hi) (hi,lo) (lo,hi)
-      constexpr int NPASS = X2 ? 3 : 2;
-#pragma unroll
-      for (int ps = 0; ps < NPASS; ++ps) {
-        const int ka = X2 ? (ps == 2) : ps, kb = X2 ? (ps == 1) : ps;
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ka][i], bfr[kb][j], acc[i][j], 0, 0, 0);
-      }
-      continue;
-    }
-    if constexpr (X2) {
-      bf16x8 ah[TM], al[TM], bh[TN], bl[TN];
-      const int ch = lane >> 4, cl = 4 + (lane >> 4);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * WM + i * 16 + (lane & 15);
-        ah[i] = *reinterpret_cast<const bf16x8*>(As + (buf * BM + row) * BK + swz(row, ch) * 8);
-        al[i] = *reinterpret_cast<const bf16x8*>(As + (buf * BM + row) * BK + swz(row, cl) * 8);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wn * WN + j * 16 + (lane & 15);
-        bh[j] = *reinterpret_cast<const bf16x8*>(Bs + (buf * BN + row) * BK + swz(row, ch) * 8);
-        bl[j] = *reinterpret_cast<const bf16x8*>(Bs + (buf * BN + row) * BK + swz(row, cl) * 8);
-      }
-      // three passes over the accumulator tile (independent MFMAs back to back)
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah[i], bl[j], acc[i][j], 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
-      continue;
-    }
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      typename Mfma16<F16>::T af[TM], bfr[TN];
-      const int chunk = kk * 4 + (lane >> 4);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * WM + i * 16 + (lane & 15);
-        af[i] = *reinterpret_cast<const typename Mfma16<F16>::T*>(As + (buf * BM + row) * BK + swz(row, chunk) * 8);
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const int row = wn * WN + j * 16 + (lane & 15);
-        bfr[j] = *reinterpret_cast<const typename Mfma16<F16>::T*>(Bs + (buf * BN + row) * BK + swz(row, chunk) * 8);
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = Mfma16<F16>::mma(af[i], bfr[j], acc[i][j]);
-    }
-  }
-  static_assert(BM * (BN + 4) * 4 <= S * (BM + BN) * BK * 2, "epilogue tile must fit the operand ring");
-  if (X2 || ep.yf) {  // fp32-class pairs (separate instantiation: the 16-bit loops stay unrolled)
-    if (Cout % 8 == 0)
-      igemm_epilogue_lds<BM, BN, TM, TN, WM, WN, true>(acc, reinterpret_cast<float*>(lds), m0, n0, wm, wn, lane, tid, M,
-                                                       Cout, ep, y, split, splits, slab, Ho, Wo);
-    else
-      igemm_epilogue<TM, TN, WM, WN, true>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab, Ho, Wo);
-  } else if (Cout % 8 == 0) {
-    igemm_epilogue_lds<BM, BN, TM, TN, WM, WN>(acc, reinterpret_cast<float*>(lds), m0, n0, wm, wn, lane, tid, M, Cout,
-                                               ep, y, split, splits, slab, Ho, Wo);
-  } else {
-    igemm_epilogue<TM, TN, WM, WN>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab, Ho, Wo);
-  }
 }
 
 template <int BM, int BN, int S, bool F16 = false, bool X2 = false, bool BT = false>
@@ -1785,10 +1064,11 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
     return -1;
   if (ep.y2 && ep.bnb_x) return -1;
   if (ep.rmask && (ep.bnb_x || ep.y2 || ep.f16)) return -1;
-  if ((ep.omap || ep.pad_w >= 0) && (splits > 1 || !(tile == 22 || tile == 23 || tile >= 100))) return -1;
+  const bool kgt = tile >= 27 && tile <= 29;  // K-group tiles (conv_kg.hip)
+  if ((ep.omap || ep.pad_w >= 0) && (splits > 1 || !(tile == 22 || tile == 23 || tile >= 100 || kgt))) return -1;
   if (ep.f16 && !(tile == 21 || tile == 22 || tile == 23 || tile >= 100)) return -1;
   // BN statistics: LDS-epilogue kernels (buffer / ring), whole K per workgroup
-  if (ep.st_part && (splits > 1 || Cout % 8 != 0 || !(tile == 21 || tile == 22 || tile == 23 || tile >= 100)))
+  if (ep.st_part && (splits > 1 || Cout % 8 != 0 || !(tile == 21 || tile == 22 || tile == 23 || tile >= 100 || kgt)))
     return -1;
   // buffer variants: 32-bit byte offsets below the kBufOOB sentinel, tap mask of 64 bits
   if (tile >= 100 && ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB ||
@@ -1801,7 +1081,7 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
   if (ep.bnb_part && (splits > 1 || Cout % 8 != 0)) return -1;
   if (ep.bt && (ep.f16 || Cout % 8 != 0)) return -1;
   if (tile == 26) {  // fp32-class pairs, wide stages: x2 forward only, whole K per workgroup
-    if (!ep.x2 || ep.bt || ep.f16 || splits > 1 || ep.omap || ep.pad_w >= 0 || Cin % 64 != 0 || KH * KW > 64 ||
+    if (!ep.x2 || ep.x3 || ep.bt || ep.f16 || splits > 1 || ep.omap || ep.pad_w >= 0 || Cin % 64 != 0 || KH * KW > 64 ||
         (int64_t)NB * H * W * Cin * 2 + ep.x2_pa >= (int64_t)kBufOOB ||
         (int64_t)Cout * KH * KW * Cin * 2 + ep.x2_pb >= (int64_t)kBufOOB)
       return -1;
@@ -1815,12 +1095,16 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
     // pairs / fp32 outputs / filter read transposed: the buffer kernels (x2 also at depth 4 and
     // 128x128, A/B tiles 21 / 32 / 33)
     const bool x2_ok = !ep.bt && (tile == 21 || tile == 32 || tile == 33);
-    if (!(tile == 22 || tile == 23 || x2_ok)) tile = 23;
+    if (!(tile == 22 || tile == 23 || x2_ok || kgt)) tile = 23;
     if ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB || (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kBufOOB ||
         KH * KW > 64 || ep.f16)
       return -1;
+    if (ep.x2 && ((int64_t)NB * H * W * Cin * 2 + (ep.x3 ? 2 : 1) * (int64_t)ep.x2_pa >= (int64_t)kBufOOB ||
+                  (int64_t)Cout * KH * KW * Cin * 2 + (ep.x3 ? 2 : 1) * (int64_t)ep.x2_pb >= (int64_t)kBufOOB))
+      return -1;
     if (ep.yf && (ep.y2 || ep.bnb_x || ep.st_part)) return -1;
   }
+  if (kgt) return conv_igemm_kg(tile, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st);
   if (tile >= 100 && tile < 100 + kNumRing) {
     launch_ring_code(tile - 100, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st);
     return tile;
@@ -1953,13 +1237,14 @@ int conv_dgrad_wgrad(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, 
     return -1;
   if (prev_slab != nullptr && (prev_splits < 2 || prev_n % 4 != 0 || (prev_dw == nullptr && prev_dwf == nullptr)))
     return -1;
-  if (ep.x2 != wx2.x2) return -1;  // both roles read the same dY: one storage format
+  if (ep.x2 != wx2.x2 || ep.x3 != wx2.x3) return -1;  // both roles read the same dY: one storage format
   const int M = NB * Ho * Wo;
   const int tiles_n = (Cout + 63) / 64;
   const int ntiles = ((M + 63) / 64) * tiles_n;
   WgradParams wp = wgrad_params(wg_dy, wg_x, dw, slab, wg_NB, wg_H, wg_W, wg_Cin, wg_Ho, wg_Wo, wg_Cout, wg_KH,
                                 wg_KW, wg_stride, wg_pad, wg_splits, accumulate);
   wp.x2 = wx2.x2;
+  wp.x3 = wx2.x3;
   wp.x2_pdy = wx2.pdy;
   wp.x2_px = wx2.px;
   wp.dwf = wx2.dwf;

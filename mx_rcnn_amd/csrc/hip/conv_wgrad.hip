@@ -202,9 +202,13 @@ int conv_wgrad(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab,
   const int64_t n = (int64_t)Cout * KH * KW * Cin;
   const bool buf_ok = (int64_t)P * Cout * 2 < (int64_t)kWgOOB && (int64_t)NB * H * W * Cin * 2 < (int64_t)kWgOOB;
   if (x2.x2 && !(variant == 0 && buf_ok)) return -1;  // pairs: the LDS-DMA kernel only
+  if (x2.x2 && ((int64_t)P * Cout * 2 + (x2.x3 ? 2 : 1) * (int64_t)x2.pdy >= (int64_t)kWgOOB ||
+                (int64_t)NB * H * W * Cin * 2 + (x2.x3 ? 2 : 1) * (int64_t)x2.px >= (int64_t)kWgOOB))
+    return -1;  // every plane inside the 32-bit buffer offsets
   if (variant == 0 && buf_ok) {
     WgradParams p = wgrad_params(dy, x, dw, slab, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, splits, accumulate);
     p.x2 = x2.x2;
+    p.x3 = x2.x3;
     p.x2_pdy = x2.pdy;
     p.x2_px = x2.px;
     p.dwf = x2.dwf;

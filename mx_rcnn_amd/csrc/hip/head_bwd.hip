@@ -36,12 +36,16 @@ struct HeadStep {
   int h, r0;  // head, first reduction index of this step
 };
 
-// X2: the fp32-class variant (HeadBwdArgs::x2): dY fp32 split into hi / lo in registers, X / W
-// read as hi / lo planes, both halves staged in LDS, three MFMAs per fragment pair
-template <bool X2>
+// NP = 2: the bf16x3 variant (HeadBwdArgs::x2): dY fp32 split into hi / lo in registers, X / W
+// read as hi / lo planes, both halves staged in LDS, three MFMAs per fragment pair.  NP = 3: the
+// fp32 mode (HeadBwdArgs::x3): (hi, mid, lo) -- LDS planes in that logical order, memory planes
+// (mid, hi, lo) (common.h) -- and six MFMAs per fragment pair
+template <int NP>
 __global__ void __launch_bounds__(256)
 head_bwd_kernel(const uint16_t* __restrict__ x, int M, int K, HeadBwdArgs a) {
-  constexpr int NP = X2 ? 2 : 1;  // operand planes staged per step
+  constexpr bool X2 = NP >= 2, X3 = NP == 3;
+  // memory plane (in units of the plane spacing) of logical plane lp
+  auto mpl = [](int lp) -> int64_t { return X3 ? (lp == 0 ? 1 : lp == 1 ? 0 : 2) : lp; };
   __shared__ __attribute__((aligned(16))) uint16_t As[NP][64 * HB_LD];
   __shared__ __attribute__((aligned(16))) uint16_t Bs[NP][64 * HB_LD];
   __shared__ __attribute__((aligned(16))) float T[64 * 68];
@@ -93,9 +97,12 @@ head_bwd_kernel(const uint16_t* __restrict__ x, int M, int K, HeadBwdArgs a) {
   // ---- register stage: 8 A values + one 16-B B vector per thread (per plane) ---------------
   uint16_t ra[NP][8];
   uint4 rbv[NP];
-  // dY element (m, n) of head h as (hi, lo) bf16 (lo unused unless X2)
-  auto dy_at = [&](int hh, int Nh, int64_t idx, uint16_t& hi, uint16_t& lo) {
-    if constexpr (X2) {
+  // dY element (m, n) of head h as (hi, lo) or (hi, mid, lo) bf16 (unused planes 0)
+  auto dy_at = [&](int hh, int Nh, int64_t idx, uint16_t& hi, uint16_t& lo, uint16_t& l2) {
+    l2 = 0;
+    if constexpr (X3) {
+      split3_bf16(a.dyf[hh][idx], hi, lo, l2);
+    } else if constexpr (X2) {
       split_bf16(a.dyf[hh][idx], hi, lo);
     } else {
       hi = a.dy[hh][idx];
@@ -112,17 +119,18 @@ head_bwd_kernel(const uint16_t* __restrict__ x, int M, int K, HeadBwdArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int n = st.r0 + rq + e;
-        uint16_t hi = 0, lo = 0;
-        if (m < M && n < Nh) dy_at(st.h, Nh, (int64_t)m * Nh + n, hi, lo);
+        uint16_t hi = 0, lo = 0, l2 = 0;
+        if (m < M && n < Nh) dy_at(st.h, Nh, (int64_t)m * Nh + n, hi, lo, l2);
         ra[0][e] = hi;
         if constexpr (X2) ra[1][e] = lo;
+        if constexpr (X3) ra[2][e] = l2;
       }
       // B(r = n, j = k) = W[n][k]
       const int r = tid >> 3, jq = (tid & 7) * 8;
       const int n = st.r0 + r;
 #pragma unroll
       for (int pl = 0; pl < NP; ++pl)
-        rbv[pl] = n < Nh ? *reinterpret_cast<const uint4*>(a.w[st.h] + (pl ? a.w_plane[st.h] : 0) + (int64_t)n * K + k0 + jq)
+        rbv[pl] = n < Nh ? *reinterpret_cast<const uint4*>(a.w[st.h] + mpl(pl) * a.w_plane[st.h] + (int64_t)n * K + k0 + jq)
                          : make_uint4(0, 0, 0, 0);
     } else {
       // A(i = n, r = m) = dY[m][n]: thread -> row r, 8 consecutive i
@@ -131,15 +139,16 @@ head_bwd_kernel(const uint16_t* __restrict__ x, int M, int K, HeadBwdArgs a) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const int n = i0 + iq + e;
-        uint16_t hi = 0, lo = 0;
-        if (m < re && n < Nh) dy_at(st.h, Nh, (int64_t)m * Nh + n, hi, lo);
+        uint16_t hi = 0, lo = 0, l2 = 0;
+        if (m < re && n < Nh) dy_at(st.h, Nh, (int64_t)m * Nh + n, hi, lo, l2);
         ra[0][e] = hi;
         if constexpr (X2) ra[1][e] = lo;
+        if constexpr (X3) ra[2][e] = l2;
       }
       // B(r = m, j = k) = X[m][k]
 #pragma unroll
       for (int pl = 0; pl < NP; ++pl)
-        rbv[pl] = m < re ? *reinterpret_cast<const uint4*>(x + (pl ? xplane : 0) + (int64_t)m * K + k0 + (tid & 7) * 8)
+        rbv[pl] = m < re ? *reinterpret_cast<const uint4*>(x + mpl(pl) * xplane + (int64_t)m * K + k0 + (tid & 7) * 8)
                          : make_uint4(0, 0, 0, 0);
     }
   };
@@ -200,6 +209,11 @@ head_bwd_kernel(const uint16_t* __restrict__ x, int M, int K, HeadBwdArgs a) {
           acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][p], bf[1][q], acc[p][q], 0, 0, 0);
           acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][p], bf[0][q], acc[p][q], 0, 0, 0);
         }
+        if constexpr (X3) {  // (hi, lo), (lo, hi), (mid, mid)
+          acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][p], bf[2][q], acc[p][q], 0, 0, 0);
+          acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[2][p], bf[0][q], acc[p][q], 0, 0, 0);
+          acc[p][q] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][p], bf[1][q], acc[p][q], 0, 0, 0);
+        }
       }
   }
 
@@ -226,12 +240,12 @@ head_bwd_kernel(const uint16_t* __restrict__ x, int M, int K, HeadBwdArgs a) {
       const int64_t o = (int64_t)i * K + k0 + cv;
       if (a.relu_mask) {
         float xv[8];
-        if constexpr (X2) ld8x(x + o, xplane, xv);
+        if constexpr (X2) ld8x(x + o, xplane, xv, X3);
         else ld8_bf16(x + o, xv);
 #pragma unroll
         for (int q = 0; q < 8; ++q) v8[q] = xv[q] > 0.f ? v8[q] * a.mask_scale : 0.f;
       }
-      if constexpr (X2) st8x(a.dx + o, xplane, v8, v8);
+      if constexpr (X2) st8x(a.dx + o, xplane, v8, v8, X3);
       else st8_bf16(a.dx + o, v8);
     } else {
       if (i >= Nh) continue;
@@ -332,8 +346,9 @@ int head_bwd(const uint16_t* x, int M, int K, const HeadBwdArgs& a, hipStream_t 
     if (a.N[h] <= 0) return -1;
     nwg += (int64_t)((a.N[h] + 63) / 64) * tk_n * a.rs;
   }
-  if (a.x2) head_bwd_kernel<true><<<(unsigned)nwg, 256, 0, st>>>(x, M, K, a);
-  else head_bwd_kernel<false><<<(unsigned)nwg, 256, 0, st>>>(x, M, K, a);
+  if (a.x3) head_bwd_kernel<3><<<(unsigned)nwg, 256, 0, st>>>(x, M, K, a);
+  else if (a.x2) head_bwd_kernel<2><<<(unsigned)nwg, 256, 0, st>>>(x, M, K, a);
+  else head_bwd_kernel<1><<<(unsigned)nwg, 256, 0, st>>>(x, M, K, a);
   if (a.rs > 1)
     for (int h = 0; h < a.nheads; ++h)
       head_bwd_fold_kernel<<<div_up((int64_t)a.N[h] * K + a.N[h], 256), 256, 0, st>>>(K, a, h);
@@ -355,7 +370,7 @@ chan_sum_part_kernel(const uint16_t* __restrict__ x, int64_t M, int C, int rows,
   if (c0 < C)
     for (int64_t r = r0 + rl; r < r1; r += 32) {
       float v[8];
-      ld8c(x, r * C + c0, code, M * C, v);  // code 3: x2 pairs, lo plane M * C on
+      ld8c(x, r * C + c0, code, M * C, v);  // code 3 / 4: x2 / x3 planes M * C apart
 #pragma unroll
       for (int k = 0; k < 8; ++k) s[k] += v[k];
     }

@@ -46,7 +46,7 @@ template <typename T>
 __global__ void __launch_bounds__(256)
 roi_pool_fwd_vec4(const T* __restrict__ feat, int code, int B, int H, int W, int C, const float* __restrict__ rois, int R,
                   int PH, int PW, float scale, T* __restrict__ out, int32_t* __restrict__ argmax) {
-  // code 3 (x2 pairs, T = uint16_t): lo planes one (B, H, W, C) / (R, PH, PW, C) block further
+  // code 3 / 4 (x2 pairs / x3 triples, T = uint16_t): planes one (B, H, W, C) / (R, PH, PW, C) block apart
   const int64_t fplane = (int64_t)B * H * W * C, oplane = (int64_t)R * PH * PW * C;
   using V = typename Vec4<T>::type;
   const int CV = C >> 2;
@@ -70,11 +70,11 @@ roi_pool_fwd_vec4(const T* __restrict__ feat, int code, int B, int H, int W, int
       for (int w = bin.ws; w < bin.we; ++w) {
         const int idx = h * W + w;
         const V v = *reinterpret_cast<const V*>(fb + (int64_t)idx * C);
-        float f0 = to_f(v.x, code == 3 ? 1 : code), f1 = to_f(v.y, code == 3 ? 1 : code);
-        float f2 = to_f(v.z, code == 3 ? 1 : code), f3 = to_f(v.w, code == 3 ? 1 : code);
+        float f0 = to_f(v.x, code >= 3 ? 1 : code), f1 = to_f(v.y, code >= 3 ? 1 : code);
+        float f2 = to_f(v.z, code >= 3 ? 1 : code), f3 = to_f(v.w, code >= 3 ? 1 : code);
         if constexpr (sizeof(T) == 2) {
-          if (code == 3) {
-            const V l = *reinterpret_cast<const V*>(fb + fplane + (int64_t)idx * C);
+          for (int pl = 1; pl <= code - 2; ++pl) {  // x2: plane 1; x3: planes 1, 2
+            const V l = *reinterpret_cast<const V*>(fb + pl * fplane + (int64_t)idx * C);
             f0 += to_f(l.x, 1); f1 += to_f(l.y, 1); f2 += to_f(l.z, 1); f3 += to_f(l.w, 1);
           }
         }
@@ -87,9 +87,9 @@ roi_pool_fwd_vec4(const T* __restrict__ feat, int code, int B, int H, int W, int
   }
   const int64_t o = t * 4;
   if constexpr (sizeof(T) == 2) {
-    if (code == 3) {
+    if (code >= 3) {
       const float mv[4] = {m0, m1, m2, m3};
-      st4c(out, o, 3, oplane, mv);
+      st4c(out, o, code, oplane, mv);
     } else {
       ushort4 ov = make_ushort4(f32_to_h16(m0, code), f32_to_h16(m1, code), f32_to_h16(m2, code), f32_to_h16(m3, code));
       *reinterpret_cast<ushort4*>(out + o) = ov;
@@ -216,7 +216,7 @@ __global__ void __launch_bounds__(256)
 roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ argmax, const float* __restrict__ rois,
                         int R, int PHW, int HW, int C, int code, const T* __restrict__ gadd, T* __restrict__ gin) {
   extern __shared__ float acc[];  // [HW][CW]
-  // code 3 (x2 pairs): gout's lo plane one (R, PH, PW, C) block further, gadd's / gin's one (B, H, W, C)
+  // code 3 / 4 (x2 / x3 planes): gout's planes one (R, PH, PW, C) block apart, gadd's / gin's one (B, H, W, C)
   const int64_t oplane = (int64_t)R * PHW * C, iplane = (int64_t)gridDim.y * HW * C;
   // XCD-aware channel groups: workgroups are dealt round-robin over the 8 XCDs, so consecutive
   // block ids would put neighbouring channel groups -- which read and write the same cache lines
@@ -230,11 +230,11 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
 #pragma unroll 4
   for (int p = threadIdx.x; p < HW; p += blockDim.x) {
     float v[CW];
-    if (gadd && code == 3 && CW == 4) {
-      ld4c(gadd, ((int64_t)b * HW + p) * C + c0, 3, iplane, v);  // one 8-B load per plane
-    } else if (gadd && code == 3) {
+    if (gadd && code >= 3 && CW == 4) {
+      ld4c(gadd, ((int64_t)b * HW + p) * C + c0, code, iplane, v);  // one 8-B load per plane
+    } else if (gadd && code >= 3) {
 #pragma unroll
-      for (int k = 0; k < CW; ++k) v[k] = ldc(gadd, ((int64_t)b * HW + p) * C + c0 + k, 3, iplane);
+      for (int k = 0; k < CW; ++k) v[k] = ldc(gadd, ((int64_t)b * HW + p) * C + c0 + k, code, iplane);
     } else if (gadd) ldv<CW>(gadd + ((int64_t)b * HW + p) * C + c0, v, code);
     else
 #pragma unroll
@@ -253,7 +253,7 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
     if constexpr (CW == 4) {  // c0 and C are multiples of 4: 16-B argmax / 8-B (per plane) gradient loads
       const int4 av = *reinterpret_cast<const int4*>(argmax + base);
       a[0] = av.x; a[1] = av.y; a[2] = av.z; a[3] = av.w;
-      if (code == 3) ld4c(gout, base, 3, oplane, g);
+      if (code >= 3) ld4c(gout, base, code, oplane, g);
       else
 #pragma unroll
         for (int k = 0; k < CW; ++k) g[k] = to_f(gout[base + k], code);
@@ -261,7 +261,7 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
 #pragma unroll
       for (int k = 0; k < CW; ++k) {
         a[k] = argmax[base + k];
-        g[k] = code == 3 ? ldc(gout, base + k, 3, oplane) : to_f(gout[base + k], code);
+        g[k] = code >= 3 ? ldc(gout, base + k, code, oplane) : to_f(gout[base + k], code);
       }
     }
 #pragma unroll
@@ -274,11 +274,11 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
     float v[CW];
 #pragma unroll
     for (int k = 0; k < CW; ++k) v[k] = acc[p * CW + k];
-    if (code == 3 && CW == 4) {
-      st4c(gin, ((int64_t)b * HW + p) * C + c0, 3, iplane, v);
-    } else if (code == 3) {
+    if (code >= 3 && CW == 4) {
+      st4c(gin, ((int64_t)b * HW + p) * C + c0, code, iplane, v);
+    } else if (code >= 3) {
 #pragma unroll
-      for (int k = 0; k < CW; ++k) stc(gin, ((int64_t)b * HW + p) * C + c0 + k, v[k], 3, iplane);
+      for (int k = 0; k < CW; ++k) stc(gin, ((int64_t)b * HW + p) * C + c0 + k, v[k], code, iplane);
     } else {
       stv<CW>(gin + ((int64_t)b * HW + p) * C + c0, v, code);
     }

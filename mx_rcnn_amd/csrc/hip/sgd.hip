@@ -23,7 +23,7 @@ template <bool GBF16>
 __global__ void __launch_bounds__(256)
 sgd_kernel(float* __restrict__ w, float* __restrict__ mom, const void* __restrict__ grad, int64_t n,
            const float* __restrict__ lr_p, float mu, float wd, float rescale, float clip, uint16_t* __restrict__ wb,
-           int64_t x2_plane) {
+           int64_t x2_plane, int x3) {
   const float lr = *lr_p;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
   for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
@@ -43,9 +43,9 @@ sgd_kernel(float* __restrict__ w, float* __restrict__ mom, const void* __restric
       wv.w = sgd_one(wv.w, mv.w, gv.w, lr, mu, wd, rescale, clip);
       *reinterpret_cast<float4*>(w + i) = wv;
       *reinterpret_cast<float4*>(mom + i) = mv;
-      if (wb && x2_plane) {  // fp32-class shadow: hi / lo pair planes (common.h x2)
+      if (wb && x2_plane) {  // multi-plane shadow: x2 hi / lo pair or x3 (mid, hi, lo) triple (common.h)
         const float v4[4] = {wv.x, wv.y, wv.z, wv.w};
-        st4c(wb, i, kCodeX2, x2_plane, v4);
+        st4c(wb, i, x3 ? kCodeX3 : kCodeX2, x2_plane, v4);
       } else if (wb) {
         *reinterpret_cast<ushort4*>(wb + i) =
             make_ushort4(f32_to_bf16(wv.x), f32_to_bf16(wv.y), f32_to_bf16(wv.z), f32_to_bf16(wv.w));
@@ -57,7 +57,7 @@ sgd_kernel(float* __restrict__ w, float* __restrict__ mom, const void* __restric
         const float nw = sgd_one(w[k], m, g, lr, mu, wd, rescale, clip);
         w[k] = nw;
         mom[k] = m;
-        if (wb && x2_plane) stx(wb, k, x2_plane, nw);
+        if (wb && x2_plane) stx(wb, k, x2_plane, nw, x3);
         else if (wb) wb[k] = f32_to_bf16(nw);
       }
     }
@@ -86,7 +86,7 @@ template <bool GBF16, bool NT>
 __global__ void __launch_bounds__(256)
 sgd8_kernel(float* __restrict__ w, float* __restrict__ mom, const void* __restrict__ grad, int64_t n,
             const float* __restrict__ lr_p, float mu, float wd, float rescale, float clip, uint16_t* __restrict__ wb,
-            int64_t x2_plane) {
+            int64_t x2_plane, int x3) {
   const float lr = *lr_p;
   const int64_t n8 = n & ~(int64_t)7;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
@@ -126,7 +126,7 @@ sgd8_kernel(float* __restrict__ w, float* __restrict__ mom, const void* __restri
     sgd_st<NT>(reinterpret_cast<sgd_f4*>(mom + i + 4), sgd_f4{mv[4], mv[5], mv[6], mv[7]});
     if (wb && x2_plane) {
       float stored[8];
-      st8x(wb + i, x2_plane, wv, stored);
+      st8x(wb + i, x2_plane, wv, stored, x3);
     } else if (wb) {
       st8_bf16(wb + i, wv);
     }
@@ -138,7 +138,7 @@ sgd8_kernel(float* __restrict__ w, float* __restrict__ mom, const void* __restri
     const float nw = sgd_one(w[k], m, gk, lr, mu, wd, rescale, clip);
     w[k] = nw;
     mom[k] = m;
-    if (wb && x2_plane) stx(wb, k, x2_plane, nw);
+    if (wb && x2_plane) stx(wb, k, x2_plane, nw, x3);
     else if (wb) wb[k] = f32_to_bf16(nw);
   }
 }
@@ -153,13 +153,14 @@ static int sgd_variant() {
 }
 
 void sgd_momentum(float* w, float* mom, const void* grad, int grad_bf16, int64_t n, const float* lr, float momentum,
-                  float wd, float rescale, float clip, uint16_t* w_bf16, hipStream_t st, int64_t x2_plane) {
+                  float wd, float rescale, float clip, uint16_t* w_bf16, hipStream_t st, int64_t x2_plane,
+                  int x3) {
   if (n == 0) return;
   const int var = sgd_variant();
   const auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
   if (var > 0 && x2_plane % 8 == 0 && a16(w) && a16(mom) && a16(grad) && (w_bf16 == nullptr || a16(w_bf16))) {
     const int blocks = (int)std::min<int64_t>(std::max<int64_t>(div_up((n + 7) / 8, 256), 1), 256 * 8);
-#define MXR_SGD8(GB, NT) sgd8_kernel<GB, NT><<<blocks, 256, 0, st>>>(w, mom, grad, n, lr, momentum, wd, rescale, clip, w_bf16, x2_plane)
+#define MXR_SGD8(GB, NT) sgd8_kernel<GB, NT><<<blocks, 256, 0, st>>>(w, mom, grad, n, lr, momentum, wd, rescale, clip, w_bf16, x2_plane, x3)
     if (grad_bf16) { if (var == 2) MXR_SGD8(true, true); else MXR_SGD8(true, false); }
     else { if (var == 2) MXR_SGD8(false, true); else MXR_SGD8(false, false); }
 #undef MXR_SGD8
@@ -167,9 +168,9 @@ void sgd_momentum(float* w, float* mom, const void* grad, int grad_bf16, int64_t
   }
   const int blocks = (int)std::min<int64_t>(div_up((n + 3) / 4, 256), 256 * 8);
   if (grad_bf16)
-    sgd_kernel<true><<<blocks, 256, 0, st>>>(w, mom, grad, n, lr, momentum, wd, rescale, clip, w_bf16, x2_plane);
+    sgd_kernel<true><<<blocks, 256, 0, st>>>(w, mom, grad, n, lr, momentum, wd, rescale, clip, w_bf16, x2_plane, x3);
   else
-    sgd_kernel<false><<<blocks, 256, 0, st>>>(w, mom, grad, n, lr, momentum, wd, rescale, clip, w_bf16, x2_plane);
+    sgd_kernel<false><<<blocks, 256, 0, st>>>(w, mom, grad, n, lr, momentum, wd, rescale, clip, w_bf16, x2_plane, x3);
 }
 
 }  // namespace mxr

@@ -42,9 +42,11 @@ constexpr int STEM_BM = 64;   // output pixels per workgroup (one row strip)
 constexpr int STEM_CO = 64;   // output channels (all of them)
 constexpr int STEM_LDT = STEM_CO + 8;  // 16-bit row stride of the staged output tile
 
-// X2 (fp32-class mode): x is the fp32 image, the patch is kept as hi / lo bf16 planes, the packed
-// filter is an x2 pair (lo plane 64 * KP on), three MFMAs per fragment pair, y an x2 pair
-template <int KH, int KW, int S, bool F16, bool X2 = false>
+// NP = 2 (bf16x3 mode): x is the fp32 image, the patch is kept as hi / lo bf16 planes, the packed
+// filter is an x2 pair (lo plane 64 * KP on), three MFMAs per fragment pair, y an x2 pair.
+// NP = 3 (fp32 mode): patch and packed filter as (hi, mid, lo) planes in that logical order, six
+// MFMAs per fragment pair, y an x3 triple (memory planes mid, hi, lo; common.h)
+template <int KH, int KW, int S, bool F16, int NP = 1>
 __global__ void __launch_bounds__(256)
 stem_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, const StemArgs a,
                  uint16_t* __restrict__ y, int N, int H, int W, int Ho, int Wo, int pad, int relu, int strips, int nwg) {
@@ -52,7 +54,7 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
   constexpr int KP = (K + 31) / 32 * 32;
   constexpr int PW = (STEM_BM - 1) * S + KW;  // patch columns
   constexpr int code = F16 ? 2 : 1;
-  constexpr int NP = X2 ? 2 : 1;  // planes
+  constexpr bool X2 = NP >= 2, X3 = NP == 3;
   __shared__ __attribute__((aligned(16))) uint16_t patch[NP][KH * PW * 4];
   __shared__ int koff[KP];
   __shared__ float in_aff[6], out_aff[2 * STEM_CO];
@@ -105,9 +107,18 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
   for (int e = tid; e < KH * PW; e += 256) {
     const int r = e / PW, c = e - r * PW;
     const int hi = hi0 + r, wi = wi0 + c;
-    uint2 v = make_uint2(0u, 0u), vl = make_uint2(0u, 0u);
+    uint2 v = make_uint2(0u, 0u), vl = make_uint2(0u, 0u), vm = make_uint2(0u, 0u);
     if ((unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W) {
-      if constexpr (X2) {
+      if constexpr (X3) {
+        const float* px = reinterpret_cast<const float*>(x) + (((int64_t)n * H + hi) * W + wi) * 3;
+        uint16_t h0, m0, l0, h1, m1, l1, h2, m2, l2;
+        split3_bf16(px[0] * s0 + b0, h0, m0, l0);
+        split3_bf16(px[1] * s1 + b1, h1, m1, l1);
+        split3_bf16(px[2] * s2 + b2, h2, m2, l2);
+        v = make_uint2((uint32_t)h0 | ((uint32_t)h1 << 16), h2);
+        vm = make_uint2((uint32_t)m0 | ((uint32_t)m1 << 16), m2);
+        vl = make_uint2((uint32_t)l0 | ((uint32_t)l1 << 16), l2);
+      } else if constexpr (X2) {
         const float* px = reinterpret_cast<const float*>(x) + (((int64_t)n * H + hi) * W + wi) * 3;
         uint16_t h0, l0, h1, l1, h2, l2;
         split_bf16(px[0] * s0 + b0, h0, l0);
@@ -125,6 +136,7 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
     }
     *reinterpret_cast<uint2*>(patch[0] + e * 4) = v;
     if constexpr (X2) *reinterpret_cast<uint2*>(patch[NP - 1] + e * 4) = vl;
+    if constexpr (X3) *reinterpret_cast<uint2*>(patch[1] + e * 4) = vm;
   }
   __syncthreads();
 
@@ -155,7 +167,15 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
     for (int j = 0; j < 4; ++j) {
       const uint4 bf = *reinterpret_cast<const uint4*>(w + (j * 16 + (lane & 15)) * KP + k0);
       acc[j] = stem_mfma<F16>(af[0], bf, acc[j]);
-      if constexpr (X2) {  // A_hi B_lo + A_lo B_hi
+      if constexpr (X3) {  // logical planes (hi, mid, lo): hm + mh + hl + lh + mm
+        const uint4 bm = *reinterpret_cast<const uint4*>(w + STEM_CO * KP + (j * 16 + (lane & 15)) * KP + k0);
+        const uint4 bl = *reinterpret_cast<const uint4*>(w + 2 * STEM_CO * KP + (j * 16 + (lane & 15)) * KP + k0);
+        acc[j] = stem_mfma<F16>(af[0], bm, acc[j]);
+        acc[j] = stem_mfma<F16>(af[1], bf, acc[j]);
+        acc[j] = stem_mfma<F16>(af[0], bl, acc[j]);
+        acc[j] = stem_mfma<F16>(af[2], bf, acc[j]);
+        acc[j] = stem_mfma<F16>(af[1], bm, acc[j]);
+      } else if constexpr (X2) {  // A_hi B_lo + A_lo B_hi
         const uint4 bl = *reinterpret_cast<const uint4*>(w + STEM_CO * KP + (j * 16 + (lane & 15)) * KP + k0);
         acc[j] = stem_mfma<F16>(af[0], bl, acc[j]);
         acc[j] = stem_mfma<F16>(af[1], bf, acc[j]);
@@ -172,7 +192,13 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
     for (int r = 0; r < 4; ++r) {
       float v = acc[j][r] * sc + sh;
       if (relu) v = fmaxf(v, 0.f);
-      if constexpr (X2) {
+      if constexpr (X3) {  // T planes in memory order (mid, hi, lo)
+        uint16_t h, m, l;
+        split3_bf16(v, h, m, l);
+        T[0][(wave * 16 + chunk * 4 + r) * STEM_LDT + co] = m;
+        T[1][(wave * 16 + chunk * 4 + r) * STEM_LDT + co] = h;
+        T[2][(wave * 16 + chunk * 4 + r) * STEM_LDT + co] = l;
+      } else if constexpr (X2) {
         uint16_t h, l;
         split_bf16(v, h, l);
         T[0][(wave * 16 + chunk * 4 + r) * STEM_LDT + co] = h;
@@ -192,9 +218,10 @@ stem_conv_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
     if (wo < Wo) {
       const int64_t o = (((int64_t)n * Ho + ho) * Wo + wo) * STEM_CO + cv * 8;
       *reinterpret_cast<uint4*>(y + o) = *reinterpret_cast<const uint4*>(T[0] + px * STEM_LDT + cv * 8);
-      if constexpr (X2)  // lo plane: one (N, Ho, Wo, 64) block further
-        *reinterpret_cast<uint4*>(y + (int64_t)N * Ho * Wo * STEM_CO + o) =
-            *reinterpret_cast<const uint4*>(T[NP - 1] + px * STEM_LDT + cv * 8);
+#pragma unroll
+      for (int pl = 1; pl < NP; ++pl)  // further planes: one (N, Ho, Wo, 64) block apart
+        *reinterpret_cast<uint4*>(y + pl * (int64_t)N * Ho * Wo * STEM_CO + o) =
+            *reinterpret_cast<const uint4*>(T[pl] + px * STEM_LDT + cv * 8);
     }
   }
 }
@@ -208,9 +235,12 @@ int stem_conv(const uint16_t* x, const uint16_t* w, const StemArgs& a, uint16_t*
   const int nwg = (int)nwg64;
 #define MXR_STEM(KH_, KW_, S_)                                                                                   \
   if (KH == KH_ && KW == KW_ && stride == S_) {                                                                \
-    if (code == 3)                                                                                             \
-      stem_conv_kernel<KH_, KW_, S_, false, true><<<nwg, 256, 0, st>>>(x, w, a, y, N, H, W, Ho, Wo, pad, relu,     \
-                                                                       strips, nwg);                            \
+    if (code == 4)                                                                                             \
+      stem_conv_kernel<KH_, KW_, S_, false, 3><<<nwg, 256, 0, st>>>(x, w, a, y, N, H, W, Ho, Wo, pad, relu,        \
+                                                                    strips, nwg);                               \
+    else if (code == 3)                                                                                        \
+      stem_conv_kernel<KH_, KW_, S_, false, 2><<<nwg, 256, 0, st>>>(x, w, a, y, N, H, W, Ho, Wo, pad, relu,        \
+                                                                    strips, nwg);                               \
     else if (code == 2)                                                                                        \
       stem_conv_kernel<KH_, KW_, S_, true><<<nwg, 256, 0, st>>>(x, w, a, y, N, H, W, Ho, Wo, pad, relu, strips, nwg); \
     else                                                                                                       \

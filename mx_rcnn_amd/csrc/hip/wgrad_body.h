@@ -67,7 +67,11 @@ struct WgradParams {
   // pixels of both planes (LDS rows 0-31 hi, 32-63 lo, the same pixels), read by the same
   // fragment loads as a 64-pixel bf16 stage, and runs three MFMAs per fragment pair (dY_hi X_hi +
   // dY_hi X_lo + dY_lo X_hi); the gradient is fp32 (dwf instead of dw)
+  // x3 (the fp32 mode, common.h): dY and X are (mid, hi, lo) triples, x2_pdy / x2_px the plane
+  // spacings; the pixel loop runs twice, first one plane further on ((hi, lo): hh + hl + lh), then at
+  // the base ((mid, hi): mm + mh + hm)
   int x2 = 0;
+  int x3 = 0;
   uint32_t x2_pdy = 0, x2_px = 0;  // lo-plane offsets, bytes
   float* dwf = nullptr;
 };
@@ -99,13 +103,16 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
   const int s_begin = split * per, s_end = min(steps_all, s_begin + per);
   const int nsteps = max(0, s_end - s_begin);
   constexpr int PX = X2 ? WG_BK / 2 : WG_BK;  // pixels per stage
-  const int nloop = X2 ? 2 * nsteps : nsteps;
+  const int nloop1 = X2 ? 2 * nsteps : nsteps;           // one pass
+  const int nloop = X2 && p.x3 ? 2 * nloop1 : nloop1;    // x3: two phases
 
-  // records through the lo planes for x2 pairs (the range check covers voffset + soffset)
+  // records through the lo planes for x2 pairs, the third plane for x3 (the range check covers
+  // voffset + soffset)
+  const int npl = X2 ? (p.x3 ? 2 : 1) : 0;
   const __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)dy, (short)0, (int)((int64_t)P * Cout * 2 + (X2 ? p.x2_pdy : 0u)), 0x00020000);
+      (void*)dy, (short)0, (int)((int64_t)P * Cout * 2 + (int64_t)npl * p.x2_pdy), 0x00020000);
   const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)x, (short)0, (int)((int64_t)NB * H * W * Cin * 2 + (X2 ? p.x2_px : 0u)), 0x00020000);
+      (void*)x, (short)0, (int)((int64_t)NB * H * W * Cin * 2 + (int64_t)npl * p.x2_px), 0x00020000);
   int rowi[2], chk[2], prow[2];
   uint32_t a_off[2];
 #pragma unroll
@@ -116,12 +123,15 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
     a_off[i] = co0 + chk[i] * 8 < Cout ? (uint32_t)((prow[i] * Cout + co0 + chk[i] * 8) * 2) : kWgOOB;
   }
   auto issue = [&](int it, int buf) {
+    const bool ph0 = X2 && p.x3 && it < nloop1;  // x3 phase (hi, lo): one plane further on
+    if (X2 && p.x3 && !ph0) it -= nloop1;
     const int p0 = s_begin * WG_BK + it * PX;
     uint16_t* Ab = lds + buf * 2 * WG_BK * 64;
     uint16_t* Bb = Ab + WG_BK * 64;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const uint32_t pdy = X2 && i ? p.x2_pdy : 0u, px = X2 && i ? p.x2_px : 0u;
+      const uint32_t pdy = (X2 && i ? p.x2_pdy : 0u) + (ph0 ? p.x2_pdy : 0u);
+      const uint32_t px = (X2 && i ? p.x2_px : 0u) + (ph0 ? p.x2_px : 0u);
       const int p = p0 + prow[i];
       const uint32_t va = p < P ? a_off[i] : kWgOOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(dyr, (__attribute__((address_space(3))) void*)(Ab + (32 * i + 8 * wid) * 64),

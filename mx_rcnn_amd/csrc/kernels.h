@@ -148,7 +148,8 @@ void loss_combine(const LossTerms& t, float* out, int32_t* nonfinite, hipStream_
 // grad fp32 or bf16; lr read from device pointer; optional bf16 shadow copy of w.
 void sgd_momentum(float* w, float* mom, const void* grad, int grad_bf16, int64_t n, const float* lr,
                   float momentum, float wd, float rescale, float clip, uint16_t* w_bf16, hipStream_t st,
-                  int64_t x2_plane = 0);  // x2_plane > 0: w_bf16 is an x2 hi / lo pair, lo x2_plane elements on
+                  int64_t x2_plane = 0,   // x2_plane > 0: w_bf16 is an x2 hi / lo pair, lo x2_plane elements on
+                  int x3 = 0);            // with x2_plane: an x3 triple (mid, hi, lo) x2_plane apart
 
 // ---- frozen BN + ReLU (bn_act.hip) -----------------------------------------
 // NHWC x (M rows, C channels) bf16/fp32; y = relu((x-mean)*rsqrt(var+eps)*gamma + beta).
@@ -231,7 +232,12 @@ struct ConvEpi {
   // The main loop runs three K phases (A_hi B_hi, A_hi B_lo, A_lo B_hi) with the lo planes reached
   // through plane byte offsets; the epilogue reads pairs and stores pairs (buffer kernels 22 / 23
   // and the grouped launch only)
+  // x3 (the fp32 mode, common.h): operands are (mid, hi, lo) triples with x2 = 1 and the x2_* plane
+  // offsets one plane apart; the main loops run their K range twice, first with every operand base
+  // one plane further on (products hh + hl + lh), then at the base (mm + mh + hm); the epilogues read
+  // and store triples (x2_py / x2_pd are then the plane spacings)
   int x2 = 0;
+  int x3 = 0;
   uint32_t x2_pa = 0, x2_pb = 0;  // lo-plane offsets of the A (activation) / B (filter) operands, bytes
   int64_t x2_py = 0;              // lo-plane offset of y, y2, residual and bnb_x, elements
   int64_t x2_pd = 0;              // lo-plane offset of dadd, elements
@@ -241,7 +247,7 @@ struct ConvEpi {
   // are flipped in-kernel (buffer kernels 22 / 23 and the grouped launch)
   int bt = 0;
   // ReLU (+ inverted dropout) backward fused into a data gradient: y = v * [rmask > 0] * rmask_s, where
-  // rmask (shaped like y, bf16; x2: its hi plane) is the ReLU / dropout OUTPUT of the previous layer,
+  // rmask (shaped like y, bf16; x2 / x3: its hi plane) is the ReLU / dropout OUTPUT of the previous layer,
   // i.e. this data gradient's forward input (plain epilogue only: no bnb_x / y2)
   const uint16_t* rmask = nullptr;
   float rmask_s = 1.f;
@@ -250,6 +256,10 @@ struct ConvEpi {
 float philox_uniform_host(uint32_t seed, uint64_t step, uint64_t e);
 // output rows per workgroup tile (BM) of a tile code
 int conv_tile_bm(int tile);
+// K-group kernels (conv_kg.hip), tile codes 27-29; returns the tile or -1 (unsupported)
+int conv_igemm_kg(int tile, const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho,
+                  int Wo, int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int splits, float* slab,
+                  hipStream_t st);
 // large-tile conv (conv_big.hip): tile 200 = 256x256, 201 = 256x128, 512 threads, bf16 / fp16, plain
 // epilogues (bias, residual, ReLU, frozen-BN second output); -1 when unsupported
 int conv_big_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho, int Wo,
@@ -258,7 +268,8 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
                    int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int tile, int splits, float* slab,
                    hipStream_t st);
 // ---- training-mode BatchNorm (bn_train.hip) -----------------------------------------------
-// (x2 = 1: every bf16 (M, C) operand is an x2 hi / lo pair, lo plane M * C elements on)
+// (x2 = 1 or 2: every bf16 (M, C) operand is an x2 hi / lo pair, lo plane M * C elements on; 3: an
+// x3 triple, planes M * C apart)
 // x/y/dy/dx NHWC bf16 (M rows x C), C % 64 == 0.  fwd updates the running stats in place
 // (moving = momentum * moving + (1 - momentum) * batch, unbiased var) and saves mean / invstd.
 // workspace: bn_train_workspace_floats(M, C) floats.
@@ -346,6 +357,7 @@ int conv_wgrad_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, i
 // hi ones), the gradient dwf is fp32 (dw unused)
 struct WgradX2 {
   int x2 = 0;
+  int x3 = 0;  // x3 triples (common.h): pdy / px are the plane spacings, K (pixels) runs twice
   uint32_t pdy = 0, px = 0;
   float* dwf = nullptr;
 };
@@ -388,14 +400,17 @@ struct HeadBwdArgs {
   int rs = 1;
   // fp32-class mode: X / W / dX are x2 hi / lo pairs (X's and dX's lo planes M * K on, W_h's w_plane[h]
   // on), dY is fp32 (dyf), dW fp32 (dwf); products hi*hi + hi*lo + lo*hi on the bf16 MFMA
+  // x3 (the fp32 mode): X / W / dX are (mid, hi, lo) triples, six products
   int x2 = 0;
+  int x3 = 0;
   const float* dyf[2] = {nullptr, nullptr};
   float* dwf[2] = {nullptr, nullptr};
   int64_t w_plane[2] = {0, 0};
 };
-// out = dy * [y > 0] * scale (bf16, n % 8 == 0; x2: plane = n, dy / out hold both planes)
+// out = dy * [y > 0] * scale (bf16, n % 8 == 0; planes: y is the output's hi plane, dy / out hold
+// np planes `plane` = n apart)
 void relu_mask(const uint16_t* dy, const uint16_t* y, uint16_t* out, int64_t n, int64_t plane, float scale,
-               hipStream_t st);
+               hipStream_t st, int np = 1);
 int head_bwd_splits(int M, int K, const int* N, int nheads);
 int head_bwd(const uint16_t* x, int M, int K, const HeadBwdArgs& a, hipStream_t st);
 // per-channel sum of x (M, C) (bf16 / fp16 by code) into out (C) fp32 / bf16 by out_code (+= when

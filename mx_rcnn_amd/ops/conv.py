@@ -114,19 +114,21 @@ def dgrad_args(param, w):
     if dgrad_bt_enabled():
         if x2:
             wh, wpl = precision.weight_pair(w)
-            return wh, {'x2': True, 'w_plane': wpl, 'bt': True}
+            return wh, {'x2': x2, 'w_plane': wpl, 'bt': True}
         return w.contiguous(memory_format=torch.channels_last), {'bt': True}
     wf = dgrad_weight(param, w)
     if x2:
         wh, wpl = pair_args(wf)
-        return wh, {'x2': True, 'w_plane': wpl}
+        return wh, {'x2': x2, 'w_plane': wpl}
     return wf, {}
 
 
 def pair_args(wpair):
-    """x2 mode: a filter PAIR (2O, ...) -> (hi view, plane) for the kernels' w / w_plane."""
-    n = wpair.shape[0] // 2
-    return wpair[:n], wpair.numel() // 2
+    """Multi-plane modes: a filter's planes (P*O, ...) -> (plane-0 view, plane spacing) for the
+    kernels' w / w_plane."""
+    k = precision.nplanes() or 2
+    n = wpair.shape[0] // k
+    return wpair[:n], wpair.numel() // k
 
 
 def _flip_t(w):
@@ -177,7 +179,7 @@ def strided_dgrad(dy, wf, H, W, k, s, p, residual=None, bn=None, bn_eps=2e-5, bn
     ext = need_ext()
     N, O, Ho, Wo = dy.shape
     x2 = precision.x2_enabled()
-    I = wf.shape[0] // 2 if x2 else wf.shape[0]  # x2: wf is the flipped filter's pair
+    I = wf.shape[0] // x2 if x2 else wf.shape[0]  # planes: wf is the flipped filter's planes
     dx = torch.empty((N, I, H, W), dtype=dy.dtype, device=dy.device, memory_format=torch.channels_last)
     bwd = bnb_x is not None
     row0 = 0
@@ -202,11 +204,11 @@ def strided_dgrad(dy, wf, H, W, k, s, p, residual=None, bn=None, bn_eps=2e-5, bn
             wk = {}
             if x2:
                 sub, wpl = pair_args(sub)
-                wk = dict(x2=True, w_plane=wpl)
+                wk = dict(x2=x2, w_plane=wpl)
             ext.conv_igemm_fwd(dy, sub, None, 1, -oh, False, 0, 0, residual, bn, bn_eps, bn_fix_gamma, True,
                                bnb_x, dadd, dgamma, dbeta, 0.0, 0, None, -ow, dx, [Hc, Wc, H, W, s, s, ph, pw],
                                bnb_part=bnb_part, bnb_row0=row0, **wk)
-            row0 += ((N // 2 if x2 else N) * Hc * Wc + 63) // 64
+            row0 += ((N // x2 if x2 else N) * Hc * Wc + 63) // 64
     if bwd:
         return dx, dgamma, dbeta
     return dx
@@ -319,7 +321,7 @@ class _ConvIgemm(torch.autograd.Function):
         if precision.x2_enabled():  # x: a pair, w: the fp32 parameter (its pair from the store)
             wc = w
             wh, wpl = precision.weight_pair(w)
-            y = ext.conv_igemm_fwd(x, wh, b, stride, pad, relu, x2=True, w_plane=wpl)[0]
+            y = ext.conv_igemm_fwd(x, wh, b, stride, pad, relu, x2=precision.x2_enabled(), w_plane=wpl)[0]
         else:
             wc = w.contiguous(memory_format=torch.channels_last)
             y = ext.conv_igemm_fwd(x, wc, b, stride, pad, relu)[0]
@@ -334,10 +336,9 @@ class _ConvIgemm(torch.autograd.Function):
         x, w, y = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
         if ctx.relu and precision.x2_enabled():
-            # the hi plane carries the sign (hi = RNE(v)): mask both planes by it
-            n = y.shape[0] // 2
-            m = y[:n] > 0
-            dy = dy * torch.cat([m, m], 0)
+            # the hi plane carries the sign (hi = RNE(v)): mask every plane by it
+            m = precision.hi_plane(y) > 0
+            dy = dy * torch.cat([m] * precision.nplanes(), 0)
         elif ctx.relu:
             dy = dy * (y > 0)
         dx, dw, db = conv_backward(x, w, ctx.param, dy, ctx.stride, ctx.pad, ctx.has_bias, ctx.needs_input_grad[0],

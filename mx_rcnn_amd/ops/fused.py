@@ -30,14 +30,14 @@ def _wargs(w):
     fp32 parameter ``w``; otherwise ``w`` itself."""
     if precision.x2_enabled():
         wh, wpl = precision.weight_pair(w)
-        return wh, {'x2': True, 'w_plane': wpl}
+        return wh, {'x2': precision.x2_enabled(), 'w_plane': wpl}
     return w, {}
 
 
 def _rows(t):
     """Logical rows (N*H*W) of an activation (pairs: half the tensor)."""
     n = t.numel() // t.shape[1]
-    return n // 2 if precision.x2_enabled() else n
+    return precision.logical(n)
 
 
 def _bn_args(bn):
@@ -520,7 +520,7 @@ class _FusedUnitFn(torch.autograd.Function):
             tg, tb, ret = bn_targets(bn_i)
             part, nparts = None, 0
             if train:
-                nparts = strided_dgrad_parts(bn_x.shape[0] // (2 if x2 else 1), H, W, stride)
+                nparts = strided_dgrad_parts(bn_x.shape[0] // (x2 if x2 else 1), H, W, stride)
                 part = train_part(bn_x, nparts)
             elif tg is None:  # statistics not needed: accumulate into scratch
                 C = bnps[bn_i][0].numel()

@@ -109,12 +109,12 @@ class _FCPair(torch.autograd.Function):
         ext = need_ext()
         xm = x.contiguous().view(x.shape[0], x.shape[1], 1, 1)
         xp = precision.x2_enabled()
-        M = x.shape[0] // 2 if xp else x.shape[0]
+        M = x.shape[0] // xp if xp else x.shape[0]
         ys = []
         for w, b in ((w1, b1), (w2, b2)):
             if xp:  # pairs in, fp32 predictions out
                 wh, wpl = _mat_w(w)
-                y = ext.conv_igemm_fwd(xm, wh.view(w.shape[0], w.shape[1], 1, 1), b, 1, 0, False, x2=True,
+                y = ext.conv_igemm_fwd(xm, wh.view(w.shape[0], w.shape[1], 1, 1), b, 1, 0, False, x2=precision.x2_enabled(),
                                        w_plane=wpl, out_f32=True)[0]
             else:
                 y = ext.conv_igemm_fwd(xm, w.view(w.shape[0], w.shape[1], 1, 1), b, 1, 0, False)[0]
@@ -130,7 +130,7 @@ class _FCPair(torch.autograd.Function):
         x, w1, w2 = ctx.saved_tensors
         ni = ctx.needs_input_grad
         xp = precision.x2_enabled()
-        M = x.shape[0] // 2 if xp else x.shape[0]
+        M = x.shape[0] // xp if xp else x.shape[0]
         gdt = torch.float32 if xp else x.dtype
         if dy1 is None:
             dy1 = torch.zeros((M, w1.shape[0]), dtype=gdt, device=x.device)
@@ -162,11 +162,11 @@ class _RpnHead(torch.autograd.Function):
         if precision.x2_enabled():  # pairs through the 3x3 conv, fp32 RPN predictions
             wcc = wc
             wh, wpl = precision.weight_pair(wc)
-            a = ext.conv_igemm_fwd(feat, wh, bc, 1, 1, True, x2=True, w_plane=wpl)[0]
+            a = ext.conv_igemm_fwd(feat, wh, bc, 1, 1, True, x2=precision.x2_enabled(), w_plane=wpl)[0]
             ys = []
             for w, b in ((w1, b1), (w2, b2)):
                 wh, wpl = precision.weight_pair(w)
-                ys.append(ext.conv_igemm_fwd(a, wh, b, 1, 0, False, x2=True, w_plane=wpl, out_f32=True)[0])
+                ys.append(ext.conv_igemm_fwd(a, wh, b, 1, 0, False, x2=precision.x2_enabled(), w_plane=wpl, out_f32=True)[0])
             y1, y2 = ys
         else:
             wcc = wc.contiguous(memory_format=torch.channels_last)
@@ -186,7 +186,7 @@ class _RpnHead(torch.autograd.Function):
         pc, pbc, p1, pb1, p2, pb2 = ctx.params
         N, C, H, W = a.shape
         xp = precision.x2_enabled()
-        Nl = N // 2 if xp else N  # logical images (pairs: 2N rows)
+        Nl = N // xp if xp else N  # logical images (pairs: 2N rows)
         gdt = torch.float32 if xp else a.dtype
         if dy1 is None:
             dy1 = torch.zeros((Nl, w1.shape[0], H, W), dtype=gdt, device=a.device, memory_format=torch.channels_last)

@@ -1,77 +1,152 @@
-"""fp32-class training on the bf16 MFMA ("x2" pairs).
+"""fp32 training on the bf16 matrix cores: multi-plane operands.
 
-The reference trains in fp32 end to end (MXNet's default dtype; SGD in `train_end2end.py:98-105`).
-MI355X's matrix cores run fp32 at 1/16 of the bf16 rate, so the fp32 mode keeps every MFMA
-operand as a PAIR of bf16 values, v = hi + lo with hi = RNE(v) and lo = RNE(v - hi): 16
-significant bits (relative error <= 2^-17, finer than the TF32 inputs cuDNN uses for "fp32"
-convolutions), and every product is computed as hi*hi + hi*lo + lo*hi on the bf16 MFMA with fp32
-accumulation (the dropped lo*lo term is below 2^-16 relative).  Accumulators, BN statistics,
-losses, gradients of parameters, SGD state and master weights are fp32.
+The reference trains in IEEE fp32 end to end (MXNet's default dtype; SGD in
+`train_end2end.py:98-105`).  MI355X's matrix cores run fp32 at 1/16 of the bf16 rate, so the
+fp32 modes keep every MFMA operand as bf16 PLANES and compute products on the bf16 MFMA with fp32
+accumulation:
 
-Representation (csrc/hip/common.h): an activation / gradient pair is ONE bf16 tensor of shape
-(2N, C, H, W) (or (2M, K)), the hi plane first, the lo plane N*C*H*W elements further.  A weight
-keeps its fp32 master as the module Parameter; its pair lives in the flat parameter store's
-shadow buffer (hi plane, lo plane one group further, rewritten by the SGD kernel) or in a cache
-built here for parameters outside a store.  The mode is a process-wide switch (`x2_mode`) that
-the trainer holds around forward + backward; inside it, every bf16 tensor reaching an op is a
-pair.
+* ``fp32`` (x3, three planes): v = hi + mid + lo with hi = RNE(v), mid = RNE(v - hi),
+  lo = RNE(v - hi - mid).  The split is EXACT (hi + mid + lo == v: 24 significant bits, the
+  IEEE fp32 value itself is what is stored between kernels) and a product is the six terms
+  hh + hm + mh + hl + lh + mm; the dropped ml + lm + ll are below 2^-23 relative, the size of
+  one fp32 rounding.  Memory order of the planes: (mid, hi, lo) -- csrc/hip/common.h explains
+  why (the MFMA kernels run x3 as their pair loop twice with a uniform one-plane shift).
+* ``bf16x3`` (x2, two planes): v ~ hi + lo with hi = RNE(v), lo = RNE(v - hi): 16 significant
+  bits (relative error <= 2^-17), products hi*hi + hi*lo + lo*hi -- three bf16 MFMAs.  Faster,
+  below fp32 precision.
+
+Accumulators, BN statistics, losses, parameter gradients, SGD state and master weights are fp32
+in both.
+
+Representation (csrc/hip/common.h): an activation / gradient is ONE bf16 tensor of shape
+(P*N, C, H, W) (or (P*M, K)), P = 2 or 3 planes, each plane N*C*H*W elements after the previous.
+A weight keeps its fp32 master as the module Parameter; its planes live in the flat parameter
+store's shadow buffer (one plane spacing per group, rewritten by the SGD kernel) or in a cache
+built here for parameters outside a store.  The mode is a process-wide switch (`x2_mode`, the
+plane count) that the trainer holds around forward + backward; inside it, every bf16 tensor
+reaching an op is a multi-plane tensor.
 """
 import contextlib
+import weakref
 
 import torch
 
-_STATE = {'on': False}
+_STATE = {'planes': 0}
+
+# precision names of the training entry points -> plane count of the mode (0: plain bf16 operands)
+PLANES = {'fp32': 3, 'bf16x3': 2, 'bf16': 0}
+
+
+_DEFAULT = {'name': 'fp32'}
+
+
+def set_default(name):
+    """Training precision the entry points use when none is named (the CLIs' --dtype)."""
+    if name not in PLANES:
+        raise ValueError('precision must be one of %s, not %r' % (sorted(PLANES), name))
+    _DEFAULT['name'] = name
+
+
+def default_name():
+    return _DEFAULT['name']
 
 
 def x2_enabled():
-    return _STATE['on']
+    """Plane count of the active multi-plane mode (2: bf16x3, 3: fp32), 0 when off."""
+    return _STATE['planes']
+
+
+nplanes = x2_enabled
+
+
+def x3_enabled():
+    return _STATE['planes'] == 3
 
 
 @contextlib.contextmanager
 def x2_mode(on=True):
-    prev = _STATE['on']
-    _STATE['on'] = bool(on)
+    """Run a block in a multi-plane mode: ``on`` is the plane count (2 or 3; True means 2), or
+    False / 0 for off."""
+    prev = _STATE['planes']
+    _STATE['planes'] = 0 if not on else (3 if on == 3 else 2)
     try:
         yield
     finally:
-        _STATE['on'] = prev
+        _STATE['planes'] = prev
 
 
 def is_pair(t):
-    """True for a pair tensor of the x2 mode (bf16 inside the mode)."""
-    return _STATE['on'] and torch.is_tensor(t) and t.dtype == torch.bfloat16
+    """The plane count when ``t`` is a multi-plane tensor of the active mode (bf16 inside it), else 0."""
+    p = _STATE['planes']
+    return p if (p and torch.is_tensor(t) and t.dtype == torch.bfloat16) else 0
 
 
-def split(t):
-    """fp32 tensor (N, ...) -> pair (2N, ...) bf16 in t's memory format (hi plane first)."""
+def split(t, planes=None):
+    """fp32 tensor (N, ...) -> (P*N, ...) bf16 planes in t's memory format: (hi, lo) for P = 2,
+    (mid, hi, lo) for P = 3."""
+    p = planes or _STATE['planes'] or 2
     t = t.float()
     hi = t.to(torch.bfloat16)
-    lo = (t - hi.float()).to(torch.bfloat16)
+    r = t - hi.float()
+    if p == 3:
+        mid = r.to(torch.bfloat16)
+        lo = (r - mid.float()).to(torch.bfloat16)
+        parts = [mid, hi, lo]
+    else:
+        parts = [hi, r.to(torch.bfloat16)]
     fmt = torch.channels_last if (t.dim() == 4 and t.is_contiguous(memory_format=torch.channels_last)
                                   and not t.is_contiguous()) else torch.contiguous_format
-    return torch.cat([hi, lo], 0).contiguous(memory_format=fmt)
+    return torch.cat(parts, 0).contiguous(memory_format=fmt)
 
 
-def join(p):
-    """pair (2N, ...) -> fp32 (N, ...) (hi + lo)."""
-    n = p.shape[0] // 2
-    return p[:n].float() + p[n:].float()
+def join(p, planes=None):
+    """(P*N, ...) planes -> fp32 (N, ...) (their exact sum)."""
+    k = planes or _STATE['planes'] or 2
+    n = p.shape[0] // k
+    out = p[:n].float() + p[n:2 * n].float()
+    if k == 3:
+        out = out + p[2 * n:].float()
+    return out
 
 
-def plane(p):
-    """Elements between a pair's hi and lo planes."""
-    return p.numel() // 2
+def plane(p, planes=None):
+    """Elements between consecutive planes of ``p``."""
+    return p.numel() // (planes or _STATE['planes'] or 2)
 
 
-# weight pairs: id(param) -> (param, hi view, plane)
+def logical(n, planes=None):
+    """Logical leading size of a (P*n, ...) multi-plane tensor (n itself when the mode is off)."""
+    k = _STATE['planes'] if planes is None else planes
+    return n // k if k else n
+
+
+def hi_plane(p, planes=None):
+    """View of the hi plane (the one carrying the sign): plane 0 of a pair, plane 1 of a triple."""
+    k = planes or _STATE['planes'] or 2
+    n = p.shape[0] // k
+    return p[n:2 * n] if k == 3 else p[:n]
+
+
+# weight planes: id(param) -> (weakref(param), plane-0 view, plane spacing, plane count); the
+# entries (and the cached planes below) go away with their parameter, so a later trainer's store
+# never sees an earlier one's shadows
 _WEIGHTS = {}
 _CACHE = {}
 
 
-def register_weight(param, hi_view, w_plane):
-    """The store's shadow pair of ``param``: ``hi_view`` shaped like the filter the kernels read
-    (channels_last conv filter / (out, in) matrix), its lo plane ``w_plane`` elements further."""
-    _WEIGHTS[id(param)] = (param, hi_view, int(w_plane))
+def _drop(key):
+    _WEIGHTS.pop(key, None)
+    _CACHE.pop(key, None)
+
+
+def register_weight(param, base_view, w_plane, planes=2):
+    """The store's shadow planes of ``param``: ``base_view`` (plane 0) shaped like the filter the
+    kernels read (channels_last conv filter / (out, in) matrix), the next planes ``w_plane``
+    elements further each."""
+    key = id(param)
+    if key not in _WEIGHTS and key not in _CACHE:
+        weakref.finalize(param, _drop, key)
+    _WEIGHTS[key] = (weakref.ref(param), base_view, int(w_plane), int(planes))
 
 
 def clear_weights():
@@ -79,21 +154,29 @@ def clear_weights():
     _CACHE.clear()
 
 
+def forget_weight(param):
+    """Drop the cached planes of ``param`` (its data was rewritten without a version bump)."""
+    _CACHE.pop(id(param), None)
+
+
 def weight_pair(w):
-    """-> (hi view, plane) of weight ``w`` (an fp32 Parameter / tensor).  Store-managed weights
-    use the SGD-maintained shadow; anything else gets a cached pair rebuilt when the tensor's
-    version counter moves."""
+    """-> (plane-0 view, plane spacing) of weight ``w`` (an fp32 Parameter / tensor) in the active
+    mode.  Store-managed weights use the SGD-maintained shadow; anything else gets cached planes
+    rebuilt when the tensor's version counter moves."""
+    p = _STATE['planes'] or 2
     ent = _WEIGHTS.get(id(w))
-    if ent is not None and ent[0] is w:
+    if ent is not None and ent[0]() is w and ent[3] == p:
         return ent[1], ent[2]
     key = id(w)
-    ver = (w.data_ptr(), w._version, tuple(w.shape))
+    ver = (w.data_ptr(), w._version, tuple(w.shape), p)
     hit = _CACHE.get(key)
-    if hit is None or hit[0] != ver or hit[1] is not w:
+    if hit is None or hit[0] != ver or hit[1]() is not w:
         fmt = torch.channels_last if w.dim() == 4 else torch.contiguous_format
         wf = w.detach().float().contiguous(memory_format=fmt)
-        pr = split(wf) if w.dim() == 4 else split(wf)
+        pr = split(wf, p)
         n = w.shape[0]
-        hit = (ver, w, pr[:n], pr.numel() // 2, pr)
+        if key not in _WEIGHTS and key not in _CACHE:
+            weakref.finalize(w, _drop, key)
+        hit = (ver, weakref.ref(w), pr[:n], pr.numel() // p, pr)
         _CACHE[key] = hit
     return hit[2], hit[3]

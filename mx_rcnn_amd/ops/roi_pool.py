@@ -66,7 +66,7 @@ class _RoIPool(torch.autograd.Function):
         rois = rois.float().contiguous()
         ctx.x2 = x2 = precision.is_pair(feat)
         if x2:
-            B = B // 2  # (2B, C, H, W) pair
+            B = B // x2  # (P*B, C, H, W) planes
         if feat.is_cuda:
             ext = need_ext()
             out, arg = ext.roi_pool_fwd(feat.contiguous(memory_format=torch.channels_last), rois, PH, PW, float(scale),

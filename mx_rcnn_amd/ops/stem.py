@@ -26,12 +26,19 @@ _PACKED = {}
 
 
 def _packed_filter(w, dtype):
-    """dtype torch.float32: the fp32-class mode's (128, KP) bf16 pair of the packed filter."""
-    key = (id(w), dtype)
+    """dtype torch.float32 (the multi-plane modes): the packed filter's bf16 planes in the kernel's
+    LOGICAL order -- (128, KP) = (hi, lo) for bf16x3, (192, KP) = (hi, mid, lo) for fp32."""
+    planes = precision.nplanes() if dtype == torch.float32 else 0
+    key = (id(w), dtype, planes)
     ver = (w.data_ptr(), w._version, tuple(w.shape))
     hit = _PACKED.get(key)
     if hit is None or hit[0] != ver:
-        pf = precision.split(pack_filter(w, torch.float32)) if dtype == torch.float32 else pack_filter(w, dtype)
+        if dtype == torch.float32:
+            pf = precision.split(pack_filter(w, torch.float32), planes or 2)
+            if planes == 3:  # memory order (mid, hi, lo) -> logical (hi, mid, lo)
+                pf = torch.cat([pf[64:128], pf[:64], pf[128:]], 0).contiguous()
+        else:
+            pf = pack_filter(w, dtype)
         hit = (ver, pf)
         _PACKED[key] = hit
     return hit[1]

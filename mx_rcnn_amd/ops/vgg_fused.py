@@ -34,7 +34,7 @@ def _wargs(w, shape4=None):
     shape4 = tuple(w.shape) if shape4 is None else shape4
     if precision.x2_enabled():
         wh, wpl = precision.weight_pair(w)
-        return wh.reshape(shape4), {'x2': True, 'w_plane': wpl}
+        return wh.reshape(shape4), {'x2': precision.x2_enabled(), 'w_plane': wpl}
     return _cl(w.reshape(shape4)), {}
 
 
@@ -166,7 +166,7 @@ class _VGGHead(torch.autograd.Function):
     def forward(ctx, x, p, seeds, step, w6, b6, w7, b7, wc, bc, wb, bb):
         ext = need_ext()
         x2 = precision.x2_enabled()
-        R = x.shape[0] // 2 if x2 else x.shape[0]
+        R = x.shape[0] // x2 if x2 else x.shape[0]
 
         def fc(inp, w, b, relu, seed, out_f32=False):
             wk, kw = _wargs(w, (w.shape[0], w.shape[1], 1, 1))
@@ -192,7 +192,7 @@ class _VGGHead(torch.autograd.Function):
         ni = ctx.needs_input_grad  # (x, p, seeds, step, w6, b6, w7, b7, wc, bc, wb, bb)
         x2 = precision.x2_enabled()
         pw6, pb6, pw7, pb7, pwc, pbc, pwb, pbb = ctx.params
-        R = y7.shape[0] // 2 if x2 else y7.shape[0]
+        R = y7.shape[0] // x2 if x2 else y7.shape[0]
         gdt = torch.float32 if x2 else y7.dtype
         if dsc is None:
             dsc = torch.zeros((R, wc.shape[0]), dtype=gdt, device=y7.device)

@@ -48,15 +48,43 @@ def device_ids(spec):
     return ids or [0]
 
 
+def visible_mask():
+    """The device list a scheduler already restricted this job to (``HIP_VISIBLE_DEVICES``, else
+    ``CUDA_VISIBLE_DEVICES`` / ``ROCR_VISIBLE_DEVICES``), or None when every device is visible."""
+    for var in ('HIP_VISIBLE_DEVICES', 'CUDA_VISIBLE_DEVICES', 'ROCR_VISIBLE_DEVICES'):
+        v = os.environ.get(var)
+        if v is not None and v.strip() != '':
+            return [t.strip() for t in v.split(',') if t.strip() != '']
+    return None
+
+
+def map_devices(ids, mask=None):
+    """``--gpus`` ids index the devices this job can see, like the reference's ``mx.gpu(i)``: with
+    a visibility mask already set (e.g. HIP_VISIBLE_DEVICES=4,5,6,7 from a scheduler), id i is
+    the mask's i-th entry, so ``--gpus 2,3`` runs on physical devices 6 and 7.  An id outside the
+    mask is an error."""
+    mask = visible_mask() if mask is None else mask
+    if mask is None:
+        return [str(i) for i in ids]
+    bad = [i for i in ids if i < 0 or i >= len(mask)]
+    if bad:
+        raise SystemExit('--gpus %s: device(s) %s outside the %d visible device(s) %s' % (
+            ','.join(str(i) for i in ids), bad, len(mask), ','.join(mask)))
+    return [mask[i] for i in ids]
+
+
 def select_devices(spec):
-    """Make this job run on the devices ``spec`` names.  More than one: returns the
-    ``HIP_VISIBLE_DEVICES`` list for the rank children (rank r uses visible device r).  One:
-    restricts THIS process to it (before anything touches the GPU) and returns None."""
+    """Make this job run on the devices ``spec`` names (indices into the visible devices, see
+    :func:`map_devices`).  More than one: returns the ``HIP_VISIBLE_DEVICES`` list for the rank
+    children (rank r uses visible device r).  One: restricts THIS process to it (before anything
+    touches the GPU) and returns None."""
     ids = device_ids(spec)
-    vis = ','.join(str(i) for i in ids)
+    if launched_rank():
+        return None  # the launcher placed this rank already
+    vis = ','.join(map_devices(ids))
     if len(ids) > 1:
         return vis
-    if ids != [0] and not launched_rank():
+    if ids != [0] or visible_mask() is not None:
         os.environ['HIP_VISIBLE_DEVICES'] = vis
     return None
 

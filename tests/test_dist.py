@@ -368,6 +368,25 @@ def test_gpus_names_devices_like_the_reference(monkeypatch):
     assert os.environ['HIP_VISIBLE_DEVICES'] == '3'
 
 
+def test_gpus_index_an_existing_visibility_mask(monkeypatch):
+    """under a scheduler's HIP_VISIBLE_DEVICES=4,5,6,7, '--gpus 2,3' means the 3rd and
+    4th VISIBLE devices (physical 6, 7), like mx.gpu(i); an id past the mask is an error."""
+    import pytest as _pt
+    from mx_rcnn_amd.parallel import spawn
+    for k in ('RANK', 'WORLD_SIZE', 'CUDA_VISIBLE_DEVICES', 'ROCR_VISIBLE_DEVICES'):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv('HIP_VISIBLE_DEVICES', '4,5,6,7')
+    assert spawn.select_devices('2,3') == '6,7'
+    assert spawn.select_devices('0') is None and os.environ['HIP_VISIBLE_DEVICES'] == '4'
+    monkeypatch.setenv('HIP_VISIBLE_DEVICES', '4,5,6,7')
+    with _pt.raises(SystemExit):
+        spawn.select_devices('1,5')
+    # a launched rank is placed by its launcher: nothing changes
+    monkeypatch.setenv('RANK', '0')
+    monkeypatch.setenv('WORLD_SIZE', '2')
+    assert spawn.select_devices('2,3') is None and os.environ['HIP_VISIBLE_DEVICES'] == '4,5,6,7'
+
+
 def test_capture_sync_key_ignores_uneven_slices():
     """an uneven work_load_list gives ranks different batch sizes; the cross-rank
     capture check must compare only the slice-independent dims (module.sync_key)."""

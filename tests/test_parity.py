@@ -173,25 +173,51 @@ def _check_grads_tight(gc, gg, cos_min=0.99, rel_max=0.02, min_layers=10):
     assert len(worst) >= min_layers
 
 
-def test_rpn_step_fp32_gpu_matches_fp32_cpu(cuda):
-    """The fp32-class GPU mode (bf16 x2 pairs, three MFMAs per product, fp32 accumulation) against
-    the fp32 CPU step: every layer's gradient cosine >= 0.99 (the bf16 mode's deep layers fall to a
-    median of ~0.9 here)."""
-    cpu, gpu = _pair('rpn', cuda, 'fp32')
+# (precision, loss tolerance, per-layer cosine floor, per-layer norm error, median cosine floor)
+# fp32: exact fp32 triples, six products -- the reference's precision; bf16x3: 16-bit pairs.
+# The R-CNN step's per-layer floor is looser than its median: a ReLU whose pre-activation lies
+# within rounding of zero flips between ANY two fp32 summation orders of this random-init network,
+# which moves a few deep BN betas' directions (see _check_grads_tight).
+RPN_TIGHT = {'fp32': (1e-4, 0.9999, 0.002, 0.99999), 'bf16x3': (1e-3, 0.99, 0.02, 0.999)}
+RCNN_TIGHT = {'fp32': (1e-4, 0.995, 0.005, 0.9999), 'bf16x3': (1e-3, 0.99, 0.02, 0.99)}
+
+
+def _median_cos(gc, gg):
+    norms = {n: float(v.norm()) for n, v in gc.items()}
+    big = max(norms.values())
+    cs = sorted(float(torch.dot(v, gg[n]) / (v.norm() * gg[n].norm() + 1e-30))
+                for n, v in gc.items() if norms[n] >= 1e-3 * big)
+    return cs[len(cs) // 2]
+
+
+@pytest.mark.parametrize('prec', ['fp32', 'bf16x3'])
+def test_rpn_step_fp32_gpu_matches_fp32_cpu(cuda, prec):
+    """The multi-plane GPU modes against the fp32 CPU step (the bf16 mode's deep layers fall to a
+    median cosine of ~0.9 here)."""
+    loss_tol, cos_min, rel_max, med_min = RPN_TIGHT[prec]
+    cpu, gpu = _pair('rpn', cuda, prec)
     b, _ = _image()
     oc, gc = _fwd_bwd(cpu, b)
     og, gg = _fwd_bwd(gpu, b)
     assert torch.equal(og['rpn_label'].cpu(), oc['rpn_label'])
     for k in ('rpn_cls_loss', 'rpn_bbox_loss'):
-        assert _rel(og[k].float().cpu().sum(), oc[k].float().sum()) <= 1e-3, (k, og[k], oc[k])
-    _check_grads_tight(gc, gg)
+        assert _rel(og[k].float().cpu().sum(), oc[k].float().sum()) <= loss_tol, (k, og[k], oc[k])
+    _check_grads_tight(gc, gg, cos_min, rel_max)
+    med = _median_cos(gc, gg)
+    print('%s rpn: median cosine %.7f' % (prec, med))
+    assert med >= med_min
 
 
-def test_rcnn_step_fp32_gpu_matches_fp32_cpu(cuda):
-    cpu, gpu = _pair('rcnn', cuda, 'fp32')
+@pytest.mark.parametrize('prec', ['fp32', 'bf16x3'])
+def test_rcnn_step_fp32_gpu_matches_fp32_cpu(cuda, prec):
+    loss_tol, cos_min, rel_max, med_min = RCNN_TIGHT[prec]
+    cpu, gpu = _pair('rcnn', cuda, prec)
     b = _rcnn_batch()
     oc, gc = _fwd_bwd(cpu, b)
     og, gg = _fwd_bwd(gpu, b)
     for k in ('cls_loss', 'bbox_loss'):
-        assert _rel(og[k].float().cpu().sum(), oc[k].float().sum()) <= 1e-3, (k, og[k], oc[k])
-    _check_grads_tight(gc, gg)
+        assert _rel(og[k].float().cpu().sum(), oc[k].float().sum()) <= loss_tol, (k, og[k], oc[k])
+    _check_grads_tight(gc, gg, cos_min, rel_max)
+    med = _median_cos(gc, gg)
+    print('%s rcnn: median cosine %.7f' % (prec, med))
+    assert med >= med_min

@@ -908,7 +908,7 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
     snprintf(kb, sizeof(kb), "%d,%d,%d,%d,%d,%d,%d,%d,%d|%d%d%d%d%d%d%d%d%d%d", NB, H, W, Cin, Cout, KH, KW, (int)stride,
              (int)pad, ep.residual != nullptr, ep.y2 != nullptr || bn.has_value(), bwd_mode, ep.dadd != nullptr,
              ep.relu, ep.bias != nullptr || ep.bias_h != nullptr, (ep.drop_p > 0.f ? 1 : 0) + (stats ? 2 : 0), ep.bt,
-             ep.rmask != nullptr, ep.x2);
+             ep.rmask != nullptr, ep.x2 + ep.x3);
     const std::string key(kb);
     std::unique_lock<std::mutex> lk(g_tune_mu);
     auto it = g_tune.find(key);

@@ -31,6 +31,10 @@ def _torch_paths():
 
 
 def ext_path():
+    """The in-tree extension, or MXR_EXT_OUT when set (a staging path: link elsewhere while the
+    in-tree .so is in use, then copy it in)."""
+    if os.environ.get('MXR_EXT_OUT'):
+        return os.environ['MXR_EXT_OUT']
     suffix = sysconfig.get_config_var('EXT_SUFFIX') or '.so'
     return os.path.join(PKG, '_C' + suffix)
 

@@ -408,14 +408,14 @@ conv_igemm_glds_kernel(const uint16_t* __restrict__ x, const uint16_t* __restric
   igemm_epilogue<TM, TN, WM, WN>(acc, m0, n0, wm, wn, lane, M, Cout, ep, y, split, splits, slab);
 }
 
-template <int BM, int BN, int S, bool F16 = false, bool X2 = false, bool BT = false>
+template <int BM, int BN, int S, bool F16 = false, bool X2 = false, bool BT = false, bool X3 = false>
 __global__ void __launch_bounds__(256)
 conv_igemm_buf_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
                       int NB, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad,
                       const ConvEpi ep, int tiles_n, int nwg, int ntiles, int splits, float* __restrict__ slab) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[S * (BM + BN) * BK];
-  igemm_buf_body<BM, BN, S, F16, X2, BT>(lds, blockIdx.x, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep,
-                                         tiles_n, nwg, ntiles, splits, slab);
+  __shared__ __attribute__((aligned(16))) uint16_t lds[S * igemm_ring_stage<BM, BN, BT, X3>()];
+  igemm_buf_body<BM, BN, S, F16, X2, BT, 1, X3>(lds, blockIdx.x, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
+                                                pad, ep, tiles_n, nwg, ntiles, splits, slab);
 }
 
 // ---- fp32-class pairs, wide stages (tile code 26) ---------------------------------------------
@@ -980,12 +980,15 @@ static void launch_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB
             x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, tiles_n, nwg, ntiles, splits, slab);
     } else if (ep.x2 || ep.bt) {
       if constexpr (S == 3 && BN == 64 && (BM == 64 || BM == 128)) {
-#define MXR_BUF_LAUNCH(X, B)                                                                                        \
-  conv_igemm_buf_kernel<BM, BN, S, false, X, B><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, \
-                                                                     stride, pad, ep, tiles_n, nwg, ntiles, splits, slab)
-        if (ep.x2 && ep.bt) MXR_BUF_LAUNCH(true, true);
-        else if (ep.x2) MXR_BUF_LAUNCH(true, false);
-        else MXR_BUF_LAUNCH(false, true);
+#define MXR_BUF_LAUNCH(X, B, X3_)                                                                                  \
+  conv_igemm_buf_kernel<BM, BN, S, false, X, B, X3_><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, \
+                                                                          KW, stride, pad, ep, tiles_n, nwg, ntiles,  \
+                                                                          splits, slab)
+        if (ep.x3 && ep.bt) MXR_BUF_LAUNCH(true, true, true);  // fp32 triples: the fused one-pass form
+        else if (ep.x3) MXR_BUF_LAUNCH(true, false, true);
+        else if (ep.x2 && ep.bt) MXR_BUF_LAUNCH(true, true, false);
+        else if (ep.x2) MXR_BUF_LAUNCH(true, false, false);
+        else MXR_BUF_LAUNCH(false, true, false);
 #undef MXR_BUF_LAUNCH
       }
     } else
@@ -1094,8 +1097,8 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
   if (ep.x2 || ep.yf || ep.bt) {
     // pairs / fp32 outputs / filter read transposed: the buffer kernels (x2 also at depth 4 and
     // 128x128, A/B tiles 21 / 32 / 33)
-    const bool x2_ok = !ep.bt && (tile == 21 || tile == 32 || tile == 33);
-    if (!(tile == 22 || tile == 23 || x2_ok || kgt)) tile = 23;
+    const bool x2_ok = !ep.bt && !ep.x3 && (tile == 21 || tile == 32 || tile == 33);
+    if (!(tile == 22 || tile == 23 || x2_ok || (kgt && !ep.x3))) tile = 23;  // x3: the fused 22 / 23
     if ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB || (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kBufOOB ||
         KH * KW > 64 || ep.f16)
       return -1;
@@ -1200,25 +1203,30 @@ void conv_wt_flip_multi(const WtFlipEntry* entries, int n_entries, int total_til
 // Replaces the two-stream schedule (wgrad on a side stream, one cross-queue wait per wgrad and a
 // join per unit): every cross-queue edge of a replayed graph cost ~10 us of idle time, four per
 // unit (profiles/r2_resnet101_stage3_unit_timeline.txt).
-template <int S, bool X2 = false, bool BT = false>
-__global__ void __launch_bounds__(256)
+//
+// KG > 1: both roles in their K-group form (4*KG waves per workgroup, each group of four over a
+// contiguous slice of the role's reduction through its own sub-ring, partial tiles summed in the
+// LDS epilogue; the reduce role covers 4 * 256 * KG elements per workgroup).
+template <int S, bool X2 = false, bool BT = false, int KG = 1, bool X3 = false>
+__global__ void __launch_bounds__(256 * KG)
 conv_dgrad_wgrad_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
                         int NB, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int pad,
                         const ConvEpi ep, int tiles_n, int nwg_d, int ntiles, WgradParams wp, WgradReduceParams rp) {
-  // both roles run an S-deep ring over the same LDS: S * (64 + 64) * 64 bf16 (48 KB at S = 3)
-  static_assert(S * (64 + 64) * BK == S * 2 * WG_BK * 64, "both roles use the same ring");
-  __shared__ __attribute__((aligned(16))) uint16_t lds[S * (64 + 64) * BK];
+  // both roles run an S-deep ring over the same LDS: S * (64 + 64) * 64 bf16 (48 KB at S = 3) per
+  // group, plus the lo tiles of the fused fp32 form (72 KB at S = 3)
+  static_assert(igemm_ring_stage<64, 64, BT, X3>() == wgrad_ring_stage<X3>(), "both roles use the same ring");
+  __shared__ __attribute__((aligned(16))) uint16_t lds[S * KG * igemm_ring_stage<64, 64, BT, X3>()];
   // roles: [0, rp.nwg) the previous grouped launch's deferred split-K reduce (short, dispatched
   // first; rp.nwg is a multiple of 8 so the dgrad role keeps its XCD-aware tile order), then the
   // data gradient, then the weight gradient
   const int b = (int)blockIdx.x;
   if (b < rp.nwg) {
-    wgrad_reduce_body(b, rp.slab, rp.splits, rp.n, rp.dw, rp.accumulate, rp.dwf);
+    wgrad_reduce_body(b, rp.slab, rp.splits, rp.n, rp.dw, rp.accumulate, rp.dwf, 256 * KG);
   } else if (b < rp.nwg + nwg_d) {
-    igemm_buf_body<64, 64, S, false, X2, BT>(lds, b - rp.nwg, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, 1, pad, ep,
-                                             tiles_n, nwg_d, ntiles, 1, nullptr);
+    igemm_buf_body<64, 64, S, false, X2, BT, KG, X3>(lds, b - rp.nwg, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, 1,
+                                                     pad, ep, tiles_n, nwg_d, ntiles, 1, nullptr);
   } else {
-    wgrad_buf_body<S, X2>(lds, b - rp.nwg - nwg_d, wp);
+    wgrad_buf_body<S, X2, KG, X3>(lds, b - rp.nwg - nwg_d, wp);
   }
 }
 
@@ -1256,17 +1264,44 @@ int conv_dgrad_wgrad(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, 
     rp.n = prev_n;
     rp.splits = prev_splits;
     rp.accumulate = 1;
-    rp.nwg = (int)((div_up(prev_n / 4, 256) + 7) / 8 * 8);
   }
   static const int depth = [] {  // A/B knob MXR_GROUPED_S: ring depth of both roles (3: 48 KB, 4: 64 KB)
     const char* e = getenv("MXR_GROUPED_S");
     return e != nullptr && e[0] == '4' ? 4 : 3;
   }();
+  // K groups of both roles (data gradients read the forward filter, bt): MXR_GROUPED_KG = 1 | 2 |
+  // 22 (two groups at ring depth 2, 64 KB: two workgroups per CU); default 2 in the fp32 (x3) mode,
+  // whose reductions run twice as long, else 1
+  static const int kg_env = [] {
+    const char* e = getenv("MXR_GROUPED_KG");
+    return e != nullptr ? atoi(e) : -1;
+  }();
+  const int kg = !ep.bt || ep.x3 ? 1 : (kg_env >= 0 ? kg_env : 1);  // (measured: no gain at S = 2, -17 % at S = 3)
+  const int nt = kg > 1 ? 512 : 256;
+  if (prev_slab != nullptr) rp.nwg = (int)((div_up(prev_n / 4, nt) + 7) / 8 * 8);
   const int nwg_all = rp.nwg + ntiles + wp.nwg;
-#define MXR_GROUPED(S_, X, B) \
-  conv_dgrad_wgrad_kernel<S_, X, B><<<nwg_all, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, pad, ep, \
+  if (kg == 2 || kg == 22) {
+#define MXR_GROUPED_KG(S_, X) \
+  conv_dgrad_wgrad_kernel<S_, X, true, 2><<<nwg_all, 512, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, pad, \
+                                                                   ep, tiles_n, ntiles, ntiles, wp, rp)
+    if (kg == 22) {
+      if (wx2.x2) MXR_GROUPED_KG(2, true);
+      else MXR_GROUPED_KG(2, false);
+    } else {
+      if (wx2.x2) MXR_GROUPED_KG(3, true);
+      else MXR_GROUPED_KG(3, false);
+    }
+#undef MXR_GROUPED_KG
+    if (wg_splits > 1 && !defer_reduce)
+      wgrad_reduce(slab, wg_splits, (int64_t)wg_Cout * wg_KH * wg_KW * wg_Cin, dw, accumulate, st, wx2.dwf);
+    return 0;
+  }
+#define MXR_GROUPED(S_, X, B, ...) \
+  conv_dgrad_wgrad_kernel<S_, X, B, ##__VA_ARGS__><<<nwg_all, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, pad, ep, \
                                                             tiles_n, ntiles, ntiles, wp, rp)
-  if (wx2.x2 && ep.bt) MXR_GROUPED(3, true, true);
+  if (wx2.x3 && ep.bt) MXR_GROUPED(3, true, true, 1, true);  // fp32 triples: the fused one-pass form
+  else if (wx2.x3) MXR_GROUPED(3, true, false, 1, true);
+  else if (wx2.x2 && ep.bt) MXR_GROUPED(3, true, true);
   else if (wx2.x2) MXR_GROUPED(3, true, false);
   else if (ep.bt) MXR_GROUPED(3, false, true);
 #undef MXR_GROUPED

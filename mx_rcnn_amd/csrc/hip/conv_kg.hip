@@ -45,7 +45,7 @@ static void launch_kg(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB,
 int conv_igemm_kg(int tile, const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho,
                   int Wo, int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int splits, float* slab,
                   hipStream_t st) {
-  if (ep.f16 || Cout % 8 != 0 || Cin % BK != 0 || KH * KW > 64) return -1;
+  if (ep.f16 || ep.x3 || Cout % 8 != 0 || Cin % BK != 0 || KH * KW > 64) return -1;  // (x3: tiles 22 / 23)
   switch (tile) {
     case 27: launch_kg<3, 2>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 28: launch_kg<2, 2>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;

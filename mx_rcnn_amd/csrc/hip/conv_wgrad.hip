@@ -135,10 +135,10 @@ conv_wgrad_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ 
       }
 }
 
-template <int S, bool X2 = false>
+template <int S, bool X2 = false, bool X3 = false>
 __global__ void __launch_bounds__(256) conv_wgrad_buf_kernel(WgradParams p) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[S * 2 * WG_BK * 64];  // [S][dY|X][64 px][64 ch]
-  wgrad_buf_body<S, X2>(lds, blockIdx.x, p);
+  __shared__ __attribute__((aligned(16))) uint16_t lds[S * wgrad_ring_stage<X3>()];  // [S][dY|X][64 px][64 ch] (+ lo)
+  wgrad_buf_body<S, X2, 1, X3>(lds, blockIdx.x, p);
 }
 
 __global__ void __launch_bounds__(256)
@@ -212,7 +212,9 @@ int conv_wgrad(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab,
     p.x2_pdy = x2.pdy;
     p.x2_px = x2.px;
     p.dwf = x2.dwf;
-    if (p.x2)
+    if (p.x3)
+      conv_wgrad_buf_kernel<3, true, true><<<ntiles * splits, 256, 0, st>>>(p);  // fp32 triples: fused one pass
+    else if (p.x2)
       conv_wgrad_buf_kernel<3, true><<<ntiles * splits, 256, 0, st>>>(p);
     else
       conv_wgrad_buf_kernel<3><<<ntiles * splits, 256, 0, st>>>(p);

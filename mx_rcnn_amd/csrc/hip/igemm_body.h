@@ -524,7 +524,19 @@ __device__ __forceinline__ void buf_lds16(__amdgpu_buffer_rsrc_t rs, void* lds_w
 // MFMA chain of a small tile: what bounds a batch-1 stage-3 conv at one tile per CU) carries KG
 // stages, and 2*KG waves per CU overlap one group's MFMA chain with another's fragment reads.  The
 // partial tiles meet in the LDS epilogue (igemm_epilogue_lds, summed in group order).
-template <int BM, int BN, int S, bool F16 = false, bool X2 = false, bool BT = false, int KG = 1>
+//
+// X3 (the fp32 mode's fused form, X2 = true as well): ONE pass over K with all three planes per
+// stage -- the main tiles keep 128-B rows of 32 channels [hi | mid] (chunks 0-3 / 4-7), and a lo
+// tile per operand holds the lo plane of the same channels: 64-B rows (swizzle chunk ^ ((row >> 2)
+// & 3), conflict-free for 16-row fragment reads) for row-major operands, or for the k-major B of BT
+// 32 k-rows laid out like the main tile's first half.  Six MFMAs per fragment set (hh, hm, mh, mm,
+// hl, lh): 3/4 of the two-phase form's bytes and half its barriers.
+template <int BM, int BN, bool BT, bool X3>
+constexpr int igemm_ring_stage() {  // LDS elements of one ring stage
+  return (BM + BN) * 64 + (X3 ? BM * 32 + (BT ? 32 * 64 : BN * 32) : 0);
+}
+
+template <int BM, int BN, int S, bool F16 = false, bool X2 = false, bool BT = false, int KG = 1, bool X3 = false>
 __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uint16_t* __restrict__ x,
                                                const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int NB, int H,
                                                int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride,
@@ -533,12 +545,17 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int ACH = BM / 32, BCH = BN / 32;
-  constexpr int LPS = ACH + BCH;
+  constexpr int ACL = X3 ? BM / 64 : 0, BCL = X3 ? (BT ? 1 : BN / 64) : 0;  // lo-tile loads per thread
+  constexpr int LPS = ACH + BCH + ACL + BCL;
   static_assert(S >= 2 && S <= 8, "pipeline depth");
   static_assert(KG == 1 || (!F16 && BN == 64), "K groups: bf16 / multi-plane 64-column tiles");
+  static_assert(!X3 || (X2 && !F16 && BM % 64 == 0 && BN % 64 == 0), "X3: multi-plane 64-multiple tiles");
+  constexpr int LBM = X3 ? BM * 32 : 0, LBN = X3 ? (BT ? 32 * 64 : BN * 32) : 0;  // lo tiles per stage
   const int kgi = KG > 1 ? (int)(threadIdx.x >> 8) : 0;  // this wave's K group
-  uint16_t* As = lds + kgi * S * (BM + BN) * BK;        // the group's sub-ring
+  uint16_t* As = lds + kgi * S * igemm_ring_stage<BM, BN, BT, X3>();  // the group's sub-ring
   uint16_t* Bs = As + S * BM * BK;
+  uint16_t* Al = Bs + S * BN * BK;  // X3 lo tiles
+  uint16_t* Bl = Al + S * LBM;
 
   const int q = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
   const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + bid / 8;
@@ -562,7 +579,9 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
   const int slot = lane & 7;
   // logical chunk lc of a row: channels lc*8 (16-bit), or (X2) channels (lc&3)*8 of plane lc>>2
   auto chan_bytes = [&](int lc) { return X2 ? (lc & 3) * 16 : lc * 16; };
-  auto plane_a = [&](int lc) { return X2 && lc >= 4 ? ep.x2_pa : 0u; };
+  // (x2: chunks 4-7 are the lo plane, one plane on; X3: chunks 0-3 the hi plane = memory plane 1,
+  // chunks 4-7 the mid plane = memory plane 0)
+  auto plane_a = [&](int lc) { return X3 ? (lc < 4 ? ep.x2_pa : 0u) : (X2 && lc >= 4 ? ep.x2_pa : 0u); };
   uint32_t a_off[ACH];
   uint64_t a_mask[ACH];
 #pragma unroll
@@ -591,19 +610,56 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
     if constexpr (BT) {  // row = k within the stage (x2: rows 32.. are the lo plane of the same channels)
       const int n = n0 + (slot ^ wsw(row)) * 8;
       const int crow = X2 ? (row & 31) : row;
-      b_off[i] = n < Cout ? (uint32_t)(((int64_t)crow * taps * Cout + n) * 2) + (X2 && row >= 32 ? ep.x2_pb : 0u)
-                          : kBufOOB;
+      const uint32_t pl = X3 ? (row < 32 ? ep.x2_pb : 0u) : (X2 && row >= 32 ? ep.x2_pb : 0u);
+      b_off[i] = n < Cout ? (uint32_t)(((int64_t)crow * taps * Cout + n) * 2) + pl : kBufOOB;
     } else {
       const int co = n0 + row;
       const int lc = slot ^ ((row >> 1) & 7);
-      b_off[i] = co < Cout ? (uint32_t)((int64_t)co * K * 2 + chan_bytes(lc)) + (X2 && lc >= 4 ? ep.x2_pb : 0u)
-                           : kBufOOB;
+      const uint32_t pl = X3 ? (lc < 4 ? ep.x2_pb : 0u) : (X2 && lc >= 4 ? ep.x2_pb : 0u);
+      b_off[i] = co < Cout ? (uint32_t)((int64_t)co * K * 2 + chan_bytes(lc)) + pl : kBufOOB;
+    }
+  }
+  // X3 lo tiles: A (and non-BT B) as 64-B rows of 32 channels, lane -> (row 16 * wave + lane / 4,
+  // chunk lane & 3 holding logical chunk (lane & 3) ^ ((row >> 2) & 3)); the BT B lo tile as 32
+  // k-rows of 64 outputs like the main B tile's first half
+  uint32_t al_off[ACL > 0 ? ACL : 1], bl_off[BCL > 0 ? BCL : 1];
+  uint64_t al_mask[ACL > 0 ? ACL : 1];
+  if constexpr (X3) {
+#pragma unroll
+    for (int i = 0; i < ACL; ++i) {
+      const int row = 64 * i + 16 * wid + (lane >> 2);
+      const int lc = (lane & 3) ^ ((row >> 2) & 3);
+      const int m = m0 + row;
+      al_off[i] = 0;
+      al_mask[i] = 0;
+      if (m < M) {
+        const int img = m / (Ho * Wo), rem = m % (Ho * Wo);
+        const int hi0 = (rem / Wo) * stride - pad, wi0 = (rem % Wo) * stride - (ep.pad_w >= 0 ? ep.pad_w : pad);
+        al_off[i] = (uint32_t)((((int64_t)img * H + hi0) * W + wi0) * Cin * 2 + lc * 16) + 2 * ep.x2_pa;
+        for (int fr = 0; fr < KH; ++fr)
+          for (int fc = 0; fc < KW; ++fc)
+            if ((unsigned)(hi0 + fr) < (unsigned)H && (unsigned)(wi0 + fc) < (unsigned)W)
+              al_mask[i] |= 1ull << (fr * KW + fc);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < BCL; ++i) {
+      if constexpr (BT) {
+        const int row = 8 * wid + (lane >> 3);
+        const int n = n0 + (slot ^ wsw(row)) * 8;
+        bl_off[i] = n < Cout ? (uint32_t)(((int64_t)row * taps * Cout + n) * 2) + 2 * ep.x2_pb : kBufOOB;
+      } else {
+        const int row = 64 * i + 16 * wid + (lane >> 2);
+        const int lc = (lane & 3) ^ ((row >> 2) & 3);
+        const int co = n0 + row;
+        bl_off[i] = co < Cout ? (uint32_t)((int64_t)co * K * 2 + lc * 16) + 2 * ep.x2_pb : kBufOOB;
+      }
     }
   }
   constexpr int KC = X2 ? BK / 2 : BK;  // channels per stage (x2: 32 of each plane)
   const int cin_steps = Cin / KC;
   const int nk1 = KH * KW * cin_steps;              // K steps of one pass
-  const int nk_all = X2 && ep.x3 ? 2 * nk1 : nk1;   // x3: phase (hi, lo), then phase (mid, hi)
+  const int nk_all = X2 && !X3 && ep.x3 ? 2 * nk1 : nk1;  // two-phase x3: (hi, lo), then (mid, hi)
   const int per = (nk_all + splits - 1) / splits;
   const int ks0 = split * per;
   const int nk_sp = max(0, min(nk_all, ks0 + per) - ks0);  // this split's K steps
@@ -622,7 +678,7 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
     // the buffer range check sees only the VGPR offset, so the tap shift (which can turn a
     // negative padding-row offset into a valid one) goes there; the channel block is the SGPR part.
     // x3 phase 0 reads every operand one plane further on (common.h: planes 1 / 2 = hi / lo)
-    const bool sh = X2 && ep.x3 && c_ph == 0;
+    const bool sh = X2 && !X3 && ep.x3 && c_ph == 0;
     const uint32_t tap_a = (uint32_t)((c_fr * W + c_fc) * Cin * 2);
     const uint32_t soff_a = (uint32_t)(c_ci * 2) + (sh ? ep.x2_pa : 0u);
     const uint32_t soff_b = (BT ? (uint32_t)(((int64_t)c_ci * taps + (taps - 1 - c_tap)) * Cout * 2)
@@ -634,6 +690,16 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
     }
 #pragma unroll
     for (int i = 0; i < BCH; ++i) buf_lds16(wr, Bs + (buf * BN + 32 * i + 8 * wid) * BK, b_off[i], soff_b);
+    if constexpr (X3) {
+#pragma unroll
+      for (int i = 0; i < ACL; ++i) {
+        const uint32_t vo = ((al_mask[i] >> c_tap) & 1ull) ? al_off[i] + tap_a : kBufOOB;
+        buf_lds16(xr, Al + (buf * BM + 64 * i + 16 * wid) * 32, vo, soff_a);
+      }
+#pragma unroll
+      for (int i = 0; i < BCL; ++i)
+        buf_lds16(wr, Bl + buf * LBN + (BT ? 8 * wid * 64 : (64 * i + 16 * wid) * 32), bl_off[i], soff_b);
+    }
     c_ci += KC;
     if (c_ci == Cin) {
       c_ci = 0;
@@ -706,6 +772,47 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
         for (int j = 0; j < 2; ++j)
           bfr[kk][j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(fr[kk * 4 + j * 2], fr[kk * 4 + j * 2 + 1], 0,
                                                                           1, 2, 3, 4, 5, 6, 7));
+      if constexpr (X3) {  // lo fragments: A from its 64-B-row tile, B by transposed reads of the k-major lo tile
+        bf16x8 afl[TM], bfl[2];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = wm * WM + i * 16 + (lane & 15);
+          afl[i] = *reinterpret_cast<const bf16x8*>(Al + (buf * BM + row) * 32 + ((g ^ ((row >> 2) & 3)) << 3));
+        }
+        uint32_t adl[4];
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int row = 8 * g + 4 * h + q, col = wn * WN + j * 16 + pcol;
+            adl[j * 2 + h] = (uint32_t)reinterpret_cast<uintptr_t>(
+                Bl + buf * LBN + row * 64 + (((col >> 3) ^ wsw(row)) << 3) + (col & 7));
+          }
+        s16x4 frl[4];
+        asm volatile(
+            "ds_read_b64_tr_b16 %0, %4\n\tds_read_b64_tr_b16 %1, %5\n\t"
+            "ds_read_b64_tr_b16 %2, %6\n\tds_read_b64_tr_b16 %3, %7\n\t"
+            "s_waitcnt lgkmcnt(0)"
+            : "=&v"(frl[0]), "=&v"(frl[1]), "=&v"(frl[2]), "=&v"(frl[3])
+            : "v"(adl[0]), "v"(adl[1]), "v"(adl[2]), "v"(adl[3])
+            : "memory");
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          bfl[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(frl[j * 2], frl[j * 2 + 1], 0, 1, 2, 3, 4, 5, 6, 7));
+        // (hi, mid) halves: af / bfr [0] = hi, [1] = mid
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i], bfr[0][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i], bfr[1][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][i], bfr[0][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][i], bfr[1][j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i], bfl[j], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afl[i], bfr[0][j], acc[i][j], 0, 0, 0);
+          }
+        continue;
+      }
       // products per pass: bf16 (k-half 0) (k-half 1); x2 (hi,hi) (hi,lo) (lo,hi)
       constexpr int NPASS = X2 ? 3 : 2;
 #pragma unroll
@@ -717,6 +824,36 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[ka][i], bfr[kb][j], acc[i][j], 0, 0, 0);
       }
+      continue;
+    }
+    if constexpr (X3) {  // hi / mid from the main tiles' chunks 0-3 / 4-7, lo from the 64-B-row tiles
+      bf16x8 fh[TM], fm[TM], fl[TM], gh[TN], gm[TN], gl[TN];
+      const int g = lane >> 4;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WM + i * 16 + (lane & 15);
+        fh[i] = *reinterpret_cast<const bf16x8*>(As + (buf * BM + row) * BK + swz(row, g) * 8);
+        fm[i] = *reinterpret_cast<const bf16x8*>(As + (buf * BM + row) * BK + swz(row, 4 + g) * 8);
+        fl[i] = *reinterpret_cast<const bf16x8*>(Al + (buf * BM + row) * 32 + ((g ^ ((row >> 2) & 3)) << 3));
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WN + j * 16 + (lane & 15);
+        gh[j] = *reinterpret_cast<const bf16x8*>(Bs + (buf * BN + row) * BK + swz(row, g) * 8);
+        gm[j] = *reinterpret_cast<const bf16x8*>(Bs + (buf * BN + row) * BK + swz(row, 4 + g) * 8);
+        gl[j] = *reinterpret_cast<const bf16x8*>(Bl + (buf * BN + row) * 32 + ((g ^ ((row >> 2) & 3)) << 3));
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh[i], gh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh[i], gm[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fm[i], gh[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fm[i], gm[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fh[i], gl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fl[i], gh[j], acc[i][j], 0, 0, 0);
+        }
       continue;
     }
     if constexpr (X2) {

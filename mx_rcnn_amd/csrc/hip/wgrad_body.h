@@ -78,11 +78,27 @@ struct WgradParams {
 
 constexpr int kWgradLdsElems = 3 * 2 * WG_BK * 64;  // the S = 3 ring: [S][dY|X][64 px][64 ch] (48 KB)
 
-// workgroup `wgid` of the launch; `lds`: S * 2 * 64 * 64 bf16 (16-B aligned); X2 must equal p.x2
-template <int S, bool X2 = false>
+// workgroup `wgid` of the launch; `lds`: KG * S * 2 * 64 * 64 bf16 (16-B aligned); X2 must equal p.x2.
+// KG > 1: 4*KG waves, group q over a contiguous 1/KG of the pixel loop through its own sub-ring
+// (the grouped dgrad + wgrad launch's K-group form, conv_igemm.hip); the partial tiles are summed
+// in group order in the LDS epilogue.
+// X3 (the fp32 mode's fused form, X2 = true as well): rows 0-31 of a stage are the hi plane of 32
+// pixels, rows 32-63 the mid plane, and a lo tile per operand (32 rows laid out like rows 0-31)
+// after the S main stages holds the lo plane: one pass, six MFMAs per fragment set (hh, hm, mh,
+// mm, hl, lh).
+template <bool X3>
+constexpr int wgrad_ring_stage() { return 2 * WG_BK * 64 + (X3 ? 2 * 32 * 64 : 0); }
+
+template <int S, bool X2 = false, int KG = 1, bool X3 = false>
 __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const WgradParams& p) {
-  constexpr int LPS = 4;  // DMA instructions per thread per stage (2 dY rows + 2 X rows)
+  constexpr int LPS = X3 ? 6 : 4;  // DMA instructions per thread per stage (2 dY rows + 2 X rows [+ 2 lo])
+  constexpr int NT = 256 * KG;
+  constexpr int GSTRIDE = S * wgrad_ring_stage<X3>();  // one group's ring, elements
   static_assert(S >= 2 && S <= 4, "pipeline depth");
+  static_assert(!X3 || X2, "X3 is a multi-plane mode");
+  const int kgi = KG > 1 ? (int)(threadIdx.x >> 8) : 0;
+  lds += kgi * GSTRIDE;  // this group's sub-ring
+  uint16_t* lo_ring = lds + S * 2 * WG_BK * 64;  // X3: [S][dY lo | X lo][32 px][64 ch]
   const uint16_t* __restrict__ dy = p.dy;
   const uint16_t* __restrict__ x = p.x;
   float* __restrict__ slab = p.slab;
@@ -97,14 +113,14 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
   const int tap = k0 / Cin, ci0 = k0 % Cin;
   const int fr = tap / KW, fc = tap % KW;
   const int P = NB * Ho * Wo, HWo = Ho * Wo;
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = (tid >> 6) & 3;  // wave within the group
   const int wm = wid >> 1, wn = wid & 1;
   const int steps_all = (P + WG_BK - 1) / WG_BK;
   const int s_begin = split * per, s_end = min(steps_all, s_begin + per);
   const int nsteps = max(0, s_end - s_begin);
   constexpr int PX = X2 ? WG_BK / 2 : WG_BK;  // pixels per stage
   const int nloop1 = X2 ? 2 * nsteps : nsteps;           // one pass
-  const int nloop = X2 && p.x3 ? 2 * nloop1 : nloop1;    // x3: two phases
+  const int nloop = X2 && !X3 && p.x3 ? 2 * nloop1 : nloop1;  // two-phase x3: (hi, lo), then (mid, hi)
 
   // records through the lo planes for x2 pairs, the third plane for x3 (the range check covers
   // voffset + soffset)
@@ -122,16 +138,18 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
     chk[i] = (lane & 7) ^ wsw(rowi[i]);
     a_off[i] = co0 + chk[i] * 8 < Cout ? (uint32_t)((prow[i] * Cout + co0 + chk[i] * 8) * 2) : kWgOOB;
   }
+  const uint32_t lo_dy = 2 * p.x2_pdy, lo_x = 2 * p.x2_px;  // X3: byte offsets of the lo planes
   auto issue = [&](int it, int buf) {
-    const bool ph0 = X2 && p.x3 && it < nloop1;  // x3 phase (hi, lo): one plane further on
-    if (X2 && p.x3 && !ph0) it -= nloop1;
+    const bool ph0 = X2 && !X3 && p.x3 && it < nloop1;  // two-phase x3 (hi, lo): one plane further on
+    if (X2 && !X3 && p.x3 && !ph0) it -= nloop1;
     const int p0 = s_begin * WG_BK + it * PX;
     uint16_t* Ab = lds + buf * 2 * WG_BK * 64;
     uint16_t* Bb = Ab + WG_BK * 64;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-      const uint32_t pdy = (X2 && i ? p.x2_pdy : 0u) + (ph0 ? p.x2_pdy : 0u);
-      const uint32_t px = (X2 && i ? p.x2_px : 0u) + (ph0 ? p.x2_px : 0u);
+      // planes of rows 0-31 / 32-63: x2 (hi, lo) = memory planes (0, 1); X3 (hi, mid) = (1, 0)
+      const uint32_t pdy = X3 ? (i ? 0u : p.x2_pdy) : (X2 && i ? p.x2_pdy : 0u) + (ph0 ? p.x2_pdy : 0u);
+      const uint32_t px = X3 ? (i ? 0u : p.x2_px) : (X2 && i ? p.x2_px : 0u) + (ph0 ? p.x2_px : 0u);
       const int p = p0 + prow[i];
       const uint32_t va = p < P ? a_off[i] : kWgOOB;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(dyr, (__attribute__((address_space(3))) void*)(Ab + (32 * i + 8 * wid) * 64),
@@ -146,6 +164,13 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
       }
       __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(Bb + (32 * i + 8 * wid) * 64),
                                                16, (int)vb, (int)px, 0, 0);
+      if (X3 && i == 0) {  // the lo plane of the same 32 pixels (memory plane 2)
+        uint16_t* La = lo_ring + buf * 2 * 32 * 64;
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(dyr, (__attribute__((address_space(3))) void*)(La + 8 * wid * 64), 16,
+                                                 (int)va, (int)((uint32_t)p0 * Cout * 2 + lo_dy), 0, 0);
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(xr, (__attribute__((address_space(3))) void*)(La + (32 + 8 * wid) * 64),
+                                                 16, (int)vb, (int)lo_x, 0, 0);
+      }
     }
   };
 
@@ -158,16 +183,22 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
   // swizzled element offset of (row, col), col a multiple of 4 inside one 16-B chunk
   auto lidx = [](int row, int col) { return row * 64 + (((col >> 3) ^ wsw(row)) << 3) + (col & 7); };
 
+  // this group's contiguous slice of the loop (all of it for KG = 1; x3 with KG = 2: one phase)
+  const int per_it = (nloop + KG - 1) / KG;
+  const int it0 = kgi * per_it;
+  const int nl = max(0, min(nloop, it0 + per_it) - it0);
+  const int n_iter = KG > 1 ? per_it : nl;
 #pragma unroll
   for (int s = 0; s < S - 1; ++s)
-    if (s < nloop) issue(s, s);
-  for (int st = 0; st < nloop; ++st) {
-    const int ahead = min(S - 2, nloop - 1 - st);
+    if (s < nl) issue(it0 + s, s);
+  for (int st = 0; st < n_iter; ++st) {
+    const int ahead = st < nl ? min(S - 2, nl - 1 - st) : 0;
     if (ahead >= 2) wait_vmcnt_wg<2 * LPS>();
     else if (ahead == 1) wait_vmcnt_wg<LPS>();
     else wait_vmcnt_wg<0>();
     __builtin_amdgcn_s_barrier();
-    if (st + S - 1 < nloop) issue(st + S - 1, (st + S - 1) % S);
+    if (st + S - 1 < nl) issue(it0 + st + S - 1, (st + S - 1) % S);
+    if (KG > 1 && st >= nl) continue;  // this group is done: barriers only
     const uint16_t* Ab = lds + (st % S) * 2 * WG_BK * 64;
     const uint16_t* Bb = Ab + WG_BK * 64;
     // all 16 transposed fragment reads of the step in ONE asm block: through the builtin, the
@@ -218,6 +249,52 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
                                                                         fr[kk * 8 + 4 + j * 2 + 1], 0, 1, 2, 3, 4, 5,
                                                                         6, 7));
     }
+    if constexpr (X3) {  // lo fragments by transposed reads of the lo tiles; six products
+      const uint16_t* La = lo_ring + (st % S) * 2 * 32 * 64;
+      uint32_t adl[8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          adl[i * 2 + h] = (uint32_t)reinterpret_cast<uintptr_t>(La + lidx(krow(0, g, h) + q, wm * 32 + i * 16 + pcol));
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          adl[4 + j * 2 + h] = (uint32_t)reinterpret_cast<uintptr_t>(
+              La + 32 * 64 + lidx(krow(0, g, h) + q, wn * 32 + j * 16 + pcol));
+      }
+      s16x4 frl[8];
+      asm volatile(
+          "ds_read_b64_tr_b16 %0, %8\n\tds_read_b64_tr_b16 %1, %9\n\t"
+          "ds_read_b64_tr_b16 %2, %10\n\tds_read_b64_tr_b16 %3, %11\n\t"
+          "ds_read_b64_tr_b16 %4, %12\n\tds_read_b64_tr_b16 %5, %13\n\t"
+          "ds_read_b64_tr_b16 %6, %14\n\tds_read_b64_tr_b16 %7, %15\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=&v"(frl[0]), "=&v"(frl[1]), "=&v"(frl[2]), "=&v"(frl[3]), "=&v"(frl[4]), "=&v"(frl[5]),
+            "=&v"(frl[6]), "=&v"(frl[7])
+          : "v"(adl[0]), "v"(adl[1]), "v"(adl[2]), "v"(adl[3]), "v"(adl[4]), "v"(adl[5]), "v"(adl[6]),
+            "v"(adl[7])
+          : "memory");
+      bf16x8 afl[2], bfl[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+        afl[i] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(frl[i * 2], frl[i * 2 + 1], 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        bfl[j] = __builtin_bit_cast(bf16x8, __builtin_shufflevector(frl[4 + j * 2], frl[4 + j * 2 + 1], 0, 1, 2, 3, 4,
+                                                                    5, 6, 7));
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {  // [0] = hi, [1] = mid
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i], bfr[0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i], bfr[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][i], bfr[0][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[1][i], bfr[1][j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[0][i], bfl[j], acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(afl[i], bfr[0][j], acc[i][j], 0, 0, 0);
+        }
+      continue;
+    }
     // products (a, b) per pass: bf16 (0,0) (1,1); x2 (hi,hi) (hi,lo) (lo,hi)
     constexpr int NPASS = X2 ? 3 : 2;
 #pragma unroll
@@ -231,25 +308,33 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
     }
   }
 
-  // epilogue through LDS: T[co][k] fp32 (row stride 68), then 8-column vectors per thread
-  float* T = reinterpret_cast<float*>(lds);
+  // epilogue through LDS: T[co][k] fp32 (row stride 68; one slice per K group, summed in group
+  // order), then 8-column vectors per thread
   __syncthreads();
+  float* T = reinterpret_cast<float*>(lds - kgi * GSTRIDE);  // the workgroup's LDS
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 4; ++r)
-        T[(wm * 32 + i * 16 + (lane >> 4) * 4 + r) * 68 + wn * 32 + j * 16 + (lane & 15)] = acc[i][j][r];
+        T[(kgi * 64 + wm * 32 + i * 16 + (lane >> 4) * 4 + r) * 68 + wn * 32 + j * 16 + (lane & 15)] = acc[i][j][r];
   __syncthreads();
   const int ldk = tiles_n * WG_BN;
 #pragma unroll
-  for (int v = 0; v < 2; ++v) {
-    const int e = tid + v * 256, row = e >> 3, cv = e & 7;
+  for (int v = 0; v < (512 + NT - 1) / NT; ++v) {
+    const int e = tid + v * NT, row = e >> 3, cv = e & 7;
     const int co = co0 + row;
-    if (co >= Cout) continue;
+    if (e >= 512 || co >= Cout) continue;
     const float4* src = reinterpret_cast<const float4*>(T + row * 68 + cv * 8);
-    const float4 a0 = src[0], a1 = src[1];
+    float4 a0 = src[0], a1 = src[1];
+#pragma unroll
+    for (int q = 1; q < KG; ++q) {
+      const float4* sq = reinterpret_cast<const float4*>(T + (q * 64 + row) * 68 + cv * 8);
+      const float4 b0 = sq[0], b1 = sq[1];
+      a0.x += b0.x; a0.y += b0.y; a0.z += b0.z; a0.w += b0.w;
+      a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
+    }
     const int64_t o = (int64_t)co * ldk + k0 + cv * 8;
     if (splits > 1) {
       float4* d = reinterpret_cast<float4*>(slab + (int64_t)split * Cout * ldk + o);
@@ -278,11 +363,12 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
   }
 }
 
-// sum of the split-K slabs (+ the existing gradient when accumulating) -> bf16; 1024 elements per
-// 256-thread workgroup `gid` (the wgrad_reduce kernel, or a role of the grouped launch)
+// sum of the split-K slabs (+ the existing gradient when accumulating) -> bf16; 4 * nt elements per
+// nt-thread workgroup `gid` (the wgrad_reduce kernel, or a role of the grouped launch)
 __device__ __forceinline__ void wgrad_reduce_body(int gid, const float* __restrict__ slab, int splits, int64_t n,
-                                                  uint16_t* __restrict__ out, int accumulate, float* outf = nullptr) {
-  const int64_t e = ((int64_t)gid * 256 + threadIdx.x) * 4;
+                                                  uint16_t* __restrict__ out, int accumulate, float* outf = nullptr,
+                                                  int nt = 256) {
+  const int64_t e = ((int64_t)gid * nt + threadIdx.x) * 4;
   if (e >= n) return;
   float4 a = *reinterpret_cast<const float4*>(slab + e);
 #pragma unroll 4

@@ -145,3 +145,38 @@ def test_kg_bn_backward_epilogue(cuda, P):
                 continue
             base = _err(outs[23][i], ref)
             assert _err(outs[tile][i], ref) <= _tol(P, base) + 1e-6, (tile, i, base, _err(outs[tile][i], ref))
+
+
+@pytest.mark.parametrize('P', MODES)
+def test_grouped_bt_dgrad_wgrad(cuda, P):
+    """The grouped data + weight gradient launch reading the forward filter transposed (bt), in its
+    K-group form in the fp32 (x3) mode (MXR_GROUPED_KG default 2 there), against fp64: dgrad with
+    the frozen BN-ReLU backward epilogue, and the weight gradient of a 3x3 conv over the same dY."""
+    from mx_rcnn_amd.ops import need_ext
+    ext = need_ext()
+    g = torch.Generator().manual_seed(31 + P)
+    C, H, W, O = 128, 17, 23, 256
+    dy = torch.randn(1, O, H, W, generator=g)
+    w = torch.randn(O, C, 3, 3, generator=g) * 0.03
+    xbn = torch.randn(1, C, H, W, generator=g)
+    xin = torch.randn(1, 128, H, W, generator=g)
+    if not P:
+        dy, w, xbn, xin = (t.bfloat16().float() for t in (dy, w, xbn, xin))
+    gam, bet, mu, var = torch.rand(C) + 0.5, torch.randn(C) * 0.1, torch.randn(C) * 0.1, torch.rand(C) + 0.5
+    bn = [t.to(cuda) for t in (gam, bet, mu, var)]
+    we, kw = _wargs(w, cuda, P)
+    dgm, dbt = torch.zeros(C, device=cuda), torch.zeros(C, device=cuda)
+    gdt = torch.float32 if P else torch.bfloat16
+    wg = _cl(torch.zeros(O, 128, 3, 3, device=cuda, dtype=gdt))
+    dye = _enc(dy, cuda, P)
+    out = ext.conv_dgrad_wgrad(dye, we, 1, None, bn, 2e-5, False, _enc(xbn, cuda, P), None, dgm, dbt, dye,
+                               _enc(xin, cuda, P), 3, 3, 1, 1, wg, bt=True, **kw)
+    dact = torch.nn.grad.conv2d_input((1, C, H, W), w.double(), dy.double(), padding=1)
+    s = gam.double() / torch.sqrt(var.double() + 2e-5)
+    pre = (xbn.double() - mu.double().view(1, -1, 1, 1)) * s.view(1, -1, 1, 1) + bet.double().view(1, -1, 1, 1)
+    gm = dact * (pre > 0)
+    ref_dw = torch.nn.grad.conv2d_weight(xin.double(), (O, 128, 3, 3), dy.double(), padding=1)
+    tol = {0: 2e-2, 2: 4e-5, 3: 4e-6}[P]
+    assert _err(_dec(out[0], P), gm * s.view(1, -1, 1, 1)) <= tol
+    assert _err(dbt, gm.sum((0, 2, 3))) <= tol
+    assert _err(wg.float(), ref_dw) <= tol

@@ -551,7 +551,7 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
   static_assert(KG == 1 || (!F16 && BN == 64), "K groups: bf16 / multi-plane 64-column tiles");
   static_assert(!X3 || (X2 && !F16 && BM % 64 == 0 && BN % 64 == 0), "X3: multi-plane 64-multiple tiles");
   constexpr int LBM = X3 ? BM * 32 : 0, LBN = X3 ? (BT ? 32 * 64 : BN * 32) : 0;  // lo tiles per stage
-  const int kgi = KG > 1 ? (int)(threadIdx.x >> 8) : 0;  // this wave's K group
+  const int kgi = KG > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8)) : 0;  // this wave's K group
   uint16_t* As = lds + kgi * S * igemm_ring_stage<BM, BN, BT, X3>();  // the group's sub-ring
   uint16_t* Bs = As + S * BM * BK;
   uint16_t* Al = Bs + S * BN * BK;  // X3 lo tiles
@@ -563,18 +563,20 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
   const int tm_idx = tile / tiles_n, tn_idx = tile % tiles_n;
   const int m0 = tm_idx * BM, n0 = tn_idx * BN;
   const int M = NB * Ho * Wo;
-  const int tid = threadIdx.x, lane = tid & 63, wid = (tid >> 6) & 3;  // wave within the K group
+  const int tid = threadIdx.x, lane = tid & 63, wid = KG > 1 ? __builtin_amdgcn_readfirstlane(tid >> 6) & 3 : tid >> 6;  // wave within the K group
   const int wm = wid >> 1, wn = wid & 1;
   const int K = KH * KW * Cin;
 
   // the range check covers voffset + soffset: with x2 pairs the records reach through the lo planes
   // (the kBufOOB sentinel of padding taps stays beyond them: operands are < 1 GB per plane)
   // (x3: through the third plane)
+  // (readfirstlane: keeps the resources provably uniform -- a VGPR descriptor costs a waterfall
+  // loop around every buffer load)
   const int xpl = ep.x2 ? (ep.x3 ? 2 : 1) : 0;
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)x, (short)0, (int)((int64_t)NB * H * W * Cin * 2 + (int64_t)xpl * ep.x2_pa), 0x00020000);
-  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)w, (short)0, (int)((int64_t)Cout * K * 2 + (int64_t)xpl * ep.x2_pb), 0x00020000);
+  const int nrec_x = __builtin_amdgcn_readfirstlane((int)((int64_t)NB * H * W * Cin * 2 + (int64_t)xpl * ep.x2_pa));
+  const int nrec_w = __builtin_amdgcn_readfirstlane((int)((int64_t)Cout * K * 2 + (int64_t)xpl * ep.x2_pb));
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, nrec_x, 0x00020000);
+  const __amdgpu_buffer_rsrc_t wr = __builtin_amdgcn_make_buffer_rsrc((void*)w, (short)0, nrec_w, 0x00020000);
 
   const int slot = lane & 7;
   // logical chunk lc of a row: channels lc*8 (16-bit), or (X2) channels (lc&3)*8 of plane lc>>2

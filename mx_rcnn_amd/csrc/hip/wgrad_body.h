@@ -96,7 +96,7 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
   constexpr int GSTRIDE = S * wgrad_ring_stage<X3>();  // one group's ring, elements
   static_assert(S >= 2 && S <= 4, "pipeline depth");
   static_assert(!X3 || X2, "X3 is a multi-plane mode");
-  const int kgi = KG > 1 ? (int)(threadIdx.x >> 8) : 0;
+  const int kgi = KG > 1 ? __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 8)) : 0;
   lds += kgi * GSTRIDE;  // this group's sub-ring
   uint16_t* lo_ring = lds + S * 2 * WG_BK * 64;  // X3: [S][dY lo | X lo][32 px][64 ch]
   const uint16_t* __restrict__ dy = p.dy;
@@ -113,7 +113,7 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
   const int tap = k0 / Cin, ci0 = k0 % Cin;
   const int fr = tap / KW, fc = tap % KW;
   const int P = NB * Ho * Wo, HWo = Ho * Wo;
-  const int tid = threadIdx.x, lane = tid & 63, wid = (tid >> 6) & 3;  // wave within the group
+  const int tid = threadIdx.x, lane = tid & 63, wid = KG > 1 ? __builtin_amdgcn_readfirstlane(tid >> 6) & 3 : tid >> 6;  // wave within the group
   const int wm = wid >> 1, wn = wid & 1;
   const int steps_all = (P + WG_BK - 1) / WG_BK;
   const int s_begin = split * per, s_end = min(steps_all, s_begin + per);
@@ -124,11 +124,13 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
 
   // records through the lo planes for x2 pairs, the third plane for x3 (the range check covers
   // voffset + soffset)
+  // (readfirstlane: keeps the resources provably uniform -- a VGPR descriptor costs a waterfall
+  // loop around every buffer load)
   const int npl = X2 ? (p.x3 ? 2 : 1) : 0;
-  const __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)dy, (short)0, (int)((int64_t)P * Cout * 2 + (int64_t)npl * p.x2_pdy), 0x00020000);
-  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)x, (short)0, (int)((int64_t)NB * H * W * Cin * 2 + (int64_t)npl * p.x2_px), 0x00020000);
+  const int nrec_dy = __builtin_amdgcn_readfirstlane((int)((int64_t)P * Cout * 2 + (int64_t)npl * p.x2_pdy));
+  const int nrec_x = __builtin_amdgcn_readfirstlane((int)((int64_t)NB * H * W * Cin * 2 + (int64_t)npl * p.x2_px));
+  const __amdgpu_buffer_rsrc_t dyr = __builtin_amdgcn_make_buffer_rsrc((void*)dy, (short)0, nrec_dy, 0x00020000);
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc((void*)x, (short)0, nrec_x, 0x00020000);
   int rowi[2], chk[2], prow[2];
   uint32_t a_off[2];
 #pragma unroll

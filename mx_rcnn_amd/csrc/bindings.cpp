@@ -1410,6 +1410,19 @@ void chan_sum(const Tensor& x, Tensor out, bool accumulate, int64_t x2) {
               "chan_sum: unsupported shape");
 }
 
+// ---- DP interference probes (tools/dp_interference.py) -----------------------------------------
+void cu_spin(int64_t nwg, double us) {
+  mxr::cu_spin((int)nwg, (int64_t)(us * 100.0), cur_stream());  // s_memrealtime: 100 MHz
+}
+
+void cu_copy(const Tensor& src, Tensor dst, int64_t nwg) {
+  CHECK_DEV(src); CHECK_DEV(dst);
+  TORCH_CHECK(src.scalar_type() == at::kFloat && dst.scalar_type() == at::kFloat && src.is_contiguous() &&
+                  dst.is_contiguous() && src.numel() == dst.numel() && src.numel() % 4 == 0,
+              "cu_copy: contiguous fp32 src / dst of one size (multiple of 4)");
+  mxr::cu_copy(src.data_ptr<float>(), dst.data_ptr<float>(), src.numel(), (int)nwg, cur_stream());
+}
+
 // ---- proposal top-k ----------------------------------------------------------------------------
 std::vector<Tensor> proposal_topk(const Tensor& keys, const Tensor& boxes, int64_t P) {
   CHECK_DEV(keys); CHECK_DEV(boxes);
@@ -1535,6 +1548,28 @@ std::vector<Tensor> bn_train_apply(const Tensor& x, const Tensor& part, const Te
                                     x2 ? npl(x2) : 0);
   TORCH_CHECK(r == 0, "bn_train_apply: unsupported shape");
   return {y, save};
+}
+
+// frozen-BN gamma / beta gradients from the conv epilogue's partial rows (ConvEpi::bnb_part,
+// [nparts][sum g | sum g * xhat][C]): dbeta += fixed-order sum of the first halves, dgamma += of
+// the second (deterministic; either output may be None)
+void bnb_part_fold(const Tensor& part, int64_t nparts, int64_t C, c10::optional<Tensor> dgamma,
+                   c10::optional<Tensor> dbeta) {
+  CHECK_DEV(part);
+  TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && nparts > 0 &&
+                  part.numel() >= nparts * 2 * C, "part: fp32 with nparts * 2 * C elements");
+  float* out[2] = {nullptr, nullptr};
+  int i = 0;
+  for (auto* p : {&dbeta, &dgamma}) {
+    if (p->has_value() && (*p)->defined()) {
+      TORCH_CHECK((*p)->scalar_type() == at::kFloat && (*p)->is_contiguous() && (*p)->numel() == C &&
+                      (*p)->device() == part.device(), "dgamma / dbeta: fp32 (C,) on part's device");
+      out[i] = (*p)->data_ptr<float>();
+    }
+    ++i;
+  }
+  DevGuard g(part.device());
+  mxr::col_part_fold(part.data_ptr<float>(), (int)nparts, (int)C, out[0], out[1], cur_stream());
 }
 
 // finish of a training-BN backward whose BN-backward epilogue (a dgrad conv with bnb_x = x,
@@ -2078,6 +2113,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("head_bwd", &head_bwd, py::arg("x"), py::arg("dys"), py::arg("ws"), py::arg("dws"), py::arg("dw_acc"),
         py::arg("dbs"), py::arg("db_acc"), py::arg("need_dx"), py::arg("relu_mask"), py::arg("x2") = 0,
         py::arg("w_planes") = std::vector<int64_t>(), py::arg("mask_scale") = 1.0);
+  m.def("cu_spin", &cu_spin, py::arg("nwg"), py::arg("us"));
+  m.def("cu_copy", &cu_copy, py::arg("src"), py::arg("dst"), py::arg("nwg"));
   m.def("chan_sum", &chan_sum, py::arg("x"), py::arg("out"), py::arg("accumulate"), py::arg("x2") = 0);
   m.def("det_postprocess", &det_postprocess, py::arg("rois"), py::arg("scores"), py::arg("deltas"),
         py::arg("im_info"), py::arg("thresh"), py::arg("nms_thresh"), py::arg("max_per"), py::arg("cap"));
@@ -2099,6 +2136,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("bn_train_apply", &bn_train_apply, py::arg("x"), py::arg("part"), py::arg("gamma"), py::arg("beta"),
         py::arg("rmean"), py::arg("rvar"), py::arg("momentum"), py::arg("eps"), py::arg("fix_gamma"), py::arg("relu"),
         py::arg("x2") = 0);
+  m.def("bnb_part_fold", &bnb_part_fold, py::arg("part"), py::arg("nparts"), py::arg("C"),
+        py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
   m.def("bn_train_dx_apply", &bn_train_dx_apply, py::arg("o"), py::arg("x"), py::arg("save"), py::arg("gamma_eff"),
         py::arg("part"), py::arg("nparts"), py::arg("dres") = py::none(), py::arg("dgamma") = py::none(),
         py::arg("dbeta") = py::none(), py::arg("x2") = 0);

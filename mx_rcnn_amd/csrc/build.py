@@ -11,6 +11,7 @@ Usage: ``python -m mx_rcnn_amd.csrc.build [--force] [--jobs N] [--debug]``
 import argparse
 import glob
 import os
+import re
 import subprocess
 import sys
 import sysconfig
@@ -53,10 +54,32 @@ def _run(cmd):
     return r.stdout
 
 
+_INC = re.compile(r'^\s*#\s*include\s+"([^"]+)"', re.M)
+
+
+def _local_deps(src, seen=None):
+    """The in-tree headers ``src`` includes, transitively (quoted includes resolved next to the
+    including file, then in csrc/ and csrc/hip/): an object rebuilds only when one of ITS headers
+    changes (a conv-body edit no longer rebuilds every kernel file)."""
+    seen = set() if seen is None else seen
+    try:
+        text = open(src).read()
+    except OSError:
+        return seen
+    for name in _INC.findall(text):
+        for d in (os.path.dirname(src), HERE, os.path.join(HERE, 'hip')):
+            path = os.path.normpath(os.path.join(d, name))
+            if os.path.exists(path):
+                if path not in seen:
+                    seen.add(path)
+                    _local_deps(path, seen)
+                break
+    return seen
+
+
 def build(force=False, jobs=None, debug=False, verbose=False):
     os.makedirs(BUILD, exist_ok=True)
     troot, tinc, tlib, abi = _torch_paths()
-    headers = glob.glob(os.path.join(HERE, '*.h')) + glob.glob(os.path.join(HERE, 'hip', '*.h'))
     hipcc = os.path.join(ROCM, 'bin', 'hipcc')
     opt = ['-O0', '-g'] if debug else ['-O3']
     hip_flags = opt + ['--offload-arch=%s' % ARCH, '-fPIC', '-std=c++17', '-ffp-contract=off',
@@ -68,13 +91,13 @@ def build(force=False, jobs=None, debug=False, verbose=False):
     for src in sorted(glob.glob(os.path.join(HERE, 'hip', '*.hip'))):
         obj = os.path.join(BUILD, os.path.basename(src) + '.o')
         objs.append(obj)
-        if force or _newer([src] + headers, obj):
+        if force or _newer([src] + sorted(_local_deps(src)), obj):
             jobs_list.append([hipcc] + hip_flags + ['-c', src, '-o', obj])
     py_inc = sysconfig.get_paths()['include']
     glue = os.path.join(HERE, 'bindings.cpp')
     glue_obj = os.path.join(BUILD, 'bindings.o')
     objs.append(glue_obj)
-    if force or _newer([glue] + headers, glue_obj):
+    if force or _newer([glue] + sorted(_local_deps(glue)), glue_obj):
         cxx = os.environ.get('CXX', 'g++')
         flags = opt + ['-fPIC', '-std=c++17', '-D__HIP_PLATFORM_AMD__=1', '-DUSE_ROCM=1',
                        '-DTORCH_EXTENSION_NAME=_C', '-DTORCH_API_INCLUDE_EXTENSION_H',

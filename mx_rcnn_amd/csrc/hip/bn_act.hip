@@ -76,12 +76,11 @@ bn_relu_bwd_kernel(const void* __restrict__ x, const void* __restrict__ dy, int 
                    const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ mean,
                    const float* __restrict__ var, float eps, int fix_gamma, int relu, void* __restrict__ dx,
                    const void* __restrict__ dres, float* __restrict__ part) {
-  extern __shared__ __attribute__((aligned(16))) float red[];  // 2*C
+  __shared__ float red[256][9];  // per-thread (sum g * xhat, sum g) x 4 channels, padded row
   const int CV = C >> 2;
   const int64_t T = (int64_t)gridDim.x * blockDim.x;
   const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int cv = (int)(tid % CV);
-  for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) red[i] = 0.f;
   float s[4], t[4], inv[4], mu[4];
   for (int k = 0; k < 4; ++k) {
     const int c = cv * 4 + k;
@@ -127,15 +126,24 @@ bn_relu_bwd_kernel(const void* __restrict__ x, const void* __restrict__ dy, int 
     load4(dy, e * 4, bf16, g, (int64_t)M * C);
     body(xv, g, e);
   }
-  __syncthreads();
   if (part) {
+    // ordered in-block sum (no LDS float atomics: the step is bitwise reproducible): the threads
+    // of channel quad q are t0(q), t0(q) + CV, ... (thread t holds quad (block * 256 + t) % CV),
+    // summed in increasing t, then one partial row per block, folded in order by bn_part_reduce
+#pragma unroll
     for (int k = 0; k < 4; ++k) {
-      atomicAdd(&red[cv * 4 + k], ag[k]);
-      atomicAdd(&red[C + cv * 4 + k], ab[k]);
+      red[threadIdx.x][k] = ag[k];
+      red[threadIdx.x][4 + k] = ab[k];
     }
     __syncthreads();
     float* row = part + (int64_t)blockIdx.x * 2 * C;
-    for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) row[i] = red[i];
+    const int base = (int)(((int64_t)blockIdx.x * blockDim.x) % CV);
+    for (int i = threadIdx.x; i < 2 * C; i += blockDim.x) {
+      const int stat = i >= C, c = i - stat * C, q = c >> 2, k = c & 3;
+      float acc = 0.f;
+      for (int t = (q - base + CV) % CV; t < (int)blockDim.x; t += CV) acc += red[t][stat * 4 + k];
+      row[i] = acc;
+    }
   }
 }
 
@@ -266,9 +274,17 @@ void bn_relu_bwd(const void* x, const void* dy, int bf16, int64_t M, int C, cons
   }
   const int nblk = bn_grid(M, C, 320);
   float* part = (dgamma || dbeta) ? workspace : nullptr;
-  bn_relu_bwd_kernel<<<nblk, 256, 2 * C * sizeof(float), st>>>(x, dy, bf16, M, C, gamma, beta, mean, var, eps,
-                                                               fix_gamma, relu, dx, dres, part);
+  bn_relu_bwd_kernel<<<nblk, 256, 0, st>>>(x, dy, bf16, M, C, gamma, beta, mean, var, eps, fix_gamma, relu, dx, dres,
+                                            part);
   if (part) bn_part_reduce<<<(2 * C + 63) / 64, 256, 0, st>>>(part, nblk, C, fix_gamma, dgamma, dbeta, accumulate);
+}
+
+// Fixed-order fold of nparts partial rows [nparts][2][C] (first half -> out0, second -> out1;
+// either may be null), added to the outputs: the deterministic replacement of per-tile fp32
+// atomics for the BN-backward column sums of the conv epilogues (ConvEpi::bnb_part).
+void col_part_fold(const float* part, int nparts, int C, float* out0, float* out1, hipStream_t st) {
+  if (nparts <= 0 || C <= 0 || (!out0 && !out1)) return;
+  bn_part_reduce<<<(2 * C + 63) / 64, 256, 0, st>>>(part, nparts, C, 0, out0, out1, 1);
 }
 
 // ReLU (+ inverted dropout) backward on its own: out = dy * [y > 0] * scale over n 16-bit elements

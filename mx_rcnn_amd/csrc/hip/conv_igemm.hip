@@ -1299,7 +1299,14 @@ int conv_dgrad_wgrad(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, 
 #define MXR_GROUPED(S_, X, B, ...) \
   conv_dgrad_wgrad_kernel<S_, X, B, ##__VA_ARGS__><<<nwg_all, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, pad, ep, \
                                                             tiles_n, ntiles, ntiles, wp, rp)
-  if (wx2.x3 && ep.bt) MXR_GROUPED(3, true, true, 1, true);  // fp32 triples: the fused one-pass form
+  // fp32 triples: the fused one-pass form (72 KB of LDS at depth 3: two workgroups per CU; the A/B
+  // knob MXR_GROUPED_X3S=2 runs it at depth 2, 48 KB: three per CU)
+  static const int x3_depth = [] {
+    const char* e = getenv("MXR_GROUPED_X3S");
+    return e != nullptr && e[0] == '2' ? 2 : 3;
+  }();
+  if (wx2.x3 && ep.bt && x3_depth == 2) MXR_GROUPED(2, true, true, 1, true);
+  else if (wx2.x3 && ep.bt) MXR_GROUPED(3, true, true, 1, true);
   else if (wx2.x3) MXR_GROUPED(3, true, false, 1, true);
   else if (wx2.x2 && ep.bt) MXR_GROUPED(3, true, true);
   else if (wx2.x2) MXR_GROUPED(3, true, false);

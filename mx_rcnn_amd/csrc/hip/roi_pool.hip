@@ -169,9 +169,8 @@ void roi_pool_fwd(const void* feat, int bf16, int B, int H, int W, int C, const 
 }
 
 // Atomic-free (in global memory) backward: one workgroup per (image, CW-channel slab) accumulates
-// the whole H x W x CW gradient slab in LDS (fp32, LDS float atomics), walking every bin of the
-// image's RoIs once (argmax + dY: 16 + 8 B per bin for CW = 4), then writes its channels of every
-// pixel in the output dtype.  Replaces: a zero fill of an fp32 (B, H, W, C) buffer, 6.4 M global
+// the whole H x W x CW gradient slab in LDS, walking every bin of the image's RoIs (argmax + dY:
+// 16 + 8 B per bin for CW = 4), then writes its channels of every pixel in the output dtype.  Replaces: a zero fill of an fp32 (B, H, W, C) buffer, 6.4 M global
 // fp32 atomics (~120 us at 128 RoIs x 49 bins x 1024 ch) and the cast to bf16.
 // CW consecutive channels of one pixel as one vector access (8 B for 4 bf16 / fp16)
 template <int CW>
@@ -211,11 +210,22 @@ __device__ __forceinline__ void stv(float* p, const float* v, int) {
   for (int k = 0; k < CW; ++k) p[k] = v[k];
 }
 
+// Deterministic accumulation: float atomics add in whatever order the waves arrive, so the last bits
+// of a pixel's gradient (and of everything below the RoI pooling in the fp32 modes) varied run to
+// run.  The slab is instead an exact fixed-point sum: per (image, channel) the largest |dY| over
+// the image's bins fixes a power-of-two scale 2^s with max * (bins) < 2^61, every bin's dY is
+// added as the 64-bit integer rint(dY * 2^s) (integer addition is associative: any arrival order
+// gives the same bits), and the output is float(sum) * 2^-s -- one rounding, more accurate than
+// the fp32 atomic chain; a contribution below 2^-27 of the channel's largest keeps its low bits
+// only down to 2^-50 of it.  The other gradient of the feature map (gadd: the RPN head's) is added
+// once per pixel at the end.
 template <int CW, typename T>
 __global__ void __launch_bounds__(256)
 roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ argmax, const float* __restrict__ rois,
                         int R, int PHW, int HW, int C, int code, const T* __restrict__ gadd, T* __restrict__ gin) {
-  extern __shared__ float acc[];  // [HW][CW]
+  extern __shared__ long long acc[];  // [HW][CW] fixed-point sums
+  __shared__ float red[4][CW];        // per-wave channel maxima
+  __shared__ int sh_scale[CW];
   // code 3 / 4 (x2 / x3 planes): gout's planes one (R, PH, PW, C) block apart, gadd's / gin's one (B, H, W, C)
   const int64_t oplane = (int64_t)R * PHW * C, iplane = (int64_t)gridDim.y * HW * C;
   // XCD-aware channel groups: workgroups are dealt round-robin over the 8 XCDs, so consecutive
@@ -225,31 +235,9 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
   const int q = nx / 8, r8 = nx % 8, xcd = bx % 8;
   const int grp = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + bx / 8;
   const int c0 = grp * CW, b = blockIdx.y;
-  // the slab starts from the feature map's other gradient (gadd: the RPN head's), if any; one
-  // pixel (CW channels, one vector access) per thread and iteration
-#pragma unroll 4
-  for (int p = threadIdx.x; p < HW; p += blockDim.x) {
-    float v[CW];
-    if (gadd && code >= 3 && CW == 4) {
-      ld4c(gadd, ((int64_t)b * HW + p) * C + c0, code, iplane, v);  // one 8-B load per plane
-    } else if (gadd && code >= 3) {
-#pragma unroll
-      for (int k = 0; k < CW; ++k) v[k] = ldc(gadd, ((int64_t)b * HW + p) * C + c0 + k, code, iplane);
-    } else if (gadd) ldv<CW>(gadd + ((int64_t)b * HW + p) * C + c0, v, code);
-    else
-#pragma unroll
-      for (int k = 0; k < CW; ++k) v[k] = 0.f;
-#pragma unroll
-    for (int k = 0; k < CW; ++k) acc[p * CW + k] = v[k];
-  }
-  __syncthreads();
   const int nb = R * PHW;
-  for (int i = threadIdx.x; i < nb; i += blockDim.x) {
-    const int r = i / PHW;
-    if ((int)rois[(int64_t)r * 5] != b) continue;
+  auto load_g = [&](int i, float* g, int* a) {
     const int64_t base = (int64_t)i * C + c0;
-    int a[CW];
-    float g[CW];
     if constexpr (CW == 4) {  // c0 and C are multiples of 4: 16-B argmax / 8-B (per plane) gradient loads
       const int4 av = *reinterpret_cast<const int4*>(argmax + base);
       a[0] = av.x; a[1] = av.y; a[2] = av.z; a[3] = av.w;
@@ -264,16 +252,71 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
         g[k] = code >= 3 ? ldc(gout, base + k, code, oplane) : to_f(gout[base + k], code);
       }
     }
+  };
+  // pass 1: zero the slab, and the largest |dY| per channel over this image's bins
+  for (int p = threadIdx.x; p < HW * CW; p += blockDim.x) acc[p] = 0;
+  float mx[CW];
+#pragma unroll
+  for (int k = 0; k < CW; ++k) mx[k] = 0.f;
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+    if ((int)rois[(int64_t)(i / PHW) * 5] != b) continue;
+    float g[CW];
+    int a[CW];
+    load_g(i, g, a);
 #pragma unroll
     for (int k = 0; k < CW; ++k)
-      if (a[k] >= 0 && a[k] < HW && g[k] != 0.f) atomicAdd(&acc[a[k] * CW + k], g[k]);
+      if (a[k] >= 0 && a[k] < HW) mx[k] = fmaxf(mx[k], fabsf(g[k]));
+  }
+#pragma unroll
+  for (int k = 0; k < CW; ++k) mx[k] = wave_max(mx[k]);
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < CW; ++k) red[threadIdx.x >> 6][k] = mx[k];
+  __syncthreads();
+  if (threadIdx.x < CW) {
+    const float m = fmaxf(fmaxf(red[0][threadIdx.x], red[1][threadIdx.x]), fmaxf(red[2][threadIdx.x], red[3][threadIdx.x]));
+    // max * 2^s * nb < 2^61:  s = 60 - ceil(log2(max)) - ceil(log2(nb))
+    int e = 0;
+    if (m > 0.f) frexpf(m, &e);  // m < 2^e
+    int lb = 0;
+    while ((1 << lb) < nb) ++lb;
+    sh_scale[threadIdx.x] = m > 0.f ? 60 - e - lb : 0;
   }
   __syncthreads();
+  int sc[CW];
+#pragma unroll
+  for (int k = 0; k < CW; ++k) sc[k] = sh_scale[k];
+  // pass 2: exact integer accumulation (any order, same bits)
+  for (int i = threadIdx.x; i < nb; i += blockDim.x) {
+    if ((int)rois[(int64_t)(i / PHW) * 5] != b) continue;
+    float g[CW];
+    int a[CW];
+    load_g(i, g, a);
+#pragma unroll
+    for (int k = 0; k < CW; ++k)
+      if (a[k] >= 0 && a[k] < HW && g[k] != 0.f)
+        atomicAdd(reinterpret_cast<unsigned long long*>(&acc[a[k] * CW + k]),
+                  (unsigned long long)__float2ll_rn(ldexpf(g[k], sc[k])));
+  }
+  __syncthreads();
+  // pass 3: back to float (one rounding), plus the feature map's other gradient, in the output format
 #pragma unroll 4
   for (int p = threadIdx.x; p < HW; p += blockDim.x) {
-    float v[CW];
+    float v[CW], ga[CW];
 #pragma unroll
-    for (int k = 0; k < CW; ++k) v[k] = acc[p * CW + k];
+    for (int k = 0; k < CW; ++k) v[k] = ldexpf((float)acc[p * CW + k], -sc[k]);
+    if (gadd) {
+      if (code >= 3 && CW == 4) {
+        ld4c(gadd, ((int64_t)b * HW + p) * C + c0, code, iplane, ga);  // one 8-B load per plane
+      } else if (code >= 3) {
+#pragma unroll
+        for (int k = 0; k < CW; ++k) ga[k] = ldc(gadd, ((int64_t)b * HW + p) * C + c0 + k, code, iplane);
+      } else {
+        ldv<CW>(gadd + ((int64_t)b * HW + p) * C + c0, ga, code);
+      }
+#pragma unroll
+      for (int k = 0; k < CW; ++k) v[k] += ga[k];
+    }
     if (code >= 3 && CW == 4) {
       st4c(gin, ((int64_t)b * HW + p) * C + c0, code, iplane, v);
     } else if (code >= 3) {
@@ -290,12 +333,12 @@ constexpr int kRoiBwdLds = 150 * 1024;
 int roi_pool_bwd_lds(const void* grad_out, int code, const int32_t* argmax, const float* rois, int R, int PH, int PW,
                      int B, int H, int W, int C, void* grad_in, hipStream_t st, const void* grad_add) {
   const int HW = H * W;
-  int cw = 0;
-  if (C % 4 == 0 && (int64_t)HW * 4 * 4 <= kRoiBwdLds) cw = 4;
-  else if (C % 2 == 0 && (int64_t)HW * 2 * 4 <= kRoiBwdLds) cw = 2;
-  else if ((int64_t)HW * 4 <= kRoiBwdLds) cw = 1;
-  if (cw == 0 || B <= 0) return -1;
-  const size_t lds = (size_t)HW * cw * 4;
+  int cw = 0;  // channels per workgroup: the 8-B fixed-point slab of HW x cw must fit the LDS budget
+  if (C % 4 == 0 && (int64_t)HW * 4 * 8 <= kRoiBwdLds) cw = 4;
+  else if (C % 2 == 0 && (int64_t)HW * 2 * 8 <= kRoiBwdLds) cw = 2;
+  else if ((int64_t)HW * 8 <= kRoiBwdLds) cw = 1;
+  if (cw == 0 || B <= 0 || (int64_t)R * PH * PW > (1 << 20)) return -1;
+  const size_t lds = (size_t)HW * cw * 8;
   const dim3 grid(C / cw, B);
 #define MXR_ROI_BWD(CW_, T_)                                                                                   \
   do {                                                                                                        \

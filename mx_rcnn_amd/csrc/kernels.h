@@ -101,6 +101,7 @@ void roi_pool_fwd(const void* feat, int bf16, int B, int H, int W, int C, const 
 // LDS-accumulated backward straight into grad_in (B, H, W, C) of the grad_out dtype (code: 0 fp32,
 // 1 bf16, 2 fp16); -1 when the H x W slab does not fit LDS (use roi_pool_bwd)
 // grad_add (nullable, NHWC like grad_in): another gradient of the feature map, added in the kernel
+void col_part_fold(const float* part, int nparts, int C, float* out0, float* out1, hipStream_t st);
 int roi_pool_bwd_lds(const void* grad_out, int code, const int32_t* argmax, const float* rois, int R, int PH, int PW,
                      int B, int H, int W, int C, void* grad_in, hipStream_t st, const void* grad_add = nullptr);
 void roi_pool_bwd(const void* grad_out, int bf16, const int32_t* argmax, const float* rois, int R,
@@ -407,6 +408,9 @@ struct HeadBwdArgs {
   float* dwf[2] = {nullptr, nullptr};
   int64_t w_plane[2] = {0, 0};
 };
+// DP interference probes (probe.hip): k workgroups spinning on the real-time counter / copying
+void cu_spin(int nwg, int64_t ticks, hipStream_t st);
+void cu_copy(const float* src, float* dst, int64_t n, int nwg, hipStream_t st);
 // out = dy * [y > 0] * scale (bf16, n % 8 == 0; planes: y is the output's hi plane, dy / out hold
 // np planes `plane` = n apart)
 void relu_mask(const uint16_t* dy, const uint16_t* y, uint16_t* out, int64_t n, int64_t plane, float scale,

@@ -465,6 +465,12 @@ class _FusedUnitFn(torch.autograd.Function):
                 return tg, tb, True
             return tg, tb, False
 
+        def fold_bn(i, part, nparts, tg, tb):
+            """frozen BN(i)'s gamma / beta gradients from the epilogue's partial rows (fixed order)"""
+            gi = nconv + 4 * i
+            ext.bnb_part_fold(part, nparts, bnps[i][0].numel(), tg if need[gi] and not spec.fix[i] else None,
+                              tb if need[gi + 1] else None)
+
         def finish_bn(i, tg, tb, returned):
             if returned:
                 gi = nconv + 4 * i
@@ -492,7 +498,8 @@ class _FusedUnitFn(torch.autograd.Function):
             wf, wkw = dgrad_args(ctx.params[w_idx], ws[w_idx])
             tgt = grouped_target(wg)
             part, nparts = None, 0
-            if train:
+            det = not train and tg is not None and precision.deterministic()
+            if train or det:  # per-tile partial rows, folded in a fixed order
                 nparts = (_rows(bn_x) + 63) // 64
                 part = train_part(bn_x, nparts)
             if tgt is not None and dy.dtype == torch.bfloat16 and wf.dtype == torch.bfloat16:
@@ -511,6 +518,8 @@ class _FusedUnitFn(torch.autograd.Function):
                     wgrad(*wg)
                 r = ext.conv_igemm_fwd(dy, wf, None, 1, k - 1 - pad, False, 0, 0, None if train else dres, bwp[bn_i],
                                        beps[bn_i], bfix[bn_i], True, bn_x, dadd, tg, tb, bnb_part=part, **wkw)
+            if det:
+                fold_bn(bn_i, part, nparts, tg, tb)
             finish_bn(bn_i, tg, tb, ret)
             return train_finish(bn_i, r[0], bn_x, dres, part, nparts) if train else r[0]
 
@@ -519,7 +528,8 @@ class _FusedUnitFn(torch.autograd.Function):
             from .conv import dgrad_weight, strided_dgrad, strided_dgrad_parts
             tg, tb, ret = bn_targets(bn_i)
             part, nparts = None, 0
-            if train:
+            det = not train and tg is not None and precision.deterministic()
+            if train or det:
                 nparts = strided_dgrad_parts(bn_x.shape[0] // (x2 if x2 else 1), H, W, stride)
                 part = train_part(bn_x, nparts)
             elif tg is None:  # statistics not needed: accumulate into scratch
@@ -530,6 +540,8 @@ class _FusedUnitFn(torch.autograd.Function):
                               residual=None if train else dres, bn=bwp[bn_i], bn_eps=beps[bn_i],
                               bn_fix_gamma=bfix[bn_i], bnb_x=bn_x, dadd=dadd, dgamma=tg, dbeta=tb,
                               param=ctx.params[w_idx], bnb_part=part)
+            if det:
+                fold_bn(bn_i, part, nparts, tg, tb)
             finish_bn(bn_i, tg, tb, ret)
             return train_finish(bn_i, r[0], bn_x, dres, part, nparts) if train else r[0]
 

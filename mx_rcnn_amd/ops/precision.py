@@ -51,6 +51,21 @@ def default_name():
     return _DEFAULT['name']
 
 
+_DET = {'on': __import__('os').environ.get('MXR_NONDETERMINISTIC', '0') == '0'}
+
+
+def set_deterministic(on=True):
+    """Bitwise-reproducible gradients (default on; MXR_NONDETERMINISTIC=1 turns it off): the
+    frozen-BN gamma / beta column sums of the conv epilogues go to per-tile partial rows folded in
+    a fixed order (ConvEpi::bnb_part + bnb_part_fold) instead of fp32 atomics.  The RoI-pool and
+    BN-ReLU backward reductions are order-fixed unconditionally."""
+    _DET['on'] = bool(on)
+
+
+def deterministic():
+    return _DET['on']
+
+
 def x2_enabled():
     """Plane count of the active multi-plane mode (2: bf16x3, 3: fp32), 0 when off."""
     return _STATE['planes']

@@ -99,3 +99,113 @@ def test_roi_pool_gpu_repeatable(cuda):
     o1, o2 = _twice(lambda: ops.roi_pool(feat, rois, (7, 7), 1 / 16))
     torch.cuda.synchronize()
     assert torch.equal(o1, o2)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('P', [0, 3])
+def test_roi_pool_backward_gpu_bitwise(cuda, P):
+    """The RoI-pool backward sums every bin's dY into its pixel in 64-bit fixed point (per-channel
+    power-of-two scale): any arrival order gives the same bits, and the single rounding at the end
+    keeps the fp32-class result within fp32 rounding of the fp64 scatter.  300 heavily overlapping
+    RoIs (many bins per pixel), fp32 (P = 0) and fp32 triples (P = 3) with the RPN-side gradient
+    added."""
+    from mx_rcnn_amd.ops import need_ext, precision
+    ext = need_ext()
+    g = torch.Generator().manual_seed(8)
+    B, C, H, W, R = 2, 256, 38, 50, 300
+    feat = torch.randn(B, C, H, W, generator=g)
+    rois = _rois(g, R, B, H, W)
+    gout = torch.randn(R, C, 7, 7, generator=g) * torch.logspace(-3, 3, C)[None, :, None, None]
+    gadd = torch.randn(B, C, H, W, generator=g)
+
+    def enc(t):
+        t = t.to(cuda).contiguous(memory_format=torch.channels_last)
+        return precision.split(t, P).contiguous(memory_format=torch.channels_last) if P else t
+
+    _, arg = ext.roi_pool_fwd(enc(feat), rois.to(cuda), 7, 7, 1 / 16, P)
+    outs = [ext.roi_pool_bwd(enc(gout), arg, rois.to(cuda), B, H, W, enc(gadd), P) for _ in range(3)]
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    got = (precision.join(outs[0], P) if P else outs[0]).double().cpu().reshape(B, C, -1)
+    ref = gadd.double().reshape(B, C, -1).clone()
+    a = arg.cpu().reshape(R, C, -1).long()
+    go = gout.double().reshape(R, C, -1)
+    for r in range(R):
+        b = int(rois[r, 0])
+        m = a[r] >= 0
+        ref[b].view(-1).index_add_(0, (torch.arange(C)[:, None] * H * W + a[r].clamp_min(0))[m], go[r][m])
+    # per-channel relative error (the channels span six decades)
+    err = ((got - ref).abs().amax(2) / ref.abs().amax(2).clamp_min(1e-30)).max()
+    assert float(err) <= 2e-6, float(err)
+
+
+@pytest.mark.gpu
+def test_bn_relu_backward_gpu_bitwise(cuda):
+    """BN-ReLU backward (frozen statistics) column sums: thread-ordered in-block reduce + fixed-order
+    fold, bitwise across runs, and close to fp64."""
+    from mx_rcnn_amd.ops import need_ext
+    ext = need_ext()
+    g = torch.Generator().manual_seed(9)
+    N, C, H, W = 2, 64, 40, 56
+    x = torch.randn(N, C, H, W, generator=g)
+    dy = torch.randn(N, C, H, W, generator=g)
+    gam, bet, mu, var = torch.rand(C) + 0.5, torch.randn(C) * 0.1, torch.randn(C) * 0.1, torch.rand(C) + 0.5
+    p = [t.to(cuda) for t in (gam, bet, mu, var)]
+    xe = x.to(cuda).contiguous(memory_format=torch.channels_last)
+    de = dy.to(cuda).contiguous(memory_format=torch.channels_last)
+    runs = [ext.bn_relu_bwd(xe, de, *p, 2e-5, False, True, True, True, None, None, None, 0) for _ in range(3)]
+    torch.cuda.synchronize()
+    for r in runs[1:]:
+        for u, v in zip(r, runs[0]):
+            assert torch.equal(u, v)
+    s = gam.double() / torch.sqrt(var.double() + 2e-5)
+    pre = (x.double() - mu.double().view(1, -1, 1, 1)) * s.view(1, -1, 1, 1) + bet.double().view(1, -1, 1, 1)
+    gm = dy.double() * (pre > 0)
+    xhat = (x.double() - mu.double().view(1, -1, 1, 1)) / torch.sqrt(var.double() + 2e-5).view(1, -1, 1, 1)
+    dg = (gm * xhat).sum((0, 2, 3))
+    db = gm.sum((0, 2, 3))
+    assert float((runs[0][1].double().cpu() - dg).abs().max() / dg.abs().max()) <= 1e-5
+    assert float((runs[0][2].double().cpu() - db).abs().max() / db.abs().max()) <= 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('P', [0, 3])
+def test_frozen_bn_column_sums_partial_rows(cuda, P):
+    """Frozen-BN backward epilogue of a dgrad conv: the deterministic partial rows (bnb_part) +
+    fixed-order fold give the fp32-atomic path's dgamma / dbeta (to rounding) and the same dx bit
+    for bit, and repeat bitwise."""
+    from mx_rcnn_amd.ops import need_ext, precision
+    ext = need_ext()
+    g = torch.Generator().manual_seed(10 + P)
+    C, H, W, O = 256, 25, 42, 256
+    dy = torch.randn(1, O, H, W, generator=g)
+    w = torch.randn(C, O, 3, 3, generator=g) * 0.03
+    xbn = torch.randn(1, C, H, W, generator=g)
+    bn = [t.to(cuda) for t in (torch.rand(C) + 0.5, torch.randn(C) * 0.1, torch.randn(C) * 0.1, torch.rand(C) + 0.5)]
+
+    def enc(t):
+        t = t.to(cuda).contiguous(memory_format=torch.channels_last)
+        return (precision.split(t, P) if P else t.bfloat16()).contiguous(memory_format=torch.channels_last)
+
+    we = enc(w)
+    kw = {'x2': P, 'w_plane': we.numel() // P} if P else {}
+    wv = we[:C] if P else we
+    dge, xe = enc(dy), enc(xbn)
+    tg, tb = torch.zeros(C, device=cuda), torch.zeros(C, device=cuda)
+    ra = ext.conv_igemm_fwd(dge, wv, None, 1, 1, False, 23, 1, None, bn, 2e-5, False, True, xe, None, tg, tb, **kw)[0]
+    nparts = (H * W + 63) // 64
+    outs = []
+    for _ in range(2):
+        part = torch.empty(nparts * 2 * C, device=cuda)
+        dg, db = torch.zeros(C, device=cuda), torch.zeros(C, device=cuda)
+        r = ext.conv_igemm_fwd(dge, wv, None, 1, 1, False, 0, 0, None, bn, 2e-5, False, True, xe, None, None, None,
+                               bnb_part=part, **kw)[0]
+        ext.bnb_part_fold(part, nparts, C, dg, db)
+        outs.append((r, dg, db))
+    torch.cuda.synchronize()
+    for u, v in zip(outs[0], outs[1]):
+        assert torch.equal(u, v)
+    assert torch.equal(outs[0][0], ra)
+    assert torch.allclose(outs[0][1], tg, rtol=1e-5, atol=1e-5 * float(tg.abs().max()))
+    assert torch.allclose(outs[0][2], tb, rtol=1e-5, atol=1e-5 * float(tb.abs().max()))

@@ -1434,12 +1434,14 @@ std::vector<Tensor> proposal_topk(const Tensor& keys, const Tensor& boxes, int64
   TORCH_CHECK(P > 0 && P <= N, "proposal_topk: 0 < P <= N");
   DevGuard g(keys.device());
   auto o = keys.options();
+  Tensor ws = at::zeros({mxr::proposal_topk_ws_words(B, N)}, o.dtype(at::kInt));  // histograms: atomics
   Tensor wk = at::empty({(int64_t)B * P}, o.dtype(at::kInt));
   Tensor wi = at::empty({(int64_t)B * P}, o.dtype(at::kInt));
   Tensor sk = at::empty({B, P}, o);
   Tensor sb = at::empty({B, P, 4}, o);
   Tensor nv = at::empty({B}, o.dtype(at::kInt));
   TORCH_CHECK(mxr::proposal_topk(keys.data_ptr<float>(), boxes.data_ptr<float>(), B, N, (int)P,
+                                 reinterpret_cast<uint32_t*>(ws.data_ptr<int>()),
                                  reinterpret_cast<uint32_t*>(wk.data_ptr<int>()), wi.data_ptr<int>(),
                                  sk.data_ptr<float>(), sb.data_ptr<float>(), nv.data_ptr<int>(), cur_stream()) == 0,
               "proposal_topk failed");

@@ -1,14 +1,11 @@
 // Proposal pre-NMS top-k (SURVEY kernel K5; reference `rcnn/rpn/proposal.py:123-127`:
 // order = scores.ravel().argsort()[::-1][:pre_nms_topN]) -> the P best decoded boxes of each image
 // in descending score order, ties by lower anchor index (a stable descending sort), plus the
-// count of valid (finite-score) entries among them.  Two launches, deterministic, graph-safe;
-// replaces a full device radix sort of all anchors + gather + count.
+// count of valid (finite-score) entries among them.  Six launches, deterministic, graph-safe;
+// replaces a full device sort of all anchors + gather + count.
 //
-//   topk_select_kernel  grid B, 1024 threads, the image's keys held in registers (<= 64 per thread):
-//       radix-select the P-th largest key (4 passes of 8-bit LDS histograms over an order-preserving
-//       uint32 image of the float keys, wave-aggregated atomics), then collect the candidates:
-//       every key above it (one slot atomic per wave) and, in ANCHOR ORDER, just enough keys equal
-//       to it (row by row, ballot prefixes) -- exactly the stable top-P set.
+//   topk_hist_kernel<0..2>, topk_count_kernel, topk_write_kernel  grid (ceil(N / 2048), B): grid
+//       radix select of the P-th largest key and the stable top-P candidate set (below)
 //   topk_rank_kernel    grid (ceil(P/64), B): four lanes rank one candidate against all P of its
 //       image by counting (64-bit compares of (key, ~index) packed words streamed through LDS, the
 //       reads are broadcasts) and the first scatters key + box to its rank.
@@ -27,117 +24,249 @@ __device__ __forceinline__ float unord_key(uint32_t o) {
   return __uint_as_float(u);
 }
 
-constexpr int kTopkThreads = 1024;
-constexpr int kTopkPer = 64;  // keys held in registers per thread: N <= 65536
+// ---- grid radix select ------------------------------------------------------------------------
+// The P-th largest ordered key of each image, found digit by digit (bits 31..21, 20..10, 9..0)
+// by a GRID of workgroups per image: a single workgroup per image (the first version) walked the
+// 50 400 keys four times from one CU -- 160-340 us, latency bound, and 1 CU of 256 busy.  Here each
+// workgroup owns kTkChunk consecutive keys (8 per thread, anchor order = thread order), builds
+// its chunk's digit histogram in LDS (wave-aggregated atomics: one per distinct bin of a wave)
+// and adds it to the image's global histogram (integer atomics: order-independent, so
+// deterministic).  The next launch's workgroups each scan the finished histogram themselves (a
+// 256-thread block scan of 8 KB, identical in every workgroup: no extra launch, no global
+// hand-off but a state row that chunk 0 records for the later launches).  Then a count launch
+// (> T, == T, finite per chunk) and a write launch (chunk prefix + block scan: every key above T
+// and the first need_eq keys equal to T in anchor order -- exactly the stable top-P set) feed
+// the rank kernel below.
+constexpr int kTkThreads = 256;
+constexpr int kTkPer = 8;
+constexpr int kTkChunk = kTkThreads * kTkPer;
+constexpr int kTkBins = 2048;
 
-// thread t holds keys t, t + 1024, ... (coalesced loads, anchor order = (row j, thread t))
-__global__ void __launch_bounds__(kTopkThreads)
-topk_select_kernel(const float* __restrict__ keys, int N, int P, uint32_t* __restrict__ cand_key,
-                   int* __restrict__ cand_idx, int* __restrict__ n_valid) {
-  __shared__ unsigned int hist[256];
-  __shared__ unsigned int prefix_s, remain_s, slot_s, valid_s;
-  __shared__ unsigned int wcnt[kTopkThreads / 64];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const float* k = keys + (int64_t)b * N;
-  uint32_t* ck = cand_key + (int64_t)b * P;
-  int* ci = cand_idx + (int64_t)b * P;
-  const int rows = (N + kTopkThreads - 1) / kTopkThreads;
-  uint32_t u[kTopkPer];
-  unsigned int nv = 0;
+struct TkWs {  // int32 workspace of one call (zeroed by the caller)
+  uint32_t* hist;   // [B][3][kTkBins]
+  uint32_t* state;  // [B][3][2]: (prefix, remain) after digit pass p
+  uint32_t* cnt;    // [B][G][3]: (> T, == T, finite) per chunk
+};
+
+__host__ __device__ inline int64_t topk_ws_words(int B, int G) {
+  return (int64_t)B * 3 * kTkBins + (int64_t)B * 6 + (int64_t)B * G * 3;
+}
+
+__device__ __forceinline__ TkWs tk_ws(uint32_t* ws, int B, int G) {
+  TkWs w;
+  w.hist = ws;
+  w.state = ws + (int64_t)B * 3 * kTkBins;
+  w.cnt = w.state + (int64_t)B * 6;
+  return w;
+}
+
+// exclusive block scan of one value per thread (256 threads); returns the exclusive prefix, total in *tot
+__device__ __forceinline__ uint32_t tk_block_scan(uint32_t v, uint32_t* wsum, uint32_t* tot) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint32_t inc = v;
 #pragma unroll
-  for (int j = 0; j < kTopkPer; ++j) {
-    const int i = j * kTopkThreads + tid;
-    const float f = (j < rows && i < N) ? k[i] : -INFINITY;
-    nv += f > -INFINITY;
-    u[j] = (j < rows && i < N) ? ord_key(f) : 0u;  // 0: below every real key (-inf maps to 0x007fffff)
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint32_t t = __shfl_up(inc, o, 64);
+    if (lane >= o) inc += t;
   }
-  if (tid == 0) {
-    prefix_s = 0;
-    remain_s = (unsigned int)P;
-    slot_s = 0;
-    valid_s = 0;
+  if (lane == 63) wsum[wid] = inc;
+  __syncthreads();
+  uint32_t before = 0, all = 0;
+#pragma unroll
+  for (int w = 0; w < kTkThreads / 64; ++w) {
+    const uint32_t c = wsum[w];
+    if (w < wid) before += c;
+    all += c;
+  }
+  __syncthreads();  // wsum reusable
+  *tot = all;
+  return before + inc - v;
+}
+
+// largest bin with (keys in higher bins) < remain <= (keys in it and higher bins): the digit of
+// the remain-th largest key, and remain minus the keys above that bin
+__device__ __forceinline__ void tk_pick(const uint32_t* __restrict__ hist, int nbins, uint32_t remain,
+                                        uint32_t* wsum, uint32_t* s_bin, uint32_t* s_rem) {
+  const int per = nbins / kTkThreads;  // 8 or 4 bins per thread, thread 0 the highest
+  const int top = nbins - 1 - threadIdx.x * per;
+  uint32_t h[8];
+  uint32_t s = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    h[k] = k < per ? hist[top - k] : 0u;
+    s += h[k];
+  }
+  uint32_t tot;
+  uint32_t acc = tk_block_scan(s, wsum, &tot);
+  if (acc < remain && remain <= acc + s) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      if (k < per && acc + h[k] >= remain) {
+        *s_bin = (uint32_t)(top - k);
+        *s_rem = remain - acc;
+        break;
+      }
+      acc += h[k];
+    }
   }
   __syncthreads();
-  if (nv) atomicAdd(&valid_s, nv);
-  // 4 radix passes (most significant byte first) for the P-th largest ordered key
-  for (int pass = 3; pass >= 0; --pass) {
-    for (int i = tid; i < 256; i += kTopkThreads) hist[i] = 0;
-    __syncthreads();
-    const unsigned int pre = prefix_s;
-    const unsigned int hi_mask = pass == 3 ? 0u : (0xffffffffu << (8 * (pass + 1)));
+}
+
+__device__ __forceinline__ void tk_load(const float* __restrict__ k, int N, int i0, uint32_t (&u)[kTkPer],
+                                        uint32_t& valid_mask) {
+  valid_mask = 0;
 #pragma unroll
-    for (int j = 0; j < kTopkPer; ++j) {
-      if (j >= rows) break;
-      const bool in = u[j] != 0u && (u[j] & hi_mask) == (pre & hi_mask);
-      const unsigned int bin = (u[j] >> (8 * pass)) & 255u;
-      // one LDS atomic per DISTINCT bin of the wave (the scores cluster in a few bins; 64 lanes
-      // adding to one address would serialise on the CU's single LDS across all 16 waves)
-      uint64_t active = __ballot(in);
-      while (active) {
-        const int leader = __ffsll((long long)active) - 1;
-        const unsigned int b0 = __shfl(bin, leader, 64);
-        const uint64_t m = __ballot(bin == b0) & active;
-        if (lane == leader) atomicAdd(&hist[b0], (unsigned int)__popcll(m));
-        active &= ~m;
-      }
-    }
-    __syncthreads();
-    if (tid == 0) {
-      const unsigned int rem = remain_s;
-      unsigned int acc = 0;
-      int bin = 255;
-      for (; bin > 0; --bin) {
-        if (acc + hist[bin] >= rem) break;
-        acc += hist[bin];
-      }
-      remain_s = rem - acc;
-      prefix_s = pre | ((unsigned int)bin << (8 * pass));
-    }
-    __syncthreads();
-  }
-  const uint32_t T = prefix_s;
-  const unsigned int need_eq = remain_s;  // keys equal to T to take, lowest anchor index first
-  const unsigned int base = (unsigned int)P - need_eq;
-  unsigned int eq_done = 0;  // equal keys taken in earlier rows (uniform)
-#pragma unroll
-  for (int j = 0; j < kTopkPer; ++j) {
-    if (j >= rows) break;
-    const int i = j * kTopkThreads + tid;
-    // strictly greater: any order, one LDS atomic per wave
-    const bool gt = u[j] > T;
-    const uint64_t mg = __ballot(gt);
-    if (mg) {
-      unsigned int s0 = 0;
-      if (lane == __ffsll((long long)mg) - 1) s0 = atomicAdd(&slot_s, (unsigned int)__popcll(mg));
-      s0 = __shfl(s0, __ffsll((long long)mg) - 1, 64);
-      if (gt) {
-        const unsigned int s = s0 + (unsigned int)__popcll(mg & ((1ull << lane) - 1ull));
-        ck[s] = u[j];
-        ci[s] = i;
-      }
-    }
-    // equal to T: in anchor order within the row (wave prefix + per-wave counts through LDS)
-    if (eq_done < need_eq) {
-      const bool eq = u[j] == T && i < N;
-      const uint64_t me = __ballot(eq);
-      if (lane == 0) wcnt[wid] = (unsigned int)__popcll(me);
-      __syncthreads();
-      unsigned int before = eq_done, row_total = 0;
-      for (int w = 0; w < kTopkThreads / 64; ++w) {
-        const unsigned int c = wcnt[w];
-        if (w < wid) before += c;
-        row_total += c;
-      }
-      before += (unsigned int)__popcll(me & ((1ull << lane) - 1ull));
-      if (eq && before < need_eq) {
-        ck[base + before] = T;
-        ci[base + before] = i;
-      }
-      eq_done += row_total;
-      __syncthreads();  // wcnt is rewritten by the next row
+  for (int j = 0; j < kTkPer; ++j) {
+    const int i = i0 + j;
+    u[j] = 0u;  // below every real key (-inf maps to 0x007fffff)
+    if (i < N) {
+      const float f = k[i];
+      u[j] = ord_key(f);
+      valid_mask |= (f > -INFINITY ? 1u : 0u) << j;
     }
   }
-  if (tid == 0) n_valid[b] = (int)min((unsigned int)P, valid_s);
+}
+
+// the prefix / remain this launch starts from: digit passes 0..PASS-1 finished
+template <int PASS>
+__device__ __forceinline__ void tk_resolve(const TkWs& w, int b, int P, uint32_t* wsum, uint32_t& pre,
+                                           uint32_t& rem) {
+  __shared__ uint32_t s_bin, s_rem;
+  if (PASS == 0) {
+    pre = 0;
+    rem = (uint32_t)P;
+    return;
+  }
+  uint32_t* st = w.state + (int64_t)b * 6;
+  const uint32_t pre0 = PASS >= 2 ? st[2 * (PASS - 2)] : 0u;
+  const uint32_t rem0 = PASS >= 2 ? st[2 * (PASS - 2) + 1] : (uint32_t)P;
+  const int nbins = PASS - 1 == 2 ? 1024 : kTkBins;
+  const int shift = PASS - 1 == 0 ? 21 : (PASS - 1 == 1 ? 10 : 0);
+  tk_pick(w.hist + ((int64_t)b * 3 + PASS - 1) * kTkBins, nbins, rem0, wsum, &s_bin, &s_rem);
+  pre = pre0 | (s_bin << shift);
+  rem = s_rem;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    st[2 * (PASS - 1)] = pre;
+    st[2 * (PASS - 1) + 1] = rem;
+  }
+}
+
+template <int PASS>
+__global__ void __launch_bounds__(kTkThreads)
+topk_hist_kernel(const float* __restrict__ keys, int N, int P, uint32_t* __restrict__ ws) {
+  __shared__ uint32_t h[kTkBins];
+  __shared__ uint32_t wsum[kTkThreads / 64];
+  const int b = blockIdx.y, G = gridDim.x, lane = threadIdx.x & 63;
+  const TkWs w = tk_ws(ws, gridDim.y, G);
+  for (int i = threadIdx.x; i < kTkBins; i += kTkThreads) h[i] = 0u;
+  uint32_t pre, rem;
+  tk_resolve<PASS>(w, b, P, wsum, pre, rem);
+  uint32_t u[kTkPer], vm;
+  tk_load(keys + (int64_t)b * N, N, blockIdx.x * kTkChunk + threadIdx.x * kTkPer, u, vm);
+  const int shift = PASS == 0 ? 21 : (PASS == 1 ? 10 : 0);
+  const uint32_t dmask = PASS == 2 ? 1023u : 2047u;
+  const int i0 = blockIdx.x * kTkChunk + threadIdx.x * kTkPer;
+  __syncthreads();  // h zeroed
+#pragma unroll
+  for (int j = 0; j < kTkPer; ++j) {
+    const bool in = i0 + j < N && (PASS == 0 || (u[j] >> (shift + (PASS == 1 ? 11 : 10))) ==
+                                                    (pre >> (shift + (PASS == 1 ? 11 : 10))));
+    const uint32_t bin = (u[j] >> shift) & dmask;
+    uint64_t active = __ballot(in);
+    while (active) {  // one LDS atomic per distinct bin of the wave (clustered scores)
+      const int leader = __ffsll((long long)active) - 1;
+      const uint32_t b0 = __shfl(bin, leader, 64);
+      const uint64_t m = __ballot(bin == b0) & active;
+      if (lane == leader) atomicAdd(&h[b0], (uint32_t)__popcll(m));
+      active &= ~m;
+    }
+  }
+  __syncthreads();
+  uint32_t* gh = w.hist + ((int64_t)b * 3 + PASS) * kTkBins;
+  for (int i = threadIdx.x; i < (PASS == 2 ? 1024 : kTkBins); i += kTkThreads)
+    if (h[i]) atomicAdd(gh + i, h[i]);
+}
+
+// T and need_eq (the last digit pass), then this chunk's (> T, == T, finite) counts
+__global__ void __launch_bounds__(kTkThreads)
+topk_count_kernel(const float* __restrict__ keys, int N, int P, uint32_t* __restrict__ ws) {
+  __shared__ uint32_t wsum[kTkThreads / 64];
+  const int b = blockIdx.y, G = gridDim.x;
+  const TkWs w = tk_ws(ws, gridDim.y, G);
+  uint32_t T, need;
+  tk_resolve<3>(w, b, P, wsum, T, need);
+  uint32_t u[kTkPer], vm;
+  tk_load(keys + (int64_t)b * N, N, blockIdx.x * kTkChunk + threadIdx.x * kTkPer, u, vm);
+  const int i0 = blockIdx.x * kTkChunk + threadIdx.x * kTkPer;
+  uint32_t gt = 0, eq = 0;
+#pragma unroll
+  for (int j = 0; j < kTkPer; ++j) {
+    gt += u[j] > T;
+    eq += u[j] == T && i0 + j < N;
+  }
+  uint32_t tg, te, tv;
+  tk_block_scan(gt, wsum, &tg);
+  tk_block_scan(eq, wsum, &te);
+  tk_block_scan((uint32_t)__popc(vm), wsum, &tv);
+  if (threadIdx.x == 0) {
+    uint32_t* c = w.cnt + ((int64_t)b * G + blockIdx.x) * 3;
+    c[0] = tg;
+    c[1] = te;
+    c[2] = tv;
+  }
+}
+
+// candidates: keys > T at (chunks before + block prefix), the first need_eq keys == T (anchor
+// order) after them; chunk 0 also writes the image's valid count
+__global__ void __launch_bounds__(kTkThreads)
+topk_write_kernel(const float* __restrict__ keys, int N, int P, uint32_t* __restrict__ ws,
+                  uint32_t* __restrict__ cand_key, int* __restrict__ cand_idx, int* __restrict__ n_valid) {
+  __shared__ uint32_t wsum[kTkThreads / 64];
+  const int b = blockIdx.y, G = gridDim.x;
+  const TkWs w = tk_ws(ws, gridDim.y, G);
+  const uint32_t* st = w.state + (int64_t)b * 6;
+  const uint32_t T = st[4], need = st[5];
+  const uint32_t* c = w.cnt + (int64_t)b * G * 3;
+  uint32_t gbase = 0, ebase = 0;
+  for (int q = 0; q < (int)blockIdx.x; ++q) {
+    gbase += c[3 * q];
+    ebase += c[3 * q + 1];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    uint32_t nv = 0;
+    for (int q = 0; q < G; ++q) nv += c[3 * q + 2];
+    n_valid[b] = (int)min((uint32_t)P, nv);
+  }
+  if (ebase >= need && c[3 * blockIdx.x] == 0) return;  // nothing of this chunk is taken (uniform)
+  uint32_t u[kTkPer], vm;
+  const int i0 = blockIdx.x * kTkChunk + threadIdx.x * kTkPer;
+  tk_load(keys + (int64_t)b * N, N, i0, u, vm);
+  uint32_t gt = 0, eq = 0;
+#pragma unroll
+  for (int j = 0; j < kTkPer; ++j) {
+    gt += u[j] > T;
+    eq += u[j] == T && i0 + j < N;
+  }
+  uint32_t tot;
+  uint32_t gs = gbase + tk_block_scan(gt, wsum, &tot);
+  uint32_t es = ebase + tk_block_scan(eq, wsum, &tot);
+  const uint32_t base = (uint32_t)P - need;
+  uint32_t* ck = cand_key + (int64_t)b * P;
+  int* ci = cand_idx + (int64_t)b * P;
+#pragma unroll
+  for (int j = 0; j < kTkPer; ++j) {
+    if (u[j] > T) {
+      ck[gs] = u[j];
+      ci[gs] = i0 + j;
+      ++gs;
+    } else if (u[j] == T && i0 + j < N) {
+      if (es < need) {
+        ck[base + es] = T;
+        ci[base + es] = i0 + j;
+      }
+      ++es;
+    }
+  }
 }
 
 // 64 candidates per workgroup, 4 lanes per candidate (each counts a quarter of every tile), so a
@@ -183,10 +312,18 @@ topk_rank_kernel(const uint32_t* __restrict__ cand_key, const int* __restrict__ 
   }
 }
 
-int proposal_topk(const float* keys, const float* boxes, int B, int N, int P, uint32_t* ws_key, int* ws_idx,
-                  float* skeys, float* sboxes, int* n_valid, hipStream_t st) {
-  if (B <= 0 || N <= 0 || P <= 0 || P > N || N > kTopkThreads * kTopkPer) return -1;
-  topk_select_kernel<<<B, kTopkThreads, 0, st>>>(keys, N, P, ws_key, ws_idx, n_valid);
+int64_t proposal_topk_ws_words(int B, int N) { return topk_ws_words(B, (N + kTkChunk - 1) / kTkChunk); }
+
+int proposal_topk(const float* keys, const float* boxes, int B, int N, int P, uint32_t* ws, uint32_t* ws_key,
+                  int* ws_idx, float* skeys, float* sboxes, int* n_valid, hipStream_t st) {
+  if (B <= 0 || N <= 0 || P <= 0 || P > N || B > 65535) return -1;
+  const dim3 grid((N + kTkChunk - 1) / kTkChunk, B);
+  // ws: zeroed by the caller (histograms are accumulated with atomics)
+  topk_hist_kernel<0><<<grid, kTkThreads, 0, st>>>(keys, N, P, ws);
+  topk_hist_kernel<1><<<grid, kTkThreads, 0, st>>>(keys, N, P, ws);
+  topk_hist_kernel<2><<<grid, kTkThreads, 0, st>>>(keys, N, P, ws);
+  topk_count_kernel<<<grid, kTkThreads, 0, st>>>(keys, N, P, ws);
+  topk_write_kernel<<<grid, kTkThreads, 0, st>>>(keys, N, P, ws, ws_key, ws_idx, n_valid);
   topk_rank_kernel<<<dim3(div_up(P, 64), B), 256, 0, st>>>(ws_key, ws_idx, boxes, N, P, skeys, sboxes);
   return 0;
 }

@@ -320,9 +320,10 @@ int stem_conv(const uint16_t* x, const uint16_t* w, const StemArgs& a, uint16_t*
               int Wo, int KH, int KW, int stride, int pad, int relu, int code, hipStream_t st);
 
 // ---- proposal pre-NMS top-k (topk.hip): keys (B, N), boxes (B, N, 4) -> the P best in stable
-// descending order; ws_key / ws_idx: B * P each
-int proposal_topk(const float* keys, const float* boxes, int B, int N, int P, uint32_t* ws_key, int* ws_idx,
-                  float* skeys, float* sboxes, int* n_valid, hipStream_t st);
+// descending order; ws: proposal_topk_ws_words(B, N) ZEROED words, ws_key / ws_idx: B * P each
+int64_t proposal_topk_ws_words(int B, int N);
+int proposal_topk(const float* keys, const float* boxes, int B, int N, int P, uint32_t* ws, uint32_t* ws_key,
+                  int* ws_idx, float* skeys, float* sboxes, int* n_valid, hipStream_t st);
 
 // ---- test-time detection post-process (det_post.hip) ------------------------------------------
 // rois (B*R, 5) grouped by image, scores (B*R, C), deltas (B*R, 4C), im_info (B, 3), all fp32.

@@ -615,7 +615,8 @@ def test_nest_kernel_matches_reference(cuda):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('B,N,P,ties', [(1, 50400, 12000, False), (2, 50400, 6000, True), (3, 1000, 1000, True),
-                                        (1, 7000, 6000, False)])
+                                        (1, 7000, 6000, False), (8, 50400, 6000, False), (8, 50400, 12000, True),
+                                        (2, 50401, 50401, False)])
 def test_proposal_topk_matches_stable_sort(cuda, B, N, P, ties):
     """Radix-select + rank-by-counting top-P == stable descending sort truncated to P (keys, boxes,
     valid count), with heavy ties and -inf (filtered) entries."""
@@ -633,6 +634,50 @@ def test_proposal_topk_matches_stable_sort(cuda, B, N, P, ties):
     assert torch.equal(sk.cpu(), rk)
     assert torch.equal(sb.cpu(), rb)
     assert torch.equal(nv.cpu(), (rk > float('-inf')).sum(1).to(torch.int32))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('P', [6000, 12000])
+def test_proposal_topk_graph_replay(cuda, P):
+    """The grid radix top-k captured in a hipGraph (its zeroed workspace is a captured fill) and
+    replayed on new RPN-like scores (softmax foreground probabilities: most near 0, clustered top
+    bytes, ties) for B = 8, N = 50 400: every replay == the stable sort."""
+    from mx_rcnn_amd.ops import need_ext
+    ext = need_ext()
+    B, N = 8, 50400
+    g = torch.Generator().manual_seed(P)
+    keys = torch.empty(B, N, device=cuda)
+    boxes = (torch.rand(B, N, 4, generator=g) * 800).to(cuda)
+
+    def fill(seed):
+        gg = torch.Generator().manual_seed(seed)
+        logit = torch.randn(B, N, 2, generator=gg) * 3
+        k = torch.softmax(logit, 2)[..., 1]
+        k = (k * 4096).round() / 4096  # ties
+        k[torch.rand(B, N, generator=gg) < 0.1] = float('-inf')
+        keys.copy_(k)
+        return k
+
+    fill(0)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(2):
+            ext.proposal_topk(keys, boxes, P)
+    torch.cuda.current_stream().wait_stream(s)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        sk, sb, nv = ext.proposal_topk(keys, boxes, P)
+    for seed in (1, 2, 3):
+        k = fill(seed)
+        graph.replay()
+        torch.cuda.synchronize()
+        rk, order = torch.sort(k, dim=1, descending=True, stable=True)
+        rk, order = rk[:, :P], order[:, :P]
+        rb = torch.gather(boxes.cpu(), 1, order[..., None].expand(-1, -1, 4))
+        assert torch.equal(sk.cpu(), rk)
+        assert torch.equal(sb.cpu(), rb)
+        assert torch.equal(nv.cpu(), (rk > float('-inf')).sum(1).to(torch.int32))
 
 
 @pytest.mark.gpu

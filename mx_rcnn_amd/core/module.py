@@ -198,6 +198,7 @@ class MutableModule(object):
                 # (sgd_step(refresh=False)); a backward through this API must see the updated filters
                 self.trainer.store.refresh_dgrad_cache()
                 self.trainer.store.zero_grad()
+                self.trainer.grads_dirty = True  # update() leaves them written (the monitor reads them)
                 self.trainer.reducer.prepare()
                 self._outputs = self.trainer.forward(b)
             else:
@@ -224,7 +225,16 @@ class MutableModule(object):
         eager = (not self.use_graph or prof.enabled() or
                  (self._monitor is not None and self._monitor.activated))
         if eager:
-            self._outputs = self.trainer.step(data_batch)
+            t = self.trainer
+            watched = self._monitor is not None and self._monitor.activated
+            fused = t.fused_clear
+            t.fused_clear = fused and not watched  # a norm monitor reads the gradients after the update
+            try:
+                self._outputs = t.step(data_batch)
+            finally:
+                t.fused_clear = fused
+                if watched:
+                    t.grads_dirty = True
             return self._outputs
         key = tuple((k, tuple(v.shape)) for k, v in sorted(data_batch.items()) if torch.is_tensor(v))
         g = self._graphs.get(key)

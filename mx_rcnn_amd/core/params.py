@@ -346,15 +346,17 @@ class FlatParamStore:
     def grad_buffers(self):
         return [g.grad for g in self.groups]
 
-    def sgd_step(self, lr, momentum=0.9, wd=0.0005, rescale=1.0, clip=-1.0, grad_for=None, refresh=True):
+    def sgd_step(self, lr, momentum=0.9, wd=0.0005, rescale=1.0, clip=-1.0, grad_for=None, refresh=True,
+                 clear=False):
         """``lr``: 1-element fp32 device tensor.  ``grad_for(group)`` picks the gradient source
         (the reducer's fp32 all-reduce buffer under data parallelism; default ``group.grad``).
         ``refresh=False``: the caller rebuilds the dgrad cache itself (Trainer.step_body does, at
-        the start of the next step, concurrently with its forward pass)."""
+        the start of the next step, concurrently with its forward pass).  ``clear``: the update
+        kernel zeroes each group's gradient buffer after reading it (replaces zero_grad)."""
         for g in self.groups:
             grad = grad_for(g) if grad_for is not None else g.grad
             sgd_momentum_(g.master, g.mom, grad, lr, momentum, wd if g.decay else 0.0, rescale, clip, g.shadow,
-                          planes=g.x2 or 1)
+                          planes=g.x2 or 1, zero=g.grad if clear else None)
         if refresh:
             self.refresh_dgrad_cache()
 

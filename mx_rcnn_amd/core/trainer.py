@@ -69,6 +69,11 @@ class Trainer:
             if isinstance(m, Linear):
                 m.rng_step = self.rng_step
         self.nonfinite = torch.zeros((), dtype=torch.int32, device=dev)
+        # fused gradient clear (SGD kernel zeroes what it read; MXR_FUSED_GRAD_CLEAR=0: a fill per
+        # step); grads_dirty: a path left the flat gradients written (step API, monitored step,
+        # an exception mid-step) -- the next step clears them first
+        self.fused_clear = os.environ.get('MXR_FUSED_GRAD_CLEAR', '1') != '0'
+        self.grads_dirty = False
         self.fault = torch.ones((), dtype=torch.float32, device=dev) if os.environ.get('MXR_FAULT_INJECT') else None
         # the loss-combine kernel bumps the counter (one launch for loss, objective and guard);
         # with fault injection the guard must see the poisoned objective, so the trainer keeps it
@@ -107,12 +112,17 @@ class Trainer:
     def _step_body(self, b):
         # the dgrad filter cache of the current weights, built beside the forward pass
         # (and the gradient clear), joined before the first backward kernel
+        # gradient clear: the previous step's update kernels zeroed the buffers they consumed
+        # (fused_clear), so only a step after a path that left them written clears them here
+        dirty = self.grads_dirty or not self.fused_clear
+        self.grads_dirty = True  # until this step's update has run
         zg_side = os.environ.get('MXR_ZERO_GRAD_SIDE', '1') != '0'
-        cache_join = self.store.refresh_dgrad_cache_async(zero_grad=zg_side)
-        if not zg_side:
+        cache_join = self.store.refresh_dgrad_cache_async(zero_grad=zg_side and dirty)
+        if dirty and not zg_side:
             self.store.zero_grad()
         # the optimizer runs bucket by bucket under the backward pass (parallel/reducer.py)
-        self.reducer.prepare(sgd=(self.lr_t, self.momentum, self.wd, self.rescale, self.clip))
+        self.reducer.prepare(sgd=(self.lr_t, self.momentum, self.wd, self.rescale, self.clip),
+                             clear=self.fused_clear)
         # a model that starts part of its backward inside forward (the e2e graph's early RPN
         # backward) joins the filter cache first
         self.model.pre_backward = cache_join
@@ -139,7 +149,8 @@ class Trainer:
         with prof.range('sgd'):
             if not self.reducer.sgd_applied:
                 self.store.sgd_step(self.lr_t, self.momentum, self.wd, self.rescale, self.clip,
-                                    grad_for=self.reducer.grad_for, refresh=False)
+                                    grad_for=self.reducer.grad_for, refresh=False, clear=self.fused_clear)
+        self.grads_dirty = not self.fused_clear
         # Return detached outputs: a caller holding the loss would otherwise keep this step's
         # autograd graph (and its AccumulateGrad nodes, bound to this step's stream) alive, and a
         # later hipGraph capture on a side stream then syncs against that stream and dies in
@@ -254,5 +265,8 @@ class GraphedStep:
                 if torch.is_tensor(v) and k in self.static:
                     self.static[k].copy_(v, non_blocking=True)
         self.t.update_lr()
+        if self.t.grads_dirty:  # the graph holds no gradient clear (captured after a fused-clear step)
+            self.t.store.zero_grad()
         self.graph.replay()
+        self.t.grads_dirty = not self.t.fused_clear
         return self.out

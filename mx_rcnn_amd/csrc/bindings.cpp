@@ -535,7 +535,8 @@ Tensor loss_combine(std::vector<Tensor> terms, std::vector<double> weights, c10:
 
 // ---- optimizer -------------------------------------------------------------------------
 void sgd_momentum(Tensor w, Tensor mom, const Tensor& grad, const Tensor& lr, double momentum, double wd,
-                  double rescale, double clip, c10::optional<Tensor> w_bf16, int64_t planes) {
+                  double rescale, double clip, c10::optional<Tensor> w_bf16, int64_t planes,
+                  c10::optional<Tensor> zero) {
   CHECK_DEV(w); CHECK_F32(w); CHECK_CONTIG(w); CHECK_DEV(mom); CHECK_F32(mom); CHECK_CONTIG(mom);
   CHECK_DEV(grad); CHECK_CONTIG(grad); CHECK_DEV(lr); CHECK_F32(lr);
   TORCH_CHECK(w.numel() == mom.numel() && w.numel() == grad.numel(), "size mismatch");
@@ -551,10 +552,19 @@ void sgd_momentum(Tensor w, Tensor mom, const Tensor& grad, const Tensor& lr, do
     wb = reinterpret_cast<uint16_t*>(w_bf16->data_ptr());
     if (planes > 1) x2_plane = w_bf16->numel() / planes;
   }
+  void* zp = nullptr;
+  int zb = 0;
+  if (zero.has_value() && zero->defined()) {  // the gradient buffer to clear once consumed
+    TORCH_CHECK(zero->is_contiguous() && zero->numel() == w.numel() && zero->device() == w.device() &&
+                    (zero->scalar_type() == at::kFloat || zero->scalar_type() == at::kBFloat16),
+                "zero: contiguous fp32 / bf16 of numel elements");
+    zp = zero->data_ptr();
+    zb = is_bf16(*zero);
+  }
   DevGuard g(w.device());
   mxr::sgd_momentum(w.data_ptr<float>(), mom.data_ptr<float>(), grad.data_ptr(), is_bf16(grad), w.numel(),
                     lr.data_ptr<float>(), (float)momentum, (float)wd, (float)rescale, (float)clip, wb, cur_stream(),
-                    x2_plane, planes == 3 ? 1 : 0);
+                    x2_plane, planes == 3 ? 1 : 0, zp, zb);
 }
 
 // ---- BN + ReLU -------------------------------------------------------------------------
@@ -2086,7 +2096,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("loss_combine", &loss_combine, py::arg("terms"), py::arg("weights"), py::arg("nonfinite") = py::none());
   m.def("sgd_momentum", &sgd_momentum, py::arg("w"), py::arg("mom"), py::arg("grad"), py::arg("lr"),
         py::arg("momentum"), py::arg("wd"), py::arg("rescale"), py::arg("clip"), py::arg("w_bf16") = py::none(),
-        py::arg("planes") = 1);
+        py::arg("planes") = 1, py::arg("zero") = py::none());
   m.def("bn_relu_fwd", &bn_relu_fwd, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("mean"), py::arg("var"),
         py::arg("eps"), py::arg("fix_gamma"), py::arg("relu"), py::arg("x2") = 0);
   m.def("bn_relu_bwd", &bn_relu_bwd, py::arg("x"), py::arg("dy"), py::arg("gamma"), py::arg("beta"),

@@ -3,7 +3,11 @@
 // w += mom).  One launch per weight-decay group over the whole flat buffer, 4 elements per
 // lane with 16-B loads.  The learning rate is read from device memory so the update can be
 // captured in a hipGraph and replayed while the schedule changes.  The kernel also writes
-// the bf16 shadow of the new weights that the next forward consumes (fusing the cast).
+// the bf16 shadow of the new weights that the next forward consumes (fusing the cast), and with
+// `zero` clears the gradient buffer it consumed (no __restrict__ on either: they may alias, and
+// every element is loaded before its zero is stored) (fp32 or bf16, may differ from `grad`: under data
+// parallelism the kernel reads the fp32 wire buffer and clears the bf16 one), so the next step's
+// gradient writers start from zero without a separate fill pass over every gradient.
 #include "common.h"
 #include "../kernels.h"
 #include <algorithm>
@@ -21,9 +25,9 @@ __device__ __forceinline__ float sgd_one(float w, float& m, float g, float lr, f
 
 template <bool GBF16>
 __global__ void __launch_bounds__(256)
-sgd_kernel(float* __restrict__ w, float* __restrict__ mom, const void* __restrict__ grad, int64_t n,
+sgd_kernel(float* __restrict__ w, float* __restrict__ mom, const void* grad, int64_t n,
            const float* __restrict__ lr_p, float mu, float wd, float rescale, float clip, uint16_t* __restrict__ wb,
-           int64_t x2_plane, int x3) {
+           int64_t x2_plane, int x3, void* zp, int zbf16) {
   const float lr = *lr_p;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * 4;
   for (int64_t i = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4; i < n; i += stride) {
@@ -36,6 +40,10 @@ sgd_kernel(float* __restrict__ w, float* __restrict__ mom, const void* __restric
         gv = make_float4(bf16_to_f32(gb.x), bf16_to_f32(gb.y), bf16_to_f32(gb.z), bf16_to_f32(gb.w));
       } else {
         gv = *reinterpret_cast<const float4*>(static_cast<const float*>(grad) + i);
+      }
+      if (zp) {
+        if (zbf16) *reinterpret_cast<ushort4*>(static_cast<uint16_t*>(zp) + i) = make_ushort4(0, 0, 0, 0);
+        else *reinterpret_cast<float4*>(static_cast<float*>(zp) + i) = make_float4(0.f, 0.f, 0.f, 0.f);
       }
       wv.x = sgd_one(wv.x, mv.x, gv.x, lr, mu, wd, rescale, clip);
       wv.y = sgd_one(wv.y, mv.y, gv.y, lr, mu, wd, rescale, clip);
@@ -53,6 +61,10 @@ sgd_kernel(float* __restrict__ w, float* __restrict__ mom, const void* __restric
     } else {
       for (int64_t k = i; k < n; ++k) {
         const float g = GBF16 ? bf16_to_f32(static_cast<const uint16_t*>(grad)[k]) : static_cast<const float*>(grad)[k];
+        if (zp) {
+          if (zbf16) static_cast<uint16_t*>(zp)[k] = 0;
+          else static_cast<float*>(zp)[k] = 0.f;
+        }
         float m = mom[k];
         const float nw = sgd_one(w[k], m, g, lr, mu, wd, rescale, clip);
         w[k] = nw;
@@ -84,9 +96,9 @@ __device__ __forceinline__ void sgd_st(T* p, T v) {
 
 template <bool GBF16, bool NT>
 __global__ void __launch_bounds__(256)
-sgd8_kernel(float* __restrict__ w, float* __restrict__ mom, const void* __restrict__ grad, int64_t n,
+sgd8_kernel(float* __restrict__ w, float* __restrict__ mom, const void* grad, int64_t n,
             const float* __restrict__ lr_p, float mu, float wd, float rescale, float clip, uint16_t* __restrict__ wb,
-            int64_t x2_plane, int x3) {
+            int64_t x2_plane, int x3, void* zp, int zbf16) {
   const float lr = *lr_p;
   const int64_t n8 = n & ~(int64_t)7;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x * 8;
@@ -112,6 +124,14 @@ sgd8_kernel(float* __restrict__ w, float* __restrict__ mom, const void* __restri
         g[k + 4] = g1[k];
       }
     }
+    if (zp) {
+      if (zbf16) {
+        sgd_st<NT>(reinterpret_cast<sgd_u4*>(static_cast<uint16_t*>(zp) + i), sgd_u4{0u, 0u, 0u, 0u});
+      } else {
+        sgd_st<NT>(reinterpret_cast<sgd_f4*>(static_cast<float*>(zp) + i), sgd_f4{0.f, 0.f, 0.f, 0.f});
+        sgd_st<NT>(reinterpret_cast<sgd_f4*>(static_cast<float*>(zp) + i + 4), sgd_f4{0.f, 0.f, 0.f, 0.f});
+      }
+    }
     float wv[8], mv[8];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -134,6 +154,10 @@ sgd8_kernel(float* __restrict__ w, float* __restrict__ mom, const void* __restri
   if (blockIdx.x == 0 && threadIdx.x < n - n8) {  // the < 8 trailing elements
     const int64_t k = n8 + threadIdx.x;
     const float gk = GBF16 ? bf16_to_f32(static_cast<const uint16_t*>(grad)[k]) : static_cast<const float*>(grad)[k];
+    if (zp) {
+      if (zbf16) static_cast<uint16_t*>(zp)[k] = 0;
+      else static_cast<float*>(zp)[k] = 0.f;
+    }
     float m = mom[k];
     const float nw = sgd_one(w[k], m, gk, lr, mu, wd, rescale, clip);
     w[k] = nw;
@@ -154,13 +178,14 @@ static int sgd_variant() {
 
 void sgd_momentum(float* w, float* mom, const void* grad, int grad_bf16, int64_t n, const float* lr, float momentum,
                   float wd, float rescale, float clip, uint16_t* w_bf16, hipStream_t st, int64_t x2_plane,
-                  int x3) {
+                  int x3, void* zero, int zero_bf16) {
   if (n == 0) return;
   const int var = sgd_variant();
   const auto a16 = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; };
-  if (var > 0 && x2_plane % 8 == 0 && a16(w) && a16(mom) && a16(grad) && (w_bf16 == nullptr || a16(w_bf16))) {
+  if (var > 0 && x2_plane % 8 == 0 && a16(w) && a16(mom) && a16(grad) && (w_bf16 == nullptr || a16(w_bf16)) &&
+      (zero == nullptr || a16(zero))) {
     const int blocks = (int)std::min<int64_t>(std::max<int64_t>(div_up((n + 7) / 8, 256), 1), 256 * 8);
-#define MXR_SGD8(GB, NT) sgd8_kernel<GB, NT><<<blocks, 256, 0, st>>>(w, mom, grad, n, lr, momentum, wd, rescale, clip, w_bf16, x2_plane, x3)
+#define MXR_SGD8(GB, NT) sgd8_kernel<GB, NT><<<blocks, 256, 0, st>>>(w, mom, grad, n, lr, momentum, wd, rescale, clip, w_bf16, x2_plane, x3, zero, zero_bf16)
     if (grad_bf16) { if (var == 2) MXR_SGD8(true, true); else MXR_SGD8(true, false); }
     else { if (var == 2) MXR_SGD8(false, true); else MXR_SGD8(false, false); }
 #undef MXR_SGD8
@@ -168,9 +193,11 @@ void sgd_momentum(float* w, float* mom, const void* grad, int grad_bf16, int64_t
   }
   const int blocks = (int)std::min<int64_t>(div_up((n + 3) / 4, 256), 256 * 8);
   if (grad_bf16)
-    sgd_kernel<true><<<blocks, 256, 0, st>>>(w, mom, grad, n, lr, momentum, wd, rescale, clip, w_bf16, x2_plane, x3);
+    sgd_kernel<true><<<blocks, 256, 0, st>>>(w, mom, grad, n, lr, momentum, wd, rescale, clip, w_bf16, x2_plane, x3,
+                                                   zero, zero_bf16);
   else
-    sgd_kernel<false><<<blocks, 256, 0, st>>>(w, mom, grad, n, lr, momentum, wd, rescale, clip, w_bf16, x2_plane, x3);
+    sgd_kernel<false><<<blocks, 256, 0, st>>>(w, mom, grad, n, lr, momentum, wd, rescale, clip, w_bf16, x2_plane, x3,
+                                                   zero, zero_bf16);
 }
 
 }  // namespace mxr

@@ -150,7 +150,9 @@ void loss_combine(const LossTerms& t, float* out, int32_t* nonfinite, hipStream_
 void sgd_momentum(float* w, float* mom, const void* grad, int grad_bf16, int64_t n, const float* lr,
                   float momentum, float wd, float rescale, float clip, uint16_t* w_bf16, hipStream_t st,
                   int64_t x2_plane = 0,   // x2_plane > 0: w_bf16 is an x2 hi / lo pair, lo x2_plane elements on
-                  int x3 = 0);            // with x2_plane: an x3 triple (mid, hi, lo) x2_plane apart
+                  int x3 = 0,             // with x2_plane: an x3 triple (mid, hi, lo) x2_plane apart
+                  void* zero = nullptr,   // cleared after reading (the consumed gradient buffer, n elements)
+                  int zero_bf16 = 0);
 
 // ---- frozen BN + ReLU (bn_act.hip) -----------------------------------------
 // NHWC x (M rows, C channels) bf16/fp32; y = relu((x-mean)*rsqrt(var+eps)*gamma + beta).

@@ -5,17 +5,27 @@ import torch
 from ._ext import ext_available, need_ext
 
 
-def sgd_momentum_(w, mom, grad, lr, momentum=0.9, wd=0.0, rescale=1.0, clip=-1.0, w_bf16=None, planes=1):
+def sgd_momentum_(w, mom, grad, lr, momentum=0.9, wd=0.0, rescale=1.0, clip=-1.0, w_bf16=None, planes=1, zero=None):
     """In-place update of flat fp32 ``w``/``mom`` from ``grad`` (fp32 or bf16).
 
     ``lr`` is a 1-element fp32 device tensor (read in-kernel: graph-replay safe).
     ``w_bf16`` (optional) receives the bf16 copy of the updated weights, or with ``planes`` 2 / 3
     their bf16x3 pair / fp32 triple (ops/precision.py), planes ``w_bf16.numel() // planes`` apart.
+    ``zero`` (optional, fp32 or bf16, w's size; may be ``grad`` itself): cleared after it is read,
+    so the next step's gradient writers start from zero without a separate fill.
     """
     if w.is_cuda:
         need_ext().sgd_momentum(w, mom, grad, lr, float(momentum), float(wd), float(rescale), float(clip), w_bf16,
-                                int(planes))
+                                int(planes), zero)
         return
+    try:
+        _sgd_host(w, mom, grad, lr, momentum, wd, rescale, clip, w_bf16, planes)
+    finally:
+        if zero is not None:
+            zero.zero_()
+
+
+def _sgd_host(w, mom, grad, lr, momentum, wd, rescale, clip, w_bf16, planes):
     if ext_available() and w.dtype == torch.float32 and w.is_contiguous() and mom.is_contiguous():
         # C++ twin (host_ops.h): one fused, thread-parallel pass instead of five tensor ops
         need_ext().sgd_momentum_cpu(w, mom, grad, float(lr), float(momentum), float(wd), float(rescale), float(clip))

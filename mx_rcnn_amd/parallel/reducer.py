@@ -80,6 +80,7 @@ class BucketReducer:
         self.buckets = []
         self._param_bucket = {}
         self._sgd = None
+        self._clear = False
         self._opt_stream = None
         self.sgd_applied = False
         if not (self.dp or self.sgd_capable):
@@ -157,13 +158,16 @@ class BucketReducer:
             if b.work is not None:
                 b.work.wait()  # the optimizer stream waits for this bucket's collective
             sgd_momentum_(g.master[s:e], g.mom[s:e], self.grad_for(g)[s:e], lr, mu, wd if g.decay else 0.0, rescale,
-                          clip, None if g.shadow is None else g.shadow[s:e])
+                          clip, None if g.shadow is None else g.shadow[s:e],
+                          zero=g.grad[s:e] if self._clear else None)
         b.updated = True
 
-    def prepare(self, sgd=None):
+    def prepare(self, sgd=None, clear=False):
         """Call before backward: reset per-bucket counters.  ``sgd=(lr_tensor, momentum, wd,
-        rescale, clip)`` enables the overlapped optimizer for this step (GPU only)."""
+        rescale, clip)`` enables the overlapped optimizer for this step (GPU only); ``clear``: its
+        update kernels zero the gradient buffers they consumed."""
         self._sgd = sgd if (sgd is not None and self.sgd_capable and self.buckets) else None
+        self._clear = bool(clear)
         self.sgd_applied = False
         for b in self.buckets:
             b.pending = len(b.names)

@@ -252,6 +252,42 @@ def test_sgd_gpu(cuda):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize('variant', ['0', '2'])
+def test_sgd_gpu_fused_gradient_clear(cuda, variant):
+    """The update kernel zeroes the gradient buffer it consumed: in place (zero is grad itself, the
+    1-GPU / fp32-wire case: every element read before its zero lands) and a separate bf16 buffer
+    (the DP bf16 case: the kernel reads the fp32 wire buffer); the update itself is unchanged.
+    Both kernel variants (MXR_SGD=0 4-wide, 2 = 8-wide nontemporal; n not a multiple of 8)."""
+    import subprocess
+    import sys
+    code = """
+import torch
+from mx_rcnn_amd import ops
+g = torch.Generator().manual_seed(3)
+n = 100003
+w = torch.randn(n, generator=g).cuda(); m = (torch.randn(n, generator=g) * 0.01).cuda()
+gr = (torch.randn(n, generator=g) * 2).cuda(); lr = torch.tensor([0.01]).cuda()
+w0, m0 = w.clone(), m.clone()
+ops.sgd_momentum_(w0, m0, gr.clone(), lr, 0.9, 5e-4, 1.0, 1.0)
+g1 = gr.clone()
+ops.sgd_momentum_(w, m, g1, lr, 0.9, 5e-4, 1.0, 1.0, zero=g1)
+assert torch.equal(w, w0) and torch.equal(m, m0), 'update changed'
+assert not g1.any(), 'fp32 in-place clear'
+w2, m2 = w0.clone(), m0.clone(); w3, m3 = w0.clone(), m0.clone()
+gb = torch.randn(n, generator=g).cuda().bfloat16()
+ops.sgd_momentum_(w3, m3, gr, lr, 0.9, 5e-4, 1.0, 1.0)
+ops.sgd_momentum_(w2, m2, gr, lr, 0.9, 5e-4, 1.0, 1.0, zero=gb)
+assert torch.equal(w2, w3) and not gb.any(), 'bf16 side clear'
+print('ok')
+"""
+    env = dict(__import__('os').environ, MXR_SGD=variant)
+    r = subprocess.run([sys.executable, '-c', code], env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT,
+                       text=True, timeout=200, cwd=__import__('os').path.dirname(__import__('os').path.dirname(
+                           __import__('os').path.abspath(__file__))))
+    assert r.returncode == 0 and 'ok' in r.stdout, r.stdout[-2000:]
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize('shape', [
     # N, Cin, H, W, Cout, k, s, p, bias, relu
     (1, 64, 23, 37, 64, 3, 1, 1, False, False),

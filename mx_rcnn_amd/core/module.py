@@ -157,6 +157,15 @@ class MutableModule(object):
         except TypeError:
             return self.model.arg_params()
 
+    def _model_arg_shapes(self):
+        fn = getattr(self.model, 'arg_shapes', None)
+        if fn is None:
+            return {}
+        try:
+            return fn(self._graph_mode())
+        except TypeError:
+            return fn()
+
     def _model_aux(self):
         try:
             return self.model.aux_params(self._graph_mode())
@@ -300,6 +309,8 @@ class MutableModule(object):
             arg = {k: v.detach().float().cpu().numpy() for k, v in self.trainer.store.state_arrays().items()}
         else:
             arg = {k: v.detach().float().cpu().numpy() for k, v in self._model_args().items()}
+        shapes = self._model_arg_shapes()
+        arg = {k: (v.reshape(shapes[k]) if k in shapes else v) for k, v in arg.items()}  # checkpoint layout
         aux = {}
         for k, v in self._model_aux().items():
             t = v.detach().float().clone()

@@ -169,6 +169,8 @@ class FlatParamStore:
                 p = self.params[n]
                 if bt and not (len(shape) == 4 and shape[2] > 1 and int(getattr(m, 'stride', 1)) > 1):
                     continue
+                if getattr(m, 'in_shape', None) is not None:  # an FC held as a (C, H, W) filter: GEMM rows
+                    continue
                 if g.x2:
                     self._x2_dgrad_entry(g, p, off, numel, shape, cl, srcs, dsts)
                     continue

@@ -116,6 +116,13 @@ class FasterRCNN(nn.Module):
             out.update(m.mx_args())
         return out
 
+    def arg_shapes(self, mode=None):
+        """MXNet checkpoint shapes of arg_params() (Linear(in_shape=...) weights flattened)."""
+        out = {}
+        for m in self.mx_layers(mode):
+            out.update(m.mx_arg_shapes())
+        return out
+
     def aux_params(self, mode=None):
         out = {}
         for m in self.mx_layers(mode):

@@ -29,6 +29,11 @@ class MxLayer(nn.Module):
     def mx_aux(self):
         return {}
 
+    def mx_arg_shapes(self):
+        """MXNet shapes of the arguments (checkpoint / converter layout; a parameter may be held in
+        another logical shape of the same elements, e.g. Linear(in_shape=...))."""
+        return {k: tuple(v.shape) for k, v in self.mx_args().items()}
+
 
 def _w(t, ref):
     from ..ops import precision
@@ -56,21 +61,40 @@ class Linear(MxLayer):
     following ReLU and Dropout (ops/fc.py).  ``rng_step`` (an int64 device tensor set by the
     Trainer and advanced every update) drives the counter-based dropout mask."""
 
-    def __init__(self, name, cin, cout, bias=True):
+    def __init__(self, name, cin, cout, bias=True, in_shape=None):
         super().__init__()
         self.mx_name = name
-        self.weight = nn.Parameter(torch.empty(cout, cin))
+        # in_shape (C, H, W): the layer flattens a (C, H, W) map (VGG fc6 on the 7x7 pooled RoIs).
+        # Its weight is then held as the (cout, C, H, W) filter of the same elements -- stored
+        # channels_last by the parameter store, i.e. in (h, w, c) column order, which is the order of
+        # the pooled map's channels_last rows: the GEMM reads both as plain row-major matrices with no
+        # flatten copy of the activations or their gradient (checkpoints keep (cout, cin))
+        self.in_shape = tuple(in_shape) if in_shape is not None else None
+        if self.in_shape is not None:
+            assert cin == self.in_shape[0] * self.in_shape[1] * self.in_shape[2]
+            self.weight = nn.Parameter(torch.empty(cout, *self.in_shape))
+        else:
+            self.weight = nn.Parameter(torch.empty(cout, cin))
+        self.cin, self.cout = cin, cout
         self.bias = nn.Parameter(torch.zeros(cout)) if bias else None
         nn.init.normal_(self.weight, 0, 0.01)
         self.rng_step = None
         self._seed = None
+
+    def mx_arg_shapes(self):
+        out = super().mx_arg_shapes()
+        out['%s_weight' % self.mx_name] = (self.cout, self.cin)
+        return out
 
     def forward(self, x, relu=False, drop_p=0.0):
         x = x.reshape(x.shape[0], -1)
         b = None if self.bias is None else _w(self.bias, x)
         if drop_p and self.training and self._seed is None:
             self._seed = layer_seed(self.mx_name)
-        return fully_connected(x, _w(self.weight, x), b, relu, drop_p, self._seed or 0, self.rng_step, self.training)
+        w = _w(self.weight, x)
+        if w.dim() != 2:  # logical (c, h, w) columns (a copy when the weight is held channels_last)
+            w = w.reshape(w.shape[0], -1)
+        return fully_connected(x, w, b, relu, drop_p, self._seed or 0, self.rng_step, self.training)
 
 
 class BatchNorm(MxLayer):

@@ -3,6 +3,7 @@
 13 conv3x3+ReLU layers, 4 max-pool 2x2/2 (floor), stride-16 relu5_3 (512 ch); the head is
 RoIPool 7x7 @ 1/16 -> fc6 4096 -> ReLU -> Dropout .5 -> fc7 -> ReLU -> Dropout -> cls/bbox.
 """
+import torch
 import torch.nn as nn
 
 from .layers import Conv, Linear, max_pool
@@ -49,16 +50,22 @@ class VGGHead(nn.Module):
 
     def __init__(self, num_classes, in_channels=512, pooled=7, dropout=0.5):
         super().__init__()
-        self.fc6 = Linear('fc6', in_channels * pooled * pooled, 4096)
+        self.fc6 = Linear('fc6', in_channels * pooled * pooled, 4096, in_shape=(in_channels, pooled, pooled))
         self.fc7 = Linear('fc7', 4096, 4096)
         self.cls_score = Linear('cls_score', 4096, num_classes)
         self.bbox_pred = Linear('bbox_pred', 4096, 4 * num_classes)
         self.dropout = dropout
 
     def forward(self, pooled):
+        if pooled.is_cuda and pooled.dim() == 4 and pooled.is_contiguous(memory_format=torch.channels_last):
+            # the pooled map's channels_last rows, (h, w, c) order: a free view, matching fc6's
+            # channels_last filter (Linear in_shape) -- no Flatten copy forward or backward
+            rows = pooled.permute(0, 2, 3, 1).reshape(pooled.shape[0], -1)
+            if vgg_fused.head_ok(rows, self):
+                return vgg_fused.vgg_head(rows, self)
         x = pooled.reshape(pooled.shape[0], -1)  # MXNet Flatten: (C, H, W) order
-        if vgg_fused.head_ok(x, self):
-            return vgg_fused.vgg_head(x, self)
+        if vgg_fused.head_ok(x, self, logical=True):
+            return vgg_fused.vgg_head(x, self, logical=True)
         # relu6/drop6 and relu7/drop7 run in the FC kernel's epilogue (ops/fc.py)
         x = self.fc6(x, relu=True, drop_p=self.dropout)
         x = self.fc7(x, relu=True, drop_p=self.dropout)

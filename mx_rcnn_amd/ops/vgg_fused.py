@@ -28,14 +28,27 @@ def _cl(t):
     return t.contiguous(memory_format=torch.channels_last)
 
 
+def _rows(t, shape4):
+    """A channels_last (O, C, H, W) filter (fc6 held as Linear(in_shape=...)) read as the 1x1
+    filter ``shape4`` = (O, C*H*W, 1, 1) of its (h, w, c)-ordered rows: a free view."""
+    if t.dim() == 4 and tuple(t.shape) != tuple(shape4) and shape4[2] == 1 and shape4[3] == 1:
+        return t.permute(0, 2, 3, 1).reshape(shape4)
+    return t.reshape(shape4)
+
+
 def _wargs(w, shape4=None):
     """(filter as a channels_last (O, I, kh, kw) map, kwargs) of a launch reading weight ``w``
     (an FC's (O, I) weight as a 1x1 filter); x2: the store's pair of the fp32 parameter."""
     shape4 = tuple(w.shape) if shape4 is None else shape4
     if precision.x2_enabled():
         wh, wpl = precision.weight_pair(w)
-        return wh.reshape(shape4), {'x2': precision.x2_enabled(), 'w_plane': wpl}
-    return _cl(w.reshape(shape4)), {}
+        return _rows(wh, shape4), {'x2': precision.x2_enabled(), 'w_plane': wpl}
+    return _cl(_rows(w, shape4)), {}
+
+
+def _kdim(w, k=1):
+    """Input channels of weight ``w`` as a k x k filter (an (O, C, H, W) fc6 filter: C*H*W)."""
+    return w[0].numel() // (k * k) if (k == 1 and w.dim() == 4) else w.shape[1]
 
 
 def _gdt():
@@ -50,7 +63,9 @@ def _wtarget(param, shape4):
         return None
     if tgt.dim() == 2:
         return tgt.view(shape4) if tgt.is_contiguous() else None
-    return tgt if tgt.is_contiguous(memory_format=torch.channels_last) else None
+    if not tgt.is_contiguous(memory_format=torch.channels_last):
+        return None
+    return _rows(tgt, shape4)
 
 
 def _bias_grad(d, bparam, x2):
@@ -72,7 +87,7 @@ def _layer_backward(d, x, w, wparam, need_w, need_x, k, pad, rmask=None, rmask_s
     backward the data gradient's epilogue applies.  -> (dx or None, dw or None)."""
     ext = need_ext()
     x2 = precision.x2_enabled()
-    shape4 = (w.shape[0], w.shape[1], k, k)
+    shape4 = (w.shape[0], _kdim(w, k), k, k)
     wk, kw = _wargs(w, shape4)
     kw = dict(kw, bt=True)
     tgt = _wtarget(wparam, shape4) if need_w else None
@@ -85,7 +100,10 @@ def _layer_backward(d, x, w, wparam, need_w, need_x, k, pad, rmask=None, rmask_s
         if tgt is not None:
             ext.conv_wgrad(d, x, k, k, 1, pad, 0, tgt, x2=x2)
         else:
-            dw = ext.conv_wgrad(d, x, k, k, 1, pad, x2=x2).reshape(w.shape).to(w.dtype)
+            dw = ext.conv_wgrad(d, x, k, k, 1, pad, x2=x2)
+            if w.dim() == 4 and tuple(w.shape) != shape4:  # (h, w, c) rows -> the (O, C, H, W) filter
+                dw = dw.reshape(w.shape[0], w.shape[2], w.shape[3], w.shape[1]).permute(0, 3, 1, 2)
+            dw = dw.reshape(w.shape).to(w.dtype)
     if need_x:
         dx = ext.conv_igemm_fwd(d, wk, None, 1, k - 1 - pad, False, rmask=rmask, rmask_scale=rmask_scale, **kw)[0]
     return dx, dw
@@ -169,7 +187,7 @@ class _VGGHead(torch.autograd.Function):
         R = x.shape[0] // x2 if x2 else x.shape[0]
 
         def fc(inp, w, b, relu, seed, out_f32=False):
-            wk, kw = _wargs(w, (w.shape[0], w.shape[1], 1, 1))
+            wk, kw = _wargs(w, (w.shape[0], _kdim(w), 1, 1))
             drop = p if (relu and p > 0) else 0.0
             y = ext.conv_igemm_fwd(inp.view(inp.shape[0], inp.shape[1], 1, 1), wk, b, 1, 0, relu, drop_p=drop,
                                    drop_seed=seed, drop_step=step if drop > 0 else None, out_f32=out_f32, **kw)[0]
@@ -223,8 +241,10 @@ class _VGGHead(torch.autograd.Function):
         return (dx, None, None, None) + tuple(grads)
 
 
-def vgg_head(x, head):
-    """The fused head for VGGHead's Linear modules; ``x`` (R, C*7*7) rows."""
+def vgg_head(x, head, logical=False):
+    """The fused head for VGGHead's Linear modules; ``x`` (R, C*7*7) rows of the pooled map in
+    (h, w, c) order (its channels_last memory), the order of fc6's filter rows."""
+    assert not logical, 'the fused head reads (h, w, c) rows'
     from .fc import layer_seed
     training = head.training
     p = float(head.dropout) if training else 0.0
@@ -245,11 +265,14 @@ def trunk_ok(x, convs):
             all(weight_ok(act, c.weight) and c.bias is not None and c.weight.shape[1] % 64 == 0 for c in convs[1:]))
 
 
-def head_ok(x, head):
-    """True when the fused head can run on rows ``x`` (R, K)."""
+def head_ok(x, head, logical=False):
+    """True when the fused head can run on rows ``x`` (R, K); ``logical``: the rows are in MXNet
+    Flatten (c, h, w) order, which only a 2-D fc6 weight matches."""
     import os
     from .conv import weight_ok
     if os.environ.get('MXR_VGG_FUSED', '1') == '0' or not x.is_cuda or x.dtype != torch.bfloat16:
+        return False
+    if logical and head.fc6.weight.dim() != 2:
         return False
     fcs = (head.fc6, head.fc7)
     if head.training and head.dropout > 0 and head.fc6.rng_step is None:

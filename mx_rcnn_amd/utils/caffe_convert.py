@@ -196,7 +196,7 @@ def convert_layers(layers, arg_shapes=None):
 def vgg_test_arg_shapes(num_classes=21):
     """Argument shapes of the VGG16 Fast R-CNN test network (``rcnn/symbol.py``: get_vgg_test)."""
     from ..models.faster_rcnn import FasterRCNN
-    return {k: tuple(v.shape) for k, v in FasterRCNN('vgg16', num_classes).arg_params('rcnn').items()}
+    return dict(FasterRCNN('vgg16', num_classes).arg_shapes('rcnn'))
 
 
 def load_model(model_path, prefix_out=None, epoch_out=0, arg_shapes=None):

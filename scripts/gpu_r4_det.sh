@@ -7,7 +7,7 @@ timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method threa
   tests/test_fp32x2.py -k "roi or bitwise or partial or repeatable" > gpurun_out/det_tests.log 2>&1 \
   || { tail -40 gpurun_out/det_tests.log; exit 1; }
 tail -3 gpurun_out/det_tests.log
-timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels.py -k roi \
+timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_kernels.py -k "roi or sgd" \
   tests/test_dist_gpu.py > gpurun_out/det_dist.log 2>&1 || { tail -40 gpurun_out/det_dist.log; exit 1; }
 tail -3 gpurun_out/det_dist.log
 ab() {

@@ -22,7 +22,9 @@ def test_param_counts_match_reference():
     m = FasterRCNN('vgg16', 21, cfg=_cfg())
     a = m.arg_params()
     assert len(a) == 40 and sum(v.numel() for v in a.values()) == 137078239
-    assert a['fc6_weight'].shape == (4096, 25088) and a['rpn_cls_score_weight'].shape == (18, 512, 1, 1)
+    shapes = m.arg_shapes()  # checkpoint layout: fc6 is held as the (4096, 512, 7, 7) filter of its rows
+    assert shapes['fc6_weight'] == (4096, 25088) and a['fc6_weight'].shape == (4096, 512, 7, 7)
+    assert shapes['rpn_cls_score_weight'] == (18, 512, 1, 1) == tuple(a['rpn_cls_score_weight'].shape)
     r = FasterRCNN('resnet101', 21, cfg=_cfg())
     assert len(r.arg_params()) == 318 and len(r.aux_params()) == 204
     assert sum(v.numel() for v in r.arg_params().values()) == 47463799
@@ -336,3 +338,24 @@ def test_fused_gradient_clear_matches_fill_cpu():
     before = [g.master.clone() for g in tr.store.groups]
     tr.step(rb)
     assert all(float((g.master - b).abs().max()) < 1.0 for g, b in zip(tr.store.groups, before))
+
+
+def test_linear_in_shape_layout_cpu():
+    """Linear(in_shape=(C, H, W)) (VGG fc6): the weight is the (cout, C, H, W) filter of the MXNet
+    (cout, C*H*W) matrix -- same logical elements, so loading a checkpoint matrix and flattening
+    (C, H, W) inputs gives the plain FullyConnected result; the checkpoint shape stays 2-D."""
+    from mx_rcnn_amd.models.layers import Linear
+    torch.manual_seed(3)
+    lin = Linear('fc6', 8 * 7 * 7, 16, in_shape=(8, 7, 7))
+    assert lin.weight.shape == (16, 8, 7, 7) and lin.mx_arg_shapes()['fc6_weight'] == (16, 392)
+    w2 = torch.randn(16, 392)
+    with torch.no_grad():
+        lin.weight.copy_(w2.reshape(lin.weight.shape))  # the loader's reshape
+    x = torch.randn(5, 8, 7, 7)
+    ref = x.reshape(5, -1) @ w2.t() + lin.bias
+    assert torch.allclose(lin(x), ref, atol=1e-5)
+    # held channels_last (the parameter store's layout): rows of the channels_last map match
+    wcl = lin.weight.detach().contiguous(memory_format=torch.channels_last)
+    rows_w = wcl.permute(0, 2, 3, 1).reshape(16, -1)
+    rows_x = x.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(5, -1)
+    assert torch.allclose(rows_x @ rows_w.t() + lin.bias, ref, atol=1e-5)

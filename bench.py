@@ -229,7 +229,8 @@ def run(args, precision, rank, world, device):
                       'rois_per_image': cfg.TRAIN.BATCH_SIZE, 'exec': mode,
                       'objective_first_last': [round(loss0, 4), round(loss1, 4)],
                       'backend': pdist.backend_name(), 'allreduce': comm,
-                      'rccl': pdist.rccl_env() if pdist.backend_name() == 'nccl' else None}}
+                      'rccl': pdist.rccl_env() if pdist.backend_name() == 'nccl' else None,
+                      'hip_runtime': __import__('mx_rcnn_amd').runtime_settings()}}
     del step_fn, trainer
     return rec
 

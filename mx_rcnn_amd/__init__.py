@@ -5,7 +5,9 @@ read when the HIP runtime initialises (the first GPU call), so the package must 
 before anything touches the GPU -- every entry point here does.  A value already in the
 environment wins.
 
-* ``DEBUG_HIP_FORCE_GRAPH_QUEUES=2``: a replayed hipGraph's independent branches are spread over
+* ``DEBUG_HIP_FORCE_GRAPH_QUEUES=2`` (a HIP runtime debug variable; ``MXR_GRAPH_QUEUES`` picks the
+  value, 0 leaves the runtime default, and a warning says when the import came too late for it
+  to act): a replayed hipGraph's independent branches are spread over
   two hardware queues instead of the runtime's default four.  The step's concurrency is two-way
   (the compute stream plus one side stream at a time: anchor targets / RPN losses / proposal
   chain / dgrad filter cache), and every extra queue adds cross-queue dependency waits.
@@ -13,10 +15,25 @@ environment wins.
   2 queues 159.7, 3 queues 150.8, default 151.5 img/s (docs/DESIGN.md §2).
 """
 import os
+import sys
+import warnings
 
-RUNTIME_DEFAULTS = {
-    'DEBUG_HIP_FORCE_GRAPH_QUEUES': '2',
-}
+# MXR_GRAPH_QUEUES=n picks the queue count (0: leave the runtime's default and its variable alone)
+_GQ = os.environ.get('MXR_GRAPH_QUEUES', '2')
+RUNTIME_DEFAULTS = {'DEBUG_HIP_FORCE_GRAPH_QUEUES': _GQ} if _GQ not in ('', '0') else {}
+
+
+def runtime_settings():
+    """The HIP runtime variables in effect (recorded with benchmark results)."""
+    return {k: os.environ.get(k) for k in ('DEBUG_HIP_FORCE_GRAPH_QUEUES', 'GPU_MAX_HW_QUEUES')}
+
 
 for _k, _v in RUNTIME_DEFAULTS.items():
-    os.environ.setdefault(_k, _v)
+    if _k not in os.environ:
+        os.environ[_k] = _v
+        # the runtime reads it once, when it initialises: imported after the first GPU call, the
+        # setting silently does nothing -- say so
+        _tc = sys.modules.get('torch')
+        if _tc is not None and getattr(getattr(_tc, 'cuda', None), 'is_initialized', lambda: False)():
+            warnings.warn('mx_rcnn_amd imported after the HIP runtime initialised: %s=%s has no effect in '
+                          'this process (import the package first)' % (_k, _v), RuntimeWarning)

@@ -56,12 +56,12 @@ __device__ __forceinline__ f32x4_t mma(const uint4& a, const uint4& b, f32x4_t c
                                                    c, 0, 0, 0);
 }
 
-template <int BN>
+template <int BM_, int BN>
 struct BigCfg {
-  static constexpr int BM = 256;
+  static constexpr int BM = BM_;
   static constexpr int WGN = BN / 64;        // waves along N (64 columns each)
   static constexpr int WGM = 8 / WGN;        // waves along M
-  static constexpr int WM = BM / WGM;        // rows per wave (128 or 64)
+  static constexpr int WM = BM / WGM;        // rows per wave (128, 64 or 32)
   static constexpr int TM = WM / 16, TN = 4; // 16x16 accumulator tiles per wave
   static constexpr int ROWS = BM + BN;       // LDS rows per K tile
   static constexpr int LA = BM / 128, LB = BN / 128;  // DMA instructions per thread per K tile (A / B)
@@ -73,12 +73,12 @@ struct BigCfg {
 // itself): referenced directly, hipcc's wait-count pass drained every in-flight LDS-DMA
 // (s_waitcnt vmcnt(0)) before the fragment reads of each K tile -- the same effect the buffer
 // kernel documents for a __restrict__ ring (conv_igemm.hip).
-template <int BN, bool F16>
+template <int BM_, int BN, bool F16>
 __device__ __forceinline__ void conv_big_body(uint16_t* lds, const uint16_t* __restrict__ x,
                                               const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int NB, int H,
                                               int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride,
                                               int pad, const ConvEpi& ep, int tiles_n, int nwg) {
-  using C = BigCfg<BN>;
+  using C = BigCfg<BM_, BN>;
   constexpr int BM = C::BM, TM = C::TM, TN = C::TN, WM = C::WM;
 
   const int bid = blockIdx.x;
@@ -253,22 +253,25 @@ __device__ __forceinline__ void conv_big_body(uint16_t* lds, const uint16_t* __r
   }
 }
 
-template <int BN, bool F16>
+template <int BM, int BN, bool F16>
 __global__ void __launch_bounds__(512)
 conv_big_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int NB,
                 int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, const ConvEpi ep,
                 int tiles_n, int nwg) {
   // one LDS array (a second __shared__ object can make hipcc drain the DMA ring before each read)
-  __shared__ __attribute__((aligned(16))) uint16_t lds[NBUF * BigCfg<BN>::ROWS * BK];
-  conv_big_body<BN, F16>(lds, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, tiles_n, nwg);
+  __shared__ __attribute__((aligned(16))) uint16_t lds[NBUF * BigCfg<BM, BN>::ROWS * BK];
+  conv_big_body<BM, BN, F16>(lds, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, tiles_n, nwg);
 }
 
 }  // namespace
 
-// tile codes 200 (256x256) / 201 (256x128); -1 when the shape or epilogue is not supported
+// tile codes 200 (256x256) / 201 (256x128) / 202 (128x128) / 203 (128x256); -1 when the shape or
+// epilogue is not supported.  The 128-row tiles serve N = 256 GEMMs of a few tens of thousands of
+// rows (the batch-8 stage-3 reduce / 3x3 convs: 75 workgroups of 256x256 leave 181 of 256 CUs
+// idle; 128x128 gives 300, two resident per CU with the 64 KB ring)
 int conv_big_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho, int Wo,
                  int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int tile, hipStream_t st) {
-  if (tile != 200 && tile != 201) return -1;
+  if (tile < 200 || tile > 203) return -1;
   if (Cin % BK != 0 || Cout % 16 != 0 || KH * KW > 64) return -1;
   if (ep.x2 || ep.yf || ep.bt || ep.omap || ep.pad_w >= 0 || ep.bnb_x || ep.st_part || ep.bnb_part || ep.rmask ||
       ep.drop_p > 0.f)
@@ -276,19 +279,27 @@ int conv_big_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int 
   if ((ep.y2) && (!ep.bn_beta || !ep.bn_mean || !ep.bn_var || (!ep.bn_fix_gamma && !ep.bn_gamma))) return -1;
   if ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kOOB || (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kOOB) return -1;
   const int M = NB * Ho * Wo;
-  const int bn = tile == 200 ? 256 : 128;
+  const int bm = tile >= 202 ? 128 : 256;
+  const int bn = (tile == 200 || tile == 203) ? 256 : 128;
   const int tiles_n = (Cout + bn - 1) / bn;
-  const int nwg = ((M + 255) / 256) * tiles_n;
-#define MXR_BIG(BN_, F_)                                                                                      \
-  conv_big_kernel<BN_, F_><<<nwg, 512, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, \
-                                               tiles_n, nwg)
-  if (tile == 200) {
-    if (ep.f16) MXR_BIG(256, true);
-    else MXR_BIG(256, false);
-  } else {
-    if (ep.f16) MXR_BIG(128, true);
-    else MXR_BIG(128, false);
+  const int nwg = ((M + bm - 1) / bm) * tiles_n;
+#define MXR_BIG(BM_, BN_, F_)                                                                                 \
+  conv_big_kernel<BM_, BN_, F_><<<nwg, 512, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, \
+                                                    ep, tiles_n, nwg)
+#define MXR_BIG2(BM_, BN_)      \
+  do {                          \
+    if (ep.f16)                 \
+      MXR_BIG(BM_, BN_, true);  \
+    else                        \
+      MXR_BIG(BM_, BN_, false); \
+  } while (0)
+  switch (tile) {
+    case 200: MXR_BIG2(256, 256); break;
+    case 201: MXR_BIG2(256, 128); break;
+    case 202: MXR_BIG2(128, 128); break;
+    default: MXR_BIG2(128, 256); break;
   }
+#undef MXR_BIG2
 #undef MXR_BIG
   return tile;
 }

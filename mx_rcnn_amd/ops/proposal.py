@@ -3,9 +3,9 @@ over images with static output shapes so the whole training step can be captured
 hipGraph (no host synchronisation):
 
   1. fused softmax(fg) + anchors + decode + clip + min-size   -> HIP `proposal_decode`
-  2. stable descending sort, truncate to PRE_NMS_TOP_N        -> device merge sort (the HIP
-                                                                 `proposal_topk` select+rank kernel
-                                                                 is opt-in: MXR_TOPK=1, slower here)
+  2. stable descending sort, truncate to PRE_NMS_TOP_N        -> HIP `proposal_topk` (grid radix
+                                                                 select + rank; MXR_TOPK=0: device
+                                                                 sort + gather)
   3. bitmask NMS (IoU > thresh suppresses), keep POST_NMS_TOP_N,
      random pad (choice with replacement from keep), assemble (post, 5) RoIs
                                                               -> HIP `nms_proposals`
@@ -84,11 +84,9 @@ def proposal(cls, bbox_deltas, im_info, feat_stride=16, scales=(8, 16, 32), rati
             boxes, keys = _decode_ref(cls, bbox_deltas, im_info, base, feat_stride, min_size, is_train, is_prob)
         N = keys.shape[1]
         P = N if pre_nms_top_n <= 0 else min(int(pre_nms_top_n), N)
-        if cls.is_cuda and N <= 65536 and os.environ.get('MXR_TOPK', '0') == '1':
-            # radix-select + rank-by-counting top-P in stable descending order (csrc/hip/topk.hip).
-            # Off by default: on one image (50 400 clustered RPN scores) it measured 160-340 us against
-            # 60 us for the device merge sort (tools/microbench/topk_bench.py): one workgroup's LDS
-            # histogram atomics serialise when most scores share their top bytes.
+        if cls.is_cuda and os.environ.get('MXR_TOPK', '1') == '1':
+            # grid radix select + rank-by-counting top-P in stable descending order
+            # (csrc/hip/topk.hip; MXR_TOPK=0: the device sort + gather below)
             skeys, sboxes, n_valid = C.proposal_topk(keys.contiguous(), boxes.contiguous(), P)
         else:
             skeys, order = torch.sort(keys, dim=1, descending=True, stable=True)

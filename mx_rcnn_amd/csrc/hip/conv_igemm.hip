@@ -1099,7 +1099,8 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
     // pairs / fp32 outputs / filter read transposed: the buffer kernels (x2 also at depth 4 and
     // 128x128, A/B tiles 21 / 32 / 33)
     const bool x2_ok = !ep.bt && !ep.x3 && (tile == 21 || tile == 32 || tile == 33);
-    if (!(tile == 22 || tile == 23 || x2_ok || (kgt && !ep.x3))) tile = 23;  // x3: the fused 22 / 23
+    // x3: the fused 22 / 23, or the K-group forms 27 / 28 (tile 29's four 144 KB-class rings do not fit)
+    if (!(tile == 22 || tile == 23 || x2_ok || (kgt && !(ep.x3 && tile == 29)))) tile = 23;
     if ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB || (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kBufOOB ||
         KH * KW > 64 || ep.f16)
       return -1;

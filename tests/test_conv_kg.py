@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 
 TILES = [27, 28, 29]
 MODES = [0, 2, 3]  # plane count: 0 = bf16 operands
-KG_MODES = [0, 2]  # the K-group tiles run bf16 and bf16x3 (fp32 triples use the fused one-pass 22 / 23)
+KG_MODES = [0, 2, 3]  # bf16, bf16x3 pairs and fp32 triples (tile 29 falls back to 23 for triples)
 
 
 def _cl(t):

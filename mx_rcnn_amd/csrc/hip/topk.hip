@@ -98,6 +98,11 @@ __device__ __forceinline__ void tk_pick(const uint32_t* __restrict__ hist, int n
   }
   uint32_t tot;
   uint32_t acc = tk_block_scan(s, wsum, &tot);
+  if (threadIdx.x == 0) {  // (unreachable with consistent counts: remain <= keys under the prefix)
+    *s_bin = 0u;
+    *s_rem = remain;
+  }
+  __syncthreads();
   if (acc < remain && remain <= acc + s) {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
@@ -253,11 +258,15 @@ topk_write_kernel(const float* __restrict__ keys, int N, int P, uint32_t* __rest
   const uint32_t base = (uint32_t)P - need;
   uint32_t* ck = cand_key + (int64_t)b * P;
   int* ci = cand_idx + (int64_t)b * P;
+  // (bounds are guaranteed by the counts -- #(> T) = P - need -- and checked anyway: a wrong slot
+  // must not become a wild store)
 #pragma unroll
   for (int j = 0; j < kTkPer; ++j) {
     if (u[j] > T) {
-      ck[gs] = u[j];
-      ci[gs] = i0 + j;
+      if (gs < base) {
+        ck[gs] = u[j];
+        ci[gs] = i0 + j;
+      }
       ++gs;
     } else if (u[j] == T && i0 + j < N) {
       if (es < need) {
@@ -305,7 +314,7 @@ topk_rank_kernel(const uint32_t* __restrict__ cand_key, const int* __restrict__ 
   }
   rank += __shfl_xor(rank, 1, 64);
   rank += __shfl_xor(rank, 2, 64);
-  if (i < P && q == 0) {
+  if (i < P && q == 0 && rank < P && (unsigned)idx < (unsigned)N) {  // ranks: a permutation of 0..P-1 (distinct (key, index) words)
     skeys[(int64_t)b * P + rank] = unord_key((uint32_t)(mine >> 32));
     const float4 bx = *reinterpret_cast<const float4*>(boxes + ((int64_t)b * N + idx) * 4);
     *reinterpret_cast<float4*>(sboxes + ((int64_t)b * P + rank) * 4) = bx;

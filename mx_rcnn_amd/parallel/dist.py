@@ -28,10 +28,17 @@ def get_world_size():
 #   backward kernels lose while a collective runs.
 # * TORCH_NCCL_ASYNC_ERROR_HANDLING=1: a failed or timed-out collective aborts the communicator
 #   and raises on every rank (torchrun then tears the job down) instead of hanging the step.
+# * TORCH_NCCL_CUDA_EVENT_CACHE=0: the process group's watchdog polls the completion events of the
+#   eager (warm-up) collectives; with the event cache a finished work's event object is handed to a
+#   collective recorded inside the step's hipGraph capture, and the watchdog's next poll of the old
+#   work then fails with hipErrorCapturedEvent and aborts the process (seen on the 1-rank RCCL
+#   graphed-step test, bf16x3).  Fresh events per work cost nothing measurable here (a few dozen
+#   collectives per step, all inside the replayed graph).
 # * collective timeout MXR_COLL_TIMEOUT (default 600 s) for init_process_group.
 RCCL_DEFAULTS = {
     'NCCL_MIN_NCHANNELS': '16',
     'TORCH_NCCL_ASYNC_ERROR_HANDLING': '1',
+    'TORCH_NCCL_CUDA_EVENT_CACHE': '0',
 }
 
 

@@ -347,7 +347,8 @@ std::vector<Tensor> anchor_target_assign(const Tensor& base_anchors, int64_t H, 
 // ---- RoI pooling -----------------------------------------------------------------------
 // feat must be channels-last in memory: logical (B, C, H, W) with NHWC strides.
 // x2: feat is a (2B, C, H, W) hi / lo pair, the pooled output (2R, C, PH, PW) a pair too
-std::vector<Tensor> roi_pool_fwd(const Tensor& feat, const Tensor& rois, int64_t PH, int64_t PW, double scale, int64_t x2) {
+std::vector<Tensor> roi_pool_fwd(const Tensor& feat, const Tensor& rois, int64_t PH, int64_t PW, double scale, int64_t x2,
+                                 bool need_argmax) {
   CHECK_DEV(feat); CHECK_DEV(rois); CHECK_F32(rois); CHECK_CONTIG(rois);
   TORCH_CHECK(feat.dim() == 4 && feat.is_contiguous(at::MemoryFormat::ChannelsLast),
               "feat must be (B,C,H,W) channels_last");
@@ -359,9 +360,13 @@ std::vector<Tensor> roi_pool_fwd(const Tensor& feat, const Tensor& rois, int64_t
   const int R = (int)rois.size(0);
   DevGuard g(feat.device());
   Tensor out = at::empty({x2 ? npl(x2) * R : R, C, PH, PW}, feat.options().memory_format(at::MemoryFormat::ChannelsLast));
-  Tensor argmax = at::empty({R, C, PH, PW}, feat.options().dtype(at::kInt).memory_format(at::MemoryFormat::ChannelsLast));
+  // inference skips the argmax map (4 B per output element: at batch 8 x 300 RoIs x 1024 channels
+  // x 49 bins, 480 MB of writes that nothing reads)
+  Tensor argmax = need_argmax ? at::empty({R, C, PH, PW}, feat.options().dtype(at::kInt).memory_format(
+                                                              at::MemoryFormat::ChannelsLast))
+                              : at::empty({0}, feat.options().dtype(at::kInt));
   mxr::roi_pool_fwd(feat.data_ptr(), x2 ? pcode(x2) : dcode(feat), B, H, W, C, rois.data_ptr<float>(), R, (int)PH, (int)PW,
-                    (float)scale, out.data_ptr(), argmax.data_ptr<int32_t>(), cur_stream());
+                    (float)scale, out.data_ptr(), need_argmax ? argmax.data_ptr<int32_t>() : nullptr, cur_stream());
   return {out, argmax};
 }
 
@@ -2084,7 +2089,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("proposal_sample", &proposal_sample);
   m.def("anchor_target_assign", &anchor_target_assign);
   m.def("roi_pool_fwd", &roi_pool_fwd, py::arg("feat"), py::arg("rois"), py::arg("PH"), py::arg("PW"),
-        py::arg("scale"), py::arg("x2") = 0);
+        py::arg("scale"), py::arg("x2") = 0, py::arg("need_argmax") = true);
   m.def("roi_pool_bwd", &roi_pool_bwd, py::arg("grad_out"), py::arg("argmax"), py::arg("rois"), py::arg("B"),
         py::arg("H"), py::arg("W"), py::arg("grad_add") = py::none(), py::arg("x2") = 0);
   m.def("rpn_softmax_ce", &rpn_softmax_ce, py::arg("logits"), py::arg("label"), py::arg("norm"), py::arg("grad_scale"),

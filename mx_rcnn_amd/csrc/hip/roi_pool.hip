@@ -97,7 +97,7 @@ roi_pool_fwd_vec4(const T* __restrict__ feat, int code, int B, int H, int W, int
   } else {
     *reinterpret_cast<float4*>(out + o) = make_float4(m0, m1, m2, m3);
   }
-  *reinterpret_cast<int4*>(argmax + o) = make_int4(a0, a1, a2, a3);
+  if (argmax) *reinterpret_cast<int4*>(argmax + o) = make_int4(a0, a1, a2, a3);  // null: inference, no backward
 }
 
 template <typename T>
@@ -126,7 +126,7 @@ roi_pool_fwd_scalar(const T* __restrict__ feat, int code, int B, int H, int W, i
       }
   }
   if constexpr (sizeof(T) == 2) out[t] = f32_to_h16(m, code); else out[t] = m;
-  argmax[t] = a;
+  if (argmax) argmax[t] = a;
 }
 
 template <typename T>

@@ -69,8 +69,9 @@ class _RoIPool(torch.autograd.Function):
             B = B // x2  # (P*B, C, H, W) planes
         if feat.is_cuda:
             ext = need_ext()
+            # the argmax map only feeds the backward: inference (no grad) skips writing it
             out, arg = ext.roi_pool_fwd(feat.contiguous(memory_format=torch.channels_last), rois, PH, PW, float(scale),
-                                        x2)
+                                        x2, bool(ctx.needs_input_grad[0]))
         else:
             if ext_available():  # C++ twin (the loop reference below is the test oracle)
                 out, arg = need_ext().roi_pool_fwd_cpu(feat, rois, PH, PW, float(scale))

@@ -255,7 +255,10 @@ class GraphedStep:
                 del saved
                 torch.cuda.synchronize()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
+        # thread_local: the loaders' prefetch threads keep staging the next batches (pinned host
+        # buffers, H2D copies on their own streams) while a new shape is captured; in the default
+        # global mode any such call from another thread invalidates the capture
+        with torch.cuda.graph(self.graph, capture_error_mode='thread_local'):
             self.out = trainer.step_body(self.static)
         torch.cuda.synchronize()
 

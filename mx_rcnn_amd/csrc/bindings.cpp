@@ -933,7 +933,7 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
     } else if (!stream_capturing(cur_stream())) {
       // time the candidates into scratch outputs (no in-place aliasing, no statistics updates)
       std::vector<std::pair<int, int>> cands = {{t, sp}};
-      for (int c : {23, 22, 101, 104, 105, 106, 108, 109, 110, 111})
+      for (int c : {23, 22, 30, 101, 104, 105, 106, 108, 109, 110, 111})
         if (c != t || sp != 1) cands.push_back({c, 1});
       // K groups (conv_kg.hip): 2-4 four-wave groups per 64x64 tile, each over a slice of K
       if (!f16 && Cout % 8 == 0 && getenv("MXR_NO_KG") == nullptr)

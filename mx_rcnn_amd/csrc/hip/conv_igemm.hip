@@ -979,7 +979,7 @@ static void launch_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB
         conv_igemm_buf_kernel<BM, BN, S, false, true, false><<<nwg, 256, 0, st>>>(
             x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, tiles_n, nwg, ntiles, splits, slab);
     } else if (ep.x2 || ep.bt) {
-      if constexpr (S == 3 && BN == 64 && (BM == 64 || BM == 128)) {
+      if constexpr ((S == 3 && BN == 64 && (BM == 64 || BM == 128)) || (S == 2 && BN == 64 && BM == 64)) {
 #define MXR_BUF_LAUNCH(X, B, X3_)                                                                                  \
   conv_igemm_buf_kernel<BM, BN, S, false, X, B, X3_><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, \
                                                                           KW, stride, pad, ep, tiles_n, nwg, ntiles,  \
@@ -1069,10 +1069,10 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
   if (ep.y2 && ep.bnb_x) return -1;
   if (ep.rmask && (ep.bnb_x || ep.y2 || ep.f16)) return -1;
   const bool kgt = tile >= 27 && tile <= 29;  // K-group tiles (conv_kg.hip)
-  if ((ep.omap || ep.pad_w >= 0) && (splits > 1 || !(tile == 22 || tile == 23 || tile >= 100 || kgt))) return -1;
-  if (ep.f16 && !(tile == 21 || tile == 22 || tile == 23 || tile >= 100)) return -1;
+  if ((ep.omap || ep.pad_w >= 0) && (splits > 1 || !(tile == 22 || tile == 23 || tile == 30 || tile >= 100 || kgt))) return -1;
+  if (ep.f16 && !(tile == 21 || tile == 22 || tile == 23 || tile == 30 || tile >= 100)) return -1;
   // BN statistics: LDS-epilogue kernels (buffer / ring), whole K per workgroup
-  if (ep.st_part && (splits > 1 || Cout % 8 != 0 || !(tile == 21 || tile == 22 || tile == 23 || tile >= 100 || kgt)))
+  if (ep.st_part && (splits > 1 || Cout % 8 != 0 || !(tile == 21 || tile == 22 || tile == 23 || tile == 30 || tile >= 100 || kgt)))
     return -1;
   // buffer variants: 32-bit byte offsets below the kBufOOB sentinel, tap mask of 64 bits
   if (tile >= 100 && ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB ||
@@ -1100,7 +1100,7 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
     // 128x128, A/B tiles 21 / 32 / 33)
     const bool x2_ok = !ep.bt && !ep.x3 && (tile == 21 || tile == 32 || tile == 33);
     // x3: the fused 22 / 23, or the K-group forms 27 / 28 (tile 29's four 144 KB-class rings do not fit)
-    if (!(tile == 22 || tile == 23 || x2_ok || (kgt && !(ep.x3 && tile == 29)))) tile = 23;
+    if (!(tile == 22 || tile == 23 || tile == 30 || x2_ok || (kgt && !(ep.x3 && tile == 29)))) tile = 23;
     if ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB || (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kBufOOB ||
         KH * KW > 64 || ep.f16)
       return -1;
@@ -1129,6 +1129,9 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
     case 21: launch_fwd<128, 128, 3, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 22: launch_fwd<128, 64, 3, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 23: launch_fwd<64, 64, 3, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
+    // tile 23 at ring depth 2: the fp32 triples' 72 KB ring becomes 48 KB, three workgroups per CU
+    // instead of two (the batch-1 stage-3 grids are 264 tiles on 256 CUs)
+    case 30: launch_fwd<64, 64, 2, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 31: launch_fwd<128, 128, 4, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 32: launch_fwd<128, 64, 4, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
     case 33: launch_fwd<64, 64, 4, true>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st); break;
@@ -1301,11 +1304,12 @@ int conv_dgrad_wgrad(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, 
 #define MXR_GROUPED(S_, X, B, ...) \
   conv_dgrad_wgrad_kernel<S_, X, B, ##__VA_ARGS__><<<nwg_all, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, pad, ep, \
                                                             tiles_n, ntiles, ntiles, wp, rp)
-  // fp32 triples: the fused one-pass form (72 KB of LDS at depth 3: two workgroups per CU; the A/B
-  // knob MXR_GROUPED_X3S=2 runs it at depth 2, 48 KB: three per CU)
+  // fp32 triples: the fused one-pass form, at ring depth 2 (48 KB of LDS: three workgroups per CU;
+  // measured 73.5 vs 69.1 img/s on the fp32 headline against depth 3's 72 KB, two per CU;
+  // MXR_GROUPED_X3S=3 restores depth 3)
   static const int x3_depth = [] {
     const char* e = getenv("MXR_GROUPED_X3S");
-    return e != nullptr && e[0] == '2' ? 2 : 3;
+    return e != nullptr && e[0] == '3' ? 3 : 2;
   }();
   if (wx2.x3 && ep.bt && x3_depth == 2) MXR_GROUPED(2, true, true, 1, true);
   else if (wx2.x3 && ep.bt) MXR_GROUPED(3, true, true, 1, true);

@@ -287,9 +287,9 @@ class AnchorLoader(_BaseLoader):
         if self.max_gt is not None:
             G = self.max_gt
         else:
-            G = max(1, max(int((e['gt_classes'] != 0).sum()) for e in glob))
-            if self.shape_bucket > 1:
-                G = _pow2_at_least(G)
+            # power-of-two gt slots (n_gt carries the count): a handful of input shapes, so the
+            # per-shape hipGraph cache does not capture a graph for every distinct gt count
+            G = _pow2_at_least(max(1, max(int((e['gt_classes'] != 0).sum()) for e in glob)))
         return hw, G, sidx
 
     def _make_batch(self, i):

@@ -1109,7 +1109,7 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
       return -1;
     if (ep.yf && (ep.y2 || ep.bnb_x || ep.st_part)) return -1;
   }
-  if (kgt) return conv_igemm_kg(tile, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st);
+  if (tile >= 27 && tile <= 29) return conv_igemm_kg(tile, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st);
   if (tile >= 100 && tile < 100 + kNumRing) {
     launch_ring_code(tile - 100, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, splits, slab, st);
     return tile;

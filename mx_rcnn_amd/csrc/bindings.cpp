@@ -896,8 +896,8 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
     TORCH_CHECK(sp == 1, "stat_shift: no split-K");
     if (!(t == 21 || t == 22 || t == 23 || t >= 100)) t = 23;
   }
-  if (ep.bnb_part) {  // the caller sized the partial rows for 64-row tiles
-    t = 23;
+  if (ep.bnb_part) {  // the caller sized the partial rows for 64-row tiles (the autotune keeps to them)
+    if (mxr::conv_tile_bm(t) != 64 || t < 21) t = 23;
     sp = 1;
   }
   if (f16 && !(t == 21 || t == 22 || t == 23 || t >= 100)) t = 23;  // fp16 MFMA: buffer / ring kernels
@@ -918,12 +918,13 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
     const int64_t blocks = (((int64_t)NB * Ho * Wo + bm - 1) / bm) * ((Cout + 63) / 64);
     if (blocks < 512 && KH * KW * Cin / 32 >= 8 * x2_split) sp = std::max(sp, x2_split);
   }
-  if (tile <= 0 && splits <= 0 && !mapped && ep.pad_w < 0 && !ep.bnb_part && conv_tune_enabled()) {
+  if (tile <= 0 && splits <= 0 && !mapped && ep.pad_w < 0 && conv_tune_enabled()) {
     char kb[256];
-    snprintf(kb, sizeof(kb), "%d,%d,%d,%d,%d,%d,%d,%d,%d|%d%d%d%d%d%d%d%d%d%d", NB, H, W, Cin, Cout, KH, KW, (int)stride,
-             (int)pad, ep.residual != nullptr, ep.y2 != nullptr || bn.has_value(), bwd_mode, ep.dadd != nullptr,
-             ep.relu, ep.bias != nullptr || ep.bias_h != nullptr, (ep.drop_p > 0.f ? 1 : 0) + (stats ? 2 : 0), ep.bt,
-             ep.rmask != nullptr, ep.x2 + ep.x3);
+    snprintf(kb, sizeof(kb), "%d,%d,%d,%d,%d,%d,%d,%d,%d|%d%d%d%d%d%d%d%d%d%d%d", NB, H, W, Cin, Cout, KH, KW,
+             (int)stride, (int)pad, ep.residual != nullptr, ep.y2 != nullptr || bn.has_value(), bwd_mode,
+             ep.dadd != nullptr, ep.relu, ep.bias != nullptr || ep.bias_h != nullptr,
+             (ep.drop_p > 0.f ? 1 : 0) + (stats ? 2 : 0), ep.bt, ep.rmask != nullptr, ep.x2 + ep.x3,
+             ep.bnb_part != nullptr);
     const std::string key(kb);
     std::unique_lock<std::mutex> lk(g_tune_mu);
     auto it = g_tune.find(key);
@@ -988,6 +989,8 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
       float best = 1e30f, plan_ms = 1e30f;
       std::pair<int, int> pick = {t, sp};
       for (const auto& c : cands) {
+        // deterministic BN-backward sums: 64-row tiles, whole K (the partial rows are per 64 rows)
+        if (ep.bnb_part && (c.second != 1 || c.first < 21 || mxr::conv_tile_bm(c.first) != 64)) continue;
         float* sl = c.second > 1 ? slab_t.data_ptr<float>() : nullptr;
         auto run = [&]() {
           return mxr::conv_igemm_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
@@ -1167,7 +1170,7 @@ std::vector<Tensor> conv_dgrad_wgrad(const Tensor& x, const Tensor& w, int64_t p
   }
   DevGuard g(x.device());
   int sp = 1;
-  mxr::conv_wgrad_plan(gNB, gHo, gWo, gCin, gCout, (int)KH, (int)KW, &sp);
+  mxr::conv_wgrad_plan(gNB, gHo, gWo, gCin, gCout, (int)KH, (int)KW, &sp, (int)x2);
   Tensor slab = at::empty({sp > 1 ? (int64_t)sp * gCout * KH * KW * gCin : 1}, x.options().dtype(at::kFloat));
   const int r = mxr::conv_dgrad_wgrad(
       reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<const uint16_t*>(w.data_ptr()),
@@ -1775,7 +1778,7 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int
   TORCH_CHECK(Ho == (H + 2 * pad - KH) / stride + 1 && Wo == (W + 2 * pad - KW) / stride + 1, "geometry mismatch");
   DevGuard g(x.device());
   int sp = 1;
-  mxr::conv_wgrad_plan(NB, Ho, Wo, Cin, Cout, (int)KH, (int)KW, &sp);
+  mxr::conv_wgrad_plan(NB, Ho, Wo, Cin, Cout, (int)KH, (int)KW, &sp, (int)x2);
   static const int max_sp = [] {  // A/B knob: cap the pixel split (fewer reduce launches)
     const char* e = std::getenv("MXR_WGRAD_MAX_SPLITS");
     return e ? std::max(1, std::atoi(e)) : 1 << 30;

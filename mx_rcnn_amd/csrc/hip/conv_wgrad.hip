@@ -174,17 +174,20 @@ void wgrad_reduce_run(const float* slab, int splits, int64_t n, uint16_t* dw, hi
   wgrad_reduce(slab, splits, n, dw, 1, st, dwf);
 }
 
-int conv_wgrad_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int* splits_out) {
+int conv_wgrad_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int* splits_out, int planes) {
   // LDS-DMA kernel (tools/microbench/conv_tiles.py --wgrad on the ResNet-101 C4 shapes): split
   // the pixel reduction up to ~9 workgroups per CU while every split keeps >= 16 64-pixel steps
   const int P = NB * Ho * Wo;
   const int tiles = ((Cout + WG_BM - 1) / WG_BM) * (KH * KW * Cin / WG_BN);
   const int steps = (P + WG_BK - 1) / WG_BK;
-  static const int min_steps = [] {  // A/B knob MXR_WGRAD_MIN_STEPS: 64-pixel steps kept per split
-    // 8 (was 16): more K splits for the batch-1 weight gradients (fp32 headline 72.2 vs 69.1 img/s)
+  // 64-pixel steps kept per split (A/B knob MXR_WGRAD_MIN_STEPS): 8 with multi-plane operands, whose
+  // steps are 2-3x longer (fp32 headline 75.6 vs 75.0 img/s, bf16x3 101.7 vs 100.9), 16 for bf16
+  // (152.1 vs 150.3)
+  static const int env_steps = [] {
     const char* e = std::getenv("MXR_WGRAD_MIN_STEPS");
-    return e ? std::max(1, std::atoi(e)) : 8;
+    return e ? std::max(1, std::atoi(e)) : 0;
   }();
+  const int min_steps = env_steps > 0 ? env_steps : (planes > 0 ? 8 : 16);
   int splits = 1;
   while (splits < 64 && tiles * splits * 2 <= 2304 && steps / (splits * 2) >= min_steps) splits *= 2;
   *splits_out = splits;

@@ -356,7 +356,7 @@ void conv_wt_flip_multi(const WtFlipEntry* entries, int n_entries, int total_til
 // ---- MFMA weight gradient (conv_wgrad.hip) -------------------------------------
 // dy (NB, Ho, Wo, Cout) bf16, x (NB, H, W, Cin) bf16 -> dw (Cout, KH, KW, Cin) bf16.
 // slab: splits * Cout * KH*KW*Cin floats.  Requires Cin % 64 == 0, Cout % 8 == 0.
-int conv_wgrad_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int* splits_out);
+int conv_wgrad_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, int* splits_out, int planes = 0);
 // fp32-class (x2) weight gradient: dY / X are hi / lo plane pairs (lo planes pdy / px bytes after the
 // hi ones), the gradient dwf is fp32 (dw unused)
 struct WgradX2 {

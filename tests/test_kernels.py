@@ -612,8 +612,9 @@ def test_bn_relu_cpu_twin_matches_tensor_path(channels_last, fix_gamma, relu, mo
 
 @pytest.mark.gpu
 def test_conv_autotune_picks_a_candidate_and_matches(cuda, monkeypatch):
-    """The per-shape autotune (first eager call) caches a tile choice; outputs equal the
-    static-plan result bitwise (every candidate accumulates in the same K order)."""
+    """The per-shape autotune (first eager call) caches a tile choice; its output is the
+    chosen tile's own output, and equals the static plan's bitwise unless the choice sums K in a
+    different order (the K-group tiles 27-29, split-K), then to bf16 rounding."""
     from mx_rcnn_amd.ops import need_ext
     ext = need_ext()
     g = torch.Generator().manual_seed(3)
@@ -621,10 +622,15 @@ def test_conv_autotune_picks_a_candidate_and_matches(cuda, monkeypatch):
     w = (torch.randn(256, 256, 3, 3, generator=g) * 0.05).bfloat16().to(cuda).contiguous(
         memory_format=torch.channels_last)
     y_tuned = ext.conv_igemm_fwd(x, w, None, 1, 1, False)[0]
-    keys = [k for k, t, s in ext.conv_tune_table() if k.startswith('1,38,61,256,256,3,3,1,1|')]
-    assert len(keys) == 1
+    hits = [(k, t, s) for k, t, s in ext.conv_tune_table() if k.startswith('1,38,61,256,256,3,3,1,1|')]
+    assert len(hits) == 1
+    _, tile, splits = hits[0]
+    assert torch.equal(y_tuned, ext.conv_igemm_fwd(x, w, None, 1, 1, False, tile, splits)[0])
     y_plan = ext.conv_igemm_fwd(x, w, None, 1, 1, False, 23, 1)[0]
-    assert torch.equal(y_tuned, y_plan)
+    if tile in (27, 28, 29) or splits > 1:
+        assert torch.allclose(y_tuned.float(), y_plan.float(), rtol=1e-2, atol=1e-2)
+    else:
+        assert torch.equal(y_tuned, y_plan)
 
 
 def test_philox_host_twin_statistics():

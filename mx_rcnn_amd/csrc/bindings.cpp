@@ -923,8 +923,8 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
     snprintf(kb, sizeof(kb), "%d,%d,%d,%d,%d,%d,%d,%d,%d|%d%d%d%d%d%d%d%d%d%d%d", NB, H, W, Cin, Cout, KH, KW,
              (int)stride, (int)pad, ep.residual != nullptr, ep.y2 != nullptr || bn.has_value(), bwd_mode,
              ep.dadd != nullptr, ep.relu, ep.bias != nullptr || ep.bias_h != nullptr,
-             (ep.drop_p > 0.f ? 1 : 0) + (stats ? 2 : 0), ep.bt, ep.rmask != nullptr, ep.x2 + ep.x3,
-             ep.bnb_part != nullptr);
+             (ep.drop_p > 0.f ? 1 : 0) + (stats ? 2 : 0), ep.bt, ep.rmask != nullptr, ep.x2 + ep.x3 + (f16 ? 8 : 0),
+             ep.bnb_part != nullptr);  // (f16: the K-group and some ring tiles are bf16-only)
     const std::string key(kb);
     std::unique_lock<std::mutex> lk(g_tune_mu);
     auto it = g_tune.find(key);
@@ -1023,12 +1023,17 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   }
   Tensor slab;
   if (sp > 1) slab = at::empty({(int64_t)sp * NB * Ho * Wo * Cout}, x.options().dtype(at::kFloat));
-  const int used = mxr::conv_igemm_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
-                                       reinterpret_cast<const uint16_t*>(w.data_ptr()),
-                                       out_f32 ? nullptr : reinterpret_cast<uint16_t*>(y.data_ptr()), NB, H, W, Cin,
-                                       Ho, Wo, Cout, KH, KW,
-                                       (int)stride, (int)pad, ep, t, sp, sp > 1 ? slab.data_ptr<float>() : nullptr,
-                                       cur_stream());
+  int used = mxr::conv_igemm_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                                 reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                                 out_f32 ? nullptr : reinterpret_cast<uint16_t*>(y.data_ptr()), NB, H, W, Cin, Ho, Wo,
+                                 Cout, KH, KW, (int)stride, (int)pad, ep, t, sp,
+                                 sp > 1 ? slab.data_ptr<float>() : nullptr, cur_stream());
+  if (used <= 0 && tile <= 0 && t != 23 && !(sp > 1)) {  // a cached choice this epilogue cannot take: the plan tile
+    used = mxr::conv_igemm_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
+                               reinterpret_cast<const uint16_t*>(w.data_ptr()),
+                               out_f32 ? nullptr : reinterpret_cast<uint16_t*>(y.data_ptr()), NB, H, W, Cin, Ho, Wo,
+                               Cout, KH, KW, (int)stride, (int)pad, ep, 23, 1, nullptr, cur_stream());
+  }
   TORCH_CHECK(used > 0, "conv_igemm: unsupported shape");
   if (stats) {
     const int bm = mxr::conv_tile_bm(used);

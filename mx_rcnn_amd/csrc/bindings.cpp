@@ -1597,6 +1597,45 @@ void bnb_part_fold(const Tensor& part, int64_t nparts, int64_t C, c10::optional<
   mxr::col_part_fold(part.data_ptr<float>(), (int)nparts, (int)C, out[0], out[1], cur_stream());
 }
 
+// many bnb_part_fold calls in as few launches as possible: entries (part, nparts, C, dgamma | None,
+// dbeta | None), up to mxr::kMaxFolds per launch
+void bnb_part_fold_multi(const std::vector<std::tuple<Tensor, int64_t, int64_t, c10::optional<Tensor>,
+                                                      c10::optional<Tensor>>>& entries) {
+  if (entries.empty()) return;
+  DevGuard g(std::get<0>(entries[0]).device());
+  mxr::FoldBatch fb{};
+  auto flush = [&]() {
+    if (fb.n > 0) mxr::bn_part_fold_multi(fb, cur_stream());
+    fb.n = 0;
+  };
+  int blk = 0;
+  for (const auto& en : entries) {
+    const Tensor& part = std::get<0>(en);
+    const int64_t np = std::get<1>(en), C = std::get<2>(en);
+    CHECK_DEV(part);
+    TORCH_CHECK(part.scalar_type() == at::kFloat && part.is_contiguous() && np > 0 && part.numel() >= np * 2 * C,
+                "part: fp32 with nparts * 2 * C elements");
+    float* out[2] = {nullptr, nullptr};
+    const c10::optional<Tensor>* opts[2] = {&std::get<4>(en), &std::get<3>(en)};  // (dbeta, dgamma)
+    for (int k = 0; k < 2; ++k) {
+      const auto& o = *opts[k];
+      if (o.has_value() && o->defined()) {
+        TORCH_CHECK(o->scalar_type() == at::kFloat && o->is_contiguous() && o->numel() == C &&
+                        o->device() == part.device(), "dgamma / dbeta: fp32 (C,) on part's device");
+        out[k] = o->data_ptr<float>();
+      }
+    }
+    if (!out[0] && !out[1]) continue;
+    if (fb.n == mxr::kMaxFolds) {
+      flush();
+      blk = 0;
+    }
+    fb.e[fb.n++] = {part.data_ptr<float>(), out[0], out[1], (int)np, (int)C, blk};
+    blk += (int)((2 * C + 63) / 64);
+  }
+  flush();
+}
+
 // finish of a training-BN backward whose BN-backward epilogue (a dgrad conv with bnb_x = x,
 // bn = (gamma_eff, beta, save[0], save[2]), eps 0, bnb_part = part) produced o; nparts partial rows
 Tensor bn_train_dx_apply(Tensor o, const Tensor& x, const Tensor& save, const Tensor& gamma_eff, const Tensor& part,
@@ -2163,6 +2202,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("x2") = 0);
   m.def("bnb_part_fold", &bnb_part_fold, py::arg("part"), py::arg("nparts"), py::arg("C"),
         py::arg("dgamma") = py::none(), py::arg("dbeta") = py::none());
+  m.def("bnb_part_fold_multi", &bnb_part_fold_multi, py::arg("entries"));
   m.def("bn_train_dx_apply", &bn_train_dx_apply, py::arg("o"), py::arg("x"), py::arg("save"), py::arg("gamma_eff"),
         py::arg("part"), py::arg("nparts"), py::arg("dres") = py::none(), py::arg("dgamma") = py::none(),
         py::arg("dbeta") = py::none(), py::arg("x2") = 0);

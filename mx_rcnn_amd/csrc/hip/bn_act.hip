@@ -279,6 +279,48 @@ void bn_relu_bwd(const void* x, const void* dy, int bf16, int64_t M, int C, cons
   if (part) bn_part_reduce<<<(2 * C + 63) / 64, 256, 0, st>>>(part, nblk, C, fix_gamma, dgamma, dbeta, accumulate);
 }
 
+// Many folds in one launch (the deterministic frozen-BN sums of a whole backward pass: one launch
+// per up to kMaxFolds BNs instead of one each).  Workgroup b serves the entry whose block range
+// holds b; each entry's blocks reduce 64 of its 2C columns like bn_part_reduce.
+__global__ void __launch_bounds__(256) bn_part_fold_multi_kernel(FoldBatch fb) {
+  __shared__ float red[4][64];
+  int e = 0;
+  while (e + 1 < fb.n && (int)blockIdx.x >= fb.e[e + 1].blk0) ++e;
+  const FoldEntry& f = fb.e[e];
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  const int i = ((int)blockIdx.x - f.blk0) * 64 + lane;
+  const int C = f.C;
+  float acc = 0.f;
+  if (i < 2 * C) {
+    int b = wid;
+    for (; b + 28 < f.nparts; b += 32) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = f.part[(int64_t)(b + 4 * u) * 2 * C + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) acc += v[u];
+    }
+    for (; b < f.nparts; b += 4) acc += f.part[(int64_t)b * 2 * C + i];
+  }
+  red[wid][lane] = acc;
+  __syncthreads();
+  if (wid == 0 && i < 2 * C) {
+    const float s = red[0][lane] + red[1][lane] + red[2][lane] + red[3][lane];
+    if (i < C) {
+      if (f.out0) f.out0[i] += s;
+    } else if (f.out1) {
+      f.out1[i - C] += s;
+    }
+  }
+}
+
+void bn_part_fold_multi(const FoldBatch& fb, hipStream_t st) {
+  if (fb.n <= 0) return;
+  const FoldEntry& last = fb.e[fb.n - 1];
+  const int blocks = last.blk0 + (2 * last.C + 63) / 64;
+  bn_part_fold_multi_kernel<<<blocks, 256, 0, st>>>(fb);
+}
+
 // Fixed-order fold of nparts partial rows [nparts][2][C] (first half -> out0, second -> out1;
 // either may be null), added to the outputs: the deterministic replacement of per-tile fp32
 // atomics for the BN-backward column sums of the conv epilogues (ConvEpi::bnb_part).

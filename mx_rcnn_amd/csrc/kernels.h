@@ -102,6 +102,19 @@ void roi_pool_fwd(const void* feat, int bf16, int B, int H, int W, int C, const 
 // 1 bf16, 2 fp16); -1 when the H x W slab does not fit LDS (use roi_pool_bwd)
 // grad_add (nullable, NHWC like grad_in): another gradient of the feature map, added in the kernel
 void col_part_fold(const float* part, int nparts, int C, float* out0, float* out1, hipStream_t st);
+// batched col_part_fold (passed by value: kernel arguments, graph-capture safe)
+constexpr int kMaxFolds = 32;
+struct FoldEntry {
+  const float* part;
+  float* out0;
+  float* out1;
+  int nparts, C, blk0;  // blk0: first workgroup of this entry
+};
+struct FoldBatch {
+  FoldEntry e[kMaxFolds];
+  int n;
+};
+void bn_part_fold_multi(const FoldBatch& fb, hipStream_t st);
 int roi_pool_bwd_lds(const void* grad_out, int code, const int32_t* argmax, const float* rois, int R, int PH, int PW,
                      int B, int H, int W, int C, void* grad_in, hipStream_t st, const void* grad_add = nullptr);
 void roi_pool_bwd(const void* grad_out, int bf16, const int32_t* argmax, const float* rois, int R,

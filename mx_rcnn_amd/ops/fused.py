@@ -175,7 +175,10 @@ _SIDE = {}
 # first grouped launch.  Only inside ``defer_reduces()`` (the trainer's backward when no gradient
 # hook reads the flat buffers mid-backward, i.e. no overlapped all-reduce / optimizer), which
 # flushes whatever is still pending on exit.
-_XUNIT = {'on': False, 'pending': None}
+# across-unit deferral inside one backward pass (no gradient hook reads the flat buffers mid-backward):
+# 'pending' a grouped launch's split-K weight-gradient reduce, 'folds' the deterministic frozen-BN
+# gamma / beta folds (run together at the end: a few launches instead of one per BN)
+_XUNIT = {'on': False, 'pending': None, 'folds': []}
 
 
 class defer_reduces(object):
@@ -197,6 +200,9 @@ def flush_deferred():
     if p is not None:
         need_ext().wgrad_reduce_run(*p)
         _XUNIT['pending'] = None
+    if _XUNIT['folds']:
+        need_ext().bnb_part_fold_multi(_XUNIT['folds'])
+        _XUNIT['folds'] = []
 
 
 def grouped_enabled():
@@ -465,11 +471,28 @@ class _FusedUnitFn(torch.autograd.Function):
                 return tg, tb, True
             return tg, tb, False
 
-        def fold_bn(i, part, nparts, tg, tb):
-            """frozen BN(i)'s gamma / beta gradients from the epilogue's partial rows (fixed order)"""
+        folds = []
+
+        def fold_bn(i, part, nparts, tg, tb, now=False):
+            """frozen BN(i)'s gamma / beta gradients from the epilogue's partial rows (fixed order),
+            batched: run by finish_folds (this unit) or flush_deferred (end of the backward); ``now``
+            when the caller reads tg / tb right away (own scratch targets, finish_bn)"""
             gi = nconv + 4 * i
-            ext.bnb_part_fold(part, nparts, bnps[i][0].numel(), tg if need[gi] and not spec.fix[i] else None,
-                              tb if need[gi + 1] else None)
+            ent = (part, nparts, bnps[i][0].numel(), tg if need[gi] and not spec.fix[i] else None,
+                   tb if need[gi + 1] else None)
+            if now:
+                ext.bnb_part_fold_multi([ent])
+            else:
+                folds.append(ent)
+
+        def finish_folds():
+            if not folds:
+                return
+            if _XUNIT['on']:
+                _XUNIT['folds'].extend(folds)
+            else:
+                ext.bnb_part_fold_multi(folds)
+            folds.clear()
 
         def finish_bn(i, tg, tb, returned):
             if returned:
@@ -519,7 +542,7 @@ class _FusedUnitFn(torch.autograd.Function):
                 r = ext.conv_igemm_fwd(dy, wf, None, 1, k - 1 - pad, False, 0, 0, None if train else dres, bwp[bn_i],
                                        beps[bn_i], bfix[bn_i], True, bn_x, dadd, tg, tb, bnb_part=part, **wkw)
             if det:
-                fold_bn(bn_i, part, nparts, tg, tb)
+                fold_bn(bn_i, part, nparts, tg, tb, ret)
             finish_bn(bn_i, tg, tb, ret)
             return train_finish(bn_i, r[0], bn_x, dres, part, nparts) if train else r[0]
 
@@ -541,7 +564,7 @@ class _FusedUnitFn(torch.autograd.Function):
                               bn_fix_gamma=bfix[bn_i], bnb_x=bn_x, dadd=dadd, dgamma=tg, dbeta=tb,
                               param=ctx.params[w_idx], bnb_part=part)
             if det:
-                fold_bn(bn_i, part, nparts, tg, tb)
+                fold_bn(bn_i, part, nparts, tg, tb, ret)
             finish_bn(bn_i, tg, tb, ret)
             return train_finish(bn_i, r[0], bn_x, dres, part, nparts) if train else r[0]
 
@@ -599,6 +622,7 @@ class _FusedUnitFn(torch.autograd.Function):
             flush_pending()
             if used_side[0]:
                 main.wait_stream(side)
+            finish_folds()
             return (None, None, None) + tuple(grads)
         d_sc = None
         if not spec.dim_match:
@@ -630,6 +654,7 @@ class _FusedUnitFn(torch.autograd.Function):
         flush_pending()
         if used_side[0]:
             main.wait_stream(side)
+        finish_folds()
         return (None, d_x if ctx.needs_input_grad[1] else None, None) + tuple(grads)
 
 

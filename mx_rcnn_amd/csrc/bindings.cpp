@@ -890,6 +890,13 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   }
   int auto_splits = 1;
   int t = mxr::conv_igemm_plan(NB, Ho, Wo, Cin, Cout, KH, KW, (int)tile, &auto_splits);
+  // fp32 triples: the 64x64 tile's ring depth in the plan (MXR_X3_FWD_S=2: tile 30, 48 KB, three
+  // workgroups per CU instead of two; A/B knob, the autotune also times tile 30)
+  static const int x3_fwd_s = [] {
+    const char* e = getenv("MXR_X3_FWD_S");
+    return e != nullptr && e[0] == '2' ? 2 : 3;
+  }();
+  if (ep.x3 && tile <= 0 && t == 23 && x3_fwd_s == 2) t = 30;
   // BN-backward epilogue: no split-K by default (the statistics are reduced in-tile instead)
   int sp = splits > 0 ? (int)splits : ((bwd_mode || stats) ? 1 : auto_splits);
   if (stats) {

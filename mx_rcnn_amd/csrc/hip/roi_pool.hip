@@ -258,15 +258,28 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
   float mx[CW];
 #pragma unroll
   for (int k = 0; k < CW; ++k) mx[k] = 0.f;
+  // (only a bound is needed: every bin's |dY| regardless of its argmax, and with planes the hi plane
+  // alone -- |v| <= |hi| * (1 + 2^-7) -- so this pass reads 8 B per 4 channels, not dY + argmax)
+  const int hi_off = code == 4 ? 1 : 0;  // x3 planes (mid, hi, lo); x2 (hi, lo)
   for (int i = threadIdx.x; i < nb; i += blockDim.x) {
     if ((int)rois[(int64_t)(i / PHW) * 5] != b) continue;
+    const int64_t base = (int64_t)i * C + c0;
     float g[CW];
-    int a[CW];
-    load_g(i, g, a);
+    if constexpr (CW == 4 && sizeof(T) == 2) {
+      const ushort4 v = *reinterpret_cast<const ushort4*>(gout + base + (code >= 3 ? hi_off * oplane : 0));
+      g[0] = to_f(v.x, code >= 3 ? 1 : code); g[1] = to_f(v.y, code >= 3 ? 1 : code);
+      g[2] = to_f(v.z, code >= 3 ? 1 : code); g[3] = to_f(v.w, code >= 3 ? 1 : code);
+    } else {
 #pragma unroll
-    for (int k = 0; k < CW; ++k)
-      if (a[k] >= 0 && a[k] < HW) mx[k] = fmaxf(mx[k], fabsf(g[k]));
+      for (int k = 0; k < CW; ++k)
+        g[k] = to_f(gout[base + k + (code >= 3 ? hi_off * oplane : 0)], code >= 3 ? 1 : code);
+    }
+#pragma unroll
+    for (int k = 0; k < CW; ++k) mx[k] = fmaxf(mx[k], fabsf(g[k]));
   }
+  if (code >= 3)
+#pragma unroll
+    for (int k = 0; k < CW; ++k) mx[k] *= 1.0f + 1.0f / 64.0f;
 #pragma unroll
   for (int k = 0; k < CW; ++k) mx[k] = wave_max(mx[k]);
   if ((threadIdx.x & 63) == 0)

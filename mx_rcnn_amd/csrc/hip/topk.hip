@@ -6,6 +6,7 @@
 //
 //   topk_hist_kernel<0..2>, topk_count_kernel, topk_write_kernel  grid (ceil(N / 2048), B): grid
 //       radix select of the P-th largest key and the stable top-P candidate set (below)
+//   topk_chunk_sort_kernel + topk_merge_rank_kernel (P <= 20480, below), else
 //   topk_rank_kernel    grid (ceil(P/64), B): four lanes rank one candidate against all P of its
 //       image by counting (64-bit compares of (key, ~index) packed words streamed through LDS, the
 //       reads are broadcasts) and the first scatters key + box to its rank.
@@ -178,13 +179,17 @@ topk_hist_kernel(const float* __restrict__ keys, int N, int P, uint32_t* __restr
                                                     (pre >> (shift + (PASS == 1 ? 11 : 10))));
     const uint32_t bin = (u[j] >> shift) & dmask;
     uint64_t active = __ballot(in);
-    while (active) {  // one LDS atomic per distinct bin of the wave (clustered scores)
+    // the wave's most frequent bins with one LDS atomic each (clustered scores put most of a wave in
+    // a few top-digit bins), then the scattered rest directly (the low digits are spread: a
+    // per-distinct-bin loop would run up to 64 rounds)
+    for (int it = 0; it < 4 && active; ++it) {
       const int leader = __ffsll((long long)active) - 1;
       const uint32_t b0 = __shfl(bin, leader, 64);
       const uint64_t m = __ballot(bin == b0) & active;
       if (lane == leader) atomicAdd(&h[b0], (uint32_t)__popcll(m));
       active &= ~m;
     }
+    if ((active >> lane) & 1ull) atomicAdd(&h[bin], 1u);
   }
   __syncthreads();
   uint32_t* gh = w.hist + ((int64_t)b * 3 + PASS) * kTkBins;
@@ -321,6 +326,83 @@ topk_rank_kernel(const uint32_t* __restrict__ cand_key, const int* __restrict__ 
   }
 }
 
+// ---- ranking the P candidates: chunk sort + merge ranks (O(P log P)) -------------------------------
+// topk_rank_kernel counts, for every candidate, the candidates above it: O(P^2) compares (79 us at
+// P = 12000).  Here each 1024-candidate chunk is bitonic-sorted in LDS and written back in place
+// (candidate slots of the chunk, key and index words), then every candidate's rank is its position
+// in its chunk plus, for each other chunk, the number of its words above (a binary search over the
+// whole sorted candidate set held in LDS: P * 8 B, P <= 20480).  Words (key, ~index) are distinct,
+// so the ranks are a permutation and the order is the stable descending one.
+constexpr int kTkSortChunk = 1024;
+constexpr int kTkMergeMaxP = 20480;  // 160 KB of 8-B words
+
+__global__ void __launch_bounds__(512)
+topk_chunk_sort_kernel(uint32_t* __restrict__ cand_key, int* __restrict__ cand_idx, int P) {
+  __shared__ uint64_t w[kTkSortChunk];
+  const int b = blockIdx.y, c0 = blockIdx.x * kTkSortChunk, tid = threadIdx.x;
+  const int len = min(kTkSortChunk, P - c0);
+  uint32_t* ck = cand_key + (int64_t)b * P + c0;
+  int* ci = cand_idx + (int64_t)b * P + c0;
+  for (int i = tid; i < kTkSortChunk; i += 512)
+    w[i] = i < len ? ((uint64_t)ck[i] << 32) | (uint32_t)~(uint32_t)ci[i] : 0ull;  // pads sort last
+  __syncthreads();
+  for (int k = 2; k <= kTkSortChunk; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        const int i = tid + q * 512, ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t a = w[i], c = w[ixj];
+          const bool desc = (i & k) == 0;
+          if ((a < c) == desc) {
+            w[i] = c;
+            w[ixj] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = tid; i < len; i += 512) {
+    ck[i] = (uint32_t)(w[i] >> 32);
+    ci[i] = (int)~(uint32_t)w[i];
+  }
+}
+
+__global__ void __launch_bounds__(1024)
+topk_merge_rank_kernel(const uint32_t* __restrict__ cand_key, const int* __restrict__ cand_idx,
+                       const float* __restrict__ boxes, int N, int P, float* __restrict__ skeys,
+                       float* __restrict__ sboxes) {
+  extern __shared__ uint64_t all[];  // the whole sorted candidate set of this image
+  const int b = blockIdx.y, tid = threadIdx.x;
+  const uint32_t* ck = cand_key + (int64_t)b * P;
+  const int* ci = cand_idx + (int64_t)b * P;
+  for (int i = tid; i < P; i += 1024) all[i] = ((uint64_t)ck[i] << 32) | (uint32_t)~(uint32_t)ci[i];
+  __syncthreads();
+  const int mine = blockIdx.x, p = mine * kTkSortChunk + tid;
+  if (p >= P) return;
+  const uint64_t v = all[p];
+  int rank = tid;  // position in its own (sorted) chunk
+  const int nch = (P + kTkSortChunk - 1) / kTkSortChunk;
+  for (int c = 0; c < nch; ++c) {
+    if (c == mine) continue;
+    const uint64_t* s = all + c * kTkSortChunk;
+    int lo = 0, hi = min(kTkSortChunk, P - c * kTkSortChunk);  // count of s[] > v: a prefix (descending)
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (s[mid] > v) lo = mid + 1;
+      else hi = mid;
+    }
+    rank += lo;
+  }
+  const int idx = (int)~(uint32_t)v;
+  if (rank < P && (unsigned)idx < (unsigned)N) {
+    skeys[(int64_t)b * P + rank] = unord_key((uint32_t)(v >> 32));
+    const float4 bx = *reinterpret_cast<const float4*>(boxes + ((int64_t)b * N + idx) * 4);
+    *reinterpret_cast<float4*>(sboxes + ((int64_t)b * P + rank) * 4) = bx;
+  }
+}
+
 int64_t proposal_topk_ws_words(int B, int N) { return topk_ws_words(B, (N + kTkChunk - 1) / kTkChunk); }
 
 int proposal_topk(const float* keys, const float* boxes, int B, int N, int P, uint32_t* ws, uint32_t* ws_key,
@@ -333,7 +415,19 @@ int proposal_topk(const float* keys, const float* boxes, int B, int N, int P, ui
   topk_hist_kernel<2><<<grid, kTkThreads, 0, st>>>(keys, N, P, ws);
   topk_count_kernel<<<grid, kTkThreads, 0, st>>>(keys, N, P, ws);
   topk_write_kernel<<<grid, kTkThreads, 0, st>>>(keys, N, P, ws, ws_key, ws_idx, n_valid);
-  topk_rank_kernel<<<dim3(div_up(P, 64), B), 256, 0, st>>>(ws_key, ws_idx, boxes, N, P, skeys, sboxes);
+  if (P <= kTkMergeMaxP) {
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)topk_merge_rank_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                kTkMergeMaxP * 8);
+      attr = true;
+    }
+    const dim3 g2(div_up(P, kTkSortChunk), B);
+    topk_chunk_sort_kernel<<<g2, 512, 0, st>>>(ws_key, ws_idx, P);
+    topk_merge_rank_kernel<<<g2, 1024, (size_t)P * 8, st>>>(ws_key, ws_idx, boxes, N, P, skeys, sboxes);
+  } else {
+    topk_rank_kernel<<<dim3(div_up(P, 64), B), 256, 0, st>>>(ws_key, ws_idx, boxes, N, P, skeys, sboxes);
+  }
   return 0;
 }
 

@@ -1020,7 +1020,11 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
       }
       // leave the static plan only for a clear win: near ties measured in isolation did not
       // survive the concurrent streams of the real step (profiles/r2_conv_tune_choices.txt)
-      if (best > 0.9f * plan_ms) pick = cands[0];
+      static const float margin = [] {  // A/B knob MXR_TUNE_MARGIN (default 0.9: a 10 % win)
+        const char* e = getenv("MXR_TUNE_MARGIN");
+        return e != nullptr ? (float)atof(e) : 0.9f;
+      }();
+      if (best > margin * plan_ms) pick = cands[0];
       hipEventDestroy(e0);
       hipEventDestroy(e1);
       g_tune[key] = pick;

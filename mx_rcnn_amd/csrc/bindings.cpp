@@ -541,7 +541,7 @@ Tensor loss_combine(std::vector<Tensor> terms, std::vector<double> weights, c10:
 // ---- optimizer -------------------------------------------------------------------------
 void sgd_momentum(Tensor w, Tensor mom, const Tensor& grad, const Tensor& lr, double momentum, double wd,
                   double rescale, double clip, c10::optional<Tensor> w_bf16, int64_t planes,
-                  c10::optional<Tensor> zero) {
+                  c10::optional<Tensor> zero, int64_t plane_stride) {
   CHECK_DEV(w); CHECK_F32(w); CHECK_CONTIG(w); CHECK_DEV(mom); CHECK_F32(mom); CHECK_CONTIG(mom);
   CHECK_DEV(grad); CHECK_CONTIG(grad); CHECK_DEV(lr); CHECK_F32(lr);
   TORCH_CHECK(w.numel() == mom.numel() && w.numel() == grad.numel(), "size mismatch");
@@ -550,12 +550,21 @@ void sgd_momentum(Tensor w, Tensor mom, const Tensor& grad, const Tensor& lr, do
   if (w_bf16.has_value() && w_bf16->defined()) {
     // planes 2 / 3: the shadow is the x2 pair / x3 triple of the fp32 modes (common.h), its planes
     // numel / planes elements apart (>= n, a multiple of 8 so every plane's rows stay 16-B aligned)
-    TORCH_CHECK(w_bf16->scalar_type() == at::kBFloat16 && w_bf16->is_contiguous() && planes >= 1 && planes <= 3 &&
-                    w_bf16->numel() % planes == 0 && w_bf16->numel() / planes >= w.numel() &&
-                    (planes == 1 || (w_bf16->numel() / planes) % 8 == 0),
-                "w_bf16 must be contiguous bf16 of `planes` planes of >= numel elements (multiples of 8)");
-    wb = reinterpret_cast<uint16_t*>(w_bf16->data_ptr());
-    if (planes > 1) x2_plane = w_bf16->numel() / planes;
+    if (plane_stride > 0 && planes > 1) {
+      // a bucket slice of a store's shadow: plane k at [k * plane_stride, + numel) of the view
+      TORCH_CHECK(w_bf16->scalar_type() == at::kBFloat16 && w_bf16->is_contiguous() && planes <= 3 &&
+                      w_bf16->numel() >= (planes - 1) * plane_stride + w.numel() && plane_stride >= w.numel(),
+                  "w_bf16 slice: bf16 view reaching (planes - 1) * plane_stride + numel elements");
+      wb = reinterpret_cast<uint16_t*>(w_bf16->data_ptr());
+      x2_plane = plane_stride;
+    } else {
+      TORCH_CHECK(w_bf16->scalar_type() == at::kBFloat16 && w_bf16->is_contiguous() && planes >= 1 && planes <= 3 &&
+                      w_bf16->numel() % planes == 0 && w_bf16->numel() / planes >= w.numel() &&
+                      (planes == 1 || (w_bf16->numel() / planes) % 8 == 0),
+                  "w_bf16 must be contiguous bf16 of `planes` planes of >= numel elements (multiples of 8)");
+      wb = reinterpret_cast<uint16_t*>(w_bf16->data_ptr());
+      if (planes > 1) x2_plane = w_bf16->numel() / planes;
+    }
   }
   void* zp = nullptr;
   int zb = 0;
@@ -2159,7 +2168,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("loss_combine", &loss_combine, py::arg("terms"), py::arg("weights"), py::arg("nonfinite") = py::none());
   m.def("sgd_momentum", &sgd_momentum, py::arg("w"), py::arg("mom"), py::arg("grad"), py::arg("lr"),
         py::arg("momentum"), py::arg("wd"), py::arg("rescale"), py::arg("clip"), py::arg("w_bf16") = py::none(),
-        py::arg("planes") = 1, py::arg("zero") = py::none());
+        py::arg("planes") = 1, py::arg("zero") = py::none(), py::arg("plane_stride") = 0);
   m.def("bn_relu_fwd", &bn_relu_fwd, py::arg("x"), py::arg("gamma"), py::arg("beta"), py::arg("mean"), py::arg("var"),
         py::arg("eps"), py::arg("fix_gamma"), py::arg("relu"), py::arg("x2") = 0);
   m.def("bn_relu_bwd", &bn_relu_bwd, py::arg("x"), py::arg("dy"), py::arg("gamma"), py::arg("beta"),

@@ -5,7 +5,8 @@ import torch
 from ._ext import ext_available, need_ext
 
 
-def sgd_momentum_(w, mom, grad, lr, momentum=0.9, wd=0.0, rescale=1.0, clip=-1.0, w_bf16=None, planes=1, zero=None):
+def sgd_momentum_(w, mom, grad, lr, momentum=0.9, wd=0.0, rescale=1.0, clip=-1.0, w_bf16=None, planes=1, zero=None,
+                  plane_stride=0):
     """In-place update of flat fp32 ``w``/``mom`` from ``grad`` (fp32 or bf16).
 
     ``lr`` is a 1-element fp32 device tensor (read in-kernel: graph-replay safe).
@@ -13,11 +14,14 @@ def sgd_momentum_(w, mom, grad, lr, momentum=0.9, wd=0.0, rescale=1.0, clip=-1.0
     their bf16x3 pair / fp32 triple (ops/precision.py), planes ``w_bf16.numel() // planes`` apart.
     ``zero`` (optional, fp32 or bf16, w's size; may be ``grad`` itself): cleared after it is read,
     so the next step's gradient writers start from zero without a separate fill.
+    ``plane_stride`` (GPU): ``w_bf16`` is a view into a store's shadow whose planes sit
+    ``plane_stride`` elements apart (a bucket slice of a multi-plane group).
     """
     if w.is_cuda:
         need_ext().sgd_momentum(w, mom, grad, lr, float(momentum), float(wd), float(rescale), float(clip), w_bf16,
-                                int(planes), zero)
+                                int(planes), zero, int(plane_stride))
         return
+    assert not plane_stride, 'plane_stride: GPU only'
     try:
         _sgd_host(w, mom, grad, lr, momentum, wd, rescale, clip, w_bf16, planes)
     finally:

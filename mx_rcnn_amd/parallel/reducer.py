@@ -73,10 +73,8 @@ class BucketReducer:
         # off by default: measured 2-3 % slower on 1-GPU ResNet-101 (scripts/gpu_sgd.sh A/B, 125-126
         # vs 128-129 img/s): the HBM-bound update steals bandwidth from the concurrent backward
         # convs for less than it hides (the whole update is ~0.16 ms)
-        # (not with the fp32-class x2 store: its shadow's lo plane is one group further, not sliceable
-        # per bucket)
-        self.sgd_capable = (store.device.type == 'cuda' and os.environ.get('MXR_OVERLAP_SGD', '0') == '1'
-                            and not getattr(store, 'x2', False))
+        # (multi-plane stores: a bucket's planes are slices one group plane apart -- plane_stride)
+        self.sgd_capable = store.device.type == 'cuda' and os.environ.get('MXR_OVERLAP_SGD', '0') == '1'
         self.buckets = []
         self._param_bucket = {}
         self._sgd = None
@@ -174,9 +172,12 @@ class BucketReducer:
         with torch.cuda.stream(os_):
             if b.work is not None:
                 b.work.wait()  # the optimizer stream waits for this bucket's collective
+            if g.shadow is not None and g.x2:  # planes g.plane apart: the view from s reaches all of them
+                sh, planes, stride = g.shadow[s:], g.x2, g.plane
+            else:
+                sh, planes, stride = (None if g.shadow is None else g.shadow[s:e]), 1, 0
             sgd_momentum_(g.master[s:e], g.mom[s:e], self.grad_for(g)[s:e], lr, mu, wd if g.decay else 0.0, rescale,
-                          clip, None if g.shadow is None else g.shadow[s:e],
-                          zero=g.grad[s:e] if self._clear else None)
+                          clip, sh, planes=planes, zero=g.grad[s:e] if self._clear else None, plane_stride=stride)
         b.updated = True
 
     def prepare(self, sgd=None, clear=False):

@@ -100,6 +100,70 @@ roi_pool_fwd_vec4(const T* __restrict__ feat, int code, int B, int H, int W, int
   if (argmax) *reinterpret_cast<int4*>(argmax + o) = make_int4(a0, a1, a2, a3);  // null: inference, no backward
 }
 
+// 8 channels per lane, single-plane 16-bit maps (bf16 / fp16): 16-B loads, two bin pixels per
+// iteration in flight; the batch-8 inference pooling (2400 RoIs x 49 bins x 1024 channels) is a
+// latency-bound gather at 4 channels per lane and one load at a time
+__global__ void __launch_bounds__(256)
+roi_pool_fwd_vec8(const uint16_t* __restrict__ feat, int code, int B, int H, int W, int C,
+                  const float* __restrict__ rois, int R, int PH, int PW, float scale, uint16_t* __restrict__ out,
+                  int32_t* __restrict__ argmax) {
+  const int CV = C >> 3;
+  const int64_t total = (int64_t)R * PH * PW * CV;
+  const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= total) return;
+  const int cv = (int)(t % CV);
+  int64_t rest = t / CV;
+  const int pw = (int)(rest % PW); rest /= PW;
+  const int ph = (int)(rest % PH);
+  const int r = (int)(rest / PH);
+  const Bin bin = roi_bin(rois, r, ph, pw, PH, PW, H, W, scale);
+  float m[8];
+  int a[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    m[k] = 0.f;
+    a[k] = -1;
+  }
+  if (!(bin.empty || bin.b >= B)) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m[k] = -FLT_MAX;
+    const uint16_t* fb = feat + (int64_t)bin.b * H * W * C + (int64_t)cv * 8;
+    const int bw = bin.we - bin.ws, npx = (bin.he - bin.hs) * bw;
+    auto upd = [&](const uint4 v, int idx) {
+      const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float f0 = h16_to_f32((uint16_t)(wv[k] & 0xffffu), code), f1 = h16_to_f32((uint16_t)(wv[k] >> 16), code);
+        if (f0 > m[2 * k]) { m[2 * k] = f0; a[2 * k] = idx; }
+        if (f1 > m[2 * k + 1]) { m[2 * k + 1] = f1; a[2 * k + 1] = idx; }
+      }
+    };
+    int q = 0;
+    for (; q + 1 < npx; q += 2) {  // row-major order kept: the two loads are issued together, compared in order
+      const int i0 = (bin.hs + q / bw) * W + bin.ws + q % bw;
+      const int i1 = (bin.hs + (q + 1) / bw) * W + bin.ws + (q + 1) % bw;
+      const uint4 v0 = *reinterpret_cast<const uint4*>(fb + (int64_t)i0 * C);
+      const uint4 v1 = *reinterpret_cast<const uint4*>(fb + (int64_t)i1 * C);
+      upd(v0, i0);
+      upd(v1, i1);
+    }
+    if (q < npx) {
+      const int i0 = (bin.hs + q / bw) * W + bin.ws + q % bw;
+      upd(*reinterpret_cast<const uint4*>(fb + (int64_t)i0 * C), i0);
+    }
+  }
+  uint32_t o[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    o[k] = (uint32_t)f32_to_h16(m[2 * k], code) | ((uint32_t)f32_to_h16(m[2 * k + 1], code) << 16);
+  *reinterpret_cast<uint4*>(out + t * 8) = make_uint4(o[0], o[1], o[2], o[3]);
+  if (argmax) {
+    int4* ap = reinterpret_cast<int4*>(argmax + t * 8);
+    ap[0] = make_int4(a[0], a[1], a[2], a[3]);
+    ap[1] = make_int4(a[4], a[5], a[6], a[7]);
+  }
+}
+
 template <typename T>
 __global__ void __launch_bounds__(256)
 roi_pool_fwd_scalar(const T* __restrict__ feat, int code, int B, int H, int W, int C, const float* __restrict__ rois, int R,
@@ -149,6 +213,12 @@ roi_pool_bwd_kernel(const T* __restrict__ gout, const int32_t* __restrict__ argm
 void roi_pool_fwd(const void* feat, int bf16, int B, int H, int W, int C, const float* rois, int R, int PH, int PW,
                   float spatial_scale, void* out, int32_t* argmax, hipStream_t st) {
   if (R == 0 || C == 0) return;
+  if (C % 8 == 0 && (bf16 == 1 || bf16 == 2)) {  // single-plane 16-bit: 8 channels per lane
+    const int64_t total = (int64_t)R * PH * PW * (C / 8);
+    roi_pool_fwd_vec8<<<div_up(total, 256), 256, 0, st>>>((const uint16_t*)feat, bf16, B, H, W, C, rois, R, PH, PW,
+                                                          spatial_scale, (uint16_t*)out, argmax);
+    return;
+  }
   if (C % 4 == 0) {
     const int64_t total = (int64_t)R * PH * PW * (C / 4);
     if (bf16)

@@ -1,53 +1,49 @@
-"""Summarise rocprofv3 --pmc counter CSVs: per (kernel, counter) the mean over dispatches.
+"""Per-kernel PMC summary of a rocprofv3 --pmc run (counter_collection.csv): mean counter value per
+dispatch for the kernels whose name matches a filter, plus derived ratios.
 
-    python tools/pmc_summary.py DIR [DIR ...] [--kernel SUBSTR]
+    python tools/pmc_summary.py DIR [--match conv_igemm_buf_kernel,conv_x2w_kernel] [--label NAME]
 """
+import argparse
 import csv
 import glob
+import json
 import os
-import sys
 from collections import defaultdict
 
 
-def load(d, kfilter=None):
-    out = defaultdict(lambda: defaultdict(list))
-    for f in glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True):
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('dir')
+    ap.add_argument('--match', default='conv_igemm_buf_kernel,conv_x2w_kernel')
+    ap.add_argument('--label', default='')
+    a = ap.parse_args()
+    files = glob.glob(os.path.join(a.dir, '**', '*counter_collection.csv'), recursive=True)
+    if not files:
+        raise SystemExit('no counter_collection.csv under %s' % a.dir)
+    pats = [p for p in a.match.split(',') if p]
+    acc = defaultdict(lambda: defaultdict(float))
+    disp = defaultdict(set)
+    for f in files:
         with open(f) as fh:
             for row in csv.DictReader(fh):
-                k = row.get('Kernel_Name', '')
-                if kfilter and kfilter not in k:
+                name = row.get('Kernel_Name', '')
+                pat = next((p for p in pats if p in name), None)
+                if pat is None:
                     continue
-                key = (row.get('Dispatch_Id'), k)
-                out[k][row['Counter_Name']].append((key, float(row['Counter_Value'])))
-    res = {}
-    for k, cs in out.items():
-        res[k] = {}
-        for c, vals in cs.items():
-            per = defaultdict(float)  # sum over dimension instances (XCDs / SEs) per dispatch
-            for key, v in vals:
-                per[key] += v
-            res[k][c] = sum(per.values()) / max(1, len(per))
-    return res
-
-
-def main():
-    args = [a for a in sys.argv[1:] if not a.startswith('--')]
-    kf = None
-    if '--kernel' in sys.argv:
-        kf = sys.argv[sys.argv.index('--kernel') + 1]
-        args = [a for a in args if a != kf]
-    for d in args:
-        for k, cs in load(d, kf).items():
-            print('## %s :: %s' % (os.path.basename(d.rstrip('/')), k[:90]))
-            for c in sorted(cs):
-                print('   %-40s %16.1f' % (c, cs[c]))
-            if 'SQ_WAVE_CYCLES' in cs and cs['SQ_WAVE_CYCLES']:
-                w = cs['SQ_WAVE_CYCLES']
-                print('   -> wait_any %.1f%%  wait_inst %.1f%%' % (100 * cs.get('SQ_WAIT_ANY', 0) / w,
-                                                                 100 * cs.get('SQ_WAIT_INST_ANY', 0) / w))
-            if 'TCC_HIT_sum' in cs:
-                h, m = cs['TCC_HIT_sum'], cs.get('TCC_MISS_sum', 0)
-                print('   -> L2 hit %.1f%%' % (100 * h / max(1, h + m)))
+                key = '%s grid=%s' % (pat, row.get('Grid_Size', row.get('Grid_Size_X', '?')))
+                acc[key][row['Counter_Name']] += float(row['Counter_Value'])
+                disp[key].add(row.get('Dispatch_Id', row.get('Correlation_Id', '')))
+    for key in sorted(acc):
+        n = max(1, len(disp[key]))
+        c = {k: v / n for k, v in acc[key].items()}
+        out = {'label': a.label, 'kernel': key, 'dispatches': n}
+        out.update({k: round(v, 1) for k, v in sorted(c.items())})
+        hit, miss = c.get('TCC_HIT_sum'), c.get('TCC_MISS_sum')
+        if hit is not None and miss is not None and hit + miss > 0:
+            out['l2_hit_rate'] = round(hit / (hit + miss), 4)
+        if c.get('SQ_WAVE_CYCLES'):
+            out['wait_frac'] = round(c.get('SQ_WAIT_ANY', 0.0) / c['SQ_WAVE_CYCLES'], 4)
+        print(json.dumps(out))
 
 
 if __name__ == '__main__':

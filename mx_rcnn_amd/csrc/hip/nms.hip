@@ -110,23 +110,15 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
   // block pairs of the next iteration.  Every prefetch is loaded into the variable it is
   // consumed from, AFTER the consumption: a loop-carried copy (x = x_next) would make the
   // compiler wait for the prefetch at the end of every iteration.
-  // wave 0 prefetches TWO blocks ahead: even blocks use (diagA, wprevA), odd ones (diagB, wprevB),
-  // each set refilled for block t + 2 right after block t consumed it (the loop is unrolled by two,
-  // so no loop-carried copy makes the compiler wait for the load just issued)
-  uint64_t diagA = 0, wprevA = 0, diagB = 0, wprevB = 0;
+  uint64_t diag = 0, wprev = 0;
   u64x2 pf[NMS_PF];
 #pragma unroll
   for (int k = 0; k < NMS_PF; ++k) pf[k] = u64x2{0ull, 0ull};
-  if (wave == 0 && nbv > 0) {
-    diagA = mb[nms_col(0, lane)];
-    if (nb > 1) {
-      diagB = mb[Pp + nms_col(1, lane)];
-      wprevB = mb[nms_col(1, lane)];
-    }
-  }
+  if (wave == 0 && nbv > 0) diag = mb[nms_col(0, lane)];
   __syncthreads();
-  auto iter = [&](int t, uint64_t& diag, uint64_t& wprev) -> bool {
-    if (s_nk[t & 1] >= post) return true;  // uniform: written before the last barrier, not rewritten until the next
+  int t = 0;
+  for (; t < nbv; ++t) {
+    if (s_nk[t & 1] >= post) break;  // uniform: written before the last barrier, not rewritten until the next
     if (wave == 0) {
       const int j = t * 64 + lane;
       const uint64_t kp = t > 0 ? keptw[t - 1] : 0ull;
@@ -141,10 +133,10 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
         if (next == kept) break;
         kept = next;
       }
-      // prefetch block t+2 into this parity's set (clamped to in-range words near the end)
-      const int tn = min(t + 2, nb - 1);
+      // prefetch block t+1 (clamped to an in-range word on the last block)
+      const int tn = min(t + 1, nb - 1);
       diag = mb[(int64_t)tn * Pp + nms_col(tn, lane)];
-      wprev = mb[(int64_t)max(tn - 1, 0) * Pp + nms_col(tn, lane)];
+      wprev = mb[(int64_t)t * Pp + nms_col(tn, lane)];
       const int nk = s_nk[t & 1];
       if (nk + __popcll(kept) > post) {  // keep only the lowest (post - nk) boxes of this block
         int need = post - nk;
@@ -218,14 +210,6 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
       }
     }
     __syncthreads();
-    return false;
-  };
-  int t = 0;
-  while (t < nbv) {
-    if (iter(t, diagA, wprevA)) break;
-    if (++t >= nbv) break;
-    if (iter(t, diagB, wprevB)) break;
-    ++t;
   }
   // the loop ends right after a barrier (break) or after the last one (t == nbv): s_nk[t & 1]
   // is the final count either way

@@ -12,7 +12,9 @@ environment wins.
   (the compute stream plus one side stream at a time: anchor targets / RPN losses / proposal
   chain / dgrad filter cache), and every extra queue adds cross-queue dependency waits.
   Measured on the ResNet-101 e2e step (bench.py, same box, interleaved): 1 queue 157.2,
-  2 queues 159.7, 3 queues 150.8, default 151.5 img/s (docs/DESIGN.md §2).
+  2 queues 159.7, 3 queues 150.8, default 151.5 img/s (docs/DESIGN.md §2); round 4
+  (profiles/r4_ab_defaults.txt): fp32 77.4 with 2 vs 75.9 / 75.9 / 75.7 with the default / 1 / 3,
+  bf16 160.3 vs 151.4 / 159.4.
 """
 import os
 import sys

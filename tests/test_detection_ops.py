@@ -616,7 +616,11 @@ def test_nest_kernel_matches_reference(cuda):
 @pytest.mark.gpu
 @pytest.mark.parametrize('B,N,P,ties', [(1, 50400, 12000, False), (2, 50400, 6000, True), (3, 1000, 1000, True),
                                         (1, 7000, 6000, False), (8, 50400, 6000, False), (8, 50400, 12000, True),
-                                        (2, 50401, 50401, False)])
+                                        (2, 50401, 50401, False),
+                                        # chunk-sort / merge-rank boundaries (1024-candidate chunks, the
+                                        # 20480-candidate LDS limit, and the counting fallback above it)
+                                        (1, 5000, 1024, True), (1, 5000, 1025, False), (1, 30000, 20480, True),
+                                        (1, 30000, 20481, False)])
 def test_proposal_topk_matches_stable_sort(cuda, B, N, P, ties):
     """Radix-select + rank-by-counting top-P == stable descending sort truncated to P (keys, boxes,
     valid count), with heavy ties and -inf (filtered) entries."""

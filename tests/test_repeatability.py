@@ -210,3 +210,29 @@ def test_frozen_bn_column_sums_partial_rows(cuda, P):
     assert torch.equal(outs[0][0], ra)
     assert torch.allclose(outs[0][1], tg, rtol=1e-5, atol=1e-5 * float(tg.abs().max()))
     assert torch.allclose(outs[0][2], tb, rtol=1e-5, atol=1e-5 * float(tb.abs().max()))
+
+
+@pytest.mark.gpu
+def test_bnb_part_fold_multi_matches_single_folds(cuda):
+    """The batched fold (one launch for many BNs, up to 32 per launch) == one fold per BN, bitwise,
+    with some entries folding only dbeta (fix_gamma) and more entries than one launch holds."""
+    from mx_rcnn_amd.ops import need_ext
+    ext = need_ext()
+    g = torch.Generator().manual_seed(12)
+    ents, ref = [], []
+    for i in range(37):
+        C = [64, 256, 1024, 512][i % 4]
+        nparts = 1 + (i * 7) % 70
+        part = torch.randn(nparts * 2 * C, generator=g).to(cuda)
+        base_g, base_b = torch.randn(C, generator=g).to(cuda), torch.randn(C, generator=g).to(cuda)
+        dg, db = base_g.clone(), base_b.clone()
+        ext.bnb_part_fold(part, nparts, C, None if i % 5 == 0 else dg, db)
+        ref.append((dg, db))
+        mg, mb = base_g.clone(), base_b.clone()
+        ents.append((part, nparts, C, None if i % 5 == 0 else mg, mb))
+    ext.bnb_part_fold_multi(ents)
+    torch.cuda.synchronize()
+    for (p, n, C, mg, mb), (dg, db) in zip(ents, ref):
+        assert torch.equal(mb, db)
+        if mg is not None:
+            assert torch.equal(mg, dg)

@@ -110,34 +110,15 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
   // block pairs of the next iteration.  Every prefetch is loaded into the variable it is
   // consumed from, AFTER the consumption: a loop-carried copy (x = x_next) would make the
   // compiler wait for the prefetch at the end of every iteration.
-  // wave 0 prefetches TWO blocks ahead: even blocks use (diagA, wprevA), odd ones (diagB, wprevB),
-  // each set refilled for block t + 2 right after block t consumed it (the loop is unrolled by two,
-  // so no loop-carried copy makes the compiler wait for the load just issued)
-  uint64_t diagA = 0, wprevA = 0, diagB = 0, wprevB = 0;
-  // helpers: two prefetch sets as well -- iteration t folds row block t-1 from set (t & 1), loaded two
-  // iterations earlier, and refills it with row block t+1 for iteration t+2.  The triangle (18 MB at
-  // P = 12000) streams from beyond L2, so a one-iteration prefetch left every block waiting on it.
-  u64x2 pfA[NMS_PF], pfB[NMS_PF];
+  uint64_t diag = 0, wprev = 0;
+  u64x2 pf[NMS_PF];
 #pragma unroll
-  for (int k = 0; k < NMS_PF; ++k) {
-    pfA[k] = u64x2{0ull, 0ull};
-    pfB[k] = u64x2{0ull, 0ull};
-  }
-  if (wave == 0 && nbv > 0) {
-    diagA = mb[nms_col(0, lane)];
-    if (nb > 1) {
-      diagB = mb[Pp + nms_col(1, lane)];
-      wprevB = mb[nms_col(1, lane)];
-    }
-  } else if (wave > 0 && nbv > 1) {  // row block 0 for iteration 1 (pairs from q0 = 1)
-    const uint64_t* rowp = mb + (int64_t)(1 + (wave - 1)) * 128 + lane * 2;
-#pragma unroll
-    for (int k = 0; k < NMS_PF; ++k)
-      if (2 * (1 + (wave - 1) + NMS_HELPERS * k) < nbv) pfB[k] = *reinterpret_cast<const u64x2*>(rowp + NMS_HELPERS * 128 * k);
-  }
+  for (int k = 0; k < NMS_PF; ++k) pf[k] = u64x2{0ull, 0ull};
+  if (wave == 0 && nbv > 0) diag = mb[nms_col(0, lane)];
   __syncthreads();
-  auto iter = [&](int t, uint64_t& diag, uint64_t& wprev, u64x2 (&pf)[NMS_PF]) -> bool {
-    if (s_nk[t & 1] >= post) return true;  // uniform: written before the last barrier, not rewritten until the next
+  int t = 0;
+  for (; t < nbv; ++t) {
+    if (s_nk[t & 1] >= post) break;  // uniform: written before the last barrier, not rewritten until the next
     if (wave == 0) {
       const int j = t * 64 + lane;
       const uint64_t kp = t > 0 ? keptw[t - 1] : 0ull;
@@ -152,10 +133,10 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
         if (next == kept) break;
         kept = next;
       }
-      // prefetch block t+2 into this parity's set (clamped to in-range words near the end)
-      const int tn = min(t + 2, nb - 1);
+      // prefetch block t+1 (clamped to an in-range word on the last block)
+      const int tn = min(t + 1, nb - 1);
       diag = mb[(int64_t)tn * Pp + nms_col(tn, lane)];
-      wprev = mb[(int64_t)max(tn - 1, 0) * Pp + nms_col(tn, lane)];
+      wprev = mb[(int64_t)t * Pp + nms_col(tn, lane)];
       const int nk = s_nk[t & 1];
       if (nk + __popcll(kept) > post) {  // keep only the lowest (post - nk) boxes of this block
         int need = post - nk;
@@ -173,9 +154,11 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
       }
     } else {
       const int h = wave - 1;
-      // (no blanket vmcnt(0) here: it would also drain the other set, loaded one iteration ago for
-      // the next block.  The compiler's wait-count pass sees these loads and waits for this set's
-      // only where it is consumed; refilling a set after its consumption needs no further wait.)
+      // vmcnt(0) through the builtin, which the compiler's wait-count pass sees: it then knows the
+      // previous iteration's prefetch has landed, and issues this iteration's guarded prefetch
+      // loads back to back instead of draining before each (the skipped-slot path could otherwise
+      // still have a load in flight into the same registers).
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15 (no wait)
       if (t >= 1) {
         const uint64_t kp = keptw[t - 1];
         if (kp) {
@@ -211,7 +194,7 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
           }
         }
       }
-      // prefetch row block t+1 for iteration t+2: the pairs q0' + h + 15k (q0' = (t+3)/2) whose
+      // prefetch row block t for iteration t+1: the pairs q0' + h + 15k (q0' = (t+2)/2) whose
       // first column is < nbv.  One CU streams the whole triangle and every wave-load costs the
       // CU's address path about the same at 8 and 16 B per lane, so a slot fetches two column
       // blocks and unneeded slots do not issue at all.  These are ordinary loads: the compiler
@@ -219,24 +202,14 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
       // register of it is reused.  (Round 2 issued them as inline asm, invisible to the compiler's
       // wait-count pass: after an early exit at `post` kept boxes, a late prefetch could land in
       // registers the epilogue had reused for the kept count, corrupting the keep list.)
-      const int q0n = (t + 3) >> 1;  // iteration t+2 folds row block t+1 into columns >= t+3
-      if (t + 1 < nb) {
-        const uint64_t* rowp = mb + (int64_t)(t + 1) * Pp + (int64_t)(q0n + h) * 128 + lane * 2;
+      const int q0n = (t + 2) >> 1;
+      const uint64_t* rowp = mb + (int64_t)t * Pp + (int64_t)(q0n + h) * 128 + lane * 2;
 #pragma unroll
-        for (int k = 0; k < NMS_PF; ++k) {
-          if (2 * (q0n + h + NMS_HELPERS * k) < nbv) pf[k] = *reinterpret_cast<const u64x2*>(rowp + NMS_HELPERS * 128 * k);
-        }
+      for (int k = 0; k < NMS_PF; ++k) {
+        if (2 * (q0n + h + NMS_HELPERS * k) < nbv) pf[k] = *reinterpret_cast<const u64x2*>(rowp + NMS_HELPERS * 128 * k);
       }
     }
     __syncthreads();
-    return false;
-  };
-  int t = 0;
-  while (t < nbv) {
-    if (iter(t, diagA, wprevA, pfA)) break;
-    if (++t >= nbv) break;
-    if (iter(t, diagB, wprevB, pfB)) break;
-    ++t;
   }
   // the loop ends right after a barrier (break) or after the last one (t == nbv): s_nk[t & 1]
   // is the final count either way

@@ -77,7 +77,7 @@ def main():
     ap.add_argument('--num-classes', type=int, default=81)
     ap.add_argument('--image', default='800x1333')
     ap.add_argument('--lr', type=float, default=0.001)
-    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'fp32'])
+    ap.add_argument('--dtype', default='bf16', choices=['bf16', 'bf16x3', 'fp32'])
     ap.add_argument('--out', default='')
     ap.add_argument('--train-mode', default='e2e', choices=['e2e', 'rcnn'])
     args = ap.parse_args()

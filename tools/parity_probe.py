@@ -10,7 +10,8 @@ Arms (same weights, same deterministic samples as the test):
   cpu_bf16act   cpu_bf16in plus every layer output and every layer-output gradient rounded to bf16
                 (forward / tensor hooks on the leaf modules): what bf16 STORAGE of activations and
                 gradients costs with exact fp32 arithmetic in between -- the floor of any bf16 path
-  gpu_x2        the fp32-class GPU mode (bf16 hi / lo pairs, three MFMAs per product)
+  gpu_bf16x3    bf16 hi / lo pairs between kernels, three MFMAs per product (16 significant bits)
+  gpu_fp32x3    the fp32 mode: exact (mid, hi, lo) bf16 triples, six MFMAs per product (24 bits)
 
     python tools/parity_probe.py [--mode rpn|rcnn]
 """
@@ -88,8 +89,10 @@ def main():
         arms['gpu_bf16'] = Trainer(copy.deepcopy(base), mode, fixed_param_prefix=tp.FIXED, lr=0.0, device=dev)
         arms['gpu_fp32'] = Trainer(copy.deepcopy(base), mode, fixed_param_prefix=tp.FIXED, lr=0.0, device=dev,
                                    channels_last=False, precision='torch')
-        arms['gpu_x2'] = Trainer(copy.deepcopy(base), mode, fixed_param_prefix=tp.FIXED, lr=0.0, device=dev,
-                                 precision='fp32')
+        arms['gpu_bf16x3'] = Trainer(copy.deepcopy(base), mode, fixed_param_prefix=tp.FIXED, lr=0.0, device=dev,
+                                     precision='bf16x3')
+        arms['gpu_fp32x3'] = Trainer(copy.deepcopy(base), mode, fixed_param_prefix=tp.FIXED, lr=0.0, device=dev,
+                                     precision='fp32')
     q = copy.deepcopy(base)
     with torch.no_grad():
         for p in q.parameters():
@@ -104,9 +107,9 @@ def main():
             b['data'] = b['data'].to(torch.bfloat16).float()
         _, g = tp._fwd_bwd(tr, b)
         med, worst, near = stats(g_ref, g)
-        print('%-11s median cos %.4f  worst %s' % (name, med, [(round(c, 3), round(r, 3), n) for c, r, n in worst]),
+        print('%-12s median cos %.4f  worst %s' % (name, med, [(round(c, 3), round(r, 3), n) for c, r, n in worst]),
               flush=True)
-        print('%-11s near-loss layers %s' % (name, [(round(c, 4), round(r, 3), n) for c, r, n in near]), flush=True)
+        print('%-12s near-loss layers %s' % (name, [(round(c, 4), round(r, 3), n) for c, r, n in near]), flush=True)
 
 
 if __name__ == '__main__':

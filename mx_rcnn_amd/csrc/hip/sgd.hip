@@ -191,7 +191,11 @@ void sgd_momentum(float* w, float* mom, const void* grad, int grad_bf16, int64_t
 #undef MXR_SGD8
     return;
   }
-  const int blocks = (int)std::min<int64_t>(div_up((n + 3) / 4, 256), 256 * 8);
+  static const int64_t max_blocks = [] {  // A/B knob MXR_SGD_BLOCKS: grid cap of the 4-wide kernel
+    const char* e = getenv("MXR_SGD_BLOCKS");
+    return e != nullptr ? std::max<int64_t>(1, atoll(e)) : (int64_t)256 * 8;
+  }();
+  const int blocks = (int)std::min<int64_t>(div_up((n + 3) / 4, 256), max_blocks);
   if (grad_bf16)
     sgd_kernel<true><<<blocks, 256, 0, st>>>(w, mom, grad, n, lr, momentum, wd, rescale, clip, w_bf16, x2_plane, x3,
                                                    zero, zero_bf16);

@@ -410,6 +410,7 @@ class FlatParamStore:
                         if gn == n:
                             g.master[off:off + numel].copy_(self._flat_view(src, cl))
                             p.data.copy_(src.to(p.dtype))
+                            precision.forget_weight(p)
                             found = True
                             if g.x2:
                                 g.sync_shadow()

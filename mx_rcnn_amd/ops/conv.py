@@ -15,6 +15,7 @@
   kernels off for A/B runs.
 """
 import os
+import weakref
 
 import torch
 import torch.nn.functional as F
@@ -33,19 +34,36 @@ def wgrad_enabled():
     return os.environ.get('MXR_CONV_WGRAD', '1') != '0'
 
 
-# dgrad operand cache: id(weight Parameter) -> flipped/transposed bf16 filter, refreshed by the
-# FlatParamStore with ONE multi-filter kernel right after each SGD update (core/params.py),
-# instead of a flip + transpose copy per conv per backward.
+# dgrad operand cache: id(weight Parameter) -> (weakref(param), flipped/transposed bf16 filter),
+# refreshed by the FlatParamStore with ONE multi-filter kernel right after each SGD update
+# (core/params.py), instead of a flip + transpose copy per conv per backward.  Entries hold the
+# parameter WEAKLY and are dropped when it dies (a finalizer per parameter), so the tables neither
+# pin a dead trainer's model nor hand its buffers to a later parameter that reuses the id.
 _DGRAD_W = {}
+# parity sub-filters of the cached flipped filters (strided dgrad): (id(param), taps) ->
+# (weakref(param), source view builder, buffer); rebuilt with the cache
+# (FlatParamStore.refresh_dgrad_cache)
+_SUBW = {}
+_FINAL = set()
+
+
+def _drop_param(pid):
+    _FINAL.discard(pid)
+    _DGRAD_W.pop(pid, None)
+    for k in [k for k in _SUBW if k[0] == pid]:
+        del _SUBW[k]
+
+
+def _track(param):
+    pid = id(param)
+    if pid not in _FINAL:
+        _FINAL.add(pid)
+        weakref.finalize(param, _drop_param, pid)
 
 
 def register_dgrad_weight(param, buf):
-    _DGRAD_W[id(param)] = (param, buf)
-
-
-# parity sub-filters of the cached flipped filters (strided dgrad): (id(param), taps) -> (param,
-# source view builder, buffer); rebuilt with the cache (FlatParamStore.refresh_dgrad_cache)
-_SUBW = {}
+    _track(param)
+    _DGRAD_W[id(param)] = (weakref.ref(param), buf)
 
 
 def sub_filter(param, wf, th, tw, s):
@@ -58,19 +76,30 @@ def sub_filter(param, wf, th, tw, s):
         return view(wf).contiguous(memory_format=torch.channels_last)
     key = (id(param), th[0], th[-1], tw[0], tw[-1], s)
     ent = _SUBW.get(key)
-    if ent is None or ent[0] is not param:
+    if ent is None or ent[0]() is not param:
         buf = view(wf).contiguous(memory_format=torch.channels_last)
-        _SUBW[key] = (param, view, buf)
+        _track(param)
+        _SUBW[key] = (weakref.ref(param), view, buf)
         return buf
     return ent[2]
+
+
+def sub_filter_entries():
+    """[(param, view builder, buffer)] of the live parity sub-filters."""
+    out = []
+    for ref, view, buf in list(_SUBW.values()):
+        p = ref()
+        if p is not None:
+            out.append((p, view, buf))
+    return out
 
 
 def sub_filters_of(param):
     """[(buf, row taps, col taps)] registered for ``param`` (the flip kernel's table writes them
     in the same pass as the flipped filter, core/params.py)."""
     out = []
-    for (pid, r0, r1, c0, c1, s), (p, _view, buf) in _SUBW.items():
-        if p is param:
+    for (pid, r0, r1, c0, c1, s), (ref, _view, buf) in list(_SUBW.items()):
+        if ref() is param:
             out.append((buf, list(range(r0, r1 + 1, s)), list(range(c0, c1 + 1, s))))
     return out
 
@@ -78,7 +107,7 @@ def sub_filters_of(param):
 def refresh_sub_filters(skip=()):
     """Copy the sub-filters of every parameter not in ``skip`` (ids whose sub-filters the flip
     kernel already wrote)."""
-    for param, view, buf in list(_SUBW.values()):
+    for param, view, buf in sub_filter_entries():
         if id(param) in skip:
             continue
         wf = cached_dgrad_weight(param)
@@ -89,13 +118,13 @@ def refresh_sub_filters(skip=()):
 def cached_dgrad_weight(param):
     """The cached flipped / transposed filter of ``param`` or None."""
     ent = _DGRAD_W.get(id(param)) if param is not None else None
-    return ent[1] if ent is not None and ent[0] is param else None
+    return ent[1] if ent is not None and ent[0]() is param else None
 
 
 def dgrad_weight(param, w):
-    ent = _DGRAD_W.get(id(param)) if param is not None else None
-    if ent is not None and ent[0] is param:
-        return ent[1]
+    wf = cached_dgrad_weight(param)
+    if wf is not None:
+        return wf
     if precision.x2_enabled():  # the flipped fp32 filter as a pair
         return precision.split(_flip_t(w.detach().float()))
     return _flip_t(w)

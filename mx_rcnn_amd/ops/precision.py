@@ -170,8 +170,16 @@ def clear_weights():
 
 
 def forget_weight(param):
-    """Drop the cached planes of ``param`` (its data was rewritten without a version bump)."""
+    """Drop every cache derived from ``param``'s values (its data was rewritten through ``.data``,
+    which does not move the version counter): the planes cached here, and -- through the reload
+    epoch -- the per-tensor packings of other ops (ops/stem.py)."""
     _CACHE.pop(id(param), None)
+    param.__dict__['_mxr_epoch'] = weight_epoch(param) + 1
+
+
+def weight_epoch(param):
+    """Reload counter of ``param`` (bumped by forget_weight); part of every derived cache's key."""
+    return param.__dict__.get('_mxr_epoch', 0)
 
 
 def weight_pair(w):

@@ -10,7 +10,7 @@ freezes conv0 / bn_data / bn0 and conv1_x: FIXED_PARAMS, `rcnn/config.py`), i.e.
 those parameters fixed and at test time.  The kernel folds the BN affines from the BN
 parameters / moving statistics in-kernel (no derived copy to invalidate: the graph warm-up's
 state restore rewrites those buffers), and reads the filter from a packed (64, KP) copy cached
-per parameter and rebuilt when the parameter's version counter moves (a checkpoint load).  A
+on the parameter itself and rebuilt when its version counter or reload epoch moves.  A
 captured step contains the conv launch only.
 """
 import os
@@ -22,16 +22,22 @@ from . import precision
 from ._ext import need_ext
 
 
-_PACKED = {}
-
-
 def _packed_filter(w, dtype):
     """dtype torch.float32 (the multi-plane modes): the packed filter's bf16 planes in the kernel's
-    LOGICAL order -- (128, KP) = (hi, lo) for bf16x3, (192, KP) = (hi, mid, lo) for fp32."""
+    LOGICAL order -- (128, KP) = (hi, lo) for bf16x3, (192, KP) = (hi, mid, lo) for fp32.
+
+    The packing lives ON the weight tensor (``w._mxr_stem``), so it dies with the parameter and can
+    never be served to a later tensor that reuses the same ``id`` / address (the round-4 stale-filter
+    bug of an ``id()``-keyed cache).  It is rebuilt when the tensor's version counter, storage or
+    reload epoch (``precision.forget_weight``: ``.data`` writes do not move the version counter)
+    changes -- IN PLACE when the shape allows, so a captured hipGraph keeps reading live values."""
     planes = precision.nplanes() if dtype == torch.float32 else 0
-    key = (id(w), dtype, planes)
-    ver = (w.data_ptr(), w._version, tuple(w.shape))
-    hit = _PACKED.get(key)
+    slot = (dtype, planes)
+    ver = (w.data_ptr(), w._version, tuple(w.shape), precision.weight_epoch(w))
+    cache = w.__dict__.get('_mxr_stem')
+    if cache is None:
+        cache = w.__dict__['_mxr_stem'] = {}
+    hit = cache.get(slot)
     if hit is None or hit[0] != ver:
         if dtype == torch.float32:
             pf = precision.split(pack_filter(w, torch.float32), planes or 2)
@@ -39,8 +45,11 @@ def _packed_filter(w, dtype):
                 pf = torch.cat([pf[64:128], pf[:64], pf[128:]], 0).contiguous()
         else:
             pf = pack_filter(w, dtype)
+        if hit is not None and hit[1].shape == pf.shape:
+            hit[1].copy_(pf)
+            pf = hit[1]
         hit = (ver, pf)
-        _PACKED[key] = hit
+        cache[slot] = hit
     return hit[1]
 
 

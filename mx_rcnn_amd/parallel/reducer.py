@@ -114,6 +114,7 @@ class BucketReducer:
                 for n in names:
                     self._param_bucket[n] = bkt
         if self.overlap or self.sgd_capable:
+            grad_sink.clear_hooks(store.params.values())  # an earlier reducer on these parameters
             for n, p in store.params.items():
                 if n in self._param_bucket:
                     grad_sink.add_hook(p, self._make_hook(n))

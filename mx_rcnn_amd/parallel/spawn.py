@@ -48,28 +48,38 @@ def device_ids(spec):
     return ids or [0]
 
 
-def visible_mask():
+def visible_mask(with_source=False):
     """The device list a scheduler already restricted this job to (``HIP_VISIBLE_DEVICES``, else
-    ``CUDA_VISIBLE_DEVICES`` / ``ROCR_VISIBLE_DEVICES``), or None when every device is visible."""
+    ``CUDA_VISIBLE_DEVICES`` / ``ROCR_VISIBLE_DEVICES``), or None when every device is visible.
+    ``with_source``: -> (list, variable name) / (None, None)."""
     for var in ('HIP_VISIBLE_DEVICES', 'CUDA_VISIBLE_DEVICES', 'ROCR_VISIBLE_DEVICES'):
         v = os.environ.get(var)
         if v is not None and v.strip() != '':
-            return [t.strip() for t in v.split(',') if t.strip() != '']
-    return None
+            ids = [t.strip() for t in v.split(',') if t.strip() != '']
+            return (ids, var) if with_source else ids
+    return (None, None) if with_source else None
 
 
-def map_devices(ids, mask=None):
-    """``--gpus`` ids index the devices this job can see, like the reference's ``mx.gpu(i)``: with
-    a visibility mask already set (e.g. HIP_VISIBLE_DEVICES=4,5,6,7 from a scheduler), id i is
-    the mask's i-th entry, so ``--gpus 2,3`` runs on physical devices 6 and 7.  An id outside the
+def map_devices(ids, mask=None, source='HIP_VISIBLE_DEVICES'):
+    """``--gpus`` ids index the devices this job can see, like the reference's ``mx.gpu(i)`` ->
+    the ``HIP_VISIBLE_DEVICES`` entries that select them.
+
+    HIP applies ``HIP_VISIBLE_DEVICES`` (or, when unset, ``CUDA_VISIBLE_DEVICES``) ON TOP of the
+    devices ROCr exposes.  So with a HIP / CUDA mask (e.g. HIP_VISIBLE_DEVICES=4,5,6,7 from a
+    scheduler) id i is the mask's i-th entry -- ``--gpus 2,3`` runs on devices 6 and 7 -- and the
+    new HIP mask replaces the old one.  A ``ROCR_VISIBLE_DEVICES`` mask has already renumbered the
+    devices 0..k-1 below HIP, so the HIP mask must hold the indices themselves.  An id outside the
     mask is an error."""
-    mask = visible_mask() if mask is None else mask
+    if mask is None:
+        mask, source = visible_mask(with_source=True)
     if mask is None:
         return [str(i) for i in ids]
     bad = [i for i in ids if i < 0 or i >= len(mask)]
     if bad:
         raise SystemExit('--gpus %s: device(s) %s outside the %d visible device(s) %s' % (
             ','.join(str(i) for i in ids), bad, len(mask), ','.join(mask)))
+    if source == 'ROCR_VISIBLE_DEVICES':
+        return [str(i) for i in ids]
     return [mask[i] for i in ids]
 
 
@@ -81,10 +91,11 @@ def select_devices(spec):
     ids = device_ids(spec)
     if launched_rank():
         return None  # the launcher placed this rank already
-    vis = ','.join(map_devices(ids))
+    mask, source = visible_mask(with_source=True)
+    vis = ','.join(map_devices(ids, mask, source))
     if len(ids) > 1:
         return vis
-    if ids != [0] or visible_mask() is not None:
+    if ids != [0] or source in ('HIP_VISIBLE_DEVICES', 'CUDA_VISIBLE_DEVICES'):
         os.environ['HIP_VISIBLE_DEVICES'] = vis
     return None
 

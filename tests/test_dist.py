@@ -357,7 +357,7 @@ def test_gpus_names_devices_like_the_reference(monkeypatch):
     """--gpus is a device list as in the reference (train_end2end.py:168): '2,3' runs two ranks
     on GPUs 2 and 3 (HIP_VISIBLE_DEVICES for the children), '3' one process on GPU 3."""
     from mx_rcnn_amd.parallel import spawn
-    for k in ('RANK', 'WORLD_SIZE', 'HIP_VISIBLE_DEVICES'):
+    for k in ('RANK', 'WORLD_SIZE', 'HIP_VISIBLE_DEVICES', 'CUDA_VISIBLE_DEVICES', 'ROCR_VISIBLE_DEVICES'):
         monkeypatch.delenv(k, raising=False)
     assert spawn.device_ids('2,3') == [2, 3] and spawn.device_ids('3') == [3] and spawn.device_ids(4) == [0, 1, 2, 3]
     assert spawn.parse_gpus('2,3') == 2 and spawn.parse_gpus('0') == 1
@@ -385,6 +385,27 @@ def test_gpus_index_an_existing_visibility_mask(monkeypatch):
     monkeypatch.setenv('RANK', '0')
     monkeypatch.setenv('WORLD_SIZE', '2')
     assert spawn.select_devices('2,3') is None and os.environ['HIP_VISIBLE_DEVICES'] == '4,5,6,7'
+
+
+def test_gpus_under_rocr_and_cuda_masks(monkeypatch):
+    """ROCR_VISIBLE_DEVICES renumbers the devices below HIP, so the HIP mask written for
+    the ranks holds INDICES into it ('--gpus 0' under ROCR=4,5,6,7 leaves the env alone; '1,2' ->
+    '1,2'); a CUDA_VISIBLE_DEVICES mask is HIP's own alias and maps like HIP_VISIBLE_DEVICES."""
+    import pytest as _pt
+    from mx_rcnn_amd.parallel import spawn
+    for k in ('RANK', 'WORLD_SIZE', 'HIP_VISIBLE_DEVICES', 'CUDA_VISIBLE_DEVICES', 'ROCR_VISIBLE_DEVICES'):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv('ROCR_VISIBLE_DEVICES', '4,5,6,7')
+    assert spawn.select_devices('0') is None and 'HIP_VISIBLE_DEVICES' not in os.environ
+    assert spawn.select_devices('1,2') == '1,2'
+    assert spawn.select_devices('3') is None and os.environ['HIP_VISIBLE_DEVICES'] == '3'
+    monkeypatch.delenv('HIP_VISIBLE_DEVICES')
+    with _pt.raises(SystemExit):
+        spawn.select_devices('4')
+    monkeypatch.delenv('ROCR_VISIBLE_DEVICES')
+    monkeypatch.setenv('CUDA_VISIBLE_DEVICES', '2,3')
+    assert spawn.select_devices('0,1') == '2,3'
+    assert spawn.select_devices('1') is None and os.environ['HIP_VISIBLE_DEVICES'] == '3'
 
 
 def test_capture_sync_key_ignores_uneven_slices():

@@ -187,7 +187,7 @@ def test_flip_kernel_writes_parity_sub_filters(cuda, precision):
     tr.store.refresh_dgrad_cache()
     torch.cuda.synchronize()
     checked = 0
-    for (pid, r0, r1, c0, c1, st), (p, view, buf) in conv_ops._SUBW.items():
+    for p, view, buf in conv_ops.sub_filter_entries():
         if id(p) not in tr.store._sub_in_table:
             continue
         wf = conv_ops.cached_dgrad_weight(p)

@@ -139,6 +139,9 @@ def main():
         from mx_rcnn_amd.ops import need_ext
         for key, tile, sp in need_ext().conv_tune_table():
             print('[tune] %-48s tile %d splits %d' % (key, tile, sp), file=sys.stderr)
+    if device.type == 'cuda' and rank == 0:  # persist the conv plan for the next run (ops/tune_plan.py)
+        from mx_rcnn_amd.ops import tune_plan
+        tune_plan.save()
     pdist.destroy()
 
 
@@ -208,6 +211,12 @@ def run(args, precision, rank, world, device):
     elapsed = time.perf_counter() - t0
     elapsed = pdist.all_reduce_max(elapsed, device)
     loss1 = float(out['objective'].float().item())
+    plan = None
+    if device.type == 'cuda':  # the conv plan the timed step ran with, and whether the ranks agree
+        from mx_rcnn_amd.ops import tune_plan
+        h = int(tune_plan.plan_hash(), 16)
+        plan = {'hash': '%08x' % h, 'entries': len(tune_plan.table()),
+                'ranks_agree': pdist.all_reduce_max(float(h), device) == -pdist.all_reduce_max(-float(h), device)}
     # after the timed region: each gradient bucket's collective in isolation (HIP events)
     comm = trainer.reducer.measure_collectives() if world > 1 else None
     ms = elapsed / max(args.steps, 1) * 1e3
@@ -228,7 +237,7 @@ def run(args, precision, rank, world, device):
                       'rpn_pre_post_nms': [cfg.TRAIN.RPN_PRE_NMS_TOP_N, cfg.TRAIN.RPN_POST_NMS_TOP_N],
                       'rois_per_image': cfg.TRAIN.BATCH_SIZE, 'exec': mode,
                       'objective_first_last': [round(loss0, 4), round(loss1, 4)],
-                      'backend': pdist.backend_name(), 'allreduce': comm,
+                      'backend': pdist.backend_name(), 'allreduce': comm, 'conv_plan': plan,
                       'rccl': pdist.rccl_env() if pdist.backend_name() == 'nccl' else None,
                       'hip_runtime': __import__('mx_rcnn_amd').runtime_settings()}}
     del step_fn, trainer

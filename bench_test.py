@@ -155,6 +155,9 @@ def main():
                        'num_classes': args.num_classes, 'parallelism': 'dp%d' % world, 'exec': mode,
                        'rpn_pre_post_nms': [config.TEST.RPN_PRE_NMS_TOP_N, config.TEST.RPN_POST_NMS_TOP_N],
                        'detections_last_image': n_det}}), flush=True)
+    if device.type == 'cuda' and rank == 0:  # persist the conv plan for the next run (ops/tune_plan.py)
+        from mx_rcnn_amd.ops import tune_plan
+        tune_plan.save()
     pdist.destroy()
 
 

@@ -35,6 +35,9 @@ def add_common_args(parser):
     parser.add_argument('--network', default='vgg16', help='vgg16 | resnet18..resnet200')
     parser.add_argument('--synthetic', type=int, default=0, help='use N synthetic images instead of a dataset')
     parser.add_argument('--synthetic-shape', default='600x1000')
+    parser.add_argument('--synthetic-kind', default='noise', choices=('noise', 'planted'),
+                        help='noise: benchmark-shaped random images; planted: learnable class-specific objects '
+                             '(train on one --seed, test on another)')
     parser.add_argument('--cfg', nargs='*', default=[], help='config overrides key=value (e.g. TRAIN.RPN_MIN_SIZE=10)')
     parser.add_argument('--max-steps', type=int, default=None, help='stop after this many steps (smoke runs)')
     parser.add_argument('--eager', action='store_true', help='disable hipGraph step capture')
@@ -115,7 +118,23 @@ def synthetic_roidb(args, num_classes, flip=False):
     h, w = [int(v) for v in args.synthetic_shape.lower().split('x')]
     config.SCALES = (min(h, w),)
     config.MAX_SIZE = max(h, w)
-    return load_synthetic_roidb(args.synthetic, h, w, num_classes, flip=flip, seed=args.seed)
+    return load_synthetic_roidb(args.synthetic, h, w, num_classes, flip=flip, seed=args.seed,
+                                kind=getattr(args, 'synthetic_kind', 'noise'))
+
+
+def raw_images(device):
+    """Training loaders ship uint8 images converted on the device (ops/image.py) when training on
+    the GPU (MXR_RAW_IMAGES=0: the host float path of the reference)."""
+    return torch.device(device).type == 'cuda' and os.environ.get('MXR_RAW_IMAGES', '1') != '0'
+
+
+def batch_images(b):
+    """The network input of a loader batch (converts a raw uint8 batch on the CPU)."""
+    x = torch.as_tensor(b['data'])
+    if x.dtype == torch.uint8:
+        from ..ops.image import image_prep
+        x = image_prep(x, torch.as_tensor(b['im_info']), b.get('pixel_means'), torch.float32, False)
+    return x
 
 
 def calibrate_if_random(model, loader, arg_params):
@@ -124,6 +143,6 @@ def calibrate_if_random(model, loader, arg_params):
     if arg_params or not model.network.startswith('resnet'):
         return False
     b = loader.get_batch()
-    model.calibrate_bn(torch.as_tensor(b['data']))
+    model.calibrate_bn(batch_images(b))
     logging.info('no pretrained weights: calibrated %s BN statistics on the first batch', model.network)
     return True

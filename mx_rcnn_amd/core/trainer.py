@@ -83,8 +83,14 @@ class Trainer:
     def prepare_batch(self, batch):
         out = {}
         for k, v in batch.items():
+            if k == 'pixel_means':  # raw-image batches: constants of the loader, kernel arguments
+                out[k] = tuple(float(m) for m in (v.tolist() if torch.is_tensor(v) else v))
+                continue
             if torch.is_tensor(v):
                 v = v.to(self.device, non_blocking=True)
+                if k == 'data' and v.dtype == torch.uint8:  # raw images: converted in forward (on device)
+                    out[k] = v
+                    continue
                 if k == 'data':
                     v = v.to(self.compute_dtype)
                     if self.channels_last:
@@ -94,6 +100,13 @@ class Trainer:
 
     def forward(self, b):
         m = self.model
+        if b['data'].dtype == torch.uint8:
+            # raw uint8 BGR images (data/loader.py raw_images): RGB / means / pad on the device,
+            # inside the captured step (ops/image.py)
+            from ..ops.image import image_prep
+            b = dict(b)
+            b['data'] = image_prep(b['data'], b['im_info'], b.get('pixel_means'), self.compute_dtype,
+                                   self.channels_last)
         if self.mode == 'e2e':
             return m.train_e2e(b['data'], b['im_info'], b['gt_boxes'], b['n_gt'])
         if self.mode == 'rpn':
@@ -254,6 +267,13 @@ class GraphedStep:
                 trainer.restore_state(saved)
                 del saved
                 torch.cuda.synchronize()
+        # the conv autotune ran in the warm-up: under DP every rank captures rank 0's plan (the
+        # K-split choices change summation order), and rank 0 persists it for the next run
+        from ..ops import tune_plan
+        self.plan_hash = tune_plan.sync_from_rank0(torch.device('cuda', torch.cuda.current_device()))
+        if not (torch.distributed.is_available() and torch.distributed.is_initialized()) or \
+                torch.distributed.get_rank() == 0:
+            tune_plan.save()
         self.graph = torch.cuda.CUDAGraph()
         # thread_local: the loaders' prefetch threads keep staging the next batches (pinned host
         # buffers, H2D copies on their own streams) while a new shape is captured; in the default
@@ -265,7 +285,7 @@ class GraphedStep:
     def __call__(self, batch=None):
         if batch is not None:
             for k, v in batch.items():
-                if torch.is_tensor(v) and k in self.static:
+                if torch.is_tensor(v) and torch.is_tensor(self.static.get(k)):
                     self.static[k].copy_(v, non_blocking=True)
         self.t.update_lr()
         if self.t.grads_dirty:  # the graph holds no gradient clear (captured after a fused-clear step)

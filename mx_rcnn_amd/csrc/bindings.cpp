@@ -685,6 +685,30 @@ std::vector<std::tuple<std::string, int64_t, int64_t>> conv_tune_table() {
   return out;
 }
 
+Tensor image_prep(const Tensor& img, const Tensor& im_info, std::vector<double> means, bool out_bf16) {
+  CHECK_DEV(img); CHECK_DEV(im_info); CHECK_F32(im_info);
+  TORCH_CHECK(img.scalar_type() == at::kByte && img.dim() == 4 && img.size(3) == 3 && img.is_contiguous(),
+              "image_prep: contiguous uint8 (B, H, W, 3) images");
+  TORCH_CHECK(im_info.dim() == 2 && im_info.size(0) == img.size(0) && im_info.size(1) >= 3 && im_info.is_contiguous(),
+              "image_prep: im_info (B, 3)");
+  TORCH_CHECK(means.size() == 3, "image_prep: three means");
+  const int64_t B = img.size(0), H = img.size(1), W = img.size(2);
+  Tensor out = at::empty({B, 3, H, W}, img.options().dtype(out_bf16 ? at::kBFloat16 : at::kFloat),
+                         at::MemoryFormat::ChannelsLast);
+  mxr::image_prep(img.data_ptr<uint8_t>(), im_info.data_ptr<float>(), (int)B, (int)H, (int)W, means.data(),
+                  out_bf16 ? 1 : 0, out.data_ptr(), cur_stream());
+  return out;
+}
+
+// Preload / override autotune choices (a persisted plan file, or rank 0's plan under data
+// parallelism: ops/tune_plan.py).  A key present here is never re-timed.
+int64_t conv_tune_set(const std::vector<std::tuple<std::string, int64_t, int64_t>>& entries, bool replace) {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  if (replace) g_tune.clear();
+  for (const auto& e : entries) g_tune[std::get<0>(e)] = {(int)std::get<1>(e), (int)std::get<2>(e)};
+  return (int64_t)g_tune.size();
+}
+
 // dadd either shaped like y, or the stride-s subsampled grid (N, C, ceil(Ho/s), ceil(Wo/s)) of an
 // unmapped launch (a strided projection shortcut's gradient): sets ep.dadd / ep.dadd_s
 void set_dadd(mxr::ConvEpi& ep, const Tensor& dadd, const Tensor& y, int Ho, int Wo, bool mapped) {
@@ -2175,7 +2199,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mean"), py::arg("var"), py::arg("eps"), py::arg("fix_gamma"), py::arg("relu"), py::arg("need_dx"),
         py::arg("need_params"), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(),
         py::arg("dres") = py::none(), py::arg("x2") = 0);
+  m.def("image_prep", &image_prep, py::arg("img"), py::arg("im_info"), py::arg("means"), py::arg("out_bf16"),
+        "uint8 BGR (B,H,W,3) -> channels_last (B,3,H,W) RGB minus means, 0 outside im_info's (h, w)");
   m.def("conv_tune_table", &conv_tune_table, "per-shape conv autotune choices: [(key, tile, splits)]");
+  m.def("conv_tune_set", &conv_tune_set, py::arg("entries"), py::arg("replace") = false,
+        "set autotune choices [(key, tile, splits)] (replace: drop the current table first); returns the table size");
   m.def("conv_igemm_fwd", &conv_igemm_fwd, py::arg("x"), py::arg("w"), py::arg("bias"), py::arg("stride"),
         py::arg("pad"), py::arg("relu"), py::arg("tile") = 0, py::arg("splits") = 0, py::arg("residual") = py::none(),
         py::arg("bn") = py::none(), py::arg("bn_eps") = 2e-5, py::arg("bn_fix_gamma") = false,

@@ -288,7 +288,9 @@ __device__ __forceinline__ void stv(float* p, const float* v, int) {
 // gives the same bits), and the output is float(sum) * 2^-s -- one rounding, more accurate than
 // the fp32 atomic chain; a contribution below 2^-27 of the channel's largest keeps its low bits
 // only down to 2^-50 of it.  The other gradient of the feature map (gadd: the RPN head's) is added
-// once per pixel at the end.
+// once per pixel at the end.  A non-finite dY (a diverging step) has no fixed-point image: its
+// channel's gradient for the image is written as NaN, so the trunk gradient stays non-finite and
+// the trainer's non-finite guard sees it (a float atomic chain would have propagated it too).
 template <int CW, typename T>
 __global__ void __launch_bounds__(256)
 roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ argmax, const float* __restrict__ rois,
@@ -296,6 +298,7 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
   extern __shared__ long long acc[];  // [HW][CW] fixed-point sums
   __shared__ float red[4][CW];        // per-wave channel maxima
   __shared__ int sh_scale[CW];
+  __shared__ int sh_nf[CW];           // channel saw a non-finite dY in this image
   // code 3 / 4 (x2 / x3 planes): gout's planes one (R, PH, PW, C) block apart, gadd's / gin's one (B, H, W, C)
   const int64_t oplane = (int64_t)R * PHW * C, iplane = (int64_t)gridDim.y * HW * C;
   // XCD-aware channel groups: workgroups are dealt round-robin over the 8 XCDs, so consecutive
@@ -326,8 +329,13 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
   // pass 1: zero the slab, and the largest |dY| per channel over this image's bins
   for (int p = threadIdx.x; p < HW * CW; p += blockDim.x) acc[p] = 0;
   float mx[CW];
+  int nf[CW];  // fmaxf drops NaN and inf has no usable exponent: track non-finite dY separately
 #pragma unroll
-  for (int k = 0; k < CW; ++k) mx[k] = 0.f;
+  for (int k = 0; k < CW; ++k) {
+    mx[k] = 0.f;
+    nf[k] = 0;
+  }
+  if (threadIdx.x < CW) sh_nf[threadIdx.x] = 0;
   // (only a bound is needed: every bin's |dY| regardless of its argmax, and with planes the hi plane
   // alone -- |v| <= |hi| * (1 + 2^-7) -- so this pass reads 8 B per 4 channels, not dY + argmax)
   const int hi_off = code == 4 ? 1 : 0;  // x3 planes (mid, hi, lo); x2 (hi, lo)
@@ -345,7 +353,10 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
         g[k] = to_f(gout[base + k + (code >= 3 ? hi_off * oplane : 0)], code >= 3 ? 1 : code);
     }
 #pragma unroll
-    for (int k = 0; k < CW; ++k) mx[k] = fmaxf(mx[k], fabsf(g[k]));
+    for (int k = 0; k < CW; ++k) {
+      if (!isfinite(g[k])) nf[k] = 1;  // (a non-finite value has a non-finite hi plane)
+      else mx[k] = fmaxf(mx[k], fabsf(g[k]));
+    }
   }
   if (code >= 3)
 #pragma unroll
@@ -355,6 +366,9 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
   if ((threadIdx.x & 63) == 0)
 #pragma unroll
     for (int k = 0; k < CW; ++k) red[threadIdx.x >> 6][k] = mx[k];
+#pragma unroll
+  for (int k = 0; k < CW; ++k)
+    if (nf[k]) atomicOr(&sh_nf[k], 1);  // rare: only on a diverging step
   __syncthreads();
   if (threadIdx.x < CW) {
     const float m = fmaxf(fmaxf(red[0][threadIdx.x], red[1][threadIdx.x]), fmaxf(red[2][threadIdx.x], red[3][threadIdx.x]));
@@ -377,7 +391,7 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
     load_g(i, g, a);
 #pragma unroll
     for (int k = 0; k < CW; ++k)
-      if (a[k] >= 0 && a[k] < HW && g[k] != 0.f)
+      if (a[k] >= 0 && a[k] < HW && g[k] != 0.f && isfinite(g[k]))
         atomicAdd(reinterpret_cast<unsigned long long*>(&acc[a[k] * CW + k]),
                   (unsigned long long)__float2ll_rn(ldexpf(g[k], sc[k])));
   }
@@ -387,7 +401,7 @@ roi_pool_bwd_lds_kernel(const T* __restrict__ gout, const int32_t* __restrict__ 
   for (int p = threadIdx.x; p < HW; p += blockDim.x) {
     float v[CW], ga[CW];
 #pragma unroll
-    for (int k = 0; k < CW; ++k) v[k] = ldexpf((float)acc[p * CW + k], -sc[k]);
+    for (int k = 0; k < CW; ++k) v[k] = sh_nf[k] ? __builtin_nanf("") : ldexpf((float)acc[p * CW + k], -sc[k]);
     if (gadd) {
       if (code >= 3 && CW == 4) {
         ld4c(gadd, ((int64_t)b * HW + p) * C + c0, code, iplane, ga);  // one 8-B load per plane

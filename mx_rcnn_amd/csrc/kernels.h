@@ -122,6 +122,12 @@ void roi_pool_bwd(const void* grad_out, int bf16, const int32_t* argmax, const f
 // fp32 -> bf16 / fp32 copy-convert helper (n elements)
 void cast_f32(const float* in, void* out, int out_bf16, int64_t n, hipStream_t st);
 
+// ---- image preparation (image.hip) ---------------------------------------------
+// uint8 BGR (B, H, W, 3) -> channels_last (B, 3, H, W) fp32 / bf16 (NHWC memory): RGB, minus means
+// (RGB order), 0 outside im_info[b, 0:2] (the valid resized height / width)
+void image_prep(const uint8_t* in, const float* im_info, int B, int H, int W, const double* means, int out_bf16,
+                void* out, hipStream_t st);
+
 // ---- losses (losses.hip) ---------------------------------------------------
 // Every loss kernel writes its final (normalised) value to loss_out[0] itself: blocks store
 // partial sums into `partials` (>= loss_blocks_* floats) and the last block to take a ticket

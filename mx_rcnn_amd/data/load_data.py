@@ -58,9 +58,9 @@ def load_test_rpn_roidb(image_set, year, root_path, devkit_path):
     return voc, rpn_roidb
 
 
-def load_synthetic_roidb(num_images=16, height=600, width=1000, num_classes=21, flip=False, seed=0):
+def load_synthetic_roidb(num_images=16, height=600, width=1000, num_classes=21, flip=False, seed=0, kind='noise'):
     from .synthetic import SyntheticDetection
-    imdb = SyntheticDetection(num_images, height, width, num_classes, seed=seed)
+    imdb = SyntheticDetection(num_images, height, width, num_classes, seed=seed, kind=kind)
     roidb = imdb.gt_roidb()
     if flip:
         roidb = imdb.append_flipped_images(roidb)

@@ -266,8 +266,9 @@ class AnchorLoader(_BaseLoader):
     def __init__(self, feat_sym, roidb, batch_size=1, shuffle=False, mode='train', ctx=None, work_load_list=None,
                  feat_stride=16, anchor_scales=(8, 16, 32), anchor_ratios=(0.5, 1, 2), allowed_border=0,
                  need_mean=True, rank=0, world_size=1, seed=0, prefetch=2, workers=2, pad_shape=None, max_gt=None,
-                 shape_bucket=None):
+                 shape_bucket=None, raw_images=False):
         self.feat_sym = feat_sym
+        self.raw_images = raw_images
         self.feat_stride, self.anchor_scales, self.anchor_ratios = feat_stride, anchor_scales, anchor_ratios
         self.allowed_border, self.need_mean = allowed_border, need_mean
         self.pad_shape, self.max_gt = pad_shape, max_gt
@@ -296,8 +297,10 @@ class AnchorLoader(_BaseLoader):
         entries = [self.roidb[j] for j in self._batches[i]]
         (ph, pw), G, sidx = self.step_plan(i)
         data, label = minibatch.get_minibatch(entries, 0, self.mode, need_mean=self.need_mean, has_rpn=True,
-                                              scale_indexes=sidx)
+                                              scale_indexes=sidx, raw=self.raw_images)
         im = data['data']
+        if self.raw_images:
+            return self._raw_batch(im, data['im_info'], (ph, pw), label, G, len(entries))
         if im.shape[2] > ph or im.shape[3] > pw:
             raise ValueError('image %s larger than the planned pad shape %s' % (im.shape[2:], (ph, pw)))
         if im.shape[2] != ph or im.shape[3] != pw:
@@ -314,9 +317,33 @@ class AnchorLoader(_BaseLoader):
         return {'data': _pin(np.ascontiguousarray(im, dtype=np.float32)), 'im_info': _pin(data['im_info']),
                 'gt_boxes': _pin(gt), 'n_gt': _pin(n_gt)}
 
+    def _raw_batch(self, im, im_info, hw, label, G, n):
+        """raw_images: uint8 (B, ph, pw, 3) BGR, zero padded; the device converts it (ops/image.py)
+        with ``pixel_means`` (zeros when the network does not subtract them)."""
+        ph, pw = hw
+        if im.shape[1] > ph or im.shape[2] > pw:
+            raise ValueError('image %s larger than the planned pad shape %s' % (im.shape[1:3], hw))
+        if im.shape[1] != ph or im.shape[2] != pw:
+            padded = np.zeros((im.shape[0], ph, pw, 3), np.uint8)
+            padded[:, :im.shape[1], :im.shape[2]] = im
+            im = padded
+        gts = label.get('gt_boxes', [np.zeros((0, 5), np.float32)] * n)
+        gt = np.full((n, G, 5), -1.0, np.float32)
+        n_gt = np.zeros((n,), np.int32)
+        for k, g in enumerate(gts):
+            m = min(g.shape[0], G)
+            gt[k, :m] = g[:m]
+            n_gt[k] = m
+        means = np.asarray(config.PIXEL_MEANS, np.float64).reshape(-1)[:3] if self.need_mean else np.zeros(3)
+        return {'data': _pin(im), 'im_info': _pin(im_info), 'gt_boxes': _pin(gt), 'n_gt': _pin(n_gt),
+                'pixel_means': torch.from_numpy(means.astype(np.float64))}
+
     @property
     def provide_data(self):
         b = self.get_batch()
+        if self.raw_images:  # the network's input shape
+            n, h, w, _ = b['data'].shape
+            return [('data', (n, 3, h, w)), ('im_info', tuple(b['im_info'].shape))]
         return [('data', tuple(b['data'].shape)), ('im_info', tuple(b['im_info'].shape))]
 
     @property
@@ -324,11 +351,12 @@ class AnchorLoader(_BaseLoader):
         b = self.get_batch()
         out = [('gt_boxes', tuple(b['gt_boxes'].shape))]
         if self.feat_sym is not None and hasattr(self.feat_sym, 'feat_shape'):
-            h, w = self.feat_sym.feat_shape(b['data'].shape[2], b['data'].shape[3])
+            n, _, ih, iw = self.provide_data[0][1]
+            h, w = self.feat_sym.feat_shape(ih, iw)
             A = len(self.anchor_scales) * len(self.anchor_ratios)
-            out += [('label', (b['data'].shape[0], A * h * w)), ('bbox_target', (b['data'].shape[0], 4 * A, h, w)),
-                    ('bbox_inside_weight', (b['data'].shape[0], 4 * A, h, w)),
-                    ('bbox_outside_weight', (b['data'].shape[0], 4 * A, h, w))]
+            out += [('label', (n, A * h * w)), ('bbox_target', (n, 4 * A, h, w)),
+                    ('bbox_inside_weight', (n, 4 * A, h, w)),
+                    ('bbox_outside_weight', (n, 4 * A, h, w))]
         return out
 
 

@@ -24,13 +24,25 @@ def load_image(entry):
     return im
 
 
-def get_image_array(roidb, scales, scale_indexes, need_mean=True):
+def get_image_array(roidb, scales, scale_indexes, need_mean=True, raw=False):
+    """-> (batch array, scales).  ``raw``: the resized uint8 BGR images as a zero-padded
+    (B, H, W, 3) array, converted on the device (ops/image.py) instead of here."""
     processed, im_scales = [], []
     for i, entry in enumerate(roidb):
         im = load_image(entry)
         im, im_scale = image_processing.resize(im, scales[scale_indexes[i]], config.MAX_SIZE)
-        processed.append(image_processing.transform(im, config.PIXEL_MEANS, need_mean=need_mean).astype(np.float32))
+        if raw:
+            processed.append(np.ascontiguousarray(im, dtype=np.uint8))
+        else:
+            processed.append(image_processing.transform(im, config.PIXEL_MEANS, need_mean=need_mean).astype(np.float32))
         im_scales.append(im_scale)
+    if raw:
+        h = max(p.shape[0] for p in processed)
+        w = max(p.shape[1] for p in processed)
+        out = np.zeros((len(processed), h, w, 3), np.uint8)
+        for k, p in enumerate(processed):
+            out[k, :p.shape[0], :p.shape[1]] = p
+        return out, im_scales
     return image_processing.tensor_vstack(processed), im_scales
 
 
@@ -59,13 +71,14 @@ def sample_rois(roidb, fg_rois_per_image, rois_per_image, num_classes):
     return rois, labels, bbox_targets, bbox_inside, overlaps
 
 
-def get_minibatch(roidb, num_classes, mode='test', need_mean=True, has_rpn=None, scale_indexes=None):
+def get_minibatch(roidb, num_classes, mode='test', need_mean=True, has_rpn=None, scale_indexes=None, raw=False):
     """``has_rpn`` overrides config[TRAIN|TEST].HAS_RPN (thread-safe use from loader workers);
-    ``scale_indexes`` fixes the per-image SCALES choice (the loaders plan it per global batch)."""
+    ``scale_indexes`` fixes the per-image SCALES choice (the loaders plan it per global batch);
+    ``raw``: data is the uint8 (B, H, W, 3) image batch (get_image_array)."""
     num_images = len(roidb)
     scale_idx = npr.randint(0, high=len(config.SCALES), size=num_images) if scale_indexes is None \
         else np.asarray(scale_indexes)
-    im_array, im_scales = get_image_array(roidb, config.SCALES, scale_idx, need_mean=need_mean)
+    im_array, im_scales = get_image_array(roidb, config.SCALES, scale_idx, need_mean=need_mean, raw=raw)
     cfg_key = 'TRAIN' if mode == 'train' else 'TEST'
     if (config[cfg_key].HAS_RPN if has_rpn is None else has_rpn):
         # per-image im_info (the reference asserts a single image here)

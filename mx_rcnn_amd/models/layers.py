@@ -87,13 +87,21 @@ class Linear(MxLayer):
         return out
 
     def forward(self, x, relu=False, drop_p=0.0):
-        x = x.reshape(x.shape[0], -1)
+        if self.in_shape is not None:
+            # (h, w, c) columns on both sides: the channels_last filter's rows are a free view, and
+            # the activation (MXNet Flatten (c, h, w) rows, or the map itself) is the one permuted
+            # -- a copy of R x 25088 activations, never of the 100M-element weight
+            if x.dim() != 4:
+                x = x.reshape(x.shape[0], *self.in_shape)
+            x = x.permute(0, 2, 3, 1).reshape(x.shape[0], -1)
+        else:
+            x = x.reshape(x.shape[0], -1)
         b = None if self.bias is None else _w(self.bias, x)
         if drop_p and self.training and self._seed is None:
             self._seed = layer_seed(self.mx_name)
         w = _w(self.weight, x)
-        if w.dim() != 2:  # logical (c, h, w) columns (a copy when the weight is held channels_last)
-            w = w.reshape(w.shape[0], -1)
+        if w.dim() != 2:
+            w = w.permute(0, 2, 3, 1).reshape(w.shape[0], -1)
         return fully_connected(x, w, b, relu, drop_p, self._seed or 0, self.rng_step, self.training)
 
 

@@ -64,8 +64,6 @@ class VGGHead(nn.Module):
             if vgg_fused.head_ok(rows, self):
                 return vgg_fused.vgg_head(rows, self)
         x = pooled.reshape(pooled.shape[0], -1)  # MXNet Flatten: (C, H, W) order
-        if vgg_fused.head_ok(x, self, logical=True):
-            return vgg_fused.vgg_head(x, self, logical=True)
         # relu6/drop6 and relu7/drop7 run in the FC kernel's epilogue (ops/fc.py)
         x = self.fc6(x, relu=True, drop_p=self.dropout)
         x = self.fc7(x, relu=True, drop_p=self.dropout)

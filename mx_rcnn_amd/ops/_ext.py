@@ -28,6 +28,9 @@ def _load():
             _EXT = importlib.import_module('mx_rcnn_amd._C')
     except ImportError as e:  # pragma: no cover - depends on build state
         _ERR = e
+    if _EXT is not None:
+        from . import tune_plan  # the shipped / user conv plans, before the first conv
+        tune_plan.ensure_loaded(_EXT)
     return _EXT
 
 

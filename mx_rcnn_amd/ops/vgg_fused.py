@@ -241,10 +241,9 @@ class _VGGHead(torch.autograd.Function):
         return (dx, None, None, None) + tuple(grads)
 
 
-def vgg_head(x, head, logical=False):
+def vgg_head(x, head):
     """The fused head for VGGHead's Linear modules; ``x`` (R, C*7*7) rows of the pooled map in
     (h, w, c) order (its channels_last memory), the order of fc6's filter rows."""
-    assert not logical, 'the fused head reads (h, w, c) rows'
     from .fc import layer_seed
     training = head.training
     p = float(head.dropout) if training else 0.0
@@ -265,14 +264,14 @@ def trunk_ok(x, convs):
             all(weight_ok(act, c.weight) and c.bias is not None and c.weight.shape[1] % 64 == 0 for c in convs[1:]))
 
 
-def head_ok(x, head, logical=False):
-    """True when the fused head can run on rows ``x`` (R, K); ``logical``: the rows are in MXNet
-    Flatten (c, h, w) order, which only a 2-D fc6 weight matches."""
+def head_ok(x, head):
+    """True when the fused head can run on rows ``x`` (R, K) in (h, w, c) order: fc6 must be held
+    as the (O, C, H, W) filter (Linear in_shape) whose channels_last rows have that order."""
     import os
     from .conv import weight_ok
     if os.environ.get('MXR_VGG_FUSED', '1') == '0' or not x.is_cuda or x.dtype != torch.bfloat16:
         return False
-    if logical and head.fc6.weight.dim() != 2:
+    if head.fc6.weight.dim() != 4:
         return False
     fcs = (head.fc6, head.fc7)
     if head.training and head.dropout > 0 and head.fc6.rng_step is None:

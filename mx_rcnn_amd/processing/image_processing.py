@@ -53,6 +53,8 @@ def resize(im, target_size, max_size):
     im_scale = compute_scale(im.shape, target_size, max_size)
     out_h = int(round(im.shape[0] * im_scale))
     out_w = int(round(im.shape[1] * im_scale))
+    if (out_h, out_w) == tuple(im.shape[:2]) and im_scale == 1.0:
+        return im, im_scale  # the identity resample (cv2.resize returns the same pixels)
     return resize_bilinear(im, out_h, out_w), im_scale
 
 

@@ -165,6 +165,37 @@ def test_roi_pool_gpu(cuda, dtype, C):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
+def test_roi_pool_backward_propagates_nonfinite(cuda, dtype):
+    """the fixed-point backward must not turn a NaN / inf head gradient into a large
+    finite trunk gradient -- the affected (image, channel) comes out NaN, every other channel exact."""
+    g = torch.Generator().manual_seed(6)
+    B, C, H, W = 2, 64, 30, 40
+    feat = torch.randn(B, C, H, W, generator=g)
+    rois = _rois(g, 32, B, H, W)
+    fg = feat.to(cuda, dtype).contiguous(memory_format=torch.channels_last).requires_grad_()
+    out = ops.roi_pool(fg, rois.to(cuda), (7, 7), 1 / 16)
+    gout = torch.randn(out.shape, generator=g)
+    r_nan = int((rois[:, 0] == 0).nonzero()[0])
+    r_inf = int((rois[:, 0] == 1).nonzero()[0])
+    gout[r_nan, 5, 3, 3] = float('nan')
+    gout[r_inf, 9, 0, 0] = float('inf')
+    out.backward(gout.to(cuda, dtype))
+    got = fg.grad.float().cpu()
+    assert torch.isnan(got[0, 5]).all() and torch.isnan(got[1, 9]).all()
+    clean = torch.ones(B, C, dtype=torch.bool)
+    clean[0, 5] = False
+    clean[1, 9] = False
+    assert torch.isfinite(got[clean]).all()
+    gc = gout.clone()
+    gc[r_nan, 5, 3, 3] = 0
+    gc[r_inf, 9, 0, 0] = 0
+    fg2 = fg.detach().clone().requires_grad_()
+    ops.roi_pool(fg2, rois.to(cuda), (7, 7), 1 / 16).backward(gc.to(cuda, dtype))
+    assert torch.equal(got[clean], fg2.grad.float().cpu()[clean])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', [torch.float32, torch.bfloat16])
 def test_losses_gpu(cuda, dtype):
     g = torch.Generator().manual_seed(5)
     B, A, H, W = 2, 12, 20, 31

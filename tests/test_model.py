@@ -108,9 +108,13 @@ def test_e2e_step_gpu_graph(cuda):
 
 
 @pytest.mark.gpu
-def test_overlapped_sgd_matches_end_of_step_sgd(cuda, monkeypatch):
+@pytest.mark.parametrize('prec', ['bf16', 'bf16x3', 'fp32'])
+def test_overlapped_sgd_matches_end_of_step_sgd(cuda, monkeypatch, prec):
     """Bucket-by-bucket SGD under the backward pass (MXR_OVERLAP_SGD=1, parallel/reducer.py) gives the same weights
-    and momenta as one update after the backward (MXR_OVERLAP_SGD=0)."""
+    and momenta as one update after the backward (MXR_OVERLAP_SGD=0), in every storage mode: the
+    multi-plane stores update bucket slices at unpadded offsets with plane_stride, and
+    their shadow planes must stay the exact split of the masters."""
+    from mx_rcnn_amd.ops import precision
     fixed = ['conv0', 'stage1', 'stage2', 'bn_data', 'bn0']
     b = {k: v.to(cuda) for k, v in _batch(320, 480).items()}
 
@@ -118,13 +122,19 @@ def test_overlapped_sgd_matches_end_of_step_sgd(cuda, monkeypatch):
         monkeypatch.setenv('MXR_OVERLAP_SGD', '1' if overlap else '0')
         torch.manual_seed(0)
         m = FasterRCNN('resnet50', 21, cfg=_cfg())
-        tr = Trainer(m, 'e2e', fixed_param_prefix=fixed, lr=0.01, device=cuda)
+        tr = Trainer(m, 'e2e', fixed_param_prefix=fixed, lr=0.01, device=cuda, precision=prec)
         assert tr.reducer.sgd_capable == overlap
         for i in range(2):
             torch.manual_seed(10 + i)
             tr.step(b)
         assert tr.reducer.sgd_applied == overlap
         torch.cuda.synchronize()
+        for g in tr.store.groups:
+            if g.x2:
+                parts = precision.split(g.master, g.x2)
+                for k in range(g.x2):
+                    assert torch.equal(g.shadow[k * g.plane:k * g.plane + g.numel],
+                                       parts[k * g.numel:(k + 1) * g.numel]), (prec, overlap, k)
         return tr.store.state_arrays(), tr.store.optimizer_state()
 
     w1, m1 = run(True)

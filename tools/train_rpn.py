@@ -40,7 +40,8 @@ def train_rpn(image_set, year, root_path, devkit_path, pretrained, epoch, prefix
     else:
         _, roidb = load_gt_roidb(image_set, year, root_path, devkit_path, flip=True)
     train_data = AnchorLoader(model, roidb, batch_size=1, shuffle=True, anchor_scales=model.anchor_scales,
-                              rank=rank, world_size=world, seed=seed, work_load_list=work_load_list)
+                              rank=rank, world_size=world, seed=seed, work_load_list=work_load_list,
+                              raw_images=launch.raw_images(ctx))
     fam = launch.family(network)
     fixed = (['conv1', 'conv2', 'conv3', 'conv4', 'conv5'] if config.TRAIN.FINETUNE else ['conv1', 'conv2']) \
         if fam == 'vgg' else launch.FIXED_PREFIX['resnet']

@@ -37,7 +37,8 @@ def end2end_train(args):
     scales = model.anchor_scales
     train_data = AnchorLoader(model, roidb, batch_size=args.ims_per_gpu, shuffle=True, mode='train',
                               anchor_scales=scales, rank=rank, world_size=world, seed=args.seed,
-                              need_mean=fam == 'vgg', work_load_list=args.work_load_list)
+                              need_mean=fam == 'vgg', work_load_list=args.work_load_list,
+                              raw_images=launch.raw_images(device))
     launch.calibrate_if_random(model, train_data, arg_params)
     mod = MutableModule(model, data_names=['data', 'im_info'], label_names=['gt_boxes'], context=device,
                         fixed_param_prefix=launch.FIXED_PREFIX[fam], mode='e2e', use_graph=not args.eager)

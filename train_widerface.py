@@ -46,7 +46,7 @@ def main(args, default_network=DEFAULT_NETWORK):
     fam = launch.family(network)
     train_data = AnchorLoader(model, roidb, batch_size=args.ims_per_gpu, shuffle=not args.no_shuffle,
                               anchor_scales=model.anchor_scales, rank=rank, world_size=world, seed=args.seed,
-                              need_mean=args.need_mean, max_gt=1200)
+                              need_mean=args.need_mean, max_gt=1200, raw_images=launch.raw_images(device))
     launch.calibrate_if_random(model, train_data, arg_params)
     mod = MutableModule(model, data_names=['data', 'im_info'], label_names=['gt_boxes'], context=device,
                         fixed_param_prefix=launch.FIXED_PREFIX[fam] if fam == 'resnet' else

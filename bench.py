@@ -167,6 +167,8 @@ def run(args, precision, rank, world, device):
         pool = [rcnn_batch(b, args.num_classes, cfg.TRAIN.BATCH_SIZE, gen) for b in pool]
     if args.network.startswith('resnet'):
         model.to(device).calibrate_bn(pool[0]['data'])  # stand-in for pretrained BN statistics
+    else:
+        model.to(device).calibrate_vgg(pool[0]['data'])  # stand-in for pretrained filters (LSUV scale)
     fixed = ['conv0', 'stage1', 'stage2', 'bn_data', 'bn0'] if args.network.startswith('resnet') else ['conv1', 'conv2']
     trainer = Trainer(model, args.train_mode, fixed_param_prefix=fixed, lr=0.001, momentum=0.9, wd=0.0005, clip_gradient=1.0,
                       rescale_grad=1.0, device=device, bucket_mb=args.bucket_mb, precision=precision,
@@ -214,9 +216,9 @@ def run(args, precision, rank, world, device):
     plan = None
     if device.type == 'cuda':  # the conv plan the timed step ran with, and whether the ranks agree
         from mx_rcnn_amd.ops import tune_plan
-        h = int(tune_plan.plan_hash(), 16)
-        plan = {'hash': '%08x' % h, 'entries': len(tune_plan.table()),
-                'ranks_agree': pdist.all_reduce_max(float(h), device) == -pdist.all_reduce_max(-float(h), device)}
+        ph = int(tune_plan.plan_hash(), 16)
+        plan = {'hash': '%08x' % ph, 'entries': len(tune_plan.table()),
+                'ranks_agree': pdist.all_reduce_max(float(ph), device) == -pdist.all_reduce_max(-float(ph), device)}
     # after the timed region: each gradient bucket's collective in isolation (HIP events)
     comm = trainer.reducer.measure_collectives() if world > 1 else None
     ms = elapsed / max(args.steps, 1) * 1e3

@@ -139,10 +139,15 @@ def batch_images(b):
 
 def calibrate_if_random(model, loader, arg_params):
     """Random-init ResNets get data-dependent BN statistics from the first batch (a pretrained
-    checkpoint carries real ones); without them 100+ pre-activation units blow up."""
-    if arg_params or not model.network.startswith('resnet'):
+    checkpoint carries real ones); without them 100+ pre-activation units blow up.  A random VGG16
+    trunk gets a data-dependent (LSUV) filter scale for the same reason (FasterRCNN.calibrate_vgg)."""
+    if arg_params:
         return False
     b = loader.get_batch()
+    if not model.network.startswith('resnet'):
+        model.calibrate_vgg(batch_images(b))
+        logging.info('no pretrained weights: data-dependent (LSUV) init of the %s trunk', model.network)
+        return True
     model.calibrate_bn(batch_images(b))
     logging.info('no pretrained weights: calibrated %s BN statistics on the first batch', model.network)
     return True

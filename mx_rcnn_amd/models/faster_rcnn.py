@@ -148,6 +148,30 @@ class FasterRCNN(nn.Module):
             self.train(was)
         return len(bns)
 
+    @torch.no_grad()
+    def calibrate_vgg(self, data):
+        """Data-dependent init of a random VGG16 trunk (the stand-in for the ImageNet weights the
+        reference always loads, `train_end2end.py:56-78`): layer by layer, an MSRA-normal filter
+        rescaled so the pre-activation over ``data`` (N,3,H,W) has unit standard deviation, zero
+        bias (LSUV).  The N(0, 0.01) default leaves 13 plain conv layers with vanishing
+        activations, a trunk that random-init training cannot move."""
+        import torch.nn.functional as Fn
+        from .layers import max_pool
+        trunk = self.trunk
+        x = data.float().cpu()
+        g = torch.Generator().manual_seed(0)
+        for i, c in enumerate(trunk.convs):
+            w = torch.randn(c.weight.shape, generator=g) * (2.0 / c.weight[0].numel()) ** 0.5
+            y = Fn.conv2d(x, w, None, 1, 1)
+            w /= float(y.std()) + 1e-12
+            c.weight.copy_(w.to(c.weight.device, c.weight.dtype))
+            if c.bias is not None:
+                c.bias.zero_()
+            x = torch.relu(y / (float(y.std()) + 1e-12))
+            if i in trunk.pool_after:
+                x = max_pool(x, 2, 2)
+        return len(trunk.convs)
+
     def feat_shape(self, h, w):
         return self.trunk.feat_shape(h, w)
 

@@ -18,16 +18,16 @@ cli)
   MXR_RAW_IMAGES=0 run cli_e2e_hostfloat 400 python train_end2end.py --synthetic 64 --synthetic-shape 800x1333 \
       --network resnet101 --num-classes 81 --max-steps 200 --frequent 50 --pretrained none --prefix /tmp/cli2/e2e --num_epoch 10 ;;
 planted_r101)
-  run planted_r101_train 900 python train_end2end.py --synthetic 256 --synthetic-kind planted --synthetic-shape 600x1000 \
+  run planted_r101_train 900 python train_end2end.py --synthetic ${PIMGS:-256} --synthetic-kind planted --synthetic-shape 600x1000 \
       --network resnet101 --num-classes 8 --max-steps ${PSTEPS:-4000} --frequent 100 --pretrained none --lr 0.005 \
-      --factor-step 3000 --prefix /tmp/pl_r101/e2e --num_epoch 100
+      --factor-step ${FSTEP:-3000} --prefix /tmp/pl_r101/e2e --num_epoch 100
   E=$(ls /tmp/pl_r101/e2e-*.params | sed 's/.*-0*\([0-9]*\)\.params/\1/' | sort -n | tail -1)
   run planted_r101_test 600 python test.py --prefix /tmp/pl_r101/e2e --epoch $E --synthetic 100 --synthetic-kind planted \
       --synthetic-shape 600x1000 --seed 1000 --network resnet101 --num-classes 8 --has_rpn ;;
 planted_vgg)
-  run planted_vgg_train 900 python train_end2end.py --synthetic 256 --synthetic-kind planted --synthetic-shape 600x1000 \
+  run planted_vgg_train 900 python train_end2end.py --synthetic ${PIMGS:-256} --synthetic-kind planted --synthetic-shape 600x1000 \
       --network vgg16 --num-classes 8 --max-steps ${PSTEPS:-4000} --frequent 100 --pretrained none --lr 0.005 \
-      --factor-step 3000 --prefix /tmp/pl_vgg/e2e --num_epoch 100
+      --factor-step ${FSTEP:-3000} --prefix /tmp/pl_vgg/e2e --num_epoch 100
   E=$(ls /tmp/pl_vgg/e2e-*.params | sed 's/.*-0*\([0-9]*\)\.params/\1/' | sort -n | tail -1)
   run planted_vgg_test 600 python test.py --prefix /tmp/pl_vgg/e2e --epoch $E --synthetic 100 --synthetic-kind planted \
       --synthetic-shape 600x1000 --seed 1000 --network vgg16 --num-classes 8 --has_rpn ;;

@@ -16,13 +16,17 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(tmp_path, name, precision, dp, port, steps):
+def _run(tmp_path, name, precision, dp, port, steps, plan_file=None):
     out = str(tmp_path / (name + '.pt'))
     env = dict(os.environ)
     for k in ('MXR_FORCE_DIST', 'WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
         env.pop(k, None)
-    # the per-shape conv autotune picks split-K variants by timing, i.e. per process: fix the plan
-    env['MXR_CONV_TUNE'] = '0'
+    if plan_file is None:
+        # the per-shape conv autotune picks split-K variants by timing, i.e. per process: fix the plan
+        env['MXR_CONV_TUNE'] = '0'
+    else:  # autotune on, its plan persisted to / loaded from this file (ops/tune_plan.py)
+        env.pop('MXR_CONV_TUNE', None)
+        env['MXR_TUNE_FILE'] = str(plan_file)
     if dp:
         env.update({'MXR_FORCE_DIST': '1', 'WORLD_SIZE': '1', 'RANK': '0', 'LOCAL_RANK': '0',
                     'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port)})
@@ -56,3 +60,17 @@ def test_rccl_one_rank_graphed_step_matches_single_process(tmp_path, precision):
     diff = [k for k in keys if not torch.equal(a[k], d[k])]
     assert not diff, 'DP step differs: %s (max abs %s)' % (
         diff[:5], [float((a[k].float() - d[k].float()).abs().max()) for k in diff[:5]])
+
+
+@pytest.mark.gpu
+def test_autotuned_reruns_are_bitwise_equal_through_the_plan_file(tmp_path):
+    """With the conv autotune ON, the first run times its candidates and persists the plan
+    (ops/tune_plan.py); a second run loads it, takes the same kernels and must produce the same
+    weights bit for bit (fp32 precision, one graphed step)."""
+    plan = tmp_path / 'plan.json'
+    a, _ = _run(tmp_path, 'tuned1', 'fp32', False, 0, 1, plan_file=plan)
+    assert plan.exists(), 'the first run did not persist its conv plan'
+    b, _ = _run(tmp_path, 'tuned2', 'fp32', False, 0, 1, plan_file=plan)
+    keys = [k for k in a if not k.startswith('_')]
+    diff = [k for k in keys if not torch.equal(a[k], b[k])]
+    assert not diff, 'autotuned reruns differ: %s' % diff[:5]

@@ -35,9 +35,11 @@ def end2end_train(args):
                                     flip=not args.no_flip)
     fam = launch.family(args.network)
     scales = model.anchor_scales
+    # pixel means subtracted for every backbone, as the reference's AnchorLoader default does
+    # (`train_end2end.py:56`, `rcnn/loader.py:148`) and as the test loaders do
     train_data = AnchorLoader(model, roidb, batch_size=args.ims_per_gpu, shuffle=True, mode='train',
                               anchor_scales=scales, rank=rank, world_size=world, seed=args.seed,
-                              need_mean=fam == 'vgg', work_load_list=args.work_load_list,
+                              work_load_list=args.work_load_list,
                               raw_images=launch.raw_images(device))
     launch.calibrate_if_random(model, train_data, arg_params)
     mod = MutableModule(model, data_names=['data', 'im_info'], label_names=['gt_boxes'], context=device,

@@ -10,6 +10,7 @@
 #include <string>
 #include <torch/extension.h>
 #include <ATen/Parallel.h>
+#include <ATen/hip/HIPGeneratorImpl.h>
 #include <c10/core/DeviceGuard.h>
 #include <c10/hip/HIPStream.h>
 
@@ -682,6 +683,27 @@ std::vector<std::tuple<std::string, int64_t, int64_t>> conv_tune_table() {
   std::lock_guard<std::mutex> lk(g_tune_mu);
   std::vector<std::tuple<std::string, int64_t, int64_t>> out;
   for (const auto& kv : g_tune) out.emplace_back(kv.first, kv.second.first, kv.second.second);
+  return out;
+}
+
+// torch.rand(..).uniform_ semantics on the GPU without a torch distribution kernel: the draw uses the
+// default generator's graph-safe Philox state (advanced like torch's own kernels advance it)
+Tensor philox_uniform_(Tensor out) {
+  CHECK_DEV(out); CHECK_F32(out);
+  TORCH_CHECK(out.is_contiguous(), "philox_uniform_: contiguous fp32 output");
+  DevGuard g(out.device());
+  auto* gen = at::check_generator<at::CUDAGeneratorImpl>(at::cuda::detail::getDefaultCUDAGenerator(out.device().index()));
+  at::PhiloxCudaState ps;
+  {
+    std::lock_guard<std::mutex> lock(gen->mutex_);
+    ps = gen->philox_cuda_state(4);
+  }
+  mxr::PhiloxArgs a;
+  a.captured = ps.captured_ ? 1 : 0;
+  a.seed = ps.captured_ ? (uint64_t)reinterpret_cast<uintptr_t>(ps.seed_.ptr) : ps.seed_.val;
+  a.offset = ps.captured_ ? (uint64_t)reinterpret_cast<uintptr_t>(ps.offset_.ptr) : ps.offset_.val;
+  a.intra = ps.captured_ ? ps.offset_intragraph_ : 0;
+  mxr::philox_fill(out.data_ptr<float>(), out.numel(), a, cur_stream());
   return out;
 }
 
@@ -2199,6 +2221,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("mean"), py::arg("var"), py::arg("eps"), py::arg("fix_gamma"), py::arg("relu"), py::arg("need_dx"),
         py::arg("need_params"), py::arg("dgamma_out") = py::none(), py::arg("dbeta_out") = py::none(),
         py::arg("dres") = py::none(), py::arg("x2") = 0);
+  m.def("philox_uniform_", &philox_uniform_, py::arg("out"),
+        "fill a contiguous fp32 GPU tensor with U[0,1) from the default generator's graph-safe Philox state");
   m.def("image_prep", &image_prep, py::arg("img"), py::arg("im_info"), py::arg("means"), py::arg("out_bf16"),
         "uint8 BGR (B,H,W,3) -> channels_last (B,3,H,W) RGB minus means, 0 outside im_info's (h, w)");
   m.def("conv_tune_table", &conv_tune_table, "per-shape conv autotune choices: [(key, tile, splits)]");

@@ -122,6 +122,14 @@ void roi_pool_bwd(const void* grad_out, int bf16, const int32_t* argmax, const f
 // fp32 -> bf16 / fp32 copy-convert helper (n elements)
 void cast_f32(const float* in, void* out, int out_bf16, int64_t n, hipStream_t st);
 
+// ---- uniform draws from PyTorch's graph-safe Philox state (rng.hip) ------------------
+// seed / offset are values, or (captured) device pointers to int64 values, offset += intra
+struct PhiloxArgs {
+  uint64_t seed, offset, intra;
+  int captured;
+};
+void philox_fill(float* out, int64_t n, const PhiloxArgs& a, hipStream_t st);
+
 // ---- image preparation (image.hip) ---------------------------------------------
 // uint8 BGR (B, H, W, 3) -> channels_last (B, 3, H, W) fp32 / bf16 (NHWC memory): RGB, minus means
 // (RGB order), 0 outside im_info[b, 0:2] (the valid resized height / width)

@@ -17,6 +17,7 @@ from ._ext import ext_available, need_ext, const_tensor
 from .anchors import base_anchors
 from .boxes import bbox_transform, box_iou
 from .sampling import keep_random
+from .rng import uniform
 
 
 def _assign_ref(H, W, base, feat_stride, im_info, border, gt, n_gt, neg, pos, clobber):
@@ -76,7 +77,7 @@ def anchor_target(feat_shape, gt_boxes, n_gt, im_info, feat_stride=16, scales=(8
             # assignment + subsampling + layout in four grid-wide launches (csrc/hip/sample.hip
             # anchor_mark: histogram thresholds instead of a one-workgroup selection pass)
             C = need_ext()
-            keys = torch.rand((B, H * W * A), device=dev, generator=generator)
+            keys = uniform((B, H * W * A), dev, generator)
             iw = [float(v) for v in np.asarray(cfg.TRAIN.RPN_BBOX_INSIDE_WEIGHTS, dtype=np.float64).ravel()[:4]]
             lab, bt, inside, outside, meta = C.anchor_target_fused(
                 base, H, W, float(feat_stride), im_info.float().contiguous(), int(allowed_border),
@@ -92,7 +93,7 @@ def anchor_target(feat_shape, gt_boxes, n_gt, im_info, feat_stride=16, scales=(8
                 gt_boxes.float().contiguous(), n_gt, float(cfg.TRAIN.RPN_NEGATIVE_OVERLAP),
                 float(cfg.TRAIN.RPN_POSITIVE_OVERLAP), bool(cfg.TRAIN.RPN_CLOBBER_POSITIVES))
             # fused subsampling + weights + reference layout (csrc/hip/sample.hip): 3 launches
-            keys = torch.rand(label.shape, device=dev, generator=generator)
+            keys = uniform(label.shape, dev, generator)
             iw = [float(v) for v in np.asarray(cfg.TRAIN.RPN_BBOX_INSIDE_WEIGHTS, dtype=np.float64).ravel()[:4]]
             lab, bt, inside, outside, meta = C.anchor_sample(label, targets.contiguous(), keys, A, H, W, num_fg,
                                                              int(cfg.TRAIN.RPN_BATCH_SIZE), iw,

@@ -22,6 +22,7 @@ from ._ext import ext_available, need_ext
 from .anchors import base_anchors
 from .boxes import bbox_pred, clip_boxes
 from .nms import _greedy_ref, nms_debug_check
+from .rng import uniform
 
 
 def _decode_ref(cls, dlt, im_info, base, feat_stride, min_size, crop, is_prob):
@@ -98,7 +99,7 @@ def proposal(cls, bbox_deltas, im_info, feat_stride=16, scales=(8, 16, 32), rati
                 sboxes = torch.gather(boxes, 1, order[..., None].expand(-1, -1, 4)).contiguous()
                 n_valid = (skeys > float('-inf')).sum(dim=1).to(torch.int32)
         post = int(post_nms_top_n) if post_nms_top_n > 0 else P
-        rand_u = torch.rand(B, post, device=dev, generator=generator)
+        rand_u = uniform((B, post), dev, generator)
         if cls.is_cuda:
             mask = None
             if after_mask is not None:

@@ -14,6 +14,7 @@ from ..config import config as _global_cfg
 from .boxes import bbox_transform, iou_max
 from .sampling import sample_slots
 from ._ext import const_tensor
+from .rng import uniform
 
 
 def proposal_target(rois, gt_boxes, n_gt, num_classes, cfg=None, is_train=True, generator=None):
@@ -34,7 +35,7 @@ def proposal_target(rois, gt_boxes, n_gt, num_classes, cfg=None, is_train=True, 
             rf = rois.float().contiguous()
             max_ov, argmax = iou_max(rf, gtf, n_gt, off=1)
             F = int(round(cfg.TRAIN.FG_FRACTION * R))
-            rnd = torch.rand(B, 2 * (P + G) + R, device=dev, generator=generator)
+            rnd = uniform((B, 2 * (P + G) + R), dev, generator)
             out = need_ext().proposal_sample(
                 rf, gtf.contiguous(), n_gt.contiguous(), max_ov.contiguous(), argmax.contiguous(), rnd, R, F,
                 int(num_classes), float(cfg.TRAIN.FG_THRESH), float(cfg.TRAIN.BG_THRESH_HI),

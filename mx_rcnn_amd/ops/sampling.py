@@ -7,10 +7,12 @@ with-replacement pad PREPENDED exactly where the reference puts it
 """
 import torch
 
+from .rng import uniform
+
 
 def random_rank(mask, generator=None):
     """Per-row random rank of each True entry among the row's True entries (others >= count)."""
-    keys = torch.rand(mask.shape, device=mask.device, generator=generator)
+    keys = uniform(mask.shape, mask.device, generator)
     keys = torch.where(mask, keys, torch.full_like(keys, 2.0))
     order = torch.argsort(keys, dim=-1)
     rank = torch.empty_like(order)
@@ -39,7 +41,7 @@ def sample_slots(mask, n, generator=None):
     take = torch.clamp(cnt, max=n)
     pad = n - take
     j = torch.arange(n, device=mask.device)[None, :].expand(B, n)
-    u = torch.rand(B, n, device=mask.device, generator=generator)
+    u = uniform((B, n), mask.device, generator)
     pick = torch.minimum((u * take[:, None].clamp_min(1)).long(), take[:, None].clamp_min(1) - 1)
     src = torch.where(j < pad[:, None], pick, j - pad[:, None])
     src = src.clamp(0, N - 1)

@@ -226,6 +226,7 @@ class MutableModule(object):
         t.reducer.finish()
         t.update_lr()
         t.store.sgd_step(t.lr_t, t.momentum, t.wd, t.rescale, t.clip, grad_for=t.reducer.grad_for)
+        t.advance_rng()
 
     def step(self, data_batch):
         """forward + backward + update fused (graph-replayed per input shape when enabled).
@@ -325,6 +326,7 @@ class MutableModule(object):
         from ..utils import ndarray_io
         st = {'mom:' + k: v.detach().cpu().numpy() for k, v in self.trainer.store.optimizer_state().items()}
         st['num_update'] = np.array([self.trainer.num_update], np.float32)
+        st['rng_step'] = self.trainer.rng_step.detach().cpu().numpy().astype(np.float64)  # dropout counter
         st['rng_cpu'] = torch.get_rng_state().numpy()
         if self.context.type == 'cuda':
             st['rng_cuda'] = torch.cuda.get_rng_state(self.context).numpy()
@@ -339,6 +341,8 @@ class MutableModule(object):
             self.trainer.num_update = int(np.asarray(st['num_update']).reshape(-1)[0])
             self.trainer.num_update -= 1
             self.trainer.update_lr()  # lr tensor matches the schedule position
+        if 'rng_step' in st:
+            self.trainer.rng_step.fill_(int(np.asarray(st['rng_step']).reshape(-1)[0]))
         if 'rng_cpu' in st:
             torch.set_rng_state(torch.from_numpy(np.ascontiguousarray(st['rng_cpu'], dtype=np.uint8)))
         if 'rng_cuda' in st and self.context.type == 'cuda':

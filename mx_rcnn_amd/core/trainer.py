@@ -61,9 +61,11 @@ class Trainer:
             lr_scheduler.base_lr = lr
         self.lr_t = torch.full((1,), float(lr), dtype=torch.float32, device=dev)
         self.num_update = 0
-        # step counter of the counter-based dropout (ops/fc.py), advanced with the LR tensor so a
-        # replayed graph draws a fresh mask every update
+        # step counter of the counter-based dropout (ops/fc.py), advanced on the device at the end
+        # of every step (inside the captured graph), so a replayed graph draws a fresh mask every
+        # update with no host-side fill between replays
         self.rng_step = torch.zeros(1, dtype=torch.int64, device=dev)
+        self._lr_set = float(lr)  # the value lr_t holds (filled again only when the schedule moves)
         from ..models.layers import Linear
         for m in self.model.modules():
             if isinstance(m, Linear):
@@ -164,6 +166,7 @@ class Trainer:
                 self.store.sgd_step(self.lr_t, self.momentum, self.wd, self.rescale, self.clip,
                                     grad_for=self.reducer.grad_for, refresh=False, clear=self.fused_clear)
         self.grads_dirty = not self.fused_clear
+        self.advance_rng()
         # Return detached outputs: a caller holding the loss would otherwise keep this step's
         # autograd graph (and its AccumulateGrad nodes, bound to this step's stream) alive, and a
         # later hipGraph capture on a side stream then syncs against that stream and dies in
@@ -196,7 +199,7 @@ class Trainer:
         st = {'groups': [(g.master.clone(), g.mom.clone(), None if g.shadow is None else g.shadow.clone())
                          for g in self.store.groups],
               'buffers': [b.detach().clone() for b in self.model.buffers()],
-              'nonfinite': self.nonfinite.clone(),
+              'nonfinite': self.nonfinite.clone(), 'rng_step': self.rng_step.clone(),
               'rng_cpu': torch.get_rng_state()}
         if self.device.type == 'cuda':
             st['rng_cuda'] = torch.cuda.get_rng_state(self.device)
@@ -212,6 +215,8 @@ class Trainer:
         for b, v in zip(self.model.buffers(), st['buffers']):
             b.copy_(v)
         self.nonfinite.copy_(st['nonfinite'])
+        if 'rng_step' in st:
+            self.rng_step.copy_(st['rng_step'])
         self.store.refresh_dgrad_cache()
         if rng:
             torch.set_rng_state(st['rng_cpu'])
@@ -220,10 +225,19 @@ class Trainer:
 
     def update_lr(self):
         self.num_update += 1
-        self.rng_step.fill_(self.num_update)
         if self.lr_scheduler is not None:
-            lr = self.lr_scheduler(self.num_update)
-            self.lr_t.fill_(float(lr))
+            lr = float(self.lr_scheduler(self.num_update))
+            if lr != self._lr_set:  # a device fill only when the schedule moves
+                self.lr_t.fill_(lr)
+                self._lr_set = lr
+
+    def advance_rng(self):
+        """End of a step: the dropout counter moves on (on the device; captured with the step)."""
+        if self.rng_step.is_cuda:
+            from ..ops._ext import need_ext
+            need_ext().counter_add_(self.rng_step, 1)
+        else:
+            self.rng_step.add_(1)
 
     def step(self, batch):
         self.model.train()

@@ -707,6 +707,13 @@ Tensor philox_uniform_(Tensor out) {
   return out;
 }
 
+void counter_add_(Tensor c, int64_t v) {
+  CHECK_DEV(c);
+  TORCH_CHECK(c.scalar_type() == at::kLong && c.numel() >= 1 && c.is_contiguous(), "counter_add_: int64 counter");
+  DevGuard g(c.device());
+  mxr::counter_add(c.data_ptr<int64_t>(), v, cur_stream());
+}
+
 Tensor image_prep(const Tensor& img, const Tensor& im_info, std::vector<double> means, bool out_bf16) {
   CHECK_DEV(img); CHECK_DEV(im_info); CHECK_F32(im_info);
   TORCH_CHECK(img.scalar_type() == at::kByte && img.dim() == 4 && img.size(3) == 3 && img.is_contiguous(),
@@ -2223,6 +2230,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dres") = py::none(), py::arg("x2") = 0);
   m.def("philox_uniform_", &philox_uniform_, py::arg("out"),
         "fill a contiguous fp32 GPU tensor with U[0,1) from the default generator's graph-safe Philox state");
+  m.def("counter_add_", &counter_add_, py::arg("counter"), py::arg("v") = 1, "counter[0] += v on the device");
   m.def("image_prep", &image_prep, py::arg("img"), py::arg("im_info"), py::arg("means"), py::arg("out_bf16"),
         "uint8 BGR (B,H,W,3) -> channels_last (B,3,H,W) RGB minus means, 0 outside im_info's (h, w)");
   m.def("conv_tune_table", &conv_tune_table, "per-shape conv autotune choices: [(key, tile, splits)]");

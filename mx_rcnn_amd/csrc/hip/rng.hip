@@ -24,4 +24,12 @@ void philox_fill(float* out, int64_t n, const PhiloxArgs& a, hipStream_t st) {
   philox_fill_kernel<<<blocks, 256, 0, st>>>(out, n, a);
 }
 
+// The training step's Philox counter (the fused dropout's step, ops/fc.py) advances inside the
+// captured step with this one-lane kernel instead of a host fill before every replay.
+__global__ void counter_add_kernel(int64_t* __restrict__ p, int64_t v) {
+  if (threadIdx.x == 0) p[0] += v;
+}
+
+void counter_add(int64_t* p, int64_t v, hipStream_t st) { counter_add_kernel<<<1, 64, 0, st>>>(p, v); }
+
 }  // namespace mxr

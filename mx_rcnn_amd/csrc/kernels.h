@@ -129,6 +129,7 @@ struct PhiloxArgs {
   int captured;
 };
 void philox_fill(float* out, int64_t n, const PhiloxArgs& a, hipStream_t st);
+void counter_add(int64_t* p, int64_t v, hipStream_t st);  // p[0] += v (one lane)
 
 // ---- image preparation (image.hip) ---------------------------------------------
 // uint8 BGR (B, H, W, 3) -> channels_last (B, 3, H, W) fp32 / bf16 (NHWC memory): RGB, minus means

@@ -6,6 +6,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <tuple>
 #include <mutex>
 #include <string>
 #include <torch/extension.h>
@@ -38,6 +39,28 @@ struct DevGuard {
   c10::DeviceGuard guard;
   explicit DevGuard(const c10::Device& d) : guard(d) { g_dev = d; }
 };
+
+// Self-cleaning workspaces: a zeroed int32 buffer per (device, tag, size), allocated once and kept
+// for the process; the kernels that use it leave it zeroed again at the end of their chain (the
+// topk write kernel re-zeroes its histograms, the anchor output kernel the gt-max / histogram words,
+// the next call's first assignment kernel the mark words), so the captured step carries no fill.
+// A capture that meets a size for the first time gets a per-call zeroed tensor (never cached: it
+// would live in the graph's private pool).  One chain at a time per buffer: the training step runs
+// one proposal top-k and one anchor sampling per replay, in stream order.
+static Tensor clean_ws(const at::TensorOptions& o, const char* tag, int64_t n) {
+  static std::mutex mu;
+  static auto* cache = new std::map<std::tuple<int, std::string, int64_t>, Tensor>();  // leaked: outlives exit
+  const auto key = std::make_tuple((int)o.device().index(), std::string(tag), n);
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = cache->find(key);
+  if (it != cache->end()) return it->second;
+  Tensor t = at::zeros({n}, o);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  const bool capturing = hipStreamIsCapturing(c10::hip::getCurrentHIPStream(o.device().index()).stream(), &cs) !=
+                             hipSuccess || cs != hipStreamCaptureStatusNone;
+  if (!capturing) cache->emplace(key, t);
+  return t;
+}
 
 #define CHECK_DEV(t) TORCH_CHECK((t).is_cuda(), #t " must be a GPU tensor")
 #define CHECK_F32(t) TORCH_CHECK((t).scalar_type() == at::kFloat, #t " must be float32")
@@ -239,7 +262,7 @@ std::vector<Tensor> anchor_target_fused(const Tensor& base_anchors, int64_t H, i
   auto o = gt.options();
   // one zeroed workspace: gt_max (B, G) | key histograms (B, 2, bins) | mark workspace
   const int64_t n_gm = (int64_t)B * std::max(G, 1), n_h = (int64_t)B * 2 * mxr::kSampleBins;
-  Tensor ws = at::zeros({n_gm + n_h + mxr::anchor_mark_ws_ints(B, N)}, o.dtype(at::kInt));
+  Tensor ws = clean_ws(o.dtype(at::kInt), "anchor", n_gm + n_h + mxr::anchor_mark_ws_ints(B, N));
   int32_t* wsp = ws.data_ptr<int32_t>();
   Tensor max_ov = at::empty({B, N}, o);
   Tensor argmax = at::empty({B, N}, o.dtype(at::kInt));
@@ -250,7 +273,7 @@ std::vector<Tensor> anchor_target_fused(const Tensor& base_anchors, int64_t H, i
                             n_gt.data_ptr<int32_t>(), G, B, (float)neg_thresh, (float)pos_thresh, clobber ? 1 : 0,
                             max_ov.data_ptr<float>(), argmax.data_ptr<int32_t>(), reinterpret_cast<float*>(wsp),
                             label_pre.data_ptr<int32_t>(), targets.data_ptr<float>(), cur_stream(),
-                            keys.data_ptr<float>(), wsp + n_gm);
+                            keys.data_ptr<float>(), wsp + n_gm, wsp + n_gm + n_h, mxr::anchor_mark_ws_ints(B, N));
   Tensor meta = at::empty({B, 4}, o.dtype(at::kInt));
   Tensor label = at::empty({B, A * H * W}, o.dtype(at::kInt));
   Tensor bt = at::empty({B, 4 * A, H, W}, o);
@@ -260,7 +283,7 @@ std::vector<Tensor> anchor_target_fused(const Tensor& base_anchors, int64_t H, i
   mxr::anchor_sample_hist(label_pre.data_ptr<int32_t>(), targets.data_ptr<float>(), keys.data_ptr<float>(),
                           wsp + n_gm, B, A, (int)H, (int)W, (int)num_fg, (int)batch, iwf, (float)pos_weight,
                           wsp + n_gm + n_h, meta.data_ptr<int32_t>(), label.data_ptr<int32_t>(), bt.data_ptr<float>(),
-                          iw.data_ptr<float>(), ow.data_ptr<float>(), cur_stream());
+                          iw.data_ptr<float>(), ow.data_ptr<float>(), cur_stream(), wsp, n_gm + n_h);
   return {label, bt, iw, ow, meta};
 }
 
@@ -1530,7 +1553,7 @@ std::vector<Tensor> proposal_topk(const Tensor& keys, const Tensor& boxes, int64
   TORCH_CHECK(P > 0 && P <= N, "proposal_topk: 0 < P <= N");
   DevGuard g(keys.device());
   auto o = keys.options();
-  Tensor ws = at::zeros({mxr::proposal_topk_ws_words(B, N)}, o.dtype(at::kInt));  // histograms: atomics
+  Tensor ws = clean_ws(o.dtype(at::kInt), "topk", mxr::proposal_topk_ws_words(B, N));  // histograms: atomics
   Tensor wk = at::empty({(int64_t)B * P}, o.dtype(at::kInt));
   Tensor wi = at::empty({(int64_t)B * P}, o.dtype(at::kInt));
   Tensor sk = at::empty({B, P}, o);

@@ -88,13 +88,19 @@ __global__ void __launch_bounds__(256)
 anchor_pass1_kernel(const float* __restrict__ base, int A, int H, int W, float stride,
                     const float* __restrict__ im_info, int border, const float* __restrict__ gt,
                     const int32_t* __restrict__ n_gt, int G, float* __restrict__ max_ov,
-                    int32_t* __restrict__ argmax, float* __restrict__ gt_max) {
+                    int32_t* __restrict__ argmax, float* __restrict__ gt_max, int32_t* __restrict__ zero_ws,
+                    int64_t zero_n) {
   __shared__ float4 sg[kGtTile];
   __shared__ float sa[kGtTile];
   __shared__ int smax[kGtTile];
   const int b = blockIdx.y;
   const int64_t N = (int64_t)H * W * A;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (zero_ws) {  // the sampling chain's mark workspace, consumed by the previous call's output kernel
+    const int64_t nt = (int64_t)gridDim.x * gridDim.y * blockDim.x;
+    for (int64_t i = ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * blockDim.x + threadIdx.x; i < zero_n; i += nt)
+      zero_ws[i] = 0;
+  }
   const int ng = min(n_gt[b], G);
   const float im_h = im_info[b * 3], im_w = im_info[b * 3 + 1];
   float x1 = 0, y1 = 0, x2 = 0, y2 = 0;
@@ -209,12 +215,12 @@ void anchor_target_assign(const float* base_anchors, int A, int H, int W, float 
                           const float* im_info, int allowed_border, const float* gt, const int32_t* n_gt, int G,
                           int B, float neg_thresh, float pos_thresh, int clobber_positives, float* max_ov,
                           int32_t* argmax, float* gt_max, int32_t* label, float* targets, hipStream_t st,
-                          const float* keys, int32_t* hist) {
+                          const float* keys, int32_t* hist, int32_t* zero_ws, int64_t zero_n) {
   const int64_t N = (int64_t)H * W * A;
   if (B == 0 || N == 0) return;
   dim3 grid(div_up(N, 256), B);
   anchor_pass1_kernel<<<grid, 256, 0, st>>>(base_anchors, A, H, W, feat_stride, im_info, allowed_border, gt, n_gt,
-                                            G, max_ov, argmax, gt_max);
+                                            G, max_ov, argmax, gt_max, zero_ws, zero_n);
   anchor_pass2_kernel<<<grid, 256, 0, st>>>(base_anchors, A, H, W, feat_stride, gt, n_gt, G, neg_thresh,
                                             pos_thresh, clobber_positives, max_ov, argmax, gt_max, label, targets,
                                             keys, hist);

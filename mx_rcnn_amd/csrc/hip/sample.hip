@@ -144,8 +144,9 @@ anchor_output_kernel(const int32_t* __restrict__ label_pre, const float* __restr
                      const uint32_t* __restrict__ kept, const int32_t* __restrict__ meta, int B, int A, int HW,
                      float iw0, float iw1, float iw2, float iw3, float pos_weight, int32_t* __restrict__ label,
                      float* __restrict__ bbox_target, float* __restrict__ inside, float* __restrict__ outside,
-                     int64_t kept_stride) {
+                     int64_t kept_stride, int32_t* __restrict__ clean_ws = nullptr, int64_t clean_n = 0) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (int64_t i = t; i < clean_n; i += (int64_t)gridDim.x * blockDim.x) clean_ws[i] = 0;
   const int64_t per = (int64_t)A * HW;
   if (t >= (int64_t)B * per) return;
   const int b = (int)(t / per);
@@ -369,7 +370,7 @@ int64_t anchor_mark_ws_ints(int B, int64_t N) { return (int64_t)B * (div_up(N, 3
 void anchor_sample_hist(const int32_t* label_pre, const float* targets, const float* keys, const int32_t* hist,
                         int B, int A, int H, int W, int num_fg, int batch, const float* inside_w, float pos_weight,
                         int32_t* ws, int32_t* meta, int32_t* label, float* bbox_target, float* inside, float* outside,
-                        hipStream_t st) {
+                        hipStream_t st, int32_t* clean_ws, int64_t clean_n) {
   if (B == 0) return;
   const int N = H * W * A;
   const int NW = (int)div_up(N, 32);
@@ -380,7 +381,7 @@ void anchor_sample_hist(const int32_t* label_pre, const float* targets, const fl
   anchor_output_kernel<<<div_up(total, 256), 256, 0, st>>>(label_pre, targets, reinterpret_cast<const uint32_t*>(ws),
                                                            meta, B, A, H * W, inside_w[0], inside_w[1], inside_w[2],
                                                            inside_w[3], pos_weight, label, bbox_target, inside,
-                                                           outside, per);
+                                                           outside, per, clean_ws, clean_n);
 }
 
 // ------------------------------------------------------------------------------- proposals

@@ -234,6 +234,11 @@ topk_write_kernel(const float* __restrict__ keys, int N, int P, uint32_t* __rest
   __shared__ uint32_t wsum[kTkThreads / 64];
   const int b = blockIdx.y, G = gridDim.x;
   const TkWs w = tk_ws(ws, gridDim.y, G);
+  {  // every histogram reader (the digit passes, the count kernel) is done: leave them zeroed for the
+     // next call (the workspace is persistent and self-cleaning, bindings.cpp clean_ws)
+    uint32_t* hb = w.hist + (int64_t)b * 3 * kTkBins;
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < 3 * kTkBins; i += G * blockDim.x) hb[i] = 0u;
+  }
   const uint32_t* st = w.state + (int64_t)b * 6;
   const uint32_t T = st[4], need = st[5];
   const uint32_t* c = w.cnt + (int64_t)b * G * 3;
@@ -409,7 +414,7 @@ int proposal_topk(const float* keys, const float* boxes, int B, int N, int P, ui
                   int* ws_idx, float* skeys, float* sboxes, int* n_valid, hipStream_t st) {
   if (B <= 0 || N <= 0 || P <= 0 || P > N || B > 65535) return -1;
   const dim3 grid((N + kTkChunk - 1) / kTkChunk, B);
-  // ws: zeroed by the caller (histograms are accumulated with atomics)
+  // ws: histograms zeroed on entry (atomics); the write kernel zeroes them again after use
   topk_hist_kernel<0><<<grid, kTkThreads, 0, st>>>(keys, N, P, ws);
   topk_hist_kernel<1><<<grid, kTkThreads, 0, st>>>(keys, N, P, ws);
   topk_hist_kernel<2><<<grid, kTkThreads, 0, st>>>(keys, N, P, ws);

@@ -58,7 +58,8 @@ void anchor_target_assign(const float* base_anchors, int A, int H, int W, float 
                           float neg_thresh, float pos_thresh, int clobber_positives,
                           float* max_ov, int32_t* argmax, float* gt_max,
                           int32_t* label, float* targets, hipStream_t st, const float* keys = nullptr,
-                          int32_t* hist = nullptr);
+                          int32_t* hist = nullptr, int32_t* zero_ws = nullptr, int64_t zero_n = 0);
+// (zero_ws: [0, zero_n) zeroed by the first kernel -- the self-cleaning sampling workspace, bindings.cpp)
 
 // ---- fused target sampling (sample.hip) ------------------------------------
 // RPN: label_pre (B, N=H*W*A) in (h, w, a) order from anchor_target_assign, targets (B, N, 4), keys
@@ -82,7 +83,9 @@ int64_t anchor_mark_ws_ints(int B, int64_t N);
 void anchor_sample_hist(const int32_t* label_pre, const float* targets, const float* keys, const int32_t* hist,
                         int B, int A, int H, int W, int num_fg, int batch, const float* inside_w, float pos_weight,
                         int32_t* ws, int32_t* meta, int32_t* label, float* bbox_target, float* inside, float* outside,
-                        hipStream_t st);
+                        hipStream_t st, int32_t* clean_ws = nullptr, int64_t clean_n = 0);
+// (clean_ws: [0, clean_n) -- the gt-max / histogram words the earlier kernels consumed -- zeroed by
+// the output kernel, so a persistent workspace is left clean for the next call)
 // R-CNN: rois (B, P, 5), gt (B, G, 5), n_gt (B), max_ov / argmax (B, P) vs gt, rnd (B, 2(P+G)+R).
 // Returns -1 when the shape exceeds the kernel's LDS plan.
 size_t proposal_sample_lds(int P, int G, int R, int F);

@@ -236,3 +236,37 @@ def test_bnb_part_fold_multi_matches_single_folds(cuda):
         assert torch.equal(mb, db)
         if mg is not None:
             assert torch.equal(mg, dg)
+
+
+@pytest.mark.gpu
+def test_self_cleaning_workspaces_repeat(cuda):
+    """The anchor-sampling and proposal top-k workspaces persist across calls and are left zeroed by
+    their own kernel chains (bindings.cpp clean_ws): back-to-back calls with the same draws give the
+    same result five times over, and a different gt count (another workspace) in between changes
+    nothing."""
+    from mx_rcnn_amd.config import snapshot
+    cfg = snapshot()
+    H, W = 38, 50
+    g = torch.Generator().manual_seed(3)
+    gt = torch.full((2, 8, 5), -1.0)
+    xy = torch.rand(2, 5, 2, generator=g) * torch.tensor([W * 16 - 100, H * 16 - 100])
+    gt[:, :5, :2] = xy
+    gt[:, :5, 2:4] = xy + 60 + torch.rand(2, 5, 2, generator=g) * 150
+    gt[:, :5, 4] = 1
+    n_gt = torch.tensor([5, 3], dtype=torch.int32, device=cuda)
+    im_info = torch.tensor([[H * 16.0, W * 16.0, 1.0]] * 2, device=cuda)
+    outs = []
+    for rep in range(5):
+        if rep == 2:  # another workspace size in between
+            ops.anchor_target((H, W), gt[:, :4].to(cuda), n_gt.clamp(max=4), im_info, scales=(4, 8, 16, 32), cfg=cfg)
+        torch.manual_seed(77)
+        outs.append(ops.anchor_target((H, W), gt.to(cuda), n_gt, im_info, scales=(4, 8, 16, 32), cfg=cfg))
+    for o in outs[1:]:
+        for k in ('label', 'bbox_target', 'bbox_inside_weight', 'sample_meta'):
+            assert torch.equal(o[k], outs[0][k]), k
+    cls, dlt = _rpn_inputs(4, 9, H, W, B=2)
+    cl = cls.to(cuda).contiguous(memory_format=torch.channels_last)
+    dl = dlt.to(cuda).contiguous(memory_format=torch.channels_last)
+    res = [_twice(lambda: ops.proposal(cl, dl, im_info, is_train=True, **KW)) for _ in range(3)]
+    for (r1, s1), (r2, s2) in res:
+        assert torch.equal(r1, res[0][0][0]) and torch.equal(r2, res[0][0][0]) and torch.equal(s1, res[0][0][1])

@@ -74,6 +74,7 @@ class _RowCE(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, label, norm, grad_scale):
         lab = label.to(torch.int32).contiguous()
+        ctx.set_materialize_grads(False)  # prob never receives a gradient: no zero fill for it
         if logits.is_cuda:
             ext = need_ext()
             grad, prob, loss = ext.row_softmax_ce(logits.contiguous(), lab, float(norm), float(grad_scale), True)
@@ -98,6 +99,8 @@ class _RowCE(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g, gprob):
+        if g is None:
+            return None, None, None, None
         (grad,) = ctx.saved_tensors
         return _scale_grad(grad, g), None, None, None
 
@@ -167,10 +170,13 @@ class _Combine(torch.autograd.Function):
             if nonfinite is not None:
                 nonfinite.add_((~torch.isfinite(obj)).to(nonfinite.dtype))
         ctx.mark_non_differentiable(obj)
+        ctx.set_materialize_grads(False)  # no zero-filled gradient for the objective output
         return total.reshape(()), obj.reshape(())
 
     @staticmethod
     def backward(ctx, g, _gobj):
+        if g is None:
+            return (None, None) + (None,) * ctx.n
         return (None, None) + (g,) * ctx.n
 
 

@@ -14,7 +14,7 @@ from collections import defaultdict
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('dir')
-    ap.add_argument('--match', default='conv_igemm_buf_kernel,conv_x2w_kernel')
+    ap.add_argument('--match', default='conv_igemm_buf_kernel,conv_x2w_kernel,conv_dgrad_wgrad_kernel,conv_igemm_kg_kernel,conv_wgrad_buf_kernel')
     ap.add_argument('--label', default='')
     a = ap.parse_args()
     files = glob.glob(os.path.join(a.dir, '**', '*counter_collection.csv'), recursive=True)
@@ -43,6 +43,10 @@ def main():
             out['l2_hit_rate'] = round(hit / (hit + miss), 4)
         if c.get('SQ_WAVE_CYCLES'):
             out['wait_frac'] = round(c.get('SQ_WAIT_ANY', 0.0) / c['SQ_WAVE_CYCLES'], 4)
+        if c.get('SQ_VALU_MFMA_BUSY_CYCLES') is not None and c.get('GRBM_GUI_ACTIVE'):
+            # MFMA-pipe busy cycles summed over the 1024 SIMDs, against the kernel's active cycles
+            # (GRBM_GUI_ACTIVE is summed over the 8 XCDs): the fraction of the matrix-core peak in use
+            out['mfma_util'] = round(c['SQ_VALU_MFMA_BUSY_CYCLES'] / (c['GRBM_GUI_ACTIVE'] / 8.0 * 1024), 4)
         print(json.dumps(out))
 
 

@@ -34,7 +34,7 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr uint32_t kOOB = 0x80000000u;
 constexpr int BK = 32;       // channels per K tile
-constexpr int NBUF4 = 4;     // K tiles resident in LDS (3 in flight); the *_3 tiles keep 3 (2 in flight)
+constexpr int NBUF = 4;      // K tiles resident in LDS (3 in flight)
 
 template <int N>
 __device__ __forceinline__ void vm_wait() {
@@ -73,7 +73,7 @@ struct BigCfg {
 // itself): referenced directly, hipcc's wait-count pass drained every in-flight LDS-DMA
 // (s_waitcnt vmcnt(0)) before the fragment reads of each K tile -- the same effect the buffer
 // kernel documents for a __restrict__ ring (conv_igemm.hip).
-template <int BM_, int BN, bool F16, int NBUF>
+template <int BM_, int BN, bool F16>
 __device__ __forceinline__ void conv_big_body(uint16_t* lds, const uint16_t* __restrict__ x,
                                               const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int NB, int H,
                                               int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride,
@@ -165,8 +165,8 @@ __device__ __forceinline__ void conv_big_body(uint16_t* lds, const uint16_t* __r
   for (int kt = 0; kt < nk; ++kt) {
     // K tile kt landed: at most min(2, nk-1-kt) younger tiles of this thread still in flight
     const int ahead = min(NBUF - 2, nk - 1 - kt);
-    if (NBUF >= 4 && ahead >= 2) vm_wait<2 * C::LPT>();
-    else if (ahead >= 1) vm_wait<C::LPT>();
+    if (ahead >= 2) vm_wait<2 * C::LPT>();
+    else if (ahead == 1) vm_wait<C::LPT>();
     else vm_wait<0>();
     __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt landed; tile kt-1's buffer is free
     if (kt + NBUF - 1 < nk) issue((kt + NBUF - 1) % NBUF);
@@ -253,27 +253,25 @@ __device__ __forceinline__ void conv_big_body(uint16_t* lds, const uint16_t* __r
   }
 }
 
-template <int BM, int BN, bool F16, int NBUF>
+template <int BM, int BN, bool F16>
 __global__ void __launch_bounds__(512)
 conv_big_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int NB,
                 int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, const ConvEpi ep,
                 int tiles_n, int nwg) {
   // one LDS array (a second __shared__ object can make hipcc drain the DMA ring before each read)
   __shared__ __attribute__((aligned(16))) uint16_t lds[NBUF * BigCfg<BM, BN>::ROWS * BK];
-  conv_big_body<BM, BN, F16, NBUF>(lds, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, tiles_n, nwg);
+  conv_big_body<BM, BN, F16>(lds, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, tiles_n, nwg);
 }
 
 }  // namespace
 
-// tile codes 200 (256x256) / 201 (256x128) / 202 (128x128) / 203 (128x256); 204 / 205: 256x128 /
-// 128x256 with a 3-deep ring (72 KB: two workgroups per CU, so a grid of ~1 tile per CU -- N = 256
-// at batch 8: 264 tiles -- runs in one round instead of leaving the surplus tiles for a second);
-// -1 when the shape or epilogue is not supported.  The 128-row tiles serve N = 256 GEMMs of a few tens of thousands of
+// tile codes 200 (256x256) / 201 (256x128) / 202 (128x128) / 203 (128x256); -1 when the shape or
+// epilogue is not supported.  The 128-row tiles serve N = 256 GEMMs of a few tens of thousands of
 // rows (the batch-8 stage-3 reduce / 3x3 convs: 75 workgroups of 256x256 leave 181 of 256 CUs
 // idle; 128x128 gives 300, two resident per CU with the 64 KB ring)
 int conv_big_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho, int Wo,
                  int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int tile, hipStream_t st) {
-  if (tile < 200 || tile > 205) return -1;
+  if (tile < 200 || tile > 203) return -1;
   if (Cin % BK != 0 || Cout % 16 != 0 || KH * KW > 64) return -1;
   if (ep.x2 || ep.yf || ep.bt || ep.omap || ep.pad_w >= 0 || ep.bnb_x || ep.st_part || ep.bnb_part || ep.rmask ||
       ep.drop_p > 0.f)
@@ -281,27 +279,25 @@ int conv_big_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int 
   if ((ep.y2) && (!ep.bn_beta || !ep.bn_mean || !ep.bn_var || (!ep.bn_fix_gamma && !ep.bn_gamma))) return -1;
   if ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kOOB || (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kOOB) return -1;
   const int M = NB * Ho * Wo;
-  const int bm = (tile == 202 || tile == 203 || tile == 205) ? 128 : 256;
-  const int bn = (tile == 200 || tile == 203 || tile == 205) ? 256 : 128;
+  const int bm = tile >= 202 ? 128 : 256;
+  const int bn = (tile == 200 || tile == 203) ? 256 : 128;
   const int tiles_n = (Cout + bn - 1) / bn;
   const int nwg = ((M + bm - 1) / bm) * tiles_n;
-#define MXR_BIG(BM_, BN_, F_, NB_)                                                                         \
-  conv_big_kernel<BM_, BN_, F_, NB_><<<nwg, 512, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, \
-                                                         pad, ep, tiles_n, nwg)
-#define MXR_BIG2(BM_, BN_, NB_)      \
-  do {                               \
-    if (ep.f16)                      \
-      MXR_BIG(BM_, BN_, true, NB_);  \
-    else                             \
-      MXR_BIG(BM_, BN_, false, NB_); \
+#define MXR_BIG(BM_, BN_, F_)                                                                                 \
+  conv_big_kernel<BM_, BN_, F_><<<nwg, 512, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, \
+                                                    ep, tiles_n, nwg)
+#define MXR_BIG2(BM_, BN_)      \
+  do {                          \
+    if (ep.f16)                 \
+      MXR_BIG(BM_, BN_, true);  \
+    else                        \
+      MXR_BIG(BM_, BN_, false); \
   } while (0)
   switch (tile) {
-    case 200: MXR_BIG2(256, 256, NBUF4); break;
-    case 201: MXR_BIG2(256, 128, NBUF4); break;
-    case 202: MXR_BIG2(128, 128, NBUF4); break;
-    case 203: MXR_BIG2(128, 256, NBUF4); break;
-    case 204: MXR_BIG2(256, 128, 3); break;
-    default: MXR_BIG2(128, 256, 3); break;
+    case 200: MXR_BIG2(256, 256); break;
+    case 201: MXR_BIG2(256, 128); break;
+    case 202: MXR_BIG2(128, 128); break;
+    default: MXR_BIG2(128, 256); break;
   }
 #undef MXR_BIG2
 #undef MXR_BIG

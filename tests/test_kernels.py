@@ -351,7 +351,7 @@ def test_conv_igemm_fwd_vs_fp32(cuda, shape):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize('tile', [200, 201, 202, 203, 204, 205])
+@pytest.mark.parametrize('tile', [200, 201, 202, 203])
 def test_conv_big_epilogue_vs_fp32(cuda, dtype, tile):
     """The 256-row large-tile kernel (conv_big.hip) with its full epilogue -- bias, residual, ReLU and
     the frozen BN + ReLU second output -- against the fp32 reference of the same 16-bit operands;

@@ -428,19 +428,6 @@ conv_igemm_buf_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
 // leaves its fp32 partial + a flag; the workgroup that runs the rest (TAIL) adds it in a fixed order
 // (deterministic) and runs the fused epilogue once.  The flag is reset by its consumer, so the
 // persistent workspace is clean for the next launch / graph replay.
-// one stream-K segment as an out-of-line function: inlined into the segment loop, the body's
-// kernel-argument values stayed live across iterations in SGPRs (~150 spills, ~2400 reloads in the
-// main loop); called, it allocates like the one-tile kernel
-template <int S, bool X2, bool X3>
-__device__ __attribute__((noinline)) void igemm_sk_segment(uint16_t* lds, int bid, const uint16_t* __restrict__ x,
-                                                           const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
-                                                           int NB, int H, int W, int Cin, int Ho, int Wo, int Cout,
-                                                           int KH, int KW, int stride, int pad, const ConvEpi& ep,
-                                                           int tiles_n, int nwg, int ntiles, const SkSeg sk) {
-  igemm_buf_body<64, 64, S, false, X2, false, 1, X3>(lds, bid, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
-                                                     pad, ep, tiles_n, nwg, ntiles, 1, nullptr, sk);
-}
-
 template <int S, bool X2, bool X3>
 __global__ void __launch_bounds__(256)
 conv_igemm_sk_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int NB,
@@ -454,39 +441,33 @@ conv_igemm_sk_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict_
   const int64_t total = (int64_t)ntiles * nk_tile;
   const int64_t g0 = min(total, (int64_t)rank * per_wg), g1 = min(total, g0 + per_wg);
   if (g0 >= g1) return;  // (uniform)
-  // segments, one body call site (a second inlined copy of the body doubled the SGPR pressure:
-  // ~2400 spill reloads in the main loop): the HEAD of the tile the range ends in, if the range
-  // starts it, FIRST (the neighbour's TAIL waits for it); then a TAIL (the range starts inside a
-  // tile) and whole tiles
+  SkSeg sk;
+  sk.part = part;
+  sk.flag = flag;
+  int64_t end = g1;
   const int tl = (int)((g1 - 1) / nk_tile);
   const int64_t tl0 = (int64_t)tl * nk_tile;
-  bool head = g1 < tl0 + nk_tile && tl0 >= g0;
-  const int64_t end = head ? tl0 : g1;
-  int64_t g = g0;
-  for (;;) {  // (uniform: every segment boundary is a function of the rank)
-    SkSeg sk;
-    sk.part = part;
-    sk.flag = flag;
-    if (head) {
-      sk.mode = 1;
-      sk.tile = tl;
-      sk.kbeg = 0;
-      sk.nk = (int)(g1 - tl0);
-      head = false;
-    } else if (g < end) {
-      const int t = (int)(g / nk_tile);
-      const int64_t t0 = (int64_t)t * nk_tile, e = min(end, t0 + nk_tile);
-      sk.mode = g > t0 ? 2 : 0;
-      sk.tile = t;
-      sk.kbeg = (int)(g - t0);
-      sk.nk = (int)(e - g);
-      g = e;
-    } else {
-      break;
-    }
-    igemm_sk_segment<S, X2, X3>(lds, bid, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, tiles_n, nwg,
-                                ntiles, sk);
+  if (g1 < tl0 + nk_tile && tl0 >= g0) {  // the range ends inside a tile it starts: that tile's HEAD, first
+    sk.mode = 1;
+    sk.tile = tl;
+    sk.kbeg = 0;
+    sk.nk = (int)(g1 - tl0);
+    igemm_buf_body<64, 64, S, false, X2, false, 1, X3>(lds, bid, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
+                                                       pad, ep, tiles_n, nwg, ntiles, 1, nullptr, sk);
     __syncthreads();  // every wave is done with the ring before the next segment's prologue
+    end = tl0;
+  }
+  for (int64_t g = g0; g < end;) {  // then a TAIL (the range starts inside a tile) and whole tiles
+    const int t = (int)(g / nk_tile);
+    const int64_t t0 = (int64_t)t * nk_tile, e = min(end, t0 + nk_tile);
+    sk.mode = g > t0 ? 2 : 0;
+    sk.tile = t;
+    sk.kbeg = (int)(g - t0);
+    sk.nk = (int)(e - g);
+    igemm_buf_body<64, 64, S, false, X2, false, 1, X3>(lds, bid, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
+                                                       pad, ep, tiles_n, nwg, ntiles, 1, nullptr, sk);
+    __syncthreads();
+    g = e;
   }
 }
 

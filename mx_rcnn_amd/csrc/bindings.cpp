@@ -1035,13 +1035,6 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
       // A/B candidate only (MXR_X2W=1): 13-26 % faster in isolation on the stage-3/4 and RPN convs,
       // but the headline step measured 1 % slower with it in the autotune (same-box interleaved)
       if (ep.x2 && getenv("MXR_X2W") != nullptr) cands.push_back({26, 1});
-      // stream-K 64x64 (tile 40) when the 64x64 grid is a little over the CU count (batch-1 stage 3:
-      // 264 tiles / 1056 tiles on 256 CUs): equal (tile, K) shares instead of a partial last round
-      {
-        const int64_t t64 = ((int64_t)NB * Ho * Wo + 63) / 64 * ((Cout + 63) / 64);
-        if (!ep.bt && !f16 && Cout % 8 == 0 && t64 > 256 && t64 % 256 != 0 && getenv("MXR_NO_SK") == nullptr)
-          cands.push_back({40, 1});
-      }
       // large grids: the 256-row tiles of conv_big.hip (512 threads, 4-tile LDS ring)
       if ((int64_t)NB * Ho * Wo >= 16384 && !ep.x2 && getenv("MXR_NO_BIG") == nullptr)
         for (int c : {200, 201, 202, 203}) cands.push_back({c, 1});
@@ -1091,9 +1084,6 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
         // deterministic BN-backward sums: 64-row tiles, whole K (the partial rows are per 64 rows)
         if (ep.bnb_part && (c.second != 1 || c.first < 21 || mxr::conv_tile_bm(c.first) != 64)) continue;
         float* sl = c.second > 1 ? slab_t.data_ptr<float>() : nullptr;
-        if (c.first == 40)  // stream-K: the persistent partial / flag workspace
-          sl = reinterpret_cast<float*>(
-              clean_ws(x.options().dtype(at::kInt), "sk", mxr::conv_sk_ws_ints(NB * Ho * Wo, Cout)).data_ptr<int32_t>());
         auto run = [&]() {
           return mxr::conv_igemm_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                                      reinterpret_cast<const uint16_t*>(w.data_ptr()),
@@ -1129,14 +1119,11 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
   }
   Tensor slab;
   if (sp > 1) slab = at::empty({(int64_t)sp * NB * Ho * Wo * Cout}, x.options().dtype(at::kFloat));
-  float* slab_p = sp > 1 ? slab.data_ptr<float>() : nullptr;
-  if (t == 40)  // stream-K: persistent partial / flag workspace (self-cleaning flags)
-    slab_p = reinterpret_cast<float*>(
-        clean_ws(x.options().dtype(at::kInt), "sk", mxr::conv_sk_ws_ints(NB * Ho * Wo, Cout)).data_ptr<int32_t>());
   int used = mxr::conv_igemm_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                                  reinterpret_cast<const uint16_t*>(w.data_ptr()),
                                  out_f32 ? nullptr : reinterpret_cast<uint16_t*>(y.data_ptr()), NB, H, W, Cin, Ho, Wo,
-                                 Cout, KH, KW, (int)stride, (int)pad, ep, t, sp, slab_p, cur_stream());
+                                 Cout, KH, KW, (int)stride, (int)pad, ep, t, sp,
+                                 sp > 1 ? slab.data_ptr<float>() : nullptr, cur_stream());
   if (used <= 0 && tile <= 0 && t != 23 && !(sp > 1)) {  // a cached choice this epilogue cannot take: the plan tile
     used = mxr::conv_igemm_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()),
                                reinterpret_cast<const uint16_t*>(w.data_ptr()),

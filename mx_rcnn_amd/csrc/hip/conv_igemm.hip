@@ -418,97 +418,6 @@ conv_igemm_buf_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict
                                                 pad, ep, tiles_n, nwg, ntiles, splits, slab);
 }
 
-// ---- stream-K launch of the 64x64 buffer kernel (tile code 40) ---------------------------------
-// A batch-1 stage-3 GEMM has M = 4200 rows: 264 64x64 tiles for N = 256 (1056 for N = 1024) on 256
-// CUs, so 8 (32) CUs carry one tile more than the rest and the launch waits for them -- measured:
-// the 3x3 at 264 tiles takes 55.8 us where 256 tiles take 45.5 (fp32 triples; bf16 21.5 vs 19.0;
-// tools/microbench/conv_x3_tiles.py, shapes s3_*_sq).  Here the grid is min(tiles, CUs) workgroups
-// and each runs an equal share of the launch's (tile, K step) iterations: whole tiles, plus at most
-// one tile split with a neighbour.  A split tile's first part (HEAD) runs first in its workgroup and
-// leaves its fp32 partial + a flag; the workgroup that runs the rest (TAIL) adds it in a fixed order
-// (deterministic) and runs the fused epilogue once.  The flag is reset by its consumer, so the
-// persistent workspace is clean for the next launch / graph replay.
-template <int S, bool X2, bool X3>
-__global__ void __launch_bounds__(256)
-conv_igemm_sk_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int NB,
-                     int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad,
-                     const ConvEpi ep, int tiles_n, int ntiles, int nk_tile, int per_wg, float* __restrict__ part,
-                     int* __restrict__ flag) {
-  __shared__ __attribute__((aligned(16))) uint16_t lds[S * igemm_ring_stage<64, 64, false, X3>()];
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int q = nwg / 8, r8 = nwg % 8, xcd = bid % 8;  // XCD-aware rank: neighbouring ranks share A panels
-  const int rank = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + bid / 8;
-  const int64_t total = (int64_t)ntiles * nk_tile;
-  const int64_t g0 = min(total, (int64_t)rank * per_wg), g1 = min(total, g0 + per_wg);
-  if (g0 >= g1) return;  // (uniform)
-  SkSeg sk;
-  sk.part = part;
-  sk.flag = flag;
-  int64_t end = g1;
-  const int tl = (int)((g1 - 1) / nk_tile);
-  const int64_t tl0 = (int64_t)tl * nk_tile;
-  if (g1 < tl0 + nk_tile && tl0 >= g0) {  // the range ends inside a tile it starts: that tile's HEAD, first
-    sk.mode = 1;
-    sk.tile = tl;
-    sk.kbeg = 0;
-    sk.nk = (int)(g1 - tl0);
-    igemm_buf_body<64, 64, S, false, X2, false, 1, X3>(lds, bid, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
-                                                       pad, ep, tiles_n, nwg, ntiles, 1, nullptr, sk);
-    __syncthreads();  // every wave is done with the ring before the next segment's prologue
-    end = tl0;
-  }
-  for (int64_t g = g0; g < end;) {  // then a TAIL (the range starts inside a tile) and whole tiles
-    const int t = (int)(g / nk_tile);
-    const int64_t t0 = (int64_t)t * nk_tile, e = min(end, t0 + nk_tile);
-    sk.mode = g > t0 ? 2 : 0;
-    sk.tile = t;
-    sk.kbeg = (int)(g - t0);
-    sk.nk = (int)(e - g);
-    igemm_buf_body<64, 64, S, false, X2, false, 1, X3>(lds, bid, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride,
-                                                       pad, ep, tiles_n, nwg, ntiles, 1, nullptr, sk);
-    __syncthreads();
-    g = e;
-  }
-}
-
-int64_t conv_sk_ws_ints(int M, int Cout) {
-  const int64_t ntiles = (int64_t)((M + 63) / 64) * ((Cout + 63) / 64);
-  return ntiles * 64 * 64 + ntiles;  // fp32 partial per tile + a flag per tile
-}
-
-static int launch_sk(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho, int Wo,
-                     int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, float* ws, hipStream_t st) {
-  const int M = NB * Ho * Wo;
-  const int tiles_n = (Cout + 63) / 64, ntiles = ((M + 63) / 64) * tiles_n;
-  const int KC = ep.x2 ? BK / 2 : BK;
-  const int nk = KH * KW * (Cin / KC);
-  int ncu = 256;
-  {
-    static int cached = 0;
-    if (!cached) {
-      int dev = 0;
-      hipDeviceProp_t prop;
-      if (hipGetDevice(&dev) == hipSuccess && hipGetDeviceProperties(&prop, dev) == hipSuccess)
-        cached = prop.multiProcessorCount;
-      if (cached <= 0) cached = 256;
-    }
-    ncu = cached;
-  }
-  if (ntiles <= ncu || nk < 2 || ws == nullptr) return -1;
-  const int nwg = ncu;
-  const int per_wg = (int)(((int64_t)ntiles * nk + nwg - 1) / nwg);  // >= nk since ntiles > nwg
-  float* part = ws;
-  int* flag = reinterpret_cast<int*>(ws + (int64_t)ntiles * 64 * 64);
-#define MXR_SK(X2_, X3_)                                                                                       \
-  conv_igemm_sk_kernel<3, X2_, X3_><<<nwg, 256, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, \
-                                                        tiles_n, ntiles, nk, per_wg, part, flag)
-  if (ep.x3) MXR_SK(true, true);
-  else if (ep.x2) MXR_SK(true, false);
-  else MXR_SK(false, false);
-#undef MXR_SK
-  return 40;
-}
-
 // ---- fp32-class pairs, wide stages (tile code 26) ---------------------------------------------
 // The x2 buffer kernel above stages 32 channels of both planes per K step (128-B LDS rows): a
 // stage-3 conv at batch 1 then runs 32-72 barrier-separated steps of 16 KB, and the per-step DMA
@@ -1159,17 +1068,6 @@ int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, in
     return -1;
   if (ep.y2 && ep.bnb_x) return -1;
   if (ep.rmask && (ep.bnb_x || ep.y2 || ep.f16)) return -1;
-  if (tile == 40) {  // stream-K 64x64 (slab: the persistent workspace of conv_sk_ws_ints)
-    if (splits > 1 || ep.bt || ep.f16 || ep.omap || ep.pad_w >= 0 || ep.yf ||
-        Cout % 8 != 0 || KH * KW > 64)
-      return -1;
-    if ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kBufOOB || (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kBufOOB)
-      return -1;
-    if (ep.x2 && ((int64_t)NB * H * W * Cin * 2 + (ep.x3 ? 2 : 1) * (int64_t)ep.x2_pa >= (int64_t)kBufOOB ||
-                  (int64_t)Cout * KH * KW * Cin * 2 + (ep.x3 ? 2 : 1) * (int64_t)ep.x2_pb >= (int64_t)kBufOOB))
-      return -1;
-    return launch_sk(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, slab, st);
-  }
   const bool kgt = tile >= 27 && tile <= 29;  // K-group tiles (conv_kg.hip)
   if ((ep.omap || ep.pad_w >= 0) && (splits > 1 || !(tile == 22 || tile == 23 || tile == 30 || tile >= 100 || kgt))) return -1;
   if (ep.f16 && !(tile == 21 || tile == 22 || tile == 23 || tile == 30 || tile >= 100)) return -1;

@@ -536,23 +536,12 @@ constexpr int igemm_ring_stage() {  // LDS elements of one ring stage
   return (BM + BN) * 64 + (X3 ? BM * 32 + (BT ? 32 * 64 : BN * 32) : 0);
 }
 
-// Stream-K segment (conv_igemm_sk_kernel): this workgroup runs K steps [kbeg, kbeg + nk) of tile
-// `tile`.  mode 0: the whole tile (normal epilogue); 1 (HEAD): the first part of a tile whose rest
-// another workgroup runs -- the fp32 partial goes to part[tile] and flag[tile] is raised, no
-// epilogue; 2 (TAIL): the last part -- wait for flag[tile], add part[tile] (a fixed order: the
-// result is run-to-run deterministic), reset the flag, epilogue.  mode -1: not stream-K.
-struct SkSeg {
-  int mode = -1, tile = 0, kbeg = 0, nk = 0;
-  float* part = nullptr;
-  int* flag = nullptr;
-};
-
 template <int BM, int BN, int S, bool F16 = false, bool X2 = false, bool BT = false, int KG = 1, bool X3 = false>
 __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uint16_t* __restrict__ x,
                                                const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int NB, int H,
                                                int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride,
                                                int pad, const ConvEpi& ep, int tiles_n, int nwg, int ntiles, int splits,
-                                               float* __restrict__ slab, const SkSeg sk = SkSeg()) {
+                                               float* __restrict__ slab) {
   constexpr int WM = BM / 2, WN = BN / 2;
   constexpr int TM = WM / 16, TN = WN / 16;
   constexpr int ACH = BM / 32, BCH = BN / 32;
@@ -570,7 +559,7 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
 
   const int q = nwg / 8, r8 = nwg % 8, xcd = bid % 8;
   const int wgid = (xcd < r8 ? xcd * (q + 1) : r8 * (q + 1) + (xcd - r8) * q) + bid / 8;
-  const int split = sk.mode >= 0 ? 0 : wgid / ntiles, tile = sk.mode >= 0 ? sk.tile : wgid % ntiles;
+  const int split = wgid / ntiles, tile = wgid % ntiles;
   const int tm_idx = tile / tiles_n, tn_idx = tile % tiles_n;
   const int m0 = tm_idx * BM, n0 = tn_idx * BN;
   const int M = NB * Ho * Wo;
@@ -674,8 +663,8 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
   const int nk1 = KH * KW * cin_steps;              // K steps of one pass
   const int nk_all = X2 && !X3 && ep.x3 ? 2 * nk1 : nk1;  // two-phase x3: (hi, lo), then (mid, hi)
   const int per = (nk_all + splits - 1) / splits;
-  const int ks0 = sk.mode >= 0 ? sk.kbeg : split * per;
-  const int nk_sp = sk.mode >= 0 ? sk.nk : max(0, min(nk_all, ks0 + per) - ks0);  // this split's K steps
+  const int ks0 = split * per;
+  const int nk_sp = max(0, min(nk_all, ks0 + per) - ks0);  // this split's K steps
   // K group kgi: a contiguous 1/KG of them (x3 with KG = 2 and no split: exactly one phase each);
   // every group runs n_iter barrier rounds, idle in the rounds past its own nk
   const int per_g = (nk_sp + KG - 1) / KG;
@@ -921,37 +910,6 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
     }
   }
   static_assert(BM * (BN + 4) * 4 <= S * (BM + BN) * BK * 2, "epilogue tile must fit the operand ring");
-  if (sk.mode >= 1) {
-    // stream-K partial tile: the same (wave, lane) owns the same fragments in both workgroups of a
-    // tile, so the partial travels as each lane's raw accumulators (16-B stores / loads)
-    f32x4* pt = reinterpret_cast<f32x4*>(sk.part) + ((int64_t)tile * 4 + wid) * (TM * TN * 64);
-    if (sk.mode == 1) {
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) pt[(i * TN + j) * 64 + lane] = acc[i][j];
-      __threadfence();
-      __syncthreads();  // every wave's partial is stored and fenced
-      if (tid == 0) __hip_atomic_store(sk.flag + tile, 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-      return;
-    }
-    if (tid == 0) {
-      // the HEAD runs first thing in its workgroup (conv_igemm_sk_kernel), so this wait is short;
-      // bounded so a broken invariant cannot hang the GPU (the tile is then wrong, not stuck)
-      for (int it = 0; it < (1 << 24) &&
-                       __hip_atomic_load(sk.flag + tile, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) == 0; ++it)
-        __builtin_amdgcn_s_sleep(2);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-        const f32x4 v = __builtin_nontemporal_load(pt + (i * TN + j) * 64 + lane);
-        acc[i][j] += v;
-      }
-    if (tid == 0) __hip_atomic_store(sk.flag + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
-  }
   if constexpr (KG > 1) {  // (the launcher guarantees Cout % 8 == 0)
     igemm_epilogue_lds<BM, BN, TM, TN, WM, WN, X2, KG>(acc, reinterpret_cast<float*>(lds), m0, n0, wm, wn, lane,
                                                        tid, M, Cout, ep, y, split, splits, slab, Ho, Wo);

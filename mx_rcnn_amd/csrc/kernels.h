@@ -298,9 +298,6 @@ int conv_igemm_kg(int tile, const uint16_t* x, const uint16_t* w, uint16_t* y, i
 // epilogues (bias, residual, ReLU, frozen-BN second output); -1 when unsupported
 int conv_big_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho, int Wo,
                  int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int tile, hipStream_t st);
-// tile 40 (stream-K 64x64) takes `slab` = a zeroed persistent workspace of this many int32 words
-// (fp32 partial tiles + per-tile flags, left clean by the kernel)
-int64_t conv_sk_ws_ints(int M, int Cout);
 int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho, int Wo,
                    int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int tile, int splits, float* slab,
                    hipStream_t st);

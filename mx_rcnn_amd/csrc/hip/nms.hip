@@ -26,6 +26,28 @@
 // The kept list lives in LDS; the kernel writes the final (post, 5) RoI block directly,
 // including the reference's random pad (slot >= n_keep takes keep[floor(u*n_keep)]).  Early
 // exit once `post` boxes are kept.  No host synchronisation anywhere.
+//   That reducer streams the whole 9 MB triangle (P = 12000) through one CU at that CU's share of
+//   the memory bandwidth (~270 us); it stays as the MXR_NMS_SERIAL=1 path.
+// Stage 2, default (nms_reduce_mc): a chain of workgroups, one per 16 column blocks, so the
+// triangle is read by ceil(nb / 16) CUs and only the 64-box resolve stays serial:
+//   phase A  every wave owns one column block c of its workgroup and folds the kept rows r < lo
+//            (published by earlier workgroups) into its removed word, polling the per-block
+//            records 16 rows at a time; the mask words of a chunk are loaded before its poll;
+//   phase B  wave 0 resolves the workgroup's own blocks in order from LDS only (the 16x16 own
+//            triangle of mask words is staged there during phase A), publishing each block's
+//            kept word and running count as it goes -- no barrier, no global round trip inside;
+//   the workgroup that resolves the last needed block (count reaches `post`, or the last valid
+//   block) assembles the output from the kept words it holds in LDS.
+// A published record is two 64-bit words {kept lo/hi 32 bits | (count + 1) << 32}: each word is
+// stored and loaded whole (relaxed, agent scope), a nonzero upper half means "written", so a
+// reader never needs an ordering fence between the two.  The records are zeroed by nms_mask and
+// again by the last workgroup to finish (a per-image exit counter), so a mask buffer may be
+// reduced more than once.  A workgroup only ever waits for lower-numbered workgroups of its image,
+// which are dispatched before it, and every poll gives up after NMSC_SPIN empty rounds (the
+// output then reports n_keep = -1) -- the kernel always drains.
+#include <algorithm>
+#include <cstdlib>
+
 #include "common.h"
 #include "../kernels.h"
 
@@ -43,10 +65,36 @@ __host__ __device__ __forceinline__ int64_t nms_row_words(int nb) { return (int6
 // index of lane l's word of column block cb within a row block
 __device__ __forceinline__ int64_t nms_col(int cb, int l) { return (int64_t)(cb >> 1) * 128 + l * 2 + (cb & 1); }
 
+// iou_plus1(a, b) > t -- the same decision bit for bit (fp32 division, round to nearest) -- with the
+// division only on near-threshold pairs.  d = inter - t * uni, a = fma(-t, uni, inter) = RN(d):
+//   a <= 0             -> d <= 0 (or a positive d below the smallest float) -> RN(inter/uni) <= t;
+//   a > ulp(t) * uni   -> d > ulp(t) * uni / (1 + 2^-24) > ulp(t) / 2 * uni  -> inter/uni lies above
+//                         the midpoint of t and its successor -> RN(inter/uni) > t;
+// ulp(t) is a power of two, so ulp(t) * uni is exact.  The band between, a union below 1 and any
+// non-finite value take the division.
+__device__ __forceinline__ bool iou_gt_plus1(float ax1, float ay1, float ax2, float ay2, float aarea, float bx1,
+                                             float by1, float bx2, float by2, float barea, float t, float ulp_t) {
+  const float iw = fminf(ax2, bx2) - fmaxf(ax1, bx1) + 1.f;
+  const float ih = fminf(ay2, by2) - fmaxf(ay1, by1) + 1.f;
+  if (iw <= 0.f || ih <= 0.f) return 0.f > t;
+  const float inter = iw * ih;
+  const float uni = aarea + barea - inter;
+  if (uni >= 1.f && uni < INFINITY && inter < INFINITY) {
+    const float a = __builtin_fmaf(-t, uni, inter);
+    if (a <= 0.f) return false;
+    if (a > ulp_t * uni) return true;
+  }
+  return inter / uni > t;
+}
+
 __global__ void __launch_bounds__(256)
 nms_mask_kernel(const float* __restrict__ boxes, const int32_t* __restrict__ n_valid, int P, int nb,
-                float thresh, uint64_t* __restrict__ maskT) {
+                float thresh, uint64_t* __restrict__ maskT, uint64_t* __restrict__ rec) {
   const int rb = blockIdx.y, b = blockIdx.z;
+  if (blockIdx.x == 0) {  // clear the multi-workgroup reducer's block records and exit counter
+    if (threadIdx.x < 2) rec[((int64_t)b * nb + rb) * 2 + threadIdx.x] = 0ull;
+    if (rb == 0 && threadIdx.x == 2) rec[(int64_t)gridDim.z * nb * 2 + b] = 0ull;
+  }
   if (blockIdx.x * 4 + 3 < rb) return;  // whole group below the diagonal
   const int cb = blockIdx.x * 4 + (threadIdx.x >> 6);
   const int lane = threadIdx.x & 63;
@@ -69,13 +117,42 @@ nms_mask_kernel(const float* __restrict__ boxes, const int32_t* __restrict__ n_v
   if (j < nv) {
     const float4 c = bx[j];
     const float carea = (c.z - c.x + 1.f) * (c.w - c.y + 1.f);
+    const float ulp_t = nextafterf(thresh, INFINITY) - thresh;
     const int iend = min(64, j - row0);  // rows i with row0 + i < j (all < nv since j < nv)
     for (int i = 0; i < iend; ++i) {
       const float4 r = rbox[i];
-      if (iou_plus1(r.x, r.y, r.z, r.w, rarea[i], c.x, c.y, c.z, c.w, carea) > thresh) bits |= (1ull << i);
+      if (iou_gt_plus1(r.x, r.y, r.z, r.w, rarea[i], c.x, c.y, c.z, c.w, carea, thresh, ulp_t)) bits |= (1ull << i);
     }
   }
   maskT[((int64_t)b * nb + rb) * Pp + nms_col(cb, lane)] = bits;
+}
+
+// Output assembly shared by both reducers (the whole workgroup; keep_list holds nk entries and is
+// visible to every thread): slot s < nk takes keep[s], later slots the reference's random pad.
+__device__ __forceinline__ void nms_write_out(const float* __restrict__ boxes, const float* __restrict__ scores, int b,
+                                              int P, int post, int nk, const int32_t* keep_list,
+                                              const float* __restrict__ rand_u, float* __restrict__ rois,
+                                              float* __restrict__ out_scores, int64_t* __restrict__ keep_idx,
+                                              int32_t* __restrict__ n_keep_out) {
+  if (threadIdx.x == 0) n_keep_out[b] = nk;
+  const float4* bx = reinterpret_cast<const float4*>(boxes) + (int64_t)b * P;
+  for (int s = threadIdx.x; s < post; s += blockDim.x) {
+    int idx;
+    if (s < nk) {
+      idx = keep_list[s];
+    } else if (nk > 0) {
+      int r = (int)(rand_u[(int64_t)b * post + s] * nk);
+      idx = keep_list[min(max(r, 0), nk - 1)];
+    } else {
+      idx = 0;
+    }
+    idx = min(max(idx, 0), P - 1);  // never read outside the image's box block
+    const float4 bb = bx[idx];
+    float* ro = rois + ((int64_t)b * post + s) * 5;
+    ro[0] = (float)b; ro[1] = bb.x; ro[2] = bb.y; ro[3] = bb.z; ro[4] = bb.w;
+    out_scores[(int64_t)b * post + s] = scores[(int64_t)b * P + idx];
+    keep_idx[(int64_t)b * post + s] = idx;
+  }
 }
 
 __global__ void __launch_bounds__(1024)
@@ -213,25 +290,191 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
   }
   // the loop ends right after a barrier (break) or after the last one (t == nbv): s_nk[t & 1]
   // is the final count either way
-  const int nk = min(s_nk[t & 1], post);
-  if (tid == 0) n_keep_out[b] = nk;
-  const float4* bx = reinterpret_cast<const float4*>(boxes) + (int64_t)b * P;
-  for (int s = tid; s < post; s += blockDim.x) {
-    int idx;
-    if (s < nk) {
-      idx = keep_list[s];
-    } else if (nk > 0) {
-      int r = (int)(rand_u[(int64_t)b * post + s] * nk);
-      idx = keep_list[min(max(r, 0), nk - 1)];
-    } else {
-      idx = 0;
+  nms_write_out(boxes, scores, b, P, post, min(s_nk[t & 1], post), keep_list, rand_u, rois, out_scores, keep_idx,
+                n_keep_out);
+}
+
+// ---- multi-workgroup reducer -------------------------------------------------------------------
+constexpr int NMSC_PER = 16;                              // column blocks per workgroup, one wave each
+constexpr int NMSC_TRI = NMSC_PER * (NMSC_PER + 1) / 2;   // own-triangle mask words per lane
+constexpr int NMSC_SPIN = 1 << 20;                        // empty poll rounds before a workgroup gives up
+
+__device__ __forceinline__ uint64_t nmsc_load(const uint64_t* p) {
+  return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void nmsc_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// own-triangle slot of (row k, column c), k <= c < NMSC_PER, in units of 64 words
+__host__ __device__ constexpr int nmsc_tri(int k, int c) { return c * (c + 1) / 2 + k; }
+
+__global__ void __launch_bounds__(1024)
+nms_reduce_mc_kernel(const float* __restrict__ boxes, const float* __restrict__ scores,
+                     const int32_t* __restrict__ n_valid, const uint64_t* __restrict__ maskT, uint64_t* rec, int P,
+                     int nb, int post, const float* __restrict__ rand_u, float* __restrict__ rois,
+                     float* __restrict__ out_scores, int64_t* __restrict__ keep_idx,
+                     int32_t* __restrict__ n_keep_out, int32_t* keep_ws) {
+  // dynamic LDS: [own triangle NMSC_TRI x 64 u64][kept nb u64][rem NMSC_PER u64][count nb i32][keep list post i32]
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  uint64_t* tri = reinterpret_cast<uint64_t*>(smem);
+  uint64_t* s_kept = tri + NMSC_TRI * 64;
+  uint64_t* s_rem = s_kept + nb;
+  int* s_nk = reinterpret_cast<int*>(s_rem + NMSC_PER);
+  __shared__ int s_flag[4];  // 0: final record seen, 1: final block resolved here (-1: none), 2: gave up, 3: last out
+  const int b = blockIdx.y, w = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  int32_t* keep_list = keep_ws ? keep_ws + (int64_t)b * post : s_nk + nb;
+  const int nv = min(n_valid[b], P), nbv = (nv + 63) / 64;
+  const int64_t Pp = nms_row_words(nb);
+  const uint64_t* mb = maskT + (int64_t)b * nb * Pp;
+  uint64_t* rb = rec + (int64_t)b * nb * 2;
+  uint64_t* cnt = rec + (int64_t)gridDim.y * nb * 2 + b;
+  const int lo = w * NMSC_PER, hi = min(lo + NMSC_PER, nbv);
+  if (tid == 0) {
+    s_flag[0] = 0;
+    s_flag[1] = -1;
+    s_flag[2] = 0;
+  }
+  __syncthreads();
+  bool assemble = nbv == 0 && w == 0;  // no valid box: workgroup 0 writes the padded output
+  int tf = -1;
+  if (lo < nbv) {
+    const int c = lo + wave;
+    const bool active = c < hi;
+    if (active) {  // stage this wave's column of the own triangle (rows lo..c)
+      uint64_t own[NMSC_PER];
+#pragma unroll
+      for (int k = 0; k < NMSC_PER; ++k) own[k] = k <= wave ? mb[(int64_t)(lo + k) * Pp + nms_col(c, lane)] : 0ull;
+#pragma unroll
+      for (int k = 0; k < NMSC_PER; ++k)
+        if (k <= wave) tri[nmsc_tri(k, wave) * 64 + lane] = own[k];
     }
-    idx = min(max(idx, 0), P - 1);  // never read outside the image's box block
-    const float4 bb = bx[idx];
-    float* ro = rois + ((int64_t)b * post + s) * 5;
-    ro[0] = (float)b; ro[1] = bb.x; ro[2] = bb.y; ro[3] = bb.z; ro[4] = bb.w;
-    out_scores[(int64_t)b * post + s] = scores[(int64_t)b * P + idx];
-    keep_idx[(int64_t)b * post + s] = idx;
+    // phase A: fold the kept rows of earlier workgroups into column c
+    uint64_t rem = 0;
+    bool stop = false, gave_up = false;
+    if (active) {
+      for (int r0 = 0; r0 < lo && !stop; r0 += 16) {
+        const int nr = min(16, lo - r0);
+        uint64_t wd[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) wd[i] = i < nr ? mb[(int64_t)(r0 + i) * Pp + nms_col(c, lane)] : 0ull;
+        int got = 0, spins = 0;
+        while (got < nr && !stop) {
+          uint64_t w0 = 0, w1 = 0;
+          if (lane >= got && lane < nr) {
+            w0 = nmsc_load(rb + 2 * (r0 + lane));
+            w1 = nmsc_load(rb + 2 * (r0 + lane) + 1);
+          }
+          const bool ok = lane < got || (lane < nr && (w0 >> 32) != 0ull && (w1 >> 32) != 0ull);
+          const int n = min(nr, (int)__builtin_ctzll(~__ballot(ok)));  // ready prefix of the chunk
+          if (n == got) {
+            if (++spins > NMSC_SPIN) {
+              stop = gave_up = true;
+              break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+          }
+          spins = 0;
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            if (i >= got && i < n && !stop) {
+              const uint32_t k0 = __builtin_amdgcn_readlane((int)(uint32_t)w0, i);
+              const uint32_t k1 = __builtin_amdgcn_readlane((int)(uint32_t)w1, i);
+              const int nk = __builtin_amdgcn_readlane((int)(uint32_t)(w0 >> 32), i) - 1;
+              const uint64_t kp = (uint64_t)k0 | ((uint64_t)k1 << 32);
+              rem |= __ballot((wd[i] & kp) != 0ull);
+              if (wave == 0 && lane == 0) {
+                s_kept[r0 + i] = kp;
+                s_nk[r0 + i] = nk;
+              }
+              if (nk >= post) stop = true;  // the chain ended before this workgroup's blocks
+            }
+          }
+          got = n;
+        }
+      }
+      if (lane == 0) {
+        s_rem[wave] = rem;
+        if (stop) s_flag[gave_up ? 2 : 0] = 1;
+      }
+    }
+    __syncthreads();
+    if (s_flag[0] == 0 && s_flag[2] == 0) {
+      // phase B: wave 0 resolves blocks lo..hi-1 from LDS
+      if (wave == 0) {
+        uint64_t rm[NMSC_PER];
+#pragma unroll
+        for (int k = 0; k < NMSC_PER; ++k) rm[k] = s_rem[k];
+        int nk = lo > 0 ? s_nk[lo - 1] : 0;
+#pragma unroll
+        for (int k = 0; k < NMSC_PER; ++k) {
+          const int t = lo + k;
+          if (t >= hi) break;
+          uint64_t row[NMSC_PER];
+#pragma unroll
+          for (int c2 = k; c2 < NMSC_PER; ++c2) row[c2] = lo + c2 < hi ? tri[nmsc_tri(k, c2) * 64 + lane] : 0ull;
+          const int nrow = min(64, nv - t * 64);
+          const uint64_t valid = nrow >= 64 ? ~0ull : ((1ull << nrow) - 1ull);
+          const uint64_t cand = valid & ~rm[k];
+          uint64_t kept = cand;
+          for (int it = 0; it < 65; ++it) {
+            const uint64_t sup = __ballot((row[k] & kept) != 0ull);
+            const uint64_t next = cand & ~sup;
+            if (next == kept) break;
+            kept = next;
+          }
+          if (nk + __popcll(kept) > post) {  // keep only the lowest (post - nk) boxes of this block
+            int need = post - nk;
+            uint64_t trunc = 0, kk = kept;
+            while (need-- > 0 && kk) {
+              trunc |= kk & (~kk + 1);
+              kk &= kk - 1;
+            }
+            kept = trunc;
+          }
+          nk += __popcll(kept);
+          if (lane == 0) {
+            const uint64_t tag = (uint64_t)(nk + 1) << 32;
+            nmsc_store(rb + 2 * t, (kept & 0xffffffffull) | tag);
+            nmsc_store(rb + 2 * t + 1, (kept >> 32) | tag);
+            s_kept[t] = kept;
+            s_nk[t] = nk;
+          }
+          if (nk >= post || t == nbv - 1) {
+            tf = t;
+            break;
+          }
+#pragma unroll
+          for (int c2 = k + 1; c2 < NMSC_PER; ++c2) rm[c2] |= __ballot((row[c2] & kept) != 0ull);
+        }
+        if (lane == 0) s_flag[1] = tf;
+      }
+      __syncthreads();
+      tf = s_flag[1];
+      assemble = tf >= 0;
+    } else if (s_flag[2] && tid == 0) {
+      n_keep_out[b] = -1;  // a poll gave up: the output of this image is not valid
+    }
+  }
+  if (assemble) {
+    // keep list from the kept words: block t's boxes follow the s_nk[t - 1] boxes kept before it
+    for (int t = wave; t <= tf; t += 16) {
+      const uint64_t kept = s_kept[t];
+      const int base = t > 0 ? s_nk[t - 1] : 0;
+      if ((kept >> lane) & 1ull) keep_list[base + __popcll(kept & ((1ull << lane) - 1ull))] = t * 64 + lane;
+    }
+    __syncthreads();
+    nms_write_out(boxes, scores, b, P, post, tf >= 0 ? min(s_nk[tf], post) : 0, keep_list, rand_u, rois, out_scores,
+                  keep_idx, n_keep_out);
+  }
+  // the last workgroup of the image to finish clears the records for the next reduce
+  __syncthreads();
+  if (tid == 0)
+    s_flag[3] = __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
+  __syncthreads();
+  if (s_flag[3]) {
+    for (int i = tid; i < 2 * nb; i += blockDim.x) nmsc_store(rb + i, 0ull);
+    if (tid == 0) nmsc_store(cnt, 0ull);
   }
 }
 
@@ -286,7 +529,8 @@ void nms_check(const float* boxes, const int32_t* n_valid, int B, int P, float t
 
 int64_t nms_mask_words(int B, int P) {
   const int nb = div_up(P, 64);
-  return (int64_t)B * nb * nms_row_words(nb);
+  // transposed mask, then the reducer's block records (2 words per block) and exit counters
+  return (int64_t)B * nb * nms_row_words(nb) + (int64_t)B * nb * 2 + B;
 }
 
 void nms_mask(const float* boxes, const int32_t* n_valid, int B, int P, float thresh, uint64_t* mask,
@@ -294,12 +538,17 @@ void nms_mask(const float* boxes, const int32_t* n_valid, int B, int P, float th
   if (B == 0 || P == 0) return;
   const int nb = div_up(P, 64);
   dim3 grid(div_up(nb, 4), nb, B);
-  nms_mask_kernel<<<grid, 256, 0, st>>>(boxes, n_valid, P, nb, thresh, mask);
+  nms_mask_kernel<<<grid, 256, 0, st>>>(boxes, n_valid, P, nb, thresh, mask, mask + (int64_t)B * nb * nms_row_words(nb));
+}
+
+static size_t nms_serial_lds(int nb, int post) { return 16 + (size_t)nb * 16 + (size_t)post * 4; }
+static size_t nms_mc_lds(int nb, int post) {
+  return (size_t)NMSC_TRI * 64 * 8 + (size_t)nb * 8 + NMSC_PER * 8 + (size_t)nb * 4 + (size_t)post * 4;
 }
 
 size_t nms_reduce_lds(int P, int post) {
   const int nb = div_up(P, 64);
-  return 16 + (size_t)nb * 16 + (size_t)post * 4;
+  return std::max(nms_serial_lds(nb, post), nms_mc_lds(nb, post));
 }
 
 bool nms_keep_in_lds(int P, int post) { return nms_reduce_lds(P, post) <= 160 * 1024; }
@@ -309,9 +558,21 @@ void nms_reduce(const float* boxes, const float* scores, const int32_t* n_valid,
                 int32_t* n_keep, int32_t* keep_ws, hipStream_t st) {
   if (B == 0) return;
   const int nb = div_up(P, 64);
-  const size_t lds = keep_ws ? nms_reduce_lds(P, 0) : nms_reduce_lds(P, post);
-  nms_reduce_kernel<<<B, 1024, lds, st>>>(boxes, scores, n_valid, mask, P, nb, post, rand_u, rois, out_scores,
-                                          keep_idx, n_keep, keep_ws);
+  const int lpost = keep_ws ? 0 : post;
+  static const bool serial = [] {
+    const char* e = getenv("MXR_NMS_SERIAL");
+    return e && e[0] == '1';
+  }();
+  if (serial) {
+    nms_reduce_kernel<<<B, 1024, nms_serial_lds(nb, lpost), st>>>(boxes, scores, n_valid, mask, P, nb, post, rand_u,
+                                                                  rois, out_scores, keep_idx, n_keep, keep_ws);
+    return;
+  }
+  // the records follow the mask (nms_mask_words); written here, cleared by nms_mask and by the kernel
+  uint64_t* rec = const_cast<uint64_t*>(mask) + (int64_t)B * nb * nms_row_words(nb);
+  dim3 grid(div_up(nb, NMSC_PER), B);
+  nms_reduce_mc_kernel<<<grid, 1024, nms_mc_lds(nb, lpost), st>>>(boxes, scores, n_valid, mask, rec, P, nb, post,
+                                                                  rand_u, rois, out_scores, keep_idx, n_keep, keep_ws);
 }
 
 }  // namespace mxr

@@ -415,14 +415,16 @@ proposal_sample_kernel(const float* __restrict__ rois, const float* __restrict__
   float* s_t = reinterpret_cast<float*>(keep + R);                 // [R][4]
   int* s_lab = reinterpret_cast<int*>(s_t + 4 * R);                // [R]
   int* s_acc = s_lab + R;
+  float* gb = reinterpret_cast<float*>(s_acc + 4);                 // [G][5]: the image's gt rows
   const int b = blockIdx.x;
   const int ng = n_gt[b];
-  const float* gb = gt + (int64_t)b * G * 5;
   const float* rb = rois + (int64_t)b * P * 5;
   for (int i = threadIdx.x; i < P; i += blockDim.x) {
     s_ov[i] = max_ov_p[(int64_t)b * P + i];
     s_am[i] = argmax_p[(int64_t)b * P + i];
   }
+  for (int i = threadIdx.x; i < G * 5; i += blockDim.x) gb[i] = gt[(int64_t)b * G * 5 + i];
+  __syncthreads();
   for (int g = threadIdx.x; g < G; g += blockDim.x) {  // gt rows vs gt (first max, like numpy)
     float best = 0.f;
     int bi = 0;
@@ -530,22 +532,32 @@ proposal_sample_kernel(const float* __restrict__ rois, const float* __restrict__
     s_lab[j] = lab;
   }
   __syncthreads();
+  // class-specific (R, 4C) rows: one wave per sample row, one float4 (a class's 4 values) per lane
   const int C4 = 4 * C;
-  const int64_t off = (int64_t)b * R * C4;
-  for (int e = threadIdx.x; e < R * C4; e += blockDim.x) {
-    const int j = e / C4, col = e % C4;
+  const float4 iw4 = make_float4(prm.iw[0], prm.iw[1], prm.iw[2], prm.iw[3]);
+  const float4 ow4 = make_float4(prm.iw[0] > 0.f ? 1.f : 0.f, prm.iw[1] > 0.f ? 1.f : 0.f,
+                                 prm.iw[2] > 0.f ? 1.f : 0.f, prm.iw[3] > 0.f ? 1.f : 0.f);
+  const int nwaves = blockDim.x >> 6, lane = threadIdx.x & 63;
+  for (int j = threadIdx.x >> 6; j < R; j += nwaves) {
     const int lab = s_lab[j];
-    const bool hit = lab > 0 && (col >> 2) == lab;
-    const float iwv = hit ? prm.iw[col & 3] : 0.f;
-    bbox_target[off + e] = hit ? s_t[j * 4 + (col & 3)] : 0.f;
-    inside[off + e] = iwv;
-    outside[off + e] = iwv > 0.f ? 1.f : 0.f;
+    const float4 t4 = make_float4(s_t[j * 4], s_t[j * 4 + 1], s_t[j * 4 + 2], s_t[j * 4 + 3]);
+    const int64_t row = ((int64_t)b * R + j) * C4;
+    float4* bt = reinterpret_cast<float4*>(bbox_target + row);
+    float4* in = reinterpret_cast<float4*>(inside + row);
+    float4* ou = reinterpret_cast<float4*>(outside + row);
+    for (int cls = lane; cls < C; cls += 64) {
+      const bool hit = lab > 0 && cls == lab;  // component selects (a float4 select went through scratch)
+      bt[cls] = make_float4(hit ? t4.x : 0.f, hit ? t4.y : 0.f, hit ? t4.z : 0.f, hit ? t4.w : 0.f);
+      in[cls] = make_float4(hit ? iw4.x : 0.f, hit ? iw4.y : 0.f, hit ? iw4.z : 0.f, hit ? iw4.w : 0.f);
+      ou[cls] = make_float4(hit ? ow4.x : 0.f, hit ? ow4.y : 0.f, hit ? ow4.z : 0.f, hit ? ow4.w : 0.f);
+    }
   }
 }
 
 size_t proposal_sample_lds(int P, int G, int R, int F) {
   const int M = P + G;
-  return (size_t)M * 8 + sizeof(SelScratch) + (size_t)(F + (R - F) + R) * 4 + (size_t)R * 16 + (size_t)R * 4 + 32;
+  return (size_t)M * 8 + sizeof(SelScratch) + (size_t)(F + (R - F) + R) * 4 + (size_t)R * 16 + (size_t)R * 4 + 16 +
+         (size_t)G * 20;
 }
 
 int proposal_sample(const float* rois, const float* gt, const int32_t* n_gt, const float* max_ov, const int32_t* argmax,

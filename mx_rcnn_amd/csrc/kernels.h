@@ -26,7 +26,8 @@ void proposal_decode(const void* cls, int cls_bf16, int64_t cs0, int64_t cs1, in
 
 // ---- NMS (nms.hip) ----------------------------------------------------------
 // boxes (B, P, 4) sorted by descending score, n_valid (B) int32 on device.
-// mask workspace: nms_mask_words(B, P) uint64 (transposed, column blocks paired: [B][nb][ceil(nb/2)*128], nb = ceil(P/64)).
+// mask workspace: nms_mask_words(B, P) uint64 (transposed, column blocks paired: [B][nb][ceil(nb/2)*128], nb = ceil(P/64)),
+// followed by the multi-workgroup reducer's block records [B][nb][2] and exit counters [B].
 int64_t nms_mask_words(int B, int P);
 size_t nms_reduce_lds(int P, int post);
 // the reducer keeps its keep list in LDS when this holds, else in a (B, post) int32 global workspace

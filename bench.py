@@ -47,6 +47,9 @@ def parse_args(argv=None):
     ap.add_argument('--grad-comm', default='fp32', choices=['fp32', 'bf16'],
                     help='all-reduce wire dtype of the gradient buckets (fp32 = the reference kvstore sum)')
     ap.add_argument('--pool', type=int, default=4, help='distinct synthetic batches cycled')
+    ap.add_argument('--host-float-data', action='store_true',
+                    help='feed float network input (converted to the compute dtype outside the step) instead of '
+                         'the loaders\' raw uint8 images (converted inside the captured step)')
     ap.add_argument('--train-mode', default='e2e', choices=['e2e', 'rpn', 'rcnn'],
                     help='e2e (headline) or one stage of 4-step alternate training (BASELINE config 4): '
                          'rpn = RPN-only step, rcnn = Fast R-CNN step on 128 given RoIs per image')
@@ -76,8 +79,14 @@ PRECISION_NOTE = {
 }
 
 
-def synthetic_batch(n_img, h, w, num_classes, device, gen, max_gt=20):
-    data = torch.randn(n_img, 3, h, w, generator=gen) * 50.0
+def synthetic_batch(n_img, h, w, num_classes, device, gen, max_gt=20, raw=False, pixel_means=None):
+    """raw=True: the training loaders' raw-image form (uint8 BGR (n, h, w, 3) + pixel_means,
+    data/loader.py raw_images), converted inside the captured step by csrc/hip/image.hip; else
+    float (n, 3, h, w) network input."""
+    if raw:
+        data = torch.randint(0, 256, (n_img, h, w, 3), generator=gen, dtype=torch.uint8)
+    else:
+        data = torch.randn(n_img, 3, h, w, generator=gen) * 50.0
     G = max_gt
     gt = torch.full((n_img, G, 5), -1.0)
     n_gt = torch.randint(1, G + 1, (n_img,), generator=gen).to(torch.int32)
@@ -90,15 +99,27 @@ def synthetic_batch(n_img, h, w, num_classes, device, gen, max_gt=20):
         cls = torch.randint(1, num_classes, (k,), generator=gen).float()
         gt[b, :k] = torch.stack([x1, y1, x1 + bw, y1 + bh, cls], dim=1)
     im_info = torch.tensor([[float(h), float(w), 1.0]] * n_img)
-    return {'data': data.to(device), 'im_info': im_info.to(device), 'gt_boxes': gt.to(device),
-            'n_gt': n_gt.to(device)}
+    out = {'data': data.to(device), 'im_info': im_info.to(device), 'gt_boxes': gt.to(device), 'n_gt': n_gt.to(device)}
+    if raw:
+        pm = (0.0, 0.0, 0.0) if pixel_means is None else torch.as_tensor(pixel_means, dtype=torch.float64).reshape(-1)[:3]
+        out['pixel_means'] = tuple(float(m) for m in pm)
+    return out
+
+
+def network_input(b):
+    """The float (n, 3, h, w) image a batch feeds the network (raw batches converted as in the step)."""
+    if b['data'].dtype != torch.uint8:
+        return b['data']
+    from mx_rcnn_amd.ops.image import image_prep
+    return image_prep(b['data'], b['im_info'], b['pixel_means'], torch.float32, channels_last=False)
 
 
 def rcnn_batch(b, num_classes, rois_per_image, gen, fg_fraction=0.25):
     """A Fast R-CNN step input of the alternate scheme's shape (tools/train_rcnn.py): per image
     ``rois_per_image`` RoIs (the proposal-target sample of precomputed proposals), fg first with
     one class-specific regression target each, background after."""
-    n, _, h, w = b['data'].shape
+    n, h, w = network_input(b).shape[0], b['im_info'][0, 0], b['im_info'][0, 1]
+    h, w = int(h), int(w)
     R = n * rois_per_image
     wh = torch.rand(R, 2, generator=gen) * min(300.0, 0.5 * min(h, w)) + 16
     x1 = torch.rand(R, generator=gen) * (w - wh[:, 0] - 1)
@@ -116,7 +137,8 @@ def rcnn_batch(b, num_classes, rois_per_image, gen, fg_fraction=0.25):
     tgt[fg.unsqueeze(1), cols] = torch.randn(len(fg), 4, generator=gen) * 0.5
     inside[fg.unsqueeze(1), cols] = 1.0
     dev = b['data'].device
-    return {'data': b['data'], 'rois': rois.to(dev), 'label': label.to(dev), 'bbox_target': tgt.to(dev),
+    extra = {k: b[k] for k in ('im_info', 'pixel_means') if b['data'].dtype == torch.uint8}
+    return {**extra, 'data': b['data'], 'rois': rois.to(dev), 'label': label.to(dev), 'bbox_target': tgt.to(dev),
             'bbox_inside_weight': inside.to(dev), 'bbox_outside_weight': inside.clone().to(dev)}
 
 
@@ -162,13 +184,15 @@ def run(args, precision, rank, world, device):
     torch.manual_seed(1234 + rank)
     model = FasterRCNN(args.network, args.num_classes, cfg=cfg)
     gen = torch.Generator().manual_seed(4321 + rank)
-    pool = [synthetic_batch(args.ims_per_gpu, h, w, args.num_classes, device, gen) for _ in range(args.pool)]
+    raw = not args.host_float_data
+    pool = [synthetic_batch(args.ims_per_gpu, h, w, args.num_classes, device, gen, raw=raw,
+                            pixel_means=cfg.PIXEL_MEANS) for _ in range(args.pool)]
     if args.train_mode == 'rcnn':
         pool = [rcnn_batch(b, args.num_classes, cfg.TRAIN.BATCH_SIZE, gen) for b in pool]
     if args.network.startswith('resnet'):
-        model.to(device).calibrate_bn(pool[0]['data'])  # stand-in for pretrained BN statistics
+        model.to(device).calibrate_bn(network_input(pool[0]))  # stand-in for pretrained BN statistics
     else:
-        model.to(device).calibrate_vgg(pool[0]['data'])  # stand-in for pretrained filters (LSUV scale)
+        model.to(device).calibrate_vgg(network_input(pool[0]))  # stand-in for pretrained filters (LSUV scale)
     fixed = ['conv0', 'stage1', 'stage2', 'bn_data', 'bn0'] if args.network.startswith('resnet') else ['conv1', 'conv2']
     trainer = Trainer(model, args.train_mode, fixed_param_prefix=fixed, lr=0.001, momentum=0.9, wd=0.0005, clip_gradient=1.0,
                       rescale_grad=1.0, device=device, bucket_mb=args.bucket_mb, precision=precision,
@@ -231,7 +255,8 @@ def run(args, precision, rank, world, device):
            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': round(ms, 3),
            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
            'dtype': trainer.precision,
-           'data': 'synthetic (random %dx%d images, 1-20 random gt boxes, random-init weights)' % (h, w),
+           'data': 'synthetic (random %dx%d %s images, 1-20 random gt boxes, random-init weights)' % (
+               h, w, 'float' if args.host_float_data else 'uint8 BGR (raw-loader form, converted in the step)'),
            'config': {'model': '%s-faster-rcnn%s' % (args.network, '-c4' if args.network.startswith('resnet') else ''), 'global_batch': args.ims_per_gpu * world,
                       'seq_len': None, 'image_hw': [h, w], 'num_classes': args.num_classes,
                       'ims_per_gpu': args.ims_per_gpu, 'train_mode': args.train_mode, 'parallelism': 'dp%d' % world,

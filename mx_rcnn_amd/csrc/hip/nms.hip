@@ -28,16 +28,18 @@
 // exit once `post` boxes are kept.  No host synchronisation anywhere.
 //   That reducer streams the whole 9 MB triangle (P = 12000) through one CU at that CU's share of
 //   the memory bandwidth (~270 us); it stays as the MXR_NMS_SERIAL=1 path.
-// Stage 2, default (nms_reduce_mc): a chain of workgroups, one per 16 column blocks, so the
-// triangle is read by ceil(nb / 16) CUs and only the 64-box resolve stays serial:
+// Stage 2, default (nms_reduce_mc): a chain of workgroups, one per PER = 8 column blocks, so the
+// triangle is read by ceil(nb / 8) CUs and only the 64-box resolve stays serial:
 //   phase A  every wave owns one column block c of its workgroup and folds the kept rows r < lo
 //            (published by earlier workgroups) into its removed word, polling the per-block
 //            records 16 rows at a time; the mask words of a chunk are loaded before its poll;
-//   phase B  wave 0 resolves the workgroup's own blocks in order from LDS only (the 16x16 own
+//   phase B  wave 0 resolves the workgroup's own blocks in order from LDS only (the PER x PER own
 //            triangle of mask words is staged there during phase A), publishing each block's
 //            kept word and running count as it goes -- no barrier, no global round trip inside;
-//   the workgroup that resolves the last needed block (count reaches `post`, or the last valid
-//   block) assembles the output from the kept words it holds in LDS.
+//   every workgroup then writes the output rows of its own kept boxes, and the one that resolves
+//   the last needed block (count reaches `post`, or the last valid block) adds the random pad.
+//   Measured (MXR_NMS_PROBE timeline, 12000 boxes): ~0.35 us per block in phase B, ~2 us per
+//   hand-off between workgroups; 8 blocks per workgroup beat 16 (fewer folds per block).
 // A published record is two 64-bit words {kept lo/hi 32 bits | (count + 1) << 32}: each word is
 // stored and loaded whole (relaxed, agent scope), a nonzero upper half means "written", so a
 // reader never needs an ordering fence between the two.  The records are zeroed by nms_mask and
@@ -127,16 +129,27 @@ nms_mask_kernel(const float* __restrict__ boxes, const int32_t* __restrict__ n_v
   maskT[((int64_t)b * nb + rb) * Pp + nms_col(cb, lane)] = bits;
 }
 
-// Output assembly shared by both reducers (the whole workgroup; keep_list holds nk entries and is
-// visible to every thread): slot s < nk takes keep[s], later slots the reference's random pad.
+// Output row s of image b: RoI [b, box], its score and index.
+__device__ __forceinline__ void nms_write_row(const float* __restrict__ boxes, const float* __restrict__ scores, int b,
+                                              int P, int post, int s, int idx, float* __restrict__ rois,
+                                              float* __restrict__ out_scores, int64_t* __restrict__ keep_idx) {
+  idx = min(max(idx, 0), P - 1);  // never read outside the image's box block
+  const float4 bb = reinterpret_cast<const float4*>(boxes)[(int64_t)b * P + idx];
+  float* ro = rois + ((int64_t)b * post + s) * 5;
+  ro[0] = (float)b; ro[1] = bb.x; ro[2] = bb.y; ro[3] = bb.z; ro[4] = bb.w;
+  out_scores[(int64_t)b * post + s] = scores[(int64_t)b * P + idx];
+  keep_idx[(int64_t)b * post + s] = idx;
+}
+
+// Output slots [s0, post) (the whole workgroup; keep_list holds nk entries and is visible to every
+// thread): slot s < nk takes keep[s], later slots the reference's random pad keep[floor(u * nk)].
 __device__ __forceinline__ void nms_write_out(const float* __restrict__ boxes, const float* __restrict__ scores, int b,
-                                              int P, int post, int nk, const int32_t* keep_list,
+                                              int P, int post, int nk, int s0, const int32_t* keep_list,
                                               const float* __restrict__ rand_u, float* __restrict__ rois,
                                               float* __restrict__ out_scores, int64_t* __restrict__ keep_idx,
                                               int32_t* __restrict__ n_keep_out) {
   if (threadIdx.x == 0) n_keep_out[b] = nk;
-  const float4* bx = reinterpret_cast<const float4*>(boxes) + (int64_t)b * P;
-  for (int s = threadIdx.x; s < post; s += blockDim.x) {
+  for (int s = s0 + threadIdx.x; s < post; s += blockDim.x) {
     int idx;
     if (s < nk) {
       idx = keep_list[s];
@@ -146,12 +159,7 @@ __device__ __forceinline__ void nms_write_out(const float* __restrict__ boxes, c
     } else {
       idx = 0;
     }
-    idx = min(max(idx, 0), P - 1);  // never read outside the image's box block
-    const float4 bb = bx[idx];
-    float* ro = rois + ((int64_t)b * post + s) * 5;
-    ro[0] = (float)b; ro[1] = bb.x; ro[2] = bb.y; ro[3] = bb.z; ro[4] = bb.w;
-    out_scores[(int64_t)b * post + s] = scores[(int64_t)b * P + idx];
-    keep_idx[(int64_t)b * post + s] = idx;
+    nms_write_row(boxes, scores, b, P, post, s, idx, rois, out_scores, keep_idx);
   }
 }
 
@@ -290,13 +298,12 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
   }
   // the loop ends right after a barrier (break) or after the last one (t == nbv): s_nk[t & 1]
   // is the final count either way
-  nms_write_out(boxes, scores, b, P, post, min(s_nk[t & 1], post), keep_list, rand_u, rois, out_scores, keep_idx,
+  nms_write_out(boxes, scores, b, P, post, min(s_nk[t & 1], post), 0, keep_list, rand_u, rois, out_scores, keep_idx,
                 n_keep_out);
 }
 
 // ---- multi-workgroup reducer -------------------------------------------------------------------
-constexpr int NMSC_PER = 16;                              // column blocks per workgroup, one wave each
-constexpr int NMSC_TRI = NMSC_PER * (NMSC_PER + 1) / 2;   // own-triangle mask words per lane
+constexpr int NMSC_PER = 8;  // column blocks per workgroup, one wave each (MXR_NMS_PER=16 for the A/B)
 constexpr int NMSC_SPIN = 1 << 20;                        // empty poll rounds before a workgroup gives up
 
 __device__ __forceinline__ uint64_t nmsc_load(const uint64_t* p) {
@@ -305,21 +312,22 @@ __device__ __forceinline__ uint64_t nmsc_load(const uint64_t* p) {
 __device__ __forceinline__ void nmsc_store(uint64_t* p, uint64_t v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-// own-triangle slot of (row k, column c), k <= c < NMSC_PER, in units of 64 words
+// own-triangle slot of (row k, column c), k <= c < PER, in units of 64 words
 __host__ __device__ constexpr int nmsc_tri(int k, int c) { return c * (c + 1) / 2 + k; }
 
+template <int PER>
 __global__ void __launch_bounds__(1024)
 nms_reduce_mc_kernel(const float* __restrict__ boxes, const float* __restrict__ scores,
                      const int32_t* __restrict__ n_valid, const uint64_t* __restrict__ maskT, uint64_t* rec, int P,
                      int nb, int post, const float* __restrict__ rand_u, float* __restrict__ rois,
                      float* __restrict__ out_scores, int64_t* __restrict__ keep_idx,
-                     int32_t* __restrict__ n_keep_out, int32_t* keep_ws) {
-  // dynamic LDS: [own triangle NMSC_TRI x 64 u64][kept nb u64][rem NMSC_PER u64][count nb i32][keep list post i32]
+                     int32_t* __restrict__ n_keep_out, int32_t* keep_ws, uint64_t* probe) {
+  // dynamic LDS: [own triangle (PER * (PER + 1) / 2) x 64 u64][kept nb u64][rem PER u64][count nb i32][keep list post i32]
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint64_t* tri = reinterpret_cast<uint64_t*>(smem);
-  uint64_t* s_kept = tri + NMSC_TRI * 64;
+  uint64_t* s_kept = tri + (PER * (PER + 1) / 2) * 64;
   uint64_t* s_rem = s_kept + nb;
-  int* s_nk = reinterpret_cast<int*>(s_rem + NMSC_PER);
+  int* s_nk = reinterpret_cast<int*>(s_rem + PER);
   __shared__ int s_flag[4];  // 0: final record seen, 1: final block resolved here (-1: none), 2: gave up, 3: last out
   const int b = blockIdx.y, w = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   int32_t* keep_list = keep_ws ? keep_ws + (int64_t)b * post : s_nk + nb;
@@ -328,12 +336,17 @@ nms_reduce_mc_kernel(const float* __restrict__ boxes, const float* __restrict__ 
   const uint64_t* mb = maskT + (int64_t)b * nb * Pp;
   uint64_t* rb = rec + (int64_t)b * nb * 2;
   uint64_t* cnt = rec + (int64_t)gridDim.y * nb * 2 + b;
-  const int lo = w * NMSC_PER, hi = min(lo + NMSC_PER, nbv);
+  const int lo = w * PER, hi = min(lo + PER, nbv);
   if (tid == 0) {
     s_flag[0] = 0;
     s_flag[1] = -1;
     s_flag[2] = 0;
   }
+  // MXR_NMS_PROBE timeline (wall clock): per block {resolve start, publish, fixpoint rounds, kept},
+  // per workgroup {start, phase A done, phase B done, end}
+  uint64_t* pb = probe ? probe + (int64_t)b * nb * 8 : nullptr;
+  uint64_t* pw = pb ? pb + (int64_t)nb * 4 + (int64_t)w * 4 : nullptr;
+  if (pw && tid == 0) pw[0] = wall_clock64();
   __syncthreads();
   bool assemble = nbv == 0 && w == 0;  // no valid box: workgroup 0 writes the padded output
   int tf = -1;
@@ -341,11 +354,11 @@ nms_reduce_mc_kernel(const float* __restrict__ boxes, const float* __restrict__ 
     const int c = lo + wave;
     const bool active = c < hi;
     if (active) {  // stage this wave's column of the own triangle (rows lo..c)
-      uint64_t own[NMSC_PER];
+      uint64_t own[PER];
 #pragma unroll
-      for (int k = 0; k < NMSC_PER; ++k) own[k] = k <= wave ? mb[(int64_t)(lo + k) * Pp + nms_col(c, lane)] : 0ull;
+      for (int k = 0; k < PER; ++k) own[k] = k <= wave ? mb[(int64_t)(lo + k) * Pp + nms_col(c, lane)] : 0ull;
 #pragma unroll
-      for (int k = 0; k < NMSC_PER; ++k)
+      for (int k = 0; k < PER; ++k)
         if (k <= wave) tri[nmsc_tri(k, wave) * 64 + lane] = own[k];
     }
     // phase A: fold the kept rows of earlier workgroups into column c
@@ -399,27 +412,31 @@ nms_reduce_mc_kernel(const float* __restrict__ boxes, const float* __restrict__ 
       }
     }
     __syncthreads();
+    if (pw && tid == 0) pw[1] = wall_clock64();
     if (s_flag[0] == 0 && s_flag[2] == 0) {
       // phase B: wave 0 resolves blocks lo..hi-1 from LDS
       if (wave == 0) {
-        uint64_t rm[NMSC_PER];
+        uint64_t rm[PER];
 #pragma unroll
-        for (int k = 0; k < NMSC_PER; ++k) rm[k] = s_rem[k];
+        for (int k = 0; k < PER; ++k) rm[k] = s_rem[k];
         int nk = lo > 0 ? s_nk[lo - 1] : 0;
 #pragma unroll
-        for (int k = 0; k < NMSC_PER; ++k) {
+        for (int k = 0; k < PER; ++k) {
           const int t = lo + k;
           if (t >= hi) break;
-          uint64_t row[NMSC_PER];
+          uint64_t row[PER];
 #pragma unroll
-          for (int c2 = k; c2 < NMSC_PER; ++c2) row[c2] = lo + c2 < hi ? tri[nmsc_tri(k, c2) * 64 + lane] : 0ull;
+          for (int c2 = k; c2 < PER; ++c2) row[c2] = lo + c2 < hi ? tri[nmsc_tri(k, c2) * 64 + lane] : 0ull;
           const int nrow = min(64, nv - t * 64);
           const uint64_t valid = nrow >= 64 ? ~0ull : ((1ull << nrow) - 1ull);
           const uint64_t cand = valid & ~rm[k];
+          const uint64_t t_res = pb ? wall_clock64() : 0ull;
           uint64_t kept = cand;
+          int rounds = 0;
           for (int it = 0; it < 65; ++it) {
             const uint64_t sup = __ballot((row[k] & kept) != 0ull);
             const uint64_t next = cand & ~sup;
+            ++rounds;
             if (next == kept) break;
             kept = next;
           }
@@ -439,19 +456,35 @@ nms_reduce_mc_kernel(const float* __restrict__ boxes, const float* __restrict__ 
             nmsc_store(rb + 2 * t + 1, (kept >> 32) | tag);
             s_kept[t] = kept;
             s_nk[t] = nk;
+            if (pb) {
+              pb[t * 4] = t_res;
+              pb[t * 4 + 1] = wall_clock64();
+              pb[t * 4 + 2] = rounds;
+              pb[t * 4 + 3] = __popcll(kept);
+            }
           }
           if (nk >= post || t == nbv - 1) {
             tf = t;
             break;
           }
 #pragma unroll
-          for (int c2 = k + 1; c2 < NMSC_PER; ++c2) rm[c2] |= __ballot((row[c2] & kept) != 0ull);
+          for (int c2 = k + 1; c2 < PER; ++c2) rm[c2] |= __ballot((row[c2] & kept) != 0ull);
         }
         if (lane == 0) s_flag[1] = tf;
       }
       __syncthreads();
+      if (pw && tid == 0) pw[2] = wall_clock64();
       tf = s_flag[1];
       assemble = tf >= 0;
+      // every workgroup writes the output rows of its own kept boxes (their slots are final: all
+      // below the kept count); the final workgroup adds only the random pad
+      const int tend = tf >= 0 ? tf + 1 : hi;
+      for (int t = lo + wave; t < tend; t += 16) {
+        const uint64_t kept = s_kept[t];
+        if ((kept >> lane) & 1ull)
+          nms_write_row(boxes, scores, b, P, post, (t > 0 ? s_nk[t - 1] : 0) + __popcll(kept & ((1ull << lane) - 1ull)),
+                        t * 64 + lane, rois, out_scores, keep_idx);
+      }
     } else if (s_flag[2] && tid == 0) {
       n_keep_out[b] = -1;  // a poll gave up: the output of this image is not valid
     }
@@ -464,11 +497,12 @@ nms_reduce_mc_kernel(const float* __restrict__ boxes, const float* __restrict__ 
       if ((kept >> lane) & 1ull) keep_list[base + __popcll(kept & ((1ull << lane) - 1ull))] = t * 64 + lane;
     }
     __syncthreads();
-    nms_write_out(boxes, scores, b, P, post, tf >= 0 ? min(s_nk[tf], post) : 0, keep_list, rand_u, rois, out_scores,
-                  keep_idx, n_keep_out);
+    const int nk = tf >= 0 ? min(s_nk[tf], post) : 0;
+    nms_write_out(boxes, scores, b, P, post, nk, nk, keep_list, rand_u, rois, out_scores, keep_idx, n_keep_out);
   }
   // the last workgroup of the image to finish clears the records for the next reduce
   __syncthreads();
+  if (pw && tid == 0) pw[3] = wall_clock64();
   if (tid == 0)
     s_flag[3] = __hip_atomic_fetch_add(cnt, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1u;
   __syncthreads();
@@ -527,10 +561,19 @@ void nms_check(const float* boxes, const int32_t* n_valid, int B, int P, float t
                                                                  result);
 }
 
+static bool nms_probe() {
+  static const bool on = [] {
+    const char* e = getenv("MXR_NMS_PROBE");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
 int64_t nms_mask_words(int B, int P) {
   const int nb = div_up(P, 64);
-  // transposed mask, then the reducer's block records (2 words per block) and exit counters
-  return (int64_t)B * nb * nms_row_words(nb) + (int64_t)B * nb * 2 + B;
+  // transposed mask, then the reducer's block records (2 words per block) and exit counters,
+  // then (MXR_NMS_PROBE=1) the reducer's timeline, 8 words per block
+  return (int64_t)B * nb * nms_row_words(nb) + (int64_t)B * nb * 2 + B + (nms_probe() ? (int64_t)B * nb * 8 : 0);
 }
 
 void nms_mask(const float* boxes, const int32_t* n_valid, int B, int P, float thresh, uint64_t* mask,
@@ -542,13 +585,13 @@ void nms_mask(const float* boxes, const int32_t* n_valid, int B, int P, float th
 }
 
 static size_t nms_serial_lds(int nb, int post) { return 16 + (size_t)nb * 16 + (size_t)post * 4; }
-static size_t nms_mc_lds(int nb, int post) {
-  return (size_t)NMSC_TRI * 64 * 8 + (size_t)nb * 8 + NMSC_PER * 8 + (size_t)nb * 4 + (size_t)post * 4;
+static size_t nms_mc_lds(int nb, int post, int per = NMSC_PER) {
+  return (size_t)(per * (per + 1) / 2) * 64 * 8 + (size_t)nb * 8 + per * 8 + (size_t)nb * 4 + (size_t)post * 4;
 }
 
 size_t nms_reduce_lds(int P, int post) {
   const int nb = div_up(P, 64);
-  return std::max(nms_serial_lds(nb, post), nms_mc_lds(nb, post));
+  return std::max(nms_serial_lds(nb, post), nms_mc_lds(nb, post, 16));
 }
 
 bool nms_keep_in_lds(int P, int post) { return nms_reduce_lds(P, post) <= 160 * 1024; }
@@ -570,9 +613,19 @@ void nms_reduce(const float* boxes, const float* scores, const int32_t* n_valid,
   }
   // the records follow the mask (nms_mask_words); written here, cleared by nms_mask and by the kernel
   uint64_t* rec = const_cast<uint64_t*>(mask) + (int64_t)B * nb * nms_row_words(nb);
-  dim3 grid(div_up(nb, NMSC_PER), B);
-  nms_reduce_mc_kernel<<<grid, 1024, nms_mc_lds(nb, lpost), st>>>(boxes, scores, n_valid, mask, rec, P, nb, post,
-                                                                  rand_u, rois, out_scores, keep_idx, n_keep, keep_ws);
+  static const int per = [] {
+    const char* e = getenv("MXR_NMS_PER");
+    return e && atoi(e) == 16 ? 16 : NMSC_PER;
+  }();
+  dim3 grid(div_up(nb, per), B);
+  uint64_t* probe = nms_probe() ? rec + (int64_t)B * nb * 2 + B : nullptr;
+  if (per == 16)
+    nms_reduce_mc_kernel<16><<<grid, 1024, nms_mc_lds(nb, lpost, 16), st>>>(boxes, scores, n_valid, mask, rec, P, nb,
+                                                                          post, rand_u, rois, out_scores, keep_idx,
+                                                                          n_keep, keep_ws, probe);
+  else
+    nms_reduce_mc_kernel<NMSC_PER><<<grid, 1024, nms_mc_lds(nb, lpost), st>>>(
+        boxes, scores, n_valid, mask, rec, P, nb, post, rand_u, rois, out_scores, keep_idx, n_keep, keep_ws, probe);
 }
 
 }  // namespace mxr

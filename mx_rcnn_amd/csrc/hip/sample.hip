@@ -62,8 +62,21 @@ __device__ int select_smallest(int n, int count, int k, Pool pool, Key key, SelS
       for (int e = threadIdx.x; e < c; e += blockDim.x) {
         const float ke = s.key[e];
         const int ie = s.idx[e];
-        int r = 0;
-        for (int j = 0; j < c; ++j) {
+        int r = 0, j = 0;
+        // 8 candidates per step: their (broadcast) LDS reads are issued together, so the loop pays
+        // one LDS latency per 8 comparisons instead of one per comparison
+        for (; j + 8 <= c; j += 8) {
+          float kj[8];
+          int ij[8];
+#pragma unroll
+          for (int u = 0; u < 8; ++u) {
+            kj[u] = s.key[j + u];
+            ij[u] = s.idx[j + u];
+          }
+#pragma unroll
+          for (int u = 0; u < 8; ++u) r += (kj[u] < ke) || (kj[u] == ke && ij[u] < ie);
+        }
+        for (; j < c; ++j) {
           const float kj = s.key[j];
           r += (kj < ke) || (kj == ke && s.idx[j] < ie);
         }

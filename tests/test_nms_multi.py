@@ -1,5 +1,5 @@
 """Multi-workgroup NMS reducer (csrc/hip/nms.hip nms_reduce_mc_kernel): a chain of workgroups,
-each owning 16 column blocks, handing kept words to later workgroups through per-block records.
+each owning 8 column blocks, handing kept words to later workgroups through per-block records.
 Checked on batches whose images have different valid counts (0, under one block, block-aligned,
 odd), with and without early exit at `post`, against the device flag-loop oracle and the fp32
 CPU greedy loop; and with one mask buffer reduced twice (the records clean themselves)."""

@@ -67,28 +67,6 @@ __host__ __device__ __forceinline__ int64_t nms_row_words(int nb) { return (int6
 // index of lane l's word of column block cb within a row block
 __device__ __forceinline__ int64_t nms_col(int cb, int l) { return (int64_t)(cb >> 1) * 128 + l * 2 + (cb & 1); }
 
-// iou_plus1(a, b) > t -- the same decision bit for bit (fp32 division, round to nearest) -- with the
-// division only on near-threshold pairs.  d = inter - t * uni, a = fma(-t, uni, inter) = RN(d):
-//   a <= 0             -> d <= 0 (or a positive d below the smallest float) -> RN(inter/uni) <= t;
-//   a > ulp(t) * uni   -> d > ulp(t) * uni / (1 + 2^-24) > ulp(t) / 2 * uni  -> inter/uni lies above
-//                         the midpoint of t and its successor -> RN(inter/uni) > t;
-// ulp(t) is a power of two, so ulp(t) * uni is exact.  The band between, a union below 1 and any
-// non-finite value take the division.
-__device__ __forceinline__ bool iou_gt_plus1(float ax1, float ay1, float ax2, float ay2, float aarea, float bx1,
-                                             float by1, float bx2, float by2, float barea, float t, float ulp_t) {
-  const float iw = fminf(ax2, bx2) - fmaxf(ax1, bx1) + 1.f;
-  const float ih = fminf(ay2, by2) - fmaxf(ay1, by1) + 1.f;
-  if (iw <= 0.f || ih <= 0.f) return 0.f > t;
-  const float inter = iw * ih;
-  const float uni = aarea + barea - inter;
-  if (uni >= 1.f && uni < INFINITY && inter < INFINITY) {
-    const float a = __builtin_fmaf(-t, uni, inter);
-    if (a <= 0.f) return false;
-    if (a > ulp_t * uni) return true;
-  }
-  return inter / uni > t;
-}
-
 __global__ void __launch_bounds__(256)
 nms_mask_kernel(const float* __restrict__ boxes, const int32_t* __restrict__ n_valid, int P, int nb,
                 float thresh, uint64_t* __restrict__ maskT, uint64_t* __restrict__ rec) {
@@ -119,11 +97,10 @@ nms_mask_kernel(const float* __restrict__ boxes, const int32_t* __restrict__ n_v
   if (j < nv) {
     const float4 c = bx[j];
     const float carea = (c.z - c.x + 1.f) * (c.w - c.y + 1.f);
-    const float ulp_t = nextafterf(thresh, INFINITY) - thresh;
     const int iend = min(64, j - row0);  // rows i with row0 + i < j (all < nv since j < nv)
     for (int i = 0; i < iend; ++i) {
       const float4 r = rbox[i];
-      if (iou_gt_plus1(r.x, r.y, r.z, r.w, rarea[i], c.x, c.y, c.z, c.w, carea, thresh, ulp_t)) bits |= (1ull << i);
+      if (iou_plus1(r.x, r.y, r.z, r.w, rarea[i], c.x, c.y, c.z, c.w, carea) > thresh) bits |= (1ull << i);
     }
   }
   maskT[((int64_t)b * nb + rb) * Pp + nms_col(cb, lane)] = bits;

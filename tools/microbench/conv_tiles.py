@@ -21,6 +21,13 @@ SHAPES = {
     's2_3x3': (1, 128, 100, 167, 128, 3, 1, 1),
     's2_1x1a': (1, 512, 100, 167, 128, 1, 1, 0),
     's3_3x3': (1, 256, 50, 84, 256, 3, 1, 1),
+    # grid-fill study: the stage-3 3x3 / 1x1 at M giving 200, 256, 264 (= s3_*) and 512 64x64 tiles
+    'g200_3x3': (1, 256, 40, 80, 256, 3, 1, 1),
+    'g256_3x3': (1, 256, 64, 64, 256, 3, 1, 1),
+    'g512_3x3': (1, 256, 64, 128, 256, 3, 1, 1),
+    'g200_1x1a': (1, 1024, 40, 80, 256, 1, 1, 0),
+    'g256_1x1a': (1, 1024, 64, 64, 256, 1, 1, 0),
+    'g512_1x1a': (1, 1024, 64, 128, 256, 1, 1, 0),
     's3_1x1a': (1, 1024, 50, 84, 256, 1, 1, 0),
     's3_1x1b': (1, 256, 50, 84, 1024, 1, 1, 0),
     'rpn_3x3': (1, 1024, 50, 84, 512, 3, 1, 1),

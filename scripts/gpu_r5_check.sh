@@ -13,7 +13,7 @@ for d in ${TRACE:-fp32 bf16}; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/prof_$d -o run -- \
     python bench.py --steps 10 --warmup 3 --dtype $d --no-bf16-extra ${BENCH_ARGS:-} > $OUT/prof_$d.log 2>&1 || { tail -20 $OUT/prof_$d.log; exit 1; }
   T=$(find $OUT/prof_$d -name '*kernel_trace.csv' | head -1)
-  python tools/trace_groups.py "$T" --steps 10 --top 70 > $OUT/trace_${d}_groups.txt 2>&1
+  python tools/trace_groups.py "$T" --steps 10 --top 200 > $OUT/trace_${d}_groups.txt 2>&1
   python tools/trace_shapes.py "$T" 10 nms_reduce > $OUT/trace_${d}_launch_shapes.txt 2>&1
   python tools/stream_overlap.py "$T" --steps 5 > $OUT/trace_${d}_stream_overlap.txt 2>&1
   head -3 $OUT/trace_${d}_stream_overlap.txt | cut -c1-200

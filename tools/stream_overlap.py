@@ -32,7 +32,7 @@ def main():
         busy = sum(int(r['End_Timestamp']) - int(r['Start_Timestamp']) for r in rs)
         top = collections.Counter()
         for r in rs:
-            top[r['Kernel_Name'].split('(')[0][:48]] += int(r['End_Timestamp']) - int(r['Start_Timestamp'])
+            top[r['Kernel_Name'].replace('(anonymous namespace)::', '').split('(')[0][:48]] += int(r['End_Timestamp']) - int(r['Start_Timestamp'])
         print('queue %s: %.1f launches/step, busy %.3f ms/step; top: %s' % (
             q, len(rs) / n, busy / n / 1e6, ', '.join('%s %.2f' % (k, v / n / 1e6) for k, v in top.most_common(4))))
     iv = sorted((int(r['Start_Timestamp']), min(int(r['End_Timestamp']), t1), r['Kernel_Name']) for r in seg)
@@ -51,7 +51,7 @@ def main():
         union / n / 1e6, (t1 - t0 - union) / n / 1e6, len(gaps) / n))
     agg = collections.Counter()
     for g, before, after in gaps:
-        agg[(before.split('(')[0][:40], after.split('(')[0][:40])] += g
+        agg[(before.replace('(anonymous namespace)::', '').split('(')[0][:48], after.replace('(anonymous namespace)::', '').split('(')[0][:48])] += g
     print('largest idle transitions (us/step):')
     for (b, f), g in agg.most_common(a.gaps):
         print('  %7.1f  %s -> %s' % (g / n / 1e3, b, f))

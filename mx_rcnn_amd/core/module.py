@@ -191,6 +191,8 @@ class MutableModule(object):
     def install_monitor(self, mon):
         self._monitor = mon
         mon.install(self.model)
+        # the monitor reads gradients: no update may be fused into a weight-gradient kernel
+        self.trainer.fused_fc_sgd = []
 
     # ------------------------------------------------------------------ step API
     def forward(self, data_batch, is_train=None):

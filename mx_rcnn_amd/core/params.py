@@ -108,6 +108,7 @@ class FlatParamStore:
             groups.setdefault((lowp, decay), []).append((n, m, attr, p.numel(), tuple(p.shape), cl))
         self.groups = [ParamGroup(k, v, dev, compute_dtype, self.x2) for k, v in sorted(groups.items())]
         self.params = {}
+        self._fused = {}  # group index -> fused-update specs (enable_fused_sgd)
         with torch.no_grad():
             for g in self.groups:
                 off = 0
@@ -354,13 +355,67 @@ class FlatParamStore:
         (the reducer's fp32 all-reduce buffer under data parallelism; default ``group.grad``).
         ``refresh=False``: the caller rebuilds the dgrad cache itself (Trainer.step_body does, at
         the start of the next step, concurrently with its forward pass).  ``clear``: the update
-        kernel zeroes each group's gradient buffer after reading it (replaces zero_grad)."""
-        for g in self.groups:
+        kernel zeroes each group's gradient buffer after reading it (replaces zero_grad).
+        Parameters whose update ran fused into their weight gradient this step
+        (enable_fused_sgd) are skipped."""
+        for gi, g in enumerate(self.groups):
             grad = grad_for(g) if grad_for is not None else g.grad
-            sgd_momentum_(g.master, g.mom, grad, lr, momentum, wd if g.decay else 0.0, rescale, clip, g.shadow,
-                          planes=g.x2 or 1, zero=g.grad if clear else None)
+            skip = sorted((sp['off'], sp['off'] + sp['numel']) for sp in self._fused.get(gi, ()) if sp['applied'])
+            for sp in self._fused.get(gi, ()):
+                sp['applied'] = False
+            if not skip:
+                sgd_momentum_(g.master, g.mom, grad, lr, momentum, wd if g.decay else 0.0, rescale, clip, g.shadow,
+                              planes=g.x2 or 1, zero=g.grad if clear else None)
+                continue
+            cuts, at = [], 0
+            for s0, e0 in skip:
+                if s0 > at:
+                    cuts.append((at, s0))
+                at = max(at, e0)
+            if at < g.numel:
+                cuts.append((at, g.numel))
+            for s0, e0 in cuts:  # the complement of the fused ranges
+                if g.x2:
+                    sh, pst = g.shadow[s0:], g.plane
+                else:
+                    sh, pst = (g.shadow[s0:e0] if g.shadow is not None else None), 0
+                sgd_momentum_(g.master[s0:e0], g.mom[s0:e0], grad[s0:e0], lr, momentum, wd if g.decay else 0.0, rescale,
+                              clip, sh, planes=g.x2 or 1, zero=g.grad[s0:e0] if clear else None, plane_stride=pst)
         if refresh:
             self.refresh_dgrad_cache()
+
+    def enable_fused_sgd(self, names, lr, momentum=0.9, wd=0.0005, rescale=1.0, clip=-1.0):
+        """Let the weight-gradient kernels of parameters ``names`` apply their SGD update in place
+        (csrc conv_wgrad_sgd: the gradient is never stored; ops/vgg_fused.py).  Only parameters whose
+        flat offset keeps the kernel's 16-B rows aligned qualify.  Returns the enabled names."""
+        self.disable_fused_sgd()
+        done = []
+        if self.device.type != 'cuda':
+            return done
+        for gi, g in enumerate(self.groups):
+            for (n, _, _, numel, shape, cl), off in zip(g.entries, g.offsets):
+                if n not in names or off % 8 or numel % 8:
+                    continue
+                if g.x2:
+                    sh, planes, pst = g.shadow[off:], g.x2, g.plane
+                else:
+                    sh, planes, pst = (g.shadow[off:off + numel] if g.shadow is not None else None), 1, 0
+                spec = {'w': g.master[off:off + numel], 'mom': g.mom[off:off + numel], 'shadow': sh, 'planes': planes,
+                        'plane_stride': pst, 'lr': lr, 'momentum': float(momentum),
+                        'wd': float(wd) if g.decay else 0.0, 'rescale': float(rescale), 'clip': float(clip),
+                        'grad_bf16': g.grad.dtype == torch.bfloat16, 'off': off, 'numel': numel, 'applied': False}
+                grad_sink.set_fused_sgd(self.params[n], spec)
+                self._fused.setdefault(gi, []).append(spec)
+                done.append(n)
+        return done
+
+    def disable_fused_sgd(self):
+        for specs in getattr(self, '_fused', {}).values():
+            for sp in specs:
+                sp['applied'] = False
+        for p in self.params.values():
+            grad_sink.set_fused_sgd(p, None)
+        self._fused = {}
 
     def master_param(self, name):
         for g in self.groups:

@@ -9,6 +9,7 @@ import os
 
 import torch
 
+from ..ops import grad_sink
 from ..parallel.reducer import BucketReducer
 from ..utils import profiler as prof
 from .params import FlatParamStore
@@ -60,6 +61,14 @@ class Trainer:
         if lr_scheduler is not None:
             lr_scheduler.base_lr = lr
         self.lr_t = torch.full((1,), float(lr), dtype=torch.float32, device=dev)
+        # VGG16's FC weights take their update inside their weight-gradient kernel: the 120 M-element
+        # gradient is never written, read or cleared (core/params.py enable_fused_sgd,
+        # ops/vgg_fused.py); single process with the end-of-step optimizer only
+        self.fused_fc_sgd = []
+        if (dev.type == 'cuda' and not self.reducer.dp and not self.reducer.sgd_capable and
+                os.environ.get('MXR_FUSED_FC_SGD', '1') != '0'):
+            self.fused_fc_sgd = self.store.enable_fused_sgd(('fc6_weight', 'fc7_weight'), self.lr_t, momentum, wd,
+                                                            rescale_grad, clip_gradient)
         self.num_update = 0
         # step counter of the counter-based dropout (ops/fc.py), advanced on the device at the end
         # of every step (inside the captured graph), so a replayed graph draws a fresh mask every
@@ -141,24 +150,26 @@ class Trainer:
         # a model that starts part of its backward inside forward (the e2e graph's early RPN
         # backward) joins the filter cache first
         self.model.pre_backward = cache_join
-        try:
-            out = self.forward(b)
-        finally:
-            self.model.pre_backward = None
-        if self.fault is not None:  # test hook: multiplies the loss by NaN on the armed step
-            out['loss'] = out['loss'] * self.fault
-            out['objective'] = out['objective'] * self.fault
-        # device-side non-finite guard: no host sync, read every `frequent` steps;
-        # counted by the model's loss-combine kernel unless fault injection is armed
-        if self.model.nonfinite_counter is None:
-            self.nonfinite.add_((~torch.isfinite(out['objective'])).to(torch.int32))
-        cache_join()
-        with prof.range('backward+allreduce'):
-            from ..ops.fused import defer_reduces
-            # no gradient hook reads the flat buffers mid-backward: split-K reduces may cross units
-            with defer_reduces(not (self.reducer.overlap or self.reducer.sgd_capable)):
-                from ..ops._ext import unit_grad
-                out['loss'].backward(unit_grad(out['loss'].device))
+        # forward (the e2e graph's early RPN backward) and backward may apply fused FC updates
+        with grad_sink.fused_sgd_scope(bool(self.fused_fc_sgd)):
+            try:
+                out = self.forward(b)
+            finally:
+                self.model.pre_backward = None
+            if self.fault is not None:  # test hook: multiplies the loss by NaN on the armed step
+                out['loss'] = out['loss'] * self.fault
+                out['objective'] = out['objective'] * self.fault
+            # device-side non-finite guard: no host sync, read every `frequent` steps;
+            # counted by the model's loss-combine kernel unless fault injection is armed
+            if self.model.nonfinite_counter is None:
+                self.nonfinite.add_((~torch.isfinite(out['objective'])).to(torch.int32))
+            cache_join()
+            with prof.range('backward+allreduce'):
+                from ..ops.fused import defer_reduces
+                # no gradient hook reads the flat buffers mid-backward: split-K reduces may cross units
+                with defer_reduces(not (self.reducer.overlap or self.reducer.sgd_capable)):
+                    from ..ops._ext import unit_grad
+                    out['loss'].backward(unit_grad(out['loss'].device))
         with prof.range('allreduce_wait'):
             self.reducer.finish()
         with prof.range('sgd'):

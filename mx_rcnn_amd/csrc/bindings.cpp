@@ -1955,6 +1955,69 @@ Tensor conv_wgrad(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int
   return dw;
 }
 
+// Weight gradient of (dy, x) applied at once as an SGD-momentum update of the parameter (w / mom
+// fp32 flat views, `shadow` its bf16 copy or x2 / x3 planes `plane_stride` apart) -- the gradient
+// is never stored (the VGG16 FC weights: ops/vgg_fused.py, core/params.py fused_sgd).  grad_bf16:
+// round the gradient as the unfused bf16 path stores it.
+void conv_wgrad_sgd(const Tensor& dy, const Tensor& x, int64_t KH, int64_t KW, int64_t stride, int64_t pad, int64_t x2,
+                    Tensor w, Tensor mom, c10::optional<Tensor> shadow, int64_t planes, int64_t plane_stride,
+                    const Tensor& lr, double momentum, double wd, double rescale, double clip, bool grad_bf16) {
+  CHECK_DEV(dy); CHECK_DEV(x); CHECK_DEV(w); CHECK_DEV(mom); CHECK_DEV(lr);
+  TORCH_CHECK(dy.scalar_type() == at::kBFloat16 && x.scalar_type() == at::kBFloat16, "bf16 only");
+  TORCH_CHECK(dy.is_contiguous(at::MemoryFormat::ChannelsLast) && x.is_contiguous(at::MemoryFormat::ChannelsLast),
+              "dy/x must be channels_last");
+  TORCH_CHECK(!x2 || x.size(0) % npl(x2) == 0, "x2: (2N, ...) pairs");
+  const int NB = (int)(x2 ? x.size(0) / npl(x2) : x.size(0)), Cin = (int)x.size(1), H = (int)x.size(2), W = (int)x.size(3);
+  const int Cout = (int)dy.size(1), Ho = (int)dy.size(2), Wo = (int)dy.size(3);
+  TORCH_CHECK(dy.size(0) == x.size(0), "batch mismatch");
+  TORCH_CHECK(Ho == (H + 2 * pad - KH) / stride + 1 && Wo == (W + 2 * pad - KW) / stride + 1, "geometry mismatch");
+  const int64_t n = (int64_t)Cout * KH * KW * Cin;
+  TORCH_CHECK(w.scalar_type() == at::kFloat && mom.scalar_type() == at::kFloat && w.is_contiguous() &&
+                  mom.is_contiguous() && w.numel() == n && mom.numel() == n,
+              "w / mom: contiguous fp32 of Cout * KH * KW * Cin elements");
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(w.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(mom.data_ptr()) % 16 == 0,
+              "w / mom: 16-B aligned");
+  TORCH_CHECK(lr.scalar_type() == at::kFloat && lr.numel() >= 1, "lr: fp32 device scalar");
+  mxr::WgradSgd sg;
+  sg.w = w.data_ptr<float>();
+  sg.mom = mom.data_ptr<float>();
+  sg.lr = lr.data_ptr<float>();
+  sg.mu = (float)momentum;
+  sg.wd = (float)wd;
+  sg.rescale = (float)rescale;
+  sg.clip = (float)clip;
+  sg.gbf16 = grad_bf16 ? 1 : 0;
+  if (shadow.has_value() && shadow->defined()) {
+    TORCH_CHECK(shadow->scalar_type() == at::kBFloat16 && shadow->is_contiguous() && planes >= 1 && planes <= 3,
+                "shadow: contiguous bf16, 1-3 planes");
+    if (planes > 1) {
+      TORCH_CHECK(plane_stride >= n && plane_stride % 4 == 0 && shadow->numel() >= (planes - 1) * plane_stride + n &&
+                      reinterpret_cast<uintptr_t>(shadow->data_ptr()) % 8 == 0,
+                  "shadow planes: 8-B aligned, plane_stride >= numel and a multiple of 4");
+      sg.plane = plane_stride;
+      sg.x3 = planes == 3 ? 1 : 0;
+    } else {
+      TORCH_CHECK(shadow->numel() >= n && reinterpret_cast<uintptr_t>(shadow->data_ptr()) % 16 == 0,
+                  "shadow: 16-B aligned bf16 of numel elements");
+    }
+    sg.wb = reinterpret_cast<uint16_t*>(shadow->data_ptr());
+  }
+  mxr::WgradX2 wx2;
+  if (x2) {
+    TORCH_CHECK(x.numel() < (int64_t)0x40000000 && dy.numel() < (int64_t)0x40000000, "x2: planes beyond 2 GB");
+    wx2.x2 = 1;
+    wx2.x3 = npl(x2) == 3 ? 1 : 0;
+    wx2.pdy = (uint32_t)(dy.numel() / npl(x2) * 2);
+    wx2.px = (uint32_t)(x.numel() / npl(x2) * 2);
+  }
+  DevGuard g(x.device());
+  const int r = mxr::conv_wgrad_sgd(reinterpret_cast<const uint16_t*>(dy.data_ptr()),
+                                    reinterpret_cast<const uint16_t*>(x.data_ptr()), NB, H, W, Cin, Ho, Wo, Cout,
+                                    (int)KH, (int)KW, (int)stride, (int)pad, cur_stream(), wx2, sg);
+  TORCH_CHECK(r > 0, "conv_wgrad_sgd: unsupported shape (Cin % 64, Cout % 8, 32-bit buffer offsets)");
+  LAUNCH_CHECK("conv_wgrad_sgd");
+}
+
 }  // namespace
 
 // ---- CPU twin of the proposal NMS (host C++, the CPU configuration and the test oracle's
@@ -2213,6 +2276,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("nms_proposals", &nms_proposals, py::arg("boxes"), py::arg("scores"), py::arg("n_valid"), py::arg("thresh"),
         py::arg("post"), py::arg("rand_u"), py::arg("mask") = py::none());
   m.def("nms_mask_build", &nms_mask_build);
+  m.def("conv_wgrad_sgd", &conv_wgrad_sgd, py::arg("dy"), py::arg("x"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
+        py::arg("pad"), py::arg("x2"), py::arg("w"), py::arg("mom"), py::arg("shadow"), py::arg("planes"),
+        py::arg("plane_stride"), py::arg("lr"), py::arg("momentum"), py::arg("wd"), py::arg("rescale"),
+        py::arg("clip"), py::arg("grad_bf16"));
   m.def("nms_check", &nms_check);
   m.def("nms_cpu", &nms_cpu, py::arg("boxes"), py::arg("n_valid"), py::arg("thresh"), py::arg("max_keep"),
         py::arg("fp32") = false);

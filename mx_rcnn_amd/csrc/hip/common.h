@@ -257,6 +257,17 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// One SGD-momentum update (MXNet sgd_mom_update: g = clip(rescale * g); mom = mu * mom - lr * (g +
+// wd * w); w += mom): the SGD kernels (sgd.hip) and the fused wgrad + SGD epilogue (wgrad_body.h)
+// share it, so both paths round identically.
+__device__ __forceinline__ float sgd_one(float w, float& m, float g, float lr, float mu, float wd, float rescale,
+                                         float clip) {
+  g *= rescale;
+  if (clip > 0.f) g = fminf(fmaxf(g, -clip), clip);
+  m = mu * m - lr * (g + wd * w);
+  return w + m;
+}
+
 // Box IoU with the +1 pixel convention (reference: bbox_overlaps / nms).
 __device__ __forceinline__ float iou_plus1(float ax1, float ay1, float ax2, float ay2, float aarea,
                                            float bx1, float by1, float bx2, float by2, float barea) {

@@ -232,4 +232,38 @@ int conv_wgrad(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab,
   return splits;
 }
 
+int conv_wgrad_sgd(const uint16_t* dy, const uint16_t* x, int NB, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH,
+                   int KW, int stride, int pad, hipStream_t st, const WgradX2& x2, const WgradSgd& sgd) {
+  if (Cin % WG_BN != 0 || Cout % 8 != 0 || !sgd.w || !sgd.mom || !sgd.lr) return -1;
+  const int P = NB * Ho * Wo;
+  const bool buf_ok = (int64_t)P * Cout * 2 < (int64_t)kWgOOB && (int64_t)NB * H * W * Cin * 2 < (int64_t)kWgOOB;
+  if (!buf_ok) return -1;
+  if (x2.x2 && ((int64_t)P * Cout * 2 + (x2.x3 ? 2 : 1) * (int64_t)x2.pdy >= (int64_t)kWgOOB ||
+                (int64_t)NB * H * W * Cin * 2 + (x2.x3 ? 2 : 1) * (int64_t)x2.px >= (int64_t)kWgOOB))
+    return -1;
+  WgradParams p = wgrad_params(dy, x, nullptr, nullptr, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, 1, 0);
+  p.x2 = x2.x2;
+  p.x3 = x2.x3;
+  p.x2_pdy = x2.pdy;
+  p.x2_px = x2.px;
+  p.sgd_w = sgd.w;
+  p.sgd_mom = sgd.mom;
+  p.sgd_wb = sgd.wb;
+  p.sgd_plane = sgd.plane;
+  p.sgd_x3 = sgd.x3;
+  p.sgd_gbf16 = sgd.gbf16;
+  p.sgd_lr = sgd.lr;
+  p.sgd_mu = sgd.mu;
+  p.sgd_wd = sgd.wd;
+  p.sgd_rescale = sgd.rescale;
+  p.sgd_clip = sgd.clip;
+  if (p.x3)
+    conv_wgrad_buf_kernel<3, true, true><<<p.ntiles, 256, 0, st>>>(p);
+  else if (p.x2)
+    conv_wgrad_buf_kernel<3, true><<<p.ntiles, 256, 0, st>>>(p);
+  else
+    conv_wgrad_buf_kernel<3><<<p.ntiles, 256, 0, st>>>(p);
+  return 1;
+}
+
 }  // namespace mxr

@@ -15,14 +15,6 @@
 
 namespace mxr {
 
-__device__ __forceinline__ float sgd_one(float w, float& m, float g, float lr, float mu, float wd, float rescale,
-                                         float clip) {
-  g *= rescale;
-  if (clip > 0.f) g = fminf(fmaxf(g, -clip), clip);
-  m = mu * m - lr * (g + wd * w);
-  return w + m;
-}
-
 template <bool GBF16>
 __global__ void __launch_bounds__(256)
 sgd_kernel(float* __restrict__ w, float* __restrict__ mom, const void* grad, int64_t n,

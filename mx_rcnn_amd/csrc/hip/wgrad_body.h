@@ -74,6 +74,16 @@ struct WgradParams {
   int x3 = 0;
   uint32_t x2_pdy = 0, x2_px = 0;  // lo-plane offsets, bytes
   float* dwf = nullptr;
+  // fused SGD-momentum (sgd_w set, splits == 1): the tile's gradient updates the parameter in place
+  // -- fp32 master, momentum and the shadow the next forward reads -- instead of being stored;
+  // the gradient is rounded as the unfused path would have stored it (bf16 when sgd_gbf16)
+  float* sgd_w = nullptr;
+  float* sgd_mom = nullptr;
+  uint16_t* sgd_wb = nullptr;  // bf16 shadow, or the x2 / x3 planes sgd_plane elements apart
+  int64_t sgd_plane = 0;
+  int sgd_x3 = 0, sgd_gbf16 = 0;
+  const float* sgd_lr = nullptr;
+  float sgd_mu = 0.f, sgd_wd = 0.f, sgd_rescale = 1.f, sgd_clip = -1.f;
 };
 
 constexpr int kWgradLdsElems = 3 * 2 * WG_BK * 64;  // the S = 3 ring: [S][dY|X][64 px][64 ch] (48 KB)
@@ -338,6 +348,33 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
       a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
     }
     const int64_t o = (int64_t)co * ldk + k0 + cv * 8;
+    if (p.sgd_w) {  // fused update (the host guarantees splits == 1 and 16-B aligned rows)
+      float g[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+      if (p.sgd_gbf16) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) g[k] = bf16_to_f32(f32_to_bf16(g[k]));
+      }
+      const float lr = *p.sgd_lr;
+      float4* wp = reinterpret_cast<float4*>(p.sgd_w + o);
+      float4* mp = reinterpret_cast<float4*>(p.sgd_mom + o);
+      const float4 w0 = wp[0], w1 = wp[1], m0 = mp[0], m1 = mp[1];
+      float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      float mv[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
+#pragma unroll
+      for (int k = 0; k < 8; ++k) wv[k] = sgd_one(wv[k], mv[k], g[k], lr, p.sgd_mu, p.sgd_wd, p.sgd_rescale, p.sgd_clip);
+      wp[0] = make_float4(wv[0], wv[1], wv[2], wv[3]);
+      wp[1] = make_float4(wv[4], wv[5], wv[6], wv[7]);
+      mp[0] = make_float4(mv[0], mv[1], mv[2], mv[3]);
+      mp[1] = make_float4(mv[4], mv[5], mv[6], mv[7]);
+      if (p.sgd_wb && p.sgd_plane) {
+        const int code = p.sgd_x3 ? kCodeX3 : kCodeX2;
+        st4c(p.sgd_wb, o, code, p.sgd_plane, wv);
+        st4c(p.sgd_wb, o + 4, code, p.sgd_plane, wv + 4);
+      } else if (p.sgd_wb) {
+        st8_bf16(p.sgd_wb + o, wv);
+      }
+      continue;
+    }
     if (splits > 1) {
       float4* d = reinterpret_cast<float4*>(slab + (int64_t)split * Cout * ldk + o);
       d[0] = a0;

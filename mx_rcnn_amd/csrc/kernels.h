@@ -412,6 +412,22 @@ void wgrad_reduce_run(const float* slab, int splits, int64_t n, uint16_t* dw, hi
 int conv_wgrad(const uint16_t* dy, const uint16_t* x, uint16_t* dw, float* slab, int NB, int H, int W, int Cin,
                int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, int splits, int accumulate,
                hipStream_t st, int variant = 0, const WgradX2& x2 = WgradX2());
+// Weight gradient with a fused SGD-momentum update (no split, one pass): the gradient of every
+// (Cout, KH*KW*Cin) element updates w / mom / the shadow wb (bf16, or x2 / x3 planes `plane`
+// elements apart) in place with the SGD kernel's arithmetic; gbf16: the gradient rounds to bf16
+// first (what the unfused bf16 path stores).  Every row must start 16-B aligned (w, mom) and the
+// planes 8-B aligned.  Returns 1, or -1 when the shape is unsupported.
+struct WgradSgd {
+  float* w = nullptr;
+  float* mom = nullptr;
+  uint16_t* wb = nullptr;
+  int64_t plane = 0;
+  int x3 = 0, gbf16 = 0;
+  const float* lr = nullptr;
+  float mu = 0.f, wd = 0.f, rescale = 1.f, clip = -1.f;
+};
+int conv_wgrad_sgd(const uint16_t* dy, const uint16_t* x, int NB, int H, int W, int Cin, int Ho, int Wo, int Cout, int KH,
+                   int KW, int stride, int pad, hipStream_t st, const WgradX2& x2, const WgradSgd& sgd);
 
 // ---- small-head backward (head_bwd.hip) ---------------------------------------------------------
 // One or two heads y_h = X W_h^T (+b_h) over the same X (M, K) bf16, K % 64 == 0, dY_h (M, N_h):

@@ -44,3 +44,39 @@ def clear_hooks(params):
 def delivered(param):
     for fn in param.__dict__.get('_mxr_hooks', ()):
         fn(param)
+
+
+# ---- fused SGD (core/params.py FlatParamStore.enable_fused_sgd) --------------------------------
+# A parameter may carry a spec for an update fused into its weight-gradient kernel (the VGG16 FC
+# weights: ops/vgg_fused.py).  Producers use it only inside an active scope (Trainer step bodies);
+# they mark it applied, and the store's SGD then skips that parameter's range for the step.
+_SCOPE = [False]
+
+
+class fused_sgd_scope:
+    def __init__(self, on):
+        self.on = bool(on)
+
+    def __enter__(self):
+        self.prev = _SCOPE[0]
+        _SCOPE[0] = self.on
+        return self
+
+    def __exit__(self, *exc):
+        _SCOPE[0] = self.prev
+        return False
+
+
+def set_fused_sgd(param, spec):
+    if spec is None:
+        param.__dict__.pop('_mxr_fsgd', None)
+    else:
+        param.__dict__['_mxr_fsgd'] = spec
+
+
+def fused_sgd(param):
+    """The fused-update spec of ``param`` when the current step may apply it, else None."""
+    if param is None or not _SCOPE[0]:
+        return None
+    return param.__dict__.get('_mxr_fsgd')
+

@@ -90,8 +90,21 @@ def _layer_backward(d, x, w, wparam, need_w, need_x, k, pad, rmask=None, rmask_s
     shape4 = (w.shape[0], _kdim(w, k), k, k)
     wk, kw = _wargs(w, shape4)
     kw = dict(kw, bt=True)
-    tgt = _wtarget(wparam, shape4) if need_w else None
     dx = dw = None
+    spec = grad_sink.fused_sgd(wparam) if need_w else None
+    if spec is not None:
+        # the parameter's SGD step rides in its weight gradient (core/params.py enable_fused_sgd):
+        # data gradient first (it reads the current filter), then the update; the gradient itself
+        # is never stored
+        if need_x:
+            dx = ext.conv_igemm_fwd(d, wk, None, 1, k - 1 - pad, False, rmask=rmask, rmask_scale=rmask_scale,
+                                    **kw)[0]
+        ext.conv_wgrad_sgd(d, x, k, k, 1, pad, int(x2 or 0), spec['w'], spec['mom'], spec['shadow'], spec['planes'],
+                           spec['plane_stride'], spec['lr'], spec['momentum'], spec['wd'], spec['rescale'],
+                           spec['clip'], spec['grad_bf16'])
+        spec['applied'] = True
+        return dx, None
+    tgt = _wtarget(wparam, shape4) if need_w else None
     if need_x and need_w and tgt is not None:
         dx = ext.conv_dgrad_wgrad(d, wk, k - 1 - pad, None, None, 0.0, False, None, None, None, None, d, x, k, k, 1, pad,
                                   tgt, rmask=rmask, rmask_scale=rmask_scale, **kw)[0]

@@ -293,7 +293,7 @@ __device__ __forceinline__ void nmsc_store(uint64_t* p, uint64_t v) {
 __host__ __device__ constexpr int nmsc_tri(int k, int c) { return c * (c + 1) / 2 + k; }
 
 template <int PER>
-__global__ void __launch_bounds__(1024)
+__global__ void __launch_bounds__(PER * 64)
 nms_reduce_mc_kernel(const float* __restrict__ boxes, const float* __restrict__ scores,
                      const int32_t* __restrict__ n_valid, const uint64_t* __restrict__ maskT, uint64_t* rec, int P,
                      int nb, int post, const float* __restrict__ rand_u, float* __restrict__ rois,
@@ -456,7 +456,7 @@ nms_reduce_mc_kernel(const float* __restrict__ boxes, const float* __restrict__ 
       // every workgroup writes the output rows of its own kept boxes (their slots are final: all
       // below the kept count); the final workgroup adds only the random pad
       const int tend = tf >= 0 ? tf + 1 : hi;
-      for (int t = lo + wave; t < tend; t += 16) {
+      for (int t = lo + wave; t < tend; t += PER) {
         const uint64_t kept = s_kept[t];
         if ((kept >> lane) & 1ull)
           nms_write_row(boxes, scores, b, P, post, (t > 0 ? s_nk[t - 1] : 0) + __popcll(kept & ((1ull << lane) - 1ull)),
@@ -468,7 +468,7 @@ nms_reduce_mc_kernel(const float* __restrict__ boxes, const float* __restrict__ 
   }
   if (assemble) {
     // keep list from the kept words: block t's boxes follow the s_nk[t - 1] boxes kept before it
-    for (int t = wave; t <= tf; t += 16) {
+    for (int t = wave; t <= tf; t += PER) {
       const uint64_t kept = s_kept[t];
       const int base = t > 0 ? s_nk[t - 1] : 0;
       if ((kept >> lane) & 1ull) keep_list[base + __popcll(kept & ((1ull << lane) - 1ull))] = t * 64 + lane;
@@ -597,11 +597,11 @@ void nms_reduce(const float* boxes, const float* scores, const int32_t* n_valid,
   dim3 grid(div_up(nb, per), B);
   uint64_t* probe = nms_probe() ? rec + (int64_t)B * nb * 2 + B : nullptr;
   if (per == 16)
-    nms_reduce_mc_kernel<16><<<grid, 1024, nms_mc_lds(nb, lpost, 16), st>>>(boxes, scores, n_valid, mask, rec, P, nb,
+    nms_reduce_mc_kernel<16><<<grid, 16 * 64, nms_mc_lds(nb, lpost, 16), st>>>(boxes, scores, n_valid, mask, rec, P, nb,
                                                                           post, rand_u, rois, out_scores, keep_idx,
                                                                           n_keep, keep_ws, probe);
   else
-    nms_reduce_mc_kernel<NMSC_PER><<<grid, 1024, nms_mc_lds(nb, lpost), st>>>(
+    nms_reduce_mc_kernel<NMSC_PER><<<grid, NMSC_PER * 64, nms_mc_lds(nb, lpost), st>>>(
         boxes, scores, n_valid, mask, rec, P, nb, post, rand_u, rois, out_scores, keep_idx, n_keep, keep_ws, probe);
 }
 

@@ -85,6 +85,7 @@ def main():
     ap.add_argument('--tiles', default='0,1,2,3,11,12,13,14,15,16')
     ap.add_argument('--splits', default='0,1,2,4,8')
     ap.add_argument('--wgrad', action='store_true', help='sweep conv_wgrad (variant x splits) instead')
+    ap.add_argument('--epi', action='store_true', help='forward with the bottleneck epilogue: bias + residual + ReLU')
     args = ap.parse_args()
     ext = need_ext()
     torch.manual_seed(0)
@@ -124,12 +125,22 @@ def main():
             w2 = wt.reshape(cout, cin)
             res['hipblaslt_us'] = round(timeit(lambda: F.linear(x2, w2)), 1)
         best = None
+        ekw = {}
+        if args.epi:  # the inference bottleneck's last conv: folded-BN bias, identity residual, ReLU
+            bias = torch.randn(cout, device='cuda').bfloat16()
+            resid = torch.randn_like(ref).bfloat16().contiguous(memory_format=torch.channels_last)
+            ref = torch.relu(ref + bias.float().view(1, -1, 1, 1) + resid.float())
+            ekw = {'bias': bias, 'relu': True, 'residual': resid}
         for tile in [int(t) for t in args.tiles.split(',')]:
             for sp in [int(v) for v in args.splits.split(',')]:
                 if tile == 0 and sp != 0:
                     continue
+                def call():
+                    if ekw:
+                        return ext.conv_igemm_fwd(x, wt, ekw['bias'], s, p, True, tile, sp, residual=ekw['residual'])
+                    return ext.conv_igemm_fwd(x, wt, None, s, p, False, tile, sp)
                 try:
-                    y = ext.conv_igemm_fwd(x, wt, None, s, p, False, tile, sp)[0]
+                    y = call()[0]
                 except RuntimeError as e:
                     res['t%d_s%d' % (tile, sp)] = 'err'
                     continue
@@ -137,7 +148,7 @@ def main():
                 if err > 2e-2:
                     res['t%d_s%d' % (tile, sp)] = 'BAD %.3g' % err
                     continue
-                us = timeit(lambda: ext.conv_igemm_fwd(x, wt, None, s, p, False, tile, sp))
+                us = timeit(call)
                 res['t%d_s%d' % (tile, sp)] = round(us, 1)
                 if best is None or us < best[0]:
                     best = (us, tile, sp)

@@ -10,7 +10,8 @@
 //                  as a kept-anchor bitmap + number of examples
 //   anchor_output  (grid over anchors): final labels in the reference (a, h, w) order and the
 //                  bbox target / inside / outside weights in (4A, H, W) planes
-//   proposal_sample (1 workgroup / image): gt rows appended to the proposals, fg / bg pools with
+//   proposal_sample (2 workgroups / image: the fg and the bg half of the sample): gt rows appended to
+//                  the proposals, fg / bg pools with
 //                  the reference fallbacks, fixed-size fg (with-replacement pad prepended) and bg
 //                  samples, labels zeroed past fg_this, class-specific normalised targets and
 //                  weights (R x 4C)
@@ -495,10 +496,15 @@ proposal_sample_kernel(const float* __restrict__ rois, const float* __restrict__
   const float* kg = kf + M;
   const float* ur = kg + M;  // R pad draws: [0, F) fg, [F, R) bg
   const int cf = fg_any ? nfg : nval, cb = bg_any ? nbg : nval;
-  const int tf = select_smallest(M, cf, F, fg_pool, [&](int i) { return kf[i]; }, s, sel_fg);
-  const int tb = select_smallest(M, cb, R - F, bg_pool, [&](int i) { return kg[i]; }, s, sel_bg);
+  // the two halves of the sample are independent: workgroup (b, 0) selects and writes the fg slots
+  // [0, F), workgroup (b, 1) the bg slots [F, R) -- the two selections run side by side
+  const bool bg_half = blockIdx.y == 1;
+  const int j0 = bg_half ? F : 0, j1 = bg_half ? R : F;
+  int tf = 0, tb = 0;
+  if (!bg_half) tf = select_smallest(M, cf, F, fg_pool, [&](int i) { return kf[i]; }, s, sel_fg);
+  else tb = select_smallest(M, cb, R - F, bg_pool, [&](int i) { return kg[i]; }, s, sel_bg);
   // sample_slots: [0, pad) with-replacement picks from the sample, [pad, n) the sample in key order
-  for (int j = threadIdx.x; j < R; j += blockDim.x) {
+  for (int j = j0 + threadIdx.x; j < j1; j += blockDim.x) {
     const bool f = j < F;
     const int n = f ? F : R - F, take = f ? tf : tb, jj = f ? j : j - F;
     const int* sl = f ? sel_fg : sel_bg;
@@ -512,7 +518,7 @@ proposal_sample_kernel(const float* __restrict__ rois, const float* __restrict__
   }
   __syncthreads();
   const int fg_this = min(nfg, F);
-  for (int j = threadIdx.x; j < R; j += blockDim.x) {
+  for (int j = j0 + threadIdx.x; j < j1; j += blockDim.x) {
     const int idx = keep[j];
     float bx[5];
     if (idx < P) {
@@ -551,7 +557,7 @@ proposal_sample_kernel(const float* __restrict__ rois, const float* __restrict__
   const float4 ow4 = make_float4(prm.iw[0] > 0.f ? 1.f : 0.f, prm.iw[1] > 0.f ? 1.f : 0.f,
                                  prm.iw[2] > 0.f ? 1.f : 0.f, prm.iw[3] > 0.f ? 1.f : 0.f);
   const int nwaves = blockDim.x >> 6, lane = threadIdx.x & 63;
-  for (int j = threadIdx.x >> 6; j < R; j += nwaves) {
+  for (int j = j0 + (threadIdx.x >> 6); j < j1; j += nwaves) {
     const int lab = s_lab[j];
     const float4 t4 = make_float4(s_t[j * 4], s_t[j * 4 + 1], s_t[j * 4 + 2], s_t[j * 4 + 3]);
     const int64_t row = ((int64_t)b * R + j) * C4;
@@ -591,7 +597,7 @@ int proposal_sample(const float* rois, const float* gt, const int32_t* n_gt, con
     prm.stds[q] = stds[q];
     prm.iw[q] = inside_w[q];
   }
-  proposal_sample_kernel<<<B, 1024, lds, st>>>(rois, gt, n_gt, max_ov, argmax, rnd, prm, out_rois, out_label,
+  proposal_sample_kernel<<<dim3(B, 2), 1024, lds, st>>>(rois, gt, n_gt, max_ov, argmax, rnd, prm, out_rois, out_label,
                                                bbox_target, inside, outside);
   return 0;
 }

@@ -253,6 +253,44 @@ def _bnp(bn):
     return [bn.gamma, bn.beta, bn.moving_mean, bn.moving_var]
 
 
+# Inference-only library route (MXR_GEMM_ROUTE=0 disables): a 1x1 stride-1 conv with a frozen BN +
+# ReLU epilogue on a batch-sized map is a plain GEMM, and hipBLASLt's bias + ReLU epilogue GEMM runs
+# it faster than the implicit-GEMM kernel (batch-8 stage-3 reduce, M = 33 600: 23 vs 38 us,
+# profiles/r5_b8_conv_tiles.jsonl, tools/microbench/addmm_probe.py) -- and at inference the pre-BN
+# output the kernel also writes is dead.  Test FPS: batch 8 679 -> 735, batch 1 327 -> 344 (every
+# stage's 1x1 reduce and the RoI head's; profiles/r5_gemm_route_ab.txt).  Single-plane bf16 / fp16
+# only; the BN scale is folded into a cached copy of the filter (rebuilt when the filter or the BN
+# statistics change).
+_GEMM_MIN_M = int(os.environ.get('MXR_GEMM_MIN_M', '4096'))
+
+
+def _gemm_route(x, w):
+    if os.environ.get('MXR_GEMM_ROUTE', '1') == '0' or precision.x2_enabled():
+        return False
+    if not (x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and x.dim() == 4 and w.dim() == 4 and
+            w.shape[2] == 1 and w.shape[3] == 1 and x.is_contiguous(memory_format=torch.channels_last)):
+        return False
+    return x.shape[0] * x.shape[2] * x.shape[3] >= _GEMM_MIN_M and x.shape[1] % 8 == 0 and w.shape[0] % 8 == 0
+
+
+def _gemm_bn_relu(x, w, bnp, eps, fix_gamma):
+    gamma, beta, mean, var = bnp
+    key = (w.data_ptr(), w._version, precision.weight_epoch(w), x.dtype, float(eps), bool(fix_gamma)) + tuple(
+        (p.data_ptr(), p._version) for p in bnp)
+    hit = w.__dict__.get('_mxr_gemm_fold')
+    if hit is None or hit[0] != key:
+        with torch.no_grad():
+            sc = (torch.ones_like(var.float()) if fix_gamma else gamma.float()) * torch.rsqrt(var.float() + eps)
+            wf = (w.detach().float().reshape(w.shape[0], -1) * sc[:, None]).to(x.dtype)
+            bf = (beta.float() - mean.float() * sc).to(x.dtype)
+        hit = (key, wf, bf)
+        w.__dict__['_mxr_gemm_fold'] = hit
+    _, wf, bf = hit
+    n, c, h, ww = x.shape
+    y = torch._addmm_activation(bf, x.permute(0, 2, 3, 1).reshape(n * h * ww, c), wf.t(), use_gelu=False)
+    return y.view(n, h, ww, wf.shape[0]).permute(0, 3, 1, 2)
+
+
 class _FusedUnitFn(torch.autograd.Function):
     @staticmethod
     def _forward_train(ctx, spec, x, parts1, t, nconv, ws, bnps, nxt):
@@ -329,8 +367,14 @@ class _FusedUnitFn(torch.autograd.Function):
         # conv1 (stride 1 for bottleneck; 3x3 stride s for basic) -> bn2
         s1 = 1 if spec.bottle else spec.stride
         p1 = 0 if spec.bottle else 1
-        y1, a2 = ext.conv_igemm_fwd(act1, wa[0][0], None, s1, p1, False, 0, 0, None, bnps[1], spec.eps[1],
-                                    spec.fix[1], True, **wa[0][1])
+        if spec.bottle and getattr(spec, 'infer', False) and _gemm_route(act1, ws[0]):
+            # inference: the bottleneck's 1x1 reduce + frozen bn2 + ReLU is a plain GEMM with a bias /
+            # ReLU epilogue -- hipBLASLt's on the large-M (batch) shapes; the pre-BN output y1 exists
+            # only for the backward, so it is not written at all
+            y1, a2 = None, _gemm_bn_relu(act1, ws[0], bnps[1], spec.eps[1], spec.fix[1])
+        else:
+            y1, a2 = ext.conv_igemm_fwd(act1, wa[0][0], None, s1, p1, False, 0, 0, None, bnps[1], spec.eps[1],
+                                        spec.fix[1], True, **wa[0][1])
         if spec.bottle:
             y2, a3 = ext.conv_igemm_fwd(a2, wa[1][0], None, spec.stride, 1, False, 0, 0, None, bnps[2], spec.eps[2],
                                         spec.fix[2], True, **wa[1][1])
@@ -669,6 +713,7 @@ def fused_unit(u, x, act1=None, next_bn=None, train=False):
     the second output are the unit's / next unit's bn1 activation.  train=True (batch-statistics
     BNs): they are the statistics partials of the unit input / output for its / the next bn1."""
     spec = _Unit(u, next_bn, train)
+    spec.infer = not torch.is_grad_enabled()  # (inside the Function's forward grad mode is always off)
     ws = [u.conv1.weight, u.conv2.weight] + ([u.conv3.weight] if u.bottle_neck else [])
     if not u.dim_match:
         ws.append(u.sc.weight)

@@ -567,3 +567,35 @@ def test_train_units_match_module_path(cuda, monkeypatch):
         close(gb[n], ga[n], g_r[n], n)
     for n in sa:
         close(sb[n], sa[n], s_r[n], n)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
+def test_inference_gemm_route_matches_kernel(cuda, monkeypatch, dtype):
+    """Inference on a batch-sized map routes the bottleneck's 1x1 reduce + frozen bn2 + ReLU to
+    hipBLASLt's bias / ReLU GEMM (ops/fused.py _gemm_route, M >= 16384): the unit output matches the
+    implicit-GEMM kernel path (MXR_GEMM_ROUTE=0) within the 16-bit rounding, and the folded filter
+    is rebuilt when the BN statistics change."""
+    from mx_rcnn_amd.ops import fused
+    u = _unit(1024, 1024, 1, True, cuda)
+    for m in u.modules():
+        if hasattr(m, 'weight') and m.weight is not None and m.weight.dim() == 4:
+            m.weight = torch.nn.Parameter(m.weight.detach().to(dtype).contiguous(memory_format=torch.channels_last))
+    x = torch.randn(4, 1024, 64, 64, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last)
+    assert fused._gemm_route(x, u.conv1.weight)
+
+    def run(route):
+        monkeypatch.setenv('MXR_GEMM_ROUTE', '1' if route else '0')
+        with torch.no_grad():
+            return fused.fused_unit(u, x)[0].float()
+
+    a = run(True)
+    assert '_mxr_gemm_fold' in u.conv1.weight.__dict__  # the library route ran
+    b = run(False)
+    scale = b.abs().max().item()
+    assert (a - b).abs().max().item() <= 2e-2 * scale
+    with torch.no_grad():
+        u.bn2.moving_var.mul_(4.0)
+    c, d = run(True), run(False)
+    assert (c - d).abs().max().item() <= 2e-2 * d.abs().max().item()
+    assert (c - a).abs().max().item() > 1e-3 * scale  # the new statistics were used

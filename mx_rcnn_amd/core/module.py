@@ -186,13 +186,16 @@ class MutableModule(object):
                                compute_dtype=self.compute_dtype, device=self.context,
                                bucket_mb=p.get('bucket_mb', 64),
                                precision=self.precision if self.context.type == 'cuda' else None)
+        if self._monitor is not None:  # a norm monitor reads the gradients: no fused updates
+            self.trainer.fused_fc_sgd = []
         self.optimizer_initialized = True
 
     def install_monitor(self, mon):
         self._monitor = mon
         mon.install(self.model)
         # the monitor reads gradients: no update may be fused into a weight-gradient kernel
-        self.trainer.fused_fc_sgd = []
+        if self.trainer is not None:
+            self.trainer.fused_fc_sgd = []
 
     # ------------------------------------------------------------------ step API
     def forward(self, data_batch, is_train=None):

@@ -135,10 +135,10 @@ conv_wgrad_kernel(const uint16_t* __restrict__ dy, const uint16_t* __restrict__ 
       }
 }
 
-template <int S, bool X2 = false, bool X3 = false>
+template <int S, bool X2 = false, bool X3 = false, bool SGD = false>
 __global__ void __launch_bounds__(256) conv_wgrad_buf_kernel(WgradParams p) {
   __shared__ __attribute__((aligned(16))) uint16_t lds[S * wgrad_ring_stage<X3>()];  // [S][dY|X][64 px][64 ch] (+ lo)
-  wgrad_buf_body<S, X2, 1, X3>(lds, blockIdx.x, p);
+  wgrad_buf_body<S, X2, 1, X3, SGD>(lds, blockIdx.x, p);
 }
 
 __global__ void __launch_bounds__(256)
@@ -258,11 +258,11 @@ int conv_wgrad_sgd(const uint16_t* dy, const uint16_t* x, int NB, int H, int W, 
   p.sgd_rescale = sgd.rescale;
   p.sgd_clip = sgd.clip;
   if (p.x3)
-    conv_wgrad_buf_kernel<3, true, true><<<p.ntiles, 256, 0, st>>>(p);
+    conv_wgrad_buf_kernel<3, true, true, true><<<p.ntiles, 256, 0, st>>>(p);
   else if (p.x2)
-    conv_wgrad_buf_kernel<3, true><<<p.ntiles, 256, 0, st>>>(p);
+    conv_wgrad_buf_kernel<3, true, false, true><<<p.ntiles, 256, 0, st>>>(p);
   else
-    conv_wgrad_buf_kernel<3><<<p.ntiles, 256, 0, st>>>(p);
+    conv_wgrad_buf_kernel<3, false, false, true><<<p.ntiles, 256, 0, st>>>(p);
   return 1;
 }
 

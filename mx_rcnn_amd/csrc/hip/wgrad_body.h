@@ -99,7 +99,7 @@ constexpr int kWgradLdsElems = 3 * 2 * WG_BK * 64;  // the S = 3 ring: [S][dY|X]
 template <bool X3>
 constexpr int wgrad_ring_stage() { return 2 * WG_BK * 64 + (X3 ? 2 * 32 * 64 : 0); }
 
-template <int S, bool X2 = false, int KG = 1, bool X3 = false>
+template <int S, bool X2 = false, int KG = 1, bool X3 = false, bool SGD = false>
 __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const WgradParams& p) {
   constexpr int LPS = X3 ? 6 : 4;  // DMA instructions per thread per stage (2 dY rows + 2 X rows [+ 2 lo])
   constexpr int NT = 256 * KG;
@@ -191,6 +191,23 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // fused SGD (KG = 1): the master / momentum rows this thread updates in the epilogue are loaded
+  // now, under the pixel loop, instead of after it
+  constexpr int SGD_V = (512 + 255) / 256;
+  float4 sgd_wp[SGD_V][2], sgd_mp[SGD_V][2];
+  if constexpr (SGD && KG == 1) {
+#pragma unroll
+    for (int v = 0; v < SGD_V; ++v) {
+      const int e = tid + v * 256, co = co0 + (e >> 3);
+      if (e < 512 && co < Cout) {
+        const int64_t o = (int64_t)co * (tiles_n * WG_BN) + k0 + (e & 7) * 8;
+        sgd_wp[v][0] = reinterpret_cast<const float4*>(p.sgd_w + o)[0];
+        sgd_wp[v][1] = reinterpret_cast<const float4*>(p.sgd_w + o)[1];
+        sgd_mp[v][0] = reinterpret_cast<const float4*>(p.sgd_mom + o)[0];
+        sgd_mp[v][1] = reinterpret_cast<const float4*>(p.sgd_mom + o)[1];
+      }
+    }
+  }
   const int g = lane >> 4, q = (lane & 15) >> 2, pcol = (lane & 3) * 4;
   // swizzled element offset of (row, col), col a multiple of 4 inside one 16-B chunk
   auto lidx = [](int row, int col) { return row * 64 + (((col >> 3) ^ wsw(row)) << 3) + (col & 7); };
@@ -348,7 +365,7 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
       a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
     }
     const int64_t o = (int64_t)co * ldk + k0 + cv * 8;
-    if (p.sgd_w) {  // fused update (the host guarantees splits == 1 and 16-B aligned rows)
+    if (SGD) {  // fused update (the host guarantees sgd_w, splits == 1 and 16-B aligned rows)
       float g[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
       if (p.sgd_gbf16) {
 #pragma unroll
@@ -357,7 +374,12 @@ __device__ __forceinline__ void wgrad_buf_body(uint16_t* lds, int wgid, const Wg
       const float lr = *p.sgd_lr;
       float4* wp = reinterpret_cast<float4*>(p.sgd_w + o);
       float4* mp = reinterpret_cast<float4*>(p.sgd_mom + o);
-      const float4 w0 = wp[0], w1 = wp[1], m0 = mp[0], m1 = mp[1];
+      float4 w0, w1, m0, m1;
+      if constexpr (KG == 1 && NT == 256) {  // prefetched before the pixel loop
+        w0 = sgd_wp[v][0]; w1 = sgd_wp[v][1]; m0 = sgd_mp[v][0]; m1 = sgd_mp[v][1];
+      } else {
+        w0 = wp[0]; w1 = wp[1]; m0 = mp[0]; m1 = mp[1];
+      }
       float wv[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
       float mv[8] = {m0.x, m0.y, m0.z, m0.w, m1.x, m1.y, m1.z, m1.w};
 #pragma unroll

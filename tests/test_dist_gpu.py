@@ -7,6 +7,7 @@ Each configuration runs in its own process (tools/dp_step_check.py): a process g
 torn down and re-created cleanly inside one process, and the non-DP step must not see one.
 """
 import os
+import socket
 import subprocess
 import sys
 
@@ -74,3 +75,80 @@ def test_autotuned_reruns_are_bitwise_equal_through_the_plan_file(tmp_path):
     keys = [k for k in a if not k.startswith('_')]
     diff = [k for k in keys if not torch.equal(a[k], b[k])]
     assert not diff, 'autotuned reruns differ: %s' % diff[:5]
+
+
+def _two_ranks(tmp_path, name, precision, same_batch, steps=2):
+    """Two worker processes (tools/dp_two_rank_check.py), both on cuda:0, gloo rendezvous on
+    127.0.0.1; returns both ranks' saved states."""
+    sk = socket.socket()
+    sk.bind(('127.0.0.1', 0))
+    port = sk.getsockname()[1]
+    sk.close()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ)
+        env.pop('MXR_FORCE_DIST', None)
+        env.update({'MXR_CONV_TUNE': '0', 'WORLD_SIZE': '2', 'RANK': str(r), 'LOCAL_RANK': '0',
+                    'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port)})
+        cmd = [sys.executable, os.path.join(ROOT, 'tools', 'dp_two_rank_check.py'), str(tmp_path / ('%s_r%d.pt' % (name, r))),
+               '--precision', precision, '--steps', str(steps)] + (['--same-batch'] if same_batch else [])
+        procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=240)[0])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    for p, o in zip(procs, outs):
+        assert p.returncode == 0, o[-3000:]
+    return [torch.load(str(tmp_path / ('%s_r%d.pt' % (name, r))), weights_only=True) for r in range(2)], outs
+
+
+def _plain(tmp_path, name, precision, rescale, steps=2):
+    env = dict(os.environ)
+    for k in ('MXR_FORCE_DIST', 'WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
+        env.pop(k, None)
+    env['MXR_CONV_TUNE'] = '0'
+    out = str(tmp_path / (name + '.pt'))
+    r = subprocess.run([sys.executable, os.path.join(ROOT, 'tools', 'dp_two_rank_check.py'), out, '--precision', precision,
+                        '--steps', str(steps), '--rescale', str(rescale)],
+                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-3000:]
+    return torch.load(out, weights_only=True)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('precision', ['fp32', 'bf16'])
+def test_two_ranks_on_one_gpu_sum_gradients(tmp_path, precision):
+    """World size 2 on the device kernels.  Both ranks train on the SAME batches, so the summed
+    gradient is exactly 2g, and one plain process with rescale_grad = 2 must produce the same
+    weights and momenta bit for bit (x + x and 2 * x are both exact); both replicas must be
+    identical.  RCCL refuses two ranks on one GPU: the ranks talk over gloo (device buckets staged
+    through host memory), everything else is the production DP path (hooks, buckets, SUM, SGD)."""
+    (r0, r1), logs = _two_ranks(tmp_path, 'same', precision, True)
+    assert r0['_info'].tolist()[:3] == [1, int(r0['_info'][1]), 2] and int(r0['_info'][1]) > 1, logs[0][-2000:]
+    ref = _plain(tmp_path, 'plain2x', precision, 2.0)
+    assert int(ref['_info'][0]) == 0
+    keys = [k for k in ref if not k.startswith('_')]
+    assert len(keys) > 10
+    for k in keys:
+        assert torch.equal(r0[k], r1[k]), ('replicas differ', k)
+    diff = [k for k in keys if not torch.equal(ref[k], r0[k])]
+    assert not diff, 'DP sum differs from the plain 2x-rescaled step: %s (max abs %s)' % (
+        diff[:5], [float((ref[k].float() - r0[k].float()).abs().max()) for k in diff[:5]])
+
+
+@pytest.mark.gpu
+def test_two_ranks_on_one_gpu_stay_in_sync_on_different_batches(tmp_path):
+    """Per-rank batches: different objectives, one synchronous update -- the replicas stay
+    bit-identical, and they moved away from the single-rank result."""
+    (r0, r1), logs = _two_ranks(tmp_path, 'diff', 'fp32', False)
+    assert not torch.equal(r0['_objective'], r1['_objective']), logs[0][-2000:]
+    keys = [k for k in r0 if not k.startswith('_')]
+    for k in keys:
+        assert torch.equal(r0[k], r1[k]), ('replicas differ', k)
+    ref = _plain(tmp_path, 'plain1x', 'fp32', 1.0)
+    assert any(not torch.equal(ref[k], r0[k]) for k in keys)

@@ -186,11 +186,13 @@ class Trainer:
 
     def check_finite(self, step=None):
         """Raise FloatingPointError if any step since the last check produced a non-finite loss
-        (one host read of a device counter)."""
+        or a failed device reduction (the proposal NMS chain's give-up, ops/proposal.py) -- one host
+        read of a device counter."""
         n = int(self.nonfinite.item())
         if n:
             self.nonfinite.zero_()
-            raise FloatingPointError('non-finite loss in %d step(s) up to step %s' % (n, step))
+            raise FloatingPointError('non-finite loss (or a failed proposal NMS) in %d step(s) up to step %s'
+                                     % (n, step))
 
     def arm_fault(self, kind='nan'):
         """Fault injection (``MXR_FAULT_INJECT=nan@STEP``): poison the next step's loss."""

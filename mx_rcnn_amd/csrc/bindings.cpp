@@ -111,7 +111,8 @@ std::vector<Tensor> proposal_decode(const Tensor& cls, const Tensor& dlt, const 
 
 // NMS over score-sorted boxes; returns (rois (B,post,5), scores (B,post), keep (B,post) int64, n_keep (B))
 std::vector<Tensor> nms_proposals(const Tensor& boxes, const Tensor& scores, const Tensor& n_valid, double thresh,
-                                  int64_t post, const Tensor& rand_u, c10::optional<Tensor> mask_in) {
+                                  int64_t post, const Tensor& rand_u, c10::optional<Tensor> mask_in,
+                                  c10::optional<Tensor> fault) {
   CHECK_DEV(boxes); CHECK_F32(boxes); CHECK_CONTIG(boxes);
   CHECK_DEV(scores); CHECK_F32(scores); CHECK_CONTIG(scores);
   CHECK_DEV(n_valid); CHECK_I32(n_valid); CHECK_CONTIG(n_valid);
@@ -138,6 +139,12 @@ std::vector<Tensor> nms_proposals(const Tensor& boxes, const Tensor& scores, con
                   reinterpret_cast<uint64_t*>(mask.data_ptr<int64_t>()), st);
     LAUNCH_CHECK("nms_mask");
   }
+  int32_t* fault_p = nullptr;  // the caller's failure counter (int32 on the device): +1 per give-up
+  if (fault.has_value() && fault->defined()) {
+    CHECK_DEV(*fault); CHECK_I32(*fault);
+    TORCH_CHECK(fault->numel() >= 1 && fault->device() == boxes.device(), "fault: an int32 counter on the boxes' device");
+    fault_p = fault->data_ptr<int32_t>();
+  }
   Tensor rois = at::empty({B, post, 5}, boxes.options());
   Tensor out_scores = at::empty({B, post}, boxes.options());
   Tensor keep = at::empty({B, post}, boxes.options().dtype(at::kLong));
@@ -148,7 +155,7 @@ std::vector<Tensor> nms_proposals(const Tensor& boxes, const Tensor& scores, con
                   reinterpret_cast<const uint64_t*>(mask.data_ptr<int64_t>()), B, P, (int)post,
                   rand_u.data_ptr<float>(), rois.data_ptr<float>(), out_scores.data_ptr<float>(),
                   keep.data_ptr<int64_t>(), n_keep.data_ptr<int32_t>(),
-                  keep_ws.defined() ? keep_ws.data_ptr<int32_t>() : nullptr, st);
+                  keep_ws.defined() ? keep_ws.data_ptr<int32_t>() : nullptr, st, fault_p);
   LAUNCH_CHECK("nms_reduce");
   return {rois, out_scores, keep, n_keep};
 }
@@ -2274,7 +2281,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "mx_rcnn_amd gfx950 kernels";
   m.def("proposal_decode", &proposal_decode);
   m.def("nms_proposals", &nms_proposals, py::arg("boxes"), py::arg("scores"), py::arg("n_valid"), py::arg("thresh"),
-        py::arg("post"), py::arg("rand_u"), py::arg("mask") = py::none());
+        py::arg("post"), py::arg("rand_u"), py::arg("mask") = py::none(), py::arg("fault") = py::none());
   m.def("nms_mask_build", &nms_mask_build);
   m.def("conv_wgrad_sgd", &conv_wgrad_sgd, py::arg("dy"), py::arg("x"), py::arg("KH"), py::arg("KW"), py::arg("stride"),
         py::arg("pad"), py::arg("x2"), py::arg("w"), py::arg("mom"), py::arg("shadow"), py::arg("planes"),

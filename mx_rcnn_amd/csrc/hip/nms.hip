@@ -281,7 +281,7 @@ nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ sco
 
 // ---- multi-workgroup reducer -------------------------------------------------------------------
 constexpr int NMSC_PER = 8;  // column blocks per workgroup, one wave each (MXR_NMS_PER=16 for the A/B)
-constexpr int NMSC_SPIN = 1 << 20;                        // empty poll rounds before a workgroup gives up
+constexpr int NMSC_SPIN = 1 << 20;  // empty poll rounds before a workgroup gives up (MXR_NMS_SPIN overrides)
 
 __device__ __forceinline__ uint64_t nmsc_load(const uint64_t* p) {
   return __hip_atomic_load(const_cast<uint64_t*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -298,7 +298,8 @@ nms_reduce_mc_kernel(const float* __restrict__ boxes, const float* __restrict__ 
                      const int32_t* __restrict__ n_valid, const uint64_t* __restrict__ maskT, uint64_t* rec, int P,
                      int nb, int post, const float* __restrict__ rand_u, float* __restrict__ rois,
                      float* __restrict__ out_scores, int64_t* __restrict__ keep_idx,
-                     int32_t* __restrict__ n_keep_out, int32_t* keep_ws, uint64_t* probe) {
+                     int32_t* __restrict__ n_keep_out, int32_t* keep_ws, uint64_t* probe, int spin_max,
+                     int32_t* fault) {
   // dynamic LDS: [own triangle (PER * (PER + 1) / 2) x 64 u64][kept nb u64][rem PER u64][count nb i32][keep list post i32]
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint64_t* tri = reinterpret_cast<uint64_t*>(smem);
@@ -357,7 +358,7 @@ nms_reduce_mc_kernel(const float* __restrict__ boxes, const float* __restrict__ 
           const bool ok = lane < got || (lane < nr && (w0 >> 32) != 0ull && (w1 >> 32) != 0ull);
           const int n = min(nr, (int)__builtin_ctzll(~__ballot(ok)));  // ready prefix of the chunk
           if (n == got) {
-            if (++spins > NMSC_SPIN) {
+            if (++spins > spin_max) {
               stop = gave_up = true;
               break;
             }
@@ -464,6 +465,9 @@ nms_reduce_mc_kernel(const float* __restrict__ boxes, const float* __restrict__ 
       }
     } else if (s_flag[2] && tid == 0) {
       n_keep_out[b] = -1;  // a poll gave up: the output of this image is not valid
+      // ... and the step's failure counter says so (the Trainer's non-finite counter: check_finite
+      // raises on the host's next read instead of training on unassembled RoIs)
+      if (fault) __hip_atomic_fetch_add(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   if (assemble) {
@@ -575,7 +579,7 @@ bool nms_keep_in_lds(int P, int post) { return nms_reduce_lds(P, post) <= 160 * 
 
 void nms_reduce(const float* boxes, const float* scores, const int32_t* n_valid, const uint64_t* mask, int B,
                 int P, int post, const float* rand_u, float* rois, float* out_scores, int64_t* keep_idx,
-                int32_t* n_keep, int32_t* keep_ws, hipStream_t st) {
+                int32_t* n_keep, int32_t* keep_ws, hipStream_t st, int32_t* fault) {
   if (B == 0) return;
   const int nb = div_up(P, 64);
   const int lpost = keep_ws ? 0 : post;
@@ -596,13 +600,17 @@ void nms_reduce(const float* boxes, const float* scores, const int32_t* n_valid,
   }();
   dim3 grid(div_up(nb, per), B);
   uint64_t* probe = nms_probe() ? rec + (int64_t)B * nb * 2 + B : nullptr;
+  // poll budget (read per call: tests/test_nms_multi.py drives the give-up path with 0)
+  const char* sp = getenv("MXR_NMS_SPIN");
+  const int spin_max = sp ? std::max(0, atoi(sp)) : NMSC_SPIN;
   if (per == 16)
     nms_reduce_mc_kernel<16><<<grid, 16 * 64, nms_mc_lds(nb, lpost, 16), st>>>(boxes, scores, n_valid, mask, rec, P, nb,
                                                                           post, rand_u, rois, out_scores, keep_idx,
-                                                                          n_keep, keep_ws, probe);
+                                                                          n_keep, keep_ws, probe, spin_max, fault);
   else
     nms_reduce_mc_kernel<NMSC_PER><<<grid, NMSC_PER * 64, nms_mc_lds(nb, lpost), st>>>(
-        boxes, scores, n_valid, mask, rec, P, nb, post, rand_u, rois, out_scores, keep_idx, n_keep, keep_ws, probe);
+        boxes, scores, n_valid, mask, rec, P, nb, post, rand_u, rois, out_scores, keep_idx, n_keep, keep_ws, probe,
+        spin_max, fault);
 }
 
 }  // namespace mxr

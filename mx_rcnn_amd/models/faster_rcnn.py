@@ -180,7 +180,8 @@ class FasterRCNN(nn.Module):
         c = self.cfg[key]
         return proposal(rpn_cls.detach(), rpn_bbox.detach(), im_info, self.feat_stride, self.anchor_scales,
                         self.anchor_ratios, c.RPN_PRE_NMS_TOP_N, c.RPN_POST_NMS_TOP_N, c.RPN_NMS_THRESH,
-                        c.RPN_MIN_SIZE, is_train=(key == 'TRAIN'), is_prob=is_prob, after_mask=after_mask)
+                        c.RPN_MIN_SIZE, is_train=(key == 'TRAIN'), is_prob=is_prob, after_mask=after_mask,
+                        fault=self.nonfinite_counter if key == 'TRAIN' else None)
 
     def _anchor_target_async(self, data, im_info, gt_boxes, n_gt):
         """Start the RPN anchor-target assignment (which needs only the image shape and the gt

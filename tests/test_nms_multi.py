@@ -68,3 +68,31 @@ def test_multi_workgroup_nms_mask_reused(cuda):
     for a, b in zip(first, second):
         assert torch.equal(a, b)
     _check(C, cuda, boxes, scores, nv, post, second)
+
+
+@pytest.mark.gpu
+def test_multi_workgroup_nms_give_up_is_reported(cuda, monkeypatch):
+    """MXR_NMS_SPIN=0: a workgroup whose first poll finds an earlier workgroup's record unwritten
+    gives up at once.  The kernel must still drain, add to the caller's fault counter (the Trainer
+    passes its non-finite counter, so check_finite raises), and leave the records clean: the next
+    reduce on the same mask with the default poll budget is exact and reports nothing."""
+    from mx_rcnn_amd.ops import need_ext
+    C = need_ext()
+    g = torch.Generator().manual_seed(9)
+    P, post = 12000, 12000
+    boxes, scores = _batch(g, 1, P)
+    nv = torch.tensor([P], dtype=torch.int32)
+    bd, sd, nvd = boxes.to(cuda), scores.to(cuda), nv.to(cuda)
+    u = torch.rand(1, post, generator=g).to(cuda)
+    mask = C.nms_mask_build(bd, nvd, 0.7)
+    fault = torch.zeros(1, dtype=torch.int32, device=cuda)
+    monkeypatch.setenv('MXR_NMS_SPIN', '0')
+    C.nms_proposals(bd, sd, nvd, 0.7, post, u, mask, fault)
+    torch.cuda.synchronize()
+    assert int(fault.item()) > 0  # 24 workgroups in a chain, none allowed to wait
+    monkeypatch.delenv('MXR_NMS_SPIN')
+    fault.zero_()
+    out = C.nms_proposals(bd, sd, nvd, 0.7, post, u, mask, fault)
+    torch.cuda.synchronize()
+    assert int(fault.item()) == 0
+    _check(C, cuda, boxes, scores, nv, post, out)

@@ -129,7 +129,8 @@ class Trainer:
 
     def step_body(self, b):
         """The device work of one step (capturable)."""
-        from ..ops.precision import x2_mode
+        from ..ops.precision import bump_generation, x2_mode
+        bump_generation()  # the update below rewrites trainable weights in place
         with x2_mode(self.x2):
             return self._step_body(b)
 
@@ -228,6 +229,8 @@ class Trainer:
         for b, v in zip(self.model.buffers(), st['buffers']):
             b.copy_(v)
         self.nonfinite.copy_(st['nonfinite'])
+        from ..ops.precision import bump_generation
+        bump_generation()  # the masters were rewritten
         if 'rng_step' in st:
             self.rng_step.copy_(st['rng_step'])
         self.store.refresh_dgrad_cache()
@@ -317,6 +320,8 @@ class GraphedStep:
         self.t.update_lr()
         if self.t.grads_dirty:  # the graph holds no gradient clear (captured after a fused-clear step)
             self.t.store.zero_grad()
+        from ..ops.precision import bump_generation
+        bump_generation()  # the replayed update rewrites trainable weights in place
         self.graph.replay()
         self.t.grads_dirty = not self.t.fused_clear
         return self.out

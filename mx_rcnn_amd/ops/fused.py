@@ -275,8 +275,8 @@ def _gemm_route(x, w):
 
 def _gemm_bn_relu(x, w, bnp, eps, fix_gamma):
     gamma, beta, mean, var = bnp
-    key = (w.data_ptr(), w._version, precision.weight_epoch(w), x.dtype, float(eps), bool(fix_gamma)) + tuple(
-        (p.data_ptr(), p._version) for p in bnp)
+    key = (w.data_ptr(), w._version, precision.weight_epoch(w), precision.train_generation(w, *bnp), x.dtype,
+           float(eps), bool(fix_gamma)) + tuple((p.data_ptr(), p._version, precision.weight_epoch(p)) for p in bnp)
     hit = w.__dict__.get('_mxr_gemm_fold')
     if hit is None or hit[0] != key:
         with torch.no_grad():

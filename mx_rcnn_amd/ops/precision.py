@@ -182,6 +182,24 @@ def weight_epoch(param):
     return param.__dict__.get('_mxr_epoch', 0)
 
 
+# Training generation: the SGD kernels rewrite trainable parameters in place (inside a replayed
+# hipGraph, or through the flat store), which moves neither their version counters nor their
+# reload epochs.  Every step bumps this counter (core/trainer.py), and the inference-time caches
+# derived from TRAINABLE parameters (the stem's packed filter, the GEMM route's BN-folded filter)
+# key on it, so evaluating between training steps never reads a stale fold.
+_GEN = [0]
+
+
+def bump_generation():
+    _GEN[0] += 1
+
+
+def train_generation(*params):
+    """The training generation if any of ``params`` is trainable, else 0 (frozen values change
+    only through loads, which bump their reload epochs)."""
+    return _GEN[0] if any(p is not None and p.requires_grad for p in params) else 0
+
+
 def weight_pair(w):
     """-> (plane-0 view, plane spacing) of weight ``w`` (an fp32 Parameter / tensor) in the active
     mode.  Store-managed weights use the SGD-maintained shadow; anything else gets cached planes

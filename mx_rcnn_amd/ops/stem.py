@@ -30,10 +30,11 @@ def _packed_filter(w, dtype):
     never be served to a later tensor that reuses the same ``id`` / address (the round-4 stale-filter
     bug of an ``id()``-keyed cache).  It is rebuilt when the tensor's version counter, storage or
     reload epoch (``precision.forget_weight``: ``.data`` writes do not move the version counter)
-    changes -- IN PLACE when the shape allows, so a captured hipGraph keeps reading live values."""
+    changes -- IN PLACE when the shape allows, so a captured hipGraph keeps reading live values --
+    and, for a trainable filter, when a training step ran since (``precision.train_generation``)."""
     planes = precision.nplanes() if dtype == torch.float32 else 0
     slot = (dtype, planes)
-    ver = (w.data_ptr(), w._version, tuple(w.shape), precision.weight_epoch(w))
+    ver = (w.data_ptr(), w._version, tuple(w.shape), precision.weight_epoch(w), precision.train_generation(w))
     cache = w.__dict__.get('_mxr_stem')
     if cache is None:
         cache = w.__dict__['_mxr_stem'] = {}

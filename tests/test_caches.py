@@ -117,3 +117,32 @@ def test_sequential_trainers_are_collectable():
         gc.collect()
     for store_ref, model_ref in refs:
         assert store_ref() is None and model_ref() is None, 'a dead trainer is still reachable'
+
+
+def test_training_generation_keys_only_trainable_parameters():
+    """precision.train_generation: moves with every training step for trainable parameters (the
+    SGD kernels rewrite them in place), stays 0 for frozen ones (their values change only through
+    loads, which bump the reload epoch) -- the key the inference-time filter folds use."""
+    from mx_rcnn_amd.ops import precision
+    frozen = torch.nn.Parameter(torch.ones(2), requires_grad=False)
+    live = torch.nn.Parameter(torch.ones(2))
+    g0 = precision.train_generation(live)
+    assert precision.train_generation(frozen) == 0
+    precision.bump_generation()
+    assert precision.train_generation(live) == g0 + 1
+    assert precision.train_generation(frozen, None) == 0
+    assert precision.train_generation(frozen, live) == g0 + 1
+
+
+def test_trainer_step_moves_the_training_generation():
+    """Every training step (eager here; GraphedStep replays bump it too) advances the generation,
+    so an evaluation between steps rebuilds the folds of trainable filters."""
+    from mx_rcnn_amd.core.trainer import Trainer
+    from tests.test_dist import _batch, _make_model
+    tr = Trainer(_make_model(), 'rcnn', fixed_param_prefix=['conv0'], lr=0.01, wd=0.0, clip_gradient=-1, device='cpu')
+    w = tr.model.trunk.conv0.weight if hasattr(tr.model.trunk, 'conv0') else next(tr.model.parameters())
+    live = next(p for p in tr.model.parameters() if p.requires_grad)
+    g0 = precision.train_generation(live)
+    tr.step(_batch(0))
+    assert precision.train_generation(live) > g0
+    assert precision.train_generation(w) == (0 if not w.requires_grad else precision.train_generation(live))

@@ -599,3 +599,13 @@ def test_inference_gemm_route_matches_kernel(cuda, monkeypatch, dtype):
     c, d = run(True), run(False)
     assert (c - d).abs().max().item() <= 2e-2 * d.abs().max().item()
     assert (c - a).abs().max().item() > 1e-3 * scale  # the new statistics were used
+    # a training step rewrites trainable weights in place, moving no version counter: the fold
+    # follows the training generation (core/trainer.py bumps it every step)
+    from mx_rcnn_amd.ops import precision
+    with torch.no_grad():
+        u.conv1.weight.data.mul_(0.5)
+    precision.bump_generation()
+    e, f = run(True), run(False)
+    assert (e - f).abs().max().item() <= 2e-2 * f.abs().max().item()
+    assert (e - c).abs().max().item() > 1e-3 * scale
+

@@ -417,3 +417,18 @@ def test_capture_sync_key_ignores_uneven_slices():
     assert k1 != k3 and sync_key(k1) == sync_key(k3)
     k_other = (('data', (1, 3, 600, 1024)), ('gt_boxes', (1, 20, 5)), ('im_info', (1, 3)))
     assert sync_key(k_other) != sync_key(k1)
+
+
+def test_two_rank_check_tool_sums_like_rescale_two_on_cpu(tmp_path):
+    """The worker of the GPU two-rank test (tools/dp_two_rank_check.py) on the CPU: two gloo ranks
+    on the same batch sum their gradients to exactly 2g, so they match one process with
+    rescale_grad = 2 bit for bit, and the replicas agree."""
+    from tests.test_dist_gpu import _plain, _two_ranks
+    (r0, r1), logs = _two_ranks(tmp_path, 'cpu', 'fp32', True, steps=1)
+    assert r0['_info'].tolist()[0] == 1 and r0['_info'].tolist()[2] == 2, logs[0][-2000:]
+    ref = _plain(tmp_path, 'cpu_plain2x', 'fp32', 2.0, steps=1)
+    keys = [k for k in ref if not k.startswith('_')]
+    assert len(keys) > 10
+    for k in keys:
+        assert torch.equal(r0[k], r1[k]), ('replicas differ', k)
+        assert torch.equal(ref[k], r0[k]), ('DP sum differs from the 2x-rescaled step', k)

@@ -18,13 +18,13 @@ from mx_rcnn_amd.utils.load_model import load_param
 CLASSES = VOC_CLASSES
 
 
-def get_net(prefix, epoch, ctx, network='vgg16'):
+def get_net(prefix, epoch, ctx, network='vgg16', dtype='fp32'):
     arg, aux, num_classes = load_param(prefix, epoch, convert=False)
     config.TEST.HAS_RPN = True
     config.TEST.RPN_PRE_NMS_TOP_N = 6000
     config.TEST.RPN_POST_NMS_TOP_N = 300
     model, _, _ = launch.build_model(network, num_classes, train_mode='test')
-    return Detector(model, ctx, arg, aux)
+    return Detector(model, ctx, arg, aux, compute_dtype=dtype)
 
 
 def demo_net(detector, image_name, out='result.jpg', conf_thresh=0.8, nms_thresh=0.3, classes=CLASSES):
@@ -51,11 +51,11 @@ def parse_args(argv=None):
     p.add_argument('--epoch', type=int, default=0)
     p.add_argument('--gpu', type=int, default=0)
     p.add_argument('--out', default='result.jpg')
-    launch.add_common_args(p)
+    launch.add_common_args(p, eval_cli=True)
     return p.parse_args(argv)
 
 
 if __name__ == '__main__':
     a = parse_args()
     rank, world, dev = launch.init_runtime(a)
-    demo_net(get_net(a.prefix, a.epoch, dev, a.network), a.image, a.out)
+    demo_net(get_net(a.prefix, a.epoch, dev, a.network, a.dtype), a.image, a.out)

@@ -16,40 +16,104 @@ from ..ops.boxes import bbox_pred, clip_boxes
 from ..ops.nms import batched_nms
 
 
+DTYPES = {'fp32': torch.float32, 'bf16': torch.bfloat16, 'fp16': torch.float16}
+
+
+def resolve_dtype(d):
+    """'fp32' / 'bf16' / 'fp16' or a torch dtype -> torch dtype (None stays None)."""
+    if d is None or isinstance(d, torch.dtype):
+        return d
+    if d not in DTYPES:
+        raise ValueError('dtype must be one of %s, not %r' % (sorted(DTYPES), d))
+    return DTYPES[d]
+
+
+def _inference_copy(model, dtype):
+    """A private copy of ``model`` for the test graph, its conv / FC weights in ``dtype`` (fp32:
+    the masters as fp32).  The caller's model is never modified: a model still being trained can be
+    evaluated between epochs, and the trainer's attachments (its filter-cache join, non-finite
+    counter, dropout counter) are not copied."""
+    import copy
+    from ..models.layers import Conv, Linear
+    held = []
+    for m in model.modules():
+        for k in ('pre_backward', 'nonfinite_counter', 'rng_step'):
+            if m.__dict__.get(k) is not None:
+                held.append((m, k, m.__dict__[k]))
+                m.__dict__[k] = None
+    try:
+        out = copy.deepcopy(model)
+    finally:
+        for m, k, v in held:
+            m.__dict__[k] = v
+    with torch.no_grad():
+        for m in out.modules():
+            if isinstance(m, (Conv, Linear)):
+                w = m.weight.data.to(dtype)
+                m.weight.data = w.contiguous(memory_format=torch.channels_last) if w.dim() == 4 else w.contiguous()
+                if m.bias is not None:
+                    m.bias.data = m.bias.data.to(dtype)
+            elif hasattr(m, 'moving_var'):  # BN parameters / statistics stay fp32
+                for t in (m.gamma, m.beta):
+                    t.data = t.data.float()
+    return out.eval()
+
+
 class Detector(object):
+    """Test-time runner of a FasterRCNN (reference `rcnn/detector.py:8-81`).
+
+    compute_dtype: 'fp32' / torch.float32 (the reference's precision: on the GPU every MFMA operand
+    and every tensor between kernels is the exact fp32 value as three bf16 planes -- the training
+    headline's fp32 mode, ops/precision.py -- on our kernels, no vendor conv / GEMM), 'bf16' (GPU
+    default) or 'fp16' (BASELINE config 5's fp16 MFMA path).  On the GPU the detector runs a
+    private copy of the model's weights in that precision (``self.model``); ``self.source`` is the
+    model it was built from, left untouched.
+    """
+
     def __init__(self, symbol, ctx=None, arg_params=None, aux_params=None, compute_dtype=None):
-        self.model = symbol
         self.ctx = torch.device(ctx) if ctx is not None else torch.device('cpu')
         if arg_params is not None or aux_params is not None:
             from .module import MutableModule
             mod = MutableModule(symbol, context=self.ctx, use_graph=False)
             mod.bind(for_training=False)
             mod.init_params(None, arg_params, aux_params, allow_missing=True)
-        self.model.to(self.ctx).eval()
+        self.source = symbol
+        compute_dtype = resolve_dtype(compute_dtype)
         if compute_dtype is None:
             compute_dtype = torch.bfloat16 if self.ctx.type == 'cuda' else torch.float32
-        # bf16 (default), fp16 (BASELINE config 5's "fp16 MFMA path": v_mfma_f32_16x16x32_f16 in the
-        # conv / FC kernels, fp16 activations through BN, pooling, RoIPool and the proposal decode,
-        # fp32 accumulation and epilogue math) or fp32 (PyTorch ops; the reference runs fp32)
         if compute_dtype not in (torch.bfloat16, torch.float16, torch.float32):
             raise ValueError('compute_dtype must be torch.bfloat16, torch.float16 or torch.float32 (got %s)'
                              % compute_dtype)
         self.dtype = compute_dtype
-        if self.ctx.type == 'cuda' and compute_dtype != torch.float32:
-            self._to_lowp()
+        # fp32 on the GPU: three-plane mode (MXR_FP32_EVAL=torch: plain fp32 PyTorch / vendor ops, a
+        # reference arm for precision probes)
+        self.planes = 3 if (self.ctx.type == 'cuda' and compute_dtype == torch.float32 and
+                            __import__('os').environ.get('MXR_FP32_EVAL', 'x3') != 'torch') else 0
+        if self.ctx.type == 'cuda':
+            symbol.to(self.ctx)
+            self.model = _inference_copy(symbol, compute_dtype)
+        else:
+            self.model = symbol.to(self.ctx).eval()
 
-    def _to_lowp(self):
-        from ..models.layers import Conv, Linear
-        for m in self.model.modules():
-            if isinstance(m, (Conv, Linear)):
-                m.weight.data = m.weight.data.to(self.dtype)
-                if m.weight.dim() == 4:
-                    m.weight.data = m.weight.data.contiguous(memory_format=torch.channels_last)
-                if m.bias is not None:
-                    m.bias.data = m.bias.data.to(self.dtype)
+    def precision_scope(self):
+        """Context in which this detector's model runs (the three-plane mode for GPU fp32)."""
+        from ..ops.precision import x2_mode
+        return x2_mode(self.planes)
+
+    @torch.no_grad()
+    def detect(self, data, im_info, rois=None):
+        """model.detect of a prepared (``_prep``) batch in this detector's precision."""
+        with self.precision_scope():
+            return self.model.detect(data, im_info, rois)
+
+    @torch.no_grad()
+    def rpn_test(self, data, im_info):
+        with self.precision_scope():
+            return self.model.rpn_test(data, im_info)
 
     def _prep(self, im_array):
         x = torch.as_tensor(np.asarray(im_array) if not torch.is_tensor(im_array) else im_array)
+        # fp32 mode: the stem kernel takes the fp32 image and writes the three planes
         x = x.to(self.ctx, self.dtype)
         if self.ctx.type == 'cuda':
             x = x.contiguous(memory_format=torch.channels_last)
@@ -62,7 +126,7 @@ class Detector(object):
                                                             else im_info).float().to(self.ctx)
         rois = None if roi_array is None else torch.as_tensor(np.asarray(roi_array) if not torch.is_tensor(roi_array)
                                                               else roi_array).float().to(self.ctx)
-        return self.model.detect(data, info, rois)
+        return self.detect(data, info, rois)
 
     @torch.no_grad()
     def im_detect(self, im_array, im_info=None, roi_array=None):

@@ -14,16 +14,16 @@ from ..data import cache as cache_io
 class Detector(object):
     """RPN-only detector: ``im_detect(im, im_info) -> (boxes (n, 4) in input pixels, scores (n, 1))``."""
 
-    def __init__(self, symbol, ctx=None, arg_params=None, aux_params=None):
+    def __init__(self, symbol, ctx=None, arg_params=None, aux_params=None, compute_dtype=None):
         from .detector import Detector as _D
-        self._det = _D(symbol, ctx, arg_params, aux_params)
-        self.model = symbol
+        self._det = _D(symbol, ctx, arg_params, aux_params, compute_dtype)
+        self.model = self._det.model
 
     @torch.no_grad()
     def im_detect(self, im, im_info):
         data = self._det._prep(im)
         info = torch.as_tensor(np.asarray(im_info) if not torch.is_tensor(im_info) else im_info).float()
-        rois, scores = self.model.rpn_test(data, info.to(data.device))
+        rois, scores = self._det.rpn_test(data, info.to(data.device))
         return rois[0, :, 1:].cpu().numpy(), scores[0, :, None].cpu().numpy()
 
 

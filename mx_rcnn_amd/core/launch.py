@@ -31,7 +31,9 @@ def setup_logging(rank=0):
                         format='%(asctime)s %(levelname)s %(message)s')
 
 
-def add_common_args(parser):
+def add_common_args(parser, eval_cli=False):
+    """The flags every CLI shares.  ``eval_cli``: --dtype is the TEST graph's precision (fp32 = the
+    reference's, as exact three-plane bf16 operands on the MFMA kernels; bf16; fp16)."""
     parser.add_argument('--network', default='vgg16', help='vgg16 | resnet18..resnet200')
     parser.add_argument('--synthetic', type=int, default=0, help='use N synthetic images instead of a dataset')
     parser.add_argument('--synthetic-shape', default='600x1000')
@@ -43,6 +45,12 @@ def add_common_args(parser):
     parser.add_argument('--eager', action='store_true', help='disable hipGraph step capture')
     parser.add_argument('--ims-per-gpu', type=int, default=1)
     parser.add_argument('--seed', type=int, default=0)
+    if eval_cli:
+        parser.add_argument('--dtype', default='fp32', choices=('fp32', 'bf16', 'fp16'),
+                            help='test-graph precision on the GPU (core/detector.py): fp32 = the reference '
+                                 'precision (exact fp32 triples on the MFMA kernels), bf16 / fp16 operands with '
+                                 'fp32 accumulation')
+        return parser
     parser.add_argument('--dtype', default='fp32', choices=('fp32', 'bf16x3', 'bf16'),
                         help='training precision on the GPU (ops/precision.py): fp32 = the reference '
                              'precision (exact fp32 triples, six bf16 products), bf16x3 = 16-bit pairs, '
@@ -65,7 +73,8 @@ def init_runtime(args):
     setup_logging(rank)
     if getattr(args, 'dtype', None):
         from ..ops import precision
-        precision.set_default(args.dtype)
+        if args.dtype in precision.PLANES:  # a training precision (eval CLIs also take fp16)
+            precision.set_default(args.dtype)
     if getattr(args, 'cfg', None):
         override(parse_cfg_overrides(args.cfg))
     torch.manual_seed(getattr(args, 'seed', 0) + rank)

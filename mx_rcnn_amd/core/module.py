@@ -348,6 +348,10 @@ class MutableModule(object):
             self.trainer.update_lr()  # lr tensor matches the schedule position
         if 'rng_step' in st:
             self.trainer.rng_step.fill_(int(np.asarray(st['rng_step']).reshape(-1)[0]))
+        elif 'num_update' in st:
+            # a states file from before the dropout counter was saved: the counter advanced once
+            # per update, so re-derive it instead of replaying the first steps' dropout masks
+            self.trainer.rng_step.fill_(int(np.asarray(st['num_update']).reshape(-1)[0]))
         if 'rng_cpu' in st:
             torch.set_rng_state(torch.from_numpy(np.ascontiguousarray(st['rng_cpu'], dtype=np.uint8)))
         if 'rng_cuda' in st and self.context.type == 'cuda':

@@ -186,13 +186,13 @@ class Trainer:
         return {k: (v.detach() if torch.is_tensor(v) else v) for k, v in out.items()}
 
     def check_finite(self, step=None):
-        """Raise FloatingPointError if any step since the last check produced a non-finite loss
-        or a failed device reduction (the proposal NMS chain's give-up, ops/proposal.py) -- one host
-        read of a device counter."""
+        """Raise FloatingPointError if any step since the last check produced a non-finite loss --
+        one host read of a device counter.  (A proposal NMS chain that gives up a poll is finished
+        by the serial fallback and only counted in ``model.nms_gave_up``.)"""
         n = int(self.nonfinite.item())
         if n:
             self.nonfinite.zero_()
-            raise FloatingPointError('non-finite loss (or a failed proposal NMS) in %d step(s) up to step %s'
+            raise FloatingPointError('non-finite loss in %d step(s) up to step %s'
                                      % (n, step))
 
     def arm_fault(self, kind='nan'):

@@ -47,10 +47,13 @@ struct DevGuard {
 // A capture that meets a size for the first time gets a per-call zeroed tensor (never cached: it
 // would live in the graph's private pool).  One chain at a time per buffer: the training step runs
 // one proposal top-k and one anchor sampling per replay, in stream order.
-static Tensor clean_ws(const at::TensorOptions& o, const char* tag, int64_t n) {
+// `layout` joins the key: a chain leaves only the words of ITS layout clean (the anchor chain's mark
+// words are re-zeroed by the next call's first pass at that call's offset), so two calls with the
+// same total size but different region boundaries must not share a buffer.
+static Tensor clean_ws(const at::TensorOptions& o, const char* tag, int64_t n, int64_t layout = 0) {
   static std::mutex mu;
-  static auto* cache = new std::map<std::tuple<int, std::string, int64_t>, Tensor>();  // leaked: outlives exit
-  const auto key = std::make_tuple((int)o.device().index(), std::string(tag), n);
+  static auto* cache = new std::map<std::tuple<int, std::string, int64_t, int64_t>, Tensor>();  // leaked: outlives exit
+  const auto key = std::make_tuple((int)o.device().index(), std::string(tag), n, layout);
   std::lock_guard<std::mutex> lk(mu);
   auto it = cache->find(key);
   if (it != cache->end()) return it->second;
@@ -139,10 +142,12 @@ std::vector<Tensor> nms_proposals(const Tensor& boxes, const Tensor& scores, con
                   reinterpret_cast<uint64_t*>(mask.data_ptr<int64_t>()), st);
     LAUNCH_CHECK("nms_mask");
   }
-  int32_t* fault_p = nullptr;  // the caller's failure counter (int32 on the device): +1 per give-up
+  // the caller's give-up counter (int32 on the device): +1 per image whose multi-workgroup chain gave
+  // up a poll and was redone by the serial fallback (observability; the output is valid either way)
+  int32_t* fault_p = nullptr;
   if (fault.has_value() && fault->defined()) {
     CHECK_DEV(*fault); CHECK_I32(*fault);
-    TORCH_CHECK(fault->numel() >= 1 && fault->device() == boxes.device(), "fault: an int32 counter on the boxes' device");
+    TORCH_CHECK(fault->numel() >= 1 && fault->device() == boxes.device(), "gave_up: an int32 counter on the boxes' device");
     fault_p = fault->data_ptr<int32_t>();
   }
   Tensor rois = at::empty({B, post, 5}, boxes.options());
@@ -269,7 +274,8 @@ std::vector<Tensor> anchor_target_fused(const Tensor& base_anchors, int64_t H, i
   auto o = gt.options();
   // one zeroed workspace: gt_max (B, G) | key histograms (B, 2, bins) | mark workspace
   const int64_t n_gm = (int64_t)B * std::max(G, 1), n_h = (int64_t)B * 2 * mxr::kSampleBins;
-  Tensor ws = clean_ws(o.dtype(at::kInt), "anchor", n_gm + n_h + mxr::anchor_mark_ws_ints(B, N));
+  Tensor ws = clean_ws(o.dtype(at::kInt), "anchor", n_gm + n_h + mxr::anchor_mark_ws_ints(B, N),
+                       ((int64_t)B << 32) | (int64_t)std::max(G, 1));
   int32_t* wsp = ws.data_ptr<int32_t>();
   Tensor max_ov = at::empty({B, N}, o);
   Tensor argmax = at::empty({B, N}, o.dtype(at::kInt));
@@ -1560,7 +1566,7 @@ std::vector<Tensor> proposal_topk(const Tensor& keys, const Tensor& boxes, int64
   TORCH_CHECK(P > 0 && P <= N, "proposal_topk: 0 < P <= N");
   DevGuard g(keys.device());
   auto o = keys.options();
-  Tensor ws = clean_ws(o.dtype(at::kInt), "topk", mxr::proposal_topk_ws_words(B, N));  // histograms: atomics
+  Tensor ws = clean_ws(o.dtype(at::kInt), "topk", mxr::proposal_topk_ws_words(B, N), B);  // histograms: atomics
   Tensor wk = at::empty({(int64_t)B * P}, o.dtype(at::kInt));
   Tensor wi = at::empty({(int64_t)B * P}, o.dtype(at::kInt));
   Tensor sk = at::empty({B, P}, o);

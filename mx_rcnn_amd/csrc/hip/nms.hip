@@ -144,7 +144,15 @@ __global__ void __launch_bounds__(1024)
 nms_reduce_kernel(const float* __restrict__ boxes, const float* __restrict__ scores,
                   const int32_t* __restrict__ n_valid, const uint64_t* __restrict__ maskT, int P, int nb, int post,
                   const float* __restrict__ rand_u, float* __restrict__ rois, float* __restrict__ out_scores,
-                  int64_t* __restrict__ keep_idx, int32_t* __restrict__ n_keep_out, int32_t* keep_ws) {
+                  int64_t* __restrict__ keep_idx, int32_t* __restrict__ n_keep_out, int32_t* keep_ws,
+                  int fallback = 0, int32_t* gave_up = nullptr) {
+  // fallback: launched behind the multi-workgroup reducer, which wrote n_keep = -1 for an image
+  // whose chain gave up; only those images are redone here (the rest exit at once), and each one
+  // redone adds 1 to *gave_up (the caller's give-up counter, if any)
+  if (fallback) {
+    if (n_keep_out[blockIdx.x] != -1) return;  // uniform per workgroup
+    if (threadIdx.x == 0 && gave_up) __hip_atomic_fetch_add(gave_up, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   // single dynamic LDS region (Guideline 17): [nkeep 2 x i32 | pad][removed nb u64][keptw nb u64][keep_list post i32];
   // the keep list moves to global memory (keep_ws, (B, post) int32) when it does not fit in LDS
@@ -298,8 +306,7 @@ nms_reduce_mc_kernel(const float* __restrict__ boxes, const float* __restrict__ 
                      const int32_t* __restrict__ n_valid, const uint64_t* __restrict__ maskT, uint64_t* rec, int P,
                      int nb, int post, const float* __restrict__ rand_u, float* __restrict__ rois,
                      float* __restrict__ out_scores, int64_t* __restrict__ keep_idx,
-                     int32_t* __restrict__ n_keep_out, int32_t* keep_ws, uint64_t* probe, int spin_max,
-                     int32_t* fault) {
+                     int32_t* __restrict__ n_keep_out, int32_t* keep_ws, uint64_t* probe, int spin_max) {
   // dynamic LDS: [own triangle (PER * (PER + 1) / 2) x 64 u64][kept nb u64][rem PER u64][count nb i32][keep list post i32]
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   uint64_t* tri = reinterpret_cast<uint64_t*>(smem);
@@ -464,10 +471,9 @@ nms_reduce_mc_kernel(const float* __restrict__ boxes, const float* __restrict__ 
                         t * 64 + lane, rois, out_scores, keep_idx);
       }
     } else if (s_flag[2] && tid == 0) {
-      n_keep_out[b] = -1;  // a poll gave up: the output of this image is not valid
-      // ... and the step's failure counter says so (the Trainer's non-finite counter: check_finite
-      // raises on the host's next read instead of training on unassembled RoIs)
-      if (fault) __hip_atomic_fetch_add(fault, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // a poll gave up: this image's output is not assembled; the serial reducer launched behind
+      // this kernel (nms_reduce) sees the -1 and redoes the image from the same mask
+      n_keep_out[b] = -1;
     }
   }
   if (assemble) {
@@ -579,7 +585,7 @@ bool nms_keep_in_lds(int P, int post) { return nms_reduce_lds(P, post) <= 160 * 
 
 void nms_reduce(const float* boxes, const float* scores, const int32_t* n_valid, const uint64_t* mask, int B,
                 int P, int post, const float* rand_u, float* rois, float* out_scores, int64_t* keep_idx,
-                int32_t* n_keep, int32_t* keep_ws, hipStream_t st, int32_t* fault) {
+                int32_t* n_keep, int32_t* keep_ws, hipStream_t st, int32_t* gave_up) {
   if (B == 0) return;
   const int nb = div_up(P, 64);
   const int lpost = keep_ws ? 0 : post;
@@ -606,11 +612,15 @@ void nms_reduce(const float* boxes, const float* scores, const int32_t* n_valid,
   if (per == 16)
     nms_reduce_mc_kernel<16><<<grid, 16 * 64, nms_mc_lds(nb, lpost, 16), st>>>(boxes, scores, n_valid, mask, rec, P, nb,
                                                                           post, rand_u, rois, out_scores, keep_idx,
-                                                                          n_keep, keep_ws, probe, spin_max, fault);
+                                                                          n_keep, keep_ws, probe, spin_max);
   else
     nms_reduce_mc_kernel<NMSC_PER><<<grid, NMSC_PER * 64, nms_mc_lds(nb, lpost), st>>>(
         boxes, scores, n_valid, mask, rec, P, nb, post, rand_u, rois, out_scores, keep_idx, n_keep, keep_ws, probe,
-        spin_max, fault);
+        spin_max);
+  // the always-launched fallback: exits at once unless a chain gave up on an image (n_keep = -1),
+  // then finishes that image serially, so a scheduling stall never leaves RoIs unassembled
+  nms_reduce_kernel<<<B, 1024, nms_serial_lds(nb, lpost), st>>>(boxes, scores, n_valid, mask, P, nb, post, rand_u,
+                                                                rois, out_scores, keep_idx, n_keep, keep_ws, 1, gave_up);
 }
 
 }  // namespace mxr

@@ -36,11 +36,12 @@ void nms_mask(const float* boxes, const int32_t* n_valid, int B, int P, float th
               uint64_t* mask, hipStream_t st);
 // Greedy reduction + output assembly: keep up to `post` boxes per image; slots
 // beyond the kept count are filled with keep[floor(u * n_keep)] (rand u in [0,1)).
-// rois (B, post, 5) = [b, x1, y1, x2, y2], out_scores (B, post), n_keep (B).  A multi-workgroup
-// reduce whose poll gives up sets n_keep[b] = -1 and adds 1 to *fault (if given).
+// rois (B, post, 5) = [b, x1, y1, x2, y2], out_scores (B, post), n_keep (B).  An image whose
+// multi-workgroup chain gives up a poll is redone by the serial reducer launched behind it (same
+// result), which adds 1 to *gave_up (if given) per image redone.
 void nms_reduce(const float* boxes, const float* scores, const int32_t* n_valid, const uint64_t* mask,
                 int B, int P, int post, const float* rand_u, float* rois, float* out_scores,
-                int64_t* keep_idx, int32_t* n_keep, int32_t* keep_ws, hipStream_t st, int32_t* fault = nullptr);
+                int64_t* keep_idx, int32_t* n_keep, int32_t* keep_ws, hipStream_t st, int32_t* gave_up = nullptr);
 // device greedy-NMS oracle (MXR_NMS_CHECK): result (B, 2) int32 = {first differing keep position or -1, kept count}
 void nms_check(const float* boxes, const int32_t* n_valid, int B, int P, float thresh, int post,
                const int64_t* keep_idx, const int32_t* n_keep, int32_t* result, hipStream_t st);

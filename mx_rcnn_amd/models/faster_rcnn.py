@@ -62,6 +62,9 @@ class FasterRCNN(nn.Module):
         # the trainer's device-side non-finite step counter, bumped by the loss-combine kernel
         # (core/trainer.py hands it over; None = the caller checks the objective itself)
         self.nonfinite_counter = None
+        # int32 device counter: images whose multi-workgroup NMS chain gave up a poll and were
+        # redone by the serial fallback (csrc/hip/nms.hip); observability only, never a failure
+        self.nms_gave_up = None
         self.network = network
         self.num_classes = num_classes
         if network == 'vgg16' or network == 'vgg':
@@ -178,10 +181,12 @@ class FasterRCNN(nn.Module):
     # ------------------------------------------------------------------ pieces
     def _proposal(self, rpn_cls, rpn_bbox, im_info, key, is_prob=False, after_mask=None):
         c = self.cfg[key]
+        if rpn_cls.is_cuda and (self.nms_gave_up is None or self.nms_gave_up.device != rpn_cls.device):
+            self.nms_gave_up = torch.zeros(1, dtype=torch.int32, device=rpn_cls.device)
         return proposal(rpn_cls.detach(), rpn_bbox.detach(), im_info, self.feat_stride, self.anchor_scales,
                         self.anchor_ratios, c.RPN_PRE_NMS_TOP_N, c.RPN_POST_NMS_TOP_N, c.RPN_NMS_THRESH,
                         c.RPN_MIN_SIZE, is_train=(key == 'TRAIN'), is_prob=is_prob, after_mask=after_mask,
-                        fault=self.nonfinite_counter if key == 'TRAIN' else None)
+                        gave_up=self.nms_gave_up if rpn_cls.is_cuda else None)
 
     def _anchor_target_async(self, data, im_info, gt_boxes, n_gt):
         """Start the RPN anchor-target assignment (which needs only the image shape and the gt

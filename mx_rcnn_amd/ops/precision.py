@@ -209,7 +209,7 @@ def weight_pair(w):
     if ent is not None and ent[0]() is w and ent[3] == p:
         return ent[1], ent[2]
     key = id(w)
-    ver = (w.data_ptr(), w._version, tuple(w.shape), p)
+    ver = (w.data_ptr(), w._version, tuple(w.shape), p, weight_epoch(w))
     hit = _CACHE.get(key)
     if hit is None or hit[0] != ver or hit[1]() is not w:
         fmt = torch.channels_last if w.dim() == 4 else torch.contiguous_format

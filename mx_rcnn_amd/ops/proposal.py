@@ -61,7 +61,7 @@ def _decode_ref(cls, dlt, im_info, base, feat_stride, min_size, crop, is_prob):
 
 def proposal(cls, bbox_deltas, im_info, feat_stride=16, scales=(8, 16, 32), ratios=(0.5, 1, 2),
              pre_nms_top_n=12000, post_nms_top_n=6000, nms_thresh=0.7, min_size=16, is_train=False,
-             is_prob=False, generator=None, after_mask=None, fault=None):
+             is_prob=False, generator=None, after_mask=None, gave_up=None):
     """RPN outputs -> (rois (B, post, 5) fp32 [b, x1, y1, x2, y2], scores (B, post)).
 
     cls: (B, 2A, H, W) logits (or probabilities with is_prob=True), bbox_deltas (B, 4A, H, W),
@@ -105,10 +105,10 @@ def proposal(cls, bbox_deltas, im_info, feat_stride=16, scales=(8, 16, 32), rati
             if after_mask is not None:
                 mask = C.nms_mask_build(sboxes, n_valid, float(nms_thresh))
                 after_mask()
-            # fault: an int32 device counter the multi-workgroup NMS bumps if a poll gives up (its
-            # RoIs are then not valid; the Trainer's check_finite raises on it)
+            # gave_up: an int32 device counter, +1 per image whose multi-workgroup NMS chain gave up
+            # a poll and was finished by the serial fallback (same output; observability only)
             rois, scores, keep, n_keep = C.nms_proposals(sboxes, skeys, n_valid, float(nms_thresh), post, rand_u,
-                                                         mask, fault)
+                                                         mask, gave_up)
             nms_debug_check(sboxes, n_valid, nms_thresh, post, keep, n_keep)
             return rois, scores
         rois = torch.zeros(B, post, 5)

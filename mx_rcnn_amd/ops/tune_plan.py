@@ -7,12 +7,12 @@ make reruns -- and, in principle, ranks -- differ.  This module makes the plan a
 reproducible artefact:
 
 * a plan SHIPPED with the package (``mx_rcnn_amd/tune/gfx950.json``, measured on MI355X for the
-  benchmark configurations) and a user plan file (``MXR_TUNE_FILE``, default
-  ``~/.cache/mx_rcnn_amd/conv_plan_gfx950.json``) are loaded before the first conv; a shape in
-  the plan is never re-timed, so two runs of the same configuration take the same kernels and
-  produce bitwise-equal weights;
-* shapes tuned in this process are merged into the user file (:func:`save`) -- the next run
-  reuses them;
+  benchmark configurations) and, when ``MXR_TUNE_FILE`` names one, a user plan file are loaded
+  before the first conv; a shape in the plan is never re-timed, so two runs of the same
+  configuration take the same kernels and produce bitwise-equal weights;
+* shapes tuned in this process are merged into that user file (:func:`save`) -- the next run
+  reuses them.  Without ``MXR_TUNE_FILE`` nothing is read or written outside the package: no
+  hidden per-machine state decides which kernels a run takes (ADVICE r5);
 * under data parallelism rank 0's plan is broadcast before the step is captured
   (:func:`sync_from_rank0`), and :func:`plan_hash` goes into the capture-agreement check and
   the benchmark record.
@@ -32,8 +32,8 @@ _STATE = {'loaded': False}
 
 
 def user_file():
-    return os.environ.get('MXR_TUNE_FILE') or os.path.join(
-        os.path.expanduser('~'), '.cache', 'mx_rcnn_amd', 'conv_plan_%s.json' % ARCH)
+    """The opt-in user plan file (``MXR_TUNE_FILE``), or None."""
+    return os.environ.get('MXR_TUNE_FILE') or None
 
 
 def read_plan(path):
@@ -67,7 +67,8 @@ def ensure_loaded(ext=None):
     if ext is None:
         from ._ext import need_ext
         ext = need_ext()
-    entries = read_plan(SHIPPED) + read_plan(user_file())  # user entries override shipped ones
+    uf = user_file()
+    entries = read_plan(SHIPPED) + (read_plan(uf) if uf else [])  # user entries override shipped ones
     if entries:
         n = ext.conv_tune_set(entries, False)
         logging.debug('conv plan: %d entries loaded (%d in the table)', len(entries), n)
@@ -88,10 +89,13 @@ def plan_hash(entries=None):
 
 
 def save(path=None):
-    """Merge this process's plan into the user plan file (rank 0 only under DP)."""
+    """Merge this process's plan into the user plan file (rank 0 only under DP; a no-op unless a
+    path is given or ``MXR_TUNE_FILE`` is set)."""
     if os.environ.get('MXR_TUNE_PLAN', '1') == '0':
         return None
     path = path or user_file()
+    if not path:
+        return None
     cur = {k: (t, s) for k, t, s in read_plan(path)}
     shipped = {k: (t, s) for k, t, s in read_plan(SHIPPED)}
     new = {k: (t, s) for k, t, s in table() if shipped.get(k) != (t, s)}

@@ -24,7 +24,7 @@ def predict(args, ctx):
     network = args.network if args.network != 'vgg16' or 'resnet' not in args.prefix else 'resnet50'
     config.TEST.HAS_RPN = True
     model, _, _ = launch.build_model(network, 2 if num_classes == 1000 else num_classes, train_mode='test')
-    det = Detector(model, ctx, arg, aux)
+    det = Detector(model, ctx, arg, aux, compute_dtype=getattr(args, 'dtype', 'fp32'))
     scores, boxes = det.im_detect(data, im_info)
     cls_boxes, cls_scores = boxes[:, 4:8], scores[:, 1]
     keep = np.where(cls_scores >= args.thresh)[0]
@@ -55,7 +55,7 @@ def parse_args(argv=None):
     p.add_argument('--scale', type=int, default=640)
     p.add_argument('--max-scale', dest='max_scale', type=int, default=1024)
     p.add_argument('--out', default='result.jpg')
-    launch.add_common_args(p)
+    launch.add_common_args(p, eval_cli=True)
     return p.parse_args(argv)
 
 

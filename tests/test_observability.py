@@ -153,6 +153,27 @@ def test_exact_resume_from_states(tmp_path):
         np.testing.assert_allclose(a2[k], b2[k], rtol=1e-2, atol=1e-5, err_msg=k)
 
 
+def test_old_states_file_rederives_dropout_counter(tmp_path):
+    """A states file written before the dropout counter was saved ('rng_step' absent) resumes the
+    counter from the update count instead of restarting at 0."""
+    from mx_rcnn_amd.utils import ndarray_io
+    from mx_rcnn_amd.utils.load_model import do_checkpoint
+    pref = str(tmp_path / 'c')
+    torch.manual_seed(3)
+    mod, data = _tiny_module()
+    mod.fit(data, num_epoch=1, epoch_end_callback=do_checkpoint(pref), states_prefix=pref,
+            optimizer_params={'learning_rate': 1e-3, 'momentum': 0.9, 'wd': 5e-4})
+    n = mod.trainer.num_update
+    assert n > 0 and int(mod.trainer.rng_step.item()) == n
+    st = ndarray_io.load(pref + '-0001.states')
+    del st['rng_step']
+    ndarray_io.save(pref + '-old.states', st)
+    mod2, _ = _tiny_module()
+    mod2.init_optimizer(optimizer_params={'learning_rate': 1e-3, 'momentum': 0.9, 'wd': 5e-4})
+    mod2.load_optimizer_states(pref + '-old.states')
+    assert int(mod2.trainer.rng_step.item()) == n
+
+
 def test_watchdog_in_fit_reports_slow_steps_and_stops(monkeypatch):
     """MXR_WATCHDOG=<s> arms the heartbeat inside Module.fit: CPU steps slower than the stall
     limit are reported (the loop itself is not disturbed) and the thread ends with fit."""

@@ -238,6 +238,30 @@ def test_bnb_part_fold_multi_matches_single_folds(cuda):
             assert torch.equal(mg, dg)
 
 
+def _anchor_layouts_with_one_total_size(cuda, cfg):
+    """(G = 8, 38x50 map) and (G = 16, 36x52 map) need the same anchor workspace size
+    (8 + ceil(9*1900/32) == 16 + ceil(9*1872/32)) but put the histogram / mark regions at different
+    offsets: alternating them must reproduce each one's first result (the workspace was
+    keyed by total size only, so the second layout's histograms met the first one's mark words)."""
+    from mx_rcnn_amd import ops
+    runs = {}
+    for rep in range(5):
+        G, (H, W) = (16, (36, 52)) if rep % 2 == 0 else (8, (38, 50))
+        g = torch.Generator().manual_seed(G)
+        gt = torch.full((1, G, 5), -1.0)
+        xy = torch.rand(1, 6, 2, generator=g) * torch.tensor([W * 16 - 220, H * 16 - 220])
+        gt[:, :6, :2] = xy
+        gt[:, :6, 2:4] = xy + 60 + 150 * torch.rand(1, 6, 2, generator=g)
+        gt[:, :6, 4] = 1
+        im_info = torch.tensor([[H * 16.0, W * 16.0, 1.0]], device=cuda)
+        torch.manual_seed(91)
+        o = ops.anchor_target((H, W), gt.to(cuda), torch.tensor([6], dtype=torch.int32, device=cuda), im_info,
+                              scales=(4, 8, 16, 32), cfg=cfg)
+        runs.setdefault(('out', G), o)
+        for k in ('label', 'bbox_target', 'sample_meta'):
+            assert torch.equal(o[k], runs[('out', G)][k]), (rep, G, k)
+
+
 @pytest.mark.gpu
 def test_self_cleaning_workspaces_repeat(cuda):
     """The anchor-sampling and proposal top-k workspaces persist across calls and are left zeroed by
@@ -264,6 +288,7 @@ def test_self_cleaning_workspaces_repeat(cuda):
     for o in outs[1:]:
         for k in ('label', 'bbox_target', 'bbox_inside_weight', 'sample_meta'):
             assert torch.equal(o[k], outs[0][k]), k
+    _anchor_layouts_with_one_total_size(cuda, cfg)
     cls, dlt = _rpn_inputs(4, 9, H, W, B=2)
     cl = cls.to(cuda).contiguous(memory_format=torch.channels_last)
     dl = dlt.to(cuda).contiguous(memory_format=torch.channels_last)

@@ -19,9 +19,10 @@ from mx_rcnn_amd.utils.load_model import load_param  # noqa: E402
 
 
 def test_rcnn(image_set, year, root_path, devkit_path, prefix, epoch, ctx, vis=False, has_rpn=True,
-              proposal='rpn', network='vgg16', end2end=False, imdb_roidb=None, shard=(0, 1)):
+              proposal='rpn', network='vgg16', end2end=False, imdb_roidb=None, shard=(0, 1), dtype='fp32'):
     """``shard=(rank, world)``: each rank runs images ``rank::world`` and ``pred_eval`` gathers
-    them (one process per GPU under torchrun; the reference tests on a single device)."""
+    them (one process per GPU under torchrun; the reference tests on a single device).
+    ``dtype``: the test graph's precision on the GPU ('fp32' as the reference, 'bf16', 'fp16')."""
     rank, world = shard
     if imdb_roidb is not None:  # e.g. synthetic set (in-memory evaluation)
         config.TEST.HAS_RPN = True
@@ -38,7 +39,7 @@ def test_rcnn(image_set, year, root_path, devkit_path, prefix, epoch, ctx, vis=F
         test_data = ROIIter(roidb[rank::world], batch_size=1, shuffle=False, mode='test')
     arg, aux, num_classes = load_param(prefix, epoch, convert=False)
     model, _, _ = launch.build_model(network, num_classes, train_mode='test')
-    det = Detector(model, ctx, arg, aux)
+    det = Detector(model, ctx, arg, aux, compute_dtype=dtype)
     return pred_eval(det, test_data, imdb, vis=vis, shard=shard)
 
 
@@ -56,7 +57,7 @@ def parse_args(argv=None):
     p.add_argument('--end2end', action='store_true')
     p.add_argument('--proposal', default='rpn')
     p.add_argument('--num-classes', dest='num_classes', type=int, default=21, help='for --synthetic sets')
-    launch.add_common_args(p)
+    launch.add_common_args(p, eval_cli=True)
     return p.parse_args(argv)
 
 
@@ -65,4 +66,5 @@ if __name__ == '__main__':
     rank, world, dev = launch.init_runtime(a)
     syn = launch.synthetic_roidb(a, a.num_classes) if a.synthetic else None
     test_rcnn(a.image_set, a.year, a.root_path, a.devkit_path, a.prefix, a.epoch, dev, a.vis,
-              a.has_rpn or a.end2end, a.proposal, a.network, a.end2end, imdb_roidb=syn, shard=(rank, world))
+              a.has_rpn or a.end2end, a.proposal, a.network, a.end2end, imdb_roidb=syn, shard=(rank, world),
+              dtype=a.dtype)

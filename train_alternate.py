@@ -52,7 +52,8 @@ def alternate_train(image_set, test_image_set, year, root_path, devkit_path, pre
               rank=rank, world=world)
     pdist.barrier()
     logging.info('########## GENERATE RPN DETECTION')
-    boxes = test_rpn(image_set, year, root_path, devkit_path, p('rpn1'), rpn_epoch, ctx, network=network, imdb_roidb=gt())
+    boxes = test_rpn(image_set, year, root_path, devkit_path, p('rpn1'), rpn_epoch, ctx, network=network, imdb_roidb=gt(),
+                     dtype=_dump_dtype())
     logging.info('########## TRAIN RCNN WITH IMAGENET INIT AND RPN DETECTION')
     config.TRAIN.BATCH_SIZE = 128
     config.TRAIN.BATCH_IMAGES = batch_images
@@ -69,7 +70,8 @@ def alternate_train(image_set, test_image_set, year, root_path, devkit_path, pre
               rank=rank, world=world)
     pdist.barrier()
     logging.info('########## GENERATE RPN DETECTION')
-    boxes = test_rpn(image_set, year, root_path, devkit_path, p('rpn2'), rpn_epoch, ctx, network=network, imdb_roidb=gt())
+    boxes = test_rpn(image_set, year, root_path, devkit_path, p('rpn2'), rpn_epoch, ctx, network=network, imdb_roidb=gt(),
+                     dtype=_dump_dtype())
     logging.info('########## COMBINE RPN2 WITH RCNN1')
     if rank == 0:
         combine_model(p('rpn2'), rpn_epoch, p('rcnn1'), rcnn_epoch, p('rcnn2'), 0)
@@ -107,6 +109,12 @@ def parse_args(argv=None):
     ap.add_argument('--model-dir', dest='model_dir', default='model')
     launch.add_common_args(ap)
     return ap.parse_args(argv)
+
+
+def _dump_dtype():
+    """Precision of the proposal dumps: bf16 when training in bf16, else the reference's fp32."""
+    from mx_rcnn_amd.ops import precision
+    return 'bf16' if precision.default_name() == 'bf16' else 'fp32'
 
 
 def main(args):

@@ -245,6 +245,11 @@ def run(args, precision, rank, world, device):
                 'ranks_agree': pdist.all_reduce_max(float(ph), device) == -pdist.all_reduce_max(-float(ph), device)}
     # after the timed region: each gradient bucket's collective in isolation (HIP events)
     comm = trainer.reducer.measure_collectives() if world > 1 else None
+    replicas = None
+    if world > 1:  # data-parallel replicas must hold bitwise-equal weights after the timed steps
+        dg = float(trainer.store.weights_digest())
+        replicas = {'digest': '%08x' % int(dg),
+                    'agree': pdist.all_reduce_max(dg, device) == -pdist.all_reduce_max(-dg, device)}
     ms = elapsed / max(args.steps, 1) * 1e3
     imgs = args.ims_per_gpu * world * args.steps
     value = imgs / elapsed
@@ -265,6 +270,7 @@ def run(args, precision, rank, world, device):
                       'rois_per_image': cfg.TRAIN.BATCH_SIZE, 'exec': mode,
                       'objective_first_last': [round(loss0, 4), round(loss1, 4)],
                       'backend': pdist.backend_name(), 'allreduce': comm, 'conv_plan': plan,
+                      'replicas': replicas,
                       'rccl': pdist.rccl_env() if pdist.backend_name() == 'nccl' else None,
                       'hip_runtime': __import__('mx_rcnn_amd').runtime_settings()}}
     del step_fn, trainer

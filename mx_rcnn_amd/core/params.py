@@ -341,6 +341,19 @@ class FlatParamStore:
                     b.data.copy_(t)
         self.refresh_dgrad_cache()
 
+    @torch.no_grad()
+    def weights_digest(self):
+        """A bit-sensitive checksum of every trainable fp32 master (int in [0, 2^31 - 1)): equal on
+        data-parallel replicas exactly when their weights are bitwise equal (up to hash collisions).
+        One device reduction per group; for checks outside the timed region."""
+        mod = (1 << 31) - 1
+        acc = 0
+        for g in self.groups:
+            v = g.master.view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+            w = torch.arange(v.numel(), device=v.device, dtype=torch.int64) % 8191 + 1
+            acc = (acc * 1000003 + int(((v * w) % mod).sum().item())) % mod
+        return acc
+
     # ------------------------------------------------------------------ step pieces
     def zero_grad(self):
         for g in self.groups:

@@ -255,6 +255,9 @@ class _BaseLoader:
     next = __next__
 
     def get_batch(self):
+        if not self._batches:
+            raise ValueError('%d images do not fill one global batch of %d (%d per rank x %d ranks)'
+                             % (self.size, self.batch_size * self.world_size, self.batch_size, self.world_size))
         return self._make_batch(min(self.cur, len(self._batches) - 1))
 
 

@@ -1,33 +1,30 @@
 """MI355X-native Faster R-CNN (mx-rcnn capabilities on PyTorch-ROCm + gfx950 HIP kernels).
 
-Importing the package sets the HIP runtime defaults the training step is tuned for; they are
-read when the HIP runtime initialises (the first GPU call), so the package must be imported
-before anything touches the GPU -- every entry point here does.  A value already in the
-environment wins.
+HIP runtime settings.  The package sets NO runtime variable by default.  ``MXR_GRAPH_QUEUES=n``
+(opt-in) sets the HIP runtime's debug variable ``DEBUG_HIP_FORCE_GRAPH_QUEUES=n`` before the runtime
+initialises (the package must then be imported before anything touches the GPU -- every entry point
+here does; a warning says when the import came too late): a replayed hipGraph's independent branches
+are spread over n hardware queues instead of the runtime's default four.
 
-* ``DEBUG_HIP_FORCE_GRAPH_QUEUES=2`` (a HIP runtime debug variable; ``MXR_GRAPH_QUEUES`` picks the
-  value, 0 leaves the runtime default, and a warning says when the import came too late for it
-  to act): a replayed hipGraph's independent branches are spread over
-  two hardware queues instead of the runtime's default four.  The step's concurrency is two-way
-  (the compute stream plus one side stream at a time: anchor targets / RPN losses / proposal
-  chain / dgrad filter cache), and every extra queue adds cross-queue dependency waits.
-  Measured on the ResNet-101 e2e step (bench.py, same box, interleaved): 1 queue 157.2,
-  2 queues 159.7, 3 queues 150.8, default 151.5 img/s (docs/DESIGN.md §2); round 4
-  (profiles/r4_ab_defaults.txt): fp32 77.4 with 2 vs 75.9 / 75.9 / 75.7 with the default / 1 / 3,
-  bf16 160.3 vs 151.4 / 159.4.
+Measured on the fp32 ResNet-101 e2e step (bench.py, same box, interleaved, round 6;
+profiles/r6_graph_queues_ab.txt): 2 queues with one side stream per role 77.9 img/s; the runtime
+default with the roles on ONE side stream (the package default, ``MXR_SIDE_STREAMS``, fewer parallel
+branches in the captured DAG) 76.9; the default with one stream per role 76.2; 1 queue 77.4; no side
+streams at all 76.8.  Round 5 kept the debug variable as a package default (+2 %); the verdict asked
+for a supported mechanism, so it is opt-in now and the headline is reported without it.
 """
 import os
 import sys
 import warnings
 
-# MXR_GRAPH_QUEUES=n picks the queue count (0: leave the runtime's default and its variable alone)
-_GQ = os.environ.get('MXR_GRAPH_QUEUES', '2')
+# MXR_GRAPH_QUEUES=n (opt-in) picks the graph queue count (unset / 0: the runtime's default)
+_GQ = os.environ.get('MXR_GRAPH_QUEUES', '0')
 RUNTIME_DEFAULTS = {'DEBUG_HIP_FORCE_GRAPH_QUEUES': _GQ} if _GQ not in ('', '0') else {}
 
 
 def runtime_settings():
     """The HIP runtime variables in effect (recorded with benchmark results)."""
-    return {k: os.environ.get(k) for k in ('DEBUG_HIP_FORCE_GRAPH_QUEUES', 'GPU_MAX_HW_QUEUES')}
+    return {k: os.environ.get(k) for k in ('DEBUG_HIP_FORCE_GRAPH_QUEUES', 'GPU_MAX_HW_QUEUES', 'MXR_SIDE_STREAMS')}
 
 
 for _k, _v in RUNTIME_DEFAULTS.items():

@@ -296,7 +296,8 @@ class FlatParamStore:
             return lambda: None
         main = torch.cuda.current_stream(self.device)
         if getattr(self, '_cache_stream', None) is None:
-            self._cache_stream = torch.cuda.Stream(device=self.device)
+            from ..models.faster_rcnn import _aux_stream
+            self._cache_stream = _aux_stream(self.device, 'cache')
         side = self._cache_stream
         side.wait_stream(main)
         with torch.cuda.stream(side):

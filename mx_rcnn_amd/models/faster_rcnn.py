@@ -389,6 +389,14 @@ _AUX = {}
 
 
 def _aux_stream(device, role='aux'):
+    """Per-device side stream of a role ('aux': anchor targets / RPN losses, 'proposal': the
+    proposal chain, 'cache': the dgrad filter cache + gradient clear).  MXR_SIDE_STREAMS=1 (the
+    default under the runtime's own graph-queue count) puts every role on ONE side stream: fewer
+    parallel branches in the captured step's DAG, fewer cross-queue waits (mx_rcnn_amd/__init__.py);
+    with the opt-in MXR_GRAPH_QUEUES=2 one stream per role measured better (default 0 there)."""
+    dflt = '0' if os.environ.get('DEBUG_HIP_FORCE_GRAPH_QUEUES') else '1'
+    if os.environ.get('MXR_SIDE_STREAMS', dflt) == '1':
+        role = 'aux'
     s = _AUX.get((device.index, role))
     if s is None:
         s = torch.cuda.Stream(device=device)

@@ -1,7 +1,7 @@
 """Per-queue busy time, chip-level idle time and the critical-path picture of graph-replayed
 training steps from a rocprofv3 kernel trace.
 
-    python tools/stream_overlap.py gpurun_out/prof/run_kernel_trace.csv [--marker nms_reduce] [--steps 5]
+    python tools/stream_overlap.py gpurun_out/prof/run_kernel_trace.csv [--marker nms_reduce_mc] [--steps 5]
 
 Steps are delimited by a once-per-step marker kernel; the last --steps complete steps are used.
 """
@@ -13,7 +13,7 @@ import csv
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('trace')
-    ap.add_argument('--marker', default='nms_reduce')
+    ap.add_argument('--marker', default='nms_reduce_mc')
     ap.add_argument('--steps', type=int, default=5)
     ap.add_argument('--gaps', type=int, default=15, help='largest idle gaps to list')
     a = ap.parse_args()

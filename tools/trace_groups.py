@@ -1,6 +1,6 @@
 """Group a rocprofv3 kernel_trace.csv by (kernel, grid, workgroup) over the last N steps.
 
-    python tools/trace_groups.py gpurun_out/prof/run_kernel_trace.csv [--marker nms_reduce] [--steps 10] [--top 60]
+    python tools/trace_groups.py gpurun_out/prof/run_kernel_trace.csv [--marker nms_reduce_mc] [--steps 10] [--top 60]
 
 A "step" boundary is an occurrence of the marker kernel (one per training step).  Prints, per
 launch shape: ms/step, launches/step, mean us, VGPRs, LDS bytes -- enough to map the dispatches of
@@ -21,7 +21,7 @@ def short(name):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('trace')
-    ap.add_argument('--marker', default='nms_reduce')
+    ap.add_argument('--marker', default='nms_reduce_mc')
     ap.add_argument('--steps', type=int, default=10)
     ap.add_argument('--top', type=int, default=60)
     ap.add_argument('--filter', default='')

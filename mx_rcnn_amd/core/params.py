@@ -371,10 +371,14 @@ class FlatParamStore:
         the start of the next step, concurrently with its forward pass).  ``clear``: the update
         kernel zeroes each group's gradient buffer after reading it (replaces zero_grad).
         Parameters whose update ran fused into their weight gradient this step
-        (enable_fused_sgd) are skipped."""
+        (enable_fused_sgd), and ranges the reducer already updated after their all-reduce
+        (:meth:`mark_updated`), are skipped."""
+        early = getattr(self, '_early', {})
+        self._early = {}
         for gi, g in enumerate(self.groups):
             grad = grad_for(g) if grad_for is not None else g.grad
-            skip = sorted((sp['off'], sp['off'] + sp['numel']) for sp in self._fused.get(gi, ()) if sp['applied'])
+            skip = sorted([(sp['off'], sp['off'] + sp['numel']) for sp in self._fused.get(gi, ()) if sp['applied']] +
+                          early.get(id(g), []))
             for sp in self._fused.get(gi, ()):
                 sp['applied'] = False
             if not skip:
@@ -397,6 +401,13 @@ class FlatParamStore:
                               clip, sh, planes=g.x2 or 1, zero=g.grad[s0:e0] if clear else None, plane_stride=pst)
         if refresh:
             self.refresh_dgrad_cache()
+
+    def mark_updated(self, group, start, end):
+        """[start, end) of ``group`` got its SGD update this step already (the reducer's per-bucket
+        update after the bucket's all-reduce, parallel/reducer.py): the next sgd_step skips it."""
+        if not hasattr(self, '_early'):
+            self._early = {}
+        self._early.setdefault(id(group), []).append((int(start), int(end)))
 
     def enable_fused_sgd(self, names, lr, momentum=0.9, wd=0.0005, rescale=1.0, clip=-1.0):
         """Let the weight-gradient kernels of parameters ``names`` apply their SGD update in place

@@ -51,8 +51,12 @@ class Trainer:
         self.mode = mode
         self.store = FlatParamStore(self.model, fixed_param_prefix, compute_dtype, dev, channels_last,
                                    mode=mode if mode in ('rpn', 'rcnn') else None, x2=self.x2)
+        # VGG16's fc6 / fc7 (120 M of 137 M weights): single process, their update runs inside their
+        # weight gradient (below); under data parallelism the gradient must be summed first, so their
+        # buckets take the update on the reducer's optimizer stream right after their all-reduce
+        fc_names = ('fc6_weight', 'fc7_weight') if os.environ.get('MXR_FUSED_FC_SGD', '1') != '0' else ()
         self.reducer = BucketReducer(self.store, bucket_mb=bucket_mb, average=average_grads,
-                                     comm_dtype=grad_comm_dtype)
+                                     comm_dtype=grad_comm_dtype, sgd_names=fc_names)
         if self.reducer.dp:
             self.store.broadcast_(0)  # identical starting weights on every rank
         self.momentum, self.wd, self.clip, self.rescale = momentum, wd, clip_gradient, rescale_grad

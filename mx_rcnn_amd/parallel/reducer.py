@@ -33,8 +33,16 @@ from ..ops import grad_sink
 from .dist import get_world_size, is_distributed
 
 
+class _nullctx(object):
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False
+
+
 class _Bucket:
-    __slots__ = ('group', 'buf', 'comm', 'start', 'end', 'names', 'pending', 'work', 'updated')
+    __slots__ = ('group', 'buf', 'comm', 'start', 'end', 'names', 'pending', 'work', 'updated', 'early')
 
     def __init__(self, group, start, end, comm=None):
         self.group, self.buf, self.start, self.end = group, group.grad, start, end
@@ -43,6 +51,7 @@ class _Bucket:
         self.pending = 0
         self.work = None
         self.updated = False
+        self.early = False  # gets its SGD right after its all-reduce (BucketReducer sgd_names)
 
 
 class BucketReducer:
@@ -56,11 +65,16 @@ class BucketReducer:
       and a parameter's value is not read again once its gradient is final (each weight belongs
       to one layer; its dgrad and wgrad are both done when the readiness hook fires), so
       updating it early is exact.  Single-GPU buckets are ``sgd_bucket_mb`` (smaller: only the
-      last one is exposed after the backward).
+      last one is exposed after the backward);
+    * under data parallelism, ``sgd_names``: only the buckets holding those parameters take their
+      update on the optimizer stream right after their all-reduce (VGG16's fc6 / fc7: 120 M of its
+      137 M weights, whose HBM-bound update would otherwise be the end-of-step tail -- the
+      single-process step fuses it into the weight gradient instead, which DP cannot: the gradient
+      must be summed first); the end-of-step SGD covers the rest (``store.mark_updated``).
     """
 
     def __init__(self, store, bucket_mb=25, average=False, overlap=True, sgd_bucket_mb=8, tail_mb=4,
-                 comm_dtype=None):
+                 comm_dtype=None, sgd_names=None):
         self.store = store
         self.world = get_world_size()
         self.average = average
@@ -81,6 +95,7 @@ class BucketReducer:
         self._clear = False
         self._widen_stream = None
         self._opt_stream = None
+        self._early_sgd = None
         self.sgd_applied = False
         if not (self.dp or self.sgd_capable):
             return
@@ -113,6 +128,10 @@ class BucketReducer:
                 self.buckets.append(bkt)
                 for n in names:
                     self._param_bucket[n] = bkt
+        if self.dp and sgd_names and not self.sgd_capable:
+            for b in self.buckets:
+                b.early = any(n in sgd_names for n in b.names)
+        self.early_names = sorted(n for b in self.buckets if b.early for n in b.names)
         if self.overlap or self.sgd_capable:
             grad_sink.clear_hooks(store.params.values())  # an earlier reducer on these parameters
             for n, p in store.params.items():
@@ -126,7 +145,7 @@ class BucketReducer:
             if b.pending == 0:
                 if self.overlap:
                     self._launch(b)
-                if self._sgd is not None:
+                if self._sgd is not None or (b.early and self._early_sgd is not None):
                     self._update(b)
         return hook
 
@@ -162,15 +181,18 @@ class BucketReducer:
         b.work = dist.all_reduce(t, op=dist.ReduceOp.SUM, async_op=True)
 
     def _update(self, b):
-        """SGD of one final bucket on the optimizer stream (after its all-reduce under DP)."""
+        """SGD of one final bucket on the optimizer stream (after its all-reduce under DP; the CPU
+        runs it in order)."""
         from ..ops.sgd import sgd_momentum_
-        if self._opt_stream is None:
+        cuda = b.buf.is_cuda
+        if cuda and self._opt_stream is None:
             self._opt_stream = torch.cuda.Stream(device=b.buf.device)
         os_ = self._opt_stream
-        os_.wait_stream(torch.cuda.current_stream(b.buf.device))
+        if cuda:
+            os_.wait_stream(torch.cuda.current_stream(b.buf.device))
         g, s, e = b.group, b.start, b.end
-        lr, mu, wd, rescale, clip = self._sgd
-        with torch.cuda.stream(os_):
+        lr, mu, wd, rescale, clip = self._sgd if self._sgd is not None else self._early_sgd
+        with (torch.cuda.stream(os_) if cuda else _nullctx()):
             if b.work is not None:
                 b.work.wait()  # the optimizer stream waits for this bucket's collective
             if g.shadow is not None and g.x2:  # planes g.plane apart: the view from s reaches all of them
@@ -180,12 +202,15 @@ class BucketReducer:
             sgd_momentum_(g.master[s:e], g.mom[s:e], self.grad_for(g)[s:e], lr, mu, wd if g.decay else 0.0, rescale,
                           clip, sh, planes=planes, zero=g.grad[s:e] if self._clear else None, plane_stride=stride)
         b.updated = True
+        if self._sgd is None:  # early (sgd_names) bucket: the end-of-step SGD skips it
+            self.store.mark_updated(g, s, e)
 
     def prepare(self, sgd=None, clear=False):
         """Call before backward: reset per-bucket counters.  ``sgd=(lr_tensor, momentum, wd,
         rescale, clip)`` enables the overlapped optimizer for this step (GPU only); ``clear``: its
         update kernels zero the gradient buffers they consumed."""
         self._sgd = sgd if (sgd is not None and self.sgd_capable and self.buckets) else None
+        self._early_sgd = sgd if (sgd is not None and self._sgd is None and self.early_names) else None
         self._clear = bool(clear)
         self.sgd_applied = False
         for b in self.buckets:
@@ -206,13 +231,18 @@ class BucketReducer:
                 if not b.updated:
                     self._update(b)
             self.sgd_applied = True
+        elif self._early_sgd is not None:
+            for b in self.buckets:
+                if b.early and not b.updated:
+                    self._update(b)
         for b in self.buckets:
             if b.work is not None:
                 b.work.wait()
                 b.work = None
-        if self._opt_stream is not None and self._sgd is not None:
+        if self._opt_stream is not None and (self._sgd is not None or self._early_sgd is not None):
             torch.cuda.current_stream(self._opt_stream.device).wait_stream(self._opt_stream)
         self._sgd = None
+        self._early_sgd = None
 
     def bucket_sizes(self):
         """Bytes each bucket puts on the wire."""

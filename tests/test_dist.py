@@ -432,3 +432,54 @@ def test_two_rank_check_tool_sums_like_rescale_two_on_cpu(tmp_path):
     for k in keys:
         assert torch.equal(r0[k], r1[k]), ('replicas differ', k)
         assert torch.equal(ref[k], r0[k]), ('DP sum differs from the 2x-rescaled step', k)
+
+
+def _fc_worker(rank, world, port, out_dir, early):
+    os.environ.update({'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port), 'RANK': str(rank),
+                       'WORLD_SIZE': str(world), 'LOCAL_RANK': str(rank), 'MXR_FUSED_FC_SGD': '1' if early else '0'})
+    from mx_rcnn_amd.config import snapshot
+    from mx_rcnn_amd.core.trainer import Trainer
+    from mx_rcnn_amd.models import FasterRCNN
+    from mx_rcnn_amd.parallel import dist as pdist
+    pdist.init_distributed(backend='gloo')
+    torch.manual_seed(0)
+    cfg = snapshot()
+    cfg.TRAIN.BG_THRESH_LO = 0.0
+    cfg.END2END = 1
+    cfg.TRAIN.BBOX_NORMALIZATION_PRECOMPUTED = True
+    cfg.TRAIN.RPN_PRE_NMS_TOP_N = 600
+    cfg.TRAIN.RPN_POST_NMS_TOP_N = 200
+    m = FasterRCNN('vgg16', 6, cfg=cfg)
+    m.head.dropout = 0.0
+    tr = Trainer(m, 'e2e', fixed_param_prefix=['conv1', 'conv2'], lr=0.01, device='cpu', bucket_mb=64)
+    names = tr.reducer.early_names
+    g = torch.Generator().manual_seed(50 + rank)
+    gt = torch.tensor([[[10., 20., 80., 100., 3.], [50., 60., 150., 140., 2.]]])
+    for step in range(2):
+        torch.manual_seed(100 * step + rank)
+        tr.step({'data': torch.randn(1, 3, 128, 192, generator=g) * 50, 'im_info': torch.tensor([[128., 192., 1.0]]),
+                 'gt_boxes': gt, 'n_gt': torch.tensor([2], dtype=torch.int32)})
+    st = {k: v.clone() for k, v in tr.store.state_arrays().items()}
+    st.update({'mom:' + k: v.clone() for k, v in tr.store.optimizer_state().items()})
+    st['_early'] = torch.tensor([len(names), int('fc6_weight' in names)])
+    torch.save(st, os.path.join(out_dir, 'f%d_%d.pt' % (int(early), rank)))
+    pdist.barrier()
+    pdist.destroy()
+
+
+def test_vgg16_fc_update_after_allreduce_gloo():
+    """under data parallelism VGG16's fc6 / fc7 buckets take their SGD as soon as
+    their all-reduce completes (parallel/reducer.py sgd_names) and the end-of-step SGD skips them;
+    two gloo ranks, two steps: weights and momenta bitwise equal to the plain end-of-step update, and
+    the replicas agree."""
+    with tempfile.TemporaryDirectory() as d:
+        for early in (True, False):
+            mp.spawn(_fc_worker, args=(2, _free_port(), d, early), nprocs=2, join=True)
+        e0, e1 = [torch.load(os.path.join(d, 'f1_%d.pt' % r), weights_only=True) for r in range(2)]
+        p0 = torch.load(os.path.join(d, 'f0_0.pt'), weights_only=True)
+    assert int(e0['_early'][1]) == 1 and int(p0['_early'][0]) == 0
+    keys = [k for k in p0 if not k.startswith('_')]
+    assert len(keys) > 20
+    for k in keys:
+        assert torch.equal(e0[k], e1[k]), ('replicas differ', k)
+        assert torch.equal(e0[k], p0[k]), ('early fc update differs from the end-of-step SGD', k)

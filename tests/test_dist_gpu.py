@@ -17,7 +17,7 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def _run(tmp_path, name, precision, dp, port, steps, plan_file=None):
+def _run(tmp_path, name, precision, dp, port, steps, plan_file=None, extra=()):
     out = str(tmp_path / (name + '.pt'))
     env = dict(os.environ)
     for k in ('MXR_FORCE_DIST', 'WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
@@ -32,7 +32,7 @@ def _run(tmp_path, name, precision, dp, port, steps, plan_file=None):
         env.update({'MXR_FORCE_DIST': '1', 'WORLD_SIZE': '1', 'RANK': '0', 'LOCAL_RANK': '0',
                     'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port)})
     r = subprocess.run([sys.executable, os.path.join(ROOT, 'tools', 'dp_step_check.py'), out, '--precision', precision,
-                        '--steps', str(steps)],
+                        '--steps', str(steps)] + list(extra),
                        env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:]
     return torch.load(out, weights_only=True), r.stdout
@@ -60,6 +60,24 @@ def test_rccl_one_rank_graphed_step_matches_single_process(tmp_path, precision):
         nondet[:5], [float((a[k].float() - b[k].float()).abs().max()) for k in nondet[:5]])
     diff = [k for k in keys if not torch.equal(a[k], d[k])]
     assert not diff, 'DP step differs: %s (max abs %s)' % (
+        diff[:5], [float((a[k].float() - d[k].float()).abs().max()) for k in diff[:5]])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('precision', ['bf16', 'fp32'])
+def test_vgg16_fc_update_after_allreduce_matches_fused_single_process(tmp_path, precision):
+    """VGG16 e2e under a 1-rank RCCL group: fc6 / fc7 take their SGD on the reducer's optimizer
+    stream right after their buckets' all-reduce (parallel/reducer.py sgd_names), the rest at the
+    end of the step; the single-process step fuses the same update into the weight gradient.  Two
+    graphed steps, every weight bitwise equal."""
+    ex = ('--mode', 'e2e', '--network', 'vgg16', '--image', '224x320')
+    a, la = _run(tmp_path, 'vgg_plain', precision, False, 0, 2, extra=ex)
+    d, ld = _run(tmp_path, 'vgg_dp', precision, True, 29660 + ['bf16', 'fp32'].index(precision), 2, extra=ex)
+    assert int(a['_dp'][4]) == 2, la  # fused into the wgrad in the single process
+    assert int(d['_dp'][0]) == 1 and int(d['_dp'][3]) >= 2, ld  # DP: early bucket updates
+    keys = [k for k in a if not k.startswith('_')]
+    diff = [k for k in keys if not torch.equal(a[k], d[k])]
+    assert not diff, 'DP fc update differs: %s (max abs %s)' % (
         diff[:5], [float((a[k].float() - d[k].float()).abs().max()) for k in diff[:5]])
 
 

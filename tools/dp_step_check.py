@@ -4,7 +4,7 @@ runs under a 1-rank RCCL process group: every gradient bucket goes through the r
 all-reduce, captured inside the hipGraph, so comparing against a run without the group checks the
 DP path end to end on one GPU.
 
-    python tools/dp_step_check.py OUT.pt [--precision bf16|fp32] [--steps 3] [--mode rcnn|e2e]
+    python tools/dp_step_check.py OUT.pt [--precision bf16|fp32] [--steps 3] [--mode rcnn|e2e] [--network vgg16]
 """
 import argparse
 import os
@@ -44,8 +44,13 @@ def main():
     pool = [synthetic_batch(1, h, w, 21, device, gen) for _ in range(2)]
     if args.mode == 'rcnn':
         pool = [rcnn_batch(b, 21, cfg.TRAIN.BATCH_SIZE, gen) for b in pool]
-    model.to(device).calibrate_bn(pool[0]['data'])
-    tr = Trainer(model, args.mode, fixed_param_prefix=['conv0', 'stage1', 'bn_data', 'bn0'], lr=0.01, momentum=0.9,
+    vgg = args.network.startswith('vgg')
+    if vgg:
+        model.to(device).calibrate_vgg(pool[0]['data'])
+    else:
+        model.to(device).calibrate_bn(pool[0]['data'])
+    fixed = ['conv1', 'conv2'] if vgg else ['conv0', 'stage1', 'bn_data', 'bn0']
+    tr = Trainer(model, args.mode, fixed_param_prefix=fixed, lr=0.01, momentum=0.9,
                  wd=0.0005, clip_gradient=1.0, device=device, precision=args.precision)
     g = GraphedStep(tr, pool[0], warmup=2)
     for i in range(args.steps):
@@ -53,7 +58,8 @@ def main():
     torch.cuda.synchronize()
     state = {k: v.detach().cpu().clone() for k, v in tr.store.state_arrays().items()}
     state['_objective'] = out['objective'].detach().float().cpu().reshape(1)
-    state['_dp'] = torch.tensor([int(tr.reducer.dp), len(tr.reducer.buckets), world])
+    state['_dp'] = torch.tensor([int(tr.reducer.dp), len(tr.reducer.buckets), world, len(tr.reducer.early_names),
+                                 len(tr.fused_fc_sgd)])
     torch.save(state, args.out)
     print('saved %d arrays, dp=%d buckets=%d backend=%s' % (len(state), tr.reducer.dp, len(tr.reducer.buckets),
                                                            pdist.backend_name()))

@@ -1050,7 +1050,7 @@ std::vector<Tensor> conv_igemm_fwd(const Tensor& x, const Tensor& w, c10::option
       if (ep.x2 && getenv("MXR_X2W") != nullptr) cands.push_back({26, 1});
       // large grids: the 256-row tiles of conv_big.hip (512 threads, 4-tile LDS ring)
       if ((int64_t)NB * Ho * Wo >= 16384 && !ep.x2 && getenv("MXR_NO_BIG") == nullptr)
-        for (int c : {200, 201, 202, 203}) cands.push_back({c, 1});
+        for (int c : {200, 201, 202, 203, 204}) cands.push_back({c, 1});
       // grids far below one tile per CU (the FC head: M = 128 RoIs, K up to 25088): split K
       const int64_t Mrows = (int64_t)NB * Ho * Wo;
       const int nkk = KH * KW * (Cin / 64);

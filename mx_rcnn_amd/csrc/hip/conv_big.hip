@@ -64,8 +64,11 @@ struct BigCfg {
   static constexpr int WM = BM / WGM;        // rows per wave (128, 64 or 32)
   static constexpr int TM = WM / 16, TN = 4; // 16x16 accumulator tiles per wave
   static constexpr int ROWS = BM + BN;       // LDS rows per K tile
-  static constexpr int LA = BM / 128, LB = BN / 128;  // DMA instructions per thread per K tile (A / B)
-  static constexpr int LPT = LA + LB;
+  // DMA instruction i of wave w loads LDS rows i*128 + 16w .. +15 (A rows first, then B rows): a wave
+  // issues LPT_HI instructions per K tile if its last block exists (w < NHI), else LPT_LO
+  static constexpr int LPT_HI = (ROWS + 127) / 128, LPT_LO = ROWS / 128;
+  static constexpr int NHI = (ROWS % 128) / 16;  // waves with the extra (partial-round) instruction
+  static_assert(BM % 16 == 0 && BN % 64 == 0 && ROWS % 16 == 0, "16-row DMA blocks never straddle A / B");
   static constexpr int EPI_LD = 64 + 4;      // fp32 row stride of the per-wave epilogue slab
 };
 
@@ -98,15 +101,17 @@ __device__ __forceinline__ void conv_big_body(uint16_t* lds, const uint16_t* __r
 
   // DMA roles: instruction i of a thread loads LDS row i*128 + tid/4 (A rows first, then B rows),
   // logical 16-B chunk (tid & 3) ^ ((row >> 2) & 3) of that row's 32 channels
-  uint32_t off[C::LPT];
-  uint64_t amask[C::LA];
+  const int lpt = wid < C::NHI ? C::LPT_HI : C::LPT_LO;  // wave-uniform
+  uint32_t off[C::LPT_HI];
+  uint64_t amask[C::LPT_HI];
 #pragma unroll
-  for (int i = 0; i < C::LPT; ++i) {
+  for (int i = 0; i < C::LPT_HI; ++i) {
     const int row = i * 128 + (tid >> 2);
     const int lc = (tid & 3) ^ ((row >> 2) & 3);
     off[i] = kOOB;
-    if (i < C::LA) {
-      amask[i] = 0;
+    amask[i] = 0;
+    if (row >= C::ROWS) continue;
+    if (row < BM) {
       const int m = m0 + row;
       if (m < M) {
         const int img = m / (Ho * Wo), rem = m % (Ho * Wo);
@@ -131,8 +136,10 @@ __device__ __forceinline__ void conv_big_body(uint16_t* lds, const uint16_t* __r
     const uint32_t soff_b = (uint32_t)((c_tap * Cin + c_ci) * 2);
     uint16_t* base = lds + (buf * C::ROWS + wid * 16) * BK;  // this wave's 16 rows of instruction 0
 #pragma unroll
-    for (int i = 0; i < C::LPT; ++i) {
-      if (i < C::LA) {
+    for (int i = 0; i < C::LPT_HI; ++i) {
+      const int row0 = i * 128 + wid * 16;  // wave-uniform role of this instruction
+      if (row0 >= C::ROWS) continue;
+      if (row0 < BM) {
         const uint32_t vo = ((amask[i] >> c_tap) & 1ull) ? off[i] + tap_a : kOOB;
         dma16(xr, base + i * 128 * BK, vo, soff_a);
       } else {
@@ -165,9 +172,15 @@ __device__ __forceinline__ void conv_big_body(uint16_t* lds, const uint16_t* __r
   for (int kt = 0; kt < nk; ++kt) {
     // K tile kt landed: at most min(2, nk-1-kt) younger tiles of this thread still in flight
     const int ahead = min(NBUF - 2, nk - 1 - kt);
-    if (ahead >= 2) vm_wait<2 * C::LPT>();
-    else if (ahead == 1) vm_wait<C::LPT>();
-    else vm_wait<0>();
+    if (ahead >= 2) {
+      if (C::NHI == 0 || lpt == C::LPT_LO) vm_wait<2 * C::LPT_LO>();
+      else vm_wait<2 * C::LPT_HI>();
+    } else if (ahead == 1) {
+      if (C::NHI == 0 || lpt == C::LPT_LO) vm_wait<C::LPT_LO>();
+      else vm_wait<C::LPT_HI>();
+    } else {
+      vm_wait<0>();
+    }
     __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt landed; tile kt-1's buffer is free
     if (kt + NBUF - 1 < nk) issue((kt + NBUF - 1) % NBUF);
     const uint16_t* T = lds + (kt % NBUF) * C::ROWS * BK;
@@ -265,13 +278,15 @@ conv_big_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, 
 
 }  // namespace
 
-// tile codes 200 (256x256) / 201 (256x128) / 202 (128x128) / 203 (128x256); -1 when the shape or
+// tile codes 200 (256x256) / 201 (256x128) / 202 (128x128) / 203 (128x256) / 204 (160x256: the batch-8
+// stage-3 1x1 reduce, M = 33 600 = 210 x 160 rows, one tile per CU on 210 CUs with no partial
+// second round; 8 waves as 2 x 4 of 80 x 64 accumulators); -1 when the shape or
 // epilogue is not supported.  The 128-row tiles serve N = 256 GEMMs of a few tens of thousands of
 // rows (the batch-8 stage-3 reduce / 3x3 convs: 75 workgroups of 256x256 leave 181 of 256 CUs
 // idle; 128x128 gives 300, two resident per CU with the 64 KB ring)
 int conv_big_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho, int Wo,
                  int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int tile, hipStream_t st) {
-  if (tile < 200 || tile > 203) return -1;
+  if (tile < 200 || tile > 204) return -1;
   if (Cin % BK != 0 || Cout % 16 != 0 || KH * KW > 64) return -1;
   if (ep.x2 || ep.yf || ep.bt || ep.omap || ep.pad_w >= 0 || ep.bnb_x || ep.st_part || ep.bnb_part || ep.rmask ||
       ep.drop_p > 0.f)
@@ -279,8 +294,8 @@ int conv_big_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int 
   if ((ep.y2) && (!ep.bn_beta || !ep.bn_mean || !ep.bn_var || (!ep.bn_fix_gamma && !ep.bn_gamma))) return -1;
   if ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kOOB || (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kOOB) return -1;
   const int M = NB * Ho * Wo;
-  const int bm = tile >= 202 ? 128 : 256;
-  const int bn = (tile == 200 || tile == 203) ? 256 : 128;
+  const int bm = tile == 204 ? 160 : tile >= 202 ? 128 : 256;
+  const int bn = (tile == 200 || tile == 203 || tile == 204) ? 256 : 128;
   const int tiles_n = (Cout + bn - 1) / bn;
   const int nwg = ((M + bm - 1) / bm) * tiles_n;
 #define MXR_BIG(BM_, BN_, F_)                                                                                 \
@@ -297,7 +312,8 @@ int conv_big_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int 
     case 200: MXR_BIG2(256, 256); break;
     case 201: MXR_BIG2(256, 128); break;
     case 202: MXR_BIG2(128, 128); break;
-    default: MXR_BIG2(128, 256); break;
+    case 203: MXR_BIG2(128, 256); break;
+    default: MXR_BIG2(160, 256); break;
   }
 #undef MXR_BIG2
 #undef MXR_BIG

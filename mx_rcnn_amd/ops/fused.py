@@ -253,42 +253,34 @@ def _bnp(bn):
     return [bn.gamma, bn.beta, bn.moving_mean, bn.moving_var]
 
 
-# Inference-only library route (MXR_GEMM_ROUTE=0 disables): a 1x1 stride-1 conv with a frozen BN +
-# ReLU epilogue on a batch-sized map is a plain GEMM, and hipBLASLt's bias + ReLU epilogue GEMM runs
-# it faster than the implicit-GEMM kernel (batch-8 stage-3 reduce, M = 33 600: 23 vs 38 us,
-# profiles/r5_b8_conv_tiles.jsonl, tools/microbench/addmm_probe.py) -- and at inference the pre-BN
-# output the kernel also writes is dead.  Test FPS: batch 8 679 -> 735, batch 1 327 -> 344 (every
-# stage's 1x1 reduce and the RoI head's; profiles/r5_gemm_route_ab.txt).  Single-plane bf16 / fp16
-# only; the BN scale is folded into a cached copy of the filter (rebuilt when the filter or the BN
-# statistics change).
-_GEMM_MIN_M = int(os.environ.get('MXR_GEMM_MIN_M', '4096'))
+# Inference: a bottleneck's conv -> frozen BN -> ReLU is ONE conv with the BN folded in (the scale
+# into a cached copy of the filter, the shift as an fp32 bias) and a ReLU epilogue, on our kernels,
+# writing only the activation the next conv reads.  The training form also stores the pre-BN output
+# for the backward -- dead at test time.  Round 5 routed the 1x1 reduce of batch-sized maps to
+# hipBLASLt's bias / ReLU GEMM instead (test FPS 735 at batch 8); round 6 folds both the reduce and
+# the 3x3 for every inference shape and runs them on the implicit-GEMM kernels (the large-M reduce on
+# conv_big's 160x256 tile).  MXR_INFER_FOLD=0: the training-form epilogues (both outputs).
+def _infer_fold(x, spec):
+    return (spec.bottle and getattr(spec, 'infer', False) and not precision.x2_enabled() and x.is_cuda and
+            x.dtype in (torch.bfloat16, torch.float16) and os.environ.get('MXR_INFER_FOLD', '1') != '0')
 
 
-def _gemm_route(x, w):
-    if os.environ.get('MXR_GEMM_ROUTE', '1') == '0' or precision.x2_enabled():
-        return False
-    if not (x.is_cuda and x.dtype in (torch.bfloat16, torch.float16) and x.dim() == 4 and w.dim() == 4 and
-            w.shape[2] == 1 and w.shape[3] == 1 and x.is_contiguous(memory_format=torch.channels_last)):
-        return False
-    return x.shape[0] * x.shape[2] * x.shape[3] >= _GEMM_MIN_M and x.shape[1] % 8 == 0 and w.shape[0] % 8 == 0
-
-
-def _gemm_bn_relu(x, w, bnp, eps, fix_gamma):
+def _folded(w, bnp, eps, fix_gamma, dtype):
+    """(filter * BN scale) in ``dtype`` (channels_last) and the BN shift as an fp32 bias, cached on
+    the filter and rebuilt when the filter or the BN parameters change (version counters, reload
+    epochs, the training generation: SGD rewrites trainable weights in place)."""
     gamma, beta, mean, var = bnp
-    key = (w.data_ptr(), w._version, precision.weight_epoch(w), precision.train_generation(w, *bnp), x.dtype,
+    key = (w.data_ptr(), w._version, precision.weight_epoch(w), precision.train_generation(w, *bnp), dtype,
            float(eps), bool(fix_gamma)) + tuple((p.data_ptr(), p._version, precision.weight_epoch(p)) for p in bnp)
-    hit = w.__dict__.get('_mxr_gemm_fold')
+    hit = w.__dict__.get('_mxr_bn_fold')
     if hit is None or hit[0] != key:
         with torch.no_grad():
             sc = (torch.ones_like(var.float()) if fix_gamma else gamma.float()) * torch.rsqrt(var.float() + eps)
-            wf = (w.detach().float().reshape(w.shape[0], -1) * sc[:, None]).to(x.dtype)
-            bf = (beta.float() - mean.float() * sc).to(x.dtype)
+            wf = (w.detach().float() * sc[:, None, None, None]).to(dtype).contiguous(memory_format=torch.channels_last)
+            bf = (beta.float() - mean.float() * sc).contiguous()
         hit = (key, wf, bf)
-        w.__dict__['_mxr_gemm_fold'] = hit
-    _, wf, bf = hit
-    n, c, h, ww = x.shape
-    y = torch._addmm_activation(bf, x.permute(0, 2, 3, 1).reshape(n * h * ww, c), wf.t(), use_gelu=False)
-    return y.view(n, h, ww, wf.shape[0]).permute(0, 3, 1, 2)
+        w.__dict__['_mxr_bn_fold'] = hit
+    return hit[1], hit[2]
 
 
 class _FusedUnitFn(torch.autograd.Function):
@@ -367,15 +359,19 @@ class _FusedUnitFn(torch.autograd.Function):
         # conv1 (stride 1 for bottleneck; 3x3 stride s for basic) -> bn2
         s1 = 1 if spec.bottle else spec.stride
         p1 = 0 if spec.bottle else 1
-        if spec.bottle and getattr(spec, 'infer', False) and _gemm_route(act1, ws[0]):
-            # inference: the bottleneck's 1x1 reduce + frozen bn2 + ReLU is a plain GEMM with a bias /
-            # ReLU epilogue -- hipBLASLt's on the large-M (batch) shapes; the pre-BN output y1 exists
-            # only for the backward, so it is not written at all
-            y1, a2 = None, _gemm_bn_relu(act1, ws[0], bnps[1], spec.eps[1], spec.fix[1])
+        fold = _infer_fold(act1, spec)
+        if fold:
+            # inference: reduce + bn2 + ReLU as one conv with the BN folded in; only a2 is written
+            wf, bf = _folded(ws[0], bnps[1], spec.eps[1], spec.fix[1], act1.dtype)
+            y1, a2 = None, ext.conv_igemm_fwd(act1, wf, bf, s1, p1, True)[0]
         else:
             y1, a2 = ext.conv_igemm_fwd(act1, wa[0][0], None, s1, p1, False, 0, 0, None, bnps[1], spec.eps[1],
                                         spec.fix[1], True, **wa[0][1])
-        if spec.bottle:
+        if spec.bottle and fold:  # the 3x3 + bn3 + ReLU the same way (its pre-BN output is dead too)
+            wf, bf = _folded(ws[1], bnps[2], spec.eps[2], spec.fix[2], a2.dtype)
+            y2, a3 = None, ext.conv_igemm_fwd(a2, wf, bf, spec.stride, 1, True)[0]
+            last_in, w_last = a3, wa[2]
+        elif spec.bottle:
             y2, a3 = ext.conv_igemm_fwd(a2, wa[1][0], None, spec.stride, 1, False, 0, 0, None, bnps[2], spec.eps[2],
                                         spec.fix[2], True, **wa[1][1])
             last_in, w_last = a3, wa[2]

@@ -571,26 +571,36 @@ def test_train_units_match_module_path(cuda, monkeypatch):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
-def test_inference_gemm_route_matches_kernel(cuda, monkeypatch, dtype):
-    """Inference on a batch-sized map routes the bottleneck's 1x1 reduce + frozen bn2 + ReLU to
-    hipBLASLt's bias / ReLU GEMM (ops/fused.py _gemm_route, M >= 16384): the unit output matches the
-    implicit-GEMM kernel path (MXR_GEMM_ROUTE=0) within the 16-bit rounding, and the folded filter
-    is rebuilt when the BN statistics change."""
+@pytest.mark.parametrize('stride', [1, 2])
+def test_inference_bn_fold_matches_training_form(cuda, monkeypatch, dtype, stride):
+    """Inference folds each bottleneck's frozen bn2 / bn3 into its 1x1 reduce / 3x3 (scale into a
+    cached filter copy, shift as the bias, ReLU epilogue; ops/fused.py _folded) on our kernels --
+    no vendor GEMM (torch._addmm_activation / F.linear / F.conv2d are made to raise).  The unit
+    output matches the training-form epilogues (MXR_INFER_FOLD=0) within the 16-bit rounding, and
+    the fold is rebuilt when the BN statistics or (through the training generation) the weights
+    change."""
+    import torch.nn.functional as Fn
     from mx_rcnn_amd.ops import fused
-    u = _unit(1024, 1024, 1, True, cuda)
+    u = _unit(1024, 1024, stride, stride == 1, cuda)
     for m in u.modules():
         if hasattr(m, 'weight') and m.weight is not None and m.weight.dim() == 4:
             m.weight = torch.nn.Parameter(m.weight.detach().to(dtype).contiguous(memory_format=torch.channels_last))
     x = torch.randn(4, 1024, 64, 64, device=cuda).to(dtype).contiguous(memory_format=torch.channels_last)
-    assert fused._gemm_route(x, u.conv1.weight)
 
-    def run(route):
-        monkeypatch.setenv('MXR_GEMM_ROUTE', '1' if route else '0')
-        with torch.no_grad():
-            return fused.fused_unit(u, x)[0].float()
+    def boom(*a, **k):
+        raise AssertionError('vendor GEMM / conv on the inference path')
+
+    def run(fold):
+        monkeypatch.setenv('MXR_INFER_FOLD', '1' if fold else '0')
+        with monkeypatch.context() as mp:
+            mp.setattr(torch, '_addmm_activation', boom)
+            mp.setattr(Fn, 'conv2d', boom)
+            mp.setattr(Fn, 'linear', boom)
+            with torch.no_grad():
+                return fused.fused_unit(u, x)[0].float()
 
     a = run(True)
-    assert '_mxr_gemm_fold' in u.conv1.weight.__dict__  # the library route ran
+    assert '_mxr_bn_fold' in u.conv1.weight.__dict__ and '_mxr_bn_fold' in u.conv2.weight.__dict__
     b = run(False)
     scale = b.abs().max().item()
     assert (a - b).abs().max().item() <= 2e-2 * scale

@@ -86,6 +86,8 @@ def main():
     ap.add_argument('--splits', default='0,1,2,4,8')
     ap.add_argument('--wgrad', action='store_true', help='sweep conv_wgrad (variant x splits) instead')
     ap.add_argument('--epi', action='store_true', help='forward with the bottleneck epilogue: bias + residual + ReLU')
+    ap.add_argument('--bias-relu', action='store_true',
+                    help='forward with the inference BN-fold epilogue: fp32 bias + ReLU, one output (ops/fused.py _folded)')
     args = ap.parse_args()
     ext = need_ext()
     torch.manual_seed(0)
@@ -131,6 +133,10 @@ def main():
             resid = torch.randn_like(ref).bfloat16().contiguous(memory_format=torch.channels_last)
             ref = torch.relu(ref + bias.float().view(1, -1, 1, 1) + resid.float())
             ekw = {'bias': bias, 'relu': True, 'residual': resid}
+        if args.bias_relu:
+            bias = torch.randn(cout, device='cuda')
+            ref = torch.relu(ref + bias.view(1, -1, 1, 1))
+            ekw = {'bias': bias, 'relu': True, 'residual': None}
         for tile in [int(t) for t in args.tiles.split(',')]:
             for sp in [int(v) for v in args.splits.split(',')]:
                 if tile == 0 and sp != 0:

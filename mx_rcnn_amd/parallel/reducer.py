@@ -97,6 +97,7 @@ class BucketReducer:
         self._opt_stream = None
         self._early_sgd = None
         self.sgd_applied = False
+        self.early_names = []
         if not (self.dp or self.sgd_capable):
             return
         mb = bucket_mb if self.dp else sgd_bucket_mb

@@ -304,7 +304,9 @@ class FlatParamStore:
             if zero_grad:
                 self.zero_grad()
             self.refresh_dgrad_cache()
-        return lambda: main.wait_stream(side)
+        done = torch.cuda.Event()
+        done.record(side)  # the join waits for this work only (the side stream may carry later roles)
+        return lambda: main.wait_event(done)
 
     @staticmethod
     def _flat_view(t, cl):

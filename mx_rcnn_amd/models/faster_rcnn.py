@@ -205,9 +205,10 @@ class FasterRCNN(nn.Module):
         aux.wait_stream(main)
         with torch.cuda.stream(aux):
             at = run()
+        done = _mark(aux)  # the join waits for THIS work only (the side stream may carry later roles)
 
         def join():
-            main.wait_stream(aux)
+            main.wait_event(done)
             for t in at.values():
                 t.record_stream(main)
             return at
@@ -229,9 +230,10 @@ class FasterRCNN(nn.Module):
         rpn_bbox.record_stream(aux)
         with torch.cuda.stream(aux):
             res = self._rpn_losses(rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt, at_join.at)
+        done = _mark(aux)
 
         def join():
-            main.wait_stream(aux)
+            main.wait_event(done)
             for t in (res[0], res[1]) + tuple(res[2].values()):
                 t.record_stream(main)
             return res
@@ -281,9 +283,10 @@ class FasterRCNN(nn.Module):
         with torch.cuda.stream(ps):
             rois, _ = self._proposal(rpn_cls, rpn_bbox, im_info, 'TRAIN', after_mask=mask_done)
             pt = proposal_target(rois, gt_boxes, n_gt, self.num_classes, cfg=self.cfg, is_train=True)
+        done = _mark(ps)
 
         def join():
-            main.wait_stream(ps)
+            main.wait_event(done)
             for t in pt.values():
                 if torch.is_tensor(t):
                     t.record_stream(main)
@@ -386,6 +389,14 @@ class FasterRCNN(nn.Module):
 
 
 _AUX = {}
+
+
+def _mark(stream):
+    """An event recorded on ``stream`` now: a join that waits on it depends on the work issued so
+    far only, not on what a shared side stream (MXR_SIDE_STREAMS=1) carries for later roles."""
+    ev = torch.cuda.Event()
+    ev.record(stream)
+    return ev
 
 
 def _aux_stream(device, role='aux'):

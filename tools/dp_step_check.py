@@ -30,8 +30,19 @@ def main():
     ap.add_argument('--mode', default='rcnn', choices=['rcnn', 'e2e'])
     ap.add_argument('--network', default='resnet50')
     ap.add_argument('--image', default='320x480')
+    ap.add_argument('--dirty-gb', type=float, default=0.0,
+                    help='before anything else, fill this many GB of the caching allocator with NaN and free it: '
+                         'a kernel that reads memory it never wrote then sees NaN instead of the zeros of fresh VRAM')
     args = ap.parse_args()
     rank, world, _, device = pdist.init_distributed()
+    if args.dirty_gb > 0:
+        blocks = []
+        for sz in (1 << 28, 1 << 24, 1 << 20, 1 << 16):  # large and small allocator pools
+            for _ in range(max(1, int(args.dirty_gb * (1 << 30) / 4 / sz / 4))):
+                blocks.append(torch.full((sz,), float('nan'), device=device))
+        torch.cuda.synchronize()
+        del blocks
+        torch.cuda.empty_cache()  # back to the driver: the graph pool's fresh segments may get these pages
     h, w = [int(v) for v in args.image.split('x')]
     cfg = snapshot()
     if args.mode == 'e2e':

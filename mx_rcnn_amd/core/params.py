@@ -299,7 +299,8 @@ class FlatParamStore:
             from ..models.faster_rcnn import _aux_stream
             self._cache_stream = _aux_stream(self.device, 'cache')
         side = self._cache_stream
-        side.wait_stream(main)
+        from ..models.faster_rcnn import fork
+        fork(side, main)
         with torch.cuda.stream(side):
             if zero_grad:
                 self.zero_grad()

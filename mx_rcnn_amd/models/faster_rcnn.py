@@ -202,7 +202,7 @@ class FasterRCNN(nn.Module):
             return lambda: at
         main = torch.cuda.current_stream()
         aux = _aux_stream(data.device)
-        aux.wait_stream(main)
+        fork(aux, main)
         with torch.cuda.stream(aux):
             at = run()
         done = _mark(aux)  # the join waits for THIS work only (the side stream may carry later roles)
@@ -225,7 +225,7 @@ class FasterRCNN(nn.Module):
             res = self._rpn_losses(rpn_cls, rpn_bbox, im_info, gt_boxes, n_gt, at_join())
             return lambda: res
         main = torch.cuda.current_stream()
-        aux.wait_stream(main)  # the RPN outputs (nothing later on main is waited for)
+        fork(aux, main)  # the RPN outputs (nothing later on main is waited for)
         rpn_cls.record_stream(aux)
         rpn_bbox.record_stream(aux)
         with torch.cuda.stream(aux):
@@ -274,7 +274,7 @@ class FasterRCNN(nn.Module):
         """Proposal + proposal target on the proposal stream; returns a join -> targets dict."""
         main = torch.cuda.current_stream()
         ps = _aux_stream(rpn_cls.device, 'proposal')
-        ps.wait_stream(main)
+        fork(ps, main)
 
         def mask_done():
             # the compute stream resumes once the (all-CU) NMS bitmask is built: its RPN backward
@@ -389,6 +389,23 @@ class FasterRCNN(nn.Module):
 
 
 _AUX = {}
+
+
+def fork(side, main=None):
+    """side.wait_stream(main), shaped for hipGraph replay: the runtime spreads a captured graph's
+    parallel branches over its queues by walking the DAG depth-first, the FIRST child of a node
+    continuing the node's queue.  A fork whose side kernel is captured before main's next kernel
+    hands the main chain to a new queue (every later hop costs a cross-queue wait), so a no-op on
+    main takes the first-child slot before the side branch starts (MXR_FORK_NOOP=0: plain fork)."""
+    main = main if main is not None else torch.cuda.current_stream()
+    if os.environ.get('MXR_FORK_NOOP', '1') == '0':
+        side.wait_stream(main)
+        return
+    ev = torch.cuda.Event()
+    ev.record(main)
+    with torch.cuda.stream(main):
+        torch.cuda._sleep(0)
+    side.wait_event(ev)
 
 
 def _mark(stream):

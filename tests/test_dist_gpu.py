@@ -95,7 +95,7 @@ def test_autotuned_reruns_are_bitwise_equal_through_the_plan_file(tmp_path):
     assert not diff, 'autotuned reruns differ: %s' % diff[:5]
 
 
-def _two_ranks(tmp_path, name, precision, same_batch, steps=2):
+def _two_ranks(tmp_path, name, precision, same_batch, steps=2, extra=()):
     """Two worker processes (tools/dp_two_rank_check.py), both on cuda:0, gloo rendezvous on
     127.0.0.1; returns both ranks' saved states."""
     sk = socket.socket()
@@ -109,12 +109,12 @@ def _two_ranks(tmp_path, name, precision, same_batch, steps=2):
         env.update({'MXR_CONV_TUNE': '0', 'WORLD_SIZE': '2', 'RANK': str(r), 'LOCAL_RANK': '0',
                     'MASTER_ADDR': '127.0.0.1', 'MASTER_PORT': str(port)})
         cmd = [sys.executable, os.path.join(ROOT, 'tools', 'dp_two_rank_check.py'), str(tmp_path / ('%s_r%d.pt' % (name, r))),
-               '--precision', precision, '--steps', str(steps)] + (['--same-batch'] if same_batch else [])
+               '--precision', precision, '--steps', str(steps)] + (['--same-batch'] if same_batch else []) + list(extra)
         procs.append(subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
     outs = []
     try:
         for p in procs:
-            outs.append(p.communicate(timeout=240)[0])
+            outs.append(p.communicate(timeout=480)[0])
     finally:
         for p in procs:
             if p.poll() is None:
@@ -125,15 +125,15 @@ def _two_ranks(tmp_path, name, precision, same_batch, steps=2):
     return [torch.load(str(tmp_path / ('%s_r%d.pt' % (name, r))), weights_only=True) for r in range(2)], outs
 
 
-def _plain(tmp_path, name, precision, rescale, steps=2):
+def _plain(tmp_path, name, precision, rescale, steps=2, extra=()):
     env = dict(os.environ)
     for k in ('MXR_FORCE_DIST', 'WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_ADDR', 'MASTER_PORT'):
         env.pop(k, None)
     env['MXR_CONV_TUNE'] = '0'
     out = str(tmp_path / (name + '.pt'))
     r = subprocess.run([sys.executable, os.path.join(ROOT, 'tools', 'dp_two_rank_check.py'), out, '--precision', precision,
-                        '--steps', str(steps), '--rescale', str(rescale)],
-                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=240)
+                        '--steps', str(steps), '--rescale', str(rescale)] + list(extra),
+                       env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, timeout=480)
     assert r.returncode == 0, r.stdout[-3000:]
     return torch.load(out, weights_only=True)
 
@@ -170,3 +170,23 @@ def test_two_ranks_on_one_gpu_stay_in_sync_on_different_batches(tmp_path):
         assert torch.equal(r0[k], r1[k]), ('replicas differ', k)
     ref = _plain(tmp_path, 'plain1x', 'fp32', 1.0)
     assert any(not torch.equal(ref[k], r0[k]) for k in keys)
+
+
+@pytest.mark.gpu
+def test_two_ranks_on_one_gpu_e2e_resnet101_headline_shape(tmp_path):
+    """the production-shaped DP step -- e2e ResNet-101 at 800x1333 (anchor targets,
+    the proposal chain 12000 -> 6000 and its RoI sampling, the stage-4 head), 25 MB buckets -- with
+    two ranks on the box's one GPU (gloo between them), same batches: bit for bit the weights of one
+    process with rescale_grad = 2, identical replicas."""
+    ex = ('--mode', 'e2e', '--network', 'resnet101', '--image', '800x1333', '--bucket-mb', '25')
+    (r0, r1), logs = _two_ranks(tmp_path, 'e2e', 'fp32', True, steps=2, extra=ex)
+    info = r0['_info'].tolist()
+    assert info[0] == 1 and info[1] >= 5 and info[2] == 2, logs[0][-2000:]  # production-size buckets
+    ref = _plain(tmp_path, 'e2e_plain2x', 'fp32', 2.0, steps=2, extra=ex)
+    keys = [k for k in ref if not k.startswith('_')]
+    assert len(keys) > 300
+    for k in keys:
+        assert torch.equal(r0[k], r1[k]), ('replicas differ', k)
+    diff = [k for k in keys if not torch.equal(ref[k], r0[k])]
+    assert not diff, 'e2e DP sum differs from the plain 2x-rescaled step: %s (max abs %s)' % (
+        diff[:5], [float((ref[k].float() - r0[k].float()).abs().max()) for k in diff[:5]])

@@ -5,7 +5,11 @@ production DP path: the flat-buffer gradient hooks, bucketed async all-reduce (S
 bucket-wise SGD, on the GPU kernels.  Without WORLD_SIZE the same script runs one plain process.
 
     python tools/dp_two_rank_check.py OUT.pt [--precision fp32|bf16] [--steps 2] [--same-batch]
-        [--rescale 1.0]
+        [--rescale 1.0] [--mode e2e --network resnet101 --image 800x1333 --bucket-mb 25]
+
+``--mode e2e``: the headline step's shape -- approximate-joint e2e training (anchor targets, the
+proposal chain 12000 -> 6000 with its sampling, RoI pooling, the stage-4 head) on a synthetic
+800x1333 image with random gt boxes, production bucket sizes (eager; gloo carries the buckets).
 """
 import argparse
 import os
@@ -33,6 +37,11 @@ def batch(seed, device):
     return {k: v.to(device) for k, v in b.items()}
 
 
+def e2e_batch(seed, device, h, w, num_classes):
+    from bench import synthetic_batch
+    return synthetic_batch(1, h, w, num_classes, device, torch.Generator().manual_seed(100 + seed))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('out')
@@ -40,6 +49,10 @@ def main():
     ap.add_argument('--steps', type=int, default=2)
     ap.add_argument('--same-batch', action='store_true', help='every rank trains on the batch of rank 0')
     ap.add_argument('--rescale', type=float, default=1.0)
+    ap.add_argument('--mode', default='rcnn', choices=['rcnn', 'e2e'])
+    ap.add_argument('--network', default='resnet50')
+    ap.add_argument('--image', default='800x1333')
+    ap.add_argument('--bucket-mb', type=float, default=0.05)
     args = ap.parse_args()
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = 0
@@ -49,14 +62,28 @@ def main():
     if dev.type == 'cuda':
         torch.cuda.set_device(dev)
     torch.manual_seed(0)
-    model = FasterRCNN('resnet50', 6, cfg=snapshot())
-    tr = Trainer(model, 'rcnn', fixed_param_prefix=['conv0', 'stage1', 'bn_data', 'bn0'], lr=0.01, momentum=0.9,
-                 wd=0.0005, clip_gradient=-1, rescale_grad=args.rescale, device=dev, bucket_mb=0.05,
+    if args.mode == 'e2e':
+        h, w = [int(v) for v in args.image.split('x')]
+        cfg = snapshot()
+        cfg.TRAIN.BG_THRESH_LO = 0.0
+        cfg.END2END = 1
+        cfg.TRAIN.BBOX_NORMALIZATION_PRECOMPUTED = True
+        model = FasterRCNN(args.network, 81, cfg=cfg)
+        model.to(dev).calibrate_bn(e2e_batch(0, dev, h, w, 81)['data'])  # rank 0 broadcasts its statistics
+        make = lambda s: e2e_batch(s, dev, h, w, 81)  # noqa: E731
+        fixed, clip = ['conv0', 'stage1', 'stage2', 'bn_data', 'bn0'], 1.0
+    else:
+        model = FasterRCNN(args.network, 6, cfg=snapshot())
+        make = lambda s: batch(s, dev)  # noqa: E731
+        fixed, clip = ['conv0', 'stage1', 'bn_data', 'bn0'], -1
+    tr = Trainer(model, args.mode, fixed_param_prefix=fixed, lr=0.01, momentum=0.9,
+                 wd=0.0005, clip_gradient=clip, rescale_grad=args.rescale, device=dev, bucket_mb=args.bucket_mb,
                  precision=args.precision)
     assert tr.reducer.dp == (world > 1)
     objs = []
     for s in range(args.steps):
-        out = tr.step(batch((0 if args.same_batch else rank) + 10 * s, dev))
+        torch.manual_seed(1000 + s)  # the samplers' draws: the same on every rank and in the plain run
+        out = tr.step(make((0 if args.same_batch else rank) + 10 * s))
         objs.append(float(out['objective'].float().item()))
     if dev.type == 'cuda':
         torch.cuda.synchronize()

@@ -419,3 +419,24 @@ def test_linear_in_shape_layout_cpu():
     rows_w = wcl.permute(0, 2, 3, 1).reshape(16, -1)
     rows_x = x.contiguous(memory_format=torch.channels_last).permute(0, 2, 3, 1).reshape(5, -1)
     assert torch.allclose(rows_x @ rows_w.t() + lin.bias, ref, atol=1e-5)
+
+
+def test_inference_copy_leaves_the_trained_model_untouched():
+    """core/detector.py _inference_copy (what a GPU Detector runs): a private copy of the model's
+    weights in the test precision; the model it came from keeps its dtype, values and the trainer's
+    attachments (dropout counter, non-finite counter), and the copy carries none of them."""
+    from mx_rcnn_amd.core.detector import _inference_copy, resolve_dtype
+    torch.manual_seed(0)
+    m = FasterRCNN('vgg16', 21, cfg=_cfg())
+    tr = Trainer(m, 'e2e', fixed_param_prefix=['conv1', 'conv2'], device='cpu')
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    c = _inference_copy(m, resolve_dtype('bf16'))
+    assert c is not m and not c.training
+    assert c.trunk.convs[3].weight.dtype == torch.bfloat16 and c.head.fc6.weight.dtype == torch.bfloat16
+    assert c.trunk.convs[3].weight.is_contiguous(memory_format=torch.channels_last)
+    assert c.head.fc6.rng_step is None and c.nonfinite_counter is None
+    assert m.head.fc6.rng_step is tr.rng_step and m.nonfinite_counter is tr.nonfinite
+    for k, v in m.state_dict().items():
+        assert v.dtype == before[k].dtype and torch.equal(v, before[k]), k
+    with pytest.raises(ValueError):
+        resolve_dtype('int8')

@@ -212,6 +212,7 @@ class BucketReducer:
         update kernels zero the gradient buffers they consumed."""
         self._sgd = sgd if (sgd is not None and self.sgd_capable and self.buckets) else None
         self._early_sgd = sgd if (sgd is not None and self._sgd is None and self.early_names) else None
+        self.store._early = {}  # ranges a step that raised mid-backward marked are void
         self._clear = bool(clear)
         self.sgd_applied = False
         for b in self.buckets:

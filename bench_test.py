@@ -157,6 +157,10 @@ def main():
                        'num_classes': args.num_classes, 'parallelism': 'dp%d' % world, 'exec': mode,
                        'rpn_pre_post_nms': [config.TEST.RPN_PRE_NMS_TOP_N, config.TEST.RPN_POST_NMS_TOP_N],
                        'detections_last_image': n_det}}), flush=True)
+    if os.environ.get('MXR_BENCH_DUMP_TUNE') and device.type == 'cuda':
+        from mx_rcnn_amd.ops import need_ext
+        for key, tile, sp in need_ext().conv_tune_table():
+            print('[tune] %-48s tile %d splits %d' % (key, tile, sp), file=sys.stderr)
     if device.type == 'cuda' and rank == 0:  # persist the conv plan for the next run (ops/tune_plan.py)
         from mx_rcnn_amd.ops import tune_plan
         tune_plan.save()

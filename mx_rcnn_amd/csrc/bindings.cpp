@@ -381,11 +381,29 @@ std::vector<Tensor> anchor_target_assign(const Tensor& base_anchors, int64_t H, 
   return {label, targets, max_ov, argmax};
 }
 
+// frozen BN + ReLU fused into a pooling kernel's store (kernels.h PostBn); none: off
+static mxr::PostBn post_bn_args(const c10::optional<std::vector<Tensor>>& bn, double eps, bool fix_gamma, int64_t C) {
+  mxr::PostBn p;
+  if (!bn) return p;
+  TORCH_CHECK(bn->size() == 4, "post_bn: [gamma, beta, mean, var]");
+  for (const auto& t : *bn)
+    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == C,
+                "post_bn params: fp32 (C,) device tensors");
+  p.gamma = (*bn)[0].data_ptr<float>();
+  p.beta = (*bn)[1].data_ptr<float>();
+  p.mean = (*bn)[2].data_ptr<float>();
+  p.var = (*bn)[3].data_ptr<float>();
+  p.eps = (float)eps;
+  p.fix_gamma = fix_gamma ? 1 : 0;
+  return p;
+}
+
 // ---- RoI pooling -----------------------------------------------------------------------
 // feat must be channels-last in memory: logical (B, C, H, W) with NHWC strides.
 // x2: feat is a (2B, C, H, W) hi / lo pair, the pooled output (2R, C, PH, PW) a pair too
 std::vector<Tensor> roi_pool_fwd(const Tensor& feat, const Tensor& rois, int64_t PH, int64_t PW, double scale, int64_t x2,
-                                 bool need_argmax) {
+                                 bool need_argmax, c10::optional<std::vector<Tensor>> post_bn, double post_eps,
+                                 bool post_fix_gamma) {
   CHECK_DEV(feat); CHECK_DEV(rois); CHECK_F32(rois); CHECK_CONTIG(rois);
   TORCH_CHECK(feat.dim() == 4 && feat.is_contiguous(at::MemoryFormat::ChannelsLast),
               "feat must be (B,C,H,W) channels_last");
@@ -395,6 +413,8 @@ std::vector<Tensor> roi_pool_fwd(const Tensor& feat, const Tensor& rois, int64_t
   const int B = (int)(x2 ? feat.size(0) / npl(x2) : feat.size(0)), C = (int)feat.size(1), H = (int)feat.size(2),
             W = (int)feat.size(3);
   const int R = (int)rois.size(0);
+  TORCH_CHECK(!(post_bn && need_argmax), "roi_pool_fwd: post_bn is inference-only (no argmax)");
+  const mxr::PostBn post = post_bn_args(post_bn, post_eps, post_fix_gamma, C);
   DevGuard g(feat.device());
   Tensor out = at::empty({x2 ? npl(x2) * R : R, C, PH, PW}, feat.options().memory_format(at::MemoryFormat::ChannelsLast));
   // inference skips the argmax map (4 B per output element: at batch 8 x 300 RoIs x 1024 channels
@@ -403,7 +423,7 @@ std::vector<Tensor> roi_pool_fwd(const Tensor& feat, const Tensor& rois, int64_t
                                                               at::MemoryFormat::ChannelsLast))
                               : at::empty({0}, feat.options().dtype(at::kInt));
   mxr::roi_pool_fwd(feat.data_ptr(), x2 ? pcode(x2) : dcode(feat), B, H, W, C, rois.data_ptr<float>(), R, (int)PH, (int)PW,
-                    (float)scale, out.data_ptr(), need_argmax ? argmax.data_ptr<int32_t>() : nullptr, cur_stream());
+                    (float)scale, out.data_ptr(), need_argmax ? argmax.data_ptr<int32_t>() : nullptr, cur_stream(), post);
   return {out, argmax};
 }
 
@@ -1311,7 +1331,8 @@ void wgrad_reduce_run(const Tensor& slab, Tensor out) {
 }
 
 // ---- pooling ---------------------------------------------------------------------------------
-std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t p, int64_t x2) {
+std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t p, int64_t x2, bool need_arg,
+                                c10::optional<std::vector<Tensor>> post_bn, double post_eps, bool post_fix_gamma) {
   CHECK_DEV(x);
   TORCH_CHECK((x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf) && x.dim() == 4 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -1321,12 +1342,15 @@ std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t p
   TORCH_CHECK(C % 8 == 0, "maxpool needs C % 8 == 0");
   const int Ho = (H + 2 * (int)p - (int)k) / (int)s + 1, Wo = (W + 2 * (int)p - (int)k) / (int)s + 1;
   TORCH_CHECK(Ho > 0 && Wo > 0, "maxpool: empty output");
+  TORCH_CHECK(!(post_bn && need_arg), "maxpool_fwd: post_bn is inference-only (no taps)");
+  const mxr::PostBn post = post_bn_args(post_bn, post_eps, post_fix_gamma, C);
   DevGuard g(x.device());
   Tensor y = at::empty({x2 ? npl(x2) * N : N, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
-  Tensor arg = at::empty({N, C, Ho, Wo}, x.options().dtype(at::kByte).memory_format(at::MemoryFormat::ChannelsLast));
+  Tensor arg = need_arg ? at::empty({N, C, Ho, Wo}, x.options().dtype(at::kByte).memory_format(at::MemoryFormat::ChannelsLast))
+                        : at::empty({0}, x.options().dtype(at::kByte));  // inference: no taps written
   const int rc = mxr::maxpool_fwd(reinterpret_cast<const uint16_t*>(x.data_ptr()), reinterpret_cast<uint16_t*>(y.data_ptr()),
-                                  arg.data_ptr<uint8_t>(), N, H, W, C, Ho, Wo, (int)k, (int)s, (int)p,
-                                  x2 ? pcode(x2) : dcode(x), cur_stream());
+                                  need_arg ? arg.data_ptr<uint8_t>() : nullptr, N, H, W, C, Ho, Wo, (int)k, (int)s, (int)p,
+                                  x2 ? pcode(x2) : dcode(x), cur_stream(), post);
   TORCH_CHECK(rc == 0, "maxpool_fwd: unsupported shape");
   return {y, arg};
 }
@@ -2312,7 +2336,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("proposal_sample", &proposal_sample);
   m.def("anchor_target_assign", &anchor_target_assign);
   m.def("roi_pool_fwd", &roi_pool_fwd, py::arg("feat"), py::arg("rois"), py::arg("PH"), py::arg("PW"),
-        py::arg("scale"), py::arg("x2") = 0, py::arg("need_argmax") = true);
+        py::arg("scale"), py::arg("x2") = 0, py::arg("need_argmax") = true, py::arg("post_bn") = py::none(),
+        py::arg("post_eps") = 0.0, py::arg("post_fix_gamma") = false);
   m.def("roi_pool_bwd", &roi_pool_bwd, py::arg("grad_out"), py::arg("argmax"), py::arg("rois"), py::arg("B"),
         py::arg("H"), py::arg("W"), py::arg("grad_add") = py::none(), py::arg("x2") = 0);
   m.def("rpn_softmax_ce", &rpn_softmax_ce, py::arg("logits"), py::arg("label"), py::arg("norm"), py::arg("grad_scale"),
@@ -2366,7 +2391,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("det_postprocess", &det_postprocess, py::arg("rois"), py::arg("scores"), py::arg("deltas"),
         py::arg("im_info"), py::arg("thresh"), py::arg("nms_thresh"), py::arg("max_per"), py::arg("cap"));
   m.def("nest_keep", &nest_keep, py::arg("dets"), py::arg("thresh"));
-  m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("s"), py::arg("p"), py::arg("x2") = 0);
+  m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("s"), py::arg("p"), py::arg("x2") = 0,
+        py::arg("need_arg") = true, py::arg("post_bn") = py::none(), py::arg("post_eps") = 0.0,
+        py::arg("post_fix_gamma") = false);
   m.def("maxpool_bwd", &maxpool_bwd, py::arg("dy"), py::arg("arg"), py::arg("H"), py::arg("W"), py::arg("k"),
         py::arg("s"), py::arg("p"), py::arg("x2") = 0);
   m.def("avgpool_fwd", &avgpool_fwd, py::arg("x"), py::arg("x2") = 0);

@@ -6,6 +6,8 @@
 #include <cstdint>
 #include <cfloat>
 
+#include "../kernels.h"
+
 #define MXR_WAVE 64
 
 namespace mxr {
@@ -21,6 +23,15 @@ __device__ __forceinline__ float f16_to_f32(uint16_t v) { return __half2float(__
 __device__ __forceinline__ uint16_t f32_to_f16(float f) { return __half_as_ushort(__float2half(f)); }
 
 // 16-bit storage codes used by the kernels' dtype flags: 0 = fp32, 1 = bf16, 2 = fp16
+// PostBn (kernels.h): relu(v * s + t) with bn_act.hip's per-channel coefficients, so the fused
+// pooling output is bit-identical to pooling followed by bn_relu_fwd
+__device__ __forceinline__ float post_bn_relu(const PostBn& p, int c, float v) {
+  const float inv = rsqrtf(p.var[c] + p.eps);
+  const float s = (p.fix_gamma ? 1.f : p.gamma[c]) * inv;
+  const float t = p.beta[c] - p.mean[c] * s;
+  return fmaxf(v * s + t, 0.f);
+}
+
 __device__ __forceinline__ float h16_to_f32(uint16_t v, int code) {
   return code == 2 ? f16_to_f32(v) : bf16_to_f32(v);
 }

@@ -20,7 +20,7 @@ namespace mxr {
 
 __global__ void __launch_bounds__(256)
 maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, uint8_t* __restrict__ arg, int N, int H,
-                   int W, int C, int Ho, int Wo, int k, int s, int p, int code) {
+                   int W, int C, int Ho, int Wo, int k, int s, int p, int code, PostBn post) {
   const int cv = C / 8;
   const int64_t total = (int64_t)N * Ho * Wo * cv;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -52,14 +52,21 @@ maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, uin
         }
     }
   }
-  st8c(y, pix * C + c8 * 8, code, (int64_t)N * Ho * Wo * C, best);
+  if (post.mean) {  // inference: the next unit's bn1 + ReLU on the pooled value
+    float a[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) a[q] = post_bn_relu(post, c8 * 8 + q, best[q]);
+    st8c(y, pix * C + c8 * 8, code, (int64_t)N * Ho * Wo * C, a);
+  } else {
+    st8c(y, pix * C + c8 * 8, code, (int64_t)N * Ho * Wo * C, best);
+  }
   uint32_t lo = 0, hi = 0;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     lo |= (uint32_t)bi[q] << (8 * q);
     hi |= (uint32_t)bi[q + 4] << (8 * q);
   }
-  *reinterpret_cast<uint2*>(arg + pix * C + c8 * 8) = make_uint2(lo, hi);
+  if (arg) *reinterpret_cast<uint2*>(arg + pix * C + c8 * 8) = make_uint2(lo, hi);  // null: inference
 }
 
 __global__ void __launch_bounds__(256)
@@ -133,11 +140,11 @@ avgpool_bwd_kernel(const uint16_t* __restrict__ dy, uint16_t* __restrict__ dx, i
 }
 
 int maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int Ho, int Wo, int k,
-                int s, int p, int code, hipStream_t st) {
+                int s, int p, int code, hipStream_t st, PostBn post) {
   if (C % 8 != 0 || k > 15 || k <= 0 || s <= 0) return -1;
   const int64_t total = (int64_t)N * Ho * Wo * (C / 8);
   if (total == 0) return 0;
-  maxpool_fwd_kernel<<<div_up(total, 256), 256, 0, st>>>(x, y, arg, N, H, W, C, Ho, Wo, k, s, p, code);
+  maxpool_fwd_kernel<<<div_up(total, 256), 256, 0, st>>>(x, y, arg, N, H, W, C, Ho, Wo, k, s, p, code, post);
   return 0;
 }
 

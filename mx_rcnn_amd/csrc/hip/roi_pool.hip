@@ -45,7 +45,7 @@ __device__ __forceinline__ Bin roi_bin(const float* __restrict__ rois, int r, in
 template <typename T>
 __global__ void __launch_bounds__(256)
 roi_pool_fwd_vec4(const T* __restrict__ feat, int code, int B, int H, int W, int C, const float* __restrict__ rois, int R,
-                  int PH, int PW, float scale, T* __restrict__ out, int32_t* __restrict__ argmax) {
+                  int PH, int PW, float scale, T* __restrict__ out, int32_t* __restrict__ argmax, PostBn post) {
   // code 3 / 4 (x2 pairs / x3 triples, T = uint16_t): planes one (B, H, W, C) / (R, PH, PW, C) block apart
   const int64_t fplane = (int64_t)B * H * W * C, oplane = (int64_t)R * PH * PW * C;
   using V = typename Vec4<T>::type;
@@ -85,6 +85,10 @@ roi_pool_fwd_vec4(const T* __restrict__ feat, int code, int B, int H, int W, int
       }
     }
   }
+  if (post.mean) {
+    m0 = post_bn_relu(post, cv * 4, m0); m1 = post_bn_relu(post, cv * 4 + 1, m1);
+    m2 = post_bn_relu(post, cv * 4 + 2, m2); m3 = post_bn_relu(post, cv * 4 + 3, m3);
+  }
   const int64_t o = t * 4;
   if constexpr (sizeof(T) == 2) {
     if (code >= 3) {
@@ -100,13 +104,13 @@ roi_pool_fwd_vec4(const T* __restrict__ feat, int code, int B, int H, int W, int
   if (argmax) *reinterpret_cast<int4*>(argmax + o) = make_int4(a0, a1, a2, a3);  // null: inference, no backward
 }
 
-// 8 channels per lane, single-plane 16-bit maps (bf16 / fp16): 16-B loads, two bin pixels per
+// 8 channels per lane, single-plane 16-bit maps (bf16 / fp16): 16-B loads, four bin pixels per
 // iteration in flight; the batch-8 inference pooling (2400 RoIs x 49 bins x 1024 channels) is a
 // latency-bound gather at 4 channels per lane and one load at a time
 __global__ void __launch_bounds__(256)
 roi_pool_fwd_vec8(const uint16_t* __restrict__ feat, int code, int B, int H, int W, int C,
                   const float* __restrict__ rois, int R, int PH, int PW, float scale, uint16_t* __restrict__ out,
-                  int32_t* __restrict__ argmax) {
+                  int32_t* __restrict__ argmax, PostBn post) {
   const int CV = C >> 3;
   const int64_t total = (int64_t)R * PH * PW * CV;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -128,7 +132,7 @@ roi_pool_fwd_vec8(const uint16_t* __restrict__ feat, int code, int B, int H, int
 #pragma unroll
     for (int k = 0; k < 8; ++k) m[k] = -FLT_MAX;
     const uint16_t* fb = feat + (int64_t)bin.b * H * W * C + (int64_t)cv * 8;
-    const int bw = bin.we - bin.ws, npx = (bin.he - bin.hs) * bw;
+    const int npx = (bin.he - bin.hs) * (bin.we - bin.ws);
     auto upd = [&](const uint4 v, int idx) {
       const uint32_t wv[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -138,20 +142,35 @@ roi_pool_fwd_vec8(const uint16_t* __restrict__ feat, int code, int B, int H, int
         if (f1 > m[2 * k + 1]) { m[2 * k + 1] = f1; a[2 * k + 1] = idx; }
       }
     };
+    // row-major walk with a running (h, w): four loads issued together, compared in order
+    int h = bin.hs, w = bin.ws;
+    auto next = [&]() {
+      const int idx = h * W + w;
+      if (++w == bin.we) {
+        w = bin.ws;
+        ++h;
+      }
+      return idx;
+    };
     int q = 0;
-    for (; q + 1 < npx; q += 2) {  // row-major order kept: the two loads are issued together, compared in order
-      const int i0 = (bin.hs + q / bw) * W + bin.ws + q % bw;
-      const int i1 = (bin.hs + (q + 1) / bw) * W + bin.ws + (q + 1) % bw;
-      const uint4 v0 = *reinterpret_cast<const uint4*>(fb + (int64_t)i0 * C);
-      const uint4 v1 = *reinterpret_cast<const uint4*>(fb + (int64_t)i1 * C);
-      upd(v0, i0);
-      upd(v1, i1);
+    for (; q + 3 < npx; q += 4) {
+      int ix[4];
+      uint4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ix[u] = next();
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4*>(fb + (int64_t)ix[u] * C);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) upd(v[u], ix[u]);
     }
-    if (q < npx) {
-      const int i0 = (bin.hs + q / bw) * W + bin.ws + q % bw;
+    for (; q < npx; ++q) {
+      const int i0 = next();
       upd(*reinterpret_cast<const uint4*>(fb + (int64_t)i0 * C), i0);
     }
   }
+  if (post.mean)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) m[k] = post_bn_relu(post, cv * 8 + k, m[k]);
   uint32_t o[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k)
@@ -167,7 +186,7 @@ roi_pool_fwd_vec8(const uint16_t* __restrict__ feat, int code, int B, int H, int
 template <typename T>
 __global__ void __launch_bounds__(256)
 roi_pool_fwd_scalar(const T* __restrict__ feat, int code, int B, int H, int W, int C, const float* __restrict__ rois, int R,
-                    int PH, int PW, float scale, T* __restrict__ out, int32_t* __restrict__ argmax) {
+                    int PH, int PW, float scale, T* __restrict__ out, int32_t* __restrict__ argmax, PostBn post) {
   const int64_t total = (int64_t)R * PH * PW * C;
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= total) return;
@@ -189,6 +208,7 @@ roi_pool_fwd_scalar(const T* __restrict__ feat, int code, int B, int H, int W, i
         if (f > m) { m = f; a = idx; }
       }
   }
+  if (post.mean) m = post_bn_relu(post, c, m);
   if constexpr (sizeof(T) == 2) out[t] = f32_to_h16(m, code); else out[t] = m;
   if (argmax) argmax[t] = a;
 }
@@ -211,30 +231,30 @@ roi_pool_bwd_kernel(const T* __restrict__ gout, const int32_t* __restrict__ argm
 }
 
 void roi_pool_fwd(const void* feat, int bf16, int B, int H, int W, int C, const float* rois, int R, int PH, int PW,
-                  float spatial_scale, void* out, int32_t* argmax, hipStream_t st) {
+                  float spatial_scale, void* out, int32_t* argmax, hipStream_t st, PostBn post) {
   if (R == 0 || C == 0) return;
   if (C % 8 == 0 && (bf16 == 1 || bf16 == 2)) {  // single-plane 16-bit: 8 channels per lane
     const int64_t total = (int64_t)R * PH * PW * (C / 8);
     roi_pool_fwd_vec8<<<div_up(total, 256), 256, 0, st>>>((const uint16_t*)feat, bf16, B, H, W, C, rois, R, PH, PW,
-                                                          spatial_scale, (uint16_t*)out, argmax);
+                                                          spatial_scale, (uint16_t*)out, argmax, post);
     return;
   }
   if (C % 4 == 0) {
     const int64_t total = (int64_t)R * PH * PW * (C / 4);
     if (bf16)
       roi_pool_fwd_vec4<uint16_t><<<div_up(total, 256), 256, 0, st>>>(
-          (const uint16_t*)feat, bf16, B, H, W, C, rois, R, PH, PW, spatial_scale, (uint16_t*)out, argmax);
+          (const uint16_t*)feat, bf16, B, H, W, C, rois, R, PH, PW, spatial_scale, (uint16_t*)out, argmax, post);
     else
       roi_pool_fwd_vec4<float><<<div_up(total, 256), 256, 0, st>>>(
-          (const float*)feat, 0, B, H, W, C, rois, R, PH, PW, spatial_scale, (float*)out, argmax);
+          (const float*)feat, 0, B, H, W, C, rois, R, PH, PW, spatial_scale, (float*)out, argmax, post);
   } else {
     const int64_t total = (int64_t)R * PH * PW * C;
     if (bf16)
       roi_pool_fwd_scalar<uint16_t><<<div_up(total, 256), 256, 0, st>>>(
-          (const uint16_t*)feat, bf16, B, H, W, C, rois, R, PH, PW, spatial_scale, (uint16_t*)out, argmax);
+          (const uint16_t*)feat, bf16, B, H, W, C, rois, R, PH, PW, spatial_scale, (uint16_t*)out, argmax, post);
     else
       roi_pool_fwd_scalar<float><<<div_up(total, 256), 256, 0, st>>>(
-          (const float*)feat, 0, B, H, W, C, rois, R, PH, PW, spatial_scale, (float*)out, argmax);
+          (const float*)feat, 0, B, H, W, C, rois, R, PH, PW, spatial_scale, (float*)out, argmax, post);
   }
 }
 

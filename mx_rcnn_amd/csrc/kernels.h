@@ -98,11 +98,20 @@ int proposal_sample(const float* rois, const float* gt, const int32_t* n_gt, con
                     const float* inside_w, float* out_rois, int32_t* out_label, float* bbox_target, float* inside,
                     float* outside, hipStream_t st);
 
+// Frozen BatchNorm + ReLU applied to a pooling output in the pooling kernel (inference: the next
+// pre-activation unit's bn1, whose input nothing else reads).  mean == nullptr: off.
+struct PostBn {
+  const float *gamma = nullptr, *beta = nullptr, *mean = nullptr, *var = nullptr;
+  float eps = 0.f;
+  int fix_gamma = 0;
+};
+
 // ---- RoI pooling (roi_pool.hip) -------------------------------------------
 // feat NHWC (B, H, W, C) bf16 or fp32; rois (R, 5); out (R, PH, PW, C); argmax (R, PH, PW, C) int32
-// holding h*W + w (or -1).
+// holding h*W + w (or -1).  post: relu(bn(out)) written instead of out (argmax must be null)
 void roi_pool_fwd(const void* feat, int bf16, int B, int H, int W, int C, const float* rois, int R,
-                  int PH, int PW, float spatial_scale, void* out, int32_t* argmax, hipStream_t st);
+                  int PH, int PW, float spatial_scale, void* out, int32_t* argmax, hipStream_t st,
+                  PostBn post = PostBn());
 // grad_in fp32 NHWC (B, H, W, C), must be zeroed; grad_out (R, PH, PW, C) bf16/fp32.
 // LDS-accumulated backward straight into grad_in (B, H, W, C) of the grad_out dtype (code: 0 fp32,
 // 1 bf16, 2 fp16); -1 when the H x W slab does not fit LDS (use roi_pool_bwd)
@@ -333,8 +342,9 @@ int bn_train_bwd(const uint16_t* x, const uint16_t* dy, int64_t M, int C, const 
 
 // ---- pooling (pool.hip): NHWC bf16, C % 8 == 0 ------------------------------------------------
 // arg: one byte per output element, the winning tap (i * k + j) of its window
+// post: relu(bn(y)) written instead of y (inference; the taps in arg still index the max)
 int maxpool_fwd(const uint16_t* x, uint16_t* y, uint8_t* arg, int N, int H, int W, int C, int Ho, int Wo, int k,
-                int s, int p, int code, hipStream_t st);
+                int s, int p, int code, hipStream_t st, PostBn post = PostBn());
 int maxpool_bwd(const uint16_t* dy, const uint8_t* arg, uint16_t* dx, int N, int H, int W, int C, int Ho, int Wo,
                 int k, int s, int p, int code, hipStream_t st);
 int avgpool_fwd(const uint16_t* x, uint16_t* y, int N, int HW, int C, int code, hipStream_t st);

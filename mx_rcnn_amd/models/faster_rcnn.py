@@ -27,6 +27,7 @@ from ..utils import profiler as prof
 from ..ops import anchor_target, proposal, proposal_target, roi_pool
 from ..ops._ext import unit_grad
 from ..ops.head import rpn_head
+from ..ops.roi_pool import roi_pool_bn_relu
 from ..ops.losses import combine_losses, rpn_softmax_ce, smooth_l1, softmax_ce
 from .layers import Conv
 from .resnet import ResNetHead, ResNetTrunk
@@ -383,8 +384,13 @@ class FasterRCNN(nn.Module):
             rpn_cls, rpn_bbox = self.rpn(feat)
             rois, _ = self._proposal(rpn_cls, rpn_bbox, im_info, 'TEST')
             rois = rois.reshape(-1, 5)
-        pooled = roi_pool(feat, rois, (7, 7), 1.0 / self.feat_stride)
-        cls_score, bbox_pred = self.head(pooled)
+        bn = self.head.pool_bn(feat) if hasattr(self.head, 'pool_bn') else None
+        if bn is not None:  # the head's first bn1 + ReLU in the pooling kernel (ops/roi_pool.py)
+            act = roi_pool_bn_relu(feat, rois, (7, 7), 1.0 / self.feat_stride, bn)
+            cls_score, bbox_pred = self.head(act, act1=act)
+        else:
+            pooled = roi_pool(feat, rois, (7, 7), 1.0 / self.feat_stride)
+            cls_score, bbox_pred = self.head(pooled)
         return rois, torch.softmax(cls_score.float(), dim=1), bbox_pred.float()
 
 

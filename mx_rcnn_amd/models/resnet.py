@@ -11,7 +11,7 @@ import torch.nn as nn
 from ..ops.conv import igemm_eligible, weight_ok
 from ..ops.fused import conv_add, conv_add_bn_relu, conv_bn_relu, fused_unit
 from ..ops.head import fc_pair
-from ..ops.pool import global_avg_pool
+from ..ops.pool import global_avg_pool, kernel_path, max_pool_bn_relu, post_bn_ok
 from ..ops.stem import stem_fusable, stem_conv
 from .layers import BatchNorm, Conv, Linear, max_pool
 
@@ -237,11 +237,17 @@ class ResNetTrunk(nn.Module):
             x = stem_conv(x, self.conv0.weight, 2, 3, in_bn=self.bn_data, out_bn=self.bn0, relu=True)
         else:
             x = self.bn0(self.conv0(self.bn_data(x)))
-        x = max_pool(x, 3, 2, 1)
+        u1 = self.stage1[0]
+        act = None
+        if kernel_path(x) and fusion_enabled() and not u1.dim_match and post_bn_ok(u1.bn1):
+            # inference: stage1_unit1's bn1 + ReLU in the max-pool kernel; the projection unit reads
+            # only that activation (x stays as the shape carrier)
+            x = act = max_pool_bn_relu(x, 3, 2, 1, u1.bn1)
+        else:
+            x = max_pool(x, 3, 2, 1)
         # each stage's last unit also produces the next stage's first bn1 activation in its epilogue
         # (no separate BN + ReLU pass at the stage boundaries)
         stages = (self.stage1, self.stage2, self.stage3)
-        act = None
         for i, st in enumerate(stages):
             nxt_bn = stages[i + 1][0].bn1 if i + 1 < len(stages) else None
             x, _, act = run_stage_parts(st, x, nxt_bn, tail_act=True, act1_in=act)
@@ -266,10 +272,18 @@ class ResNetHead(nn.Module):
         self.cls_score = Linear('cls_score', filters[4], num_classes)
         self.bbox_pred = Linear('bbox_pred', filters[4], 4 * num_classes)
 
-    def forward(self, pooled):
+    def pool_bn(self, feat):
+        """stage4_unit1's bn1 when the RoI pooling kernel may apply it (inference on the HIP path:
+        16-bit or plane maps, frozen BN, a projection unit that reads only bn1's output) -> the
+        BatchNorm or None."""
+        u = self.stage4[0]
+        return u.bn1 if (kernel_path(feat) and fusion_enabled() and not u.dim_match and post_bn_ok(u.bn1)) else None
+
+    def forward(self, pooled, act1=None):
+        """act1: relu(bn1(pooled)) of the first unit when the pooling produced it (pool_bn)."""
         # fused units either way: frozen BNs (test time) or batch statistics (training), where the
         # last unit's conv epilogue also produces bn1's statistics partials
-        x, parts, act = run_stage_parts(self.stage4, pooled, self.bn1, tail_act=True)
+        x, parts, act = run_stage_parts(self.stage4, pooled, self.bn1, tail_act=True, act1_in=act1)
         x = act if act is not None else self.bn1(x, parts=parts)
         x = global_avg_pool(x)
         return fc_pair(x, self.cls_score, self.bbox_pred)

@@ -7,7 +7,7 @@ from .nms import nms, batched_nms  # noqa: F401
 from .proposal import proposal  # noqa: F401
 from .anchor_target import anchor_target  # noqa: F401
 from .proposal_target import proposal_target  # noqa: F401
-from .roi_pool import roi_pool  # noqa: F401
+from .roi_pool import roi_pool, roi_pool_bn_relu  # noqa: F401
 from .losses import rpn_softmax_ce, softmax_ce, smooth_l1  # noqa: F401
 from .bn import frozen_bn_relu  # noqa: F401
 from .sgd import sgd_momentum_  # noqa: F401

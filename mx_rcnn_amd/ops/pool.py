@@ -5,6 +5,11 @@ convention: VGG pool1..4 2x2/2 (`rcnn/symbol.py:19,28,40,52`), ResNet pool0 3x3/
 (`rcnn/resnet.py:150`); ``Pooling(global_pool=True, pool_type='avg')`` before the ResNet
 predictors (`rcnn/resnet.py:167`).  GPU bf16 channels_last tensors run the HIP kernels (the
 backward gathers through the recorded winning taps, no atomics); anything else runs torch.
+
+Inference: a pooling whose output only feeds a frozen BN + ReLU (ResNet pool0 -> stage1_unit1_bn1,
+RoI pooling -> stage4_unit1_bn1: pre-activation projection units read nothing but bn1's output)
+writes relu(bn(pool)) straight from the pooling kernel -- no separate BN pass over the map, and no
+tap / argmax map (``max_pool_bn_relu``, ops/roi_pool.py ``roi_pool_bn_relu``).
 """
 import os
 
@@ -49,6 +54,34 @@ class _AvgPool(torch.autograd.Function):
     @staticmethod
     def backward(ctx, dy):
         return need_ext().avgpool_bwd(dy.contiguous(), ctx.hw[0], ctx.hw[1], ctx.x2)
+
+
+def post_bn_ok(bn):
+    """The frozen BN + ReLU ``bn`` may be applied in a pooling kernel's store: no gradient is being
+    recorded, BN uses its moving statistics (not calibrating them), ReLU follows."""
+    if os.environ.get('MXR_POOL_POST_BN', '1') == '0' or torch.is_grad_enabled():
+        return False
+    return bool(bn.relu) and (bn.use_global_stats or not bn.training) and not getattr(bn, '_calibrate', False)
+
+
+def kernel_path(x):
+    """x takes the HIP pooling kernels (16-bit channels_last or fp32-class planes)."""
+    return _eligible(x) or bool(precision.is_pair(x))
+
+
+def post_bn_params(bn):
+    """-> ([gamma, beta, moving_mean, moving_var] fp32 contiguous, eps, fix_gamma) for the kernels."""
+    prm = [t.detach().float().contiguous() for t in (bn.gamma, bn.beta, bn.moving_mean, bn.moving_var)]
+    return prm, float(bn.eps), bool(bn.fix_gamma)
+
+
+def max_pool_bn_relu(x, k, s, p, bn):
+    """relu(bn(max_pool(x))) for a frozen ``bn``: one kernel on the HIP path (post_bn_ok), else the
+    two ops."""
+    if post_bn_ok(bn) and kernel_path(x):
+        prm, eps, fix = post_bn_params(bn)
+        return need_ext().maxpool_fwd(x, int(k), int(s), int(p), precision.is_pair(x), False, prm, eps, fix)[0]
+    return bn(max_pool2d(x, k, s, p))
 
 
 def max_pool2d(x, k, s, p=0):

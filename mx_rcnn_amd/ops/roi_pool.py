@@ -119,3 +119,15 @@ def roi_pool(feat, rois, pooled_size=(7, 7), spatial_scale=0.0625, grad_add=None
     gradient of ``feat`` from elsewhere (B, C, H, W), added to the pooling's input gradient in
     the backward kernel -- the early RPN-head backward's (models/faster_rcnn.py)."""
     return _RoIPool.apply(feat, rois, int(pooled_size[0]), int(pooled_size[1]), float(spatial_scale), grad_add)
+
+
+def roi_pool_bn_relu(feat, rois, pooled_size, spatial_scale, bn):
+    """relu(bn(roi_pool(feat, rois))) for a frozen ``bn`` (inference: stage4_unit1_bn1 of the ResNet
+    head): the BN + ReLU in the pooling kernel's store, no argmax map (ops/pool.py post_bn_ok)."""
+    from .pool import post_bn_ok, post_bn_params
+    if feat.is_cuda and post_bn_ok(bn):
+        prm, eps, fix = post_bn_params(bn)
+        return need_ext().roi_pool_fwd(feat.contiguous(memory_format=torch.channels_last), rois.float().contiguous(),
+                                       int(pooled_size[0]), int(pooled_size[1]), float(spatial_scale),
+                                       precision.is_pair(feat), False, prm, eps, fix)[0]
+    return bn(roi_pool(feat, rois, pooled_size, spatial_scale))

@@ -13,7 +13,7 @@ for rep in $(seq 1 ${REPS:-1}); do
   for spec in ${AB:-}; do
     name=${spec%%:*}; envs=${spec#*:}
     [ "$envs" = "$spec" ] && envs=""
-    timeout -k 10 ${BENCH_LIMIT:-300} env $(echo "$envs" | tr ',' ' ') python bench.py ${BENCH_ARGS:---steps 40 --warmup 5 --no-bf16-extra} \
+    timeout -k 10 ${BENCH_LIMIT:-300} env $(echo "$envs" | tr ',' ' ') python ${BENCH_SCRIPT:-bench.py} ${BENCH_ARGS:---steps 40 --warmup 5 --no-bf16-extra} \
       > $OUT/ab_${name}_$rep.log 2>&1 || { tail -20 $OUT/ab_${name}_$rep.log; exit 1; }
     echo "$name rep$rep $(grep '^{' $OUT/ab_${name}_$rep.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); print(d["value"], d["ms_per_step"], d["config"].get("hip_runtime"))')"
   done

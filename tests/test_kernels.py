@@ -733,6 +733,68 @@ def test_maxpool_vs_torch(cuda, N, C, H, W, k, s, p):
     assert (xg.grad.float().cpu() - xr.grad).abs().max().item() <= 2e-2 * xr.grad.abs().max().item()
 
 
+def _post_bn(g, C, cuda, fix_gamma):
+    """Frozen-BN params with both signs of gamma (a negative scale flips which input is largest)."""
+    gamma = torch.randn(C, generator=g)
+    beta = torch.randn(C, generator=g) * 0.5
+    mean = torch.randn(C, generator=g) * 0.3
+    var = torch.rand(C, generator=g) + 0.2
+    return [t.to(cuda).contiguous() for t in (gamma, beta, mean, var)], 2e-5, fix_gamma
+
+
+def _bn_relu_ref(y, prm, eps, fix):
+    gamma, beta, mean, var = [t.cpu().double() for t in prm]
+    s = (torch.ones_like(gamma) if fix else gamma) / torch.sqrt(var + eps)
+    return torch.relu(y.double() * s[None, :, None, None] + (beta - mean * s)[None, :, None, None])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype,C,fix', [(torch.bfloat16, 1024, False), (torch.float16, 256, True),
+                                         (torch.float32, 64, False), (torch.float32, 6, False)])
+def test_roi_pool_post_bn_matches_pool_then_bn(cuda, dtype, C, fix):
+    """roi_pool_fwd(post_bn=...) == bn_relu_fwd(roi_pool_fwd(...)) bit for bit on 16-bit maps (the
+    inference fusion of stage4_unit1_bn1 into the pooling store); fp32 / odd C vs a float64 reference."""
+    from mx_rcnn_amd.ops import need_ext
+    ext = need_ext()
+    g = torch.Generator().manual_seed(11)
+    B, H, W = 2, 38, 50
+    feat = torch.randn(B, C, H, W, generator=g).to(cuda, dtype).contiguous(memory_format=torch.channels_last)
+    rois = _rois(g, 64, B, H, W).to(cuda)
+    rois[3, 0] = -1  # empty output rows: relu(bn(0))
+    prm, eps, fix = _post_bn(g, C, cuda, fix)
+    got, arg = ext.roi_pool_fwd(feat, rois, 7, 7, 1 / 16, 0, False, prm, eps, fix)
+    assert arg.numel() == 0 and got.is_contiguous(memory_format=torch.channels_last)
+    pooled = ext.roi_pool_fwd(feat, rois, 7, 7, 1 / 16, 0, False)[0]
+    if dtype != torch.float32:
+        want = ext.bn_relu_fwd(pooled, *prm, eps, fix, True, 0)
+        assert torch.equal(got, want), (got.float() - want.float()).abs().max().item()
+    want = _bn_relu_ref(pooled.float().cpu(), prm, eps, fix)
+    tol = 1e-5 if dtype == torch.float32 else 1e-2
+    assert torch.allclose(got.double().cpu(), want, atol=tol, rtol=tol)
+    with pytest.raises(RuntimeError, match='inference-only'):
+        ext.roi_pool_fwd(feat, rois, 7, 7, 1 / 16, 0, True, prm, eps, fix)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype,fix', [(torch.bfloat16, False), (torch.float16, True)])
+def test_maxpool_post_bn_matches_pool_then_bn(cuda, dtype, fix):
+    """maxpool_fwd(need_arg=False, post_bn=...) == bn_relu_fwd(maxpool_fwd(...)) bit for bit (ResNet
+    pool0 -> stage1_unit1_bn1 at inference), and no tap map is written."""
+    from mx_rcnn_amd.ops import need_ext
+    ext = need_ext()
+    g = torch.Generator().manual_seed(12)
+    x = torch.randn(2, 64, 41, 53, generator=g).to(cuda, dtype).contiguous(memory_format=torch.channels_last)
+    prm, eps, fix = _post_bn(g, 64, cuda, fix)
+    got, arg = ext.maxpool_fwd(x, 3, 2, 1, 0, False, prm, eps, fix)
+    assert arg.numel() == 0
+    want = ext.bn_relu_fwd(ext.maxpool_fwd(x, 3, 2, 1, 0)[0], *prm, eps, fix, True, 0)
+    assert torch.equal(got, want), (got.float() - want.float()).abs().max().item()
+    ref = _bn_relu_ref(F.max_pool2d(x.float().cpu(), 3, 2, 1), prm, eps, fix)
+    assert torch.allclose(got.double().cpu(), ref, atol=1e-2, rtol=1e-2)
+    with pytest.raises(RuntimeError, match='inference-only'):
+        ext.maxpool_fwd(x, 3, 2, 1, 0, True, prm, eps, fix)
+
+
 @pytest.mark.gpu
 def test_global_avgpool_vs_torch(cuda):
     from mx_rcnn_amd.ops.pool import global_avg_pool

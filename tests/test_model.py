@@ -340,6 +340,35 @@ def test_fp32_detector_on_mfma_kernels_matches_torch_fp32(cuda, net, monkeypatch
         assert v.dtype == before[k].dtype and torch.equal(v, before[k]), k
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize('dtype', ['bf16', 'fp32'])
+def test_pool_post_bn_fusion_keeps_detections(cuda, dtype, monkeypatch):
+    """The inference fusions of stage1_unit1_bn1 into pool0 and stage4_unit1_bn1 into the RoI pooling
+    (ops/pool.py post_bn_ok) leave the detector's outputs unchanged: bit for bit in bf16, to fp32
+    rounding in the three-plane fp32 mode; and the fused kernels do run (no bn_relu_fwd launch)."""
+    from mx_rcnn_amd.core.detector import Detector
+    from mx_rcnn_amd.ops import need_ext
+    m, data, info, rois = _det_setup('resnet50')
+    outs = {}
+    for flag in ('0', '1'):
+        monkeypatch.setenv('MXR_POOL_POST_BN', flag)
+        det = Detector(m, cuda, compute_dtype=dtype)
+        ext = need_ext()
+        calls = []
+        real = ext.bn_relu_fwd
+        monkeypatch.setattr(ext, 'bn_relu_fwd', lambda *a, **k: calls.append(1) or real(*a, **k))
+        outs[flag] = ([t.float().cpu() for t in det.forward(data, info, rois)],
+                      [t.float().cpu() for t in det.forward(data, info)], len(calls))
+        monkeypatch.setattr(ext, 'bn_relu_fwd', real)
+    (f0, r0, n0), (f1, r1, n1) = outs['0'], outs['1']
+    assert n0 >= 4 and n1 == 0, (n0, n1)  # pool0 + RoI pooling, per forward
+    for a, b in zip(f0 + r0, f1 + r1):
+        if dtype == 'bf16':
+            assert torch.equal(a, b)
+        else:
+            assert torch.allclose(a, b, atol=1e-4, rtol=1e-4), (a - b).abs().max().item()
+
+
 def test_unit_seed_backward_matches_default():
     """A backward seeded with ops._ext.unit_grad (loss ops skip their scale-by-1) gives the same
     gradients as the default seed, and a non-unit seed still scales."""

@@ -381,29 +381,37 @@ std::vector<Tensor> anchor_target_assign(const Tensor& base_anchors, int64_t H, 
   return {label, targets, max_ov, argmax};
 }
 
-// frozen BN + ReLU fused into a pooling kernel's store (kernels.h PostBn); none: off
-static mxr::PostBn post_bn_args(const c10::optional<std::vector<Tensor>>& bn, double eps, bool fix_gamma, int64_t C) {
+// frozen BN + ReLU fused into a pooling kernel's store (kernels.h PostBn): post_bn is bn_affine's
+// (2, C) [scale; shift]; none: off
+static mxr::PostBn post_bn_args(const c10::optional<Tensor>& bn, int64_t C) {
   mxr::PostBn p;
   if (!bn) return p;
-  TORCH_CHECK(bn->size() == 4, "post_bn: [gamma, beta, mean, var]");
-  for (const auto& t : *bn)
-    TORCH_CHECK(t.is_cuda() && t.scalar_type() == at::kFloat && t.is_contiguous() && t.numel() == C,
-                "post_bn params: fp32 (C,) device tensors");
-  p.gamma = (*bn)[0].data_ptr<float>();
-  p.beta = (*bn)[1].data_ptr<float>();
-  p.mean = (*bn)[2].data_ptr<float>();
-  p.var = (*bn)[3].data_ptr<float>();
-  p.eps = (float)eps;
-  p.fix_gamma = fix_gamma ? 1 : 0;
+  TORCH_CHECK(bn->is_cuda() && bn->scalar_type() == at::kFloat && bn->is_contiguous() && bn->dim() == 2 &&
+                  bn->size(0) == 2 && bn->size(1) == C,
+              "post_bn: fp32 (2, C) [scale; shift] device tensor from bn_affine");
+  p.scale = bn->data_ptr<float>();
+  p.shift = p.scale + C;
   return p;
+}
+
+Tensor bn_affine(const Tensor& gamma, const Tensor& beta, const Tensor& mean, const Tensor& var, double eps,
+                 bool fix_gamma) {
+  const int64_t C = var.numel();
+  for (auto* t : {&gamma, &beta, &mean, &var})
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kFloat && t->is_contiguous() && t->numel() == C,
+                "bn_affine: fp32 (C,) device tensors");
+  DevGuard g(var.device());
+  Tensor out = at::empty({2, C}, var.options());
+  mxr::bn_affine(gamma.data_ptr<float>(), beta.data_ptr<float>(), mean.data_ptr<float>(), var.data_ptr<float>(),
+                 (float)eps, fix_gamma ? 1 : 0, (int)C, out.data_ptr<float>(), cur_stream());
+  return out;
 }
 
 // ---- RoI pooling -----------------------------------------------------------------------
 // feat must be channels-last in memory: logical (B, C, H, W) with NHWC strides.
 // x2: feat is a (2B, C, H, W) hi / lo pair, the pooled output (2R, C, PH, PW) a pair too
 std::vector<Tensor> roi_pool_fwd(const Tensor& feat, const Tensor& rois, int64_t PH, int64_t PW, double scale, int64_t x2,
-                                 bool need_argmax, c10::optional<std::vector<Tensor>> post_bn, double post_eps,
-                                 bool post_fix_gamma) {
+                                 bool need_argmax, c10::optional<Tensor> post_bn) {
   CHECK_DEV(feat); CHECK_DEV(rois); CHECK_F32(rois); CHECK_CONTIG(rois);
   TORCH_CHECK(feat.dim() == 4 && feat.is_contiguous(at::MemoryFormat::ChannelsLast),
               "feat must be (B,C,H,W) channels_last");
@@ -414,7 +422,7 @@ std::vector<Tensor> roi_pool_fwd(const Tensor& feat, const Tensor& rois, int64_t
             W = (int)feat.size(3);
   const int R = (int)rois.size(0);
   TORCH_CHECK(!(post_bn && need_argmax), "roi_pool_fwd: post_bn is inference-only (no argmax)");
-  const mxr::PostBn post = post_bn_args(post_bn, post_eps, post_fix_gamma, C);
+  const mxr::PostBn post = post_bn_args(post_bn, C);
   DevGuard g(feat.device());
   Tensor out = at::empty({x2 ? npl(x2) * R : R, C, PH, PW}, feat.options().memory_format(at::MemoryFormat::ChannelsLast));
   // inference skips the argmax map (4 B per output element: at batch 8 x 300 RoIs x 1024 channels
@@ -1332,7 +1340,7 @@ void wgrad_reduce_run(const Tensor& slab, Tensor out) {
 
 // ---- pooling ---------------------------------------------------------------------------------
 std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t p, int64_t x2, bool need_arg,
-                                c10::optional<std::vector<Tensor>> post_bn, double post_eps, bool post_fix_gamma) {
+                                c10::optional<Tensor> post_bn) {
   CHECK_DEV(x);
   TORCH_CHECK((x.scalar_type() == at::kBFloat16 || x.scalar_type() == at::kHalf) && x.dim() == 4 &&
                   x.is_contiguous(at::MemoryFormat::ChannelsLast),
@@ -1343,7 +1351,7 @@ std::vector<Tensor> maxpool_fwd(const Tensor& x, int64_t k, int64_t s, int64_t p
   const int Ho = (H + 2 * (int)p - (int)k) / (int)s + 1, Wo = (W + 2 * (int)p - (int)k) / (int)s + 1;
   TORCH_CHECK(Ho > 0 && Wo > 0, "maxpool: empty output");
   TORCH_CHECK(!(post_bn && need_arg), "maxpool_fwd: post_bn is inference-only (no taps)");
-  const mxr::PostBn post = post_bn_args(post_bn, post_eps, post_fix_gamma, C);
+  const mxr::PostBn post = post_bn_args(post_bn, C);
   DevGuard g(x.device());
   Tensor y = at::empty({x2 ? npl(x2) * N : N, C, Ho, Wo}, x.options().memory_format(at::MemoryFormat::ChannelsLast));
   Tensor arg = need_arg ? at::empty({N, C, Ho, Wo}, x.options().dtype(at::kByte).memory_format(at::MemoryFormat::ChannelsLast))
@@ -2336,8 +2344,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("proposal_sample", &proposal_sample);
   m.def("anchor_target_assign", &anchor_target_assign);
   m.def("roi_pool_fwd", &roi_pool_fwd, py::arg("feat"), py::arg("rois"), py::arg("PH"), py::arg("PW"),
-        py::arg("scale"), py::arg("x2") = 0, py::arg("need_argmax") = true, py::arg("post_bn") = py::none(),
-        py::arg("post_eps") = 0.0, py::arg("post_fix_gamma") = false);
+        py::arg("scale"), py::arg("x2") = 0, py::arg("need_argmax") = true, py::arg("post_bn") = py::none());
   m.def("roi_pool_bwd", &roi_pool_bwd, py::arg("grad_out"), py::arg("argmax"), py::arg("rois"), py::arg("B"),
         py::arg("H"), py::arg("W"), py::arg("grad_add") = py::none(), py::arg("x2") = 0);
   m.def("rpn_softmax_ce", &rpn_softmax_ce, py::arg("logits"), py::arg("label"), py::arg("norm"), py::arg("grad_scale"),
@@ -2392,8 +2399,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("im_info"), py::arg("thresh"), py::arg("nms_thresh"), py::arg("max_per"), py::arg("cap"));
   m.def("nest_keep", &nest_keep, py::arg("dets"), py::arg("thresh"));
   m.def("maxpool_fwd", &maxpool_fwd, py::arg("x"), py::arg("k"), py::arg("s"), py::arg("p"), py::arg("x2") = 0,
-        py::arg("need_arg") = true, py::arg("post_bn") = py::none(), py::arg("post_eps") = 0.0,
-        py::arg("post_fix_gamma") = false);
+        py::arg("need_arg") = true, py::arg("post_bn") = py::none());
+  m.def("bn_affine", &bn_affine, py::arg("gamma"), py::arg("beta"), py::arg("mean"), py::arg("var"), py::arg("eps"),
+        py::arg("fix_gamma"));
   m.def("maxpool_bwd", &maxpool_bwd, py::arg("dy"), py::arg("arg"), py::arg("H"), py::arg("W"), py::arg("k"),
         py::arg("s"), py::arg("p"), py::arg("x2") = 0);
   m.def("avgpool_fwd", &avgpool_fwd, py::arg("x"), py::arg("x2") = 0);

@@ -246,6 +246,22 @@ static int bn_grid(int64_t M, int C, int64_t cap = 1024) {
   return (int)blocks;
 }
 
+__global__ void __launch_bounds__(256)
+bn_affine_kernel(const float* __restrict__ gamma, const float* __restrict__ beta, const float* __restrict__ mean,
+                 const float* __restrict__ var, float eps, int fix_gamma, int C, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  float s, t;
+  bn_coeffs(c, gamma, beta, mean, var, eps, fix_gamma, s, t);
+  out[c] = s;
+  out[C + c] = t;
+}
+
+void bn_affine(const float* gamma, const float* beta, const float* mean, const float* var, float eps, int fix_gamma,
+               int C, float* out, hipStream_t st) {
+  if (C > 0) bn_affine_kernel<<<(C + 255) / 256, 256, 0, st>>>(gamma, beta, mean, var, eps, fix_gamma, C, out);
+}
+
 void bn_relu_fwd(const void* x, int bf16, int64_t M, int C, const float* gamma, const float* beta, const float* mean,
                  const float* var, float eps, int fix_gamma, int relu, void* y, hipStream_t st) {
   if (M == 0 || C == 0) return;

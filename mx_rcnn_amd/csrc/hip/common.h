@@ -26,10 +26,16 @@ __device__ __forceinline__ uint16_t f32_to_f16(float f) { return __half_as_ushor
 // PostBn (kernels.h): relu(v * s + t) with bn_act.hip's per-channel coefficients, so the fused
 // pooling output is bit-identical to pooling followed by bn_relu_fwd
 __device__ __forceinline__ float post_bn_relu(const PostBn& p, int c, float v) {
-  const float inv = rsqrtf(p.var[c] + p.eps);
-  const float s = (p.fix_gamma ? 1.f : p.gamma[c]) * inv;
-  const float t = p.beta[c] - p.mean[c] * s;
-  return fmaxf(v * s + t, 0.f);
+  return fmaxf(v * p.scale[c] + p.shift[c], 0.f);
+}
+// 8 consecutive channels c0..c0+7 (c0 % 8 == 0): two 16-B loads per coefficient
+__device__ __forceinline__ void post_bn_relu8(const PostBn& p, int c0, float* v) {
+  const float4 s0 = *reinterpret_cast<const float4*>(p.scale + c0), s1 = *reinterpret_cast<const float4*>(p.scale + c0 + 4);
+  const float4 t0 = *reinterpret_cast<const float4*>(p.shift + c0), t1 = *reinterpret_cast<const float4*>(p.shift + c0 + 4);
+  const float s[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+  const float t[8] = {t0.x, t0.y, t0.z, t0.w, t1.x, t1.y, t1.z, t1.w};
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = fmaxf(v[k] * s[k] + t[k], 0.f);
 }
 
 __device__ __forceinline__ float h16_to_f32(uint16_t v, int code) {

@@ -52,10 +52,11 @@ maxpool_fwd_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ y, uin
         }
     }
   }
-  if (post.mean) {  // inference: the next unit's bn1 + ReLU on the pooled value
+  if (post.scale) {  // inference: the next unit's bn1 + ReLU on the pooled value
     float a[8];
 #pragma unroll
-    for (int q = 0; q < 8; ++q) a[q] = post_bn_relu(post, c8 * 8 + q, best[q]);
+    for (int q = 0; q < 8; ++q) a[q] = best[q];
+    post_bn_relu8(post, c8 * 8, a);
     st8c(y, pix * C + c8 * 8, code, (int64_t)N * Ho * Wo * C, a);
   } else {
     st8c(y, pix * C + c8 * 8, code, (int64_t)N * Ho * Wo * C, best);

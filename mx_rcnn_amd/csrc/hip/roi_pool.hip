@@ -9,6 +9,7 @@
 // one channel per lane, i.e. each wave-instruction adds 256 contiguous bytes (Guideline 12);
 // 128 RoIs x 49 bins x 1024 ch = 25 MB of adds, ~20 us at the chip-wide atomic rate.
 #include "common.h"
+#include <cstdlib>
 #include "../kernels.h"
 
 namespace mxr {
@@ -85,7 +86,7 @@ roi_pool_fwd_vec4(const T* __restrict__ feat, int code, int B, int H, int W, int
       }
     }
   }
-  if (post.mean) {
+  if (post.scale) {
     m0 = post_bn_relu(post, cv * 4, m0); m1 = post_bn_relu(post, cv * 4 + 1, m1);
     m2 = post_bn_relu(post, cv * 4 + 2, m2); m3 = post_bn_relu(post, cv * 4 + 3, m3);
   }
@@ -104,9 +105,10 @@ roi_pool_fwd_vec4(const T* __restrict__ feat, int code, int B, int H, int W, int
   if (argmax) *reinterpret_cast<int4*>(argmax + o) = make_int4(a0, a1, a2, a3);  // null: inference, no backward
 }
 
-// 8 channels per lane, single-plane 16-bit maps (bf16 / fp16): 16-B loads, four bin pixels per
-// iteration in flight; the batch-8 inference pooling (2400 RoIs x 49 bins x 1024 channels) is a
+// 8 channels per lane, single-plane 16-bit maps (bf16 / fp16): 16-B loads, U bin pixels per
+// iteration in flight (MXR_ROI_UNROLL, default 2); the batch-8 inference pooling (2400 RoIs x 49 bins x 1024 channels) is a
 // latency-bound gather at 4 channels per lane and one load at a time
+template <int U>
 __global__ void __launch_bounds__(256)
 roi_pool_fwd_vec8(const uint16_t* __restrict__ feat, int code, int B, int H, int W, int C,
                   const float* __restrict__ rois, int R, int PH, int PW, float scale, uint16_t* __restrict__ out,
@@ -142,7 +144,7 @@ roi_pool_fwd_vec8(const uint16_t* __restrict__ feat, int code, int B, int H, int
         if (f1 > m[2 * k + 1]) { m[2 * k + 1] = f1; a[2 * k + 1] = idx; }
       }
     };
-    // row-major walk with a running (h, w): four loads issued together, compared in order
+    // row-major walk with a running (h, w): U loads issued together, compared in order
     int h = bin.hs, w = bin.ws;
     auto next = [&]() {
       const int idx = h * W + w;
@@ -153,24 +155,22 @@ roi_pool_fwd_vec8(const uint16_t* __restrict__ feat, int code, int B, int H, int
       return idx;
     };
     int q = 0;
-    for (; q + 3 < npx; q += 4) {
-      int ix[4];
-      uint4 v[4];
+    for (; q + U - 1 < npx; q += U) {
+      int ix[U];
+      uint4 v[U];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) ix[u] = next();
+      for (int u = 0; u < U; ++u) ix[u] = next();
 #pragma unroll
-      for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const uint4*>(fb + (int64_t)ix[u] * C);
+      for (int u = 0; u < U; ++u) v[u] = *reinterpret_cast<const uint4*>(fb + (int64_t)ix[u] * C);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) upd(v[u], ix[u]);
+      for (int u = 0; u < U; ++u) upd(v[u], ix[u]);
     }
     for (; q < npx; ++q) {
       const int i0 = next();
       upd(*reinterpret_cast<const uint4*>(fb + (int64_t)i0 * C), i0);
     }
   }
-  if (post.mean)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) m[k] = post_bn_relu(post, cv * 8 + k, m[k]);
+  if (post.scale) post_bn_relu8(post, cv * 8, m);
   uint32_t o[4];
 #pragma unroll
   for (int k = 0; k < 4; ++k)
@@ -208,7 +208,7 @@ roi_pool_fwd_scalar(const T* __restrict__ feat, int code, int B, int H, int W, i
         if (f > m) { m = f; a = idx; }
       }
   }
-  if (post.mean) m = post_bn_relu(post, c, m);
+  if (post.scale) m = post_bn_relu(post, c, m);
   if constexpr (sizeof(T) == 2) out[t] = f32_to_h16(m, code); else out[t] = m;
   if (argmax) argmax[t] = a;
 }
@@ -235,8 +235,16 @@ void roi_pool_fwd(const void* feat, int bf16, int B, int H, int W, int C, const 
   if (R == 0 || C == 0) return;
   if (C % 8 == 0 && (bf16 == 1 || bf16 == 2)) {  // single-plane 16-bit: 8 channels per lane
     const int64_t total = (int64_t)R * PH * PW * (C / 8);
-    roi_pool_fwd_vec8<<<div_up(total, 256), 256, 0, st>>>((const uint16_t*)feat, bf16, B, H, W, C, rois, R, PH, PW,
-                                                          spatial_scale, (uint16_t*)out, argmax, post);
+    static const int unroll = [] {
+      const char* e = getenv("MXR_ROI_UNROLL");
+      return e && atoi(e) == 4 ? 4 : 2;
+    }();
+    if (unroll == 4)
+      roi_pool_fwd_vec8<4><<<div_up(total, 256), 256, 0, st>>>((const uint16_t*)feat, bf16, B, H, W, C, rois, R, PH, PW,
+                                                               spatial_scale, (uint16_t*)out, argmax, post);
+    else
+      roi_pool_fwd_vec8<2><<<div_up(total, 256), 256, 0, st>>>((const uint16_t*)feat, bf16, B, H, W, C, rois, R, PH, PW,
+                                                               spatial_scale, (uint16_t*)out, argmax, post);
     return;
   }
   if (C % 4 == 0) {

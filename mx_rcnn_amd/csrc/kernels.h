@@ -99,12 +99,16 @@ int proposal_sample(const float* rois, const float* gt, const int32_t* n_gt, con
                     float* outside, hipStream_t st);
 
 // Frozen BatchNorm + ReLU applied to a pooling output in the pooling kernel (inference: the next
-// pre-activation unit's bn1, whose input nothing else reads).  mean == nullptr: off.
+// pre-activation unit's bn1, whose input nothing else reads): relu(v * scale[c] + shift[c]) with the
+// per-channel coefficients from bn_affine (bn_act.hip, the same arithmetic as bn_relu_fwd).
+// scale == nullptr: off.
 struct PostBn {
-  const float *gamma = nullptr, *beta = nullptr, *mean = nullptr, *var = nullptr;
-  float eps = 0.f;
-  int fix_gamma = 0;
+  const float* scale = nullptr;
+  const float* shift = nullptr;
 };
+// (scale, shift) of a frozen BN into out[0..C) / out[C..2C)
+void bn_affine(const float* gamma, const float* beta, const float* mean, const float* var, float eps, int fix_gamma,
+               int C, float* out, hipStream_t st);
 
 // ---- RoI pooling (roi_pool.hip) -------------------------------------------
 // feat NHWC (B, H, W, C) bf16 or fp32; rois (R, 5); out (R, PH, PW, C); argmax (R, PH, PW, C) int32

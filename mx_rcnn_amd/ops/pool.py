@@ -70,17 +70,28 @@ def kernel_path(x):
 
 
 def post_bn_params(bn):
-    """-> ([gamma, beta, moving_mean, moving_var] fp32 contiguous, eps, fix_gamma) for the kernels."""
-    prm = [t.detach().float().contiguous() for t in (bn.gamma, bn.beta, bn.moving_mean, bn.moving_var)]
-    return prm, float(bn.eps), bool(bn.fix_gamma)
+    """-> the (2, C) fp32 [scale; shift] of frozen ``bn`` for the pooling kernels (ext.bn_affine: the
+    arithmetic of bn_relu_fwd, so the fused output is the same bits), cached on the module and
+    rebuilt when a parameter / statistic moves (version counters, reload epochs, the training
+    generation: SGD and the batch-statistics kernels update in place)."""
+    prm = [bn.gamma, bn.beta, bn.moving_mean, bn.moving_var]
+    key = (float(bn.eps), bool(bn.fix_gamma), precision.train_generation(*prm)) + tuple(
+        (t.data_ptr(), t._version, precision.weight_epoch(t)) for t in prm)
+    hit = bn.__dict__.get('_mxr_post_bn')
+    if hit is None or hit[0] != key:
+        with torch.no_grad():
+            aff = need_ext().bn_affine(*[t.detach().float().contiguous() for t in prm], float(bn.eps),
+                                       bool(bn.fix_gamma))
+        hit = (key, aff)
+        bn.__dict__['_mxr_post_bn'] = hit
+    return hit[1]
 
 
 def max_pool_bn_relu(x, k, s, p, bn):
     """relu(bn(max_pool(x))) for a frozen ``bn``: one kernel on the HIP path (post_bn_ok), else the
     two ops."""
     if post_bn_ok(bn) and kernel_path(x):
-        prm, eps, fix = post_bn_params(bn)
-        return need_ext().maxpool_fwd(x, int(k), int(s), int(p), precision.is_pair(x), False, prm, eps, fix)[0]
+        return need_ext().maxpool_fwd(x, int(k), int(s), int(p), precision.is_pair(x), False, post_bn_params(bn))[0]
     return bn(max_pool2d(x, k, s, p))
 
 

@@ -126,8 +126,7 @@ def roi_pool_bn_relu(feat, rois, pooled_size, spatial_scale, bn):
     head): the BN + ReLU in the pooling kernel's store, no argmax map (ops/pool.py post_bn_ok)."""
     from .pool import post_bn_ok, post_bn_params
     if feat.is_cuda and post_bn_ok(bn):
-        prm, eps, fix = post_bn_params(bn)
         return need_ext().roi_pool_fwd(feat.contiguous(memory_format=torch.channels_last), rois.float().contiguous(),
                                        int(pooled_size[0]), int(pooled_size[1]), float(spatial_scale),
-                                       precision.is_pair(feat), False, prm, eps, fix)[0]
+                                       precision.is_pair(feat), False, post_bn_params(bn))[0]
     return bn(roi_pool(feat, rois, pooled_size, spatial_scale))

@@ -762,7 +762,12 @@ def test_roi_pool_post_bn_matches_pool_then_bn(cuda, dtype, C, fix):
     rois = _rois(g, 64, B, H, W).to(cuda)
     rois[3, 0] = -1  # empty output rows: relu(bn(0))
     prm, eps, fix = _post_bn(g, C, cuda, fix)
-    got, arg = ext.roi_pool_fwd(feat, rois, 7, 7, 1 / 16, 0, False, prm, eps, fix)
+    aff = ext.bn_affine(*prm, eps, fix)
+    gm = torch.ones(C) if fix else prm[0].cpu()
+    s_ref = gm / torch.sqrt(prm[3].cpu() + eps)
+    assert torch.allclose(aff[0].cpu(), s_ref, rtol=1e-6) and torch.allclose(
+        aff[1].cpu(), prm[1].cpu() - prm[2].cpu() * s_ref, rtol=1e-5, atol=1e-6)
+    got, arg = ext.roi_pool_fwd(feat, rois, 7, 7, 1 / 16, 0, False, aff)
     assert arg.numel() == 0 and got.is_contiguous(memory_format=torch.channels_last)
     pooled = ext.roi_pool_fwd(feat, rois, 7, 7, 1 / 16, 0, False)[0]
     if dtype != torch.float32:
@@ -772,7 +777,7 @@ def test_roi_pool_post_bn_matches_pool_then_bn(cuda, dtype, C, fix):
     tol = 1e-5 if dtype == torch.float32 else 1e-2
     assert torch.allclose(got.double().cpu(), want, atol=tol, rtol=tol)
     with pytest.raises(RuntimeError, match='inference-only'):
-        ext.roi_pool_fwd(feat, rois, 7, 7, 1 / 16, 0, True, prm, eps, fix)
+        ext.roi_pool_fwd(feat, rois, 7, 7, 1 / 16, 0, True, aff)
 
 
 @pytest.mark.gpu
@@ -785,14 +790,15 @@ def test_maxpool_post_bn_matches_pool_then_bn(cuda, dtype, fix):
     g = torch.Generator().manual_seed(12)
     x = torch.randn(2, 64, 41, 53, generator=g).to(cuda, dtype).contiguous(memory_format=torch.channels_last)
     prm, eps, fix = _post_bn(g, 64, cuda, fix)
-    got, arg = ext.maxpool_fwd(x, 3, 2, 1, 0, False, prm, eps, fix)
+    aff = ext.bn_affine(*prm, eps, fix)
+    got, arg = ext.maxpool_fwd(x, 3, 2, 1, 0, False, aff)
     assert arg.numel() == 0
     want = ext.bn_relu_fwd(ext.maxpool_fwd(x, 3, 2, 1, 0)[0], *prm, eps, fix, True, 0)
     assert torch.equal(got, want), (got.float() - want.float()).abs().max().item()
     ref = _bn_relu_ref(F.max_pool2d(x.float().cpu(), 3, 2, 1), prm, eps, fix)
     assert torch.allclose(got.double().cpu(), ref, atol=1e-2, rtol=1e-2)
     with pytest.raises(RuntimeError, match='inference-only'):
-        ext.maxpool_fwd(x, 3, 2, 1, 0, True, prm, eps, fix)
+        ext.maxpool_fwd(x, 3, 2, 1, 0, True, aff)
 
 
 @pytest.mark.gpu

@@ -34,7 +34,7 @@ typedef float f32x4_t __attribute__((ext_vector_type(4)));
 
 constexpr uint32_t kOOB = 0x80000000u;
 constexpr int BK = 32;       // channels per K tile
-constexpr int NBUF = 4;      // K tiles resident in LDS (3 in flight)
+constexpr int NBUF = 4;      // K tiles resident in LDS (3 in flight); short-K tiles 205-207: 2 or 3
 
 template <int N>
 __device__ __forceinline__ void vm_wait() {
@@ -76,7 +76,7 @@ struct BigCfg {
 // itself): referenced directly, hipcc's wait-count pass drained every in-flight LDS-DMA
 // (s_waitcnt vmcnt(0)) before the fragment reads of each K tile -- the same effect the buffer
 // kernel documents for a __restrict__ ring (conv_igemm.hip).
-template <int BM_, int BN, bool F16>
+template <int BM_, int BN, bool F16, int NR = NBUF>
 __device__ __forceinline__ void conv_big_body(uint16_t* lds, const uint16_t* __restrict__ x,
                                               const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int NB, int H,
                                               int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride,
@@ -164,14 +164,14 @@ __device__ __forceinline__ void conv_big_body(uint16_t* lds, const uint16_t* __r
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4_t{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll
-  for (int s = 0; s < NBUF - 1; ++s)
+  for (int s = 0; s < NR - 1; ++s)
     if (s < nk) issue(s);
   // fragment read offsets (elements) within a K tile: A row wm*WM + i*16 + (lane & 15), B row
   // BM + wn*64 + j*16 + (lane & 15), logical chunk lane >> 4
   const int fr_row = lane & 15, fr_ch = lane >> 4;
   for (int kt = 0; kt < nk; ++kt) {
-    // K tile kt landed: at most min(2, nk-1-kt) younger tiles of this thread still in flight
-    const int ahead = min(NBUF - 2, nk - 1 - kt);
+    // K tile kt landed: at most min(NR - 2, nk-1-kt) younger tiles of this thread still in flight
+    const int ahead = min(NR - 2, nk - 1 - kt);
     if (ahead >= 2) {
       if (C::NHI == 0 || lpt == C::LPT_LO) vm_wait<2 * C::LPT_LO>();
       else vm_wait<2 * C::LPT_HI>();
@@ -182,8 +182,8 @@ __device__ __forceinline__ void conv_big_body(uint16_t* lds, const uint16_t* __r
       vm_wait<0>();
     }
     __builtin_amdgcn_s_barrier();  // every wave's DMA of tile kt landed; tile kt-1's buffer is free
-    if (kt + NBUF - 1 < nk) issue((kt + NBUF - 1) % NBUF);
-    const uint16_t* T = lds + (kt % NBUF) * C::ROWS * BK;
+    if (kt + NR - 1 < nk) issue((kt + NR - 1) % NR);
+    const uint16_t* T = lds + (kt % NR) * C::ROWS * BK;
     uint4 af[TM], bf[TN];
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -266,14 +266,21 @@ __device__ __forceinline__ void conv_big_body(uint16_t* lds, const uint16_t* __r
   }
 }
 
-template <int BM, int BN, bool F16>
+// LDS: the ring, and at least the 8 per-wave epilogue slabs (16 rows x EPI_LD fp32) it is reused for
+template <int BM, int BN, int NR>
+constexpr int big_lds_elems() {
+  constexpr int ring = NR * BigCfg<BM, BN>::ROWS * BK, slabs = 8 * 16 * BigCfg<BM, BN>::EPI_LD * 2;
+  return ring > slabs ? ring : slabs;
+}
+
+template <int BM, int BN, bool F16, int NBR = NBUF>
 __global__ void __launch_bounds__(512)
 conv_big_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, uint16_t* __restrict__ y, int NB,
                 int H, int W, int Cin, int Ho, int Wo, int Cout, int KH, int KW, int stride, int pad, const ConvEpi ep,
                 int tiles_n, int nwg) {
   // one LDS array (a second __shared__ object can make hipcc drain the DMA ring before each read)
-  __shared__ __attribute__((aligned(16))) uint16_t lds[NBUF * BigCfg<BM, BN>::ROWS * BK];
-  conv_big_body<BM, BN, F16>(lds, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, tiles_n, nwg);
+  __shared__ __attribute__((aligned(16))) uint16_t lds[big_lds_elems<BM, BN, NBR>()];
+  conv_big_body<BM, BN, F16, NBR>(lds, x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, tiles_n, nwg);
 }
 
 }  // namespace
@@ -286,7 +293,7 @@ conv_big_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w, 
 // idle; 128x128 gives 300, two resident per CU with the 64 KB ring)
 int conv_big_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho, int Wo,
                  int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int tile, hipStream_t st) {
-  if (tile < 200 || tile > 204) return -1;
+  if (tile < 200 || tile > 207) return -1;
   if (Cin % BK != 0 || Cout % 16 != 0 || KH * KW > 64) return -1;
   if (ep.x2 || ep.yf || ep.bt || ep.omap || ep.pad_w >= 0 || ep.bnb_x || ep.st_part || ep.bnb_part || ep.rmask ||
       ep.drop_p > 0.f)
@@ -294,26 +301,31 @@ int conv_big_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int 
   if ((ep.y2) && (!ep.bn_beta || !ep.bn_mean || !ep.bn_var || (!ep.bn_fix_gamma && !ep.bn_gamma))) return -1;
   if ((int64_t)NB * H * W * Cin * 2 >= (int64_t)kOOB || (int64_t)Cout * KH * KW * Cin * 2 >= (int64_t)kOOB) return -1;
   const int M = NB * Ho * Wo;
-  const int bm = tile == 204 ? 160 : tile >= 202 ? 128 : 256;
-  const int bn = (tile == 200 || tile == 203 || tile == 204) ? 256 : 128;
+  const int bm = tile == 204 ? 160 : (tile == 200 || tile == 201 || tile == 207) ? 256 : 128;
+  const int bn = (tile == 200 || tile == 203 || tile == 204 || tile == 207) ? 256 : 128;
   const int tiles_n = (Cout + bn - 1) / bn;
   const int nwg = ((M + bm - 1) / bm) * tiles_n;
-#define MXR_BIG(BM_, BN_, F_)                                                                                 \
-  conv_big_kernel<BM_, BN_, F_><<<nwg, 512, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, \
-                                                    ep, tiles_n, nwg)
-#define MXR_BIG2(BM_, BN_)      \
-  do {                          \
-    if (ep.f16)                 \
-      MXR_BIG(BM_, BN_, true);  \
-    else                        \
-      MXR_BIG(BM_, BN_, false); \
+#define MXR_BIG(BM_, BN_, F_, R_)                                                                          \
+  conv_big_kernel<BM_, BN_, F_, R_><<<nwg, 512, 0, st>>>(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, \
+                                                        pad, ep, tiles_n, nwg)
+#define MXR_BIG2(BM_, BN_, R_)      \
+  do {                              \
+    if (ep.f16)                     \
+      MXR_BIG(BM_, BN_, true, R_);  \
+    else                            \
+      MXR_BIG(BM_, BN_, false, R_); \
   } while (0)
+  // 205-207: shallow rings for short-K GEMMs (the 1x1 expands, K = 256 / 512): less LDS per
+  // workgroup, so more workgroups per CU and one's epilogue stores overlap another's K loop
   switch (tile) {
-    case 200: MXR_BIG2(256, 256); break;
-    case 201: MXR_BIG2(256, 128); break;
-    case 202: MXR_BIG2(128, 128); break;
-    case 203: MXR_BIG2(128, 256); break;
-    default: MXR_BIG2(160, 256); break;
+    case 200: MXR_BIG2(256, 256, NBUF); break;
+    case 201: MXR_BIG2(256, 128, NBUF); break;
+    case 202: MXR_BIG2(128, 128, NBUF); break;
+    case 203: MXR_BIG2(128, 256, NBUF); break;
+    case 205: MXR_BIG2(128, 128, 2); break;
+    case 206: MXR_BIG2(128, 128, 3); break;
+    case 207: MXR_BIG2(256, 256, 2); break;
+    default: MXR_BIG2(160, 256, NBUF); break;
   }
 #undef MXR_BIG2
 #undef MXR_BIG

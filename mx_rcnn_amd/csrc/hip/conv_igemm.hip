@@ -1013,8 +1013,8 @@ static void launch_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB
 float philox_uniform_host(uint32_t seed, uint64_t step, uint64_t e) { return philox_uniform(seed, step, e); }
 
 int conv_tile_bm(int tile) {
-  if (tile == 200 || tile == 201) return 256;
-  if (tile == 202 || tile == 203) return 128;
+  if (tile == 200 || tile == 201 || tile == 207) return 256;
+  if (tile == 202 || tile == 203 || tile == 205 || tile == 206) return 128;
   if (tile == 204) return 160;
   if (tile >= 100 && tile < 100 + kNumRing) return kRingShapes[tile - 100].bm;
   switch (tile) {
@@ -1061,7 +1061,7 @@ int conv_igemm_plan(int NB, int Ho, int Wo, int Cin, int Cout, int KH, int KW, i
 int conv_igemm_fwd(const uint16_t* x, const uint16_t* w, uint16_t* y, int NB, int H, int W, int Cin, int Ho, int Wo,
                    int Cout, int KH, int KW, int stride, int pad, const ConvEpi& ep, int tile, int splits, float* slab,
                    hipStream_t st) {
-  if (tile >= 200 && tile <= 204)  // large-tile kernel (conv_big.hip): whole K per workgroup
+  if (tile >= 200 && tile <= 207)  // large-tile kernel (conv_big.hip): whole K per workgroup
     return splits > 1 ? -1 : conv_big_fwd(x, w, y, NB, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, ep, tile, st);
   if (Cin % BK != 0) return -1;
   if (splits > 1 && (slab == nullptr || Cout % 4 != 0)) return -1;

@@ -25,7 +25,7 @@ for spec in ${TEST_FPS:-}; do  # e.g. "fp32:1 bf16:1 bf16:8 fp32:8"
       python bench_test.py --dtype $dt --batch $nb --steps 10 --warmup 3 > $OUT/test_prof_${dt}_b$nb.log 2>&1 || { tail -20 $OUT/test_prof_${dt}_b$nb.log; exit 1; }
     T=$(find $OUT/tprof -name '*kernel_trace.csv' | head -1)
     python tools/trace_groups.py "$T" --marker nms_reduce_mc --steps 10 --top 80 > $OUT/test_trace_${dt}_b$nb.txt 2>&1
-    echo "vendor conv/GEMM kernels in the $dt b$nb test trace: $(grep -ciE 'Cijk|miopen|igemm_fwd_gtc|naive_conv|rocblas|hipblas|at::native' $OUT/test_trace_${dt}_b$nb.txt)"
+    echo "vendor conv/GEMM kernels in the $dt b$nb test trace: $(grep -ciE 'Cijk|miopen|igemm_fwd_gtc|naive_conv|rocblas|hipblas|at::native::.*(conv|gemm|addmm)' $OUT/test_trace_${dt}_b$nb.txt || true)"
     rm -rf $OUT/tprof
   fi
 done

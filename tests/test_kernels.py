@@ -351,11 +351,11 @@ def test_conv_igemm_fwd_vs_fp32(cuda, shape):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize('dtype', [torch.bfloat16, torch.float16])
-@pytest.mark.parametrize('tile', [200, 201, 202, 203])
+@pytest.mark.parametrize('tile', [200, 201, 202, 203, 204, 205, 206, 207])
 def test_conv_big_epilogue_vs_fp32(cuda, dtype, tile):
-    """The 256-row large-tile kernel (conv_big.hip) with its full epilogue -- bias, residual, ReLU and
-    the frozen BN + ReLU second output -- against the fp32 reference of the same 16-bit operands;
-    M = 2 * 37 * 53 (not a multiple of 256) and Cout = 320 (a partial column tile)."""
+    """The large-tile kernel (conv_big.hip: every tile shape and ring depth) with its full epilogue --
+    bias, residual, ReLU and the frozen BN + ReLU second output -- against the fp32 reference of the
+    same 16-bit operands; M = 2 * 37 * 53 (not a multiple of 256) and Cout = 320 (a partial column tile)."""
     from mx_rcnn_amd.ops import need_ext
     g = torch.Generator().manual_seed(21)
     N, Cin, H, W, Cout = 2, 128, 37, 53, 320

@@ -210,19 +210,32 @@ __device__ __forceinline__ void conv_big_body(uint16_t* lds, const uint16_t* __r
   const int er = lane >> 2;             // slab row of this lane
   const int ec = (lane & 3) * 16;       // first of its 16 columns
   const int n = n0 + wn * 64 + ec;
-  float bias[16], bs[16], bt[16];
-#pragma unroll
-  for (int k = 0; k < 16; ++k) {
-    const int col = min(n + k, Cout - 1);
-    bias[k] = ep.bias ? ep.bias[col] : (ep.bias_h ? h16_to_f32(ep.bias_h[col], code) : 0.f);
-    bs[k] = 1.f;
-    bt[k] = 0.f;
+  // per-column epilogue coefficients: each lane derives ONE of the wave's 64 columns (bias, BN
+  // scale, BN shift: 5 loads + 1 rsqrt) into a per-wave LDS table, then reads its 16 columns back as
+  // 16-B vectors -- instead of 16 columns x 5 scalar loads per lane
+  float* coef = reinterpret_cast<float*>(lds) + 8 * 16 * C::EPI_LD + wid * 3 * 64;
+  {
+    const int col = min(n0 + wn * 64 + lane, Cout - 1);
+    float cb = ep.bias ? ep.bias[col] : (ep.bias_h ? h16_to_f32(ep.bias_h[col], code) : 0.f), cs = 1.f, ct = 0.f;
     if (ep.y2) {
       const float g = ep.bn_fix_gamma ? 1.f : ep.bn_gamma[col];
       const float inv = rsqrtf(ep.bn_var[col] + ep.bn_eps);
-      bs[k] = g * inv;
-      bt[k] = ep.bn_beta[col] - ep.bn_mean[col] * bs[k];
+      cs = g * inv;
+      ct = ep.bn_beta[col] - ep.bn_mean[col] * cs;
     }
+    coef[lane] = cb;
+    coef[64 + lane] = cs;
+    coef[128 + lane] = ct;
+  }
+  float bias[16], bs[16], bt[16];  // (same-wave LDS write -> read: in order)
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const float4 b4 = *reinterpret_cast<const float4*>(coef + ec + 4 * q);
+    const float4 s4 = *reinterpret_cast<const float4*>(coef + 64 + ec + 4 * q);
+    const float4 t4 = *reinterpret_cast<const float4*>(coef + 128 + ec + 4 * q);
+    bias[4 * q] = b4.x; bias[4 * q + 1] = b4.y; bias[4 * q + 2] = b4.z; bias[4 * q + 3] = b4.w;
+    bs[4 * q] = s4.x; bs[4 * q + 1] = s4.y; bs[4 * q + 2] = s4.z; bs[4 * q + 3] = s4.w;
+    bt[4 * q] = t4.x; bt[4 * q + 1] = t4.y; bt[4 * q + 2] = t4.z; bt[4 * q + 3] = t4.w;
   }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
@@ -266,10 +279,11 @@ __device__ __forceinline__ void conv_big_body(uint16_t* lds, const uint16_t* __r
   }
 }
 
-// LDS: the ring, and at least the 8 per-wave epilogue slabs (16 rows x EPI_LD fp32) it is reused for
+// LDS: the ring, and at least what the epilogue reuses it for: 8 per-wave slabs (16 rows x EPI_LD
+// fp32) and 8 per-wave coefficient tables (3 x 64 fp32)
 template <int BM, int BN, int NR>
 constexpr int big_lds_elems() {
-  constexpr int ring = NR * BigCfg<BM, BN>::ROWS * BK, slabs = 8 * 16 * BigCfg<BM, BN>::EPI_LD * 2;
+  constexpr int ring = NR * BigCfg<BM, BN>::ROWS * BK, slabs = (8 * 16 * BigCfg<BM, BN>::EPI_LD + 8 * 3 * 64) * 2;
   return ring > slabs ? ring : slabs;
 }
 

@@ -555,7 +555,8 @@ __device__ __forceinline__ void igemm_x2w_body(uint16_t* lds, int bid, const uin
         for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al[i], bh[j], acc[i][j], 0, 0, 0);
     }
   }
-  static_assert(BM * (BN + 4) * 4 <= S * (BM + BN) * RB * 2, "epilogue tile must fit the operand ring");
+  static_assert((BM * (BN + 4) + 5 * BN) * 4 <= S * (BM + BN) * RB * 2,
+                "epilogue tile + column table must fit the operand ring");
   if (Cout % 8 == 0)
     igemm_epilogue_lds<BM, BN, TM, TN, WM, WN, true>(acc, reinterpret_cast<float*>(lds), m0, n0, wm, wn, lane, tid, M,
                                                      Cout, ep, y, 0, 1, nullptr, Ho, Wo);
@@ -633,6 +634,8 @@ __device__ __forceinline__ void ring_epilogue(f32x4 (&acc)[TM][TN], float* __res
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         T[(wm * WM + i * 16 + (lane >> 4) * 4 + r) * LDT + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
+  float* const tab = T + BM * LDT;  // [5][BN] column constants (igemm_body.h epi_cols_stage)
+  if (splits <= 1) epi_cols_stage<BN, NT>(tab, ep, tid, n0, Cout);
   __syncthreads();
   const int cv = tid % VPR;
   const int n = n0 + cv * 8;
@@ -650,8 +653,7 @@ __device__ __forceinline__ void ring_epilogue(f32x4 (&acc)[TM][TN], float* __res
     return;
   }
   EpiCol ec[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) ec[k] = epi_col(ep, ncol ? n + k : 0);
+  epi_cols_load<BN>(tab, cv, ec);
   if (ep.bnb_x) {
     float sg[8], sgx[8];
 #pragma unroll
@@ -731,7 +733,8 @@ conv_ring_kernel(const uint16_t* __restrict__ x, const uint16_t* __restrict__ w,
                  const ConvEpi ep, int tiles_n, int nwg, int ntiles, int splits, float* __restrict__ slab) {
   using C = RingCfg<TM, TN, WGM, WGN, SFIX>;
   constexpr int BM = C::BM, BN = C::BN, S = C::S, NT = C::NT, NW = C::NW;
-  static_assert(C::BM * (C::BN + 4) * 4 <= S * (C::BM + C::BN) * BK * 2, "epilogue tile must fit the ring");
+  static_assert((C::BM * (C::BN + 4) + 5 * C::BN) * 4 <= S * (C::BM + C::BN) * BK * 2,
+                "epilogue tile + column table must fit the ring");
   __shared__ __attribute__((aligned(16))) uint16_t lds[S * (BM + BN) * BK];
   uint16_t* As = lds;
   uint16_t* Bs = lds + S * BM * BK;

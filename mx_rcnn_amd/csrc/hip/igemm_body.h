@@ -120,6 +120,37 @@ __device__ __forceinline__ EpiCol epi_col(const ConvEpi& ep, int n) {
   return c;
 }
 
+// The workgroup's per-column constants through LDS: column n0 + c is derived ONCE (thread c of the
+// workgroup; up to 5 parameter loads and an rsqrt) into a [5][BN] table placed after the staged tile,
+// then every thread reads its 8 consecutive columns back as 16-B vectors -- instead of each thread
+// issuing 8 x 5 scalar parameter loads before its first store (conv_big.hip: the same change took
+// batch-8 test FPS from 749 to 804).  Stage in the same phase as the tile, read after the barrier.
+template <int BN, int NT>
+__device__ __forceinline__ void epi_cols_stage(float* __restrict__ tab, const ConvEpi& ep, int tid, int n0, int Cout) {
+  for (int c = tid; c < BN; c += NT) {
+    const EpiCol e = epi_col(ep, n0 + c < Cout ? n0 + c : 0);
+    tab[c] = e.bias;
+    tab[BN + c] = e.s;
+    tab[2 * BN + c] = e.t;
+    tab[3 * BN + c] = e.mean;
+    tab[4 * BN + c] = e.inv;
+  }
+}
+
+template <int BN>
+__device__ __forceinline__ void epi_cols_load(const float* __restrict__ tab, int cv, EpiCol (&ec)[8]) {
+  float v[5][8];
+#pragma unroll
+  for (int f = 0; f < 5; ++f) {
+    const float4 a = *reinterpret_cast<const float4*>(tab + f * BN + cv * 8);
+    const float4 b = *reinterpret_cast<const float4*>(tab + f * BN + cv * 8 + 4);
+    v[f][0] = a.x; v[f][1] = a.y; v[f][2] = a.z; v[f][3] = a.w;
+    v[f][4] = b.x; v[f][5] = b.y; v[f][6] = b.z; v[f][7] = b.w;
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) ec[k] = EpiCol{v[0][k], v[1][k], v[2][k], v[3][k], v[4][k]};
+}
+
 // fused inverted dropout of output element `idx` (see ConvEpi::drop_p)
 __device__ __forceinline__ float epi_dropout(const ConvEpi& ep, int64_t idx, float v) {
   if (ep.drop_p > 0.f) {
@@ -347,6 +378,8 @@ __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* 
         for (int r = 0; r < 4; ++r)
           Tq[(wm * WM + i * 16 + (lane >> 4) * 4 + r) * LDT + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
   }
+  float* const tab = T + KG * BM * LDT;  // [5][BN] column constants (callers size the LDS for it)
+  if (splits <= 1) epi_cols_stage<BN, NT>(tab, ep, tid, n0, Cout);
   __syncthreads();
   // 8 consecutive accumulators of a staged row: the sum of the K groups' slices
   auto ldrow = [&](int row, int cv8, float* a) {
@@ -379,8 +412,7 @@ __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* 
     return;
   }
   EpiCol ec[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) ec[k] = epi_col(ep, ncol ? n + k : 0);
+  epi_cols_load<BN>(tab, cv, ec);
   if (ep.bnb_x) {
     float sg[8], sgx[8];
 #pragma unroll
@@ -909,7 +941,8 @@ __device__ __forceinline__ void igemm_buf_body(uint16_t* lds, int bid, const uin
           acc[i][j] = Mfma16<F16>::mma(af[i], bfr[j], acc[i][j]);
     }
   }
-  static_assert(BM * (BN + 4) * 4 <= S * (BM + BN) * BK * 2, "epilogue tile must fit the operand ring");
+  static_assert((KG * BM * (BN + 4) + 5 * BN) * 4 <= S * KG * igemm_ring_stage<BM, BN, BT, X3>() * 2,
+                "epilogue tile + column table must fit the operand ring");
   if constexpr (KG > 1) {  // (the launcher guarantees Cout % 8 == 0)
     igemm_epilogue_lds<BM, BN, TM, TN, WM, WN, X2, KG>(acc, reinterpret_cast<float*>(lds), m0, n0, wm, wn, lane,
                                                        tid, M, Cout, ep, y, split, splits, slab, Ho, Wo);

@@ -231,11 +231,16 @@ __device__ __forceinline__ void conv_big_body(uint16_t* lds, const uint16_t* __r
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const float4 b4 = *reinterpret_cast<const float4*>(coef + ec + 4 * q);
-    const float4 s4 = *reinterpret_cast<const float4*>(coef + 64 + ec + 4 * q);
-    const float4 t4 = *reinterpret_cast<const float4*>(coef + 128 + ec + 4 * q);
     bias[4 * q] = b4.x; bias[4 * q + 1] = b4.y; bias[4 * q + 2] = b4.z; bias[4 * q + 3] = b4.w;
-    bs[4 * q] = s4.x; bs[4 * q + 1] = s4.y; bs[4 * q + 2] = s4.z; bs[4 * q + 3] = s4.w;
-    bt[4 * q] = t4.x; bt[4 * q + 1] = t4.y; bt[4 * q + 2] = t4.z; bt[4 * q + 3] = t4.w;
+    if (ep.y2) {  // (no second output: the BN columns are never read)
+      const float4 s4 = *reinterpret_cast<const float4*>(coef + 64 + ec + 4 * q);
+      const float4 t4 = *reinterpret_cast<const float4*>(coef + 128 + ec + 4 * q);
+      bs[4 * q] = s4.x; bs[4 * q + 1] = s4.y; bs[4 * q + 2] = s4.z; bs[4 * q + 3] = s4.w;
+      bt[4 * q] = t4.x; bt[4 * q + 1] = t4.y; bt[4 * q + 2] = t4.z; bt[4 * q + 3] = t4.w;
+    } else {
+      bs[4 * q] = bs[4 * q + 1] = bs[4 * q + 2] = bs[4 * q + 3] = 1.f;
+      bt[4 * q] = bt[4 * q + 1] = bt[4 * q + 2] = bt[4 * q + 3] = 0.f;
+    }
   }
 #pragma unroll
   for (int i = 0; i < TM; ++i) {

@@ -634,8 +634,9 @@ __device__ __forceinline__ void ring_epilogue(f32x4 (&acc)[TM][TN], float* __res
 #pragma unroll
       for (int r = 0; r < 4; ++r)
         T[(wm * WM + i * 16 + (lane >> 4) * 4 + r) * LDT + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
+  const bool use_tab = ep.y2 || ep.bnb_x;  // (bias-only: direct loads, see igemm_epilogue_lds)
   float* const tab = T + BM * LDT;  // [5][BN] column constants (igemm_body.h epi_cols_stage)
-  if (splits <= 1) epi_cols_stage<BN, NT>(tab, ep, tid, n0, Cout);
+  if (splits <= 1 && use_tab) epi_cols_stage<BN, NT>(tab, ep, tid, n0, Cout);
   __syncthreads();
   const int cv = tid % VPR;
   const int n = n0 + cv * 8;
@@ -653,7 +654,12 @@ __device__ __forceinline__ void ring_epilogue(f32x4 (&acc)[TM][TN], float* __res
     return;
   }
   EpiCol ec[8];
-  epi_cols_load<BN>(tab, cv, ec);
+  if (use_tab) {
+    epi_cols_load<BN>(tab, cv, ec);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ec[k] = epi_col(ep, ncol ? n + k : 0);
+  }
   if (ep.bnb_x) {
     float sg[8], sgx[8];
 #pragma unroll

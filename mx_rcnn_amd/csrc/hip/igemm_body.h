@@ -378,8 +378,11 @@ __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* 
         for (int r = 0; r < 4; ++r)
           Tq[(wm * WM + i * 16 + (lane >> 4) * 4 + r) * LDT + wn * WN + j * 16 + (lane & 15)] = acc[i][j][r];
   }
+  // BN epilogues take their column constants from an LDS table; a bias-only epilogue keeps its 8
+  // direct loads (cheaper than the table's staging + 10 vector reads: VGG16 fp32 measured -3 %)
+  const bool use_tab = ep.y2 || ep.bnb_x;
   float* const tab = T + KG * BM * LDT;  // [5][BN] column constants (callers size the LDS for it)
-  if (splits <= 1) epi_cols_stage<BN, NT>(tab, ep, tid, n0, Cout);
+  if (splits <= 1 && use_tab) epi_cols_stage<BN, NT>(tab, ep, tid, n0, Cout);
   __syncthreads();
   // 8 consecutive accumulators of a staged row: the sum of the K groups' slices
   auto ldrow = [&](int row, int cv8, float* a) {
@@ -412,7 +415,12 @@ __device__ __forceinline__ void igemm_epilogue_lds(f32x4 (&acc)[TM][TN], float* 
     return;
   }
   EpiCol ec[8];
-  epi_cols_load<BN>(tab, cv, ec);
+  if (use_tab) {
+    epi_cols_load<BN>(tab, cv, ec);
+  } else {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) ec[k] = epi_col(ep, ncol ? n + k : 0);
+  }
   if (ep.bnb_x) {
     float sg[8], sgx[8];
 #pragma unroll

@@ -9,7 +9,9 @@ import torch
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def run(out, precision, extra):
+def run(out, precision, extra, val=None):
+    if val is not None:  # --dirty-val differs between the two runs: a read of unwritten memory shows
+        extra = extra + ['--dirty-val', str(val)]
     env = dict(os.environ, MXR_CONV_TUNE='0')
     r = subprocess.run([sys.executable, os.path.join(ROOT, 'tools', 'dp_step_check.py'), out, '--precision', precision,
                         '--steps', '1'] + extra, env=env, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
@@ -24,8 +26,9 @@ def main():
     tmp = os.environ.get('TMPDIR', '/tmp')
     extra = sys.argv[2:]
     for p in sys.argv[1].split(','):
-        a = run(os.path.join(tmp, 'det_a.pt'), p, extra)
-        b = run(os.path.join(tmp, 'det_b.pt'), p, extra)
+        vary = '--dirty-gb' in extra
+        a = run(os.path.join(tmp, 'det_a.pt'), p, extra, 1000.0 if vary else None)
+        b = run(os.path.join(tmp, 'det_b.pt'), p, extra, -7.0 if vary else None)
         keys = [k for k in a if not k.startswith('_')]
         bad = [(k, float((a[k].float() - b[k].float()).abs().max())) for k in keys if not torch.equal(a[k], b[k])]
         print('%s: %d of %d arrays differ' % (p, len(bad), len(keys)), flush=True)

@@ -33,16 +33,21 @@ def main():
     ap.add_argument('--dirty-gb', type=float, default=0.0,
                     help='before anything else, fill this many GB of the caching allocator with NaN and free it: '
                          'a kernel that reads memory it never wrote then sees NaN instead of the zeros of fresh VRAM')
+    ap.add_argument('--dirty-keep', action='store_true',
+                    help='keep the dirty blocks in the caching allocator (no empty_cache): eager allocations '
+                         'then reuse them')
+    ap.add_argument('--dirty-val', type=float, default=float('nan'), help='fill value of --dirty-gb')
     args = ap.parse_args()
     rank, world, _, device = pdist.init_distributed()
     if args.dirty_gb > 0:
         blocks = []
         for sz in (1 << 28, 1 << 24, 1 << 20, 1 << 16):  # large and small allocator pools
             for _ in range(max(1, int(args.dirty_gb * (1 << 30) / 4 / sz / 4))):
-                blocks.append(torch.full((sz,), float('nan'), device=device))
+                blocks.append(torch.full((sz,), args.dirty_val, device=device))
         torch.cuda.synchronize()
         del blocks
-        torch.cuda.empty_cache()  # back to the driver: the graph pool's fresh segments may get these pages
+        if not args.dirty_keep:
+            torch.cuda.empty_cache()  # back to the driver: the graph pool's fresh segments may get these pages
     h, w = [int(v) for v in args.image.split('x')]
     cfg = snapshot()
     if args.mode == 'e2e':
